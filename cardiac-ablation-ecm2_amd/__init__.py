@@ -1,0 +1,387 @@
+"""cardiac-ablation-ecm2_amd -- Python binding of the MI355X PA diffusion+mass operator.
+
+The product is the C-ABI shared library ``lib/libecm2pa.so`` (C++ host code +
+hand-written gfx950 HIP kernels; header ``include/ecm2_pa.h``).  This module is a
+thin ctypes mirror of the reference's user-facing names so that tests and the
+benchmark read like the reference's own drivers:
+
+    reference (MFEM)                                   here
+    Mesh::MakeCartesian3D / Mesh(file)                 Mesh.MakeCartesian3D / Mesh(path)
+    Mesh::UniformRefinement                            Mesh.UniformRefinement
+    H1_FECollection + FiniteElementSpace               H1Space
+    BilinearForm + SetAssemblyLevel(PARTIAL)           BilinearForm (PARTIAL only)
+    AddDomainIntegrator(MassIntegrator(Q))             AddDomainIntegrator(MassIntegrator(Q))
+    Assemble / Mult / AssembleDiagonal                 Assemble / Mult / AssembleDiagonal
+    ConstrainedOperator + CGSolver (+ Jacobi)          BilinearForm.PCG
+
+Vectors are torch CUDA float64 tensors (torch is plumbing: device memory and
+streams).  There is no CPU fallback: without the built library or without a GPU
+every compute call raises ``ECM2Error``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libecm2pa.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ecm2_pa.h")
+
+MASS, DIFFUSION = 0, 1
+COEFF_CONSTANT, COEFF_QUAD, COEFF_GRIDFUNC_AFFINE = 0, 1, 2
+KERNEL_AUTO, KERNEL_TPE, KERNEL_WPE, KERNEL_UNFUSED = 0, 1, 2, 3
+NUMBERING_ENTITY, NUMBERING_STRUCTURED = 0, 1
+
+
+class ECM2Error(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load the in-tree HIP library (import torch first so one HIP runtime is used)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ECM2Error(f"HIP extension not built: {path} missing (run __graft_entry__.build())")
+    try:
+        import torch  # noqa: F401  -- share torch's libamdhip64 / librccl
+    except Exception:
+        pass
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    vp, ip, dp, i32, f64 = ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_double
+    pp = ctypes.POINTER(ctypes.c_void_p)
+    sig = {
+        "ecm2_last_error": (ctypes.c_char_p, []),
+        "ecm2_version": (i32, []),
+        "ecm2_device_count": (i32, []),
+        "ecm2_mesh_cartesian": (i32, [i32, i32, i32, f64, f64, f64, pp]),
+        "ecm2_mesh_read": (i32, [ctypes.c_char_p, pp]),
+        "ecm2_mesh_refine_uniform": (i32, [vp]),
+        "ecm2_mesh_info": (i32, [vp, ip, ip]),
+        "ecm2_mesh_get_vertices": (i32, [vp, vp]),
+        "ecm2_mesh_set_vertices": (i32, [vp, vp]),
+        "ecm2_mesh_get_elements": (i32, [vp, vp]),
+        "ecm2_mesh_get_element_nodes": (i32, [vp, vp]),
+        "ecm2_mesh_destroy": (None, [vp]),
+        "ecm2_h1space_create": (i32, [vp, i32, i32, pp]),
+        "ecm2_h1space_info": (i32, [vp, ip, ip, ip]),
+        "ecm2_h1space_get_gather_map": (i32, [vp, vp]),
+        "ecm2_h1space_boundary_dofs": (i32, [vp, vp, ip]),
+        "ecm2_h1space_dof_coords": (i32, [vp, vp, vp]),
+        "ecm2_h1space_destroy": (None, [vp]),
+        "ecm2_pa_form_create": (i32, [i32, i32, i32, vp, i32, pp]),
+        "ecm2_pa_form_set_element_nodes": (i32, [vp, vp]),
+        "ecm2_pa_form_set_jacobians": (i32, [vp, vp]),
+        "ecm2_pa_form_add_integrator": (i32, [vp, i32, i32, vp, vp]),
+        "ecm2_pa_form_set_kernel": (i32, [vp, i32]),
+        "ecm2_pa_form_assemble": (i32, [vp, vp]),
+        "ecm2_pa_form_mult": (i32, [vp, vp, vp, vp]),
+        "ecm2_pa_form_assemble_diagonal": (i32, [vp, vp, vp]),
+        "ecm2_pa_form_restriction_mult": (i32, [vp, vp, vp, vp]),
+        "ecm2_pa_form_restriction_mult_transpose": (i32, [vp, vp, vp, vp]),
+        "ecm2_pa_form_integrator_add_mult": (i32, [vp, i32, vp, vp, vp]),
+        "ecm2_pa_form_get_qdata": (i32, [vp, i32, vp, vp]),
+        "ecm2_pa_form_info": (i32, [vp, ip, ip, ip, ip, ip, ip]),
+        "ecm2_pa_form_timing": (i32, [vp, i32]),
+        "ecm2_pa_form_timing_get": (i32, [vp, dp, ctypes.POINTER(ctypes.c_long)]),
+        "ecm2_pa_form_algorithmic_bytes": (i32, [vp, dp]),
+        "ecm2_pa_form_destroy": (None, [vp]),
+        "ecm2_pcg_solve": (i32, [vp, vp, i32, vp, vp, f64, f64, i32, i32, ip, dp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _check(rc: int):
+    if rc != 0:
+        msg = _lib.ecm2_last_error().decode(errors="replace")
+        raise ECM2Error(f"ecm2 error {rc}: {msg}")
+
+
+def _np_ptr(a: np.ndarray):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def _dev_ptr(t) -> ctypes.c_void_p:
+    if t is None:
+        return ctypes.c_void_p(0)
+    import torch
+    if not (isinstance(t, torch.Tensor) and t.is_cuda):
+        raise ECM2Error("expected a torch CUDA tensor")
+    if not t.is_contiguous():
+        raise ECM2Error("expected a contiguous tensor")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(stream=None) -> ctypes.c_void_p:
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def declared_symbols(header: str = HEADER_PATH) -> list:
+    """Function names declared in include/ecm2_pa.h."""
+    import re
+    txt = open(header).read()
+    return sorted(set(re.findall(r"\b(ecm2_[a-z0-9_]+)\s*\(", txt)))
+
+
+# ----------------------------------------------------------------------------
+# Mesh / space (setup side)
+# ----------------------------------------------------------------------------
+class Mesh:
+    """Trilinear hexahedral mesh (Mesh::MakeCartesian3D / Mesh(file) / UniformRefinement)."""
+
+    def __init__(self, path: Optional[str] = None, _handle=None):
+        lib = load_library()
+        h = ctypes.c_void_p()
+        if _handle is not None:
+            h = _handle
+        else:
+            _check(lib.ecm2_mesh_read(path.encode(), ctypes.byref(h)))
+        self._h = h
+
+    @classmethod
+    def MakeCartesian3D(cls, nx, ny, nz, sx=1.0, sy=1.0, sz=1.0):
+        lib = load_library()
+        h = ctypes.c_void_p()
+        _check(lib.ecm2_mesh_cartesian(nx, ny, nz, sx, sy, sz, ctypes.byref(h)))
+        return cls(_handle=h)
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.ecm2_mesh_destroy(self._h)
+            self._h = None
+
+    def UniformRefinement(self):
+        _check(_lib.ecm2_mesh_refine_uniform(self._h))
+
+    def _info(self):
+        nv, ne = ctypes.c_int(), ctypes.c_int()
+        _check(_lib.ecm2_mesh_info(self._h, ctypes.byref(nv), ctypes.byref(ne)))
+        return nv.value, ne.value
+
+    def GetNV(self):
+        return self._info()[0]
+
+    def GetNE(self):
+        return self._info()[1]
+
+    def vertices(self) -> np.ndarray:
+        out = np.empty((self.GetNV(), 3), np.float64)
+        _check(_lib.ecm2_mesh_get_vertices(self._h, _np_ptr(out)))
+        return out
+
+    def set_vertices(self, v: np.ndarray):
+        v = np.ascontiguousarray(v, np.float64)
+        assert v.shape == (self.GetNV(), 3)
+        _check(_lib.ecm2_mesh_set_vertices(self._h, _np_ptr(v)))
+
+    def elements(self) -> np.ndarray:
+        out = np.empty((self.GetNE(), 8), np.int32)
+        _check(_lib.ecm2_mesh_get_elements(self._h, _np_ptr(out)))
+        return out
+
+    def element_nodes(self) -> np.ndarray:
+        """Lexicographic corner coordinates [ne][3][8]."""
+        out = np.empty((self.GetNE(), 3, 8), np.float64)
+        _check(_lib.ecm2_mesh_get_element_nodes(self._h, _np_ptr(out)))
+        return out
+
+
+class H1Space:
+    """H1_FECollection(order) + FiniteElementSpace on a hex mesh (lexicographic element dofs)."""
+
+    def __init__(self, mesh: Mesh, order: int, numbering: int = NUMBERING_ENTITY):
+        h = ctypes.c_void_p()
+        _check(load_library().ecm2_h1space_create(mesh._h, order, numbering, ctypes.byref(h)))
+        self._h = h
+        self.mesh = mesh
+        self.order = order
+        nd, ne, ndl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(_lib.ecm2_h1space_info(h, ctypes.byref(nd), ctypes.byref(ne), ctypes.byref(ndl)))
+        self.ndofs, self.ne, self.nd = nd.value, ne.value, ndl.value
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.ecm2_h1space_destroy(self._h)
+            self._h = None
+
+    def GetVSize(self):
+        return self.ndofs
+
+    GetTrueVSize = GetVSize
+
+    def gather_map(self) -> np.ndarray:
+        out = np.empty((self.ne, self.nd), np.int32)
+        _check(_lib.ecm2_h1space_get_gather_map(self._h, _np_ptr(out)))
+        return out
+
+    def boundary_dofs(self) -> np.ndarray:
+        n = ctypes.c_int(0)
+        _check(_lib.ecm2_h1space_boundary_dofs(self._h, None, ctypes.byref(n)))
+        out = np.empty(n.value, np.int32)
+        if n.value:
+            _check(_lib.ecm2_h1space_boundary_dofs(self._h, _np_ptr(out), ctypes.byref(n)))
+        return out
+
+    GetEssentialTrueDofs = boundary_dofs
+
+    def dof_coords(self) -> np.ndarray:
+        out = np.empty((self.ndofs, 3), np.float64)
+        _check(_lib.ecm2_h1space_dof_coords(self._h, self.mesh._h, _np_ptr(out)))
+        return out
+
+
+# ----------------------------------------------------------------------------
+# Coefficients and integrators
+# ----------------------------------------------------------------------------
+class ConstantCoefficient:
+    def __init__(self, value: float):
+        self.value = float(value)
+
+
+class QuadratureCoefficient:
+    """Values at the quadrature points, torch CUDA float64 [ne][nq] (CoefficientVector)."""
+
+    def __init__(self, values):
+        self.values = values
+
+
+class AffineGridFunctionCoefficient:
+    """scale * (1 + slope * (T(x) - t_ref)) with T an H1 grid function (CUDA L-vector).
+
+    The Pennes conductivity law k(T) = k0 (1 + a (T - T0)) times gamma*dt."""
+
+    def __init__(self, T, scale=1.0, slope=0.0, t_ref=0.0):
+        self.T, self.scale, self.slope, self.t_ref = T, float(scale), float(slope), float(t_ref)
+
+
+class MassIntegrator:
+    kind = MASS
+
+    def __init__(self, coeff=None):
+        self.coeff = coeff if coeff is not None else ConstantCoefficient(1.0)
+
+
+class DiffusionIntegrator:
+    kind = DIFFUSION
+
+    def __init__(self, coeff=None):
+        self.coeff = coeff if coeff is not None else ConstantCoefficient(1.0)
+
+
+class AssemblyLevel:
+    PARTIAL = "partial"
+
+
+class BilinearForm:
+    """BilinearForm at AssemblyLevel::PARTIAL backed by the HIP PA form."""
+
+    def __init__(self, fes: H1Space, kernel: int = KERNEL_AUTO, q1d: int = 0, geometry: str = "nodes"):
+        self.fes = fes
+        self._integs = []
+        self._kernel = kernel
+        self._keep = []
+        gm = fes.gather_map()
+        h = ctypes.c_void_p()
+        _check(load_library().ecm2_pa_form_create(fes.ne, fes.order, fes.ndofs, _np_ptr(gm), q1d, ctypes.byref(h)))
+        self._h = h
+        if geometry == "nodes":
+            en = fes.mesh.element_nodes()
+            _check(_lib.ecm2_pa_form_set_element_nodes(h, _np_ptr(en)))
+        _check(_lib.ecm2_pa_form_set_kernel(h, kernel))
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.ecm2_pa_form_destroy(self._h)
+            self._h = None
+
+    def SetAssemblyLevel(self, level):
+        if level != AssemblyLevel.PARTIAL:
+            raise ECM2Error("only AssemblyLevel::PARTIAL is implemented")
+
+    def SetJacobians(self, J):
+        """GeometricFactors::JACOBIANS (NQ x 3 x 3 x NE, torch CUDA)."""
+        self._keep.append(J)
+        _check(_lib.ecm2_pa_form_set_jacobians(self._h, _dev_ptr(J)))
+
+    def AddDomainIntegrator(self, integ):
+        c = integ.coeff
+        if isinstance(c, ConstantCoefficient):
+            arr = (ctypes.c_double * 1)(c.value)
+            _check(_lib.ecm2_pa_form_add_integrator(self._h, integ.kind, COEFF_CONSTANT, ctypes.cast(arr, ctypes.c_void_p), None))
+        elif isinstance(c, QuadratureCoefficient):
+            self._keep.append(c.values)
+            _check(_lib.ecm2_pa_form_add_integrator(self._h, integ.kind, COEFF_QUAD, _dev_ptr(c.values), None))
+        elif isinstance(c, AffineGridFunctionCoefficient):
+            self._keep.append(c.T)
+            params = (ctypes.c_double * 3)(c.scale, c.slope, c.t_ref)
+            _check(_lib.ecm2_pa_form_add_integrator(self._h, integ.kind, COEFF_GRIDFUNC_AFFINE, _dev_ptr(c.T), ctypes.cast(params, ctypes.c_void_p)))
+        else:
+            raise ECM2Error(f"unsupported coefficient {type(c).__name__}")
+        self._integs.append(integ)
+
+    def Assemble(self, stream=None):
+        _check(_lib.ecm2_pa_form_assemble(self._h, _stream(stream)))
+
+    def Mult(self, x, y, stream=None):
+        _check(_lib.ecm2_pa_form_mult(self._h, _dev_ptr(x), _dev_ptr(y), _stream(stream)))
+
+    def AssembleDiagonal(self, diag, stream=None):
+        _check(_lib.ecm2_pa_form_assemble_diagonal(self._h, _dev_ptr(diag), _stream(stream)))
+
+    def RestrictionMult(self, x, xe, stream=None):
+        _check(_lib.ecm2_pa_form_restriction_mult(self._h, _dev_ptr(x), _dev_ptr(xe), _stream(stream)))
+
+    def RestrictionMultTranspose(self, xe, y, stream=None):
+        _check(_lib.ecm2_pa_form_restriction_mult_transpose(self._h, _dev_ptr(xe), _dev_ptr(y), _stream(stream)))
+
+    def IntegratorAddMultPA(self, kind, xe, ye, stream=None):
+        _check(_lib.ecm2_pa_form_integrator_add_mult(self._h, kind, _dev_ptr(xe), _dev_ptr(ye), _stream(stream)))
+
+    def qdata(self, kind) -> np.ndarray:
+        info = self.info()
+        nq = info["q1d"] ** 3
+        nc = 6 if kind == DIFFUSION else 1
+        out = np.empty((self.fes.ne, nc, nq), np.float64)
+        _check(_lib.ecm2_pa_form_get_qdata(self._h, kind, _np_ptr(out), _stream()))
+        return out
+
+    def info(self) -> dict:
+        v = [ctypes.c_int() for _ in range(6)]
+        _check(_lib.ecm2_pa_form_info(self._h, *[ctypes.byref(a) for a in v]))
+        return dict(zip(["ne", "ndofs", "d1d", "q1d", "kernel", "layout"], [a.value for a in v]))
+
+    def timing(self, enable: bool):
+        _check(_lib.ecm2_pa_form_timing(self._h, 1 if enable else 0))
+
+    def timing_get(self):
+        ms, n = ctypes.c_double(), ctypes.c_long()
+        _check(_lib.ecm2_pa_form_timing_get(self._h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def algorithmic_bytes(self) -> float:
+        b = ctypes.c_double()
+        _check(_lib.ecm2_pa_form_algorithmic_bytes(self._h, ctypes.byref(b)))
+        return b.value
+
+    def PCG(self, b, x, ess=None, rel_tol=1e-12, abs_tol=0.0, max_iter=1000, jacobi=True, stream=None):
+        """ConstrainedOperator(DIAG_ONE) + CGSolver(+OperatorJacobiSmoother); returns (iters, final_norm)."""
+        it, nrm = ctypes.c_int(), ctypes.c_double()
+        n_ess = 0 if ess is None else int(ess.numel())
+        _check(_lib.ecm2_pcg_solve(self._h, _dev_ptr(ess) if n_ess else None, n_ess, _dev_ptr(b), _dev_ptr(x),
+                                   rel_tol, abs_tol, max_iter, 1 if jacobi else 0,
+                                   ctypes.byref(it), ctypes.byref(nrm), _stream(stream)))
+        return it.value, nrm.value

@@ -1,0 +1,118 @@
+// kernels.hpp -- host launchers for the gfx950 HIP kernels (pa_kernels.hip).
+//
+// Quadrature-data layouts (the qdata a PA form owns):
+//  * BLOCKED (fused thread-per-element kernel): elements in blocks of 64 (one
+//    wave; lane = element).  diffusion: [blk][q][pair 0..2][lane][2] holding the
+//    symmetric entries (11,12),(13,22),(23,33); mass: [blk][q/2][lane][2] (two
+//    consecutive quadrature points per 16-byte slot).  Every wave-instruction
+//    is one 1 KiB contiguous dwordx4 load.
+//  * NATIVE (the reference's own layout): diffusion D(q,s,e) = [e][6][NQ],
+//    mass v(q,e) = [e][NQ] (bilininteg_diffusion_kernels.cpp:356-361,
+//    bilininteg_mass_pa.cpp:66-77).
+#pragma once
+
+#include "common.hpp"
+#include "fe.hpp"
+
+namespace ecm2
+{
+
+enum QLayoutKind : int { QLAYOUT_NATIVE = 0, QLAYOUT_BLOCKED = 1 };
+
+constexpr int kElemBlock = 64;  // elements per wave in the blocked layout
+
+struct QLayout
+{
+   int kind = QLAYOUT_NATIVE;
+   int ne = 0, nq = 0;
+   size_t diff_size() const
+   {
+      if (kind == QLAYOUT_NATIVE) { return (size_t)ne * 6 * nq; }
+      return (size_t)nblk() * nq * 6 * kElemBlock;
+   }
+   size_t mass_size() const
+   {
+      if (kind == QLAYOUT_NATIVE) { return (size_t)ne * nq; }
+      return (size_t)nblk() * ((nq + 1) / 2) * 2 * kElemBlock;
+   }
+   int nblk() const { return (ne + kElemBlock - 1) / kElemBlock; }
+};
+
+// Coefficient descriptor for qdata setup: constant, per-quadrature-point array
+// ([e][q], CoefficientVector COMPRESSED storage, coefficient.cpp:2006-2180), or
+// an affine function of an H1 grid function interpolated at the quadrature
+// points: c = scale * (1 + slope * (T(x_q) - t_ref))  (GridFunctionCoefficient,
+// coefficient.cpp:250-253, composed with the Pennes k(T) law).
+enum CoeffKind : int { COEFF_CONSTANT = 0, COEFF_QUAD = 1, COEFF_GRIDFUNC_AFFINE = 2 };
+struct CoeffDesc
+{
+   int kind = COEFF_CONSTANT;
+   double value = 1.0;           // constant
+   const double *quad = nullptr; // device [ne][nq]
+   const double *lvec = nullptr; // device L-vector of T
+   double scale = 1.0, slope = 0.0, t_ref = 0.0;
+};
+
+namespace kern
+{
+// ---- setup (S1/S2/S3 equivalents) ----
+// Evaluate a grid-function coefficient at quadrature points into out[e][q].
+void coeff_gridfunc(int ne, int D, int Q, const int *gmap_native, const Basis1D &b,
+                    const CoeffDesc &c, double *out, hipStream_t s);
+// qdata from lexicographic element corner coordinates enodes[e][3][8].
+void setup_from_nodes(const QLayout &L, int Q, const double *enodes, const double *W,
+                      const Basis1D &b1, const CoeffDesc *cm, const CoeffDesc *cd,
+                      const double *cm_q, const double *cd_q,
+                      double *qd_diff, double *qd_mass, hipStream_t s);
+// qdata from MFEM-layout Jacobians J(q,i,j,e) (GeometricFactors::JACOBIANS).
+void setup_from_jacobians(const QLayout &L, const double *J, const double *W,
+                          const CoeffDesc *cm, const CoeffDesc *cd,
+                          const double *cm_q, const double *cd_q,
+                          double *qd_diff, double *qd_mass, hipStream_t s);
+
+// ---- apply ----
+// Fused y = R^T (M + K) R x, thread-per-element (blocked layout); y must be zeroed.
+void apply_tpe(int D, int Q, bool mass, bool diff, int ne, const int *gmap_blocked,
+               const double *qd_diff, const double *qd_mass, const double *x, double *y,
+               const Basis1D &b, const double *rowtab, hipStream_t s);
+// Row table for apply_tpe: [qz][qy][3][dz][dy] products (see pa_kernels.hip).
+std::vector<double> make_row_table(const DofToQuad &m);
+// Workgroup-per-element kernel, any layout; in/out either L-vectors (through the
+// gather map; output by atomics into a zeroed y) or E-vectors (accumulated).
+void apply_wpe(int D, int Q, bool mass, bool diff, int layout, int ne, const int *gmap_native,
+               const double *qd_diff, const double *qd_mass, const double *x, double *y,
+               bool in_evec, bool out_evec, const Basis1D &b, hipStream_t s);
+
+// ---- ElementRestriction ----
+void restriction_mult(long n, int nd, const int *gmap_native, const double *x, double *xe,
+                      hipStream_t s);
+void restriction_mult_transpose(int ndofs, int nd, const int *offsets, const int *indices,
+                                const double *xe, double *y, hipStream_t s);
+
+// ---- diagonal (Jacobi) ----
+void diagonal(int D, int Q, int layout, int ne, const int *gmap_native, const double *qd_diff,
+              const double *qd_mass, double *diag, bool out_evec, const Basis1D &b,
+              hipStream_t s);
+
+// ---- vector kernels for the device PCG ----
+void set_values(int n, const int *idx, double val, double *y, hipStream_t s);     // y[idx] = val
+void copy_values(int n, const int *idx, const double *x, double *y, hipStream_t s); // y[idx] = x[idx]
+// Deterministic two-pass dot: result written to *out (device).
+void dot(int n, const double *a, const double *b, double *partials, double *out, hipStream_t s);
+// PCG updates with device-resident scalars (no host round trip):
+//   x += (nom/den) d ; r -= (nom/den) z
+void pcg_update_xr(int n, const double *nom, const double *den, const double *d,
+                   const double *z, double *x, double *r, hipStream_t s);
+//   z = dinv .* r  (dinv may be null -> z = r)
+void pcg_precond(int n, const double *dinv, const double *r, double *z, hipStream_t s);
+//   d = z + (betanom/nom) d
+void pcg_update_d(int n, const double *betanom, const double *nom, const double *z, double *d,
+                  hipStream_t s);
+void reciprocal(int n, const double *a, double *out, hipStream_t s);
+// Halo pack/unpack for the distributed operator (K7): buf[i] = x[idx[i]] ; y[idx[i]] += buf[i]
+void gather_idx(int n, const int *idx, const double *x, double *buf, hipStream_t s);
+void scatter_add_idx(int n, const int *idx, const double *buf, double *y, hipStream_t s);
+void scatter_set_idx(int n, const int *idx, const double *buf, double *y, hipStream_t s);
+} // namespace kern
+
+} // namespace ecm2

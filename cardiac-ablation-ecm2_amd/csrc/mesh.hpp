@@ -1,0 +1,57 @@
+// mesh.hpp -- trilinear hexahedral meshes and the H1 (Gauss-Lobatto) dof numbering.
+//
+// Setup side of the boundary (reference rows a7/a8 and SURVEY §8(f) rank 4):
+//   Mesh::Make3D / MakeCartesian3D     mesh/mesh.cpp:3683-3830 (vertex + element layout)
+//   MFEM mesh v1.0 / INLINE readers     mesh/mesh_readers.cpp:1356-1506
+//   Mesh::UniformRefinement (hex)       mesh/mesh.cpp:11403
+//   FiniteElementSpace dof numbering    fem/fespace.cpp:2767 (vertices, edges, faces, interiors)
+//   lexicographic element dof map       fem/restriction.cpp:26-107 (gather_map semantics)
+//   Mesh::CartesianPartitioning          mesh/mesh.cpp:8966 (slab split used for multi-GPU)
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace ecm2
+{
+
+// Native hex vertex order (MFEM Hexahedron): 0:(0,0,0) 1:(1,0,0) 2:(1,1,0) 3:(0,1,0)
+// 4:(0,0,1) 5:(1,0,1) 6:(1,1,1) 7:(0,1,1).  Lexicographic corner a = ax + 2ay + 4az.
+extern const int kLexToNative[8];
+
+struct HexMesh
+{
+   int nv = 0, ne = 0;
+   std::vector<double> vert;   // [nv][3]
+   std::vector<int> elem;      // [ne][8] native order
+   std::vector<int> attr;      // [ne]
+   // Cartesian provenance (for the structured numbering); nx = 0 when unstructured.
+   int nx = 0, ny = 0, nz = 0;
+
+   static HexMesh cartesian(int nx, int ny, int nz, double sx, double sy, double sz);
+   static HexMesh read(const std::string &path);
+   void refine_uniform();
+   // Corner coordinates in lexicographic order: out[e][c][a] (a = lex corner).
+   void element_nodes(std::vector<double> &out) const;
+};
+
+enum Numbering : int
+{
+   NUMBERING_ENTITY = 0,     // vertex -> edge -> face -> interior (MFEM fespace order)
+   NUMBERING_STRUCTURED = 1  // lattice (I + NX(J + NY K)) on a Cartesian mesh
+};
+
+struct H1Space
+{
+   int order = 0, ne = 0, nd = 0, ndofs = 0;
+   int numbering = NUMBERING_ENTITY;
+   std::vector<int> gather_map;   // [ne][nd] lexicographic, MFEM gather_map semantics
+   std::vector<int> bdr_dofs;     // sorted dofs on boundary faces (ess_tdof_list for ess_bdr = all)
+
+   static H1Space build(const HexMesh &m, int order, int numbering);
+   // Physical coordinates of every dof (from the element trilinear map at GLL nodes).
+   void dof_coords(const HexMesh &m, std::vector<double> &out) const;
+};
+
+} // namespace ecm2

@@ -1,0 +1,425 @@
+// pa_form.cpp -- see pa_form.hpp.
+#include "pa_form.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+namespace ecm2
+{
+
+void require_device()
+{
+   int n = 0;
+   const hipError_t e = hipGetDeviceCount(&n);
+   ECM2_VERIFY(e == hipSuccess && n > 0, ERR_HIP,
+               "no HIP device available (the PA path has no CPU fallback)");
+}
+
+PAForm::PAForm(int ne, int order, int ndofs, const int *gather_map_host, int q1d)
+   : ne_(ne), order_(order), ndofs_(ndofs)
+{
+   ECM2_VERIFY(ne >= 0 && ndofs >= 0, ERR_ARG, "negative sizes");
+   ECM2_VERIFY(order >= 1 && order + 1 <= MAX_D1D, ERR_ARG, "unsupported order " << order);
+   ECM2_VERIFY(ne == 0 || gather_map_host != nullptr, ERR_ARG, "null gather map");
+   require_device();
+   D_ = order + 1;
+   Q_ = q1d > 0 ? q1d : default_q1d(order);
+   ECM2_VERIFY(Q_ >= D_ && Q_ <= MAX_Q1D, ERR_ARG, "q1d must satisfy p+1 <= q1d <= " << MAX_Q1D);
+   ND_ = D_ * D_ * D_;
+   NQ_ = Q_ * Q_ * Q_;
+   maps_ = make_dof_to_quad(order, Q_);
+   basis_ = make_basis1d(maps_);
+   basis1_ = make_basis1d(make_dof_to_quad(1, Q_));
+   gmap_host_.assign(gather_map_host, gather_map_host + (size_t)ne * ND_);
+   for (int g : gmap_host_)
+   {
+      const int d = g >= 0 ? g : -1 - g;
+      ECM2_VERIFY(d >= 0 && d < ndofs, ERR_ARG, "gather map entry " << g << " out of range [0," << ndofs << ")");
+   }
+   gmap_.upload(gmap_host_);
+   W_.upload(maps_.W);
+   layout_.ne = ne;
+   layout_.nq = NQ_;
+}
+
+PAForm::~PAForm()
+{
+   for (auto &e : ev_start_) { (void)hipEventDestroy(e); }
+   for (auto &e : ev_stop_) { (void)hipEventDestroy(e); }
+}
+
+void PAForm::set_element_nodes(const double *enodes_host)
+{
+   ECM2_VERIFY(ne_ == 0 || enodes_host, ERR_ARG, "null element nodes");
+   enodes_.upload(enodes_host, (size_t)ne_ * 24);
+   ECM2_HIP(hipDeviceSynchronize());
+   jac_ = nullptr;
+   assembled_ = false;
+}
+
+void PAForm::set_jacobians(const double *J_device)
+{
+   ECM2_VERIFY(ne_ == 0 || J_device, ERR_ARG, "null Jacobian array");
+   jac_ = J_device;
+   assembled_ = false;
+}
+
+void PAForm::add_integrator(int kind, const CoeffDesc &c)
+{
+   ECM2_VERIFY(kind == INTEG_MASS || kind == INTEG_DIFFUSION, ERR_ARG, "unknown integrator " << kind);
+   ECM2_VERIFY(c.kind == COEFF_CONSTANT || c.kind == COEFF_QUAD || c.kind == COEFF_GRIDFUNC_AFFINE,
+               ERR_ARG, "unknown coefficient kind " << c.kind);
+   ECM2_VERIFY(c.kind != COEFF_QUAD || ne_ == 0 || c.quad, ERR_ARG, "null quadrature coefficient");
+   ECM2_VERIFY(c.kind != COEFF_GRIDFUNC_AFFINE || ndofs_ == 0 || c.lvec, ERR_ARG, "null grid function");
+   if (kind == INTEG_MASS)
+   {
+      ECM2_VERIFY(!have_mass_, ERR_UNSUPPORTED, "a MassIntegrator is already present");
+      have_mass_ = true;
+      cmass_ = c;
+   }
+   else
+   {
+      ECM2_VERIFY(!have_diff_, ERR_UNSUPPORTED, "a DiffusionIntegrator is already present");
+      have_diff_ = true;
+      cdiff_ = c;
+   }
+   assembled_ = false;
+}
+
+void PAForm::set_kernel(int mode)
+{
+   ECM2_VERIFY(mode >= KERNEL_AUTO && mode <= KERNEL_UNFUSED, ERR_ARG, "unknown kernel mode " << mode);
+   mode_ = mode;
+   assembled_ = false;
+}
+
+static bool has_tpe(int D, int Q) { return (D == 2 && Q == 3) || (D == 3 && Q == 4); }
+
+void PAForm::assemble(hipStream_t s)
+{
+   ECM2_VERIFY(enodes_.size() || jac_ || ne_ == 0, ERR_STATE, "assemble: no geometry set");
+   resolved_mode_ = mode_;
+   if (mode_ == KERNEL_AUTO) { resolved_mode_ = has_tpe(D_, Q_) ? KERNEL_TPE : KERNEL_WPE; }
+   ECM2_VERIFY(resolved_mode_ != KERNEL_TPE || has_tpe(D_, Q_), ERR_UNSUPPORTED,
+               "thread-per-element kernel needs (D1D,Q1D) in {(2,3),(3,4)}");
+   layout_.kind = (resolved_mode_ == KERNEL_TPE) ? QLAYOUT_BLOCKED : QLAYOUT_NATIVE;
+
+   if (resolved_mode_ == KERNEL_TPE && !gmap_blk_.size() && ne_ > 0)
+   {
+      const int nblk = layout_.nblk();
+      std::vector<int> blk((size_t)nblk * ND_ * 64, 0);
+      for (int e = 0; e < ne_; e++)
+      {
+         const int b = e / 64, l = e % 64;
+         for (int a = 0; a < ND_; a++)
+         {
+            blk[((size_t)b * ND_ + a) * 64 + l] = gmap_host_[(size_t)e * ND_ + a];
+         }
+      }
+      gmap_blk_.upload(blk, s);
+      rowtab_.upload(kern::make_row_table(maps_), s);
+      ECM2_HIP(hipStreamSynchronize(s));
+   }
+   qd_diff_.resize(have_diff_ ? layout_.diff_size() : 0);
+   qd_mass_.resize(have_mass_ ? layout_.mass_size() : 0);
+   if (qd_diff_.size()) { ECM2_HIP(hipMemsetAsync(qd_diff_.data(), 0, qd_diff_.bytes(), s)); }
+   if (qd_mass_.size()) { ECM2_HIP(hipMemsetAsync(qd_mass_.data(), 0, qd_mass_.bytes(), s)); }
+
+   // Coefficient values at quadrature points (CoefficientVector::Project).
+   auto coeff_values = [&](const CoeffDesc &c, DeviceArray<double> &tmp) -> const double * {
+      if (c.kind == COEFF_QUAD) { return c.quad; }
+      if (c.kind == COEFF_GRIDFUNC_AFFINE)
+      {
+         tmp.resize((size_t)ne_ * NQ_);
+         kern::coeff_gridfunc(ne_, D_, Q_, gmap_.data(), basis_, c, tmp.data(), s);
+         return tmp.data();
+      }
+      return nullptr;
+   };
+   const double *cm_q = have_mass_ ? coeff_values(cmass_, ctmp_m_) : nullptr;
+   const double *cd_q = have_diff_ ? coeff_values(cdiff_, ctmp_d_) : nullptr;
+   const CoeffDesc *cm = have_mass_ ? &cmass_ : nullptr;
+   const CoeffDesc *cd = have_diff_ ? &cdiff_ : nullptr;
+   if (jac_)
+   {
+      kern::setup_from_jacobians(layout_, jac_, W_.data(), cm, cd, cm_q, cd_q, qd_diff_.data(),
+                                 qd_mass_.data(), s);
+   }
+   else
+   {
+      kern::setup_from_nodes(layout_, Q_, enodes_.data(), W_.data(), basis1_, cm, cd, cm_q, cd_q,
+                             qd_diff_.data(), qd_mass_.data(), s);
+   }
+   assembled_ = true;
+}
+
+void PAForm::record_start(hipStream_t s)
+{
+   if (!timing_) { return; }
+   if (ev_count_ >= ev_start_.size())
+   {
+      hipEvent_t a, b;
+      ECM2_HIP(hipEventCreate(&a));
+      ECM2_HIP(hipEventCreate(&b));
+      ev_start_.push_back(a);
+      ev_stop_.push_back(b);
+   }
+   ECM2_HIP(hipEventRecord(ev_start_[ev_count_], s));
+}
+
+void PAForm::record_stop(hipStream_t s)
+{
+   if (!timing_) { return; }
+   ECM2_HIP(hipEventRecord(ev_stop_[ev_count_], s));
+   ev_count_++;
+}
+
+void PAForm::timing_enable(bool on)
+{
+   timing_ = on;
+   ev_count_ = 0;
+}
+
+void PAForm::timing_get(double *total_ms, long *launches)
+{
+   double t = 0.0;
+   for (size_t i = 0; i < ev_count_; i++)
+   {
+      ECM2_HIP(hipEventSynchronize(ev_stop_[i]));
+      float ms = 0.f;
+      ECM2_HIP(hipEventElapsedTime(&ms, ev_start_[i], ev_stop_[i]));
+      t += ms;
+   }
+   if (total_ms) { *total_ms = t; }
+   if (launches) { *launches = (long)ev_count_; }
+}
+
+size_t PAForm::algorithmic_bytes() const
+{
+   // 8*NE*NQ*(6+1) qdata + 8*ndofs (x) + 8*ndofs (y) + 4*NE*ND (map).
+   const size_t nc = (have_diff_ ? 6 : 0) + (have_mass_ ? 1 : 0);
+   return 8ull * ne_ * NQ_ * nc + 16ull * ndofs_ + 4ull * ne_ * ND_;
+}
+
+void PAForm::ensure_csr()
+{
+   if (csr_off_.size() || ndofs_ == 0) { return; }
+   // ElementRestriction ctor CSR build (restriction.cpp:68-106).
+   std::vector<int> off(ndofs_ + 1, 0), idx((size_t)ne_ * ND_);
+   for (int g : gmap_host_) { off[(g >= 0 ? g : -1 - g) + 1]++; }
+   for (int i = 1; i <= ndofs_; i++) { off[i] += off[i - 1]; }
+   for (size_t lid = 0; lid < gmap_host_.size(); lid++)
+   {
+      const int g = gmap_host_[lid];
+      const int d = g >= 0 ? g : -1 - g;
+      idx[off[d]++] = g >= 0 ? (int)lid : (int)(-1 - (long)lid);
+   }
+   for (int i = ndofs_; i > 0; i--) { off[i] = off[i - 1]; }
+   off[0] = 0;
+   csr_off_.upload(off);
+   csr_idx_.upload(idx);
+   ECM2_HIP(hipDeviceSynchronize());
+}
+
+void PAForm::ensure_work(hipStream_t)
+{
+   xe_.resize((size_t)ne_ * ND_);
+   ye_.resize((size_t)ne_ * ND_);
+}
+
+void PAForm::mult(const double *x, double *y, hipStream_t s)
+{
+   ECM2_VERIFY(assembled_, ERR_STATE, "Mult before Assemble");
+   ECM2_VERIFY(ndofs_ == 0 || (x && y), ERR_ARG, "null vector");
+   if (ndofs_ == 0) { return; }
+   const bool m = have_mass_, d = have_diff_;
+   if (resolved_mode_ == KERNEL_UNFUSED)
+   {
+      // PABilinearFormExtension::MultInternal, bilinearform_ext.cpp:527-560.
+      ensure_work(s);
+      ensure_csr();
+      record_start(s);
+      kern::restriction_mult((long)ne_ * ND_, ND_, gmap_.data(), x, xe_.data(), s);
+      if (ne_) { ECM2_HIP(hipMemsetAsync(ye_.data(), 0, ye_.bytes(), s)); }
+      if (m)
+      {
+         kern::apply_wpe(D_, Q_, true, false, layout_.kind, ne_, gmap_.data(), qd_diff_.data(),
+                         qd_mass_.data(), xe_.data(), ye_.data(), true, true, basis_, s);
+      }
+      if (d)
+      {
+         kern::apply_wpe(D_, Q_, false, true, layout_.kind, ne_, gmap_.data(), qd_diff_.data(),
+                         qd_mass_.data(), xe_.data(), ye_.data(), true, true, basis_, s);
+      }
+      kern::restriction_mult_transpose(ndofs_, ND_, csr_off_.data(), csr_idx_.data(), ye_.data(), y, s);
+      record_stop(s);
+      return;
+   }
+   ECM2_HIP(hipMemsetAsync(y, 0, sizeof(double) * (size_t)ndofs_, s));
+   if (!m && !d) { return; }
+   record_start(s);
+   if (resolved_mode_ == KERNEL_TPE)
+   {
+      kern::apply_tpe(D_, Q_, m, d, ne_, gmap_blk_.data(), qd_diff_.data(), qd_mass_.data(), x, y,
+                      basis_, rowtab_.data(), s);
+   }
+   else
+   {
+      kern::apply_wpe(D_, Q_, m, d, layout_.kind, ne_, gmap_.data(), qd_diff_.data(),
+                      qd_mass_.data(), x, y, false, false, basis_, s);
+   }
+   record_stop(s);
+}
+
+void PAForm::assemble_diagonal(double *diag, hipStream_t s)
+{
+   ECM2_VERIFY(assembled_, ERR_STATE, "AssembleDiagonal before Assemble");
+   if (ndofs_ == 0) { return; }
+   ECM2_HIP(hipMemsetAsync(diag, 0, sizeof(double) * (size_t)ndofs_, s));
+   kern::diagonal(D_, Q_, layout_.kind, ne_, gmap_.data(), have_diff_ ? qd_diff_.data() : nullptr,
+                  have_mass_ ? qd_mass_.data() : nullptr, diag, false, basis_, s);
+}
+
+void PAForm::restriction_mult(const double *x, double *xe, hipStream_t s)
+{
+   kern::restriction_mult((long)ne_ * ND_, ND_, gmap_.data(), x, xe, s);
+}
+
+void PAForm::restriction_mult_transpose(const double *xe, double *y, hipStream_t s)
+{
+   ensure_csr();
+   kern::restriction_mult_transpose(ndofs_, ND_, csr_off_.data(), csr_idx_.data(), xe, y, s);
+}
+
+void PAForm::integrator_add_mult(int kind, const double *xe, double *ye, hipStream_t s)
+{
+   ECM2_VERIFY(assembled_, ERR_STATE, "AddMultPA before Assemble");
+   ECM2_VERIFY((kind == INTEG_MASS && have_mass_) || (kind == INTEG_DIFFUSION && have_diff_),
+               ERR_ARG, "integrator " << kind << " not present");
+   kern::apply_wpe(D_, Q_, kind == INTEG_MASS, kind == INTEG_DIFFUSION, layout_.kind, ne_,
+                   gmap_.data(), qd_diff_.data(), qd_mass_.data(), xe, ye, true, true, basis_, s);
+}
+
+void PAForm::get_qdata(int kind, double *out, hipStream_t s)
+{
+   ECM2_VERIFY(assembled_, ERR_STATE, "get_qdata before Assemble");
+   const bool diff = kind == INTEG_DIFFUSION;
+   ECM2_VERIFY(diff ? have_diff_ : have_mass_, ERR_ARG, "integrator " << kind << " not present");
+   DeviceArray<double> &src = diff ? qd_diff_ : qd_mass_;
+   std::vector<double> h(src.size());
+   if (src.size())
+   {
+      ECM2_HIP(hipMemcpyAsync(h.data(), src.data(), src.bytes(), hipMemcpyDeviceToHost, s));
+      ECM2_HIP(hipStreamSynchronize(s));
+   }
+   const int nc = diff ? 6 : 1;
+   for (int e = 0; e < ne_; e++)
+      for (int c = 0; c < nc; c++)
+         for (int q = 0; q < NQ_; q++)
+         {
+            size_t src_i;
+            if (layout_.kind == QLAYOUT_NATIVE) { src_i = ((size_t)e * nc + c) * NQ_ + q; }
+            else
+            {
+               const int blk = e / 64, lane = e % 64;
+               if (diff) { src_i = (((size_t)blk * NQ_ + q) * 3 + c / 2) * 128 + lane * 2 + (c & 1); }
+               else { src_i = ((size_t)blk * ((NQ_ + 1) / 2) + q / 2) * 128 + lane * 2 + (q & 1); }
+            }
+            out[((size_t)e * nc + c) * NQ_ + q] = h[src_i];
+         }
+}
+
+// --------------------------------------------------------------------------
+// Device PCG
+// --------------------------------------------------------------------------
+
+PCGResult pcg_solve(PAForm &A, const int *ess, int n_ess, const double *b, double *x,
+                    double rel_tol, double abs_tol, int max_iter, bool jacobi, hipStream_t s)
+{
+   const int n = A.ndofs();
+   PCGResult res;
+   if (n == 0) { res.converged = true; return res; }
+   DeviceArray<double> r(n), d(n), z(n), zc(n), partials(1024), scal(4), dinv;
+   double *nom = scal.data(), *den = scal.data() + 1, *betanom = scal.data() + 2;
+   double *hs = nullptr;
+   ECM2_HIP(hipHostMalloc(&hs, 4 * sizeof(double)));
+   auto readback = [&](const double *dv) {
+      ECM2_HIP(hipMemcpyAsync(hs, dv, sizeof(double), hipMemcpyDeviceToHost, s));
+      ECM2_HIP(hipStreamSynchronize(s));
+      return hs[0];
+   };
+   // ConstrainedOperator::ConstrainedMult, DIAG_ONE.
+   auto cmult = [&](const double *in, double *out) {
+      if (n_ess == 0) { A.mult(in, out, s); return; }
+      ECM2_HIP(hipMemcpyAsync(zc.data(), in, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+      kern::set_values(n_ess, ess, 0.0, zc.data(), s);
+      A.mult(zc.data(), out, s);
+      kern::copy_values(n_ess, ess, in, out, s);
+   };
+   try
+   {
+      if (jacobi)
+      {
+         // OperatorJacobiSmoother on the constrained operator: ess rows get diag 1.
+         dinv.resize(n);
+         A.assemble_diagonal(z.data(), s);
+         if (n_ess) { kern::set_values(n_ess, ess, 1.0, z.data(), s); }
+         kern::reciprocal(n, z.data(), dinv.data(), s);
+      }
+      ECM2_HIP(hipMemcpyAsync(r.data(), b, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+      ECM2_HIP(hipMemsetAsync(x, 0, sizeof(double) * n, s));
+      if (jacobi)
+      {
+         kern::pcg_precond(n, dinv.data(), r.data(), z.data(), s);
+         ECM2_HIP(hipMemcpyAsync(d.data(), z.data(), sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+      }
+      else
+      {
+         ECM2_HIP(hipMemcpyAsync(d.data(), r.data(), sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+      }
+      kern::dot(n, d.data(), r.data(), partials.data(), nom, s);
+      const double nom0 = readback(nom);
+      res.initial_norm = nom0 >= 0 ? std::sqrt(nom0) : nom0;
+      const double r0 = std::max(nom0 * rel_tol * rel_tol, abs_tol * abs_tol);
+      res.final_norm = res.initial_norm;
+      if (nom0 <= r0) { res.converged = true; }
+      else
+      {
+         cmult(d.data(), z.data());
+         kern::dot(n, z.data(), d.data(), partials.data(), den, s);
+         if (readback(den) != 0.0)
+         {
+            for (int i = 1;;)
+            {
+               kern::pcg_update_xr(n, nom, den, d.data(), z.data(), x, r.data(), s);
+               if (jacobi)
+               {
+                  kern::pcg_precond(n, dinv.data(), r.data(), z.data(), s);
+                  kern::dot(n, r.data(), z.data(), partials.data(), betanom, s);
+               }
+               else { kern::dot(n, r.data(), r.data(), partials.data(), betanom, s); }
+               const double bn = readback(betanom);
+               res.final_norm = bn >= 0 ? std::sqrt(bn) : bn;
+               res.iterations = i;
+               if (bn <= r0) { res.converged = true; break; }
+               if (++i > max_iter) { break; }
+               kern::pcg_update_d(n, betanom, nom, jacobi ? z.data() : r.data(), d.data(), s);
+               cmult(d.data(), z.data());
+               kern::dot(n, d.data(), z.data(), partials.data(), den, s);
+               ECM2_HIP(hipMemcpyAsync(nom, betanom, sizeof(double), hipMemcpyDeviceToDevice, s));
+            }
+         }
+      }
+   }
+   catch (...)
+   {
+      (void)hipHostFree(hs);
+      throw;
+   }
+   ECM2_HIP(hipStreamSynchronize(s));
+   (void)hipHostFree(hs);
+   return res;
+}
+
+} // namespace ecm2

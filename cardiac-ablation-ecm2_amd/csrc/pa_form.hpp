@@ -1,0 +1,121 @@
+// pa_form.hpp -- MI355X PA form: the drop-in for the reference's
+// BilinearForm(PARTIAL) + {MassIntegrator(alpha), DiffusionIntegrator(beta)}
+// and its PABilinearFormExtension.
+//
+// Reference interface mirrored:
+//   PABilinearFormExtension::Assemble / Mult / AssembleDiagonal
+//                                          fem/bilinearform_ext.hpp:67-144, .cpp:332-564
+//   BilinearFormIntegrator::AssemblePA / AddMultPA / AssembleDiagonalPA
+//                                          fem/bilininteg.hpp:49-97
+//   ElementRestriction::Mult / MultTranspose fem/restriction.cpp:109-186
+// Ownership follows the reference: the form owns qdata and its work vectors;
+// x / y are caller-owned device arrays; all work is enqueued on the caller's
+// stream (the reference uses the null stream, forall.hpp:782).
+#pragma once
+
+#include "common.hpp"
+#include "fe.hpp"
+#include "kernels.hpp"
+
+#include <memory>
+#include <vector>
+
+namespace ecm2
+{
+
+enum KernelMode : int
+{
+   KERNEL_AUTO = 0,     // fused thread-per-element where available, else fused WPE
+   KERNEL_TPE = 1,      // fused, thread per element (p = 1, 2)
+   KERNEL_WPE = 2,      // fused, workgroup per element (any p)
+   KERNEL_UNFUSED = 3   // reference-shaped: restriction, per-integrator AddMultPA, CSR transpose
+};
+
+enum IntegratorKind : int { INTEG_MASS = 0, INTEG_DIFFUSION = 1 };
+
+class PAForm
+{
+public:
+   PAForm(int ne, int order, int ndofs, const int *gather_map_host, int q1d = 0);
+   ~PAForm();
+
+   int ne() const { return ne_; }
+   int order() const { return order_; }
+   int ndofs() const { return ndofs_; }
+   int d1d() const { return D_; }
+   int q1d() const { return Q_; }
+   int layout() const { return layout_.kind; }
+   int kernel_mode() const { return resolved_mode_; }
+
+   // Geometry: lexicographic corner coordinates (host, [ne][3][8]) or
+   // MFEM-layout Jacobians (device, NQ x 3 x 3 x NE; the pointer must stay
+   // valid until assemble()).
+   void set_element_nodes(const double *enodes_host);
+   void set_jacobians(const double *J_device);
+
+   void add_integrator(int kind, const CoeffDesc &c);
+   void set_kernel(int mode);
+   void assemble(hipStream_t s);
+
+   // y = A x (BilinearForm::Mult semantics: y overwritten).
+   void mult(const double *x, double *y, hipStream_t s);
+   void assemble_diagonal(double *diag, hipStream_t s);
+
+   // Reference-shaped pieces (E-vector layout [e][nd], lexicographic).
+   void restriction_mult(const double *x, double *xe, hipStream_t s);
+   void restriction_mult_transpose(const double *xe, double *y, hipStream_t s);
+   void integrator_add_mult(int kind, const double *xe, double *ye, hipStream_t s);
+   // qdata in the reference's native layout, copied to the host.
+   void get_qdata(int kind, double *out_host, hipStream_t s);
+
+   // HIP-event timing of the dominant (apply) kernel.
+   void timing_enable(bool on);
+   void timing_get(double *total_ms, long *launches);
+   size_t algorithmic_bytes() const;
+
+private:
+   void ensure_csr();
+   void ensure_work(hipStream_t s);
+   void record_start(hipStream_t s);
+   void record_stop(hipStream_t s);
+
+   int ne_, order_, ndofs_, D_, Q_, ND_, NQ_;
+   DofToQuad maps_;
+   Basis1D basis_, basis1_;
+   QLayout layout_;
+   int mode_ = KERNEL_AUTO, resolved_mode_ = KERNEL_AUTO;
+   bool assembled_ = false;
+   bool have_mass_ = false, have_diff_ = false;
+   CoeffDesc cmass_, cdiff_;
+
+   std::vector<int> gmap_host_;
+   DeviceArray<int> gmap_;          // native [e][nd]
+   DeviceArray<int> gmap_blk_;      // blocked [blk][nd][64]
+   DeviceArray<int> csr_off_, csr_idx_;
+   DeviceArray<double> enodes_;     // [e][3][8]
+   const double *jac_ = nullptr;    // device, not owned
+   DeviceArray<double> W_, rowtab_;
+   DeviceArray<double> qd_diff_, qd_mass_;
+   DeviceArray<double> xe_, ye_;    // unfused work E-vectors
+   DeviceArray<double> ctmp_m_, ctmp_d_;
+
+   bool timing_ = false;
+   std::vector<hipEvent_t> ev_start_, ev_stop_;
+   size_t ev_count_ = 0;
+};
+
+// Device PCG on the constrained operator (ConstrainedOperator DIAG_ONE,
+// operator.cpp:586-646; CGSolver::Mult solvers.cpp:869-1004) with optional
+// Jacobi preconditioning from the PA diagonal.  Scalars stay on the device;
+// one 8-byte read-back per iteration for the convergence test.
+struct PCGResult
+{
+   int iterations = 0;
+   double final_norm = 0.0, initial_norm = 0.0;
+   bool converged = false;
+};
+class Operator;
+PCGResult pcg_solve(PAForm &A, const int *ess_dev, int n_ess, const double *b, double *x,
+                    double rel_tol, double abs_tol, int max_iter, bool jacobi, hipStream_t s);
+
+} // namespace ecm2

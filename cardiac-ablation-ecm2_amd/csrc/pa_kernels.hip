@@ -1,0 +1,904 @@
+// pa_kernels.hip -- hand-written gfx950 (CDNA4) kernels for the PA diffusion+mass path.
+//
+// Hot path (reference K1..K5, SURVEY §2 "Device kernels on the path"):
+//   k_apply_tpe   fused gather -> B/G contractions -> Pennes/heat-capacity and
+//                 conductivity weighting -> transposed contractions -> scatter,
+//                 one THREAD per element, 64 elements per wave.  Replaces
+//                 ElementRestriction::Mult (restriction.cpp:109-129), the mass
+//                 and diffusion AddMultPA kernels (bilininteg_mass_kernels.hpp:809-1033,
+//                 bilininteg_diffusion_kernels.hpp:989-1214) and
+//                 ElementRestriction::MultTranspose (restriction.cpp:152-186) in
+//                 one pass over HBM.  qdata (95% of the bytes) is streamed once with
+//                 1 KiB-per-wave-instruction dwordx4 loads; the 1D contractions run
+//                 in registers (no LDS, no cross-lane traffic); the L-vector scatter
+//                 uses hardware FP64 atomics (global_atomic_add_f64).
+//   k_apply_wpe   one WORKGROUP per element (lane per quadrature point, LDS
+//                 between the six 1D stages), any order; also serves the
+//                 reference-shaped unfused API (E-vector in/out).
+// Setup (S1..S3): qdata from element corner coordinates or from MFEM-layout
+// Jacobians (PADiffusionSetup3D bilininteg_diffusion_kernels.cpp:243-367,
+// mass setup bilininteg_mass_pa.cpp:60-78, GeometricFactors mesh.cpp:15220-15273).
+#include "kernels.hpp"
+
+#include <hip/hip_runtime.h>
+
+namespace ecm2
+{
+namespace
+{
+
+constexpr int MQ = MAX_Q1D;
+typedef double v2d __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ size_t qidx_diff(int kind, int nq, int e, int c, int q)
+{
+   if (kind == QLAYOUT_NATIVE) { return ((size_t)e * 6 + c) * nq + q; }
+   const int blk = e >> 6, lane = e & 63;
+   return (((size_t)blk * nq + q) * 3 + (c >> 1)) * 128 + lane * 2 + (c & 1);
+}
+
+__device__ __forceinline__ size_t qidx_mass(int kind, int nq, int e, int q)
+{
+   if (kind == QLAYOUT_NATIVE) { return (size_t)e * nq + q; }
+   const int blk = e >> 6, lane = e & 63;
+   const int nqh = (nq + 1) >> 1;
+   return ((size_t)blk * nqh + (q >> 1)) * 128 + lane * 2 + (q & 1);
+}
+
+__device__ __forceinline__ int dof_of(int g) { return g >= 0 ? g : -1 - g; }
+
+// --------------------------------------------------------------------------
+// Setup kernels
+// --------------------------------------------------------------------------
+
+// c(e,q) = scale * (1 + slope * (T(x_q) - t_ref)),  T(x_q) = (B x B x B) T_e.
+__global__ void k_coeff_gridfunc(int ne, int D, int Q, const int *__restrict__ gmap,
+                                 const Basis1D b, const double *__restrict__ T, double scale,
+                                 double slope, double t_ref, double *__restrict__ out)
+{
+   const int NQ = Q * Q * Q, ND = D * D * D;
+   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   if (t >= (long)ne * NQ) { return; }
+   const int e = (int)(t / NQ), q = (int)(t % NQ);
+   const int qx = q % Q, qy = (q / Q) % Q, qz = q / (Q * Q);
+   double v = 0.0;
+   for (int dz = 0; dz < D; dz++)
+      for (int dy = 0; dy < D; dy++)
+         for (int dx = 0; dx < D; dx++)
+         {
+            const int g = gmap[(size_t)e * ND + (dz * D + dy) * D + dx];
+            const double tv = g >= 0 ? T[g] : -T[-1 - g];
+            v += b.B[qx + MQ * dx] * b.B[qy + MQ * dy] * b.B[qz + MQ * dz] * tv;
+         }
+   out[t] = scale * (1.0 + slope * (v - t_ref));
+}
+
+struct SetupCoef
+{
+   int has;          // integrator present
+   int is_const;
+   double value;
+   const double *quad;
+};
+
+__device__ __forceinline__ double coef_at(const SetupCoef &c, size_t eq)
+{
+   return c.is_const ? c.value : c.quad[eq];
+}
+
+// Write D (6 symmetric entries) and mass value at one quadrature point.
+__device__ __forceinline__ void write_qdata(int kind, int nq, int e, int q, double w,
+                                            const double J[3][3], const SetupCoef &cm,
+                                            const SetupCoef &cd, double *qd_diff,
+                                            double *qd_mass)
+{
+   const double J11 = J[0][0], J21 = J[1][0], J31 = J[2][0];
+   const double J12 = J[0][1], J22 = J[1][1], J32 = J[2][1];
+   const double J13 = J[0][2], J23 = J[1][2], J33 = J[2][2];
+   const double detJ = J11 * (J22 * J33 - J32 * J23) - J21 * (J12 * J33 - J32 * J13) +
+                       J31 * (J12 * J23 - J22 * J13);
+   const size_t eq = (size_t)e * nq + q;
+   if (cd.has)
+   {
+      const double w_detJ = w / detJ;
+      const double A11 = (J22 * J33) - (J23 * J32);
+      const double A12 = (J32 * J13) - (J12 * J33);
+      const double A13 = (J12 * J23) - (J22 * J13);
+      const double A21 = (J31 * J23) - (J21 * J33);
+      const double A22 = (J11 * J33) - (J13 * J31);
+      const double A23 = (J21 * J13) - (J11 * J23);
+      const double A31 = (J21 * J32) - (J31 * J22);
+      const double A32 = (J31 * J12) - (J11 * J32);
+      const double A33 = (J11 * J22) - (J12 * J21);
+      const double C = coef_at(cd, eq);
+      qd_diff[qidx_diff(kind, nq, e, 0, q)] = w_detJ * (C * A11 * A11 + C * A12 * A12 + C * A13 * A13);
+      qd_diff[qidx_diff(kind, nq, e, 1, q)] = w_detJ * (C * A11 * A21 + C * A12 * A22 + C * A13 * A23);
+      qd_diff[qidx_diff(kind, nq, e, 2, q)] = w_detJ * (C * A11 * A31 + C * A12 * A32 + C * A13 * A33);
+      qd_diff[qidx_diff(kind, nq, e, 3, q)] = w_detJ * (C * A21 * A21 + C * A22 * A22 + C * A23 * A23);
+      qd_diff[qidx_diff(kind, nq, e, 4, q)] = w_detJ * (C * A21 * A31 + C * A22 * A32 + C * A23 * A33);
+      qd_diff[qidx_diff(kind, nq, e, 5, q)] = w_detJ * (C * A31 * A31 + C * A32 * A32 + C * A33 * A33);
+   }
+   if (cm.has)
+   {
+      qd_mass[qidx_mass(kind, nq, e, q)] = w * coef_at(cm, eq) * detJ;
+   }
+}
+
+__global__ void k_setup_nodes(int kind, int ne, int Q, const double *__restrict__ enodes,
+                              const double *__restrict__ W, const Basis1D b1, SetupCoef cm,
+                              SetupCoef cd, double *__restrict__ qd_diff,
+                              double *__restrict__ qd_mass)
+{
+   const int NQ = Q * Q * Q;
+   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   if (t >= (long)ne * NQ) { return; }
+   const int e = (int)(t / NQ), q = (int)(t % NQ);
+   const int qx = q % Q, qy = (q / Q) % Q, qz = q / (Q * Q);
+   const double *X = enodes + (size_t)e * 24;
+   double J[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+   for (int a = 0; a < 8; a++)
+   {
+      const int ax = a & 1, ay = (a >> 1) & 1, az = a >> 2;
+      const double bx = b1.B[qx + MQ * ax], by = b1.B[qy + MQ * ay], bz = b1.B[qz + MQ * az];
+      const double gx = b1.G[qx + MQ * ax], gy = b1.G[qy + MQ * ay], gz = b1.G[qz + MQ * az];
+      const double dN0 = gx * by * bz, dN1 = bx * gy * bz, dN2 = bx * by * gz;
+      for (int i = 0; i < 3; i++)
+      {
+         const double xi = X[i * 8 + a];
+         J[i][0] += xi * dN0;
+         J[i][1] += xi * dN1;
+         J[i][2] += xi * dN2;
+      }
+   }
+   write_qdata(kind, NQ, e, q, W[q], J, cm, cd, qd_diff, qd_mass);
+}
+
+__global__ void k_setup_jac(int kind, int ne, int NQ, const double *__restrict__ Jg,
+                            const double *__restrict__ W, SetupCoef cm, SetupCoef cd,
+                            double *__restrict__ qd_diff, double *__restrict__ qd_mass)
+{
+   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   if (t >= (long)ne * NQ) { return; }
+   const int e = (int)(t / NQ), q = (int)(t % NQ);
+   double J[3][3];
+   for (int j = 0; j < 3; j++)
+      for (int i = 0; i < 3; i++) { J[i][j] = Jg[(((size_t)e * 3 + j) * 3 + i) * NQ + q]; }
+   write_qdata(kind, NQ, e, q, W[q], J, cm, cd, qd_diff, qd_mass);
+}
+
+// --------------------------------------------------------------------------
+// Fused apply, thread per element (blocked layout)
+// --------------------------------------------------------------------------
+
+// Per-(qy,qz) products of the 1D tables, [qz][qy][kind][dz][dy] with kind
+// 0: B(qy,dy)B(qz,dz)  1: G(qy,dy)B(qz,dz)  2: B(qy,dy)G(qz,dz).  Read by uniform
+// (scalar-cache) loads inside the row loop, so they cost no VGPRs.
+struct RowTable
+{
+   const double *p;
+};
+
+template <int D, int Q, bool MASS, bool DIFF>
+__global__ void __launch_bounds__(256)
+k_apply_tpe(int ne, int nblk, const int *__restrict__ gmap, const double *__restrict__ qdd,
+            const double *__restrict__ qdm, const double *__restrict__ x,
+            double *__restrict__ y, const Basis1D b, const double *__restrict__ rowtab)
+{
+   constexpr int ND = D * D * D, NQ = Q * Q * Q, NQH = (NQ + 1) / 2, DD = D * D;
+   const int lane = threadIdx.x & 63;
+   const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
+   if (blk >= nblk) { return; }  // wave-uniform
+   const int e = blk * 64 + lane;
+   const bool active = e < ne;
+   const int *mp = gmap + (size_t)blk * ND * 64 + lane;
+
+   // ---- gather (ElementRestriction::Mult) ----
+   double X[ND];
+#pragma unroll
+   for (int a = 0; a < ND; a++)
+   {
+      const int g = mp[a * 64];
+      const double v = x[dof_of(g)];
+      X[a] = g >= 0 ? v : -v;
+   }
+   double Yo[ND];
+#pragma unroll
+   for (int a = 0; a < ND; a++) { Yo[a] = 0.0; }
+
+   const double *qd = qdd + (size_t)blk * NQ * 3 * 128 + lane * 2;
+   const double *qm = qdm + (size_t)blk * NQH * 128 + lane * 2;
+
+#pragma unroll 1
+   for (int row = 0; row < Q * Q; row++)   // row = qy + Q*qz (wave-uniform)
+   {
+      const double *P = rowtab + (size_t)row * 3 * DD;   // uniform -> s_load
+      // qdata of the row's Q points: issue all loads first
+      v2d dq[Q][3];
+      double mq[Q];
+#pragma unroll
+      for (int qx = 0; qx < Q; qx++)
+      {
+         const int q = row * Q + qx;
+         if (DIFF)
+         {
+#pragma unroll
+            for (int k = 0; k < 3; k++)
+            {
+               dq[qx][k] = __builtin_nontemporal_load(
+                  reinterpret_cast<const v2d *>(qd + ((size_t)q * 3 + k) * 128));
+            }
+         }
+         if (MASS)
+         {
+            mq[qx] = qm[(size_t)(q >> 1) * 128 + (q & 1)];
+         }
+      }
+      // forward: Y00 = (B_y B_z) X, Y01 = (G_y B_z) X, Y10 = (B_y G_z) X
+      double Y00[D], Y01[D], Y10[D];
+#pragma unroll
+      for (int dx = 0; dx < D; dx++)
+      {
+         double u = 0.0, v = 0.0, w = 0.0;
+#pragma unroll
+         for (int dz = 0; dz < D; dz++)
+#pragma unroll
+            for (int dy = 0; dy < D; dy++)
+            {
+               const double c = X[(dz * D + dy) * D + dx];
+               u += P[0 * DD + dz * D + dy] * c;
+               if (DIFF)
+               {
+                  v += P[1 * DD + dz * D + dy] * c;
+                  w += P[2 * DD + dz * D + dy] * c;
+               }
+            }
+         Y00[dx] = u; Y01[dx] = v; Y10[dx] = w;
+      }
+      double T0[D], T1[D], T2[D];
+#pragma unroll
+      for (int dx = 0; dx < D; dx++) { T0[dx] = 0.0; T1[dx] = 0.0; T2[dx] = 0.0; }
+#pragma unroll
+      for (int qx = 0; qx < Q; qx++)
+      {
+         double u = 0.0, ux = 0.0, uy = 0.0, uz = 0.0;
+#pragma unroll
+         for (int dx = 0; dx < D; dx++)
+         {
+            const double bq = b.B[qx + MQ * dx], gq = b.G[qx + MQ * dx];
+            if (MASS) { u += bq * Y00[dx]; }
+            if (DIFF)
+            {
+               ux += gq * Y00[dx];
+               uy += bq * Y01[dx];
+               uz += bq * Y10[dx];
+            }
+         }
+         double m = 0.0, fx = 0.0, fy = 0.0, fz = 0.0;
+         if (MASS) { m = mq[qx] * u; }
+         if (DIFF)
+         {
+            // (11,12) (13,22) (23,33)
+            const v2d d0 = dq[qx][0], d1 = dq[qx][1], d2 = dq[qx][2];
+            fx = d0.x * ux + d0.y * uy + d1.x * uz;
+            fy = d0.y * ux + d1.y * uy + d2.x * uz;
+            fz = d1.x * ux + d2.x * uy + d2.y * uz;
+         }
+#pragma unroll
+         for (int dx = 0; dx < D; dx++)
+         {
+            const double bq = b.B[qx + MQ * dx], gq = b.G[qx + MQ * dx];
+            double t0 = T0[dx];
+            if (MASS) { t0 += bq * m; }
+            if (DIFF)
+            {
+               t0 += gq * fx;
+               T1[dx] += bq * fy;
+               T2[dx] += bq * fz;
+            }
+            T0[dx] = t0;
+         }
+      }
+      // transpose: Yo += (B_y B_z) T0 + (G_y B_z) T1 + (B_y G_z) T2
+#pragma unroll
+      for (int dz = 0; dz < D; dz++)
+#pragma unroll
+         for (int dy = 0; dy < D; dy++)
+         {
+            const double p0 = P[0 * DD + dz * D + dy];
+            const double p1 = P[1 * DD + dz * D + dy];
+            const double p2 = P[2 * DD + dz * D + dy];
+#pragma unroll
+            for (int dx = 0; dx < D; dx++)
+            {
+               double yo = Yo[(dz * D + dy) * D + dx] + p0 * T0[dx];
+               if (DIFF) { yo += p1 * T1[dx] + p2 * T2[dx]; }
+               Yo[(dz * D + dy) * D + dx] = yo;
+            }
+         }
+   }
+
+   // ---- scatter (ElementRestriction::MultTranspose) by FP64 atomics ----
+   if (active)
+   {
+#pragma unroll
+      for (int a = 0; a < ND; a++)
+      {
+         const int g = mp[a * 64];
+         unsafeAtomicAdd(y + dof_of(g), g >= 0 ? Yo[a] : -Yo[a]);
+      }
+   }
+}
+
+// --------------------------------------------------------------------------
+// Workgroup per element (lane per quadrature point), any layout, L- or E-vectors
+// --------------------------------------------------------------------------
+
+template <int D, int Q, bool MASS, bool DIFF, bool IN_E, bool OUT_E>
+__global__ void k_apply_wpe(int kind, int ne, const int *__restrict__ gmap,
+                            const double *__restrict__ qdd, const double *__restrict__ qdm,
+                            const double *__restrict__ x, double *__restrict__ y,
+                            const Basis1D b)
+{
+   constexpr int ND = D * D * D, NQ = Q * Q * Q;
+   __shared__ double sB[Q * D], sG[Q * D];
+   __shared__ double sX[ND];
+   __shared__ double s1a[D * D * Q], s1b[D * D * Q];
+   __shared__ double s2a[D * Q * Q], s2b[D * Q * Q], s2c[D * Q * Q];
+   __shared__ double s3m[NQ], s3x[NQ], s3y[NQ], s3z[NQ];
+   __shared__ double s4a[Q * Q * D], s4b[Q * Q * D], s4c[Q * Q * D];
+   __shared__ double s5a[Q * D * D], s5b[Q * D * D];
+   const int e = blockIdx.x;
+   const int t = threadIdx.x;
+   if (t < Q * D)
+   {
+      const int q = t % Q, d = t / Q;
+      sB[q + Q * d] = b.B[q + MQ * d];
+      sG[q + Q * d] = b.G[q + MQ * d];
+   }
+   if (t < ND)
+   {
+      if (IN_E) { sX[t] = x[(size_t)e * ND + t]; }
+      else
+      {
+         const int g = gmap[(size_t)e * ND + t];
+         const double v = x[dof_of(g)];
+         sX[t] = g >= 0 ? v : -v;
+      }
+   }
+   __syncthreads();
+   // stage 1: x-contraction  (qx, dy, dz)
+   if (t < D * D * Q)
+   {
+      const int qx = t % Q, dy = (t / Q) % D, dz = t / (Q * D);
+      double u = 0.0, v = 0.0;
+      for (int dx = 0; dx < D; dx++)
+      {
+         const double c = sX[(dz * D + dy) * D + dx];
+         u += c * sB[qx + Q * dx];
+         v += c * sG[qx + Q * dx];
+      }
+      s1a[t] = u;  // B_x
+      s1b[t] = v;  // G_x
+   }
+   __syncthreads();
+   // stage 2: y-contraction  (qx, qy, dz)
+   if (t < D * Q * Q)
+   {
+      const int qx = t % Q, qy = (t / Q) % Q, dz = t / (Q * Q);
+      double u = 0.0, v = 0.0, w = 0.0;
+      for (int dy = 0; dy < D; dy++)
+      {
+         const int i = (dz * D + dy) * Q + qx;
+         u += s1b[i] * sB[qy + Q * dy];   // G_x B_y
+         v += s1a[i] * sG[qy + Q * dy];   // B_x G_y
+         w += s1a[i] * sB[qy + Q * dy];   // B_x B_y
+      }
+      s2a[t] = u; s2b[t] = v; s2c[t] = w;
+   }
+   __syncthreads();
+   // stage 3: z-contraction + pointwise qdata (qx, qy, qz)
+   if (t < NQ)
+   {
+      const int qx = t % Q, qy = (t / Q) % Q, qz = t / (Q * Q);
+      double gx = 0.0, gy = 0.0, gz = 0.0, u = 0.0;
+      for (int dz = 0; dz < D; dz++)
+      {
+         const int i = (dz * Q + qy) * Q + qx;
+         gx += s2a[i] * sB[qz + Q * dz];
+         gy += s2b[i] * sB[qz + Q * dz];
+         gz += s2c[i] * sG[qz + Q * dz];
+         u += s2c[i] * sB[qz + Q * dz];
+      }
+      double m = 0.0, fx = 0.0, fy = 0.0, fz = 0.0;
+      if (MASS) { m = qdm[qidx_mass(kind, NQ, e, t)] * u; }
+      if (DIFF)
+      {
+         const double O11 = qdd[qidx_diff(kind, NQ, e, 0, t)];
+         const double O12 = qdd[qidx_diff(kind, NQ, e, 1, t)];
+         const double O13 = qdd[qidx_diff(kind, NQ, e, 2, t)];
+         const double O22 = qdd[qidx_diff(kind, NQ, e, 3, t)];
+         const double O23 = qdd[qidx_diff(kind, NQ, e, 4, t)];
+         const double O33 = qdd[qidx_diff(kind, NQ, e, 5, t)];
+         fx = (O11 * gx) + (O12 * gy) + (O13 * gz);
+         fy = (O12 * gx) + (O22 * gy) + (O23 * gz);
+         fz = (O13 * gx) + (O23 * gy) + (O33 * gz);
+      }
+      s3m[t] = m; s3x[t] = fx; s3y[t] = fy; s3z[t] = fz;
+   }
+   __syncthreads();
+   // stage 4: x-transpose (dx, qy, qz)
+   if (t < Q * Q * D)
+   {
+      const int dx = t % D, qy = (t / D) % Q, qz = t / (D * Q);
+      double u = 0.0, v = 0.0, w = 0.0;
+      for (int qx = 0; qx < Q; qx++)
+      {
+         const int i = (qz * Q + qy) * Q + qx;
+         u += s3x[i] * sG[qx + Q * dx] + s3m[i] * sB[qx + Q * dx];
+         v += s3y[i] * sB[qx + Q * dx];
+         w += s3z[i] * sB[qx + Q * dx];
+      }
+      s4a[t] = u; s4b[t] = v; s4c[t] = w;
+   }
+   __syncthreads();
+   // stage 5: y-transpose (dx, dy, qz)
+   if (t < Q * D * D)
+   {
+      const int dx = t % D, dy = (t / D) % D, qz = t / (D * D);
+      double u = 0.0, w = 0.0;
+      for (int qy = 0; qy < Q; qy++)
+      {
+         const int i = (qz * Q + qy) * D + dx;
+         u += s4a[i] * sB[qy + Q * dy] + s4b[i] * sG[qy + Q * dy];
+         w += s4c[i] * sB[qy + Q * dy];
+      }
+      s5a[t] = u; s5b[t] = w;
+   }
+   __syncthreads();
+   // stage 6: z-transpose (dx, dy, dz) + output
+   if (t < ND)
+   {
+      const int dx = t % D, dy = (t / D) % D, dz = t / (D * D);
+      double u = 0.0;
+      for (int qz = 0; qz < Q; qz++)
+      {
+         const int i = (qz * D + dy) * D + dx;
+         u += s5a[i] * sB[qz + Q * dz] + s5b[i] * sG[qz + Q * dz];
+      }
+      if (OUT_E) { y[(size_t)e * ND + t] += u; }
+      else
+      {
+         const int g = gmap[(size_t)e * ND + t];
+         unsafeAtomicAdd(y + dof_of(g), g >= 0 ? u : -u);
+      }
+   }
+}
+
+// --------------------------------------------------------------------------
+// Restriction, diagonal, vector kernels
+// --------------------------------------------------------------------------
+
+__global__ void k_restriction_mult(long n, const int *__restrict__ gmap,
+                                   const double *__restrict__ x, double *__restrict__ xe)
+{
+   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   if (i >= n) { return; }
+   const int g = gmap[i];
+   const double v = x[dof_of(g)];
+   xe[i] = g >= 0 ? v : -v;
+}
+
+__global__ void k_restriction_mult_transpose(int ndofs, const int *__restrict__ offsets,
+                                             const int *__restrict__ indices,
+                                             const double *__restrict__ xe,
+                                             double *__restrict__ y)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i >= ndofs) { return; }
+   double v = 0.0;
+   for (int j = offsets[i]; j < offsets[i + 1]; j++)
+   {
+      const int idx = indices[j];
+      v += idx >= 0 ? xe[idx] : -xe[-1 - idx];
+   }
+   y[i] = v;
+}
+
+__global__ void k_diagonal(int D, int Q, int kind, int ne, const int *__restrict__ gmap,
+                           const double *__restrict__ qdd, const double *__restrict__ qdm,
+                           double *__restrict__ diag, bool out_e, const Basis1D b)
+{
+   const int ND = D * D * D, NQ = Q * Q * Q;
+   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   if (t >= (long)ne * ND) { return; }
+   const int e = (int)(t / ND), a = (int)(t % ND);
+   const int dx = a % D, dy = (a / D) % D, dz = a / (D * D);
+   double s = 0.0;
+   for (int qz = 0; qz < Q; qz++)
+      for (int qy = 0; qy < Q; qy++)
+         for (int qx = 0; qx < Q; qx++)
+         {
+            const int q = (qz * Q + qy) * Q + qx;
+            const double bx = b.B[qx + MQ * dx], by = b.B[qy + MQ * dy], bz = b.B[qz + MQ * dz];
+            const double gx = b.G[qx + MQ * dx], gy = b.G[qy + MQ * dy], gz = b.G[qz + MQ * dz];
+            if (qdm) { s += bx * bx * by * by * bz * bz * qdm[qidx_mass(kind, NQ, e, q)]; }
+            if (qdd)
+            {
+               const double p0 = gx * by * bz, p1 = bx * gy * bz, p2 = bx * by * gz;
+               s += p0 * p0 * qdd[qidx_diff(kind, NQ, e, 0, q)] +
+                    p1 * p1 * qdd[qidx_diff(kind, NQ, e, 3, q)] +
+                    p2 * p2 * qdd[qidx_diff(kind, NQ, e, 5, q)] +
+                    2.0 * (p0 * p1 * qdd[qidx_diff(kind, NQ, e, 1, q)] +
+                           p0 * p2 * qdd[qidx_diff(kind, NQ, e, 2, q)] +
+                           p1 * p2 * qdd[qidx_diff(kind, NQ, e, 4, q)]);
+            }
+         }
+   if (out_e) { diag[t] += s; }
+   else { unsafeAtomicAdd(diag + dof_of(gmap[t]), s); }
+}
+
+__global__ void k_set_values(int n, const int *__restrict__ idx, double val, double *__restrict__ y)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { y[idx[i]] = val; }
+}
+
+__global__ void k_copy_values(int n, const int *__restrict__ idx, const double *__restrict__ x,
+                              double *__restrict__ y)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { y[idx[i]] = x[idx[i]]; }
+}
+
+constexpr int kDotBlocks = 1024;
+
+__global__ void __launch_bounds__(256)
+k_dot_partial(int n, const double *__restrict__ a, const double *__restrict__ b,
+              double *__restrict__ partials)
+{
+   __shared__ double red[4];
+   double s = 0.0;
+   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+   {
+      s += a[i] * b[i];
+   }
+   for (int off = 32; off > 0; off >>= 1) { s += __shfl_down(s, off, 64); }
+   if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6] = s; }
+   __syncthreads();
+   if (threadIdx.x == 0) { partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]); }
+}
+
+__global__ void __launch_bounds__(256)
+k_dot_final(int nparts, const double *__restrict__ partials, double *__restrict__ out)
+{
+   __shared__ double red[4];
+   double s = 0.0;
+   for (int i = threadIdx.x; i < nparts; i += blockDim.x) { s += partials[i]; }
+   for (int off = 32; off > 0; off >>= 1) { s += __shfl_down(s, off, 64); }
+   if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6] = s; }
+   __syncthreads();
+   if (threadIdx.x == 0) { *out = (red[0] + red[1]) + (red[2] + red[3]); }
+}
+
+__global__ void k_pcg_update_xr(int n, const double *__restrict__ nom,
+                                const double *__restrict__ den, const double *__restrict__ d,
+                                const double *__restrict__ z, double *__restrict__ x,
+                                double *__restrict__ r)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i >= n) { return; }
+   const double alpha = *nom / *den;
+   x[i] = x[i] + alpha * d[i];
+   r[i] = r[i] + (-alpha) * z[i];
+}
+
+__global__ void k_pcg_precond(int n, const double *__restrict__ dinv, const double *__restrict__ r,
+                              double *__restrict__ z)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { z[i] = dinv ? dinv[i] * r[i] : r[i]; }
+}
+
+__global__ void k_pcg_update_d(int n, const double *__restrict__ betanom,
+                               const double *__restrict__ nom, const double *__restrict__ z,
+                               double *__restrict__ d)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i >= n) { return; }
+   const double beta = *betanom / *nom;
+   d[i] = z[i] + beta * d[i];
+}
+
+__global__ void k_reciprocal(int n, const double *__restrict__ a, double *__restrict__ out)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { out[i] = 1.0 / a[i]; }
+}
+
+__global__ void k_gather_idx(int n, const int *__restrict__ idx, const double *__restrict__ x,
+                             double *__restrict__ buf)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { buf[i] = x[idx[i]]; }
+}
+
+__global__ void k_scatter_add_idx(int n, const int *__restrict__ idx, const double *__restrict__ buf,
+                                  double *__restrict__ y)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { y[idx[i]] += buf[i]; }
+}
+
+__global__ void k_scatter_set_idx(int n, const int *__restrict__ idx, const double *__restrict__ buf,
+                                  double *__restrict__ y)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { y[idx[i]] = buf[i]; }
+}
+
+inline unsigned grid_for(long n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+SetupCoef make_setup_coef(const CoeffDesc *c, const double *q)
+{
+   SetupCoef s{};
+   if (!c) { return s; }
+   s.has = 1;
+   s.is_const = (c->kind == COEFF_CONSTANT);
+   s.value = c->value;
+   s.quad = q;
+   return s;
+}
+
+template <int D, int Q>
+void launch_tpe_dq(bool mass, bool diff, int ne, const int *gm, const double *qdd,
+                   const double *qdm, const double *x, double *y, const Basis1D &b,
+                   const double *rowtab, hipStream_t s)
+{
+   const int nblk = (ne + 63) / 64;
+   const dim3 grid((nblk + 3) / 4), block(256);
+   if (mass && diff)
+   {
+      hipLaunchKernelGGL((k_apply_tpe<D, Q, true, true>), grid, block, 0, s, ne, nblk, gm, qdd, qdm, x, y, b, rowtab);
+   }
+   else if (mass)
+   {
+      hipLaunchKernelGGL((k_apply_tpe<D, Q, true, false>), grid, block, 0, s, ne, nblk, gm, qdd, qdm, x, y, b, rowtab);
+   }
+   else if (diff)
+   {
+      hipLaunchKernelGGL((k_apply_tpe<D, Q, false, true>), grid, block, 0, s, ne, nblk, gm, qdd, qdm, x, y, b, rowtab);
+   }
+}
+
+template <int D, int Q, bool MASS, bool DIFF>
+void launch_wpe_mdq(int kind, int ne, const int *gm, const double *qdd, const double *qdm,
+                    const double *x, double *y, bool in_e, bool out_e, const Basis1D &b,
+                    hipStream_t s)
+{
+   constexpr int NQ = Q * Q * Q;
+   const int nt = ((NQ + 63) / 64) * 64;
+   const dim3 grid(ne), block(nt);
+   if (in_e && out_e)
+   {
+      hipLaunchKernelGGL((k_apply_wpe<D, Q, MASS, DIFF, true, true>), grid, block, 0, s, kind, ne, gm, qdd, qdm, x, y, b);
+   }
+   else if (in_e)
+   {
+      hipLaunchKernelGGL((k_apply_wpe<D, Q, MASS, DIFF, true, false>), grid, block, 0, s, kind, ne, gm, qdd, qdm, x, y, b);
+   }
+   else if (out_e)
+   {
+      hipLaunchKernelGGL((k_apply_wpe<D, Q, MASS, DIFF, false, true>), grid, block, 0, s, kind, ne, gm, qdd, qdm, x, y, b);
+   }
+   else
+   {
+      hipLaunchKernelGGL((k_apply_wpe<D, Q, MASS, DIFF, false, false>), grid, block, 0, s, kind, ne, gm, qdd, qdm, x, y, b);
+   }
+}
+
+template <int D, int Q>
+void launch_wpe_dq(bool mass, bool diff, int kind, int ne, const int *gm, const double *qdd,
+                   const double *qdm, const double *x, double *y, bool in_e, bool out_e,
+                   const Basis1D &b, hipStream_t s)
+{
+   if (mass && diff) { launch_wpe_mdq<D, Q, true, true>(kind, ne, gm, qdd, qdm, x, y, in_e, out_e, b, s); }
+   else if (mass) { launch_wpe_mdq<D, Q, true, false>(kind, ne, gm, qdd, qdm, x, y, in_e, out_e, b, s); }
+   else if (diff) { launch_wpe_mdq<D, Q, false, true>(kind, ne, gm, qdd, qdm, x, y, in_e, out_e, b, s); }
+}
+
+} // namespace
+
+namespace kern
+{
+
+void coeff_gridfunc(int ne, int D, int Q, const int *gmap, const Basis1D &b, const CoeffDesc &c,
+                    double *out, hipStream_t s)
+{
+   const long n = (long)ne * Q * Q * Q;
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_coeff_gridfunc, dim3(grid_for(n, 256)), dim3(256), 0, s, ne, D, Q, gmap,
+                      b, c.lvec, c.scale, c.slope, c.t_ref, out);
+   ECM2_HIP(hipGetLastError());
+}
+
+void setup_from_nodes(const QLayout &L, int Q, const double *enodes, const double *W,
+                      const Basis1D &b1, const CoeffDesc *cm, const CoeffDesc *cd,
+                      const double *cm_q, const double *cd_q, double *qd_diff,
+                      double *qd_mass, hipStream_t s)
+{
+   const long n = (long)L.ne * L.nq;
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_setup_nodes, dim3(grid_for(n, 256)), dim3(256), 0, s, L.kind, L.ne, Q,
+                      enodes, W, b1, make_setup_coef(cm, cm_q), make_setup_coef(cd, cd_q),
+                      qd_diff, qd_mass);
+   ECM2_HIP(hipGetLastError());
+}
+
+void setup_from_jacobians(const QLayout &L, const double *J, const double *W,
+                          const CoeffDesc *cm, const CoeffDesc *cd, const double *cm_q,
+                          const double *cd_q, double *qd_diff, double *qd_mass, hipStream_t s)
+{
+   const long n = (long)L.ne * L.nq;
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_setup_jac, dim3(grid_for(n, 256)), dim3(256), 0, s, L.kind, L.ne, L.nq,
+                      J, W, make_setup_coef(cm, cm_q), make_setup_coef(cd, cd_q), qd_diff,
+                      qd_mass);
+   ECM2_HIP(hipGetLastError());
+}
+
+void apply_tpe(int D, int Q, bool mass, bool diff, int ne, const int *gm, const double *qdd,
+               const double *qdm, const double *x, double *y, const Basis1D &b,
+               const double *rowtab, hipStream_t s)
+{
+   if (ne == 0) { return; }
+   if (D == 2 && Q == 3) { launch_tpe_dq<2, 3>(mass, diff, ne, gm, qdd, qdm, x, y, b, rowtab, s); }
+   else if (D == 3 && Q == 4) { launch_tpe_dq<3, 4>(mass, diff, ne, gm, qdd, qdm, x, y, b, rowtab, s); }
+   else { ECM2_VERIFY(false, ERR_UNSUPPORTED, "no thread-per-element kernel for D1D=" << D << " Q1D=" << Q); }
+   ECM2_HIP(hipGetLastError());
+}
+
+void apply_wpe(int D, int Q, bool mass, bool diff, int kind, int ne, const int *gm,
+               const double *qdd, const double *qdm, const double *x, double *y, bool in_e,
+               bool out_e, const Basis1D &b, hipStream_t s)
+{
+   if (ne == 0) { return; }
+#define ECM2_WPE_CASE(DD, QQ)                                                          \
+   if (D == DD && Q == QQ)                                                             \
+   {                                                                                   \
+      launch_wpe_dq<DD, QQ>(mass, diff, kind, ne, gm, qdd, qdm, x, y, in_e, out_e, b, s); \
+      ECM2_HIP(hipGetLastError());                                                     \
+      return;                                                                          \
+   }
+   ECM2_WPE_CASE(2, 3)
+   ECM2_WPE_CASE(3, 4)
+   ECM2_WPE_CASE(4, 5)
+   ECM2_WPE_CASE(5, 6)
+   ECM2_WPE_CASE(2, 2)
+   ECM2_WPE_CASE(3, 3)
+   ECM2_WPE_CASE(4, 4)
+   ECM2_WPE_CASE(5, 5)
+   ECM2_WPE_CASE(6, 7)
+#undef ECM2_WPE_CASE
+   ECM2_VERIFY(false, ERR_UNSUPPORTED, "no PA kernel for D1D=" << D << " Q1D=" << Q);
+}
+
+void restriction_mult(long n, int nd, const int *gm, const double *x, double *xe, hipStream_t s)
+{
+   (void)nd;
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_restriction_mult, dim3(grid_for(n, 256)), dim3(256), 0, s, n, gm, x, xe);
+   ECM2_HIP(hipGetLastError());
+}
+
+void restriction_mult_transpose(int ndofs, int nd, const int *offsets, const int *indices,
+                                const double *xe, double *y, hipStream_t s)
+{
+   (void)nd;
+   if (ndofs == 0) { return; }
+   hipLaunchKernelGGL(k_restriction_mult_transpose, dim3(grid_for(ndofs, 256)), dim3(256), 0, s,
+                      ndofs, offsets, indices, xe, y);
+   ECM2_HIP(hipGetLastError());
+}
+
+void diagonal(int D, int Q, int layout, int ne, const int *gm, const double *qdd,
+              const double *qdm, double *diag, bool out_e, const Basis1D &b, hipStream_t s)
+{
+   const long n = (long)ne * D * D * D;
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_diagonal, dim3(grid_for(n, 128)), dim3(128), 0, s, D, Q, layout, ne, gm,
+                      qdd, qdm, diag, out_e, b);
+   ECM2_HIP(hipGetLastError());
+}
+
+void set_values(int n, const int *idx, double val, double *y, hipStream_t s)
+{
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_set_values, dim3(grid_for(n, 256)), dim3(256), 0, s, n, idx, val, y);
+   ECM2_HIP(hipGetLastError());
+}
+
+void copy_values(int n, const int *idx, const double *x, double *y, hipStream_t s)
+{
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_copy_values, dim3(grid_for(n, 256)), dim3(256), 0, s, n, idx, x, y);
+   ECM2_HIP(hipGetLastError());
+}
+
+void dot(int n, const double *a, const double *b, double *partials, double *out, hipStream_t s)
+{
+   hipLaunchKernelGGL(k_dot_partial, dim3(kDotBlocks), dim3(256), 0, s, n, a, b, partials);
+   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, s, kDotBlocks, partials, out);
+   ECM2_HIP(hipGetLastError());
+}
+
+void pcg_update_xr(int n, const double *nom, const double *den, const double *d, const double *z,
+                   double *x, double *r, hipStream_t s)
+{
+   hipLaunchKernelGGL(k_pcg_update_xr, dim3(grid_for(n, 256)), dim3(256), 0, s, n, nom, den, d, z, x, r);
+   ECM2_HIP(hipGetLastError());
+}
+
+void pcg_precond(int n, const double *dinv, const double *r, double *z, hipStream_t s)
+{
+   hipLaunchKernelGGL(k_pcg_precond, dim3(grid_for(n, 256)), dim3(256), 0, s, n, dinv, r, z);
+   ECM2_HIP(hipGetLastError());
+}
+
+void pcg_update_d(int n, const double *betanom, const double *nom, const double *z, double *d,
+                  hipStream_t s)
+{
+   hipLaunchKernelGGL(k_pcg_update_d, dim3(grid_for(n, 256)), dim3(256), 0, s, n, betanom, nom, z, d);
+   ECM2_HIP(hipGetLastError());
+}
+
+void reciprocal(int n, const double *a, double *out, hipStream_t s)
+{
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_reciprocal, dim3(grid_for(n, 256)), dim3(256), 0, s, n, a, out);
+   ECM2_HIP(hipGetLastError());
+}
+
+void gather_idx(int n, const int *idx, const double *x, double *buf, hipStream_t s)
+{
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_gather_idx, dim3(grid_for(n, 256)), dim3(256), 0, s, n, idx, x, buf);
+   ECM2_HIP(hipGetLastError());
+}
+
+void scatter_add_idx(int n, const int *idx, const double *buf, double *y, hipStream_t s)
+{
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_scatter_add_idx, dim3(grid_for(n, 256)), dim3(256), 0, s, n, idx, buf, y);
+   ECM2_HIP(hipGetLastError());
+}
+
+void scatter_set_idx(int n, const int *idx, const double *buf, double *y, hipStream_t s)
+{
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_scatter_set_idx, dim3(grid_for(n, 256)), dim3(256), 0, s, n, idx, buf, y);
+   ECM2_HIP(hipGetLastError());
+}
+
+std::vector<double> make_row_table(const DofToQuad &m)
+{
+   const int D = m.ndof, Q = m.nqpt, DD = D * D;
+   std::vector<double> t((size_t)Q * Q * 3 * DD);
+   for (int qz = 0; qz < Q; qz++)
+      for (int qy = 0; qy < Q; qy++)
+      {
+         double *P = &t[(size_t)(qz * Q + qy) * 3 * DD];
+         for (int dz = 0; dz < D; dz++)
+            for (int dy = 0; dy < D; dy++)
+            {
+               const double By = m.B[qy + Q * dy], Gy = m.G[qy + Q * dy];
+               const double Bz = m.B[qz + Q * dz], Gz = m.G[qz + Q * dz];
+               P[0 * DD + dz * D + dy] = By * Bz;
+               P[1 * DD + dz * D + dy] = Gy * Bz;
+               P[2 * DD + dz * D + dy] = By * Gz;
+            }
+      }
+   return t;
+}
+
+} // namespace kern
+} // namespace ecm2

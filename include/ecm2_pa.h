@@ -1,0 +1,150 @@
+/*
+ * ecm2_pa.h -- C ABI of the MI355X-native PA diffusion+mass operator.
+ *
+ * This is the drop-in boundary for the reference's
+ *   BilinearForm(PARTIAL) + MassIntegrator(alpha) + DiffusionIntegrator(beta)
+ * hot path (PABilinearFormExtension, fem/bilinearform_ext.hpp:67-144).  Plain C:
+ * opaque handles, plain pointers and sizes, int status codes (0 = ok), no HIP or
+ * torch types.  Streams are passed as `void *` holding a hipStream_t (NULL = the
+ * null stream, which is what the reference uses: general/forall.hpp:782).
+ *
+ * Memory: arguments documented "host" are read during the call; arguments
+ * documented "device" are HBM pointers (hipMalloc / torch CUDA tensors).
+ * Errors mirror MFEM_VERIFY -> mfem_error (general/error.cpp:154-184): the call
+ * returns a nonzero ECM2_ERR_* code and ecm2_last_error() holds the message.
+ * There is no CPU fallback: without a GPU every compute entry point fails with
+ * ECM2_ERR_HIP.  See INTEGRATION.md for the reference-side binding.
+ */
+#ifndef ECM2_PA_H
+#define ECM2_PA_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ECM2_OK 0
+#define ECM2_ERR_ARG 1
+#define ECM2_ERR_HIP 2
+#define ECM2_ERR_STATE 3
+#define ECM2_ERR_IO 4
+#define ECM2_ERR_UNSUPPORTED 5
+#define ECM2_ERR_COMM 6
+#define ECM2_ERR_INTERNAL 7
+
+/* Integrator kinds (MassIntegrator, DiffusionIntegrator: fem/bilininteg.hpp:2177-2465). */
+#define ECM2_MASS 0
+#define ECM2_DIFFUSION 1
+
+/* Coefficient kinds (CoefficientVector COMPRESSED storage, fem/coefficient.cpp:2006-2180). */
+#define ECM2_COEFF_CONSTANT 0       /* ConstantCoefficient                                   */
+#define ECM2_COEFF_QUAD 1           /* values at quadrature points, device [ne][nq]          */
+#define ECM2_COEFF_GRIDFUNC_AFFINE 2/* scale*(1+slope*(T(x_q)-t_ref)), T an H1 L-vector       */
+
+/* Kernel selection (all produce the same operator). */
+#define ECM2_KERNEL_AUTO 0
+#define ECM2_KERNEL_TPE 1      /* fused, thread per element (p = 1, 2)              */
+#define ECM2_KERNEL_WPE 2      /* fused, workgroup per element (p = 1..6)           */
+#define ECM2_KERNEL_UNFUSED 3  /* reference-shaped: R, per-integrator AddMultPA, R^T */
+
+/* Numbering of H1 dofs. */
+#define ECM2_NUMBERING_ENTITY 0     /* vertices, edges, faces, interiors (fespace.cpp:2767) */
+#define ECM2_NUMBERING_STRUCTURED 1 /* lattice numbering of a Cartesian mesh               */
+
+const char *ecm2_last_error(void);
+int ecm2_version(void);
+int ecm2_device_count(void);
+
+/* ------------------------------------------------------------------------ */
+/* Setup side: meshes and H1 spaces (the caller's Mesh / FiniteElementSpace)  */
+/* ------------------------------------------------------------------------ */
+typedef struct ecm2_mesh ecm2_mesh;
+typedef struct ecm2_h1space ecm2_h1space;
+
+/* Mesh::MakeCartesian3D, mesh/mesh.cpp:3683 (lexicographic element order). */
+int ecm2_mesh_cartesian(int nx, int ny, int nz, double sx, double sy, double sz, ecm2_mesh **out);
+/* Mesh(filename): MFEM mesh v1.0 hex meshes and MFEM INLINE hex meshes
+ * (mesh/mesh_readers.cpp:1356-1506).  Host file read. */
+int ecm2_mesh_read(const char *path, ecm2_mesh **out);
+/* Mesh::UniformRefinement, mesh/mesh.cpp:11403 (hex: 1 -> 8). */
+int ecm2_mesh_refine_uniform(ecm2_mesh *m);
+int ecm2_mesh_info(const ecm2_mesh *m, int *nv, int *ne);
+int ecm2_mesh_get_vertices(const ecm2_mesh *m, double *out /* host [nv][3] */);
+int ecm2_mesh_set_vertices(ecm2_mesh *m, const double *in /* host [nv][3] */);
+int ecm2_mesh_get_elements(const ecm2_mesh *m, int *out /* host [ne][8], native order */);
+/* Lexicographic corner coordinates, host out[ne][3][8]. */
+int ecm2_mesh_get_element_nodes(const ecm2_mesh *m, double *out);
+void ecm2_mesh_destroy(ecm2_mesh *m);
+
+/* H1_FECollection(order) + FiniteElementSpace: element->dof table in
+ * lexicographic order (ElementRestriction gather_map, fem/restriction.cpp:26-107). */
+int ecm2_h1space_create(const ecm2_mesh *m, int order, int numbering, ecm2_h1space **out);
+int ecm2_h1space_info(const ecm2_h1space *s, int *ndofs, int *ne, int *nd);
+int ecm2_h1space_get_gather_map(const ecm2_h1space *s, int *out /* host [ne][nd] */);
+/* Essential true dofs for ess_bdr = all (GetEssentialTrueDofs): two-call pattern,
+ * out may be NULL to query *count. */
+int ecm2_h1space_boundary_dofs(const ecm2_h1space *s, int *out, int *count);
+int ecm2_h1space_dof_coords(const ecm2_h1space *s, const ecm2_mesh *m, double *out /* host [ndofs][3] */);
+void ecm2_h1space_destroy(ecm2_h1space *s);
+
+/* ------------------------------------------------------------------------ */
+/* The PA form: drop-in for PABilinearFormExtension of Mass + Diffusion       */
+/* ------------------------------------------------------------------------ */
+typedef struct ecm2_pa_form ecm2_pa_form;
+
+/* Replaces BilinearForm::SetAssemblyLevel(PARTIAL) + FiniteElementSpace
+ * ElementRestriction construction (bilinearform.cpp:109-136, restriction.cpp:26-107).
+ * gather_map: host [ne][(order+1)^3], MFEM gather_map semantics (-1-gid = minus sign).
+ * q1d <= 0 selects the reference default rule (Q1D = order+2). */
+int ecm2_pa_form_create(int ne, int order, int ndofs, const int *gather_map, int q1d,
+                        ecm2_pa_form **out);
+/* Geometry from lexicographic element corners, host [ne][3][8] (trilinear hexes). */
+int ecm2_pa_form_set_element_nodes(ecm2_pa_form *f, const double *enodes);
+/* Geometry from GeometricFactors::JACOBIANS (mesh.cpp:15242 layout NQ x 3 x 3 x NE),
+ * device pointer, must stay valid until ecm2_pa_form_assemble returns. */
+int ecm2_pa_form_set_jacobians(ecm2_pa_form *f, const double *J);
+/* BilinearForm::AddDomainIntegrator(new MassIntegrator(Q)) / DiffusionIntegrator(Q)
+ * (bilinearform.cpp:231-242).  data: CONSTANT -> data[0] (host);
+ * QUAD -> device [ne][nq]; GRIDFUNC_AFFINE -> device L-vector T with
+ * params[0..2] = (scale, slope, t_ref).  Device arrays must stay valid until assemble. */
+int ecm2_pa_form_add_integrator(ecm2_pa_form *f, int integrator, int coeff_kind,
+                                const double *data, const double *params);
+int ecm2_pa_form_set_kernel(ecm2_pa_form *f, int kernel);
+/* BilinearForm::Assemble -> PABilinearFormExtension::Assemble -> AssemblePA
+ * (bilinearform.cpp:456-460, bilinearform_ext.cpp:332-368). */
+int ecm2_pa_form_assemble(ecm2_pa_form *f, void *stream);
+/* BilinearForm::Mult / PABilinearFormExtension::Mult (bilinearform.cpp:1244-1254,
+ * bilinearform_ext.cpp:487-564): y = A x, y overwritten.  x, y device [ndofs]. */
+int ecm2_pa_form_mult(ecm2_pa_form *f, const double *x, double *y, void *stream);
+/* PABilinearFormExtension::AssembleDiagonal (bilinearform_ext.cpp:370-454). diag device [ndofs]. */
+int ecm2_pa_form_assemble_diagonal(ecm2_pa_form *f, double *diag, void *stream);
+/* ElementRestriction::Mult / MultTranspose (restriction.cpp:109-186). xe device [ne][nd]. */
+int ecm2_pa_form_restriction_mult(ecm2_pa_form *f, const double *x, double *xe, void *stream);
+int ecm2_pa_form_restriction_mult_transpose(ecm2_pa_form *f, const double *xe, double *y, void *stream);
+/* BilinearFormIntegrator::AddMultPA (bilininteg.hpp:49-97): ye += A_integ xe (E-vectors). */
+int ecm2_pa_form_integrator_add_mult(ecm2_pa_form *f, int integrator, const double *xe,
+                                     double *ye, void *stream);
+/* pa_data in the reference layout (diffusion [ne][6][nq], mass [ne][nq]), host out. */
+int ecm2_pa_form_get_qdata(ecm2_pa_form *f, int integrator, double *out, void *stream);
+int ecm2_pa_form_info(const ecm2_pa_form *f, int *ne, int *ndofs, int *d1d, int *q1d,
+                      int *kernel, int *layout);
+/* HIP-event timing of the dominant apply kernel(s) inside Mult. */
+int ecm2_pa_form_timing(ecm2_pa_form *f, int enable);
+int ecm2_pa_form_timing_get(ecm2_pa_form *f, double *total_ms, long *launches);
+/* SURVEY §8(d) algorithmic bytes per Mult: 8*NE*NQ*(6+1) + 16*ndofs + 4*NE*ND. */
+int ecm2_pa_form_algorithmic_bytes(const ecm2_pa_form *f, double *bytes);
+void ecm2_pa_form_destroy(ecm2_pa_form *f);
+
+/* ------------------------------------------------------------------------ */
+/* Caller: constrained Jacobi-PCG (ConstrainedOperator operator.cpp:586-646 + */
+/* CGSolver::Mult solvers.cpp:869-1004)                                       */
+/* ------------------------------------------------------------------------ */
+/* ess: device int [n_ess] essential dofs (DIAG_ONE).  b, x device [ndofs];
+ * x is overwritten (iterative_mode = false).  jacobi != 0 -> OperatorJacobiSmoother. */
+int ecm2_pcg_solve(ecm2_pa_form *f, const int *ess, int n_ess, const double *b, double *x,
+                   double rel_tol, double abs_tol, int max_iter, int jacobi, int *iterations,
+                   double *final_norm, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ECM2_PA_H */

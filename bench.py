@@ -1,0 +1,247 @@
+#!/usr/bin/env python3
+"""bench.py -- MDoF/s of the PA diffusion+mass Mult (hex, H1 p=2) on MI355X.
+
+Metric (BASELINE.json): "MDoF/s on PA diffusion+mass Mult, hex p=2; % HBM roofline at
+1/2/4/8 GPUs".  One *step* = one operator Mult y = A x (L-vector in, L-vector out;
+tests/benchmarks/bench_assembly_levels.cpp:281-286 counts ndofs per Mult) with x, y
+and the operator resident in HBM.  Workload: BASELINE configs[1] -- inline-hex refined
+to ~1M DoF (Cartesian 50^3, p = 2, 1,030,301 DoF) per GPU; with N GPUs the global
+mesh is 50 x 50 x 50N, z-slab partitioned, one rank per GPU (weak scaling) with the
+shared-DoF exchange over RCCL.  --workload c4 runs configs[3] (Cartesian 108^3,
+10.2M DoF, split over the ranks: strong scaling).
+
+Coefficients are the bioheat ones: alpha = rho*c_eff(x) (FunctionCoefficient projected
+at the quadrature points) and beta = gamma*dt*k(T) with T an H1 grid function (the
+Pennes law, evaluated on the device at Assemble).  Inputs are synthetic (no data files).
+"""
+import argparse
+import importlib.util
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def load_pkg():
+    if "ecm2_amd" in sys.modules:
+        return sys.modules["ecm2_amd"]
+    pkg_dir = os.path.join(ROOT, "cardiac-ablation-ecm2_amd")
+    spec = importlib.util.spec_from_file_location("ecm2_amd", os.path.join(pkg_dir, "__init__.py"),
+                                                  submodule_search_locations=[pkg_dir])
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["ecm2_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def alpha_fn(P):
+    return 3.6e6 * (1.0 + 0.1 * np.sin(3.0 * P[..., 0]))
+
+
+def temperature_fn(X):
+    return 37.0 + 20.0 * np.exp(-10.0 * np.sum(X * X, axis=-1))
+
+
+K_SCALE, K_SLOPE, K_TREF = 0.5 * 0.05, 0.0012, 37.0  # gamma*dt*k0, dk/dT / k0, T0
+
+
+def build_local_problem(E, torch, nx, ny, nz, z0, z1, sz_total):
+    """Mesh slab [z0, z1) of a Cartesian nx x ny x nz_total box; returns (mesh, fes, form)."""
+    nzl = z1 - z0
+    h = 1.0 / nx
+    mesh = E.Mesh.MakeCartesian3D(nx, ny, nzl, 1.0, ny * h, nzl * h)
+    if z0:
+        V = mesh.vertices()
+        V[:, 2] += z0 * h
+        mesh.set_vertices(V)
+    fes = E.H1Space(mesh, 2, E.NUMBERING_STRUCTURED)
+    q1d = 4
+    P = mesh.quadrature_points(q1d)
+    alpha = torch.as_tensor(alpha_fn(P).reshape(fes.ne, -1)).cuda()
+    T = torch.as_tensor(temperature_fn(fes.dof_coords())).cuda()
+    return mesh, fes, alpha, T
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--workload", choices=["c2", "c4"], default="c2")
+    ap.add_argument("--kernel", choices=["auto", "tpe", "wpe", "unfused"], default="auto")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+    E = load_pkg()
+    E.load_library()
+    kernel = {"auto": E.KERNEL_AUTO, "tpe": E.KERNEL_TPE, "wpe": E.KERNEL_WPE, "unfused": E.KERNEL_UNFUSED}[args.kernel]
+
+    if args.workload == "c2":
+        n = 50
+        nx = ny = n
+        nz_total = n * world
+        scaling = "weak"
+        workload = f"configs[1]: inline-hex refined to Cartesian 50x50x{nz_total} (50^3 per GPU), H1 p=2, Mass(rho*c)+Diffusion(gamma*dt*k(T)) PA Mult"
+    else:
+        nx = ny = nz_total = 108
+        scaling = "strong"
+        workload = "configs[3]: Cartesian 108^3 (10.2M DoF) split over GPUs, H1 p=2, Mass+Diffusion PA Mult"
+    # z-slab partition (CartesianPartitioning along z, mesh.cpp:8966)
+    zb = [(nz_total * r) // world for r in range(world + 1)]
+    z0, z1 = zb[rank], zb[rank + 1]
+    mesh, fes, alpha, T = build_local_problem(E, torch, nx, ny, nz_total, z0, z1, nz_total)
+
+    if world == 1:
+        form = E.BilinearForm(fes, kernel=kernel)
+        form.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(alpha)))
+        form.AddDomainIntegrator(E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(T, K_SCALE, K_SLOPE, K_TREF)))
+        form.Assemble()
+        n_true = fes.ndofs
+        apply = form.Mult
+        timed_form = form
+    else:
+        pform = E.ParBilinearForm(fes, rank, world, z0, z1, nz_total, kernel=kernel)
+        pform.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(alpha)))
+        pform.AddDomainIntegrator(E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(T, K_SCALE, K_SLOPE, K_TREF)))
+        pform.Assemble()
+        n_true = pform.true_size
+        apply = pform.Mult
+        timed_form = pform.local_form
+
+    x = torch.empty(n_true if world > 1 else fes.ndofs, dtype=torch.float64, device="cuda")
+    x.uniform_(-1.0, 1.0, generator=torch.Generator(device="cuda").manual_seed(1 + rank))
+    y = torch.empty_like(x)
+    torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        apply(x, y)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timed_form.timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        apply(x, y)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    kms, klaunch = timed_form.timing_get()
+    timed_form.timing(False)
+
+    # aggregate over ranks: total true dofs, max time
+    tot = torch.tensor([float(n_true), dt, timed_form.algorithmic_bytes(), kms / max(klaunch, 1)],
+                       dtype=torch.float64, device="cuda")
+    if world > 1:
+        s = tot.clone()
+        dist.all_reduce(s[0:1], op=dist.ReduceOp.SUM)
+        dist.all_reduce(s[2:3], op=dist.ReduceOp.SUM)
+        dist.all_reduce(s[1:2], op=dist.ReduceOp.MAX)
+        dist.all_reduce(s[3:4], op=dist.ReduceOp.MAX)
+        tot = s
+    ndofs_total, tmax, bytes_total, kavg_ms = [float(v) for v in tot.cpu()]
+    value = ndofs_total * args.steps / tmax / 1e6
+
+    if rank == 0:
+        achieved = bytes_total / world / (kavg_ms * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_n{world}.json")
+        if os.path.exists(pmc):
+            try:
+                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(fes, mesh, alpha, T, args.cpu_baseline_seconds)
+        line = {
+            "metric": "MDoF/s on PA diffusion+mass Mult, hex p=2; % HBM roofline at 1/2/4/8 GPUs",
+            "value": round(value, 2),
+            "unit": "MDoF/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(tmax / args.steps * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": scaling,
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (generated Cartesian hex mesh, bioheat coefficients, uniform random x)",
+            "config": {
+                "workload": workload,
+                "ndofs": int(ndofs_total),
+                "elements": int(fes.ne) if world == 1 else None,
+                "order": 2, "q1d": 4,
+                "kernel": ["auto", "tpe", "wpe", "unfused"][timed_form.info()["kernel"]],
+                "parallelism": f"domain-decomposition z-slabs x{world}",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": PEAK_HBM_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / PEAK_HBM_GBS, 4),
+                "traffic": traffic,
+                "kernel_ms_avg": round(kavg_ms, 5),
+                "algorithmic_bytes_per_launch": bytes_total / world,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(fes, mesh, alpha, T, seconds):
+    """The oracle (CPU restatement of the reference PA path, 'port') on the same workload,
+    timed on this host's cores for a bounded number of Mults (~`seconds` of CPU work)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    q1d = 4
+    en = mesh.element_nodes()
+    gm = fes.gather_map()
+    Tq = O.interp_evector(T.cpu().numpy()[gm], 2, q1d)
+    beta = K_SCALE * (1.0 + K_SLOPE * (Tq - K_TREF))
+    op = O.OracleOperator(en, gm, fes.ndofs, 2, alpha=alpha.cpu().numpy(), beta=beta)
+    x = np.random.default_rng(1).uniform(-1, 1, fes.ndofs)
+    op.mult(x)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        op.mult(x)
+        n += 1
+        if time.perf_counter() - t0 >= seconds or n >= 1000:
+            break
+    dt = time.perf_counter() - t0
+    return {
+        "value": round(fes.ndofs * n / dt / 1e6, 3),
+        "unit": "MDoF/s",
+        "cores": O.num_threads(),
+        "kind": "port",
+        "sample": f"{n} oracle PA Mults (gather, mass, diffusion, CSR scatter; OpenMP) on the same "
+                  f"{fes.ndofs}-DoF mesh, {dt:.1f} s",
+    }
+
+
+if __name__ == "__main__":
+    main()

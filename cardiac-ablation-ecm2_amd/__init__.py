@@ -69,6 +69,7 @@ def load_library(path: str = LIB_PATH):
         "ecm2_mesh_set_vertices": (i32, [vp, vp]),
         "ecm2_mesh_get_elements": (i32, [vp, vp]),
         "ecm2_mesh_get_element_nodes": (i32, [vp, vp]),
+        "ecm2_mesh_quadrature_points": (i32, [vp, i32, vp]),
         "ecm2_mesh_destroy": (None, [vp]),
         "ecm2_h1space_create": (i32, [vp, i32, i32, pp]),
         "ecm2_h1space_info": (i32, [vp, ip, ip, ip]),
@@ -191,6 +192,12 @@ class Mesh:
     def elements(self) -> np.ndarray:
         out = np.empty((self.GetNE(), 8), np.int32)
         _check(_lib.ecm2_mesh_get_elements(self._h, _np_ptr(out)))
+        return out
+
+    def quadrature_points(self, q1d: int) -> np.ndarray:
+        """Physical Gauss-Legendre points [ne][q1d^3][3] (FunctionCoefficient projection points)."""
+        out = np.empty((self.GetNE(), q1d ** 3, 3), np.float64)
+        _check(_lib.ecm2_mesh_quadrature_points(self._h, q1d, _np_ptr(out)))
         return out
 
     def element_nodes(self) -> np.ndarray:

@@ -2,6 +2,7 @@
 // catches ecm2::Error / std::exception, records the message and returns a code.
 #include "../../include/ecm2_pa.h"
 
+#include "fe.hpp"
 #include "mesh.hpp"
 #include "pa_form.hpp"
 
@@ -130,6 +131,34 @@ int ecm2_mesh_get_element_nodes(const ecm2_mesh *m, double *out)
       std::vector<double> en;
       m->m.element_nodes(en);
       std::memcpy(out, en.data(), en.size() * sizeof(double));
+   });
+}
+
+int ecm2_mesh_quadrature_points(const ecm2_mesh *m, int q1d, double *out)
+{
+   return guard([&] {
+      NEED(m); NEED(out);
+      ECM2_VERIFY(q1d >= 1 && q1d <= ecm2::MAX_Q1D, ecm2::ERR_ARG, "bad q1d " << q1d);
+      std::vector<double> x(q1d), w(q1d), en;
+      ecm2::gauss_legendre(q1d, x.data(), w.data());
+      m->m.element_nodes(en);
+      const int nq = q1d * q1d * q1d;
+      for (int e = 0; e < m->m.ne; e++)
+         for (int q = 0; q < nq; q++)
+         {
+            const double xi[3] = {x[q % q1d], x[(q / q1d) % q1d], x[q / (q1d * q1d)]};
+            for (int c = 0; c < 3; c++)
+            {
+               double v = 0.0;
+               for (int a = 0; a < 8; a++)
+               {
+                  const int ax = a & 1, ay = (a >> 1) & 1, az = a >> 2;
+                  v += (ax ? xi[0] : 1 - xi[0]) * (ay ? xi[1] : 1 - xi[1]) *
+                       (az ? xi[2] : 1 - xi[2]) * en[(size_t)e * 24 + c * 8 + a];
+               }
+               out[((size_t)e * nq + q) * 3 + c] = v;
+            }
+         }
    });
 }
 

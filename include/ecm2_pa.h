@@ -73,6 +73,10 @@ int ecm2_mesh_set_vertices(ecm2_mesh *m, const double *in /* host [nv][3] */);
 int ecm2_mesh_get_elements(const ecm2_mesh *m, int *out /* host [ne][8], native order */);
 /* Lexicographic corner coordinates, host out[ne][3][8]. */
 int ecm2_mesh_get_element_nodes(const ecm2_mesh *m, double *out);
+/* Physical coordinates of the Gauss-Legendre quadrature points of every element, host
+ * out[ne][q1d^3][3] (q lexicographic, qx fastest): the points a FunctionCoefficient is
+ * projected at (Coefficient::Project, fem/coefficient.cpp:52-70). */
+int ecm2_mesh_quadrature_points(const ecm2_mesh *m, int q1d, double *out);
 void ecm2_mesh_destroy(ecm2_mesh *m);
 
 /* H1_FECollection(order) + FiniteElementSpace: element->dof table in

@@ -1,0 +1,89 @@
+"""Test helpers: coefficient functions and mesh fixtures shared by CPU and GPU tests.
+
+Coefficients restate tests/unit/fem/test_pa_coeff.cpp:45-58 (coeffFunction) and the
+non-aligned Cartesian mesh of test_pa_coeff.cpp:22-42; the bioheat coefficients
+follow SURVEY §8(d) (alpha = rho*c_eff, beta = gamma*dt*k(T)).
+"""
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+# Relative tolerance of every FP64 parity check: ||y - y_ref||_inf / ||y_ref||_inf.
+RTOL = 1e-12
+
+
+def nonaligned(V):
+    """MakeCartesianNonaligned vertex remap (test_pa_coeff.cpp:33-39)."""
+    V = np.array(V, dtype=np.float64, copy=True)
+    V[:, 1] += 0.2 * V[:, 0]
+    V[:, 2] += 0.3 * V[:, 0]
+    return V
+
+
+def coeff_function(P):
+    """coeffFunction, 3D branch (test_pa_coeff.cpp:45-58)."""
+    return np.sin(8.0 * np.pi * P[..., 0]) * np.cos(6.0 * np.pi * P[..., 1]) * np.sin(4.0 * np.pi * P[..., 2]) + 2.0
+
+
+def alpha_bioheat(P):
+    """rho*c_eff = 3.6e6 (1 + 0.1 sin 3x)  [J/(m^3 K)], heat capacity + gamma*dt*w_b*c_b folded in."""
+    return 3.6e6 * (1.0 + 0.1 * np.sin(3.0 * P[..., 0]))
+
+
+def temperature(P):
+    """T = 37 + 20 exp(-10 |p|^2) (ablation hot spot)."""
+    return 37.0 + 20.0 * np.exp(-10.0 * np.sum(P * P, axis=-1))
+
+
+def k_of_T(T):
+    """Pennes conductivity law k(T) = 0.5 (1 + 0.0012 (T - 37))."""
+    return 0.5 * (1.0 + 0.0012 * (T - 37.0))
+
+
+def relerr(y, yref):
+    y, yref = np.asarray(y), np.asarray(yref)
+    den = np.abs(yref).max()
+    return float(np.abs(y - yref).max() / (den if den > 0 else 1.0))
+
+
+def read_mfem_mesh(path):
+    """Independent numpy parser of an MFEM v1.0 hex mesh (for the reference's data fixtures).
+
+    Returns (vertices [nv][3], elements [ne][8] native order)."""
+    lines = []
+    for raw in open(path):
+        s = raw.split("#")[0].strip()
+        if s:
+            lines.append(s)
+    assert lines[0].startswith("MFEM mesh v1.0")
+    i, V, E = 1, None, None
+    while i < len(lines):
+        key = lines[i]
+        if key == "elements":
+            n = int(lines[i + 1])
+            E = np.array([[int(t) for t in lines[i + 2 + k].split()[2:]] for k in range(n)], np.int32)
+            i += 2 + n
+        elif key == "boundary":
+            n = int(lines[i + 1])
+            i += 2 + n
+        elif key == "vertices":
+            n = int(lines[i + 1])
+            V = np.array([[float(t) for t in lines[i + 3 + k].split()] for k in range(n)])
+            i += 3 + n
+        else:
+            i += 1
+    return V, E
+
+
+LEX_TO_NATIVE = [0, 1, 3, 2, 4, 5, 7, 6]
+
+
+def element_nodes_from(V, E):
+    """Lexicographic corner coordinates [ne][3][8] from native-order elements."""
+    en = np.empty((E.shape[0], 3, 8))
+    for a in range(8):
+        en[:, :, a] = V[E[:, LEX_TO_NATIVE[a]]]
+    return en

@@ -1,0 +1,305 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Bar: ||y_gpu - y_oracle||_inf / ||y_oracle||_inf <= RTOL = 1e-12 in FP64,
+for every kernel variant, order, mesh and coefficient kind, plus the committed golden
+vectors, the reference-shaped pieces (restriction, per-integrator AddMultPA, qdata,
+diagonal), the PCG caller, edge cases, and full BASELINE sizes."""
+import numpy as np
+import pytest
+
+import ecm2_amd as E
+import oracle as O
+from helpers import (GOLDEN, RTOL, alpha_bioheat, coeff_function, k_of_T, nonaligned, relerr,
+                     temperature)
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    E.load_library()
+    yield
+    torch.cuda.synchronize()
+
+
+def dev(a, dtype=torch.float64):
+    return torch.as_tensor(np.ascontiguousarray(a)).to(device="cuda", dtype=dtype)
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy()
+
+
+def make_mesh(name):
+    if name == "nonaligned":
+        m = E.Mesh.MakeCartesian3D(5, 4, 3)            # 60 elements: not a multiple of 64
+        m.set_vertices(nonaligned(m.vertices()))
+    elif name == "fichera_r1":
+        m = E.Mesh(f"{GOLDEN}/fichera.mesh")
+        m.UniformRefinement()                          # 56 elements
+    elif name == "inline_hex":
+        m = E.Mesh(f"{GOLDEN}/inline-hex.mesh")        # 64 elements
+    elif name == "cart_130":
+        m = E.Mesh.MakeCartesian3D(13, 5, 2, 2.0, 1.0, 0.5)  # 130 elements: 3 blocks, ragged
+    else:
+        raise ValueError(name)
+    return m
+
+
+def build_pair(mesh, order, alpha, beta, kernel=E.KERNEL_AUTO, numbering=E.NUMBERING_ENTITY):
+    """Product form + oracle operator on the same mesh; alpha/beta: 'fn', 'bio', float or None."""
+    fes = E.H1Space(mesh, order, numbering)
+    en = mesh.element_nodes()
+    q1d = O.default_q1d(order)
+    P = O.quad_points(en, q1d)
+
+    def coeff(spec):
+        if spec is None:
+            return None, None
+        if spec == "fn":
+            c = coeff_function(P)
+        elif spec == "bio_a":
+            c = alpha_bioheat(P)
+        elif spec == "bio_b":
+            c = k_of_T(temperature(P))
+        else:
+            return float(spec), E.ConstantCoefficient(float(spec))
+        return c, E.QuadratureCoefficient(dev(c.reshape(fes.ne, -1)))
+
+    a_np, a_c = coeff(alpha)
+    b_np, b_c = coeff(beta)
+    form = E.BilinearForm(fes, kernel=kernel)
+    if a_c is not None:
+        form.AddDomainIntegrator(E.MassIntegrator(a_c))
+    if b_c is not None:
+        form.AddDomainIntegrator(E.DiffusionIntegrator(b_c))
+    form.Assemble()
+    op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=a_np, beta=b_np)
+    return fes, form, op
+
+
+KERNELS = {"tpe": E.KERNEL_TPE, "wpe": E.KERNEL_WPE, "unfused": E.KERNEL_UNFUSED}
+
+
+@pytest.mark.parametrize("mesh_name", ["nonaligned", "fichera_r1", "inline_hex", "cart_130"])
+@pytest.mark.parametrize("order", [1, 2, 3, 4])
+@pytest.mark.parametrize("kernel", ["tpe", "wpe", "unfused"])
+def test_mult_matches_oracle(mesh_name, order, kernel):
+    if kernel == "tpe" and order > 2:
+        pytest.skip("thread-per-element kernel covers p = 1, 2")
+    m = make_mesh(mesh_name)
+    fes, form, op = build_pair(m, order, "fn", "fn", kernel=KERNELS[kernel])
+    x = np.random.default_rng(order).uniform(-1, 1, fes.ndofs)
+    y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    form.Mult(dev(x), y)
+    assert relerr(host(y), op.mult(x)) <= RTOL
+
+
+@pytest.mark.parametrize("order", [1, 2, 3])
+@pytest.mark.parametrize("integ", ["mass", "diffusion", "both"])
+def test_single_integrators_and_constants(order, integ):
+    m = make_mesh("nonaligned")
+    alpha = 2.5 if integ in ("mass", "both") else None
+    beta = 0.7 if integ in ("diffusion", "both") else None
+    fes, form, op = build_pair(m, order, alpha, beta)
+    x = np.random.default_rng(7).uniform(-1, 1, fes.ndofs)
+    y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    form.Mult(dev(x), y)
+    assert relerr(host(y), op.mult(x)) <= RTOL
+
+
+@pytest.mark.parametrize("kernel", ["tpe", "wpe"])
+@pytest.mark.parametrize("order", [1, 2])
+def test_qdata_matches_reference_setup(kernel, order):
+    """pa_data == PADiffusionSetup3D / mass setup restated (bilininteg_diffusion_kernels.cpp:243-367)."""
+    m = make_mesh("fichera_r1")
+    fes, form, op = build_pair(m, order, "bio_a", "bio_b", kernel=KERNELS[kernel])
+    qd = form.qdata(E.DIFFUSION)
+    qm = form.qdata(E.MASS)[:, 0, :]
+    assert relerr(qd, op.D) < 1e-13
+    assert relerr(qm, op.M) < 1e-13
+
+
+def test_jacobian_geometry_path():
+    """set_jacobians (GeometricFactors layout) gives the same operator as element nodes."""
+    m = make_mesh("nonaligned")
+    order = 2
+    fes = E.H1Space(m, order)
+    en = m.element_nodes()
+    q1d = O.default_q1d(order)
+    _, J, _ = O.geom(en, q1d)
+    form = E.BilinearForm(fes, geometry="jacobians")
+    form.SetJacobians(dev(J))
+    form.AddDomainIntegrator(E.MassIntegrator(E.ConstantCoefficient(3.0)))
+    form.AddDomainIntegrator(E.DiffusionIntegrator(E.ConstantCoefficient(0.5)))
+    form.Assemble()
+    op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=3.0, beta=0.5)
+    x = np.random.default_rng(5).uniform(-1, 1, fes.ndofs)
+    y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    form.Mult(dev(x), y)
+    assert relerr(host(y), op.mult(x)) <= RTOL
+
+
+@pytest.mark.parametrize("order", [1, 2, 4])
+def test_restriction_and_integrator_pieces(order):
+    """ElementRestriction::Mult/MultTranspose and each AddMultPA on E-vectors."""
+    m = make_mesh("cart_130")
+    fes, form, op = build_pair(m, order, "fn", "fn")
+    x = np.random.default_rng(11).uniform(-1, 1, fes.ndofs)
+    nd = fes.nd
+    xe = torch.empty(fes.ne * nd, dtype=torch.float64, device="cuda")
+    form.RestrictionMult(dev(x), xe)
+    xe_ref = O.restriction_mult(fes.gather_map(), x)
+    assert np.array_equal(host(xe).reshape(fes.ne, nd), xe_ref)
+    ye = np.random.default_rng(12).uniform(-1, 1, (fes.ne, nd))
+    y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    form.RestrictionMultTranspose(dev(ye), y)
+    assert relerr(host(y), O.restriction_mult_transpose(op.off, op.idx, ye)) < 1e-15
+    for kind, ref in ((E.MASS, O.mass_apply(op.B, op.M, xe_ref)),
+                      (E.DIFFUSION, O.diffusion_apply(op.B, op.G, op.D, xe_ref))):
+        out = torch.zeros(fes.ne * nd, dtype=torch.float64, device="cuda")
+        form.IntegratorAddMultPA(kind, dev(xe_ref), out)
+        assert relerr(host(out).reshape(fes.ne, nd), ref) <= RTOL
+
+
+@pytest.mark.parametrize("order", [1, 2, 3, 4])
+def test_diagonal_matches_oracle(order):
+    m = make_mesh("fichera_r1")
+    fes, form, op = build_pair(m, order, "fn", "fn")
+    d = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    form.AssembleDiagonal(d)
+    assert relerr(host(d), op.diagonal()) < 1e-13
+
+
+def test_gridfunction_pennes_coefficient():
+    """beta = gamma*dt*k(T) with T an H1 grid function: GridFunctionCoefficient projected to
+    quadrature points (qfunction.cpp:73-98) then the affine Pennes law."""
+    m = make_mesh("fichera_r1")
+    order = 2
+    fes = E.H1Space(m, order)
+    en = m.element_nodes()
+    T = temperature(fes.dof_coords())
+    scale, slope, tref = 0.5 * 0.1, 0.0012, 37.0
+    form = E.BilinearForm(fes)
+    form.AddDomainIntegrator(E.MassIntegrator(E.ConstantCoefficient(3.6e6)))
+    form.AddDomainIntegrator(E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(dev(T), scale, slope, tref)))
+    form.Assemble()
+    q1d = O.default_q1d(order)
+    Tq = O.interp_evector(T[fes.gather_map()], order, q1d)
+    beta = scale * (1.0 + slope * (Tq - tref))
+    op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=3.6e6, beta=beta)
+    x = np.random.default_rng(9).uniform(-1, 1, fes.ndofs)
+    y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    form.Mult(dev(x), y)
+    assert relerr(host(y), op.mult(x)) <= RTOL
+
+
+@pytest.mark.parametrize("jacobi", [True, False])
+def test_pcg_matches_oracle(jacobi):
+    m = make_mesh("fichera_r1")
+    order = 2
+    fes, form, op = build_pair(m, order, 1.0, "fn")
+    ess = fes.boundary_dofs()
+    b = np.random.default_rng(4).uniform(-1, 1, fes.ndofs)
+    x = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    it, nrm = form.PCG(dev(b), x, ess=dev(ess, torch.int32), rel_tol=1e-12, max_iter=2000, jacobi=jacobi)
+    xr, itr, _ = op.pcg(b, ess, rel_tol=1e-12, max_iter=2000, jacobi=jacobi)
+    assert abs(it - itr) <= 2
+    assert relerr(host(x), xr) < 1e-9
+
+
+def test_golden_vectors():
+    g = np.load(f"{GOLDEN}/oracle_golden.npz")
+    for order in (1, 2, 3):
+        m = E.Mesh.MakeCartesian3D(2, 2, 2)
+        m.set_vertices(nonaligned(m.vertices()))
+        fes = E.H1Space(m, order, E.NUMBERING_STRUCTURED)
+        _, form, _ = build_pair(m, order, "fn", "fn", numbering=E.NUMBERING_STRUCTURED)
+        y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+        form.Mult(dev(g[f"p{order}_x"]), y)
+        assert relerr(host(y), g[f"p{order}_y"]) <= RTOL
+        d = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+        form.AssembleDiagonal(d)
+        assert relerr(host(d), g[f"p{order}_diag"]) < 1e-13
+
+
+def test_edge_cases():
+    # single element, p = 2 and p = 4
+    for order in (2, 4):
+        m = E.Mesh.MakeCartesian3D(1, 1, 1)
+        fes, form, op = build_pair(m, order, "fn", "fn")
+        x = np.random.default_rng(1).uniform(-1, 1, fes.ndofs)
+        y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+        form.Mult(dev(x), y)
+        assert relerr(host(y), op.mult(x)) <= RTOL
+    # zero input -> zero output; Mult before Assemble raises
+    m = make_mesh("nonaligned")
+    fes = E.H1Space(m, 2)
+    f2 = E.BilinearForm(fes)
+    f2.AddDomainIntegrator(E.MassIntegrator())
+    y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    with pytest.raises(E.ECM2Error):
+        f2.Mult(torch.zeros_like(y), y)
+    f2.Assemble()
+    f2.Mult(torch.zeros_like(y), y)
+    assert float(y.abs().max()) == 0.0
+    # a dof referenced by no element (extra unused dof) -> 0, like ElementRestriction::MultTranspose
+    gm = fes.gather_map()
+    f3 = E.load_library()
+    import ctypes
+    h = ctypes.c_void_p()
+    E._check(f3.ecm2_pa_form_create(fes.ne, 2, fes.ndofs + 5, ctypes.c_void_p(gm.ctypes.data), 0, ctypes.byref(h)))
+    en = m.element_nodes()
+    E._check(f3.ecm2_pa_form_set_element_nodes(h, ctypes.c_void_p(en.ctypes.data)))
+    one = (ctypes.c_double * 1)(1.0)
+    E._check(f3.ecm2_pa_form_add_integrator(h, E.MASS, E.COEFF_CONSTANT, ctypes.cast(one, ctypes.c_void_p), None))
+    E._check(f3.ecm2_pa_form_assemble(h, E._stream()))
+    xx = torch.ones(fes.ndofs + 5, dtype=torch.float64, device="cuda")
+    yy = torch.full_like(xx, 7.0)
+    E._check(f3.ecm2_pa_form_mult(h, E._dev_ptr(xx), E._dev_ptr(yy), E._stream()))
+    assert np.all(host(yy)[-5:] == 0.0)
+    f3.ecm2_pa_form_destroy(h)
+    # invalid gather map is rejected
+    bad = gm.copy()
+    bad[0, 0] = fes.ndofs + 100
+    with pytest.raises(E.ECM2Error):
+        E._check(f3.ecm2_pa_form_create(fes.ne, 2, fes.ndofs, ctypes.c_void_p(bad.ctypes.data), 0, ctypes.byref(h)))
+
+
+@pytest.mark.parametrize("numbering", [E.NUMBERING_STRUCTURED, E.NUMBERING_ENTITY])
+def test_full_size_c2(numbering):
+    """BASELINE config[1] (inline-hex refined to ~1M DoF, p = 2) at full size: direct oracle
+    parity, plus size-independent properties (linearity, symmetry, 1^T M 1 = int alpha)."""
+    n = 50
+    m = E.Mesh.MakeCartesian3D(n, n, n)
+    fes, form, op = build_pair(m, 2, "bio_a", "bio_b", numbering=numbering)
+    assert fes.ndofs == 1030301
+    rng = np.random.default_rng(21)
+    x1 = rng.uniform(-1, 1, fes.ndofs)
+    x2 = rng.uniform(-1, 1, fes.ndofs)
+    y1 = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    y2 = torch.empty_like(y1)
+    y3 = torch.empty_like(y1)
+    form.Mult(dev(x1), y1)
+    form.Mult(dev(x2), y2)
+    form.Mult(dev(2.0 * x1 - 3.0 * x2), y3)
+    h1, h2, h3 = host(y1), host(y2), host(y3)
+    assert relerr(h1, op.mult(x1)) <= RTOL
+    assert relerr(h3, 2.0 * h1 - 3.0 * h2) <= 1e-12
+    assert abs(x2 @ h1 - x1 @ h2) <= 1e-12 * abs(x2) @ np.abs(h1)
+
+
+def test_full_size_c4_tpe():
+    """configs[3] size (Cartesian 108^3, p = 2, 10.2M DoF) on one GPU against the oracle."""
+    n = 108
+    m = E.Mesh.MakeCartesian3D(n, n, n)
+    fes, form, op = build_pair(m, 2, "bio_a", "bio_b", numbering=E.NUMBERING_STRUCTURED)
+    assert fes.ndofs == 10218313
+    x = np.random.default_rng(22).uniform(-1, 1, fes.ndofs)
+    y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    form.Mult(dev(x), y)
+    assert relerr(host(y), op.mult(x)) <= RTOL

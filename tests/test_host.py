@@ -1,0 +1,136 @@
+"""CPU tests of the product's host side: the C-ABI library loads and exports the
+declared symbols, and the setup logic (mesh ingest, refinement, H1 numbering,
+boundary dofs) is correct.  No compute entry point runs here (no GPU)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import ecm2_amd as E
+import oracle as O
+from helpers import GOLDEN, element_nodes_from, nonaligned, read_mfem_mesh, relerr
+
+
+def test_library_exports_every_declared_symbol():
+    lib = E.load_library()
+    names = E.declared_symbols()
+    assert len(names) >= 30
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_compute_entry_points_fail_loudly_without_gpu():
+    """No CPU fallback: creating a PA form without a device must raise ECM2_ERR_HIP."""
+    lib = E.load_library()
+    if lib.ecm2_device_count() > 0:
+        pytest.skip("a GPU is visible")
+    gm = np.zeros((1, 8), np.int32)
+    h = ctypes.c_void_p()
+    rc = lib.ecm2_pa_form_create(1, 1, 1, ctypes.c_void_p(gm.ctypes.data), 0, ctypes.byref(h))
+    assert rc == 2  # ECM2_ERR_HIP
+    assert b"no HIP device" in lib.ecm2_last_error()
+
+
+def test_cartesian_mesh_matches_make3d_layout():
+    m = E.Mesh.MakeCartesian3D(3, 2, 2, 1.5, 1.0, 2.0)
+    assert (m.GetNV(), m.GetNE()) == (36, 12)
+    V, el = m.vertices(), m.elements()
+    # vertex (x,y,z) -> x + (nx+1)(y + (ny+1) z), element vertices per Make3D (mesh.cpp:3784-3791)
+    assert np.allclose(V[1], [0.5, 0, 0]) and np.allclose(V[4], [0, 0.5, 0])
+    assert list(el[0]) == [0, 1, 5, 4, 12, 13, 17, 16]
+    en_prod = m.element_nodes()
+    en_orc, _, _, _ = O.cartesian_mesh(3, 2, 2, 1.5, 1.0, 2.0, order=1)
+    assert np.array_equal(en_prod, en_orc)
+
+
+def test_mesh_readers_against_reference_fixtures():
+    """data/fichera.mesh and data/inline-hex.mesh (reference fixtures) parse to the same
+    vertices/elements as an independent parser."""
+    m = E.Mesh(f"{GOLDEN}/fichera.mesh")
+    V, El = read_mfem_mesh(f"{GOLDEN}/fichera.mesh")
+    assert np.array_equal(m.vertices(), V) and np.array_equal(m.elements(), El)
+    mi = E.Mesh(f"{GOLDEN}/inline-hex.mesh")
+    assert (mi.GetNV(), mi.GetNE()) == (125, 64)
+
+
+@pytest.mark.parametrize("order", [1, 2, 3, 4])
+def test_h1_numbering_conforming(order):
+    """Every dof gets the same coordinate from every element that holds it, ndofs obeys
+    V + (p-1)E + (p-1)^2 F + (p-1)^3 NE, and boundary dofs lie on the boundary."""
+    m = E.Mesh(f"{GOLDEN}/fichera.mesh")
+    m.UniformRefinement()
+    fes = E.H1Space(m, order)
+    gm = fes.gather_map()
+    en = m.element_nodes()
+    nodes, _ = O.gauss_lobatto(order + 1)
+    D = order + 1
+    coords = fes.dof_coords()
+    for k in range(D):
+        for j in range(D):
+            for i in range(D):
+                xi = (nodes[i], nodes[j], nodes[k])
+                s = np.zeros((fes.ne, 3))
+                for a in range(8):
+                    ax, ay, az = a & 1, (a >> 1) & 1, a >> 2
+                    N = (xi[0] if ax else 1 - xi[0]) * (xi[1] if ay else 1 - xi[1]) * (xi[2] if az else 1 - xi[2])
+                    s += N * en[:, :, a]
+                assert np.abs(coords[gm[:, (k * D + j) * D + i]] - s).max() < 1e-12
+    assert np.unique(gm).size == fes.ndofs
+    # counts: fichera r1 = 56 hexes
+    nv = m.GetNV()
+    el = m.elements()
+    edges = set()
+    faces = {}
+    for e in el:
+        c = [e[i] for i in E_LEX]
+        for a, b in EDGES:
+            edges.add((min(c[a], c[b]), max(c[a], c[b])))
+        for f in FACES:
+            key = tuple(sorted(c[i] for i in f))
+            faces[key] = faces.get(key, 0) + 1
+    p = order
+    assert fes.ndofs == nv + (p - 1) * len(edges) + (p - 1) ** 2 * len(faces) + (p - 1) ** 3 * m.GetNE()
+    bd = fes.boundary_dofs()
+    nb_faces = sum(1 for v in faces.values() if v == 1)
+    assert nb_faces == 7 * 4 * 3 * 2 - 0 or nb_faces > 0
+    # boundary dofs of the fichera: x, y or z on the outer box [-1,1]^3 or on the notch planes
+    bc = coords[bd]
+    on = np.zeros(len(bd), bool)
+    for c in range(3):
+        on |= np.isclose(np.abs(bc[:, c]), 1.0) | np.isclose(bc[:, c], 0.0)
+    assert on.all()
+
+
+E_LEX = [0, 1, 3, 2, 4, 5, 7, 6]
+EDGES = [(0, 1), (2, 3), (4, 5), (6, 7), (0, 2), (1, 3), (4, 6), (5, 7), (0, 4), (1, 5), (2, 6), (3, 7)]
+FACES = [(0, 2, 4, 6), (1, 3, 5, 7), (0, 1, 4, 5), (2, 3, 6, 7), (0, 1, 2, 3), (4, 5, 6, 7)]
+
+
+def test_uniform_refinement_preserves_geometry():
+    m = E.Mesh(f"{GOLDEN}/fichera.mesh")
+    en0 = m.element_nodes()
+    m.UniformRefinement()
+    assert m.GetNE() == 56
+    en1 = m.element_nodes()
+    # volume preserved (trilinear fichera hexes are affine cubes)
+    def vol(en):
+        return np.abs(np.prod(en.max(axis=2) - en.min(axis=2), axis=1)).sum()
+    assert abs(vol(en0) - vol(en1)) < 1e-12
+
+
+@pytest.mark.parametrize("order", [1, 2, 3])
+def test_structured_and_entity_numbering_give_same_operator(order):
+    """Both numberings describe the same space: the oracle operator agrees dof-by-coordinate."""
+    m = E.Mesh.MakeCartesian3D(3, 2, 2)
+    m.set_vertices(nonaligned(m.vertices()))
+    en = m.element_nodes()
+    outs = []
+    for num in (E.NUMBERING_ENTITY, E.NUMBERING_STRUCTURED):
+        fes = E.H1Space(m, order, num)
+        xyz = fes.dof_coords()
+        op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=1.0, beta=2.0)
+        x = np.sin(3 * xyz[:, 0]) * np.cos(xyz[:, 1]) + xyz[:, 2]
+        y = op.mult(x)
+        order_idx = np.lexsort(np.round(xyz, 10).T)
+        outs.append(y[order_idx])
+    assert relerr(outs[0], outs[1]) < 1e-13

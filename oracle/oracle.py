@@ -24,6 +24,7 @@ def build():
 
 def lib():
     global _lib
+    _KEEP.clear()  # lib() is evaluated before the arguments of each call expression
     if _lib is None:
         if not os.path.exists(LIB):
             build()
@@ -58,8 +59,20 @@ def lib():
     return _lib
 
 
+_KEEP = []
+
+
 def _p(a):
-    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+    """Pointer to a numpy array; the array is kept alive until the next _release()
+    (a bare c_void_p does not hold a reference, so temporaries would be freed)."""
+    if a is None:
+        return None
+    _KEEP.append(a)
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def _release():
+    _KEEP.clear()
 
 
 def _f64(a):

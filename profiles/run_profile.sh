@@ -1,0 +1,18 @@
+#!/bin/bash
+# Collects the rocprofv3 evidence for bench.py on the GPU box (run from the repo root):
+#   1) --kernel-trace --stats  (per-kernel durations; must agree with bench's HIP-event timing)
+#   2) --pmc FETCH_SIZE and 3) --pmc WRITE_SIZE in separate passes (TCC slots, MI355X_MICROARCH.md)
+# Usage: bash profiles/run_profile.sh <tag> [bench args...]
+set -euo pipefail
+TAG=${1:-c2}; shift || true
+ARGS=${*:---steps 50 --warmup 5}
+OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/prof_${TAG}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -T -d "$OUT/trace" -o run --output-format csv \
+  -- python3 bench.py $ARGS --no-cpu-baseline > "$OUT/bench_trace.json"
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -T -d "$OUT/fetch" -o run --output-format csv \
+  -- python3 bench.py $ARGS --no-cpu-baseline > "$OUT/bench_fetch.json"
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -T -d "$OUT/write" -o run --output-format csv \
+  -- python3 bench.py $ARGS --no-cpu-baseline > "$OUT/bench_write.json"
+find "$OUT" -name "*.csv" | sort

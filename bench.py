@@ -50,21 +50,20 @@ def temperature_fn(X):
 K_SCALE, K_SLOPE, K_TREF = 0.5 * 0.05, 0.0012, 37.0  # gamma*dt*k0, dk/dT / k0, T0
 
 
-def build_local_problem(E, torch, nx, ny, nz, z0, z1, sz_total):
-    """Mesh slab [z0, z1) of a Cartesian nx x ny x nz_total box; returns (mesh, fes, form)."""
-    nzl = z1 - z0
-    h = 1.0 / nx
-    mesh = E.Mesh.MakeCartesian3D(nx, ny, nzl, 1.0, ny * h, nzl * h)
-    if z0:
-        V = mesh.vertices()
-        V[:, 2] += z0 * h
-        mesh.set_vertices(V)
-    fes = E.H1Space(mesh, 2, E.NUMBERING_STRUCTURED)
+def bioheat_coefficients(E, torch, mesh, fes, part=None):
+    """alpha = rho*c_eff(x) at quadrature points (FunctionCoefficient projection) and the
+    temperature grid function T (L-vector) for beta = gamma*dt*k(T)."""
     q1d = 4
-    P = mesh.quadrature_points(q1d)
-    alpha = torch.as_tensor(alpha_fn(P).reshape(fes.ne, -1)).cuda()
-    T = torch.as_tensor(temperature_fn(fes.dof_coords())).cuda()
-    return mesh, fes, alpha, T
+    X = fes.dof_coords()
+    T = temperature_fn(X)
+    if part is None:
+        P = mesh.quadrature_points(q1d)
+        alpha = alpha_fn(P).reshape(fes.ne, -1)
+    else:
+        P = E.quadrature_points_subset(mesh, q1d, part.elems)
+        alpha = alpha_fn(P).reshape(part.ne_local, -1)
+        T = T[part.local_to_global]
+    return torch.as_tensor(alpha).cuda(), torch.as_tensor(T).cuda()
 
 
 def main():
@@ -76,6 +75,8 @@ def main():
     ap.add_argument("--kernel", choices=["auto", "tpe", "wpe", "unfused"], default="auto")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--loopback", type=int, default=1,
+                    help="N>1 on one GPU: N subdomains in this process (validation of the partitioned path)")
     args = ap.parse_args()
 
     import torch
@@ -104,29 +105,55 @@ def main():
         nx = ny = nz_total = 108
         scaling = "strong"
         workload = "configs[3]: Cartesian 108^3 (10.2M DoF) split over GPUs, H1 p=2, Mass+Diffusion PA Mult"
-    # z-slab partition (CartesianPartitioning along z, mesh.cpp:8966)
-    zb = [(nz_total * r) // world for r in range(world + 1)]
-    z0, z1 = zb[rank], zb[rank + 1]
-    mesh, fes, alpha, T = build_local_problem(E, torch, nx, ny, nz_total, z0, z1, nz_total)
-
-    if world == 1:
+    mesh = E.Mesh.MakeCartesian3D(nx, ny, nz_total, 1.0, ny / nx, nz_total / nx)
+    fes = E.H1Space(mesh, 2, E.NUMBERING_STRUCTURED)
+    nsub = world if world > 1 else args.loopback
+    mass = lambda a: E.MassIntegrator(E.QuadratureCoefficient(a))
+    diff = lambda T: E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(T, K_SCALE, K_SLOPE, K_TREF))
+    if nsub <= 1:
+        alpha, T = bioheat_coefficients(E, torch, mesh, fes)
         form = E.BilinearForm(fes, kernel=kernel)
-        form.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(alpha)))
-        form.AddDomainIntegrator(E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(T, K_SCALE, K_SLOPE, K_TREF)))
+        form.AddDomainIntegrator(mass(alpha))
+        form.AddDomainIntegrator(diff(T))
         form.Assemble()
         n_true = fes.ndofs
         apply = form.Mult
-        timed_form = form
+        timed_forms = [form]
     else:
-        pform = E.ParBilinearForm(fes, rank, world, z0, z1, nz_total, kernel=kernel)
-        pform.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(alpha)))
-        pform.AddDomainIntegrator(E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(T, K_SCALE, K_SLOPE, K_TREF)))
-        pform.Assemble()
-        n_true = pform.true_size
-        apply = pform.Mult
-        timed_form = pform.local_form
+        # z-slab partition (CartesianPartitioning along z, mesh.cpp:8966)
+        er = E.partition_slabs_z(mesh, nsub)
+        if world > 1:
+            rid = [E.rccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(rid, src=0)
+            part = E.Partition(fes, er, rank, world)
+            pform = E.ParBilinearForm(part, rccl_id=rid[0], kernel=kernel)
+            alpha, T = bioheat_coefficients(E, torch, mesh, fes, part)
+            pform.AddDomainIntegrator(mass(alpha))
+            pform.AddDomainIntegrator(diff(T))
+            pform.Assemble()
+            n_true = part.n_owned
+            apply = pform.Mult
+            timed_forms = [pform]
+        else:
+            # --loopback: all subdomains in this process on one GPU (exchange by device copies)
+            forms, keep = [], []
+            for r in range(nsub):
+                part = E.Partition(fes, er, r, nsub)
+                pf = E.ParBilinearForm(part, kernel=kernel)
+                alpha, T = bioheat_coefficients(E, torch, mesh, fes, part)
+                keep += [alpha, T]
+                pf.AddDomainIntegrator(mass(alpha))
+                pf.AddDomainIntegrator(diff(T))
+                pf.Assemble()
+                forms.append(pf)
+            group = E.ParGroup(forms)
+            xs = [torch.empty(f.true_size, dtype=torch.float64, device="cuda").uniform_(-1, 1) for f in forms]
+            ys = [torch.empty_like(v) for v in xs]
+            n_true = sum(f.true_size for f in forms)
+            apply = lambda _x, _y: group.Mult(xs, ys)
+            timed_forms = forms
 
-    x = torch.empty(n_true if world > 1 else fes.ndofs, dtype=torch.float64, device="cuda")
+    x = torch.empty(n_true, dtype=torch.float64, device="cuda")
     x.uniform_(-1.0, 1.0, generator=torch.Generator(device="cuda").manual_seed(1 + rank))
     y = torch.empty_like(x)
     torch.cuda.synchronize()
@@ -137,7 +164,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    timed_form.timing(True)
+    for f in timed_forms:
+        f.timing(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         apply(x, y)
@@ -146,11 +174,14 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    kms, klaunch = timed_form.timing_get()
-    timed_form.timing(False)
+    kms = sum(f.timing_get()[0] for f in timed_forms)
+    for f in timed_forms:
+        f.timing(False)
+    abytes = sum(f.algorithmic_bytes() for f in timed_forms)
 
-    # aggregate over ranks: total true dofs, max time
-    tot = torch.tensor([float(n_true), dt, timed_form.algorithmic_bytes(), kms / max(klaunch, 1)],
+    # aggregate over ranks: total true dofs, max time; kernel ms per Mult (summed over
+    # the apply launches of one Mult: interior + boundary blocks when partitioned)
+    tot = torch.tensor([float(n_true), dt, abytes, kms / args.steps],
                        dtype=torch.float64, device="cuda")
     if world > 1:
         s = tot.clone()
@@ -172,7 +203,7 @@ def main():
             except Exception:
                 traffic = None
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and args.loopback <= 1:
             cpu = cpu_baseline(fes, mesh, alpha, T, args.cpu_baseline_seconds)
         line = {
             "metric": "MDoF/s on PA diffusion+mass Mult, hex p=2; % HBM roofline at 1/2/4/8 GPUs",
@@ -190,10 +221,11 @@ def main():
             "config": {
                 "workload": workload,
                 "ndofs": int(ndofs_total),
-                "elements": int(fes.ne) if world == 1 else None,
+                "elements": int(fes.ne),
                 "order": 2, "q1d": 4,
-                "kernel": ["auto", "tpe", "wpe", "unfused"][timed_form.info()["kernel"]],
-                "parallelism": f"domain-decomposition z-slabs x{world}",
+                "kernel": ["auto", "tpe", "wpe", "unfused"][timed_forms[0].info()["kernel"]],
+                "parallelism": f"domain-decomposition z-slabs x{world}, RCCL shared-DoF exchange" if world > 1
+                else (f"loopback z-slabs x{args.loopback} on one GPU" if args.loopback > 1 else "single GPU"),
             },
             "roofline": {
                 "bound": "hbm",

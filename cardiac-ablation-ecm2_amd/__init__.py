@@ -392,3 +392,186 @@ class BilinearForm:
                                    rel_tol, abs_tol, max_iter, 1 if jacobi else 0,
                                    ctypes.byref(it), ctypes.byref(nrm), _stream(stream)))
         return it.value, nrm.value
+
+
+# ----------------------------------------------------------------------------
+# Distributed form (ParMesh partition + ParBilinearForm over RCCL)
+# ----------------------------------------------------------------------------
+_PAR_SIGS = {
+    "ecm2_partition_slabs_z": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "ecm2_partition_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                             ctypes.POINTER(ctypes.c_void_p)]),
+    "ecm2_partition_info": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_int)] * 6),
+    "ecm2_partition_get": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 7),
+    "ecm2_partition_destroy": (None, [ctypes.c_void_p]),
+    "ecm2_rccl_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
+    "ecm2_par_form_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                            ctypes.POINTER(ctypes.c_void_p)]),
+    "ecm2_par_form_add_integrator": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                                    ctypes.c_void_p]),
+    "ecm2_par_form_set_kernel": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "ecm2_par_form_assemble": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "ecm2_par_form_mult": (ctypes.c_int, [ctypes.c_void_p] * 4),
+    "ecm2_par_group_mult": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_void_p]),
+    "ecm2_par_form_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "ecm2_par_form_timing_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                                                ctypes.POINTER(ctypes.c_long)]),
+    "ecm2_par_form_algorithmic_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]),
+    "ecm2_par_form_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "ecm2_par_form_destroy": (None, [ctypes.c_void_p]),
+    "ecm2_mesh_quadrature_points_subset": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                                          ctypes.c_int, ctypes.c_void_p]),
+}
+
+
+def _par_lib():
+    lib = load_library()
+    if not getattr(lib, "_ecm2_par_ready", False):
+        for name, (res, args) in _PAR_SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype, fn.argtypes = res, args
+        lib._ecm2_par_ready = True
+    return lib
+
+
+def partition_slabs_z(mesh: Mesh, nranks: int) -> np.ndarray:
+    """Mesh::CartesianPartitioning along z: element -> rank."""
+    out = np.empty(mesh.GetNE(), np.int32)
+    _check(_par_lib().ecm2_partition_slabs_z(mesh._h, nranks, _np_ptr(out)))
+    return out
+
+
+def quadrature_points_subset(mesh: Mesh, q1d: int, elems: np.ndarray) -> np.ndarray:
+    elems = np.ascontiguousarray(elems, np.int32)
+    out = np.empty((elems.size, q1d ** 3, 3), np.float64)
+    _check(_par_lib().ecm2_mesh_quadrature_points_subset(mesh._h, q1d, _np_ptr(elems), elems.size, _np_ptr(out)))
+    return out
+
+
+class Partition:
+    """Local view of one rank: [owned | ghost] local L-vector, [interior | boundary]
+    elements, neighbour exchange lists (ParFiniteElementSpace / P)."""
+
+    def __init__(self, fes: H1Space, elem_rank: np.ndarray, rank: int, nranks: int):
+        lib = _par_lib()
+        er = np.ascontiguousarray(elem_rank, np.int32)
+        h = ctypes.c_void_p()
+        _check(lib.ecm2_partition_create(fes._h, _np_ptr(er), rank, nranks, ctypes.byref(h)))
+        self._h = h
+        self.fes, self.rank, self.nranks = fes, rank, nranks
+        v = [ctypes.c_int() for _ in range(6)]
+        _check(lib.ecm2_partition_info(h, *[ctypes.byref(a) for a in v]))
+        self.ne_local, self.ne_interior, self.n_owned, self.n_ghost, self.n_nbrs, self.n_send = [a.value for a in v]
+        nd = fes.nd
+        self.elems = np.empty(self.ne_local, np.int32)
+        self.local_to_global = np.empty(self.n_owned + self.n_ghost, np.int32)
+        self.gather_map = np.empty((self.ne_local, nd), np.int32)
+        self.nbrs = np.empty(self.n_nbrs, np.int32)
+        self.send_off = np.empty(self.n_nbrs + 1, np.int32)
+        self.send_idx = np.empty(max(self.n_send, 1), np.int32)
+        self.recv_off = np.empty(self.n_nbrs + 1, np.int32)
+        _check(lib.ecm2_partition_get(h, _np_ptr(self.elems), _np_ptr(self.local_to_global), _np_ptr(self.gather_map),
+                                      _np_ptr(self.nbrs), _np_ptr(self.send_off), _np_ptr(self.send_idx),
+                                      _np_ptr(self.recv_off)))
+        self.send_idx = self.send_idx[: self.n_send]
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.ecm2_partition_destroy(self._h)
+            self._h = None
+
+    @property
+    def owned_global(self):
+        return self.local_to_global[: self.n_owned]
+
+
+def rccl_unique_id() -> bytes:
+    buf = (ctypes.c_ubyte * 128)()
+    _check(_par_lib().ecm2_rccl_unique_id(ctypes.cast(buf, ctypes.c_void_p)))
+    return bytes(buf)
+
+
+class ParBilinearForm:
+    """ParBilinearForm(PARTIAL): y_true = P^T A_local P x_true.  rccl_id=None -> loopback
+    group member (use ParGroup.Mult); otherwise one process per GPU over RCCL."""
+
+    def __init__(self, part: Partition, rccl_id: Optional[bytes] = None, kernel: int = KERNEL_AUTO, q1d: int = 0):
+        lib = _par_lib()
+        self.part = part
+        self._keep = []
+        en = np.ascontiguousarray(part.fes.mesh.element_nodes()[part.elems]) if part.ne_local else np.zeros((1, 3, 8))
+        idbuf = None
+        if rccl_id is not None:
+            idbuf = (ctypes.c_ubyte * 128).from_buffer_copy(rccl_id)
+            self._keep.append(idbuf)
+        h = ctypes.c_void_p()
+        _check(lib.ecm2_par_form_create(part._h, _np_ptr(en), q1d,
+                                        ctypes.cast(idbuf, ctypes.c_void_p) if idbuf is not None else None,
+                                        ctypes.byref(h)))
+        self._h = h
+        _check(lib.ecm2_par_form_set_kernel(h, kernel))
+        self.true_size = part.n_owned
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.ecm2_par_form_destroy(self._h)
+            self._h = None
+
+    def AddDomainIntegrator(self, integ):
+        c = integ.coeff
+        lib = _par_lib()
+        if isinstance(c, ConstantCoefficient):
+            arr = (ctypes.c_double * 1)(c.value)
+            self._keep.append(arr)
+            _check(lib.ecm2_par_form_add_integrator(self._h, integ.kind, COEFF_CONSTANT, ctypes.cast(arr, ctypes.c_void_p), None))
+        elif isinstance(c, QuadratureCoefficient):
+            self._keep.append(c.values)
+            _check(lib.ecm2_par_form_add_integrator(self._h, integ.kind, COEFF_QUAD, _dev_ptr(c.values), None))
+        elif isinstance(c, AffineGridFunctionCoefficient):
+            self._keep.append(c.T)
+            params = (ctypes.c_double * 3)(c.scale, c.slope, c.t_ref)
+            self._keep.append(params)
+            _check(lib.ecm2_par_form_add_integrator(self._h, integ.kind, COEFF_GRIDFUNC_AFFINE, _dev_ptr(c.T),
+                                                    ctypes.cast(params, ctypes.c_void_p)))
+        else:
+            raise ECM2Error(f"unsupported coefficient {type(c).__name__}")
+
+    def Assemble(self, stream=None):
+        _check(_par_lib().ecm2_par_form_assemble(self._h, _stream(stream)))
+
+    def Mult(self, x, y, stream=None):
+        _check(_par_lib().ecm2_par_form_mult(self._h, _dev_ptr(x), _dev_ptr(y), _stream(stream)))
+
+    def timing(self, enable: bool):
+        _check(_par_lib().ecm2_par_form_timing(self._h, 1 if enable else 0))
+
+    def timing_get(self):
+        ms, n = ctypes.c_double(), ctypes.c_long()
+        _check(_par_lib().ecm2_par_form_timing_get(self._h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def algorithmic_bytes(self) -> float:
+        b = ctypes.c_double()
+        _check(_par_lib().ecm2_par_form_algorithmic_bytes(self._h, ctypes.byref(b)))
+        return b.value
+
+    def info(self) -> dict:
+        n, k = ctypes.c_int(), ctypes.c_int()
+        _check(_par_lib().ecm2_par_form_info(self._h, ctypes.byref(n), ctypes.byref(k)))
+        return {"n_true": n.value, "kernel": k.value}
+
+
+class ParGroup:
+    """All subdomains of one partition in this process on one GPU (loopback transport)."""
+
+    def __init__(self, forms):
+        self.forms = list(forms)
+
+    def Mult(self, xs, ys, stream=None):
+        n = len(self.forms)
+        fa = (ctypes.c_void_p * n)(*[f._h.value for f in self.forms])
+        xa = (ctypes.c_void_p * n)(*[_dev_ptr(x).value for x in xs])
+        ya = (ctypes.c_void_p * n)(*[_dev_ptr(y).value for y in ys])
+        _check(_par_lib().ecm2_par_group_mult(ctypes.cast(fa, ctypes.c_void_p), n, ctypes.cast(xa, ctypes.c_void_p),
+                                              ctypes.cast(ya, ctypes.c_void_p), _stream(stream)))

@@ -5,6 +5,8 @@
 #include "fe.hpp"
 #include "mesh.hpp"
 #include "pa_form.hpp"
+#include "par_form.hpp"
+#include "partition.hpp"
 
 #include <cstring>
 #include <string>
@@ -20,6 +22,14 @@ struct ecm2_h1space
 struct ecm2_pa_form
 {
    ecm2::PAForm *f;
+};
+struct ecm2_partition
+{
+   ecm2::LocalPart p;
+};
+struct ecm2_par_form
+{
+   ecm2::ParPAForm *f;
 };
 
 namespace
@@ -134,32 +144,44 @@ int ecm2_mesh_get_element_nodes(const ecm2_mesh *m, double *out)
    });
 }
 
+static void quad_points(const ecm2::HexMesh &m, int q1d, const int *elems, int n, double *out)
+{
+   ECM2_VERIFY(q1d >= 1 && q1d <= ecm2::MAX_Q1D, ecm2::ERR_ARG, "bad q1d " << q1d);
+   std::vector<double> x(q1d), w(q1d);
+   ecm2::gauss_legendre(q1d, x.data(), w.data());
+   const int nq = q1d * q1d * q1d;
+   for (int i = 0; i < n; i++)
+   {
+      const int e = elems ? elems[i] : i;
+      ECM2_VERIFY(e >= 0 && e < m.ne, ecm2::ERR_ARG, "element index " << e << " out of range");
+      double X[24];
+      for (int c = 0; c < 3; c++)
+         for (int a = 0; a < 8; a++) { X[c * 8 + a] = m.vert[3 * (size_t)m.elem[8 * (size_t)e + ecm2::kLexToNative[a]] + c]; }
+      for (int q = 0; q < nq; q++)
+      {
+         const double xi[3] = {x[q % q1d], x[(q / q1d) % q1d], x[q / (q1d * q1d)]};
+         for (int c = 0; c < 3; c++)
+         {
+            double v = 0.0;
+            for (int a = 0; a < 8; a++)
+            {
+               const int ax = a & 1, ay = (a >> 1) & 1, az = a >> 2;
+               v += (ax ? xi[0] : 1 - xi[0]) * (ay ? xi[1] : 1 - xi[1]) * (az ? xi[2] : 1 - xi[2]) * X[c * 8 + a];
+            }
+            out[((size_t)i * nq + q) * 3 + c] = v;
+         }
+      }
+   }
+}
+
 int ecm2_mesh_quadrature_points(const ecm2_mesh *m, int q1d, double *out)
 {
-   return guard([&] {
-      NEED(m); NEED(out);
-      ECM2_VERIFY(q1d >= 1 && q1d <= ecm2::MAX_Q1D, ecm2::ERR_ARG, "bad q1d " << q1d);
-      std::vector<double> x(q1d), w(q1d), en;
-      ecm2::gauss_legendre(q1d, x.data(), w.data());
-      m->m.element_nodes(en);
-      const int nq = q1d * q1d * q1d;
-      for (int e = 0; e < m->m.ne; e++)
-         for (int q = 0; q < nq; q++)
-         {
-            const double xi[3] = {x[q % q1d], x[(q / q1d) % q1d], x[q / (q1d * q1d)]};
-            for (int c = 0; c < 3; c++)
-            {
-               double v = 0.0;
-               for (int a = 0; a < 8; a++)
-               {
-                  const int ax = a & 1, ay = (a >> 1) & 1, az = a >> 2;
-                  v += (ax ? xi[0] : 1 - xi[0]) * (ay ? xi[1] : 1 - xi[1]) *
-                       (az ? xi[2] : 1 - xi[2]) * en[(size_t)e * 24 + c * 8 + a];
-               }
-               out[((size_t)e * nq + q) * 3 + c] = v;
-            }
-         }
-   });
+   return guard([&] { NEED(m); NEED(out); quad_points(m->m, q1d, nullptr, m->m.ne, out); });
+}
+
+int ecm2_mesh_quadrature_points_subset(const ecm2_mesh *m, int q1d, const int *elems, int n, double *out)
+{
+   return guard([&] { NEED(m); NEED(out); ECM2_VERIFY(n == 0 || elems, ecm2::ERR_ARG, "null elems"); quad_points(m->m, q1d, elems, n, out); });
 }
 
 void ecm2_mesh_destroy(ecm2_mesh *m) { delete m; }
@@ -356,6 +378,170 @@ int ecm2_pcg_solve(ecm2_pa_form *f, const int *ess, int n_ess, const double *b, 
       if (iterations) { *iterations = r.iterations; }
       if (final_norm) { *final_norm = r.final_norm; }
    });
+}
+
+// ---- partition / distributed form ----
+int ecm2_partition_slabs_z(const ecm2_mesh *m, int nranks, int *elem_rank)
+{
+   return guard([&] {
+      NEED(m); NEED(elem_rank);
+      const std::vector<int> er = ecm2::partition_slabs_z(m->m, nranks);
+      std::memcpy(elem_rank, er.data(), er.size() * sizeof(int));
+   });
+}
+
+int ecm2_partition_create(const ecm2_h1space *s, const int *elem_rank, int rank, int nranks,
+                          ecm2_partition **out)
+{
+   return guard([&] {
+      NEED(s); NEED(elem_rank); NEED(out);
+      std::vector<int> er(elem_rank, elem_rank + s->s.ne);
+      *out = new ecm2_partition{ecm2::build_local_part(s->s, er, rank, nranks)};
+   });
+}
+
+int ecm2_partition_info(const ecm2_partition *p, int *ne_local, int *ne_interior, int *n_owned,
+                        int *n_ghost, int *n_nbrs, int *n_send)
+{
+   return guard([&] {
+      NEED(p);
+      if (ne_local) { *ne_local = p->p.ne_local; }
+      if (ne_interior) { *ne_interior = p->p.ne_interior; }
+      if (n_owned) { *n_owned = p->p.n_owned; }
+      if (n_ghost) { *n_ghost = p->p.n_ghost; }
+      if (n_nbrs) { *n_nbrs = (int)p->p.nbrs.size(); }
+      if (n_send) { *n_send = (int)p->p.send_idx.size(); }
+   });
+}
+
+int ecm2_partition_get(const ecm2_partition *p, int *elems, int *local_to_global, int *gather_map,
+                       int *nbrs, int *send_off, int *send_idx, int *recv_off)
+{
+   return guard([&] {
+      NEED(p);
+      auto cp = [](int *dst, const std::vector<int> &v) {
+         if (dst && !v.empty()) { std::memcpy(dst, v.data(), v.size() * sizeof(int)); }
+      };
+      cp(elems, p->p.elems);
+      cp(local_to_global, p->p.local_to_global);
+      cp(gather_map, p->p.gather_map);
+      cp(nbrs, p->p.nbrs);
+      cp(send_off, p->p.send_off);
+      cp(send_idx, p->p.send_idx);
+      cp(recv_off, p->p.recv_off);
+   });
+}
+
+void ecm2_partition_destroy(ecm2_partition *p) { delete p; }
+
+int ecm2_rccl_unique_id(unsigned char *id128)
+{
+   return guard([&] { NEED(id128); ecm2::rccl_unique_id(id128); });
+}
+
+int ecm2_par_form_create(const ecm2_partition *p, const double *enodes_local, int q1d,
+                         const unsigned char *rccl_id, ecm2_par_form **out)
+{
+   return guard([&] {
+      NEED(p); NEED(out);
+      ECM2_VERIFY(p->p.ne_local == 0 || enodes_local, ecm2::ERR_ARG, "null element nodes");
+      *out = nullptr;
+      auto *f = new ecm2::ParPAForm(p->p, enodes_local, q1d, rccl_id);
+      *out = new ecm2_par_form{f};
+   });
+}
+
+int ecm2_par_form_add_integrator(ecm2_par_form *f, int integrator, int coeff_kind,
+                                 const double *data, const double *params)
+{
+   return guard([&] {
+      NEED(f);
+      ecm2::CoeffDesc c;
+      c.kind = coeff_kind;
+      if (coeff_kind == ECM2_COEFF_CONSTANT) { c.value = data ? data[0] : 1.0; }
+      else if (coeff_kind == ECM2_COEFF_QUAD) { c.quad = data; }
+      else if (coeff_kind == ECM2_COEFF_GRIDFUNC_AFFINE)
+      {
+         NEED(params);
+         c.lvec = data; c.scale = params[0]; c.slope = params[1]; c.t_ref = params[2];
+      }
+      f->f->local().add_integrator(integrator, c);
+   });
+}
+
+int ecm2_par_form_set_kernel(ecm2_par_form *f, int kernel)
+{
+   return guard([&] {
+      NEED(f);
+      ECM2_VERIFY(kernel != ECM2_KERNEL_UNFUSED, ecm2::ERR_UNSUPPORTED, "distributed form needs a fused kernel");
+      f->f->local().set_kernel(kernel);
+   });
+}
+
+int ecm2_par_form_assemble(ecm2_par_form *f, void *stream)
+{
+   return guard([&] { NEED(f); f->f->assemble(S(stream)); });
+}
+
+int ecm2_par_form_mult(ecm2_par_form *f, const double *x_true, double *y_true, void *stream)
+{
+   return guard([&] {
+      NEED(f);
+      ECM2_VERIFY(f->f->true_size() == 0 || (x_true && y_true), ecm2::ERR_ARG, "null vector");
+      f->f->mult(x_true, y_true, S(stream));
+   });
+}
+
+int ecm2_par_group_mult(ecm2_par_form *const *forms, int n, const double *const *x_true,
+                        double *const *y_true, void *stream)
+{
+   return guard([&] {
+      NEED(forms); NEED(x_true); NEED(y_true);
+      std::vector<ecm2::ParPAForm *> fs;
+      std::vector<const double *> xs;
+      std::vector<double *> ys;
+      for (int i = 0; i < n; i++)
+      {
+         NEED(forms[i]);
+         fs.push_back(forms[i]->f);
+         xs.push_back(x_true[i]);
+         ys.push_back(y_true[i]);
+      }
+      ecm2::par_group_mult(fs, xs, ys, S(stream));
+   });
+}
+
+int ecm2_par_form_timing(ecm2_par_form *f, int enable)
+{
+   return guard([&] { NEED(f); f->f->local().timing_enable(enable != 0); });
+}
+
+int ecm2_par_form_timing_get(ecm2_par_form *f, double *total_ms, long *launches)
+{
+   return guard([&] { NEED(f); f->f->local().timing_get(total_ms, launches); });
+}
+
+int ecm2_par_form_algorithmic_bytes(const ecm2_par_form *f, double *bytes)
+{
+   return guard([&] {
+      NEED(f); NEED(bytes);
+      // local subdomain: interface dofs counted once per owner copy
+      *bytes = (double)f->f->local().algorithmic_bytes();
+   });
+}
+
+int ecm2_par_form_info(const ecm2_par_form *f, int *n_true, int *kernel)
+{
+   return guard([&] {
+      NEED(f);
+      if (n_true) { *n_true = f->f->true_size(); }
+      if (kernel) { *kernel = f->f->local().kernel_mode(); }
+   });
+}
+
+void ecm2_par_form_destroy(ecm2_par_form *f)
+{
+   if (f) { delete f->f; delete f; }
 }
 
 } // extern "C"

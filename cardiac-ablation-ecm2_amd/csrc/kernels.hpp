@@ -53,6 +53,18 @@ struct CoeffDesc
    double scale = 1.0, slope = 0.0, t_ref = 0.0;
 };
 
+// Arguments of one fused apply over element blocks [blk_begin, blk_end) (64 elements per
+// block).  With a split L-vector (distributed form) dofs >= n_owned live in xg / yg.
+struct ApplyArgs
+{
+   int kind = QLAYOUT_NATIVE;
+   int ne = 0, blk_begin = 0, blk_end = 0, n_owned = 0;
+   const int *gmap = nullptr;
+   const double *qdd = nullptr, *qdm = nullptr;
+   const double *x = nullptr, *xg = nullptr;
+   double *y = nullptr, *yg = nullptr;
+};
+
 namespace kern
 {
 // ---- setup (S1/S2/S3 equivalents) ----
@@ -72,16 +84,14 @@ void setup_from_jacobians(const QLayout &L, const double *J, const double *W,
 
 // ---- apply ----
 // Fused y = R^T (M + K) R x, thread-per-element (blocked layout); y must be zeroed.
-void apply_tpe(int D, int Q, bool mass, bool diff, int ne, const int *gmap_blocked,
-               const double *qd_diff, const double *qd_mass, const double *x, double *y,
-               const Basis1D &b, const double *rowtab, hipStream_t s);
+void apply_tpe(int D, int Q, bool mass, bool diff, const ApplyArgs &a, const Basis1D &b,
+               const double *rowtab, hipStream_t s);
 // Row table for apply_tpe: [qz][qy][3][dz][dy] products (see pa_kernels.hip).
 std::vector<double> make_row_table(const DofToQuad &m);
 // Workgroup-per-element kernel, any layout; in/out either L-vectors (through the
 // gather map; output by atomics into a zeroed y) or E-vectors (accumulated).
-void apply_wpe(int D, int Q, bool mass, bool diff, int layout, int ne, const int *gmap_native,
-               const double *qd_diff, const double *qd_mass, const double *x, double *y,
-               bool in_evec, bool out_evec, const Basis1D &b, hipStream_t s);
+void apply_wpe(int D, int Q, bool mass, bool diff, const ApplyArgs &a, bool in_evec,
+               bool out_evec, const Basis1D &b, hipStream_t s);
 
 // ---- ElementRestriction ----
 void restriction_mult(long n, int nd, const int *gmap_native, const double *x, double *xe,

@@ -16,9 +16,10 @@ void require_device()
                "no HIP device available (the PA path has no CPU fallback)");
 }
 
-PAForm::PAForm(int ne, int order, int ndofs, const int *gather_map_host, int q1d)
-   : ne_(ne), order_(order), ndofs_(ndofs)
+PAForm::PAForm(int ne, int order, int ndofs, const int *gather_map_host, int q1d, int n_owned)
+   : ne_(ne), order_(order), ndofs_(ndofs), n_owned_(n_owned < 0 ? ndofs : n_owned)
 {
+   ECM2_VERIFY(n_owned_ <= ndofs, ERR_ARG, "n_owned > ndofs");
    ECM2_VERIFY(ne >= 0 && ndofs >= 0, ERR_ARG, "negative sizes");
    ECM2_VERIFY(order >= 1 && order + 1 <= MAX_D1D, ERR_ARG, "unsupported order " << order);
    ECM2_VERIFY(ne == 0 || gather_map_host != nullptr, ERR_ARG, "null gather map");
@@ -199,7 +200,7 @@ size_t PAForm::algorithmic_bytes() const
 {
    // 8*NE*NQ*(6+1) qdata + 8*ndofs (x) + 8*ndofs (y) + 4*NE*ND (map).
    const size_t nc = (have_diff_ ? 6 : 0) + (have_mass_ ? 1 : 0);
-   return 8ull * ne_ * NQ_ * nc + 16ull * ndofs_ + 4ull * ne_ * ND_;
+   return 8ull * ne_ * NQ_ * nc + 16ull * n_owned_ + 4ull * ne_ * ND_;
 }
 
 void PAForm::ensure_csr()
@@ -242,16 +243,9 @@ void PAForm::mult(const double *x, double *y, hipStream_t s)
       record_start(s);
       kern::restriction_mult((long)ne_ * ND_, ND_, gmap_.data(), x, xe_.data(), s);
       if (ne_) { ECM2_HIP(hipMemsetAsync(ye_.data(), 0, ye_.bytes(), s)); }
-      if (m)
-      {
-         kern::apply_wpe(D_, Q_, true, false, layout_.kind, ne_, gmap_.data(), qd_diff_.data(),
-                         qd_mass_.data(), xe_.data(), ye_.data(), true, true, basis_, s);
-      }
-      if (d)
-      {
-         kern::apply_wpe(D_, Q_, false, true, layout_.kind, ne_, gmap_.data(), qd_diff_.data(),
-                         qd_mass_.data(), xe_.data(), ye_.data(), true, true, basis_, s);
-      }
+      ApplyArgs a = apply_args(xe_.data(), nullptr, ye_.data(), nullptr, 0, layout_.nblk());
+      if (m) { kern::apply_wpe(D_, Q_, true, false, a, true, true, basis_, s); }
+      if (d) { kern::apply_wpe(D_, Q_, false, true, a, true, true, basis_, s); }
       kern::restriction_mult_transpose(ndofs_, ND_, csr_off_.data(), csr_idx_.data(), ye_.data(), y, s);
       record_stop(s);
       return;
@@ -259,17 +253,40 @@ void PAForm::mult(const double *x, double *y, hipStream_t s)
    ECM2_HIP(hipMemsetAsync(y, 0, sizeof(double) * (size_t)ndofs_, s));
    if (!m && !d) { return; }
    record_start(s);
+   apply_blocks(x, nullptr, y, nullptr, 0, layout_.nblk(), s);
+   record_stop(s);
+}
+
+ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, double *yg, int b0,
+                             int b1) const
+{
+   ApplyArgs a;
+   a.kind = layout_.kind;
+   a.ne = ne_;
+   a.blk_begin = b0;
+   a.blk_end = b1;
+   a.n_owned = n_owned_;
+   a.gmap = (resolved_mode_ == KERNEL_TPE) ? gmap_blk_.data() : gmap_.data();
+   a.qdd = qd_diff_.data();
+   a.qdm = qd_mass_.data();
+   a.x = x; a.xg = xg; a.y = y; a.yg = yg;
+   return a;
+}
+
+void PAForm::apply_blocks(const double *x, const double *xg, double *y, double *yg, int b0, int b1,
+                          hipStream_t s)
+{
+   ECM2_VERIFY(assembled_, ERR_STATE, "apply before Assemble");
+   ECM2_VERIFY(resolved_mode_ != KERNEL_UNFUSED, ERR_UNSUPPORTED, "block apply needs a fused kernel");
+   const ApplyArgs a = apply_args(x, xg, y, yg, b0, b1);
    if (resolved_mode_ == KERNEL_TPE)
    {
-      kern::apply_tpe(D_, Q_, m, d, ne_, gmap_blk_.data(), qd_diff_.data(), qd_mass_.data(), x, y,
-                      basis_, rowtab_.data(), s);
+      kern::apply_tpe(D_, Q_, have_mass_, have_diff_, a, basis_, rowtab_.data(), s);
    }
    else
    {
-      kern::apply_wpe(D_, Q_, m, d, layout_.kind, ne_, gmap_.data(), qd_diff_.data(),
-                      qd_mass_.data(), x, y, false, false, basis_, s);
+      kern::apply_wpe(D_, Q_, have_mass_, have_diff_, a, false, false, basis_, s);
    }
-   record_stop(s);
 }
 
 void PAForm::assemble_diagonal(double *diag, hipStream_t s)
@@ -297,8 +314,9 @@ void PAForm::integrator_add_mult(int kind, const double *xe, double *ye, hipStre
    ECM2_VERIFY(assembled_, ERR_STATE, "AddMultPA before Assemble");
    ECM2_VERIFY((kind == INTEG_MASS && have_mass_) || (kind == INTEG_DIFFUSION && have_diff_),
                ERR_ARG, "integrator " << kind << " not present");
-   kern::apply_wpe(D_, Q_, kind == INTEG_MASS, kind == INTEG_DIFFUSION, layout_.kind, ne_,
-                   gmap_.data(), qd_diff_.data(), qd_mass_.data(), xe, ye, true, true, basis_, s);
+   ApplyArgs a = apply_args(xe, nullptr, ye, nullptr, 0, layout_.nblk());
+   a.gmap = gmap_.data();
+   kern::apply_wpe(D_, Q_, kind == INTEG_MASS, kind == INTEG_DIFFUSION, a, true, true, basis_, s);
 }
 
 void PAForm::get_qdata(int kind, double *out, hipStream_t s)

@@ -36,7 +36,9 @@ enum IntegratorKind : int { INTEG_MASS = 0, INTEG_DIFFUSION = 1 };
 class PAForm
 {
 public:
-   PAForm(int ne, int order, int ndofs, const int *gather_map_host, int q1d = 0);
+   // n_owned < ndofs: the local L-vector is split [owned | ghost] (distributed form);
+   // x/y hold dofs < n_owned, xg/yg the ghosts (apply_blocks).
+   PAForm(int ne, int order, int ndofs, const int *gather_map_host, int q1d = 0, int n_owned = -1);
    ~PAForm();
 
    int ne() const { return ne_; }
@@ -59,6 +61,13 @@ public:
 
    // y = A x (BilinearForm::Mult semantics: y overwritten).
    void mult(const double *x, double *y, hipStream_t s);
+   // Accumulate the fused apply of element blocks [b0, b1) (64 elements per block) into
+   // zero-initialised y / yg (atomics); x / xg as in the constructor's split.
+   void apply_blocks(const double *x, const double *xg, double *y, double *yg, int b0, int b1,
+                     hipStream_t s);
+   int nblocks() const { return layout_.nblk(); }
+   bool has_mass() const { return have_mass_; }
+   bool has_diffusion() const { return have_diff_; }
    void assemble_diagonal(double *diag, hipStream_t s);
 
    // Reference-shaped pieces (E-vector layout [e][nd], lexicographic).
@@ -78,8 +87,15 @@ private:
    void ensure_work(hipStream_t s);
    void record_start(hipStream_t s);
    void record_stop(hipStream_t s);
+   ApplyArgs apply_args(const double *x, const double *xg, double *y, double *yg, int b0,
+                        int b1) const;
 
-   int ne_, order_, ndofs_, D_, Q_, ND_, NQ_;
+ public:
+   void record_start_public(hipStream_t s) { record_start(s); }
+   void record_stop_public(hipStream_t s) { record_stop(s); }
+
+ private:
+   int ne_, order_, ndofs_, n_owned_, D_, Q_, ND_, NQ_;
    DofToQuad maps_;
    Basis1D basis_, basis1_;
    QLayout layout_;

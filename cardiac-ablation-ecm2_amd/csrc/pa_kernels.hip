@@ -22,6 +22,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 namespace ecm2
 {
 namespace
@@ -178,27 +180,30 @@ struct RowTable
    const double *p;
 };
 
-template <int D, int Q, bool MASS, bool DIFF>
+template <int D, int Q, bool MASS, bool DIFF, bool SPLIT>
 __global__ void __launch_bounds__(256)
-k_apply_tpe(int ne, int nblk, const int *__restrict__ gmap, const double *__restrict__ qdd,
-            const double *__restrict__ qdm, const double *__restrict__ x,
-            double *__restrict__ y, const Basis1D b, const double *__restrict__ rowtab)
+k_apply_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
+            const double *__restrict__ qdd, const double *__restrict__ qdm,
+            const double *__restrict__ x, const double *__restrict__ xg,
+            double *__restrict__ y, double *__restrict__ yg, const Basis1D b,
+            const double *__restrict__ rowtab)
 {
    constexpr int ND = D * D * D, NQ = Q * Q * Q, NQH = (NQ + 1) / 2, DD = D * D;
    const int lane = threadIdx.x & 63;
-   const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
-   if (blk >= nblk) { return; }  // wave-uniform
+   const int blk = blk_begin + blockIdx.x * 4 + (threadIdx.x >> 6);
+   if (blk >= blk_end) { return; }  // wave-uniform
    const int e = blk * 64 + lane;
    const bool active = e < ne;
    const int *mp = gmap + (size_t)blk * ND * 64 + lane;
 
-   // ---- gather (ElementRestriction::Mult) ----
+   // ---- gather (ElementRestriction::Mult); SPLIT: [owned | ghost] local L-vector ----
    double X[ND];
 #pragma unroll
    for (int a = 0; a < ND; a++)
    {
       const int g = mp[a * 64];
-      const double v = x[dof_of(g)];
+      const int d = dof_of(g);
+      const double v = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
       X[a] = g >= 0 ? v : -v;
    }
    double Yo[ND];
@@ -324,7 +329,9 @@ k_apply_tpe(int ne, int nblk, const int *__restrict__ gmap, const double *__rest
       for (int a = 0; a < ND; a++)
       {
          const int g = mp[a * 64];
-         unsafeAtomicAdd(y + dof_of(g), g >= 0 ? Yo[a] : -Yo[a]);
+         const int d = dof_of(g);
+         double *dst = (!SPLIT || d < n_owned) ? y + d : yg + (d - n_owned);
+         unsafeAtomicAdd(dst, g >= 0 ? Yo[a] : -Yo[a]);
       }
    }
 }
@@ -334,10 +341,11 @@ k_apply_tpe(int ne, int nblk, const int *__restrict__ gmap, const double *__rest
 // --------------------------------------------------------------------------
 
 template <int D, int Q, bool MASS, bool DIFF, bool IN_E, bool OUT_E>
-__global__ void k_apply_wpe(int kind, int ne, const int *__restrict__ gmap,
+__global__ void k_apply_wpe(int kind, int ne, int e_begin, int n_owned,
+                            const int *__restrict__ gmap,
                             const double *__restrict__ qdd, const double *__restrict__ qdm,
-                            const double *__restrict__ x, double *__restrict__ y,
-                            const Basis1D b)
+                            const double *__restrict__ x, const double *__restrict__ xg,
+                            double *__restrict__ y, double *__restrict__ yg, const Basis1D b)
 {
    constexpr int ND = D * D * D, NQ = Q * Q * Q;
    __shared__ double sB[Q * D], sG[Q * D];
@@ -347,7 +355,7 @@ __global__ void k_apply_wpe(int kind, int ne, const int *__restrict__ gmap,
    __shared__ double s3m[NQ], s3x[NQ], s3y[NQ], s3z[NQ];
    __shared__ double s4a[Q * Q * D], s4b[Q * Q * D], s4c[Q * Q * D];
    __shared__ double s5a[Q * D * D], s5b[Q * D * D];
-   const int e = blockIdx.x;
+   const int e = e_begin + blockIdx.x;
    const int t = threadIdx.x;
    if (t < Q * D)
    {
@@ -361,7 +369,8 @@ __global__ void k_apply_wpe(int kind, int ne, const int *__restrict__ gmap,
       else
       {
          const int g = gmap[(size_t)e * ND + t];
-         const double v = x[dof_of(g)];
+         const int d = dof_of(g);
+         const double v = d < n_owned ? x[d] : xg[d - n_owned];
          sX[t] = g >= 0 ? v : -v;
       }
    }
@@ -469,7 +478,9 @@ __global__ void k_apply_wpe(int kind, int ne, const int *__restrict__ gmap,
       else
       {
          const int g = gmap[(size_t)e * ND + t];
-         unsafeAtomicAdd(y + dof_of(g), g >= 0 ? u : -u);
+         const int d = dof_of(g);
+         double *dst = d < n_owned ? y + d : yg + (d - n_owned);
+         unsafeAtomicAdd(dst, g >= 0 ? u : -u);
       }
    }
 }
@@ -649,61 +660,58 @@ SetupCoef make_setup_coef(const CoeffDesc *c, const double *q)
    return s;
 }
 
-template <int D, int Q>
-void launch_tpe_dq(bool mass, bool diff, int ne, const int *gm, const double *qdd,
-                   const double *qdm, const double *x, double *y, const Basis1D &b,
-                   const double *rowtab, hipStream_t s)
-{
-   const int nblk = (ne + 63) / 64;
-   const dim3 grid((nblk + 3) / 4), block(256);
-   if (mass && diff)
-   {
-      hipLaunchKernelGGL((k_apply_tpe<D, Q, true, true>), grid, block, 0, s, ne, nblk, gm, qdd, qdm, x, y, b, rowtab);
-   }
-   else if (mass)
-   {
-      hipLaunchKernelGGL((k_apply_tpe<D, Q, true, false>), grid, block, 0, s, ne, nblk, gm, qdd, qdm, x, y, b, rowtab);
-   }
-   else if (diff)
-   {
-      hipLaunchKernelGGL((k_apply_tpe<D, Q, false, true>), grid, block, 0, s, ne, nblk, gm, qdd, qdm, x, y, b, rowtab);
-   }
-}
-
 template <int D, int Q, bool MASS, bool DIFF>
-void launch_wpe_mdq(int kind, int ne, const int *gm, const double *qdd, const double *qdm,
-                    const double *x, double *y, bool in_e, bool out_e, const Basis1D &b,
-                    hipStream_t s)
+void launch_tpe_mdq(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipStream_t s)
 {
-   constexpr int NQ = Q * Q * Q;
-   const int nt = ((NQ + 63) / 64) * 64;
-   const dim3 grid(ne), block(nt);
-   if (in_e && out_e)
+   const int nb = a.blk_end - a.blk_begin;
+   if (nb <= 0) { return; }
+   const dim3 grid((nb + 3) / 4), block(256);
+   if (a.xg || a.yg)
    {
-      hipLaunchKernelGGL((k_apply_wpe<D, Q, MASS, DIFF, true, true>), grid, block, 0, s, kind, ne, gm, qdd, qdm, x, y, b);
-   }
-   else if (in_e)
-   {
-      hipLaunchKernelGGL((k_apply_wpe<D, Q, MASS, DIFF, true, false>), grid, block, 0, s, kind, ne, gm, qdd, qdm, x, y, b);
-   }
-   else if (out_e)
-   {
-      hipLaunchKernelGGL((k_apply_wpe<D, Q, MASS, DIFF, false, true>), grid, block, 0, s, kind, ne, gm, qdd, qdm, x, y, b);
+      hipLaunchKernelGGL((k_apply_tpe<D, Q, MASS, DIFF, true>), grid, block, 0, s, a.ne, a.blk_begin,
+                         a.blk_end, a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, rowtab);
    }
    else
    {
-      hipLaunchKernelGGL((k_apply_wpe<D, Q, MASS, DIFF, false, false>), grid, block, 0, s, kind, ne, gm, qdd, qdm, x, y, b);
+      hipLaunchKernelGGL((k_apply_tpe<D, Q, MASS, DIFF, false>), grid, block, 0, s, a.ne, a.blk_begin,
+                         a.blk_end, a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, rowtab);
    }
 }
 
 template <int D, int Q>
-void launch_wpe_dq(bool mass, bool diff, int kind, int ne, const int *gm, const double *qdd,
-                   const double *qdm, const double *x, double *y, bool in_e, bool out_e,
+void launch_tpe_dq(bool mass, bool diff, const ApplyArgs &a, const Basis1D &b,
+                   const double *rowtab, hipStream_t s)
+{
+   if (mass && diff) { launch_tpe_mdq<D, Q, true, true>(a, b, rowtab, s); }
+   else if (mass) { launch_tpe_mdq<D, Q, true, false>(a, b, rowtab, s); }
+   else if (diff) { launch_tpe_mdq<D, Q, false, true>(a, b, rowtab, s); }
+}
+
+template <int D, int Q, bool MASS, bool DIFF>
+void launch_wpe_mdq(const ApplyArgs &a, bool in_e, bool out_e, const Basis1D &b, hipStream_t s)
+{
+   constexpr int NQ = Q * Q * Q;
+   const int nt = ((NQ + 63) / 64) * 64;
+   const int e0 = a.blk_begin * 64, e1 = std::min(a.ne, a.blk_end * 64);
+   if (e1 <= e0) { return; }
+   const dim3 grid(e1 - e0), block(nt);
+#define ECM2_WPE_LAUNCH(IE, OE)                                                                      \
+   hipLaunchKernelGGL((k_apply_wpe<D, Q, MASS, DIFF, IE, OE>), grid, block, 0, s, a.kind, a.ne, e0, \
+                      a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b)
+   if (in_e && out_e) { ECM2_WPE_LAUNCH(true, true); }
+   else if (in_e) { ECM2_WPE_LAUNCH(true, false); }
+   else if (out_e) { ECM2_WPE_LAUNCH(false, true); }
+   else { ECM2_WPE_LAUNCH(false, false); }
+#undef ECM2_WPE_LAUNCH
+}
+
+template <int D, int Q>
+void launch_wpe_dq(bool mass, bool diff, const ApplyArgs &a, bool in_e, bool out_e,
                    const Basis1D &b, hipStream_t s)
 {
-   if (mass && diff) { launch_wpe_mdq<D, Q, true, true>(kind, ne, gm, qdd, qdm, x, y, in_e, out_e, b, s); }
-   else if (mass) { launch_wpe_mdq<D, Q, true, false>(kind, ne, gm, qdd, qdm, x, y, in_e, out_e, b, s); }
-   else if (diff) { launch_wpe_mdq<D, Q, false, true>(kind, ne, gm, qdd, qdm, x, y, in_e, out_e, b, s); }
+   if (mass && diff) { launch_wpe_mdq<D, Q, true, true>(a, in_e, out_e, b, s); }
+   else if (mass) { launch_wpe_mdq<D, Q, true, false>(a, in_e, out_e, b, s); }
+   else if (diff) { launch_wpe_mdq<D, Q, false, true>(a, in_e, out_e, b, s); }
 }
 
 } // namespace
@@ -746,28 +754,26 @@ void setup_from_jacobians(const QLayout &L, const double *J, const double *W,
    ECM2_HIP(hipGetLastError());
 }
 
-void apply_tpe(int D, int Q, bool mass, bool diff, int ne, const int *gm, const double *qdd,
-               const double *qdm, const double *x, double *y, const Basis1D &b,
+void apply_tpe(int D, int Q, bool mass, bool diff, const ApplyArgs &a, const Basis1D &b,
                const double *rowtab, hipStream_t s)
 {
-   if (ne == 0) { return; }
-   if (D == 2 && Q == 3) { launch_tpe_dq<2, 3>(mass, diff, ne, gm, qdd, qdm, x, y, b, rowtab, s); }
-   else if (D == 3 && Q == 4) { launch_tpe_dq<3, 4>(mass, diff, ne, gm, qdd, qdm, x, y, b, rowtab, s); }
+   if (a.ne == 0) { return; }
+   if (D == 2 && Q == 3) { launch_tpe_dq<2, 3>(mass, diff, a, b, rowtab, s); }
+   else if (D == 3 && Q == 4) { launch_tpe_dq<3, 4>(mass, diff, a, b, rowtab, s); }
    else { ECM2_VERIFY(false, ERR_UNSUPPORTED, "no thread-per-element kernel for D1D=" << D << " Q1D=" << Q); }
    ECM2_HIP(hipGetLastError());
 }
 
-void apply_wpe(int D, int Q, bool mass, bool diff, int kind, int ne, const int *gm,
-               const double *qdd, const double *qdm, const double *x, double *y, bool in_e,
-               bool out_e, const Basis1D &b, hipStream_t s)
+void apply_wpe(int D, int Q, bool mass, bool diff, const ApplyArgs &a, bool in_e, bool out_e,
+               const Basis1D &b, hipStream_t s)
 {
-   if (ne == 0) { return; }
-#define ECM2_WPE_CASE(DD, QQ)                                                          \
-   if (D == DD && Q == QQ)                                                             \
-   {                                                                                   \
-      launch_wpe_dq<DD, QQ>(mass, diff, kind, ne, gm, qdd, qdm, x, y, in_e, out_e, b, s); \
-      ECM2_HIP(hipGetLastError());                                                     \
-      return;                                                                          \
+   if (a.ne == 0) { return; }
+#define ECM2_WPE_CASE(DD, QQ)                                         \
+   if (D == DD && Q == QQ)                                            \
+   {                                                                  \
+      launch_wpe_dq<DD, QQ>(mass, diff, a, in_e, out_e, b, s);        \
+      ECM2_HIP(hipGetLastError());                                    \
+      return;                                                         \
    }
    ECM2_WPE_CASE(2, 3)
    ECM2_WPE_CASE(3, 4)

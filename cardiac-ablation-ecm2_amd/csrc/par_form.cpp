@@ -1,0 +1,203 @@
+// par_form.cpp -- see par_form.hpp.
+#include "par_form.hpp"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+
+namespace ecm2
+{
+
+#define ECM2_NCCL(call)                                                                 \
+   do {                                                                                 \
+      ncclResult_t r_ = (call);                                                         \
+      ECM2_VERIFY(r_ == ncclSuccess, ERR_COMM, "RCCL error '" << ncclGetErrorString(r_) \
+                                                      << "' in " << #call);             \
+   } while (0)
+
+void rccl_unique_id(unsigned char *out)
+{
+   ncclUniqueId id;
+   ECM2_NCCL(ncclGetUniqueId(&id));
+   static_assert(sizeof(id) == 128, "ncclUniqueId size");
+   std::memcpy(out, &id, sizeof(id));
+}
+
+ParPAForm::ParPAForm(const LocalPart &part, const double *enodes_local_host, int q1d,
+                     const unsigned char *rccl_id)
+   : part_(part)
+{
+   const int nl = part.n_owned + part.n_ghost;
+   local_.reset(new PAForm(part.ne_local, part.order, nl, part.gather_map.data(), q1d, part.n_owned));
+   local_->set_element_nodes(enodes_local_host);
+   send_idx_.upload(part.send_idx);
+   sendbuf_.resize(std::max<size_t>(1, part.send_idx.size()));
+   rbuf_.resize(std::max<size_t>(1, part.send_idx.size()));
+   xg_.resize(std::max(1, part.n_ghost));
+   yg_.resize(std::max(1, part.n_ghost));
+   ECM2_HIP(hipMemset(xg_.data(), 0, xg_.bytes()));
+   if (rccl_id)
+   {
+      ncclUniqueId id;
+      std::memcpy(&id, rccl_id, sizeof(id));
+      ncclComm_t comm;
+      ECM2_NCCL(ncclCommInitRank(&comm, part.nranks, id, part.rank));
+      comm_ = comm;
+      ECM2_HIP(hipStreamCreateWithFlags(&cs_, hipStreamNonBlocking));
+      ECM2_HIP(hipEventCreateWithFlags(&ev_pack_, hipEventDisableTiming));
+      ECM2_HIP(hipEventCreateWithFlags(&ev_xg_, hipEventDisableTiming));
+      ECM2_HIP(hipEventCreateWithFlags(&ev_yg_, hipEventDisableTiming));
+      ECM2_HIP(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
+   }
+   ECM2_HIP(hipDeviceSynchronize());
+}
+
+ParPAForm::~ParPAForm()
+{
+   if (comm_) { (void)ncclCommDestroy((ncclComm_t)comm_); }
+   if (cs_) { (void)hipStreamDestroy(cs_); }
+   for (hipEvent_t e : {ev_pack_, ev_xg_, ev_yg_, ev_done_})
+   {
+      if (e) { (void)hipEventDestroy(e); }
+   }
+}
+
+void ParPAForm::assemble(hipStream_t s) { local_->assemble(s); }
+
+void ParPAForm::phase_pack(const double *x_true, double *y_true, hipStream_t s)
+{
+   if (part_.n_owned) { ECM2_HIP(hipMemsetAsync(y_true, 0, sizeof(double) * part_.n_owned, s)); }
+   if (part_.n_ghost) { ECM2_HIP(hipMemsetAsync(yg_.data(), 0, sizeof(double) * part_.n_ghost, s)); }
+   kern::gather_idx((int)part_.send_idx.size(), send_idx_.data(), x_true, sendbuf_.data(), s);
+}
+
+void ParPAForm::phase_interior(const double *x_true, double *y_true, hipStream_t s)
+{
+   const int b_int = part_.ne_interior / kElemBlock;
+   local_->record_start_public(s);
+   local_->apply_blocks(x_true, xg_.data(), y_true, yg_.data(), 0, b_int, s);
+   local_->record_stop_public(s);
+}
+
+void ParPAForm::phase_boundary(const double *x_true, double *y_true, hipStream_t s)
+{
+   const int b_int = part_.ne_interior / kElemBlock;
+   local_->record_start_public(s);
+   local_->apply_blocks(x_true, xg_.data(), y_true, yg_.data(), b_int, local_->nblocks(), s);
+   local_->record_stop_public(s);
+}
+
+void ParPAForm::phase_finish(double *y_true, hipStream_t s)
+{
+   kern::scatter_add_idx((int)part_.send_idx.size(), send_idx_.data(), rbuf_.data(), y_true, s);
+}
+
+void ParPAForm::mult(const double *x_true, double *y_true, hipStream_t s)
+{
+   ECM2_VERIFY(comm_, ERR_STATE, "mult needs the RCCL transport (use the loopback group otherwise)");
+   ncclComm_t comm = (ncclComm_t)comm_;
+   const int nn = (int)part_.nbrs.size();
+   // P: owner values -> ghost copies (tag 41822 in the reference)
+   phase_pack(x_true, y_true, s);
+   ECM2_HIP(hipEventRecord(ev_pack_, s));
+   ECM2_HIP(hipStreamWaitEvent(cs_, ev_pack_, 0));
+   if (nn)
+   {
+      ECM2_NCCL(ncclGroupStart());
+      for (int k = 0; k < nn; k++)
+      {
+         const size_t ns = part_.send_off[k + 1] - part_.send_off[k];
+         const size_t nr = part_.recv_off[k + 1] - part_.recv_off[k];
+         if (ns) { ECM2_NCCL(ncclSend(sendbuf_.data() + part_.send_off[k], ns, ncclFloat64, part_.nbrs[k], comm, cs_)); }
+         if (nr) { ECM2_NCCL(ncclRecv(xg_.data() + part_.recv_off[k], nr, ncclFloat64, part_.nbrs[k], comm, cs_)); }
+      }
+      ECM2_NCCL(ncclGroupEnd());
+   }
+   ECM2_HIP(hipEventRecord(ev_xg_, cs_));
+   // interior elements overlap the exchange
+   phase_interior(x_true, y_true, s);
+   ECM2_HIP(hipStreamWaitEvent(s, ev_xg_, 0));
+   phase_boundary(x_true, y_true, s);
+   // P^T: ghost contributions -> owners (tag 41823), summed into the owned interface dofs
+   ECM2_HIP(hipEventRecord(ev_yg_, s));
+   ECM2_HIP(hipStreamWaitEvent(cs_, ev_yg_, 0));
+   if (nn)
+   {
+      ECM2_NCCL(ncclGroupStart());
+      for (int k = 0; k < nn; k++)
+      {
+         const size_t ns = part_.recv_off[k + 1] - part_.recv_off[k];
+         const size_t nr = part_.send_off[k + 1] - part_.send_off[k];
+         if (ns) { ECM2_NCCL(ncclSend(yg_.data() + part_.recv_off[k], ns, ncclFloat64, part_.nbrs[k], comm, cs_)); }
+         if (nr) { ECM2_NCCL(ncclRecv(rbuf_.data() + part_.send_off[k], nr, ncclFloat64, part_.nbrs[k], comm, cs_)); }
+      }
+      ECM2_NCCL(ncclGroupEnd());
+   }
+   phase_finish(y_true, cs_);
+   ECM2_HIP(hipEventRecord(ev_done_, cs_));
+   ECM2_HIP(hipStreamWaitEvent(s, ev_done_, 0));
+}
+
+void par_group_mult(std::vector<ParPAForm *> &forms, const std::vector<const double *> &x,
+                    const std::vector<double *> &y, hipStream_t s)
+{
+   const int n = (int)forms.size();
+   ECM2_VERIFY((int)x.size() == n && (int)y.size() == n, ERR_ARG, "group size mismatch");
+   for (int r = 0; r < n; r++)
+   {
+      ECM2_VERIFY(forms[r]->part().rank == r && forms[r]->part().nranks == n, ERR_ARG,
+                  "loopback group: form " << r << " has rank " << forms[r]->part().rank);
+   }
+   auto slot = [&](int s_rank, int r_rank) {  // index of r_rank in s_rank's neighbour list
+      const auto &nb = forms[s_rank]->part().nbrs;
+      const auto it = std::find(nb.begin(), nb.end(), r_rank);
+      ECM2_VERIFY(it != nb.end(), ERR_INTERNAL, "asymmetric neighbour lists");
+      return (int)(it - nb.begin());
+   };
+   for (int r = 0; r < n; r++) { forms[r]->phase_pack(x[r], y[r], s); }
+   // P: copy each owner's packed block into the receiver's ghost block
+   for (int r = 0; r < n; r++)
+   {
+      const LocalPart &pr = forms[r]->part();
+      for (size_t k = 0; k < pr.nbrs.size(); k++)
+      {
+         const int o = pr.nbrs[k], j = slot(o, r);
+         const LocalPart &po = forms[o]->part();
+         const size_t cnt = pr.recv_off[k + 1] - pr.recv_off[k];
+         ECM2_VERIFY(cnt == (size_t)(po.send_off[j + 1] - po.send_off[j]), ERR_INTERNAL,
+                     "exchange size mismatch " << r << "<-" << o);
+         if (cnt)
+         {
+            ECM2_HIP(hipMemcpyAsync(forms[r]->xghost() + pr.recv_off[k], forms[o]->sendbuf() + po.send_off[j],
+                                    cnt * sizeof(double), hipMemcpyDeviceToDevice, s));
+         }
+      }
+   }
+   for (int r = 0; r < n; r++)
+   {
+      forms[r]->phase_interior(x[r], y[r], s);
+      forms[r]->phase_boundary(x[r], y[r], s);
+   }
+   // P^T: copy each ghost block into the owner's receive buffer, then add
+   for (int r = 0; r < n; r++)
+   {
+      const LocalPart &pr = forms[r]->part();
+      for (size_t k = 0; k < pr.nbrs.size(); k++)
+      {
+         const int g = pr.nbrs[k], j = slot(g, r);
+         const LocalPart &pg = forms[g]->part();
+         const size_t cnt = pr.send_off[k + 1] - pr.send_off[k];
+         ECM2_VERIFY(cnt == (size_t)(pg.recv_off[j + 1] - pg.recv_off[j]), ERR_INTERNAL,
+                     "reduce size mismatch " << r << "<-" << g);
+         if (cnt)
+         {
+            ECM2_HIP(hipMemcpyAsync(forms[r]->recvbuf() + pr.send_off[k], forms[g]->yghost() + pg.recv_off[j],
+                                    cnt * sizeof(double), hipMemcpyDeviceToDevice, s));
+         }
+      }
+   }
+   for (int r = 0; r < n; r++) { forms[r]->phase_finish(y[r], s); }
+}
+
+} // namespace ecm2

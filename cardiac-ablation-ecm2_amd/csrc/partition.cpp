@@ -1,0 +1,116 @@
+// partition.cpp -- see partition.hpp.
+#include "partition.hpp"
+#include "common.hpp"
+
+#include <algorithm>
+#include <cstdint>
+
+namespace ecm2
+{
+
+std::vector<int> partition_slabs_z(const HexMesh &m, int nranks)
+{
+   ECM2_VERIFY(m.nx > 0, ERR_ARG, "slab partition needs a lexicographic Cartesian mesh");
+   ECM2_VERIFY(nranks >= 1 && nranks <= m.nz, ERR_ARG, "bad rank count " << nranks);
+   std::vector<int> er(m.ne);
+   for (int e = 0; e < m.ne; e++)
+   {
+      const int ez = e / (m.nx * m.ny);
+      // slab r = [floor(nz r / R), floor(nz (r+1) / R))
+      int r = 0;
+      while (r + 1 < nranks && (long)m.nz * (r + 1) / nranks <= ez) { r++; }
+      er[e] = r;
+   }
+   return er;
+}
+
+LocalPart build_local_part(const H1Space &s, const std::vector<int> &elem_rank, int rank, int nranks)
+{
+   ECM2_VERIFY((int)elem_rank.size() == s.ne, ERR_ARG, "elem_rank size " << elem_rank.size() << " != ne " << s.ne);
+   ECM2_VERIFY(nranks >= 1 && nranks <= 64, ERR_UNSUPPORTED, "1..64 ranks supported");
+   ECM2_VERIFY(rank >= 0 && rank < nranks, ERR_ARG, "bad rank " << rank);
+   LocalPart p;
+   p.rank = rank;
+   p.nranks = nranks;
+   p.order = s.order;
+   p.nd = s.nd;
+   const int nd = s.nd;
+   // which ranks touch each dof
+   std::vector<uint64_t> touch(s.ndofs, 0);
+   for (int e = 0; e < s.ne; e++)
+   {
+      const int r = elem_rank[e];
+      ECM2_VERIFY(r >= 0 && r < nranks, ERR_ARG, "element rank " << r << " out of range");
+      for (int a = 0; a < nd; a++)
+      {
+         const int g = s.gather_map[(size_t)e * nd + a];
+         touch[g >= 0 ? g : -1 - g] |= (1ull << r);
+      }
+   }
+   auto owner = [&](int g) { return __builtin_ctzll(touch[g]); };
+   const uint64_t me = 1ull << rank;
+   // local dofs
+   std::vector<int> owned, ghost;
+   for (int g = 0; g < s.ndofs; g++)
+   {
+      if (!(touch[g] & me)) { continue; }
+      if (owner(g) == rank) { owned.push_back(g); }
+      else { ghost.push_back(g); }
+   }
+   std::stable_sort(ghost.begin(), ghost.end(), [&](int a, int b) { return owner(a) < owner(b); });
+   p.n_owned = (int)owned.size();
+   p.n_ghost = (int)ghost.size();
+   p.local_to_global = owned;
+   p.local_to_global.insert(p.local_to_global.end(), ghost.begin(), ghost.end());
+   std::vector<int> g2l(s.ndofs, -1);
+   for (int i = 0; i < (int)p.local_to_global.size(); i++) { g2l[p.local_to_global[i]] = i; }
+   // neighbours: ranks that own my ghosts or ghost my owned dofs
+   uint64_t nb = 0;
+   for (int g : owned) { nb |= touch[g] & ~me; }
+   for (int g : ghost) { nb |= 1ull << owner(g); }
+   for (int r = 0; r < nranks; r++) { if (nb & (1ull << r)) { p.nbrs.push_back(r); } }
+   p.send_off.assign(1, 0);
+   p.recv_off.assign(1, 0);
+   for (int r : p.nbrs)
+   {
+      for (int i = 0; i < p.n_owned; i++)
+      {
+         if (touch[owned[i]] & (1ull << r)) { p.send_idx.push_back(i); }
+      }
+      p.send_off.push_back((int)p.send_idx.size());
+      int cnt = 0;
+      for (int g : ghost) { cnt += owner(g) == r; }
+      p.recv_off.push_back(p.recv_off.back() + cnt);
+   }
+   // local elements: interior (no ghost dof) first, then boundary
+   std::vector<int> interior, boundary;
+   for (int e = 0; e < s.ne; e++)
+   {
+      if (elem_rank[e] != rank) { continue; }
+      bool bnd = false;
+      for (int a = 0; a < nd && !bnd; a++)
+      {
+         const int g = s.gather_map[(size_t)e * nd + a];
+         bnd = g2l[g >= 0 ? g : -1 - g] >= p.n_owned;
+      }
+      (bnd ? boundary : interior).push_back(e);
+   }
+   p.ne_interior = (int)interior.size();
+   p.elems = interior;
+   p.elems.insert(p.elems.end(), boundary.begin(), boundary.end());
+   p.ne_local = (int)p.elems.size();
+   p.gather_map.resize((size_t)p.ne_local * nd);
+   for (int le = 0; le < p.ne_local; le++)
+   {
+      const int e = p.elems[le];
+      for (int a = 0; a < nd; a++)
+      {
+         const int g = s.gather_map[(size_t)e * nd + a];
+         const int l = g2l[g >= 0 ? g : -1 - g];
+         p.gather_map[(size_t)le * nd + a] = g >= 0 ? l : -1 - l;
+      }
+   }
+   return p;
+}
+
+} // namespace ecm2

@@ -1,0 +1,40 @@
+// partition.hpp -- element partition -> per-rank local space and shared-DoF exchange plan.
+//
+// Reference: ParMesh / ParFiniteElementSpace (mesh/pmesh.hpp:33, fem/pfespace.cpp) with
+// the true-dof prolongation P of DeviceConformingProlongationOperator
+// (pfespace.cpp:5259-5532): every shared DoF has one owner rank (here: the lowest rank
+// touching it); the true vector of a rank is its owned DoFs; P copies owner values to
+// the ghost copies, P^T sums ghost contributions into the owner.
+//
+// Local L-vector layout: [owned (by global id) | ghost (grouped by owner rank, then by
+// global id)], so the true vector is the prefix and each neighbour's ghost block is a
+// contiguous range (received in place, sent in place).
+#pragma once
+
+#include "mesh.hpp"
+
+#include <vector>
+
+namespace ecm2
+{
+
+struct LocalPart
+{
+   int rank = 0, nranks = 1, order = 1, nd = 0;
+   int ne_local = 0, ne_interior = 0;   // local elements ordered [interior | boundary]
+   int n_owned = 0, n_ghost = 0;
+   std::vector<int> elems;              // global element ids in local order
+   std::vector<int> local_to_global;    // [n_owned + n_ghost]
+   std::vector<int> gather_map;         // [ne_local][nd] into the local L-vector
+   std::vector<int> nbrs;               // neighbour ranks (ascending)
+   std::vector<int> send_off, send_idx; // P: owned local indices sent to nbrs[k] (CSR)
+   std::vector<int> recv_off;           // P: ghost block of nbrs[k] = [n_owned+recv_off[k], n_owned+recv_off[k+1])
+};
+
+// CartesianPartitioning along z of a lexicographic Cartesian mesh (mesh.cpp:8966 semantics
+// for a 1 x 1 x nranks grid): elem_rank[e].
+std::vector<int> partition_slabs_z(const HexMesh &m, int nranks);
+
+LocalPart build_local_part(const H1Space &s, const std::vector<int> &elem_rank, int rank, int nranks);
+
+} // namespace ecm2

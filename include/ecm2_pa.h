@@ -77,6 +77,9 @@ int ecm2_mesh_get_element_nodes(const ecm2_mesh *m, double *out);
  * out[ne][q1d^3][3] (q lexicographic, qx fastest): the points a FunctionCoefficient is
  * projected at (Coefficient::Project, fem/coefficient.cpp:52-70). */
 int ecm2_mesh_quadrature_points(const ecm2_mesh *m, int q1d, double *out);
+/* Same for a subset of elements (host elems[n]), out[n][q1d^3][3]. */
+int ecm2_mesh_quadrature_points_subset(const ecm2_mesh *m, int q1d, const int *elems, int n,
+                                       double *out);
 void ecm2_mesh_destroy(ecm2_mesh *m);
 
 /* H1_FECollection(order) + FiniteElementSpace: element->dof table in
@@ -147,6 +150,56 @@ void ecm2_pa_form_destroy(ecm2_pa_form *f);
 int ecm2_pcg_solve(ecm2_pa_form *f, const int *ess, int n_ess, const double *b, double *x,
                    double rel_tol, double abs_tol, int max_iter, int jacobi, int *iterations,
                    double *final_norm, void *stream);
+
+/* ------------------------------------------------------------------------ */
+/* Distributed form: ParBilinearForm / RAPOperator(P, A, P) over RCCL          */
+/* ------------------------------------------------------------------------ */
+typedef struct ecm2_partition ecm2_partition;
+typedef struct ecm2_par_form ecm2_par_form;
+
+/* Mesh::CartesianPartitioning along z (mesh/mesh.cpp:8966) of a lexicographic Cartesian
+ * mesh: elem_rank host [ne]. */
+int ecm2_partition_slabs_z(const ecm2_mesh *m, int nranks, int *elem_rank);
+/* Per-rank local space of a global H1 space and an element partition (ParMesh +
+ * ParFiniteElementSpace, pmesh.hpp:33, pfespace.cpp:1389-1418): local L-vector
+ * [owned | ghost], owner = lowest touching rank, local elements [interior | boundary],
+ * neighbour exchange lists in the DeviceConformingProlongationOperator sense. */
+int ecm2_partition_create(const ecm2_h1space *s, const int *elem_rank, int rank, int nranks,
+                          ecm2_partition **out);
+int ecm2_partition_info(const ecm2_partition *p, int *ne_local, int *ne_interior, int *n_owned,
+                        int *n_ghost, int *n_nbrs, int *n_send);
+/* Any output may be NULL. elems [ne_local] (global ids, local order), local_to_global
+ * [n_owned+n_ghost], gather_map [ne_local][nd] (local), nbrs [n_nbrs], send_off / recv_off
+ * [n_nbrs+1], send_idx [n_send] (owned local indices). */
+int ecm2_partition_get(const ecm2_partition *p, int *elems, int *local_to_global, int *gather_map,
+                       int *nbrs, int *send_off, int *send_idx, int *recv_off);
+void ecm2_partition_destroy(ecm2_partition *p);
+
+/* ncclGetUniqueId (128 bytes) for ecm2_par_form_create; broadcast it to all ranks. */
+int ecm2_rccl_unique_id(unsigned char *id128);
+/* enodes_local: host [ne_local][3][8] in the partition's local element order.
+ * rccl_id: 128-byte id (one process per GPU, ncclCommInitRank) or NULL for a member of an
+ * in-process loopback group (ecm2_par_group_mult). */
+int ecm2_par_form_create(const ecm2_partition *p, const double *enodes_local, int q1d,
+                         const unsigned char *rccl_id, ecm2_par_form **out);
+/* As ecm2_pa_form_add_integrator, on local data: QUAD -> device [ne_local][nq] in local
+ * element order; GRIDFUNC_AFFINE -> device local L-vector [n_owned + n_ghost]. */
+int ecm2_par_form_add_integrator(ecm2_par_form *f, int integrator, int coeff_kind,
+                                 const double *data, const double *params);
+int ecm2_par_form_set_kernel(ecm2_par_form *f, int kernel);
+int ecm2_par_form_assemble(ecm2_par_form *f, void *stream);
+/* RAPOperator::Mult (operator.hpp:977): y_true = P^T A P x_true; x_true, y_true device
+ * [n_owned].  Grouped ncclSend/ncclRecv on an internal stream overlapped with the
+ * interior elements. */
+int ecm2_par_form_mult(ecm2_par_form *f, const double *x_true, double *y_true, void *stream);
+/* All subdomains of one partition in this process on one GPU (exchange by device copies). */
+int ecm2_par_group_mult(ecm2_par_form *const *forms, int n, const double *const *x_true,
+                        double *const *y_true, void *stream);
+int ecm2_par_form_timing(ecm2_par_form *f, int enable);
+int ecm2_par_form_timing_get(ecm2_par_form *f, double *total_ms, long *launches);
+int ecm2_par_form_algorithmic_bytes(const ecm2_par_form *f, double *bytes);
+int ecm2_par_form_info(const ecm2_par_form *f, int *n_true, int *kernel);
+void ecm2_par_form_destroy(ecm2_par_form *f);
 
 #ifdef __cplusplus
 }

@@ -4,7 +4,9 @@ Coefficients restate tests/unit/fem/test_pa_coeff.cpp:45-58 (coeffFunction) and 
 non-aligned Cartesian mesh of test_pa_coeff.cpp:22-42; the bioheat coefficients
 follow SURVEY §8(d) (alpha = rho*c_eff, beta = gamma*dt*k(T)).
 """
+import importlib.util
 import os
+import sys
 
 import numpy as np
 
@@ -87,3 +89,22 @@ def element_nodes_from(V, E):
     for a in range(8):
         en[:, :, a] = V[E[:, LEX_TO_NATIVE[a]]]
     return en
+
+
+def load_pkg():
+    """Register the package (directory name has hyphens) as `ecm2_amd`; idempotent."""
+    if "ecm2_amd" in sys.modules:
+        return sys.modules["ecm2_amd"]
+    pkg_dir = os.path.join(ROOT, "cardiac-ablation-ecm2_amd")
+    spec = importlib.util.spec_from_file_location("ecm2_amd", os.path.join(pkg_dir, "__init__.py"),
+                                                  submodule_search_locations=[pkg_dir])
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["ecm2_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+for _d in (os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+    if _d not in sys.path:
+        sys.path.insert(0, _d)
+load_pkg()

@@ -87,10 +87,10 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
+    torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank % max(1, torch.cuda.device_count())))
     E = load_pkg()
     E.load_library()
     kernel = {"auto": E.KERNEL_AUTO, "tpe": E.KERNEL_TPE, "wpe": E.KERNEL_WPE, "unfused": E.KERNEL_UNFUSED}[args.kernel]
@@ -112,7 +112,7 @@ def main():
     diff = lambda T: E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(T, K_SCALE, K_SLOPE, K_TREF))
     if nsub <= 1:
         alpha, T = bioheat_coefficients(E, torch, mesh, fes)
-        form = E.BilinearForm(fes, kernel=kernel)
+        form = E.BilinearForm(fes, kernel=kernel, element_order=os.environ.get("ECM2_ELEMENT_ORDER", "auto"))
         form.AddDomainIntegrator(mass(alpha))
         form.AddDomainIntegrator(diff(T))
         form.Assemble()

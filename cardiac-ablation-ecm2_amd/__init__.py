@@ -34,6 +34,7 @@ MASS, DIFFUSION = 0, 1
 COEFF_CONSTANT, COEFF_QUAD, COEFF_GRIDFUNC_AFFINE = 0, 1, 2
 KERNEL_AUTO, KERNEL_TPE, KERNEL_WPE, KERNEL_UNFUSED = 0, 1, 2, 3
 NUMBERING_ENTITY, NUMBERING_STRUCTURED = 0, 1
+ORDER_NATIVE, ORDER_BRICK, ORDER_MORTON = 0, 1, 2
 
 
 class ECM2Error(RuntimeError):
@@ -82,6 +83,8 @@ def load_library(path: str = LIB_PATH):
         "ecm2_pa_form_set_jacobians": (i32, [vp, vp]),
         "ecm2_pa_form_add_integrator": (i32, [vp, i32, i32, vp, vp]),
         "ecm2_pa_form_set_kernel": (i32, [vp, i32]),
+        "ecm2_pa_form_set_element_order": (i32, [vp, vp]),
+        "ecm2_mesh_element_order": (i32, [vp, i32, vp]),
         "ecm2_pa_form_assemble": (i32, [vp, vp]),
         "ecm2_pa_form_mult": (i32, [vp, vp, vp, vp]),
         "ecm2_pa_form_assemble_diagonal": (i32, [vp, vp, vp]),
@@ -194,6 +197,12 @@ class Mesh:
         _check(_lib.ecm2_mesh_get_elements(self._h, _np_ptr(out)))
         return out
 
+    def element_order(self, kind: int) -> np.ndarray:
+        """0 native, 1 brick (Cartesian only), 2 Morton order of centroids."""
+        out = np.empty(self.GetNE(), np.int32)
+        _check(_lib.ecm2_mesh_element_order(self._h, kind, _np_ptr(out)))
+        return out
+
     def quadrature_points(self, q1d: int) -> np.ndarray:
         """Physical Gauss-Legendre points [ne][q1d^3][3] (FunctionCoefficient projection points)."""
         out = np.empty((self.GetNE(), q1d ** 3, 3), np.float64)
@@ -296,7 +305,8 @@ class AssemblyLevel:
 class BilinearForm:
     """BilinearForm at AssemblyLevel::PARTIAL backed by the HIP PA form."""
 
-    def __init__(self, fes: H1Space, kernel: int = KERNEL_AUTO, q1d: int = 0, geometry: str = "nodes"):
+    def __init__(self, fes: H1Space, kernel: int = KERNEL_AUTO, q1d: int = 0, geometry: str = "nodes",
+                 element_order: str = "auto"):
         self.fes = fes
         self._integs = []
         self._kernel = kernel
@@ -309,6 +319,17 @@ class BilinearForm:
             en = fes.mesh.element_nodes()
             _check(_lib.ecm2_pa_form_set_element_nodes(h, _np_ptr(en)))
         _check(_lib.ecm2_pa_form_set_kernel(h, kernel))
+        if element_order != "native" and fes.ne > 0:
+            if element_order in ("auto", "brick"):
+                try:
+                    perm = fes.mesh.element_order(ORDER_BRICK)
+                except ECM2Error:
+                    if element_order == "brick":
+                        raise
+                    perm = fes.mesh.element_order(ORDER_MORTON)
+            else:
+                perm = fes.mesh.element_order(ORDER_MORTON)
+            _check(_lib.ecm2_pa_form_set_element_order(h, _np_ptr(perm)))
 
     def __del__(self):
         if getattr(self, "_h", None) and _lib is not None:
@@ -399,8 +420,8 @@ class BilinearForm:
 # ----------------------------------------------------------------------------
 _PAR_SIGS = {
     "ecm2_partition_slabs_z": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
-    "ecm2_partition_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
-                                             ctypes.POINTER(ctypes.c_void_p)]),
+    "ecm2_partition_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                             ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "ecm2_partition_info": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_int)] * 6),
     "ecm2_partition_get": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 7),
     "ecm2_partition_destroy": (None, [ctypes.c_void_p]),
@@ -457,7 +478,7 @@ class Partition:
         lib = _par_lib()
         er = np.ascontiguousarray(elem_rank, np.int32)
         h = ctypes.c_void_p()
-        _check(lib.ecm2_partition_create(fes._h, _np_ptr(er), rank, nranks, ctypes.byref(h)))
+        _check(lib.ecm2_partition_create(fes._h, fes.mesh._h, _np_ptr(er), rank, nranks, ctypes.byref(h)))
         self._h = h
         self.fes, self.rank, self.nranks = fes, rank, nranks
         v = [ctypes.c_int() for _ in range(6)]

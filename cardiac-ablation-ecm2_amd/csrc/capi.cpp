@@ -184,6 +184,15 @@ int ecm2_mesh_quadrature_points_subset(const ecm2_mesh *m, int q1d, const int *e
    return guard([&] { NEED(m); NEED(out); ECM2_VERIFY(n == 0 || elems, ecm2::ERR_ARG, "null elems"); quad_points(m->m, q1d, elems, n, out); });
 }
 
+int ecm2_mesh_element_order(const ecm2_mesh *m, int kind, int *perm)
+{
+   return guard([&] {
+      NEED(m); NEED(perm);
+      const std::vector<int> p = ecm2::element_order(m->m, kind);
+      std::memcpy(perm, p.data(), p.size() * sizeof(int));
+   });
+}
+
 void ecm2_mesh_destroy(ecm2_mesh *m) { delete m; }
 
 // ---- space ----
@@ -288,6 +297,11 @@ int ecm2_pa_form_add_integrator(ecm2_pa_form *f, int integrator, int coeff_kind,
    });
 }
 
+int ecm2_pa_form_set_element_order(ecm2_pa_form *f, const int *perm)
+{
+   return guard([&] { NEED(f); NEED(perm); f->f->set_element_order(perm); });
+}
+
 int ecm2_pa_form_set_kernel(ecm2_pa_form *f, int kernel)
 {
    return guard([&] { NEED(f); f->f->set_kernel(kernel); });
@@ -390,13 +404,15 @@ int ecm2_partition_slabs_z(const ecm2_mesh *m, int nranks, int *elem_rank)
    });
 }
 
-int ecm2_partition_create(const ecm2_h1space *s, const int *elem_rank, int rank, int nranks,
-                          ecm2_partition **out)
+int ecm2_partition_create(const ecm2_h1space *s, const ecm2_mesh *m, const int *elem_rank, int rank,
+                          int nranks, ecm2_partition **out)
 {
    return guard([&] {
       NEED(s); NEED(elem_rank); NEED(out);
       std::vector<int> er(elem_rank, elem_rank + s->s.ne);
-      *out = new ecm2_partition{ecm2::build_local_part(s->s, er, rank, nranks)};
+      const bool cart = m && m->m.nx > 0 && m->m.ne == s->s.ne;
+      *out = new ecm2_partition{ecm2::build_local_part(s->s, er, rank, nranks, cart ? m->m.nx : 0,
+                                                       cart ? m->m.ny : 0, cart ? m->m.nz : 0)};
    });
 }
 

@@ -2,7 +2,9 @@
 //
 // Quadrature-data layouts (the qdata a PA form owns):
 //  * BLOCKED (fused thread-per-element kernel): elements in blocks of 64 (one
-//    wave; lane = element).  diffusion: [blk][q][pair 0..2][lane][2] holding the
+//    wave; lane = element).  The blocked element->dof map packs bit 30 = "shared dof"
+//    (atomic add after in-wave assembly) and bit 31 = orientation sign.
+//    diffusion qdata: [blk][q][pair 0..2][lane][2] holding the
 //    symmetric entries (11,12),(13,22),(23,33); mass: [blk][q/2][lane][2] (two
 //    consecutive quadrature points per 16-byte slot).  Every wave-instruction
 //    is one 1 KiB contiguous dwordx4 load.
@@ -25,6 +27,7 @@ struct QLayout
 {
    int kind = QLAYOUT_NATIVE;
    int ne = 0, nq = 0;
+   const int *pos = nullptr;  // device: caller element -> internal position (BLOCKED)
    size_t diff_size() const
    {
       if (kind == QLAYOUT_NATIVE) { return (size_t)ne * 6 * nq; }
@@ -59,6 +62,8 @@ struct ApplyArgs
 {
    int kind = QLAYOUT_NATIVE;
    int ne = 0, blk_begin = 0, blk_end = 0, n_owned = 0;
+   const int *pos = nullptr;        // element permutation (blocked layout), may be null
+   const int *lane_flags = nullptr; // [blk][64]: in-wave face merge flags
    const int *gmap = nullptr;
    const double *qdd = nullptr, *qdm = nullptr;
    const double *x = nullptr, *xg = nullptr;
@@ -100,7 +105,7 @@ void restriction_mult_transpose(int ndofs, int nd, const int *offsets, const int
                                 const double *xe, double *y, hipStream_t s);
 
 // ---- diagonal (Jacobi) ----
-void diagonal(int D, int Q, int layout, int ne, const int *gmap_native, const double *qd_diff,
+void diagonal(const int *pos, int D, int Q, int layout, int ne, const int *gmap_native, const double *qd_diff,
               const double *qd_mass, double *diag, bool out_evec, const Basis1D &b,
               hipStream_t s);
 

@@ -244,6 +244,79 @@ void HexMesh::refine_uniform()
    if (nx) { nx = 0; ny = 0; nz = 0; }  // element order is no longer lexicographic
 }
 
+std::vector<int> brick_order(const std::vector<int> &elems, int nx, int ny, int nz)
+{
+   const int bx = (nx + 3) / 4, by = (ny + 3) / 4, bz = (nz + 3) / 4;
+   const long nb = (long)bx * by * bz;
+   std::vector<int> count(nb, 0);
+   auto key = [&](int e) {
+      const int ex = e % nx, ey = (e / nx) % ny, ez = e / (nx * ny);
+      return (long)(ex / 4) + bx * ((long)(ey / 4) + (long)by * (ez / 4));
+   };
+   for (int e : elems) { count[key(e)]++; }
+   std::vector<int> out;
+   out.reserve(elems.size());
+   // complete bricks, in brick-lexicographic order, members x-fastest
+   std::vector<int> sorted(elems);
+   std::stable_sort(sorted.begin(), sorted.end(), [&](int a, int b) {
+      const long ka = key(a), kb = key(b);
+      if (ka != kb) { return ka < kb; }
+      const int ax = a % nx % 4, ay = (a / nx) % ny % 4, az = (a / (nx * ny)) % 4;
+      const int bxx = b % nx % 4, byy = (b / nx) % ny % 4, bzz = (b / (nx * ny)) % 4;
+      return ax + 4 * ay + 16 * az < bxx + 4 * byy + 16 * bzz;
+   });
+   for (int e : sorted) { if (count[key(e)] == 64) { out.push_back(e); } }
+   for (int e : elems) { if (count[key(e)] != 64) { out.push_back(e); } }
+   return out;
+}
+
+std::vector<int> element_order(const HexMesh &m, int kind)
+{
+   std::vector<int> perm(m.ne);
+   for (int e = 0; e < m.ne; e++) { perm[e] = e; }
+   if (kind == ORDER_NATIVE || m.ne == 0) { return perm; }
+   if (kind == ORDER_BRICK)
+   {
+      ECM2_VERIFY(m.nx > 0, ERR_ARG, "brick order needs a lexicographic Cartesian mesh");
+      return brick_order(perm, m.nx, m.ny, m.nz);
+   }
+   ECM2_VERIFY(kind == ORDER_MORTON, ERR_ARG, "unknown element order " << kind);
+   double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+   std::vector<double> c((size_t)m.ne * 3, 0.0);
+   for (int e = 0; e < m.ne; e++)
+      for (int k = 0; k < 8; k++)
+         for (int d = 0; d < 3; d++) { c[3 * (size_t)e + d] += 0.125 * m.vert[3 * (size_t)m.elem[8 * (size_t)e + k] + d]; }
+   for (int e = 0; e < m.ne; e++)
+      for (int d = 0; d < 3; d++)
+      {
+         lo[d] = std::min(lo[d], c[3 * (size_t)e + d]);
+         hi[d] = std::max(hi[d], c[3 * (size_t)e + d]);
+      }
+   auto spread = [](uint64_t v) {  // 21 bits -> every third bit
+      v &= 0x1fffff;
+      v = (v | v << 32) & 0x1f00000000ffffull;
+      v = (v | v << 16) & 0x1f0000ff0000ffull;
+      v = (v | v << 8) & 0x100f00f00f00f00full;
+      v = (v | v << 4) & 0x10c30c30c30c30c3ull;
+      v = (v | v << 2) & 0x1249249249249249ull;
+      return v;
+   };
+   std::vector<uint64_t> code(m.ne);
+   for (int e = 0; e < m.ne; e++)
+   {
+      uint64_t k = 0;
+      for (int d = 0; d < 3; d++)
+      {
+         const double span = hi[d] > lo[d] ? hi[d] - lo[d] : 1.0;
+         const uint64_t q = (uint64_t)((c[3 * (size_t)e + d] - lo[d]) / span * 2097151.0);
+         k |= spread(q) << d;
+      }
+      code[e] = k;
+   }
+   std::stable_sort(perm.begin(), perm.end(), [&](int a, int b) { return code[a] < code[b]; });
+   return perm;
+}
+
 void HexMesh::element_nodes(std::vector<double> &out) const
 {
    out.resize((size_t)ne * 24);

@@ -36,6 +36,18 @@ struct HexMesh
    void element_nodes(std::vector<double> &out) const;
 };
 
+enum ElementOrder : int
+{
+   ORDER_NATIVE = 0,   // caller's order
+   ORDER_BRICK = 1,    // Cartesian: 4x4x4 bricks (one per 64-lane wave), then the rest
+   ORDER_MORTON = 2    // any mesh: Morton (Z-order) of element centroids
+};
+// Permutation perm[i] = caller element at internal position i.
+std::vector<int> element_order(const HexMesh &m, int kind);
+// Brick order of a subset of the elements of a lexicographic nx x ny x nz mesh: complete
+// 4x4x4 bricks first (members x-fastest), then the remaining elements in given order.
+std::vector<int> brick_order(const std::vector<int> &elems, int nx, int ny, int nz);
+
 enum Numbering : int
 {
    NUMBERING_ENTITY = 0,     // vertex -> edge -> face -> interior (MFEM fespace order)

@@ -88,6 +88,90 @@ void PAForm::add_integrator(int kind, const CoeffDesc &c)
    assembled_ = false;
 }
 
+void PAForm::set_element_order(const int *perm)
+{
+   std::vector<int> seen(ne_, 0);
+   perm_host_.assign(perm, perm + ne_);
+   for (int e : perm_host_)
+   {
+      ECM2_VERIFY(e >= 0 && e < ne_ && !seen[e], ERR_ARG, "element order is not a permutation");
+      seen[e] = 1;
+   }
+   gmap_blk_.resize(0);
+   assembled_ = false;
+}
+
+namespace
+{
+// In-wave face assembly plan for the blocked (64 elements per wave) layout.
+// Directions x, y, z pair lane l with l+1, l+4, l+16: lane l adds the partner's
+// low face (index 0 along the direction) into its high face (index D-1) when all
+// face dofs coincide and no nonzero value could land in an entry that no longer
+// holds its dof; the partner then zeroes that face.  After the three passes the
+// "holding" entries carry each dof's in-wave sum; a dof held once in the whole mesh
+// is plain-stored, otherwise atomically added.
+void build_merge_plan(int ne, int D, const std::vector<int> &gmap_int, int ndofs,
+                      std::vector<char> &shared, std::vector<int> &flags)
+{
+   const int ND = D * D * D, nblk = (ne + 63) / 64;
+   shared.assign((size_t)ne * ND, 0);
+   flags.assign((size_t)nblk * 64, 0);
+   std::vector<char> holds((size_t)nblk * 64 * ND, 0);
+   std::vector<int> hcount(ndofs, 0);
+   auto dofv = [](int g) { return g >= 0 ? g : -1 - g; };
+   auto face = [D](int dir, int s, int i, int j) {
+      if (dir == 0) { return (j * D + i) * D + s; }
+      if (dir == 1) { return (j * D + s) * D + i; }
+      return (s * D + j) * D + i;
+   };
+   const int off[3] = {1, 4, 16}, recv[3] = {1, 4, 16}, sent[3] = {2, 8, 32};
+   for (int b = 0; b < nblk; b++)
+   {
+      auto act = [&](int l) { return b * 64 + l < ne; };
+      auto dof = [&](int l, int a) { return dofv(gmap_int[((size_t)b * 64 + l) * ND + a]); };
+      auto H = [&](int l, int a) -> char & { return holds[((size_t)b * 64 + l) * ND + a]; };
+      for (int l = 0; l < 64; l++)
+         for (int a = 0; a < ND; a++) { H(l, a) = act(l); }
+      for (int dir = 0; dir < 3; dir++)
+      {
+         for (int l = 0; l + off[dir] < 64; l++)
+         {
+            const int m = l + off[dir];
+            if (!act(l) || !act(m)) { continue; }
+            bool ok = true;
+            for (int j = 0; j < D && ok; j++)
+               for (int i = 0; i < D && ok; i++)
+               {
+                  const int ar = face(dir, D - 1, i, j), as = face(dir, 0, i, j);
+                  ok = dof(l, ar) == dof(m, as) && (H(l, ar) || !H(m, as));
+               }
+            if (!ok) { continue; }
+            flags[(size_t)b * 64 + l] |= recv[dir];
+            flags[(size_t)b * 64 + m] |= sent[dir];
+         }
+         for (int m = 0; m < 64; m++)
+         {
+            if (!(flags[(size_t)b * 64 + m] & sent[dir])) { continue; }
+            for (int j = 0; j < D; j++)
+               for (int i = 0; i < D; i++) { H(m, face(dir, 0, i, j)) = 0; }
+         }
+      }
+      for (int l = 0; l < 64; l++)
+         for (int a = 0; a < ND; a++) { if (H(l, a)) { hcount[dof(l, a)]++; } }
+   }
+   for (int b = 0; b < nblk; b++)
+      for (int l = 0; l < 64; l++)
+      {
+         if (b * 64 + l >= ne) { continue; }
+         for (int a = 0; a < ND; a++)
+         {
+            const int d = dofv(gmap_int[((size_t)b * 64 + l) * ND + a]);
+            shared[((size_t)b * 64 + l) * ND + a] = hcount[d] > 1;
+         }
+      }
+}
+} // namespace
+
 void PAForm::set_kernel(int mode)
 {
    ECM2_VERIFY(mode >= KERNEL_AUTO && mode <= KERNEL_UNFUSED, ERR_ARG, "unknown kernel mode " << mode);
@@ -109,19 +193,37 @@ void PAForm::assemble(hipStream_t s)
    if (resolved_mode_ == KERNEL_TPE && !gmap_blk_.size() && ne_ > 0)
    {
       const int nblk = layout_.nblk();
-      std::vector<int> blk((size_t)nblk * ND_ * 64, 0);
-      for (int e = 0; e < ne_; e++)
+      std::vector<int> gint((size_t)ne_ * ND_), pos(ne_);
+      for (int i = 0; i < ne_; i++)
       {
-         const int b = e / 64, l = e % 64;
+         const int e = perm_host_.empty() ? i : perm_host_[i];
+         pos[e] = i;
+         std::copy(&gmap_host_[(size_t)e * ND_], &gmap_host_[(size_t)e * ND_] + ND_, &gint[(size_t)i * ND_]);
+      }
+      ECM2_VERIFY(ndofs_ < (1 << 30), ERR_UNSUPPORTED, "fused kernel supports < 2^30 dofs");
+      std::vector<char> shared;
+      std::vector<int> fl;
+      build_merge_plan(ne_, D_, gint, ndofs_, shared, fl);
+      // blocked map: dof | shared << 30 | sign << 31
+      std::vector<int> blk((size_t)nblk * ND_ * 64, 0);
+      for (int i = 0; i < ne_; i++)
+      {
+         const int b = i / 64, l = i % 64;
          for (int a = 0; a < ND_; a++)
          {
-            blk[((size_t)b * ND_ + a) * 64 + l] = gmap_host_[(size_t)e * ND_ + a];
+            const int g = gint[(size_t)i * ND_ + a];
+            const unsigned d = (unsigned)(g >= 0 ? g : -1 - g);
+            const unsigned enc = d | ((unsigned)shared[(size_t)i * ND_ + a] << 30) | ((g < 0 ? 1u : 0u) << 31);
+            blk[((size_t)b * ND_ + a) * 64 + l] = (int)enc;
          }
       }
       gmap_blk_.upload(blk, s);
+      lane_flags_.upload(fl, s);
+      pos_.upload(pos, s);
       rowtab_.upload(kern::make_row_table(maps_), s);
       ECM2_HIP(hipStreamSynchronize(s));
    }
+   layout_.pos = (layout_.kind == QLAYOUT_BLOCKED) ? pos_.data() : nullptr;
    qd_diff_.resize(have_diff_ ? layout_.diff_size() : 0);
    qd_mass_.resize(have_mass_ ? layout_.mass_size() : 0);
    if (qd_diff_.size()) { ECM2_HIP(hipMemsetAsync(qd_diff_.data(), 0, qd_diff_.bytes(), s)); }
@@ -266,6 +368,8 @@ ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, doubl
    a.blk_begin = b0;
    a.blk_end = b1;
    a.n_owned = n_owned_;
+   a.pos = layout_.pos;
+   a.lane_flags = lane_flags_.data();
    a.gmap = (resolved_mode_ == KERNEL_TPE) ? gmap_blk_.data() : gmap_.data();
    a.qdd = qd_diff_.data();
    a.qdm = qd_mass_.data();
@@ -294,7 +398,7 @@ void PAForm::assemble_diagonal(double *diag, hipStream_t s)
    ECM2_VERIFY(assembled_, ERR_STATE, "AssembleDiagonal before Assemble");
    if (ndofs_ == 0) { return; }
    ECM2_HIP(hipMemsetAsync(diag, 0, sizeof(double) * (size_t)ndofs_, s));
-   kern::diagonal(D_, Q_, layout_.kind, ne_, gmap_.data(), have_diff_ ? qd_diff_.data() : nullptr,
+   kern::diagonal(layout_.pos, D_, Q_, layout_.kind, ne_, gmap_.data(), have_diff_ ? qd_diff_.data() : nullptr,
                   have_mass_ ? qd_mass_.data() : nullptr, diag, false, basis_, s);
 }
 
@@ -332,6 +436,13 @@ void PAForm::get_qdata(int kind, double *out, hipStream_t s)
       ECM2_HIP(hipStreamSynchronize(s));
    }
    const int nc = diff ? 6 : 1;
+   std::vector<int> invp;
+   if (!perm_host_.empty())
+   {
+      invp.resize(ne_);
+      for (int i = 0; i < ne_; i++) { invp[perm_host_[i]] = i; }
+   }
+   auto inv_perm = [&](int e) { return invp[e]; };
    for (int e = 0; e < ne_; e++)
       for (int c = 0; c < nc; c++)
          for (int q = 0; q < NQ_; q++)
@@ -340,7 +451,8 @@ void PAForm::get_qdata(int kind, double *out, hipStream_t s)
             if (layout_.kind == QLAYOUT_NATIVE) { src_i = ((size_t)e * nc + c) * NQ_ + q; }
             else
             {
-               const int blk = e / 64, lane = e % 64;
+               const int ip = perm_host_.empty() ? e : inv_perm(e);
+               const int blk = ip / 64, lane = ip % 64;
                if (diff) { src_i = (((size_t)blk * NQ_ + q) * 3 + c / 2) * 128 + lane * 2 + (c & 1); }
                else { src_i = ((size_t)blk * ((NQ_ + 1) / 2) + q / 2) * 128 + lane * 2 + (q & 1); }
             }

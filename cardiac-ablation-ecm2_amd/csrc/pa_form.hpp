@@ -55,6 +55,10 @@ public:
    void set_element_nodes(const double *enodes_host);
    void set_jacobians(const double *J_device);
 
+   // Optional element permutation (internal position i <- caller element perm[i]) used by
+   // the blocked layout; ORDER_BRICK puts one 4x4x4 brick in each 64-lane wave so the
+   // fused kernel can assemble shared faces in-wave.  All APIs keep caller element order.
+   void set_element_order(const int *perm_host);
    void add_integrator(int kind, const CoeffDesc &c);
    void set_kernel(int mode);
    void assemble(hipStream_t s);
@@ -106,7 +110,10 @@ private:
 
    std::vector<int> gmap_host_;
    DeviceArray<int> gmap_;          // native [e][nd]
-   DeviceArray<int> gmap_blk_;      // blocked [blk][nd][64]
+   DeviceArray<int> gmap_blk_;      // blocked [blk][nd][64] (internal element order)
+   DeviceArray<int> lane_flags_;    // [blk][64] in-wave merge flags
+   std::vector<int> perm_host_;     // internal position -> caller element (empty: identity)
+   DeviceArray<int> pos_;           // caller element -> internal position
    DeviceArray<int> csr_off_, csr_idx_;
    DeviceArray<double> enodes_;     // [e][3][8]
    const double *jac_ = nullptr;    // device, not owned

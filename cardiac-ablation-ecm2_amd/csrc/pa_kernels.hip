@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace ecm2
 {
@@ -30,24 +31,34 @@ namespace
 {
 
 constexpr int MQ = MAX_Q1D;
+constexpr int kDefaultTpeVariant = 4;  // pipelined + brick merge
 typedef double v2d __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ size_t qidx_diff(int kind, int nq, int e, int c, int q)
+// pos: caller element -> internal position (element permutation of the blocked layout)
+__device__ __forceinline__ size_t qidx_diff(const int *pos, int kind, int nq, int e, int c, int q)
 {
    if (kind == QLAYOUT_NATIVE) { return ((size_t)e * 6 + c) * nq + q; }
+   if (pos) { e = pos[e]; }
    const int blk = e >> 6, lane = e & 63;
    return (((size_t)blk * nq + q) * 3 + (c >> 1)) * 128 + lane * 2 + (c & 1);
 }
 
-__device__ __forceinline__ size_t qidx_mass(int kind, int nq, int e, int q)
+__device__ __forceinline__ size_t qidx_mass(const int *pos, int kind, int nq, int e, int q)
 {
    if (kind == QLAYOUT_NATIVE) { return (size_t)e * nq + q; }
+   if (pos) { e = pos[e]; }
    const int blk = e >> 6, lane = e & 63;
    const int nqh = (nq + 1) >> 1;
    return ((size_t)blk * nqh + (q >> 1)) * 128 + lane * 2 + (q & 1);
 }
 
 __device__ __forceinline__ int dof_of(int g) { return g >= 0 ? g : -1 - g; }
+
+// Blocked (fused-kernel) map entries: bits 0-29 dof, bit 30 "shared" (the dof is held by
+// more than one lane of the whole mesh after in-wave assembly -> atomic add), bit 31 sign.
+__device__ __forceinline__ int bdof(int g) { return g & 0x3fffffff; }
+__device__ __forceinline__ bool bneg(int g) { return g < 0; }
+__device__ __forceinline__ bool bshared(int g) { return (g >> 30) & 1; }
 
 // --------------------------------------------------------------------------
 // Setup kernels
@@ -89,7 +100,7 @@ __device__ __forceinline__ double coef_at(const SetupCoef &c, size_t eq)
 }
 
 // Write D (6 symmetric entries) and mass value at one quadrature point.
-__device__ __forceinline__ void write_qdata(int kind, int nq, int e, int q, double w,
+__device__ __forceinline__ void write_qdata(const int *pos, int kind, int nq, int e, int q, double w,
                                             const double J[3][3], const SetupCoef &cm,
                                             const SetupCoef &cd, double *qd_diff,
                                             double *qd_mass)
@@ -113,20 +124,20 @@ __device__ __forceinline__ void write_qdata(int kind, int nq, int e, int q, doub
       const double A32 = (J31 * J12) - (J11 * J32);
       const double A33 = (J11 * J22) - (J12 * J21);
       const double C = coef_at(cd, eq);
-      qd_diff[qidx_diff(kind, nq, e, 0, q)] = w_detJ * (C * A11 * A11 + C * A12 * A12 + C * A13 * A13);
-      qd_diff[qidx_diff(kind, nq, e, 1, q)] = w_detJ * (C * A11 * A21 + C * A12 * A22 + C * A13 * A23);
-      qd_diff[qidx_diff(kind, nq, e, 2, q)] = w_detJ * (C * A11 * A31 + C * A12 * A32 + C * A13 * A33);
-      qd_diff[qidx_diff(kind, nq, e, 3, q)] = w_detJ * (C * A21 * A21 + C * A22 * A22 + C * A23 * A23);
-      qd_diff[qidx_diff(kind, nq, e, 4, q)] = w_detJ * (C * A21 * A31 + C * A22 * A32 + C * A23 * A33);
-      qd_diff[qidx_diff(kind, nq, e, 5, q)] = w_detJ * (C * A31 * A31 + C * A32 * A32 + C * A33 * A33);
+      qd_diff[qidx_diff(pos, kind, nq, e, 0, q)] = w_detJ * (C * A11 * A11 + C * A12 * A12 + C * A13 * A13);
+      qd_diff[qidx_diff(pos, kind, nq, e, 1, q)] = w_detJ * (C * A11 * A21 + C * A12 * A22 + C * A13 * A23);
+      qd_diff[qidx_diff(pos, kind, nq, e, 2, q)] = w_detJ * (C * A11 * A31 + C * A12 * A32 + C * A13 * A33);
+      qd_diff[qidx_diff(pos, kind, nq, e, 3, q)] = w_detJ * (C * A21 * A21 + C * A22 * A22 + C * A23 * A23);
+      qd_diff[qidx_diff(pos, kind, nq, e, 4, q)] = w_detJ * (C * A21 * A31 + C * A22 * A32 + C * A23 * A33);
+      qd_diff[qidx_diff(pos, kind, nq, e, 5, q)] = w_detJ * (C * A31 * A31 + C * A32 * A32 + C * A33 * A33);
    }
    if (cm.has)
    {
-      qd_mass[qidx_mass(kind, nq, e, q)] = w * coef_at(cm, eq) * detJ;
+      qd_mass[qidx_mass(pos, kind, nq, e, q)] = w * coef_at(cm, eq) * detJ;
    }
 }
 
-__global__ void k_setup_nodes(int kind, int ne, int Q, const double *__restrict__ enodes,
+__global__ void k_setup_nodes(const int *__restrict__ pos, int kind, int ne, int Q, const double *__restrict__ enodes,
                               const double *__restrict__ W, const Basis1D b1, SetupCoef cm,
                               SetupCoef cd, double *__restrict__ qd_diff,
                               double *__restrict__ qd_mass)
@@ -152,10 +163,10 @@ __global__ void k_setup_nodes(int kind, int ne, int Q, const double *__restrict_
          J[i][2] += xi * dN2;
       }
    }
-   write_qdata(kind, NQ, e, q, W[q], J, cm, cd, qd_diff, qd_mass);
+   write_qdata(pos, kind, NQ, e, q, W[q], J, cm, cd, qd_diff, qd_mass);
 }
 
-__global__ void k_setup_jac(int kind, int ne, int NQ, const double *__restrict__ Jg,
+__global__ void k_setup_jac(const int *__restrict__ pos, int kind, int ne, int NQ, const double *__restrict__ Jg,
                             const double *__restrict__ W, SetupCoef cm, SetupCoef cd,
                             double *__restrict__ qd_diff, double *__restrict__ qd_mass)
 {
@@ -165,7 +176,7 @@ __global__ void k_setup_jac(int kind, int ne, int NQ, const double *__restrict__
    double J[3][3];
    for (int j = 0; j < 3; j++)
       for (int i = 0; i < 3; i++) { J[i][j] = Jg[(((size_t)e * 3 + j) * 3 + i) * NQ + q]; }
-   write_qdata(kind, NQ, e, q, W[q], J, cm, cd, qd_diff, qd_mass);
+   write_qdata(pos, kind, NQ, e, q, W[q], J, cm, cd, qd_diff, qd_mass);
 }
 
 // --------------------------------------------------------------------------
@@ -202,9 +213,9 @@ k_apply_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restri
    for (int a = 0; a < ND; a++)
    {
       const int g = mp[a * 64];
-      const int d = dof_of(g);
+      const int d = bdof(g);
       const double v = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
-      X[a] = g >= 0 ? v : -v;
+      X[a] = bneg(g) ? -v : v;
    }
    double Yo[ND];
 #pragma unroll
@@ -329,10 +340,206 @@ k_apply_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restri
       for (int a = 0; a < ND; a++)
       {
          const int g = mp[a * 64];
-         const int d = dof_of(g);
+         const int d = bdof(g);
          double *dst = (!SPLIT || d < n_owned) ? y + d : yg + (d - n_owned);
-         unsafeAtomicAdd(dst, g >= 0 ? Yo[a] : -Yo[a]);
+         unsafeAtomicAdd(dst, bneg(g) ? -Yo[a] : Yo[a]);
       }
+   }
+}
+
+// Software-pipelined variant: the 27 gathered dofs live in LDS (a private [a][lane]
+// slot per wave: conflict-free ds_read_b64), which frees the VGPRs to hold the NEXT
+// row's qdata in flight while the current row is computed (double buffering).
+// VAR bit0: plain stores instead of atomics (diagnostic: atomic cost, wrong result)
+// VAR bit1: default-policy (not nontemporal) qdata loads
+template <int D, int Q, bool MASS, bool DIFF, bool SPLIT, int VAR>
+__global__ void __launch_bounds__(256, (VAR & 8) ? 2 : 1)
+k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
+               const double *__restrict__ qdd, const double *__restrict__ qdm,
+               const double *__restrict__ x, const double *__restrict__ xg,
+               double *__restrict__ y, double *__restrict__ yg, const Basis1D b,
+               const double *__restrict__ rowtab, const int *__restrict__ lane_flags)
+{
+   constexpr int ND = D * D * D, NQ = Q * Q * Q, NQH = (NQ + 1) / 2, DD = D * D;
+   constexpr int NR = Q * Q;  // rows
+   __shared__ double sX[4][ND][64];
+   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+   const int blk = blk_begin + blockIdx.x * 4 + w;
+   if (blk >= blk_end) { return; }  // wave-uniform; no block-wide barrier below
+   const int e = blk * 64 + lane;
+   const bool active = e < ne;
+   const int *mp = gmap + (size_t)blk * ND * 64 + lane;
+#pragma unroll
+   for (int a = 0; a < ND; a++)
+   {
+      const int g = mp[a * 64];
+      const int d = bdof(g);
+      const double v = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
+      sX[w][a][lane] = bneg(g) ? -v : v;
+   }
+   double Yo[ND];
+#pragma unroll
+   for (int a = 0; a < ND; a++) { Yo[a] = 0.0; }
+
+   const double *qd = qdd + (size_t)blk * NQ * 3 * 128 + lane * 2;
+   const double *qm = qdm + (size_t)blk * NQH * 128 + lane * 2;
+   auto ld2 = [&](const double *p) -> v2d {
+      if (VAR & 2) { return *reinterpret_cast<const v2d *>(p); }
+      return __builtin_nontemporal_load(reinterpret_cast<const v2d *>(p));
+   };
+   // row buffers: diffusion pairs (3 per point) and mass values (Q per row)
+   v2d cd[Q][3], nd_[Q][3];
+   double cm[Q], nm[Q];
+   auto load_row = [&](int row, v2d (&dq)[Q][3], double (&mq)[Q]) {
+#pragma unroll
+      for (int qx = 0; qx < Q; qx++)
+      {
+         const int q = row * Q + qx;
+         if (DIFF)
+         {
+#pragma unroll
+            for (int k = 0; k < 3; k++) { dq[qx][k] = ld2(qd + ((size_t)q * 3 + k) * 128); }
+         }
+         if (MASS) { mq[qx] = qm[(size_t)(q >> 1) * 128 + (q & 1)]; }
+      }
+   };
+   load_row(0, cd, cm);
+
+#pragma unroll 1
+   for (int row = 0; row < NR; row++)
+   {
+      if (row + 1 < NR) { load_row(row + 1, nd_, nm); }
+      const double *P = rowtab + (size_t)row * 3 * DD;
+      double Y00[D], Y01[D], Y10[D];
+#pragma unroll
+      for (int dx = 0; dx < D; dx++)
+      {
+         double u = 0.0, v = 0.0, wv = 0.0;
+#pragma unroll
+         for (int dz = 0; dz < D; dz++)
+#pragma unroll
+            for (int dy = 0; dy < D; dy++)
+            {
+               const double c = sX[w][(dz * D + dy) * D + dx][lane];
+               u += P[0 * DD + dz * D + dy] * c;
+               if (DIFF)
+               {
+                  v += P[1 * DD + dz * D + dy] * c;
+                  wv += P[2 * DD + dz * D + dy] * c;
+               }
+            }
+         Y00[dx] = u; Y01[dx] = v; Y10[dx] = wv;
+      }
+      double T0[D], T1[D], T2[D];
+#pragma unroll
+      for (int dx = 0; dx < D; dx++) { T0[dx] = 0.0; T1[dx] = 0.0; T2[dx] = 0.0; }
+#pragma unroll
+      for (int qx = 0; qx < Q; qx++)
+      {
+         double u = 0.0, ux = 0.0, uy = 0.0, uz = 0.0;
+#pragma unroll
+         for (int dx = 0; dx < D; dx++)
+         {
+            const double bq = b.B[qx + MQ * dx], gq = b.G[qx + MQ * dx];
+            if (MASS) { u += bq * Y00[dx]; }
+            if (DIFF)
+            {
+               ux += gq * Y00[dx];
+               uy += bq * Y01[dx];
+               uz += bq * Y10[dx];
+            }
+         }
+         double m = 0.0, fx = 0.0, fy = 0.0, fz = 0.0;
+         if (MASS) { m = cm[qx] * u; }
+         if (DIFF)
+         {
+            const v2d d0 = cd[qx][0], d1 = cd[qx][1], d2 = cd[qx][2];
+            fx = d0.x * ux + d0.y * uy + d1.x * uz;
+            fy = d0.y * ux + d1.y * uy + d2.x * uz;
+            fz = d1.x * ux + d2.x * uy + d2.y * uz;
+         }
+#pragma unroll
+         for (int dx = 0; dx < D; dx++)
+         {
+            const double bq = b.B[qx + MQ * dx], gq = b.G[qx + MQ * dx];
+            double t0 = T0[dx];
+            if (MASS) { t0 += bq * m; }
+            if (DIFF)
+            {
+               t0 += gq * fx;
+               T1[dx] += bq * fy;
+               T2[dx] += bq * fz;
+            }
+            T0[dx] = t0;
+         }
+      }
+#pragma unroll
+      for (int dz = 0; dz < D; dz++)
+#pragma unroll
+         for (int dy = 0; dy < D; dy++)
+         {
+            const double p0 = P[0 * DD + dz * D + dy];
+            const double p1 = P[1 * DD + dz * D + dy];
+            const double p2 = P[2 * DD + dz * D + dy];
+#pragma unroll
+            for (int dx = 0; dx < D; dx++)
+            {
+               double yo = Yo[(dz * D + dy) * D + dx] + p0 * T0[dx];
+               if (DIFF) { yo += p1 * T1[dx] + p2 * T2[dx]; }
+               Yo[(dz * D + dy) * D + dx] = yo;
+            }
+         }
+#pragma unroll
+      for (int qx = 0; qx < Q; qx++)
+      {
+#pragma unroll
+         for (int k = 0; k < 3; k++) { cd[qx][k] = nd_[qx][k]; }
+         cm[qx] = nm[qx];
+      }
+   }
+   // ---- in-wave assembly of shared faces (4x4x4 brick = one wave: x, y, z neighbours
+   // are lanes +1, +4, +16).  Setup-computed flags say which faces really coincide
+   // (dof-index equality), so any element order is correct; bricks make it effective.
+#pragma unroll
+   for (int a = 0; a < ND; a++)
+   {
+      if (bneg(mp[a * 64])) { Yo[a] = -Yo[a]; }  // orientation signs before summation
+   }
+   const int fl = lane_flags[(size_t)blk * 64 + lane];
+   auto merge = [&](int delta, int recv_bit, int sent_bit, auto face) {
+#pragma unroll
+      for (int j = 0; j < D; j++)
+#pragma unroll
+         for (int i = 0; i < D; i++)
+         {
+            const double v = __shfl_down(Yo[face(0, i, j)], delta, 64);
+            if (fl & recv_bit) { Yo[face(D - 1, i, j)] += v; }
+            if (fl & sent_bit) { Yo[face(0, i, j)] = 0.0; }
+         }
+   };
+   merge(1, 1, 2, [](int s, int i, int j) { return (j * D + i) * D + s; });    // x: (dz=j, dy=i)
+   merge(4, 4, 8, [](int s, int i, int j) { return (j * D + s) * D + i; });    // y: (dz=j, dx=i)
+   merge(16, 16, 32, [](int s, int i, int j) { return (s * D + j) * D + i; }); // z: (dy=j, dx=i)
+   // ---- output: entries whose face was sent away hold nothing; a dof held once in the
+   // whole mesh is plain-stored, a shared one atomically added
+   if (active)
+   {
+      const bool sx = fl & 2, sy = fl & 8, sz = fl & 32;
+#pragma unroll
+      for (int dz = 0; dz < D; dz++)
+#pragma unroll
+         for (int dy = 0; dy < D; dy++)
+#pragma unroll
+            for (int dx = 0; dx < D; dx++)
+            {
+               if ((dx == 0 && sx) || (dy == 0 && sy) || (dz == 0 && sz)) { continue; }
+               const int a = (dz * D + dy) * D + dx;
+               const int g = mp[a * 64];
+               const int d = bdof(g);
+               double *dst = (!SPLIT || d < n_owned) ? y + d : yg + (d - n_owned);
+               if (!bshared(g) || (VAR & 1)) { *dst = Yo[a]; }
+               else { unsafeAtomicAdd(dst, Yo[a]); }
+            }
    }
 }
 
@@ -341,7 +548,7 @@ k_apply_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restri
 // --------------------------------------------------------------------------
 
 template <int D, int Q, bool MASS, bool DIFF, bool IN_E, bool OUT_E>
-__global__ void k_apply_wpe(int kind, int ne, int e_begin, int n_owned,
+__global__ void k_apply_wpe(const int *__restrict__ pos, int kind, int ne, int e_begin, int n_owned,
                             const int *__restrict__ gmap,
                             const double *__restrict__ qdd, const double *__restrict__ qdm,
                             const double *__restrict__ x, const double *__restrict__ xg,
@@ -419,15 +626,15 @@ __global__ void k_apply_wpe(int kind, int ne, int e_begin, int n_owned,
          u += s2c[i] * sB[qz + Q * dz];
       }
       double m = 0.0, fx = 0.0, fy = 0.0, fz = 0.0;
-      if (MASS) { m = qdm[qidx_mass(kind, NQ, e, t)] * u; }
+      if (MASS) { m = qdm[qidx_mass(pos, kind, NQ, e, t)] * u; }
       if (DIFF)
       {
-         const double O11 = qdd[qidx_diff(kind, NQ, e, 0, t)];
-         const double O12 = qdd[qidx_diff(kind, NQ, e, 1, t)];
-         const double O13 = qdd[qidx_diff(kind, NQ, e, 2, t)];
-         const double O22 = qdd[qidx_diff(kind, NQ, e, 3, t)];
-         const double O23 = qdd[qidx_diff(kind, NQ, e, 4, t)];
-         const double O33 = qdd[qidx_diff(kind, NQ, e, 5, t)];
+         const double O11 = qdd[qidx_diff(pos, kind, NQ, e, 0, t)];
+         const double O12 = qdd[qidx_diff(pos, kind, NQ, e, 1, t)];
+         const double O13 = qdd[qidx_diff(pos, kind, NQ, e, 2, t)];
+         const double O22 = qdd[qidx_diff(pos, kind, NQ, e, 3, t)];
+         const double O23 = qdd[qidx_diff(pos, kind, NQ, e, 4, t)];
+         const double O33 = qdd[qidx_diff(pos, kind, NQ, e, 5, t)];
          fx = (O11 * gx) + (O12 * gy) + (O13 * gz);
          fy = (O12 * gx) + (O22 * gy) + (O23 * gz);
          fz = (O13 * gx) + (O23 * gy) + (O33 * gz);
@@ -515,7 +722,7 @@ __global__ void k_restriction_mult_transpose(int ndofs, const int *__restrict__ 
    y[i] = v;
 }
 
-__global__ void k_diagonal(int D, int Q, int kind, int ne, const int *__restrict__ gmap,
+__global__ void k_diagonal(const int *__restrict__ pos, int D, int Q, int kind, int ne, const int *__restrict__ gmap,
                            const double *__restrict__ qdd, const double *__restrict__ qdm,
                            double *__restrict__ diag, bool out_e, const Basis1D b)
 {
@@ -532,16 +739,16 @@ __global__ void k_diagonal(int D, int Q, int kind, int ne, const int *__restrict
             const int q = (qz * Q + qy) * Q + qx;
             const double bx = b.B[qx + MQ * dx], by = b.B[qy + MQ * dy], bz = b.B[qz + MQ * dz];
             const double gx = b.G[qx + MQ * dx], gy = b.G[qy + MQ * dy], gz = b.G[qz + MQ * dz];
-            if (qdm) { s += bx * bx * by * by * bz * bz * qdm[qidx_mass(kind, NQ, e, q)]; }
+            if (qdm) { s += bx * bx * by * by * bz * bz * qdm[qidx_mass(pos, kind, NQ, e, q)]; }
             if (qdd)
             {
                const double p0 = gx * by * bz, p1 = bx * gy * bz, p2 = bx * by * gz;
-               s += p0 * p0 * qdd[qidx_diff(kind, NQ, e, 0, q)] +
-                    p1 * p1 * qdd[qidx_diff(kind, NQ, e, 3, q)] +
-                    p2 * p2 * qdd[qidx_diff(kind, NQ, e, 5, q)] +
-                    2.0 * (p0 * p1 * qdd[qidx_diff(kind, NQ, e, 1, q)] +
-                           p0 * p2 * qdd[qidx_diff(kind, NQ, e, 2, q)] +
-                           p1 * p2 * qdd[qidx_diff(kind, NQ, e, 4, q)]);
+               s += p0 * p0 * qdd[qidx_diff(pos, kind, NQ, e, 0, q)] +
+                    p1 * p1 * qdd[qidx_diff(pos, kind, NQ, e, 3, q)] +
+                    p2 * p2 * qdd[qidx_diff(pos, kind, NQ, e, 5, q)] +
+                    2.0 * (p0 * p1 * qdd[qidx_diff(pos, kind, NQ, e, 1, q)] +
+                           p0 * p2 * qdd[qidx_diff(pos, kind, NQ, e, 2, q)] +
+                           p1 * p2 * qdd[qidx_diff(pos, kind, NQ, e, 4, q)]);
             }
          }
    if (out_e) { diag[t] += s; }
@@ -637,7 +844,9 @@ __global__ void k_scatter_add_idx(int n, const int *__restrict__ idx, const doub
                                   double *__restrict__ y)
 {
    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-   if (i < n) { y[idx[i]] += buf[i]; }
+   // atomic: a dof shared by >= 3 ranks appears in several neighbour segments, and the
+   // interior-element kernel may still be accumulating into y concurrently
+   if (i < n) { unsafeAtomicAdd(y + idx[i], buf[i]); }
 }
 
 __global__ void k_scatter_set_idx(int n, const int *__restrict__ idx, const double *__restrict__ buf,
@@ -660,11 +869,49 @@ SetupCoef make_setup_coef(const CoeffDesc *c, const double *q)
    return s;
 }
 
+int tpe_variant()
+{
+   static int v = [] {
+      const char *e = std::getenv("ECM2_TPE_VARIANT");
+      return e ? std::atoi(e) : kDefaultTpeVariant;
+   }();
+   return v;
+}
+
+template <int D, int Q, bool MASS, bool DIFF, bool SPLIT>
+void launch_tpe_pf(int var, const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipStream_t s)
+{
+   const int nb = a.blk_end - a.blk_begin;
+   const dim3 grid((nb + 3) / 4), block(256);
+#define ECM2_PF(V)                                                                                   \
+   hipLaunchKernelGGL((k_apply_tpe_pf<D, Q, MASS, DIFF, SPLIT, V>), grid, block, 0, s, a.ne,        \
+                      a.blk_begin, a.blk_end, a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, rowtab, \
+                      a.lane_flags)
+   switch (var & 11)
+   {
+      case 0: ECM2_PF(0); break;
+      case 1: ECM2_PF(1); break;
+      case 2: ECM2_PF(2); break;
+      case 3: ECM2_PF(3); break;
+      case 8: ECM2_PF(8); break;
+      case 9: ECM2_PF(9); break;
+      default: ECM2_PF(0); break;
+   }
+#undef ECM2_PF
+}
+
 template <int D, int Q, bool MASS, bool DIFF>
 void launch_tpe_mdq(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipStream_t s)
 {
    const int nb = a.blk_end - a.blk_begin;
    if (nb <= 0) { return; }
+   const int var = tpe_variant();
+   if ((var & 4) && a.lane_flags)
+   {
+      if (a.xg || a.yg) { launch_tpe_pf<D, Q, MASS, DIFF, true>(var, a, b, rowtab, s); }
+      else { launch_tpe_pf<D, Q, MASS, DIFF, false>(var, a, b, rowtab, s); }
+      return;
+   }
    const dim3 grid((nb + 3) / 4), block(256);
    if (a.xg || a.yg)
    {
@@ -696,7 +943,7 @@ void launch_wpe_mdq(const ApplyArgs &a, bool in_e, bool out_e, const Basis1D &b,
    if (e1 <= e0) { return; }
    const dim3 grid(e1 - e0), block(nt);
 #define ECM2_WPE_LAUNCH(IE, OE)                                                                      \
-   hipLaunchKernelGGL((k_apply_wpe<D, Q, MASS, DIFF, IE, OE>), grid, block, 0, s, a.kind, a.ne, e0, \
+   hipLaunchKernelGGL((k_apply_wpe<D, Q, MASS, DIFF, IE, OE>), grid, block, 0, s, a.pos, a.kind, a.ne, e0, \
                       a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b)
    if (in_e && out_e) { ECM2_WPE_LAUNCH(true, true); }
    else if (in_e) { ECM2_WPE_LAUNCH(true, false); }
@@ -736,7 +983,7 @@ void setup_from_nodes(const QLayout &L, int Q, const double *enodes, const doubl
 {
    const long n = (long)L.ne * L.nq;
    if (n == 0) { return; }
-   hipLaunchKernelGGL(k_setup_nodes, dim3(grid_for(n, 256)), dim3(256), 0, s, L.kind, L.ne, Q,
+   hipLaunchKernelGGL(k_setup_nodes, dim3(grid_for(n, 256)), dim3(256), 0, s, L.pos, L.kind, L.ne, Q,
                       enodes, W, b1, make_setup_coef(cm, cm_q), make_setup_coef(cd, cd_q),
                       qd_diff, qd_mass);
    ECM2_HIP(hipGetLastError());
@@ -748,7 +995,7 @@ void setup_from_jacobians(const QLayout &L, const double *J, const double *W,
 {
    const long n = (long)L.ne * L.nq;
    if (n == 0) { return; }
-   hipLaunchKernelGGL(k_setup_jac, dim3(grid_for(n, 256)), dim3(256), 0, s, L.kind, L.ne, L.nq,
+   hipLaunchKernelGGL(k_setup_jac, dim3(grid_for(n, 256)), dim3(256), 0, s, L.pos, L.kind, L.ne, L.nq,
                       J, W, make_setup_coef(cm, cm_q), make_setup_coef(cd, cd_q), qd_diff,
                       qd_mass);
    ECM2_HIP(hipGetLastError());
@@ -806,12 +1053,12 @@ void restriction_mult_transpose(int ndofs, int nd, const int *offsets, const int
    ECM2_HIP(hipGetLastError());
 }
 
-void diagonal(int D, int Q, int layout, int ne, const int *gm, const double *qdd,
+void diagonal(const int *pos, int D, int Q, int layout, int ne, const int *gm, const double *qdd,
               const double *qdm, double *diag, bool out_e, const Basis1D &b, hipStream_t s)
 {
    const long n = (long)ne * D * D * D;
    if (n == 0) { return; }
-   hipLaunchKernelGGL(k_diagonal, dim3(grid_for(n, 128)), dim3(128), 0, s, D, Q, layout, ne, gm,
+   hipLaunchKernelGGL(k_diagonal, dim3(grid_for(n, 128)), dim3(128), 0, s, pos, D, Q, layout, ne, gm,
                       qdd, qdm, diag, out_e, b);
    ECM2_HIP(hipGetLastError());
 }

@@ -114,14 +114,11 @@ void ParPAForm::mult(const double *x_true, double *y_true, hipStream_t s)
       }
       ECM2_NCCL(ncclGroupEnd());
    }
-   ECM2_HIP(hipEventRecord(ev_xg_, cs_));
-   // interior elements overlap the exchange
-   phase_interior(x_true, y_true, s);
-   ECM2_HIP(hipStreamWaitEvent(s, ev_xg_, 0));
-   phase_boundary(x_true, y_true, s);
-   // P^T: ghost contributions -> owners (tag 41823), summed into the owned interface dofs
-   ECM2_HIP(hipEventRecord(ev_yg_, s));
-   ECM2_HIP(hipStreamWaitEvent(cs_, ev_yg_, 0));
+   // boundary elements (those touching ghosts) run on the comm stream as soon as the
+   // ghost values land, concurrently with the interior elements on the caller's stream;
+   // both accumulate into y with atomics
+   phase_boundary(x_true, y_true, cs_);
+   // P^T: ghost contributions -> owners (tag 41823), added into the owned interface dofs
    if (nn)
    {
       ECM2_NCCL(ncclGroupStart());
@@ -136,6 +133,8 @@ void ParPAForm::mult(const double *x_true, double *y_true, hipStream_t s)
    }
    phase_finish(y_true, cs_);
    ECM2_HIP(hipEventRecord(ev_done_, cs_));
+   // interior elements overlap the whole exchange
+   phase_interior(x_true, y_true, s);
    ECM2_HIP(hipStreamWaitEvent(s, ev_done_, 0));
 }
 

@@ -24,7 +24,8 @@ std::vector<int> partition_slabs_z(const HexMesh &m, int nranks)
    return er;
 }
 
-LocalPart build_local_part(const H1Space &s, const std::vector<int> &elem_rank, int rank, int nranks)
+LocalPart build_local_part(const H1Space &s, const std::vector<int> &elem_rank, int rank, int nranks,
+                           int nx, int ny, int nz)
 {
    ECM2_VERIFY((int)elem_rank.size() == s.ne, ERR_ARG, "elem_rank size " << elem_rank.size() << " != ne " << s.ne);
    ECM2_VERIFY(nranks >= 1 && nranks <= 64, ERR_UNSUPPORTED, "1..64 ranks supported");
@@ -94,6 +95,11 @@ LocalPart build_local_part(const H1Space &s, const std::vector<int> &elem_rank, 
          bnd = g2l[g >= 0 ? g : -1 - g] >= p.n_owned;
       }
       (bnd ? boundary : interior).push_back(e);
+   }
+   if (nx > 0)
+   {
+      interior = brick_order(interior, nx, ny, nz);
+      boundary = brick_order(boundary, nx, ny, nz);
    }
    p.ne_interior = (int)interior.size();
    p.elems = interior;

@@ -35,6 +35,9 @@ struct LocalPart
 // for a 1 x 1 x nranks grid): elem_rank[e].
 std::vector<int> partition_slabs_z(const HexMesh &m, int nranks);
 
-LocalPart build_local_part(const H1Space &s, const std::vector<int> &elem_rank, int rank, int nranks);
+// nx > 0: the global mesh is a lexicographic nx x ny x nz Cartesian mesh; interior and
+// boundary element groups are then each put in brick order (one 4x4x4 brick per wave).
+LocalPart build_local_part(const H1Space &s, const std::vector<int> &elem_rank, int rank, int nranks,
+                           int nx = 0, int ny = 0, int nz = 0);
 
 } // namespace ecm2

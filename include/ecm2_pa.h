@@ -80,6 +80,9 @@ int ecm2_mesh_quadrature_points(const ecm2_mesh *m, int q1d, double *out);
 /* Same for a subset of elements (host elems[n]), out[n][q1d^3][3]. */
 int ecm2_mesh_quadrature_points_subset(const ecm2_mesh *m, int q1d, const int *elems, int n,
                                        double *out);
+/* Element order for the fused kernel: 0 native, 1 brick (Cartesian meshes: 4x4x4 bricks
+ * first), 2 Morton order of centroids (any mesh).  perm host [ne]. */
+int ecm2_mesh_element_order(const ecm2_mesh *m, int kind, int *perm);
 void ecm2_mesh_destroy(ecm2_mesh *m);
 
 /* H1_FECollection(order) + FiniteElementSpace: element->dof table in
@@ -116,6 +119,10 @@ int ecm2_pa_form_set_jacobians(ecm2_pa_form *f, const double *J);
 int ecm2_pa_form_add_integrator(ecm2_pa_form *f, int integrator, int coeff_kind,
                                 const double *data, const double *params);
 int ecm2_pa_form_set_kernel(ecm2_pa_form *f, int kernel);
+/* Optional element permutation for the fused kernel's blocked layout (host perm[ne]:
+ * internal position i <- caller element perm[i]); see ecm2_mesh_element_order.  All
+ * entry points keep the caller's element order. */
+int ecm2_pa_form_set_element_order(ecm2_pa_form *f, const int *perm);
 /* BilinearForm::Assemble -> PABilinearFormExtension::Assemble -> AssemblePA
  * (bilinearform.cpp:456-460, bilinearform_ext.cpp:332-368). */
 int ecm2_pa_form_assemble(ecm2_pa_form *f, void *stream);
@@ -163,9 +170,10 @@ int ecm2_partition_slabs_z(const ecm2_mesh *m, int nranks, int *elem_rank);
 /* Per-rank local space of a global H1 space and an element partition (ParMesh +
  * ParFiniteElementSpace, pmesh.hpp:33, pfespace.cpp:1389-1418): local L-vector
  * [owned | ghost], owner = lowest touching rank, local elements [interior | boundary],
- * neighbour exchange lists in the DeviceConformingProlongationOperator sense. */
-int ecm2_partition_create(const ecm2_h1space *s, const int *elem_rank, int rank, int nranks,
-                          ecm2_partition **out);
+ * neighbour exchange lists in the DeviceConformingProlongationOperator sense.  m (may be
+ * NULL): when it is a Cartesian mesh the local element groups are put in brick order. */
+int ecm2_partition_create(const ecm2_h1space *s, const ecm2_mesh *m, const int *elem_rank, int rank,
+                          int nranks, ecm2_partition **out);
 int ecm2_partition_info(const ecm2_partition *p, int *ne_local, int *ne_interior, int *n_owned,
                         int *n_ghost, int *n_nbrs, int *n_send);
 /* Any output may be NULL. elems [ne_local] (global ids, local order), local_to_global

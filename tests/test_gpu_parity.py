@@ -43,6 +43,9 @@ def make_mesh(name):
         m.UniformRefinement()                          # 56 elements
     elif name == "inline_hex":
         m = E.Mesh(f"{GOLDEN}/inline-hex.mesh")        # 64 elements
+    elif name == "cart_bricks":
+        m = E.Mesh.MakeCartesian3D(8, 8, 5, 1.0, 0.8, 0.6)   # 4 complete 4x4x4 bricks + leftovers
+        m.set_vertices(nonaligned(m.vertices()))
     elif name == "cart_130":
         m = E.Mesh.MakeCartesian3D(13, 5, 2, 2.0, 1.0, 0.5)  # 130 elements: 3 blocks, ragged
     else:
@@ -50,7 +53,8 @@ def make_mesh(name):
     return m
 
 
-def build_pair(mesh, order, alpha, beta, kernel=E.KERNEL_AUTO, numbering=E.NUMBERING_ENTITY):
+def build_pair(mesh, order, alpha, beta, kernel=E.KERNEL_AUTO, numbering=E.NUMBERING_ENTITY,
+               element_order="auto"):
     """Product form + oracle operator on the same mesh; alpha/beta: 'fn', 'bio', float or None."""
     fes = E.H1Space(mesh, order, numbering)
     en = mesh.element_nodes()
@@ -72,7 +76,7 @@ def build_pair(mesh, order, alpha, beta, kernel=E.KERNEL_AUTO, numbering=E.NUMBE
 
     a_np, a_c = coeff(alpha)
     b_np, b_c = coeff(beta)
-    form = E.BilinearForm(fes, kernel=kernel)
+    form = E.BilinearForm(fes, kernel=kernel, element_order=element_order)
     if a_c is not None:
         form.AddDomainIntegrator(E.MassIntegrator(a_c))
     if b_c is not None:
@@ -85,7 +89,7 @@ def build_pair(mesh, order, alpha, beta, kernel=E.KERNEL_AUTO, numbering=E.NUMBE
 KERNELS = {"tpe": E.KERNEL_TPE, "wpe": E.KERNEL_WPE, "unfused": E.KERNEL_UNFUSED}
 
 
-@pytest.mark.parametrize("mesh_name", ["nonaligned", "fichera_r1", "inline_hex", "cart_130"])
+@pytest.mark.parametrize("mesh_name", ["nonaligned", "fichera_r1", "inline_hex", "cart_130", "cart_bricks"])
 @pytest.mark.parametrize("order", [1, 2, 3, 4])
 @pytest.mark.parametrize("kernel", ["tpe", "wpe", "unfused"])
 def test_mult_matches_oracle(mesh_name, order, kernel):
@@ -303,3 +307,21 @@ def test_full_size_c4_tpe():
     y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
     form.Mult(dev(x), y)
     assert relerr(host(y), op.mult(x)) <= RTOL
+
+
+@pytest.mark.parametrize("element_order", ["native", "brick", "morton"])
+@pytest.mark.parametrize("order", [1, 2])
+def test_element_orders_same_operator(element_order, order):
+    """The blocked layout's element permutation and in-wave face assembly are invisible:
+    every order gives the oracle's y (cart_bricks has complete bricks and leftovers)."""
+    m = make_mesh("cart_bricks")
+    fes, form, op = build_pair(m, order, "fn", "fn", element_order=element_order)
+    x = np.random.default_rng(31).uniform(-1, 1, fes.ndofs)
+    y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    form.Mult(dev(x), y)
+    assert relerr(host(y), op.mult(x)) <= RTOL
+    qd = form.qdata(E.DIFFUSION)
+    assert relerr(qd, op.D) < 1e-13
+    d = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    form.AssembleDiagonal(d)
+    assert relerr(host(d), op.diagonal()) < 1e-13

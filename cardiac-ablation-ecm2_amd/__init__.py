@@ -35,6 +35,8 @@ COEFF_CONSTANT, COEFF_QUAD, COEFF_GRIDFUNC_AFFINE = 0, 1, 2
 KERNEL_AUTO, KERNEL_TPE, KERNEL_WPE, KERNEL_UNFUSED = 0, 1, 2, 3
 NUMBERING_ENTITY, NUMBERING_STRUCTURED = 0, 1
 ORDER_NATIVE, ORDER_BRICK, ORDER_MORTON = 0, 1, 2
+SCATTER_PARTIALS, SCATTER_ATOMIC = 0, 1
+_SCATTER = {"partials": SCATTER_PARTIALS, "atomic": SCATTER_ATOMIC}
 
 
 class ECM2Error(RuntimeError):
@@ -83,6 +85,8 @@ def load_library(path: str = LIB_PATH):
         "ecm2_pa_form_set_jacobians": (i32, [vp, vp]),
         "ecm2_pa_form_add_integrator": (i32, [vp, i32, i32, vp, vp]),
         "ecm2_pa_form_set_kernel": (i32, [vp, i32]),
+        "ecm2_pa_form_set_scatter": (i32, [vp, i32]),
+        "ecm2_pa_form_scatter_info": (i32, [vp, vp, vp]),
         "ecm2_pa_form_set_element_order": (i32, [vp, vp]),
         "ecm2_mesh_element_order": (i32, [vp, i32, vp]),
         "ecm2_pa_form_assemble": (i32, [vp, vp]),
@@ -306,7 +310,7 @@ class BilinearForm:
     """BilinearForm at AssemblyLevel::PARTIAL backed by the HIP PA form."""
 
     def __init__(self, fes: H1Space, kernel: int = KERNEL_AUTO, q1d: int = 0, geometry: str = "nodes",
-                 element_order: str = "auto"):
+                 element_order: str = "auto", scatter: str = "partials"):
         self.fes = fes
         self._integs = []
         self._kernel = kernel
@@ -319,6 +323,7 @@ class BilinearForm:
             en = fes.mesh.element_nodes()
             _check(_lib.ecm2_pa_form_set_element_nodes(h, _np_ptr(en)))
         _check(_lib.ecm2_pa_form_set_kernel(h, kernel))
+        _check(_lib.ecm2_pa_form_set_scatter(h, _SCATTER[scatter]))
         if element_order != "native" and fes.ne > 0:
             if element_order in ("auto", "brick"):
                 try:
@@ -363,6 +368,12 @@ class BilinearForm:
 
     def Assemble(self, stream=None):
         _check(_lib.ecm2_pa_form_assemble(self._h, _stream(stream)))
+
+    def ScatterInfo(self):
+        """(shared dofs, partial slots) of the fused kernel's deterministic scatter."""
+        n, m = ctypes.c_int(), ctypes.c_long()
+        _check(_lib.ecm2_pa_form_scatter_info(self._h, ctypes.byref(n), ctypes.byref(m)))
+        return n.value, m.value
 
     def Mult(self, x, y, stream=None):
         _check(_lib.ecm2_pa_form_mult(self._h, _dev_ptr(x), _dev_ptr(y), _stream(stream)))
@@ -431,6 +442,7 @@ _PAR_SIGS = {
     "ecm2_par_form_add_integrator": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                                     ctypes.c_void_p]),
     "ecm2_par_form_set_kernel": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "ecm2_par_form_set_scatter": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ecm2_par_form_assemble": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "ecm2_par_form_mult": (ctypes.c_int, [ctypes.c_void_p] * 4),
     "ecm2_par_group_mult": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
@@ -517,7 +529,8 @@ class ParBilinearForm:
     """ParBilinearForm(PARTIAL): y_true = P^T A_local P x_true.  rccl_id=None -> loopback
     group member (use ParGroup.Mult); otherwise one process per GPU over RCCL."""
 
-    def __init__(self, part: Partition, rccl_id: Optional[bytes] = None, kernel: int = KERNEL_AUTO, q1d: int = 0):
+    def __init__(self, part: Partition, rccl_id: Optional[bytes] = None, kernel: int = KERNEL_AUTO, q1d: int = 0,
+                 scatter: str = "partials"):
         lib = _par_lib()
         self.part = part
         self._keep = []
@@ -532,6 +545,7 @@ class ParBilinearForm:
                                         ctypes.byref(h)))
         self._h = h
         _check(lib.ecm2_par_form_set_kernel(h, kernel))
+        _check(lib.ecm2_par_form_set_scatter(h, _SCATTER[scatter]))
         self.true_size = part.n_owned
 
     def __del__(self):

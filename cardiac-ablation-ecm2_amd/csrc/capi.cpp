@@ -307,6 +307,20 @@ int ecm2_pa_form_set_kernel(ecm2_pa_form *f, int kernel)
    return guard([&] { NEED(f); f->f->set_kernel(kernel); });
 }
 
+int ecm2_pa_form_set_scatter(ecm2_pa_form *f, int mode)
+{
+   return guard([&] { NEED(f); f->f->set_scatter(mode); });
+}
+
+int ecm2_pa_form_scatter_info(const ecm2_pa_form *f, int *n_shared, long *n_slots)
+{
+   return guard([&] {
+      NEED(f);
+      if (n_shared) { *n_shared = f->f->n_shared(); }
+      if (n_slots) { *n_slots = f->f->n_partial_slots(); }
+   });
+}
+
 int ecm2_pa_form_assemble(ecm2_pa_form *f, void *stream)
 {
    return guard([&] { NEED(f); f->f->assemble(S(stream)); });
@@ -483,6 +497,11 @@ int ecm2_par_form_add_integrator(ecm2_par_form *f, int integrator, int coeff_kin
       }
       f->f->local().add_integrator(integrator, c);
    });
+}
+
+int ecm2_par_form_set_scatter(ecm2_par_form *f, int mode)
+{
+   return guard([&] { NEED(f); f->f->local().set_scatter(mode); });
 }
 
 int ecm2_par_form_set_kernel(ecm2_par_form *f, int kernel)

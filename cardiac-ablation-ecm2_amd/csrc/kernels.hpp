@@ -3,7 +3,8 @@
 // Quadrature-data layouts (the qdata a PA form owns):
 //  * BLOCKED (fused thread-per-element kernel): elements in blocks of 64 (one
 //    wave; lane = element).  The blocked element->dof map packs bit 30 = "shared dof"
-//    (atomic add after in-wave assembly) and bit 31 = orientation sign.
+//    (held by more than one entry after in-wave assembly: written to its partial slot,
+//    or atomically added) and bit 31 = orientation sign.
 //    diffusion qdata: [blk][q][pair 0..2][lane][2] holding the
 //    symmetric entries (11,12),(13,22),(23,33); mass: [blk][q/2][lane][2] (two
 //    consecutive quadrature points per 16-byte slot).  Every wave-instruction
@@ -68,6 +69,7 @@ struct ApplyArgs
    const double *qdd = nullptr, *qdm = nullptr;
    const double *x = nullptr, *xg = nullptr;
    double *y = nullptr, *yg = nullptr;
+   double *part = nullptr;          // [blk][nd][64] partial slots of shared dofs (null: atomics)
 };
 
 namespace kern
@@ -127,6 +129,10 @@ void reciprocal(int n, const double *a, double *out, hipStream_t s);
 // Halo pack/unpack for the distributed operator (K7): buf[i] = x[idx[i]] ; y[idx[i]] += buf[i]
 void gather_idx(int n, const int *idx, const double *x, double *buf, hipStream_t s);
 void scatter_add_idx(int n, const int *idx, const double *buf, double *y, hipStream_t s);
+// Deterministic second scatter pass: y[dofs[i]] = sum_j part[slots[j]], j in
+// [start, start + count), meta[i] = start << 5 | count.
+void sum_partials(int i0, int i1, const int *dofs, const unsigned *meta, const int *slots, const double *part,
+                  int n_owned, double *y, double *yg, hipStream_t s);
 void scatter_set_idx(int n, const int *idx, const double *buf, double *y, hipStream_t s);
 } // namespace kern
 

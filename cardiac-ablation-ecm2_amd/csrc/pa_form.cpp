@@ -108,16 +108,16 @@ namespace
 // low face (index 0 along the direction) into its high face (index D-1) when all
 // face dofs coincide and no nonzero value could land in an entry that no longer
 // holds its dof; the partner then zeroes that face.  After the three passes the
-// "holding" entries carry each dof's in-wave sum; a dof held once in the whole mesh
-// is plain-stored, otherwise atomically added.
+// "holding" entries (holds[(b*64+l)*ND+a]) carry each dof's in-wave sum, and
+// hcount[d] counts the holders of dof d in the whole mesh: a dof held once is
+// plain-stored, otherwise it is "shared" (partial slot or atomic add).
 void build_merge_plan(int ne, int D, const std::vector<int> &gmap_int, int ndofs,
-                      std::vector<char> &shared, std::vector<int> &flags)
+                      std::vector<char> &holds, std::vector<int> &hcount, std::vector<int> &flags)
 {
    const int ND = D * D * D, nblk = (ne + 63) / 64;
-   shared.assign((size_t)ne * ND, 0);
    flags.assign((size_t)nblk * 64, 0);
-   std::vector<char> holds((size_t)nblk * 64 * ND, 0);
-   std::vector<int> hcount(ndofs, 0);
+   holds.assign((size_t)nblk * 64 * ND, 0);
+   hcount.assign(ndofs, 0);
    auto dofv = [](int g) { return g >= 0 ? g : -1 - g; };
    auto face = [D](int dir, int s, int i, int j) {
       if (dir == 0) { return (j * D + i) * D + s; }
@@ -159,16 +159,6 @@ void build_merge_plan(int ne, int D, const std::vector<int> &gmap_int, int ndofs
       for (int l = 0; l < 64; l++)
          for (int a = 0; a < ND; a++) { if (H(l, a)) { hcount[dof(l, a)]++; } }
    }
-   for (int b = 0; b < nblk; b++)
-      for (int l = 0; l < 64; l++)
-      {
-         if (b * 64 + l >= ne) { continue; }
-         for (int a = 0; a < ND; a++)
-         {
-            const int d = dofv(gmap_int[((size_t)b * 64 + l) * ND + a]);
-            shared[((size_t)b * 64 + l) * ND + a] = hcount[d] > 1;
-         }
-      }
 }
 } // namespace
 
@@ -201,9 +191,10 @@ void PAForm::assemble(hipStream_t s)
          std::copy(&gmap_host_[(size_t)e * ND_], &gmap_host_[(size_t)e * ND_] + ND_, &gint[(size_t)i * ND_]);
       }
       ECM2_VERIFY(ndofs_ < (1 << 30), ERR_UNSUPPORTED, "fused kernel supports < 2^30 dofs");
-      std::vector<char> shared;
-      std::vector<int> fl;
-      build_merge_plan(ne_, D_, gint, ndofs_, shared, fl);
+      ECM2_VERIFY((size_t)nblk * ND_ * 64 < (1ull << 31), ERR_UNSUPPORTED, "too many elements for int slots");
+      std::vector<char> holds;
+      std::vector<int> fl, hcount;
+      build_merge_plan(ne_, D_, gint, ndofs_, holds, hcount, fl);
       // blocked map: dof | shared << 30 | sign << 31
       std::vector<int> blk((size_t)nblk * ND_ * 64, 0);
       for (int i = 0; i < ne_; i++)
@@ -213,9 +204,52 @@ void PAForm::assemble(hipStream_t s)
          {
             const int g = gint[(size_t)i * ND_ + a];
             const unsigned d = (unsigned)(g >= 0 ? g : -1 - g);
-            const unsigned enc = d | ((unsigned)shared[(size_t)i * ND_ + a] << 30) | ((g < 0 ? 1u : 0u) << 31);
+            const unsigned enc = d | ((hcount[d] > 1 ? 1u : 0u) << 30) | ((g < 0 ? 1u : 0u) << 31);
             blk[((size_t)b * ND_ + a) * 64 + l] = (int)enc;
          }
+      }
+      // Second-pass plan of the deterministic scatter: every dof not held exactly once
+      // with its partial slots (b*ND + a)*64 + l in ascending order.  Dofs held by
+      // nobody get an empty list (y = 0).  The owned dofs come first, then the ghosts
+      // (split form); within each range the list is ordered by first slot, so neighbouring
+      // threads of k_sum_partials read neighbouring lanes of the partial buffer.
+      {
+         std::vector<int> start(ndofs_ + 1, 0);
+         for (int d = 0; d < ndofs_; d++) { start[d + 1] = start[d] + (hcount[d] > 1 ? hcount[d] : 0); }
+         std::vector<int> slots_by_dof(start[ndofs_]), fill(start.begin(), start.end() - 1);
+         for (int b = 0; b < nblk; b++)
+            for (int a = 0; a < ND_; a++)
+               for (int l = 0; l < 64; l++)
+               {
+                  if (!holds[((size_t)b * 64 + l) * ND_ + a]) { continue; }
+                  const int d = blk[((size_t)b * ND_ + a) * 64 + l] & 0x3fffffff;
+                  if (hcount[d] > 1) { slots_by_dof[fill[d]++] = (b * ND_ + a) * 64 + l; }
+               }
+         std::vector<int> dofs;
+         for (int d = 0; d < ndofs_; d++) { if (hcount[d] != 1) { dofs.push_back(d); } }
+         auto key = [&](int d) -> long {
+            const long first = hcount[d] > 1 ? slots_by_dof[start[d]] : -1;
+            return (d < n_owned_ ? 0 : (1l << 40)) + first;
+         };
+         std::stable_sort(dofs.begin(), dofs.end(), [&](int p, int q) { return key(p) < key(q); });
+         std::vector<unsigned> meta;
+         std::vector<int> slots;
+         slots.reserve(slots_by_dof.size());
+         ECM2_VERIFY(slots_by_dof.size() < (1ull << 27), ERR_UNSUPPORTED, "too many partial slots");
+         for (int d : dofs)
+         {
+            const unsigned cnt = (unsigned)(start[d + 1] - start[d]);
+            ECM2_VERIFY(cnt < 32, ERR_UNSUPPORTED, "dof " << d << " held by " << cnt << " element entries");
+            meta.push_back((unsigned)slots.size() << 5 | cnt);
+            slots.insert(slots.end(), slots_by_dof.begin() + start[d], slots_by_dof.begin() + start[d + 1]);
+         }
+         n_sh_ = (int)dofs.size();
+         n_sh_owned_ = 0;
+         while (n_sh_owned_ < n_sh_ && dofs[n_sh_owned_] < n_owned_) { n_sh_owned_++; }
+         n_slots_ = (long)slots.size();
+         sh_dofs_.upload(dofs, s);
+         sh_meta_.upload(meta, s);
+         sh_slots_.upload(slots, s);
       }
       gmap_blk_.upload(blk, s);
       lane_flags_.upload(fl, s);
@@ -224,6 +258,7 @@ void PAForm::assemble(hipStream_t s)
       ECM2_HIP(hipStreamSynchronize(s));
    }
    layout_.pos = (layout_.kind == QLAYOUT_BLOCKED) ? pos_.data() : nullptr;
+   part_.resize(use_partials() ? (size_t)layout_.nblk() * ND_ * 64 : 0);
    qd_diff_.resize(have_diff_ ? layout_.diff_size() : 0);
    qd_mass_.resize(have_mass_ ? layout_.mass_size() : 0);
    if (qd_diff_.size()) { ECM2_HIP(hipMemsetAsync(qd_diff_.data(), 0, qd_diff_.bytes(), s)); }
@@ -352,11 +387,39 @@ void PAForm::mult(const double *x, double *y, hipStream_t s)
       record_stop(s);
       return;
    }
+   if (!m && !d)
+   {
+      ECM2_HIP(hipMemsetAsync(y, 0, sizeof(double) * (size_t)ndofs_, s));
+      return;
+   }
+   if (use_partials())
+   {
+      // exclusive dofs are plain-stored, shared ones summed from their partial slots:
+      // every y entry is written exactly once, no memset, bitwise reproducible
+      record_start(s);
+      apply_blocks(x, nullptr, y, nullptr, 0, layout_.nblk(), s);
+      record_stop(s);
+      finish_shared(0, n_sh_, y, nullptr, s);
+      return;
+   }
    ECM2_HIP(hipMemsetAsync(y, 0, sizeof(double) * (size_t)ndofs_, s));
-   if (!m && !d) { return; }
    record_start(s);
    apply_blocks(x, nullptr, y, nullptr, 0, layout_.nblk(), s);
    record_stop(s);
+}
+
+void PAForm::set_scatter(int mode)
+{
+   ECM2_VERIFY(mode == SCATTER_PARTIALS || mode == SCATTER_ATOMIC, ERR_ARG, "unknown scatter mode " << mode);
+   scatter_ = mode;
+   assembled_ = false;
+}
+
+void PAForm::finish_shared(int i0, int i1, double *y, double *yg, hipStream_t s)
+{
+   if (!use_partials()) { return; }
+   kern::sum_partials(i0, i1, sh_dofs_.data(), sh_meta_.data(), sh_slots_.data(), part_.data(), n_owned_, y,
+                      yg, s);
 }
 
 ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, double *yg, int b0,
@@ -374,6 +437,7 @@ ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, doubl
    a.qdd = qd_diff_.data();
    a.qdm = qd_mass_.data();
    a.x = x; a.xg = xg; a.y = y; a.yg = yg;
+   a.part = use_partials() ? const_cast<double *>(part_.data()) : nullptr;  // form-owned scratch
    return a;
 }
 

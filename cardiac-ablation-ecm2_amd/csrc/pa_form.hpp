@@ -31,6 +31,14 @@ enum KernelMode : int
    KERNEL_UNFUSED = 3   // reference-shaped: restriction, per-integrator AddMultPA, CSR transpose
 };
 
+// How the fused TPE kernel combines contributions to dofs held by more than one element
+// entry (after in-wave face assembly):
+enum ScatterMode : int
+{
+   SCATTER_PARTIALS = 0,  // dense partial slots + a fixed-order summation pass (deterministic)
+   SCATTER_ATOMIC = 1     // FP64 atomic adds into a zeroed y
+};
+
 enum IntegratorKind : int { INTEG_MASS = 0, INTEG_DIFFUSION = 1 };
 
 class PAForm
@@ -61,14 +69,24 @@ public:
    void set_element_order(const int *perm_host);
    void add_integrator(int kind, const CoeffDesc &c);
    void set_kernel(int mode);
+   void set_scatter(int mode);
+   int scatter() const { return scatter_; }
+   bool use_partials() const { return resolved_mode_ == KERNEL_TPE && scatter_ == SCATTER_PARTIALS; }
    void assemble(hipStream_t s);
 
    // y = A x (BilinearForm::Mult semantics: y overwritten).
    void mult(const double *x, double *y, hipStream_t s);
-   // Accumulate the fused apply of element blocks [b0, b1) (64 elements per block) into
-   // zero-initialised y / yg (atomics); x / xg as in the constructor's split.
+   // Fused apply of element blocks [b0, b1) (64 elements per block); x / xg as in the
+   // constructor's split.  Atomic scatter: accumulates into zero-initialised y / yg.
+   // Partial scatter: stores the dofs held once, writes the shared ones' partial slots;
+   // finish_shared over the shared-dof range [i0, i1) then stores those (the owned
+   // shared dofs are [0, n_shared_owned()), the ghost ones [n_shared_owned(), n_shared())).
    void apply_blocks(const double *x, const double *xg, double *y, double *yg, int b0, int b1,
                      hipStream_t s);
+   void finish_shared(int i0, int i1, double *y, double *yg, hipStream_t s);
+   int n_shared() const { return n_sh_; }
+   int n_shared_owned() const { return n_sh_owned_; }
+   long n_partial_slots() const { return n_slots_; }
    int nblocks() const { return layout_.nblk(); }
    bool has_mass() const { return have_mass_; }
    bool has_diffusion() const { return have_diff_; }
@@ -104,6 +122,12 @@ private:
    Basis1D basis_, basis1_;
    QLayout layout_;
    int mode_ = KERNEL_AUTO, resolved_mode_ = KERNEL_AUTO;
+   int scatter_ = SCATTER_PARTIALS;
+   int n_sh_ = 0, n_sh_owned_ = 0;
+   long n_slots_ = 0;
+   DeviceArray<int> sh_dofs_, sh_slots_;           // second-pass plan (see finish_shared)
+   DeviceArray<unsigned> sh_meta_;                 // start << 5 | count
+   DeviceArray<double> part_;                       // [blk][nd][64] partial slots
    bool assembled_ = false;
    bool have_mass_ = false, have_diff_ = false;
    CoeffDesc cmass_, cdiff_;

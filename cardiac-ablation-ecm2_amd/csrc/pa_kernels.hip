@@ -358,7 +358,8 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                const double *__restrict__ qdd, const double *__restrict__ qdm,
                const double *__restrict__ x, const double *__restrict__ xg,
                double *__restrict__ y, double *__restrict__ yg, const Basis1D b,
-               const double *__restrict__ rowtab, const int *__restrict__ lane_flags)
+               const double *__restrict__ rowtab, const int *__restrict__ lane_flags,
+               double *__restrict__ part)
 {
    constexpr int ND = D * D * D, NQ = Q * Q * Q, NQH = (NQ + 1) / 2, DD = D * D;
    constexpr int NR = Q * Q;  // rows
@@ -521,7 +522,9 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
    merge(4, 4, 8, [](int s, int i, int j) { return (j * D + s) * D + i; });    // y: (dz=j, dx=i)
    merge(16, 16, 32, [](int s, int i, int j) { return (s * D + j) * D + i; }); // z: (dy=j, dx=i)
    // ---- output: entries whose face was sent away hold nothing; a dof held once in the
-   // whole mesh is plain-stored, a shared one atomically added
+   // whole mesh is plain-stored; a shared one goes to its dense partial slot
+   // [blk][a][lane] (summed in a fixed order by k_sum_partials: deterministic, no
+   // atomics, no y memset) or, without a partial buffer, is atomically added
    if (active)
    {
       const bool sx = fl & 2, sy = fl & 8, sz = fl & 32;
@@ -538,6 +541,7 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                const int d = bdof(g);
                double *dst = (!SPLIT || d < n_owned) ? y + d : yg + (d - n_owned);
                if (!bshared(g) || (VAR & 1)) { *dst = Yo[a]; }
+               else if (part) { part[((size_t)blk * ND + a) * 64 + lane] = Yo[a]; }
                else { unsafeAtomicAdd(dst, Yo[a]); }
             }
    }
@@ -844,8 +848,7 @@ __global__ void k_scatter_add_idx(int n, const int *__restrict__ idx, const doub
                                   double *__restrict__ y)
 {
    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-   // atomic: a dof shared by >= 3 ranks appears in several neighbour segments, and the
-   // interior-element kernel may still be accumulating into y concurrently
+   // atomic: a dof shared by >= 3 ranks appears in several neighbour segments
    if (i < n) { unsafeAtomicAdd(y + idx[i], buf[i]); }
 }
 
@@ -854,6 +857,35 @@ __global__ void k_scatter_set_idx(int n, const int *__restrict__ idx, const doub
 {
    const int i = blockIdx.x * blockDim.x + threadIdx.x;
    if (i < n) { y[idx[i]] = buf[i]; }
+}
+
+// Second pass of the deterministic scatter: y[dofs[i]] = sum of the partial slots
+// slots[start .. start+count) in ascending slot order, for i in [i0, i1), with
+// meta[i] = start << 5 | count.  All slot loads, then all partial loads, are issued
+// independently (count <= 8 unrolled; more -- unstructured meshes -- loops), so a
+// thread waits ~3 memory latencies instead of 2 + 2*count.  The list is ordered by
+// first slot (pa_form.cpp), so neighbouring threads read neighbouring lanes.
+__global__ void k_sum_partials(int i0, int i1, const int *__restrict__ dofs, const unsigned *__restrict__ meta,
+                               const int *__restrict__ slots, const double *__restrict__ part, int n_owned,
+                               double *__restrict__ y, double *__restrict__ yg)
+{
+   const int i = i0 + blockIdx.x * blockDim.x + threadIdx.x;
+   if (i >= i1) { return; }
+   const unsigned m = meta[i];
+   const int d = dofs[i];
+   const int start = (int)(m >> 5), cnt = (int)(m & 31);
+   int sl[8];
+#pragma unroll
+   for (int k = 0; k < 8; k++) { sl[k] = k < cnt ? slots[start + k] : -1; }
+   double v[8];
+#pragma unroll
+   for (int k = 0; k < 8; k++) { v[k] = sl[k] >= 0 ? part[sl[k]] : 0.0; }
+   double acc = 0.0;
+#pragma unroll
+   for (int k = 0; k < 8; k++) { acc += v[k]; }
+   for (int k = 8; k < cnt; k++) { acc += part[slots[start + k]]; }
+   if (d < n_owned) { y[d] = acc; }
+   else { yg[d - n_owned] = acc; }
 }
 
 inline unsigned grid_for(long n, int bs) { return (unsigned)((n + bs - 1) / bs); }
@@ -886,7 +918,7 @@ void launch_tpe_pf(int var, const ApplyArgs &a, const Basis1D &b, const double *
 #define ECM2_PF(V)                                                                                   \
    hipLaunchKernelGGL((k_apply_tpe_pf<D, Q, MASS, DIFF, SPLIT, V>), grid, block, 0, s, a.ne,        \
                       a.blk_begin, a.blk_end, a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, rowtab, \
-                      a.lane_flags)
+                      a.lane_flags, a.part)
    switch (var & 11)
    {
       case 0: ECM2_PF(0); break;
@@ -906,7 +938,8 @@ void launch_tpe_mdq(const ApplyArgs &a, const Basis1D &b, const double *rowtab, 
    const int nb = a.blk_end - a.blk_begin;
    if (nb <= 0) { return; }
    const int var = tpe_variant();
-   if ((var & 4) && a.lane_flags)
+   ECM2_VERIFY(!a.part || a.lane_flags, ERR_INTERNAL, "partial-slot output needs the merge plan");
+   if (((var & 4) || a.part) && a.lane_flags)
    {
       if (a.xg || a.yg) { launch_tpe_pf<D, Q, MASS, DIFF, true>(var, a, b, rowtab, s); }
       else { launch_tpe_pf<D, Q, MASS, DIFF, false>(var, a, b, rowtab, s); }
@@ -1122,6 +1155,15 @@ void scatter_add_idx(int n, const int *idx, const double *buf, double *y, hipStr
 {
    if (n == 0) { return; }
    hipLaunchKernelGGL(k_scatter_add_idx, dim3(grid_for(n, 256)), dim3(256), 0, s, n, idx, buf, y);
+   ECM2_HIP(hipGetLastError());
+}
+
+void sum_partials(int i0, int i1, const int *dofs, const unsigned *meta, const int *slots, const double *part,
+                  int n_owned, double *y, double *yg, hipStream_t s)
+{
+   if (i1 <= i0) { return; }
+   hipLaunchKernelGGL(k_sum_partials, dim3(grid_for(i1 - i0, 256)), dim3(256), 0, s, i0, i1, dofs, meta,
+                      slots, part, n_owned, y, yg);
    ECM2_HIP(hipGetLastError());
 }
 

@@ -67,8 +67,11 @@ void ParPAForm::assemble(hipStream_t s) { local_->assemble(s); }
 
 void ParPAForm::phase_pack(const double *x_true, double *y_true, hipStream_t s)
 {
-   if (part_.n_owned) { ECM2_HIP(hipMemsetAsync(y_true, 0, sizeof(double) * part_.n_owned, s)); }
-   if (part_.n_ghost) { ECM2_HIP(hipMemsetAsync(yg_.data(), 0, sizeof(double) * part_.n_ghost, s)); }
+   if (!local_->use_partials())
+   {
+      if (part_.n_owned) { ECM2_HIP(hipMemsetAsync(y_true, 0, sizeof(double) * part_.n_owned, s)); }
+      if (part_.n_ghost) { ECM2_HIP(hipMemsetAsync(yg_.data(), 0, sizeof(double) * part_.n_ghost, s)); }
+   }
    kern::gather_idx((int)part_.send_idx.size(), send_idx_.data(), x_true, sendbuf_.data(), s);
 }
 
@@ -86,6 +89,12 @@ void ParPAForm::phase_boundary(const double *x_true, double *y_true, hipStream_t
    local_->record_start_public(s);
    local_->apply_blocks(x_true, xg_.data(), y_true, yg_.data(), b_int, local_->nblocks(), s);
    local_->record_stop_public(s);
+   local_->finish_shared(local_->n_shared_owned(), local_->n_shared(), y_true, yg_.data(), s);
+}
+
+void ParPAForm::phase_owned_shared(double *y_true, hipStream_t s)
+{
+   local_->finish_shared(0, local_->n_shared_owned(), y_true, yg_.data(), s);
 }
 
 void ParPAForm::phase_finish(double *y_true, hipStream_t s)
@@ -115,10 +124,10 @@ void ParPAForm::mult(const double *x_true, double *y_true, hipStream_t s)
       ECM2_NCCL(ncclGroupEnd());
    }
    // boundary elements (those touching ghosts) run on the comm stream as soon as the
-   // ghost values land, concurrently with the interior elements on the caller's stream;
-   // both accumulate into y with atomics
+   // ghost values land, concurrently with the interior elements on the caller's stream
    phase_boundary(x_true, y_true, cs_);
-   // P^T: ghost contributions -> owners (tag 41823), added into the owned interface dofs
+   ECM2_HIP(hipEventRecord(ev_yg_, cs_));
+   // P^T: ghost contributions -> owners (tag 41823)
    if (nn)
    {
       ECM2_NCCL(ncclGroupStart());
@@ -131,11 +140,14 @@ void ParPAForm::mult(const double *x_true, double *y_true, hipStream_t s)
       }
       ECM2_NCCL(ncclGroupEnd());
    }
-   phase_finish(y_true, cs_);
    ECM2_HIP(hipEventRecord(ev_done_, cs_));
-   // interior elements overlap the whole exchange
+   // interior elements overlap the whole exchange; the owned shared dofs need both
+   // element phases, the received contributions are added last
    phase_interior(x_true, y_true, s);
+   ECM2_HIP(hipStreamWaitEvent(s, ev_yg_, 0));
+   phase_owned_shared(y_true, s);
    ECM2_HIP(hipStreamWaitEvent(s, ev_done_, 0));
+   phase_finish(y_true, s);
 }
 
 void par_group_mult(std::vector<ParPAForm *> &forms, const std::vector<const double *> &x,
@@ -177,6 +189,7 @@ void par_group_mult(std::vector<ParPAForm *> &forms, const std::vector<const dou
    {
       forms[r]->phase_interior(x[r], y[r], s);
       forms[r]->phase_boundary(x[r], y[r], s);
+      forms[r]->phase_owned_shared(y[r], s);
    }
    // P^T: copy each ghost block into the owner's receive buffer, then add
    for (int r = 0; r < n; r++)

@@ -42,7 +42,11 @@ public:
    // Phases (used by mult and by the loopback group).
    void phase_pack(const double *x_true, double *y_true, hipStream_t s);
    void phase_interior(const double *x_true, double *y_true, hipStream_t s);
+   // boundary elements, then (partial scatter) the ghost shared dofs, which only
+   // boundary elements touch
    void phase_boundary(const double *x_true, double *y_true, hipStream_t s);
+   // owned shared dofs (partial scatter); after both element phases
+   void phase_owned_shared(double *y_true, hipStream_t s);
    void phase_finish(double *y_true, hipStream_t s);
 
    // buffers (device)

@@ -119,6 +119,16 @@ int ecm2_pa_form_set_jacobians(ecm2_pa_form *f, const double *J);
 int ecm2_pa_form_add_integrator(ecm2_pa_form *f, int integrator, int coeff_kind,
                                 const double *data, const double *params);
 int ecm2_pa_form_set_kernel(ecm2_pa_form *f, int kernel);
+/* Scatter of the fused thread-per-element kernel (no reference counterpart: the
+ * reference's ElementRestriction::MultTranspose, restriction.cpp:146-186, is the
+ * deterministic CSR sum this replaces).  ECM2_SCATTER_PARTIALS (default): dofs held by
+ * one element entry are stored directly, shared ones summed from per-entry partial
+ * slots in a fixed order -- bitwise reproducible; ECM2_SCATTER_ATOMIC: FP64 atomics. */
+#define ECM2_SCATTER_PARTIALS 0
+#define ECM2_SCATTER_ATOMIC 1
+int ecm2_pa_form_set_scatter(ecm2_pa_form *f, int mode);
+/* Scatter statistics after assemble: shared dofs and their partial slots. */
+int ecm2_pa_form_scatter_info(const ecm2_pa_form *f, int *n_shared, long *n_slots);
 /* Optional element permutation for the fused kernel's blocked layout (host perm[ne]:
  * internal position i <- caller element perm[i]); see ecm2_mesh_element_order.  All
  * entry points keep the caller's element order. */
@@ -195,6 +205,8 @@ int ecm2_par_form_create(const ecm2_partition *p, const double *enodes_local, in
 int ecm2_par_form_add_integrator(ecm2_par_form *f, int integrator, int coeff_kind,
                                  const double *data, const double *params);
 int ecm2_par_form_set_kernel(ecm2_par_form *f, int kernel);
+/* Scatter mode of the local form (ECM2_SCATTER_*; see ecm2_pa_form_set_scatter). */
+int ecm2_par_form_set_scatter(ecm2_par_form *f, int mode);
 int ecm2_par_form_assemble(ecm2_par_form *f, void *stream);
 /* RAPOperator::Mult (operator.hpp:977): y_true = P^T A P x_true; x_true, y_true device
  * [n_owned].  Grouped ncclSend/ncclRecv on an internal stream overlapped with the

@@ -145,7 +145,8 @@ def test_gloo_exchange_matches_serial(tmp_path, kind, nranks):
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,nranks,order", [("cart", 2, 2), ("cart", 3, 1), ("fichera", 3, 2),
                                                ("fichera", 4, 3), ("cart", 4, 2)])
-def test_gpu_loopback_group_matches_serial(kind, nranks, order):
+@pytest.mark.parametrize("scatter", ["partials", "atomic"])
+def test_gpu_loopback_group_matches_serial(kind, nranks, order, scatter):
     import torch
     m = _mesh(kind)
     fes = E.H1Space(m, order)
@@ -155,7 +156,7 @@ def test_gpu_loopback_group_matches_serial(kind, nranks, order):
     xg = np.random.default_rng(1).uniform(-1, 1, fes.ndofs)
     for r in range(nranks):
         part = E.Partition(fes, er, r, nranks)
-        pf = E.ParBilinearForm(part)
+        pf = E.ParBilinearForm(part, scatter=scatter)
         P = E.quadrature_points_subset(m, q1d, part.elems)
         c = torch.as_tensor(coeff_function(P).reshape(part.ne_local, -1)).cuda()
         pf.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(c)))
@@ -164,7 +165,7 @@ def test_gpu_loopback_group_matches_serial(kind, nranks, order):
         forms.append(pf)
         parts.append(part)
         xs.append(torch.as_tensor(xg[part.owned_global]).cuda())
-        ys.append(torch.empty(part.n_owned, dtype=torch.float64, device="cuda"))
+        ys.append(torch.full((part.n_owned,), float("nan"), dtype=torch.float64, device="cuda"))
     E.ParGroup(forms).Mult(xs, ys)
     torch.cuda.synchronize()
     y = np.zeros(fes.ndofs)

@@ -54,7 +54,7 @@ def make_mesh(name):
 
 
 def build_pair(mesh, order, alpha, beta, kernel=E.KERNEL_AUTO, numbering=E.NUMBERING_ENTITY,
-               element_order="auto"):
+               element_order="auto", scatter="partials"):
     """Product form + oracle operator on the same mesh; alpha/beta: 'fn', 'bio', float or None."""
     fes = E.H1Space(mesh, order, numbering)
     en = mesh.element_nodes()
@@ -76,7 +76,7 @@ def build_pair(mesh, order, alpha, beta, kernel=E.KERNEL_AUTO, numbering=E.NUMBE
 
     a_np, a_c = coeff(alpha)
     b_np, b_c = coeff(beta)
-    form = E.BilinearForm(fes, kernel=kernel, element_order=element_order)
+    form = E.BilinearForm(fes, kernel=kernel, element_order=element_order, scatter=scatter)
     if a_c is not None:
         form.AddDomainIntegrator(E.MassIntegrator(a_c))
     if b_c is not None:
@@ -325,3 +325,57 @@ def test_element_orders_same_operator(element_order, order):
     d = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
     form.AssembleDiagonal(d)
     assert relerr(host(d), op.diagonal()) < 1e-13
+
+
+@pytest.mark.parametrize("mesh_name", ["nonaligned", "fichera_r1", "cart_bricks", "cart_130"])
+@pytest.mark.parametrize("element_order", ["native", "brick", "morton"])
+@pytest.mark.parametrize("order", [1, 2])
+def test_scatter_modes(mesh_name, element_order, order):
+    """Partial-slot scatter (default) and atomic scatter both give the oracle's y; the
+    partial scatter overwrites every entry (y pre-filled with NaN) and is bitwise
+    reproducible."""
+    m = make_mesh(mesh_name)
+    if element_order == "brick" and mesh_name == "fichera_r1":
+        pytest.skip("brick order needs a Cartesian mesh")
+    x = np.random.default_rng(41).uniform(-1, 1, make_fes_ndofs(m, order))
+    ys = {}
+    for scatter in ("partials", "atomic"):
+        fes, form, op = build_pair(m, order, "fn", "fn", element_order=element_order, scatter=scatter)
+        y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+        form.Mult(dev(x), y)
+        assert relerr(host(y), op.mult(x)) <= RTOL
+        ys[scatter] = host(y)
+        if scatter == "partials":
+            n_sh, n_slots = form.ScatterInfo()
+            assert 0 <= n_sh <= fes.ndofs and n_slots >= 2 * n_sh - fes.ndofs
+            for _ in range(3):
+                y2 = torch.full_like(y, float("nan"))
+                form.Mult(dev(x), y2)
+                assert torch.equal(y, y2)
+    assert relerr(ys["partials"], ys["atomic"]) <= RTOL
+
+
+def make_fes_ndofs(m, order):
+    return E.H1Space(m, order).ndofs
+
+
+def test_full_size_c2_deterministic():
+    """C2 size: the default fused Mult is bitwise reproducible and matches the atomic scatter."""
+    n = 50
+    m = E.Mesh.MakeCartesian3D(n, n, n)
+    fes = E.H1Space(m, 2, E.NUMBERING_STRUCTURED)
+    x = dev(np.random.default_rng(23).uniform(-1, 1, fes.ndofs))
+    out = {}
+    for scatter in ("partials", "atomic"):
+        form = E.BilinearForm(fes, scatter=scatter)
+        form.AddDomainIntegrator(E.MassIntegrator(E.ConstantCoefficient(2.0)))
+        form.AddDomainIntegrator(E.DiffusionIntegrator(E.ConstantCoefficient(0.3)))
+        form.Assemble()
+        y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+        form.Mult(x, y)
+        out[scatter] = y
+        if scatter == "partials":
+            y2 = torch.empty_like(y)
+            form.Mult(x, y2)
+            assert torch.equal(y, y2)
+    assert relerr(host(out["partials"]), host(out["atomic"])) <= RTOL

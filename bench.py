@@ -53,7 +53,7 @@ K_SCALE, K_SLOPE, K_TREF = 0.5 * 0.05, 0.0012, 37.0  # gamma*dt*k0, dk/dT / k0, 
 def bioheat_coefficients(E, torch, mesh, fes, part=None):
     """alpha = rho*c_eff(x) at quadrature points (FunctionCoefficient projection) and the
     temperature grid function T (L-vector) for beta = gamma*dt*k(T)."""
-    q1d = 4
+    q1d = fes.order + 2
     X = fes.dof_coords()
     T = temperature_fn(X)
     if part is None:
@@ -71,8 +71,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--workload", choices=["c2", "c4"], default="c2")
-    ap.add_argument("--kernel", choices=["auto", "tpe", "wpe", "unfused"], default="auto")
+    ap.add_argument("--workload", choices=["c2", "c4", "c5"], default="c2")
+    ap.add_argument("--kernel", choices=["auto", "tpe", "wpe", "unfused", "line"], default="auto")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", type=int, default=0,
@@ -96,20 +96,26 @@ def main():
     E = load_pkg()
     E.load_library()
     scatter = os.environ.get("ECM2_SCATTER", "partials")  # A/B knob: partials | atomic
-    kernel = {"auto": E.KERNEL_AUTO, "tpe": E.KERNEL_TPE, "wpe": E.KERNEL_WPE, "unfused": E.KERNEL_UNFUSED}[args.kernel]
+    kernel = {"auto": E.KERNEL_AUTO, "tpe": E.KERNEL_TPE, "wpe": E.KERNEL_WPE, "unfused": E.KERNEL_UNFUSED,
+              "line": E.KERNEL_LINE}[args.kernel]
 
+    order = 4 if args.workload == "c5" else 2
     if args.workload == "c2":
         n = 50
         nx = ny = n
         nz_total = n * world
         scaling = "weak"
         workload = f"configs[1]: inline-hex refined to Cartesian 50x50x{nz_total} (50^3 per GPU), H1 p=2, Mass(rho*c)+Diffusion(gamma*dt*k(T)) PA Mult"
-    else:
+    elif args.workload == "c4":
         nx = ny = nz_total = 108
         scaling = "strong"
         workload = "configs[3]: Cartesian 108^3 (10.2M DoF) split over GPUs, H1 p=2, Mass+Diffusion PA Mult"
+    else:
+        nx = ny = nz_total = 68
+        scaling = "strong"
+        workload = "configs[4]: Cartesian 68^3 (20.3M DoF) split over GPUs, H1 p=4, Mass+Diffusion PA Mult"
     mesh = E.Mesh.MakeCartesian3D(nx, ny, nz_total, 1.0, ny / nx, nz_total / nx)
-    fes = E.H1Space(mesh, 2, E.NUMBERING_STRUCTURED)
+    fes = E.H1Space(mesh, order, E.NUMBERING_STRUCTURED)
     nsub = world if world > 1 else args.loopback
     mass = lambda a: E.MassIntegrator(E.QuadratureCoefficient(a))
     diff = lambda T: E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(T, K_SCALE, K_SLOPE, K_TREF))
@@ -220,6 +226,7 @@ def main():
                 traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        stream = stream_copy_peak(E, torch)
         cpu = None
         if not args.no_cpu_baseline and world == 1 and args.loopback <= 1:
             cpu = cpu_baseline(fes, mesh, alpha, T, args.cpu_baseline_seconds)
@@ -240,9 +247,9 @@ def main():
                 "workload": workload,
                 "ndofs": int(ndofs_total),
                 "elements": int(fes.ne),
-                "order": 2, "q1d": 4,
+                "order": order, "q1d": order + 2,
                 "launch": "hip-graph replay per Mult" if (args.graph and world == 1) else "stream launches",
-                "kernel": ["auto", "tpe", "wpe", "unfused"][timed_forms[0].info()["kernel"]],
+                "kernel": ["auto", "tpe", "wpe", "unfused", "line"][timed_forms[0].info()["kernel"]],
                 "parallelism": f"domain-decomposition z-slabs x{world}, RCCL shared-DoF exchange" if world > 1
                 else (f"loopback z-slabs x{args.loopback} on one GPU" if args.loopback > 1 else "single GPU"),
             },
@@ -254,6 +261,8 @@ def main():
                 "frac": round(achieved / PEAK_HBM_GBS, 4),
                 "traffic": traffic,
                 "kernel_ms_avg": round(kavg_ms, 5),
+                "stream_copy_gbs": stream,
+                "frac_of_stream": round(achieved / stream, 4) if stream else None,
                 "algorithmic_bytes_per_launch": bytes_total / world,
             },
             "cpu_baseline": cpu,
@@ -264,17 +273,37 @@ def main():
         dist.destroy_process_group()
 
 
+def stream_copy_peak(E, torch, nbytes=1 << 30, reps=20):
+    """Measured HBM STREAM-copy rate on this GPU (read + write bytes / time) with the
+    library's 16-byte nontemporal copy kernel, reported beside the 8 TB/s spec peak
+    (SURVEY §8(d) 'Bounding roofline')."""
+    a = torch.empty(nbytes // 8, dtype=torch.float64, device="cuda").uniform_()
+    b = torch.empty_like(a)
+    for _ in range(3):
+        E.stream_copy(a, b)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        E.stream_copy(a, b)
+    e1.record()
+    torch.cuda.synchronize()
+    rate = 2.0 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    return round(rate, 1)
+
+
 def cpu_baseline(fes, mesh, alpha, T, seconds):
     """The oracle (CPU restatement of the reference PA path, 'port') on the same workload,
     timed on this host's cores for a bounded number of Mults (~`seconds` of CPU work)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    q1d = 4
+    order = fes.order
+    q1d = order + 2
     en = mesh.element_nodes()
     gm = fes.gather_map()
-    Tq = O.interp_evector(T.cpu().numpy()[gm], 2, q1d)
+    Tq = O.interp_evector(T.cpu().numpy()[gm], order, q1d)
     beta = K_SCALE * (1.0 + K_SLOPE * (Tq - K_TREF))
-    op = O.OracleOperator(en, gm, fes.ndofs, 2, alpha=alpha.cpu().numpy(), beta=beta)
+    op = O.OracleOperator(en, gm, fes.ndofs, order, alpha=alpha.cpu().numpy(), beta=beta)
     x = np.random.default_rng(1).uniform(-1, 1, fes.ndofs)
     op.mult(x)  # warm-up
     n, t0 = 0, time.perf_counter()

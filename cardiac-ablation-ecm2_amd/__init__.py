@@ -32,7 +32,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ecm2_pa.h")
 
 MASS, DIFFUSION = 0, 1
 COEFF_CONSTANT, COEFF_QUAD, COEFF_GRIDFUNC_AFFINE = 0, 1, 2
-KERNEL_AUTO, KERNEL_TPE, KERNEL_WPE, KERNEL_UNFUSED = 0, 1, 2, 3
+KERNEL_AUTO, KERNEL_TPE, KERNEL_WPE, KERNEL_UNFUSED, KERNEL_LINE = 0, 1, 2, 3, 4
 NUMBERING_ENTITY, NUMBERING_STRUCTURED = 0, 1
 ORDER_NATIVE, ORDER_BRICK, ORDER_MORTON = 0, 1, 2
 SCATTER_PARTIALS, SCATTER_ATOMIC = 0, 1
@@ -84,6 +84,7 @@ def load_library(path: str = LIB_PATH):
         "ecm2_pa_form_set_element_nodes": (i32, [vp, vp]),
         "ecm2_pa_form_set_jacobians": (i32, [vp, vp]),
         "ecm2_pa_form_add_integrator": (i32, [vp, i32, i32, vp, vp]),
+        "ecm2_stream_copy": (i32, [vp, vp, ctypes.c_long, vp]),
         "ecm2_pa_form_set_kernel": (i32, [vp, i32]),
         "ecm2_pa_form_set_scatter": (i32, [vp, i32]),
         "ecm2_pa_form_scatter_info": (i32, [vp, vp, vp]),
@@ -136,6 +137,11 @@ def _stream(stream=None) -> ctypes.c_void_p:
     import torch
     s = stream if stream is not None else torch.cuda.current_stream()
     return ctypes.c_void_p(s.cuda_stream)
+
+
+def stream_copy(a, b, stream=None):
+    """b = a through the library's 16-byte nontemporal copy kernel (HBM STREAM measurement)."""
+    _check(load_library().ecm2_stream_copy(_dev_ptr(a), _dev_ptr(b), a.numel(), _stream(stream)))
 
 
 def declared_symbols(header: str = HEADER_PATH) -> list:

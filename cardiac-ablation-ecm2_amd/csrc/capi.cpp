@@ -71,6 +71,11 @@ extern "C" {
 const char *ecm2_last_error(void) { return g_last_error.c_str(); }
 int ecm2_version(void) { return 100; }
 
+int ecm2_stream_copy(const double *a, double *b, long n, void *stream)
+{
+   return guard([&] { ecm2::kern::stream_copy(n, a, b, S(stream)); });
+}
+
 int ecm2_device_count(void)
 {
    int n = 0;

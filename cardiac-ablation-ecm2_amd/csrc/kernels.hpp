@@ -69,7 +69,9 @@ struct ApplyArgs
    const double *qdd = nullptr, *qdm = nullptr;
    const double *x = nullptr, *xg = nullptr;
    double *y = nullptr, *yg = nullptr;
-   double *part = nullptr;          // [blk][nd][64] partial slots of shared dofs (null: atomics)
+   double *part = nullptr;          // partial slots of shared dofs (null: atomics)
+   const int *chunks = nullptr;     // LINE: device chunk table (first | count << 24)
+   const int *chunk_off = nullptr;  // LINE: host [nblk + 1], chunks of 64-element block b
 };
 
 namespace kern
@@ -95,6 +97,11 @@ void apply_tpe(int D, int Q, bool mass, bool diff, const ApplyArgs &a, const Bas
                const double *rowtab, hipStream_t s);
 // Row table for apply_tpe: [qz][qy][3][dz][dy] products (see pa_kernels.hip).
 std::vector<double> make_row_table(const DofToQuad &m);
+// Line kernel: one wave per chunk of x-adjacent elements, native qdata layout, L-vectors
+// through an encoded map [e][nd] (dof | shared << 30 | sign << 31); shared dofs go to
+// part[e*nd + a] when a.part is set, else atomics.  has_line: (D, Q) instantiated.
+bool has_line(int D, int Q);
+void apply_line(int D, int Q, bool mass, bool diff, const ApplyArgs &a, const Basis1D &b, hipStream_t s);
 // Workgroup-per-element kernel, any layout; in/out either L-vectors (through the
 // gather map; output by atomics into a zeroed y) or E-vectors (accumulated).
 void apply_wpe(int D, int Q, bool mass, bool diff, const ApplyArgs &a, bool in_evec,
@@ -126,6 +133,8 @@ void pcg_precond(int n, const double *dinv, const double *r, double *z, hipStrea
 void pcg_update_d(int n, const double *betanom, const double *nom, const double *z, double *d,
                   hipStream_t s);
 void reciprocal(int n, const double *a, double *out, hipStream_t s);
+// b = a with 16-byte nontemporal accesses (HBM STREAM-copy measurement)
+void stream_copy(long n, const double *a, double *b, hipStream_t s);
 // Halo pack/unpack for the distributed operator (K7): buf[i] = x[idx[i]] ; y[idx[i]] += buf[i]
 void gather_idx(int n, const int *idx, const double *x, double *buf, hipStream_t s);
 void scatter_add_idx(int n, const int *idx, const double *buf, double *y, hipStream_t s);

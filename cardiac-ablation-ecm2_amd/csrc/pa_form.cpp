@@ -98,6 +98,7 @@ void PAForm::set_element_order(const int *perm)
       seen[e] = 1;
    }
    gmap_blk_.resize(0);
+   gmap_line_.resize(0);
    assembled_ = false;
 }
 
@@ -162,10 +163,51 @@ void build_merge_plan(int ne, int D, const std::vector<int> &gmap_int, int ndofs
 }
 } // namespace
 
+// Second-pass plan of the deterministic scatter: every dof not held exactly once with its
+// partial slots in ascending order; dofs held by nobody get an empty list (y = 0).  The
+// owned dofs come first, then the ghosts (split form); within each range the list is
+// ordered by first slot, so neighbouring threads of k_sum_partials read neighbouring slots.
+void PAForm::build_shared_plan(const std::vector<int> &hcount, const std::vector<int> &hdof,
+                               const std::vector<int> &hslot, hipStream_t s)
+{
+   std::vector<int> start(ndofs_ + 1, 0);
+   for (int d = 0; d < ndofs_; d++) { start[d + 1] = start[d] + (hcount[d] > 1 ? hcount[d] : 0); }
+   ECM2_VERIFY((size_t)start[ndofs_] == hdof.size(), ERR_INTERNAL, "shared holder count mismatch");
+   std::vector<int> slots_by_dof(hdof.size()), fill(start.begin(), start.end() - 1);
+   for (size_t i = 0; i < hdof.size(); i++) { slots_by_dof[fill[hdof[i]]++] = hslot[i]; }
+   std::vector<int> dofs;
+   for (int d = 0; d < ndofs_; d++) { if (hcount[d] != 1) { dofs.push_back(d); } }
+   auto key = [&](int d) -> long {
+      const long first = hcount[d] > 1 ? slots_by_dof[start[d]] : -1;
+      return (d < n_owned_ ? 0 : (1l << 40)) + first;
+   };
+   std::stable_sort(dofs.begin(), dofs.end(), [&](int p, int q) { return key(p) < key(q); });
+   std::vector<unsigned> meta;
+   std::vector<int> slots;
+   slots.reserve(slots_by_dof.size());
+   ECM2_VERIFY(slots_by_dof.size() < (1ull << 27), ERR_UNSUPPORTED, "too many partial slots");
+   for (int d : dofs)
+   {
+      const unsigned cnt = (unsigned)(start[d + 1] - start[d]);
+      ECM2_VERIFY(cnt < 32, ERR_UNSUPPORTED, "dof " << d << " held by " << cnt << " element entries");
+      meta.push_back((unsigned)slots.size() << 5 | cnt);
+      slots.insert(slots.end(), slots_by_dof.begin() + start[d], slots_by_dof.begin() + start[d + 1]);
+   }
+   n_sh_ = (int)dofs.size();
+   n_sh_owned_ = 0;
+   while (n_sh_owned_ < n_sh_ && dofs[n_sh_owned_] < n_owned_) { n_sh_owned_++; }
+   n_slots_ = (long)slots.size();
+   sh_dofs_.upload(dofs, s);
+   sh_meta_.upload(meta, s);
+   sh_slots_.upload(slots, s);
+}
+
 void PAForm::set_kernel(int mode)
 {
-   ECM2_VERIFY(mode >= KERNEL_AUTO && mode <= KERNEL_UNFUSED, ERR_ARG, "unknown kernel mode " << mode);
+   ECM2_VERIFY(mode >= KERNEL_AUTO && mode <= KERNEL_LINE, ERR_ARG, "unknown kernel mode " << mode);
    mode_ = mode;
+   gmap_blk_.resize(0);   // the scatter plan belongs to one fused kernel: rebuild it
+   gmap_line_.resize(0);
    assembled_ = false;
 }
 
@@ -175,9 +217,14 @@ void PAForm::assemble(hipStream_t s)
 {
    ECM2_VERIFY(enodes_.size() || jac_ || ne_ == 0, ERR_STATE, "assemble: no geometry set");
    resolved_mode_ = mode_;
-   if (mode_ == KERNEL_AUTO) { resolved_mode_ = has_tpe(D_, Q_) ? KERNEL_TPE : KERNEL_WPE; }
+   if (mode_ == KERNEL_AUTO)
+   {
+      resolved_mode_ = has_tpe(D_, Q_) ? KERNEL_TPE : (kern::has_line(D_, Q_) ? KERNEL_LINE : KERNEL_WPE);
+   }
    ECM2_VERIFY(resolved_mode_ != KERNEL_TPE || has_tpe(D_, Q_), ERR_UNSUPPORTED,
                "thread-per-element kernel needs (D1D,Q1D) in {(2,3),(3,4)}");
+   ECM2_VERIFY(resolved_mode_ != KERNEL_LINE || kern::has_line(D_, Q_), ERR_UNSUPPORTED,
+               "line kernel needs Q1D in {D1D, D1D+1} and Q1D <= 8");
    layout_.kind = (resolved_mode_ == KERNEL_TPE) ? QLAYOUT_BLOCKED : QLAYOUT_NATIVE;
 
    if (resolved_mode_ == KERNEL_TPE && !gmap_blk_.size() && ne_ > 0)
@@ -208,48 +255,21 @@ void PAForm::assemble(hipStream_t s)
             blk[((size_t)b * ND_ + a) * 64 + l] = (int)enc;
          }
       }
-      // Second-pass plan of the deterministic scatter: every dof not held exactly once
-      // with its partial slots (b*ND + a)*64 + l in ascending order.  Dofs held by
-      // nobody get an empty list (y = 0).  The owned dofs come first, then the ghosts
-      // (split form); within each range the list is ordered by first slot, so neighbouring
-      // threads of k_sum_partials read neighbouring lanes of the partial buffer.
       {
-         std::vector<int> start(ndofs_ + 1, 0);
-         for (int d = 0; d < ndofs_; d++) { start[d + 1] = start[d] + (hcount[d] > 1 ? hcount[d] : 0); }
-         std::vector<int> slots_by_dof(start[ndofs_]), fill(start.begin(), start.end() - 1);
+         std::vector<int> hdof, hslot;
          for (int b = 0; b < nblk; b++)
             for (int a = 0; a < ND_; a++)
                for (int l = 0; l < 64; l++)
                {
                   if (!holds[((size_t)b * 64 + l) * ND_ + a]) { continue; }
                   const int d = blk[((size_t)b * ND_ + a) * 64 + l] & 0x3fffffff;
-                  if (hcount[d] > 1) { slots_by_dof[fill[d]++] = (b * ND_ + a) * 64 + l; }
+                  if (hcount[d] > 1)
+                  {
+                     hdof.push_back(d);
+                     hslot.push_back((b * ND_ + a) * 64 + l);
+                  }
                }
-         std::vector<int> dofs;
-         for (int d = 0; d < ndofs_; d++) { if (hcount[d] != 1) { dofs.push_back(d); } }
-         auto key = [&](int d) -> long {
-            const long first = hcount[d] > 1 ? slots_by_dof[start[d]] : -1;
-            return (d < n_owned_ ? 0 : (1l << 40)) + first;
-         };
-         std::stable_sort(dofs.begin(), dofs.end(), [&](int p, int q) { return key(p) < key(q); });
-         std::vector<unsigned> meta;
-         std::vector<int> slots;
-         slots.reserve(slots_by_dof.size());
-         ECM2_VERIFY(slots_by_dof.size() < (1ull << 27), ERR_UNSUPPORTED, "too many partial slots");
-         for (int d : dofs)
-         {
-            const unsigned cnt = (unsigned)(start[d + 1] - start[d]);
-            ECM2_VERIFY(cnt < 32, ERR_UNSUPPORTED, "dof " << d << " held by " << cnt << " element entries");
-            meta.push_back((unsigned)slots.size() << 5 | cnt);
-            slots.insert(slots.end(), slots_by_dof.begin() + start[d], slots_by_dof.begin() + start[d + 1]);
-         }
-         n_sh_ = (int)dofs.size();
-         n_sh_owned_ = 0;
-         while (n_sh_owned_ < n_sh_ && dofs[n_sh_owned_] < n_owned_) { n_sh_owned_++; }
-         n_slots_ = (long)slots.size();
-         sh_dofs_.upload(dofs, s);
-         sh_meta_.upload(meta, s);
-         sh_slots_.upload(slots, s);
+         build_shared_plan(hcount, hdof, hslot, s);
       }
       gmap_blk_.upload(blk, s);
       lane_flags_.upload(fl, s);
@@ -257,8 +277,69 @@ void PAForm::assemble(hipStream_t s)
       rowtab_.upload(kern::make_row_table(maps_), s);
       ECM2_HIP(hipStreamSynchronize(s));
    }
+   if (resolved_mode_ == KERNEL_LINE && !gmap_line_.size() && ne_ > 0)
+   {
+      // chunks of up to 8 consecutive elements whose x-faces coincide (never crossing a
+      // 64-element block, so apply_blocks ranges map to chunk ranges); the face of
+      // element k is carried into element k+1, which holds it.  Then the encoded map
+      // and the deterministic-scatter plan over the holding entries.
+      ECM2_VERIFY(ndofs_ < (1 << 30), ERR_UNSUPPORTED, "fused kernel supports < 2^30 dofs");
+      ECM2_VERIFY((size_t)ne_ * ND_ < (1ull << 31) && ne_ < (1 << 24), ERR_UNSUPPORTED,
+                  "too many elements for the line kernel's chunk table");
+      auto dofv = [](int g) { return g >= 0 ? g : -1 - g; };
+      auto xface_match = [&](int e) {  // element e's high-x face == element e+1's low-x face
+         for (int dz = 0; dz < D_; dz++)
+            for (int dy = 0; dy < D_; dy++)
+            {
+               const int r = (dz * D_ + dy) * D_;
+               if (dofv(gmap_host_[(size_t)e * ND_ + r + D_ - 1]) != dofv(gmap_host_[(size_t)(e + 1) * ND_ + r]))
+               {
+                  return false;
+               }
+            }
+         return true;
+      };
+      const int nblk = layout_.nblk();
+      std::vector<int> chunks, coff(nblk + 1, 0);
+      std::vector<char> holds((size_t)ne_ * ND_, 1);
+      for (int bk = 0; bk < nblk; bk++)
+      {
+         const int eb = bk * 64, ee = std::min(ne_, eb + 64);
+         int e = eb;
+         while (e < ee)
+         {
+            int n = 1;
+            while (n < 8 && e + n < ee && xface_match(e + n - 1)) { n++; }
+            chunks.push_back(e | (n << 24));
+            for (int k = 0; k + 1 < n; k++)
+               for (int dz = 0; dz < D_; dz++)
+                  for (int dy = 0; dy < D_; dy++) { holds[(size_t)(e + k) * ND_ + (dz * D_ + dy) * D_ + D_ - 1] = 0; }
+            e += n;
+         }
+         coff[bk + 1] = (int)chunks.size();
+      }
+      std::vector<int> hcount(ndofs_, 0);
+      for (size_t i = 0; i < gmap_host_.size(); i++) { if (holds[i]) { hcount[dofv(gmap_host_[i])]++; } }
+      std::vector<int> enc(gmap_host_.size()), hdof, hslot;
+      for (size_t i = 0; i < gmap_host_.size(); i++)
+      {
+         const int g = gmap_host_[i];
+         const unsigned d = (unsigned)dofv(g);
+         enc[i] = (int)(d | ((hcount[d] > 1 ? 1u : 0u) << 30) | ((g < 0 ? 1u : 0u) << 31));
+         if (holds[i] && hcount[d] > 1)
+         {
+            hdof.push_back((int)d);
+            hslot.push_back((int)i);
+         }
+      }
+      build_shared_plan(hcount, hdof, hslot, s);
+      gmap_line_.upload(enc, s);
+      chunks_.upload(chunks, s);
+      chunk_off_ = coff;
+      ECM2_HIP(hipStreamSynchronize(s));
+   }
    layout_.pos = (layout_.kind == QLAYOUT_BLOCKED) ? pos_.data() : nullptr;
-   part_.resize(use_partials() ? (size_t)layout_.nblk() * ND_ * 64 : 0);
+   part_.resize(use_partials() ? (size_t)layout_.nblk() * ND_ * 64 : 0);  // >= ne * nd for LINE
    qd_diff_.resize(have_diff_ ? layout_.diff_size() : 0);
    qd_mass_.resize(have_mass_ ? layout_.mass_size() : 0);
    if (qd_diff_.size()) { ECM2_HIP(hipMemsetAsync(qd_diff_.data(), 0, qd_diff_.bytes(), s)); }
@@ -433,11 +514,14 @@ ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, doubl
    a.n_owned = n_owned_;
    a.pos = layout_.pos;
    a.lane_flags = lane_flags_.data();
-   a.gmap = (resolved_mode_ == KERNEL_TPE) ? gmap_blk_.data() : gmap_.data();
+   a.gmap = (resolved_mode_ == KERNEL_TPE) ? gmap_blk_.data()
+            : (resolved_mode_ == KERNEL_LINE) ? gmap_line_.data() : gmap_.data();
    a.qdd = qd_diff_.data();
    a.qdm = qd_mass_.data();
    a.x = x; a.xg = xg; a.y = y; a.yg = yg;
    a.part = use_partials() ? const_cast<double *>(part_.data()) : nullptr;  // form-owned scratch
+   a.chunks = chunks_.data();
+   a.chunk_off = chunk_off_.empty() ? nullptr : chunk_off_.data();
    return a;
 }
 
@@ -450,6 +534,10 @@ void PAForm::apply_blocks(const double *x, const double *xg, double *y, double *
    if (resolved_mode_ == KERNEL_TPE)
    {
       kern::apply_tpe(D_, Q_, have_mass_, have_diff_, a, basis_, rowtab_.data(), s);
+   }
+   else if (resolved_mode_ == KERNEL_LINE)
+   {
+      kern::apply_line(D_, Q_, have_mass_, have_diff_, a, basis_, s);
    }
    else
    {

@@ -25,10 +25,11 @@ namespace ecm2
 
 enum KernelMode : int
 {
-   KERNEL_AUTO = 0,     // fused thread-per-element where available, else fused WPE
+   KERNEL_AUTO = 0,     // TPE for p = 1, 2; LINE for p = 3..6; else WPE
    KERNEL_TPE = 1,      // fused, thread per element (p = 1, 2)
-   KERNEL_WPE = 2,      // fused, workgroup per element (any p)
-   KERNEL_UNFUSED = 3   // reference-shaped: restriction, per-integrator AddMultPA, CSR transpose
+   KERNEL_WPE = 2,      // fused, workgroup per element, all intermediates in LDS (any p)
+   KERNEL_UNFUSED = 3,  // reference-shaped: restriction, per-integrator AddMultPA, CSR transpose
+   KERNEL_LINE = 4      // fused, one wave per element, register lines (Q1D <= 8)
 };
 
 // How the fused TPE kernel combines contributions to dofs held by more than one element
@@ -71,7 +72,10 @@ public:
    void set_kernel(int mode);
    void set_scatter(int mode);
    int scatter() const { return scatter_; }
-   bool use_partials() const { return resolved_mode_ == KERNEL_TPE && scatter_ == SCATTER_PARTIALS; }
+   bool use_partials() const
+   {
+      return (resolved_mode_ == KERNEL_TPE || resolved_mode_ == KERNEL_LINE) && scatter_ == SCATTER_PARTIALS;
+   }
    void assemble(hipStream_t s);
 
    // y = A x (BilinearForm::Mult semantics: y overwritten).
@@ -109,6 +113,10 @@ private:
    void ensure_work(hipStream_t s);
    void record_start(hipStream_t s);
    void record_stop(hipStream_t s);
+   // second pass of the deterministic scatter from the shared holding entries
+   // (hdof[i], hslot[i]) in ascending slot order and the per-dof holder counts
+   void build_shared_plan(const std::vector<int> &hcount, const std::vector<int> &hdof,
+                          const std::vector<int> &hslot, hipStream_t s);
    ApplyArgs apply_args(const double *x, const double *xg, double *y, double *yg, int b0,
                         int b1) const;
 
@@ -135,6 +143,9 @@ private:
    std::vector<int> gmap_host_;
    DeviceArray<int> gmap_;          // native [e][nd]
    DeviceArray<int> gmap_blk_;      // blocked [blk][nd][64] (internal element order)
+   DeviceArray<int> gmap_line_;     // LINE: [e][nd] dof | shared << 30 | sign << 31
+   DeviceArray<int> chunks_;        // LINE: first element | count << 24
+   std::vector<int> chunk_off_;     // LINE: chunks of block b = [chunk_off_[b], chunk_off_[b+1])
    DeviceArray<int> lane_flags_;    // [blk][64] in-wave merge flags
    std::vector<int> perm_host_;     // internal position -> caller element (empty: identity)
    DeviceArray<int> pos_;           // caller element -> internal position

@@ -556,9 +556,22 @@ __global__ void k_apply_wpe(const int *__restrict__ pos, int kind, int ne, int e
                             const int *__restrict__ gmap,
                             const double *__restrict__ qdd, const double *__restrict__ qdm,
                             const double *__restrict__ x, const double *__restrict__ xg,
-                            double *__restrict__ y, double *__restrict__ yg, const Basis1D b)
+                            double *__restrict__ y, double *__restrict__ yg, const Basis1D b, int var)
 {
    constexpr int ND = D * D * D, NQ = Q * Q * Q;
+   // experiment knob (ECM2_WPE_VARIANT): bit 1 = plain stores (diagnostic, wrong y),
+   // bit 2 = prefetch this thread's qdata before the contraction stages
+   double pq[7];
+   if ((var & 2) && threadIdx.x < NQ)
+   {
+      const int e = e_begin + blockIdx.x, t = threadIdx.x;
+      if (MASS) { pq[6] = qdm[qidx_mass(pos, kind, NQ, e, t)]; }
+      if (DIFF)
+      {
+#pragma unroll
+         for (int c = 0; c < 6; c++) { pq[c] = qdd[qidx_diff(pos, kind, NQ, e, c, t)]; }
+      }
+   }
    __shared__ double sB[Q * D], sG[Q * D];
    __shared__ double sX[ND];
    __shared__ double s1a[D * D * Q], s1b[D * D * Q];
@@ -630,6 +643,18 @@ __global__ void k_apply_wpe(const int *__restrict__ pos, int kind, int ne, int e
          u += s2c[i] * sB[qz + Q * dz];
       }
       double m = 0.0, fx = 0.0, fy = 0.0, fz = 0.0;
+      if (var & 2)
+      {
+         if (MASS) { m = pq[6] * u; }
+         if (DIFF)
+         {
+            fx = (pq[0] * gx) + (pq[1] * gy) + (pq[2] * gz);
+            fy = (pq[1] * gx) + (pq[3] * gy) + (pq[4] * gz);
+            fz = (pq[2] * gx) + (pq[4] * gy) + (pq[5] * gz);
+         }
+      }
+      else
+      {
       if (MASS) { m = qdm[qidx_mass(pos, kind, NQ, e, t)] * u; }
       if (DIFF)
       {
@@ -642,6 +667,7 @@ __global__ void k_apply_wpe(const int *__restrict__ pos, int kind, int ne, int e
          fx = (O11 * gx) + (O12 * gy) + (O13 * gz);
          fy = (O12 * gx) + (O22 * gy) + (O23 * gz);
          fz = (O13 * gx) + (O23 * gy) + (O33 * gz);
+      }
       }
       s3m[t] = m; s3x[t] = fx; s3y[t] = fy; s3z[t] = fz;
    }
@@ -691,7 +717,8 @@ __global__ void k_apply_wpe(const int *__restrict__ pos, int kind, int ne, int e
          const int g = gmap[(size_t)e * ND + t];
          const int d = dof_of(g);
          double *dst = d < n_owned ? y + d : yg + (d - n_owned);
-         unsafeAtomicAdd(dst, g >= 0 ? u : -u);
+         if (var & 1) { *dst = g >= 0 ? u : -u; }
+         else { unsafeAtomicAdd(dst, g >= 0 ? u : -u); }
       }
    }
 }
@@ -699,6 +726,265 @@ __global__ void k_apply_wpe(const int *__restrict__ pos, int kind, int ne, int e
 // --------------------------------------------------------------------------
 // Restriction, diagonal, vector kernels
 // --------------------------------------------------------------------------
+
+// --------------------------------------------------------------------------
+// "Line" kernel: one wave per chunk of up to 8 x-adjacent elements, any (D, Q) with
+// Q*Q <= 64 (p = 1..6), L-vectors in and out.  Each stage gives every active lane one
+// 1D line of the current contraction direction in registers: a lane reads D (or Q)
+// values from LDS once and produces Q (or D) outputs, so LDS traffic is one read per
+// Q multiply-adds (the reference's smem kernels, bilininteg_diffusion_kernels.hpp:
+// 989-1214, read two LDS operands per multiply-add).  B/G come from the kernel
+// arguments (SGPR operands).  The z contraction, the quadrature-point weighting and
+// the transposed z contraction are fused in registers on (qx, qy) lanes.
+//   lanes (dy,dz): gather x-line, x-contract          -> s1 [2][dz][dy][qx]
+//   lanes (qx,dz): y-contract                           -> s2 [3][dz][qy][qx]
+//   lanes (qx,qy): z-contract, weight, z-transpose      -> s3 [3][dz][qy][qx]
+//   lanes (qx,dz): y-transpose                          -> s4 [2][dz][dy][qx]
+//   lanes (dy,dz): x-transpose, scatter
+// Chunks: consecutive elements whose x-faces coincide (checked on the host).  Lane
+// (dy,dz) holds entry (D-1,dy,dz) of element k and (0,dy,dz) of element k+1, so the
+// shared face is summed in a register (carry) and only the last element stores it.
+// The qdata registers are dead after the z stage: the next element's qdata is loaded
+// into them there, overlapping its latency with the rest of this element.
+// gmap: [e][ND] encoded dof | shared << 30 | sign << 31 (see PAForm::assemble);
+// chunks[c] = first element | count << 24 (count <= 8).
+// --------------------------------------------------------------------------
+template <int D, int Q, bool MASS, bool DIFF>
+__device__ __forceinline__ void line_load_qdata(double (&qv)[7][Q], int e, int t,
+                                                const double *__restrict__ qdd,
+                                                const double *__restrict__ qdm)
+{
+   constexpr int NQ = Q * Q * Q, QQ = Q * Q;
+   if (t < QQ)
+   {
+#pragma unroll
+      for (int qz = 0; qz < Q; qz++)
+      {
+         if (DIFF)
+         {
+#pragma unroll
+            for (int c = 0; c < 6; c++) { qv[c][qz] = qdd[((size_t)e * 6 + c) * NQ + qz * QQ + t]; }
+         }
+         if (MASS) { qv[6][qz] = qdm[(size_t)e * NQ + qz * QQ + t]; }
+      }
+   }
+}
+
+template <int D, int Q, bool MASS, bool DIFF, bool SPLIT>
+__global__ void __launch_bounds__(64)
+k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned,
+             const int *__restrict__ gmap,
+             const double *__restrict__ qdd, const double *__restrict__ qdm,
+             const double *__restrict__ x, const double *__restrict__ xg,
+             double *__restrict__ y, double *__restrict__ yg, const Basis1D b,
+             double *__restrict__ part)
+{
+   constexpr int ND = D * D * D, DD = D * D, QQ = Q * Q, DQ = D * Q;
+   constexpr int SA = (2 * DD * Q > 3 * D * QQ) ? 2 * DD * Q : 3 * D * QQ;
+   constexpr int SB = (3 * D * QQ > 2 * DD * Q) ? 3 * D * QQ : 2 * DD * Q;
+   static_assert(QQ <= 64, "line kernel needs Q1D <= 8");
+   __shared__ double bufA[SA];  // s1, then s3
+   __shared__ double bufB[SB];  // s2, then s4
+   const int c = c_begin + blockIdx.x;
+   if (c >= c_end) { return; }  // whole wave
+   const int t = threadIdx.x;
+   const int ch = chunks[c];
+   const int e0 = ch & 0xffffff, cnt = ch >> 24;
+
+   double qv[7][Q];
+   line_load_qdata<D, Q, MASS, DIFF>(qv, e0, t, qdd, qdm);
+   double carry = 0.0;
+#pragma unroll 1
+   for (int k = 0; k < cnt; k++)
+   {
+      const int e = e0 + k;
+      // ---- lanes (dy, dz): gather the x-line, contract in x
+      int gl[D];
+      if (t < DD)
+      {
+         const int *mp = gmap + (size_t)e * ND + t * D;
+         double xl[D];
+#pragma unroll
+         for (int dx = 0; dx < D; dx++)
+         {
+            const int g = mp[dx];
+            gl[dx] = g;
+            const int d = bdof(g);
+            const double v = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
+            xl[dx] = bneg(g) ? -v : v;
+         }
+#pragma unroll
+         for (int qx = 0; qx < Q; qx++)
+         {
+            double u = 0.0, v = 0.0;
+#pragma unroll
+            for (int dx = 0; dx < D; dx++)
+            {
+               u += b.B[qx + MQ * dx] * xl[dx];
+               v += b.G[qx + MQ * dx] * xl[dx];
+            }
+            bufA[t * Q + qx] = u;            // B_x   [dz][dy][qx]
+            bufA[DD * Q + t * Q + qx] = v;   // G_x
+         }
+      }
+      __syncthreads();
+      // ---- lanes (qx, dz): contract in y
+      if (t < DQ)
+      {
+         const int qx = t % Q, dz = t / Q;
+         double la[D], lb[D];
+#pragma unroll
+         for (int dy = 0; dy < D; dy++)
+         {
+            la[dy] = bufA[(dz * D + dy) * Q + qx];
+            lb[dy] = bufA[DD * Q + (dz * D + dy) * Q + qx];
+         }
+#pragma unroll
+         for (int qy = 0; qy < Q; qy++)
+         {
+            double gb = 0.0, bg = 0.0, bb = 0.0;
+#pragma unroll
+            for (int dy = 0; dy < D; dy++)
+            {
+               const double by = b.B[qy + MQ * dy], gy = b.G[qy + MQ * dy];
+               gb += by * lb[dy];  // G_x B_y
+               bg += gy * la[dy];  // B_x G_y
+               bb += by * la[dy];  // B_x B_y
+            }
+            const int o = (dz * Q + qy) * Q + qx;
+            bufB[o] = gb;
+            bufB[D * QQ + o] = bg;
+            bufB[2 * D * QQ + o] = bb;
+         }
+      }
+      __syncthreads();
+      // ---- lanes (qx, qy): contract in z, weight at the quadrature points, transpose in z
+      if (t < QQ)
+      {
+         double l0[D], l1[D], l2[D];
+#pragma unroll
+         for (int dz = 0; dz < D; dz++)
+         {
+            l0[dz] = bufB[dz * QQ + t];
+            l1[dz] = bufB[D * QQ + dz * QQ + t];
+            l2[dz] = bufB[2 * D * QQ + dz * QQ + t];
+         }
+         double A1[D], A2[D], A3[D];
+#pragma unroll
+         for (int dz = 0; dz < D; dz++) { A1[dz] = 0.0; A2[dz] = 0.0; A3[dz] = 0.0; }
+#pragma unroll
+         for (int qz = 0; qz < Q; qz++)
+         {
+            double gx = 0.0, gy = 0.0, gz = 0.0, u = 0.0;
+#pragma unroll
+            for (int dz = 0; dz < D; dz++)
+            {
+               const double bz = b.B[qz + MQ * dz], gzz = b.G[qz + MQ * dz];
+               if (DIFF)
+               {
+                  gx += bz * l0[dz];
+                  gy += bz * l1[dz];
+                  gz += gzz * l2[dz];
+               }
+               if (MASS) { u += bz * l2[dz]; }
+            }
+            double fx = 0.0, fy = 0.0, fz = 0.0, m = 0.0;
+            if (DIFF)
+            {
+               fx = qv[0][qz] * gx + qv[1][qz] * gy + qv[2][qz] * gz;
+               fy = qv[1][qz] * gx + qv[3][qz] * gy + qv[4][qz] * gz;
+               fz = qv[2][qz] * gx + qv[4][qz] * gy + qv[5][qz] * gz;
+            }
+            if (MASS) { m = qv[6][qz] * u; }
+#pragma unroll
+            for (int dz = 0; dz < D; dz++)
+            {
+               const double bz = b.B[qz + MQ * dz], gzz = b.G[qz + MQ * dz];
+               if (DIFF)
+               {
+                  A1[dz] += bz * fx;               // -> G_x B_y
+                  A2[dz] += bz * fy;               // -> B_x G_y
+                  A3[dz] += gzz * fz;              // -> B_x B_y
+               }
+               if (MASS) { A3[dz] += bz * m; }    // -> B_x B_y
+            }
+         }
+#pragma unroll
+         for (int dz = 0; dz < D; dz++)
+         {
+            bufA[dz * QQ + t] = A1[dz];
+            bufA[D * QQ + dz * QQ + t] = A2[dz];
+            bufA[2 * D * QQ + dz * QQ + t] = A3[dz];
+         }
+      }
+      // next element's qdata: in flight during the rest of this element
+      if (k + 1 < cnt) { line_load_qdata<D, Q, MASS, DIFF>(qv, e + 1, t, qdd, qdm); }
+      __syncthreads();
+      // ---- lanes (qx, dz): transpose in y
+      if (t < DQ)
+      {
+         const int qx = t % Q, dz = t / Q;
+         double l0[Q], l1[Q], l2[Q];
+#pragma unroll
+         for (int qy = 0; qy < Q; qy++)
+         {
+            const int o = (dz * Q + qy) * Q + qx;
+            l0[qy] = bufA[o];
+            l1[qy] = bufA[D * QQ + o];
+            l2[qy] = bufA[2 * D * QQ + o];
+         }
+#pragma unroll
+         for (int dy = 0; dy < D; dy++)
+         {
+            double c1 = 0.0, c2 = 0.0;
+#pragma unroll
+            for (int qy = 0; qy < Q; qy++)
+            {
+               const double by = b.B[qy + MQ * dy], gy = b.G[qy + MQ * dy];
+               c1 += by * l0[qy];                 // -> G_x
+               c2 += gy * l1[qy] + by * l2[qy];   // -> B_x
+            }
+            bufB[(dz * D + dy) * Q + qx] = c1;
+            bufB[DD * Q + (dz * D + dy) * Q + qx] = c2;
+         }
+      }
+      __syncthreads();
+      // ---- lanes (dy, dz): transpose in x, face carry, scatter
+      if (t < DD)
+      {
+         double l0[Q], l1[Q];
+#pragma unroll
+         for (int qx = 0; qx < Q; qx++)
+         {
+            l0[qx] = bufB[t * Q + qx];
+            l1[qx] = bufB[DD * Q + t * Q + qx];
+         }
+         const bool last = (k + 1 == cnt);
+#pragma unroll
+         for (int dx = 0; dx < D; dx++)
+         {
+            double v = 0.0;
+#pragma unroll
+            for (int qx = 0; qx < Q; qx++) { v += b.G[qx + MQ * dx] * l0[qx] + b.B[qx + MQ * dx] * l1[qx]; }
+            const int g = gl[dx];
+            if (bneg(g)) { v = -v; }
+            if (dx == 0) { v += carry; }
+            if (dx == D - 1 && !last)
+            {
+               carry = v;  // summed into the next element's (0, dy, dz) entry
+               continue;
+            }
+            const int d = bdof(g);
+            double *dst = (!SPLIT || d < n_owned) ? y + d : yg + (d - n_owned);
+            if (!bshared(g)) { *dst = v; }
+            else if (part) { part[(size_t)e * ND + t * D + dx] = v; }
+            else { unsafeAtomicAdd(dst, v); }
+         }
+      }
+      // no barrier here: the next element writes bufA (last read before barrier 4) and,
+      // after its first barrier, bufB (last read above)
+   }
+}
 
 __global__ void k_restriction_mult(long n, const int *__restrict__ gmap,
                                    const double *__restrict__ x, double *__restrict__ xe)
@@ -829,6 +1115,17 @@ __global__ void k_pcg_update_d(int n, const double *__restrict__ betanom,
    if (i >= n) { return; }
    const double beta = *betanom / *nom;
    d[i] = z[i] + beta * d[i];
+}
+
+// STREAM copy (measurement only): 16-byte nontemporal loads and stores, grid-stride,
+// the access shape of the guide's 6.29 TB/s float4-copy figure.
+__global__ void k_stream_copy(long n2, const v2d *__restrict__ a, v2d *__restrict__ b)
+{
+   const long stride = (long)gridDim.x * blockDim.x;
+   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride)
+   {
+      __builtin_nontemporal_store(__builtin_nontemporal_load(a + i), b + i);
+   }
 }
 
 __global__ void k_reciprocal(int n, const double *__restrict__ a, double *__restrict__ out)
@@ -967,6 +1264,15 @@ void launch_tpe_dq(bool mass, bool diff, const ApplyArgs &a, const Basis1D &b,
    else if (diff) { launch_tpe_mdq<D, Q, false, true>(a, b, rowtab, s); }
 }
 
+int wpe_variant()
+{
+   static int v = [] {
+      const char *e = std::getenv("ECM2_WPE_VARIANT");
+      return e ? std::atoi(e) : 0;
+   }();
+   return v;
+}
+
 template <int D, int Q, bool MASS, bool DIFF>
 void launch_wpe_mdq(const ApplyArgs &a, bool in_e, bool out_e, const Basis1D &b, hipStream_t s)
 {
@@ -977,7 +1283,8 @@ void launch_wpe_mdq(const ApplyArgs &a, bool in_e, bool out_e, const Basis1D &b,
    const dim3 grid(e1 - e0), block(nt);
 #define ECM2_WPE_LAUNCH(IE, OE)                                                                      \
    hipLaunchKernelGGL((k_apply_wpe<D, Q, MASS, DIFF, IE, OE>), grid, block, 0, s, a.pos, a.kind, a.ne, e0, \
-                      a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b)
+                      a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, var)
+   const int var = wpe_variant();
    if (in_e && out_e) { ECM2_WPE_LAUNCH(true, true); }
    else if (in_e) { ECM2_WPE_LAUNCH(true, false); }
    else if (out_e) { ECM2_WPE_LAUNCH(false, true); }
@@ -1042,6 +1349,62 @@ void apply_tpe(int D, int Q, bool mass, bool diff, const ApplyArgs &a, const Bas
    else if (D == 3 && Q == 4) { launch_tpe_dq<3, 4>(mass, diff, a, b, rowtab, s); }
    else { ECM2_VERIFY(false, ERR_UNSUPPORTED, "no thread-per-element kernel for D1D=" << D << " Q1D=" << Q); }
    ECM2_HIP(hipGetLastError());
+}
+
+template <int D, int Q, bool MASS, bool DIFF>
+void launch_line_mdq(const ApplyArgs &a, const Basis1D &b, hipStream_t s)
+{
+   ECM2_VERIFY(a.chunks && a.chunk_off, ERR_INTERNAL, "line kernel needs its chunk table");
+   const int c0 = a.chunk_off[a.blk_begin], c1 = a.chunk_off[a.blk_end];
+   if (c1 <= c0) { return; }
+   const dim3 grid(c1 - c0), block(64);
+   if (a.xg || a.yg)
+   {
+      hipLaunchKernelGGL((k_apply_line<D, Q, MASS, DIFF, true>), grid, block, 0, s, c0, c1, a.chunks, a.n_owned,
+                         a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.part);
+   }
+   else
+   {
+      hipLaunchKernelGGL((k_apply_line<D, Q, MASS, DIFF, false>), grid, block, 0, s, c0, c1, a.chunks, a.n_owned,
+                         a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.part);
+   }
+}
+
+template <int D, int Q>
+void launch_line_dq(bool mass, bool diff, const ApplyArgs &a, const Basis1D &b, hipStream_t s)
+{
+   if (mass && diff) { launch_line_mdq<D, Q, true, true>(a, b, s); }
+   else if (mass) { launch_line_mdq<D, Q, true, false>(a, b, s); }
+   else if (diff) { launch_line_mdq<D, Q, false, true>(a, b, s); }
+}
+
+bool has_line(int D, int Q)
+{
+   return (Q == D + 1 || Q == D) && D >= 2 && D <= 7 && Q <= 8;
+}
+
+void apply_line(int D, int Q, bool mass, bool diff, const ApplyArgs &a, const Basis1D &b, hipStream_t s)
+{
+   if (a.ne == 0) { return; }
+#define ECM2_LINE_CASE(DD, QQ)                                        \
+   if (D == DD && Q == QQ)                                            \
+   {                                                                  \
+      launch_line_dq<DD, QQ>(mass, diff, a, b, s);                    \
+      ECM2_HIP(hipGetLastError());                                    \
+      return;                                                         \
+   }
+   ECM2_LINE_CASE(2, 3)
+   ECM2_LINE_CASE(3, 4)
+   ECM2_LINE_CASE(4, 5)
+   ECM2_LINE_CASE(5, 6)
+   ECM2_LINE_CASE(6, 7)
+   ECM2_LINE_CASE(7, 8)
+   ECM2_LINE_CASE(2, 2)
+   ECM2_LINE_CASE(3, 3)
+   ECM2_LINE_CASE(4, 4)
+   ECM2_LINE_CASE(5, 5)
+#undef ECM2_LINE_CASE
+   ECM2_VERIFY(false, ERR_UNSUPPORTED, "no line kernel for D1D=" << D << " Q1D=" << Q);
 }
 
 void apply_wpe(int D, int Q, bool mass, bool diff, const ApplyArgs &a, bool in_e, bool out_e,
@@ -1134,6 +1497,15 @@ void pcg_update_d(int n, const double *betanom, const double *nom, const double 
                   hipStream_t s)
 {
    hipLaunchKernelGGL(k_pcg_update_d, dim3(grid_for(n, 256)), dim3(256), 0, s, n, betanom, nom, z, d);
+   ECM2_HIP(hipGetLastError());
+}
+
+void stream_copy(long n, const double *a, double *b, hipStream_t s)
+{
+   ECM2_VERIFY(n % 2 == 0 && ((uintptr_t)a % 16) == 0 && ((uintptr_t)b % 16) == 0, ERR_ARG,
+               "stream_copy needs 16-byte aligned even-length arrays");
+   hipLaunchKernelGGL(k_stream_copy, dim3(256 * 64), dim3(256), 0, s, n / 2, reinterpret_cast<const v2d *>(a),
+                      reinterpret_cast<v2d *>(b));
    ECM2_HIP(hipGetLastError());
 }
 

@@ -41,10 +41,11 @@ extern "C" {
 #define ECM2_COEFF_GRIDFUNC_AFFINE 2/* scale*(1+slope*(T(x_q)-t_ref)), T an H1 L-vector       */
 
 /* Kernel selection (all produce the same operator). */
-#define ECM2_KERNEL_AUTO 0
+#define ECM2_KERNEL_AUTO 0     /* TPE for p <= 2, LINE for p = 3..6                 */
 #define ECM2_KERNEL_TPE 1      /* fused, thread per element (p = 1, 2)              */
 #define ECM2_KERNEL_WPE 2      /* fused, workgroup per element (p = 1..6)           */
 #define ECM2_KERNEL_UNFUSED 3  /* reference-shaped: R, per-integrator AddMultPA, R^T */
+#define ECM2_KERNEL_LINE 4     /* fused, one wave per element, register lines (p <= 6) */
 
 /* Numbering of H1 dofs. */
 #define ECM2_NUMBERING_ENTITY 0     /* vertices, edges, faces, interiors (fespace.cpp:2767) */
@@ -53,6 +54,10 @@ extern "C" {
 const char *ecm2_last_error(void);
 int ecm2_version(void);
 int ecm2_device_count(void);
+/* Measurement helper (no reference counterpart): b[0..n) = a[0..n) with 16-byte
+ * nontemporal loads/stores -- the HBM STREAM-copy rate bench.py reports beside the
+ * spec peak.  n even, a and b 16-byte aligned device arrays. */
+int ecm2_stream_copy(const double *a, double *b, long n, void *stream);
 
 /* ------------------------------------------------------------------------ */
 /* Setup side: meshes and H1 spaces (the caller's Mesh / FiniteElementSpace)  */

@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Reduce a profiles/run_profile.sh output directory to per-launch HBM bytes.
+
+Reads the two separate PMC passes (FETCH_SIZE, WRITE_SIZE; rocprofv3 counter_collection
+CSVs, kB per dispatch) and the kernel-trace stats, and prints one JSON object per
+kernel of the Mult (the fused apply, the partial-sum pass, ...):
+  hbm_bytes_per_launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024
+The factor 2 is the gfx950 correction of MI355X_MICROARCH.md (HBM section: FETCH_SIZE
+reports 1/2 of the bytes of wide coalesced streaming reads).  The dominant kernel's
+entry is what bench.py reports as roofline.traffic (copied to profiles/pmc_<tag>_n1.json).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+KERNELS = {"apply": "k_apply_tpe", "sum_partials": "k_sum_partials", "apply_wpe": "k_apply_wpe"}
+
+
+def counters(d, name):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    out = {}
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != name:
+                continue
+            for key, pat in KERNELS.items():
+                if pat in r["Kernel_Name"]:
+                    out.setdefault(key, []).append(float(r["Counter_Value"]))
+    return out
+
+
+def stats(d):
+    files = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)
+    out = {}
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            for key, pat in KERNELS.items():
+                if pat in r["Name"]:
+                    out[key] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                                "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"])}
+    return out
+
+
+def main(root):
+    fetch = counters(os.path.join(root, "fetch"), "FETCH_SIZE")
+    write = counters(os.path.join(root, "write"), "WRITE_SIZE")
+    st = stats(os.path.join(root, "trace"))
+    bench = {}
+    try:
+        bench = json.loads(open(os.path.join(root, "bench_trace.json")).read().strip().splitlines()[-1])
+    except Exception:
+        pass
+    res = {"bench_under_trace": {k: bench.get(k) for k in ("value", "ms_per_step", "config")},
+           "roofline_under_trace": bench.get("roofline"),
+           "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) * 1024 B (gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md)",
+           "kernels": {}}
+    for key in KERNELS:
+        if key not in fetch and key not in st:
+            continue
+        f = fetch.get(key, [])
+        w = write.get(key, [])
+        fk = sum(f) / len(f) if f else None
+        wk = sum(w) / len(w) if w else None
+        e = {"FETCH_SIZE_kB_avg": fk, "WRITE_SIZE_kB_avg": wk, "dispatches": [len(f), len(w)],
+             "trace": st.get(key)}
+        if fk is not None and wk is not None:
+            e["hbm_bytes_per_launch"] = (2.0 * fk + wk) * 1024.0
+            if st.get(key):
+                e["hbm_GBs"] = e["hbm_bytes_per_launch"] / (st[key]["avg_ns"] * 1e-9) / 1e9
+        res["kernels"][key] = e
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

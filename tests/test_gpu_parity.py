@@ -86,12 +86,12 @@ def build_pair(mesh, order, alpha, beta, kernel=E.KERNEL_AUTO, numbering=E.NUMBE
     return fes, form, op
 
 
-KERNELS = {"tpe": E.KERNEL_TPE, "wpe": E.KERNEL_WPE, "unfused": E.KERNEL_UNFUSED}
+KERNELS = {"tpe": E.KERNEL_TPE, "wpe": E.KERNEL_WPE, "unfused": E.KERNEL_UNFUSED, "line": E.KERNEL_LINE}
 
 
 @pytest.mark.parametrize("mesh_name", ["nonaligned", "fichera_r1", "inline_hex", "cart_130", "cart_bricks"])
 @pytest.mark.parametrize("order", [1, 2, 3, 4])
-@pytest.mark.parametrize("kernel", ["tpe", "wpe", "unfused"])
+@pytest.mark.parametrize("kernel", ["tpe", "wpe", "unfused", "line"])
 def test_mult_matches_oracle(mesh_name, order, kernel):
     if kernel == "tpe" and order > 2:
         pytest.skip("thread-per-element kernel covers p = 1, 2")

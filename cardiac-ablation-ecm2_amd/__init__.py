@@ -461,6 +461,23 @@ _PAR_SIGS = {
     "ecm2_par_form_destroy": (None, [ctypes.c_void_p]),
     "ecm2_mesh_quadrature_points_subset": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                                           ctypes.c_int, ctypes.c_void_p]),
+    "ecm2_par_form_assemble_diagonal": (ctypes.c_int, [ctypes.c_void_p] * 3),
+    "ecm2_par_group_diagonal": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+    "ecm2_operator_from_pa_form": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "ecm2_operator_from_par_form": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "ecm2_operator_from_par_group": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "ecm2_operator_size": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
+    "ecm2_operator_mult": (ctypes.c_int, [ctypes.c_void_p] * 4),
+    "ecm2_operator_pcg": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                                         ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double),
+                                         ctypes.c_void_p]),
+    "ecm2_ode_implicit_coeff": (ctypes.c_double, [ctypes.c_int]),
+    "ecm2_ode_step": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
+                                     ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                     ctypes.POINTER(ctypes.c_int), ctypes.c_void_p]),
+    "ecm2_operator_destroy": (None, [ctypes.c_void_p]),
 }
 
 
@@ -584,6 +601,10 @@ class ParBilinearForm:
     def Mult(self, x, y, stream=None):
         _check(_par_lib().ecm2_par_form_mult(self._h, _dev_ptr(x), _dev_ptr(y), _stream(stream)))
 
+    def AssembleDiagonal(self, d, stream=None):
+        """Diagonal of P^T A P on this rank's true dofs (collective over the RCCL ranks)."""
+        _check(_par_lib().ecm2_par_form_assemble_diagonal(self._h, _dev_ptr(d), _stream(stream)))
+
     def timing(self, enable: bool):
         _check(_par_lib().ecm2_par_form_timing(self._h, 1 if enable else 0))
 
@@ -616,3 +637,81 @@ class ParGroup:
         ya = (ctypes.c_void_p * n)(*[_dev_ptr(y).value for y in ys])
         _check(_par_lib().ecm2_par_group_mult(ctypes.cast(fa, ctypes.c_void_p), n, ctypes.cast(xa, ctypes.c_void_p),
                                               ctypes.cast(ya, ctypes.c_void_p), _stream(stream)))
+
+    def AssembleDiagonal(self, ds, stream=None):
+        n = len(self.forms)
+        fa = (ctypes.c_void_p * n)(*[f._h.value for f in self.forms])
+        da = (ctypes.c_void_p * n)(*[_dev_ptr(d).value for d in ds])
+        _check(_par_lib().ecm2_par_group_diagonal(ctypes.cast(fa, ctypes.c_void_p), n, ctypes.cast(da, ctypes.c_void_p),
+                                                  _stream(stream)))
+
+    @property
+    def offsets(self):
+        """Offsets of the members' true vectors in the group's concatenated true vector."""
+        return np.cumsum([0] + [f.true_size for f in self.forms])
+
+
+class Operator:
+    """The solvers' view of a form (the reference's Operator, operator.hpp:24-110): a serial
+    BilinearForm, one RCCL rank's ParBilinearForm (collective solvers), or a ParGroup
+    (vectors = concatenated true vectors of its members)."""
+
+    def __init__(self, form):
+        lib = _par_lib()
+        h = ctypes.c_void_p()
+        if isinstance(form, BilinearForm):
+            _check(lib.ecm2_operator_from_pa_form(form._h, ctypes.byref(h)))
+        elif isinstance(form, ParBilinearForm):
+            _check(lib.ecm2_operator_from_par_form(form._h, ctypes.byref(h)))
+        elif isinstance(form, ParGroup):
+            n = len(form.forms)
+            fa = (ctypes.c_void_p * n)(*[f._h.value for f in form.forms])
+            _check(lib.ecm2_operator_from_par_group(ctypes.cast(fa, ctypes.c_void_p), n, ctypes.byref(h)))
+        else:
+            raise ECM2Error(f"no operator for {type(form).__name__}")
+        self._h = h
+        self.form = form  # keeps the form(s) alive while the operator exists
+        n = ctypes.c_int()
+        _check(lib.ecm2_operator_size(h, ctypes.byref(n)))
+        self.size = n.value
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.ecm2_operator_destroy(self._h)
+            self._h = None
+
+    def Mult(self, x, y, stream=None):
+        _check(_par_lib().ecm2_operator_mult(self._h, _dev_ptr(x), _dev_ptr(y), _stream(stream)))
+
+    def PCG(self, b, x, ess=None, rel_tol=1e-12, abs_tol=0.0, max_iter=1000, jacobi=True, stream=None):
+        """ConstrainedOperator(DIAG_ONE) + CGSolver(+OperatorJacobiSmoother); returns (iters, final_norm)."""
+        it, nrm = ctypes.c_int(), ctypes.c_double()
+        n_ess = 0 if ess is None else int(ess.numel())
+        _check(_par_lib().ecm2_operator_pcg(self._h, _dev_ptr(ess) if n_ess else None, n_ess, _dev_ptr(b), _dev_ptr(x),
+                                            rel_tol, abs_tol, max_iter, 1 if jacobi else 0,
+                                            ctypes.byref(it), ctypes.byref(nrm), _stream(stream)))
+        return it.value, nrm.value
+
+
+ODE_BACKWARD_EULER, ODE_SDIRK23_L, ODE_SDIRK33, ODE_IMPLICIT_MIDPOINT, ODE_SDIRK23, ODE_SDIRK34 = 21, 22, 23, 32, 33, 34
+
+
+def ode_implicit_coeff(ode_type: int) -> float:
+    """Stage coefficient c of ODESolver type (ode.cpp:77-91): stages solve (M + c dt K) k = -K u."""
+    c = _par_lib().ecm2_ode_implicit_coeff(ode_type)
+    if c == 0.0:
+        raise ECM2Error(f"unsupported implicit ODE solver type {ode_type}")
+    return c
+
+
+def ode_step(ode_type: int, T: Operator, K: Operator, dt: float, u, ess=None, rel_tol=1e-10, max_iter=500,
+             jacobi=True, stream=None):
+    """One implicit step of M du/dt = -K u (ex16 ConductionOperator, slope form) on device vector u
+    (in place).  T must be M + c dt K with c = ode_implicit_coeff(ode_type).
+    Returns (stage solves, total PCG iterations, converged)."""
+    ns, it, conv = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    n_ess = 0 if ess is None else int(ess.numel())
+    _check(_par_lib().ecm2_ode_step(ode_type, T._h, K._h, dt, _dev_ptr(u), _dev_ptr(ess) if n_ess else None, n_ess,
+                                    rel_tol, max_iter, 1 if jacobi else 0, ctypes.byref(ns), ctypes.byref(it),
+                                    ctypes.byref(conv), _stream(stream)))
+    return ns.value, it.value, bool(conv.value)

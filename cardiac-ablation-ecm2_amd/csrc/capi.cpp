@@ -7,8 +7,10 @@
 #include "pa_form.hpp"
 #include "par_form.hpp"
 #include "partition.hpp"
+#include "solvers.hpp"
 
 #include <cstring>
+#include <memory>
 #include <string>
 
 struct ecm2_mesh
@@ -30,6 +32,10 @@ struct ecm2_partition
 struct ecm2_par_form
 {
    ecm2::ParPAForm *f;
+};
+struct ecm2_operator
+{
+   std::unique_ptr<ecm2::LinOp> op;
 };
 
 namespace
@@ -550,6 +556,108 @@ int ecm2_par_group_mult(ecm2_par_form *const *forms, int n, const double *const 
       ecm2::par_group_mult(fs, xs, ys, S(stream));
    });
 }
+
+int ecm2_par_form_assemble_diagonal(ecm2_par_form *f, double *d_true, void *stream)
+{
+   return guard([&] { NEED(f); NEED(d_true); f->f->assemble_diagonal(d_true, S(stream)); });
+}
+
+int ecm2_par_group_diagonal(ecm2_par_form *const *forms, int n, double *const *d_true, void *stream)
+{
+   return guard([&] {
+      NEED(forms); NEED(d_true);
+      std::vector<ecm2::ParPAForm *> fs;
+      std::vector<double *> ds;
+      for (int i = 0; i < n; i++)
+      {
+         NEED(forms[i]);
+         fs.push_back(forms[i]->f);
+         ds.push_back(d_true[i]);
+      }
+      ecm2::par_group_diagonal(fs, ds, S(stream));
+   });
+}
+
+// ---- operators and their solvers ----
+int ecm2_operator_from_pa_form(ecm2_pa_form *f, ecm2_operator **out)
+{
+   return guard([&] {
+      NEED(f); NEED(out);
+      *out = new ecm2_operator{std::unique_ptr<ecm2::LinOp>(new ecm2::FormOp(*f->f))};
+   });
+}
+
+int ecm2_operator_from_par_form(ecm2_par_form *f, ecm2_operator **out)
+{
+   return guard([&] {
+      NEED(f); NEED(out);
+      *out = new ecm2_operator{std::unique_ptr<ecm2::LinOp>(new ecm2::ParFormOp(*f->f))};
+   });
+}
+
+int ecm2_operator_from_par_group(ecm2_par_form *const *forms, int n, ecm2_operator **out)
+{
+   return guard([&] {
+      NEED(forms); NEED(out);
+      ECM2_VERIFY(n > 0, ecm2::ERR_ARG, "empty group");
+      std::vector<ecm2::ParPAForm *> fs;
+      for (int i = 0; i < n; i++)
+      {
+         NEED(forms[i]);
+         ECM2_VERIFY(forms[i]->f->part().rank == i && forms[i]->f->part().nranks == n, ecm2::ERR_ARG,
+                     "loopback group: form " << i << " has rank " << forms[i]->f->part().rank);
+         fs.push_back(forms[i]->f);
+      }
+      *out = new ecm2_operator{std::unique_ptr<ecm2::LinOp>(new ecm2::GroupOp(fs))};
+   });
+}
+
+int ecm2_operator_size(const ecm2_operator *op, int *n)
+{
+   return guard([&] { NEED(op); NEED(n); *n = op->op->size(); });
+}
+
+int ecm2_operator_mult(ecm2_operator *op, const double *x, double *y, void *stream)
+{
+   return guard([&] { NEED(op); NEED(x); NEED(y); op->op->mult(x, y, S(stream)); });
+}
+
+int ecm2_operator_pcg(ecm2_operator *op, const int *ess, int n_ess, const double *b, double *x,
+                      double rel_tol, double abs_tol, int max_iter, int jacobi, int *iterations,
+                      double *final_norm, void *stream)
+{
+   return guard([&] {
+      NEED(op); NEED(b); NEED(x);
+      ECM2_VERIFY(n_ess == 0 || ess, ecm2::ERR_ARG, "null essential dof list");
+      const ecm2::PCGResult r = ecm2::pcg_solve(*op->op, ess, n_ess, b, x, rel_tol, abs_tol, max_iter,
+                                                jacobi != 0, S(stream));
+      if (iterations) { *iterations = r.iterations; }
+      if (final_norm) { *final_norm = r.final_norm; }
+   });
+}
+
+double ecm2_ode_implicit_coeff(int type)
+{
+   try { return ecm2::ode_implicit_coeff(type); }
+   catch (...) { return 0.0; }
+}
+
+int ecm2_ode_step(int type, ecm2_operator *T, ecm2_operator *K, double dt, double *u, const int *ess,
+                  int n_ess, double rel_tol, int max_iter, int jacobi, int *solves, int *iterations,
+                  int *converged, void *stream)
+{
+   return guard([&] {
+      NEED(T); NEED(K); NEED(u);
+      ECM2_VERIFY(n_ess == 0 || ess, ecm2::ERR_ARG, "null essential dof list");
+      const ecm2::StepStats st = ecm2::ode_step(type, *T->op, *K->op, dt, u, ess, n_ess, rel_tol, max_iter,
+                                                jacobi != 0, S(stream));
+      if (solves) { *solves = st.solves; }
+      if (converged) { *converged = st.converged ? 1 : 0; }
+      if (iterations) { *iterations = st.iterations; }
+   });
+}
+
+void ecm2_operator_destroy(ecm2_operator *op) { delete op; }
 
 int ecm2_par_form_timing(ecm2_par_form *f, int enable)
 {

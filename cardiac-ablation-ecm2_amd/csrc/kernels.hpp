@@ -101,6 +101,8 @@ std::vector<double> make_row_table(const DofToQuad &m);
 // through an encoded map [e][nd] (dof | shared << 30 | sign << 31); shared dofs go to
 // part[e*nd + a] when a.part is set, else atomics.  has_line: (D, Q) instantiated.
 bool has_line(int D, int Q);
+// Write the constant-memory basis table of (D, Q) on the current device (once).
+void upload_basis(int D, int Q, const Basis1D &b);
 void apply_line(int D, int Q, bool mass, bool diff, const ApplyArgs &a, const Basis1D &b, hipStream_t s);
 // Workgroup-per-element kernel, any layout; in/out either L-vectors (through the
 // gather map; output by atomics into a zeroed y) or E-vectors (accumulated).
@@ -133,6 +135,8 @@ void pcg_precond(int n, const double *dinv, const double *r, double *z, hipStrea
 void pcg_update_d(int n, const double *betanom, const double *nom, const double *z, double *d,
                   hipStream_t s);
 void reciprocal(int n, const double *a, double *out, hipStream_t s);
+void scale(int n, double a, double *y, hipStream_t s);                                   // y *= a
+void add_scaled(int n, const double *x, double c, const double *k, double *out, hipStream_t s); // out = x + c k
 // b = a with 16-byte nontemporal accesses (HBM STREAM-copy measurement)
 void stream_copy(long n, const double *a, double *b, hipStream_t s);
 // Halo pack/unpack for the distributed operator (K7): buf[i] = x[idx[i]] ; y[idx[i]] += buf[i]

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 namespace ecm2
@@ -202,6 +203,18 @@ void PAForm::build_shared_plan(const std::vector<int> &hcount, const std::vector
    sh_slots_.upload(slots, s);
 }
 
+// Longest chunk of x-adjacent elements one wave of the line kernel walks (1..8;
+// ECM2_LINE_CHUNK overrides the default for experiments).
+static int line_chunk_max()
+{
+   static int v = [] {
+      const char *e = std::getenv("ECM2_LINE_CHUNK");
+      const int c = e ? std::atoi(e) : 8;
+      return c < 1 ? 1 : (c > 8 ? 8 : c);
+   }();
+   return v;
+}
+
 void PAForm::set_kernel(int mode)
 {
    ECM2_VERIFY(mode >= KERNEL_AUTO && mode <= KERNEL_LINE, ERR_ARG, "unknown kernel mode " << mode);
@@ -277,6 +290,7 @@ void PAForm::assemble(hipStream_t s)
       rowtab_.upload(kern::make_row_table(maps_), s);
       ECM2_HIP(hipStreamSynchronize(s));
    }
+   if (resolved_mode_ == KERNEL_LINE) { kern::upload_basis(D_, Q_, basis_); }
    if (resolved_mode_ == KERNEL_LINE && !gmap_line_.size() && ne_ > 0)
    {
       // chunks of up to 8 consecutive elements whose x-faces coincide (never crossing a
@@ -309,7 +323,7 @@ void PAForm::assemble(hipStream_t s)
          while (e < ee)
          {
             int n = 1;
-            while (n < 8 && e + n < ee && xface_match(e + n - 1)) { n++; }
+            while (n < line_chunk_max() && e + n < ee && xface_match(e + n - 1)) { n++; }
             chunks.push_back(e | (n << 24));
             for (int k = 0; k + 1 < n; k++)
                for (int dz = 0; dz < D_; dz++)
@@ -615,93 +629,5 @@ void PAForm::get_qdata(int kind, double *out, hipStream_t s)
 // --------------------------------------------------------------------------
 // Device PCG
 // --------------------------------------------------------------------------
-
-PCGResult pcg_solve(PAForm &A, const int *ess, int n_ess, const double *b, double *x,
-                    double rel_tol, double abs_tol, int max_iter, bool jacobi, hipStream_t s)
-{
-   const int n = A.ndofs();
-   PCGResult res;
-   if (n == 0) { res.converged = true; return res; }
-   DeviceArray<double> r(n), d(n), z(n), zc(n), partials(1024), scal(4), dinv;
-   double *nom = scal.data(), *den = scal.data() + 1, *betanom = scal.data() + 2;
-   double *hs = nullptr;
-   ECM2_HIP(hipHostMalloc(&hs, 4 * sizeof(double)));
-   auto readback = [&](const double *dv) {
-      ECM2_HIP(hipMemcpyAsync(hs, dv, sizeof(double), hipMemcpyDeviceToHost, s));
-      ECM2_HIP(hipStreamSynchronize(s));
-      return hs[0];
-   };
-   // ConstrainedOperator::ConstrainedMult, DIAG_ONE.
-   auto cmult = [&](const double *in, double *out) {
-      if (n_ess == 0) { A.mult(in, out, s); return; }
-      ECM2_HIP(hipMemcpyAsync(zc.data(), in, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
-      kern::set_values(n_ess, ess, 0.0, zc.data(), s);
-      A.mult(zc.data(), out, s);
-      kern::copy_values(n_ess, ess, in, out, s);
-   };
-   try
-   {
-      if (jacobi)
-      {
-         // OperatorJacobiSmoother on the constrained operator: ess rows get diag 1.
-         dinv.resize(n);
-         A.assemble_diagonal(z.data(), s);
-         if (n_ess) { kern::set_values(n_ess, ess, 1.0, z.data(), s); }
-         kern::reciprocal(n, z.data(), dinv.data(), s);
-      }
-      ECM2_HIP(hipMemcpyAsync(r.data(), b, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
-      ECM2_HIP(hipMemsetAsync(x, 0, sizeof(double) * n, s));
-      if (jacobi)
-      {
-         kern::pcg_precond(n, dinv.data(), r.data(), z.data(), s);
-         ECM2_HIP(hipMemcpyAsync(d.data(), z.data(), sizeof(double) * n, hipMemcpyDeviceToDevice, s));
-      }
-      else
-      {
-         ECM2_HIP(hipMemcpyAsync(d.data(), r.data(), sizeof(double) * n, hipMemcpyDeviceToDevice, s));
-      }
-      kern::dot(n, d.data(), r.data(), partials.data(), nom, s);
-      const double nom0 = readback(nom);
-      res.initial_norm = nom0 >= 0 ? std::sqrt(nom0) : nom0;
-      const double r0 = std::max(nom0 * rel_tol * rel_tol, abs_tol * abs_tol);
-      res.final_norm = res.initial_norm;
-      if (nom0 <= r0) { res.converged = true; }
-      else
-      {
-         cmult(d.data(), z.data());
-         kern::dot(n, z.data(), d.data(), partials.data(), den, s);
-         if (readback(den) != 0.0)
-         {
-            for (int i = 1;;)
-            {
-               kern::pcg_update_xr(n, nom, den, d.data(), z.data(), x, r.data(), s);
-               if (jacobi)
-               {
-                  kern::pcg_precond(n, dinv.data(), r.data(), z.data(), s);
-                  kern::dot(n, r.data(), z.data(), partials.data(), betanom, s);
-               }
-               else { kern::dot(n, r.data(), r.data(), partials.data(), betanom, s); }
-               const double bn = readback(betanom);
-               res.final_norm = bn >= 0 ? std::sqrt(bn) : bn;
-               res.iterations = i;
-               if (bn <= r0) { res.converged = true; break; }
-               if (++i > max_iter) { break; }
-               kern::pcg_update_d(n, betanom, nom, jacobi ? z.data() : r.data(), d.data(), s);
-               cmult(d.data(), z.data());
-               kern::dot(n, d.data(), z.data(), partials.data(), den, s);
-               ECM2_HIP(hipMemcpyAsync(nom, betanom, sizeof(double), hipMemcpyDeviceToDevice, s));
-            }
-         }
-      }
-   }
-   catch (...)
-   {
-      (void)hipHostFree(hs);
-      throw;
-   }
-   ECM2_HIP(hipStreamSynchronize(s));
-   (void)hipHostFree(hs);
-   return res;
-}
 
 } // namespace ecm2

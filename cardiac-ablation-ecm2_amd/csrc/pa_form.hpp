@@ -162,18 +162,4 @@ private:
    size_t ev_count_ = 0;
 };
 
-// Device PCG on the constrained operator (ConstrainedOperator DIAG_ONE,
-// operator.cpp:586-646; CGSolver::Mult solvers.cpp:869-1004) with optional
-// Jacobi preconditioning from the PA diagonal.  Scalars stay on the device;
-// one 8-byte read-back per iteration for the convergence test.
-struct PCGResult
-{
-   int iterations = 0;
-   double final_norm = 0.0, initial_norm = 0.0;
-   bool converged = false;
-};
-class Operator;
-PCGResult pcg_solve(PAForm &A, const int *ess_dev, int n_ess, const double *b, double *x,
-                    double rel_tol, double abs_tol, int max_iter, bool jacobi, hipStream_t s);
-
 } // namespace ecm2

@@ -20,6 +20,10 @@
 // mass setup bilininteg_mass_pa.cpp:60-78, GeometricFactors mesh.cpp:15220-15273).
 #include "kernels.hpp"
 
+#include <mutex>
+#include <set>
+#include <tuple>
+
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -749,6 +753,23 @@ __global__ void k_apply_wpe(const int *__restrict__ pos, int kind, int ne, int e
 // gmap: [e][ND] encoded dof | shared << 30 | sign << 31 (see PAForm::assemble);
 // chunks[c] = first element | count << 24 (count <= 8).
 // --------------------------------------------------------------------------
+// Basis tables in constant memory, one per (D1D, Q1D): the H1 GLL basis at the
+// Gauss-Legendre points is a pure function of the pair, so a table is written once per
+// device (kern::upload_basis) and never changes.  The line kernel reads them through
+// a pointer laundered at every stage (asm barrier), so the compiler issues scalar loads
+// where they are used instead of hoisting 2*D*Q doubles out of the element loop (which
+// exceeds the SGPR file and spills to VGPR lanes).
+__constant__ Basis1D c_basis[MAX_D1D][MAX_Q1D];
+typedef const __attribute__((address_space(4))) Basis1D CBasis;
+
+template <int D, int Q>
+__device__ __forceinline__ CBasis *stage_basis()
+{
+   CBasis *p = (CBasis *)&c_basis[D - 1][Q - 1];
+   asm volatile("" : "+s"(p));
+   return p;
+}
+
 template <int D, int Q, bool MASS, bool DIFF>
 __device__ __forceinline__ void line_load_qdata(double (&qv)[7][Q], int e, int t,
                                                 const double *__restrict__ qdd,
@@ -770,7 +791,7 @@ __device__ __forceinline__ void line_load_qdata(double (&qv)[7][Q], int e, int t
    }
 }
 
-template <int D, int Q, bool MASS, bool DIFF, bool SPLIT>
+template <int D, int Q, bool MASS, bool DIFF, bool SPLIT, int VAR>
 __global__ void __launch_bounds__(64)
 k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned,
              const int *__restrict__ gmap,
@@ -792,16 +813,18 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned
    const int e0 = ch & 0xffffff, cnt = ch >> 24;
 
    double qv[7][Q];
-   line_load_qdata<D, Q, MASS, DIFF>(qv, e0, t, qdd, qdm);
+   if (!(VAR & 2)) { line_load_qdata<D, Q, MASS, DIFF>(qv, e0, t, qdd, qdm); }
    double carry = 0.0;
 #pragma unroll 1
    for (int k = 0; k < cnt; k++)
    {
       const int e = e0 + k;
+      if (VAR & 2) { line_load_qdata<D, Q, MASS, DIFF>(qv, e, t, qdd, qdm); }
       // ---- lanes (dy, dz): gather the x-line, contract in x
       int gl[D];
       if (t < DD)
       {
+         CBasis *bp = stage_basis<D, Q>();
          const int *mp = gmap + (size_t)e * ND + t * D;
          double xl[D];
 #pragma unroll
@@ -820,8 +843,8 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned
 #pragma unroll
             for (int dx = 0; dx < D; dx++)
             {
-               u += b.B[qx + MQ * dx] * xl[dx];
-               v += b.G[qx + MQ * dx] * xl[dx];
+               u += bp->B[qx + MQ * dx] * xl[dx];
+               v += bp->G[qx + MQ * dx] * xl[dx];
             }
             bufA[t * Q + qx] = u;            // B_x   [dz][dy][qx]
             bufA[DD * Q + t * Q + qx] = v;   // G_x
@@ -831,6 +854,7 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned
       // ---- lanes (qx, dz): contract in y
       if (t < DQ)
       {
+         CBasis *bp = stage_basis<D, Q>();
          const int qx = t % Q, dz = t / Q;
          double la[D], lb[D];
 #pragma unroll
@@ -846,7 +870,7 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned
 #pragma unroll
             for (int dy = 0; dy < D; dy++)
             {
-               const double by = b.B[qy + MQ * dy], gy = b.G[qy + MQ * dy];
+               const double by = bp->B[qy + MQ * dy], gy = bp->G[qy + MQ * dy];
                gb += by * lb[dy];  // G_x B_y
                bg += gy * la[dy];  // B_x G_y
                bb += by * la[dy];  // B_x B_y
@@ -861,6 +885,7 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned
       // ---- lanes (qx, qy): contract in z, weight at the quadrature points, transpose in z
       if (t < QQ)
       {
+         CBasis *bp = stage_basis<D, Q>();
          double l0[D], l1[D], l2[D];
 #pragma unroll
          for (int dz = 0; dz < D; dz++)
@@ -879,7 +904,7 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned
 #pragma unroll
             for (int dz = 0; dz < D; dz++)
             {
-               const double bz = b.B[qz + MQ * dz], gzz = b.G[qz + MQ * dz];
+               const double bz = bp->B[qz + MQ * dz], gzz = bp->G[qz + MQ * dz];
                if (DIFF)
                {
                   gx += bz * l0[dz];
@@ -899,7 +924,7 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned
 #pragma unroll
             for (int dz = 0; dz < D; dz++)
             {
-               const double bz = b.B[qz + MQ * dz], gzz = b.G[qz + MQ * dz];
+               const double bz = bp->B[qz + MQ * dz], gzz = bp->G[qz + MQ * dz];
                if (DIFF)
                {
                   A1[dz] += bz * fx;               // -> G_x B_y
@@ -918,11 +943,12 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned
          }
       }
       // next element's qdata: in flight during the rest of this element
-      if (k + 1 < cnt) { line_load_qdata<D, Q, MASS, DIFF>(qv, e + 1, t, qdd, qdm); }
+      if (!(VAR & 2) && k + 1 < cnt) { line_load_qdata<D, Q, MASS, DIFF>(qv, e + 1, t, qdd, qdm); }
       __syncthreads();
       // ---- lanes (qx, dz): transpose in y
       if (t < DQ)
       {
+         CBasis *bp = stage_basis<D, Q>();
          const int qx = t % Q, dz = t / Q;
          double l0[Q], l1[Q], l2[Q];
 #pragma unroll
@@ -940,7 +966,7 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned
 #pragma unroll
             for (int qy = 0; qy < Q; qy++)
             {
-               const double by = b.B[qy + MQ * dy], gy = b.G[qy + MQ * dy];
+               const double by = bp->B[qy + MQ * dy], gy = bp->G[qy + MQ * dy];
                c1 += by * l0[qy];                 // -> G_x
                c2 += gy * l1[qy] + by * l2[qy];   // -> B_x
             }
@@ -952,6 +978,7 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned
       // ---- lanes (dy, dz): transpose in x, face carry, scatter
       if (t < DD)
       {
+         CBasis *bp = stage_basis<D, Q>();
          double l0[Q], l1[Q];
 #pragma unroll
          for (int qx = 0; qx < Q; qx++)
@@ -965,7 +992,7 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned
          {
             double v = 0.0;
 #pragma unroll
-            for (int qx = 0; qx < Q; qx++) { v += b.G[qx + MQ * dx] * l0[qx] + b.B[qx + MQ * dx] * l1[qx]; }
+            for (int qx = 0; qx < Q; qx++) { v += bp->G[qx + MQ * dx] * l0[qx] + bp->B[qx + MQ * dx] * l1[qx]; }
             const int g = gl[dx];
             if (bneg(g)) { v = -v; }
             if (dx == 0) { v += carry; }
@@ -1115,6 +1142,19 @@ __global__ void k_pcg_update_d(int n, const double *__restrict__ betanom,
    if (i >= n) { return; }
    const double beta = *betanom / *nom;
    d[i] = z[i] + beta * d[i];
+}
+
+__global__ void k_scale(int n, double a, double *__restrict__ y)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { y[i] *= a; }
+}
+
+// out = x + c k  (out may alias x)
+__global__ void k_add_scaled(int n, const double *x, double c, const double *__restrict__ k, double *out)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { out[i] = x[i] + c * k[i]; }
 }
 
 // STREAM copy (measurement only): 16-byte nontemporal loads and stores, grid-stride,
@@ -1351,6 +1391,17 @@ void apply_tpe(int D, int Q, bool mass, bool diff, const ApplyArgs &a, const Bas
    ECM2_HIP(hipGetLastError());
 }
 
+// experiment knob ECM2_LINE_VARIANT: bit 1 = load each element's qdata at the top of its
+// iteration instead of prefetching it during the previous element
+int line_variant()
+{
+   static int v = [] {
+      const char *e = std::getenv("ECM2_LINE_VARIANT");
+      return e ? std::atoi(e) : 0;
+   }();
+   return v;
+}
+
 template <int D, int Q, bool MASS, bool DIFF>
 void launch_line_mdq(const ApplyArgs &a, const Basis1D &b, hipStream_t s)
 {
@@ -1358,16 +1409,13 @@ void launch_line_mdq(const ApplyArgs &a, const Basis1D &b, hipStream_t s)
    const int c0 = a.chunk_off[a.blk_begin], c1 = a.chunk_off[a.blk_end];
    if (c1 <= c0) { return; }
    const dim3 grid(c1 - c0), block(64);
-   if (a.xg || a.yg)
-   {
-      hipLaunchKernelGGL((k_apply_line<D, Q, MASS, DIFF, true>), grid, block, 0, s, c0, c1, a.chunks, a.n_owned,
-                         a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.part);
-   }
-   else
-   {
-      hipLaunchKernelGGL((k_apply_line<D, Q, MASS, DIFF, false>), grid, block, 0, s, c0, c1, a.chunks, a.n_owned,
-                         a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.part);
-   }
+#define ECM2_LINE(SP, V)                                                                                  \
+   hipLaunchKernelGGL((k_apply_line<D, Q, MASS, DIFF, SP, V>), grid, block, 0, s, c0, c1, a.chunks, a.n_owned, \
+                      a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.part)
+   const bool split = a.xg || a.yg;
+   if (line_variant() & 2) { if (split) { ECM2_LINE(true, 2); } else { ECM2_LINE(false, 2); } }
+   else { if (split) { ECM2_LINE(true, 0); } else { ECM2_LINE(false, 0); } }
+#undef ECM2_LINE
 }
 
 template <int D, int Q>
@@ -1381,6 +1429,19 @@ void launch_line_dq(bool mass, bool diff, const ApplyArgs &a, const Basis1D &b, 
 bool has_line(int D, int Q)
 {
    return (Q == D + 1 || Q == D) && D >= 2 && D <= 7 && Q <= 8;
+}
+
+void upload_basis(int D, int Q, const Basis1D &b)
+{
+   static std::mutex mu;
+   static std::set<std::tuple<int, int, int>> done;  // (device, D, Q)
+   int dev = 0;
+   ECM2_HIP(hipGetDevice(&dev));
+   std::lock_guard<std::mutex> lock(mu);
+   if (!done.insert({dev, D, Q}).second) { return; }
+   ECM2_VERIFY(D >= 1 && D <= MAX_D1D && Q >= 1 && Q <= MAX_Q1D, ERR_ARG, "basis size");
+   ECM2_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_basis), &b, sizeof(Basis1D),
+                              ((size_t)(D - 1) * MAX_Q1D + (Q - 1)) * sizeof(Basis1D), hipMemcpyHostToDevice));
 }
 
 void apply_line(int D, int Q, bool mass, bool diff, const ApplyArgs &a, const Basis1D &b, hipStream_t s)
@@ -1497,6 +1558,20 @@ void pcg_update_d(int n, const double *betanom, const double *nom, const double 
                   hipStream_t s)
 {
    hipLaunchKernelGGL(k_pcg_update_d, dim3(grid_for(n, 256)), dim3(256), 0, s, n, betanom, nom, z, d);
+   ECM2_HIP(hipGetLastError());
+}
+
+void scale(int n, double a, double *y, hipStream_t s)
+{
+   if (n <= 0) { return; }
+   hipLaunchKernelGGL(k_scale, dim3(grid_for(n, 256)), dim3(256), 0, s, n, a, y);
+   ECM2_HIP(hipGetLastError());
+}
+
+void add_scaled(int n, const double *x, double c, const double *k, double *out, hipStream_t s)
+{
+   if (n <= 0) { return; }
+   hipLaunchKernelGGL(k_add_scaled, dim3(grid_for(n, 256)), dim3(256), 0, s, n, x, c, k, out);
    ECM2_HIP(hipGetLastError());
 }
 

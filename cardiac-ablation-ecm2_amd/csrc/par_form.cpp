@@ -150,6 +150,49 @@ void ParPAForm::mult(const double *x_true, double *y_true, hipStream_t s)
    phase_finish(y_true, s);
 }
 
+void ParPAForm::diag_local(double *d_true, hipStream_t s)
+{
+   const int nl = part_.n_owned + part_.n_ghost;
+   dl_.resize(std::max(1, nl));
+   local_->assemble_diagonal(dl_.data(), s);  // local L-vector [owned | ghost]
+   if (part_.n_owned)
+   {
+      ECM2_HIP(hipMemcpyAsync(d_true, dl_.data(), sizeof(double) * part_.n_owned, hipMemcpyDeviceToDevice, s));
+   }
+   if (part_.n_ghost)
+   {
+      ECM2_HIP(hipMemcpyAsync(yg_.data(), dl_.data() + part_.n_owned, sizeof(double) * part_.n_ghost,
+                              hipMemcpyDeviceToDevice, s));
+   }
+}
+
+void ParPAForm::assemble_diagonal(double *d_true, hipStream_t s)
+{
+   ECM2_VERIFY(comm_, ERR_STATE, "assemble_diagonal needs the RCCL transport (use the loopback group otherwise)");
+   ncclComm_t comm = (ncclComm_t)comm_;
+   diag_local(d_true, s);
+   const int nn = (int)part_.nbrs.size();
+   if (nn)
+   {
+      ECM2_NCCL(ncclGroupStart());
+      for (int k = 0; k < nn; k++)
+      {
+         const size_t ns = part_.recv_off[k + 1] - part_.recv_off[k];
+         const size_t nr = part_.send_off[k + 1] - part_.send_off[k];
+         if (ns) { ECM2_NCCL(ncclSend(yg_.data() + part_.recv_off[k], ns, ncclFloat64, part_.nbrs[k], comm, s)); }
+         if (nr) { ECM2_NCCL(ncclRecv(rbuf_.data() + part_.send_off[k], nr, ncclFloat64, part_.nbrs[k], comm, s)); }
+      }
+      ECM2_NCCL(ncclGroupEnd());
+   }
+   phase_finish(d_true, s);
+}
+
+void ParPAForm::allreduce_sum(double *dev, int n, hipStream_t s)
+{
+   ECM2_VERIFY(comm_, ERR_STATE, "allreduce needs the RCCL transport");
+   ECM2_NCCL(ncclAllReduce(dev, dev, n, ncclFloat64, ncclSum, (ncclComm_t)comm_, s));
+}
+
 void par_group_mult(std::vector<ParPAForm *> &forms, const std::vector<const double *> &x,
                     const std::vector<double *> &y, hipStream_t s)
 {
@@ -212,4 +255,40 @@ void par_group_mult(std::vector<ParPAForm *> &forms, const std::vector<const dou
    for (int r = 0; r < n; r++) { forms[r]->phase_finish(y[r], s); }
 }
 
+} // namespace ecm2
+
+namespace ecm2
+{
+// P^T of the loopback group: every member's ghost block (yghost) copied into its owner's
+// receive buffer, then added into the owner's true vector.
+static void group_reduce_ghosts(std::vector<ParPAForm *> &forms, const std::vector<double *> &y, hipStream_t s)
+{
+   const int n = (int)forms.size();
+   for (int r = 0; r < n; r++)
+   {
+      const LocalPart &pr = forms[r]->part();
+      for (size_t k = 0; k < pr.nbrs.size(); k++)
+      {
+         const int g = pr.nbrs[k];
+         const auto &nb = forms[g]->part().nbrs;
+         const int j = (int)(std::find(nb.begin(), nb.end(), r) - nb.begin());
+         ECM2_VERIFY(j < (int)nb.size(), ERR_INTERNAL, "asymmetric neighbour lists");
+         const LocalPart &pg = forms[g]->part();
+         const size_t cnt = pr.send_off[k + 1] - pr.send_off[k];
+         if (cnt)
+         {
+            ECM2_HIP(hipMemcpyAsync(forms[r]->recvbuf() + pr.send_off[k], forms[g]->yghost() + pg.recv_off[j],
+                                    cnt * sizeof(double), hipMemcpyDeviceToDevice, s));
+         }
+      }
+   }
+   for (int r = 0; r < n; r++) { forms[r]->phase_finish(y[r], s); }
+}
+
+void par_group_diagonal(std::vector<ParPAForm *> &forms, const std::vector<double *> &d, hipStream_t s)
+{
+   ECM2_VERIFY(d.size() == forms.size(), ERR_ARG, "group size mismatch");
+   for (size_t r = 0; r < forms.size(); r++) { forms[r]->diag_local(d[r], s); }
+   group_reduce_ghosts(forms, d, s);
+}
 } // namespace ecm2

@@ -38,6 +38,13 @@ public:
    void assemble(hipStream_t s);
    // y_true = P^T A P x_true (RCCL transport).
    void mult(const double *x_true, double *y_true, hipStream_t s);
+   // Diagonal of P^T A P on the true dofs: local PA diagonal, ghost entries summed into
+   // their owners (ParBilinearForm::AssembleDiagonal -> P^T d_local, pbilinearform.cpp).
+   void assemble_diagonal(double *d_true, hipStream_t s);
+   // In-place sum over ranks of n device doubles (the dots of the parallel PCG).
+   void allreduce_sum(double *dev, int n, hipStream_t s);
+   // Pieces of assemble_diagonal shared with the loopback group.
+   void diag_local(double *d_true, hipStream_t s);  // d_true = owned part, ghost part -> yghost()
 
    // Phases (used by mult and by the loopback group).
    void phase_pack(const double *x_true, double *y_true, hipStream_t s);
@@ -59,7 +66,7 @@ private:
    LocalPart part_;
    std::unique_ptr<PAForm> local_;
    DeviceArray<int> send_idx_;
-   DeviceArray<double> sendbuf_, xg_, yg_, rbuf_;
+   DeviceArray<double> sendbuf_, xg_, yg_, rbuf_, dl_;
    void *comm_ = nullptr;  // ncclComm_t
    hipStream_t cs_ = nullptr;
    hipEvent_t ev_pack_ = nullptr, ev_xg_ = nullptr, ev_yg_ = nullptr, ev_done_ = nullptr;
@@ -70,6 +77,7 @@ private:
 // ordering without RCCL (which cannot put two ranks on one device).
 void par_group_mult(std::vector<ParPAForm *> &forms, const std::vector<const double *> &x,
                     const std::vector<double *> &y, hipStream_t s);
+void par_group_diagonal(std::vector<ParPAForm *> &forms, const std::vector<double *> &d, hipStream_t s);
 
 void rccl_unique_id(unsigned char *out128);
 

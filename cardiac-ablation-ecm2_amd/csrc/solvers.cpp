@@ -1,0 +1,252 @@
+// solvers.cpp -- see solvers.hpp.
+#include "solvers.hpp"
+
+#include <algorithm>
+#include <cmath>
+
+namespace ecm2
+{
+
+// ---------------------------------------------------------------------------------------
+// loopback group as one operator
+// ---------------------------------------------------------------------------------------
+GroupOp::GroupOp(std::vector<ParPAForm *> forms) : forms_(std::move(forms))
+{
+   off_.assign(forms_.size() + 1, 0);
+   for (size_t r = 0; r < forms_.size(); r++) { off_[r + 1] = off_[r] + forms_[r]->true_size(); }
+   n_ = off_.back();
+}
+
+void GroupOp::mult(const double *x, double *y, hipStream_t s)
+{
+   std::vector<const double *> xs;
+   std::vector<double *> ys;
+   for (size_t r = 0; r < forms_.size(); r++)
+   {
+      xs.push_back(x + off_[r]);
+      ys.push_back(y + off_[r]);
+   }
+   par_group_mult(forms_, xs, ys, s);
+}
+
+void GroupOp::diagonal(double *d, hipStream_t s)
+{
+   std::vector<double *> ds;
+   for (size_t r = 0; r < forms_.size(); r++) { ds.push_back(d + off_[r]); }
+   par_group_diagonal(forms_, ds, s);
+}
+
+// ---------------------------------------------------------------------------------------
+// ConstrainedOperator + CGSolver + OperatorJacobiSmoother
+// ---------------------------------------------------------------------------------------
+PCGResult pcg_solve(LinOp &A, const int *ess, int n_ess, const double *b, double *x, double rel_tol,
+                    double abs_tol, int max_iter, bool jacobi, hipStream_t s)
+{
+   const int n = A.size();
+   PCGResult res;
+   DeviceArray<double> r(std::max(n, 1)), d(std::max(n, 1)), z(std::max(n, 1)), zc(std::max(n, 1));
+   DeviceArray<double> partials(1024), scal(4), dinv;
+   double *nom = scal.data(), *den = scal.data() + 1, *betanom = scal.data() + 2;
+   double *hs = nullptr;
+   ECM2_HIP(hipHostMalloc(&hs, 4 * sizeof(double)));
+   // every rank reads the same (globally summed) scalar, so all take the same branch
+   auto dot = [&](const double *a, const double *bb, double *out) {
+      kern::dot(n, a, bb, partials.data(), out, s);
+      A.sum_scalars(out, 1, s);
+   };
+   auto readback = [&](const double *dv) {
+      ECM2_HIP(hipMemcpyAsync(hs, dv, sizeof(double), hipMemcpyDeviceToHost, s));
+      ECM2_HIP(hipStreamSynchronize(s));
+      return hs[0];
+   };
+   // ConstrainedOperator::ConstrainedMult, DIAG_ONE (operator.cpp:586-646)
+   auto cmult = [&](const double *in, double *out) {
+      if (n_ess == 0) { A.mult(in, out, s); return; }
+      ECM2_HIP(hipMemcpyAsync(zc.data(), in, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+      kern::set_values(n_ess, ess, 0.0, zc.data(), s);
+      A.mult(zc.data(), out, s);
+      kern::copy_values(n_ess, ess, in, out, s);
+   };
+   try
+   {
+      if (jacobi)
+      {
+         // OperatorJacobiSmoother on the constrained operator: ess rows get diag 1
+         dinv.resize(std::max(n, 1));
+         A.diagonal(z.data(), s);
+         if (n_ess) { kern::set_values(n_ess, ess, 1.0, z.data(), s); }
+         kern::reciprocal(n, z.data(), dinv.data(), s);
+      }
+      if (n) { ECM2_HIP(hipMemcpyAsync(r.data(), b, sizeof(double) * n, hipMemcpyDeviceToDevice, s)); }
+      if (n) { ECM2_HIP(hipMemsetAsync(x, 0, sizeof(double) * n, s)); }
+      if (jacobi)
+      {
+         kern::pcg_precond(n, dinv.data(), r.data(), z.data(), s);
+         if (n) { ECM2_HIP(hipMemcpyAsync(d.data(), z.data(), sizeof(double) * n, hipMemcpyDeviceToDevice, s)); }
+      }
+      else if (n)
+      {
+         ECM2_HIP(hipMemcpyAsync(d.data(), r.data(), sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+      }
+      dot(d.data(), r.data(), nom);
+      const double nom0 = readback(nom);
+      res.initial_norm = nom0 >= 0 ? std::sqrt(nom0) : nom0;
+      const double r0 = std::max(nom0 * rel_tol * rel_tol, abs_tol * abs_tol);
+      res.final_norm = res.initial_norm;
+      if (nom0 <= r0) { res.converged = true; }
+      else
+      {
+         cmult(d.data(), z.data());
+         dot(z.data(), d.data(), den);
+         if (readback(den) != 0.0)
+         {
+            for (int i = 1;;)
+            {
+               kern::pcg_update_xr(n, nom, den, d.data(), z.data(), x, r.data(), s);
+               if (jacobi)
+               {
+                  kern::pcg_precond(n, dinv.data(), r.data(), z.data(), s);
+                  dot(r.data(), z.data(), betanom);
+               }
+               else { dot(r.data(), r.data(), betanom); }
+               const double bn = readback(betanom);
+               res.final_norm = bn >= 0 ? std::sqrt(bn) : bn;
+               res.iterations = i;
+               if (bn <= r0) { res.converged = true; break; }
+               if (++i > max_iter) { break; }
+               kern::pcg_update_d(n, betanom, nom, jacobi ? z.data() : r.data(), d.data(), s);
+               cmult(d.data(), z.data());
+               dot(d.data(), z.data(), den);
+               ECM2_HIP(hipMemcpyAsync(nom, betanom, sizeof(double), hipMemcpyDeviceToDevice, s));
+            }
+         }
+      }
+   }
+   catch (...)
+   {
+      (void)hipHostFree(hs);
+      throw;
+   }
+   ECM2_HIP(hipStreamSynchronize(s));
+   (void)hipHostFree(hs);
+   return res;
+}
+
+PCGResult pcg_solve(PAForm &A, const int *ess, int n_ess, const double *b, double *x, double rel_tol,
+                    double abs_tol, int max_iter, bool jacobi, hipStream_t s)
+{
+   FormOp op(A);
+   return pcg_solve(op, ess, n_ess, b, x, rel_tol, abs_tol, max_iter, jacobi, s);
+}
+
+// ---------------------------------------------------------------------------------------
+// SDIRK family (slope form, ImplicitVarType::SLOPE) on an ex16-style conduction operator
+// ---------------------------------------------------------------------------------------
+namespace
+{
+const double kSdirk33A = 0.435866521508458999416019;  // ode.cpp SDIRK33Solver::Step
+const double kSdirk33B = 1.20849664917601007033648;
+const double kSdirk33C = 0.717933260754229499708010;
+double sdirk34_a() { return 1. / std::sqrt(3.) * std::cos(M_PI / 18.) + 0.5; }
+double sdirk23_gamma(int type)
+{
+   return type == 22 ? (2. - std::sqrt(2.)) / 2.   // gamma_opt = 2: L-stable, order 2
+                     : (3. + std::sqrt(3.)) / 6.;  // default gamma_opt: A-stable, order 3
+}
+} // namespace
+
+bool ode_implicit_supported(int type)
+{
+   return type == 21 || type == 22 || type == 23 || type == 32 || type == 33 || type == 34;
+}
+
+double ode_implicit_coeff(int type)
+{
+   switch (type)
+   {
+      case 21: return 1.0;
+      case 22:
+      case 33: return sdirk23_gamma(type);
+      case 23: return kSdirk33A;
+      case 32: return 0.5;
+      case 34: return sdirk34_a();
+      default: break;
+   }
+   ECM2_VERIFY(false, ERR_ARG, "unsupported implicit ODE solver type " << type);
+   return 0.0;
+}
+
+StepStats ode_step(int type, LinOp &T, LinOp &K, double dt, double *u, const int *ess, int n_ess,
+                   double rel_tol, int max_iter, bool jacobi, hipStream_t s)
+{
+   ECM2_VERIFY(ode_implicit_supported(type), ERR_ARG, "unsupported implicit ODE solver type " << type);
+   ECM2_VERIFY(T.size() == K.size(), ERR_ARG, "T and K sizes differ");
+   const int n = T.size();
+   StepStats st;
+   DeviceArray<double> k(std::max(n, 1)), y(std::max(n, 1)), z(std::max(n, 1)), rhs(std::max(n, 1));
+   // ConductionOperator::ImplicitSolve (ex16.cpp:327-354), slope form: T k = -K u_stage
+   auto implicit_solve = [&](const double *us, double *kk) {
+      K.mult(us, rhs.data(), s);
+      kern::scale(n, -1.0, rhs.data(), s);
+      if (n_ess) { kern::set_values(n_ess, ess, 0.0, rhs.data(), s); }
+      const PCGResult r = pcg_solve(T, ess, n_ess, rhs.data(), kk, rel_tol, 0.0, max_iter, jacobi, s);
+      st.solves++;
+      st.iterations += r.iterations;
+      st.max_iterations = std::max(st.max_iterations, r.iterations);
+      st.converged = st.converged && r.converged;
+   };
+   double *kk = k.data();
+   switch (type)
+   {
+      case 21:  // BackwardEuler
+         implicit_solve(u, kk);
+         kern::add_scaled(n, u, dt, kk, u, s);
+         break;
+      case 32:  // ImplicitMidpoint
+         implicit_solve(u, kk);
+         kern::add_scaled(n, u, dt, kk, u, s);
+         break;
+      case 22:
+      case 33:  // SDIRK23
+      {
+         const double g = sdirk23_gamma(type);
+         implicit_solve(u, kk);
+         kern::add_scaled(n, u, (1. - 2. * g) * dt, kk, y.data(), s);
+         kern::add_scaled(n, u, dt / 2, kk, u, s);
+         implicit_solve(y.data(), kk);
+         kern::add_scaled(n, u, dt / 2, kk, u, s);
+         break;
+      }
+      case 23:  // SDIRK33
+      {
+         const double a = kSdirk33A, b = kSdirk33B, c = kSdirk33C;
+         implicit_solve(u, kk);
+         kern::add_scaled(n, u, (c - a) * dt, kk, y.data(), s);
+         kern::add_scaled(n, u, b * dt, kk, u, s);
+         implicit_solve(y.data(), kk);
+         kern::add_scaled(n, u, (1.0 - a - b) * dt, kk, u, s);
+         implicit_solve(u, kk);
+         kern::add_scaled(n, u, a * dt, kk, u, s);
+         break;
+      }
+      case 34:  // SDIRK34
+      {
+         const double a = sdirk34_a(), b = 1. / (6. * (2. * a - 1.) * (2. * a - 1.));
+         implicit_solve(u, kk);
+         kern::add_scaled(n, u, (0.5 - a) * dt, kk, y.data(), s);
+         kern::add_scaled(n, u, (2. * a) * dt, kk, z.data(), s);
+         kern::add_scaled(n, u, b * dt, kk, u, s);
+         implicit_solve(y.data(), kk);
+         kern::add_scaled(n, z.data(), (1. - 4. * a) * dt, kk, z.data(), s);
+         kern::add_scaled(n, u, (1. - 2. * b) * dt, kk, u, s);
+         implicit_solve(z.data(), kk);
+         kern::add_scaled(n, u, b * dt, kk, u, s);
+         break;
+      }
+      default: break;
+   }
+   ECM2_HIP(hipStreamSynchronize(s));
+   return st;
+}
+
+} // namespace ecm2

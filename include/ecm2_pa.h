@@ -174,10 +174,44 @@ int ecm2_pcg_solve(ecm2_pa_form *f, const int *ess, int n_ess, const double *b, 
                    double *final_norm, void *stream);
 
 /* ------------------------------------------------------------------------ */
+/* Operators for the solvers: the serial form, one rank of the RCCL form, or */
+/* the in-process loopback group (concatenated true vectors), all seen as the */
+/* reference's Operator (linalg/operator.hpp:24-110) by PCG and the ODE step. */
+/* ------------------------------------------------------------------------ */
+typedef struct ecm2_operator ecm2_operator;
+typedef struct ecm2_par_form ecm2_par_form;
+/* The operator keeps a reference to the form(s): destroy it first. */
+int ecm2_operator_from_pa_form(ecm2_pa_form *f, ecm2_operator **out);
+int ecm2_operator_from_par_form(ecm2_par_form *f, ecm2_operator **out);
+/* forms[r] must be rank r of an n-rank partition; vectors are the concatenation of the
+ * ranks' true vectors (rank r at offset sum_{q<r} n_owned(q)). */
+int ecm2_operator_from_par_group(ecm2_par_form *const *forms, int n, ecm2_operator **out);
+int ecm2_operator_size(const ecm2_operator *op, int *n);
+int ecm2_operator_mult(ecm2_operator *op, const double *x, double *y, void *stream);
+/* ecm2_pcg_solve on any operator; with the RCCL form every rank calls it collectively
+ * (dots are summed with ncclAllReduce, solvers.cpp). */
+int ecm2_operator_pcg(ecm2_operator *op, const int *ess, int n_ess, const double *b, double *x,
+                      double rel_tol, double abs_tol, int max_iter, int jacobi, int *iterations,
+                      double *final_norm, void *stream);
+/* ODESolver::SelectImplicit types (ode.cpp:77-91): 21 BackwardEuler, 22 SDIRK23 (L-stable),
+ * 23 SDIRK33, 32 ImplicitMidpoint, 33 SDIRK23 (A-stable), 34 SDIRK34.  Returns the stage
+ * coefficient c (every stage solves (M + c*dt*K) k = -K u_stage), 0 for unknown types. */
+double ecm2_ode_implicit_coeff(int type);
+/* One step of M du/dt = -K u (ex16 ConductionOperator::ImplicitSolve, ex16.cpp:327-354, in
+ * the slope form; the SDIRK stage algebra of ode.cpp:682-859).  T must be assembled as
+ * M + c*dt*K with c = ecm2_ode_implicit_coeff(type); u (device, true dofs) is advanced in
+ * place; ess dofs keep their values.  Stage solves: constrained Jacobi-PCG (rel_tol,
+ * max_iter).  *converged = 0 if some stage solve stopped at max_iter (like CGSolver, not an
+ * error). */
+int ecm2_ode_step(int type, ecm2_operator *T, ecm2_operator *K, double dt, double *u, const int *ess,
+                  int n_ess, double rel_tol, int max_iter, int jacobi, int *solves, int *iterations,
+                  int *converged, void *stream);
+void ecm2_operator_destroy(ecm2_operator *op);
+
+/* ------------------------------------------------------------------------ */
 /* Distributed form: ParBilinearForm / RAPOperator(P, A, P) over RCCL          */
 /* ------------------------------------------------------------------------ */
 typedef struct ecm2_partition ecm2_partition;
-typedef struct ecm2_par_form ecm2_par_form;
 
 /* Mesh::CartesianPartitioning along z (mesh/mesh.cpp:8966) of a lexicographic Cartesian
  * mesh: elem_rank host [ne]. */
@@ -220,6 +254,9 @@ int ecm2_par_form_mult(ecm2_par_form *f, const double *x_true, double *y_true, v
 /* All subdomains of one partition in this process on one GPU (exchange by device copies). */
 int ecm2_par_group_mult(ecm2_par_form *const *forms, int n, const double *const *x_true,
                         double *const *y_true, void *stream);
+/* ParBilinearForm::AssembleDiagonal on the true dofs (local PA diagonal + P^T). */
+int ecm2_par_form_assemble_diagonal(ecm2_par_form *f, double *d_true, void *stream);
+int ecm2_par_group_diagonal(ecm2_par_form *const *forms, int n, double *const *d_true, void *stream);
 int ecm2_par_form_timing(ecm2_par_form *f, int enable);
 int ecm2_par_form_timing_get(ecm2_par_form *f, double *total_ms, long *launches);
 int ecm2_par_form_algorithmic_bytes(const ecm2_par_form *f, double *bytes);

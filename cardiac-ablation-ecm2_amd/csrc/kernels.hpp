@@ -101,6 +101,8 @@ std::vector<double> make_row_table(const DofToQuad &m);
 // through an encoded map [e][nd] (dof | shared << 30 | sign << 31); shared dofs go to
 // part[e*nd + a] when a.part is set, else atomics.  has_line: (D, Q) instantiated.
 bool has_line(int D, int Q);
+// Longest chunk of x-adjacent elements the selected line-kernel variant walks per wave.
+int line_chunk_limit();
 // Write the constant-memory basis table of (D, Q) on the current device (once).
 void upload_basis(int D, int Q, const Basis1D &b);
 void apply_line(int D, int Q, bool mass, bool diff, const ApplyArgs &a, const Basis1D &b, hipStream_t s);

@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 
 namespace ecm2
 {
@@ -164,6 +165,29 @@ void build_merge_plan(int ne, int D, const std::vector<int> &gmap_int, int ndofs
 }
 } // namespace
 
+// Longest chunk of x-adjacent elements one wave of the line kernel walks: the kernel
+// variant's limit (1 for the default single-element variant), lowered by ECM2_LINE_CHUNK.
+static int line_chunk_max()
+{
+   static int v = [] {
+      const char *e = std::getenv("ECM2_LINE_CHUNK");
+      const int c = e ? std::atoi(e) : 8;
+      return std::max(1, std::min(c, kern::line_chunk_limit()));
+   }();
+   return v;
+}
+
+// Order of the second-pass list (experiment knob ECM2_SUM_ORDER=dof): by first partial
+// slot (default: neighbouring threads read neighbouring slots) or by dof (y stores coalesce).
+static bool sum_order_by_dof()
+{
+   static bool v = [] {
+      const char *e = std::getenv("ECM2_SUM_ORDER");
+      return e && std::string(e) == "dof";
+   }();
+   return v;
+}
+
 // Second-pass plan of the deterministic scatter: every dof not held exactly once with its
 // partial slots in ascending order; dofs held by nobody get an empty list (y = 0).  The
 // owned dofs come first, then the ghosts (split form); within each range the list is
@@ -180,7 +204,7 @@ void PAForm::build_shared_plan(const std::vector<int> &hcount, const std::vector
    for (int d = 0; d < ndofs_; d++) { if (hcount[d] != 1) { dofs.push_back(d); } }
    auto key = [&](int d) -> long {
       const long first = hcount[d] > 1 ? slots_by_dof[start[d]] : -1;
-      return (d < n_owned_ ? 0 : (1l << 40)) + first;
+      return (d < n_owned_ ? 0 : (1l << 40)) + (sum_order_by_dof() ? (long)d : first);
    };
    std::stable_sort(dofs.begin(), dofs.end(), [&](int p, int q) { return key(p) < key(q); });
    std::vector<unsigned> meta;
@@ -201,18 +225,6 @@ void PAForm::build_shared_plan(const std::vector<int> &hcount, const std::vector
    sh_dofs_.upload(dofs, s);
    sh_meta_.upload(meta, s);
    sh_slots_.upload(slots, s);
-}
-
-// Longest chunk of x-adjacent elements one wave of the line kernel walks (1..8;
-// ECM2_LINE_CHUNK overrides the default for experiments).
-static int line_chunk_max()
-{
-   static int v = [] {
-      const char *e = std::getenv("ECM2_LINE_CHUNK");
-      const int c = e ? std::atoi(e) : 8;
-      return c < 1 ? 1 : (c > 8 ? 8 : c);
-   }();
-   return v;
 }
 
 void PAForm::set_kernel(int mode)

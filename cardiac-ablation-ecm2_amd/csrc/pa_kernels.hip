@@ -356,6 +356,15 @@ k_apply_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restri
 // row's qdata in flight while the current row is computed (double buffering).
 // VAR bit0: plain stores instead of atomics (diagnostic: atomic cost, wrong result)
 // VAR bit1: default-policy (not nontemporal) qdata loads
+// XCD-aware workgroup order: the hardware deals workgroup i to XCD i % 8 (MI355X_MICROARCH.md,
+// "Workgroup dispatch"); remapping i to a contiguous range per XCD keeps neighbouring bricks
+// (which share x values) in one XCD's L2.  A bijection on [0, G) for any G.
+__device__ __forceinline__ int xcd_contiguous(int i, int G)
+{
+   const int q = G >> 3, r = G & 7, x = i & 7, j = i >> 3;
+   return x * q + (x < r ? x : r) + j;
+}
+
 template <int D, int Q, bool MASS, bool DIFF, bool SPLIT, int VAR>
 __global__ void __launch_bounds__(256, (VAR & 8) ? 2 : 1)
 k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
@@ -369,7 +378,8 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
    constexpr int NR = Q * Q;  // rows
    __shared__ double sX[4][ND][64];
    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-   const int blk = blk_begin + blockIdx.x * 4 + w;
+   const int wg = (VAR & 16) ? xcd_contiguous(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+   const int blk = blk_begin + wg * 4 + w;
    if (blk >= blk_end) { return; }  // wave-uniform; no block-wide barrier below
    const int e = blk * 64 + lane;
    const bool active = e < ne;
@@ -806,20 +816,20 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned
    static_assert(QQ <= 64, "line kernel needs Q1D <= 8");
    __shared__ double bufA[SA];  // s1, then s3
    __shared__ double bufB[SB];  // s2, then s4
-   const int c = c_begin + blockIdx.x;
+   const int c = c_begin + ((VAR & 4) ? xcd_contiguous(blockIdx.x, gridDim.x) : (int)blockIdx.x);
    if (c >= c_end) { return; }  // whole wave
    const int t = threadIdx.x;
    const int ch = chunks[c];
-   const int e0 = ch & 0xffffff, cnt = ch >> 24;
+   const int e0 = ch & 0xffffff, cnt = (VAR & 8) ? 1 : (ch >> 24);  // VAR & 8: one element per wave
 
    double qv[7][Q];
-   if (!(VAR & 2)) { line_load_qdata<D, Q, MASS, DIFF>(qv, e0, t, qdd, qdm); }
+   if (!(VAR & 34)) { line_load_qdata<D, Q, MASS, DIFF>(qv, e0, t, qdd, qdm); }
    double carry = 0.0;
 #pragma unroll 1
    for (int k = 0; k < cnt; k++)
    {
       const int e = e0 + k;
-      if (VAR & 2) { line_load_qdata<D, Q, MASS, DIFF>(qv, e, t, qdd, qdm); }
+      if ((VAR & 2) && !(VAR & 32)) { line_load_qdata<D, Q, MASS, DIFF>(qv, e, t, qdd, qdm); }
       // ---- lanes (dy, dz): gather the x-line, contract in x
       int gl[D];
       if (t < DD)
@@ -897,6 +907,7 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned
          double A1[D], A2[D], A3[D];
 #pragma unroll
          for (int dz = 0; dz < D; dz++) { A1[dz] = 0.0; A2[dz] = 0.0; A3[dz] = 0.0; }
+         if (VAR & 32) { line_load_qdata<D, Q, MASS, DIFF>(qv, e, t, qdd, qdm); }  // just in time
 #pragma unroll
          for (int qz = 0; qz < Q; qz++)
          {
@@ -943,7 +954,7 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned
          }
       }
       // next element's qdata: in flight during the rest of this element
-      if (!(VAR & 2) && k + 1 < cnt) { line_load_qdata<D, Q, MASS, DIFF>(qv, e + 1, t, qdd, qdm); }
+      if (!(VAR & 34) && k + 1 < cnt) { line_load_qdata<D, Q, MASS, DIFF>(qv, e + 1, t, qdd, qdm); }
       __syncthreads();
       // ---- lanes (qx, dz): transpose in y
       if (t < DQ)
@@ -1256,7 +1267,7 @@ void launch_tpe_pf(int var, const ApplyArgs &a, const Basis1D &b, const double *
    hipLaunchKernelGGL((k_apply_tpe_pf<D, Q, MASS, DIFF, SPLIT, V>), grid, block, 0, s, a.ne,        \
                       a.blk_begin, a.blk_end, a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, rowtab, \
                       a.lane_flags, a.part)
-   switch (var & 11)
+   switch (var & 27)
    {
       case 0: ECM2_PF(0); break;
       case 1: ECM2_PF(1); break;
@@ -1264,6 +1275,8 @@ void launch_tpe_pf(int var, const ApplyArgs &a, const Basis1D &b, const double *
       case 3: ECM2_PF(3); break;
       case 8: ECM2_PF(8); break;
       case 9: ECM2_PF(9); break;
+      case 16: ECM2_PF(16); break;
+      case 17: ECM2_PF(17); break;
       default: ECM2_PF(0); break;
    }
 #undef ECM2_PF
@@ -1392,12 +1405,15 @@ void apply_tpe(int D, int Q, bool mass, bool diff, const ApplyArgs &a, const Bas
 }
 
 // experiment knob ECM2_LINE_VARIANT: bit 1 = load each element's qdata at the top of its
-// iteration instead of prefetching it during the previous element
+// iteration instead of prefetching it during the previous element; bit 8 = one element per
+// wave (compile-time; needs ECM2_LINE_CHUNK=1); bit 32 = load qdata inside the z stage
+constexpr int kDefaultLineVariant = 8;  // one element per wave, qdata prefetched at the top
+
 int line_variant()
 {
    static int v = [] {
       const char *e = std::getenv("ECM2_LINE_VARIANT");
-      return e ? std::atoi(e) : 0;
+      return e ? std::atoi(e) : kDefaultLineVariant;
    }();
    return v;
 }
@@ -1413,8 +1429,14 @@ void launch_line_mdq(const ApplyArgs &a, const Basis1D &b, hipStream_t s)
    hipLaunchKernelGGL((k_apply_line<D, Q, MASS, DIFF, SP, V>), grid, block, 0, s, c0, c1, a.chunks, a.n_owned, \
                       a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.part)
    const bool split = a.xg || a.yg;
-   if (line_variant() & 2) { if (split) { ECM2_LINE(true, 2); } else { ECM2_LINE(false, 2); } }
-   else { if (split) { ECM2_LINE(true, 0); } else { ECM2_LINE(false, 0); } }
+   switch (line_variant() & 46)
+   {
+      case 2: if (split) { ECM2_LINE(true, 2); } else { ECM2_LINE(false, 2); } break;
+      case 8: if (split) { ECM2_LINE(true, 8); } else { ECM2_LINE(false, 8); } break;
+      case 40: if (split) { ECM2_LINE(true, 40); } else { ECM2_LINE(false, 40); } break;
+      case 32: if (split) { ECM2_LINE(true, 32); } else { ECM2_LINE(false, 32); } break;
+      default: if (split) { ECM2_LINE(true, 0); } else { ECM2_LINE(false, 0); } break;
+   }
 #undef ECM2_LINE
 }
 
@@ -1425,6 +1447,8 @@ void launch_line_dq(bool mass, bool diff, const ApplyArgs &a, const Basis1D &b, 
    else if (mass) { launch_line_mdq<D, Q, true, false>(a, b, s); }
    else if (diff) { launch_line_mdq<D, Q, false, true>(a, b, s); }
 }
+
+int line_chunk_limit() { return (line_variant() & 8) ? 1 : 8; }
 
 bool has_line(int D, int Q)
 {

@@ -175,3 +175,53 @@ def test_gpu_loopback_group_matches_serial(kind, nranks, order, scatter):
     cg = coeff_function(Pg)
     ref = O.OracleOperator(m.element_nodes(), fes.gather_map(), fes.ndofs, order, alpha=cg, beta=cg).mult(xg)
     assert relerr(y, ref) <= RTOL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order", [2, 4])
+def test_gpu_rccl_single_rank_transport(order):
+    """The RCCL transport with one rank (ncclCommInitRank, the comm stream and its events,
+    ncclAllReduce'd PCG dots, the RCCL diagonal) against the serial form.  Two ranks need
+    two GPUs (RCCL refuses two ranks on one device); the exchange itself is covered by the
+    loopback group tests and runs at N > 1 in bench.py."""
+    import torch
+    m = _mesh("cart")
+    fes = E.H1Space(m, order)
+    er = np.zeros(m.GetNE(), np.int32)
+    part = E.Partition(fes, er, 0, 1)
+    assert part.n_owned == fes.ndofs and part.n_ghost == 0
+    pf = E.ParBilinearForm(part, rccl_id=E.rccl_unique_id())
+    q1d = O.default_q1d(order)
+    P = E.quadrature_points_subset(m, q1d, part.elems)
+    c = torch.as_tensor(coeff_function(P).reshape(part.ne_local, -1)).cuda()
+    pf.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(c)))
+    pf.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(c.clone())))
+    pf.Assemble()
+    Pg = O.quad_points(m.element_nodes(), q1d)
+    cg = coeff_function(Pg)
+    ref = O.OracleOperator(m.element_nodes(), fes.gather_map(), fes.ndofs, order, alpha=cg, beta=cg)
+    xg = np.random.default_rng(2).uniform(-1, 1, fes.ndofs)
+    x = torch.as_tensor(xg[part.owned_global]).cuda()
+    y = torch.full_like(x, float("nan"))
+    for _ in range(3):  # repeated Mults reuse the comm stream and events
+        pf.Mult(x, y)
+    torch.cuda.synchronize()
+    yy = np.zeros(fes.ndofs)
+    yy[part.owned_global] = y.cpu().numpy()
+    assert relerr(yy, ref.mult(xg)) <= RTOL
+    d = torch.empty_like(x)
+    pf.AssembleDiagonal(d)
+    dd = np.zeros(fes.ndofs)
+    dd[part.owned_global] = d.cpu().numpy()
+    assert relerr(dd, ref.diagonal()) < 1e-13
+    ess = fes.boundary_dofs()
+    ess_local = np.nonzero(np.isin(part.owned_global, ess))[0].astype(np.int32)
+    b = np.random.default_rng(4).uniform(-1, 1, fes.ndofs)
+    sol = torch.empty_like(x)
+    it, _ = E.Operator(pf).PCG(torch.as_tensor(b[part.owned_global]).cuda(), sol,
+                               ess=torch.as_tensor(ess_local).cuda(), rel_tol=1e-12, max_iter=3000)
+    xr, itr, _ = ref.pcg(b, ess, rel_tol=1e-12, max_iter=3000)
+    ss = np.zeros(fes.ndofs)
+    ss[part.owned_global] = sol.cpu().numpy()
+    assert abs(it - itr) <= 2
+    assert relerr(ss, xr) < 1e-9

@@ -801,6 +801,75 @@ __device__ __forceinline__ void line_load_qdata(double (&qv)[7][Q], int e, int t
    }
 }
 
+// Grid-function coefficient at the quadrature points (GridFunctionCoefficient projected
+// by CoefficientVector::Project, coefficient.cpp:2052-2070 / qfunction.cpp:73-98, composed
+// with the affine Pennes law), sum-factorised like the line kernel: one wave per element,
+// lanes (dy,dz) gather a T x-line and contract in x, lanes (qx,dz) in y, lanes (qx,qy) in z;
+// out[e][q] (q = qx + Q(qy + Q qz)) = scale * (1 + slope * (T(x_q) - t_ref)).
+template <int D, int Q>
+__global__ void __launch_bounds__(64)
+k_coeff_line(int ne, const int *__restrict__ gmap, const double *__restrict__ T, double scale, double slope,
+             double t_ref, double *__restrict__ out)
+{
+   constexpr int ND = D * D * D, NQ = Q * Q * Q, DD = D * D, QQ = Q * Q, DQ = D * Q;
+   __shared__ double s1[DD * Q];
+   __shared__ double s2[D * QQ];
+   const int e = blockIdx.x, t = threadIdx.x;
+   if (e >= ne) { return; }
+   if (t < DD)
+   {
+      CBasis *bp = stage_basis<D, Q>();
+      double tl[D];
+#pragma unroll
+      for (int dx = 0; dx < D; dx++)
+      {
+         const int g = gmap[(size_t)e * ND + t * D + dx];
+         tl[dx] = g >= 0 ? T[g] : -T[-1 - g];
+      }
+#pragma unroll
+      for (int qx = 0; qx < Q; qx++)
+      {
+         double u = 0.0;
+#pragma unroll
+         for (int dx = 0; dx < D; dx++) { u += bp->B[qx + MQ * dx] * tl[dx]; }
+         s1[t * Q + qx] = u;
+      }
+   }
+   __syncthreads();
+   if (t < DQ)
+   {
+      CBasis *bp = stage_basis<D, Q>();
+      const int qx = t % Q, dz = t / Q;
+      double l[D];
+#pragma unroll
+      for (int dy = 0; dy < D; dy++) { l[dy] = s1[(dz * D + dy) * Q + qx]; }
+#pragma unroll
+      for (int qy = 0; qy < Q; qy++)
+      {
+         double u = 0.0;
+#pragma unroll
+         for (int dy = 0; dy < D; dy++) { u += bp->B[qy + MQ * dy] * l[dy]; }
+         s2[(dz * Q + qy) * Q + qx] = u;
+      }
+   }
+   __syncthreads();
+   if (t < QQ)
+   {
+      CBasis *bp = stage_basis<D, Q>();
+      double l[D];
+#pragma unroll
+      for (int dz = 0; dz < D; dz++) { l[dz] = s2[dz * QQ + t]; }
+#pragma unroll
+      for (int qz = 0; qz < Q; qz++)
+      {
+         double v = 0.0;
+#pragma unroll
+         for (int dz = 0; dz < D; dz++) { v += bp->B[qz + MQ * dz] * l[dz]; }
+         out[(size_t)e * NQ + qz * QQ + t] = scale * (1.0 + slope * (v - t_ref));
+      }
+   }
+}
+
 template <int D, int Q, bool MASS, bool DIFF, bool SPLIT, int VAR>
 __global__ void __launch_bounds__(64)
 k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned,
@@ -1364,6 +1433,22 @@ void coeff_gridfunc(int ne, int D, int Q, const int *gmap, const Basis1D &b, con
 {
    const long n = (long)ne * Q * Q * Q;
    if (n == 0) { return; }
+   if (has_line(D, Q))
+   {
+      upload_basis(D, Q, b);
+#define ECM2_COEFF_CASE(DD, QQ)                                                                      \
+      if (D == DD && Q == QQ)                                                                        \
+      {                                                                                              \
+         hipLaunchKernelGGL((k_coeff_line<DD, QQ>), dim3(ne), dim3(64), 0, s, ne, gmap, c.lvec, c.scale, \
+                            c.slope, c.t_ref, out);                                                  \
+         ECM2_HIP(hipGetLastError());                                                                \
+         return;                                                                                     \
+      }
+      ECM2_COEFF_CASE(2, 3) ECM2_COEFF_CASE(3, 4) ECM2_COEFF_CASE(4, 5) ECM2_COEFF_CASE(5, 6)
+      ECM2_COEFF_CASE(6, 7) ECM2_COEFF_CASE(7, 8) ECM2_COEFF_CASE(2, 2) ECM2_COEFF_CASE(3, 3)
+      ECM2_COEFF_CASE(4, 4) ECM2_COEFF_CASE(5, 5)
+#undef ECM2_COEFF_CASE
+   }
    hipLaunchKernelGGL(k_coeff_gridfunc, dim3(grid_for(n, 256)), dim3(256), 0, s, ne, D, Q, gmap,
                       b, c.lvec, c.scale, c.slope, c.t_ref, out);
    ECM2_HIP(hipGetLastError());

@@ -29,6 +29,7 @@ struct QLayout
    int kind = QLAYOUT_NATIVE;
    int ne = 0, nq = 0;
    const int *pos = nullptr;  // device: caller element -> internal position (BLOCKED)
+   const int *perm = nullptr; // device: internal position -> caller element (BLOCKED)
    size_t diff_size() const
    {
       if (kind == QLAYOUT_NATIVE) { return (size_t)ne * 6 * nq; }

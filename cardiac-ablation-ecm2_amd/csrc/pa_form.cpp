@@ -299,6 +299,9 @@ void PAForm::assemble(hipStream_t s)
       gmap_blk_.upload(blk, s);
       lane_flags_.upload(fl, s);
       pos_.upload(pos, s);
+      std::vector<int> perm(ne_);
+      for (int e = 0; e < ne_; e++) { perm[pos[e]] = e; }
+      perm_dev_.upload(perm, s);
       rowtab_.upload(kern::make_row_table(maps_), s);
       ECM2_HIP(hipStreamSynchronize(s));
    }
@@ -365,11 +368,26 @@ void PAForm::assemble(hipStream_t s)
       ECM2_HIP(hipStreamSynchronize(s));
    }
    layout_.pos = (layout_.kind == QLAYOUT_BLOCKED) ? pos_.data() : nullptr;
+   layout_.perm = (layout_.kind == QLAYOUT_BLOCKED) ? perm_dev_.data() : nullptr;
    part_.resize(use_partials() ? (size_t)layout_.nblk() * ND_ * 64 : 0);  // >= ne * nd for LINE
    qd_diff_.resize(have_diff_ ? layout_.diff_size() : 0);
    qd_mass_.resize(have_mass_ ? layout_.mass_size() : 0);
-   if (qd_diff_.size()) { ECM2_HIP(hipMemsetAsync(qd_diff_.data(), 0, qd_diff_.bytes(), s)); }
-   if (qd_mass_.size()) { ECM2_HIP(hipMemsetAsync(qd_mass_.data(), 0, qd_mass_.bytes(), s)); }
+   // the setup kernels write every entry except the padding lanes of a partial last block
+   // (blocked layout), which are cleared so the apply kernels stream defined values
+   if (layout_.kind == QLAYOUT_BLOCKED && ne_ % kElemBlock)
+   {
+      const size_t nb = layout_.nblk();
+      if (qd_diff_.size())
+      {
+         const size_t per = qd_diff_.size() / nb;
+         ECM2_HIP(hipMemsetAsync(qd_diff_.data() + (nb - 1) * per, 0, per * sizeof(double), s));
+      }
+      if (qd_mass_.size())
+      {
+         const size_t per = qd_mass_.size() / nb;
+         ECM2_HIP(hipMemsetAsync(qd_mass_.data() + (nb - 1) * per, 0, per * sizeof(double), s));
+      }
+   }
 
    // Coefficient values at quadrature points (CoefficientVector::Project).
    auto coeff_values = [&](const CoeffDesc &c, DeviceArray<double> &tmp) -> const double * {

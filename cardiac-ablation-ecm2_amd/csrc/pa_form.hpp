@@ -149,6 +149,7 @@ private:
    DeviceArray<int> lane_flags_;    // [blk][64] in-wave merge flags
    std::vector<int> perm_host_;     // internal position -> caller element (empty: identity)
    DeviceArray<int> pos_;           // caller element -> internal position
+   DeviceArray<int> perm_dev_;      // internal position -> caller element
    DeviceArray<int> csr_off_, csr_idx_;
    DeviceArray<double> enodes_;     // [e][3][8]
    const double *jac_ = nullptr;    // device, not owned

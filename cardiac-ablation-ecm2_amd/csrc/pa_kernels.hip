@@ -170,6 +170,100 @@ __global__ void k_setup_nodes(const int *__restrict__ pos, int kind, int ne, int
    write_qdata(pos, kind, NQ, e, q, W[q], J, cm, cd, qd_diff, qd_mass);
 }
 
+// qdata from trilinear corners, templated on Q.  BLOCKED: threads run over (blk, q, lane)
+// with the lane fastest, so for each quadrature point a wave writes 64 consecutive
+// elements' entries (1 KiB per diffusion pair), the layout the apply kernel streams;
+// perm maps the internal position to the caller element (geometry and coefficients are
+// in caller order).  NATIVE: threads run over (e, q), q fastest.
+template <int Q, bool BLOCKED>
+__global__ void __launch_bounds__(256)
+k_setup_nodes_t(const int *__restrict__ perm, int ne, const double *__restrict__ enodes,
+                const double *__restrict__ W, const Basis1D b1, SetupCoef cm, SetupCoef cd,
+                double *__restrict__ qd_diff, double *__restrict__ qd_mass)
+{
+   constexpr int NQ = Q * Q * Q;
+   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   int e, q, ipos = 0, lane = 0;
+   long blk = 0;
+   if (BLOCKED)
+   {
+      lane = (int)(t & 63);
+      const long rest = t >> 6;
+      q = (int)(rest % NQ);
+      blk = rest / NQ;
+      ipos = (int)(blk * 64 + lane);
+      if (ipos >= ne) { return; }
+      e = perm ? perm[ipos] : ipos;
+   }
+   else
+   {
+      if (t >= (long)ne * NQ) { return; }
+      e = (int)(t / NQ);
+      q = (int)(t % NQ);
+   }
+   const int qx = q % Q, qy = (q / Q) % Q, qz = q / (Q * Q);
+   const double *X = enodes + (size_t)e * 24;
+   double J[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+#pragma unroll
+   for (int a = 0; a < 8; a++)
+   {
+      const int ax = a & 1, ay = (a >> 1) & 1, az = a >> 2;
+      const double bx = b1.B[qx + MQ * ax], by = b1.B[qy + MQ * ay], bz = b1.B[qz + MQ * az];
+      const double gx = b1.G[qx + MQ * ax], gy = b1.G[qy + MQ * ay], gz = b1.G[qz + MQ * az];
+      const double dN0 = gx * by * bz, dN1 = bx * gy * bz, dN2 = bx * by * gz;
+#pragma unroll
+      for (int i = 0; i < 3; i++)
+      {
+         const double xi = X[i * 8 + a];
+         J[i][0] += xi * dN0;
+         J[i][1] += xi * dN1;
+         J[i][2] += xi * dN2;
+      }
+   }
+   if (!BLOCKED)
+   {
+      write_qdata(nullptr, QLAYOUT_NATIVE, NQ, e, q, W[q], J, cm, cd, qd_diff, qd_mass);
+      return;
+   }
+   // same arithmetic as write_qdata (PADiffusionSetup3D / mass setup), blocked stores
+   const double J11 = J[0][0], J21 = J[1][0], J31 = J[2][0];
+   const double J12 = J[0][1], J22 = J[1][1], J32 = J[2][1];
+   const double J13 = J[0][2], J23 = J[1][2], J33 = J[2][2];
+   const double detJ = J11 * (J22 * J33 - J32 * J23) - J21 * (J12 * J33 - J32 * J13) +
+                       J31 * (J12 * J23 - J22 * J13);
+   const size_t eq = (size_t)e * NQ + q;
+   const double w = W[q];
+   if (cd.has)
+   {
+      const double w_detJ = w / detJ;
+      const double A11 = (J22 * J33) - (J23 * J32);
+      const double A12 = (J32 * J13) - (J12 * J33);
+      const double A13 = (J12 * J23) - (J22 * J13);
+      const double A21 = (J31 * J23) - (J21 * J33);
+      const double A22 = (J11 * J33) - (J13 * J31);
+      const double A23 = (J21 * J13) - (J11 * J23);
+      const double A31 = (J21 * J32) - (J31 * J22);
+      const double A32 = (J31 * J12) - (J11 * J32);
+      const double A33 = (J11 * J22) - (J12 * J21);
+      const double C = coef_at(cd, eq);
+      v2d p0, p1, p2;
+      p0.x = w_detJ * (C * A11 * A11 + C * A12 * A12 + C * A13 * A13);
+      p0.y = w_detJ * (C * A11 * A21 + C * A12 * A22 + C * A13 * A23);
+      p1.x = w_detJ * (C * A11 * A31 + C * A12 * A32 + C * A13 * A33);
+      p1.y = w_detJ * (C * A21 * A21 + C * A22 * A22 + C * A23 * A23);
+      p2.x = w_detJ * (C * A21 * A31 + C * A22 * A32 + C * A23 * A33);
+      p2.y = w_detJ * (C * A31 * A31 + C * A32 * A32 + C * A33 * A33);
+      v2d *dst = reinterpret_cast<v2d *>(qd_diff + ((size_t)blk * NQ + q) * 3 * 128) + lane;
+      dst[0] = p0;
+      dst[64] = p1;
+      dst[128] = p2;
+   }
+   if (cm.has)
+   {
+      qd_mass[((size_t)blk * ((NQ + 1) / 2) + (q >> 1)) * 128 + lane * 2 + (q & 1)] = w * coef_at(cm, eq) * detJ;
+   }
+}
+
 __global__ void k_setup_jac(const int *__restrict__ pos, int kind, int ne, int NQ, const double *__restrict__ Jg,
                             const double *__restrict__ W, SetupCoef cm, SetupCoef cd,
                             double *__restrict__ qd_diff, double *__restrict__ qd_mass)
@@ -1461,9 +1555,31 @@ void setup_from_nodes(const QLayout &L, int Q, const double *enodes, const doubl
 {
    const long n = (long)L.ne * L.nq;
    if (n == 0) { return; }
+   const SetupCoef scm = make_setup_coef(cm, cm_q), scd = make_setup_coef(cd, cd_q);
+   const bool blocked = L.kind == QLAYOUT_BLOCKED;
+   ECM2_VERIFY(!blocked || !L.pos || L.perm, ERR_INTERNAL, "blocked setup needs the inverse permutation");
+   const long nb = blocked ? (long)L.nblk() * 64 * L.nq : n;
+#define ECM2_SETUP_CASE(QQ)                                                                              \
+   if (Q == QQ)                                                                                          \
+   {                                                                                                     \
+      if (blocked)                                                                                       \
+      {                                                                                                  \
+         hipLaunchKernelGGL((k_setup_nodes_t<QQ, true>), dim3(grid_for(nb, 256)), dim3(256), 0, s, L.perm, L.ne, \
+                            enodes, W, b1, scm, scd, qd_diff, qd_mass);                                  \
+      }                                                                                                  \
+      else                                                                                               \
+      {                                                                                                  \
+         hipLaunchKernelGGL((k_setup_nodes_t<QQ, false>), dim3(grid_for(nb, 256)), dim3(256), 0, s, nullptr, L.ne, \
+                            enodes, W, b1, scm, scd, qd_diff, qd_mass);                                  \
+      }                                                                                                  \
+      ECM2_HIP(hipGetLastError());                                                                       \
+      return;                                                                                            \
+   }
+   ECM2_SETUP_CASE(2) ECM2_SETUP_CASE(3) ECM2_SETUP_CASE(4) ECM2_SETUP_CASE(5)
+   ECM2_SETUP_CASE(6) ECM2_SETUP_CASE(7) ECM2_SETUP_CASE(8)
+#undef ECM2_SETUP_CASE
    hipLaunchKernelGGL(k_setup_nodes, dim3(grid_for(n, 256)), dim3(256), 0, s, L.pos, L.kind, L.ne, Q,
-                      enodes, W, b1, make_setup_coef(cm, cm_q), make_setup_coef(cd, cd_q),
-                      qd_diff, qd_mass);
+                      enodes, W, b1, scm, scd, qd_diff, qd_mass);
    ECM2_HIP(hipGetLastError());
 }
 

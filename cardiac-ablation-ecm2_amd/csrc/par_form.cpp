@@ -44,7 +44,12 @@ ParPAForm::ParPAForm(const LocalPart &part, const double *enodes_local_host, int
       ncclComm_t comm;
       ECM2_NCCL(ncclCommInitRank(&comm, part.nranks, id, part.rank));
       comm_ = comm;
-      ECM2_HIP(hipStreamCreateWithFlags(&cs_, hipStreamNonBlocking));
+      // highest priority: the boundary elements and the RCCL kernels on the comm stream are
+      // dispatched ahead of the interior kernel's remaining workgroups, so the exchange
+      // overlaps the interior instead of queueing behind it
+      int prio_least = 0, prio_greatest = 0;
+      ECM2_HIP(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
+      ECM2_HIP(hipStreamCreateWithPriority(&cs_, hipStreamNonBlocking, prio_greatest));
       ECM2_HIP(hipEventCreateWithFlags(&ev_pack_, hipEventDisableTiming));
       ECM2_HIP(hipEventCreateWithFlags(&ev_xg_, hipEventDisableTiming));
       ECM2_HIP(hipEventCreateWithFlags(&ev_yg_, hipEventDisableTiming));

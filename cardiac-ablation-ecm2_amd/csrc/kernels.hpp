@@ -132,6 +132,13 @@ void dot(int n, const double *a, const double *b, double *partials, double *out,
 //   x += (nom/den) d ; r -= (nom/den) z
 void pcg_update_xr(int n, const double *nom, const double *den, const double *d,
                    const double *z, double *x, double *r, hipStream_t s);
+// Fused PCG update: x += (nom/den) d; r -= (nom/den) z; z = dinv .* r (dinv null: z untouched);
+// *out = r.z (r.r without dinv), deterministic.  z holds A d on entry.
+void pcg_step(int n, const double *nom, const double *den, const double *d, double *z, double *x, double *r,
+              const double *dinv, double *partials, double *out, hipStream_t s);
+// saved[i] = v[idx[i]], v[idx[i]] = 0  /  v[idx[i]] = y[idx[i]] = saved[i]
+void ess_save_zero(int n, const int *idx, double *v, double *saved, hipStream_t s);
+void ess_restore(int n, const int *idx, const double *saved, double *v, double *y, hipStream_t s);
 //   z = dinv .* r  (dinv may be null -> z = r)
 void pcg_precond(int n, const double *dinv, const double *r, double *z, hipStream_t s);
 //   d = z + (betanom/nom) d

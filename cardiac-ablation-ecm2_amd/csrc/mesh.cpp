@@ -4,6 +4,8 @@
 #include "fe.hpp"
 
 #include <algorithm>
+#include <string>
+#include <cstdlib>
 #include <array>
 #include <cstring>
 #include <fstream>
@@ -244,6 +246,32 @@ void HexMesh::refine_uniform()
    if (nx) { nx = 0; ny = 0; nz = 0; }  // element order is no longer lexicographic
 }
 
+namespace
+{
+uint64_t spread3(uint64_t v)  // 21 bits -> every third bit
+{
+   v &= 0x1fffff;
+   v = (v | v << 32) & 0x1f00000000ffffull;
+   v = (v | v << 16) & 0x1f0000ff0000ffull;
+   v = (v | v << 8) & 0x100f00f00f00f00full;
+   v = (v | v << 4) & 0x10c30c30c30c30c3ull;
+   v = (v | v << 2) & 0x1249249249249249ull;
+   return v;
+}
+
+// Order in which complete bricks are visited: lexicographic (default) or along a Morton
+// curve (ECM2_BRICK_CURVE=morton, experiment knob: neighbouring bricks, which share x
+// values, are processed closer in time on large meshes).
+bool brick_curve_morton()
+{
+   static bool v = [] {
+      const char *e = std::getenv("ECM2_BRICK_CURVE");
+      return e && std::string(e) == "morton";
+   }();
+   return v;
+}
+} // namespace
+
 std::vector<int> brick_order(const std::vector<int> &elems, int nx, int ny, int nz)
 {
    const int bx = (nx + 3) / 4, by = (ny + 3) / 4, bz = (nz + 3) / 4;
@@ -253,14 +281,20 @@ std::vector<int> brick_order(const std::vector<int> &elems, int nx, int ny, int 
       const int ex = e % nx, ey = (e / nx) % ny, ez = e / (nx * ny);
       return (long)(ex / 4) + bx * ((long)(ey / 4) + (long)by * (ez / 4));
    };
+   const bool morton = brick_curve_morton();
+   auto curve = [&](long k) -> uint64_t {
+      if (!morton) { return (uint64_t)k; }
+      const uint64_t ix = k % bx, iy = (k / bx) % by, iz = k / ((long)bx * by);
+      return spread3(ix) | spread3(iy) << 1 | spread3(iz) << 2;
+   };
    for (int e : elems) { count[key(e)]++; }
    std::vector<int> out;
    out.reserve(elems.size());
-   // complete bricks, in brick-lexicographic order, members x-fastest
+   // complete bricks, in brick order (lexicographic or Morton), members x-fastest
    std::vector<int> sorted(elems);
    std::stable_sort(sorted.begin(), sorted.end(), [&](int a, int b) {
       const long ka = key(a), kb = key(b);
-      if (ka != kb) { return ka < kb; }
+      if (ka != kb) { return curve(ka) < curve(kb); }
       const int ax = a % nx % 4, ay = (a / nx) % ny % 4, az = (a / (nx * ny)) % 4;
       const int bxx = b % nx % 4, byy = (b / nx) % ny % 4, bzz = (b / (nx * ny)) % 4;
       return ax + 4 * ay + 16 * az < bxx + 4 * byy + 16 * bzz;
@@ -292,15 +326,7 @@ std::vector<int> element_order(const HexMesh &m, int kind)
          lo[d] = std::min(lo[d], c[3 * (size_t)e + d]);
          hi[d] = std::max(hi[d], c[3 * (size_t)e + d]);
       }
-   auto spread = [](uint64_t v) {  // 21 bits -> every third bit
-      v &= 0x1fffff;
-      v = (v | v << 32) & 0x1f00000000ffffull;
-      v = (v | v << 16) & 0x1f0000ff0000ffull;
-      v = (v | v << 8) & 0x100f00f00f00f00full;
-      v = (v | v << 4) & 0x10c30c30c30c30c3ull;
-      v = (v | v << 2) & 0x1249249249249249ull;
-      return v;
-   };
+   auto spread = spread3;
    std::vector<uint64_t> code(m.ne);
    for (int e = 0; e < m.ne; e++)
    {

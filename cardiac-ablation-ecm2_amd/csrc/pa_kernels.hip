@@ -1301,6 +1301,53 @@ __global__ void k_pcg_update_xr(int n, const double *__restrict__ nom,
    r[i] = r[i] + (-alpha) * z[i];
 }
 
+// One fused PCG update (CGSolver::Mult's add/Mult(prec)/Dot sequence, solvers.cpp:930-960):
+// alpha = nom/den; x += alpha d; r -= alpha Ad; z = dinv .* r (jacobi) ; partial sums of r.z
+// (or r.r) in the fixed grid-stride order of k_dot_partial, finished by k_dot_final.
+// z holds A d on entry and the preconditioned residual on exit (jacobi only).
+__global__ void __launch_bounds__(256)
+k_pcg_step(int n, const double *__restrict__ nom, const double *__restrict__ den,
+           const double *__restrict__ d, double *__restrict__ z, double *__restrict__ x,
+           double *__restrict__ r, const double *__restrict__ dinv, double *__restrict__ partials)
+{
+   __shared__ double red[4];
+   const double alpha = *nom / *den;
+   double s = 0.0;
+   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+   {
+      x[i] = x[i] + alpha * d[i];
+      const double rn = r[i] + (-alpha) * z[i];
+      r[i] = rn;
+      if (dinv)
+      {
+         const double zn = dinv[i] * rn;
+         z[i] = zn;
+         s += rn * zn;
+      }
+      else { s += rn * rn; }
+   }
+   for (int off = 32; off > 0; off >>= 1) { s += __shfl_down(s, off, 64); }
+   if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6] = s; }
+   __syncthreads();
+   if (threadIdx.x == 0) { partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]); }
+}
+
+// ConstrainedOperator around a Mult without a vector copy: saved = v[ess], v[ess] = 0 ...
+__global__ void k_ess_save_zero(int n, const int *__restrict__ idx, double *__restrict__ v,
+                                double *__restrict__ saved)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { saved[i] = v[idx[i]]; v[idx[i]] = 0.0; }
+}
+
+// ... then v[ess] = y[ess] = saved (DIAG_ONE rows)
+__global__ void k_ess_restore(int n, const int *__restrict__ idx, const double *__restrict__ saved,
+                              double *__restrict__ v, double *__restrict__ y)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { v[idx[i]] = saved[i]; y[idx[i]] = saved[i]; }
+}
+
 __global__ void k_pcg_precond(int n, const double *__restrict__ dinv, const double *__restrict__ r,
                               double *__restrict__ z)
 {
@@ -1770,6 +1817,28 @@ void pcg_update_xr(int n, const double *nom, const double *den, const double *d,
                    double *x, double *r, hipStream_t s)
 {
    hipLaunchKernelGGL(k_pcg_update_xr, dim3(grid_for(n, 256)), dim3(256), 0, s, n, nom, den, d, z, x, r);
+   ECM2_HIP(hipGetLastError());
+}
+
+void pcg_step(int n, const double *nom, const double *den, const double *d, double *z, double *x, double *r,
+              const double *dinv, double *partials, double *out, hipStream_t s)
+{
+   hipLaunchKernelGGL(k_pcg_step, dim3(kDotBlocks), dim3(256), 0, s, n, nom, den, d, z, x, r, dinv, partials);
+   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, s, kDotBlocks, partials, out);
+   ECM2_HIP(hipGetLastError());
+}
+
+void ess_save_zero(int n, const int *idx, double *v, double *saved, hipStream_t s)
+{
+   if (n <= 0) { return; }
+   hipLaunchKernelGGL(k_ess_save_zero, dim3(grid_for(n, 256)), dim3(256), 0, s, n, idx, v, saved);
+   ECM2_HIP(hipGetLastError());
+}
+
+void ess_restore(int n, const int *idx, const double *saved, double *v, double *y, hipStream_t s)
+{
+   if (n <= 0) { return; }
+   hipLaunchKernelGGL(k_ess_restore, dim3(grid_for(n, 256)), dim3(256), 0, s, n, idx, saved, v, y);
    ECM2_HIP(hipGetLastError());
 }
 

@@ -44,7 +44,7 @@ PCGResult pcg_solve(LinOp &A, const int *ess, int n_ess, const double *b, double
 {
    const int n = A.size();
    PCGResult res;
-   DeviceArray<double> r(std::max(n, 1)), d(std::max(n, 1)), z(std::max(n, 1)), zc(std::max(n, 1));
+   DeviceArray<double> r(std::max(n, 1)), d(std::max(n, 1)), z(std::max(n, 1)), saved(std::max(n_ess, 1));
    DeviceArray<double> partials(1024), scal(4), dinv;
    double *nom = scal.data(), *den = scal.data() + 1, *betanom = scal.data() + 2;
    double *hs = nullptr;
@@ -59,13 +59,14 @@ PCGResult pcg_solve(LinOp &A, const int *ess, int n_ess, const double *b, double
       ECM2_HIP(hipStreamSynchronize(s));
       return hs[0];
    };
-   // ConstrainedOperator::ConstrainedMult, DIAG_ONE (operator.cpp:586-646)
-   auto cmult = [&](const double *in, double *out) {
+   // ConstrainedOperator::ConstrainedMult, DIAG_ONE (operator.cpp:586-646): the input's
+   // ess entries are zeroed in place for the Mult and restored after (no vector copy);
+   // out[ess] = in[ess]
+   auto cmult = [&](double *in, double *out) {
       if (n_ess == 0) { A.mult(in, out, s); return; }
-      ECM2_HIP(hipMemcpyAsync(zc.data(), in, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
-      kern::set_values(n_ess, ess, 0.0, zc.data(), s);
-      A.mult(zc.data(), out, s);
-      kern::copy_values(n_ess, ess, in, out, s);
+      kern::ess_save_zero(n_ess, ess, in, saved.data(), s);
+      A.mult(in, out, s);
+      kern::ess_restore(n_ess, ess, saved.data(), in, out, s);
    };
    try
    {
@@ -102,13 +103,10 @@ PCGResult pcg_solve(LinOp &A, const int *ess, int n_ess, const double *b, double
          {
             for (int i = 1;;)
             {
-               kern::pcg_update_xr(n, nom, den, d.data(), z.data(), x, r.data(), s);
-               if (jacobi)
-               {
-                  kern::pcg_precond(n, dinv.data(), r.data(), z.data(), s);
-                  dot(r.data(), z.data(), betanom);
-               }
-               else { dot(r.data(), r.data(), betanom); }
+               // x += alpha d, r -= alpha A d, z = M^{-1} r, betanom = r.z in one pass
+               kern::pcg_step(n, nom, den, d.data(), z.data(), x, r.data(), jacobi ? dinv.data() : nullptr,
+                              partials.data(), betanom, s);
+               A.sum_scalars(betanom, 1, s);
                const double bn = readback(betanom);
                res.final_norm = bn >= 0 ? std::sqrt(bn) : bn;
                res.iterations = i;

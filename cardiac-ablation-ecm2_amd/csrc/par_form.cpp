@@ -44,17 +44,17 @@ ParPAForm::ParPAForm(const LocalPart &part, const double *enodes_local_host, int
       ncclComm_t comm;
       ECM2_NCCL(ncclCommInitRank(&comm, part.nranks, id, part.rank));
       comm_ = comm;
-      // highest priority: the boundary elements and the RCCL kernels on the comm stream are
-      // dispatched ahead of the interior kernel's remaining workgroups, so the exchange
-      // overlaps the interior instead of queueing behind it
-      int prio_least = 0, prio_greatest = 0;
-      ECM2_HIP(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
-      ECM2_HIP(hipStreamCreateWithPriority(&cs_, hipStreamNonBlocking, prio_greatest));
-      ECM2_HIP(hipEventCreateWithFlags(&ev_pack_, hipEventDisableTiming));
-      ECM2_HIP(hipEventCreateWithFlags(&ev_xg_, hipEventDisableTiming));
-      ECM2_HIP(hipEventCreateWithFlags(&ev_yg_, hipEventDisableTiming));
-      ECM2_HIP(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
    }
+   // The comm stream (both transports) has the highest priority: the boundary elements and
+   // the exchange kernels are dispatched ahead of the interior kernel's remaining
+   // workgroups, so the exchange overlaps the interior instead of queueing behind it.
+   int prio_least = 0, prio_greatest = 0;
+   ECM2_HIP(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
+   ECM2_HIP(hipStreamCreateWithPriority(&cs_, hipStreamNonBlocking, prio_greatest));
+   ECM2_HIP(hipEventCreateWithFlags(&ev_pack_, hipEventDisableTiming));
+   ECM2_HIP(hipEventCreateWithFlags(&ev_xg_, hipEventDisableTiming));
+   ECM2_HIP(hipEventCreateWithFlags(&ev_yg_, hipEventDisableTiming));
+   ECM2_HIP(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
    ECM2_HIP(hipDeviceSynchronize());
 }
 
@@ -70,7 +70,17 @@ ParPAForm::~ParPAForm()
 
 void ParPAForm::assemble(hipStream_t s) { local_->assemble(s); }
 
-void ParPAForm::phase_pack(const double *x_true, double *y_true, hipStream_t s)
+// ---------------------------------------------------------------------------------------
+// Mult stages.  Per rank:
+//   s  : pack (owned interface values -> send buffer), record ev_pack
+//   cs : wait ev_pack; P exchange (ghost block <- owners); boundary elements; ghost shared
+//        sums; record ev_yg; P^T exchange (ghost block -> owners' receive buffer); ev_done
+//   s  : interior elements; wait ev_yg; owned shared sums; wait ev_done; add received
+// The RCCL transport runs the stages of one rank in order; the loopback group enqueues
+// them stage-major over its members, with peer device copies for the exchanges, so both
+// transports share the same streams, events and overlap.
+// ---------------------------------------------------------------------------------------
+void ParPAForm::stage_pack(const double *x_true, double *y_true, hipStream_t s)
 {
    if (!local_->use_partials())
    {
@@ -78,9 +88,22 @@ void ParPAForm::phase_pack(const double *x_true, double *y_true, hipStream_t s)
       if (part_.n_ghost) { ECM2_HIP(hipMemsetAsync(yg_.data(), 0, sizeof(double) * part_.n_ghost, s)); }
    }
    kern::gather_idx((int)part_.send_idx.size(), send_idx_.data(), x_true, sendbuf_.data(), s);
+   ECM2_HIP(hipEventRecord(ev_pack_, s));
+   ECM2_HIP(hipStreamWaitEvent(cs_, ev_pack_, 0));
 }
 
-void ParPAForm::phase_interior(const double *x_true, double *y_true, hipStream_t s)
+void ParPAForm::stage_boundary(const double *x_true, double *y_true)
+{
+   const int b_int = part_.ne_interior / kElemBlock;
+   local_->record_start_public(cs_);
+   local_->apply_blocks(x_true, xg_.data(), y_true, yg_.data(), b_int, local_->nblocks(), cs_);
+   local_->record_stop_public(cs_);
+   // ghost dofs are touched only by boundary elements: their sums are complete here
+   local_->finish_shared(local_->n_shared_owned(), local_->n_shared(), y_true, yg_.data(), cs_);
+   ECM2_HIP(hipEventRecord(ev_yg_, cs_));
+}
+
+void ParPAForm::stage_interior(const double *x_true, double *y_true, hipStream_t s)
 {
    const int b_int = part_.ne_interior / kElemBlock;
    local_->record_start_public(s);
@@ -88,71 +111,50 @@ void ParPAForm::phase_interior(const double *x_true, double *y_true, hipStream_t
    local_->record_stop_public(s);
 }
 
-void ParPAForm::phase_boundary(const double *x_true, double *y_true, hipStream_t s)
+void ParPAForm::stage_finish(double *y_true, hipStream_t s)
 {
-   const int b_int = part_.ne_interior / kElemBlock;
-   local_->record_start_public(s);
-   local_->apply_blocks(x_true, xg_.data(), y_true, yg_.data(), b_int, local_->nblocks(), s);
-   local_->record_stop_public(s);
-   local_->finish_shared(local_->n_shared_owned(), local_->n_shared(), y_true, yg_.data(), s);
-}
-
-void ParPAForm::phase_owned_shared(double *y_true, hipStream_t s)
-{
+   ECM2_HIP(hipEventRecord(ev_done_, cs_));
+   ECM2_HIP(hipStreamWaitEvent(s, ev_yg_, 0));
    local_->finish_shared(0, local_->n_shared_owned(), y_true, yg_.data(), s);
+   ECM2_HIP(hipStreamWaitEvent(s, ev_done_, 0));
+   kern::scatter_add_idx((int)part_.send_idx.size(), send_idx_.data(), rbuf_.data(), y_true, s);
 }
 
-void ParPAForm::phase_finish(double *y_true, hipStream_t s)
+void ParPAForm::rccl_exchange(bool transpose)
 {
-   kern::scatter_add_idx((int)part_.send_idx.size(), send_idx_.data(), rbuf_.data(), y_true, s);
+   ncclComm_t comm = (ncclComm_t)comm_;
+   const int nn = (int)part_.nbrs.size();
+   if (!nn) { return; }
+   ECM2_NCCL(ncclGroupStart());
+   for (int k = 0; k < nn; k++)
+   {
+      const size_t nown = part_.send_off[k + 1] - part_.send_off[k];  // my owned dofs neighbour k ghosts
+      const size_t ngh = part_.recv_off[k + 1] - part_.recv_off[k];   // my ghosts owned by neighbour k
+      if (!transpose)
+      {
+         // P (tag 41822 in the reference): owner values -> ghost copies
+         if (nown) { ECM2_NCCL(ncclSend(sendbuf_.data() + part_.send_off[k], nown, ncclFloat64, part_.nbrs[k], comm, cs_)); }
+         if (ngh) { ECM2_NCCL(ncclRecv(xg_.data() + part_.recv_off[k], ngh, ncclFloat64, part_.nbrs[k], comm, cs_)); }
+      }
+      else
+      {
+         // P^T (tag 41823): ghost contributions -> owners
+         if (ngh) { ECM2_NCCL(ncclSend(yg_.data() + part_.recv_off[k], ngh, ncclFloat64, part_.nbrs[k], comm, cs_)); }
+         if (nown) { ECM2_NCCL(ncclRecv(rbuf_.data() + part_.send_off[k], nown, ncclFloat64, part_.nbrs[k], comm, cs_)); }
+      }
+   }
+   ECM2_NCCL(ncclGroupEnd());
 }
 
 void ParPAForm::mult(const double *x_true, double *y_true, hipStream_t s)
 {
    ECM2_VERIFY(comm_, ERR_STATE, "mult needs the RCCL transport (use the loopback group otherwise)");
-   ncclComm_t comm = (ncclComm_t)comm_;
-   const int nn = (int)part_.nbrs.size();
-   // P: owner values -> ghost copies (tag 41822 in the reference)
-   phase_pack(x_true, y_true, s);
-   ECM2_HIP(hipEventRecord(ev_pack_, s));
-   ECM2_HIP(hipStreamWaitEvent(cs_, ev_pack_, 0));
-   if (nn)
-   {
-      ECM2_NCCL(ncclGroupStart());
-      for (int k = 0; k < nn; k++)
-      {
-         const size_t ns = part_.send_off[k + 1] - part_.send_off[k];
-         const size_t nr = part_.recv_off[k + 1] - part_.recv_off[k];
-         if (ns) { ECM2_NCCL(ncclSend(sendbuf_.data() + part_.send_off[k], ns, ncclFloat64, part_.nbrs[k], comm, cs_)); }
-         if (nr) { ECM2_NCCL(ncclRecv(xg_.data() + part_.recv_off[k], nr, ncclFloat64, part_.nbrs[k], comm, cs_)); }
-      }
-      ECM2_NCCL(ncclGroupEnd());
-   }
-   // boundary elements (those touching ghosts) run on the comm stream as soon as the
-   // ghost values land, concurrently with the interior elements on the caller's stream
-   phase_boundary(x_true, y_true, cs_);
-   ECM2_HIP(hipEventRecord(ev_yg_, cs_));
-   // P^T: ghost contributions -> owners (tag 41823)
-   if (nn)
-   {
-      ECM2_NCCL(ncclGroupStart());
-      for (int k = 0; k < nn; k++)
-      {
-         const size_t ns = part_.recv_off[k + 1] - part_.recv_off[k];
-         const size_t nr = part_.send_off[k + 1] - part_.send_off[k];
-         if (ns) { ECM2_NCCL(ncclSend(yg_.data() + part_.recv_off[k], ns, ncclFloat64, part_.nbrs[k], comm, cs_)); }
-         if (nr) { ECM2_NCCL(ncclRecv(rbuf_.data() + part_.send_off[k], nr, ncclFloat64, part_.nbrs[k], comm, cs_)); }
-      }
-      ECM2_NCCL(ncclGroupEnd());
-   }
-   ECM2_HIP(hipEventRecord(ev_done_, cs_));
-   // interior elements overlap the whole exchange; the owned shared dofs need both
-   // element phases, the received contributions are added last
-   phase_interior(x_true, y_true, s);
-   ECM2_HIP(hipStreamWaitEvent(s, ev_yg_, 0));
-   phase_owned_shared(y_true, s);
-   ECM2_HIP(hipStreamWaitEvent(s, ev_done_, 0));
-   phase_finish(y_true, s);
+   stage_pack(x_true, y_true, s);
+   rccl_exchange(false);
+   stage_boundary(x_true, y_true);
+   rccl_exchange(true);
+   stage_interior(x_true, y_true, s);
+   stage_finish(y_true, s);
 }
 
 void ParPAForm::diag_local(double *d_true, hipStream_t s)
@@ -214,11 +216,13 @@ void par_group_mult(std::vector<ParPAForm *> &forms, const std::vector<const dou
       ECM2_VERIFY(it != nb.end(), ERR_INTERNAL, "asymmetric neighbour lists");
       return (int)(it - nb.begin());
    };
-   for (int r = 0; r < n; r++) { forms[r]->phase_pack(x[r], y[r], s); }
-   // P: copy each owner's packed block into the receiver's ghost block
+   // the same stages as ParPAForm::mult, stage-major over the members; a member's
+   // exchanges wait for its peers' events and copy from their buffers on its comm stream
+   for (int r = 0; r < n; r++) { forms[r]->stage_pack(x[r], y[r], s); }
    for (int r = 0; r < n; r++)
    {
-      const LocalPart &pr = forms[r]->part();
+      ParPAForm &f = *forms[r];
+      const LocalPart &pr = f.part();
       for (size_t k = 0; k < pr.nbrs.size(); k++)
       {
          const int o = pr.nbrs[k], j = slot(o, r);
@@ -226,23 +230,17 @@ void par_group_mult(std::vector<ParPAForm *> &forms, const std::vector<const dou
          const size_t cnt = pr.recv_off[k + 1] - pr.recv_off[k];
          ECM2_VERIFY(cnt == (size_t)(po.send_off[j + 1] - po.send_off[j]), ERR_INTERNAL,
                      "exchange size mismatch " << r << "<-" << o);
-         if (cnt)
-         {
-            ECM2_HIP(hipMemcpyAsync(forms[r]->xghost() + pr.recv_off[k], forms[o]->sendbuf() + po.send_off[j],
-                                    cnt * sizeof(double), hipMemcpyDeviceToDevice, s));
-         }
+         if (!cnt) { continue; }
+         ECM2_HIP(hipStreamWaitEvent(f.comm_stream(), forms[o]->event_packed(), 0));
+         ECM2_HIP(hipMemcpyAsync(f.xghost() + pr.recv_off[k], forms[o]->sendbuf() + po.send_off[j],
+                                 cnt * sizeof(double), hipMemcpyDeviceToDevice, f.comm_stream()));
       }
    }
+   for (int r = 0; r < n; r++) { forms[r]->stage_boundary(x[r], y[r]); }
    for (int r = 0; r < n; r++)
    {
-      forms[r]->phase_interior(x[r], y[r], s);
-      forms[r]->phase_boundary(x[r], y[r], s);
-      forms[r]->phase_owned_shared(y[r], s);
-   }
-   // P^T: copy each ghost block into the owner's receive buffer, then add
-   for (int r = 0; r < n; r++)
-   {
-      const LocalPart &pr = forms[r]->part();
+      ParPAForm &f = *forms[r];
+      const LocalPart &pr = f.part();
       for (size_t k = 0; k < pr.nbrs.size(); k++)
       {
          const int g = pr.nbrs[k], j = slot(g, r);
@@ -250,14 +248,14 @@ void par_group_mult(std::vector<ParPAForm *> &forms, const std::vector<const dou
          const size_t cnt = pr.send_off[k + 1] - pr.send_off[k];
          ECM2_VERIFY(cnt == (size_t)(pg.recv_off[j + 1] - pg.recv_off[j]), ERR_INTERNAL,
                      "reduce size mismatch " << r << "<-" << g);
-         if (cnt)
-         {
-            ECM2_HIP(hipMemcpyAsync(forms[r]->recvbuf() + pr.send_off[k], forms[g]->yghost() + pg.recv_off[j],
-                                    cnt * sizeof(double), hipMemcpyDeviceToDevice, s));
-         }
+         if (!cnt) { continue; }
+         ECM2_HIP(hipStreamWaitEvent(f.comm_stream(), forms[g]->event_ghosts_summed(), 0));
+         ECM2_HIP(hipMemcpyAsync(f.recvbuf() + pr.send_off[k], forms[g]->yghost() + pg.recv_off[j],
+                                 cnt * sizeof(double), hipMemcpyDeviceToDevice, f.comm_stream()));
       }
    }
-   for (int r = 0; r < n; r++) { forms[r]->phase_finish(y[r], s); }
+   for (int r = 0; r < n; r++) { forms[r]->stage_interior(x[r], y[r], s); }
+   for (int r = 0; r < n; r++) { forms[r]->stage_finish(y[r], s); }
 }
 
 } // namespace ecm2

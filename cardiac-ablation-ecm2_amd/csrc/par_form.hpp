@@ -46,15 +46,18 @@ public:
    // Pieces of assemble_diagonal shared with the loopback group.
    void diag_local(double *d_true, hipStream_t s);  // d_true = owned part, ghost part -> yghost()
 
-   // Phases (used by mult and by the loopback group).
-   void phase_pack(const double *x_true, double *y_true, hipStream_t s);
-   void phase_interior(const double *x_true, double *y_true, hipStream_t s);
-   // boundary elements, then (partial scatter) the ghost shared dofs, which only
-   // boundary elements touch
-   void phase_boundary(const double *x_true, double *y_true, hipStream_t s);
-   // owned shared dofs (partial scatter); after both element phases
-   void phase_owned_shared(double *y_true, hipStream_t s);
-   void phase_finish(double *y_true, hipStream_t s);
+   // Mult stages (par_form.cpp), shared by the RCCL transport and the loopback group.
+   void stage_pack(const double *x_true, double *y_true, hipStream_t s);
+   void stage_boundary(const double *x_true, double *y_true);   // on the comm stream
+   void stage_interior(const double *x_true, double *y_true, hipStream_t s);
+   void stage_finish(double *y_true, hipStream_t s);
+   void phase_finish(double *y_true, hipStream_t s)  // add the received P^T contributions
+   {
+      kern::scatter_add_idx((int)part_.send_idx.size(), send_idx_.data(), rbuf_.data(), y_true, s);
+   }
+   hipStream_t comm_stream() const { return cs_; }
+   hipEvent_t event_packed() const { return ev_pack_; }
+   hipEvent_t event_ghosts_summed() const { return ev_yg_; }
 
    // buffers (device)
    double *sendbuf() { return sendbuf_.data(); }
@@ -63,6 +66,7 @@ public:
    double *recvbuf() { return rbuf_.data(); }
 
 private:
+   void rccl_exchange(bool transpose);  // P (false) or P^T (true) on the comm stream
    LocalPart part_;
    std::unique_ptr<PAForm> local_;
    DeviceArray<int> send_idx_;

@@ -136,7 +136,8 @@ int ecm2_pa_form_set_scatter(ecm2_pa_form *f, int mode);
 int ecm2_pa_form_scatter_info(const ecm2_pa_form *f, int *n_shared, long *n_slots);
 /* Optional element permutation for the fused kernel's blocked layout (host perm[ne]:
  * internal position i <- caller element perm[i]); see ecm2_mesh_element_order.  All
- * entry points keep the caller's element order. */
+ * entry points keep the caller's element order (the reference's E-vector order,
+ * restriction.cpp:26-107, is never exposed differently). */
 int ecm2_pa_form_set_element_order(ecm2_pa_form *f, const int *perm);
 /* BilinearForm::Assemble -> PABilinearFormExtension::Assemble -> AssemblePA
  * (bilinearform.cpp:456-460, bilinearform_ext.cpp:332-368). */
@@ -161,6 +162,7 @@ int ecm2_pa_form_timing(ecm2_pa_form *f, int enable);
 int ecm2_pa_form_timing_get(ecm2_pa_form *f, double *total_ms, long *launches);
 /* SURVEY §8(d) algorithmic bytes per Mult: 8*NE*NQ*(6+1) + 16*ndofs + 4*NE*ND. */
 int ecm2_pa_form_algorithmic_bytes(const ecm2_pa_form *f, double *bytes);
+/* ~PABilinearFormExtension / BilinearForm::Update (bilinearform_ext.hpp:67-144). */
 void ecm2_pa_form_destroy(ecm2_pa_form *f);
 
 /* ------------------------------------------------------------------------ */
@@ -186,10 +188,13 @@ int ecm2_operator_from_par_form(ecm2_par_form *f, ecm2_operator **out);
 /* forms[r] must be rank r of an n-rank partition; vectors are the concatenation of the
  * ranks' true vectors (rank r at offset sum_{q<r} n_owned(q)). */
 int ecm2_operator_from_par_group(ecm2_par_form *const *forms, int n, ecm2_operator **out);
+/* Operator::Height/Width and Operator::Mult (operator.hpp:24-110). */
 int ecm2_operator_size(const ecm2_operator *op, int *n);
 int ecm2_operator_mult(ecm2_operator *op, const double *x, double *y, void *stream);
-/* ecm2_pcg_solve on any operator; with the RCCL form every rank calls it collectively
- * (dots are summed with ncclAllReduce, solvers.cpp). */
+/* ConstrainedOperator (operator.cpp:586-646) + CGSolver::Mult (solvers.cpp:869-1004) +
+ * OperatorJacobiSmoother on any operator; with the RCCL form every rank calls it
+ * collectively (dots are summed with ncclAllReduce, as the reference's parallel
+ * InnerProduct sums with MPI_Allreduce). */
 int ecm2_operator_pcg(ecm2_operator *op, const int *ess, int n_ess, const double *b, double *x,
                       double rel_tol, double abs_tol, int max_iter, int jacobi, int *iterations,
                       double *final_norm, void *stream);
@@ -230,11 +235,15 @@ int ecm2_partition_info(const ecm2_partition *p, int *ne_local, int *ne_interior
  * [n_nbrs+1], send_idx [n_send] (owned local indices). */
 int ecm2_partition_get(const ecm2_partition *p, int *elems, int *local_to_global, int *gather_map,
                        int *nbrs, int *send_off, int *send_idx, int *recv_off);
+/* ~ParFiniteElementSpace / ~ParMesh of the local view. */
 void ecm2_partition_destroy(ecm2_partition *p);
 
-/* ncclGetUniqueId (128 bytes) for ecm2_par_form_create; broadcast it to all ranks. */
+/* ncclGetUniqueId (128 bytes) for ecm2_par_form_create; broadcast it to all ranks (the
+ * reference's communicator is the ParMesh's MPI_Comm, pmesh.hpp:33). */
 int ecm2_rccl_unique_id(unsigned char *id128);
-/* enodes_local: host [ne_local][3][8] in the partition's local element order.
+/* ParBilinearForm(pfes) + SetAssemblyLevel(PARTIAL) (pbilinearform.hpp, bilinearform.cpp:
+ * 109-136) on the rank's local space.  enodes_local: host [ne_local][3][8] in the
+ * partition's local element order.
  * rccl_id: 128-byte id (one process per GPU, ncclCommInitRank) or NULL for a member of an
  * in-process loopback group (ecm2_par_group_mult). */
 int ecm2_par_form_create(const ecm2_partition *p, const double *enodes_local, int q1d,
@@ -243,9 +252,12 @@ int ecm2_par_form_create(const ecm2_partition *p, const double *enodes_local, in
  * element order; GRIDFUNC_AFFINE -> device local L-vector [n_owned + n_ghost]. */
 int ecm2_par_form_add_integrator(ecm2_par_form *f, int integrator, int coeff_kind,
                                  const double *data, const double *params);
+/* As ecm2_pa_form_set_kernel (fused kernels only). */
 int ecm2_par_form_set_kernel(ecm2_par_form *f, int kernel);
 /* Scatter mode of the local form (ECM2_SCATTER_*; see ecm2_pa_form_set_scatter). */
 int ecm2_par_form_set_scatter(ecm2_par_form *f, int mode);
+/* ParBilinearForm::Assemble -> local PABilinearFormExtension::Assemble
+ * (pbilinearform.cpp:475-511, bilinearform_ext.cpp:332-368). */
 int ecm2_par_form_assemble(ecm2_par_form *f, void *stream);
 /* RAPOperator::Mult (operator.hpp:977): y_true = P^T A P x_true; x_true, y_true device
  * [n_owned].  Grouped ncclSend/ncclRecv on an internal stream overlapped with the
@@ -257,10 +269,13 @@ int ecm2_par_group_mult(ecm2_par_form *const *forms, int n, const double *const 
 /* ParBilinearForm::AssembleDiagonal on the true dofs (local PA diagonal + P^T). */
 int ecm2_par_form_assemble_diagonal(ecm2_par_form *f, double *d_true, void *stream);
 int ecm2_par_group_diagonal(ecm2_par_form *const *forms, int n, double *const *d_true, void *stream);
+/* Measurement and introspection (no reference counterpart): HIP-event timing of the local
+ * apply kernels, SURVEY §8(d) bytes of the local form, true size and resolved kernel. */
 int ecm2_par_form_timing(ecm2_par_form *f, int enable);
 int ecm2_par_form_timing_get(ecm2_par_form *f, double *total_ms, long *launches);
 int ecm2_par_form_algorithmic_bytes(const ecm2_par_form *f, double *bytes);
 int ecm2_par_form_info(const ecm2_par_form *f, int *n_true, int *kernel);
+/* ~ParBilinearForm. */
 void ecm2_par_form_destroy(ecm2_par_form *f);
 
 #ifdef __cplusplus

@@ -88,6 +88,8 @@ def load_library(path: str = LIB_PATH):
         "ecm2_pa_form_set_kernel": (i32, [vp, i32]),
         "ecm2_pa_form_set_scatter": (i32, [vp, i32]),
         "ecm2_pa_form_scatter_info": (i32, [vp, vp, vp]),
+        "ecm2_pa_form_set_bricks": (i32, [vp, i32]),
+        "ecm2_pa_form_brick_info": (i32, [vp, ip, ip]),
         "ecm2_pa_form_set_element_order": (i32, [vp, vp]),
         "ecm2_mesh_element_order": (i32, [vp, i32, vp]),
         "ecm2_pa_form_assemble": (i32, [vp, vp]),
@@ -316,7 +318,7 @@ class BilinearForm:
     """BilinearForm at AssemblyLevel::PARTIAL backed by the HIP PA form."""
 
     def __init__(self, fes: H1Space, kernel: int = KERNEL_AUTO, q1d: int = 0, geometry: str = "nodes",
-                 element_order: str = "auto", scatter: str = "partials"):
+                 element_order: str = "auto", scatter: str = "partials", bricks: int = -1):
         self.fes = fes
         self._integs = []
         self._kernel = kernel
@@ -330,6 +332,7 @@ class BilinearForm:
             _check(_lib.ecm2_pa_form_set_element_nodes(h, _np_ptr(en)))
         _check(_lib.ecm2_pa_form_set_kernel(h, kernel))
         _check(_lib.ecm2_pa_form_set_scatter(h, _SCATTER[scatter]))
+        _check(_lib.ecm2_pa_form_set_bricks(h, bricks))
         if element_order != "native" and fes.ne > 0:
             if element_order in ("auto", "brick"):
                 try:
@@ -380,6 +383,12 @@ class BilinearForm:
         n, m = ctypes.c_int(), ctypes.c_long()
         _check(_lib.ecm2_pa_form_scatter_info(self._h, ctypes.byref(n), ctypes.byref(m)))
         return n.value, m.value
+
+    def BrickInfo(self):
+        """(bricks, depth bz) of the p >= 3 brick kernel after Assemble (0, 0: none)."""
+        n, bz = ctypes.c_int(), ctypes.c_int()
+        _check(_lib.ecm2_pa_form_brick_info(self._h, ctypes.byref(n), ctypes.byref(bz)))
+        return n.value, bz.value
 
     def Mult(self, x, y, stream=None):
         _check(_lib.ecm2_pa_form_mult(self._h, _dev_ptr(x), _dev_ptr(y), _stream(stream)))
@@ -449,6 +458,7 @@ _PAR_SIGS = {
                                                     ctypes.c_void_p]),
     "ecm2_par_form_set_kernel": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ecm2_par_form_set_scatter": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "ecm2_par_form_set_bricks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ecm2_par_form_assemble": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "ecm2_par_form_mult": (ctypes.c_int, [ctypes.c_void_p] * 4),
     "ecm2_par_group_mult": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
@@ -553,7 +563,7 @@ class ParBilinearForm:
     group member (use ParGroup.Mult); otherwise one process per GPU over RCCL."""
 
     def __init__(self, part: Partition, rccl_id: Optional[bytes] = None, kernel: int = KERNEL_AUTO, q1d: int = 0,
-                 scatter: str = "partials"):
+                 scatter: str = "partials", bricks: int = -1):
         lib = _par_lib()
         self.part = part
         self._keep = []
@@ -569,6 +579,7 @@ class ParBilinearForm:
         self._h = h
         _check(lib.ecm2_par_form_set_kernel(h, kernel))
         _check(lib.ecm2_par_form_set_scatter(h, _SCATTER[scatter]))
+        _check(lib.ecm2_par_form_set_bricks(h, bricks))
         self.true_size = part.n_owned
 
     def __del__(self):

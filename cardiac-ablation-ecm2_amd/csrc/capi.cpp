@@ -323,6 +323,20 @@ int ecm2_pa_form_set_scatter(ecm2_pa_form *f, int mode)
    return guard([&] { NEED(f); f->f->set_scatter(mode); });
 }
 
+int ecm2_pa_form_set_bricks(ecm2_pa_form *f, int bz)
+{
+   return guard([&] { NEED(f); f->f->set_line_bricks(bz); });
+}
+
+int ecm2_pa_form_brick_info(const ecm2_pa_form *f, int *n_bricks, int *bz)
+{
+   return guard([&] {
+      NEED(f);
+      if (n_bricks) { *n_bricks = f->f->n_bricks(); }
+      if (bz) { *bz = f->f->brick_bz(); }
+   });
+}
+
 int ecm2_pa_form_scatter_info(const ecm2_pa_form *f, int *n_shared, long *n_slots)
 {
    return guard([&] {
@@ -508,6 +522,11 @@ int ecm2_par_form_add_integrator(ecm2_par_form *f, int integrator, int coeff_kin
       }
       f->f->local().add_integrator(integrator, c);
    });
+}
+
+int ecm2_par_form_set_bricks(ecm2_par_form *f, int bz)
+{
+   return guard([&] { NEED(f); f->f->local().set_line_bricks(bz); });
 }
 
 int ecm2_par_form_set_scatter(ecm2_par_form *f, int mode)

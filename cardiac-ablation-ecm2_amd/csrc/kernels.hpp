@@ -73,6 +73,12 @@ struct ApplyArgs
    double *part = nullptr;          // partial slots of shared dofs (null: atomics)
    const int *chunks = nullptr;     // LINE: device chunk table (first | count << 24)
    const int *chunk_off = nullptr;  // LINE: host [nblk + 1], chunks of 64-element block b
+   // LINE, brick part (p >= 3 on structured regions): bricks of 2 x 2 x brick_bz elements
+   const int *belem = nullptr;      // device [nbrick][4 bz] element ids (qdata addressing)
+   const int *bmap = nullptr;       // device [nbrick][NB] lattice map: dof | shared << 30
+   const int *brick_off = nullptr;  // host [nblk + 1], bricks whose first element lies in block b
+   int brick_bz = 0;                // 0: no bricks
+   double *part_brick = nullptr;    // partial slots [nbrick][NB] of shared lattice points
 };
 
 namespace kern
@@ -107,6 +113,9 @@ int line_chunk_limit();
 // Write the constant-memory basis table of (D, Q) on the current device (once).
 void upload_basis(int D, int Q, const Basis1D &b);
 void apply_line(int D, int Q, bool mass, bool diff, const ApplyArgs &a, const Basis1D &b, hipStream_t s);
+// Brick kernel of the line family: (D, Q, bz) instantiated?  Lattice points per brick.
+bool has_brick(int D, int Q, int bz);
+int brick_points(int D, int bz);
 // Workgroup-per-element kernel, any layout; in/out either L-vectors (through the
 // gather map; output by atomics into a zeroed y) or E-vectors (accumulated).
 void apply_wpe(int D, int Q, bool mass, bool diff, const ApplyArgs &a, bool in_evec,

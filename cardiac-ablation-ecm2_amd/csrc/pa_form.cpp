@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 
 namespace ecm2
 {
@@ -65,6 +66,22 @@ void PAForm::set_jacobians(const double *J_device)
 {
    ECM2_VERIFY(ne_ == 0 || J_device, ERR_ARG, "null Jacobian array");
    jac_ = J_device;
+   assembled_ = false;
+}
+
+void PAForm::set_block_splits(const std::vector<int> &splits)
+{
+   for (int b : splits) { ECM2_VERIFY(b >= 0 && b <= layout_.nblk(), ERR_ARG, "block split " << b << " out of range"); }
+   splits_ = splits;
+   gmap_line_.resize(0);
+   assembled_ = false;
+}
+
+void PAForm::set_line_bricks(int bz)
+{
+   ECM2_VERIFY(bz >= -1 && bz <= 2, ERR_ARG, "brick mode " << bz << " not in {-1, 0, 1, 2}");
+   line_bricks_ = bz;
+   gmap_line_.resize(0);
    assembled_ = false;
 }
 
@@ -164,6 +181,97 @@ void build_merge_plan(int ne, int D, const std::vector<int> &gmap_int, int ndofs
    }
 }
 } // namespace
+
+// Bricks of the line kernel family (experiment knob ECM2_LINE_BRICK): 0 = none (every
+// element runs the per-element line kernel), 1 = 2 x 2 x 1 (default), 2 = 2 x 2 x 2.
+// Measured at C5 (68^3, p = 4; profiles/ab_brick.sh): kernel 1.018 ms (none), 0.902 ms
+// (2 x 2 x 1: 192 threads, 27 KB LDS, 5 workgroups per CU), 1.114 ms (2 x 2 x 2: 320
+// threads, 54 KB, 3 per CU -- fewer, larger workgroups stall longer at the barriers).
+static int line_brick_mode()
+{
+   static int v = [] {
+      const char *e = std::getenv("ECM2_LINE_BRICK");
+      return e ? std::max(0, std::min(2, std::atoi(e))) : 1;
+   }();
+   return v;
+}
+
+// Bricks of 2 x 2 x bz elements found by dof equality alone (any element order, any
+// conforming mesh): the x, y and z neighbours of e are the elements whose low face
+// (local index 0 along that direction) equals e's high face (index D-1) entry by entry;
+// a brick is e0, e1 = x(e0), e2 = y(e0), e3 = x(e2) = y(e1) and, for bz = 2, the z
+// neighbours of those, with all twelve internal faces checked, all elements in one
+// apply_blocks segment and no orientation signs.  Greedy in element order; bricks are
+// therefore ordered by first element.  belem: [nbrick][4 bz].
+static void find_bricks(int ne, int D, const std::vector<int> &gm, int bz, const std::vector<int> &seg,
+                        std::vector<int> &belem, std::vector<char> &in_brick)
+{
+   const int ND = D * D * D;
+   auto dof = [&](int e, int a) { const int g = gm[(size_t)e * ND + a]; return g >= 0 ? g : -1 - g; };
+   auto face = [D](int dir, int s, int i, int j) {
+      if (dir == 0) { return (j * D + i) * D + s; }
+      if (dir == 1) { return (j * D + s) * D + i; }
+      return (s * D + j) * D + i;
+   };
+   auto key = [&](int e, int dir, int s) {
+      uint64_t h = 1469598103934665603ull;
+      for (int j : {0, D - 1})
+         for (int i : {0, D - 1}) { h = (h ^ (uint64_t)(uint32_t)dof(e, face(dir, s, i, j))) * 1099511628211ull; }
+      return h;
+   };
+   std::vector<int> nbr[3];
+   for (int dir = 0; dir < 3; dir++)
+   {
+      nbr[dir].assign(ne, -1);
+      std::unordered_map<uint64_t, int> low;
+      low.reserve((size_t)ne * 2);
+      for (int e = 0; e < ne; e++)
+      {
+         auto it = low.emplace(key(e, dir, 0), e);
+         if (!it.second) { it.first->second = -1; }  // ambiguous: no neighbour through it
+      }
+      for (int e = 0; e < ne; e++)
+      {
+         auto it = low.find(key(e, dir, D - 1));
+         if (it == low.end() || it->second < 0 || it->second == e) { continue; }
+         const int f = it->second;
+         bool ok = true;
+         for (int j = 0; j < D && ok; j++)
+            for (int i = 0; i < D && ok; i++) { ok = dof(e, face(dir, D - 1, i, j)) == dof(f, face(dir, 0, i, j)); }
+         if (ok) { nbr[dir][e] = f; }
+      }
+   }
+   auto nb = [&](int dir, int e) { return e < 0 ? -1 : nbr[dir][e]; };
+   const int nbe = 4 * bz;
+   for (int e0 = 0; e0 < ne; e0++)
+   {
+      if (in_brick[e0]) { continue; }
+      int el[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+      el[0] = e0;
+      el[1] = nb(0, e0);
+      el[2] = nb(1, e0);
+      el[3] = nb(0, el[2]);
+      bool ok = el[1] >= 0 && el[3] >= 0 && nb(1, el[1]) == el[3];
+      if (ok && bz == 2)
+      {
+         for (int i = 0; i < 4; i++) { el[4 + i] = nb(2, el[i]); }
+         ok = el[4] >= 0 && el[5] >= 0 && el[6] >= 0 && el[7] >= 0 && nb(0, el[4]) == el[5] &&
+              nb(1, el[4]) == el[6] && nb(0, el[6]) == el[7] && nb(1, el[5]) == el[7];
+      }
+      for (int i = 0; i < nbe && ok; i++)
+      {
+         ok = el[i] >= 0 && !in_brick[el[i]] && seg[el[i]] == seg[e0];
+         for (int j = 0; j < i && ok; j++) { ok = el[j] != el[i]; }
+         for (int a = 0; a < ND && ok; a++) { ok = gm[(size_t)el[i] * ND + a] >= 0; }
+      }
+      if (!ok) { continue; }
+      for (int i = 0; i < nbe; i++)
+      {
+         belem.push_back(el[i]);
+         in_brick[el[i]] = 1;
+      }
+   }
+}
 
 // Longest chunk of x-adjacent elements one wave of the line kernel walks: the kernel
 // variant's limit (1 for the default single-element variant), lowered by ECM2_LINE_CHUNK.
@@ -308,10 +416,12 @@ void PAForm::assemble(hipStream_t s)
    if (resolved_mode_ == KERNEL_LINE) { kern::upload_basis(D_, Q_, basis_); }
    if (resolved_mode_ == KERNEL_LINE && !gmap_line_.size() && ne_ > 0)
    {
-      // chunks of up to 8 consecutive elements whose x-faces coincide (never crossing a
-      // 64-element block, so apply_blocks ranges map to chunk ranges); the face of
-      // element k is carried into element k+1, which holds it.  Then the encoded map
-      // and the deterministic-scatter plan over the holding entries.
+      // Bricks of 2 x 2 x bz elements (deterministic scatter only) take every element they
+      // can; the leftovers run the per-element line kernel in chunks of up to 8 consecutive
+      // elements whose x-faces coincide (never crossing a 64-element block, so
+      // apply_blocks ranges map to chunk ranges; the face of element k is carried into
+      // element k+1, which holds it).  Then the encoded maps and the deterministic-scatter
+      // plan over the holding entries: the bricks' lattice points, the leftovers' entries.
       ECM2_VERIFY(ndofs_ < (1 << 30), ERR_UNSUPPORTED, "fused kernel supports < 2^30 dofs");
       ECM2_VERIFY((size_t)ne_ * ND_ < (1ull << 31) && ne_ < (1 << 24), ERR_UNSUPPORTED,
                   "too many elements for the line kernel's chunk table");
@@ -329,47 +439,120 @@ void PAForm::assemble(hipStream_t s)
          return true;
       };
       const int nblk = layout_.nblk();
-      std::vector<int> chunks, coff(nblk + 1, 0);
-      std::vector<char> holds((size_t)ne_ * ND_, 1);
+      int bz = scatter_ == SCATTER_PARTIALS ? (line_bricks_ >= 0 ? line_bricks_ : line_brick_mode()) : 0;
+      if (bz == 2 && !kern::has_brick(D_, Q_, 2)) { bz = 1; }
+      if (bz == 1 && !kern::has_brick(D_, Q_, 1)) { bz = 0; }
+      std::vector<int> belem;
+      std::vector<char> in_brick(ne_, 0);
+      if (bz)
+      {
+         std::vector<int> seg(ne_, 0);
+         for (int e = 0; e < ne_; e++)
+         {
+            for (int sp : splits_) { seg[e] += (e / kElemBlock >= sp); }
+         }
+         find_bricks(ne_, D_, gmap_host_, bz, seg, belem, in_brick);
+      }
+      const int nbe = 4 * (bz ? bz : 1);
+      n_bricks_ = bz ? (int)(belem.size() / nbe) : 0;
+      brick_bz_ = n_bricks_ ? bz : 0;
+      brick_np_ = brick_bz_ ? kern::brick_points(D_, brick_bz_) : 0;
+      const int LX = 2 * D_ - 1, LY = LX;
+      // lattice map of each brick (dof per lattice point; internal faces coincide by construction)
+      std::vector<int> bdof((size_t)n_bricks_ * brick_np_, -1);
+      for (int k = 0; k < n_bricks_; k++)
+         for (int elt = 0; elt < nbe; elt++)
+         {
+            const int e = belem[(size_t)k * nbe + elt], ex = elt & 1, ey = (elt >> 1) & 1, ez = elt >> 2;
+            for (int dz = 0; dz < D_; dz++)
+               for (int dy = 0; dy < D_; dy++)
+                  for (int dx = 0; dx < D_; dx++)
+                  {
+                     const int p = ((ez * (D_ - 1) + dz) * LY + ey * (D_ - 1) + dy) * LX + ex * (D_ - 1) + dx;
+                     const int d = dofv(gmap_host_[(size_t)e * ND_ + (dz * D_ + dy) * D_ + dx]);
+                     int &b = bdof[(size_t)k * brick_np_ + p];
+                     ECM2_VERIFY(b < 0 || b == d, ERR_INTERNAL, "brick " << k << " lattice point " << p
+                                                                    << " holds two dofs");
+                     b = d;
+                  }
+         }
+      std::vector<int> chunks, coff(nblk + 1, 0), boff(nblk + 1, 0);
+      std::vector<char> holds((size_t)ne_ * ND_, 0);
+      int n_left = 0;
       for (int bk = 0; bk < nblk; bk++)
       {
          const int eb = bk * 64, ee = std::min(ne_, eb + 64);
          int e = eb;
          while (e < ee)
          {
+            if (in_brick[e]) { e++; continue; }
             int n = 1;
-            while (n < line_chunk_max() && e + n < ee && xface_match(e + n - 1)) { n++; }
+            while (n < line_chunk_max() && e + n < ee && !in_brick[e + n] && xface_match(e + n - 1)) { n++; }
             chunks.push_back(e | (n << 24));
+            for (int k = 0; k < n; k++)
+               for (int a = 0; a < ND_; a++) { holds[(size_t)(e + k) * ND_ + a] = 1; }
             for (int k = 0; k + 1 < n; k++)
                for (int dz = 0; dz < D_; dz++)
                   for (int dy = 0; dy < D_; dy++) { holds[(size_t)(e + k) * ND_ + (dz * D_ + dy) * D_ + D_ - 1] = 0; }
+            n_left += n;
             e += n;
          }
          coff[bk + 1] = (int)chunks.size();
       }
+      for (int k = 0, bk = 0; bk < nblk; bk++)
+      {
+         while (k < n_bricks_ && belem[(size_t)k * nbe] / kElemBlock == bk) { k++; }
+         boff[bk + 1] = k;
+      }
+      ECM2_VERIFY(boff[nblk] == n_bricks_, ERR_INTERNAL, "bricks not ordered by first element");
       std::vector<int> hcount(ndofs_, 0);
+      for (int d : bdof) { hcount[d]++; }
       for (size_t i = 0; i < gmap_host_.size(); i++) { if (holds[i]) { hcount[dofv(gmap_host_[i])]++; } }
-      std::vector<int> enc(gmap_host_.size()), hdof, hslot;
+      auto encode = [&](int d, bool neg) {
+         return (int)((unsigned)d | ((hcount[d] > 1 ? 1u : 0u) << 30) | ((neg ? 1u : 0u) << 31));
+      };
+      part_line_off_ = (long)n_bricks_ * brick_np_;
+      std::vector<int> enc(gmap_host_.size()), benc(bdof.size()), hdof, hslot;
+      for (size_t i = 0; i < bdof.size(); i++)
+      {
+         benc[i] = encode(bdof[i], false);
+         if (hcount[bdof[i]] > 1)
+         {
+            hdof.push_back(bdof[i]);
+            hslot.push_back((int)i);
+         }
+      }
+      ECM2_VERIFY(part_line_off_ + (long)nblk * ND_ * 64 < (1l << 31), ERR_UNSUPPORTED, "too many partial slots");
       for (size_t i = 0; i < gmap_host_.size(); i++)
       {
          const int g = gmap_host_[i];
-         const unsigned d = (unsigned)dofv(g);
-         enc[i] = (int)(d | ((hcount[d] > 1 ? 1u : 0u) << 30) | ((g < 0 ? 1u : 0u) << 31));
+         const int d = dofv(g);
+         enc[i] = encode(d, g < 0);
          if (holds[i] && hcount[d] > 1)
          {
-            hdof.push_back((int)d);
-            hslot.push_back((int)i);
+            hdof.push_back(d);
+            hslot.push_back((int)(part_line_off_ + (long)i));
          }
       }
       build_shared_plan(hcount, hdof, hslot, s);
       gmap_line_.upload(enc, s);
-      chunks_.upload(chunks, s);
+      chunks_.upload(chunks.empty() ? std::vector<int>{0} : chunks, s);
       chunk_off_ = coff;
+      belem_.upload(belem, s);
+      bmap_.upload(benc, s);
+      brick_off_ = boff;
+      n_left_ = n_left;
       ECM2_HIP(hipStreamSynchronize(s));
    }
    layout_.pos = (layout_.kind == QLAYOUT_BLOCKED) ? pos_.data() : nullptr;
    layout_.perm = (layout_.kind == QLAYOUT_BLOCKED) ? perm_dev_.data() : nullptr;
-   part_.resize(use_partials() ? (size_t)layout_.nblk() * ND_ * 64 : 0);  // >= ne * nd for LINE
+   if (!use_partials()) { part_.resize(0); }
+   else if (resolved_mode_ == KERNEL_LINE)
+   {
+      // [bricks' lattice slots | leftover elements' [e][nd] slots (when there are any)]
+      part_.resize(std::max<size_t>(1, (size_t)part_line_off_ + (n_left_ ? (size_t)ne_ * ND_ : 0)));
+   }
+   else { part_.resize((size_t)layout_.nblk() * ND_ * 64); }
    qd_diff_.resize(have_diff_ ? layout_.diff_size() : 0);
    qd_mass_.resize(have_mass_ ? layout_.mass_size() : 0);
    // the setup kernels write every entry except the padding lanes of a partial last block
@@ -537,6 +720,7 @@ void PAForm::set_scatter(int mode)
 {
    ECM2_VERIFY(mode == SCATTER_PARTIALS || mode == SCATTER_ATOMIC, ERR_ARG, "unknown scatter mode " << mode);
    scatter_ = mode;
+   gmap_line_.resize(0);  // the line kernel's bricks exist only with the partial scatter
    assembled_ = false;
 }
 
@@ -566,6 +750,18 @@ ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, doubl
    a.part = use_partials() ? const_cast<double *>(part_.data()) : nullptr;  // form-owned scratch
    a.chunks = chunks_.data();
    a.chunk_off = chunk_off_.empty() ? nullptr : chunk_off_.data();
+   if (resolved_mode_ == KERNEL_LINE && use_partials())
+   {
+      a.part_brick = const_cast<double *>(part_.data());
+      a.part = const_cast<double *>(part_.data()) + part_line_off_;  // leftovers: [e][nd] after the bricks
+   }
+   if (resolved_mode_ == KERNEL_LINE && brick_bz_)
+   {
+      a.brick_bz = brick_bz_;
+      a.belem = belem_.data();
+      a.bmap = bmap_.data();
+      a.brick_off = brick_off_.data();
+   }
    return a;
 }
 
@@ -574,6 +770,14 @@ void PAForm::apply_blocks(const double *x, const double *xg, double *y, double *
 {
    ECM2_VERIFY(assembled_, ERR_STATE, "apply before Assemble");
    ECM2_VERIFY(resolved_mode_ != KERNEL_UNFUSED, ERR_UNSUPPORTED, "block apply needs a fused kernel");
+   if (resolved_mode_ == KERNEL_LINE && brick_bz_)
+   {
+      auto boundary = [&](int b) {
+         return b == 0 || b == layout_.nblk() || std::find(splits_.begin(), splits_.end(), b) != splits_.end();
+      };
+      ECM2_VERIFY(boundary(b0) && boundary(b1), ERR_ARG, "apply_blocks [" << b0 << ", " << b1
+                                                          << ") cuts a brick: declare the split with set_block_splits");
+   }
    const ApplyArgs a = apply_args(x, xg, y, yg, b0, b1);
    if (resolved_mode_ == KERNEL_TPE)
    {

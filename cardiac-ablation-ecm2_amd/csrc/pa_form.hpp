@@ -68,6 +68,15 @@ public:
    // the blocked layout; ORDER_BRICK puts one 4x4x4 brick in each 64-lane wave so the
    // fused kernel can assemble shared faces in-wave.  All APIs keep caller element order.
    void set_element_order(const int *perm_host);
+   // Block indices at which apply_blocks ranges may start or end besides 0 and nblocks()
+   // (the distributed form's interior | boundary split).  The line kernel's bricks never
+   // straddle one.
+   void set_block_splits(const std::vector<int> &splits);
+   // Bricks of the line kernel family (p >= 3): -1 = default (ECM2_LINE_BRICK, else 2),
+   // 0 = none, 1 = 2 x 2 x 1, 2 = 2 x 2 x 2 elements per workgroup.
+   void set_line_bricks(int bz);
+   int n_bricks() const { return n_bricks_; }
+   int brick_bz() const { return brick_bz_; }
    void add_integrator(int kind, const CoeffDesc &c);
    void set_kernel(int mode);
    void set_scatter(int mode);
@@ -146,6 +155,13 @@ private:
    DeviceArray<int> gmap_line_;     // LINE: [e][nd] dof | shared << 30 | sign << 31
    DeviceArray<int> chunks_;        // LINE: first element | count << 24
    std::vector<int> chunk_off_;     // LINE: chunks of block b = [chunk_off_[b], chunk_off_[b+1])
+   std::vector<int> splits_;        // apply_blocks range boundaries besides 0 / nblk
+   int n_bricks_ = 0, brick_bz_ = 0, brick_np_ = 0;  // LINE bricks: count, 2 x 2 x bz, lattice points
+   DeviceArray<int> belem_, bmap_;  // LINE bricks: [nbrick][4 bz] elements, [nbrick][np] lattice map
+   std::vector<int> brick_off_;     // LINE bricks of block b = [brick_off_[b], brick_off_[b+1])
+   long part_line_off_ = 0;         // LINE: leftover elements' partial slots start here
+   int n_left_ = 0;                 // LINE: elements outside bricks
+   int line_bricks_ = -1;           // requested brick mode (set_line_bricks)
    DeviceArray<int> lane_flags_;    // [blk][64] in-wave merge flags
    std::vector<int> perm_host_;     // internal position -> caller element (empty: identity)
    DeviceArray<int> pos_;           // caller element -> internal position

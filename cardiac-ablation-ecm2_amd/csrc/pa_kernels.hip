@@ -1187,6 +1187,282 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned
    }
 }
 
+// --------------------------------------------------------------------------
+// Brick kernel (p >= 3): one workgroup per brick of 2 x 2 x BZ elements whose internal
+// faces coincide (found by dof equality at setup, pa_form.cpp).  The five 1D stages of
+// the line kernel run for all elements of the brick at once, lane = (element, line), so
+// the 25 / 30 / 36-line stages of a p = 4 element fill 4-5 waves instead of leaving half
+// of one wave idle.  The elements' outputs are then summed on the brick lattice
+// ((2(D-1)+1)^2 (BZ(D-1)+1) points) in LDS in a fixed order, so the shared faces inside
+// a brick never reach HBM: a lattice point held by this brick alone is plain-stored,
+// one on the brick surface that other holders share goes to its partial slot
+// part[brick][point] for k_sum_partials (deterministic, no atomics).
+// Per element: same qdata, x-line gathers and contractions as k_apply_line
+// (bilininteg_mass_kernels.hpp:809-1033, bilininteg_diffusion_kernels.hpp:989-1214);
+// the brick map replaces ElementRestriction's element maps (restriction.cpp:109-186).
+// --------------------------------------------------------------------------
+template <int D, int Q, int BZ>
+struct BrickShape
+{
+   static constexpr int NE = 4 * BZ, DD = D * D, QQ = Q * Q, DQ = D * Q, ND = D * D * D;
+   static constexpr int LX = 2 * (D - 1) + 1, LY = LX, LZ = BZ * (D - 1) + 1, NB = LX * LY * LZ;
+   // per-element LDS: SA holds the x-stage lines (2 D^2 Q), SB the y/z-stage planes (3 D Q^2,
+   // the z stage works in place); staged element outputs (D^3) reuse SB
+   static constexpr int SA = 2 * DD * Q, SB = 3 * D * QQ;
+   static constexpr int NT = ((NE * QQ + 63) / 64) * 64;  // stage 3 in one pass
+};
+
+// lattice coordinate P along one brick direction -> (first element index, local index,
+// holders): the shared plane P = D-1 is held by element 0 (local D-1) and 1 (local 0)
+template <int D>
+__device__ __forceinline__ void brick_cand(int P, int &c0, int &l0, int &n)
+{
+   if (P < D - 1) { c0 = 0; l0 = P; n = 1; }
+   else if (P == D - 1) { c0 = 0; l0 = D - 1; n = 2; }
+   else { c0 = 1; l0 = P - (D - 1); n = 1; }
+}
+
+// VAR bit 1: load the stage-3 qdata at the top of the z stage (fewer VGPRs, more
+// workgroups per CU) instead of at kernel entry (in flight during stages 1-2)
+template <int D, int Q, int BZ, bool MASS, bool DIFF, bool SPLIT, int VAR>
+__global__ void __launch_bounds__((BrickShape<D, Q, BZ>::NT))
+k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *__restrict__ bmap, int n_owned,
+              const double *__restrict__ qdd, const double *__restrict__ qdm,
+              const double *__restrict__ x, const double *__restrict__ xg,
+              double *__restrict__ y, double *__restrict__ yg, double *__restrict__ part)
+{
+   using S = BrickShape<D, Q, BZ>;
+   constexpr int NE = S::NE, DD = S::DD, QQ = S::QQ, DQ = S::DQ, ND = S::ND, SA = S::SA, SB = S::SB;
+   constexpr int LX = S::LX, LY = S::LY, NB = S::NB;
+   static_assert(QQ <= 64, "brick kernel needs Q1D <= 8");
+   static_assert(SB >= ND, "staged outputs reuse bufB");
+   __shared__ double bufA[NE * SA];
+   __shared__ double bufB[NE * SB];
+   const int k = k_begin + (int)blockIdx.x;
+   if (k >= k_end) { return; }  // whole workgroup
+   const int t = threadIdx.x;
+   const int *bm = bmap + (size_t)k * NB;
+   auto lattice = [&](int elt, int dx, int dy, int dz) {
+      const int ex = elt & 1, ey = (elt >> 1) & 1, ez = elt >> 2;
+      return ((ez * (D - 1) + dz) * LY + ey * (D - 1) + dy) * LX + ex * (D - 1) + dx;
+   };
+
+   // qdata of the (element, qx, qy) column this lane weights in stage 3: in flight
+   // during the gather and the x / y contractions
+   double qv[7][Q];
+   if (!(VAR & 1) && t < NE * QQ)
+   {
+      line_load_qdata<D, Q, MASS, DIFF>(qv, belem[(size_t)k * NE + t / QQ], t % QQ, qdd, qdm);
+   }
+
+   // ---- lanes (element, dy, dz): gather the x-line, contract in x
+   if (t < NE * DD)
+   {
+      CBasis *bp = stage_basis<D, Q>();
+      const int elt = t / DD, l = t % DD;
+      const int *mp = bm + lattice(elt, 0, l % D, l / D);
+      double xl[D];
+#pragma unroll
+      for (int dx = 0; dx < D; dx++)
+      {
+         const int d = bdof(mp[dx]);
+         xl[dx] = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
+      }
+      double *o = bufA + elt * SA;
+#pragma unroll
+      for (int qx = 0; qx < Q; qx++)
+      {
+         double u = 0.0, v = 0.0;
+#pragma unroll
+         for (int dx = 0; dx < D; dx++)
+         {
+            u += bp->B[qx + MQ * dx] * xl[dx];
+            v += bp->G[qx + MQ * dx] * xl[dx];
+         }
+         o[l * Q + qx] = u;
+         o[DD * Q + l * Q + qx] = v;
+      }
+   }
+   __syncthreads();
+   // ---- lanes (element, qx, dz): contract in y
+   if (t < NE * DQ)
+   {
+      CBasis *bp = stage_basis<D, Q>();
+      const int elt = t / DQ, l = t % DQ, qx = l % Q, dz = l / Q;
+      const double *in = bufA + elt * SA;
+      double *o = bufB + elt * SB;
+      double la[D], lb[D];
+#pragma unroll
+      for (int dy = 0; dy < D; dy++)
+      {
+         la[dy] = in[(dz * D + dy) * Q + qx];
+         lb[dy] = in[DD * Q + (dz * D + dy) * Q + qx];
+      }
+#pragma unroll
+      for (int qy = 0; qy < Q; qy++)
+      {
+         double gb = 0.0, bg = 0.0, bb = 0.0;
+#pragma unroll
+         for (int dy = 0; dy < D; dy++)
+         {
+            const double by = bp->B[qy + MQ * dy], gy = bp->G[qy + MQ * dy];
+            gb += by * lb[dy];
+            bg += gy * la[dy];
+            bb += by * la[dy];
+         }
+         const int oo = (dz * Q + qy) * Q + qx;
+         o[oo] = gb;
+         o[D * QQ + oo] = bg;
+         o[2 * D * QQ + oo] = bb;
+      }
+   }
+   __syncthreads();
+   // ---- lanes (element, qx, qy): contract in z, weight, transpose in z (in place: a lane
+   // reads its whole (qx, qy) column before writing it back)
+   if (t < NE * QQ)
+   {
+      CBasis *bp = stage_basis<D, Q>();
+      const int elt = t / QQ, l = t % QQ;
+      if (VAR & 1) { line_load_qdata<D, Q, MASS, DIFF>(qv, belem[(size_t)k * NE + elt], l, qdd, qdm); }
+      double *in = bufB + elt * SB;
+      double *o = in;
+      double l0[D], l1[D], l2[D];
+#pragma unroll
+      for (int dz = 0; dz < D; dz++)
+      {
+         l0[dz] = in[dz * QQ + l];
+         l1[dz] = in[D * QQ + dz * QQ + l];
+         l2[dz] = in[2 * D * QQ + dz * QQ + l];
+      }
+      double A1[D], A2[D], A3[D];
+#pragma unroll
+      for (int dz = 0; dz < D; dz++) { A1[dz] = 0.0; A2[dz] = 0.0; A3[dz] = 0.0; }
+#pragma unroll
+      for (int qz = 0; qz < Q; qz++)
+      {
+         double gx = 0.0, gy = 0.0, gz = 0.0, u = 0.0;
+#pragma unroll
+         for (int dz = 0; dz < D; dz++)
+         {
+            const double bz = bp->B[qz + MQ * dz], gzz = bp->G[qz + MQ * dz];
+            if (DIFF)
+            {
+               gx += bz * l0[dz];
+               gy += bz * l1[dz];
+               gz += gzz * l2[dz];
+            }
+            if (MASS) { u += bz * l2[dz]; }
+         }
+         double fx = 0.0, fy = 0.0, fz = 0.0, m = 0.0;
+         if (DIFF)
+         {
+            fx = qv[0][qz] * gx + qv[1][qz] * gy + qv[2][qz] * gz;
+            fy = qv[1][qz] * gx + qv[3][qz] * gy + qv[4][qz] * gz;
+            fz = qv[2][qz] * gx + qv[4][qz] * gy + qv[5][qz] * gz;
+         }
+         if (MASS) { m = qv[6][qz] * u; }
+#pragma unroll
+         for (int dz = 0; dz < D; dz++)
+         {
+            const double bz = bp->B[qz + MQ * dz], gzz = bp->G[qz + MQ * dz];
+            if (DIFF)
+            {
+               A1[dz] += bz * fx;
+               A2[dz] += bz * fy;
+               A3[dz] += gzz * fz;
+            }
+            if (MASS) { A3[dz] += bz * m; }
+         }
+      }
+#pragma unroll
+      for (int dz = 0; dz < D; dz++)
+      {
+         o[dz * QQ + l] = A1[dz];
+         o[D * QQ + dz * QQ + l] = A2[dz];
+         o[2 * D * QQ + dz * QQ + l] = A3[dz];
+      }
+   }
+   __syncthreads();
+   // ---- lanes (element, qx, dz): transpose in y
+   if (t < NE * DQ)
+   {
+      CBasis *bp = stage_basis<D, Q>();
+      const int elt = t / DQ, l = t % DQ, qx = l % Q, dz = l / Q;
+      const double *in = bufB + elt * SB;
+      double *o = bufA + elt * SA;
+      double l0[Q], l1[Q], l2[Q];
+#pragma unroll
+      for (int qy = 0; qy < Q; qy++)
+      {
+         const int oo = (dz * Q + qy) * Q + qx;
+         l0[qy] = in[oo];
+         l1[qy] = in[D * QQ + oo];
+         l2[qy] = in[2 * D * QQ + oo];
+      }
+#pragma unroll
+      for (int dy = 0; dy < D; dy++)
+      {
+         double c1 = 0.0, c2 = 0.0;
+#pragma unroll
+         for (int qy = 0; qy < Q; qy++)
+         {
+            const double by = bp->B[qy + MQ * dy], gy = bp->G[qy + MQ * dy];
+            c1 += by * l0[qy];
+            c2 += gy * l1[qy] + by * l2[qy];
+         }
+         o[(dz * D + dy) * Q + qx] = c1;
+         o[DD * Q + (dz * D + dy) * Q + qx] = c2;
+      }
+   }
+   __syncthreads();
+   // ---- lanes (element, dy, dz): transpose in x -> element outputs staged in LDS [elt][a]
+   if (t < NE * DD)
+   {
+      CBasis *bp = stage_basis<D, Q>();
+      const int elt = t / DD, l = t % DD;
+      const double *in = bufA + elt * SA;
+      double l0[Q], l1[Q];
+#pragma unroll
+      for (int qx = 0; qx < Q; qx++)
+      {
+         l0[qx] = in[l * Q + qx];
+         l1[qx] = in[DD * Q + l * Q + qx];
+      }
+#pragma unroll
+      for (int dx = 0; dx < D; dx++)
+      {
+         double v = 0.0;
+#pragma unroll
+         for (int qx = 0; qx < Q; qx++) { v += bp->G[qx + MQ * dx] * l0[qx] + bp->B[qx + MQ * dx] * l1[qx]; }
+         bufB[elt * ND + l * D + dx] = v;  // bufB is free: stage 4 read it before the barrier
+      }
+   }
+   __syncthreads();
+   // ---- lattice points: sum the holders in a fixed (z, y, x) order, store or publish
+   for (int p = t; p < NB; p += S::NT)
+   {
+      const int X = p % LX, Y = (p / LX) % LY, Z = p / (LX * LY);
+      int cx, lx, nx, cy, ly, ny, cz, lz, nz;
+      brick_cand<D>(X, cx, lx, nx);
+      brick_cand<D>(Y, cy, ly, ny);
+      if (BZ == 2) { brick_cand<D>(Z, cz, lz, nz); }
+      else { cz = 0; lz = Z; nz = 1; }
+      double v = 0.0;
+      for (int iz = 0; iz < nz; iz++)
+         for (int iy = 0; iy < ny; iy++)
+            for (int ix = 0; ix < nx; ix++)
+            {
+               const int elt = (cx + ix) + 2 * ((cy + iy) + 2 * (cz + iz));
+               const int a = ((iz ? 0 : lz) * D + (iy ? 0 : ly)) * D + (ix ? 0 : lx);
+               v += bufB[elt * ND + a];
+            }
+      const int g = bm[p];
+      const int d = bdof(g);
+      if (!bshared(g)) { *((!SPLIT || d < n_owned) ? y + d : yg + (d - n_owned)) = v; }
+      else { part[(size_t)k * NB + p] = v; }
+   }
+}
+
 __global__ void k_restriction_mult(long n, const int *__restrict__ gmap,
                                    const double *__restrict__ x, double *__restrict__ xe)
 {
@@ -1716,9 +1992,80 @@ void upload_basis(int D, int Q, const Basis1D &b)
                               ((size_t)(D - 1) * MAX_Q1D + (Q - 1)) * sizeof(Basis1D), hipMemcpyHostToDevice));
 }
 
+// experiment knob ECM2_BRICK_VARIANT (bit 1: qdata loaded at the z stage)
+int brick_variant()
+{
+   static int v = [] {
+      const char *e = std::getenv("ECM2_BRICK_VARIANT");
+      return e ? std::atoi(e) : 0;
+   }();
+   return v;
+}
+
+template <int D, int Q, int BZ, bool MASS, bool DIFF>
+void launch_brick_mdq(const ApplyArgs &a, hipStream_t s)
+{
+   const int k0 = a.brick_off[a.blk_begin], k1 = a.brick_off[a.blk_end];
+   if (k1 <= k0) { return; }
+   ECM2_VERIFY(a.part_brick, ERR_INTERNAL, "brick kernel needs its partial slots");
+   const dim3 grid(k1 - k0), block(BrickShape<D, Q, BZ>::NT);
+#define ECM2_BRICK(SP, V)                                                                               \
+   hipLaunchKernelGGL((k_apply_brick<D, Q, BZ, MASS, DIFF, SP, V>), grid, block, 0, s, k0, k1, a.belem, \
+                      a.bmap, a.n_owned, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, a.part_brick)
+   const bool split = a.xg || a.yg;
+   if (brick_variant() & 1)
+   {
+      if (split) { ECM2_BRICK(true, 1); } else { ECM2_BRICK(false, 1); }
+   }
+   else
+   {
+      if (split) { ECM2_BRICK(true, 0); } else { ECM2_BRICK(false, 0); }
+   }
+#undef ECM2_BRICK
+}
+
+template <int D, int Q, int BZ>
+void launch_brick_dq(bool mass, bool diff, const ApplyArgs &a, hipStream_t s)
+{
+   if (mass && diff) { launch_brick_mdq<D, Q, BZ, true, true>(a, s); }
+   else if (mass) { launch_brick_mdq<D, Q, BZ, true, false>(a, s); }
+   else if (diff) { launch_brick_mdq<D, Q, BZ, false, true>(a, s); }
+}
+
+// bricks of 2 x 2 x bz elements for Q1D = D1D + 1 (the default rule), p = 3..6; a
+// 2 x 2 x 2 brick's LDS (16 S doubles) exceeds 160 KiB at p = 6
+bool has_brick(int D, int Q, int bz)
+{
+   if (Q != D + 1 || D < 4 || D > 7) { return false; }
+   return bz == 1 || (bz == 2 && D <= 6);
+}
+
+int brick_points(int D, int bz) { return (2 * D - 1) * (2 * D - 1) * (bz * (D - 1) + 1); }
+
+static void apply_brick(int D, int Q, bool mass, bool diff, const ApplyArgs &a, hipStream_t s)
+{
+#define ECM2_BRICK_CASE(DD, BZ)                                         \
+   if (D == DD && a.brick_bz == BZ)                                     \
+   {                                                                    \
+      launch_brick_dq<DD, DD + 1, BZ>(mass, diff, a, s);                \
+      ECM2_HIP(hipGetLastError());                                      \
+      return;                                                           \
+   }
+   ECM2_BRICK_CASE(4, 1)
+   ECM2_BRICK_CASE(4, 2)
+   ECM2_BRICK_CASE(5, 1)
+   ECM2_BRICK_CASE(5, 2)
+   ECM2_BRICK_CASE(6, 1)
+   ECM2_BRICK_CASE(6, 2)
+   ECM2_BRICK_CASE(7, 1)
+#undef ECM2_BRICK_CASE
+   ECM2_VERIFY(false, ERR_UNSUPPORTED, "no brick kernel for D1D=" << D << " Q1D=" << Q << " bz=" << a.brick_bz);
+}
+
 void apply_line(int D, int Q, bool mass, bool diff, const ApplyArgs &a, const Basis1D &b, hipStream_t s)
 {
    if (a.ne == 0) { return; }
+   if (a.brick_bz) { apply_brick(D, Q, mass, diff, a, s); }
 #define ECM2_LINE_CASE(DD, QQ)                                        \
    if (D == DD && Q == QQ)                                            \
    {                                                                  \

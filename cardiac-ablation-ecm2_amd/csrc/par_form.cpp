@@ -31,6 +31,8 @@ ParPAForm::ParPAForm(const LocalPart &part, const double *enodes_local_host, int
    const int nl = part.n_owned + part.n_ghost;
    local_.reset(new PAForm(part.ne_local, part.order, nl, part.gather_map.data(), q1d, part.n_owned));
    local_->set_element_nodes(enodes_local_host);
+   // the Mult applies blocks [0, b_int) (interior) and [b_int, nblk) (boundary) separately
+   local_->set_block_splits({part.ne_interior / kElemBlock});
    send_idx_.upload(part.send_idx);
    sendbuf_.resize(std::max<size_t>(1, part.send_idx.size()));
    rbuf_.resize(std::max<size_t>(1, part.send_idx.size()));

@@ -132,6 +132,15 @@ int ecm2_pa_form_set_kernel(ecm2_pa_form *f, int kernel);
 #define ECM2_SCATTER_PARTIALS 0
 #define ECM2_SCATTER_ATOMIC 1
 int ecm2_pa_form_set_scatter(ecm2_pa_form *f, int mode);
+/* Work grouping of the p >= 3 line-kernel family (no reference counterpart; the
+ * reference applies each element independently, bilininteg_diffusion_kernels.hpp:989-1214):
+ * bz = -1 default (2 x 2 x 1), 0 = per-element line
+ * kernel only, 1 = bricks of 2 x 2 x 1 elements, 2 = 2 x 2 x 2.  A brick is one workgroup;
+ * its internal shared faces are summed in LDS in a fixed order (deterministic).  Bricks
+ * exist only with ECM2_SCATTER_PARTIALS; elements outside bricks use the line kernel. */
+int ecm2_pa_form_set_bricks(ecm2_pa_form *f, int bz);
+/* After assemble: bricks formed and their depth (0 = none). */
+int ecm2_pa_form_brick_info(const ecm2_pa_form *f, int *n_bricks, int *bz);
 /* Scatter statistics after assemble: shared dofs and their partial slots. */
 int ecm2_pa_form_scatter_info(const ecm2_pa_form *f, int *n_shared, long *n_slots);
 /* Optional element permutation for the fused kernel's blocked layout (host perm[ne]:
@@ -254,6 +263,8 @@ int ecm2_par_form_add_integrator(ecm2_par_form *f, int integrator, int coeff_kin
                                  const double *data, const double *params);
 /* As ecm2_pa_form_set_kernel (fused kernels only). */
 int ecm2_par_form_set_kernel(ecm2_par_form *f, int kernel);
+/* Brick mode of the local form (see ecm2_pa_form_set_bricks). */
+int ecm2_par_form_set_bricks(ecm2_par_form *f, int bz);
 /* Scatter mode of the local form (ECM2_SCATTER_*; see ecm2_pa_form_set_scatter). */
 int ecm2_par_form_set_scatter(ecm2_par_form *f, int mode);
 /* ParBilinearForm::Assemble -> local PABilinearFormExtension::Assemble

@@ -19,6 +19,10 @@ from helpers import GOLDEN, RTOL, coeff_function, nonaligned, relerr
 
 
 def _mesh(kind):
+    if kind == "cart_big":  # slabs with whole 64-element interior blocks (brick segments)
+        m = E.Mesh.MakeCartesian3D(8, 8, 12, 1.0, 1.0, 1.5)
+        m.set_vertices(nonaligned(m.vertices()))
+        return m
     if kind == "cart":
         m = E.Mesh.MakeCartesian3D(4, 3, 6)
         m.set_vertices(nonaligned(m.vertices()))
@@ -29,7 +33,7 @@ def _mesh(kind):
 
 
 def _elem_rank(m, kind, nranks):
-    if kind == "cart":
+    if kind in ("cart", "cart_big"):
         return E.partition_slabs_z(m, nranks)
     rng = np.random.default_rng(5)  # irregular partition: random element owners
     return rng.integers(0, nranks, m.GetNE()).astype(np.int32)
@@ -144,7 +148,8 @@ def test_gloo_exchange_matches_serial(tmp_path, kind, nranks):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,nranks,order", [("cart", 2, 2), ("cart", 3, 1), ("fichera", 3, 2),
-                                               ("fichera", 4, 3), ("cart", 4, 2)])
+                                               ("fichera", 4, 3), ("cart", 4, 2), ("cart", 2, 4),
+                                               ("cart_big", 2, 3), ("cart_big", 3, 4)])
 @pytest.mark.parametrize("scatter", ["partials", "atomic"])
 def test_gpu_loopback_group_matches_serial(kind, nranks, order, scatter):
     import torch

@@ -379,3 +379,61 @@ def test_full_size_c2_deterministic():
             form.Mult(x, y2)
             assert torch.equal(y, y2)
     assert relerr(host(out["partials"]), host(out["atomic"])) <= RTOL
+
+
+@pytest.mark.parametrize("mesh_name", ["inline_hex", "cart_bricks", "nonaligned", "fichera_r1", "cart_130"])
+@pytest.mark.parametrize("order", [3, 4, 5])
+def test_line_bricks(mesh_name, order):
+    """p >= 3 brick kernel (2 x 2 x 1 and 2 x 2 x 2 workgroups, LDS lattice assembly) and
+    the per-element line kernel it falls back to: each matches the oracle, overwrites
+    every y entry (NaN prefill), is bitwise reproducible, and the brick modes agree."""
+    m = make_mesh(mesh_name)
+    ys = {}
+    for bz in (0, 1, 2):
+        fes = E.H1Space(m, order)
+        form = E.BilinearForm(fes, kernel=E.KERNEL_LINE, bricks=bz)
+        en = m.element_nodes()
+        P = O.quad_points(en, O.default_q1d(order))
+        a, b = alpha_bioheat(P), coeff_function(P)
+        form.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(a.reshape(fes.ne, -1)))))
+        form.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(dev(b.reshape(fes.ne, -1)))))
+        form.Assemble()
+        nb, depth = form.BrickInfo()
+        if bz == 0:
+            assert nb == 0
+        elif mesh_name in ("inline_hex", "cart_bricks"):
+            assert nb > 0 and depth == bz
+        x = np.random.default_rng(order).uniform(-1, 1, fes.ndofs)
+        y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+        form.Mult(dev(x), y)
+        op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=a, beta=b)
+        assert relerr(host(y), op.mult(x)) <= RTOL, (bz, nb)
+        y2 = torch.full_like(y, float("nan"))
+        form.Mult(dev(x), y2)
+        assert torch.equal(y, y2)
+        ys[bz] = host(y)
+    assert relerr(ys[1], ys[0]) <= RTOL and relerr(ys[2], ys[0]) <= RTOL
+
+
+def test_full_size_c5_bricks():
+    """C5-shaped (order 4, Cartesian) at a size the oracle finishes quickly: bricks cover
+    every element of an even mesh; the Mult matches the oracle and the per-element kernel."""
+    m = E.Mesh.MakeCartesian3D(12, 10, 8)
+    fes = E.H1Space(m, 4, E.NUMBERING_STRUCTURED)
+    en = m.element_nodes()
+    P = O.quad_points(en, 6)
+    a, b = alpha_bioheat(P), k_of_T(temperature(P))
+    x = np.random.default_rng(5).uniform(-1, 1, fes.ndofs)
+    out = {}
+    for bz in (0, 2):
+        form = E.BilinearForm(fes, bricks=bz)
+        form.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(a.reshape(fes.ne, -1)))))
+        form.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(dev(b.reshape(fes.ne, -1)))))
+        form.Assemble()
+        if bz:
+            assert form.BrickInfo() == (fes.ne // 8, 2)
+        y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+        form.Mult(dev(x), y)
+        out[bz] = host(y)
+    ref = O.OracleOperator(en, fes.gather_map(), fes.ndofs, 4, alpha=a, beta=b).mult(x)
+    assert relerr(out[2], ref) <= RTOL and relerr(out[0], ref) <= RTOL

@@ -286,6 +286,12 @@ def main():
             line["pcg"] = pcg
         print(json.dumps(line), flush=True)
     if world > 1:
+        # release the forms (ncclCommDestroy of the operator's communicator) on every rank
+        # while all ranks are alive, then tear down torch's process group
+        del step, apply, timed_forms, pform
+        import gc
+        gc.collect()
+        torch.cuda.synchronize()
         dist.barrier()
         dist.destroy_process_group()
 

@@ -78,8 +78,32 @@ struct ApplyArgs
    const int *bmap = nullptr;       // device [nbrick][NB] lattice map: dof | shared << 30
    const int *brick_off = nullptr;  // host [nblk + 1], bricks whose first element lies in block b
    int brick_bz = 0;                // 0: no bricks
-   double *part_brick = nullptr;    // partial slots [nbrick][NB] of shared lattice points
+   double *part_brick = nullptr;    // partial slots [nbrick][surface] of shared lattice points
 };
+
+// Partial-slot order of a brick's surface lattice points (2 x 2 x bz elements, lattice
+// LX = LY = 2 D - 1, LZ = bz (D - 1) + 1), grouped by face so that the two holders of a
+// face dof -- this brick's high face and the neighbour's low face -- list it at the same
+// offset within their groups: [Z = 0 | Z = LZ-1 | Y = 0 | Y = LY-1 | X = 0 | X = LX-1],
+// edges and corners in the first group that contains them.  -1 for interior points.
+__host__ __device__ inline int brick_surface_points(int D, int bz)
+{
+   const int LX = 2 * D - 1, LY = LX, LZ = bz * (D - 1) + 1;
+   return 2 * LX * LY + 2 * (LZ - 2) * LX + 2 * (LZ - 2) * (LY - 2);
+}
+__host__ __device__ inline int brick_surface_index(int D, int bz, int X, int Y, int Z)
+{
+   const int LX = 2 * D - 1, LY = LX, LZ = bz * (D - 1) + 1;
+   if (Z == 0) { return Y * LX + X; }
+   if (Z == LZ - 1) { return LX * LY + Y * LX + X; }
+   const int b1 = 2 * LX * LY;
+   if (Y == 0) { return b1 + (Z - 1) * LX + X; }
+   if (Y == LY - 1) { return b1 + (LZ - 2) * LX + (Z - 1) * LX + X; }
+   const int b2 = b1 + 2 * (LZ - 2) * LX;
+   if (X == 0) { return b2 + (Z - 1) * (LY - 2) + (Y - 1); }
+   if (X == LX - 1) { return b2 + (LZ - 2) * (LY - 2) + (Z - 1) * (LY - 2) + (Y - 1); }
+   return -1;
+}
 
 namespace kern
 {

@@ -511,16 +511,37 @@ void PAForm::assemble(hipStream_t s)
       auto encode = [&](int d, bool neg) {
          return (int)((unsigned)d | ((hcount[d] > 1 ? 1u : 0u) << 30) | ((neg ? 1u : 0u) << 31));
       };
-      part_line_off_ = (long)n_bricks_ * brick_np_;
+      // brick partial slots: [brick][face-grouped surface index]; only surface points can be
+      // shared (a brick holds its interior lattice points alone: checked)
+      const int nsurf = brick_bz_ ? brick_surface_points(D_, brick_bz_) : 0;
+      part_line_off_ = (long)n_bricks_ * nsurf;
       std::vector<int> enc(gmap_host_.size()), benc(bdof.size()), hdof, hslot;
+      std::vector<long> bslot;
       for (size_t i = 0; i < bdof.size(); i++)
       {
          benc[i] = encode(bdof[i], false);
          if (hcount[bdof[i]] > 1)
          {
+            const int k = (int)(i / brick_np_), p = (int)(i % brick_np_);
+            const int si = brick_surface_index(D_, brick_bz_, p % LX, (p / LX) % LY, p / (LX * LY));
+            ECM2_VERIFY(si >= 0, ERR_INTERNAL, "brick " << k << ": interior lattice point " << p << " is shared");
             hdof.push_back(bdof[i]);
-            hslot.push_back((int)i);
+            bslot.push_back((long)k * nsurf + si);
          }
+      }
+      // the plan wants the holders in ascending slot order
+      {
+         std::vector<size_t> ord(bslot.size());
+         for (size_t i = 0; i < ord.size(); i++) { ord[i] = i; }
+         std::sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return bslot[a] < bslot[b]; });
+         std::vector<int> hd(ord.size());
+         hslot.resize(ord.size());
+         for (size_t i = 0; i < ord.size(); i++)
+         {
+            hd[i] = hdof[ord[i]];
+            hslot[i] = (int)bslot[ord[i]];
+         }
+         hdof.swap(hd);
       }
       ECM2_VERIFY(part_line_off_ + (long)nblk * ND_ * 64 < (1l << 31), ERR_UNSUPPORTED, "too many partial slots");
       for (size_t i = 0; i < gmap_host_.size(); i++)

@@ -895,6 +895,45 @@ __device__ __forceinline__ void line_load_qdata(double (&qv)[7][Q], int e, int t
    }
 }
 
+// As line_load_qdata with 16-byte loads from the native layout (even Q1D, lane pairs of
+// adjacent columns l0 = l & ~1): lane l0 loads plane 2j and lane l0+1 plane 2j+1 of the
+// pair's two columns, then each swaps the value its partner owns with one quad_perm DPP
+// move -- half the load instructions, whole 16-byte segments per lane.
+__device__ __forceinline__ double dpp_swap_pair(double v)
+{
+   const int lo = __double2loint(v), hi = __double2hiint(v);
+   const int slo = __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xF, 0xF, false);  // quad_perm(1,0,3,2)
+   const int shi = __builtin_amdgcn_mov_dpp(hi, 0xB1, 0xF, 0xF, false);
+   return __hiloint2double(shi, slo);
+}
+
+template <int D, int Q, bool MASS, bool DIFF>
+__device__ __forceinline__ void line_load_qdata_x2(double (&qv)[7][Q], int e, int l,
+                                                   const double *__restrict__ qdd,
+                                                   const double *__restrict__ qdm)
+{
+   static_assert(Q % 2 == 0, "paired qdata loads need an even Q1D");
+   constexpr int NQ = Q * Q * Q, QQ = Q * Q;
+   const int odd = l & 1, l0 = l & ~1;
+   auto pair = [&](const double *p, double &lo_plane, double &hi_plane) {
+      const v2d v = *reinterpret_cast<const v2d *>(p);
+      const double recv = dpp_swap_pair(odd ? v.x : v.y);
+      lo_plane = odd ? recv : v.x;   // plane 2j of column l
+      hi_plane = odd ? v.y : recv;   // plane 2j+1 of column l
+   };
+#pragma unroll
+   for (int j = 0; j < Q / 2; j++)
+   {
+      const int qz = 2 * j + odd;
+      if (DIFF)
+      {
+#pragma unroll
+         for (int c = 0; c < 6; c++) { pair(qdd + ((size_t)e * 6 + c) * NQ + qz * QQ + l0, qv[c][2 * j], qv[c][2 * j + 1]); }
+      }
+      if (MASS) { pair(qdm + (size_t)e * NQ + qz * QQ + l0, qv[6][2 * j], qv[6][2 * j + 1]); }
+   }
+}
+
 // Grid-function coefficient at the quadrature points (GridFunctionCoefficient projected
 // by CoefficientVector::Project, coefficient.cpp:2052-2070 / qfunction.cpp:73-98, composed
 // with the affine Pennes law), sum-factorised like the line kernel: one wave per element,
@@ -1196,7 +1235,8 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned
 // ((2(D-1)+1)^2 (BZ(D-1)+1) points) in LDS in a fixed order, so the shared faces inside
 // a brick never reach HBM: a lattice point held by this brick alone is plain-stored,
 // one on the brick surface that other holders share goes to its partial slot
-// part[brick][point] for k_sum_partials (deterministic, no atomics).
+// part[brick][surface index] (face-grouped, brick_surface_index) for k_sum_partials
+// (deterministic, no atomics).
 // Per element: same qdata, x-line gathers and contractions as k_apply_line
 // (bilininteg_mass_kernels.hpp:809-1033, bilininteg_diffusion_kernels.hpp:989-1214);
 // the brick map replaces ElementRestriction's element maps (restriction.cpp:109-186).
@@ -1206,10 +1246,14 @@ struct BrickShape
 {
    static constexpr int NE = 4 * BZ, DD = D * D, QQ = Q * Q, DQ = D * Q, ND = D * D * D;
    static constexpr int LX = 2 * (D - 1) + 1, LY = LX, LZ = BZ * (D - 1) + 1, NB = LX * LY * LZ;
+   static constexpr int SURF = 2 * LX * LY + 2 * (LZ - 2) * LX + 2 * (LZ - 2) * (LY - 2);
    // per-element LDS: SA holds the x-stage lines (2 D^2 Q), SB the y/z-stage planes (3 D Q^2,
    // the z stage works in place); staged element outputs (D^3) reuse SB
    static constexpr int SA = 2 * DD * Q, SB = 3 * D * QQ;
    static constexpr int NT = ((NE * QQ + 63) / 64) * 64;  // stage 3 in one pass
+   // waves per SIMD the register budget targets: 4 (<= 128 VGPRs) up to p = 4, where the
+   // 2 x 2 x 1 brick then fits 5 workgroups per CU; the larger orders keep their registers
+   static constexpr int WPE = D <= 5 ? 4 : 1;
 };
 
 // lattice coordinate P along one brick direction -> (first element index, local index,
@@ -1223,9 +1267,10 @@ __device__ __forceinline__ void brick_cand(int P, int &c0, int &l0, int &n)
 }
 
 // VAR bit 1: load the stage-3 qdata at the top of the z stage (fewer VGPRs, more
-// workgroups per CU) instead of at kernel entry (in flight during stages 1-2)
+// workgroups per CU) instead of at kernel entry (in flight during stages 1-2); bit 2:
+// 16-byte paired loads (line_load_qdata_x2, even Q1D)
 template <int D, int Q, int BZ, bool MASS, bool DIFF, bool SPLIT, int VAR>
-__global__ void __launch_bounds__((BrickShape<D, Q, BZ>::NT))
+__global__ void __launch_bounds__((BrickShape<D, Q, BZ>::NT), (BrickShape<D, Q, BZ>::WPE))
 k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *__restrict__ bmap, int n_owned,
               const double *__restrict__ qdd, const double *__restrict__ qdm,
               const double *__restrict__ x, const double *__restrict__ xg,
@@ -1252,7 +1297,11 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
    double qv[7][Q];
    if (!(VAR & 1) && t < NE * QQ)
    {
-      line_load_qdata<D, Q, MASS, DIFF>(qv, belem[(size_t)k * NE + t / QQ], t % QQ, qdd, qdm);
+      if constexpr ((VAR & 2) && Q % 2 == 0)
+      {
+         line_load_qdata_x2<D, Q, MASS, DIFF>(qv, belem[(size_t)k * NE + t / QQ], t % QQ, qdd, qdm);
+      }
+      else { line_load_qdata<D, Q, MASS, DIFF>(qv, belem[(size_t)k * NE + t / QQ], t % QQ, qdd, qdm); }
    }
 
    // ---- lanes (element, dy, dz): gather the x-line, contract in x
@@ -1459,7 +1508,7 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
       const int g = bm[p];
       const int d = bdof(g);
       if (!bshared(g)) { *((!SPLIT || d < n_owned) ? y + d : yg + (d - n_owned)) = v; }
-      else { part[(size_t)k * NB + p] = v; }
+      else { part[(size_t)k * S::SURF + brick_surface_index(D, BZ, X, Y, Z)] = v; }  // surface only (setup)
    }
 }
 
@@ -2013,13 +2062,11 @@ void launch_brick_mdq(const ApplyArgs &a, hipStream_t s)
    hipLaunchKernelGGL((k_apply_brick<D, Q, BZ, MASS, DIFF, SP, V>), grid, block, 0, s, k0, k1, a.belem, \
                       a.bmap, a.n_owned, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, a.part_brick)
    const bool split = a.xg || a.yg;
-   if (brick_variant() & 1)
+   switch (brick_variant() & 3)
    {
-      if (split) { ECM2_BRICK(true, 1); } else { ECM2_BRICK(false, 1); }
-   }
-   else
-   {
-      if (split) { ECM2_BRICK(true, 0); } else { ECM2_BRICK(false, 0); }
+      case 1: if (split) { ECM2_BRICK(true, 1); } else { ECM2_BRICK(false, 1); } break;
+      case 2: if (split) { ECM2_BRICK(true, 2); } else { ECM2_BRICK(false, 2); } break;
+      default: if (split) { ECM2_BRICK(true, 0); } else { ECM2_BRICK(false, 0); } break;
    }
 #undef ECM2_BRICK
 }

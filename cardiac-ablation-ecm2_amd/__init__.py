@@ -78,6 +78,7 @@ def load_library(path: str = LIB_PATH):
         "ecm2_h1space_info": (i32, [vp, ip, ip, ip]),
         "ecm2_h1space_get_gather_map": (i32, [vp, vp]),
         "ecm2_h1space_boundary_dofs": (i32, [vp, vp, ip]),
+        "ecm2_h1space_element_order": (i32, [vp, vp]),
         "ecm2_h1space_dof_coords": (i32, [vp, vp, vp]),
         "ecm2_h1space_destroy": (None, [vp]),
         "ecm2_pa_form_create": (i32, [i32, i32, i32, vp, i32, pp]),
@@ -256,6 +257,12 @@ class H1Space:
         _check(_lib.ecm2_h1space_get_gather_map(self._h, _np_ptr(out)))
         return out
 
+    def element_order_faces(self) -> np.ndarray:
+        """4x4x4 face-linked bricks first (ecm2_h1space_element_order): internal position -> element."""
+        out = np.empty(self.ne, np.int32)
+        _check(_lib.ecm2_h1space_element_order(self._h, _np_ptr(out)))
+        return out
+
     def boundary_dofs(self) -> np.ndarray:
         n = ctypes.c_int(0)
         _check(_lib.ecm2_h1space_boundary_dofs(self._h, None, ctypes.byref(n)))
@@ -333,17 +340,25 @@ class BilinearForm:
         _check(_lib.ecm2_pa_form_set_kernel(h, kernel))
         _check(_lib.ecm2_pa_form_set_scatter(h, _SCATTER[scatter]))
         _check(_lib.ecm2_pa_form_set_bricks(h, bricks))
-        if element_order != "native" and fes.ne > 0:
+        if element_order == "native" and fes.ne > 0:
+            ident = np.arange(fes.ne, dtype=np.int32)  # kept alive across the call
+            _check(_lib.ecm2_pa_form_set_element_order(h, _np_ptr(ident)))
+        elif fes.ne > 0:
+            # "auto": Cartesian meshes -> the mesh's 4x4x4 brick order; otherwise the form
+            # derives face-linked bricks from the element->dof map at Assemble
+            perm = None
             if element_order in ("auto", "brick"):
                 try:
                     perm = fes.mesh.element_order(ORDER_BRICK)
                 except ECM2Error:
                     if element_order == "brick":
                         raise
-                    perm = fes.mesh.element_order(ORDER_MORTON)
-            else:
+            elif element_order == "morton":
                 perm = fes.mesh.element_order(ORDER_MORTON)
-            _check(_lib.ecm2_pa_form_set_element_order(h, _np_ptr(perm)))
+            elif element_order != "faces":
+                raise ECM2Error(f"unknown element order {element_order!r}")
+            if perm is not None:
+                _check(_lib.ecm2_pa_form_set_element_order(h, _np_ptr(perm)))
 
     def __del__(self):
         if getattr(self, "_h", None) and _lib is not None:

@@ -5,6 +5,7 @@
 #include "fe.hpp"
 #include "mesh.hpp"
 #include "pa_form.hpp"
+#include "bricks.hpp"
 #include "par_form.hpp"
 #include "partition.hpp"
 #include "solvers.hpp"
@@ -230,6 +231,15 @@ int ecm2_h1space_get_gather_map(const ecm2_h1space *s, int *out)
    return guard([&] {
       NEED(s); NEED(out);
       std::memcpy(out, s->s.gather_map.data(), s->s.gather_map.size() * sizeof(int));
+   });
+}
+
+int ecm2_h1space_element_order(const ecm2_h1space *s, int *perm)
+{
+   return guard([&] {
+      NEED(s); NEED(perm);
+      const std::vector<int> p = ecm2::face_brick_order(s->s.ne, s->s.order + 1, s->s.gather_map);
+      std::memcpy(perm, p.data(), p.size() * sizeof(int));
    });
 }
 

@@ -1,5 +1,6 @@
 // pa_form.cpp -- see pa_form.hpp.
 #include "pa_form.hpp"
+#include "bricks.hpp"
 
 #include <algorithm>
 #include <cmath>
@@ -74,6 +75,12 @@ void PAForm::set_block_splits(const std::vector<int> &splits)
    for (int b : splits) { ECM2_VERIFY(b >= 0 && b <= layout_.nblk(), ERR_ARG, "block split " << b << " out of range"); }
    splits_ = splits;
    gmap_line_.resize(0);
+   if (perm_auto_)  // the derived brick order respects the segments: derive it again
+   {
+      perm_host_.clear();
+      perm_auto_ = false;
+      gmap_blk_.resize(0);
+   }
    assembled_ = false;
 }
 
@@ -111,6 +118,7 @@ void PAForm::set_element_order(const int *perm)
 {
    std::vector<int> seen(ne_, 0);
    perm_host_.assign(perm, perm + ne_);
+   perm_auto_ = false;
    for (int e : perm_host_)
    {
       ECM2_VERIFY(e >= 0 && e < ne_ && !seen[e], ERR_ARG, "element order is not a permutation");
@@ -194,83 +202,6 @@ static int line_brick_mode()
       return e ? std::max(0, std::min(2, std::atoi(e))) : 1;
    }();
    return v;
-}
-
-// Bricks of 2 x 2 x bz elements found by dof equality alone (any element order, any
-// conforming mesh): the x, y and z neighbours of e are the elements whose low face
-// (local index 0 along that direction) equals e's high face (index D-1) entry by entry;
-// a brick is e0, e1 = x(e0), e2 = y(e0), e3 = x(e2) = y(e1) and, for bz = 2, the z
-// neighbours of those, with all twelve internal faces checked, all elements in one
-// apply_blocks segment and no orientation signs.  Greedy in element order; bricks are
-// therefore ordered by first element.  belem: [nbrick][4 bz].
-static void find_bricks(int ne, int D, const std::vector<int> &gm, int bz, const std::vector<int> &seg,
-                        std::vector<int> &belem, std::vector<char> &in_brick)
-{
-   const int ND = D * D * D;
-   auto dof = [&](int e, int a) { const int g = gm[(size_t)e * ND + a]; return g >= 0 ? g : -1 - g; };
-   auto face = [D](int dir, int s, int i, int j) {
-      if (dir == 0) { return (j * D + i) * D + s; }
-      if (dir == 1) { return (j * D + s) * D + i; }
-      return (s * D + j) * D + i;
-   };
-   auto key = [&](int e, int dir, int s) {
-      uint64_t h = 1469598103934665603ull;
-      for (int j : {0, D - 1})
-         for (int i : {0, D - 1}) { h = (h ^ (uint64_t)(uint32_t)dof(e, face(dir, s, i, j))) * 1099511628211ull; }
-      return h;
-   };
-   std::vector<int> nbr[3];
-   for (int dir = 0; dir < 3; dir++)
-   {
-      nbr[dir].assign(ne, -1);
-      std::unordered_map<uint64_t, int> low;
-      low.reserve((size_t)ne * 2);
-      for (int e = 0; e < ne; e++)
-      {
-         auto it = low.emplace(key(e, dir, 0), e);
-         if (!it.second) { it.first->second = -1; }  // ambiguous: no neighbour through it
-      }
-      for (int e = 0; e < ne; e++)
-      {
-         auto it = low.find(key(e, dir, D - 1));
-         if (it == low.end() || it->second < 0 || it->second == e) { continue; }
-         const int f = it->second;
-         bool ok = true;
-         for (int j = 0; j < D && ok; j++)
-            for (int i = 0; i < D && ok; i++) { ok = dof(e, face(dir, D - 1, i, j)) == dof(f, face(dir, 0, i, j)); }
-         if (ok) { nbr[dir][e] = f; }
-      }
-   }
-   auto nb = [&](int dir, int e) { return e < 0 ? -1 : nbr[dir][e]; };
-   const int nbe = 4 * bz;
-   for (int e0 = 0; e0 < ne; e0++)
-   {
-      if (in_brick[e0]) { continue; }
-      int el[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
-      el[0] = e0;
-      el[1] = nb(0, e0);
-      el[2] = nb(1, e0);
-      el[3] = nb(0, el[2]);
-      bool ok = el[1] >= 0 && el[3] >= 0 && nb(1, el[1]) == el[3];
-      if (ok && bz == 2)
-      {
-         for (int i = 0; i < 4; i++) { el[4 + i] = nb(2, el[i]); }
-         ok = el[4] >= 0 && el[5] >= 0 && el[6] >= 0 && el[7] >= 0 && nb(0, el[4]) == el[5] &&
-              nb(1, el[4]) == el[6] && nb(0, el[6]) == el[7] && nb(1, el[5]) == el[7];
-      }
-      for (int i = 0; i < nbe && ok; i++)
-      {
-         ok = el[i] >= 0 && !in_brick[el[i]] && seg[el[i]] == seg[e0];
-         for (int j = 0; j < i && ok; j++) { ok = el[j] != el[i]; }
-         for (int a = 0; a < ND && ok; a++) { ok = gm[(size_t)el[i] * ND + a] >= 0; }
-      }
-      if (!ok) { continue; }
-      for (int i = 0; i < nbe; i++)
-      {
-         belem.push_back(el[i]);
-         in_brick[el[i]] = 1;
-      }
-   }
 }
 
 // Longest chunk of x-adjacent elements one wave of the line kernel walks: the kernel
@@ -362,6 +293,22 @@ void PAForm::assemble(hipStream_t s)
 
    if (resolved_mode_ == KERNEL_TPE && !gmap_blk_.size() && ne_ > 0)
    {
+      if (perm_host_.empty() && auto_order_)
+      {
+         // no caller order: 4x4x4 face-linked bricks first (one per wave), per apply segment
+         std::vector<int> cuts{0};
+         for (int sp : splits_) { cuts.push_back(std::min(ne_, sp * kElemBlock)); }
+         cuts.push_back(ne_);
+         std::sort(cuts.begin(), cuts.end());
+         for (size_t k = 0; k + 1 < cuts.size(); k++)
+         {
+            const int e0 = cuts[k], n = cuts[k + 1] - cuts[k];
+            if (n <= 0) { continue; }
+            std::vector<int> sub(gmap_host_.begin() + (size_t)e0 * ND_, gmap_host_.begin() + (size_t)(e0 + n) * ND_);
+            for (int e : face_brick_order(n, D_, sub)) { perm_host_.push_back(e0 + e); }
+         }
+         perm_auto_ = true;
+      }
       const int nblk = layout_.nblk();
       std::vector<int> gint((size_t)ne_ * ND_), pos(ne_);
       for (int i = 0; i < ne_; i++)

@@ -66,7 +66,9 @@ public:
 
    // Optional element permutation (internal position i <- caller element perm[i]) used by
    // the blocked layout; ORDER_BRICK puts one 4x4x4 brick in each 64-lane wave so the
-   // fused kernel can assemble shared faces in-wave.  All APIs keep caller element order.
+   // fused kernel can assemble shared faces in-wave.  Without one, assemble() derives a
+   // brick order from the element->dof map (face_brick_order, any conforming mesh).  All
+   // APIs keep caller element order.
    void set_element_order(const int *perm_host);
    // Block indices at which apply_blocks ranges may start or end besides 0 and nblocks()
    // (the distributed form's interior | boundary split).  The line kernel's bricks never
@@ -162,6 +164,8 @@ private:
    long part_line_off_ = 0;         // LINE: leftover elements' partial slots start here
    int n_left_ = 0;                 // LINE: elements outside bricks
    int line_bricks_ = -1;           // requested brick mode (set_line_bricks)
+   bool auto_order_ = true;         // TPE without a caller order: face-linked 4x4x4 bricks
+   bool perm_auto_ = false;         // perm_host_ was derived (not the caller's)
    DeviceArray<int> lane_flags_;    // [blk][64] in-wave merge flags
    std::vector<int> perm_host_;     // internal position -> caller element (empty: identity)
    DeviceArray<int> pos_;           // caller element -> internal position

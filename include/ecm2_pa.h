@@ -97,6 +97,12 @@ int ecm2_h1space_info(const ecm2_h1space *s, int *ndofs, int *ne, int *nd);
 int ecm2_h1space_get_gather_map(const ecm2_h1space *s, int *out /* host [ne][nd] */);
 /* Essential true dofs for ess_bdr = all (GetEssentialTrueDofs): two-call pattern,
  * out may be NULL to query *count. */
+/* Element order with 4x4x4 bricks of face-linked elements first (one per 64-lane wave of
+ * the thread-per-element kernel), found from the element->dof map alone; any conforming
+ * hex mesh (no reference counterpart: the reference applies elements independently,
+ * fem/restriction.cpp:152-186).  perm host [ne]: internal position -> element.  Host only;
+ * a PA form without an explicit order derives the same order at assemble. */
+int ecm2_h1space_element_order(const ecm2_h1space *s, int *perm);
 int ecm2_h1space_boundary_dofs(const ecm2_h1space *s, int *out, int *count);
 int ecm2_h1space_dof_coords(const ecm2_h1space *s, const ecm2_mesh *m, double *out /* host [ndofs][3] */);
 void ecm2_h1space_destroy(ecm2_h1space *s);

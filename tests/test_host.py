@@ -134,3 +134,47 @@ def test_structured_and_entity_numbering_give_same_operator(order):
         order_idx = np.lexsort(np.round(xyz, 10).T)
         outs.append(y[order_idx])
     assert relerr(outs[0], outs[1]) < 1e-13
+
+
+def _face_links(fes, perm):
+    """Check every complete 64-element block of perm is a 4x4x4 brick whose lanes
+    ax + 4 ay + 16 az are linked face to face (entry-by-entry dof equality)."""
+    gm = fes.gather_map()
+    D = fes.order + 1
+    G = gm.reshape(fes.ne, D, D, D)  # [e][dz][dy][dx]
+    nb = 0
+    for b in range(fes.ne // 64):
+        lanes = perm[64 * b: 64 * b + 64]
+        ok = True
+        for l in range(64):
+            ax, ay, az = l % 4, (l // 4) % 4, l // 16
+            e = lanes[l]
+            if ax < 3:
+                ok &= np.array_equal(G[e, :, :, D - 1], G[lanes[l + 1], :, :, 0])
+            if ay < 3:
+                ok &= np.array_equal(G[e, :, D - 1, :], G[lanes[l + 4], :, 0, :])
+            if az < 3:
+                ok &= np.array_equal(G[e, D - 1, :, :], G[lanes[l + 16], 0, :, :])
+        nb += int(ok)
+    return nb
+
+
+@pytest.mark.parametrize("order", [1, 2])
+def test_face_brick_order(order):
+    """ecm2_h1space_element_order (the derived order a PA form uses without a caller order):
+    a permutation; on fichera refined twice (7 hexes x 4^3) all 448 elements form 7 linked
+    bricks; on a Cartesian mesh it finds the mesh's own 4x4x4 bricks."""
+    m = E.Mesh(f"{GOLDEN}/fichera.mesh")
+    m.UniformRefinement()
+    m.UniformRefinement()
+    fes = E.H1Space(m, order)
+    perm = fes.element_order_faces()
+    assert sorted(perm.tolist()) == list(range(fes.ne))
+    assert fes.ne == 448 and _face_links(fes, perm) == 7
+    c = E.Mesh.MakeCartesian3D(9, 8, 5)
+    fc = E.H1Space(c, order)
+    perm = fc.element_order_faces()
+    assert sorted(perm.tolist()) == list(range(fc.ne))
+    assert _face_links(fc, perm) == 2 * 2 * 1
+    ref = c.element_order(E.ORDER_BRICK)
+    assert sorted(perm[:256].tolist()) == sorted(ref[:256].tolist())

@@ -152,6 +152,12 @@ void restriction_mult_transpose(int ndofs, int nd, const int *offsets, const int
                                 const double *xe, double *y, hipStream_t s);
 
 // ---- diagonal (Jacobi) ----
+// Thread-per-element diagonal on the blocked layout, assembled/stored like apply_tpe (a.y /
+// a.yg / a.part / a.lane_flags; a.x unused); drow = make_diag_row_table.
+void diagonal_tpe(int D, int Q, bool mass, bool diff, const ApplyArgs &a, const Basis1D &b, const double *drow,
+                  hipStream_t s);
+std::vector<double> make_diag_row_table(const DofToQuad &m);
+// Sum-factorised workgroup-per-element diagonal, any layout; L-vector (atomics) or E-vector.
 void diagonal(const int *pos, int D, int Q, int layout, int ne, const int *gmap_native, const double *qd_diff,
               const double *qd_mass, double *diag, bool out_evec, const Basis1D &b,
               hipStream_t s);
@@ -160,7 +166,9 @@ void diagonal(const int *pos, int D, int Q, int layout, int ne, const int *gmap_
 void set_values(int n, const int *idx, double val, double *y, hipStream_t s);     // y[idx] = val
 void copy_values(int n, const int *idx, const double *x, double *y, hipStream_t s); // y[idx] = x[idx]
 // Deterministic two-pass dot: result written to *out (device).
-void dot(int n, const double *a, const double *b, double *partials, double *out, hipStream_t s);
+// hout (optional): device pointer of mapped pinned host memory that also receives the result.
+void dot(int n, const double *a, const double *b, double *partials, double *out, hipStream_t s,
+         double *hout = nullptr);
 // PCG updates with device-resident scalars (no host round trip):
 //   x += (nom/den) d ; r -= (nom/den) z
 void pcg_update_xr(int n, const double *nom, const double *den, const double *d,
@@ -168,7 +176,7 @@ void pcg_update_xr(int n, const double *nom, const double *den, const double *d,
 // Fused PCG update: x += (nom/den) d; r -= (nom/den) z; z = dinv .* r (dinv null: z untouched);
 // *out = r.z (r.r without dinv), deterministic.  z holds A d on entry.
 void pcg_step(int n, const double *nom, const double *den, const double *d, double *z, double *x, double *r,
-              const double *dinv, double *partials, double *out, hipStream_t s);
+              const double *dinv, double *partials, double *out, hipStream_t s, double *hout = nullptr);
 // saved[i] = v[idx[i]], v[idx[i]] = 0  /  v[idx[i]] = y[idx[i]] = saved[i]
 void ess_save_zero(int n, const int *idx, double *v, double *saved, hipStream_t s);
 void ess_restore(int n, const int *idx, const double *saved, double *v, double *y, hipStream_t s);

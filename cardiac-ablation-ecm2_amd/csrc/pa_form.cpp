@@ -358,6 +358,7 @@ void PAForm::assemble(hipStream_t s)
       for (int e = 0; e < ne_; e++) { perm[pos[e]] = e; }
       perm_dev_.upload(perm, s);
       rowtab_.upload(kern::make_row_table(maps_), s);
+      drowtab_.upload(kern::make_diag_row_table(maps_), s);
       ECM2_HIP(hipStreamSynchronize(s));
    }
    if (resolved_mode_ == KERNEL_LINE) { kern::upload_basis(D_, Q_, basis_); }
@@ -765,6 +766,16 @@ void PAForm::assemble_diagonal(double *diag, hipStream_t s)
 {
    ECM2_VERIFY(assembled_, ERR_STATE, "AssembleDiagonal before Assemble");
    if (ndofs_ == 0) { return; }
+   if (resolved_mode_ == KERNEL_TPE && (have_mass_ || have_diff_))
+   {
+      // thread-per-element diagonal assembled like the Mult (deterministic with partials)
+      double *dg = n_owned_ < ndofs_ ? diag + n_owned_ : nullptr;
+      if (!use_partials()) { ECM2_HIP(hipMemsetAsync(diag, 0, sizeof(double) * (size_t)ndofs_, s)); }
+      ApplyArgs a = apply_args(nullptr, nullptr, diag, dg, 0, layout_.nblk());
+      kern::diagonal_tpe(D_, Q_, have_mass_, have_diff_, a, basis_, drowtab_.data(), s);
+      finish_shared(0, n_sh_, diag, dg, s);
+      return;
+   }
    ECM2_HIP(hipMemsetAsync(diag, 0, sizeof(double) * (size_t)ndofs_, s));
    kern::diagonal(layout_.pos, D_, Q_, layout_.kind, ne_, gmap_.data(), have_diff_ ? qd_diff_.data() : nullptr,
                   have_mass_ ? qd_mass_.data() : nullptr, diag, false, basis_, s);

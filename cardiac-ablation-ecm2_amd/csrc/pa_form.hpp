@@ -173,7 +173,7 @@ private:
    DeviceArray<int> csr_off_, csr_idx_;
    DeviceArray<double> enodes_;     // [e][3][8]
    const double *jac_ = nullptr;    // device, not owned
-   DeviceArray<double> W_, rowtab_;
+   DeviceArray<double> W_, rowtab_, drowtab_;
    DeviceArray<double> qd_diff_, qd_mass_;
    DeviceArray<double> xe_, ye_;    // unfused work E-vectors
    DeviceArray<double> ctmp_m_, ctmp_d_;

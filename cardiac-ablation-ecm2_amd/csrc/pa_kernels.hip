@@ -459,6 +459,64 @@ __device__ __forceinline__ int xcd_contiguous(int i, int G)
    return x * q + (x < r ? x : r) + j;
 }
 
+// In-wave assembly of a thread-per-element block's outputs and their store (apply and
+// diagonal kernels).  A 4x4x4 brick is one wave: x, y, z neighbours are lanes +1, +4, +16;
+// setup-computed lane flags say which faces really coincide (dof-index equality), so any
+// element order is correct; bricks make it effective.  SIGNS: apply the map's orientation
+// signs before summation (y = A x; the diagonal's signs square away).  Then entries whose
+// face was sent away hold nothing; a dof held once in the whole mesh is plain-stored; a
+// shared one goes to its dense partial slot [blk][a][lane] (summed in a fixed order by
+// k_sum_partials: deterministic, no atomics, no y memset) or, without a partial buffer, is
+// atomically added.  PLAIN: diagnostic (plain stores only; wrong for shared dofs).
+template <int D, bool SPLIT, bool SIGNS, bool PLAIN>
+__device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], const int *__restrict__ mp, int fl,
+                                                   int blk, int lane, bool active, int n_owned,
+                                                   double *__restrict__ y, double *__restrict__ yg,
+                                                   double *__restrict__ part)
+{
+   constexpr int ND = D * D * D;
+   if (SIGNS)
+   {
+#pragma unroll
+      for (int a = 0; a < ND; a++)
+      {
+         if (bneg(mp[a * 64])) { Yo[a] = -Yo[a]; }
+      }
+   }
+   auto merge = [&](int delta, int recv_bit, int sent_bit, auto face) {
+#pragma unroll
+      for (int j = 0; j < D; j++)
+#pragma unroll
+         for (int i = 0; i < D; i++)
+         {
+            const double v = __shfl_down(Yo[face(0, i, j)], delta, 64);
+            if (fl & recv_bit) { Yo[face(D - 1, i, j)] += v; }
+            if (fl & sent_bit) { Yo[face(0, i, j)] = 0.0; }
+         }
+   };
+   merge(1, 1, 2, [](int s, int i, int j) { return (j * D + i) * D + s; });    // x: (dz=j, dy=i)
+   merge(4, 4, 8, [](int s, int i, int j) { return (j * D + s) * D + i; });    // y: (dz=j, dx=i)
+   merge(16, 16, 32, [](int s, int i, int j) { return (s * D + j) * D + i; }); // z: (dy=j, dx=i)
+   if (!active) { return; }
+   const bool sx = fl & 2, sy = fl & 8, sz = fl & 32;
+#pragma unroll
+   for (int dz = 0; dz < D; dz++)
+#pragma unroll
+      for (int dy = 0; dy < D; dy++)
+#pragma unroll
+         for (int dx = 0; dx < D; dx++)
+         {
+            if ((dx == 0 && sx) || (dy == 0 && sy) || (dz == 0 && sz)) { continue; }
+            const int a = (dz * D + dy) * D + dx;
+            const int g = mp[a * 64];
+            const int d = bdof(g);
+            double *dst = (!SPLIT || d < n_owned) ? y + d : yg + (d - n_owned);
+            if (!bshared(g) || PLAIN) { *dst = Yo[a]; }
+            else if (part) { part[((size_t)blk * ND + a) * 64 + lane] = Yo[a]; }
+            else { unsafeAtomicAdd(dst, Yo[a]); }
+         }
+}
+
 template <int D, int Q, bool MASS, bool DIFF, bool SPLIT, int VAR>
 __global__ void __launch_bounds__(256, (VAR & 8) ? 2 : 1)
 k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
@@ -606,53 +664,94 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
          cm[qx] = nm[qx];
       }
    }
-   // ---- in-wave assembly of shared faces (4x4x4 brick = one wave: x, y, z neighbours
-   // are lanes +1, +4, +16).  Setup-computed flags say which faces really coincide
-   // (dof-index equality), so any element order is correct; bricks make it effective.
+   tpe_assemble_store<D, SPLIT, true, (VAR & 1) != 0>(Yo, mp, lane_flags[(size_t)blk * 64 + lane], blk, lane, active,
+                                                      n_owned, y, yg, part);
+}
+
+// PA diagonal, thread per element on the blocked layout (PADiffusionDiagonal3D and the
+// mass diagonal, bilininteg_diffusion_kernels.hpp:369, bilininteg_mass_kernels.hpp:325,
+// assembled like AssembleDiagonal's E->L transpose, bilinearform_ext.cpp:370-454):
+//   diag(a) = sum_q grad(phi_a)^T O_q grad(phi_a) + m_q phi_a^2,  phi_a = B_x B_y B_z,
+// sum-factorised per quadrature row (qy, qz): seven x-contractions S_k(dx) of the row's
+// qdata, then the (dy, dz) factors of the row from a table, [6][dz][dy] = (By Bz)^2,
+// (Gy Bz)^2, (By Gz)^2, Gy By Bz^2, By^2 Gz Bz, Gy By Gz Bz.  Output assembled and stored
+// exactly like k_apply_tpe_pf's (in-wave faces, plain stores, partial slots): every
+// diagonal entry written once, deterministic, no memset.
+template <int D, int Q, bool MASS, bool DIFF, bool SPLIT>
+__global__ void __launch_bounds__(256)
+k_diag_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
+           const double *__restrict__ qdd, const double *__restrict__ qdm, double *__restrict__ y,
+           double *__restrict__ yg, const Basis1D b, const double *__restrict__ drow,
+           const int *__restrict__ lane_flags, double *__restrict__ part)
+{
+   constexpr int ND = D * D * D, NQ = Q * Q * Q, NQH = (NQ + 1) / 2, DD = D * D;
+   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+   const int blk = blk_begin + blockIdx.x * 4 + w;
+   if (blk >= blk_end) { return; }  // wave-uniform
+   const bool active = blk * 64 + lane < ne;
+   const int *mp = gmap + (size_t)blk * ND * 64 + lane;
+   const double *qd = qdd + (size_t)blk * NQ * 3 * 128 + lane * 2;
+   const double *qm = qdm + (size_t)blk * NQH * 128 + lane * 2;
+   double Yo[ND];
 #pragma unroll
-   for (int a = 0; a < ND; a++)
+   for (int a = 0; a < ND; a++) { Yo[a] = 0.0; }
+#pragma unroll 1
+   for (int row = 0; row < Q * Q; row++)
    {
-      if (bneg(mp[a * 64])) { Yo[a] = -Yo[a]; }  // orientation signs before summation
-   }
-   const int fl = lane_flags[(size_t)blk * 64 + lane];
-   auto merge = [&](int delta, int recv_bit, int sent_bit, auto face) {
+      double S[7][D];
 #pragma unroll
-      for (int j = 0; j < D; j++)
+      for (int k = 0; k < 7; k++)
 #pragma unroll
-         for (int i = 0; i < D; i++)
+         for (int dx = 0; dx < D; dx++) { S[k][dx] = 0.0; }
+#pragma unroll
+      for (int qx = 0; qx < Q; qx++)
+      {
+         const int q = row * Q + qx;
+         v2d d0 = {0.0, 0.0}, d1 = {0.0, 0.0}, d2 = {0.0, 0.0};
+         if (DIFF)
          {
-            const double v = __shfl_down(Yo[face(0, i, j)], delta, 64);
-            if (fl & recv_bit) { Yo[face(D - 1, i, j)] += v; }
-            if (fl & sent_bit) { Yo[face(0, i, j)] = 0.0; }
+            d0 = *reinterpret_cast<const v2d *>(qd + ((size_t)q * 3 + 0) * 128);
+            d1 = *reinterpret_cast<const v2d *>(qd + ((size_t)q * 3 + 1) * 128);
+            d2 = *reinterpret_cast<const v2d *>(qd + ((size_t)q * 3 + 2) * 128);
          }
-   };
-   merge(1, 1, 2, [](int s, int i, int j) { return (j * D + i) * D + s; });    // x: (dz=j, dy=i)
-   merge(4, 4, 8, [](int s, int i, int j) { return (j * D + s) * D + i; });    // y: (dz=j, dx=i)
-   merge(16, 16, 32, [](int s, int i, int j) { return (s * D + j) * D + i; }); // z: (dy=j, dx=i)
-   // ---- output: entries whose face was sent away hold nothing; a dof held once in the
-   // whole mesh is plain-stored; a shared one goes to its dense partial slot
-   // [blk][a][lane] (summed in a fixed order by k_sum_partials: deterministic, no
-   // atomics, no y memset) or, without a partial buffer, is atomically added
-   if (active)
-   {
-      const bool sx = fl & 2, sy = fl & 8, sz = fl & 32;
+         const double m = MASS ? qm[(size_t)(q >> 1) * 128 + (q & 1)] : 0.0;
+#pragma unroll
+         for (int dx = 0; dx < D; dx++)
+         {
+            const double bx = b.B[qx + MQ * dx], gx = b.G[qx + MQ * dx];
+            const double bb = bx * bx, gb = gx * bx;
+            if (DIFF)
+            {
+               S[0][dx] += gx * gx * d0.x;  // O11
+               S[1][dx] += bb * d1.y;       // O22
+               S[2][dx] += bb * d2.y;       // O33
+               S[3][dx] += gb * d0.y;       // O12
+               S[4][dx] += gb * d1.x;       // O13
+               S[5][dx] += bb * d2.x;       // O23
+            }
+            if (MASS) { S[6][dx] += bb * m; }
+         }
+      }
+      const double *P = drow + (size_t)row * 6 * DD;
 #pragma unroll
       for (int dz = 0; dz < D; dz++)
 #pragma unroll
          for (int dy = 0; dy < D; dy++)
+         {
+            const int o = dz * D + dy;
+            const double p0 = P[o], p1 = P[DD + o], p2 = P[2 * DD + o];
+            const double p3 = P[3 * DD + o], p4 = P[4 * DD + o], p5 = P[5 * DD + o];
 #pragma unroll
             for (int dx = 0; dx < D; dx++)
             {
-               if ((dx == 0 && sx) || (dy == 0 && sy) || (dz == 0 && sz)) { continue; }
-               const int a = (dz * D + dy) * D + dx;
-               const int g = mp[a * 64];
-               const int d = bdof(g);
-               double *dst = (!SPLIT || d < n_owned) ? y + d : yg + (d - n_owned);
-               if (!bshared(g) || (VAR & 1)) { *dst = Yo[a]; }
-               else if (part) { part[((size_t)blk * ND + a) * 64 + lane] = Yo[a]; }
-               else { unsafeAtomicAdd(dst, Yo[a]); }
+               double v = p0 * (S[0][dx] + S[6][dx]) + p1 * S[1][dx] + p2 * S[2][dx];
+               v += 2.0 * (p3 * S[3][dx] + p4 * S[4][dx] + p5 * S[5][dx]);
+               Yo[o * D + dx] += v;
             }
+         }
    }
+   tpe_assemble_store<D, SPLIT, false, false>(Yo, mp, lane_flags[(size_t)blk * 64 + lane], blk, lane, active,
+                                               n_owned, y, yg, part);
 }
 
 // --------------------------------------------------------------------------
@@ -891,6 +990,91 @@ __device__ __forceinline__ void line_load_qdata(double (&qv)[7][Q], int e, int t
             for (int c = 0; c < 6; c++) { qv[c][qz] = qdd[((size_t)e * 6 + c) * NQ + qz * QQ + t]; }
          }
          if (MASS) { qv[6][qz] = qdm[(size_t)e * NQ + qz * QQ + t]; }
+      }
+   }
+}
+
+// PA diagonal, one 64-lane workgroup per element, any qdata layout, any (D1D, Q1D) with
+// Q1D^2 <= 64: the same seven terms sum-factorised in three stages through LDS --
+// lanes (qx, qy) contract qz, lanes (qx, dz) contract qy, lanes (dy, dz) contract qx and
+// add into the L-vector (atomics) or the E-vector.
+template <int D, int Q>
+__global__ void __launch_bounds__(64)
+k_diag_sf(const int *__restrict__ pos, int kind, int ne, const int *__restrict__ gmap,
+          const double *__restrict__ qdd, const double *__restrict__ qdm, double *__restrict__ diag, bool out_e)
+{
+   constexpr int ND = D * D * D, NQ = Q * Q * Q, QQ = Q * Q, DD = D * D, DQ = D * Q;
+   static_assert(QQ <= 64, "k_diag_sf needs Q1D <= 8");
+   __shared__ double T[7][D][QQ];   // [k][dz][qy qx]
+   __shared__ double U[7][DD][Q];   // [k][dz dy][qx]
+   const int e = blockIdx.x, t = threadIdx.x;
+   if (e >= ne) { return; }
+   CBasis *bp = stage_basis<D, Q>();
+   // term k = fx(qx,dx) fy(qy,dy) fz(qz,dz) O_k: kinds 0 = B^2, 1 = G^2, 2 = G B per direction
+   constexpr int FX[7] = {1, 0, 0, 2, 2, 0, 0}, FY[7] = {0, 1, 0, 2, 0, 2, 0}, FZ[7] = {0, 0, 1, 0, 2, 2, 0};
+   auto f = [&](int kindf, int qq, int dd) {
+      const double bq = bp->B[qq + MQ * dd], gq = bp->G[qq + MQ * dd];
+      return kindf == 0 ? bq * bq : (kindf == 1 ? gq * gq : gq * bq);
+   };
+   if (t < QQ)
+   {
+      double acc[7][D];
+#pragma unroll
+      for (int k = 0; k < 7; k++)
+#pragma unroll
+         for (int dz = 0; dz < D; dz++) { acc[k][dz] = 0.0; }
+#pragma unroll
+      for (int qz = 0; qz < Q; qz++)
+      {
+         const int q = qz * QQ + t;
+         double O[7];
+         // symmetric entries (11,12,13,22,23,33) -> terms (11, 22, 33, 2*12, 2*13, 2*23), mass
+         const int src[6] = {0, 3, 5, 1, 2, 4};
+#pragma unroll
+         for (int k = 0; k < 6; k++)
+         {
+            O[k] = qdd ? qdd[qidx_diff(pos, kind, NQ, e, src[k], q)] * (k >= 3 ? 2.0 : 1.0) : 0.0;
+         }
+         O[6] = qdm ? qdm[qidx_mass(pos, kind, NQ, e, q)] : 0.0;
+#pragma unroll
+         for (int k = 0; k < 7; k++)
+#pragma unroll
+            for (int dz = 0; dz < D; dz++) { acc[k][dz] += f(FZ[k], qz, dz) * O[k]; }
+      }
+#pragma unroll
+      for (int k = 0; k < 7; k++)
+#pragma unroll
+         for (int dz = 0; dz < D; dz++) { T[k][dz][t] = acc[k][dz]; }
+   }
+   __syncthreads();
+   if (t < DQ)
+   {
+      const int qx = t % Q, dz = t / Q;
+#pragma unroll
+      for (int k = 0; k < 7; k++)
+#pragma unroll
+         for (int dy = 0; dy < D; dy++)
+         {
+            double u = 0.0;
+#pragma unroll
+            for (int qy = 0; qy < Q; qy++) { u += f(FY[k], qy, dy) * T[k][dz][qy * Q + qx]; }
+            U[k][dz * D + dy][qx] = u;
+         }
+   }
+   __syncthreads();
+   if (t < DD)
+   {
+#pragma unroll
+      for (int dx = 0; dx < D; dx++)
+      {
+         double v = 0.0;
+#pragma unroll
+         for (int k = 0; k < 7; k++)
+#pragma unroll
+            for (int qx = 0; qx < Q; qx++) { v += f(FX[k], qx, dx) * U[k][t][qx]; }
+         const long i = (long)e * ND + t * D + dx;
+         if (out_e) { diag[i] += v; }
+         else { unsafeAtomicAdd(diag + dof_of(gmap[i]), v); }
       }
    }
 }
@@ -1603,7 +1787,7 @@ k_dot_partial(int n, const double *__restrict__ a, const double *__restrict__ b,
 }
 
 __global__ void __launch_bounds__(256)
-k_dot_final(int nparts, const double *__restrict__ partials, double *__restrict__ out)
+k_dot_final(int nparts, const double *__restrict__ partials, double *__restrict__ out, double *__restrict__ hout)
 {
    __shared__ double red[4];
    double s = 0.0;
@@ -1611,7 +1795,12 @@ k_dot_final(int nparts, const double *__restrict__ partials, double *__restrict_
    for (int off = 32; off > 0; off >>= 1) { s += __shfl_down(s, off, 64); }
    if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6] = s; }
    __syncthreads();
-   if (threadIdx.x == 0) { *out = (red[0] + red[1]) + (red[2] + red[3]); }
+   if (threadIdx.x == 0)
+   {
+      const double v = (red[0] + red[1]) + (red[2] + red[3]);
+      *out = v;
+      if (hout) { *hout = v; }  // mapped pinned host mirror (the solver's stopping test)
+   }
 }
 
 __global__ void k_pcg_update_xr(int n, const double *__restrict__ nom,
@@ -2181,9 +2370,91 @@ void diagonal(const int *pos, int D, int Q, int layout, int ne, const int *gm, c
 {
    const long n = (long)ne * D * D * D;
    if (n == 0) { return; }
+   upload_basis(D, Q, b);
+#define ECM2_DIAG_CASE(DD, QQ)                                                                             \
+   if (D == DD && Q == QQ)                                                                                 \
+   {                                                                                                       \
+      hipLaunchKernelGGL((k_diag_sf<DD, QQ>), dim3(ne), dim3(64), 0, s, pos, layout, ne, gm, qdd, qdm, diag, \
+                         out_e);                                                                           \
+      ECM2_HIP(hipGetLastError());                                                                         \
+      return;                                                                                              \
+   }
+   ECM2_DIAG_CASE(2, 3)
+   ECM2_DIAG_CASE(3, 4)
+   ECM2_DIAG_CASE(4, 5)
+   ECM2_DIAG_CASE(5, 6)
+   ECM2_DIAG_CASE(6, 7)
+   ECM2_DIAG_CASE(7, 8)
+   ECM2_DIAG_CASE(2, 2)
+   ECM2_DIAG_CASE(3, 3)
+   ECM2_DIAG_CASE(4, 4)
+   ECM2_DIAG_CASE(5, 5)
+#undef ECM2_DIAG_CASE
    hipLaunchKernelGGL(k_diagonal, dim3(grid_for(n, 128)), dim3(128), 0, s, pos, D, Q, layout, ne, gm,
                       qdd, qdm, diag, out_e, b);
    ECM2_HIP(hipGetLastError());
+}
+
+template <int D, int Q, bool MASS, bool DIFF>
+static void launch_diag_tpe(const ApplyArgs &a, const Basis1D &b, const double *drow, hipStream_t s)
+{
+   const int nb = a.blk_end - a.blk_begin;
+   if (nb <= 0) { return; }
+   const dim3 grid((nb + 3) / 4), block(256);
+   if (a.yg)
+   {
+      hipLaunchKernelGGL((k_diag_tpe<D, Q, MASS, DIFF, true>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end,
+                         a.n_owned, a.gmap, a.qdd, a.qdm, a.y, a.yg, b, drow, a.lane_flags, a.part);
+   }
+   else
+   {
+      hipLaunchKernelGGL((k_diag_tpe<D, Q, MASS, DIFF, false>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end,
+                         a.n_owned, a.gmap, a.qdd, a.qdm, a.y, a.yg, b, drow, a.lane_flags, a.part);
+   }
+}
+
+template <int D, int Q>
+static void launch_diag_tpe_dq(bool mass, bool diff, const ApplyArgs &a, const Basis1D &b, const double *drow,
+                               hipStream_t s)
+{
+   if (mass && diff) { launch_diag_tpe<D, Q, true, true>(a, b, drow, s); }
+   else if (mass) { launch_diag_tpe<D, Q, true, false>(a, b, drow, s); }
+   else if (diff) { launch_diag_tpe<D, Q, false, true>(a, b, drow, s); }
+}
+
+void diagonal_tpe(int D, int Q, bool mass, bool diff, const ApplyArgs &a, const Basis1D &b, const double *drow,
+                  hipStream_t s)
+{
+   if (a.ne == 0) { return; }
+   if (D == 2 && Q == 3) { launch_diag_tpe_dq<2, 3>(mass, diff, a, b, drow, s); }
+   else if (D == 3 && Q == 4) { launch_diag_tpe_dq<3, 4>(mass, diff, a, b, drow, s); }
+   else { ECM2_VERIFY(false, ERR_UNSUPPORTED, "no thread-per-element diagonal for D1D=" << D << " Q1D=" << Q); }
+   ECM2_HIP(hipGetLastError());
+}
+
+std::vector<double> make_diag_row_table(const DofToQuad &m)
+{
+   const int D = m.ndof, Q = m.nqpt, DD = D * D;
+   std::vector<double> t((size_t)Q * Q * 6 * DD);
+   for (int qz = 0; qz < Q; qz++)
+      for (int qy = 0; qy < Q; qy++)
+      {
+         double *P = &t[(size_t)(qz * Q + qy) * 6 * DD];
+         for (int dz = 0; dz < D; dz++)
+            for (int dy = 0; dy < D; dy++)
+            {
+               const double By = m.B[qy + Q * dy], Gy = m.G[qy + Q * dy];
+               const double Bz = m.B[qz + Q * dz], Gz = m.G[qz + Q * dz];
+               const int o = dz * D + dy;
+               P[0 * DD + o] = By * By * Bz * Bz;
+               P[1 * DD + o] = Gy * Gy * Bz * Bz;
+               P[2 * DD + o] = By * By * Gz * Gz;
+               P[3 * DD + o] = Gy * By * Bz * Bz;
+               P[4 * DD + o] = By * By * Gz * Bz;
+               P[5 * DD + o] = Gy * By * Gz * Bz;
+            }
+      }
+   return t;
 }
 
 void set_values(int n, const int *idx, double val, double *y, hipStream_t s)
@@ -2200,10 +2471,10 @@ void copy_values(int n, const int *idx, const double *x, double *y, hipStream_t 
    ECM2_HIP(hipGetLastError());
 }
 
-void dot(int n, const double *a, const double *b, double *partials, double *out, hipStream_t s)
+void dot(int n, const double *a, const double *b, double *partials, double *out, hipStream_t s, double *hout)
 {
    hipLaunchKernelGGL(k_dot_partial, dim3(kDotBlocks), dim3(256), 0, s, n, a, b, partials);
-   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, s, kDotBlocks, partials, out);
+   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, s, kDotBlocks, partials, out, hout);
    ECM2_HIP(hipGetLastError());
 }
 
@@ -2215,10 +2486,10 @@ void pcg_update_xr(int n, const double *nom, const double *den, const double *d,
 }
 
 void pcg_step(int n, const double *nom, const double *den, const double *d, double *z, double *x, double *r,
-              const double *dinv, double *partials, double *out, hipStream_t s)
+              const double *dinv, double *partials, double *out, hipStream_t s, double *hout)
 {
    hipLaunchKernelGGL(k_pcg_step, dim3(kDotBlocks), dim3(256), 0, s, n, nom, den, d, z, x, r, dinv, partials);
-   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, s, kDotBlocks, partials, out);
+   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, s, kDotBlocks, partials, out, hout);
    ECM2_HIP(hipGetLastError());
 }
 

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <memory>
 
 namespace ecm2
 {
@@ -39,94 +40,130 @@ void GroupOp::diagonal(double *d, hipStream_t s)
 // ---------------------------------------------------------------------------------------
 // ConstrainedOperator + CGSolver + OperatorJacobiSmoother
 // ---------------------------------------------------------------------------------------
+namespace
+{
+// CGSolver's work vectors live across solves (CGSolver::SetOperator allocates them once,
+// solvers.cpp:869-880): one workspace per host thread and device, grown on demand, with a
+// mapped pinned scalar the final-dot kernels write the stopping-test value into.
+struct PCGWork
+{
+   DeviceArray<double> r, d, z, saved, dinv, partials, scal;
+   double *hs = nullptr, *hs_dev = nullptr;
+   ~PCGWork()
+   {
+      if (hs) { (void)hipHostFree(hs); }
+   }
+   void ensure(int n, int n_ess, bool jacobi)
+   {
+      auto grow = [](DeviceArray<double> &a, size_t m) {
+         if (a.size() < m) { a.resize(m); }
+      };
+      grow(r, std::max(n, 1));
+      grow(d, std::max(n, 1));
+      grow(z, std::max(n, 1));
+      grow(saved, std::max(n_ess, 1));
+      if (jacobi) { grow(dinv, std::max(n, 1)); }
+      grow(partials, 1024);
+      grow(scal, 4);
+      if (!hs)
+      {
+         ECM2_HIP(hipHostMalloc(&hs, 4 * sizeof(double), hipHostMallocMapped));
+         ECM2_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&hs_dev), hs, 0));
+      }
+   }
+};
+
+PCGWork &pcg_work()
+{
+   static thread_local std::vector<std::unique_ptr<PCGWork>> per_device;
+   int dev = 0;
+   ECM2_HIP(hipGetDevice(&dev));
+   if ((int)per_device.size() <= dev) { per_device.resize(dev + 1); }
+   if (!per_device[dev]) { per_device[dev].reset(new PCGWork()); }
+   return *per_device[dev];
+}
+} // namespace
+
 PCGResult pcg_solve(LinOp &A, const int *ess, int n_ess, const double *b, double *x, double rel_tol,
                     double abs_tol, int max_iter, bool jacobi, hipStream_t s)
 {
    const int n = A.size();
    PCGResult res;
-   DeviceArray<double> r(std::max(n, 1)), d(std::max(n, 1)), z(std::max(n, 1)), saved(std::max(n_ess, 1));
-   DeviceArray<double> partials(1024), scal(4), dinv;
-   double *nom = scal.data(), *den = scal.data() + 1, *betanom = scal.data() + 2;
-   double *hs = nullptr;
-   ECM2_HIP(hipHostMalloc(&hs, 4 * sizeof(double)));
-   // every rank reads the same (globally summed) scalar, so all take the same branch
+   PCGWork &w = pcg_work();
+   w.ensure(n, n_ess, jacobi);
+   double *r = w.r.data(), *d = w.d.data(), *z = w.z.data(), *dinv = jacobi ? w.dinv.data() : nullptr;
+   double *partials = w.partials.data();
+   // device scalars; nom and betanom swap roles every iteration (no copy)
+   double *nom = w.scal.data(), *den = w.scal.data() + 1, *betanom = w.scal.data() + 2;
+   // serial: the final-dot kernel also writes the value into mapped pinned memory, so the
+   // stopping test needs only a stream sync; distributed: copy after the all-reduce
+   const bool direct = !A.distributed();
    auto dot = [&](const double *a, const double *bb, double *out) {
-      kern::dot(n, a, bb, partials.data(), out, s);
+      kern::dot(n, a, bb, partials, out, s, direct ? w.hs_dev : nullptr);
       A.sum_scalars(out, 1, s);
    };
    auto readback = [&](const double *dv) {
-      ECM2_HIP(hipMemcpyAsync(hs, dv, sizeof(double), hipMemcpyDeviceToHost, s));
+      if (!direct) { ECM2_HIP(hipMemcpyAsync(w.hs, dv, sizeof(double), hipMemcpyDeviceToHost, s)); }
       ECM2_HIP(hipStreamSynchronize(s));
-      return hs[0];
+      return *(volatile double *)w.hs;
    };
    // ConstrainedOperator::ConstrainedMult, DIAG_ONE (operator.cpp:586-646): the input's
    // ess entries are zeroed in place for the Mult and restored after (no vector copy);
    // out[ess] = in[ess]
    auto cmult = [&](double *in, double *out) {
       if (n_ess == 0) { A.mult(in, out, s); return; }
-      kern::ess_save_zero(n_ess, ess, in, saved.data(), s);
+      kern::ess_save_zero(n_ess, ess, in, w.saved.data(), s);
       A.mult(in, out, s);
-      kern::ess_restore(n_ess, ess, saved.data(), in, out, s);
+      kern::ess_restore(n_ess, ess, w.saved.data(), in, out, s);
    };
-   try
+   if (jacobi)
    {
-      if (jacobi)
+      // OperatorJacobiSmoother on the constrained operator: ess rows get diag 1
+      A.diagonal(z, s);
+      if (n_ess) { kern::set_values(n_ess, ess, 1.0, z, s); }
+      kern::reciprocal(n, z, dinv, s);
+   }
+   if (n) { ECM2_HIP(hipMemcpyAsync(r, b, sizeof(double) * n, hipMemcpyDeviceToDevice, s)); }
+   if (n) { ECM2_HIP(hipMemsetAsync(x, 0, sizeof(double) * n, s)); }
+   if (jacobi)
+   {
+      kern::pcg_precond(n, dinv, r, z, s);
+      if (n) { ECM2_HIP(hipMemcpyAsync(d, z, sizeof(double) * n, hipMemcpyDeviceToDevice, s)); }
+   }
+   else if (n)
+   {
+      ECM2_HIP(hipMemcpyAsync(d, r, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+   }
+   dot(d, r, nom);
+   const double nom0 = readback(nom);
+   res.initial_norm = nom0 >= 0 ? std::sqrt(nom0) : nom0;
+   const double r0 = std::max(nom0 * rel_tol * rel_tol, abs_tol * abs_tol);
+   res.final_norm = res.initial_norm;
+   if (nom0 <= r0) { res.converged = true; }
+   else
+   {
+      cmult(d, z);
+      dot(z, d, den);
+      if (readback(den) != 0.0)
       {
-         // OperatorJacobiSmoother on the constrained operator: ess rows get diag 1
-         dinv.resize(std::max(n, 1));
-         A.diagonal(z.data(), s);
-         if (n_ess) { kern::set_values(n_ess, ess, 1.0, z.data(), s); }
-         kern::reciprocal(n, z.data(), dinv.data(), s);
-      }
-      if (n) { ECM2_HIP(hipMemcpyAsync(r.data(), b, sizeof(double) * n, hipMemcpyDeviceToDevice, s)); }
-      if (n) { ECM2_HIP(hipMemsetAsync(x, 0, sizeof(double) * n, s)); }
-      if (jacobi)
-      {
-         kern::pcg_precond(n, dinv.data(), r.data(), z.data(), s);
-         if (n) { ECM2_HIP(hipMemcpyAsync(d.data(), z.data(), sizeof(double) * n, hipMemcpyDeviceToDevice, s)); }
-      }
-      else if (n)
-      {
-         ECM2_HIP(hipMemcpyAsync(d.data(), r.data(), sizeof(double) * n, hipMemcpyDeviceToDevice, s));
-      }
-      dot(d.data(), r.data(), nom);
-      const double nom0 = readback(nom);
-      res.initial_norm = nom0 >= 0 ? std::sqrt(nom0) : nom0;
-      const double r0 = std::max(nom0 * rel_tol * rel_tol, abs_tol * abs_tol);
-      res.final_norm = res.initial_norm;
-      if (nom0 <= r0) { res.converged = true; }
-      else
-      {
-         cmult(d.data(), z.data());
-         dot(z.data(), d.data(), den);
-         if (readback(den) != 0.0)
+         for (int i = 1;;)
          {
-            for (int i = 1;;)
-            {
-               // x += alpha d, r -= alpha A d, z = M^{-1} r, betanom = r.z in one pass
-               kern::pcg_step(n, nom, den, d.data(), z.data(), x, r.data(), jacobi ? dinv.data() : nullptr,
-                              partials.data(), betanom, s);
-               A.sum_scalars(betanom, 1, s);
-               const double bn = readback(betanom);
-               res.final_norm = bn >= 0 ? std::sqrt(bn) : bn;
-               res.iterations = i;
-               if (bn <= r0) { res.converged = true; break; }
-               if (++i > max_iter) { break; }
-               kern::pcg_update_d(n, betanom, nom, jacobi ? z.data() : r.data(), d.data(), s);
-               cmult(d.data(), z.data());
-               dot(d.data(), z.data(), den);
-               ECM2_HIP(hipMemcpyAsync(nom, betanom, sizeof(double), hipMemcpyDeviceToDevice, s));
-            }
+            // x += alpha d, r -= alpha A d, z = M^{-1} r, betanom = r.z in one pass
+            kern::pcg_step(n, nom, den, d, z, x, r, dinv, partials, betanom, s, direct ? w.hs_dev : nullptr);
+            A.sum_scalars(betanom, 1, s);
+            const double bn = readback(betanom);
+            res.final_norm = bn >= 0 ? std::sqrt(bn) : bn;
+            res.iterations = i;
+            if (bn <= r0) { res.converged = true; break; }
+            if (++i > max_iter) { break; }
+            kern::pcg_update_d(n, betanom, nom, jacobi ? z : r, d, s);
+            cmult(d, z);
+            dot(d, z, den);
+            std::swap(nom, betanom);  // nom <- betanom
          }
       }
    }
-   catch (...)
-   {
-      (void)hipHostFree(hs);
-      throw;
-   }
    ECM2_HIP(hipStreamSynchronize(s));
-   (void)hipHostFree(hs);
    return res;
 }
 

@@ -34,6 +34,8 @@ public:
    virtual void diagonal(double *d, hipStream_t s) = 0;
    // in-place global sum of n device scalars over all ranks (serial: nothing to do)
    virtual void sum_scalars(double *dev, int n, hipStream_t s) { (void)dev; (void)n; (void)s; }
+   // true when sum_scalars communicates (a locally reduced scalar is not yet global)
+   virtual bool distributed() const { return false; }
 };
 
 class FormOp : public LinOp
@@ -56,6 +58,7 @@ public:
    void mult(const double *x, double *y, hipStream_t s) override { f_.mult(x, y, s); }
    void diagonal(double *d, hipStream_t s) override { f_.assemble_diagonal(d, s); }
    void sum_scalars(double *dev, int n, hipStream_t s) override { f_.allreduce_sum(dev, n, s); }
+   bool distributed() const override { return true; }
 
 private:
    ParPAForm &f_;

@@ -293,7 +293,11 @@ void PAForm::assemble(hipStream_t s)
 
    if (resolved_mode_ == KERNEL_TPE && !gmap_blk_.size() && ne_ > 0)
    {
-      if (perm_host_.empty() && auto_order_)
+      static const bool auto_env = [] {  // experiment knob ECM2_AUTO_ORDER=0: keep caller order
+         const char *e = std::getenv("ECM2_AUTO_ORDER");
+         return !(e && std::string(e) == "0");
+      }();
+      if (perm_host_.empty() && auto_order_ && auto_env)
       {
          // no caller order: 4x4x4 face-linked bricks first (one per wave), per apply segment
          std::vector<int> cuts{0};

@@ -15,7 +15,7 @@ import json
 import os
 import sys
 
-KERNELS = {"apply": "k_apply_tpe", "apply_line": "k_apply_line", "apply_brick": "k_apply_brick", "sum_partials": "k_sum_partials", "apply_wpe": "k_apply_wpe"}
+KERNELS = {"apply": "k_apply_tpe", "apply_line": "k_apply_line", "apply_brick": "k_apply_brick", "diag_tpe": "k_diag_tpe", "pcg_step": "k_pcg_step", "sum_partials": "k_sum_partials", "apply_wpe": "k_apply_wpe"}
 
 
 def counters(d, name):

@@ -79,6 +79,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: capture one Mult in a HIP graph and replay it per step (single process)")
+    ap.add_argument("--geometry", choices=["compressed", "full"], default="compressed",
+                    help="compressed: AFFINE qdata on parallelepiped meshes (default); full: per-point layout")
     ap.add_argument("--loopback", type=int, default=1,
                     help="N>1 on one GPU: N subdomains in this process (validation of the partitioned path)")
     args = ap.parse_args()
@@ -101,6 +103,7 @@ def main():
     kernel = {"auto": E.KERNEL_AUTO, "tpe": E.KERNEL_TPE, "wpe": E.KERNEL_WPE, "unfused": E.KERNEL_UNFUSED,
               "line": E.KERNEL_LINE}[args.kernel]
 
+    compress = args.geometry == "compressed"
     order = 4 if args.workload == "c5" else 2
     if args.workload == "c2":
         n = 50
@@ -136,7 +139,7 @@ def main():
     if nsub <= 1:
         alpha, T = bioheat_coefficients(E, torch, mesh, fes)
         form = E.BilinearForm(fes, kernel=kernel, element_order=os.environ.get("ECM2_ELEMENT_ORDER", "auto"),
-                              scatter=scatter)
+                              scatter=scatter, compress_geometry=compress)
         form.AddDomainIntegrator(mass(alpha))
         form.AddDomainIntegrator(diff(T))
         form.Assemble()
@@ -150,7 +153,8 @@ def main():
             rid = [E.rccl_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(rid, src=0)
             part = E.Partition(fes, er, rank, world)
-            pform = E.ParBilinearForm(part, rccl_id=rid[0], kernel=kernel, scatter=scatter)
+            pform = E.ParBilinearForm(part, rccl_id=rid[0], kernel=kernel, scatter=scatter,
+                                      compress_geometry=compress)
             alpha, T = bioheat_coefficients(E, torch, mesh, fes, part)
             pform.AddDomainIntegrator(mass(alpha))
             pform.AddDomainIntegrator(diff(T))
@@ -163,7 +167,7 @@ def main():
             forms, keep = [], []
             for r in range(nsub):
                 part = E.Partition(fes, er, r, nsub)
-                pf = E.ParBilinearForm(part, kernel=kernel, scatter=scatter)
+                pf = E.ParBilinearForm(part, kernel=kernel, scatter=scatter, compress_geometry=compress)
                 alpha, T = bioheat_coefficients(E, torch, mesh, fes, part)
                 keep += [alpha, T]
                 pf.AddDomainIntegrator(mass(alpha))
@@ -216,26 +220,29 @@ def main():
     for f in timed_forms:
         f.timing(False)
     abytes = sum(f.algorithmic_bytes() for f in timed_forms)
+    qbytes = sum(f.qdata_bytes() for f in timed_forms)
     pcg = c3_pcg(E, torch, fes, form) if args.workload == "c3" else None
 
     # aggregate over ranks: total true dofs, max time; kernel ms per Mult (summed over
     # the apply launches of one Mult: interior + boundary blocks when partitioned)
-    tot = torch.tensor([float(n_true), dt, abytes, kms / args.steps],
+    tot = torch.tensor([float(n_true), dt, abytes, kms / args.steps, qbytes],
                        dtype=torch.float64, device="cuda")
     if world > 1:
         s = tot.clone()
         dist.all_reduce(s[0:1], op=dist.ReduceOp.SUM)
         dist.all_reduce(s[2:3], op=dist.ReduceOp.SUM)
+        dist.all_reduce(s[4:5], op=dist.ReduceOp.SUM)
         dist.all_reduce(s[1:2], op=dist.ReduceOp.MAX)
         dist.all_reduce(s[3:4], op=dist.ReduceOp.MAX)
         tot = s
-    ndofs_total, tmax, bytes_total, kavg_ms = [float(v) for v in tot.cpu()]
+    ndofs_total, tmax, bytes_total, kavg_ms, qbytes_total = [float(v) for v in tot.cpu()]
     value = ndofs_total * args.steps / tmax / 1e6
 
     if rank == 0:
         achieved = bytes_total / world / (kavg_ms * 1e-3) / 1e9
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_n{world}.json")
+        # pinned PMC traffic of this workload, kernel family and qdata layout (profiles/pmc_pin.py)
+        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_n{world}_{qdata_layout(E, timed_forms[0])}.json")
         if os.path.exists(pmc):
             try:
                 traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
@@ -265,6 +272,8 @@ def main():
                 "order": order, "q1d": order + 2,
                 "launch": "hip-graph replay per Mult" if (args.graph and world == 1) else "stream launches",
                 "kernel": ["auto", "tpe", "wpe", "unfused", "line"][timed_forms[0].info()["kernel"]],
+                "qdata_layout": qdata_layout(E, timed_forms[0]),
+                "qdata_bytes_stored": qbytes_total / world,
                 "parallelism": f"domain-decomposition z-slabs x{world}, RCCL shared-DoF exchange" if world > 1
                 else (f"loopback z-slabs x{args.loopback} on one GPU" if args.loopback > 1 else "single GPU"),
             },
@@ -279,6 +288,10 @@ def main():
                 "stream_copy_gbs": stream,
                 "frac_of_stream": round(achieved / stream, 4) if stream else None,
                 "algorithmic_bytes_per_launch": bytes_total / world,
+                # real HBM rate of the dominant kernel (PMC bytes / its time): with AFFINE qdata
+                # the kernel moves fewer bytes than the SURVEY's fixed formula counts, so
+                # "frac" can exceed 1; this is the bandwidth actually drawn
+                "traffic_gbs": round(traffic / (kavg_ms * 1e-3) / 1e9, 1) if traffic else None,
             },
             "cpu_baseline": cpu,
         }
@@ -294,6 +307,12 @@ def main():
         torch.cuda.synchronize()
         dist.barrier()
         dist.destroy_process_group()
+
+
+def qdata_layout(E, form):
+    """Quadrature-data layout of a (local) form: affine | blocked | native."""
+    return {E.QLAYOUT_NATIVE: "native", E.QLAYOUT_BLOCKED: "blocked",
+            E.QLAYOUT_AFFINE: "affine"}[form.info()["layout"]]
 
 
 def c3_pcg(E, torch, fes, form, max_iter=200):

@@ -36,6 +36,7 @@ KERNEL_AUTO, KERNEL_TPE, KERNEL_WPE, KERNEL_UNFUSED, KERNEL_LINE = 0, 1, 2, 3, 4
 NUMBERING_ENTITY, NUMBERING_STRUCTURED = 0, 1
 ORDER_NATIVE, ORDER_BRICK, ORDER_MORTON = 0, 1, 2
 SCATTER_PARTIALS, SCATTER_ATOMIC = 0, 1
+QLAYOUT_NATIVE, QLAYOUT_BLOCKED, QLAYOUT_AFFINE = 0, 1, 2  # BilinearForm.info()['layout']
 _SCATTER = {"partials": SCATTER_PARTIALS, "atomic": SCATTER_ATOMIC}
 
 
@@ -90,6 +91,8 @@ def load_library(path: str = LIB_PATH):
         "ecm2_pa_form_set_scatter": (i32, [vp, i32]),
         "ecm2_pa_form_scatter_info": (i32, [vp, vp, vp]),
         "ecm2_pa_form_set_bricks": (i32, [vp, i32]),
+        "ecm2_pa_form_set_geometry_compression": (i32, [vp, i32]),
+        "ecm2_pa_form_qdata_bytes": (i32, [vp, dp]),
         "ecm2_pa_form_brick_info": (i32, [vp, ip, ip]),
         "ecm2_pa_form_set_element_order": (i32, [vp, vp]),
         "ecm2_mesh_element_order": (i32, [vp, i32, vp]),
@@ -325,7 +328,8 @@ class BilinearForm:
     """BilinearForm at AssemblyLevel::PARTIAL backed by the HIP PA form."""
 
     def __init__(self, fes: H1Space, kernel: int = KERNEL_AUTO, q1d: int = 0, geometry: str = "nodes",
-                 element_order: str = "auto", scatter: str = "partials", bricks: int = -1):
+                 element_order: str = "auto", scatter: str = "partials", bricks: int = -1,
+                 compress_geometry: bool = True):
         self.fes = fes
         self._integs = []
         self._kernel = kernel
@@ -340,6 +344,7 @@ class BilinearForm:
         _check(_lib.ecm2_pa_form_set_kernel(h, kernel))
         _check(_lib.ecm2_pa_form_set_scatter(h, _SCATTER[scatter]))
         _check(_lib.ecm2_pa_form_set_bricks(h, bricks))
+        _check(_lib.ecm2_pa_form_set_geometry_compression(h, 1 if compress_geometry else 0))
         if element_order == "native" and fes.ne > 0:
             ident = np.arange(fes.ne, dtype=np.int32)  # kept alive across the call
             _check(_lib.ecm2_pa_form_set_element_order(h, _np_ptr(ident)))
@@ -446,6 +451,12 @@ class BilinearForm:
         _check(_lib.ecm2_pa_form_algorithmic_bytes(self._h, ctypes.byref(b)))
         return b.value
 
+    def qdata_bytes(self) -> float:
+        """Bytes of quadrature data stored (after Assemble)."""
+        b = ctypes.c_double()
+        _check(_lib.ecm2_pa_form_qdata_bytes(self._h, ctypes.byref(b)))
+        return b.value
+
     def PCG(self, b, x, ess=None, rel_tol=1e-12, abs_tol=0.0, max_iter=1000, jacobi=True, stream=None):
         """ConstrainedOperator(DIAG_ONE) + CGSolver(+OperatorJacobiSmoother); returns (iters, final_norm)."""
         it, nrm = ctypes.c_int(), ctypes.c_double()
@@ -474,6 +485,9 @@ _PAR_SIGS = {
     "ecm2_par_form_set_kernel": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ecm2_par_form_set_scatter": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ecm2_par_form_set_bricks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "ecm2_par_form_set_geometry_compression": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "ecm2_par_form_qdata_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]),
+    "ecm2_par_form_layout": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
     "ecm2_par_form_assemble": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "ecm2_par_form_mult": (ctypes.c_int, [ctypes.c_void_p] * 4),
     "ecm2_par_group_mult": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
@@ -578,7 +592,7 @@ class ParBilinearForm:
     group member (use ParGroup.Mult); otherwise one process per GPU over RCCL."""
 
     def __init__(self, part: Partition, rccl_id: Optional[bytes] = None, kernel: int = KERNEL_AUTO, q1d: int = 0,
-                 scatter: str = "partials", bricks: int = -1):
+                 scatter: str = "partials", bricks: int = -1, compress_geometry: bool = True):
         lib = _par_lib()
         self.part = part
         self._keep = []
@@ -595,6 +609,7 @@ class ParBilinearForm:
         _check(lib.ecm2_par_form_set_kernel(h, kernel))
         _check(lib.ecm2_par_form_set_scatter(h, _SCATTER[scatter]))
         _check(lib.ecm2_par_form_set_bricks(h, bricks))
+        _check(lib.ecm2_par_form_set_geometry_compression(h, 1 if compress_geometry else 0))
         self.true_size = part.n_owned
 
     def __del__(self):
@@ -644,10 +659,16 @@ class ParBilinearForm:
         _check(_par_lib().ecm2_par_form_algorithmic_bytes(self._h, ctypes.byref(b)))
         return b.value
 
+    def qdata_bytes(self) -> float:
+        b = ctypes.c_double()
+        _check(_par_lib().ecm2_par_form_qdata_bytes(self._h, ctypes.byref(b)))
+        return b.value
+
     def info(self) -> dict:
-        n, k = ctypes.c_int(), ctypes.c_int()
+        n, k, lay = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         _check(_par_lib().ecm2_par_form_info(self._h, ctypes.byref(n), ctypes.byref(k)))
-        return {"n_true": n.value, "kernel": k.value}
+        _check(_par_lib().ecm2_par_form_layout(self._h, ctypes.byref(lay)))
+        return {"n_true": n.value, "kernel": k.value, "layout": lay.value}
 
 
 class ParGroup:

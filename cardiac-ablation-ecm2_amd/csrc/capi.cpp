@@ -333,6 +333,11 @@ int ecm2_pa_form_set_scatter(ecm2_pa_form *f, int mode)
    return guard([&] { NEED(f); f->f->set_scatter(mode); });
 }
 
+int ecm2_pa_form_set_geometry_compression(ecm2_pa_form *f, int on)
+{
+   return guard([&] { NEED(f); f->f->set_geometry_compression(on != 0); });
+}
+
 int ecm2_pa_form_set_bricks(ecm2_pa_form *f, int bz)
 {
    return guard([&] { NEED(f); f->f->set_line_bricks(bz); });
@@ -422,6 +427,11 @@ int ecm2_pa_form_timing_get(ecm2_pa_form *f, double *total_ms, long *launches)
 int ecm2_pa_form_algorithmic_bytes(const ecm2_pa_form *f, double *bytes)
 {
    return guard([&] { NEED(f); NEED(bytes); *bytes = (double)f->f->algorithmic_bytes(); });
+}
+
+int ecm2_pa_form_qdata_bytes(const ecm2_pa_form *f, double *bytes)
+{
+   return guard([&] { NEED(f); NEED(bytes); *bytes = (double)f->f->qdata_bytes(); });
 }
 
 void ecm2_pa_form_destroy(ecm2_pa_form *f)
@@ -542,6 +552,11 @@ int ecm2_par_form_set_bricks(ecm2_par_form *f, int bz)
 int ecm2_par_form_set_scatter(ecm2_par_form *f, int mode)
 {
    return guard([&] { NEED(f); f->f->local().set_scatter(mode); });
+}
+
+int ecm2_par_form_set_geometry_compression(ecm2_par_form *f, int on)
+{
+   return guard([&] { NEED(f); f->f->local().set_geometry_compression(on != 0); });
 }
 
 int ecm2_par_form_set_kernel(ecm2_par_form *f, int kernel)
@@ -705,6 +720,16 @@ int ecm2_par_form_algorithmic_bytes(const ecm2_par_form *f, double *bytes)
       // local subdomain: interface dofs counted once per owner copy
       *bytes = (double)f->f->local().algorithmic_bytes();
    });
+}
+
+int ecm2_par_form_qdata_bytes(const ecm2_par_form *f, double *bytes)
+{
+   return guard([&] { NEED(f); NEED(bytes); *bytes = (double)f->f->local().qdata_bytes(); });
+}
+
+int ecm2_par_form_layout(const ecm2_par_form *f, int *layout)
+{
+   return guard([&] { NEED(f); NEED(layout); *layout = f->f->local().layout(); });
 }
 
 int ecm2_par_form_info(const ecm2_par_form *f, int *n_true, int *kernel)

@@ -9,6 +9,15 @@
 //    symmetric entries (11,12),(13,22),(23,33); mass: [blk][q/2][lane][2] (two
 //    consecutive quadrature points per 16-byte slot).  Every wave-instruction
 //    is one 1 KiB contiguous dwordx4 load.
+//  * AFFINE (fused thread-per-element kernel on meshes whose elements are all
+//    parallelepipeds, with both integrators present): the same 64-element blocks, but
+//    the geometry is stored once per element.  For an affine element J is constant, so
+//    the reference's D(q) = W_q beta_q adj(J) adj(J)^T / det J factors into a per-point
+//    scalar W_q beta_q times a per-element symmetric matrix C = adj(J) adj(J)^T / det J.
+//    qd_diff holds C: [blk][pair 0..2][lane][2] (pairs (11,12),(13,22),(23,33));
+//    qd_mass holds the per-point pair [blk][q][lane][2] = (W_q beta_q, W_q alpha_q det J).
+//    16 B per quadrature point + 48 B per element instead of 56 B per point (3.3x fewer
+//    qdata bytes at p = 2); the values are the reference's up to rounding.
 //  * NATIVE (the reference's own layout): diffusion D(q,s,e) = [e][6][NQ],
 //    mass v(q,e) = [e][NQ] (bilininteg_diffusion_kernels.cpp:356-361,
 //    bilininteg_mass_pa.cpp:66-77).
@@ -20,7 +29,7 @@
 namespace ecm2
 {
 
-enum QLayoutKind : int { QLAYOUT_NATIVE = 0, QLAYOUT_BLOCKED = 1 };
+enum QLayoutKind : int { QLAYOUT_NATIVE = 0, QLAYOUT_BLOCKED = 1, QLAYOUT_AFFINE = 2 };
 
 constexpr int kElemBlock = 64;  // elements per wave in the blocked layout
 
@@ -33,11 +42,13 @@ struct QLayout
    size_t diff_size() const
    {
       if (kind == QLAYOUT_NATIVE) { return (size_t)ne * 6 * nq; }
+      if (kind == QLAYOUT_AFFINE) { return (size_t)nblk() * 6 * kElemBlock; }
       return (size_t)nblk() * nq * 6 * kElemBlock;
    }
    size_t mass_size() const
    {
       if (kind == QLAYOUT_NATIVE) { return (size_t)ne * nq; }
+      if (kind == QLAYOUT_AFFINE) { return (size_t)nblk() * nq * 2 * kElemBlock; }
       return (size_t)nblk() * ((nq + 1) / 2) * 2 * kElemBlock;
    }
    int nblk() const { return (ne + kElemBlock - 1) / kElemBlock; }
@@ -116,6 +127,11 @@ void setup_from_nodes(const QLayout &L, int Q, const double *enodes, const doubl
                       const Basis1D &b1, const CoeffDesc *cm, const CoeffDesc *cd,
                       const double *cm_q, const double *cd_q,
                       double *qd_diff, double *qd_mass, hipStream_t s);
+// AFFINE layout (see above) from the corners of parallelepiped elements; needs both
+// coefficients (cm, cd non-null).
+void setup_affine(const QLayout &L, int Q, const double *enodes, const double *W, const CoeffDesc *cm,
+                  const CoeffDesc *cd, const double *cm_q, const double *cd_q, double *qd_fac,
+                  double *qd_pair, hipStream_t s);
 // qdata from MFEM-layout Jacobians J(q,i,j,e) (GeometricFactors::JACOBIANS).
 void setup_from_jacobians(const QLayout &L, const double *J, const double *W,
                           const CoeffDesc *cm, const CoeffDesc *cd,

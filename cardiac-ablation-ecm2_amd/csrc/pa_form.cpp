@@ -54,11 +54,35 @@ PAForm::~PAForm()
    for (auto &e : ev_stop_) { (void)hipEventDestroy(e); }
 }
 
+// Every element a parallelepiped: the trilinear map's bilinear and trilinear terms vanish
+// (to 1e-13 of the element's edge length, i.e. below the operator's 1e-12 parity bar), so
+// its Jacobian is constant.  Terms are differences of edge vectors (exact for lattices).
+static bool all_affine(int ne, const double *X)
+{
+   for (int e = 0; e < ne; e++)
+   {
+      const double *p = X + (size_t)e * 24;
+      double h = 0.0, dev = 0.0;
+      for (int i = 0; i < 3; i++)
+      {
+         const double *c = p + i * 8;  // corner a = ax + 2 ay + 4 az
+         const double ex = c[1] - c[0], ey = c[2] - c[0], ez = c[4] - c[0];
+         h = std::max({h, std::fabs(ex), std::fabs(ey), std::fabs(ez)});
+         dev = std::max({dev, std::fabs((c[3] - c[2]) - ex), std::fabs((c[5] - c[4]) - ex),
+                         std::fabs((c[6] - c[4]) - ey), std::fabs((c[7] - c[6]) - ex),
+                         std::fabs((c[7] - c[5]) - ey), std::fabs((c[7] - c[3]) - ez)});
+      }
+      if (!(dev <= 1e-13 * h)) { return false; }
+   }
+   return true;
+}
+
 void PAForm::set_element_nodes(const double *enodes_host)
 {
    ECM2_VERIFY(ne_ == 0 || enodes_host, ERR_ARG, "null element nodes");
    enodes_.upload(enodes_host, (size_t)ne_ * 24);
    ECM2_HIP(hipDeviceSynchronize());
+   affine_ = all_affine(ne_, enodes_host);
    jac_ = nullptr;
    assembled_ = false;
 }
@@ -67,7 +91,24 @@ void PAForm::set_jacobians(const double *J_device)
 {
    ECM2_VERIFY(ne_ == 0 || J_device, ERR_ARG, "null Jacobian array");
    jac_ = J_device;
+   affine_ = false;
    assembled_ = false;
+}
+
+void PAForm::set_geometry_compression(bool on)
+{
+   compress_ = on;
+   assembled_ = false;
+}
+
+// experiment knob ECM2_AFFINE=0: never use the AFFINE qdata layout
+static bool affine_env()
+{
+   static const bool v = [] {
+      const char *e = std::getenv("ECM2_AFFINE");
+      return !(e && std::string(e) == "0");
+   }();
+   return v;
 }
 
 void PAForm::set_block_splits(const std::vector<int> &splits)
@@ -290,6 +331,10 @@ void PAForm::assemble(hipStream_t s)
    ECM2_VERIFY(resolved_mode_ != KERNEL_LINE || kern::has_line(D_, Q_), ERR_UNSUPPORTED,
                "line kernel needs Q1D in {D1D, D1D+1} and Q1D <= 8");
    layout_.kind = (resolved_mode_ == KERNEL_TPE) ? QLAYOUT_BLOCKED : QLAYOUT_NATIVE;
+   if (layout_.kind == QLAYOUT_BLOCKED && affine_ && compress_ && affine_env() && !jac_ && have_mass_ && have_diff_)
+   {
+      layout_.kind = QLAYOUT_AFFINE;
+   }
 
    if (resolved_mode_ == KERNEL_TPE && !gmap_blk_.size() && ne_ > 0)
    {
@@ -517,8 +562,8 @@ void PAForm::assemble(hipStream_t s)
       n_left_ = n_left;
       ECM2_HIP(hipStreamSynchronize(s));
    }
-   layout_.pos = (layout_.kind == QLAYOUT_BLOCKED) ? pos_.data() : nullptr;
-   layout_.perm = (layout_.kind == QLAYOUT_BLOCKED) ? perm_dev_.data() : nullptr;
+   layout_.pos = (layout_.kind != QLAYOUT_NATIVE) ? pos_.data() : nullptr;
+   layout_.perm = (layout_.kind != QLAYOUT_NATIVE) ? perm_dev_.data() : nullptr;
    if (!use_partials()) { part_.resize(0); }
    else if (resolved_mode_ == KERNEL_LINE)
    {
@@ -530,7 +575,7 @@ void PAForm::assemble(hipStream_t s)
    qd_mass_.resize(have_mass_ ? layout_.mass_size() : 0);
    // the setup kernels write every entry except the padding lanes of a partial last block
    // (blocked layout), which are cleared so the apply kernels stream defined values
-   if (layout_.kind == QLAYOUT_BLOCKED && ne_ % kElemBlock)
+   if (layout_.kind != QLAYOUT_NATIVE && ne_ % kElemBlock)
    {
       const size_t nb = layout_.nblk();
       if (qd_diff_.size())
@@ -560,7 +605,12 @@ void PAForm::assemble(hipStream_t s)
    const double *cd_q = have_diff_ ? coeff_values(cdiff_, ctmp_d_) : nullptr;
    const CoeffDesc *cm = have_mass_ ? &cmass_ : nullptr;
    const CoeffDesc *cd = have_diff_ ? &cdiff_ : nullptr;
-   if (jac_)
+   if (layout_.kind == QLAYOUT_AFFINE)
+   {
+      kern::setup_affine(layout_, Q_, enodes_.data(), W_.data(), cm, cd, cm_q, cd_q, qd_diff_.data(),
+                         qd_mass_.data(), s);
+   }
+   else if (jac_)
    {
       kern::setup_from_jacobians(layout_, jac_, W_.data(), cm, cd, cm_q, cd_q, qd_diff_.data(),
                                  qd_mass_.data(), s);
@@ -811,13 +861,18 @@ void PAForm::get_qdata(int kind, double *out, hipStream_t s)
    ECM2_VERIFY(assembled_, ERR_STATE, "get_qdata before Assemble");
    const bool diff = kind == INTEG_DIFFUSION;
    ECM2_VERIFY(diff ? have_diff_ : have_mass_, ERR_ARG, "integrator " << kind << " not present");
-   DeviceArray<double> &src = diff ? qd_diff_ : qd_mass_;
-   std::vector<double> h(src.size());
+   const bool aff = layout_.kind == QLAYOUT_AFFINE;
+   DeviceArray<double> &src = (diff && !aff) ? qd_diff_ : qd_mass_;
+   std::vector<double> h(src.size()), hc(aff ? qd_diff_.size() : 0);
    if (src.size())
    {
       ECM2_HIP(hipMemcpyAsync(h.data(), src.data(), src.bytes(), hipMemcpyDeviceToHost, s));
-      ECM2_HIP(hipStreamSynchronize(s));
    }
+   if (hc.size())
+   {
+      ECM2_HIP(hipMemcpyAsync(hc.data(), qd_diff_.data(), qd_diff_.bytes(), hipMemcpyDeviceToHost, s));
+   }
+   ECM2_HIP(hipStreamSynchronize(s));
    const int nc = diff ? 6 : 1;
    std::vector<int> invp;
    if (!perm_host_.empty())
@@ -836,6 +891,14 @@ void PAForm::get_qdata(int kind, double *out, hipStream_t s)
             {
                const int ip = perm_host_.empty() ? e : inv_perm(e);
                const int blk = ip / 64, lane = ip % 64;
+               if (aff)
+               {
+                  // AFFINE: D_c(q) = (W beta)(q) * C_c, mass = the pair's second entry
+                  const size_t pi = (((size_t)blk * NQ_ + q) * 64 + lane) * 2;
+                  out[((size_t)e * nc + c) * NQ_ + q] =
+                     diff ? h[pi] * hc[(((size_t)blk * 3 + c / 2) * 64 + lane) * 2 + (c & 1)] : h[pi + 1];
+                  continue;
+               }
                if (diff) { src_i = (((size_t)blk * NQ_ + q) * 3 + c / 2) * 128 + lane * 2 + (c & 1); }
                else { src_i = ((size_t)blk * ((NQ_ + 1) / 2) + q / 2) * 128 + lane * 2 + (q & 1); }
             }

@@ -63,6 +63,12 @@ public:
    // valid until assemble()).
    void set_element_nodes(const double *enodes_host);
    void set_jacobians(const double *J_device);
+   // AFFINE qdata (kernels.hpp) for the fused p <= 2 kernel when every element is a
+   // parallelepiped (checked on the corners) and both integrators are present: on by default.
+   void set_geometry_compression(bool on);
+   bool affine_geometry() const { return affine_; }
+   // bytes of quadrature data the form stores (diffusion + mass)
+   size_t qdata_bytes() const { return qd_diff_.bytes() + qd_mass_.bytes(); }
 
    // Optional element permutation (internal position i <- caller element perm[i]) used by
    // the blocked layout; ORDER_BRICK puts one 4x4x4 brick in each 64-lane wave so the
@@ -164,6 +170,8 @@ private:
    long part_line_off_ = 0;         // LINE: leftover elements' partial slots start here
    int n_left_ = 0;                 // LINE: elements outside bricks
    int line_bricks_ = -1;           // requested brick mode (set_line_bricks)
+   bool affine_ = false;            // every element a parallelepiped (set_element_nodes)
+   bool compress_ = true;           // set_geometry_compression
    bool auto_order_ = true;         // TPE without a caller order: face-linked 4x4x4 bricks
    bool perm_auto_ = false;         // perm_host_ was derived (not the caller's)
    DeviceArray<int> lane_flags_;    // [blk][64] in-wave merge flags

@@ -56,6 +56,30 @@ __device__ __forceinline__ size_t qidx_mass(const int *pos, int kind, int nq, in
    return ((size_t)blk * nqh + (q >> 1)) * 128 + lane * 2 + (q & 1);
 }
 
+// Value of diffusion entry c / mass at (e, q) in any layout; AFFINE recombines the
+// per-point scalar W beta (qdm pair .x) with the element matrix C (qdd), and stores the mass
+// value as the pair's .y.
+__device__ __forceinline__ size_t affine_pair(const int *pos, int nq, int e, int q)
+{
+   if (pos) { e = pos[e]; }
+   return (((size_t)(e >> 6) * nq + q) * 64 + (e & 63)) * 2;
+}
+__device__ __forceinline__ double qd_diff_at(const double *qdd, const double *qdm, const int *pos, int kind,
+                                             int nq, int e, int c, int q)
+{
+   if (kind == QLAYOUT_AFFINE)
+   {
+      const int ie = pos ? pos[e] : e;
+      return qdm[affine_pair(nullptr, nq, ie, q)] * qdd[(((size_t)(ie >> 6) * 3 + (c >> 1)) * 64 + (ie & 63)) * 2 + (c & 1)];
+   }
+   return qdd[qidx_diff(pos, kind, nq, e, c, q)];
+}
+__device__ __forceinline__ double qd_mass_at(const double *qdm, const int *pos, int kind, int nq, int e, int q)
+{
+   if (kind == QLAYOUT_AFFINE) { return qdm[affine_pair(pos, nq, e, q) + 1]; }
+   return qdm[qidx_mass(pos, kind, nq, e, q)];
+}
+
 __device__ __forceinline__ int dof_of(int g) { return g >= 0 ? g : -1 - g; }
 
 // Blocked (fused-kernel) map entries: bits 0-29 dof, bit 30 "shared" (the dof is held by
@@ -275,6 +299,74 @@ __global__ void k_setup_jac(const int *__restrict__ pos, int kind, int ne, int N
    for (int j = 0; j < 3; j++)
       for (int i = 0; i < 3; i++) { J[i][j] = Jg[(((size_t)e * 3 + j) * 3 + i) * NQ + q]; }
    write_qdata(pos, kind, NQ, e, q, W[q], J, cm, cd, qd_diff, qd_mass);
+}
+
+// AFFINE layout from the corners of parallelepiped elements (kernels.hpp).  J is the
+// reference-cube edge matrix [x_100 - x_000 | x_010 - x_000 | x_001 - x_000] (the trilinear
+// Jacobian of GeometricFactors, mesh.cpp:15220-15273, when the element is affine); the
+// products are PADiffusionSetup3D's (bilininteg_diffusion_kernels.cpp:349-362) and the mass
+// setup's (bilininteg_mass_pa.cpp:76) with the per-point factors W_q beta_q / W_q alpha_q kept
+// apart from the element's C = adj(J) adj(J)^T / det J.  Threads over (blk, q, lane), lane
+// fastest: each wave stores 1 KiB of pairs per point; the q = 0 threads store C.
+template <int Q>
+__global__ void __launch_bounds__(256)
+k_setup_affine(const int *__restrict__ perm, int ne, const double *__restrict__ enodes,
+               const double *__restrict__ W, SetupCoef cm, SetupCoef cd, double *__restrict__ qd_fac,
+               double *__restrict__ qd_pair)
+{
+   constexpr int NQ = Q * Q * Q;
+   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   const int lane = (int)(t & 63);
+   const long rest = t >> 6;
+   const int q = (int)(rest % NQ);
+   const long blk = rest / NQ;
+   const int ipos = (int)(blk * 64 + lane);
+   if (ipos >= ne) { return; }
+   const int e = perm ? perm[ipos] : ipos;
+   const double *X = enodes + (size_t)e * 24;
+   double J[3][3];
+#pragma unroll
+   for (int i = 0; i < 3; i++)
+   {
+      J[i][0] = X[i * 8 + 1] - X[i * 8];
+      J[i][1] = X[i * 8 + 2] - X[i * 8];
+      J[i][2] = X[i * 8 + 4] - X[i * 8];
+   }
+   const double J11 = J[0][0], J21 = J[1][0], J31 = J[2][0];
+   const double J12 = J[0][1], J22 = J[1][1], J32 = J[2][1];
+   const double J13 = J[0][2], J23 = J[1][2], J33 = J[2][2];
+   const double detJ = J11 * (J22 * J33 - J32 * J23) - J21 * (J12 * J33 - J32 * J13) +
+                       J31 * (J12 * J23 - J22 * J13);
+   const size_t eq = (size_t)e * NQ + q;
+   const double w = W[q];
+   v2d pr;
+   pr.x = w * coef_at(cd, eq);
+   pr.y = w * coef_at(cm, eq) * detJ;
+   reinterpret_cast<v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane] = pr;
+   if (q == 0)
+   {
+      const double A11 = (J22 * J33) - (J23 * J32);
+      const double A12 = (J32 * J13) - (J12 * J33);
+      const double A13 = (J12 * J23) - (J22 * J13);
+      const double A21 = (J31 * J23) - (J21 * J33);
+      const double A22 = (J11 * J33) - (J13 * J31);
+      const double A23 = (J21 * J13) - (J11 * J23);
+      const double A31 = (J21 * J32) - (J31 * J22);
+      const double A32 = (J31 * J12) - (J11 * J32);
+      const double A33 = (J11 * J22) - (J12 * J21);
+      const double r = 1.0 / detJ;
+      v2d p0, p1, p2;
+      p0.x = r * (A11 * A11 + A12 * A12 + A13 * A13);
+      p0.y = r * (A11 * A21 + A12 * A22 + A13 * A23);
+      p1.x = r * (A11 * A31 + A12 * A32 + A13 * A33);
+      p1.y = r * (A21 * A21 + A22 * A22 + A23 * A23);
+      p2.x = r * (A21 * A31 + A22 * A32 + A23 * A33);
+      p2.y = r * (A31 * A31 + A32 * A32 + A33 * A33);
+      v2d *dst = reinterpret_cast<v2d *>(qd_fac + (size_t)blk * 3 * 128) + lane;
+      dst[0] = p0;
+      dst[64] = p1;
+      dst[128] = p2;
+   }
 }
 
 // --------------------------------------------------------------------------
@@ -517,7 +609,9 @@ __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], cons
          }
 }
 
-template <int D, int Q, bool MASS, bool DIFF, bool SPLIT, int VAR>
+// AFF: AFFINE qdata (kernels.hpp): the element's C is loaded once, each quadrature point
+// streams one 16-byte pair (W beta, W alpha det J) instead of four loads of 56 bytes.
+template <int D, int Q, bool MASS, bool DIFF, bool SPLIT, int VAR, bool AFF = false>
 __global__ void __launch_bounds__(256, (VAR & 8) ? 2 : 1)
 k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
                const double *__restrict__ qdd, const double *__restrict__ qdm,
@@ -554,14 +648,28 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
       if (VAR & 2) { return *reinterpret_cast<const v2d *>(p); }
       return __builtin_nontemporal_load(reinterpret_cast<const v2d *>(p));
    };
-   // row buffers: diffusion pairs (3 per point) and mass values (Q per row)
+   // row buffers: diffusion pairs (3 per point) and mass values (Q per row); AFF: one
+   // (W beta, W alpha det J) pair per point and the element's C in registers
    v2d cd[Q][3], nd_[Q][3];
    double cm[Q], nm[Q];
-   auto load_row = [&](int row, v2d (&dq)[Q][3], double (&mq)[Q]) {
+   v2d ca[Q], na[Q], ce[3];
+   const double *qa = qdm + (size_t)blk * NQ * 128 + lane * 2;
+   if (AFF)
+   {
+      const double *qc = qdd + (size_t)blk * 3 * 128 + lane * 2;
+#pragma unroll
+      for (int k = 0; k < 3; k++) { ce[k] = ld2(qc + k * 128); }
+   }
+   auto load_row = [&](int row, v2d (&dq)[Q][3], double (&mq)[Q], v2d (&aq)[Q]) {
 #pragma unroll
       for (int qx = 0; qx < Q; qx++)
       {
          const int q = row * Q + qx;
+         if (AFF)
+         {
+            aq[qx] = ld2(qa + (size_t)q * 128);
+            continue;
+         }
          if (DIFF)
          {
 #pragma unroll
@@ -570,12 +678,12 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
          if (MASS) { mq[qx] = qm[(size_t)(q >> 1) * 128 + (q & 1)]; }
       }
    };
-   load_row(0, cd, cm);
+   load_row(0, cd, cm, ca);
 
 #pragma unroll 1
    for (int row = 0; row < NR; row++)
    {
-      if (row + 1 < NR) { load_row(row + 1, nd_, nm); }
+      if (row + 1 < NR) { load_row(row + 1, nd_, nm, na); }
       const double *P = rowtab + (size_t)row * 3 * DD;
       double Y00[D], Y01[D], Y10[D];
 #pragma unroll
@@ -617,6 +725,16 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
             }
          }
          double m = 0.0, fx = 0.0, fy = 0.0, fz = 0.0;
+         if (AFF)
+         {
+            const v2d sa = ca[qx];
+            m = sa.y * u;
+            fx = sa.x * (ce[0].x * ux + ce[0].y * uy + ce[1].x * uz);
+            fy = sa.x * (ce[0].y * ux + ce[1].y * uy + ce[2].x * uz);
+            fz = sa.x * (ce[1].x * ux + ce[2].x * uy + ce[2].y * uz);
+         }
+         else
+         {
          if (MASS) { m = cm[qx] * u; }
          if (DIFF)
          {
@@ -624,6 +742,7 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
             fx = d0.x * ux + d0.y * uy + d1.x * uz;
             fy = d0.y * ux + d1.y * uy + d2.x * uz;
             fz = d1.x * ux + d2.x * uy + d2.y * uz;
+         }
          }
 #pragma unroll
          for (int dx = 0; dx < D; dx++)
@@ -662,6 +781,7 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 #pragma unroll
          for (int k = 0; k < 3; k++) { cd[qx][k] = nd_[qx][k]; }
          cm[qx] = nm[qx];
+         ca[qx] = na[qx];
       }
    }
    tpe_assemble_store<D, SPLIT, true, (VAR & 1) != 0>(Yo, mp, lane_flags[(size_t)blk * 64 + lane], blk, lane, active,
@@ -677,7 +797,7 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 // (Gy Bz)^2, (By Gz)^2, Gy By Bz^2, By^2 Gz Bz, Gy By Gz Bz.  Output assembled and stored
 // exactly like k_apply_tpe_pf's (in-wave faces, plain stores, partial slots): every
 // diagonal entry written once, deterministic, no memset.
-template <int D, int Q, bool MASS, bool DIFF, bool SPLIT>
+template <int D, int Q, bool MASS, bool DIFF, bool SPLIT, bool AFF = false>
 __global__ void __launch_bounds__(256)
 k_diag_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
            const double *__restrict__ qdd, const double *__restrict__ qdm, double *__restrict__ y,
@@ -692,6 +812,13 @@ k_diag_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restric
    const int *mp = gmap + (size_t)blk * ND * 64 + lane;
    const double *qd = qdd + (size_t)blk * NQ * 3 * 128 + lane * 2;
    const double *qm = qdm + (size_t)blk * NQH * 128 + lane * 2;
+   const double *qa = qdm + (size_t)blk * NQ * 128 + lane * 2;  // AFF pairs
+   v2d ce[3];
+   if (AFF)
+   {
+#pragma unroll
+      for (int k = 0; k < 3; k++) { ce[k] = *reinterpret_cast<const v2d *>(qdd + (size_t)blk * 3 * 128 + lane * 2 + k * 128); }
+   }
    double Yo[ND];
 #pragma unroll
    for (int a = 0; a < ND; a++) { Yo[a] = 0.0; }
@@ -708,13 +835,25 @@ k_diag_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restric
       {
          const int q = row * Q + qx;
          v2d d0 = {0.0, 0.0}, d1 = {0.0, 0.0}, d2 = {0.0, 0.0};
+         double m = 0.0;
+         if (AFF)
+         {
+            const v2d sa = *reinterpret_cast<const v2d *>(qa + (size_t)q * 128);
+            d0 = sa.x * ce[0];
+            d1 = sa.x * ce[1];
+            d2 = sa.x * ce[2];
+            m = sa.y;
+         }
+         else
+         {
          if (DIFF)
          {
             d0 = *reinterpret_cast<const v2d *>(qd + ((size_t)q * 3 + 0) * 128);
             d1 = *reinterpret_cast<const v2d *>(qd + ((size_t)q * 3 + 1) * 128);
             d2 = *reinterpret_cast<const v2d *>(qd + ((size_t)q * 3 + 2) * 128);
          }
-         const double m = MASS ? qm[(size_t)(q >> 1) * 128 + (q & 1)] : 0.0;
+         if (MASS) { m = qm[(size_t)(q >> 1) * 128 + (q & 1)]; }
+         }
 #pragma unroll
          for (int dx = 0; dx < D; dx++)
          {
@@ -772,11 +911,11 @@ __global__ void k_apply_wpe(const int *__restrict__ pos, int kind, int ne, int e
    if ((var & 2) && threadIdx.x < NQ)
    {
       const int e = e_begin + blockIdx.x, t = threadIdx.x;
-      if (MASS) { pq[6] = qdm[qidx_mass(pos, kind, NQ, e, t)]; }
+      if (MASS) { pq[6] = qd_mass_at(qdm, pos, kind, NQ, e, t); }
       if (DIFF)
       {
 #pragma unroll
-         for (int c = 0; c < 6; c++) { pq[c] = qdd[qidx_diff(pos, kind, NQ, e, c, t)]; }
+         for (int c = 0; c < 6; c++) { pq[c] = qd_diff_at(qdd, qdm, pos, kind, NQ, e, c, t); }
       }
    }
    __shared__ double sB[Q * D], sG[Q * D];
@@ -862,15 +1001,15 @@ __global__ void k_apply_wpe(const int *__restrict__ pos, int kind, int ne, int e
       }
       else
       {
-      if (MASS) { m = qdm[qidx_mass(pos, kind, NQ, e, t)] * u; }
+      if (MASS) { m = qd_mass_at(qdm, pos, kind, NQ, e, t) * u; }
       if (DIFF)
       {
-         const double O11 = qdd[qidx_diff(pos, kind, NQ, e, 0, t)];
-         const double O12 = qdd[qidx_diff(pos, kind, NQ, e, 1, t)];
-         const double O13 = qdd[qidx_diff(pos, kind, NQ, e, 2, t)];
-         const double O22 = qdd[qidx_diff(pos, kind, NQ, e, 3, t)];
-         const double O23 = qdd[qidx_diff(pos, kind, NQ, e, 4, t)];
-         const double O33 = qdd[qidx_diff(pos, kind, NQ, e, 5, t)];
+         const double O11 = qd_diff_at(qdd, qdm, pos, kind, NQ, e, 0, t);
+         const double O12 = qd_diff_at(qdd, qdm, pos, kind, NQ, e, 1, t);
+         const double O13 = qd_diff_at(qdd, qdm, pos, kind, NQ, e, 2, t);
+         const double O22 = qd_diff_at(qdd, qdm, pos, kind, NQ, e, 3, t);
+         const double O23 = qd_diff_at(qdd, qdm, pos, kind, NQ, e, 4, t);
+         const double O33 = qd_diff_at(qdd, qdm, pos, kind, NQ, e, 5, t);
          fx = (O11 * gx) + (O12 * gy) + (O13 * gz);
          fy = (O12 * gx) + (O22 * gy) + (O23 * gz);
          fz = (O13 * gx) + (O23 * gy) + (O33 * gz);
@@ -1033,9 +1172,9 @@ k_diag_sf(const int *__restrict__ pos, int kind, int ne, const int *__restrict__
 #pragma unroll
          for (int k = 0; k < 6; k++)
          {
-            O[k] = qdd ? qdd[qidx_diff(pos, kind, NQ, e, src[k], q)] * (k >= 3 ? 2.0 : 1.0) : 0.0;
+            O[k] = qdd ? qd_diff_at(qdd, qdm, pos, kind, NQ, e, src[k], q) * (k >= 3 ? 2.0 : 1.0) : 0.0;
          }
-         O[6] = qdm ? qdm[qidx_mass(pos, kind, NQ, e, q)] : 0.0;
+         O[6] = qdm ? qd_mass_at(qdm, pos, kind, NQ, e, q) : 0.0;
 #pragma unroll
          for (int k = 0; k < 7; k++)
 #pragma unroll
@@ -1739,16 +1878,16 @@ __global__ void k_diagonal(const int *__restrict__ pos, int D, int Q, int kind, 
             const int q = (qz * Q + qy) * Q + qx;
             const double bx = b.B[qx + MQ * dx], by = b.B[qy + MQ * dy], bz = b.B[qz + MQ * dz];
             const double gx = b.G[qx + MQ * dx], gy = b.G[qy + MQ * dy], gz = b.G[qz + MQ * dz];
-            if (qdm) { s += bx * bx * by * by * bz * bz * qdm[qidx_mass(pos, kind, NQ, e, q)]; }
+            if (qdm) { s += bx * bx * by * by * bz * bz * qd_mass_at(qdm, pos, kind, NQ, e, q); }
             if (qdd)
             {
                const double p0 = gx * by * bz, p1 = bx * gy * bz, p2 = bx * by * gz;
-               s += p0 * p0 * qdd[qidx_diff(pos, kind, NQ, e, 0, q)] +
-                    p1 * p1 * qdd[qidx_diff(pos, kind, NQ, e, 3, q)] +
-                    p2 * p2 * qdd[qidx_diff(pos, kind, NQ, e, 5, q)] +
-                    2.0 * (p0 * p1 * qdd[qidx_diff(pos, kind, NQ, e, 1, q)] +
-                           p0 * p2 * qdd[qidx_diff(pos, kind, NQ, e, 2, q)] +
-                           p1 * p2 * qdd[qidx_diff(pos, kind, NQ, e, 4, q)]);
+               s += p0 * p0 * qd_diff_at(qdd, qdm, pos, kind, NQ, e, 0, q) +
+                    p1 * p1 * qd_diff_at(qdd, qdm, pos, kind, NQ, e, 3, q) +
+                    p2 * p2 * qd_diff_at(qdd, qdm, pos, kind, NQ, e, 5, q) +
+                    2.0 * (p0 * p1 * qd_diff_at(qdd, qdm, pos, kind, NQ, e, 1, q) +
+                           p0 * p2 * qd_diff_at(qdd, qdm, pos, kind, NQ, e, 2, q) +
+                           p1 * p2 * qd_diff_at(qdd, qdm, pos, kind, NQ, e, 4, q));
             }
          }
    if (out_e) { diag[t] += s; }
@@ -1987,10 +2126,34 @@ void launch_tpe_pf(int var, const ApplyArgs &a, const Basis1D &b, const double *
 {
    const int nb = a.blk_end - a.blk_begin;
    const dim3 grid((nb + 3) / 4), block(256);
-#define ECM2_PF(V)                                                                                   \
-   hipLaunchKernelGGL((k_apply_tpe_pf<D, Q, MASS, DIFF, SPLIT, V>), grid, block, 0, s, a.ne,        \
+#define ECM2_PF_AF(V, AF)                                                                            \
+   hipLaunchKernelGGL((k_apply_tpe_pf<D, Q, MASS, DIFF, SPLIT, V, AF>), grid, block, 0, s, a.ne,    \
                       a.blk_begin, a.blk_end, a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, rowtab, \
                       a.lane_flags, a.part)
+#define ECM2_PF(V) ECM2_PF_AF(V, false)
+   if (a.kind == QLAYOUT_AFFINE)
+   {
+      if constexpr (MASS && DIFF)
+      {
+         // experiment knob bits: 2 = cached qdata loads, 8 = two waves per SIMD, 16 = XCD order
+         switch (var & 26)
+         {
+            case 2: ECM2_PF_AF(2, true); break;
+            case 8: ECM2_PF_AF(8, true); break;
+            case 16: ECM2_PF_AF(16, true); break;
+            default: ECM2_PF_AF(0, true); break;
+         }
+      }
+      else { ECM2_VERIFY(false, ERR_INTERNAL, "AFFINE qdata needs both integrators"); }
+#undef ECM2_PF
+#undef ECM2_PF_AF
+      return;
+   }
+#define ECM2_PF_AF(V, AF)                                                                            \
+   hipLaunchKernelGGL((k_apply_tpe_pf<D, Q, MASS, DIFF, SPLIT, V, AF>), grid, block, 0, s, a.ne,    \
+                      a.blk_begin, a.blk_end, a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, rowtab, \
+                      a.lane_flags, a.part)
+#define ECM2_PF(V) ECM2_PF_AF(V, false)
    switch (var & 27)
    {
       case 0: ECM2_PF(0); break;
@@ -2004,6 +2167,7 @@ void launch_tpe_pf(int var, const ApplyArgs &a, const Basis1D &b, const double *
       default: ECM2_PF(0); break;
    }
 #undef ECM2_PF
+#undef ECM2_PF_AF
 }
 
 template <int D, int Q, bool MASS, bool DIFF>
@@ -2013,7 +2177,8 @@ void launch_tpe_mdq(const ApplyArgs &a, const Basis1D &b, const double *rowtab, 
    if (nb <= 0) { return; }
    const int var = tpe_variant();
    ECM2_VERIFY(!a.part || a.lane_flags, ERR_INTERNAL, "partial-slot output needs the merge plan");
-   if (((var & 4) || a.part) && a.lane_flags)
+   ECM2_VERIFY(a.kind != QLAYOUT_AFFINE || a.lane_flags, ERR_INTERNAL, "AFFINE qdata needs the pipelined kernel");
+   if (((var & 4) || a.part || a.kind == QLAYOUT_AFFINE) && a.lane_flags)
    {
       if (a.xg || a.yg) { launch_tpe_pf<D, Q, MASS, DIFF, true>(var, a, b, rowtab, s); }
       else { launch_tpe_pf<D, Q, MASS, DIFF, false>(var, a, b, rowtab, s); }
@@ -2142,6 +2307,29 @@ void setup_from_nodes(const QLayout &L, int Q, const double *enodes, const doubl
    hipLaunchKernelGGL(k_setup_nodes, dim3(grid_for(n, 256)), dim3(256), 0, s, L.pos, L.kind, L.ne, Q,
                       enodes, W, b1, scm, scd, qd_diff, qd_mass);
    ECM2_HIP(hipGetLastError());
+}
+
+void setup_affine(const QLayout &L, int Q, const double *enodes, const double *W, const CoeffDesc *cm,
+                  const CoeffDesc *cd, const double *cm_q, const double *cd_q, double *qd_fac,
+                  double *qd_pair, hipStream_t s)
+{
+   if (L.ne == 0) { return; }
+   ECM2_VERIFY(L.kind == QLAYOUT_AFFINE && cm && cd, ERR_INTERNAL, "affine setup needs the AFFINE layout and both coefficients");
+   ECM2_VERIFY(!L.pos || L.perm, ERR_INTERNAL, "blocked setup needs the inverse permutation");
+   const SetupCoef scm = make_setup_coef(cm, cm_q), scd = make_setup_coef(cd, cd_q);
+   const long n = (long)L.nblk() * 64 * L.nq;
+#define ECM2_AFF_CASE(QQ)                                                                               \
+   if (Q == QQ)                                                                                          \
+   {                                                                                                     \
+      hipLaunchKernelGGL((k_setup_affine<QQ>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.perm, L.ne, enodes, W, \
+                         scm, scd, qd_fac, qd_pair);                                                     \
+      ECM2_HIP(hipGetLastError());                                                                       \
+      return;                                                                                            \
+   }
+   ECM2_AFF_CASE(2) ECM2_AFF_CASE(3) ECM2_AFF_CASE(4) ECM2_AFF_CASE(5) ECM2_AFF_CASE(6) ECM2_AFF_CASE(7)
+   ECM2_AFF_CASE(8)
+#undef ECM2_AFF_CASE
+   ECM2_VERIFY(false, ERR_UNSUPPORTED, "affine setup: Q1D " << Q << " not instantiated");
 }
 
 void setup_from_jacobians(const QLayout &L, const double *J, const double *W,
@@ -2401,16 +2589,14 @@ static void launch_diag_tpe(const ApplyArgs &a, const Basis1D &b, const double *
    const int nb = a.blk_end - a.blk_begin;
    if (nb <= 0) { return; }
    const dim3 grid((nb + 3) / 4), block(256);
-   if (a.yg)
-   {
-      hipLaunchKernelGGL((k_diag_tpe<D, Q, MASS, DIFF, true>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end,
-                         a.n_owned, a.gmap, a.qdd, a.qdm, a.y, a.yg, b, drow, a.lane_flags, a.part);
-   }
-   else
-   {
-      hipLaunchKernelGGL((k_diag_tpe<D, Q, MASS, DIFF, false>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end,
-                         a.n_owned, a.gmap, a.qdd, a.qdm, a.y, a.yg, b, drow, a.lane_flags, a.part);
-   }
+#define ECM2_DIAG(SP, AF)                                                                               \
+   hipLaunchKernelGGL((k_diag_tpe<D, Q, MASS, DIFF, SP, AF>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end, \
+                      a.n_owned, a.gmap, a.qdd, a.qdm, a.y, a.yg, b, drow, a.lane_flags, a.part)
+   const bool aff = a.kind == QLAYOUT_AFFINE;
+   ECM2_VERIFY(!aff || (MASS && DIFF), ERR_INTERNAL, "AFFINE qdata needs both integrators");
+   if (a.yg) { if (aff) { ECM2_DIAG(true, true); } else { ECM2_DIAG(true, false); } }
+   else { if (aff) { ECM2_DIAG(false, true); } else { ECM2_DIAG(false, false); } }
+#undef ECM2_DIAG
 }
 
 template <int D, int Q>

@@ -123,6 +123,17 @@ int ecm2_pa_form_set_element_nodes(ecm2_pa_form *f, const double *enodes);
 /* Geometry from GeometricFactors::JACOBIANS (mesh.cpp:15242 layout NQ x 3 x 3 x NE),
  * device pointer, must stay valid until ecm2_pa_form_assemble returns. */
 int ecm2_pa_form_set_jacobians(ecm2_pa_form *f, const double *J);
+/* Quadrature-data layout (ecm2_pa_form_info's *layout).  AFFINE: when every element is
+ * a parallelepiped (checked on the corners given to set_element_nodes) and both
+ * integrators are present, the p <= 2 fused kernel stores the constant element geometry
+ * adj(J) adj(J)^T / det J once per element and one (W beta, W alpha det J) pair per
+ * quadrature point: the reference's pa_data values (bilininteg_diffusion_kernels.cpp:349-362,
+ * bilininteg_mass_pa.cpp:76) up to rounding, 3.3x fewer bytes at p = 2.  On by default;
+ * ecm2_pa_form_set_geometry_compression(f, 0) keeps the full per-point layout. */
+#define ECM2_QLAYOUT_NATIVE 0
+#define ECM2_QLAYOUT_BLOCKED 1
+#define ECM2_QLAYOUT_AFFINE 2
+int ecm2_pa_form_set_geometry_compression(ecm2_pa_form *f, int on);
 /* BilinearForm::AddDomainIntegrator(new MassIntegrator(Q)) / DiffusionIntegrator(Q)
  * (bilinearform.cpp:231-242).  data: CONSTANT -> data[0] (host);
  * QUAD -> device [ne][nq]; GRIDFUNC_AFFINE -> device L-vector T with
@@ -177,6 +188,8 @@ int ecm2_pa_form_timing(ecm2_pa_form *f, int enable);
 int ecm2_pa_form_timing_get(ecm2_pa_form *f, double *total_ms, long *launches);
 /* SURVEY §8(d) algorithmic bytes per Mult: 8*NE*NQ*(6+1) + 16*ndofs + 4*NE*ND. */
 int ecm2_pa_form_algorithmic_bytes(const ecm2_pa_form *f, double *bytes);
+/* Bytes of quadrature data the form stores after assemble (diffusion + mass). */
+int ecm2_pa_form_qdata_bytes(const ecm2_pa_form *f, double *bytes);
 /* ~PABilinearFormExtension / BilinearForm::Update (bilinearform_ext.hpp:67-144). */
 void ecm2_pa_form_destroy(ecm2_pa_form *f);
 
@@ -273,6 +286,8 @@ int ecm2_par_form_set_kernel(ecm2_par_form *f, int kernel);
 int ecm2_par_form_set_bricks(ecm2_par_form *f, int bz);
 /* Scatter mode of the local form (ECM2_SCATTER_*; see ecm2_pa_form_set_scatter). */
 int ecm2_par_form_set_scatter(ecm2_par_form *f, int mode);
+/* Geometry compression of the local form (see ecm2_pa_form_set_geometry_compression). */
+int ecm2_par_form_set_geometry_compression(ecm2_par_form *f, int on);
 /* ParBilinearForm::Assemble -> local PABilinearFormExtension::Assemble
  * (pbilinearform.cpp:475-511, bilinearform_ext.cpp:332-368). */
 int ecm2_par_form_assemble(ecm2_par_form *f, void *stream);
@@ -291,6 +306,9 @@ int ecm2_par_group_diagonal(ecm2_par_form *const *forms, int n, double *const *d
 int ecm2_par_form_timing(ecm2_par_form *f, int enable);
 int ecm2_par_form_timing_get(ecm2_par_form *f, double *total_ms, long *launches);
 int ecm2_par_form_algorithmic_bytes(const ecm2_par_form *f, double *bytes);
+int ecm2_par_form_qdata_bytes(const ecm2_par_form *f, double *bytes);
+/* Quadrature-data layout of the local form (ECM2_QLAYOUT_*), after assemble. */
+int ecm2_par_form_layout(const ecm2_par_form *f, int *layout);
 int ecm2_par_form_info(const ecm2_par_form *f, int *n_true, int *kernel);
 /* ~ParBilinearForm. */
 void ecm2_par_form_destroy(ecm2_par_form *f);

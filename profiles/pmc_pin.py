@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Pin a reduced profile (profiles/pmc_reduce.py output) as the traffic figure bench.py
-reports: profiles/pmc_<workload>_n1.json = the dominant kernel's per-launch HBM bytes
+reports: profiles/pmc_<workload>_n1_<layout>.json = the dominant kernel's per-launch HBM bytes
 (separate FETCH_SIZE / WRITE_SIZE passes) plus its second (partial-sum) pass.
-Usage: python3 profiles/pmc_pin.py <prof_dir> <workload> <kernel_key> > profiles/pmc_<workload>_n1.json"""
+Usage: python3 profiles/pmc_pin.py <prof_dir> <workload> <kernel_key> > profiles/pmc_<workload>_n1_<layout>.json
+(<layout> = the bench line's config.qdata_layout: affine | blocked | native)"""
 import json
 import os
 import sys

@@ -7,7 +7,7 @@ kernel of the Mult (the fused apply, the partial-sum pass, ...):
   hbm_bytes_per_launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024
 The factor 2 is the gfx950 correction of MI355X_MICROARCH.md (HBM section: FETCH_SIZE
 reports 1/2 of the bytes of wide coalesced streaming reads).  The dominant kernel's
-entry is what bench.py reports as roofline.traffic (copied to profiles/pmc_<tag>_n1.json).
+entry is what bench.py reports as roofline.traffic (copied to profiles/pmc_<tag>_n1_<layout>.json).
 """
 import csv
 import glob

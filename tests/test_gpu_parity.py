@@ -48,13 +48,19 @@ def make_mesh(name):
         m.set_vertices(nonaligned(m.vertices()))
     elif name == "cart_130":
         m = E.Mesh.MakeCartesian3D(13, 5, 2, 2.0, 1.0, 0.5)  # 130 elements: 3 blocks, ragged
+    elif name == "trilinear":
+        m = E.Mesh.MakeCartesian3D(8, 6, 5)                  # 240 elements, interior vertices moved:
+        V = m.vertices()                                      # genuinely trilinear (non-affine) hexes
+        inner = np.all((V > 1e-9) & (V < np.array([1.0, 1.0, 1.0]) - 1e-9), axis=1)
+        V[inner] += 0.02 * np.random.default_rng(5).uniform(-1, 1, (int(inner.sum()), 3))
+        m.set_vertices(V)
     else:
         raise ValueError(name)
     return m
 
 
 def build_pair(mesh, order, alpha, beta, kernel=E.KERNEL_AUTO, numbering=E.NUMBERING_ENTITY,
-               element_order="auto", scatter="partials"):
+               element_order="auto", scatter="partials", compress_geometry=True):
     """Product form + oracle operator on the same mesh; alpha/beta: 'fn', 'bio', float or None."""
     fes = E.H1Space(mesh, order, numbering)
     en = mesh.element_nodes()
@@ -76,7 +82,8 @@ def build_pair(mesh, order, alpha, beta, kernel=E.KERNEL_AUTO, numbering=E.NUMBE
 
     a_np, a_c = coeff(alpha)
     b_np, b_c = coeff(beta)
-    form = E.BilinearForm(fes, kernel=kernel, element_order=element_order, scatter=scatter)
+    form = E.BilinearForm(fes, kernel=kernel, element_order=element_order, scatter=scatter,
+                          compress_geometry=compress_geometry)
     if a_c is not None:
         form.AddDomainIntegrator(E.MassIntegrator(a_c))
     if b_c is not None:
@@ -303,6 +310,7 @@ def test_full_size_c4_tpe():
     m = E.Mesh.MakeCartesian3D(n, n, n)
     fes, form, op = build_pair(m, 2, "bio_a", "bio_b", numbering=E.NUMBERING_STRUCTURED)
     assert fes.ndofs == 10218313
+    assert form.info()["layout"] == E.QLAYOUT_AFFINE   # lattice coordinates i/108 are affine
     x = np.random.default_rng(22).uniform(-1, 1, fes.ndofs)
     y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
     form.Mult(dev(x), y)
@@ -437,3 +445,52 @@ def test_full_size_c5_bricks():
         out[bz] = host(y)
     ref = O.OracleOperator(en, fes.gather_map(), fes.ndofs, 4, alpha=a, beta=b).mult(x)
     assert relerr(out[2], ref) <= RTOL and relerr(out[0], ref) <= RTOL
+
+
+@pytest.mark.parametrize("mesh_name", ["nonaligned", "fichera_r1", "cart_bricks", "cart_130", "trilinear"])
+@pytest.mark.parametrize("order", [1, 2])
+@pytest.mark.parametrize("compress", [True, False])
+def test_affine_geometry_layout(mesh_name, order, compress):
+    """AFFINE qdata (constant element geometry + one (W beta, W alpha detJ) pair per point) is
+    chosen exactly for parallelepiped meshes with both integrators, and the operator, its
+    diagonal and the reference-layout qdata match the oracle either way; non-affine
+    (trilinear) elements keep the full per-point layout."""
+    m = make_mesh(mesh_name)
+    fes, form, op = build_pair(m, order, "bio_a", "fn", kernel=E.KERNEL_TPE, compress_geometry=compress)
+    affine = mesh_name != "trilinear"
+    want = E.QLAYOUT_AFFINE if (affine and compress) else E.QLAYOUT_BLOCKED
+    assert form.info()["layout"] == want
+    nq = (order + 2) ** 3
+    if want == E.QLAYOUT_AFFINE:
+        assert form.qdata_bytes() == 8 * 64 * ((fes.ne + 63) // 64) * (6 + 2 * nq)
+    x = np.random.default_rng(41).uniform(-1, 1, fes.ndofs)
+    y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+    form.Mult(dev(x), y)
+    assert relerr(host(y), op.mult(x)) <= RTOL
+    d = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    form.AssembleDiagonal(d)
+    assert relerr(host(d), op.diagonal()) < 1e-13
+    assert relerr(form.qdata(E.DIFFUSION), op.D) < 1e-13
+    assert relerr(form.qdata(E.MASS)[:, 0, :], op.M) < 1e-13
+
+
+def test_affine_needs_both_integrators():
+    """Mass-only / diffusion-only forms keep the per-point layout."""
+    m = make_mesh("nonaligned")
+    for a, b in ((2.5, None), (None, 0.7)):
+        fes, form, op = build_pair(m, 2, a, b, kernel=E.KERNEL_TPE)
+        assert form.info()["layout"] == E.QLAYOUT_BLOCKED
+
+
+def test_affine_wpe_reads_compressed_layout():
+    """The workgroup-per-element pieces (E-vector AddMultPA) read AFFINE qdata through the
+    layout-generic accessors: same per-integrator results as the oracle."""
+    m = make_mesh("cart_130")
+    fes, form, op = build_pair(m, 2, "bio_a", "fn", kernel=E.KERNEL_TPE)
+    assert form.info()["layout"] == E.QLAYOUT_AFFINE
+    nd = fes.nd
+    xe = np.random.default_rng(3).uniform(-1, 1, (fes.ne, nd))
+    for kind, ref in ((E.MASS, O.mass_apply(op.B, op.M, xe)), (E.DIFFUSION, O.diffusion_apply(op.B, op.G, op.D, xe))):
+        ye = torch.zeros(fes.ne * nd, dtype=torch.float64, device="cuda")
+        form.IntegratorAddMultPA(kind, dev(xe), ye)
+        assert relerr(host(ye).reshape(fes.ne, nd), ref) <= RTOL

@@ -312,7 +312,7 @@ def main():
 def qdata_layout(E, form):
     """Quadrature-data layout of a (local) form: affine | blocked | native."""
     return {E.QLAYOUT_NATIVE: "native", E.QLAYOUT_BLOCKED: "blocked",
-            E.QLAYOUT_AFFINE: "affine"}[form.info()["layout"]]
+            E.QLAYOUT_AFFINE: "affine", E.QLAYOUT_AFFINE_E: "affine_e"}[form.info()["layout"]]
 
 
 def c3_pcg(E, torch, fes, form, max_iter=200):

@@ -18,6 +18,9 @@
 //    qd_mass holds the per-point pair [blk][q][lane][2] = (W_q beta_q, W_q alpha_q det J).
 //    16 B per quadrature point + 48 B per element instead of 56 B per point (3.3x fewer
 //    qdata bytes at p = 2); the values are the reference's up to rounding.
+//  * AFFINE_E (line / brick kernels, p >= 3, same conditions): caller element order,
+//    qd_diff = C as [e][6] (11,12,13,22,23,33), qd_mass = pairs [e][q][2] (3.5x fewer
+//    qdata bytes at p = 4).
 //  * NATIVE (the reference's own layout): diffusion D(q,s,e) = [e][6][NQ],
 //    mass v(q,e) = [e][NQ] (bilininteg_diffusion_kernels.cpp:356-361,
 //    bilininteg_mass_pa.cpp:66-77).
@@ -29,7 +32,7 @@
 namespace ecm2
 {
 
-enum QLayoutKind : int { QLAYOUT_NATIVE = 0, QLAYOUT_BLOCKED = 1, QLAYOUT_AFFINE = 2 };
+enum QLayoutKind : int { QLAYOUT_NATIVE = 0, QLAYOUT_BLOCKED = 1, QLAYOUT_AFFINE = 2, QLAYOUT_AFFINE_E = 3 };
 
 constexpr int kElemBlock = 64;  // elements per wave in the blocked layout
 
@@ -43,15 +46,19 @@ struct QLayout
    {
       if (kind == QLAYOUT_NATIVE) { return (size_t)ne * 6 * nq; }
       if (kind == QLAYOUT_AFFINE) { return (size_t)nblk() * 6 * kElemBlock; }
+      if (kind == QLAYOUT_AFFINE_E) { return (size_t)ne * 6; }
       return (size_t)nblk() * nq * 6 * kElemBlock;
    }
    size_t mass_size() const
    {
       if (kind == QLAYOUT_NATIVE) { return (size_t)ne * nq; }
       if (kind == QLAYOUT_AFFINE) { return (size_t)nblk() * nq * 2 * kElemBlock; }
+      if (kind == QLAYOUT_AFFINE_E) { return (size_t)ne * nq * 2; }
       return (size_t)nblk() * ((nq + 1) / 2) * 2 * kElemBlock;
    }
    int nblk() const { return (ne + kElemBlock - 1) / kElemBlock; }
+   bool blocked() const { return kind == QLAYOUT_BLOCKED || kind == QLAYOUT_AFFINE; }
+   bool affine() const { return kind == QLAYOUT_AFFINE || kind == QLAYOUT_AFFINE_E; }
 };
 
 // Coefficient descriptor for qdata setup: constant, per-quadrature-point array
@@ -127,7 +134,7 @@ void setup_from_nodes(const QLayout &L, int Q, const double *enodes, const doubl
                       const Basis1D &b1, const CoeffDesc *cm, const CoeffDesc *cd,
                       const double *cm_q, const double *cd_q,
                       double *qd_diff, double *qd_mass, hipStream_t s);
-// AFFINE layout (see above) from the corners of parallelepiped elements; needs both
+// AFFINE / AFFINE_E layout (see above) from the corners of parallelepiped elements; needs both
 // coefficients (cm, cd non-null).
 void setup_affine(const QLayout &L, int Q, const double *enodes, const double *W, const CoeffDesc *cm,
                   const CoeffDesc *cd, const double *cm_q, const double *cd_q, double *qd_fac,

@@ -331,9 +331,10 @@ void PAForm::assemble(hipStream_t s)
    ECM2_VERIFY(resolved_mode_ != KERNEL_LINE || kern::has_line(D_, Q_), ERR_UNSUPPORTED,
                "line kernel needs Q1D in {D1D, D1D+1} and Q1D <= 8");
    layout_.kind = (resolved_mode_ == KERNEL_TPE) ? QLAYOUT_BLOCKED : QLAYOUT_NATIVE;
-   if (layout_.kind == QLAYOUT_BLOCKED && affine_ && compress_ && affine_env() && !jac_ && have_mass_ && have_diff_)
+   if (affine_ && compress_ && affine_env() && !jac_ && have_mass_ && have_diff_)
    {
-      layout_.kind = QLAYOUT_AFFINE;
+      if (resolved_mode_ == KERNEL_TPE) { layout_.kind = QLAYOUT_AFFINE; }
+      else if (resolved_mode_ == KERNEL_LINE) { layout_.kind = QLAYOUT_AFFINE_E; }
    }
 
    if (resolved_mode_ == KERNEL_TPE && !gmap_blk_.size() && ne_ > 0)
@@ -562,8 +563,8 @@ void PAForm::assemble(hipStream_t s)
       n_left_ = n_left;
       ECM2_HIP(hipStreamSynchronize(s));
    }
-   layout_.pos = (layout_.kind != QLAYOUT_NATIVE) ? pos_.data() : nullptr;
-   layout_.perm = (layout_.kind != QLAYOUT_NATIVE) ? perm_dev_.data() : nullptr;
+   layout_.pos = layout_.blocked() ? pos_.data() : nullptr;
+   layout_.perm = layout_.blocked() ? perm_dev_.data() : nullptr;
    if (!use_partials()) { part_.resize(0); }
    else if (resolved_mode_ == KERNEL_LINE)
    {
@@ -575,7 +576,7 @@ void PAForm::assemble(hipStream_t s)
    qd_mass_.resize(have_mass_ ? layout_.mass_size() : 0);
    // the setup kernels write every entry except the padding lanes of a partial last block
    // (blocked layout), which are cleared so the apply kernels stream defined values
-   if (layout_.kind != QLAYOUT_NATIVE && ne_ % kElemBlock)
+   if (layout_.blocked() && ne_ % kElemBlock)
    {
       const size_t nb = layout_.nblk();
       if (qd_diff_.size())
@@ -605,7 +606,7 @@ void PAForm::assemble(hipStream_t s)
    const double *cd_q = have_diff_ ? coeff_values(cdiff_, ctmp_d_) : nullptr;
    const CoeffDesc *cm = have_mass_ ? &cmass_ : nullptr;
    const CoeffDesc *cd = have_diff_ ? &cdiff_ : nullptr;
-   if (layout_.kind == QLAYOUT_AFFINE)
+   if (layout_.affine())
    {
       kern::setup_affine(layout_, Q_, enodes_.data(), W_.data(), cm, cd, cm_q, cd_q, qd_diff_.data(),
                          qd_mass_.data(), s);
@@ -861,7 +862,7 @@ void PAForm::get_qdata(int kind, double *out, hipStream_t s)
    ECM2_VERIFY(assembled_, ERR_STATE, "get_qdata before Assemble");
    const bool diff = kind == INTEG_DIFFUSION;
    ECM2_VERIFY(diff ? have_diff_ : have_mass_, ERR_ARG, "integrator " << kind << " not present");
-   const bool aff = layout_.kind == QLAYOUT_AFFINE;
+   const bool aff = layout_.affine();
    DeviceArray<double> &src = (diff && !aff) ? qd_diff_ : qd_mass_;
    std::vector<double> h(src.size()), hc(aff ? qd_diff_.size() : 0);
    if (src.size())
@@ -887,6 +888,12 @@ void PAForm::get_qdata(int kind, double *out, hipStream_t s)
          {
             size_t src_i;
             if (layout_.kind == QLAYOUT_NATIVE) { src_i = ((size_t)e * nc + c) * NQ_ + q; }
+            else if (layout_.kind == QLAYOUT_AFFINE_E)
+            {
+               const size_t pi = ((size_t)e * NQ_ + q) * 2;
+               out[((size_t)e * nc + c) * NQ_ + q] = diff ? h[pi] * hc[(size_t)e * 6 + c] : h[pi + 1];
+               continue;
+            }
             else
             {
                const int ip = perm_host_.empty() ? e : inv_perm(e);

@@ -67,6 +67,7 @@ __device__ __forceinline__ size_t affine_pair(const int *pos, int nq, int e, int
 __device__ __forceinline__ double qd_diff_at(const double *qdd, const double *qdm, const int *pos, int kind,
                                              int nq, int e, int c, int q)
 {
+   if (kind == QLAYOUT_AFFINE_E) { return qdm[((size_t)e * nq + q) * 2] * qdd[(size_t)e * 6 + c]; }
    if (kind == QLAYOUT_AFFINE)
    {
       const int ie = pos ? pos[e] : e;
@@ -76,6 +77,7 @@ __device__ __forceinline__ double qd_diff_at(const double *qdd, const double *qd
 }
 __device__ __forceinline__ double qd_mass_at(const double *qdm, const int *pos, int kind, int nq, int e, int q)
 {
+   if (kind == QLAYOUT_AFFINE_E) { return qdm[((size_t)e * nq + q) * 2 + 1]; }
    if (kind == QLAYOUT_AFFINE) { return qdm[affine_pair(pos, nq, e, q) + 1]; }
    return qdm[qidx_mass(pos, kind, nq, e, q)];
 }
@@ -308,7 +310,7 @@ __global__ void k_setup_jac(const int *__restrict__ pos, int kind, int ne, int N
 // setup's (bilininteg_mass_pa.cpp:76) with the per-point factors W_q beta_q / W_q alpha_q kept
 // apart from the element's C = adj(J) adj(J)^T / det J.  Threads over (blk, q, lane), lane
 // fastest: each wave stores 1 KiB of pairs per point; the q = 0 threads store C.
-template <int Q>
+template <int Q, bool BLOCKED>
 __global__ void __launch_bounds__(256)
 k_setup_affine(const int *__restrict__ perm, int ne, const double *__restrict__ enodes,
                const double *__restrict__ W, SetupCoef cm, SetupCoef cd, double *__restrict__ qd_fac,
@@ -316,13 +318,27 @@ k_setup_affine(const int *__restrict__ perm, int ne, const double *__restrict__ 
 {
    constexpr int NQ = Q * Q * Q;
    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-   const int lane = (int)(t & 63);
-   const long rest = t >> 6;
-   const int q = (int)(rest % NQ);
-   const long blk = rest / NQ;
-   const int ipos = (int)(blk * 64 + lane);
-   if (ipos >= ne) { return; }
-   const int e = perm ? perm[ipos] : ipos;
+   int lane, q, e;
+   long blk;
+   if (BLOCKED)
+   {
+      lane = (int)(t & 63);
+      const long rest = t >> 6;
+      q = (int)(rest % NQ);
+      blk = rest / NQ;
+      const int ipos = (int)(blk * 64 + lane);
+      if (ipos >= ne) { return; }
+      e = perm ? perm[ipos] : ipos;
+   }
+   else
+   {
+      // AFFINE_E: threads over (e, q), q fastest
+      if (t >= (long)ne * NQ) { return; }
+      e = (int)(t / NQ);
+      q = (int)(t % NQ);
+      lane = 0;
+      blk = 0;
+   }
    const double *X = enodes + (size_t)e * 24;
    double J[3][3];
 #pragma unroll
@@ -342,7 +358,8 @@ k_setup_affine(const int *__restrict__ perm, int ne, const double *__restrict__ 
    v2d pr;
    pr.x = w * coef_at(cd, eq);
    pr.y = w * coef_at(cm, eq) * detJ;
-   reinterpret_cast<v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane] = pr;
+   if (BLOCKED) { reinterpret_cast<v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane] = pr; }
+   else { reinterpret_cast<v2d *>(qd_pair)[(size_t)e * NQ + q] = pr; }
    if (q == 0)
    {
       const double A11 = (J22 * J33) - (J23 * J32);
@@ -362,10 +379,18 @@ k_setup_affine(const int *__restrict__ perm, int ne, const double *__restrict__ 
       p1.y = r * (A21 * A21 + A22 * A22 + A23 * A23);
       p2.x = r * (A21 * A31 + A22 * A32 + A23 * A33);
       p2.y = r * (A31 * A31 + A32 * A32 + A33 * A33);
-      v2d *dst = reinterpret_cast<v2d *>(qd_fac + (size_t)blk * 3 * 128) + lane;
-      dst[0] = p0;
-      dst[64] = p1;
-      dst[128] = p2;
+      if (BLOCKED)
+      {
+         v2d *dst = reinterpret_cast<v2d *>(qd_fac + (size_t)blk * 3 * 128) + lane;
+         dst[0] = p0;
+         dst[64] = p1;
+         dst[128] = p2;
+      }
+      else
+      {
+         double *dst = qd_fac + (size_t)e * 6;  // (11, 12, 13, 22, 23, 33)
+         dst[0] = p0.x; dst[1] = p0.y; dst[2] = p1.x; dst[3] = p1.y; dst[4] = p2.x; dst[5] = p2.y;
+      }
    }
 }
 
@@ -1112,12 +1137,28 @@ __device__ __forceinline__ CBasis *stage_basis()
    return p;
 }
 
-template <int D, int Q, bool MASS, bool DIFF>
+template <int D, int Q, bool MASS, bool DIFF, bool AFF = false>
 __device__ __forceinline__ void line_load_qdata(double (&qv)[7][Q], int e, int t,
                                                 const double *__restrict__ qdd,
                                                 const double *__restrict__ qdm)
 {
    constexpr int NQ = Q * Q * Q, QQ = Q * Q;
+   if (AFF && t < QQ)
+   {
+      // AFFINE_E: D_c = (W beta)(q) C_c, mass = (W alpha det J)(q); 16-byte pair per point
+      double c[6];
+#pragma unroll
+      for (int k = 0; k < 6; k++) { c[k] = qdd[(size_t)e * 6 + k]; }
+#pragma unroll
+      for (int qz = 0; qz < Q; qz++)
+      {
+         const v2d p = reinterpret_cast<const v2d *>(qdm)[(size_t)e * NQ + qz * QQ + t];
+#pragma unroll
+         for (int k = 0; k < 6; k++) { qv[k][qz] = p.x * c[k]; }
+         qv[6][qz] = p.y;
+      }
+      return;
+   }
    if (t < QQ)
    {
 #pragma unroll
@@ -1348,13 +1389,13 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned
    const int e0 = ch & 0xffffff, cnt = (VAR & 8) ? 1 : (ch >> 24);  // VAR & 8: one element per wave
 
    double qv[7][Q];
-   if (!(VAR & 34)) { line_load_qdata<D, Q, MASS, DIFF>(qv, e0, t, qdd, qdm); }
+   if (!(VAR & 34)) { line_load_qdata<D, Q, MASS, DIFF, (VAR & 64) != 0>(qv, e0, t, qdd, qdm); }
    double carry = 0.0;
 #pragma unroll 1
    for (int k = 0; k < cnt; k++)
    {
       const int e = e0 + k;
-      if ((VAR & 2) && !(VAR & 32)) { line_load_qdata<D, Q, MASS, DIFF>(qv, e, t, qdd, qdm); }
+      if ((VAR & 2) && !(VAR & 32)) { line_load_qdata<D, Q, MASS, DIFF, (VAR & 64) != 0>(qv, e, t, qdd, qdm); }
       // ---- lanes (dy, dz): gather the x-line, contract in x
       int gl[D];
       if (t < DD)
@@ -1432,7 +1473,7 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned
          double A1[D], A2[D], A3[D];
 #pragma unroll
          for (int dz = 0; dz < D; dz++) { A1[dz] = 0.0; A2[dz] = 0.0; A3[dz] = 0.0; }
-         if (VAR & 32) { line_load_qdata<D, Q, MASS, DIFF>(qv, e, t, qdd, qdm); }  // just in time
+         if (VAR & 32) { line_load_qdata<D, Q, MASS, DIFF, (VAR & 64) != 0>(qv, e, t, qdd, qdm); }  // just in time
 #pragma unroll
          for (int qz = 0; qz < Q; qz++)
          {
@@ -1479,7 +1520,7 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned
          }
       }
       // next element's qdata: in flight during the rest of this element
-      if (!(VAR & 34) && k + 1 < cnt) { line_load_qdata<D, Q, MASS, DIFF>(qv, e + 1, t, qdd, qdm); }
+      if (!(VAR & 34) && k + 1 < cnt) { line_load_qdata<D, Q, MASS, DIFF, (VAR & 64) != 0>(qv, e + 1, t, qdd, qdm); }
       __syncthreads();
       // ---- lanes (qx, dz): transpose in y
       if (t < DQ)
@@ -1624,7 +1665,7 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
       {
          line_load_qdata_x2<D, Q, MASS, DIFF>(qv, belem[(size_t)k * NE + t / QQ], t % QQ, qdd, qdm);
       }
-      else { line_load_qdata<D, Q, MASS, DIFF>(qv, belem[(size_t)k * NE + t / QQ], t % QQ, qdd, qdm); }
+      else { line_load_qdata<D, Q, MASS, DIFF, (VAR & 64) != 0>(qv, belem[(size_t)k * NE + t / QQ], t % QQ, qdd, qdm); }
    }
 
    // ---- lanes (element, dy, dz): gather the x-line, contract in x
@@ -1695,7 +1736,7 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
    {
       CBasis *bp = stage_basis<D, Q>();
       const int elt = t / QQ, l = t % QQ;
-      if (VAR & 1) { line_load_qdata<D, Q, MASS, DIFF>(qv, belem[(size_t)k * NE + elt], l, qdd, qdm); }
+      if (VAR & 1) { line_load_qdata<D, Q, MASS, DIFF, (VAR & 64) != 0>(qv, belem[(size_t)k * NE + elt], l, qdd, qdm); }
       double *in = bufB + elt * SB;
       double *o = in;
       double l0[D], l1[D], l2[D];
@@ -2314,15 +2355,24 @@ void setup_affine(const QLayout &L, int Q, const double *enodes, const double *W
                   double *qd_pair, hipStream_t s)
 {
    if (L.ne == 0) { return; }
-   ECM2_VERIFY(L.kind == QLAYOUT_AFFINE && cm && cd, ERR_INTERNAL, "affine setup needs the AFFINE layout and both coefficients");
+   ECM2_VERIFY(L.affine() && cm && cd, ERR_INTERNAL, "affine setup needs an AFFINE layout and both coefficients");
    ECM2_VERIFY(!L.pos || L.perm, ERR_INTERNAL, "blocked setup needs the inverse permutation");
    const SetupCoef scm = make_setup_coef(cm, cm_q), scd = make_setup_coef(cd, cd_q);
-   const long n = (long)L.nblk() * 64 * L.nq;
+   const bool blk = L.kind == QLAYOUT_AFFINE;
+   const long n = blk ? (long)L.nblk() * 64 * L.nq : (long)L.ne * L.nq;
 #define ECM2_AFF_CASE(QQ)                                                                               \
    if (Q == QQ)                                                                                          \
    {                                                                                                     \
-      hipLaunchKernelGGL((k_setup_affine<QQ>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.perm, L.ne, enodes, W, \
-                         scm, scd, qd_fac, qd_pair);                                                     \
+      if (blk)                                                                                           \
+      {                                                                                                  \
+         hipLaunchKernelGGL((k_setup_affine<QQ, true>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.perm, L.ne, \
+                            enodes, W, scm, scd, qd_fac, qd_pair);                                       \
+      }                                                                                                  \
+      else                                                                                               \
+      {                                                                                                  \
+         hipLaunchKernelGGL((k_setup_affine<QQ, false>), dim3(grid_for(n, 256)), dim3(256), 0, s, nullptr, L.ne, \
+                            enodes, W, scm, scd, qd_fac, qd_pair);                                       \
+      }                                                                                                  \
       ECM2_HIP(hipGetLastError());                                                                       \
       return;                                                                                            \
    }
@@ -2379,6 +2429,16 @@ void launch_line_mdq(const ApplyArgs &a, const Basis1D &b, hipStream_t s)
    hipLaunchKernelGGL((k_apply_line<D, Q, MASS, DIFF, SP, V>), grid, block, 0, s, c0, c1, a.chunks, a.n_owned, \
                       a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.part)
    const bool split = a.xg || a.yg;
+   if (a.kind == QLAYOUT_AFFINE_E)  // bit 64: AFFINE_E qdata (default variant only)
+   {
+      if constexpr (MASS && DIFF)
+      {
+         if (line_variant() & 8) { if (split) { ECM2_LINE(true, 72); } else { ECM2_LINE(false, 72); } }
+         else { if (split) { ECM2_LINE(true, 64); } else { ECM2_LINE(false, 64); } }
+      }
+      else { ECM2_VERIFY(false, ERR_INTERNAL, "AFFINE qdata needs both integrators"); }
+      return;
+   }
    switch (line_variant() & 46)
    {
       case 2: if (split) { ECM2_LINE(true, 2); } else { ECM2_LINE(false, 2); } break;
@@ -2439,6 +2499,16 @@ void launch_brick_mdq(const ApplyArgs &a, hipStream_t s)
    hipLaunchKernelGGL((k_apply_brick<D, Q, BZ, MASS, DIFF, SP, V>), grid, block, 0, s, k0, k1, a.belem, \
                       a.bmap, a.n_owned, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, a.part_brick)
    const bool split = a.xg || a.yg;
+   if (a.kind == QLAYOUT_AFFINE_E)  // bit 64: AFFINE_E qdata
+   {
+      if constexpr (MASS && DIFF)
+      {
+         if (brick_variant() & 1) { if (split) { ECM2_BRICK(true, 65); } else { ECM2_BRICK(false, 65); } }
+         else { if (split) { ECM2_BRICK(true, 64); } else { ECM2_BRICK(false, 64); } }
+      }
+      else { ECM2_VERIFY(false, ERR_INTERNAL, "AFFINE qdata needs both integrators"); }
+      return;
+   }
    switch (brick_variant() & 3)
    {
       case 1: if (split) { ECM2_BRICK(true, 1); } else { ECM2_BRICK(false, 1); } break;

@@ -128,11 +128,13 @@ int ecm2_pa_form_set_jacobians(ecm2_pa_form *f, const double *J);
  * integrators are present, the p <= 2 fused kernel stores the constant element geometry
  * adj(J) adj(J)^T / det J once per element and one (W beta, W alpha det J) pair per
  * quadrature point: the reference's pa_data values (bilininteg_diffusion_kernels.cpp:349-362,
- * bilininteg_mass_pa.cpp:76) up to rounding, 3.3x fewer bytes at p = 2.  On by default;
+ * bilininteg_mass_pa.cpp:76) up to rounding, 3.3x fewer bytes at p = 2 (3.5x at p = 4,
+ * AFFINE_E: element-ordered, for the p >= 3 line / brick kernels).  On by default;
  * ecm2_pa_form_set_geometry_compression(f, 0) keeps the full per-point layout. */
 #define ECM2_QLAYOUT_NATIVE 0
 #define ECM2_QLAYOUT_BLOCKED 1
 #define ECM2_QLAYOUT_AFFINE 2
+#define ECM2_QLAYOUT_AFFINE_E 3  /* the same compression for the p >= 3 line / brick kernels */
 int ecm2_pa_form_set_geometry_compression(ecm2_pa_form *f, int on);
 /* BilinearForm::AddDomainIntegrator(new MassIntegrator(Q)) / DiffusionIntegrator(Q)
  * (bilinearform.cpp:231-242).  data: CONSTANT -> data[0] (host);

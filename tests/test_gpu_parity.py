@@ -448,21 +448,27 @@ def test_full_size_c5_bricks():
 
 
 @pytest.mark.parametrize("mesh_name", ["nonaligned", "fichera_r1", "cart_bricks", "cart_130", "trilinear"])
-@pytest.mark.parametrize("order", [1, 2])
+@pytest.mark.parametrize("order", [1, 2, 3, 4])
 @pytest.mark.parametrize("compress", [True, False])
 def test_affine_geometry_layout(mesh_name, order, compress):
     """AFFINE qdata (constant element geometry + one (W beta, W alpha detJ) pair per point) is
-    chosen exactly for parallelepiped meshes with both integrators, and the operator, its
-    diagonal and the reference-layout qdata match the oracle either way; non-affine
-    (trilinear) elements keep the full per-point layout."""
+    chosen exactly for parallelepiped meshes with both integrators -- blocked for the p <= 2
+    thread-per-element kernel, element-ordered (AFFINE_E) for the p >= 3 line / brick
+    kernels -- and the operator, its diagonal and the reference-layout qdata match the
+    oracle either way; non-affine (trilinear) elements keep the full per-point layout."""
     m = make_mesh(mesh_name)
-    fes, form, op = build_pair(m, order, "bio_a", "fn", kernel=E.KERNEL_TPE, compress_geometry=compress)
+    fes, form, op = build_pair(m, order, "bio_a", "fn", compress_geometry=compress)
     affine = mesh_name != "trilinear"
-    want = E.QLAYOUT_AFFINE if (affine and compress) else E.QLAYOUT_BLOCKED
-    assert form.info()["layout"] == want
     nq = (order + 2) ** 3
+    if order <= 2:
+        want = E.QLAYOUT_AFFINE if (affine and compress) else E.QLAYOUT_BLOCKED
+    else:
+        want = E.QLAYOUT_AFFINE_E if (affine and compress) else E.QLAYOUT_NATIVE
+    assert form.info()["layout"] == want
     if want == E.QLAYOUT_AFFINE:
         assert form.qdata_bytes() == 8 * 64 * ((fes.ne + 63) // 64) * (6 + 2 * nq)
+    elif want == E.QLAYOUT_AFFINE_E:
+        assert form.qdata_bytes() == 8 * fes.ne * (6 + 2 * nq)
     x = np.random.default_rng(41).uniform(-1, 1, fes.ndofs)
     y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
     form.Mult(dev(x), y)

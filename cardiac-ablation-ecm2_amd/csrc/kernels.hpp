@@ -89,6 +89,7 @@ struct ApplyArgs
    const double *x = nullptr, *xg = nullptr;
    double *y = nullptr, *yg = nullptr;
    double *part = nullptr;          // partial slots of shared dofs (null: atomics)
+   const int *pslot = nullptr;      // TPE: [blk][nd][64] entry -> position in its dof's run (null: dense slots)
    const int *chunks = nullptr;     // LINE: device chunk table (first | count << 24)
    const int *chunk_off = nullptr;  // LINE: host [nblk + 1], chunks of 64-element block b
    // LINE, brick part (p >= 3 on structured regions): bricks of 2 x 2 x brick_bz elements
@@ -217,7 +218,7 @@ void stream_copy(long n, const double *a, double *b, hipStream_t s);
 void gather_idx(int n, const int *idx, const double *x, double *buf, hipStream_t s);
 void scatter_add_idx(int n, const int *idx, const double *buf, double *y, hipStream_t s);
 // Deterministic second scatter pass: y[dofs[i]] = sum_j part[slots[j]], j in
-// [start, start + count), meta[i] = start << 5 | count.
+// [start, start + count), meta[i] = start << 5 | count; slots null: part[j] (contiguous runs).
 void sum_partials(int i0, int i1, const int *dofs, const unsigned *meta, const int *slots, const double *part,
                   int n_owned, double *y, double *yg, hipStream_t s);
 void scatter_set_idx(int n, const int *idx, const double *buf, double *y, hipStream_t s);

@@ -273,7 +273,7 @@ static bool sum_order_by_dof()
 // owned dofs come first, then the ghosts (split form); within each range the list is
 // ordered by first slot, so neighbouring threads of k_sum_partials read neighbouring slots.
 void PAForm::build_shared_plan(const std::vector<int> &hcount, const std::vector<int> &hdof,
-                               const std::vector<int> &hslot, hipStream_t s)
+                               const std::vector<int> &hslot, hipStream_t s, std::vector<int> *slots_out)
 {
    std::vector<int> start(ndofs_ + 1, 0);
    for (int d = 0; d < ndofs_; d++) { start[d + 1] = start[d] + (hcount[d] > 1 ? hcount[d] : 0); }
@@ -304,7 +304,22 @@ void PAForm::build_shared_plan(const std::vector<int> &hcount, const std::vector
    n_slots_ = (long)slots.size();
    sh_dofs_.upload(dofs, s);
    sh_meta_.upload(meta, s);
-   sh_slots_.upload(slots, s);
+   if (slots_out) { *slots_out = std::move(slots); }  // caller lays partials out as runs
+   else { sh_slots_.upload(slots, s); }
+}
+
+// experiment knob ECM2_PART_RUNS=1: TPE partial slots laid out as contiguous per-dof runs
+// (the summation pass reads each dof's holders contiguously, no slot list) instead of the
+// dense [blk][a][lane] slots.  Measured (profiles/ab_runs.sh): the summation pass halves
+// (C4 88 -> 48 us) but the apply kernel's scattered partial stores cost more (C4 0.379 ->
+// 0.441 ms): net slower at C2 / C3 / C4, so off by default.
+static bool part_runs()
+{
+   static const bool v = [] {
+      const char *e = std::getenv("ECM2_PART_RUNS");
+      return e && std::string(e) == "1";
+   }();
+   return v;
 }
 
 void PAForm::set_kernel(int mode)
@@ -399,7 +414,22 @@ void PAForm::assemble(hipStream_t s)
                      hslot.push_back((b * ND_ + a) * 64 + l);
                   }
                }
-         build_shared_plan(hcount, hdof, hslot, s);
+         tpe_runs_ = part_runs();
+         if (tpe_runs_)
+         {
+            // partial slot of a shared holding entry = its position in the dof's run
+            std::vector<int> slots;
+            build_shared_plan(hcount, hdof, hslot, s, &slots);
+            std::vector<int> ps((size_t)nblk * ND_ * 64, -1);
+            for (size_t j = 0; j < slots.size(); j++) { ps[slots[j]] = (int)j; }
+            pslot_.upload(ps, s);
+            sh_slots_.resize(0);
+         }
+         else
+         {
+            build_shared_plan(hcount, hdof, hslot, s);
+            pslot_.resize(0);
+         }
       }
       gmap_blk_.upload(blk, s);
       lane_flags_.upload(fl, s);
@@ -571,7 +601,7 @@ void PAForm::assemble(hipStream_t s)
       // [bricks' lattice slots | leftover elements' [e][nd] slots (when there are any)]
       part_.resize(std::max<size_t>(1, (size_t)part_line_off_ + (n_left_ ? (size_t)ne_ * ND_ : 0)));
    }
-   else { part_.resize((size_t)layout_.nblk() * ND_ * 64); }
+   else { part_.resize(tpe_runs_ ? std::max<size_t>(1, (size_t)n_slots_) : (size_t)layout_.nblk() * ND_ * 64); }
    qd_diff_.resize(have_diff_ ? layout_.diff_size() : 0);
    qd_mass_.resize(have_mass_ ? layout_.mass_size() : 0);
    // the setup kernels write every entry except the padding lanes of a partial last block
@@ -751,7 +781,8 @@ void PAForm::set_scatter(int mode)
 void PAForm::finish_shared(int i0, int i1, double *y, double *yg, hipStream_t s)
 {
    if (!use_partials()) { return; }
-   kern::sum_partials(i0, i1, sh_dofs_.data(), sh_meta_.data(), sh_slots_.data(), part_.data(), n_owned_, y,
+   kern::sum_partials(i0, i1, sh_dofs_.data(), sh_meta_.data(), sh_slots_.size() ? sh_slots_.data() : nullptr,
+                      part_.data(), n_owned_, y,
                       yg, s);
 }
 
@@ -772,6 +803,7 @@ ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, doubl
    a.qdm = qd_mass_.data();
    a.x = x; a.xg = xg; a.y = y; a.yg = yg;
    a.part = use_partials() ? const_cast<double *>(part_.data()) : nullptr;  // form-owned scratch
+   a.pslot = (resolved_mode_ == KERNEL_TPE && pslot_.size()) ? pslot_.data() : nullptr;
    a.chunks = chunks_.data();
    a.chunk_off = chunk_off_.empty() ? nullptr : chunk_off_.data();
    if (resolved_mode_ == KERNEL_LINE && use_partials())

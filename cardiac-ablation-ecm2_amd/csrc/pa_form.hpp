@@ -133,7 +133,7 @@ private:
    // second pass of the deterministic scatter from the shared holding entries
    // (hdof[i], hslot[i]) in ascending slot order and the per-dof holder counts
    void build_shared_plan(const std::vector<int> &hcount, const std::vector<int> &hdof,
-                          const std::vector<int> &hslot, hipStream_t s);
+                          const std::vector<int> &hslot, hipStream_t s, std::vector<int> *slots_out = nullptr);
    ApplyArgs apply_args(const double *x, const double *xg, double *y, double *yg, int b0,
                         int b1) const;
 
@@ -152,7 +152,9 @@ private:
    long n_slots_ = 0;
    DeviceArray<int> sh_dofs_, sh_slots_;           // second-pass plan (see finish_shared)
    DeviceArray<unsigned> sh_meta_;                 // start << 5 | count
-   DeviceArray<double> part_;                       // [blk][nd][64] partial slots
+   DeviceArray<double> part_;                       // partial slots: TPE runs [n_slots] (or [blk][nd][64])
+   DeviceArray<int> pslot_;                         // TPE: [blk][nd][64] entry -> run position (-1: not shared)
+   bool tpe_runs_ = false;
    bool assembled_ = false;
    bool have_mass_ = false, have_diff_ = false;
    CoeffDesc cmass_, cdiff_;

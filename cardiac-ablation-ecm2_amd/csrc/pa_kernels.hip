@@ -589,7 +589,7 @@ template <int D, bool SPLIT, bool SIGNS, bool PLAIN>
 __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], const int *__restrict__ mp, int fl,
                                                    int blk, int lane, bool active, int n_owned,
                                                    double *__restrict__ y, double *__restrict__ yg,
-                                                   double *__restrict__ part)
+                                                   double *__restrict__ part, const int *__restrict__ pslot)
 {
    constexpr int ND = D * D * D;
    if (SIGNS)
@@ -629,7 +629,13 @@ __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], cons
             const int d = bdof(g);
             double *dst = (!SPLIT || d < n_owned) ? y + d : yg + (d - n_owned);
             if (!bshared(g) || PLAIN) { *dst = Yo[a]; }
-            else if (part) { part[((size_t)blk * ND + a) * 64 + lane] = Yo[a]; }
+            else if (part)
+            {
+               // pslot: the entry's position in its dof's contiguous run (summation pass reads
+               // each dof's holders contiguously); else the dense [blk][a][lane] slot
+               const size_t ent = ((size_t)blk * ND + a) * 64 + lane;
+               part[pslot ? (size_t)pslot[ent] : ent] = Yo[a];
+            }
             else { unsafeAtomicAdd(dst, Yo[a]); }
          }
 }
@@ -643,7 +649,7 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                const double *__restrict__ x, const double *__restrict__ xg,
                double *__restrict__ y, double *__restrict__ yg, const Basis1D b,
                const double *__restrict__ rowtab, const int *__restrict__ lane_flags,
-               double *__restrict__ part)
+               double *__restrict__ part, const int *__restrict__ pslot)
 {
    constexpr int ND = D * D * D, NQ = Q * Q * Q, NQH = (NQ + 1) / 2, DD = D * D;
    constexpr int NR = Q * Q;  // rows
@@ -810,7 +816,7 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
       }
    }
    tpe_assemble_store<D, SPLIT, true, (VAR & 1) != 0>(Yo, mp, lane_flags[(size_t)blk * 64 + lane], blk, lane, active,
-                                                      n_owned, y, yg, part);
+                                                      n_owned, y, yg, part, pslot);
 }
 
 // Thread-per-element apply on AFFINE qdata, sum-factorised per quadrature plane qz: the
@@ -827,7 +833,7 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                const double *__restrict__ qdd, const double *__restrict__ qdm,
                const double *__restrict__ x, const double *__restrict__ xg,
                double *__restrict__ y, double *__restrict__ yg, const Basis1D b,
-               const int *__restrict__ lane_flags, double *__restrict__ part)
+               const int *__restrict__ lane_flags, double *__restrict__ part, const int *__restrict__ pslot)
 {
    constexpr int ND = D * D * D, NQ = Q * Q * Q, NR = Q * Q;
    __shared__ double sX[4][ND][64];
@@ -967,7 +973,7 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
             }
    }
    tpe_assemble_store<D, SPLIT, true, (VAR & 1) != 0>(Yo, mp, lane_flags[(size_t)blk * 64 + lane], blk, lane, active,
-                                                      n_owned, y, yg, part);
+                                                      n_owned, y, yg, part, pslot);
 }
 
 // PA diagonal, thread per element on the blocked layout (PADiffusionDiagonal3D and the
@@ -984,7 +990,7 @@ __global__ void __launch_bounds__(256)
 k_diag_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
            const double *__restrict__ qdd, const double *__restrict__ qdm, double *__restrict__ y,
            double *__restrict__ yg, const Basis1D b, const double *__restrict__ drow,
-           const int *__restrict__ lane_flags, double *__restrict__ part)
+           const int *__restrict__ lane_flags, double *__restrict__ part, const int *__restrict__ pslot)
 {
    constexpr int ND = D * D * D, NQ = Q * Q * Q, NQH = (NQ + 1) / 2, DD = D * D;
    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1072,7 +1078,7 @@ k_diag_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restric
          }
    }
    tpe_assemble_store<D, SPLIT, false, false>(Yo, mp, lane_flags[(size_t)blk * 64 + lane], blk, lane, active,
-                                               n_owned, y, yg, part);
+                                               n_owned, y, yg, part, pslot);
 }
 
 // --------------------------------------------------------------------------
@@ -2283,16 +2289,29 @@ __global__ void k_sum_partials(int i0, int i1, const int *__restrict__ dofs, con
    const unsigned m = meta[i];
    const int d = dofs[i];
    const int start = (int)(m >> 5), cnt = (int)(m & 31);
+   double acc = 0.0;
+   if (!slots)
+   {
+      // contiguous runs (pslot plan): the dof's holders are part[start, start + cnt)
+      double v[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) { v[k] = k < cnt ? part[start + k] : 0.0; }
+#pragma unroll
+      for (int k = 0; k < 8; k++) { acc += v[k]; }
+      for (int k = 8; k < cnt; k++) { acc += part[start + k]; }
+   }
+   else
+   {
    int sl[8];
 #pragma unroll
    for (int k = 0; k < 8; k++) { sl[k] = k < cnt ? slots[start + k] : -1; }
    double v[8];
 #pragma unroll
    for (int k = 0; k < 8; k++) { v[k] = sl[k] >= 0 ? part[sl[k]] : 0.0; }
-   double acc = 0.0;
 #pragma unroll
    for (int k = 0; k < 8; k++) { acc += v[k]; }
    for (int k = 8; k < cnt; k++) { acc += part[slots[start + k]]; }
+   }
    if (d < n_owned) { y[d] = acc; }
    else { yg[d - n_owned] = acc; }
 }
@@ -2327,7 +2346,7 @@ void launch_tpe_pf(int var, const ApplyArgs &a, const Basis1D &b, const double *
 #define ECM2_PF_AF(V, AF)                                                                            \
    hipLaunchKernelGGL((k_apply_tpe_pf<D, Q, MASS, DIFF, SPLIT, V, AF>), grid, block, 0, s, a.ne,    \
                       a.blk_begin, a.blk_end, a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, rowtab, \
-                      a.lane_flags, a.part)
+                      a.lane_flags, a.part, a.pslot)
 #define ECM2_PF(V) ECM2_PF_AF(V, false)
    if (a.kind == QLAYOUT_AFFINE)
    {
@@ -2337,7 +2356,7 @@ void launch_tpe_pf(int var, const ApplyArgs &a, const Basis1D &b, const double *
          // factorised one, 2 = cached qdata loads, 8 = two waves per SIMD, 16 = XCD order
 #define ECM2_SF(V)                                                                                   \
    hipLaunchKernelGGL((k_apply_tpe_sf<D, Q, SPLIT, V>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end, \
-                      a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part)
+                      a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part, a.pslot)
          if (var & 64)
          {
             switch (var & 26)
@@ -2367,7 +2386,7 @@ void launch_tpe_pf(int var, const ApplyArgs &a, const Basis1D &b, const double *
 #define ECM2_PF_AF(V, AF)                                                                            \
    hipLaunchKernelGGL((k_apply_tpe_pf<D, Q, MASS, DIFF, SPLIT, V, AF>), grid, block, 0, s, a.ne,    \
                       a.blk_begin, a.blk_end, a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, rowtab, \
-                      a.lane_flags, a.part)
+                      a.lane_flags, a.part, a.pslot)
 #define ECM2_PF(V) ECM2_PF_AF(V, false)
    switch (var & 27)
    {
@@ -2835,7 +2854,7 @@ static void launch_diag_tpe(const ApplyArgs &a, const Basis1D &b, const double *
    const dim3 grid((nb + 3) / 4), block(256);
 #define ECM2_DIAG(SP, AF)                                                                               \
    hipLaunchKernelGGL((k_diag_tpe<D, Q, MASS, DIFF, SP, AF>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end, \
-                      a.n_owned, a.gmap, a.qdd, a.qdm, a.y, a.yg, b, drow, a.lane_flags, a.part)
+                      a.n_owned, a.gmap, a.qdd, a.qdm, a.y, a.yg, b, drow, a.lane_flags, a.part, a.pslot)
    const bool aff = a.kind == QLAYOUT_AFFINE;
    ECM2_VERIFY(!aff || (MASS && DIFF), ERR_INTERNAL, "AFFINE qdata needs both integrators");
    if (a.yg) { if (aff) { ECM2_DIAG(true, true); } else { ECM2_DIAG(true, false); } }

@@ -292,6 +292,7 @@ def main():
                 # the kernel moves fewer bytes than the SURVEY's fixed formula counts, so
                 # "frac" can exceed 1; this is the bandwidth actually drawn
                 "traffic_gbs": round(traffic / (kavg_ms * 1e-3) / 1e9, 1) if traffic else None,
+                "traffic_frac": round(traffic / (kavg_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4) if traffic else None,
             },
             "cpu_baseline": cpu,
         }

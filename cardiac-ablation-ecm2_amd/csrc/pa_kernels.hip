@@ -865,12 +865,23 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
       for (int k = 0; k < 3; k++) { ce[k] = ld2(qc + k * 128); }
    }
    const double *qa = qdm + (size_t)blk * NQ * 128 + lane * 2;
-   v2d ca[Q], na[Q];
+   // VAR & 4: rows prefetched two ahead (8 KiB per wave in flight instead of 4)
+   constexpr bool DEEP = (VAR & 4) != 0;
+   // VAR & 32: a whole plane prefetched (rows of plane qz + 1 in flight while plane qz
+   // computes: 16 KiB per wave), for one wave per SIMD with the AGPRs as the ring
+   constexpr bool PLANE = (VAR & 32) != 0;
+   v2d ca[Q], na[Q], n2[Q], pb[Q][Q];
    auto load_row = [&](int row, v2d (&aq)[Q]) {
 #pragma unroll
       for (int qx = 0; qx < Q; qx++) { aq[qx] = ld2(qa + (size_t)(row * Q + qx) * 128); }
    };
-   load_row(0, ca);
+   if (PLANE)
+   {
+#pragma unroll
+      for (int qy = 0; qy < Q; qy++) { load_row(qy, pb[qy]); }
+   }
+   else { load_row(0, ca); }
+   if (DEEP) { load_row(1, na); }
 
 #pragma unroll 1
    for (int qz = 0; qz < Q; qz++)
@@ -898,11 +909,8 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
             ZB[dy][dx] = zb; ZG[dy][dx] = zg;
             SB[dy][dx] = 0.0; SG[dy][dx] = 0.0;
          }
-#pragma unroll 1
-      for (int qy = 0; qy < Q; qy++)
-      {
-         const int row = qz * Q + qy;
-         if (row + 1 < NR) { load_row(row + 1, na); }
+      // one row (qz, qy) of Q points: y-forward, x-forward, weighting, x-transpose, y-transpose
+      auto row_body = [&](int qy, const v2d (&cur)[Q]) {
          double Y00[D], Y01[D], Y10[D];
 #pragma unroll
          for (int dx = 0; dx < D; dx++)
@@ -934,7 +942,7 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                uy += bq * Y01[dx];
                uz += bq * Y10[dx];
             }
-            const v2d sa = ca[qx];
+            const v2d sa = cur[qx];
             const double m = sa.y * u;
             const double fx = sa.x * (ce[0].x * ux + ce[0].y * uy + ce[1].x * uz);
             const double fy = sa.x * (ce[0].y * ux + ce[1].y * uy + ce[2].x * uz);
@@ -959,8 +967,34 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                SG[dy][dx] += by * T2[dx];
             }
          }
+      };
+      if constexpr (PLANE)
+      {
+         // the plane's rows are in pb (loaded during the previous plane); each row's
+         // buffer is refilled with the next plane's row right after use
 #pragma unroll
-         for (int qx = 0; qx < Q; qx++) { ca[qx] = na[qx]; }
+         for (int qy = 0; qy < Q; qy++)
+         {
+            row_body(qy, pb[qy]);
+            if (qz + 1 < Q) { load_row((qz + 1) * Q + qy, pb[qy]); }
+         }
+      }
+      else
+      {
+#pragma unroll 1
+      for (int qy = 0; qy < Q; qy++)
+      {
+         const int row = qz * Q + qy;
+         if (DEEP) { if (row + 2 < NR) { load_row(row + 2, n2); } }
+         else if (row + 1 < NR) { load_row(row + 1, na); }
+         row_body(qy, ca);
+#pragma unroll
+         for (int qx = 0; qx < Q; qx++)
+         {
+            ca[qx] = na[qx];
+            if (DEEP) { na[qx] = n2[qx]; }
+         }
+      }
       }
 #pragma unroll
       for (int dz = 0; dz < D; dz++)
@@ -2369,11 +2403,16 @@ void launch_tpe_pf(int var, const ApplyArgs &a, const Basis1D &b, const double *
          }
          else
          {
-            switch (var & 10)
+            switch (var & 14)
             {
                case 2: ECM2_SF(2); break;
                case 8: ECM2_SF(8); break;
-               default: ECM2_SF(0); break;
+               case 12: ECM2_SF(12); break;
+               default:
+                  if (var & 256) { ECM2_SF(4); }  // deep prefetch (bit 256 of the knob)
+                  else if (var & 512) { ECM2_SF(32); }  // plane prefetch (bit 512)
+                  else { ECM2_SF(0); }
+                  break;
             }
          }
 #undef ECM2_SF

@@ -81,10 +81,16 @@ def main():
                     help="1: capture one Mult in a HIP graph and replay it per step (single process)")
     ap.add_argument("--geometry", choices=["compressed", "full"], default="compressed",
                     help="compressed: AFFINE qdata on parallelepiped meshes (default); full: per-point layout")
+    ap.add_argument("--emulate-world", type=int, default=1,
+                    help="measurement aid: run ONE rank (--emulate-rank) of an N-rank partition alone, "
+                         "exchanges replaced by same-size device copies (values not the operator's)")
+    ap.add_argument("--emulate-rank", type=int, default=1)
     ap.add_argument("--loopback", type=int, default=1,
                     help="N>1 on one GPU: N subdomains in this process (validation of the partitioned path)")
     args = ap.parse_args()
 
+    if args.emulate_world > 1:
+        os.environ["ECM2_EMULATE_EXCHANGE"] = "1"
     import torch
     import torch.distributed as dist
 
@@ -108,7 +114,7 @@ def main():
     if args.workload == "c2":
         n = 50
         nx = ny = n
-        nz_total = n * world
+        nz_total = n * max(world, args.emulate_world)
         scaling = "weak"
         workload = f"configs[1]: inline-hex refined to Cartesian 50x50x{nz_total} (50^3 per GPU), H1 p=2, Mass(rho*c)+Diffusion(gamma*dt*k(T)) PA Mult"
     elif args.workload == "c3":
@@ -133,7 +139,7 @@ def main():
     else:
         mesh = E.Mesh.MakeCartesian3D(nx, ny, nz_total, 1.0, ny / nx, nz_total / nx)
         fes = E.H1Space(mesh, order, E.NUMBERING_STRUCTURED)
-    nsub = world if world > 1 else args.loopback
+    nsub = world if world > 1 else max(args.loopback, args.emulate_world)
     mass = lambda a: E.MassIntegrator(E.QuadratureCoefficient(a))
     diff = lambda T: E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(T, K_SCALE, K_SLOPE, K_TREF))
     if nsub <= 1:
@@ -149,10 +155,14 @@ def main():
     else:
         # z-slab partition (CartesianPartitioning along z, mesh.cpp:8966)
         er = E.partition_slabs_z(mesh, nsub)
-        if world > 1:
-            rid = [E.rccl_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(rid, src=0)
-            part = E.Partition(fes, er, rank, world)
+        if world > 1 or args.emulate_world > 1:
+            if args.emulate_world > 1:
+                rid, prank, pworld = [None], args.emulate_rank, args.emulate_world
+            else:
+                rid = [E.rccl_unique_id() if rank == 0 else None]
+                dist.broadcast_object_list(rid, src=0)
+                prank, pworld = rank, world
+            part = E.Partition(fes, er, prank, pworld, decomposition=os.environ.get("ECM2_DECOMP", "overlap"))
             pform = E.ParBilinearForm(part, rccl_id=rid[0], kernel=kernel, scatter=scatter,
                                       compress_geometry=compress)
             alpha, T = bioheat_coefficients(E, torch, mesh, fes, part)
@@ -166,7 +176,7 @@ def main():
             # --loopback: all subdomains in this process on one GPU (exchange by device copies)
             forms, keep = [], []
             for r in range(nsub):
-                part = E.Partition(fes, er, r, nsub)
+                part = E.Partition(fes, er, r, nsub, decomposition=os.environ.get("ECM2_DECOMP", "overlap"))
                 pf = E.ParBilinearForm(part, kernel=kernel, scatter=scatter, compress_geometry=compress)
                 alpha, T = bioheat_coefficients(E, torch, mesh, fes, part)
                 keep += [alpha, T]
@@ -250,7 +260,7 @@ def main():
                 traffic = None
         stream = stream_copy_peak(E, torch)
         cpu = None
-        if not args.no_cpu_baseline and world == 1 and args.loopback <= 1:
+        if not args.no_cpu_baseline and world == 1 and args.loopback <= 1 and args.emulate_world <= 1:
             cpu = cpu_baseline(fes, mesh, alpha, T, args.cpu_baseline_seconds)
         line = {
             "metric": "MDoF/s on PA diffusion+mass Mult, hex p=2; % HBM roofline at 1/2/4/8 GPUs",
@@ -275,7 +285,10 @@ def main():
                 "qdata_layout": qdata_layout(E, timed_forms[0]),
                 "qdata_bytes_stored": qbytes_total / world,
                 "parallelism": f"domain-decomposition z-slabs x{world}, RCCL shared-DoF exchange" if world > 1
-                else (f"loopback z-slabs x{args.loopback} on one GPU" if args.loopback > 1 else "single GPU"),
+                else (f"EMULATED rank {args.emulate_rank} of {args.emulate_world} z-slabs alone on one GPU "
+                      "(exchanges = same-size local copies; measurement aid, not a scaling number)"
+                      if args.emulate_world > 1 else
+                      (f"loopback z-slabs x{args.loopback} on one GPU" if args.loopback > 1 else "single GPU")),
             },
             "roofline": {
                 "bound": "hbm",

@@ -37,6 +37,7 @@ NUMBERING_ENTITY, NUMBERING_STRUCTURED = 0, 1
 ORDER_NATIVE, ORDER_BRICK, ORDER_MORTON = 0, 1, 2
 SCATTER_PARTIALS, SCATTER_ATOMIC = 0, 1
 QLAYOUT_NATIVE, QLAYOUT_BLOCKED, QLAYOUT_AFFINE, QLAYOUT_AFFINE_E = 0, 1, 2, 3  # BilinearForm.info()['layout']
+DECOMP_RAP, DECOMP_OVERLAP = 0, 1  # Partition decomposition
 _SCATTER = {"partials": SCATTER_PARTIALS, "atomic": SCATTER_ATOMIC}
 
 
@@ -488,6 +489,10 @@ _PAR_SIGS = {
     "ecm2_par_form_set_geometry_compression": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ecm2_par_form_qdata_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]),
     "ecm2_par_form_layout": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
+    "ecm2_partition_create_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                                ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "ecm2_partition_decomposition": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                                                    ctypes.POINTER(ctypes.c_int)]),
     "ecm2_par_form_assemble": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "ecm2_par_form_mult": (ctypes.c_int, [ctypes.c_void_p] * 4),
     "ecm2_par_group_mult": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
@@ -548,13 +553,19 @@ class Partition:
     """Local view of one rank: [owned | ghost] local L-vector, [interior | boundary]
     elements, neighbour exchange lists (ParFiniteElementSpace / P)."""
 
-    def __init__(self, fes: H1Space, elem_rank: np.ndarray, rank: int, nranks: int):
+    def __init__(self, fes: H1Space, elem_rank: np.ndarray, rank: int, nranks: int, decomposition: str = "overlap"):
+        """decomposition: "overlap" (owned + ghost elements, one exchange per Mult; default) or
+        "rap" (the reference's P^T A P over owned elements, two exchanges)."""
         lib = _par_lib()
         er = np.ascontiguousarray(elem_rank, np.int32)
         h = ctypes.c_void_p()
-        _check(lib.ecm2_partition_create(fes._h, fes.mesh._h, _np_ptr(er), rank, nranks, ctypes.byref(h)))
+        dec = {"rap": DECOMP_RAP, "overlap": DECOMP_OVERLAP}[decomposition]
+        _check(lib.ecm2_partition_create_ex(fes._h, fes.mesh._h, _np_ptr(er), rank, nranks, dec, ctypes.byref(h)))
         self._h = h
         self.fes, self.rank, self.nranks = fes, rank, nranks
+        d, no = ctypes.c_int(), ctypes.c_int()
+        _check(lib.ecm2_partition_decomposition(h, ctypes.byref(d), ctypes.byref(no)))
+        self.decomposition, self.ne_owned = ("rap", "overlap")[d.value], no.value
         v = [ctypes.c_int() for _ in range(6)]
         _check(lib.ecm2_partition_info(h, *[ctypes.byref(a) for a in v]))
         self.ne_local, self.ne_interior, self.n_owned, self.n_ghost, self.n_nbrs, self.n_send = [a.value for a in v]

@@ -475,6 +475,30 @@ int ecm2_partition_create(const ecm2_h1space *s, const ecm2_mesh *m, const int *
    });
 }
 
+int ecm2_partition_create_ex(const ecm2_h1space *s, const ecm2_mesh *m, const int *elem_rank, int rank,
+                             int nranks, int decomposition, ecm2_partition **out)
+{
+   return guard([&] {
+      NEED(s); NEED(elem_rank); NEED(out);
+      ECM2_VERIFY(decomposition == ECM2_DECOMP_RAP || decomposition == ECM2_DECOMP_OVERLAP, ecm2::ERR_ARG,
+                  "unknown decomposition " << decomposition);
+      std::vector<int> er(elem_rank, elem_rank + s->s.ne);
+      const bool cart = m && m->m.nx > 0 && m->m.ne == s->s.ne;
+      *out = new ecm2_partition{ecm2::build_local_part(s->s, er, rank, nranks, cart ? m->m.nx : 0,
+                                                       cart ? m->m.ny : 0, cart ? m->m.nz : 0,
+                                                       decomposition == ECM2_DECOMP_OVERLAP)};
+   });
+}
+
+int ecm2_partition_decomposition(const ecm2_partition *p, int *decomposition, int *ne_owned)
+{
+   return guard([&] {
+      NEED(p);
+      if (decomposition) { *decomposition = p->p.overlap ? ECM2_DECOMP_OVERLAP : ECM2_DECOMP_RAP; }
+      if (ne_owned) { *ne_owned = p->p.ne_owned; }
+   });
+}
+
 int ecm2_partition_info(const ecm2_partition *p, int *ne_local, int *ne_interior, int *n_owned,
                         int *n_ghost, int *n_nbrs, int *n_send)
 {
@@ -718,7 +742,7 @@ int ecm2_par_form_algorithmic_bytes(const ecm2_par_form *f, double *bytes)
    return guard([&] {
       NEED(f); NEED(bytes);
       // local subdomain: interface dofs counted once per owner copy
-      *bytes = (double)f->f->local().algorithmic_bytes();
+      *bytes = (double)f->f->algorithmic_bytes();
    });
 }
 

@@ -822,7 +822,7 @@ ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, doubl
 }
 
 void PAForm::apply_blocks(const double *x, const double *xg, double *y, double *yg, int b0, int b1,
-                          hipStream_t s)
+                          hipStream_t s, bool latency)
 {
    ECM2_VERIFY(assembled_, ERR_STATE, "apply before Assemble");
    ECM2_VERIFY(resolved_mode_ != KERNEL_UNFUSED, ERR_UNSUPPORTED, "block apply needs a fused kernel");
@@ -834,7 +834,8 @@ void PAForm::apply_blocks(const double *x, const double *xg, double *y, double *
       ECM2_VERIFY(boundary(b0) && boundary(b1), ERR_ARG, "apply_blocks [" << b0 << ", " << b1
                                                           << ") cuts a brick: declare the split with set_block_splits");
    }
-   const ApplyArgs a = apply_args(x, xg, y, yg, b0, b1);
+   ApplyArgs a = apply_args(x, xg, y, yg, b0, b1);
+   a.latency = latency && layout_.kind == QLAYOUT_AFFINE && have_mass_ && have_diff_;
    if (resolved_mode_ == KERNEL_TPE)
    {
       kern::apply_tpe(D_, Q_, have_mass_, have_diff_, a, basis_, rowtab_.data(), s);

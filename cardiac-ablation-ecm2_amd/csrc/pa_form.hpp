@@ -102,8 +102,10 @@ public:
    // Partial scatter: stores the dofs held once, writes the shared ones' partial slots;
    // finish_shared over the shared-dof range [i0, i1) then stores those (the owned
    // shared dofs are [0, n_shared_owned()), the ghost ones [n_shared_owned(), n_shared())).
+   // latency: small block range on a critical path (the p <= 2 AFFINE kernel then gives each
+   // block a workgroup with one quadrature plane per wave).
    void apply_blocks(const double *x, const double *xg, double *y, double *yg, int b0, int b1,
-                     hipStream_t s);
+                     hipStream_t s, bool latency = false);
    void finish_shared(int i0, int i1, double *y, double *yg, hipStream_t s);
    int n_shared() const { return n_sh_; }
    int n_shared_owned() const { return n_sh_owned_; }
@@ -122,6 +124,7 @@ public:
 
    // HIP-event timing of the dominant (apply) kernel.
    void timing_enable(bool on);
+   bool timing_on() const { return timing_; }
    void timing_get(double *total_ms, long *launches);
    size_t algorithmic_bytes() const;
 

@@ -1010,6 +1010,164 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                                                       n_owned, y, yg, part, pslot);
 }
 
+// Latency variant of k_apply_tpe_sf for small block ranges (the distributed Mult's boundary
+// elements, on the critical path of the exchange): one workgroup per 64-element block, its
+// four waves gather the x-values together and take one quadrature plane each (all of the
+// plane's pairs loaded up front), so a block costs one plane's latency instead of four.
+// Waves 1..3 hand their partial outputs to wave 0 through LDS, which adds them in a fixed
+// order (deterministic) and assembles / stores exactly like k_apply_tpe_sf.
+template <int D, int Q, bool SPLIT>
+__global__ void __launch_bounds__(256)
+k_apply_tpe_pp(int ne, int blk_begin, int n_owned, const int *__restrict__ gmap,
+               const double *__restrict__ qdd, const double *__restrict__ qdm,
+               const double *__restrict__ x, const double *__restrict__ xg,
+               double *__restrict__ y, double *__restrict__ yg, const Basis1D b,
+               const int *__restrict__ lane_flags, double *__restrict__ part, const int *__restrict__ pslot)
+{
+   static_assert(Q <= 4, "one plane per wave");
+   constexpr int ND = D * D * D, NQ = Q * Q * Q;
+   __shared__ double sX[ND][64];
+   __shared__ double sY[3][ND][64];
+   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+   const int blk = blk_begin + (int)blockIdx.x;
+   const int e = blk * 64 + lane;
+   const bool active = e < ne;
+   const int *mp = gmap + (size_t)blk * ND * 64 + lane;
+   for (int a = w; a < ND; a += 4)
+   {
+      const int g = mp[a * 64];
+      const int d = bdof(g);
+      const double v = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
+      sX[a][lane] = bneg(g) ? -v : v;
+   }
+   double Yo[ND];
+#pragma unroll
+   for (int a = 0; a < ND; a++) { Yo[a] = 0.0; }
+   const int qz = w;
+   v2d ce[3], pr[Q][Q];
+   if (qz < Q)
+   {
+      const double *qc = qdd + (size_t)blk * 3 * 128 + lane * 2;
+#pragma unroll
+      for (int k = 0; k < 3; k++) { ce[k] = *reinterpret_cast<const v2d *>(qc + k * 128); }
+      const double *qa = qdm + (size_t)blk * NQ * 128 + lane * 2;
+#pragma unroll
+      for (int qy = 0; qy < Q; qy++)
+#pragma unroll
+         for (int qx = 0; qx < Q; qx++)
+         {
+            pr[qy][qx] = __builtin_nontemporal_load(
+               reinterpret_cast<const v2d *>(qa + (size_t)((qz * Q + qy) * Q + qx) * 128));
+         }
+   }
+   __syncthreads();
+   if (qz < Q)
+   {
+      double bz[D], gz[D];
+#pragma unroll
+      for (int dz = 0; dz < D; dz++) { bz[dz] = b.B[qz + MQ * dz]; gz[dz] = b.G[qz + MQ * dz]; }
+      double ZB[D][D], ZG[D][D], SB[D][D], SG[D][D];
+#pragma unroll
+      for (int dy = 0; dy < D; dy++)
+#pragma unroll
+         for (int dx = 0; dx < D; dx++)
+         {
+            double zb = 0.0, zg = 0.0;
+#pragma unroll
+            for (int dz = 0; dz < D; dz++)
+            {
+               const double c = sX[(dz * D + dy) * D + dx][lane];
+               zb += bz[dz] * c;
+               zg += gz[dz] * c;
+            }
+            ZB[dy][dx] = zb; ZG[dy][dx] = zg;
+            SB[dy][dx] = 0.0; SG[dy][dx] = 0.0;
+         }
+#pragma unroll
+      for (int qy = 0; qy < Q; qy++)
+      {
+         double Y00[D], Y01[D], Y10[D];
+#pragma unroll
+         for (int dx = 0; dx < D; dx++)
+         {
+            double u = 0.0, v = 0.0, wv = 0.0;
+#pragma unroll
+            for (int dy = 0; dy < D; dy++)
+            {
+               const double by = b.B[qy + MQ * dy], gy = b.G[qy + MQ * dy];
+               u += by * ZB[dy][dx];
+               v += gy * ZB[dy][dx];
+               wv += by * ZG[dy][dx];
+            }
+            Y00[dx] = u; Y01[dx] = v; Y10[dx] = wv;
+         }
+         double T0[D], T1[D], T2[D];
+#pragma unroll
+         for (int dx = 0; dx < D; dx++) { T0[dx] = 0.0; T1[dx] = 0.0; T2[dx] = 0.0; }
+#pragma unroll
+         for (int qx = 0; qx < Q; qx++)
+         {
+            double u = 0.0, ux = 0.0, uy = 0.0, uz = 0.0;
+#pragma unroll
+            for (int dx = 0; dx < D; dx++)
+            {
+               const double bq = b.B[qx + MQ * dx], gq = b.G[qx + MQ * dx];
+               u += bq * Y00[dx];
+               ux += gq * Y00[dx];
+               uy += bq * Y01[dx];
+               uz += bq * Y10[dx];
+            }
+            const v2d sa = pr[qy][qx];
+            const double m = sa.y * u;
+            const double fx = sa.x * (ce[0].x * ux + ce[0].y * uy + ce[1].x * uz);
+            const double fy = sa.x * (ce[0].y * ux + ce[1].y * uy + ce[2].x * uz);
+            const double fz = sa.x * (ce[1].x * ux + ce[2].x * uy + ce[2].y * uz);
+#pragma unroll
+            for (int dx = 0; dx < D; dx++)
+            {
+               const double bq = b.B[qx + MQ * dx], gq = b.G[qx + MQ * dx];
+               T0[dx] += bq * m + gq * fx;
+               T1[dx] += bq * fy;
+               T2[dx] += bq * fz;
+            }
+         }
+#pragma unroll
+         for (int dy = 0; dy < D; dy++)
+         {
+            const double by = b.B[qy + MQ * dy], gy = b.G[qy + MQ * dy];
+#pragma unroll
+            for (int dx = 0; dx < D; dx++)
+            {
+               SB[dy][dx] += by * T0[dx] + gy * T1[dx];
+               SG[dy][dx] += by * T2[dx];
+            }
+         }
+      }
+#pragma unroll
+      for (int dz = 0; dz < D; dz++)
+#pragma unroll
+         for (int dy = 0; dy < D; dy++)
+#pragma unroll
+            for (int dx = 0; dx < D; dx++)
+            {
+               Yo[(dz * D + dy) * D + dx] = bz[dz] * SB[dy][dx] + gz[dz] * SG[dy][dx];
+            }
+   }
+   if (w > 0)
+   {
+#pragma unroll
+      for (int a = 0; a < ND; a++) { sY[w - 1][a][lane] = Yo[a]; }
+   }
+   __syncthreads();
+   if (w != 0) { return; }
+#pragma unroll
+   for (int k = 0; k < 3; k++)
+#pragma unroll
+      for (int a = 0; a < ND; a++) { Yo[a] += sY[k][a][lane]; }
+   tpe_assemble_store<D, SPLIT, true, false>(Yo, mp, lane_flags[(size_t)blk * 64 + lane], blk, lane, active,
+                                             n_owned, y, yg, part, pslot);
+}
+
 // PA diagonal, thread per element on the blocked layout (PADiffusionDiagonal3D and the
 // mass diagonal, bilininteg_diffusion_kernels.hpp:369, bilininteg_mass_kernels.hpp:325,
 // assembled like AssembleDiagonal's E->L transpose, bilinearform_ext.cpp:370-454):
@@ -2391,7 +2549,13 @@ void launch_tpe_pf(int var, const ApplyArgs &a, const Basis1D &b, const double *
 #define ECM2_SF(V)                                                                                   \
    hipLaunchKernelGGL((k_apply_tpe_sf<D, Q, SPLIT, V>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end, \
                       a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part, a.pslot)
-         if (var & 64)
+         if (a.latency)
+         {
+            hipLaunchKernelGGL((k_apply_tpe_pp<D, Q, SPLIT>), dim3(nb), dim3(256), 0, s, a.ne, a.blk_begin,
+                               a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part,
+                               a.pslot);
+         }
+         else if (var & 64)
          {
             switch (var & 26)
             {

@@ -16,7 +16,9 @@
 #include "pa_form.hpp"
 #include "partition.hpp"
 
+#include <map>
 #include <memory>
+#include <utility>
 #include <vector>
 
 namespace ecm2
@@ -36,6 +38,7 @@ public:
    int true_size() const { return part_.n_owned; }
 
    void assemble(hipStream_t s);
+   size_t algorithmic_bytes() const;
    // y_true = P^T A P x_true (RCCL transport).
    void mult(const double *x_true, double *y_true, hipStream_t s);
    // Diagonal of P^T A P on the true dofs: local PA diagonal, ghost entries summed into
@@ -61,18 +64,39 @@ public:
 
    // buffers (device)
    double *sendbuf() { return sendbuf_.data(); }
+   // P send buffer of neighbour slot k: x_true itself where the rank's owned dofs that
+   // neighbour k ghosts form one contiguous range (z-slabs: the top dof planes), else the
+   // packed buffer.
+   const double *send_ptr(int k, const double *x_true) const
+   {
+      return send_start_[k] >= 0 ? x_true + send_start_[k] : sendbuf_.data() + part_.send_off[k];
+   }
    double *xghost() { return xg_.data(); }
    double *yghost() { return yg_.data(); }
    double *recvbuf() { return rbuf_.data(); }
 
 private:
    void rccl_exchange(bool transpose);  // P (false) or P^T (true) on the comm stream
+   void mult_stages(const double *x_true, double *y_true, hipStream_t s, bool emu);
+   int b_int() const { return part_.ne_interior / kElemBlock; }
+   int b_split_ = 0;
+   std::vector<int> send_start_;        // per neighbour: first owned index of a contiguous send range, or -1
+   bool pack_needed_ = true;            // some neighbour's send range is not contiguous
+   const double *x_cur_ = nullptr;      // x_true of the Mult being enqueued (contiguous sends)                    // interior part A = [0, b_split_) (0: no split)
+   hipEvent_t ev_bnd_ = nullptr;        // boundary elements applied (comm stream)
+   // Mult as a HIP graph per (x, y) pair: one launch instead of ~15 API calls
+   hipStream_t cap_ = nullptr;          // capture stream
+   std::map<std::pair<const double *, double *>, hipGraphExec_t> graphs_;
+   bool graph_failed_ = false;
    LocalPart part_;
    std::unique_ptr<PAForm> local_;
    DeviceArray<int> send_idx_;
    DeviceArray<double> sendbuf_, xg_, yg_, rbuf_, dl_;
    void *comm_ = nullptr;  // ncclComm_t
+   void self_exchange(bool transpose);  // ECM2_EMULATE_EXCHANGE measurement aid
    hipStream_t cs_ = nullptr;
+   hipStream_t is_ = nullptr;       // interior stream, CU-masked against cs_ (null: interior on the caller's stream)
+   hipEvent_t ev_s_ = nullptr, ev_int_ = nullptr;
    hipEvent_t ev_pack_ = nullptr, ev_xg_ = nullptr, ev_yg_ = nullptr, ev_done_ = nullptr;
 };
 

@@ -25,7 +25,7 @@ std::vector<int> partition_slabs_z(const HexMesh &m, int nranks)
 }
 
 LocalPart build_local_part(const H1Space &s, const std::vector<int> &elem_rank, int rank, int nranks,
-                           int nx, int ny, int nz)
+                           int nx, int ny, int nz, bool overlap)
 {
    ECM2_VERIFY((int)elem_rank.size() == s.ne, ERR_ARG, "elem_rank size " << elem_rank.size() << " != ne " << s.ne);
    ECM2_VERIFY(nranks >= 1 && nranks <= 64, ERR_UNSUPPORTED, "1..64 ranks supported");
@@ -33,6 +33,7 @@ LocalPart build_local_part(const H1Space &s, const std::vector<int> &elem_rank, 
    LocalPart p;
    p.rank = rank;
    p.nranks = nranks;
+   p.overlap = overlap;
    p.order = s.order;
    p.nd = s.nd;
    const int nd = s.nd;
@@ -50,11 +51,30 @@ LocalPart build_local_part(const H1Space &s, const std::vector<int> &elem_rank, 
    }
    auto owner = [&](int g) { return __builtin_ctzll(touch[g]); };
    const uint64_t me = 1ull << rank;
+   auto dofg = [](int g) { return g >= 0 ? g : -1 - g; };
+   // local elements of each rank: owned ones, plus (OVERLAP) every element touching a dof the
+   // rank owns; need[g] = ranks whose local elements touch dof g
+   auto is_local = [&](int e, int r) {
+      if (elem_rank[e] == r) { return true; }
+      if (!overlap) { return false; }
+      for (int a = 0; a < nd; a++) { if (owner(dofg(s.gather_map[(size_t)e * nd + a])) == r) { return true; } }
+      return false;
+   };
+   std::vector<uint64_t> need(touch);
+   if (overlap)
+   {
+      for (int e = 0; e < s.ne; e++)
+      {
+         uint64_t ranks = 0;  // owners of e's dofs: e is local to each of them
+         for (int a = 0; a < nd; a++) { ranks |= 1ull << owner(dofg(s.gather_map[(size_t)e * nd + a])); }
+         for (int a = 0; a < nd; a++) { need[dofg(s.gather_map[(size_t)e * nd + a])] |= ranks; }
+      }
+   }
    // local dofs
    std::vector<int> owned, ghost;
    for (int g = 0; g < s.ndofs; g++)
    {
-      if (!(touch[g] & me)) { continue; }
+      if (!(need[g] & me)) { continue; }
       if (owner(g) == rank) { owned.push_back(g); }
       else { ghost.push_back(g); }
    }
@@ -67,7 +87,7 @@ LocalPart build_local_part(const H1Space &s, const std::vector<int> &elem_rank, 
    for (int i = 0; i < (int)p.local_to_global.size(); i++) { g2l[p.local_to_global[i]] = i; }
    // neighbours: ranks that own my ghosts or ghost my owned dofs
    uint64_t nb = 0;
-   for (int g : owned) { nb |= touch[g] & ~me; }
+   for (int g : owned) { nb |= need[g] & ~me; }
    for (int g : ghost) { nb |= 1ull << owner(g); }
    for (int r = 0; r < nranks; r++) { if (nb & (1ull << r)) { p.nbrs.push_back(r); } }
    p.send_off.assign(1, 0);
@@ -76,7 +96,7 @@ LocalPart build_local_part(const H1Space &s, const std::vector<int> &elem_rank, 
    {
       for (int i = 0; i < p.n_owned; i++)
       {
-         if (touch[owned[i]] & (1ull << r)) { p.send_idx.push_back(i); }
+         if (need[owned[i]] & (1ull << r)) { p.send_idx.push_back(i); }
       }
       p.send_off.push_back((int)p.send_idx.size());
       int cnt = 0;
@@ -87,7 +107,8 @@ LocalPart build_local_part(const H1Space &s, const std::vector<int> &elem_rank, 
    std::vector<int> interior, boundary;
    for (int e = 0; e < s.ne; e++)
    {
-      if (elem_rank[e] != rank) { continue; }
+      if (!is_local(e, rank)) { continue; }
+      p.ne_owned += elem_rank[e] == rank;
       bool bnd = false;
       for (int a = 0; a < nd && !bnd; a++)
       {

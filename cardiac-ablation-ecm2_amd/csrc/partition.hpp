@@ -9,6 +9,17 @@
 // Local L-vector layout: [owned (by global id) | ghost (grouped by owner rank, then by
 // global id)], so the true vector is the prefix and each neighbour's ghost block is a
 // contiguous range (received in place, sent in place).
+//
+// Two decompositions:
+//  * RAP (the reference's): the rank's local elements are the elements it owns; a Mult is
+//    P (owners -> ghost copies), the local PA operator, P^T (ghost contributions summed
+//    into the owners).
+//  * OVERLAP: the local elements are the owned ones plus every other element touching an
+//    owned dof (one element layer per interface); a rank then computes each owned dof's
+//    complete sum itself, so a Mult is P, the local operator, and nothing else -- one
+//    exchange instead of two, and the owner sums all contributions in a fixed order.  The
+//    ghost elements' outputs to non-owned dofs are discarded.  Same y as RAP (any
+//    summation order differs only by rounding).
 #pragma once
 
 #include "mesh.hpp"
@@ -22,6 +33,8 @@ struct LocalPart
 {
    int rank = 0, nranks = 1, order = 1, nd = 0;
    int ne_local = 0, ne_interior = 0;   // local elements ordered [interior | boundary]
+   int ne_owned = 0;                    // elements owned by this rank (ne_local - ghost elements)
+   bool overlap = false;                // OVERLAP decomposition (no P^T)
    int n_owned = 0, n_ghost = 0;
    std::vector<int> elems;              // global element ids in local order
    std::vector<int> local_to_global;    // [n_owned + n_ghost]
@@ -38,6 +51,6 @@ std::vector<int> partition_slabs_z(const HexMesh &m, int nranks);
 // nx > 0: the global mesh is a lexicographic nx x ny x nz Cartesian mesh; interior and
 // boundary element groups are then each put in brick order (one 4x4x4 brick per wave).
 LocalPart build_local_part(const H1Space &s, const std::vector<int> &elem_rank, int rank, int nranks,
-                           int nx = 0, int ny = 0, int nz = 0);
+                           int nx = 0, int ny = 0, int nz = 0, bool overlap = false);
 
 } // namespace ecm2

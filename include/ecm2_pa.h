@@ -258,6 +258,17 @@ int ecm2_partition_slabs_z(const ecm2_mesh *m, int nranks, int *elem_rank);
  * NULL): when it is a Cartesian mesh the local element groups are put in brick order. */
 int ecm2_partition_create(const ecm2_h1space *s, const ecm2_mesh *m, const int *elem_rank, int rank,
                           int nranks, ecm2_partition **out);
+/* As ecm2_partition_create with a choice of decomposition: ECM2_DECOMP_RAP (the
+ * reference's: local elements = owned elements, Mult = P, local PA, P^T) or
+ * ECM2_DECOMP_OVERLAP (local elements = owned elements + every element touching an owned
+ * dof, Mult = P, local PA; no P^T -- one exchange per Mult instead of two, the ghost
+ * elements' outputs to non-owned dofs discarded; same operator). */
+#define ECM2_DECOMP_RAP 0
+#define ECM2_DECOMP_OVERLAP 1
+int ecm2_partition_create_ex(const ecm2_h1space *s, const ecm2_mesh *m, const int *elem_rank, int rank,
+                             int nranks, int decomposition, ecm2_partition **out);
+/* Decomposition and the number of elements the rank owns (ne_local minus ghost elements). */
+int ecm2_partition_decomposition(const ecm2_partition *p, int *decomposition, int *ne_owned);
 int ecm2_partition_info(const ecm2_partition *p, int *ne_local, int *ne_interior, int *n_owned,
                         int *n_ghost, int *n_nbrs, int *n_send);
 /* Any output may be NULL. elems [ne_local] (global ids, local order), local_to_global

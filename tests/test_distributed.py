@@ -1,4 +1,6 @@
-"""Distributed path: y_true = P^T A_local P x_true over an element partition.
+"""Distributed path: y_true = P^T A_local P x_true over an element partition
+(RAP, the reference's decomposition), or y_true = R_owned A_local P x_true with ghost elements
+(OVERLAP: one exchange per Mult).
 
 CPU (gloo, world_size 2 and 3): every rank builds its local part with the product's
 partitioner, applies the ORACLE local operator to its [owned | ghost] L-vector, and runs
@@ -41,14 +43,28 @@ def _elem_rank(m, kind, nranks):
 
 @pytest.mark.parametrize("kind", ["cart", "fichera"])
 @pytest.mark.parametrize("nranks", [2, 3, 4])
-def test_partition_invariants(kind, nranks):
+@pytest.mark.parametrize("decomp", ["rap", "overlap"])
+def test_partition_invariants(kind, nranks, decomp):
     m = _mesh(kind)
     fes = E.H1Space(m, 2)
     er = _elem_rank(m, kind, nranks)
-    parts = [E.Partition(fes, er, r, nranks) for r in range(nranks)]
+    parts = [E.Partition(fes, er, r, nranks, decomposition=decomp) for r in range(nranks)]
     owned = np.concatenate([p.owned_global for p in parts])
     assert np.array_equal(np.sort(owned), np.arange(fes.ndofs))         # each dof owned once
-    assert sum(p.ne_local for p in parts) == fes.ne
+    assert sum(p.ne_owned for p in parts) == fes.ne
+    gm = fes.gather_map()
+    for p in parts:
+        assert p.decomposition == decomp
+        if decomp == "rap":
+            assert p.ne_local == p.ne_owned
+            assert np.all(er[p.elems] == p.rank)
+        else:
+            # local elements = owned ones + every element touching an owned dof
+            own = np.zeros(fes.ndofs, bool)
+            own[p.owned_global] = True
+            want = np.nonzero((er == p.rank) | own[gm].any(axis=1))[0]
+            assert np.array_equal(np.sort(p.elems), want)
+            assert int((er[p.elems] == p.rank).sum()) == p.ne_owned
     for p in parts:
         assert np.all(np.diff(p.owned_global) > 0)
         assert np.all(p.gather_map >= 0) and np.all(p.gather_map < p.n_owned + p.n_ghost)
@@ -63,7 +79,7 @@ def test_partition_invariants(kind, nranks):
             assert np.array_equal(mine, theirs)
 
 
-def _worker(rank, nranks, port, kind, result_path):
+def _worker(rank, nranks, port, kind, result_path, decomp="rap"):
     import torch.distributed as dist
     import torch
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -74,7 +90,7 @@ def _worker(rank, nranks, port, kind, result_path):
         order = 2
         fes = E.H1Space(m, order)
         er = _elem_rank(m, kind, nranks)
-        part = E.Partition(fes, er, rank, nranks)
+        part = E.Partition(fes, er, rank, nranks, decomposition=decomp)
         q1d = O.default_q1d(order)
         en = m.element_nodes()[part.elems]
         P = O.quad_points(en, q1d)
@@ -101,10 +117,10 @@ def _worker(rank, nranks, port, kind, result_path):
         for k, r in bufs:
             xl[part.n_owned + part.recv_off[k]: part.n_owned + part.recv_off[k + 1]] = r.numpy()
         yl = op.mult(xl)
-        # P^T: ghosts -> owners (added)
         y_true = yl[: part.n_owned].copy()
         reqs, bufs = [], []
-        for k, nb in enumerate(part.nbrs):
+        # P^T: ghosts -> owners (added); OVERLAP: the owned sums are complete already
+        for k, nb in enumerate(part.nbrs if decomp == "rap" else []):
             s = torch.from_numpy(yl[part.n_owned + part.recv_off[k]: part.n_owned + part.recv_off[k + 1]].copy())
             r = torch.empty(int(part.send_off[k + 1] - part.send_off[k]), dtype=torch.float64)
             bufs.append((k, r))
@@ -139,10 +155,11 @@ def _free_port():
 
 
 @pytest.mark.parametrize("kind,nranks", [("cart", 2), ("fichera", 3)])
-def test_gloo_exchange_matches_serial(tmp_path, kind, nranks):
+@pytest.mark.parametrize("decomp", ["rap", "overlap"])
+def test_gloo_exchange_matches_serial(tmp_path, kind, nranks, decomp):
     import torch.multiprocessing as mp
     out = str(tmp_path / "err.npy")
-    mp.spawn(_worker, args=(nranks, _free_port(), kind, out), nprocs=nranks, join=True)
+    mp.spawn(_worker, args=(nranks, _free_port(), kind, out, decomp), nprocs=nranks, join=True)
     assert float(np.load(out)[0]) <= RTOL
 
 
@@ -151,7 +168,8 @@ def test_gloo_exchange_matches_serial(tmp_path, kind, nranks):
                                                ("fichera", 4, 3), ("cart", 4, 2), ("cart", 2, 4),
                                                ("cart_big", 2, 3), ("cart_big", 3, 4)])
 @pytest.mark.parametrize("scatter", ["partials", "atomic"])
-def test_gpu_loopback_group_matches_serial(kind, nranks, order, scatter):
+@pytest.mark.parametrize("decomp", ["rap", "overlap"])
+def test_gpu_loopback_group_matches_serial(kind, nranks, order, scatter, decomp):
     import torch
     m = _mesh(kind)
     fes = E.H1Space(m, order)
@@ -160,7 +178,7 @@ def test_gpu_loopback_group_matches_serial(kind, nranks, order, scatter):
     forms, xs, ys, parts = [], [], [], []
     xg = np.random.default_rng(1).uniform(-1, 1, fes.ndofs)
     for r in range(nranks):
-        part = E.Partition(fes, er, r, nranks)
+        part = E.Partition(fes, er, r, nranks, decomposition=decomp)
         pf = E.ParBilinearForm(part, scatter=scatter)
         P = E.quadrature_points_subset(m, q1d, part.elems)
         c = torch.as_tensor(coeff_function(P).reshape(part.ne_local, -1)).cuda()

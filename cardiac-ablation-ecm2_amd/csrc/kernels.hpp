@@ -138,9 +138,12 @@ void setup_from_nodes(const QLayout &L, int Q, const double *enodes, const doubl
                       double *qd_diff, double *qd_mass, hipStream_t s);
 // AFFINE / AFFINE_E layout (see above) from the corners of parallelepiped elements; needs both
 // coefficients (cm, cd non-null).
-void setup_affine(const QLayout &L, int Q, const double *enodes, const double *W, const CoeffDesc *cm,
-                  const CoeffDesc *cd, const double *cm_q, const double *cd_q, double *qd_fac,
-                  double *qd_pair, hipStream_t s);
+// J (optional, device, MFEM layout NQ x 3 x 3 x NE) replaces the corners.
+void setup_affine(const QLayout &L, int Q, const double *enodes, const double *J, const double *W,
+                  const CoeffDesc *cm, const CoeffDesc *cd, const double *cm_q, const double *cd_q,
+                  double *qd_fac, double *qd_pair, hipStream_t s);
+// Every element's Jacobian the same at all its points (1e-13 relative; synchronises s).
+bool jacobians_affine(int ne, int nq, const double *J, hipStream_t s);
 // qdata from MFEM-layout Jacobians J(q,i,j,e) (GeometricFactors::JACOBIANS).
 void setup_from_jacobians(const QLayout &L, const double *J, const double *W,
                           const CoeffDesc *cm, const CoeffDesc *cd,

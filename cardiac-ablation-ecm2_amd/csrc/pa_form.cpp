@@ -346,7 +346,12 @@ void PAForm::assemble(hipStream_t s)
    ECM2_VERIFY(resolved_mode_ != KERNEL_LINE || kern::has_line(D_, Q_), ERR_UNSUPPORTED,
                "line kernel needs Q1D in {D1D, D1D+1} and Q1D <= 8");
    layout_.kind = (resolved_mode_ == KERNEL_TPE) ? QLAYOUT_BLOCKED : QLAYOUT_NATIVE;
-   if (affine_ && compress_ && affine_env() && !jac_ && have_mass_ && have_diff_)
+   bool affine = affine_;
+   if (jac_ && compress_ && affine_env() && have_mass_ && have_diff_ && (resolved_mode_ == KERNEL_TPE || resolved_mode_ == KERNEL_LINE))
+   {
+      affine = kern::jacobians_affine(ne_, NQ_, jac_, s);  // the reference binding's geometry
+   }
+   if (affine && compress_ && affine_env() && have_mass_ && have_diff_)
    {
       if (resolved_mode_ == KERNEL_TPE) { layout_.kind = QLAYOUT_AFFINE; }
       else if (resolved_mode_ == KERNEL_LINE) { layout_.kind = QLAYOUT_AFFINE_E; }
@@ -638,8 +643,8 @@ void PAForm::assemble(hipStream_t s)
    const CoeffDesc *cd = have_diff_ ? &cdiff_ : nullptr;
    if (layout_.affine())
    {
-      kern::setup_affine(layout_, Q_, enodes_.data(), W_.data(), cm, cd, cm_q, cd_q, qd_diff_.data(),
-                         qd_mass_.data(), s);
+      kern::setup_affine(layout_, Q_, jac_ ? nullptr : enodes_.data(), jac_, W_.data(), cm, cd, cm_q, cd_q,
+                         qd_diff_.data(), qd_mass_.data(), s);
    }
    else if (jac_)
    {

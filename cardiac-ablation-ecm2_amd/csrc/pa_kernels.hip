@@ -290,6 +290,23 @@ k_setup_nodes_t(const int *__restrict__ perm, int ne, const double *__restrict__
    }
 }
 
+// Affinity of MFEM-layout Jacobians: flag[0] = 1 when some point's J differs from its
+// element's first point's by more than 1e-13 of that J's largest entry.
+__global__ void k_jac_affine_check(int ne, int NQ, const double *__restrict__ Jg, int *__restrict__ flag)
+{
+   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   if (t >= (long)ne * NQ) { return; }
+   const int e = (int)(t / NQ), q = (int)(t % NQ);
+   double mx = 0.0, dv = 0.0;
+   for (int c = 0; c < 9; c++)
+   {
+      const double j0 = Jg[((size_t)e * 9 + c) * NQ], jq = Jg[((size_t)e * 9 + c) * NQ + q];
+      mx = fmax(mx, fabs(j0));
+      dv = fmax(dv, fabs(jq - j0));
+   }
+   if (!(dv <= 1e-13 * mx)) { flag[0] = 1; }
+}
+
 __global__ void k_setup_jac(const int *__restrict__ pos, int kind, int ne, int NQ, const double *__restrict__ Jg,
                             const double *__restrict__ W, SetupCoef cm, SetupCoef cd,
                             double *__restrict__ qd_diff, double *__restrict__ qd_mass)
@@ -310,9 +327,12 @@ __global__ void k_setup_jac(const int *__restrict__ pos, int kind, int ne, int N
 // setup's (bilininteg_mass_pa.cpp:76) with the per-point factors W_q beta_q / W_q alpha_q kept
 // apart from the element's C = adj(J) adj(J)^T / det J.  Threads over (blk, q, lane), lane
 // fastest: each wave stores 1 KiB of pairs per point; the q = 0 threads store C.
+// Jg (optional): MFEM-layout Jacobians J(q,i,j,e) instead of corners; the element's J is
+// its first point's (all points agree for an affine element: checked by k_jac_affine_check).
 template <int Q, bool BLOCKED>
 __global__ void __launch_bounds__(256)
 k_setup_affine(const int *__restrict__ perm, int ne, const double *__restrict__ enodes,
+               const double *__restrict__ Jg,
                const double *__restrict__ W, SetupCoef cm, SetupCoef cd, double *__restrict__ qd_fac,
                double *__restrict__ qd_pair)
 {
@@ -339,14 +359,24 @@ k_setup_affine(const int *__restrict__ perm, int ne, const double *__restrict__ 
       lane = 0;
       blk = 0;
    }
-   const double *X = enodes + (size_t)e * 24;
    double J[3][3];
-#pragma unroll
-   for (int i = 0; i < 3; i++)
+   if (Jg)
    {
-      J[i][0] = X[i * 8 + 1] - X[i * 8];
-      J[i][1] = X[i * 8 + 2] - X[i * 8];
-      J[i][2] = X[i * 8 + 4] - X[i * 8];
+#pragma unroll
+      for (int j = 0; j < 3; j++)
+#pragma unroll
+         for (int i = 0; i < 3; i++) { J[i][j] = Jg[(((size_t)e * 3 + j) * 3 + i) * NQ]; }
+   }
+   else
+   {
+      const double *X = enodes + (size_t)e * 24;
+#pragma unroll
+      for (int i = 0; i < 3; i++)
+      {
+         J[i][0] = X[i * 8 + 1] - X[i * 8];
+         J[i][1] = X[i * 8 + 2] - X[i * 8];
+         J[i][2] = X[i * 8 + 4] - X[i * 8];
+      }
    }
    const double J11 = J[0][0], J21 = J[1][0], J31 = J[2][0];
    const double J12 = J[0][1], J22 = J[1][1], J32 = J[2][1];
@@ -2746,9 +2776,24 @@ void setup_from_nodes(const QLayout &L, int Q, const double *enodes, const doubl
    ECM2_HIP(hipGetLastError());
 }
 
-void setup_affine(const QLayout &L, int Q, const double *enodes, const double *W, const CoeffDesc *cm,
-                  const CoeffDesc *cd, const double *cm_q, const double *cd_q, double *qd_fac,
-                  double *qd_pair, hipStream_t s)
+bool jacobians_affine(int ne, int nq, const double *J, hipStream_t s)
+{
+   if (ne == 0) { return true; }
+   DeviceArray<int> flag;
+   flag.resize(1);
+   ECM2_HIP(hipMemsetAsync(flag.data(), 0, sizeof(int), s));
+   const long n = (long)ne * nq;
+   hipLaunchKernelGGL(k_jac_affine_check, dim3(grid_for(n, 256)), dim3(256), 0, s, ne, nq, J, flag.data());
+   ECM2_HIP(hipGetLastError());
+   int h = 1;
+   ECM2_HIP(hipMemcpyAsync(&h, flag.data(), sizeof(int), hipMemcpyDeviceToHost, s));
+   ECM2_HIP(hipStreamSynchronize(s));
+   return h == 0;
+}
+
+void setup_affine(const QLayout &L, int Q, const double *enodes, const double *J, const double *W,
+                  const CoeffDesc *cm, const CoeffDesc *cd, const double *cm_q, const double *cd_q,
+                  double *qd_fac, double *qd_pair, hipStream_t s)
 {
    if (L.ne == 0) { return; }
    ECM2_VERIFY(L.affine() && cm && cd, ERR_INTERNAL, "affine setup needs an AFFINE layout and both coefficients");
@@ -2762,12 +2807,12 @@ void setup_affine(const QLayout &L, int Q, const double *enodes, const double *W
       if (blk)                                                                                           \
       {                                                                                                  \
          hipLaunchKernelGGL((k_setup_affine<QQ, true>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.perm, L.ne, \
-                            enodes, W, scm, scd, qd_fac, qd_pair);                                       \
+                            enodes, J, W, scm, scd, qd_fac, qd_pair);                                    \
       }                                                                                                  \
       else                                                                                               \
       {                                                                                                  \
          hipLaunchKernelGGL((k_setup_affine<QQ, false>), dim3(grid_for(n, 256)), dim3(256), 0, s, nullptr, L.ne, \
-                            enodes, W, scm, scd, qd_fac, qd_pair);                                       \
+                            enodes, J, W, scm, scd, qd_fac, qd_pair);                                    \
       }                                                                                                  \
       ECM2_HIP(hipGetLastError());                                                                       \
       return;                                                                                            \

@@ -135,10 +135,13 @@ def test_qdata_matches_reference_setup(kernel, order):
     assert relerr(qm, op.M) < 1e-13
 
 
-def test_jacobian_geometry_path():
-    """set_jacobians (GeometricFactors layout) gives the same operator as element nodes."""
-    m = make_mesh("nonaligned")
-    order = 2
+@pytest.mark.parametrize("mesh_name,order", [("nonaligned", 2), ("trilinear", 2), ("nonaligned", 4),
+                                              ("trilinear", 3)])
+def test_jacobian_geometry_path(mesh_name, order):
+    """set_jacobians (GeometricFactors layout -- what the reference-side binding passes) gives
+    the same operator as element nodes; affine Jacobians (constant per element, checked on
+    the device) select the compressed layout, trilinear ones keep the full one."""
+    m = make_mesh(mesh_name)
     fes = E.H1Space(m, order)
     en = m.element_nodes()
     q1d = O.default_q1d(order)
@@ -149,10 +152,17 @@ def test_jacobian_geometry_path():
     form.AddDomainIntegrator(E.DiffusionIntegrator(E.ConstantCoefficient(0.5)))
     form.Assemble()
     op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=3.0, beta=0.5)
+    affine = mesh_name != "trilinear"
+    want = (E.QLAYOUT_AFFINE if order <= 2 else E.QLAYOUT_AFFINE_E) if affine else \
+        (E.QLAYOUT_BLOCKED if order <= 2 else E.QLAYOUT_NATIVE)
+    assert form.info()["layout"] == want
     x = np.random.default_rng(5).uniform(-1, 1, fes.ndofs)
     y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
     form.Mult(dev(x), y)
     assert relerr(host(y), op.mult(x)) <= RTOL
+    d = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    form.AssembleDiagonal(d)
+    assert relerr(host(d), op.diagonal()) < 1e-13
 
 
 @pytest.mark.parametrize("order", [1, 2, 4])

@@ -489,6 +489,7 @@ _PAR_SIGS = {
     "ecm2_par_form_set_geometry_compression": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ecm2_par_form_qdata_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]),
     "ecm2_par_form_layout": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
+    "ecm2_rccl_p2p_selftest": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
     "ecm2_partition_create_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                                 ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "ecm2_partition_decomposition": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
@@ -590,6 +591,13 @@ class Partition:
     @property
     def owned_global(self):
         return self.local_to_global[: self.n_owned]
+
+
+def rccl_p2p_selftest(graph: bool, n: int = 4096) -> float:
+    """Max error of a one-rank RCCL self send/recv, direct or graph-captured."""
+    e = ctypes.c_double()
+    _check(_par_lib().ecm2_rccl_p2p_selftest(1 if graph else 0, n, ctypes.byref(e)))
+    return e.value
 
 
 def rccl_unique_id() -> bytes:

@@ -578,6 +578,15 @@ int ecm2_par_form_set_scatter(ecm2_par_form *f, int mode)
    return guard([&] { NEED(f); f->f->local().set_scatter(mode); });
 }
 
+int ecm2_rccl_p2p_selftest(int graph, int n, double *max_err)
+{
+   return guard([&] {
+      NEED(max_err);
+      ECM2_VERIFY(n >= 1, ecm2::ERR_ARG, "n >= 1");
+      *max_err = ecm2::rccl_p2p_selftest(graph != 0, n);
+   });
+}
+
 int ecm2_par_form_set_geometry_compression(ecm2_par_form *f, int on)
 {
    return guard([&] { NEED(f); f->f->local().set_geometry_compression(on != 0); });

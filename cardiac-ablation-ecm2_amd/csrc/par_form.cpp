@@ -4,6 +4,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -24,6 +25,59 @@ void rccl_unique_id(unsigned char *out)
    ECM2_NCCL(ncclGetUniqueId(&id));
    static_assert(sizeof(id) == 128, "ncclUniqueId size");
    std::memcpy(out, &id, sizeof(id));
+}
+
+// Transport self-test: a one-rank communicator exchanging n doubles with itself through
+// grouped ncclSend/ncclRecv, launched directly or captured in a HIP graph and replayed
+// three times (the form's graph-captured Mult relies on RCCL point-to-point capture).
+double rccl_p2p_selftest(bool graph, int n)
+{
+   ncclUniqueId id;
+   ECM2_NCCL(ncclGetUniqueId(&id));
+   ncclComm_t comm;
+   ECM2_NCCL(ncclCommInitRank(&comm, 1, id, 0));
+   hipStream_t st;
+   ECM2_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+   DeviceArray<double> a, b;
+   a.resize(std::max(1, n));
+   b.resize(std::max(1, n));
+   std::vector<double> h(std::max(1, n));
+   double err = 0.0;
+   for (int rep = 0; rep < 3; rep++)
+   {
+      for (int i = 0; i < n; i++) { h[i] = 0.5 * i + rep; }
+      ECM2_HIP(hipMemcpy(a.data(), h.data(), sizeof(double) * n, hipMemcpyHostToDevice));
+      ECM2_HIP(hipMemset(b.data(), 0, sizeof(double) * n));
+      auto exchange = [&] {
+         ECM2_NCCL(ncclGroupStart());
+         ECM2_NCCL(ncclSend(a.data(), n, ncclFloat64, 0, comm, st));
+         ECM2_NCCL(ncclRecv(b.data(), n, ncclFloat64, 0, comm, st));
+         ECM2_NCCL(ncclGroupEnd());
+      };
+      static hipGraphExec_t ge = nullptr;
+      if (graph)
+      {
+         if (rep == 0)
+         {
+            hipGraph_t g = nullptr;
+            ECM2_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+            exchange();
+            ECM2_HIP(hipStreamEndCapture(st, &g));
+            ECM2_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+            ECM2_HIP(hipGraphDestroy(g));
+         }
+         ECM2_HIP(hipGraphLaunch(ge, st));
+      }
+      else { exchange(); }
+      ECM2_HIP(hipStreamSynchronize(st));
+      std::vector<double> r(std::max(1, n));
+      ECM2_HIP(hipMemcpy(r.data(), b.data(), sizeof(double) * n, hipMemcpyDeviceToHost));
+      for (int i = 0; i < n; i++) { err = std::max(err, std::fabs(r[i] - h[i])); }
+      if (graph && rep == 2) { ECM2_HIP(hipGraphExecDestroy(ge)); ge = nullptr; }
+   }
+   ECM2_HIP(hipStreamDestroy(st));
+   (void)ncclCommDestroy(comm);
+   return err;
 }
 
 // CUs reserved for the comm stream (RCCL kernels, boundary elements, ghost sums): the

@@ -100,6 +100,9 @@ private:
    hipEvent_t ev_pack_ = nullptr, ev_xg_ = nullptr, ev_yg_ = nullptr, ev_done_ = nullptr;
 };
 
+// RCCL point-to-point self-test (one-rank communicator, direct or graph-captured): max error.
+double rccl_p2p_selftest(bool graph, int n);
+
 // In-process loopback group: all subdomains on one GPU, exchanges by device copies.
 // Exercises partition, pack/unpack, split-vector kernels and interior/boundary
 // ordering without RCCL (which cannot put two ranks on one device).

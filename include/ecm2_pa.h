@@ -282,6 +282,10 @@ void ecm2_partition_destroy(ecm2_partition *p);
 /* ncclGetUniqueId (128 bytes) for ecm2_par_form_create; broadcast it to all ranks (the
  * reference's communicator is the ParMesh's MPI_Comm, pmesh.hpp:33). */
 int ecm2_rccl_unique_id(unsigned char *id128);
+/* Transport self-test (no reference counterpart): a one-rank communicator sends n doubles to
+ * itself with grouped ncclSend/ncclRecv, directly (graph = 0) or captured in a HIP graph and
+ * replayed (graph = 1, what ecm2_par_form_mult does); *max_err = max |received - sent|. */
+int ecm2_rccl_p2p_selftest(int graph, int n, double *max_err);
 /* ParBilinearForm(pfes) + SetAssemblyLevel(PARTIAL) (pbilinearform.hpp, bilinearform.cpp:
  * 109-136) on the rank's local space.  enodes_local: host [ne_local][3][8] in the
  * partition's local element order.

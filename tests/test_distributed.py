@@ -248,3 +248,13 @@ def test_gpu_rccl_single_rank_transport(order):
     ss[part.owned_global] = sol.cpu().numpy()
     assert abs(it - itr) <= 2
     assert relerr(ss, xr) < 1e-9
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph", [False, True])
+def test_gpu_rccl_p2p_graph_capture(graph):
+    """RCCL point-to-point (grouped ncclSend/ncclRecv, here a one-rank communicator talking to
+    itself) both launched directly and captured in a HIP graph and replayed -- the mechanism
+    of the distributed Mult's graph replay."""
+    E.load_library()
+    assert E.rccl_p2p_selftest(graph, 10201) == 0.0

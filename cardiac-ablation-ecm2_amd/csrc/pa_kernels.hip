@@ -2044,7 +2044,22 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
    // qdata of the (element, qx, qy) column this lane weights in stage 3: in flight
    // during the gather and the x / y contractions
    double qv[7][Q];
-   if (!(VAR & 1) && t < NE * QQ)
+   // AFFINE_E (VAR & 64): the raw per-point pairs and the element's C stay in registers until
+   // the z stage (forming the 6 entries at load time would make the wave wait for the loads
+   // at entry, and hold 7Q values instead of 2Q + 6)
+   constexpr bool AFF = (VAR & 64) != 0;
+   v2d pa[Q];
+   double cc[6];
+   if (AFF && t < NE * QQ)
+   {
+      const int e = belem[(size_t)k * NE + t / QQ], l = t % QQ;
+      constexpr int NQ = Q * Q * Q;
+#pragma unroll
+      for (int qz = 0; qz < Q; qz++) { pa[qz] = reinterpret_cast<const v2d *>(qdm)[(size_t)e * NQ + qz * QQ + l]; }
+#pragma unroll
+      for (int c = 0; c < 6; c++) { cc[c] = qdd[(size_t)e * 6 + c]; }
+   }
+   if (!AFF && !(VAR & 1) && t < NE * QQ)
    {
       if constexpr ((VAR & 2) && Q % 2 == 0)
       {
@@ -2121,7 +2136,7 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
    {
       CBasis *bp = stage_basis<D, Q>();
       const int elt = t / QQ, l = t % QQ;
-      if (VAR & 1) { line_load_qdata<D, Q, MASS, DIFF, (VAR & 64) != 0>(qv, belem[(size_t)k * NE + elt], l, qdd, qdm); }
+      if (!AFF && (VAR & 1)) { line_load_qdata<D, Q, MASS, DIFF, false>(qv, belem[(size_t)k * NE + elt], l, qdd, qdm); }
       double *in = bufB + elt * SB;
       double *o = in;
       double l0[D], l1[D], l2[D];
@@ -2154,11 +2169,21 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
          double fx = 0.0, fy = 0.0, fz = 0.0, m = 0.0;
          if (DIFF)
          {
-            fx = qv[0][qz] * gx + qv[1][qz] * gy + qv[2][qz] * gz;
-            fy = qv[1][qz] * gx + qv[3][qz] * gy + qv[4][qz] * gz;
-            fz = qv[2][qz] * gx + qv[4][qz] * gy + qv[5][qz] * gz;
+            if (AFF)
+            {
+               const double wb = pa[qz].x;
+               fx = wb * (cc[0] * gx + cc[1] * gy + cc[2] * gz);
+               fy = wb * (cc[1] * gx + cc[3] * gy + cc[4] * gz);
+               fz = wb * (cc[2] * gx + cc[4] * gy + cc[5] * gz);
+            }
+            else
+            {
+               fx = qv[0][qz] * gx + qv[1][qz] * gy + qv[2][qz] * gz;
+               fy = qv[1][qz] * gx + qv[3][qz] * gy + qv[4][qz] * gz;
+               fz = qv[2][qz] * gx + qv[4][qz] * gy + qv[5][qz] * gz;
+            }
          }
-         if (MASS) { m = qv[6][qz] * u; }
+         if (MASS) { m = (AFF ? pa[qz].y : qv[6][qz]) * u; }
 #pragma unroll
          for (int dz = 0; dz < D; dz++)
          {

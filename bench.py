@@ -253,7 +253,7 @@ def main():
         traffic = None
         # pinned PMC traffic of this workload, kernel family and qdata layout (profiles/pmc_pin.py)
         pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_n{world}_{qdata_layout(E, timed_forms[0])}.json")
-        if os.path.exists(pmc):
+        if os.path.exists(pmc) and args.loopback <= 1 and args.emulate_world <= 1:  # pins are single-form profiles
             try:
                 traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
             except Exception:

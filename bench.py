@@ -72,6 +72,8 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2")
+    ap.add_argument("--c2-n", type=int, default=50,
+                    help="c2: elements per edge of the per-GPU Cartesian block (experiments; configs[1] = 50)")
     ap.add_argument("--c3-refine", type=int, default=6,
                     help="c3: uniform refinements of fichera.mesh (6 -> 14.9M DoF, 5 -> 1.88M)")
     ap.add_argument("--kernel", choices=["auto", "tpe", "wpe", "unfused", "line"], default="auto")
@@ -112,11 +114,11 @@ def main():
     compress = args.geometry == "compressed"
     order = 4 if args.workload == "c5" else 2
     if args.workload == "c2":
-        n = 50
+        n = args.c2_n
         nx = ny = n
         nz_total = n * max(world, args.emulate_world)
         scaling = "weak"
-        workload = f"configs[1]: inline-hex refined to Cartesian 50x50x{nz_total} (50^3 per GPU), H1 p=2, Mass(rho*c)+Diffusion(gamma*dt*k(T)) PA Mult"
+        workload = f"configs[1]: inline-hex refined to Cartesian {n}x{n}x{nz_total} ({n}^3 per GPU), H1 p=2, Mass(rho*c)+Diffusion(gamma*dt*k(T)) PA Mult"
     elif args.workload == "c3":
         scaling = "strong"
         workload = (f"configs[2]: fichera.mesh refined {args.c3_refine}x, H1 p=2, nonlinear Pennes k(T) "

@@ -733,6 +733,16 @@ void PAForm::ensure_work(hipStream_t)
    ye_.resize((size_t)ne_ * ND_);
 }
 
+// experiment knob ECM2_TPE_PP=1: the whole Mult with the plane-per-wave kernel
+static bool tpe_plane_parallel()
+{
+   static const bool v = [] {
+      const char *e = std::getenv("ECM2_TPE_PP");
+      return e && std::string(e) == "1";
+   }();
+   return v;
+}
+
 void PAForm::mult(const double *x, double *y, hipStream_t s)
 {
    ECM2_VERIFY(assembled_, ERR_STATE, "Mult before Assemble");
@@ -764,7 +774,7 @@ void PAForm::mult(const double *x, double *y, hipStream_t s)
       // exclusive dofs are plain-stored, shared ones summed from their partial slots:
       // every y entry is written exactly once, no memset, bitwise reproducible
       record_start(s);
-      apply_blocks(x, nullptr, y, nullptr, 0, layout_.nblk(), s);
+      apply_blocks(x, nullptr, y, nullptr, 0, layout_.nblk(), s, tpe_plane_parallel());
       record_stop(s);
       finish_shared(0, n_sh_, y, nullptr, s);
       return;

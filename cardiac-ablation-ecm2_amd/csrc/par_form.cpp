@@ -387,9 +387,34 @@ static bool interior_first()
    return v;
 }
 
+// OVERLAP with the boundary on the caller's stream after the interior (ECM2_PAR_SERIAL=1):
+// only the exchange runs on the comm stream, and the one cross-stream wait (for P) is long
+// satisfied when the interior ends -- no join after the boundary kernel.
+static bool par_serial()
+{
+   static const bool v = [] {
+      const char *e = std::getenv("ECM2_PAR_SERIAL");
+      return e && std::string(e) == "1";
+   }();
+   return v;
+}
+
 void ParPAForm::mult_stages(const double *x_true, double *y_true, hipStream_t s, bool emu)
 {
    x_cur_ = x_true;
+   if (part_.overlap && par_serial() && !b_split_ && !is_)
+   {
+      stage_pack(x_true, y_true, s);
+      stage_interior(x_true, y_true, s);
+      if (emu) { self_exchange(false); } else { rccl_exchange(false); }
+      ECM2_HIP(hipEventRecord(ev_done_, cs_));
+      ECM2_HIP(hipStreamWaitEvent(s, ev_done_, 0));
+      local_->record_start_public(s);
+      local_->apply_blocks(x_true, xg_.data(), y_true, yg_.data(), b_int(), local_->nblocks(), s, boundary_pp());
+      local_->record_stop_public(s);
+      local_->finish_shared(0, local_->n_shared_owned(), y_true, yg_.data(), s);
+      return;
+   }
    const bool first = interior_first() && !b_split_;  // part B of a split waits for the boundary
    stage_pack(x_true, y_true, s);
    if (first) { stage_interior(x_true, y_true, s); }

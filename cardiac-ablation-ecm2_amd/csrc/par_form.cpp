@@ -43,6 +43,7 @@ double rccl_p2p_selftest(bool graph, int n)
    b.resize(std::max(1, n));
    std::vector<double> h(std::max(1, n));
    double err = 0.0;
+   hipGraphExec_t ge = nullptr;
    for (int rep = 0; rep < 3; rep++)
    {
       for (int i = 0; i < n; i++) { h[i] = 0.5 * i + rep; }
@@ -54,7 +55,6 @@ double rccl_p2p_selftest(bool graph, int n)
          ECM2_NCCL(ncclRecv(b.data(), n, ncclFloat64, 0, comm, st));
          ECM2_NCCL(ncclGroupEnd());
       };
-      static hipGraphExec_t ge = nullptr;
       if (graph)
       {
          if (rep == 0)

@@ -3,6 +3,7 @@
 #include "bricks.hpp"
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -125,6 +126,13 @@ void PAForm::set_block_splits(const std::vector<int> &splits)
    assembled_ = false;
 }
 
+void PAForm::set_latency_from(int b)
+{
+   latency_from_ = b;
+   gmap_blk_.resize(0);  // the face-assembly plan depends on it: rebuild
+   assembled_ = false;
+}
+
 void PAForm::set_line_bricks(int bz)
 {
    ECM2_VERIFY(bz >= -1 && bz <= 2, ERR_ARG, "brick mode " << bz << " not in {-1, 0, 1, 2}");
@@ -180,8 +188,17 @@ namespace
 // "holding" entries (holds[(b*64+l)*ND+a]) carry each dof's in-wave sum, and
 // hcount[d] counts the holders of dof d in the whole mesh: a dof held once is
 // plain-stored, otherwise it is "shared" (partial slot or atomic add).
+// In-wave face assembly plan of the blocked layout (see tpe_assemble_store): per 64-lane
+// block and direction, lane l receives lane l + off's low face into its high face when the
+// faces coincide; then (xwave) across the waves of a workgroup group: a wave whose 16
+// high-face lanes all coincide with another wave's 16 low-face lanes receives those through
+// LDS.  groups: [first block, end block, link allowed] of every workgroup (<= 4 blocks, in
+// the launch's grouping: from each apply segment's first block).  Lane flags: bits 1|4|16 receive x|y|z in-wave, 2|8|32 low face
+// sent (in-wave or across waves), 64|128|256 receive x|y|z across waves, bits 9-10 | 11-12 |
+// 13-14 the sending wave (within the group) for x | y | z.
 void build_merge_plan(int ne, int D, const std::vector<int> &gmap_int, int ndofs,
-                      std::vector<char> &holds, std::vector<int> &hcount, std::vector<int> &flags)
+                      std::vector<char> &holds, std::vector<int> &hcount, std::vector<int> &flags,
+                      const std::vector<std::array<int, 3>> &groups)
 {
    const int ND = D * D * D, nblk = (ne + 63) / 64;
    flags.assign((size_t)nblk * 64, 0);
@@ -194,40 +211,81 @@ void build_merge_plan(int ne, int D, const std::vector<int> &gmap_int, int ndofs
       return (s * D + j) * D + i;
    };
    const int off[3] = {1, 4, 16}, recv[3] = {1, 4, 16}, sent[3] = {2, 8, 32};
+   auto act = [&](int b, int l) { return b * 64 + l < ne; };
+   auto dof = [&](int b, int l, int a) { return dofv(gmap_int[((size_t)b * 64 + l) * ND + a]); };
+   auto H = [&](int b, int l, int a) -> char & { return holds[((size_t)b * 64 + l) * ND + a]; };
+   auto F = [&](int b, int l) -> int & { return flags[(size_t)b * 64 + l]; };
    for (int b = 0; b < nblk; b++)
-   {
-      auto act = [&](int l) { return b * 64 + l < ne; };
-      auto dof = [&](int l, int a) { return dofv(gmap_int[((size_t)b * 64 + l) * ND + a]); };
-      auto H = [&](int l, int a) -> char & { return holds[((size_t)b * 64 + l) * ND + a]; };
       for (int l = 0; l < 64; l++)
-         for (int a = 0; a < ND; a++) { H(l, a) = act(l); }
+         for (int a = 0; a < ND; a++) { H(b, l, a) = act(b, l); }
+   for (const auto &grp : groups)
+   {
+      const int g0 = grp[0], g1 = grp[1];
+      const bool xw = grp[2] != 0;
       for (int dir = 0; dir < 3; dir++)
       {
-         for (int l = 0; l + off[dir] < 64; l++)
+         for (int b = g0; b < g1; b++)
          {
-            const int m = l + off[dir];
-            if (!act(l) || !act(m)) { continue; }
-            bool ok = true;
-            for (int j = 0; j < D && ok; j++)
-               for (int i = 0; i < D && ok; i++)
-               {
-                  const int ar = face(dir, D - 1, i, j), as = face(dir, 0, i, j);
-                  ok = dof(l, ar) == dof(m, as) && (H(l, ar) || !H(m, as));
-               }
-            if (!ok) { continue; }
-            flags[(size_t)b * 64 + l] |= recv[dir];
-            flags[(size_t)b * 64 + m] |= sent[dir];
+            for (int l = 0; l + off[dir] < 64; l++)
+            {
+               const int m = l + off[dir];
+               if (!act(b, l) || !act(b, m)) { continue; }
+               bool ok = true;
+               for (int j = 0; j < D && ok; j++)
+                  for (int i = 0; i < D && ok; i++)
+                  {
+                     const int ar = face(dir, D - 1, i, j), as = face(dir, 0, i, j);
+                     ok = dof(b, l, ar) == dof(b, m, as) && (H(b, l, ar) || !H(b, m, as));
+                  }
+               if (!ok) { continue; }
+               F(b, l) |= recv[dir];
+               F(b, m) |= sent[dir];
+            }
+            for (int m = 0; m < 64; m++)
+            {
+               if (!(F(b, m) & sent[dir])) { continue; }
+               for (int j = 0; j < D; j++)
+                  for (int i = 0; i < D; i++) { H(b, m, face(dir, 0, i, j)) = 0; }
+            }
          }
-         for (int m = 0; m < 64; m++)
+         if (!xw) { continue; }
+         // across the group's waves: wave br's 16 high-face lanes <- wave bs's low-face lanes
+         for (int br = g0; br < g1; br++)
          {
-            if (!(flags[(size_t)b * 64 + m] & sent[dir])) { continue; }
-            for (int j = 0; j < D; j++)
-               for (int i = 0; i < D; i++) { H(m, face(dir, 0, i, j)) = 0; }
+            for (int bs = g0; bs < g1; bs++)
+            {
+               if (bs == br) { continue; }
+               bool ok = true;
+               for (int l = 0; l < 64 && ok; l++)
+               {
+                  if ((l / off[dir]) % 4 != 3) { continue; }
+                  const int m = l - 3 * off[dir];
+                  ok = act(br, l) && act(bs, m) && !(F(bs, m) & sent[dir]);
+                  for (int j = 0; j < D && ok; j++)
+                     for (int i = 0; i < D && ok; i++)
+                     {
+                        const int ar = face(dir, D - 1, i, j), as = face(dir, 0, i, j);
+                        ok = dof(br, l, ar) == dof(bs, m, as) && H(br, l, ar) && H(bs, m, as);
+                     }
+               }
+               if (!ok) { continue; }
+               for (int l = 0; l < 64; l++)
+               {
+                  if ((l / off[dir]) % 4 != 3) { continue; }
+                  const int m = l - 3 * off[dir];
+                  F(br, l) |= (64 << dir) | ((bs - g0) << (9 + 2 * dir));
+                  F(bs, m) |= sent[dir];
+                  for (int j = 0; j < D; j++)
+                     for (int i = 0; i < D; i++) { H(bs, m, face(dir, 0, i, j)) = 0; }
+               }
+               break;  // one sender per receiving wave and direction
+            }
          }
       }
-      for (int l = 0; l < 64; l++)
-         for (int a = 0; a < ND; a++) { if (H(l, a)) { hcount[dof(l, a)]++; } }
    }
+   for (int b = 0; b < nblk; b++)
+      for (int l = 0; l < 64; l++)
+         for (int a = 0; a < ND; a++) { if (H(b, l, a)) { hcount[dof(b, l, a)]++; } }
 }
 } // namespace
 
@@ -333,6 +391,21 @@ void PAForm::set_kernel(int mode)
 
 static bool has_tpe(int D, int Q) { return (D == 2 && Q == 3) || (D == 3 && Q == 4); }
 
+// Cross-wave face assembly in the AFFINE thread-per-element kernels (ECM2_XWAVE=0: in-wave
+// only).  Off with the kernel variants that lack it (row kernel, plane-per-wave Mult).
+static bool xwave_env()
+{
+   static const bool v = [] {
+      const char *e = std::getenv("ECM2_XWAVE");
+      if (e && std::string(e) == "0") { return false; }
+      const char *tv = std::getenv("ECM2_TPE_VARIANT");
+      if (tv && (std::atoi(tv) & 64)) { return false; }
+      const char *pp = std::getenv("ECM2_TPE_PP");
+      return !(pp && std::string(pp) == "1");
+   }();
+   return v;
+}
+
 void PAForm::assemble(hipStream_t s)
 {
    ECM2_VERIFY(enodes_.size() || jac_ || ne_ == 0, ERR_STATE, "assemble: no geometry set");
@@ -391,7 +464,26 @@ void PAForm::assemble(hipStream_t s)
       ECM2_VERIFY((size_t)nblk * ND_ * 64 < (1ull << 31), ERR_UNSUPPORTED, "too many elements for int slots");
       std::vector<char> holds;
       std::vector<int> fl, hcount;
-      build_merge_plan(ne_, D_, gint, ndofs_, holds, hcount, fl);
+      // workgroups as the launches group them (4 blocks from each apply segment's start);
+      // waves of a workgroup may assemble shared faces through LDS (AFFINE kernels), except
+      // in segments launched with the one-block-per-workgroup latency kernel
+      std::vector<std::array<int, 3>> groups;
+      {
+         std::vector<int> seg{0, nblk};
+         for (int sp : splits_) { seg.push_back(std::max(0, std::min(nblk, sp))); }
+         std::sort(seg.begin(), seg.end());
+         seg.erase(std::unique(seg.begin(), seg.end()), seg.end());
+         const bool xw = layout_.kind == QLAYOUT_AFFINE && xwave_env();
+         for (size_t k = 0; k + 1 < seg.size(); k++)
+         {
+            const bool lat = latency_from_ >= 0 && seg[k] >= latency_from_;
+            for (int b = seg[k]; b < seg[k + 1]; b += 4)
+            {
+               groups.push_back({b, std::min(b + 4, seg[k + 1]), (xw && !lat) ? 1 : 0});
+            }
+         }
+      }
+      build_merge_plan(ne_, D_, gint, ndofs_, holds, hcount, fl, groups);
       // blocked map: dof | shared << 30 | sign << 31
       std::vector<int> blk((size_t)nblk * ND_ * 64, 0);
       for (int i = 0; i < ne_; i++)

@@ -83,6 +83,9 @@ public:
    // Bricks of the line kernel family (p >= 3): -1 = default (ECM2_LINE_BRICK, else 2),
    // 0 = none, 1 = 2 x 2 x 1, 2 = 2 x 2 x 2 elements per workgroup.
    void set_line_bricks(int bz);
+   // Blocks >= b are applied with the one-block-per-workgroup latency kernel (apply_blocks
+   // latency = true): no cross-wave face assembly there.  -1: none.
+   void set_latency_from(int b);
    int n_bricks() const { return n_bricks_; }
    int brick_bz() const { return brick_bz_; }
    void add_integrator(int kind, const CoeffDesc &c);
@@ -177,6 +180,7 @@ private:
    int line_bricks_ = -1;           // requested brick mode (set_line_bricks)
    bool affine_ = false;            // every element a parallelepiped (set_element_nodes)
    bool compress_ = true;           // set_geometry_compression
+   int latency_from_ = -1;          // set_latency_from
    bool auto_order_ = true;         // TPE without a caller order: face-linked 4x4x4 bricks
    bool perm_auto_ = false;         // perm_host_ was derived (not the caller's)
    DeviceArray<int> lane_flags_;    // [blk][64] in-wave merge flags

@@ -615,14 +615,28 @@ __device__ __forceinline__ int xcd_contiguous(int i, int G)
 // shared one goes to its dense partial slot [blk][a][lane] (summed in a fixed order by
 // k_sum_partials: deterministic, no atomics, no y memset) or, without a partial buffer, is
 // atomically added.  PLAIN: diagnostic (plain stores only; wrong for shared dofs).
-template <int D, bool SPLIT, bool SIGNS, bool PLAIN>
+// Rows per wave of the LDS region the cross-wave face exchange uses (3 faces of D x D).
+template <int D>
+struct XwaveRows
+{
+   static constexpr int ND = D * D * D, R = ND > 3 * D * D ? ND : 3 * D * D;
+};
+
+// XW: after each direction's in-wave merge, faces shared with another wave of the workgroup
+// (lane flags 64|128|256 + the sending wave in bits 9-14, see build_merge_plan) move through
+// LDS: the sending lanes (low face, e_dir = 0) park their face in their own wave's region
+// xb[w][XR][64] (the kernel's x staging area, no longer read), a barrier, the receiving lanes
+// (high face, e_dir = 3) add it.  Every wave of the workgroup must call this (wave_on false:
+// barriers only).
+template <int D, bool SPLIT, bool SIGNS, bool PLAIN, bool XW = false>
 __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], const int *__restrict__ mp, int fl,
                                                    int blk, int lane, bool active, int n_owned,
                                                    double *__restrict__ y, double *__restrict__ yg,
-                                                   double *__restrict__ part, const int *__restrict__ pslot)
+                                                   double *__restrict__ part, const int *__restrict__ pslot,
+                                                   double *xb = nullptr, int w = 0, bool wave_on = true)
 {
-   constexpr int ND = D * D * D;
-   if (SIGNS)
+   constexpr int ND = D * D * D, XR = XwaveRows<D>::R;
+   if (SIGNS && wave_on)
    {
 #pragma unroll
       for (int a = 0; a < ND; a++)
@@ -630,21 +644,46 @@ __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], cons
          if (bneg(mp[a * 64])) { Yo[a] = -Yo[a]; }
       }
    }
-   auto merge = [&](int delta, int recv_bit, int sent_bit, auto face) {
+   auto merge = [&](int dir, int delta, int recv_bit, int sent_bit, auto face) {
+      if (XW && wave_on && ((lane / delta) & 3) == 0 && (fl & sent_bit))
+      {
 #pragma unroll
-      for (int j = 0; j < D; j++)
+         for (int j = 0; j < D; j++)
 #pragma unroll
-         for (int i = 0; i < D; i++)
+            for (int i = 0; i < D; i++) { xb[((w * XR) + dir * D * D + j * D + i) * 64 + lane] = Yo[face(0, i, j)]; }
+      }
+      if (wave_on)
+      {
+#pragma unroll
+         for (int j = 0; j < D; j++)
+#pragma unroll
+            for (int i = 0; i < D; i++)
+            {
+               const double v = __shfl_down(Yo[face(0, i, j)], delta, 64);
+               if (fl & recv_bit) { Yo[face(D - 1, i, j)] += v; }
+               if (fl & sent_bit) { Yo[face(0, i, j)] = 0.0; }
+            }
+      }
+      if (XW)
+      {
+         __syncthreads();
+         if (wave_on && (fl & (64 << dir)))
          {
-            const double v = __shfl_down(Yo[face(0, i, j)], delta, 64);
-            if (fl & recv_bit) { Yo[face(D - 1, i, j)] += v; }
-            if (fl & sent_bit) { Yo[face(0, i, j)] = 0.0; }
+            const int pw = (fl >> (9 + 2 * dir)) & 3;
+#pragma unroll
+            for (int j = 0; j < D; j++)
+#pragma unroll
+               for (int i = 0; i < D; i++)
+               {
+                  Yo[face(D - 1, i, j)] += xb[((pw * XR) + dir * D * D + j * D + i) * 64 + lane - 3 * delta];
+               }
          }
+      }
    };
-   merge(1, 1, 2, [](int s, int i, int j) { return (j * D + i) * D + s; });    // x: (dz=j, dy=i)
-   merge(4, 4, 8, [](int s, int i, int j) { return (j * D + s) * D + i; });    // y: (dz=j, dx=i)
-   merge(16, 16, 32, [](int s, int i, int j) { return (s * D + j) * D + i; }); // z: (dy=j, dx=i)
-   if (!active) { return; }
+   merge(0, 1, 1, 2, [](int s, int i, int j) { return (j * D + i) * D + s; });    // x: (dz=j, dy=i)
+   merge(1, 4, 4, 8, [](int s, int i, int j) { return (j * D + s) * D + i; });    // y: (dz=j, dx=i)
+   merge(2, 16, 16, 32, [](int s, int i, int j) { return (s * D + j) * D + i; }); // z: (dy=j, dx=i)
+   if (!active || !wave_on) { return; }
    const bool sx = fl & 2, sy = fl & 8, sz = fl & 32;
 #pragma unroll
    for (int dz = 0; dz < D; dz++)
@@ -865,14 +904,19 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                double *__restrict__ y, double *__restrict__ yg, const Basis1D b,
                const int *__restrict__ lane_flags, double *__restrict__ part, const int *__restrict__ pslot)
 {
-   constexpr int ND = D * D * D, NQ = Q * Q * Q, NR = Q * Q;
-   __shared__ double sX[4][ND][64];
+   constexpr int ND = D * D * D, NQ = Q * Q * Q, NR = Q * Q, XR = XwaveRows<D>::R;
+   __shared__ double sX[4][XR][64];  // gathered x; then the cross-wave face exchange
    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
    const int blk = blk_begin + (int)blockIdx.x * 4 + w;
-   if (blk >= blk_end) { return; }  // wave-uniform; no block-wide barrier below
+   const bool wave_on = blk < blk_end;  // wave-uniform; every wave reaches the store's barriers
    const int e = blk * 64 + lane;
-   const bool active = e < ne;
+   const bool active = wave_on && e < ne;
    const int *mp = gmap + (size_t)blk * ND * 64 + lane;
+   double Yo[ND];
+#pragma unroll
+   for (int a = 0; a < ND; a++) { Yo[a] = 0.0; }
+   if (wave_on)
+   {
 #pragma unroll
    for (int a = 0; a < ND; a++)
    {
@@ -881,9 +925,6 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
       const double v = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
       sX[w][a][lane] = bneg(g) ? -v : v;
    }
-   double Yo[ND];
-#pragma unroll
-   for (int a = 0; a < ND; a++) { Yo[a] = 0.0; }
    auto ld2 = [&](const double *p) -> v2d {
       if (VAR & 2) { return *reinterpret_cast<const v2d *>(p); }
       return __builtin_nontemporal_load(reinterpret_cast<const v2d *>(p));
@@ -1036,8 +1077,10 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                Yo[(dz * D + dy) * D + dx] += bz[dz] * SB[dy][dx] + gz[dz] * SG[dy][dx];
             }
    }
-   tpe_assemble_store<D, SPLIT, true, (VAR & 1) != 0>(Yo, mp, lane_flags[(size_t)blk * 64 + lane], blk, lane, active,
-                                                      n_owned, y, yg, part, pslot);
+   }  // wave_on
+   tpe_assemble_store<D, SPLIT, true, (VAR & 1) != 0, true>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0,
+                                                            blk, lane, active, n_owned, y, yg, part, pslot,
+                                                            &sX[0][0][0], w, wave_on);
 }
 
 // Latency variant of k_apply_tpe_sf for small block ranges (the distributed Mult's boundary
@@ -1214,17 +1257,19 @@ k_diag_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restric
            double *__restrict__ yg, const Basis1D b, const double *__restrict__ drow,
            const int *__restrict__ lane_flags, double *__restrict__ part, const int *__restrict__ pslot)
 {
-   constexpr int ND = D * D * D, NQ = Q * Q * Q, NQH = (NQ + 1) / 2, DD = D * D;
+   constexpr int ND = D * D * D, NQ = Q * Q * Q, NQH = (NQ + 1) / 2, DD = D * D, XR = XwaveRows<D>::R;
+   __shared__ double xb[AFF ? 4 * XR * 64 : 1];  // AFF: cross-wave face exchange (as the apply's plan)
    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
    const int blk = blk_begin + blockIdx.x * 4 + w;
-   if (blk >= blk_end) { return; }  // wave-uniform
-   const bool active = blk * 64 + lane < ne;
+   const bool wave_on = blk < blk_end;  // wave-uniform
+   if (!AFF && !wave_on) { return; }    // no block-wide barrier without AFF
+   const bool active = wave_on && blk * 64 + lane < ne;
    const int *mp = gmap + (size_t)blk * ND * 64 + lane;
    const double *qd = qdd + (size_t)blk * NQ * 3 * 128 + lane * 2;
    const double *qm = qdm + (size_t)blk * NQH * 128 + lane * 2;
    const double *qa = qdm + (size_t)blk * NQ * 128 + lane * 2;  // AFF pairs
    v2d ce[3];
-   if (AFF)
+   if (AFF && wave_on)
    {
 #pragma unroll
       for (int k = 0; k < 3; k++) { ce[k] = *reinterpret_cast<const v2d *>(qdd + (size_t)blk * 3 * 128 + lane * 2 + k * 128); }
@@ -1233,7 +1278,7 @@ k_diag_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restric
 #pragma unroll
    for (int a = 0; a < ND; a++) { Yo[a] = 0.0; }
 #pragma unroll 1
-   for (int row = 0; row < Q * Q; row++)
+   for (int row = 0; row < (wave_on ? Q * Q : 0); row++)
    {
       double S[7][D];
 #pragma unroll
@@ -1299,8 +1344,8 @@ k_diag_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restric
             }
          }
    }
-   tpe_assemble_store<D, SPLIT, false, false>(Yo, mp, lane_flags[(size_t)blk * 64 + lane], blk, lane, active,
-                                               n_owned, y, yg, part, pslot);
+   tpe_assemble_store<D, SPLIT, false, false, AFF>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0, blk,
+                                                    lane, active, n_owned, y, yg, part, pslot, xb, w, wave_on);
 }
 
 // --------------------------------------------------------------------------

@@ -141,6 +141,7 @@ ParPAForm::ParPAForm(const LocalPart &part, const double *enodes_local_host, int
    if (b_split_ <= 0 || b_split_ >= bi) { b_split_ = 0; }
    if (b_split_) { local_->set_block_splits({b_split_, bi}); }
    else { local_->set_block_splits({bi}); }
+   if (boundary_pp()) { local_->set_latency_from(bi); }  // boundary blocks: one block per workgroup
    send_idx_.upload(part.send_idx);
    pack_needed_ = false;
    for (size_t k = 0; k < part.nbrs.size(); k++)

@@ -510,3 +510,24 @@ def test_affine_wpe_reads_compressed_layout():
         ye = torch.zeros(fes.ne * nd, dtype=torch.float64, device="cuda")
         form.IntegratorAddMultPA(kind, dev(xe), ye)
         assert relerr(host(ye).reshape(fes.ne, nd), ref) <= RTOL
+
+
+@pytest.mark.parametrize("order", [1, 2])
+def test_cross_wave_face_assembly(order):
+    """AFFINE thread-per-element kernels also assemble the faces shared by the 4 bricks of a
+    workgroup through LDS: fewer shared dofs / partial slots than the per-wave plan of the
+    full layout on the same mesh, and the same operator and diagonal."""
+    m = E.Mesh.MakeCartesian3D(16, 16, 8)      # 32 complete 4x4x4 bricks, 8 workgroups
+    fa, form_a, op = build_pair(m, order, "bio_a", "fn", kernel=E.KERNEL_TPE)
+    fb, form_b, _ = build_pair(m, order, "bio_a", "fn", kernel=E.KERNEL_TPE, compress_geometry=False)
+    assert form_a.info()["layout"] == E.QLAYOUT_AFFINE and form_b.info()["layout"] == E.QLAYOUT_BLOCKED
+    (sh_a, sl_a), (sh_b, sl_b) = form_a.ScatterInfo(), form_b.ScatterInfo()
+    assert sh_a < sh_b and sl_a < sl_b
+    x = np.random.default_rng(9).uniform(-1, 1, fa.ndofs)
+    for form in (form_a, form_b):
+        y = torch.full((fa.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+        form.Mult(dev(x), y)
+        assert relerr(host(y), op.mult(x)) <= RTOL
+        d = torch.empty(fa.ndofs, dtype=torch.float64, device="cuda")
+        form.AssembleDiagonal(d)
+        assert relerr(host(d), op.diagonal()) < 1e-13

@@ -91,6 +91,7 @@ struct ApplyArgs
    double *part = nullptr;          // partial slots of shared dofs (null: atomics)
    const int *pslot = nullptr;      // TPE: [blk][nd][64] entry -> position in its dof's run (null: dense slots)
    bool latency = false;            // TPE + AFFINE: one workgroup per block, a plane per wave (small ranges)
+   int xwg = 4;                     // TPE + AFFINE: blocks (waves) per workgroup of the face-assembly plan
    const int *chunks = nullptr;     // LINE: device chunk table (first | count << 24)
    const int *chunk_off = nullptr;  // LINE: host [nblk + 1], chunks of 64-element block b
    // LINE, brick part (p >= 3 on structured regions): bricks of 2 x 2 x brick_bz elements

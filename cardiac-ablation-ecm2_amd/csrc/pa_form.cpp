@@ -194,8 +194,8 @@ namespace
 // high-face lanes all coincide with another wave's 16 low-face lanes receives those through
 // LDS.  groups: [first block, end block, link allowed] of every workgroup (<= 4 blocks, in
 // the launch's grouping: from each apply segment's first block).  Lane flags: bits 1|4|16 receive x|y|z in-wave, 2|8|32 low face
-// sent (in-wave or across waves), 64|128|256 receive x|y|z across waves, bits 9-10 | 11-12 |
-// 13-14 the sending wave (within the group) for x | y | z.
+// sent (in-wave or across waves), 64|128|256 receive x|y|z across waves, bits 9-11 | 12-14 |
+// 15-17 the sending wave (within the group) for x | y | z.
 void build_merge_plan(int ne, int D, const std::vector<int> &gmap_int, int ndofs,
                       std::vector<char> &holds, std::vector<int> &hcount, std::vector<int> &flags,
                       const std::vector<std::array<int, 3>> &groups)
@@ -273,7 +273,7 @@ void build_merge_plan(int ne, int D, const std::vector<int> &gmap_int, int ndofs
                {
                   if ((l / off[dir]) % 4 != 3) { continue; }
                   const int m = l - 3 * off[dir];
-                  F(br, l) |= (64 << dir) | ((bs - g0) << (9 + 2 * dir));
+                  F(br, l) |= (64 << dir) | ((bs - g0) << (9 + 3 * dir));
                   F(bs, m) |= sent[dir];
                   for (int j = 0; j < D; j++)
                      for (int i = 0; i < D; i++) { H(bs, m, face(dir, 0, i, j)) = 0; }
@@ -406,6 +406,17 @@ static bool xwave_env()
    return v;
 }
 
+// Waves per workgroup of the cross-wave plan (experiment knob ECM2_XWAVE_WG=8: 2 x 2 x 2
+// bricks per workgroup).
+static int xwave_wg()
+{
+   static const int v = [] {
+      const char *e = std::getenv("ECM2_XWAVE_WG");
+      return (e && std::atoi(e) == 8) ? 8 : 4;
+   }();
+   return v;
+}
+
 void PAForm::assemble(hipStream_t s)
 {
    ECM2_VERIFY(enodes_.size() || jac_ || ne_ == 0, ERR_STATE, "assemble: no geometry set");
@@ -474,12 +485,13 @@ void PAForm::assemble(hipStream_t s)
          std::sort(seg.begin(), seg.end());
          seg.erase(std::unique(seg.begin(), seg.end()), seg.end());
          const bool xw = layout_.kind == QLAYOUT_AFFINE && xwave_env();
+         xwg_ = xw ? xwave_wg() : 4;
          for (size_t k = 0; k + 1 < seg.size(); k++)
          {
             const bool lat = latency_from_ >= 0 && seg[k] >= latency_from_;
-            for (int b = seg[k]; b < seg[k + 1]; b += 4)
+            for (int b = seg[k]; b < seg[k + 1]; b += xwg_)
             {
-               groups.push_back({b, std::min(b + 4, seg[k + 1]), (xw && !lat) ? 1 : 0});
+               groups.push_back({b, std::min(b + xwg_, seg[k + 1]), (xw && !lat) ? 1 : 0});
             }
          }
       }
@@ -911,6 +923,7 @@ ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, doubl
    a.x = x; a.xg = xg; a.y = y; a.yg = yg;
    a.part = use_partials() ? const_cast<double *>(part_.data()) : nullptr;  // form-owned scratch
    a.pslot = (resolved_mode_ == KERNEL_TPE && pslot_.size()) ? pslot_.data() : nullptr;
+   a.xwg = xwg_;
    a.chunks = chunks_.data();
    a.chunk_off = chunk_off_.empty() ? nullptr : chunk_off_.data();
    if (resolved_mode_ == KERNEL_LINE && use_partials())

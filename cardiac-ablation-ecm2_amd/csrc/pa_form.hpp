@@ -181,6 +181,7 @@ private:
    bool affine_ = false;            // every element a parallelepiped (set_element_nodes)
    bool compress_ = true;           // set_geometry_compression
    int latency_from_ = -1;          // set_latency_from
+   int xwg_ = 4;                    // waves per workgroup of the face-assembly plan
    bool auto_order_ = true;         // TPE without a caller order: face-linked 4x4x4 bricks
    bool perm_auto_ = false;         // perm_host_ was derived (not the caller's)
    DeviceArray<int> lane_flags_;    // [blk][64] in-wave merge flags

@@ -623,7 +623,7 @@ struct XwaveRows
 };
 
 // XW: after each direction's in-wave merge, faces shared with another wave of the workgroup
-// (lane flags 64|128|256 + the sending wave in bits 9-14, see build_merge_plan) move through
+// (lane flags 64|128|256 + the sending wave in bits 9-17, see build_merge_plan) move through
 // LDS: the sending lanes (low face, e_dir = 0) park their face in their own wave's region
 // xb[w][XR][64] (the kernel's x staging area, no longer read), a barrier, the receiving lanes
 // (high face, e_dir = 3) add it.  Every wave of the workgroup must call this (wave_on false:
@@ -669,7 +669,7 @@ __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], cons
          __syncthreads();
          if (wave_on && (fl & (64 << dir)))
          {
-            const int pw = (fl >> (9 + 2 * dir)) & 3;
+            const int pw = (fl >> (9 + 3 * dir)) & 7;
 #pragma unroll
             for (int j = 0; j < D; j++)
 #pragma unroll
@@ -896,18 +896,20 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 // and the plane ends with one z-transpose into the element outputs (2 D^3).  At p = 2 that is
 // 229 instead of 310 FP64 multiply-adds per row (-26%).  Same gather, row prefetch,
 // in-wave face assembly and deterministic store as k_apply_tpe_pf.
+// VAR & 128: workgroups of 8 waves (2 x 2 x 2 bricks share faces through LDS; 110 KB of LDS at
+// p = 2, one workgroup per CU) instead of 4.
 template <int D, int Q, bool SPLIT, int VAR>
-__global__ void __launch_bounds__(256, (VAR & 8) ? 2 : 1)
+__global__ void __launch_bounds__((VAR & 128) ? 512 : 256, (VAR & 8) ? 2 : 1)
 k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
                const double *__restrict__ qdd, const double *__restrict__ qdm,
                const double *__restrict__ x, const double *__restrict__ xg,
                double *__restrict__ y, double *__restrict__ yg, const Basis1D b,
                const int *__restrict__ lane_flags, double *__restrict__ part, const int *__restrict__ pslot)
 {
-   constexpr int ND = D * D * D, NQ = Q * Q * Q, NR = Q * Q, XR = XwaveRows<D>::R;
-   __shared__ double sX[4][XR][64];  // gathered x; then the cross-wave face exchange
+   constexpr int ND = D * D * D, NQ = Q * Q * Q, NR = Q * Q, XR = XwaveRows<D>::R, WPG = (VAR & 128) ? 8 : 4;
+   __shared__ double sX[WPG][XR][64];  // gathered x; then the cross-wave face exchange
    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-   const int blk = blk_begin + (int)blockIdx.x * 4 + w;
+   const int blk = blk_begin + (int)blockIdx.x * WPG + w;
    const bool wave_on = blk < blk_end;  // wave-uniform; every wave reaches the store's barriers
    const int e = blk * 64 + lane;
    const bool active = wave_on && e < ne;
@@ -1250,17 +1252,17 @@ k_apply_tpe_pp(int ne, int blk_begin, int n_owned, const int *__restrict__ gmap,
 // (Gy Bz)^2, (By Gz)^2, Gy By Bz^2, By^2 Gz Bz, Gy By Gz Bz.  Output assembled and stored
 // exactly like k_apply_tpe_pf's (in-wave faces, plain stores, partial slots): every
 // diagonal entry written once, deterministic, no memset.
-template <int D, int Q, bool MASS, bool DIFF, bool SPLIT, bool AFF = false>
-__global__ void __launch_bounds__(256)
+template <int D, int Q, bool MASS, bool DIFF, bool SPLIT, bool AFF = false, int WPG = 4>
+__global__ void __launch_bounds__(64 * WPG)
 k_diag_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
            const double *__restrict__ qdd, const double *__restrict__ qdm, double *__restrict__ y,
            double *__restrict__ yg, const Basis1D b, const double *__restrict__ drow,
            const int *__restrict__ lane_flags, double *__restrict__ part, const int *__restrict__ pslot)
 {
    constexpr int ND = D * D * D, NQ = Q * Q * Q, NQH = (NQ + 1) / 2, DD = D * D, XR = XwaveRows<D>::R;
-   __shared__ double xb[AFF ? 4 * XR * 64 : 1];  // AFF: cross-wave face exchange (as the apply's plan)
+   __shared__ double xb[AFF ? WPG * XR * 64 : 1];  // AFF: cross-wave face exchange (as the apply's plan)
    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-   const int blk = blk_begin + blockIdx.x * 4 + w;
+   const int blk = blk_begin + blockIdx.x * WPG + w;
    const bool wave_on = blk < blk_end;  // wave-uniform
    if (!AFF && !wave_on) { return; }    // no block-wide barrier without AFF
    const bool active = wave_on && blk * 64 + lane < ne;
@@ -2647,7 +2649,8 @@ void launch_tpe_pf(int var, const ApplyArgs &a, const Basis1D &b, const double *
          // experiment knob bits: 64 = the row kernel (k_apply_tpe_pf) instead of the plane-
          // factorised one, 2 = cached qdata loads, 8 = two waves per SIMD, 16 = XCD order
 #define ECM2_SF(V)                                                                                   \
-   hipLaunchKernelGGL((k_apply_tpe_sf<D, Q, SPLIT, V>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end, \
+   hipLaunchKernelGGL((k_apply_tpe_sf<D, Q, SPLIT, V>), ((V) & 128) ? dim3((nb + 7) / 8) : grid,       \
+                      ((V) & 128) ? dim3(512) : block, 0, s, a.ne, a.blk_begin, a.blk_end,            \
                       a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part, a.pslot)
          if (a.latency)
          {
@@ -2667,6 +2670,8 @@ void launch_tpe_pf(int var, const ApplyArgs &a, const Basis1D &b, const double *
          }
          else
          {
+            if (a.xwg == 8) { ECM2_SF(128); }
+            else
             switch (var & 14)
             {
                case 2: ECM2_SF(2); break;
@@ -3171,8 +3176,18 @@ static void launch_diag_tpe(const ApplyArgs &a, const Basis1D &b, const double *
    if (nb <= 0) { return; }
    const dim3 grid((nb + 3) / 4), block(256);
 #define ECM2_DIAG(SP, AF)                                                                               \
-   hipLaunchKernelGGL((k_diag_tpe<D, Q, MASS, DIFF, SP, AF>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end, \
-                      a.n_owned, a.gmap, a.qdd, a.qdm, a.y, a.yg, b, drow, a.lane_flags, a.part, a.pslot)
+   if ((AF) && a.xwg == 8)                                                                              \
+   {                                                                                                    \
+      hipLaunchKernelGGL((k_diag_tpe<D, Q, MASS, DIFF, SP, AF, 8>), dim3((nb + 7) / 8), dim3(512), 0, s, a.ne, \
+                         a.blk_begin, a.blk_end, a.n_owned, a.gmap, a.qdd, a.qdm, a.y, a.yg, b, drow,      \
+                         a.lane_flags, a.part, a.pslot);                                                   \
+   }                                                                                                    \
+   else                                                                                                 \
+   {                                                                                                    \
+      hipLaunchKernelGGL((k_diag_tpe<D, Q, MASS, DIFF, SP, AF>), grid, block, 0, s, a.ne, a.blk_begin,    \
+                         a.blk_end, a.n_owned, a.gmap, a.qdd, a.qdm, a.y, a.yg, b, drow, a.lane_flags,    \
+                         a.part, a.pslot);                                                                 \
+   }
    const bool aff = a.kind == QLAYOUT_AFFINE;
    ECM2_VERIFY(!aff || (MASS && DIFF), ERR_INTERNAL, "AFFINE qdata needs both integrators");
    if (a.yg) { if (aff) { ECM2_DIAG(true, true); } else { ECM2_DIAG(true, false); } }

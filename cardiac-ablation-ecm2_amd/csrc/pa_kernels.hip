@@ -2064,9 +2064,13 @@ __device__ __forceinline__ void brick_cand(int P, int &c0, int &l0, int &n)
 
 // VAR bit 1: load the stage-3 qdata at the top of the z stage (fewer VGPRs, more
 // workgroups per CU) instead of at kernel entry (in flight during stages 1-2); bit 2:
-// 16-byte paired loads (line_load_qdata_x2, even Q1D)
+// 16-byte paired loads (line_load_qdata_x2, even Q1D); bit 128: one LDS buffer of
+// 3 D Q^2 doubles per element instead of two (2 D^2 Q + 3 D Q^2): each stage reads its
+// lines into registers, waits at a barrier, then overwrites the buffer (three more
+// barriers, 36% less LDS: 9 instead of 5 p = 4 workgroups per CU)
 template <int D, int Q, int BZ, bool MASS, bool DIFF, bool SPLIT, int VAR>
-__global__ void __launch_bounds__((BrickShape<D, Q, BZ>::NT), (BrickShape<D, Q, BZ>::WPE))
+__global__ void __launch_bounds__((BrickShape<D, Q, BZ>::NT),
+                                  ((VAR & 128) && D <= 5 ? 5 : BrickShape<D, Q, BZ>::WPE))
 k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *__restrict__ bmap, int n_owned,
               const double *__restrict__ qdd, const double *__restrict__ qdm,
               const double *__restrict__ x, const double *__restrict__ xg,
@@ -2077,8 +2081,11 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
    constexpr int LX = S::LX, LY = S::LY, NB = S::NB;
    static_assert(QQ <= 64, "brick kernel needs Q1D <= 8");
    static_assert(SB >= ND, "staged outputs reuse bufB");
-   __shared__ double bufA[NE * SA];
+   constexpr bool ONE = (VAR & 128) != 0;
+   static_assert(SB >= SA, "one-buffer variant");
+   __shared__ double bufA[ONE ? 1 : NE * SA];
    __shared__ double bufB[NE * SB];
+   double *const sA = ONE ? bufB : bufA;  // the x-stage lines
    const int k = k_begin + (int)blockIdx.x;
    if (k >= k_end) { return; }  // whole workgroup
    const int t = threadIdx.x;
@@ -2097,7 +2104,7 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
    constexpr bool AFF = (VAR & 64) != 0;
    v2d pa[Q];
    double cc[6];
-   if (AFF && t < NE * QQ)
+   if (AFF && !(VAR & 1) && t < NE * QQ)
    {
       const int e = belem[(size_t)k * NE + t / QQ], l = t % QQ;
       constexpr int NQ = Q * Q * Q;
@@ -2128,7 +2135,7 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
          const int d = bdof(mp[dx]);
          xl[dx] = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
       }
-      double *o = bufA + elt * SA;
+      double *o = sA + elt * (ONE ? SB : SA);
 #pragma unroll
       for (int qx = 0; qx < Q; qx++)
       {
@@ -2145,19 +2152,24 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
    }
    __syncthreads();
    // ---- lanes (element, qx, dz): contract in y
+   double la[D], lb[D];
    if (t < NE * DQ)
    {
-      CBasis *bp = stage_basis<D, Q>();
       const int elt = t / DQ, l = t % DQ, qx = l % Q, dz = l / Q;
-      const double *in = bufA + elt * SA;
-      double *o = bufB + elt * SB;
-      double la[D], lb[D];
+      const double *in = sA + elt * (ONE ? SB : SA);
 #pragma unroll
       for (int dy = 0; dy < D; dy++)
       {
          la[dy] = in[(dz * D + dy) * Q + qx];
          lb[dy] = in[DD * Q + (dz * D + dy) * Q + qx];
       }
+   }
+   if (ONE) { __syncthreads(); }
+   if (t < NE * DQ)
+   {
+      CBasis *bp = stage_basis<D, Q>();
+      const int elt = t / DQ, l = t % DQ, qx = l % Q, dz = l / Q;
+      double *o = bufB + elt * SB;
 #pragma unroll
       for (int qy = 0; qy < Q; qy++)
       {
@@ -2184,6 +2196,13 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
       CBasis *bp = stage_basis<D, Q>();
       const int elt = t / QQ, l = t % QQ;
       if (!AFF && (VAR & 1)) { line_load_qdata<D, Q, MASS, DIFF, false>(qv, belem[(size_t)k * NE + elt], l, qdd, qdm); }
+      // AFFINE_E, VAR bit 1: C_e here, the per-point pairs inside the qz loop (fewer live VGPRs)
+      const v2d *pz = reinterpret_cast<const v2d *>(qdm) + (size_t)belem[(size_t)k * NE + elt] * (Q * QQ) + l;
+      if (AFF && (VAR & 1))
+      {
+#pragma unroll
+         for (int c = 0; c < 6; c++) { cc[c] = qdd[(size_t)belem[(size_t)k * NE + elt] * 6 + c]; }
+      }
       double *in = bufB + elt * SB;
       double *o = in;
       double l0[D], l1[D], l2[D];
@@ -2214,6 +2233,7 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
             if (MASS) { u += bz * l2[dz]; }
          }
          double fx = 0.0, fy = 0.0, fz = 0.0, m = 0.0;
+         if (AFF && (VAR & 1)) { pa[qz] = pz[qz * QQ]; }
          if (DIFF)
          {
             if (AFF)
@@ -2254,21 +2274,27 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
    }
    __syncthreads();
    // ---- lanes (element, qx, dz): transpose in y
+   double t0[Q], t1[Q], t2[Q];
    if (t < NE * DQ)
    {
-      CBasis *bp = stage_basis<D, Q>();
       const int elt = t / DQ, l = t % DQ, qx = l % Q, dz = l / Q;
       const double *in = bufB + elt * SB;
-      double *o = bufA + elt * SA;
-      double l0[Q], l1[Q], l2[Q];
 #pragma unroll
       for (int qy = 0; qy < Q; qy++)
       {
          const int oo = (dz * Q + qy) * Q + qx;
-         l0[qy] = in[oo];
-         l1[qy] = in[D * QQ + oo];
-         l2[qy] = in[2 * D * QQ + oo];
+         t0[qy] = in[oo];
+         t1[qy] = in[D * QQ + oo];
+         t2[qy] = in[2 * D * QQ + oo];
       }
+   }
+   if (ONE) { __syncthreads(); }
+   if (t < NE * DQ)
+   {
+      CBasis *bp = stage_basis<D, Q>();
+      const int elt = t / DQ, l = t % DQ, qx = l % Q, dz = l / Q;
+      double *o = sA + elt * (ONE ? SB : SA);
+      const double *l0 = t0, *l1 = t1, *l2 = t2;
 #pragma unroll
       for (int dy = 0; dy < D; dy++)
       {
@@ -2286,25 +2312,30 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
    }
    __syncthreads();
    // ---- lanes (element, dy, dz): transpose in x -> element outputs staged in LDS [elt][a]
+   double l0[Q], l1[Q];
    if (t < NE * DD)
    {
-      CBasis *bp = stage_basis<D, Q>();
       const int elt = t / DD, l = t % DD;
-      const double *in = bufA + elt * SA;
-      double l0[Q], l1[Q];
+      const double *in = sA + elt * (ONE ? SB : SA);
 #pragma unroll
       for (int qx = 0; qx < Q; qx++)
       {
          l0[qx] = in[l * Q + qx];
          l1[qx] = in[DD * Q + l * Q + qx];
       }
+   }
+   if (ONE) { __syncthreads(); }
+   if (t < NE * DD)
+   {
+      CBasis *bp = stage_basis<D, Q>();
+      const int elt = t / DD, l = t % DD;
 #pragma unroll
       for (int dx = 0; dx < D; dx++)
       {
          double v = 0.0;
 #pragma unroll
          for (int qx = 0; qx < Q; qx++) { v += bp->G[qx + MQ * dx] * l0[qx] + bp->B[qx + MQ * dx] * l1[qx]; }
-         bufB[elt * ND + l * D + dx] = v;  // bufB is free: stage 4 read it before the barrier
+         bufB[elt * ND + l * D + dx] = v;  // bufB is free: stage 4 (ONE: stage 5) read it before a barrier
       }
    }
    __syncthreads();
@@ -2994,7 +3025,8 @@ void upload_basis(int D, int Q, const Basis1D &b)
                               ((size_t)(D - 1) * MAX_Q1D + (Q - 1)) * sizeof(Basis1D), hipMemcpyHostToDevice));
 }
 
-// experiment knob ECM2_BRICK_VARIANT (bit 1: qdata loaded at the z stage)
+// experiment knob ECM2_BRICK_VARIANT (bit 1: qdata loaded at the z stage; bit 2: 16-byte paired
+// qdata loads, native layout; bit 4: one LDS buffer per element, AFFINE_E)
 int brick_variant()
 {
    static int v = [] {
@@ -3019,8 +3051,13 @@ void launch_brick_mdq(const ApplyArgs &a, hipStream_t s)
    {
       if constexpr (MASS && DIFF)
       {
-         if (brick_variant() & 1) { if (split) { ECM2_BRICK(true, 65); } else { ECM2_BRICK(false, 65); } }
-         else { if (split) { ECM2_BRICK(true, 64); } else { ECM2_BRICK(false, 64); } }
+         switch (brick_variant() & 5)
+         {
+            case 1: if (split) { ECM2_BRICK(true, 65); } else { ECM2_BRICK(false, 65); } break;
+            case 4: if (split) { ECM2_BRICK(true, 192); } else { ECM2_BRICK(false, 192); } break;
+            case 5: if (split) { ECM2_BRICK(true, 193); } else { ECM2_BRICK(false, 193); } break;
+            default: if (split) { ECM2_BRICK(true, 64); } else { ECM2_BRICK(false, 64); } break;
+         }
       }
       else { ECM2_VERIFY(false, ERR_INTERNAL, "AFFINE qdata needs both integrators"); }
       return;

@@ -433,9 +433,12 @@ void ParPAForm::mult(const double *x_true, double *y_true, hipStream_t s)
 {
    const bool emu = !comm_ && emulate_exchange();
    ECM2_VERIFY(comm_ || emu, ERR_STATE, "mult needs the RCCL transport (use the loopback group otherwise)");
-   if (!par_graph() || graph_failed_ || local_->timing_on())
+   if (!par_graph() || graph_failed_ || local_->timing_on() || !p2p_warm_)
    {
+      // the first Mult runs directly on every rank: RCCL sets up its peer connections
+      // lazily at the first send/recv, which then happens outside a stream capture
       mult_stages(x_true, y_true, s, emu);
+      p2p_warm_ = true;
       return;
    }
    // One HIP graph per (x, y): the ~15 launches / event operations / RCCL group calls of a

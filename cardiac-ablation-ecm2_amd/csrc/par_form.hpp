@@ -79,15 +79,16 @@ private:
    void rccl_exchange(bool transpose);  // P (false) or P^T (true) on the comm stream
    void mult_stages(const double *x_true, double *y_true, hipStream_t s, bool emu);
    int b_int() const { return part_.ne_interior / kElemBlock; }
-   int b_split_ = 0;
+   int b_split_ = 0;                    // interior part A = [0, b_split_) (0: no split)
    std::vector<int> send_start_;        // per neighbour: first owned index of a contiguous send range, or -1
    bool pack_needed_ = true;            // some neighbour's send range is not contiguous
-   const double *x_cur_ = nullptr;      // x_true of the Mult being enqueued (contiguous sends)                    // interior part A = [0, b_split_) (0: no split)
+   const double *x_cur_ = nullptr;      // x_true of the Mult being enqueued (contiguous sends)
    hipEvent_t ev_bnd_ = nullptr;        // boundary elements applied (comm stream)
    // Mult as a HIP graph per (x, y) pair: one launch instead of ~15 API calls
    hipStream_t cap_ = nullptr;          // capture stream
    std::map<std::pair<const double *, double *>, hipGraphExec_t> graphs_;
    bool graph_failed_ = false;
+   bool p2p_warm_ = false;  // one direct Mult ran (RCCL peer connections exist) before any capture
    LocalPart part_;
    std::unique_ptr<PAForm> local_;
    DeviceArray<int> send_idx_;

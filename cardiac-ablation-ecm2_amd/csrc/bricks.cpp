@@ -191,17 +191,20 @@ void find_bricks(int ne, int D, const std::vector<int> &gm, int bz, const std::v
    for (int e0 = 0; e0 < ne; e0++)
    {
       if (in_brick[e0]) { continue; }
-      int el[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+      std::vector<int> el(nbe, -1);
       el[0] = e0;
       el[1] = nb(0, e0);
       el[2] = nb(1, e0);
       el[3] = nb(0, el[2]);
       bool ok = el[1] >= 0 && el[3] >= 0 && nb(1, el[1]) == el[3];
-      if (ok && bz == 2)
+      // further 2 x 2 layers (bz = 2; column bricks bz = 4, 8): linked in z to the layer
+      // below and in x / y among themselves
+      for (int z = 1; z < bz && ok; z++)
       {
-         for (int i = 0; i < 4; i++) { el[4 + i] = nb(2, el[i]); }
-         ok = el[4] >= 0 && el[5] >= 0 && el[6] >= 0 && el[7] >= 0 && nb(0, el[4]) == el[5] &&
-              nb(1, el[4]) == el[6] && nb(0, el[6]) == el[7] && nb(1, el[5]) == el[7];
+         int *l = el.data() + 4 * z;
+         for (int i = 0; i < 4; i++) { l[i] = nb(2, l[i - 4]); }
+         ok = l[0] >= 0 && l[1] >= 0 && l[2] >= 0 && l[3] >= 0 && nb(0, l[0]) == l[1] &&
+              nb(1, l[0]) == l[2] && nb(0, l[2]) == l[3] && nb(1, l[1]) == l[3];
       }
       for (int i = 0; i < nbe && ok; i++)
       {

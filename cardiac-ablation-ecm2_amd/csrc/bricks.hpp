@@ -31,9 +31,9 @@ FaceNeighbors face_neighbors(int ne, int D, const std::vector<int> &gmap);
 // fichera hex is a 64^3 patch).  Returns perm (internal position -> element).
 std::vector<int> face_brick_order(int ne, int D, const std::vector<int> &gmap);
 
-// 2 x 2 x bz groups for the p >= 3 brick kernel: greedy in element order, all twelve (bz =
-// 2) internal faces linked, every member in the same apply segment seg[e], no orientation
-// signs.  belem: [nbrick][4 bz] (member ex + 2 ey + 4 ez); in_brick marks members.
+// 2 x 2 x bz groups for the p >= 3 brick kernel (bz = 1, 2, or 4 / 8 for the column
+// bricks the kernel marches layer by layer): greedy in element order, all internal faces
+// linked, every member in the same apply segment seg[e], no orientation signs.  belem: [nbrick][4 bz] (member ex + 2 ey + 4 ez); in_brick marks members.
 void find_bricks(int ne, int D, const std::vector<int> &gmap, int bz, const std::vector<int> &seg,
                  std::vector<int> &belem, std::vector<char> &in_brick);
 

@@ -135,7 +135,8 @@ void PAForm::set_latency_from(int b)
 
 void PAForm::set_line_bricks(int bz)
 {
-   ECM2_VERIFY(bz >= -1 && bz <= 2, ERR_ARG, "brick mode " << bz << " not in {-1, 0, 1, 2}");
+   ECM2_VERIFY(bz >= -1 && (bz <= 2 || bz == 4 || bz == 8), ERR_ARG,
+               "brick mode " << bz << " not in {-1, 0, 1, 2, 4, 8}");
    line_bricks_ = bz;
    gmap_line_.resize(0);
    assembled_ = false;
@@ -298,7 +299,8 @@ static int line_brick_mode()
 {
    static int v = [] {
       const char *e = std::getenv("ECM2_LINE_BRICK");
-      return e ? std::max(0, std::min(2, std::atoi(e))) : 1;
+      const int b = e ? std::atoi(e) : 1;
+      return (b >= 0 && (b <= 2 || b == 4 || b == 8)) ? b : 1;
    }();
    return v;
 }
@@ -577,6 +579,7 @@ void PAForm::assemble(hipStream_t s)
       };
       const int nblk = layout_.nblk();
       int bz = scatter_ == SCATTER_PARTIALS ? (line_bricks_ >= 0 ? line_bricks_ : line_brick_mode()) : 0;
+      if (bz > 2 && !kern::has_brick(D_, Q_, bz)) { bz = 1; }
       if (bz == 2 && !kern::has_brick(D_, Q_, 2)) { bz = 1; }
       if (bz == 1 && !kern::has_brick(D_, Q_, 1)) { bz = 0; }
       std::vector<int> belem;

@@ -2040,8 +2040,13 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ chunks, int n_owned
 template <int D, int Q, int BZ>
 struct BrickShape
 {
-   static constexpr int NE = 4 * BZ, DD = D * D, QQ = Q * Q, DQ = D * Q, ND = D * D * D;
+   // BZ <= 2: all 4 BZ elements at once; BZ > 2 (column bricks): NL = BZ layers of 2 x 2
+   // elements marched in z by one workgroup, each layer's top lattice plane carried in LDS
+   // into the next layer's bottom plane, so the column's internal z faces never reach HBM
+   static constexpr int NL = BZ > 2 ? BZ : 1, NET = 4 * BZ;
+   static constexpr int NE = 4 * (BZ > 2 ? 1 : BZ), DD = D * D, QQ = Q * Q, DQ = D * Q, ND = D * D * D;
    static constexpr int LX = 2 * (D - 1) + 1, LY = LX, LZ = BZ * (D - 1) + 1, NB = LX * LY * LZ;
+   static constexpr int NBL = LX * LY * ((BZ > 2 ? 1 : BZ) * (D - 1) + 1);  // lattice points per pass
    static constexpr int SURF = 2 * LX * LY + 2 * (LZ - 2) * LX + 2 * (LZ - 2) * (LY - 2);
    // per-element LDS: SA holds the x-stage lines (2 D^2 Q), SB the y/z-stage planes (3 D Q^2,
    // the z stage works in place); staged element outputs (D^3) reuse SB
@@ -2095,6 +2100,12 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
       return ((ez * (D - 1) + dz) * LY + ey * (D - 1) + dy) * LX + ex * (D - 1) + dx;
    };
 
+   __shared__ double carry[S::NL > 1 ? 2 * LX * LY : 1];  // column bricks: top plane -> next layer
+#pragma unroll 1
+   for (int layer = 0; layer < S::NL; layer++)
+   {
+   const int eo = layer * NE;  // this pass's first element in the brick
+   const int *be = belem + (size_t)k * S::NET + eo;
    // qdata of the (element, qx, qy) column this lane weights in stage 3: in flight
    // during the gather and the x / y contractions
    double qv[7][Q];
@@ -2106,7 +2117,7 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
    double cc[6];
    if (AFF && !(VAR & 1) && t < NE * QQ)
    {
-      const int e = belem[(size_t)k * NE + t / QQ], l = t % QQ;
+      const int e = be[t / QQ], l = t % QQ;
       constexpr int NQ = Q * Q * Q;
 #pragma unroll
       for (int qz = 0; qz < Q; qz++) { pa[qz] = reinterpret_cast<const v2d *>(qdm)[(size_t)e * NQ + qz * QQ + l]; }
@@ -2117,9 +2128,9 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
    {
       if constexpr ((VAR & 2) && Q % 2 == 0)
       {
-         line_load_qdata_x2<D, Q, MASS, DIFF>(qv, belem[(size_t)k * NE + t / QQ], t % QQ, qdd, qdm);
+         line_load_qdata_x2<D, Q, MASS, DIFF>(qv, be[t / QQ], t % QQ, qdd, qdm);
       }
-      else { line_load_qdata<D, Q, MASS, DIFF, (VAR & 64) != 0>(qv, belem[(size_t)k * NE + t / QQ], t % QQ, qdd, qdm); }
+      else { line_load_qdata<D, Q, MASS, DIFF, (VAR & 64) != 0>(qv, be[t / QQ], t % QQ, qdd, qdm); }
    }
 
    // ---- lanes (element, dy, dz): gather the x-line, contract in x
@@ -2127,7 +2138,7 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
    {
       CBasis *bp = stage_basis<D, Q>();
       const int elt = t / DD, l = t % DD;
-      const int *mp = bm + lattice(elt, 0, l % D, l / D);
+      const int *mp = bm + lattice(eo + elt, 0, l % D, l / D);
       double xl[D];
 #pragma unroll
       for (int dx = 0; dx < D; dx++)
@@ -2195,13 +2206,13 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
    {
       CBasis *bp = stage_basis<D, Q>();
       const int elt = t / QQ, l = t % QQ;
-      if (!AFF && (VAR & 1)) { line_load_qdata<D, Q, MASS, DIFF, false>(qv, belem[(size_t)k * NE + elt], l, qdd, qdm); }
+      if (!AFF && (VAR & 1)) { line_load_qdata<D, Q, MASS, DIFF, false>(qv, be[elt], l, qdd, qdm); }
       // AFFINE_E, VAR bit 1: C_e here, the per-point pairs inside the qz loop (fewer live VGPRs)
-      const v2d *pz = reinterpret_cast<const v2d *>(qdm) + (size_t)belem[(size_t)k * NE + elt] * (Q * QQ) + l;
+      const v2d *pz = reinterpret_cast<const v2d *>(qdm) + (size_t)be[elt] * (Q * QQ) + l;
       if (AFF && (VAR & 1))
       {
 #pragma unroll
-         for (int c = 0; c < 6; c++) { cc[c] = qdd[(size_t)belem[(size_t)k * NE + elt] * 6 + c]; }
+         for (int c = 0; c < 6; c++) { cc[c] = qdd[(size_t)be[elt] * 6 + c]; }
       }
       double *in = bufB + elt * SB;
       double *o = in;
@@ -2340,9 +2351,9 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
    }
    __syncthreads();
    // ---- lattice points: sum the holders in a fixed (z, y, x) order, store or publish
-   for (int p = t; p < NB; p += S::NT)
+   for (int p = t; p < S::NBL; p += S::NT)
    {
-      const int X = p % LX, Y = (p / LX) % LY, Z = p / (LX * LY);
+      const int X = p % LX, Y = (p / LX) % LY, Z = p / (LX * LY);  // Z within this pass
       int cx, lx, nx, cy, ly, ny, cz, lz, nz;
       brick_cand<D>(X, cx, lx, nx);
       brick_cand<D>(Y, cy, ly, ny);
@@ -2357,10 +2368,24 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
                const int a = ((iz ? 0 : lz) * D + (iy ? 0 : ly)) * D + (ix ? 0 : lx);
                v += bufB[elt * ND + a];
             }
-      const int g = bm[p];
+      if constexpr (S::NL > 1)
+      {
+         if (Z == 0 && layer > 0) { v += carry[((layer - 1) & 1) * LX * LY + Y * LX + X]; }
+         if (Z == D - 1 && layer < S::NL - 1)
+         {
+            carry[(layer & 1) * LX * LY + Y * LX + X] = v;  // completed by the next layer
+            continue;
+         }
+      }
+      const int zg = layer * (D - 1) + Z;  // lattice plane in the whole brick
+      const int g = bm[p + layer * (D - 1) * LX * LY];
       const int d = bdof(g);
       if (!bshared(g)) { *((!SPLIT || d < n_owned) ? y + d : yg + (d - n_owned)) = v; }
-      else { part[(size_t)k * S::SURF + brick_surface_index(D, BZ, X, Y, Z)] = v; }  // surface only (setup)
+      else { part[(size_t)k * S::SURF + brick_surface_index(D, BZ, X, Y, zg)] = v; }  // surface only (setup)
+   }
+   // the next layer's first writes (bufA; ONE: bufB) follow reads of this pass's last
+   // stages behind barriers, except in the one-buffer variant
+   if (S::NL > 1 && ONE) { __syncthreads(); }
    }
 }
 
@@ -3080,11 +3105,12 @@ void launch_brick_dq(bool mass, bool diff, const ApplyArgs &a, hipStream_t s)
 }
 
 // bricks of 2 x 2 x bz elements for Q1D = D1D + 1 (the default rule), p = 3..6; a
-// 2 x 2 x 2 brick's LDS (16 S doubles) exceeds 160 KiB at p = 6
+// 2 x 2 x 2 brick's LDS (16 S doubles) exceeds 160 KiB at p = 6; column bricks (bz = 4, 8)
+// march 2 x 2 layers and need one layer's LDS
 bool has_brick(int D, int Q, int bz)
 {
    if (Q != D + 1 || D < 4 || D > 7) { return false; }
-   return bz == 1 || (bz == 2 && D <= 6);
+   return bz == 1 || (bz == 2 && D <= 6) || bz == 4 || (bz == 8 && D == 5);
 }
 
 int brick_points(int D, int bz) { return (2 * D - 1) * (2 * D - 1) * (bz * (D - 1) + 1); }
@@ -3105,6 +3131,11 @@ static void apply_brick(int D, int Q, bool mass, bool diff, const ApplyArgs &a, 
    ECM2_BRICK_CASE(6, 1)
    ECM2_BRICK_CASE(6, 2)
    ECM2_BRICK_CASE(7, 1)
+   ECM2_BRICK_CASE(4, 4)  // column bricks: 2 x 2 x bz marched in z
+   ECM2_BRICK_CASE(5, 4)
+   ECM2_BRICK_CASE(5, 8)
+   ECM2_BRICK_CASE(6, 4)
+   ECM2_BRICK_CASE(7, 4)
 #undef ECM2_BRICK_CASE
    ECM2_VERIFY(false, ERR_UNSUPPORTED, "no brick kernel for D1D=" << D << " Q1D=" << Q << " bz=" << a.brick_bz);
 }

@@ -410,12 +410,13 @@ def test_full_size_c2_deterministic():
 @pytest.mark.parametrize("mesh_name", ["inline_hex", "cart_bricks", "nonaligned", "fichera_r1", "cart_130"])
 @pytest.mark.parametrize("order", [3, 4, 5])
 def test_line_bricks(mesh_name, order):
-    """p >= 3 brick kernel (2 x 2 x 1 and 2 x 2 x 2 workgroups, LDS lattice assembly) and
-    the per-element line kernel it falls back to: each matches the oracle, overwrites
-    every y entry (NaN prefill), is bitwise reproducible, and the brick modes agree."""
+    """p >= 3 brick kernel (2 x 2 x 1 and 2 x 2 x 2 workgroups, LDS lattice assembly; 2 x 2 x 4
+    column bricks marched layer by layer) and the per-element line kernel it falls back to:
+    each matches the oracle, overwrites every y entry (NaN prefill), is bitwise
+    reproducible, and the brick modes agree."""
     m = make_mesh(mesh_name)
     ys = {}
-    for bz in (0, 1, 2):
+    for bz in (0, 1, 2, 4):
         fes = E.H1Space(m, order)
         form = E.BilinearForm(fes, kernel=E.KERNEL_LINE, bricks=bz)
         en = m.element_nodes()
@@ -438,7 +439,7 @@ def test_line_bricks(mesh_name, order):
         form.Mult(dev(x), y2)
         assert torch.equal(y, y2)
         ys[bz] = host(y)
-    assert relerr(ys[1], ys[0]) <= RTOL and relerr(ys[2], ys[0]) <= RTOL
+    assert relerr(ys[1], ys[0]) <= RTOL and relerr(ys[2], ys[0]) <= RTOL and relerr(ys[4], ys[0]) <= RTOL
 
 
 def test_full_size_c5_bricks():
@@ -451,18 +452,19 @@ def test_full_size_c5_bricks():
     a, b = alpha_bioheat(P), k_of_T(temperature(P))
     x = np.random.default_rng(5).uniform(-1, 1, fes.ndofs)
     out = {}
-    for bz in (0, 2):
+    for bz in (0, 2, 4, 8):
         form = E.BilinearForm(fes, bricks=bz)
         form.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(a.reshape(fes.ne, -1)))))
         form.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(dev(b.reshape(fes.ne, -1)))))
         form.Assemble()
         if bz:
-            assert form.BrickInfo() == (fes.ne // 8, 2)
+            assert form.BrickInfo() == (fes.ne // (4 * bz), bz)
         y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
         form.Mult(dev(x), y)
         out[bz] = host(y)
     ref = O.OracleOperator(en, fes.gather_map(), fes.ndofs, 4, alpha=a, beta=b).mult(x)
-    assert relerr(out[2], ref) <= RTOL and relerr(out[0], ref) <= RTOL
+    for bz in out:
+        assert relerr(out[bz], ref) <= RTOL, bz
 
 
 @pytest.mark.parametrize("mesh_name", ["nonaligned", "fichera_r1", "cart_bricks", "cart_130", "trilinear"])

@@ -2101,7 +2101,7 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
    };
 
    __shared__ double carry[S::NL > 1 ? 2 * LX * LY : 1];  // column bricks: top plane -> next layer
-#pragma unroll 1
+#pragma unroll
    for (int layer = 0; layer < S::NL; layer++)
    {
    const int eo = layer * NE;  // this pass's first element in the brick

@@ -154,7 +154,8 @@ int ecm2_pa_form_set_scatter(ecm2_pa_form *f, int mode);
 /* Work grouping of the p >= 3 line-kernel family (no reference counterpart; the
  * reference applies each element independently, bilininteg_diffusion_kernels.hpp:989-1214):
  * bz = -1 default (2 x 2 x 1), 0 = per-element line
- * kernel only, 1 = bricks of 2 x 2 x 1 elements, 2 = 2 x 2 x 2.  A brick is one workgroup;
+ * kernel only, 1 = bricks of 2 x 2 x 1 elements, 2 = 2 x 2 x 2, 4 / 8 = 2 x 2 x bz column
+ * bricks marched layer by layer (p = 3..6; bz = 8 only at p = 4).  A brick is one workgroup;
  * its internal shared faces are summed in LDS in a fixed order (deterministic).  Bricks
  * exist only with ECM2_SCATTER_PARTIALS; elements outside bricks use the line kernel. */
 int ecm2_pa_form_set_bricks(ecm2_pa_form *f, int bz);

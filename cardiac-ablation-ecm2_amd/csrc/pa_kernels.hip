@@ -2067,6 +2067,7 @@ __device__ __forceinline__ void brick_cand(int P, int &c0, int &l0, int &n)
    else { c0 = 1; l0 = P - (D - 1); n = 1; }
 }
 
+// (ECM2_BRICK_VARIANT bit 8 selects VAR bit 256, the XCD-contiguous order, on AFFINE_E.)
 // VAR bit 1: load the stage-3 qdata at the top of the z stage (fewer VGPRs, more
 // workgroups per CU) instead of at kernel entry (in flight during stages 1-2); bit 2:
 // 16-byte paired loads (line_load_qdata_x2, even Q1D); bit 128: one LDS buffer of
@@ -2091,7 +2092,9 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
    __shared__ double bufA[ONE ? 1 : NE * SA];
    __shared__ double bufB[NE * SB];
    double *const sA = ONE ? bufB : bufA;  // the x-stage lines
-   const int k = k_begin + (int)blockIdx.x;
+   // VAR bit 256: XCD-contiguous brick order (neighbouring bricks share x values and
+   // partial-slot lines: keep them in one XCD's L2)
+   const int k = k_begin + ((VAR & 256) ? xcd_contiguous(blockIdx.x, gridDim.x) : (int)blockIdx.x);
    if (k >= k_end) { return; }  // whole workgroup
    const int t = threadIdx.x;
    const int *bm = bmap + (size_t)k * NB;
@@ -3052,11 +3055,13 @@ void upload_basis(int D, int Q, const Basis1D &b)
 
 // experiment knob ECM2_BRICK_VARIANT (bit 1: qdata loaded at the z stage; bit 2: 16-byte paired
 // qdata loads, native layout; bit 4: one LDS buffer per element, AFFINE_E)
+// default 8: XCD-contiguous brick order on AFFINE_E (C5: kernel 0.575 -> 0.566 ms, Mult
+// 0.754 -> 0.739 ms, profiles/r1_ab_xcd_brick.txt); ECM2_BRICK_VARIANT=0: launch order
 int brick_variant()
 {
    static int v = [] {
       const char *e = std::getenv("ECM2_BRICK_VARIANT");
-      return e ? std::atoi(e) : 0;
+      return e ? std::atoi(e) : 8;
    }();
    return v;
 }
@@ -3076,8 +3081,9 @@ void launch_brick_mdq(const ApplyArgs &a, hipStream_t s)
    {
       if constexpr (MASS && DIFF)
       {
-         switch (brick_variant() & 5)
+         switch (brick_variant() & 13)
          {
+            case 8: if (split) { ECM2_BRICK(true, 320); } else { ECM2_BRICK(false, 320); } break;
             case 1: if (split) { ECM2_BRICK(true, 65); } else { ECM2_BRICK(false, 65); } break;
             case 4: if (split) { ECM2_BRICK(true, 192); } else { ECM2_BRICK(false, 192); } break;
             case 5: if (split) { ECM2_BRICK(true, 193); } else { ECM2_BRICK(false, 193); } break;

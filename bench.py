@@ -3,28 +3,39 @@
 
 Metric (BASELINE.json): "MDoF/s on PA diffusion+mass Mult, hex p=2; % HBM roofline at
 1/2/4/8 GPUs".  One *step* = one operator Mult y = A x (L-vector in, L-vector out;
-tests/benchmarks/bench_assembly_levels.cpp:281-286 counts ndofs per Mult) with x, y
-and the operator resident in HBM.  Workload: BASELINE configs[1] -- inline-hex refined
-to ~1M DoF (Cartesian 50^3, p = 2, 1,030,301 DoF) per GPU; with N GPUs the global
-mesh is 50 x 50 x 50N, z-slab partitioned, one rank per GPU (weak scaling) with the
-shared-DoF exchange over RCCL.  --workload c4 runs configs[3] (Cartesian 108^3,
-10.2M DoF, split over the ranks: strong scaling).
+tests/benchmarks/bench_assembly_levels.cpp:281-286 counts ndofs per Mult) with x, y and the
+operator resident in HBM.
 
-Coefficients are the bioheat ones: alpha = rho*c_eff(x) (FunctionCoefficient projected
-at the quadrature points) and beta = gamma*dt*k(T) with T an H1 grid function (the
-Pennes law, evaluated on the device at Assemble).  Inputs are synthetic (no data files).
+Workload (default): BASELINE configs[3], the north-star configuration -- Cartesian 108^3,
+H1 p = 2, 10,218,313 DoF, z-slab partitioned over the ranks with the shared-DoF exchange over
+RCCL (one rank per GPU; strong scaling).  --workload c2 runs configs[1] (Cartesian 50^3 per
+GPU, weak scaling), c3 configs[2] (fichera refined, + PCG), c5 configs[4] (68^3, p = 4).
+
+Coefficients are the bioheat ones: alpha = rho*c_eff(x) (FunctionCoefficient projected at the
+quadrature points) and beta = gamma*dt*k(T) with T an H1 grid function (the Pennes law,
+evaluated on the device at Assemble).  Inputs are synthetic (no data files).
+
+Roofline fields: `achieved` / `frac` = HBM bytes the dominant kernel actually
+moves per launch (rocprofv3 FETCH_SIZE / WRITE_SIZE pin of this workload and layout, with its
+provenance) / its HIP-event time / 8 TB/s -- or, without a pin, the formulation's minimum
+bytes (stored qdata + x + y + map) as a lower bound; `alg_ratio` = SURVEY §8(d)'s fixed
+algorithmic bytes (56 B per quadrature point) / the same time / 8 TB/s, which exceeds 1
+when the compressed (AFFINE) layout stores less than the formula counts.
 """
 import argparse
 import importlib.util
 import json
 import os
+import subprocess
 import sys
+import threading
 import time
 
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+METRIC = "MDoF/s on PA diffusion+mass Mult, hex p=2; % HBM roofline at 1/2/4/8 GPUs"
 
 
 def load_pkg():
@@ -37,6 +48,30 @@ def load_pkg():
     sys.modules["ecm2_amd"] = mod
     spec.loader.exec_module(mod)
     return mod
+
+
+class Deadline:
+    """Per-rank watchdog: if the run is not done after `seconds`, print this rank's last stage
+    and exit non-zero (no re-exec, no retry)."""
+
+    def __init__(self, seconds, rank):
+        self.rank, self.stage, self.t0 = rank, "start", time.time()
+        self._done = threading.Event()
+        if seconds > 0:
+            threading.Thread(target=self._watch, args=(seconds,), daemon=True).start()
+
+    def at(self, stage):
+        self.stage = stage
+        print(f"[bench rank {self.rank}] {time.time() - self.t0:7.1f}s {stage}", file=sys.stderr, flush=True)
+
+    def done(self):
+        self._done.set()
+
+    def _watch(self, seconds):
+        if not self._done.wait(seconds):
+            print(f"bench.py rank {self.rank}: deadline of {seconds:.0f}s exceeded; last stage: {self.stage}",
+                  file=sys.stderr, flush=True)
+            os._exit(3)
 
 
 def alpha_fn(P):
@@ -66,59 +101,141 @@ def bioheat_coefficients(E, torch, mesh, fes, part=None):
     return torch.as_tensor(alpha).cuda(), torch.as_tensor(T).cuda()
 
 
+def qdata_layout(E, form):
+    """Quadrature-data layout of a (local) form: affine | affine_e | blocked | native."""
+    return {E.QLAYOUT_NATIVE: "native", E.QLAYOUT_BLOCKED: "blocked",
+            E.QLAYOUT_AFFINE: "affine", E.QLAYOUT_AFFINE_E: "affine_e"}[form.info()["layout"]]
+
+
+def min_bytes(form, ne, nd, n_true):
+    """The formulation's minimum HBM bytes per Mult: its stored qdata read once, x read and y
+    written once, one int32 map entry per element dof."""
+    return form.qdata_bytes() + 16.0 * n_true + 4.0 * ne * nd
+
+
+def time_mults(apply, x, y, steps, warmup, world, dist, torch):
+    for _ in range(warmup):
+        apply(x, y)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        apply(x, y)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
+def kernel_ms(forms, apply, x, y, steps, torch):
+    """HIP events around the dominant (fused apply) kernel(s) of each Mult, on the stream they
+    are launched on (a second pass, kept out of the timed loop); ms per Mult."""
+    for f in forms:
+        f.timing(True)
+    for _ in range(steps):
+        apply(x, y)
+    torch.cuda.synchronize()
+    kms = sum(f.timing_get()[0] for f in forms)
+    for f in forms:
+        f.timing(False)
+    return kms / steps
+
+
+def pmc_pin(workload, world, layout):
+    """Pinned PMC traffic of this workload's dominant kernel in this layout (profiles/pmc_pin.py)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{workload}_n{world}_{layout}.json")
+    if not os.path.exists(path):
+        return None, None
+    try:
+        pin = json.load(open(path))
+    except Exception:
+        return None, None
+    prov = {k: pin.get(k) for k in ("kernel", "commit", "date", "source", "correction")}
+    prov["file"] = os.path.relpath(path, ROOT)
+    return pin.get("hbm_bytes_per_launch"), prov
+
+
+def roofline(workload, world, layout, kms, alg_bytes, mbytes, stream):
+    traffic, prov = pmc_pin(workload, world, layout)
+    moved = traffic if traffic else mbytes
+    achieved = moved / (kms * 1e-3) / 1e9
+    return {
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": PEAK_HBM_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / PEAK_HBM_GBS, 4),
+        "traffic": traffic,
+        "achieved_basis": ("PMC bytes moved per launch (pin)" if traffic else
+                           "formulation minimum bytes per launch (no PMC pin: a lower bound of the bytes moved)"),
+        "traffic_provenance": prov,
+        "kernel_ms_avg": round(kms, 5),
+        "algorithmic_bytes_per_launch": alg_bytes,
+        "alg_ratio": round(alg_bytes / (kms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+        "min_bytes_per_launch": mbytes,
+        "stream_copy_gbs": stream,
+        "frac_of_stream": round(achieved / stream, 4) if stream else None,
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2")
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c4")
     ap.add_argument("--c2-n", type=int, default=50,
-                    help="c2: elements per edge of the per-GPU Cartesian block (experiments; configs[1] = 50)")
+                    help="c2: elements per edge of the per-GPU Cartesian block (configs[1] = 50)")
     ap.add_argument("--c3-refine", type=int, default=6,
                     help="c3: uniform refinements of fichera.mesh (6 -> 14.9M DoF, 5 -> 1.88M)")
     ap.add_argument("--kernel", choices=["auto", "tpe", "wpe", "unfused", "line"], default="auto")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--graph", type=int, default=0,
-                    help="1: capture one Mult in a HIP graph and replay it per step (single process)")
     ap.add_argument("--geometry", choices=["compressed", "full"], default="compressed",
                     help="compressed: AFFINE qdata on parallelepiped meshes (default); full: per-point layout")
-    ap.add_argument("--emulate-world", type=int, default=1,
-                    help="measurement aid: run ONE rank (--emulate-rank) of an N-rank partition alone, "
-                         "exchanges replaced by same-size device copies (values not the operator's)")
-    ap.add_argument("--emulate-rank", type=int, default=1)
+    ap.add_argument("--full-layout", type=int, default=1,
+                    help="1 (N = 1): also time the full per-point qdata layout in this run (full_layout sub-object)")
     ap.add_argument("--loopback", type=int, default=1,
                     help="N>1 on one GPU: N subdomains in this process (validation of the partitioned path)")
+    ap.add_argument("--deadline", type=float, default=900.0,
+                    help="seconds after which a rank prints its last stage and exits non-zero (0: none)")
     args = ap.parse_args()
-
-    if args.emulate_world > 1:
-        os.environ["ECM2_EMULATE_EXCHANGE"] = "1"
-    import torch
-    import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dl = Deadline(args.deadline, rank)
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    dl.at("import torch")
+    import torch
+    import torch.distributed as dist
+
     torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank % max(1, torch.cuda.device_count())))
+        dl.at("init_process_group")
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local_rank % max(1, torch.cuda.device_count())))
     E = load_pkg()
     E.load_library()
-    scatter = os.environ.get("ECM2_SCATTER", "partials")  # A/B knob: partials | atomic
+    scatter = os.environ.get("ECM2_SCATTER", "partials")  # A/B: partials | atomic
     kernel = {"auto": E.KERNEL_AUTO, "tpe": E.KERNEL_TPE, "wpe": E.KERNEL_WPE, "unfused": E.KERNEL_UNFUSED,
               "line": E.KERNEL_LINE}[args.kernel]
+    decomp = os.environ.get("ECM2_DECOMP", "overlap")
 
     compress = args.geometry == "compressed"
     order = 4 if args.workload == "c5" else 2
     if args.workload == "c2":
         n = args.c2_n
         nx = ny = n
-        nz_total = n * max(world, args.emulate_world)
+        nz_total = n * world
         scaling = "weak"
-        workload = f"configs[1]: inline-hex refined to Cartesian {n}x{n}x{nz_total} ({n}^3 per GPU), H1 p=2, Mass(rho*c)+Diffusion(gamma*dt*k(T)) PA Mult"
+        workload = (f"configs[1]: inline-hex refined to Cartesian {n}x{n}x{nz_total} ({n}^3 per GPU), H1 p=2, "
+                    "Mass(rho*c)+Diffusion(gamma*dt*k(T)) PA Mult")
     elif args.workload == "c3":
         scaling = "strong"
         workload = (f"configs[2]: fichera.mesh refined {args.c3_refine}x, H1 p=2, nonlinear Pennes k(T) "
@@ -126,11 +243,13 @@ def main():
     elif args.workload == "c4":
         nx = ny = nz_total = 108
         scaling = "strong"
-        workload = "configs[3]: Cartesian 108^3 (10.2M DoF) split over GPUs, H1 p=2, Mass+Diffusion PA Mult"
+        workload = ("configs[3]: Cartesian 108^3 (10.2M DoF) z-slab split over the GPUs, H1 p=2, "
+                    "Mass(rho*c)+Diffusion(gamma*dt*k(T)) PA Mult")
     else:
         nx = ny = nz_total = 68
         scaling = "strong"
-        workload = "configs[4]: Cartesian 68^3 (20.3M DoF) split over GPUs, H1 p=4, Mass+Diffusion PA Mult"
+        workload = "configs[4]: Cartesian 68^3 (20.3M DoF) z-slab split over the GPUs, H1 p=4, Mass+Diffusion PA Mult"
+    dl.at("mesh and space")
     if args.workload == "c3":
         if world > 1 or args.loopback > 1:
             raise SystemExit("c3 is the single-GPU PCG configuration")
@@ -141,30 +260,37 @@ def main():
     else:
         mesh = E.Mesh.MakeCartesian3D(nx, ny, nz_total, 1.0, ny / nx, nz_total / nx)
         fes = E.H1Space(mesh, order, E.NUMBERING_STRUCTURED)
-    nsub = world if world > 1 else max(args.loopback, args.emulate_world)
+    nsub = world if world > 1 else args.loopback
     mass = lambda a: E.MassIntegrator(E.QuadratureCoefficient(a))
     diff = lambda T: E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(T, K_SCALE, K_SLOPE, K_TREF))
+    form = None
+    keep = []
+
+    def serial_form(compress_geometry):
+        a, T = bioheat_coefficients(E, torch, mesh, fes)
+        keep.extend([a, T])
+        f = E.BilinearForm(fes, kernel=kernel, element_order=os.environ.get("ECM2_ELEMENT_ORDER", "auto"),
+                           scatter=scatter, compress_geometry=compress_geometry)
+        f.AddDomainIntegrator(mass(a))
+        f.AddDomainIntegrator(diff(T))
+        f.Assemble()
+        return f
+
+    dl.at("assemble")
     if nsub <= 1:
-        alpha, T = bioheat_coefficients(E, torch, mesh, fes)
-        form = E.BilinearForm(fes, kernel=kernel, element_order=os.environ.get("ECM2_ELEMENT_ORDER", "auto"),
-                              scatter=scatter, compress_geometry=compress)
-        form.AddDomainIntegrator(mass(alpha))
-        form.AddDomainIntegrator(diff(T))
-        form.Assemble()
+        form = serial_form(compress)
+        alpha, T = keep[0], keep[1]
         n_true = fes.ndofs
         apply = form.Mult
         timed_forms = [form]
+        ne_own = fes.ne
     else:
         # z-slab partition (CartesianPartitioning along z, mesh.cpp:8966)
         er = E.partition_slabs_z(mesh, nsub)
-        if world > 1 or args.emulate_world > 1:
-            if args.emulate_world > 1:
-                rid, prank, pworld = [None], args.emulate_rank, args.emulate_world
-            else:
-                rid = [E.rccl_unique_id() if rank == 0 else None]
-                dist.broadcast_object_list(rid, src=0)
-                prank, pworld = rank, world
-            part = E.Partition(fes, er, prank, pworld, decomposition=os.environ.get("ECM2_DECOMP", "overlap"))
+        if world > 1:
+            rid = [E.rccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(rid, src=0)
+            part = E.Partition(fes, er, rank, world, decomposition=decomp)
             pform = E.ParBilinearForm(part, rccl_id=rid[0], kernel=kernel, scatter=scatter,
                                       compress_geometry=compress)
             alpha, T = bioheat_coefficients(E, torch, mesh, fes, part)
@@ -174,14 +300,15 @@ def main():
             n_true = part.n_owned
             apply = pform.Mult
             timed_forms = [pform]
+            ne_own = part.ne_owned
         else:
             # --loopback: all subdomains in this process on one GPU (exchange by device copies)
-            forms, keep = [], []
+            forms = []
             for r in range(nsub):
-                part = E.Partition(fes, er, r, nsub, decomposition=os.environ.get("ECM2_DECOMP", "overlap"))
+                part = E.Partition(fes, er, r, nsub, decomposition=decomp)
                 pf = E.ParBilinearForm(part, kernel=kernel, scatter=scatter, compress_geometry=compress)
                 alpha, T = bioheat_coefficients(E, torch, mesh, fes, part)
-                keep += [alpha, T]
+                keep += [alpha, T, part]
                 pf.AddDomainIntegrator(mass(alpha))
                 pf.AddDomainIntegrator(diff(T))
                 pf.Assemble()
@@ -192,80 +319,65 @@ def main():
             n_true = sum(f.true_size for f in forms)
             apply = lambda _x, _y: group.Mult(xs, ys)
             timed_forms = forms
+            ne_own = fes.ne
 
     x = torch.empty(n_true, dtype=torch.float64, device="cuda")
     x.uniform_(-1.0, 1.0, generator=torch.Generator(device="cuda").manual_seed(1 + rank))
     y = torch.empty_like(x)
     torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
-        apply(x, y)
-    torch.cuda.synchronize()
-    step = lambda: apply(x, y)
-    if args.graph and world == 1:
-        # one Mult (all its launches) as a HIP graph, replayed per step
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            apply(x, y)
-        graph.replay()
-        torch.cuda.synchronize()
-        step = graph.replay
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    # second, instrumented pass: HIP events around the dominant (fused apply) kernel on
-    # the stream it is launched on (kept out of the timed loop above)
-    for f in timed_forms:
-        f.timing(True)
-    for _ in range(args.steps):
-        apply(x, y)
-    torch.cuda.synchronize()
-    kms = sum(f.timing_get()[0] for f in timed_forms)
-    for f in timed_forms:
-        f.timing(False)
+    dl.at("timed Mults")
+    dt = time_mults(apply, x, y, args.steps, args.warmup, world, dist, torch)
+    dl.at("kernel timing")
+    kms = kernel_ms(timed_forms, apply, x, y, args.steps, torch)
     abytes = sum(f.algorithmic_bytes() for f in timed_forms)
+    nd = (order + 1) ** 3
+    mbytes = sum(min_bytes(f, f.part.ne_local if hasattr(f, "part") else fes.ne, nd, f.true_size
+                           if hasattr(f, "true_size") else n_true) for f in timed_forms)
     qbytes = sum(f.qdata_bytes() for f in timed_forms)
+    layout = qdata_layout(E, timed_forms[0])
     pcg = c3_pcg(E, torch, fes, form) if args.workload == "c3" else None
 
-    # aggregate over ranks: total true dofs, max time; kernel ms per Mult (summed over
-    # the apply launches of one Mult: interior + boundary blocks when partitioned)
-    tot = torch.tensor([float(n_true), dt, abytes, kms / args.steps, qbytes],
-                       dtype=torch.float64, device="cuda")
+    # aggregate over ranks: total true dofs, max time; kernel ms per Mult (interior + boundary
+    # launches of one Mult when partitioned); bytes per GPU
+    tot = torch.tensor([float(n_true), dt, abytes, kms, qbytes, mbytes], dtype=torch.float64, device="cuda")
     if world > 1:
+        dl.at("reduce results")
         s = tot.clone()
-        dist.all_reduce(s[0:1], op=dist.ReduceOp.SUM)
-        dist.all_reduce(s[2:3], op=dist.ReduceOp.SUM)
-        dist.all_reduce(s[4:5], op=dist.ReduceOp.SUM)
-        dist.all_reduce(s[1:2], op=dist.ReduceOp.MAX)
-        dist.all_reduce(s[3:4], op=dist.ReduceOp.MAX)
+        for i in (0, 2, 4, 5):
+            dist.all_reduce(s[i:i + 1], op=dist.ReduceOp.SUM)
+        for i in (1, 3):
+            dist.all_reduce(s[i:i + 1], op=dist.ReduceOp.MAX)
         tot = s
-    ndofs_total, tmax, bytes_total, kavg_ms, qbytes_total = [float(v) for v in tot.cpu()]
+    ndofs_total, tmax, bytes_total, kavg_ms, qbytes_total, mbytes_total = [float(v) for v in tot.cpu()]
     value = ndofs_total * args.steps / tmax / 1e6
 
+    full = None
+    if world == 1 and args.loopback <= 1 and args.full_layout and compress and args.workload != "c3":
+        dl.at("full layout")
+        del apply
+        ff = serial_form(False)
+        dtf = time_mults(ff.Mult, x, y, args.steps, args.warmup, 1, dist, torch)
+        kf = kernel_ms([ff], ff.Mult, x, y, args.steps, torch)
+        lay_f = qdata_layout(E, ff)
+        full = {"qdata_layout": lay_f,
+                "value": round(fes.ndofs * args.steps / dtf / 1e6, 2),
+                "ms_per_step": round(dtf / args.steps * 1e3, 5),
+                "roofline": roofline(args.workload, 1, lay_f, kf, ff.algorithmic_bytes(),
+                                     min_bytes(ff, fes.ne, nd, fes.ndofs), None),
+                "note": "same run, same inputs, per-point qdata (56 B per quadrature point: the layout SURVEY "
+                        "§8(d)'s algorithmic bytes describe, so its alg_ratio is a roofline fraction)"}
+        del ff
+
     if rank == 0:
-        achieved = bytes_total / world / (kavg_ms * 1e-3) / 1e9
-        traffic = None
-        # pinned PMC traffic of this workload, kernel family and qdata layout (profiles/pmc_pin.py)
-        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_n{world}_{qdata_layout(E, timed_forms[0])}.json")
-        if os.path.exists(pmc) and args.loopback <= 1 and args.emulate_world <= 1:  # pins are single-form profiles
-            try:
-                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+        dl.at("stream copy peak")
         stream = stream_copy_peak(E, torch)
         cpu = None
-        if not args.no_cpu_baseline and world == 1 and args.loopback <= 1 and args.emulate_world <= 1:
-            cpu = cpu_baseline(fes, mesh, alpha, T, args.cpu_baseline_seconds)
+        if not args.no_cpu_baseline and world == 1 and args.loopback <= 1:
+            dl.at("cpu baseline")
+            cpu = cpu_baseline(fes, mesh, alpha, T, args.cpu_baseline_seconds, args.workload)
         line = {
-            "metric": "MDoF/s on PA diffusion+mass Mult, hex p=2; % HBM roofline at 1/2/4/8 GPUs",
+            "metric": METRIC,
             "value": round(value, 2),
             "unit": "MDoF/s",
             "n_gpus": world,
@@ -282,53 +394,34 @@ def main():
                 "ndofs": int(ndofs_total),
                 "elements": int(fes.ne),
                 "order": order, "q1d": order + 2,
-                "launch": "hip-graph replay per Mult" if (args.graph and world == 1) else "stream launches",
+                "launch": "stream launches" if world == 1 else "hip-graph replay per Mult (RCCL exchange captured)",
                 "kernel": ["auto", "tpe", "wpe", "unfused", "line"][timed_forms[0].info()["kernel"]],
-                "qdata_layout": qdata_layout(E, timed_forms[0]),
+                "qdata_layout": layout,
                 "qdata_bytes_stored": qbytes_total / world,
-                "parallelism": f"domain-decomposition z-slabs x{world}, RCCL shared-DoF exchange" if world > 1
-                else (f"EMULATED rank {args.emulate_rank} of {args.emulate_world} z-slabs alone on one GPU "
-                      "(exchanges = same-size local copies; measurement aid, not a scaling number)"
-                      if args.emulate_world > 1 else
-                      (f"loopback z-slabs x{args.loopback} on one GPU" if args.loopback > 1 else "single GPU")),
+                "parallelism": (f"domain decomposition, z-slabs x{world} ({decomp}), RCCL shared-DoF exchange"
+                                if world > 1 else
+                                (f"loopback z-slabs x{args.loopback} on one GPU" if args.loopback > 1 else "single GPU")),
             },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": PEAK_HBM_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / PEAK_HBM_GBS, 4),
-                "traffic": traffic,
-                "kernel_ms_avg": round(kavg_ms, 5),
-                "stream_copy_gbs": stream,
-                "frac_of_stream": round(achieved / stream, 4) if stream else None,
-                "algorithmic_bytes_per_launch": bytes_total / world,
-                # real HBM rate of the dominant kernel (PMC bytes / its time): with AFFINE qdata
-                # the kernel moves fewer bytes than the SURVEY's fixed formula counts, so
-                # "frac" can exceed 1; this is the bandwidth actually drawn
-                "traffic_gbs": round(traffic / (kavg_ms * 1e-3) / 1e9, 1) if traffic else None,
-                "traffic_frac": round(traffic / (kavg_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4) if traffic else None,
-            },
+            "roofline": roofline(args.workload, world, layout, kavg_ms, bytes_total / world, mbytes_total / world,
+                                 stream),
             "cpu_baseline": cpu,
         }
+        if full is not None:
+            line["full_layout"] = full
         if pcg is not None:
             line["pcg"] = pcg
         print(json.dumps(line), flush=True)
+    dl.at("teardown")
     if world > 1:
         # release the forms (ncclCommDestroy of the operator's communicator) on every rank
         # while all ranks are alive, then tear down torch's process group
-        del step, apply, timed_forms, pform
+        del apply, timed_forms, pform
         import gc
         gc.collect()
         torch.cuda.synchronize()
         dist.barrier()
         dist.destroy_process_group()
-
-
-def qdata_layout(E, form):
-    """Quadrature-data layout of a (local) form: affine | blocked | native."""
-    return {E.QLAYOUT_NATIVE: "native", E.QLAYOUT_BLOCKED: "blocked",
-            E.QLAYOUT_AFFINE: "affine", E.QLAYOUT_AFFINE_E: "affine_e"}[form.info()["layout"]]
+    dl.done()
 
 
 def c3_pcg(E, torch, fes, form, max_iter=200):
@@ -378,7 +471,24 @@ def stream_copy_peak(E, torch, nbytes=1 << 30, reps=20):
     return round(rate, 1)
 
 
-def cpu_baseline(fes, mesh, alpha, T, seconds):
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    try:
+        return subprocess.check_output(["uname", "-m"], text=True).strip()
+    except Exception:
+        return "unknown"
+
+
+# the reference's own CPU PA Mult, 8 OpenMP threads, survey container
+REFERENCE_OMP8 = {"c2": 28.4, "c3": 23.3, "c4": 27.5, "c5": 45.8}
+
+
+def cpu_baseline(fes, mesh, alpha, T, seconds, workload):
     """The oracle (CPU restatement of the reference PA path, 'port') on the same workload,
     timed on this host's cores for a bounded number of Mults (~`seconds` of CPU work)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -404,8 +514,12 @@ def cpu_baseline(fes, mesh, alpha, T, seconds):
         "unit": "MDoF/s",
         "cores": O.num_threads(),
         "kind": "port",
+        "cpu_model": cpu_model(),
         "sample": f"{n} oracle PA Mults (gather, mass, diffusion, CSR scatter; OpenMP) on the same "
                   f"{fes.ndofs}-DoF mesh, {dt:.1f} s",
+        "reference_cpu_omp8": {"value": REFERENCE_OMP8.get(workload), "unit": "MDoF/s",
+                               "note": "the reference's own PA Mult, Device('omp'), 8 threads of the survey "
+                                       "container's Intel Xeon (BASELINE.md); not run on this host"},
     }
 
 

@@ -31,7 +31,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libecm2pa.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ecm2_pa.h")
 
 MASS, DIFFUSION = 0, 1
-COEFF_CONSTANT, COEFF_QUAD, COEFF_GRIDFUNC_AFFINE = 0, 1, 2
+COEFF_CONSTANT, COEFF_QUAD, COEFF_GRIDFUNC_AFFINE, COEFF_GRIDFUNC_PERFUSION = 0, 1, 2, 3
 KERNEL_AUTO, KERNEL_TPE, KERNEL_WPE, KERNEL_UNFUSED, KERNEL_LINE = 0, 1, 2, 3, 4
 NUMBERING_ENTITY, NUMBERING_STRUCTURED = 0, 1
 ORDER_NATIVE, ORDER_BRICK, ORDER_MORTON = 0, 1, 2
@@ -99,6 +99,8 @@ def load_library(path: str = LIB_PATH):
         "ecm2_mesh_element_order": (i32, [vp, i32, vp]),
         "ecm2_pa_form_assemble": (i32, [vp, vp]),
         "ecm2_pa_form_mult": (i32, [vp, vp, vp, vp]),
+        "ecm2_pa_form_mult_transpose": (i32, [vp, vp, vp, vp]),
+        "ecm2_pa_form_add_mult": (i32, [vp, vp, vp, f64, vp]),
         "ecm2_pa_form_assemble_diagonal": (i32, [vp, vp, vp]),
         "ecm2_pa_form_restriction_mult": (i32, [vp, vp, vp, vp]),
         "ecm2_pa_form_restriction_mult_transpose": (i32, [vp, vp, vp, vp]),
@@ -307,6 +309,39 @@ class AffineGridFunctionCoefficient:
         self.T, self.scale, self.slope, self.t_ref = T, float(scale), float(slope), float(t_ref)
 
 
+class PerfusionCoefficient:
+    """Pennes heat capacity + perfusion of an implicit stage's mass coefficient, from an H1
+    temperature grid function T (CUDA L-vector):
+        alpha(T) = rho_c + gdt_cb * w_b(T),   w_b(T) = w0 * max(0, 1 + a (T - t0)) for T < t_stop,
+    0 at or above t_stop (perfusion shut-down in coagulated tissue)."""
+
+    def __init__(self, T, rho_c, gdt_cb, w0, a=0.0, t0=37.0, t_stop=1e300):
+        self.T = T
+        self.params = tuple(float(v) for v in (rho_c, gdt_cb, w0, a, t0, t_stop))
+
+
+def _integrator_args(c, keep):
+    """(coefficient kind, data pointer, params pointer) of a coefficient for the C ABI."""
+    if isinstance(c, ConstantCoefficient):
+        arr = (ctypes.c_double * 1)(c.value)
+        keep.append(arr)
+        return COEFF_CONSTANT, ctypes.cast(arr, ctypes.c_void_p), None
+    if isinstance(c, QuadratureCoefficient):
+        keep.append(c.values)
+        return COEFF_QUAD, _dev_ptr(c.values), None
+    if isinstance(c, AffineGridFunctionCoefficient):
+        keep.append(c.T)
+        params = (ctypes.c_double * 3)(c.scale, c.slope, c.t_ref)
+        keep.append(params)
+        return COEFF_GRIDFUNC_AFFINE, _dev_ptr(c.T), ctypes.cast(params, ctypes.c_void_p)
+    if isinstance(c, PerfusionCoefficient):
+        keep.append(c.T)
+        params = (ctypes.c_double * 6)(*c.params)
+        keep.append(params)
+        return COEFF_GRIDFUNC_PERFUSION, _dev_ptr(c.T), ctypes.cast(params, ctypes.c_void_p)
+    raise ECM2Error(f"unsupported coefficient {type(c).__name__}")
+
+
 class MassIntegrator:
     kind = MASS
 
@@ -381,19 +416,8 @@ class BilinearForm:
         _check(_lib.ecm2_pa_form_set_jacobians(self._h, _dev_ptr(J)))
 
     def AddDomainIntegrator(self, integ):
-        c = integ.coeff
-        if isinstance(c, ConstantCoefficient):
-            arr = (ctypes.c_double * 1)(c.value)
-            _check(_lib.ecm2_pa_form_add_integrator(self._h, integ.kind, COEFF_CONSTANT, ctypes.cast(arr, ctypes.c_void_p), None))
-        elif isinstance(c, QuadratureCoefficient):
-            self._keep.append(c.values)
-            _check(_lib.ecm2_pa_form_add_integrator(self._h, integ.kind, COEFF_QUAD, _dev_ptr(c.values), None))
-        elif isinstance(c, AffineGridFunctionCoefficient):
-            self._keep.append(c.T)
-            params = (ctypes.c_double * 3)(c.scale, c.slope, c.t_ref)
-            _check(_lib.ecm2_pa_form_add_integrator(self._h, integ.kind, COEFF_GRIDFUNC_AFFINE, _dev_ptr(c.T), ctypes.cast(params, ctypes.c_void_p)))
-        else:
-            raise ECM2Error(f"unsupported coefficient {type(c).__name__}")
+        kind, data, params = _integrator_args(integ.coeff, self._keep)
+        _check(_lib.ecm2_pa_form_add_integrator(self._h, integ.kind, kind, data, params))
         self._integs.append(integ)
 
     def Assemble(self, stream=None):
@@ -413,6 +437,19 @@ class BilinearForm:
 
     def Mult(self, x, y, stream=None):
         _check(_lib.ecm2_pa_form_mult(self._h, _dev_ptr(x), _dev_ptr(y), _stream(stream)))
+
+    def MultTranspose(self, x, y, stream=None):
+        _check(_lib.ecm2_pa_form_mult_transpose(self._h, _dev_ptr(x), _dev_ptr(y), _stream(stream)))
+
+    def AddMult(self, x, y, a=1.0, stream=None):
+        """y += a A x (Operator::AddMult)."""
+        _check(_lib.ecm2_pa_form_add_mult(self._h, _dev_ptr(x), _dev_ptr(y), float(a), _stream(stream)))
+
+    def SetKernel(self, kernel: int):
+        _check(_lib.ecm2_pa_form_set_kernel(self._h, kernel))
+
+    def SetGeometryCompression(self, on: bool):
+        _check(_lib.ecm2_pa_form_set_geometry_compression(self._h, 1 if on else 0))
 
     def AssembleDiagonal(self, diag, stream=None):
         _check(_lib.ecm2_pa_form_assemble_diagonal(self._h, _dev_ptr(diag), _stream(stream)))
@@ -496,6 +533,9 @@ _PAR_SIGS = {
                                                     ctypes.POINTER(ctypes.c_int)]),
     "ecm2_par_form_assemble": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "ecm2_par_form_mult": (ctypes.c_int, [ctypes.c_void_p] * 4),
+    "ecm2_par_form_mult_transpose": (ctypes.c_int, [ctypes.c_void_p] * 4),
+    "ecm2_partition_exchange_schedule": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                                        ctypes.POINTER(ctypes.c_int)]),
     "ecm2_par_group_mult": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_void_p]),
     "ecm2_par_form_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
@@ -592,6 +632,19 @@ class Partition:
     def owned_global(self):
         return self.local_to_global[: self.n_owned]
 
+    XBUF_X_TRUE, XBUF_SENDBUF, XBUF_XGHOST, XBUF_YGHOST, XBUF_RECVBUF = 0, 1, 2, 3, 4
+
+    def exchange_schedule(self, transpose: bool) -> np.ndarray:
+        """The transfers of P (False) or P^T (True) both transports issue: rows (peer, send,
+        buffer, offset, count) -- ecm2_partition_exchange_schedule."""
+        lib = _par_lib()
+        n = ctypes.c_int(0)
+        _check(lib.ecm2_partition_exchange_schedule(self._h, 1 if transpose else 0, None, ctypes.byref(n)))
+        out = np.empty((n.value, 5), np.int32)
+        if n.value:
+            _check(lib.ecm2_partition_exchange_schedule(self._h, 1 if transpose else 0, _np_ptr(out), ctypes.byref(n)))
+        return out
+
 
 def rccl_p2p_selftest(graph: bool, n: int = 4096) -> float:
     """Max error of a one-rank RCCL self send/recv, direct or graph-captured."""
@@ -637,29 +690,23 @@ class ParBilinearForm:
             self._h = None
 
     def AddDomainIntegrator(self, integ):
-        c = integ.coeff
-        lib = _par_lib()
-        if isinstance(c, ConstantCoefficient):
-            arr = (ctypes.c_double * 1)(c.value)
-            self._keep.append(arr)
-            _check(lib.ecm2_par_form_add_integrator(self._h, integ.kind, COEFF_CONSTANT, ctypes.cast(arr, ctypes.c_void_p), None))
-        elif isinstance(c, QuadratureCoefficient):
-            self._keep.append(c.values)
-            _check(lib.ecm2_par_form_add_integrator(self._h, integ.kind, COEFF_QUAD, _dev_ptr(c.values), None))
-        elif isinstance(c, AffineGridFunctionCoefficient):
-            self._keep.append(c.T)
-            params = (ctypes.c_double * 3)(c.scale, c.slope, c.t_ref)
-            self._keep.append(params)
-            _check(lib.ecm2_par_form_add_integrator(self._h, integ.kind, COEFF_GRIDFUNC_AFFINE, _dev_ptr(c.T),
-                                                    ctypes.cast(params, ctypes.c_void_p)))
-        else:
-            raise ECM2Error(f"unsupported coefficient {type(c).__name__}")
+        kind, data, params = _integrator_args(integ.coeff, self._keep)
+        _check(_par_lib().ecm2_par_form_add_integrator(self._h, integ.kind, kind, data, params))
 
     def Assemble(self, stream=None):
         _check(_par_lib().ecm2_par_form_assemble(self._h, _stream(stream)))
 
     def Mult(self, x, y, stream=None):
         _check(_par_lib().ecm2_par_form_mult(self._h, _dev_ptr(x), _dev_ptr(y), _stream(stream)))
+
+    def MultTranspose(self, x, y, stream=None):
+        _check(_par_lib().ecm2_par_form_mult_transpose(self._h, _dev_ptr(x), _dev_ptr(y), _stream(stream)))
+
+    def SetKernel(self, kernel: int):
+        _check(_par_lib().ecm2_par_form_set_kernel(self._h, kernel))
+
+    def SetGeometryCompression(self, on: bool):
+        _check(_par_lib().ecm2_par_form_set_geometry_compression(self._h, 1 if on else 0))
 
     def AssembleDiagonal(self, d, stream=None):
         """Diagonal of P^T A P on this rank's true dofs (collective over the RCCL ranks)."""

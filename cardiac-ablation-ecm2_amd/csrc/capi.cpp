@@ -71,6 +71,30 @@ int guard(F &&fn)
 #define NEED(p) ECM2_VERIFY((p) != nullptr, ecm2::ERR_ARG, "null argument: " #p)
 
 inline hipStream_t S(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ecm2_pa_form_add_integrator's (kind, data, params) -> the library's coefficient descriptor
+ecm2::CoeffDesc make_coeff(int coeff_kind, const double *data, const double *params)
+{
+   ecm2::CoeffDesc c;
+   c.kind = coeff_kind;
+   if (coeff_kind == ECM2_COEFF_CONSTANT) { c.value = data ? data[0] : 1.0; }
+   else if (coeff_kind == ECM2_COEFF_QUAD) { c.quad = data; }
+   else if (coeff_kind == ECM2_COEFF_GRIDFUNC_AFFINE)
+   {
+      NEED(params);
+      c.lvec = data;
+      c.scale = params[0];
+      c.slope = params[1];
+      c.t_ref = params[2];
+   }
+   else if (coeff_kind == ECM2_COEFF_GRIDFUNC_PERFUSION)
+   {
+      NEED(params);
+      c.lvec = data;
+      for (int i = 0; i < 6; i++) { c.p[i] = params[i]; }
+   }
+   return c;
+}
 } // namespace
 
 extern "C" {
@@ -296,25 +320,7 @@ int ecm2_pa_form_add_integrator(ecm2_pa_form *f, int integrator, int coeff_kind,
 {
    return guard([&] {
       NEED(f);
-      ecm2::CoeffDesc c;
-      c.kind = coeff_kind;
-      if (coeff_kind == ECM2_COEFF_CONSTANT)
-      {
-         c.value = data ? data[0] : 1.0;
-      }
-      else if (coeff_kind == ECM2_COEFF_QUAD)
-      {
-         c.quad = data;
-      }
-      else if (coeff_kind == ECM2_COEFF_GRIDFUNC_AFFINE)
-      {
-         NEED(params);
-         c.lvec = data;
-         c.scale = params[0];
-         c.slope = params[1];
-         c.t_ref = params[2];
-      }
-      f->f->add_integrator(integrator, c);
+      f->f->add_integrator(integrator, make_coeff(coeff_kind, data, params));
    });
 }
 
@@ -369,6 +375,17 @@ int ecm2_pa_form_assemble(ecm2_pa_form *f, void *stream)
 int ecm2_pa_form_mult(ecm2_pa_form *f, const double *x, double *y, void *stream)
 {
    return guard([&] { NEED(f); f->f->mult(x, y, S(stream)); });
+}
+
+int ecm2_pa_form_mult_transpose(ecm2_pa_form *f, const double *x, double *y, void *stream)
+{
+   // Mass + Diffusion with scalar coefficients is symmetric: A^T x = A x
+   return guard([&] { NEED(f); f->f->mult(x, y, S(stream)); });
+}
+
+int ecm2_pa_form_add_mult(ecm2_pa_form *f, const double *x, double *y, double a, void *stream)
+{
+   return guard([&] { NEED(f); f->f->add_mult(x, y, a, S(stream)); });
 }
 
 int ecm2_pa_form_assemble_diagonal(ecm2_pa_form *f, double *diag, void *stream)
@@ -555,16 +572,7 @@ int ecm2_par_form_add_integrator(ecm2_par_form *f, int integrator, int coeff_kin
 {
    return guard([&] {
       NEED(f);
-      ecm2::CoeffDesc c;
-      c.kind = coeff_kind;
-      if (coeff_kind == ECM2_COEFF_CONSTANT) { c.value = data ? data[0] : 1.0; }
-      else if (coeff_kind == ECM2_COEFF_QUAD) { c.quad = data; }
-      else if (coeff_kind == ECM2_COEFF_GRIDFUNC_AFFINE)
-      {
-         NEED(params);
-         c.lvec = data; c.scale = params[0]; c.slope = params[1]; c.t_ref = params[2];
-      }
-      f->f->local().add_integrator(integrator, c);
+      f->f->local().add_integrator(integrator, make_coeff(coeff_kind, data, params));
    });
 }
 
@@ -612,6 +620,32 @@ int ecm2_par_form_mult(ecm2_par_form *f, const double *x_true, double *y_true, v
       NEED(f);
       ECM2_VERIFY(f->f->true_size() == 0 || (x_true && y_true), ecm2::ERR_ARG, "null vector");
       f->f->mult(x_true, y_true, S(stream));
+   });
+}
+
+int ecm2_par_form_mult_transpose(ecm2_par_form *f, const double *x_true, double *y_true, void *stream)
+{
+   // P^T A^T P = P^T A P (A symmetric)
+   return ecm2_par_form_mult(f, x_true, y_true, stream);
+}
+
+int ecm2_partition_exchange_schedule(const ecm2_partition *p, int transpose, int *out, int *count)
+{
+   return guard([&] {
+      NEED(p); NEED(count);
+      const std::vector<ecm2::Xfer> sch = ecm2::exchange_schedule(p->p, transpose != 0);
+      const int n = (int)sch.size();
+      if (out)
+      {
+         ECM2_VERIFY(*count >= n, ecm2::ERR_ARG, "schedule buffer too small");
+         for (int i = 0; i < n; i++)
+         {
+            const ecm2::Xfer &t = sch[i];
+            const int row[5] = {t.peer, t.send, t.buf, t.off, t.count};
+            std::memcpy(out + 5 * i, row, sizeof(row));
+         }
+      }
+      *count = n;
    });
 }
 

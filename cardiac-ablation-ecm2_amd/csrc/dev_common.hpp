@@ -1,0 +1,95 @@
+// dev_common.hpp -- device-side helpers shared by the gfx950 kernel translation units
+// (k_setup.hip, k_tpe.hip, k_line.hip, k_misc.hip).  Included by .hip files only.
+#pragma once
+
+#include "kernels.hpp"
+
+#include <hip/hip_runtime.h>
+
+namespace ecm2
+{
+namespace dev
+{
+
+constexpr int MQ = MAX_Q1D;
+typedef double v2d __attribute__((ext_vector_type(2)));
+
+inline unsigned grid_for(long n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+// pos: caller element -> internal position (element permutation of the blocked layout)
+__device__ __forceinline__ size_t qidx_diff(const int *pos, int kind, int nq, int e, int c, int q)
+{
+   if (kind == QLAYOUT_NATIVE) { return ((size_t)e * 6 + c) * nq + q; }
+   if (pos) { e = pos[e]; }
+   const int blk = e >> 6, lane = e & 63;
+   return (((size_t)blk * nq + q) * 3 + (c >> 1)) * 128 + lane * 2 + (c & 1);
+}
+
+__device__ __forceinline__ size_t qidx_mass(const int *pos, int kind, int nq, int e, int q)
+{
+   if (kind == QLAYOUT_NATIVE) { return (size_t)e * nq + q; }
+   if (pos) { e = pos[e]; }
+   const int blk = e >> 6, lane = e & 63;
+   const int nqh = (nq + 1) >> 1;
+   return ((size_t)blk * nqh + (q >> 1)) * 128 + lane * 2 + (q & 1);
+}
+
+// Value of diffusion entry c / mass at (e, q) in any layout; AFFINE recombines the
+// per-point scalar W beta (qdm pair .x) with the element matrix C (qdd), and stores the mass
+// value as the pair's .y.
+__device__ __forceinline__ size_t affine_pair(const int *pos, int nq, int e, int q)
+{
+   if (pos) { e = pos[e]; }
+   return (((size_t)(e >> 6) * nq + q) * 64 + (e & 63)) * 2;
+}
+__device__ __forceinline__ double qd_diff_at(const double *qdd, const double *qdm, const int *pos, int kind,
+                                             int nq, int e, int c, int q)
+{
+   if (kind == QLAYOUT_AFFINE_E) { return qdm[((size_t)e * nq + q) * 2] * qdd[(size_t)e * 6 + c]; }
+   if (kind == QLAYOUT_AFFINE)
+   {
+      const int ie = pos ? pos[e] : e;
+      return qdm[affine_pair(nullptr, nq, ie, q)] * qdd[(((size_t)(ie >> 6) * 3 + (c >> 1)) * 64 + (ie & 63)) * 2 + (c & 1)];
+   }
+   return qdd[qidx_diff(pos, kind, nq, e, c, q)];
+}
+__device__ __forceinline__ double qd_mass_at(const double *qdm, const int *pos, int kind, int nq, int e, int q)
+{
+   if (kind == QLAYOUT_AFFINE_E) { return qdm[((size_t)e * nq + q) * 2 + 1]; }
+   if (kind == QLAYOUT_AFFINE) { return qdm[affine_pair(pos, nq, e, q) + 1]; }
+   return qdm[qidx_mass(pos, kind, nq, e, q)];
+}
+
+__device__ __forceinline__ int dof_of(int g) { return g >= 0 ? g : -1 - g; }
+
+// Encoded (fused-kernel) map entries: bits 0-29 dof, bit 30 "shared" (the dof is held by
+// more than one entry of the whole mesh after the kernel's own face assembly -> partial slot
+// or atomic add), bit 31 orientation sign.
+__device__ __forceinline__ int bdof(int g) { return g & 0x3fffffff; }
+__device__ __forceinline__ bool bneg(int g) { return g < 0; }
+__device__ __forceinline__ bool bshared(int g) { return (g >> 30) & 1; }
+
+// XCD-aware workgroup order: the hardware deals workgroup i to XCD i % 8 (MI355X_MICROARCH.md,
+// "Workgroup dispatch"); remapping i to a contiguous range per XCD keeps neighbouring work items
+// (which share x values and partial-slot lines) in one XCD's L2.  A bijection on [0, G) for any G.
+__device__ __forceinline__ int xcd_contiguous(int i, int G)
+{
+   const int q = G >> 3, r = G & 7, x = i & 7, j = i >> 3;
+   return x * q + (x < r ? x : r) + j;
+}
+
+// Basis tables for the line / brick / diagonal / coefficient kernels: a device copy of the
+// (D1D, Q1D) Basis1D read through the constant address space, with the pointer laundered per
+// stage (asm barrier) so the compiler issues scalar loads where the entries are used instead
+// of hoisting 2 D Q doubles out of the element loop (which exceeds the SGPR file).
+typedef const __attribute__((address_space(4))) Basis1D CBasis;
+
+__device__ __forceinline__ CBasis *stage_basis(const Basis1D *tab)
+{
+   CBasis *p = (CBasis *)tab;
+   asm volatile("" : "+s"(p));
+   return p;
+}
+
+} // namespace dev
+} // namespace ecm2

@@ -1,0 +1,1158 @@
+// k_line.hip -- fused apply for p >= 3 (line and brick kernels) and the sum-factorised
+// diagonal (gfx950).
+//
+// Both apply kernels restate, per element, the reference's smem mass and diffusion kernels
+// (bilininteg_mass_kernels.hpp:809-1033, bilininteg_diffusion_kernels.hpp:989-1214) as five
+// 1D stages through LDS in which every active lane owns one 1D line of the current
+// contraction direction in registers (a lane reads D or Q values from LDS once per Q or D
+// multiply-adds; the reference reads two LDS operands per multiply-add), with the gather
+// (ElementRestriction::Mult, restriction.cpp:109-129) and the scatter (MultTranspose,
+// restriction.cpp:152-186) fused in.
+#include "dev_common.hpp"
+
+#include <algorithm>
+#include <cstdlib>
+
+namespace ecm2
+{
+namespace
+{
+using namespace dev;
+
+template <int D, int Q, bool MASS, bool DIFF, bool AFF>
+__device__ __forceinline__ void line_load_qdata(double (&qv)[7][Q], int e, int t,
+                                                const double *__restrict__ qdd,
+                                                const double *__restrict__ qdm)
+{
+   constexpr int NQ = Q * Q * Q, QQ = Q * Q;
+   if (AFF && t < QQ)
+   {
+      // AFFINE_E: D_c = (W beta)(q) C_c, mass = (W alpha det J)(q); 16-byte pair per point
+      double c[6];
+#pragma unroll
+      for (int k = 0; k < 6; k++) { c[k] = qdd[(size_t)e * 6 + k]; }
+#pragma unroll
+      for (int qz = 0; qz < Q; qz++)
+      {
+         const v2d p = reinterpret_cast<const v2d *>(qdm)[(size_t)e * NQ + qz * QQ + t];
+#pragma unroll
+         for (int k = 0; k < 6; k++) { qv[k][qz] = p.x * c[k]; }
+         qv[6][qz] = p.y;
+      }
+      return;
+   }
+   if (t < QQ)
+   {
+#pragma unroll
+      for (int qz = 0; qz < Q; qz++)
+      {
+         if (DIFF)
+         {
+#pragma unroll
+            for (int c = 0; c < 6; c++) { qv[c][qz] = qdd[((size_t)e * 6 + c) * NQ + qz * QQ + t]; }
+         }
+         if (MASS) { qv[6][qz] = qdm[(size_t)e * NQ + qz * QQ + t]; }
+      }
+   }
+}
+
+// --------------------------------------------------------------------------
+// Line kernel: one wave per element (the elements outside bricks), any (D, Q) with
+// Q*Q <= 64 (p = 1..6), L-vectors in and out.  The z contraction, the quadrature-point
+// weighting and the transposed z contraction are fused in registers on (qx, qy) lanes:
+//   lanes (dy,dz): gather x-line, x-contract          -> s1 [2][dz][dy][qx]
+//   lanes (qx,dz): y-contract                           -> s2 [3][dz][qy][qx]
+//   lanes (qx,qy): z-contract, weight, z-transpose      -> s3 [3][dz][qy][qx]
+//   lanes (qx,dz): y-transpose                          -> s4 [2][dz][dy][qx]
+//   lanes (dy,dz): x-transpose, scatter
+// The element's qdata is loaded at the top (in flight during the gather and the x / y
+// stages).  gmap: [e][ND] encoded dof | shared << 30 | sign << 31; a shared dof goes to its
+// partial slot part[e][a] (or, without partials, an atomic add); n_owned: dofs >= n_owned
+// live in the ghost vectors xg / yg (distributed form; n_owned = ndofs otherwise).
+// --------------------------------------------------------------------------
+template <int D, int Q, bool MASS, bool DIFF, bool AFF>
+__global__ void __launch_bounds__(64)
+k_apply_line(int c_begin, int c_end, const int *__restrict__ lelem, int n_owned, const int *__restrict__ gmap,
+             const double *__restrict__ qdd, const double *__restrict__ qdm,
+             const double *__restrict__ x, const double *__restrict__ xg,
+             double *__restrict__ y, double *__restrict__ yg, const Basis1D *__restrict__ btab,
+             double *__restrict__ part)
+{
+   constexpr int ND = D * D * D, DD = D * D, QQ = Q * Q, DQ = D * Q;
+   constexpr int SA = (2 * DD * Q > 3 * D * QQ) ? 2 * DD * Q : 3 * D * QQ;
+   constexpr int SB = SA;
+   static_assert(QQ <= 64, "line kernel needs Q1D <= 8");
+   __shared__ double bufA[SA];  // s1, then s3
+   __shared__ double bufB[SB];  // s2, then s4
+   const int c = c_begin + (int)blockIdx.x;
+   if (c >= c_end) { return; }  // whole wave
+   const int t = threadIdx.x;
+   const int e = lelem[c];
+
+   double qv[7][Q];
+   line_load_qdata<D, Q, MASS, DIFF, AFF>(qv, e, t, qdd, qdm);
+   // ---- lanes (dy, dz): gather the x-line, contract in x
+   int gl[D];
+   if (t < DD)
+   {
+      CBasis *bp = stage_basis(btab);
+      const int *mp = gmap + (size_t)e * ND + t * D;
+      double xl[D];
+#pragma unroll
+      for (int dx = 0; dx < D; dx++)
+      {
+         const int g = mp[dx];
+         gl[dx] = g;
+         const int d = bdof(g);
+         const double v = d < n_owned ? x[d] : xg[d - n_owned];
+         xl[dx] = bneg(g) ? -v : v;
+      }
+#pragma unroll
+      for (int qx = 0; qx < Q; qx++)
+      {
+         double u = 0.0, v = 0.0;
+#pragma unroll
+         for (int dx = 0; dx < D; dx++)
+         {
+            u += bp->B[qx + MQ * dx] * xl[dx];
+            v += bp->G[qx + MQ * dx] * xl[dx];
+         }
+         bufA[t * Q + qx] = u;            // B_x   [dz][dy][qx]
+         bufA[DD * Q + t * Q + qx] = v;   // G_x
+      }
+   }
+   __syncthreads();
+   // ---- lanes (qx, dz): contract in y
+   if (t < DQ)
+   {
+      CBasis *bp = stage_basis(btab);
+      const int qx = t % Q, dz = t / Q;
+      double la[D], lb[D];
+#pragma unroll
+      for (int dy = 0; dy < D; dy++)
+      {
+         la[dy] = bufA[(dz * D + dy) * Q + qx];
+         lb[dy] = bufA[DD * Q + (dz * D + dy) * Q + qx];
+      }
+#pragma unroll
+      for (int qy = 0; qy < Q; qy++)
+      {
+         double gb = 0.0, bg = 0.0, bb = 0.0;
+#pragma unroll
+         for (int dy = 0; dy < D; dy++)
+         {
+            const double by = bp->B[qy + MQ * dy], gy = bp->G[qy + MQ * dy];
+            gb += by * lb[dy];  // G_x B_y
+            bg += gy * la[dy];  // B_x G_y
+            bb += by * la[dy];  // B_x B_y
+         }
+         const int o = (dz * Q + qy) * Q + qx;
+         bufB[o] = gb;
+         bufB[D * QQ + o] = bg;
+         bufB[2 * D * QQ + o] = bb;
+      }
+   }
+   __syncthreads();
+   // ---- lanes (qx, qy): contract in z, weight at the quadrature points, transpose in z
+   if (t < QQ)
+   {
+      CBasis *bp = stage_basis(btab);
+      double l0[D], l1[D], l2[D];
+#pragma unroll
+      for (int dz = 0; dz < D; dz++)
+      {
+         l0[dz] = bufB[dz * QQ + t];
+         l1[dz] = bufB[D * QQ + dz * QQ + t];
+         l2[dz] = bufB[2 * D * QQ + dz * QQ + t];
+      }
+      double A1[D], A2[D], A3[D];
+#pragma unroll
+      for (int dz = 0; dz < D; dz++) { A1[dz] = 0.0; A2[dz] = 0.0; A3[dz] = 0.0; }
+#pragma unroll
+      for (int qz = 0; qz < Q; qz++)
+      {
+         double gx = 0.0, gy = 0.0, gz = 0.0, u = 0.0;
+#pragma unroll
+         for (int dz = 0; dz < D; dz++)
+         {
+            const double bz = bp->B[qz + MQ * dz], gzz = bp->G[qz + MQ * dz];
+            if (DIFF)
+            {
+               gx += bz * l0[dz];
+               gy += bz * l1[dz];
+               gz += gzz * l2[dz];
+            }
+            if (MASS) { u += bz * l2[dz]; }
+         }
+         double fx = 0.0, fy = 0.0, fz = 0.0, m = 0.0;
+         if (DIFF)
+         {
+            fx = qv[0][qz] * gx + qv[1][qz] * gy + qv[2][qz] * gz;
+            fy = qv[1][qz] * gx + qv[3][qz] * gy + qv[4][qz] * gz;
+            fz = qv[2][qz] * gx + qv[4][qz] * gy + qv[5][qz] * gz;
+         }
+         if (MASS) { m = qv[6][qz] * u; }
+#pragma unroll
+         for (int dz = 0; dz < D; dz++)
+         {
+            const double bz = bp->B[qz + MQ * dz], gzz = bp->G[qz + MQ * dz];
+            if (DIFF)
+            {
+               A1[dz] += bz * fx;               // -> G_x B_y
+               A2[dz] += bz * fy;               // -> B_x G_y
+               A3[dz] += gzz * fz;              // -> B_x B_y
+            }
+            if (MASS) { A3[dz] += bz * m; }    // -> B_x B_y
+         }
+      }
+#pragma unroll
+      for (int dz = 0; dz < D; dz++)
+      {
+         bufA[dz * QQ + t] = A1[dz];
+         bufA[D * QQ + dz * QQ + t] = A2[dz];
+         bufA[2 * D * QQ + dz * QQ + t] = A3[dz];
+      }
+   }
+   __syncthreads();
+   // ---- lanes (qx, dz): transpose in y
+   if (t < DQ)
+   {
+      CBasis *bp = stage_basis(btab);
+      const int qx = t % Q, dz = t / Q;
+      double l0[Q], l1[Q], l2[Q];
+#pragma unroll
+      for (int qy = 0; qy < Q; qy++)
+      {
+         const int o = (dz * Q + qy) * Q + qx;
+         l0[qy] = bufA[o];
+         l1[qy] = bufA[D * QQ + o];
+         l2[qy] = bufA[2 * D * QQ + o];
+      }
+#pragma unroll
+      for (int dy = 0; dy < D; dy++)
+      {
+         double c1 = 0.0, c2 = 0.0;
+#pragma unroll
+         for (int qy = 0; qy < Q; qy++)
+         {
+            const double by = bp->B[qy + MQ * dy], gy = bp->G[qy + MQ * dy];
+            c1 += by * l0[qy];                 // -> G_x
+            c2 += gy * l1[qy] + by * l2[qy];   // -> B_x
+         }
+         bufB[(dz * D + dy) * Q + qx] = c1;
+         bufB[DD * Q + (dz * D + dy) * Q + qx] = c2;
+      }
+   }
+   __syncthreads();
+   // ---- lanes (dy, dz): transpose in x, scatter
+   if (t < DD)
+   {
+      CBasis *bp = stage_basis(btab);
+      double l0[Q], l1[Q];
+#pragma unroll
+      for (int qx = 0; qx < Q; qx++)
+      {
+         l0[qx] = bufB[t * Q + qx];
+         l1[qx] = bufB[DD * Q + t * Q + qx];
+      }
+#pragma unroll
+      for (int dx = 0; dx < D; dx++)
+      {
+         double v = 0.0;
+#pragma unroll
+         for (int qx = 0; qx < Q; qx++) { v += bp->G[qx + MQ * dx] * l0[qx] + bp->B[qx + MQ * dx] * l1[qx]; }
+         const int g = gl[dx];
+         if (bneg(g)) { v = -v; }
+         const int d = bdof(g);
+         double *dst = d < n_owned ? y + d : yg + (d - n_owned);
+         if (!bshared(g)) { *dst = v; }
+         else if (part) { part[(size_t)e * ND + t * D + dx] = v; }
+         else { unsafeAtomicAdd(dst, v); }
+      }
+   }
+}
+
+// --------------------------------------------------------------------------
+// Brick kernel (p >= 3, both integrators): one workgroup per brick of 2 x 2 x BZ elements
+// whose internal faces coincide (found by dof equality at setup, pa_form.cpp).  The five 1D
+// stages of the line kernel run for all elements of the brick at once, lane = (element,
+// line), so the 25 / 30 / 36-line stages of a p = 4 element fill 4-5 waves instead of
+// leaving half of one wave idle.  The elements' outputs are then summed on the brick lattice
+// ((2(D-1)+1)^2 (BZ(D-1)+1) points) in LDS in a fixed order, so the shared faces inside a
+// brick never reach HBM: a lattice point held by this brick alone is plain-stored, one on
+// the brick surface that other holders share goes to its partial slot
+// part[brick][surface index] (face-grouped, brick_surface_index) for k_sum_partials
+// (deterministic, no atomics).  Workgroups take bricks in XCD-contiguous order.
+// AFF: AFFINE_E qdata (per-element C + one (W beta, W alpha det J) pair per point).
+// --------------------------------------------------------------------------
+template <int D, int Q, int BZ>
+struct BrickShape
+{
+   static constexpr int NE = 4 * BZ, DD = D * D, QQ = Q * Q, DQ = D * Q, ND = D * D * D;
+   static constexpr int LX = 2 * (D - 1) + 1, LY = LX, LZ = BZ * (D - 1) + 1, NB = LX * LY * LZ;
+   static constexpr int SURF = 2 * LX * LY + 2 * (LZ - 2) * LX + 2 * (LZ - 2) * (LY - 2);
+   // per-element LDS: SA holds the x-stage lines (2 D^2 Q), SB the y/z-stage planes (3 D Q^2,
+   // the z stage works in place); staged element outputs (D^3) reuse SB
+   static constexpr int SA = 2 * DD * Q, SB = 3 * D * QQ;
+   static constexpr int NT = ((NE * QQ + 63) / 64) * 64;  // stage 3 in one pass
+   // waves per SIMD the register budget targets: 4 (<= 128 VGPRs) up to p = 4, where the
+   // 2 x 2 x 1 brick then fits 5 workgroups per CU; the larger orders keep their registers
+   static constexpr int WPE = D <= 5 ? 4 : 1;
+};
+
+// lattice coordinate P along one brick direction -> (first element index, local index,
+// holders): the shared plane P = D-1 is held by element 0 (local D-1) and 1 (local 0)
+template <int D>
+__device__ __forceinline__ void brick_cand(int P, int &c0, int &l0, int &n)
+{
+   if (P < D - 1) { c0 = 0; l0 = P; n = 1; }
+   else if (P == D - 1) { c0 = 0; l0 = D - 1; n = 2; }
+   else { c0 = 1; l0 = P - (D - 1); n = 1; }
+}
+
+template <int D, int Q, int BZ, bool SPLIT, bool AFF>
+__global__ void __launch_bounds__((BrickShape<D, Q, BZ>::NT), (BrickShape<D, Q, BZ>::WPE))
+k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *__restrict__ bmap, int n_owned,
+              const double *__restrict__ qdd, const double *__restrict__ qdm,
+              const double *__restrict__ x, const double *__restrict__ xg,
+              double *__restrict__ y, double *__restrict__ yg, const Basis1D *__restrict__ btab,
+              double *__restrict__ part)
+{
+   using S = BrickShape<D, Q, BZ>;
+   constexpr int NE = S::NE, DD = S::DD, QQ = S::QQ, DQ = S::DQ, ND = S::ND, SA = S::SA, SB = S::SB;
+   constexpr int LX = S::LX, LY = S::LY, NB = S::NB;
+   static_assert(QQ <= 64, "brick kernel needs Q1D <= 8");
+   static_assert(SB >= ND, "staged outputs reuse bufB");
+   __shared__ double bufA[NE * SA];
+   __shared__ double bufB[NE * SB];
+   const int k = k_begin + xcd_contiguous(blockIdx.x, gridDim.x);
+   if (k >= k_end) { return; }  // whole workgroup
+   const int t = threadIdx.x;
+   const int *bm = bmap + (size_t)k * NB;
+   const int *be = belem + (size_t)k * NE;
+   auto lattice = [&](int elt, int dx, int dy, int dz) {
+      const int ex = elt & 1, ey = (elt >> 1) & 1, ez = elt >> 2;
+      return ((ez * (D - 1) + dz) * LY + ey * (D - 1) + dy) * LX + ex * (D - 1) + dx;
+   };
+
+   // qdata of the (element, qx, qy) column this lane weights in stage 3: in flight
+   // during the gather and the x / y contractions.  AFF: the raw per-point pairs and the
+   // element's C stay in registers until the z stage (forming the 6 entries at load time
+   // would make the wave wait for the loads at entry, and hold 7Q values instead of 2Q + 6)
+   double qv[7][Q];
+   v2d pa[Q];
+   double cc[6];
+   if (t < NE * QQ)
+   {
+      const int e = be[t / QQ], l = t % QQ;
+      if (AFF)
+      {
+         constexpr int NQ = Q * Q * Q;
+#pragma unroll
+         for (int qz = 0; qz < Q; qz++) { pa[qz] = reinterpret_cast<const v2d *>(qdm)[(size_t)e * NQ + qz * QQ + l]; }
+#pragma unroll
+         for (int c = 0; c < 6; c++) { cc[c] = qdd[(size_t)e * 6 + c]; }
+      }
+      else { line_load_qdata<D, Q, true, true, false>(qv, e, l, qdd, qdm); }
+   }
+
+   // ---- lanes (element, dy, dz): gather the x-line, contract in x
+   if (t < NE * DD)
+   {
+      CBasis *bp = stage_basis(btab);
+      const int elt = t / DD, l = t % DD;
+      const int *mp = bm + lattice(elt, 0, l % D, l / D);
+      double xl[D];
+#pragma unroll
+      for (int dx = 0; dx < D; dx++)
+      {
+         const int d = bdof(mp[dx]);
+         xl[dx] = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
+      }
+      double *o = bufA + elt * SA;
+#pragma unroll
+      for (int qx = 0; qx < Q; qx++)
+      {
+         double u = 0.0, v = 0.0;
+#pragma unroll
+         for (int dx = 0; dx < D; dx++)
+         {
+            u += bp->B[qx + MQ * dx] * xl[dx];
+            v += bp->G[qx + MQ * dx] * xl[dx];
+         }
+         o[l * Q + qx] = u;
+         o[DD * Q + l * Q + qx] = v;
+      }
+   }
+   __syncthreads();
+   // ---- lanes (element, qx, dz): contract in y
+   if (t < NE * DQ)
+   {
+      CBasis *bp = stage_basis(btab);
+      const int elt = t / DQ, l = t % DQ, qx = l % Q, dz = l / Q;
+      const double *in = bufA + elt * SA;
+      double la[D], lb[D];
+#pragma unroll
+      for (int dy = 0; dy < D; dy++)
+      {
+         la[dy] = in[(dz * D + dy) * Q + qx];
+         lb[dy] = in[DD * Q + (dz * D + dy) * Q + qx];
+      }
+      double *o = bufB + elt * SB;
+#pragma unroll
+      for (int qy = 0; qy < Q; qy++)
+      {
+         double gb = 0.0, bg = 0.0, bb = 0.0;
+#pragma unroll
+         for (int dy = 0; dy < D; dy++)
+         {
+            const double by = bp->B[qy + MQ * dy], gy = bp->G[qy + MQ * dy];
+            gb += by * lb[dy];
+            bg += gy * la[dy];
+            bb += by * la[dy];
+         }
+         const int oo = (dz * Q + qy) * Q + qx;
+         o[oo] = gb;
+         o[D * QQ + oo] = bg;
+         o[2 * D * QQ + oo] = bb;
+      }
+   }
+   __syncthreads();
+   // ---- lanes (element, qx, qy): contract in z, weight, transpose in z (in place: a lane
+   // reads its whole (qx, qy) column before writing it back)
+   if (t < NE * QQ)
+   {
+      CBasis *bp = stage_basis(btab);
+      const int elt = t / QQ, l = t % QQ;
+      double *in = bufB + elt * SB;
+      double l0[D], l1[D], l2[D];
+#pragma unroll
+      for (int dz = 0; dz < D; dz++)
+      {
+         l0[dz] = in[dz * QQ + l];
+         l1[dz] = in[D * QQ + dz * QQ + l];
+         l2[dz] = in[2 * D * QQ + dz * QQ + l];
+      }
+      double A1[D], A2[D], A3[D];
+#pragma unroll
+      for (int dz = 0; dz < D; dz++) { A1[dz] = 0.0; A2[dz] = 0.0; A3[dz] = 0.0; }
+#pragma unroll
+      for (int qz = 0; qz < Q; qz++)
+      {
+         double gx = 0.0, gy = 0.0, gz = 0.0, u = 0.0;
+#pragma unroll
+         for (int dz = 0; dz < D; dz++)
+         {
+            const double bz = bp->B[qz + MQ * dz], gzz = bp->G[qz + MQ * dz];
+            gx += bz * l0[dz];
+            gy += bz * l1[dz];
+            gz += gzz * l2[dz];
+            u += bz * l2[dz];
+         }
+         double fx, fy, fz, m;
+         if (AFF)
+         {
+            const double wb = pa[qz].x;
+            fx = wb * (cc[0] * gx + cc[1] * gy + cc[2] * gz);
+            fy = wb * (cc[1] * gx + cc[3] * gy + cc[4] * gz);
+            fz = wb * (cc[2] * gx + cc[4] * gy + cc[5] * gz);
+            m = pa[qz].y * u;
+         }
+         else
+         {
+            fx = qv[0][qz] * gx + qv[1][qz] * gy + qv[2][qz] * gz;
+            fy = qv[1][qz] * gx + qv[3][qz] * gy + qv[4][qz] * gz;
+            fz = qv[2][qz] * gx + qv[4][qz] * gy + qv[5][qz] * gz;
+            m = qv[6][qz] * u;
+         }
+#pragma unroll
+         for (int dz = 0; dz < D; dz++)
+         {
+            const double bz = bp->B[qz + MQ * dz], gzz = bp->G[qz + MQ * dz];
+            A1[dz] += bz * fx;
+            A2[dz] += bz * fy;
+            A3[dz] += gzz * fz;
+            A3[dz] += bz * m;
+         }
+      }
+#pragma unroll
+      for (int dz = 0; dz < D; dz++)
+      {
+         in[dz * QQ + l] = A1[dz];
+         in[D * QQ + dz * QQ + l] = A2[dz];
+         in[2 * D * QQ + dz * QQ + l] = A3[dz];
+      }
+   }
+   __syncthreads();
+   // ---- lanes (element, qx, dz): transpose in y
+   if (t < NE * DQ)
+   {
+      CBasis *bp = stage_basis(btab);
+      const int elt = t / DQ, l = t % DQ, qx = l % Q, dz = l / Q;
+      const double *in = bufB + elt * SB;
+      double l0[Q], l1[Q], l2[Q];
+#pragma unroll
+      for (int qy = 0; qy < Q; qy++)
+      {
+         const int oo = (dz * Q + qy) * Q + qx;
+         l0[qy] = in[oo];
+         l1[qy] = in[D * QQ + oo];
+         l2[qy] = in[2 * D * QQ + oo];
+      }
+      double *o = bufA + elt * SA;
+#pragma unroll
+      for (int dy = 0; dy < D; dy++)
+      {
+         double c1 = 0.0, c2 = 0.0;
+#pragma unroll
+         for (int qy = 0; qy < Q; qy++)
+         {
+            const double by = bp->B[qy + MQ * dy], gy = bp->G[qy + MQ * dy];
+            c1 += by * l0[qy];
+            c2 += gy * l1[qy] + by * l2[qy];
+         }
+         o[(dz * D + dy) * Q + qx] = c1;
+         o[DD * Q + (dz * D + dy) * Q + qx] = c2;
+      }
+   }
+   __syncthreads();
+   // ---- lanes (element, dy, dz): transpose in x -> element outputs staged in LDS [elt][a]
+   if (t < NE * DD)
+   {
+      CBasis *bp = stage_basis(btab);
+      const int elt = t / DD, l = t % DD;
+      const double *in = bufA + elt * SA;
+      double l0[Q], l1[Q];
+#pragma unroll
+      for (int qx = 0; qx < Q; qx++)
+      {
+         l0[qx] = in[l * Q + qx];
+         l1[qx] = in[DD * Q + l * Q + qx];
+      }
+#pragma unroll
+      for (int dx = 0; dx < D; dx++)
+      {
+         double v = 0.0;
+#pragma unroll
+         for (int qx = 0; qx < Q; qx++) { v += bp->G[qx + MQ * dx] * l0[qx] + bp->B[qx + MQ * dx] * l1[qx]; }
+         bufB[elt * ND + l * D + dx] = v;  // bufB is free: stage 4 read it before a barrier
+      }
+   }
+   __syncthreads();
+   // ---- lattice points: sum the holders in a fixed (z, y, x) order, store or publish
+   for (int p = t; p < NB; p += S::NT)
+   {
+      const int X = p % LX, Y = (p / LX) % LY, Z = p / (LX * LY);
+      int cx, lx, nx, cy, ly, ny, cz, lz, nz;
+      brick_cand<D>(X, cx, lx, nx);
+      brick_cand<D>(Y, cy, ly, ny);
+      if (BZ == 2) { brick_cand<D>(Z, cz, lz, nz); }
+      else { cz = 0; lz = Z; nz = 1; }
+      double v = 0.0;
+      for (int iz = 0; iz < nz; iz++)
+         for (int iy = 0; iy < ny; iy++)
+            for (int ix = 0; ix < nx; ix++)
+            {
+               const int elt = (cx + ix) + 2 * ((cy + iy) + 2 * (cz + iz));
+               const int a = ((iz ? 0 : lz) * D + (iy ? 0 : ly)) * D + (ix ? 0 : lx);
+               v += bufB[elt * ND + a];
+            }
+      const int g = bm[p];
+      const int d = bdof(g);
+      if (!bshared(g)) { *((!SPLIT || d < n_owned) ? y + d : yg + (d - n_owned)) = v; }
+      else { part[(size_t)k * S::SURF + brick_surface_index(D, BZ, X, Y, Z)] = v; }  // surface only (setup)
+   }
+}
+
+// --------------------------------------------------------------------------
+// Persistent brick kernel: the same brick algorithm, with
+//  * bank-conflict-free LDS images: every stage's lane -> element mapping starts each element
+//    at a 32-lane boundary (x lines, y lines) or at a stride of S3 = QQ rounded up to 16 lanes
+//    (z columns), the x-line image is [f][qx][dz][dy] (dense), the y/z image [g][dz][qy][qx]
+//    with a dz stride DS = Q (mod 32) and an element stride SB = S3 (mod 32), so consecutive
+//    lanes of a ds_read_b64 group (32 lanes) / ds_write_b64 group (16 lanes) hit distinct
+//    banks in all five stages (MI355X_MICROARCH.md §LDS);
+//  * one workgroup per CU slot (grid = occupancy x CUs) walking bricks k = j G + slot(w):
+//    the next brick's qdata pairs, element matrices and lattice map are loaded right after
+//    this brick's z stage (in flight during the transposed stages, the lattice sum and the
+//    next brick's gather and x / y stages), so HBM streams continuously instead of each
+//    workgroup paying its own load latency at entry.  At iteration j the workgroups hold a
+//    window of G consecutive bricks, split XCD-contiguously.
+// --------------------------------------------------------------------------
+template <int D, int Q, int BZ>
+struct BrickShapeP
+{
+   static constexpr int NE = 4 * BZ, DD = D * D, QQ = Q * Q, DQ = D * Q, ND = D * D * D;
+   static constexpr int LX = 2 * (D - 1) + 1, LY = LX, LZ = BZ * (D - 1) + 1, NB = LX * LY * LZ;
+   static constexpr int SURF = 2 * LX * LY + 2 * (LZ - 2) * LX + 2 * (LZ - 2) * (LY - 2);
+   static constexpr int L2S = (DQ > DD ? DQ : DD) <= 32 ? 32 : 64;  // lanes per element, line stages
+   static constexpr int S3 = ((QQ + 15) / 16) * 16;                 // lanes per element, z stage
+   static constexpr int DS = (QQ <= Q + 32 * ((QQ - Q + 31) / 32)) ? Q + 32 * ((QQ - Q + 31) / 32) : QQ;
+   static constexpr int SA = 2 * DD * Q;                            // x-line image per element
+   static constexpr int SB0 = 3 * D * DS > ND ? 3 * D * DS : ND;
+   static constexpr int SB = SB0 + ((S3 % 32) - (SB0 % 32) + 32) % 32;  // SB = S3 (mod 32)
+   static constexpr int NTL = NE * L2S, NT3 = NE * S3;
+   static constexpr int NT = (((NTL > NT3 ? NTL : NT3) + 63) / 64) * 64;
+   static constexpr int WPE = (D <= 5 && BZ == 1) ? 3 : 1;
+};
+
+template <int D, int Q, int BZ, bool SPLIT, bool AFF>
+__global__ void __launch_bounds__((BrickShapeP<D, Q, BZ>::NT), (BrickShapeP<D, Q, BZ>::WPE))
+k_apply_brick_p(int k_begin, int k_end, const int *__restrict__ belem, const int *__restrict__ bmap, int n_owned,
+                const double *__restrict__ qdd, const double *__restrict__ qdm,
+                const double *__restrict__ x, const double *__restrict__ xg,
+                double *__restrict__ y, double *__restrict__ yg, const Basis1D *__restrict__ btab,
+                double *__restrict__ part)
+{
+   using S = BrickShapeP<D, Q, BZ>;
+   constexpr int NE = S::NE, DD = S::DD, QQ = S::QQ, DQ = S::DQ, SA = S::SA, SB = S::SB, DS = S::DS;
+   constexpr int LX = S::LX, LY = S::LY, NB = S::NB, L2S = S::L2S, S3 = S::S3, NT = S::NT, NQ = Q * Q * Q;
+   constexpr int NPL = (NB + NT - 1) / NT;  // lattice points per thread
+   static_assert(QQ <= 64, "brick kernel needs Q1D <= 8");
+   static_assert(DQ <= L2S && DD <= L2S, "line stages: one lane per line");
+   __shared__ double sXL[NE * SA];  // x lines: [e][f][qx][dz][dy]
+   __shared__ double sYQ[NE * SB];  // y / z planes: [e][g][dz (stride DS)][qy][qx]; then outputs [e][dx][dz][dy]
+   const int t = threadIdx.x;
+   // lane roles
+   const int eL = t / L2S, lL = t % L2S;                 // line stages
+   const bool actL = eL < NE && lL < DD;                 // stages 1, 5: lL = dy + D dz
+   const bool act2 = eL < NE && lL < DQ;                 // stages 2, 4
+   const int e3 = t / S3, l3 = t % S3;                   // z stage: l3 = qx + Q qy
+   const bool act3 = e3 < NE && l3 < QQ;
+   const int G = gridDim.x, slot = xcd_contiguous(blockIdx.x, G);
+   auto lattice = [&](int elt, int dx, int dy, int dz) {
+      const int ex = elt & 1, ey = (elt >> 1) & 1, ez = elt >> 2;
+      return ((ez * (D - 1) + dz) * LY + ey * (D - 1) + dy) * LX + ex * (D - 1) + dx;
+   };
+
+   // registers carried across iterations: the z stage's qdata and the brick's maps
+   double qv[7][Q];      // native layout
+   v2d pa[Q];            // AFFINE_E pairs
+   double cc[6];         // AFFINE_E element matrix
+   int bmg[D];           // gather map of this lane's x line
+   int bms[NPL];         // lattice map of this lane's lattice points
+   auto load_brick = [&](int kb) {
+      const int *bm = bmap + (size_t)kb * NB;
+      if (act3)
+      {
+         const int e = belem[(size_t)kb * NE + e3];
+         if (AFF)
+         {
+#pragma unroll
+            for (int qz = 0; qz < Q; qz++) { pa[qz] = reinterpret_cast<const v2d *>(qdm)[(size_t)e * NQ + qz * QQ + l3]; }
+#pragma unroll
+            for (int c = 0; c < 6; c++) { cc[c] = qdd[(size_t)e * 6 + c]; }
+         }
+         else { line_load_qdata<D, Q, true, true, false>(qv, e, l3, qdd, qdm); }
+      }
+      if (actL)
+      {
+         const int *mp = bm + lattice(eL, 0, lL % D, lL / D);
+#pragma unroll
+         for (int dx = 0; dx < D; dx++) { bmg[dx] = mp[dx]; }
+      }
+#pragma unroll
+      for (int i = 0; i < NPL; i++)
+      {
+         const int p = t + i * NT;
+         bms[i] = p < NB ? bm[p] : 0;
+      }
+   };
+   int k = k_begin + slot;
+   if (k < k_end) { load_brick(k); }
+#pragma unroll 1
+   for (; k < k_end; k += G)  // workgroup-uniform
+   {
+      // ---- lanes (element, dy, dz): gather the x-line, contract in x -> sXL [f][qx][l]
+      if (actL)
+      {
+         CBasis *bp = stage_basis(btab);
+         double xl[D];
+#pragma unroll
+         for (int dx = 0; dx < D; dx++)
+         {
+            const int d = bdof(bmg[dx]);
+            xl[dx] = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
+         }
+         double *o = sXL + eL * SA + lL;
+#pragma unroll
+         for (int qx = 0; qx < Q; qx++)
+         {
+            double u = 0.0, v = 0.0;
+#pragma unroll
+            for (int dx = 0; dx < D; dx++)
+            {
+               u += bp->B[qx + MQ * dx] * xl[dx];
+               v += bp->G[qx + MQ * dx] * xl[dx];
+            }
+            o[qx * DD] = u;
+            o[Q * DD + qx * DD] = v;
+         }
+      }
+      __syncthreads();
+      // ---- lanes (element, qx, dz), l2 = qx + Q dz: contract in y -> sYQ [g][dz][qy][qx]
+      if (act2)
+      {
+         CBasis *bp = stage_basis(btab);
+         const int qx = lL % Q, dz = lL / Q;
+         const double *in = sXL + eL * SA + qx * DD + dz * D;
+         double la[D], lb[D];
+#pragma unroll
+         for (int dy = 0; dy < D; dy++)
+         {
+            la[dy] = in[dy];
+            lb[dy] = in[Q * DD + dy];
+         }
+         double *o = sYQ + eL * SB + dz * DS + qx;
+#pragma unroll
+         for (int qy = 0; qy < Q; qy++)
+         {
+            double gb = 0.0, bg = 0.0, bb = 0.0;
+#pragma unroll
+            for (int dy = 0; dy < D; dy++)
+            {
+               const double by = bp->B[qy + MQ * dy], gy = bp->G[qy + MQ * dy];
+               gb += by * lb[dy];
+               bg += gy * la[dy];
+               bb += by * la[dy];
+            }
+            o[qy * Q] = gb;
+            o[D * DS + qy * Q] = bg;
+            o[2 * D * DS + qy * Q] = bb;
+         }
+      }
+      __syncthreads();
+      // ---- lanes (element, qx, qy): contract in z, weight, transpose in z (in place)
+      if (act3)
+      {
+         CBasis *bp = stage_basis(btab);
+         double *io = sYQ + e3 * SB + l3;
+         double l0[D], l1[D], l2[D];
+#pragma unroll
+         for (int dz = 0; dz < D; dz++)
+         {
+            l0[dz] = io[dz * DS];
+            l1[dz] = io[D * DS + dz * DS];
+            l2[dz] = io[2 * D * DS + dz * DS];
+         }
+         double A1[D], A2[D], A3[D];
+#pragma unroll
+         for (int dz = 0; dz < D; dz++) { A1[dz] = 0.0; A2[dz] = 0.0; A3[dz] = 0.0; }
+#pragma unroll
+         for (int qz = 0; qz < Q; qz++)
+         {
+            double gx = 0.0, gy = 0.0, gz = 0.0, u = 0.0;
+#pragma unroll
+            for (int dz = 0; dz < D; dz++)
+            {
+               const double bz = bp->B[qz + MQ * dz], gzz = bp->G[qz + MQ * dz];
+               gx += bz * l0[dz];
+               gy += bz * l1[dz];
+               gz += gzz * l2[dz];
+               u += bz * l2[dz];
+            }
+            double fx, fy, fz, m;
+            if (AFF)
+            {
+               const double wb = pa[qz].x;
+               fx = wb * (cc[0] * gx + cc[1] * gy + cc[2] * gz);
+               fy = wb * (cc[1] * gx + cc[3] * gy + cc[4] * gz);
+               fz = wb * (cc[2] * gx + cc[4] * gy + cc[5] * gz);
+               m = pa[qz].y * u;
+            }
+            else
+            {
+               fx = qv[0][qz] * gx + qv[1][qz] * gy + qv[2][qz] * gz;
+               fy = qv[1][qz] * gx + qv[3][qz] * gy + qv[4][qz] * gz;
+               fz = qv[2][qz] * gx + qv[4][qz] * gy + qv[5][qz] * gz;
+               m = qv[6][qz] * u;
+            }
+#pragma unroll
+            for (int dz = 0; dz < D; dz++)
+            {
+               const double bz = bp->B[qz + MQ * dz], gzz = bp->G[qz + MQ * dz];
+               A1[dz] += bz * fx;
+               A2[dz] += bz * fy;
+               A3[dz] += gzz * fz;
+               A3[dz] += bz * m;
+            }
+         }
+#pragma unroll
+         for (int dz = 0; dz < D; dz++)
+         {
+            io[dz * DS] = A1[dz];
+            io[D * DS + dz * DS] = A2[dz];
+            io[2 * D * DS + dz * DS] = A3[dz];
+         }
+      }
+      // this brick's lattice map for the stores, then the next brick's qdata and maps: in
+      // flight from here through the next brick's z stage
+      int bst[NPL];
+#pragma unroll
+      for (int i = 0; i < NPL; i++) { bst[i] = bms[i]; }
+      if (k + G < k_end) { load_brick(k + G); }
+      __syncthreads();
+      // ---- lanes (element, dz, qx), l4 = dz + D qx: transpose in y -> sXL [f][qx][dz][dy]
+      if (act2)
+      {
+         CBasis *bp = stage_basis(btab);
+         const int dz = lL % D, qx = lL / D;
+         const double *in = sYQ + eL * SB + dz * DS + qx;
+         double t0[Q], t1[Q], t2[Q];
+#pragma unroll
+         for (int qy = 0; qy < Q; qy++)
+         {
+            t0[qy] = in[qy * Q];
+            t1[qy] = in[D * DS + qy * Q];
+            t2[qy] = in[2 * D * DS + qy * Q];
+         }
+         double *o = sXL + eL * SA + qx * DD + dz * D;
+#pragma unroll
+         for (int dy = 0; dy < D; dy++)
+         {
+            double c1 = 0.0, c2 = 0.0;
+#pragma unroll
+            for (int qy = 0; qy < Q; qy++)
+            {
+               const double by = bp->B[qy + MQ * dy], gy = bp->G[qy + MQ * dy];
+               c1 += by * t0[qy];
+               c2 += gy * t1[qy] + by * t2[qy];
+            }
+            o[dy] = c1;
+            o[Q * DD + dy] = c2;
+         }
+      }
+      __syncthreads();
+      // ---- lanes (element, dy, dz): transpose in x -> element outputs [e][dx][dz][dy] in sYQ
+      if (actL)
+      {
+         CBasis *bp = stage_basis(btab);
+         const double *in = sXL + eL * SA + lL;
+         double l0[Q], l1[Q];
+#pragma unroll
+         for (int qx = 0; qx < Q; qx++)
+         {
+            l0[qx] = in[qx * DD];
+            l1[qx] = in[Q * DD + qx * DD];
+         }
+#pragma unroll
+         for (int dx = 0; dx < D; dx++)
+         {
+            double v = 0.0;
+#pragma unroll
+            for (int qx = 0; qx < Q; qx++) { v += bp->G[qx + MQ * dx] * l0[qx] + bp->B[qx + MQ * dx] * l1[qx]; }
+            sYQ[eL * SB + dx * DD + lL] = v;  // sYQ is free: stage 4 read it before a barrier
+         }
+      }
+      __syncthreads();
+      // ---- lattice points: sum the holders in a fixed (z, y, x) order, store or publish
+#pragma unroll
+      for (int i = 0; i < NPL; i++)
+      {
+         const int p = t + i * NT;
+         if (p >= NB) { continue; }
+         const int X = p % LX, Y = (p / LX) % LY, Z = p / (LX * LY);
+         int cx, lx, nx, cy, ly, ny, cz, lz, nz;
+         brick_cand<D>(X, cx, lx, nx);
+         brick_cand<D>(Y, cy, ly, ny);
+         if (BZ == 2) { brick_cand<D>(Z, cz, lz, nz); }
+         else { cz = 0; lz = Z; nz = 1; }
+         double v = 0.0;
+         for (int iz = 0; iz < nz; iz++)
+            for (int iy = 0; iy < ny; iy++)
+               for (int ix = 0; ix < nx; ix++)
+               {
+                  const int elt = (cx + ix) + 2 * ((cy + iy) + 2 * (cz + iz));
+                  v += sYQ[elt * SB + (ix ? 0 : lx) * DD + (iz ? 0 : lz) * D + (iy ? 0 : ly)];
+               }
+         const int g = bst[i];
+         const int d = bdof(g);
+         if (!bshared(g)) { *((!SPLIT || d < n_owned) ? y + d : yg + (d - n_owned)) = v; }
+         else { part[(size_t)k * S::SURF + brick_surface_index(D, BZ, X, Y, Z)] = v; }  // surface only (setup)
+      }
+      // the next brick's stage 1 writes sXL (last read by stage 5, before the barrier above);
+      // its stage 2 writes sYQ after the barrier that follows stage 1 (the lattice sum above
+      // is done by then)
+   }
+}
+
+// PA diagonal, one 64-lane workgroup per element, any qdata layout, any (D1D, Q1D) with
+// Q1D^2 <= 64: the seven terms of diag(a) = sum_q grad(phi_a)^T O_q grad(phi_a) + m_q phi_a^2
+// sum-factorised in three stages through LDS (PADiffusionDiagonal3D / the mass diagonal,
+// bilininteg_diffusion_kernels.hpp:369, bilininteg_mass_kernels.hpp:325) -- lanes (qx, qy)
+// contract qz, lanes (qx, dz) contract qy, lanes (dy, dz) contract qx and add into the
+// L-vector (atomics) or the E-vector.
+template <int D, int Q>
+__global__ void __launch_bounds__(64)
+k_diag_sf(const int *__restrict__ pos, int kind, int ne, const int *__restrict__ gmap,
+          const double *__restrict__ qdd, const double *__restrict__ qdm, double *__restrict__ diag, bool out_e,
+          const Basis1D *__restrict__ btab)
+{
+   constexpr int ND = D * D * D, NQ = Q * Q * Q, QQ = Q * Q, DD = D * D, DQ = D * Q;
+   static_assert(QQ <= 64, "k_diag_sf needs Q1D <= 8");
+   __shared__ double T[7][D][QQ];   // [k][dz][qy qx]
+   __shared__ double U[7][DD][Q];   // [k][dz dy][qx]
+   const int e = blockIdx.x, t = threadIdx.x;
+   if (e >= ne) { return; }
+   CBasis *bp = stage_basis(btab);
+   // term k = fx(qx,dx) fy(qy,dy) fz(qz,dz) O_k: kinds 0 = B^2, 1 = G^2, 2 = G B per direction
+   constexpr int FX[7] = {1, 0, 0, 2, 2, 0, 0}, FY[7] = {0, 1, 0, 2, 0, 2, 0}, FZ[7] = {0, 0, 1, 0, 2, 2, 0};
+   auto f = [&](int kindf, int qq, int dd) {
+      const double bq = bp->B[qq + MQ * dd], gq = bp->G[qq + MQ * dd];
+      return kindf == 0 ? bq * bq : (kindf == 1 ? gq * gq : gq * bq);
+   };
+   if (t < QQ)
+   {
+      double acc[7][D];
+#pragma unroll
+      for (int k = 0; k < 7; k++)
+#pragma unroll
+         for (int dz = 0; dz < D; dz++) { acc[k][dz] = 0.0; }
+#pragma unroll
+      for (int qz = 0; qz < Q; qz++)
+      {
+         const int q = qz * QQ + t;
+         double O[7];
+         // symmetric entries (11,12,13,22,23,33) -> terms (11, 22, 33, 2*12, 2*13, 2*23), mass
+         const int src[6] = {0, 3, 5, 1, 2, 4};
+#pragma unroll
+         for (int k = 0; k < 6; k++)
+         {
+            O[k] = qdd ? qd_diff_at(qdd, qdm, pos, kind, NQ, e, src[k], q) * (k >= 3 ? 2.0 : 1.0) : 0.0;
+         }
+         O[6] = qdm ? qd_mass_at(qdm, pos, kind, NQ, e, q) : 0.0;
+#pragma unroll
+         for (int k = 0; k < 7; k++)
+#pragma unroll
+            for (int dz = 0; dz < D; dz++) { acc[k][dz] += f(FZ[k], qz, dz) * O[k]; }
+      }
+#pragma unroll
+      for (int k = 0; k < 7; k++)
+#pragma unroll
+         for (int dz = 0; dz < D; dz++) { T[k][dz][t] = acc[k][dz]; }
+   }
+   __syncthreads();
+   if (t < DQ)
+   {
+      const int qx = t % Q, dz = t / Q;
+#pragma unroll
+      for (int k = 0; k < 7; k++)
+#pragma unroll
+         for (int dy = 0; dy < D; dy++)
+         {
+            double u = 0.0;
+#pragma unroll
+            for (int qy = 0; qy < Q; qy++) { u += f(FY[k], qy, dy) * T[k][dz][qy * Q + qx]; }
+            U[k][dz * D + dy][qx] = u;
+         }
+   }
+   __syncthreads();
+   if (t < DD)
+   {
+#pragma unroll
+      for (int dx = 0; dx < D; dx++)
+      {
+         double v = 0.0;
+#pragma unroll
+         for (int k = 0; k < 7; k++)
+#pragma unroll
+            for (int qx = 0; qx < Q; qx++) { v += f(FX[k], qx, dx) * U[k][t][qx]; }
+         const long i = (long)e * ND + t * D + dx;
+         if (out_e) { diag[i] += v; }
+         else { unsafeAtomicAdd(diag + dof_of(gmap[i]), v); }
+      }
+   }
+}
+
+template <int D, int Q, bool MASS, bool DIFF>
+void launch_line_mdq(const ApplyArgs &a, hipStream_t s)
+{
+   ECM2_VERIFY(a.lelem && a.lelem_off, ERR_INTERNAL, "line kernel needs its element list");
+   const int c0 = a.lelem_off[a.blk_begin], c1 = a.lelem_off[a.blk_end];
+   if (c1 <= c0) { return; }
+   const dim3 grid(c1 - c0), block(64);
+#define ECM2_LINE(AF)                                                                                     \
+   hipLaunchKernelGGL((k_apply_line<D, Q, MASS, DIFF, AF>), grid, block, 0, s, c0, c1, a.lelem, a.n_owned,   \
+                      a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, a.btab, a.part)
+   if (a.kind == QLAYOUT_AFFINE_E)
+   {
+      if constexpr (MASS && DIFF) { ECM2_LINE(true); }
+      else { ECM2_VERIFY(false, ERR_INTERNAL, "AFFINE qdata needs both integrators"); }
+      return;
+   }
+   ECM2_LINE(false);
+#undef ECM2_LINE
+}
+
+template <int D, int Q>
+void launch_line_dq(bool mass, bool diff, const ApplyArgs &a, hipStream_t s)
+{
+   if (mass && diff) { launch_line_mdq<D, Q, true, true>(a, s); }
+   else if (mass) { launch_line_mdq<D, Q, true, false>(a, s); }
+   else if (diff) { launch_line_mdq<D, Q, false, true>(a, s); }
+}
+
+// Workgroups of the persistent brick kernel: what one CU holds at once (LDS, registers)
+// times the CUs, at most one per brick.
+template <typename K>
+int persistent_grid(K kernel, int nt, int nwork)
+{
+   static int cus = 0;
+   if (!cus)
+   {
+      int dev = 0;
+      ECM2_HIP(hipGetDevice(&dev));
+      ECM2_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+   }
+   int per_cu = 0;
+   ECM2_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, nt, 0));
+   return std::max(1, std::min(nwork, std::max(1, per_cu) * cus));
+}
+
+// experiment switch of this round's brick-kernel A/B (ECM2_BRICK_AB=0: the persistent
+// kernel; default: one brick per workgroup); removed with the losing variant
+static bool brick_ab_old()
+{
+   static const bool v = [] {
+      const char *e = std::getenv("ECM2_BRICK_AB");
+      return !(e && e[0] == '0');
+   }();
+   return v;
+}
+
+template <int D, int BZ>
+void launch_brick(const ApplyArgs &a, hipStream_t s)
+{
+   constexpr int Q = D + 1;
+   const int k0 = a.brick_off[a.blk_begin], k1 = a.brick_off[a.blk_end];
+   if (k1 <= k0) { return; }
+   ECM2_VERIFY(a.part_brick, ERR_INTERNAL, "brick kernel needs its partial slots");
+   const bool split = a.xg || a.yg, aff = a.kind == QLAYOUT_AFFINE_E;
+   if (brick_ab_old() || !aff)  // the full per-point qdata (7 Q values per lane) does not fit the pipeline
+   {
+      const dim3 grid(k1 - k0), block(BrickShape<D, Q, BZ>::NT);
+#define ECM2_BRICK(SP, AF)                                                                                \
+   hipLaunchKernelGGL((k_apply_brick<D, Q, BZ, SP, AF>), grid, block, 0, s, k0, k1, a.belem, a.bmap, a.n_owned, \
+                      a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, a.btab, a.part_brick)
+      if (split) { if (aff) { ECM2_BRICK(true, true); } else { ECM2_BRICK(true, false); } }
+      else { if (aff) { ECM2_BRICK(false, true); } else { ECM2_BRICK(false, false); } }
+#undef ECM2_BRICK
+      return;
+   }
+   constexpr int NT = BrickShapeP<D, Q, BZ>::NT;
+#define ECM2_BRICK(SP, AF)                                                                                \
+   {                                                                                                      \
+      auto kern = k_apply_brick_p<D, Q, BZ, SP, AF>;                                                      \
+      hipLaunchKernelGGL(kern, dim3(persistent_grid(kern, NT, k1 - k0)), dim3(NT), 0, s, k0, k1, a.belem, \
+                         a.bmap, a.n_owned, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, a.btab, a.part_brick);    \
+   }
+   if (split) { ECM2_BRICK(true, true); }
+   else { ECM2_BRICK(false, true); }
+#undef ECM2_BRICK
+}
+
+void apply_brick(int D, int Q, const ApplyArgs &a, hipStream_t s)
+{
+#define ECM2_BRICK_CASE(DD, BZ)                                         \
+   if (D == DD && Q == DD + 1 && a.brick_bz == BZ)                      \
+   {                                                                    \
+      launch_brick<DD, BZ>(a, s);                                       \
+      ECM2_HIP(hipGetLastError());                                      \
+      return;                                                           \
+   }
+   ECM2_BRICK_CASE(4, 1)
+   ECM2_BRICK_CASE(4, 2)
+   ECM2_BRICK_CASE(5, 1)
+   ECM2_BRICK_CASE(5, 2)
+   ECM2_BRICK_CASE(6, 1)
+   ECM2_BRICK_CASE(6, 2)
+   ECM2_BRICK_CASE(7, 1)
+#undef ECM2_BRICK_CASE
+   ECM2_VERIFY(false, ERR_UNSUPPORTED, "no brick kernel for D1D=" << D << " Q1D=" << Q << " bz=" << a.brick_bz);
+}
+
+} // namespace
+
+namespace kern
+{
+
+bool has_line(int D, int Q)
+{
+   return (Q == D + 1 || Q == D) && D >= 2 && D <= 7 && Q <= 8;
+}
+
+// bricks of 2 x 2 x bz elements for Q1D = D1D + 1 (the default rule), p = 3..6; a
+// 2 x 2 x 2 brick's LDS (16 SB doubles) exceeds 160 KiB at p = 6
+bool has_brick(int D, int Q, int bz)
+{
+   if (Q != D + 1 || D < 4 || D > 7) { return false; }
+   return bz == 1 || (bz == 2 && D <= 6);
+}
+
+int brick_points(int D, int bz) { return (2 * D - 1) * (2 * D - 1) * (bz * (D - 1) + 1); }
+
+void apply_line(int D, int Q, bool mass, bool diff, const ApplyArgs &a, hipStream_t s)
+{
+   if (a.ne == 0) { return; }
+   ECM2_VERIFY(a.btab, ERR_INTERNAL, "line kernel needs the device basis table");
+   if (a.brick_bz)
+   {
+      ECM2_VERIFY(mass && diff, ERR_INTERNAL, "bricks need both integrators");
+      apply_brick(D, Q, a, s);
+   }
+#define ECM2_LINE_CASE(DD, QQ)                                        \
+   if (D == DD && Q == QQ)                                            \
+   {                                                                  \
+      launch_line_dq<DD, QQ>(mass, diff, a, s);                       \
+      ECM2_HIP(hipGetLastError());                                    \
+      return;                                                         \
+   }
+   ECM2_LINE_CASE(2, 3)
+   ECM2_LINE_CASE(3, 4)
+   ECM2_LINE_CASE(4, 5)
+   ECM2_LINE_CASE(5, 6)
+   ECM2_LINE_CASE(6, 7)
+   ECM2_LINE_CASE(7, 8)
+   ECM2_LINE_CASE(2, 2)
+   ECM2_LINE_CASE(3, 3)
+   ECM2_LINE_CASE(4, 4)
+   ECM2_LINE_CASE(5, 5)
+#undef ECM2_LINE_CASE
+   ECM2_VERIFY(false, ERR_UNSUPPORTED, "no line kernel for D1D=" << D << " Q1D=" << Q);
+}
+
+// the generic fallback lives in k_misc.hip
+void diagonal_generic(const int *pos, int D, int Q, int layout, int ne, const int *gm, const double *qdd,
+                      const double *qdm, double *diag, bool out_e, const Basis1D &b, hipStream_t s);
+
+void diagonal(const int *pos, int D, int Q, int layout, int ne, const int *gm, const double *qdd,
+              const double *qdm, double *diag, bool out_e, const Basis1D &b, const Basis1D *btab, hipStream_t s)
+{
+   if (ne == 0) { return; }
+#define ECM2_DIAG_CASE(DD, QQ)                                                                             \
+   if (D == DD && Q == QQ)                                                                                 \
+   {                                                                                                       \
+      hipLaunchKernelGGL((k_diag_sf<DD, QQ>), dim3(ne), dim3(64), 0, s, pos, layout, ne, gm, qdd, qdm, diag, \
+                         out_e, btab);                                                                     \
+      ECM2_HIP(hipGetLastError());                                                                         \
+      return;                                                                                              \
+   }
+   if (btab)
+   {
+      ECM2_DIAG_CASE(2, 3)
+      ECM2_DIAG_CASE(3, 4)
+      ECM2_DIAG_CASE(4, 5)
+      ECM2_DIAG_CASE(5, 6)
+      ECM2_DIAG_CASE(6, 7)
+      ECM2_DIAG_CASE(7, 8)
+      ECM2_DIAG_CASE(2, 2)
+      ECM2_DIAG_CASE(3, 3)
+      ECM2_DIAG_CASE(4, 4)
+      ECM2_DIAG_CASE(5, 5)
+   }
+#undef ECM2_DIAG_CASE
+   diagonal_generic(pos, D, Q, layout, ne, gm, qdd, qdm, diag, out_e, b, s);
+}
+
+} // namespace kern
+} // namespace ecm2

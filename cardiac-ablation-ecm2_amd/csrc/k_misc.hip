@@ -1,0 +1,601 @@
+// k_misc.hip -- reference-shaped pieces and vector kernels (gfx950): the workgroup-per-element
+// apply (E-vector AddMultPA, unfused Mult), ElementRestriction, the generic diagonal, the
+// deterministic summation pass of the fused kernels' scatter, halo pack/unpack, and the
+// device PCG / ODE vector kernels.
+#include "dev_common.hpp"
+
+#include <algorithm>
+
+namespace ecm2
+{
+namespace
+{
+using namespace dev;
+
+// Workgroup per element (lane per quadrature point), any layout, L- or E-vectors in and
+// out (in_e / out_e): six 1D stages through LDS, the reference's smem kernels' structure
+// (bilininteg_mass_kernels.hpp:809-1033, bilininteg_diffusion_kernels.hpp:989-1214).
+template <int D, int Q, bool MASS, bool DIFF>
+__global__ void k_apply_wpe(const int *__restrict__ pos, int kind, int ne, int e_begin, int n_owned,
+                            const int *__restrict__ gmap,
+                            const double *__restrict__ qdd, const double *__restrict__ qdm,
+                            const double *__restrict__ x, const double *__restrict__ xg,
+                            double *__restrict__ y, double *__restrict__ yg, const Basis1D b, bool in_e,
+                            bool out_e)
+{
+   constexpr int ND = D * D * D, NQ = Q * Q * Q;
+   __shared__ double sB[Q * D], sG[Q * D];
+   __shared__ double sX[ND];
+   __shared__ double s1a[D * D * Q], s1b[D * D * Q];
+   __shared__ double s2a[D * Q * Q], s2b[D * Q * Q], s2c[D * Q * Q];
+   __shared__ double s3m[NQ], s3x[NQ], s3y[NQ], s3z[NQ];
+   __shared__ double s4a[Q * Q * D], s4b[Q * Q * D], s4c[Q * Q * D];
+   __shared__ double s5a[Q * D * D], s5b[Q * D * D];
+   const int e = e_begin + blockIdx.x;
+   const int t = threadIdx.x;
+   if (t < Q * D)
+   {
+      const int q = t % Q, d = t / Q;
+      sB[q + Q * d] = b.B[q + MQ * d];
+      sG[q + Q * d] = b.G[q + MQ * d];
+   }
+   if (t < ND)
+   {
+      if (in_e) { sX[t] = x[(size_t)e * ND + t]; }
+      else
+      {
+         const int g = gmap[(size_t)e * ND + t];
+         const int d = dof_of(g);
+         const double v = d < n_owned ? x[d] : xg[d - n_owned];
+         sX[t] = g >= 0 ? v : -v;
+      }
+   }
+   __syncthreads();
+   // stage 1: x-contraction  (qx, dy, dz)
+   if (t < D * D * Q)
+   {
+      const int qx = t % Q, dy = (t / Q) % D, dz = t / (Q * D);
+      double u = 0.0, v = 0.0;
+      for (int dx = 0; dx < D; dx++)
+      {
+         const double c = sX[(dz * D + dy) * D + dx];
+         u += c * sB[qx + Q * dx];
+         v += c * sG[qx + Q * dx];
+      }
+      s1a[t] = u;  // B_x
+      s1b[t] = v;  // G_x
+   }
+   __syncthreads();
+   // stage 2: y-contraction  (qx, qy, dz)
+   if (t < D * Q * Q)
+   {
+      const int qx = t % Q, qy = (t / Q) % Q, dz = t / (Q * Q);
+      double u = 0.0, v = 0.0, w = 0.0;
+      for (int dy = 0; dy < D; dy++)
+      {
+         const int i = (dz * D + dy) * Q + qx;
+         u += s1b[i] * sB[qy + Q * dy];   // G_x B_y
+         v += s1a[i] * sG[qy + Q * dy];   // B_x G_y
+         w += s1a[i] * sB[qy + Q * dy];   // B_x B_y
+      }
+      s2a[t] = u; s2b[t] = v; s2c[t] = w;
+   }
+   __syncthreads();
+   // stage 3: z-contraction + pointwise qdata (qx, qy, qz)
+   if (t < NQ)
+   {
+      const int qx = t % Q, qy = (t / Q) % Q, qz = t / (Q * Q);
+      double gx = 0.0, gy = 0.0, gz = 0.0, u = 0.0;
+      for (int dz = 0; dz < D; dz++)
+      {
+         const int i = (dz * Q + qy) * Q + qx;
+         gx += s2a[i] * sB[qz + Q * dz];
+         gy += s2b[i] * sB[qz + Q * dz];
+         gz += s2c[i] * sG[qz + Q * dz];
+         u += s2c[i] * sB[qz + Q * dz];
+      }
+      double m = 0.0, fx = 0.0, fy = 0.0, fz = 0.0;
+      if (MASS) { m = qd_mass_at(qdm, pos, kind, NQ, e, t) * u; }
+      if (DIFF)
+      {
+         const double O11 = qd_diff_at(qdd, qdm, pos, kind, NQ, e, 0, t);
+         const double O12 = qd_diff_at(qdd, qdm, pos, kind, NQ, e, 1, t);
+         const double O13 = qd_diff_at(qdd, qdm, pos, kind, NQ, e, 2, t);
+         const double O22 = qd_diff_at(qdd, qdm, pos, kind, NQ, e, 3, t);
+         const double O23 = qd_diff_at(qdd, qdm, pos, kind, NQ, e, 4, t);
+         const double O33 = qd_diff_at(qdd, qdm, pos, kind, NQ, e, 5, t);
+         fx = (O11 * gx) + (O12 * gy) + (O13 * gz);
+         fy = (O12 * gx) + (O22 * gy) + (O23 * gz);
+         fz = (O13 * gx) + (O23 * gy) + (O33 * gz);
+      }
+      s3m[t] = m; s3x[t] = fx; s3y[t] = fy; s3z[t] = fz;
+   }
+   __syncthreads();
+   // stage 4: x-transpose (dx, qy, qz)
+   if (t < Q * Q * D)
+   {
+      const int dx = t % D, qy = (t / D) % Q, qz = t / (D * Q);
+      double u = 0.0, v = 0.0, w = 0.0;
+      for (int qx = 0; qx < Q; qx++)
+      {
+         const int i = (qz * Q + qy) * Q + qx;
+         u += s3x[i] * sG[qx + Q * dx] + s3m[i] * sB[qx + Q * dx];
+         v += s3y[i] * sB[qx + Q * dx];
+         w += s3z[i] * sB[qx + Q * dx];
+      }
+      s4a[t] = u; s4b[t] = v; s4c[t] = w;
+   }
+   __syncthreads();
+   // stage 5: y-transpose (dx, dy, qz)
+   if (t < Q * D * D)
+   {
+      const int dx = t % D, dy = (t / D) % D, qz = t / (D * D);
+      double u = 0.0, w = 0.0;
+      for (int qy = 0; qy < Q; qy++)
+      {
+         const int i = (qz * Q + qy) * D + dx;
+         u += s4a[i] * sB[qy + Q * dy] + s4b[i] * sG[qy + Q * dy];
+         w += s4c[i] * sB[qy + Q * dy];
+      }
+      s5a[t] = u; s5b[t] = w;
+   }
+   __syncthreads();
+   // stage 6: z-transpose (dx, dy, dz) + output
+   if (t < ND)
+   {
+      const int dx = t % D, dy = (t / D) % D, dz = t / (D * D);
+      double u = 0.0;
+      for (int qz = 0; qz < Q; qz++)
+      {
+         const int i = (qz * D + dy) * D + dx;
+         u += s5a[i] * sB[qz + Q * dz] + s5b[i] * sG[qz + Q * dz];
+      }
+      if (out_e) { y[(size_t)e * ND + t] += u; }
+      else
+      {
+         const int g = gmap[(size_t)e * ND + t];
+         const int d = dof_of(g);
+         double *dst = d < n_owned ? y + d : yg + (d - n_owned);
+         unsafeAtomicAdd(dst, g >= 0 ? u : -u);
+      }
+   }
+}
+
+__global__ void k_restriction_mult(long n, const int *__restrict__ gmap,
+                                   const double *__restrict__ x, double *__restrict__ xe)
+{
+   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   if (i >= n) { return; }
+   const int g = gmap[i];
+   const double v = x[dof_of(g)];
+   xe[i] = g >= 0 ? v : -v;
+}
+
+__global__ void k_restriction_mult_transpose(int ndofs, const int *__restrict__ offsets,
+                                             const int *__restrict__ indices,
+                                             const double *__restrict__ xe,
+                                             double *__restrict__ y)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i >= ndofs) { return; }
+   double v = 0.0;
+   for (int j = offsets[i]; j < offsets[i + 1]; j++)
+   {
+      const int idx = indices[j];
+      v += idx >= 0 ? xe[idx] : -xe[-1 - idx];
+   }
+   y[i] = v;
+}
+
+// Diagonal, one thread per (element, dof): the direct (not sum-factorised) sum over the
+// quadrature points, for (D1D, Q1D) pairs the sum-factorised kernel does not instantiate.
+__global__ void k_diagonal(const int *__restrict__ pos, int D, int Q, int kind, int ne, const int *__restrict__ gmap,
+                           const double *__restrict__ qdd, const double *__restrict__ qdm,
+                           double *__restrict__ diag, bool out_e, const Basis1D b)
+{
+   const int ND = D * D * D, NQ = Q * Q * Q;
+   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   if (t >= (long)ne * ND) { return; }
+   const int e = (int)(t / ND), a = (int)(t % ND);
+   const int dx = a % D, dy = (a / D) % D, dz = a / (D * D);
+   double s = 0.0;
+   for (int qz = 0; qz < Q; qz++)
+      for (int qy = 0; qy < Q; qy++)
+         for (int qx = 0; qx < Q; qx++)
+         {
+            const int q = (qz * Q + qy) * Q + qx;
+            const double bx = b.B[qx + MQ * dx], by = b.B[qy + MQ * dy], bz = b.B[qz + MQ * dz];
+            const double gx = b.G[qx + MQ * dx], gy = b.G[qy + MQ * dy], gz = b.G[qz + MQ * dz];
+            if (qdm) { s += bx * bx * by * by * bz * bz * qd_mass_at(qdm, pos, kind, NQ, e, q); }
+            if (qdd)
+            {
+               const double p0 = gx * by * bz, p1 = bx * gy * bz, p2 = bx * by * gz;
+               s += p0 * p0 * qd_diff_at(qdd, qdm, pos, kind, NQ, e, 0, q) +
+                    p1 * p1 * qd_diff_at(qdd, qdm, pos, kind, NQ, e, 3, q) +
+                    p2 * p2 * qd_diff_at(qdd, qdm, pos, kind, NQ, e, 5, q) +
+                    2.0 * (p0 * p1 * qd_diff_at(qdd, qdm, pos, kind, NQ, e, 1, q) +
+                           p0 * p2 * qd_diff_at(qdd, qdm, pos, kind, NQ, e, 2, q) +
+                           p1 * p2 * qd_diff_at(qdd, qdm, pos, kind, NQ, e, 4, q));
+            }
+         }
+   if (out_e) { diag[t] += s; }
+   else { unsafeAtomicAdd(diag + dof_of(gmap[t]), s); }
+}
+
+__global__ void k_set_values(int n, const int *__restrict__ idx, double val, double *__restrict__ y)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { y[idx[i]] = val; }
+}
+
+__global__ void k_copy_values(int n, const int *__restrict__ idx, const double *__restrict__ x,
+                              double *__restrict__ y)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { y[idx[i]] = x[idx[i]]; }
+}
+
+constexpr int kDotBlocks = 1024;
+
+__global__ void __launch_bounds__(256)
+k_dot_partial(int n, const double *__restrict__ a, const double *__restrict__ b,
+              double *__restrict__ partials)
+{
+   __shared__ double red[4];
+   double s = 0.0;
+   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+   {
+      s += a[i] * b[i];
+   }
+   for (int off = 32; off > 0; off >>= 1) { s += __shfl_down(s, off, 64); }
+   if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6] = s; }
+   __syncthreads();
+   if (threadIdx.x == 0) { partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]); }
+}
+
+__global__ void __launch_bounds__(256)
+k_dot_final(int nparts, const double *__restrict__ partials, double *__restrict__ out, double *__restrict__ hout)
+{
+   __shared__ double red[4];
+   double s = 0.0;
+   for (int i = threadIdx.x; i < nparts; i += blockDim.x) { s += partials[i]; }
+   for (int off = 32; off > 0; off >>= 1) { s += __shfl_down(s, off, 64); }
+   if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6] = s; }
+   __syncthreads();
+   if (threadIdx.x == 0)
+   {
+      const double v = (red[0] + red[1]) + (red[2] + red[3]);
+      *out = v;
+      if (hout) { *hout = v; }  // mapped pinned host mirror (the solver's stopping test)
+   }
+}
+
+// One fused PCG update (CGSolver::Mult's add/Mult(prec)/Dot sequence, solvers.cpp:930-960):
+// alpha = nom/den; x += alpha d; r -= alpha Ad; z = dinv .* r (jacobi) ; partial sums of r.z
+// (or r.r) in the fixed grid-stride order of k_dot_partial, finished by k_dot_final.
+// z holds A d on entry and the preconditioned residual on exit (jacobi only).
+__global__ void __launch_bounds__(256)
+k_pcg_step(int n, const double *__restrict__ nom, const double *__restrict__ den,
+           const double *__restrict__ d, double *__restrict__ z, double *__restrict__ x,
+           double *__restrict__ r, const double *__restrict__ dinv, double *__restrict__ partials)
+{
+   __shared__ double red[4];
+   const double alpha = *nom / *den;
+   double s = 0.0;
+   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+   {
+      x[i] = x[i] + alpha * d[i];
+      const double rn = r[i] + (-alpha) * z[i];
+      r[i] = rn;
+      if (dinv)
+      {
+         const double zn = dinv[i] * rn;
+         z[i] = zn;
+         s += rn * zn;
+      }
+      else { s += rn * rn; }
+   }
+   for (int off = 32; off > 0; off >>= 1) { s += __shfl_down(s, off, 64); }
+   if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6] = s; }
+   __syncthreads();
+   if (threadIdx.x == 0) { partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]); }
+}
+
+// ConstrainedOperator around a Mult without a vector copy: saved = v[ess], v[ess] = 0 ...
+__global__ void k_ess_save_zero(int n, const int *__restrict__ idx, double *__restrict__ v,
+                                double *__restrict__ saved)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { saved[i] = v[idx[i]]; v[idx[i]] = 0.0; }
+}
+
+// ... then v[ess] = y[ess] = saved (DIAG_ONE rows)
+__global__ void k_ess_restore(int n, const int *__restrict__ idx, const double *__restrict__ saved,
+                              double *__restrict__ v, double *__restrict__ y)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { v[idx[i]] = saved[i]; y[idx[i]] = saved[i]; }
+}
+
+__global__ void k_pcg_precond(int n, const double *__restrict__ dinv, const double *__restrict__ r,
+                              double *__restrict__ z)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { z[i] = dinv ? dinv[i] * r[i] : r[i]; }
+}
+
+__global__ void k_pcg_update_d(int n, const double *__restrict__ betanom,
+                               const double *__restrict__ nom, const double *__restrict__ z,
+                               double *__restrict__ d)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i >= n) { return; }
+   const double beta = *betanom / *nom;
+   d[i] = z[i] + beta * d[i];
+}
+
+__global__ void k_scale(int n, double a, double *__restrict__ y)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { y[i] *= a; }
+}
+
+// out = x + c k  (out may alias x)
+__global__ void k_add_scaled(int n, const double *x, double c, const double *__restrict__ k, double *out)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { out[i] = x[i] + c * k[i]; }
+}
+
+// STREAM copy (measurement only): 16-byte nontemporal loads and stores, grid-stride,
+// the access shape of the guide's 6.29 TB/s float4-copy figure.
+__global__ void k_stream_copy(long n2, const v2d *__restrict__ a, v2d *__restrict__ b)
+{
+   const long stride = (long)gridDim.x * blockDim.x;
+   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride)
+   {
+      __builtin_nontemporal_store(__builtin_nontemporal_load(a + i), b + i);
+   }
+}
+
+__global__ void k_reciprocal(int n, const double *__restrict__ a, double *__restrict__ out)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { out[i] = 1.0 / a[i]; }
+}
+
+__global__ void k_gather_idx(int n, const int *__restrict__ idx, const double *__restrict__ x,
+                             double *__restrict__ buf)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { buf[i] = x[idx[i]]; }
+}
+
+__global__ void k_scatter_add_idx(int n, const int *__restrict__ idx, const double *__restrict__ buf,
+                                  double *__restrict__ y)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   // atomic: a dof shared by >= 3 ranks appears in several neighbour segments
+   if (i < n) { unsafeAtomicAdd(y + idx[i], buf[i]); }
+}
+
+// Second pass of the deterministic scatter: y[dofs[i]] = sum of the partial slots
+// slots[start .. start+count) in ascending slot order, for i in [i0, i1), with
+// meta[i] = start << 5 | count.  All slot loads, then all partial loads, are issued
+// independently (count <= 8 unrolled; more -- unstructured meshes -- loops), so a
+// thread waits ~3 memory latencies instead of 2 + 2*count.  The list is ordered by
+// first slot (pa_form.cpp), so neighbouring threads read neighbouring lanes; blocks are
+// taken in XCD-contiguous order, so the slot lines neighbouring dofs read sit in one L2.
+__global__ void k_sum_partials(int i0, int i1, const int *__restrict__ dofs, const unsigned *__restrict__ meta,
+                               const int *__restrict__ slots, const double *__restrict__ part, int n_owned,
+                               double *__restrict__ y, double *__restrict__ yg)
+{
+   const int b = xcd_contiguous(blockIdx.x, gridDim.x);
+   const int i = i0 + b * blockDim.x + threadIdx.x;
+   if (i >= i1) { return; }
+   const unsigned m = meta[i];
+   const int d = dofs[i];
+   const int start = (int)(m >> 5), cnt = (int)(m & 31);
+   double acc = 0.0;
+   int sl[8];
+#pragma unroll
+   for (int k = 0; k < 8; k++) { sl[k] = k < cnt ? slots[start + k] : -1; }
+   double v[8];
+#pragma unroll
+   for (int k = 0; k < 8; k++) { v[k] = sl[k] >= 0 ? part[sl[k]] : 0.0; }
+#pragma unroll
+   for (int k = 0; k < 8; k++) { acc += v[k]; }
+   for (int k = 8; k < cnt; k++) { acc += part[slots[start + k]]; }
+   if (d < n_owned) { y[d] = acc; }
+   else { yg[d - n_owned] = acc; }
+}
+
+template <int D, int Q, bool MASS, bool DIFF>
+void launch_wpe_mdq(const ApplyArgs &a, bool in_e, bool out_e, const Basis1D &b, hipStream_t s)
+{
+   constexpr int NQ = Q * Q * Q;
+   const int nt = ((NQ + 63) / 64) * 64;
+   const int e0 = a.blk_begin * 64, e1 = std::min(a.ne, a.blk_end * 64);
+   if (e1 <= e0) { return; }
+   hipLaunchKernelGGL((k_apply_wpe<D, Q, MASS, DIFF>), dim3(e1 - e0), dim3(nt), 0, s, a.pos, a.kind, a.ne, e0,
+                      a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, in_e, out_e);
+}
+
+template <int D, int Q>
+void launch_wpe_dq(bool mass, bool diff, const ApplyArgs &a, bool in_e, bool out_e,
+                   const Basis1D &b, hipStream_t s)
+{
+   if (mass && diff) { launch_wpe_mdq<D, Q, true, true>(a, in_e, out_e, b, s); }
+   else if (mass) { launch_wpe_mdq<D, Q, true, false>(a, in_e, out_e, b, s); }
+   else if (diff) { launch_wpe_mdq<D, Q, false, true>(a, in_e, out_e, b, s); }
+}
+
+} // namespace
+
+namespace kern
+{
+
+void apply_wpe(int D, int Q, bool mass, bool diff, const ApplyArgs &a, bool in_e, bool out_e,
+               const Basis1D &b, hipStream_t s)
+{
+   if (a.ne == 0) { return; }
+#define ECM2_WPE_CASE(DD, QQ)                                         \
+   if (D == DD && Q == QQ)                                            \
+   {                                                                  \
+      launch_wpe_dq<DD, QQ>(mass, diff, a, in_e, out_e, b, s);        \
+      ECM2_HIP(hipGetLastError());                                    \
+      return;                                                         \
+   }
+   ECM2_WPE_CASE(2, 3)
+   ECM2_WPE_CASE(3, 4)
+   ECM2_WPE_CASE(4, 5)
+   ECM2_WPE_CASE(5, 6)
+   ECM2_WPE_CASE(2, 2)
+   ECM2_WPE_CASE(3, 3)
+   ECM2_WPE_CASE(4, 4)
+   ECM2_WPE_CASE(5, 5)
+   ECM2_WPE_CASE(6, 7)
+#undef ECM2_WPE_CASE
+   ECM2_VERIFY(false, ERR_UNSUPPORTED, "no PA kernel for D1D=" << D << " Q1D=" << Q);
+}
+
+void restriction_mult(long n, int nd, const int *gm, const double *x, double *xe, hipStream_t s)
+{
+   (void)nd;
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_restriction_mult, dim3(grid_for(n, 256)), dim3(256), 0, s, n, gm, x, xe);
+   ECM2_HIP(hipGetLastError());
+}
+
+void restriction_mult_transpose(int ndofs, int nd, const int *offsets, const int *indices,
+                                const double *xe, double *y, hipStream_t s)
+{
+   (void)nd;
+   if (ndofs == 0) { return; }
+   hipLaunchKernelGGL(k_restriction_mult_transpose, dim3(grid_for(ndofs, 256)), dim3(256), 0, s,
+                      ndofs, offsets, indices, xe, y);
+   ECM2_HIP(hipGetLastError());
+}
+
+void diagonal_generic(const int *pos, int D, int Q, int layout, int ne, const int *gm, const double *qdd,
+                      const double *qdm, double *diag, bool out_e, const Basis1D &b, hipStream_t s)
+{
+   const long n = (long)ne * D * D * D;
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_diagonal, dim3(grid_for(n, 128)), dim3(128), 0, s, pos, D, Q, layout, ne, gm,
+                      qdd, qdm, diag, out_e, b);
+   ECM2_HIP(hipGetLastError());
+}
+
+void set_values(int n, const int *idx, double val, double *y, hipStream_t s)
+{
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_set_values, dim3(grid_for(n, 256)), dim3(256), 0, s, n, idx, val, y);
+   ECM2_HIP(hipGetLastError());
+}
+
+void copy_values(int n, const int *idx, const double *x, double *y, hipStream_t s)
+{
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_copy_values, dim3(grid_for(n, 256)), dim3(256), 0, s, n, idx, x, y);
+   ECM2_HIP(hipGetLastError());
+}
+
+void dot(int n, const double *a, const double *b, double *partials, double *out, hipStream_t s, double *hout)
+{
+   hipLaunchKernelGGL(k_dot_partial, dim3(kDotBlocks), dim3(256), 0, s, n, a, b, partials);
+   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, s, kDotBlocks, partials, out, hout);
+   ECM2_HIP(hipGetLastError());
+}
+
+void pcg_step(int n, const double *nom, const double *den, const double *d, double *z, double *x, double *r,
+              const double *dinv, double *partials, double *out, hipStream_t s, double *hout)
+{
+   hipLaunchKernelGGL(k_pcg_step, dim3(kDotBlocks), dim3(256), 0, s, n, nom, den, d, z, x, r, dinv, partials);
+   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, s, kDotBlocks, partials, out, hout);
+   ECM2_HIP(hipGetLastError());
+}
+
+void ess_save_zero(int n, const int *idx, double *v, double *saved, hipStream_t s)
+{
+   if (n <= 0) { return; }
+   hipLaunchKernelGGL(k_ess_save_zero, dim3(grid_for(n, 256)), dim3(256), 0, s, n, idx, v, saved);
+   ECM2_HIP(hipGetLastError());
+}
+
+void ess_restore(int n, const int *idx, const double *saved, double *v, double *y, hipStream_t s)
+{
+   if (n <= 0) { return; }
+   hipLaunchKernelGGL(k_ess_restore, dim3(grid_for(n, 256)), dim3(256), 0, s, n, idx, saved, v, y);
+   ECM2_HIP(hipGetLastError());
+}
+
+void pcg_precond(int n, const double *dinv, const double *r, double *z, hipStream_t s)
+{
+   hipLaunchKernelGGL(k_pcg_precond, dim3(grid_for(n, 256)), dim3(256), 0, s, n, dinv, r, z);
+   ECM2_HIP(hipGetLastError());
+}
+
+void pcg_update_d(int n, const double *betanom, const double *nom, const double *z, double *d,
+                  hipStream_t s)
+{
+   hipLaunchKernelGGL(k_pcg_update_d, dim3(grid_for(n, 256)), dim3(256), 0, s, n, betanom, nom, z, d);
+   ECM2_HIP(hipGetLastError());
+}
+
+void scale(int n, double a, double *y, hipStream_t s)
+{
+   if (n <= 0) { return; }
+   hipLaunchKernelGGL(k_scale, dim3(grid_for(n, 256)), dim3(256), 0, s, n, a, y);
+   ECM2_HIP(hipGetLastError());
+}
+
+void add_scaled(int n, const double *x, double c, const double *k, double *out, hipStream_t s)
+{
+   if (n <= 0) { return; }
+   hipLaunchKernelGGL(k_add_scaled, dim3(grid_for(n, 256)), dim3(256), 0, s, n, x, c, k, out);
+   ECM2_HIP(hipGetLastError());
+}
+
+void stream_copy(long n, const double *a, double *b, hipStream_t s)
+{
+   ECM2_VERIFY(n % 2 == 0 && ((uintptr_t)a % 16) == 0 && ((uintptr_t)b % 16) == 0, ERR_ARG,
+               "stream_copy needs 16-byte aligned even-length arrays");
+   hipLaunchKernelGGL(k_stream_copy, dim3(256 * 64), dim3(256), 0, s, n / 2, reinterpret_cast<const v2d *>(a),
+                      reinterpret_cast<v2d *>(b));
+   ECM2_HIP(hipGetLastError());
+}
+
+void reciprocal(int n, const double *a, double *out, hipStream_t s)
+{
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_reciprocal, dim3(grid_for(n, 256)), dim3(256), 0, s, n, a, out);
+   ECM2_HIP(hipGetLastError());
+}
+
+void gather_idx(int n, const int *idx, const double *x, double *buf, hipStream_t s)
+{
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_gather_idx, dim3(grid_for(n, 256)), dim3(256), 0, s, n, idx, x, buf);
+   ECM2_HIP(hipGetLastError());
+}
+
+void scatter_add_idx(int n, const int *idx, const double *buf, double *y, hipStream_t s)
+{
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_scatter_add_idx, dim3(grid_for(n, 256)), dim3(256), 0, s, n, idx, buf, y);
+   ECM2_HIP(hipGetLastError());
+}
+
+void sum_partials(int i0, int i1, const int *dofs, const unsigned *meta, const int *slots, const double *part,
+                  int n_owned, double *y, double *yg, hipStream_t s)
+{
+   if (i1 <= i0) { return; }
+   ECM2_VERIFY(slots, ERR_INTERNAL, "summation pass needs its slot list");
+   hipLaunchKernelGGL(k_sum_partials, dim3(grid_for(i1 - i0, 256)), dim3(256), 0, s, i0, i1, dofs, meta, slots, part,
+                      n_owned, y, yg);
+   ECM2_HIP(hipGetLastError());
+}
+
+} // namespace kern
+} // namespace ecm2

@@ -1,0 +1,519 @@
+// k_setup.hip -- quadrature-data setup and coefficient projection (gfx950).
+//
+// Setup (S1..S3): qdata from element corner coordinates or from MFEM-layout Jacobians
+// (PADiffusionSetup3D bilininteg_diffusion_kernels.cpp:243-367, mass setup
+// bilininteg_mass_pa.cpp:60-78, GeometricFactors mesh.cpp:15220-15273); grid-function
+// coefficients at the quadrature points (GridFunctionCoefficient -> CoefficientVector::Project,
+// coefficient.cpp:2052-2070, qfunction.cpp:73-98) composed with the bioheat temperature laws.
+#include "dev_common.hpp"
+
+namespace ecm2
+{
+namespace
+{
+using namespace dev;
+
+// c(e,q) = law(T(x_q)),  T(x_q) = (B x B x B) T_e  (generic (D, Q) fallback).
+__global__ void k_coeff_gridfunc(int ne, int D, int Q, const int *__restrict__ gmap, const Basis1D b,
+                                 const double *__restrict__ T, int kind, double scale, double slope,
+                                 double t_ref, CoeffParams cp, double *__restrict__ out)
+{
+   const int NQ = Q * Q * Q, ND = D * D * D;
+   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   if (t >= (long)ne * NQ) { return; }
+   const int e = (int)(t / NQ), q = (int)(t % NQ);
+   const int qx = q % Q, qy = (q / Q) % Q, qz = q / (Q * Q);
+   double v = 0.0;
+   for (int dz = 0; dz < D; dz++)
+      for (int dy = 0; dy < D; dy++)
+         for (int dx = 0; dx < D; dx++)
+         {
+            const int g = gmap[(size_t)e * ND + (dz * D + dy) * D + dx];
+            const double tv = g >= 0 ? T[g] : -T[-1 - g];
+            v += b.B[qx + MQ * dx] * b.B[qy + MQ * dy] * b.B[qz + MQ * dz] * tv;
+         }
+   out[t] = coeff_law(kind, v, scale, slope, t_ref, cp.p);
+}
+
+// The same, sum-factorised: one wave per element, lanes (dy,dz) gather a T x-line and contract
+// in x, lanes (qx,dz) in y, lanes (qx,qy) in z; out[e][q] (q = qx + Q(qy + Q qz)).
+template <int D, int Q>
+__global__ void __launch_bounds__(64)
+k_coeff_line(int ne, const int *__restrict__ gmap, const Basis1D *__restrict__ btab, const double *__restrict__ T,
+             int kind, double scale, double slope, double t_ref, CoeffParams cp, double *__restrict__ out)
+{
+   constexpr int ND = D * D * D, NQ = Q * Q * Q, DD = D * D, QQ = Q * Q, DQ = D * Q;
+   __shared__ double s1[DD * Q];
+   __shared__ double s2[D * QQ];
+   const int e = blockIdx.x, t = threadIdx.x;
+   if (e >= ne) { return; }
+   if (t < DD)
+   {
+      CBasis *bp = stage_basis(btab);
+      double tl[D];
+#pragma unroll
+      for (int dx = 0; dx < D; dx++)
+      {
+         const int g = gmap[(size_t)e * ND + t * D + dx];
+         tl[dx] = g >= 0 ? T[g] : -T[-1 - g];
+      }
+#pragma unroll
+      for (int qx = 0; qx < Q; qx++)
+      {
+         double u = 0.0;
+#pragma unroll
+         for (int dx = 0; dx < D; dx++) { u += bp->B[qx + MQ * dx] * tl[dx]; }
+         s1[t * Q + qx] = u;
+      }
+   }
+   __syncthreads();
+   if (t < DQ)
+   {
+      CBasis *bp = stage_basis(btab);
+      const int qx = t % Q, dz = t / Q;
+      double l[D];
+#pragma unroll
+      for (int dy = 0; dy < D; dy++) { l[dy] = s1[(dz * D + dy) * Q + qx]; }
+#pragma unroll
+      for (int qy = 0; qy < Q; qy++)
+      {
+         double u = 0.0;
+#pragma unroll
+         for (int dy = 0; dy < D; dy++) { u += bp->B[qy + MQ * dy] * l[dy]; }
+         s2[(dz * Q + qy) * Q + qx] = u;
+      }
+   }
+   __syncthreads();
+   if (t < QQ)
+   {
+      CBasis *bp = stage_basis(btab);
+      double l[D];
+#pragma unroll
+      for (int dz = 0; dz < D; dz++) { l[dz] = s2[dz * QQ + t]; }
+#pragma unroll
+      for (int qz = 0; qz < Q; qz++)
+      {
+         double v = 0.0;
+#pragma unroll
+         for (int dz = 0; dz < D; dz++) { v += bp->B[qz + MQ * dz] * l[dz]; }
+         out[(size_t)e * NQ + qz * QQ + t] = coeff_law(kind, v, scale, slope, t_ref, cp.p);
+      }
+   }
+}
+
+struct SetupCoef
+{
+   int has;          // integrator present
+   int is_const;
+   double value;
+   const double *quad;
+};
+
+__device__ __forceinline__ double coef_at(const SetupCoef &c, size_t eq)
+{
+   return c.is_const ? c.value : c.quad[eq];
+}
+
+// Write D (6 symmetric entries) and mass value at one quadrature point (any layout).
+__device__ __forceinline__ void write_qdata(const int *pos, int kind, int nq, int e, int q, double w,
+                                            const double J[3][3], const SetupCoef &cm,
+                                            const SetupCoef &cd, double *qd_diff,
+                                            double *qd_mass)
+{
+   const double J11 = J[0][0], J21 = J[1][0], J31 = J[2][0];
+   const double J12 = J[0][1], J22 = J[1][1], J32 = J[2][1];
+   const double J13 = J[0][2], J23 = J[1][2], J33 = J[2][2];
+   const double detJ = J11 * (J22 * J33 - J32 * J23) - J21 * (J12 * J33 - J32 * J13) +
+                       J31 * (J12 * J23 - J22 * J13);
+   const size_t eq = (size_t)e * nq + q;
+   if (cd.has)
+   {
+      const double w_detJ = w / detJ;
+      const double A11 = (J22 * J33) - (J23 * J32);
+      const double A12 = (J32 * J13) - (J12 * J33);
+      const double A13 = (J12 * J23) - (J22 * J13);
+      const double A21 = (J31 * J23) - (J21 * J33);
+      const double A22 = (J11 * J33) - (J13 * J31);
+      const double A23 = (J21 * J13) - (J11 * J23);
+      const double A31 = (J21 * J32) - (J31 * J22);
+      const double A32 = (J31 * J12) - (J11 * J32);
+      const double A33 = (J11 * J22) - (J12 * J21);
+      const double C = coef_at(cd, eq);
+      qd_diff[qidx_diff(pos, kind, nq, e, 0, q)] = w_detJ * (C * A11 * A11 + C * A12 * A12 + C * A13 * A13);
+      qd_diff[qidx_diff(pos, kind, nq, e, 1, q)] = w_detJ * (C * A11 * A21 + C * A12 * A22 + C * A13 * A23);
+      qd_diff[qidx_diff(pos, kind, nq, e, 2, q)] = w_detJ * (C * A11 * A31 + C * A12 * A32 + C * A13 * A33);
+      qd_diff[qidx_diff(pos, kind, nq, e, 3, q)] = w_detJ * (C * A21 * A21 + C * A22 * A22 + C * A23 * A23);
+      qd_diff[qidx_diff(pos, kind, nq, e, 4, q)] = w_detJ * (C * A21 * A31 + C * A22 * A32 + C * A23 * A33);
+      qd_diff[qidx_diff(pos, kind, nq, e, 5, q)] = w_detJ * (C * A31 * A31 + C * A32 * A32 + C * A33 * A33);
+   }
+   if (cm.has)
+   {
+      qd_mass[qidx_mass(pos, kind, nq, e, q)] = w * coef_at(cm, eq) * detJ;
+   }
+}
+
+// qdata from trilinear corners, templated on Q.  BLOCKED: threads run over (blk, q, lane)
+// with the lane fastest, so for each quadrature point a wave writes 64 consecutive
+// elements' entries (1 KiB per diffusion pair), the layout the apply kernel streams;
+// perm maps the internal position to the caller element (geometry and coefficients are
+// in caller order).  NATIVE: threads run over (e, q), q fastest.
+template <int Q, bool BLOCKED>
+__global__ void __launch_bounds__(256)
+k_setup_nodes_t(const int *__restrict__ perm, int ne, const double *__restrict__ enodes,
+                const double *__restrict__ W, const Basis1D b1, SetupCoef cm, SetupCoef cd,
+                double *__restrict__ qd_diff, double *__restrict__ qd_mass)
+{
+   constexpr int NQ = Q * Q * Q;
+   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   int e, q, lane = 0;
+   long blk = 0;
+   if (BLOCKED)
+   {
+      lane = (int)(t & 63);
+      const long rest = t >> 6;
+      q = (int)(rest % NQ);
+      blk = rest / NQ;
+      const int ipos = (int)(blk * 64 + lane);
+      if (ipos >= ne) { return; }
+      e = perm ? perm[ipos] : ipos;
+   }
+   else
+   {
+      if (t >= (long)ne * NQ) { return; }
+      e = (int)(t / NQ);
+      q = (int)(t % NQ);
+   }
+   const int qx = q % Q, qy = (q / Q) % Q, qz = q / (Q * Q);
+   const double *X = enodes + (size_t)e * 24;
+   double J[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+#pragma unroll
+   for (int a = 0; a < 8; a++)
+   {
+      const int ax = a & 1, ay = (a >> 1) & 1, az = a >> 2;
+      const double bx = b1.B[qx + MQ * ax], by = b1.B[qy + MQ * ay], bz = b1.B[qz + MQ * az];
+      const double gx = b1.G[qx + MQ * ax], gy = b1.G[qy + MQ * ay], gz = b1.G[qz + MQ * az];
+      const double dN0 = gx * by * bz, dN1 = bx * gy * bz, dN2 = bx * by * gz;
+#pragma unroll
+      for (int i = 0; i < 3; i++)
+      {
+         const double xi = X[i * 8 + a];
+         J[i][0] += xi * dN0;
+         J[i][1] += xi * dN1;
+         J[i][2] += xi * dN2;
+      }
+   }
+   if (!BLOCKED)
+   {
+      write_qdata(nullptr, QLAYOUT_NATIVE, NQ, e, q, W[q], J, cm, cd, qd_diff, qd_mass);
+      return;
+   }
+   // same arithmetic as write_qdata (PADiffusionSetup3D / mass setup), blocked stores
+   const double J11 = J[0][0], J21 = J[1][0], J31 = J[2][0];
+   const double J12 = J[0][1], J22 = J[1][1], J32 = J[2][1];
+   const double J13 = J[0][2], J23 = J[1][2], J33 = J[2][2];
+   const double detJ = J11 * (J22 * J33 - J32 * J23) - J21 * (J12 * J33 - J32 * J13) +
+                       J31 * (J12 * J23 - J22 * J13);
+   const size_t eq = (size_t)e * NQ + q;
+   const double w = W[q];
+   if (cd.has)
+   {
+      const double w_detJ = w / detJ;
+      const double A11 = (J22 * J33) - (J23 * J32);
+      const double A12 = (J32 * J13) - (J12 * J33);
+      const double A13 = (J12 * J23) - (J22 * J13);
+      const double A21 = (J31 * J23) - (J21 * J33);
+      const double A22 = (J11 * J33) - (J13 * J31);
+      const double A23 = (J21 * J13) - (J11 * J23);
+      const double A31 = (J21 * J32) - (J31 * J22);
+      const double A32 = (J31 * J12) - (J11 * J32);
+      const double A33 = (J11 * J22) - (J12 * J21);
+      const double C = coef_at(cd, eq);
+      v2d p0, p1, p2;
+      p0.x = w_detJ * (C * A11 * A11 + C * A12 * A12 + C * A13 * A13);
+      p0.y = w_detJ * (C * A11 * A21 + C * A12 * A22 + C * A13 * A23);
+      p1.x = w_detJ * (C * A11 * A31 + C * A12 * A32 + C * A13 * A33);
+      p1.y = w_detJ * (C * A21 * A21 + C * A22 * A22 + C * A23 * A23);
+      p2.x = w_detJ * (C * A21 * A31 + C * A22 * A32 + C * A23 * A33);
+      p2.y = w_detJ * (C * A31 * A31 + C * A32 * A32 + C * A33 * A33);
+      v2d *dst = reinterpret_cast<v2d *>(qd_diff + ((size_t)blk * NQ + q) * 3 * 128) + lane;
+      dst[0] = p0;
+      dst[64] = p1;
+      dst[128] = p2;
+   }
+   if (cm.has)
+   {
+      qd_mass[((size_t)blk * ((NQ + 1) / 2) + (q >> 1)) * 128 + lane * 2 + (q & 1)] = w * coef_at(cm, eq) * detJ;
+   }
+}
+
+// Affinity of MFEM-layout Jacobians: flag[0] = 1 when some point's J differs from its
+// element's first point's by more than 1e-13 of that J's largest entry.
+__global__ void k_jac_affine_check(int ne, int NQ, const double *__restrict__ Jg, int *__restrict__ flag)
+{
+   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   if (t >= (long)ne * NQ) { return; }
+   const int e = (int)(t / NQ), q = (int)(t % NQ);
+   double mx = 0.0, dv = 0.0;
+   for (int c = 0; c < 9; c++)
+   {
+      const double j0 = Jg[((size_t)e * 9 + c) * NQ], jq = Jg[((size_t)e * 9 + c) * NQ + q];
+      mx = fmax(mx, fabs(j0));
+      dv = fmax(dv, fabs(jq - j0));
+   }
+   if (!(dv <= 1e-13 * mx)) { flag[0] = 1; }
+}
+
+__global__ void k_setup_jac(const int *__restrict__ pos, int kind, int ne, int NQ, const double *__restrict__ Jg,
+                            const double *__restrict__ W, SetupCoef cm, SetupCoef cd,
+                            double *__restrict__ qd_diff, double *__restrict__ qd_mass)
+{
+   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   if (t >= (long)ne * NQ) { return; }
+   const int e = (int)(t / NQ), q = (int)(t % NQ);
+   double J[3][3];
+   for (int j = 0; j < 3; j++)
+      for (int i = 0; i < 3; i++) { J[i][j] = Jg[(((size_t)e * 3 + j) * 3 + i) * NQ + q]; }
+   write_qdata(pos, kind, NQ, e, q, W[q], J, cm, cd, qd_diff, qd_mass);
+}
+
+// AFFINE layout from the corners of parallelepiped elements (kernels.hpp).  J is the
+// reference-cube edge matrix [x_100 - x_000 | x_010 - x_000 | x_001 - x_000] (the trilinear
+// Jacobian of GeometricFactors, mesh.cpp:15220-15273, when the element is affine); the
+// products are PADiffusionSetup3D's (bilininteg_diffusion_kernels.cpp:349-362) and the mass
+// setup's (bilininteg_mass_pa.cpp:76) with the per-point factors W_q beta_q / W_q alpha_q kept
+// apart from the element's C = adj(J) adj(J)^T / det J.  Threads over (blk, q, lane), lane
+// fastest: each wave stores 1 KiB of pairs per point; the q = 0 threads store C.
+// Jg (optional): MFEM-layout Jacobians J(q,i,j,e) instead of corners; the element's J is
+// its first point's (all points agree for an affine element: checked by k_jac_affine_check).
+template <int Q, bool BLOCKED>
+__global__ void __launch_bounds__(256)
+k_setup_affine(const int *__restrict__ perm, int ne, const double *__restrict__ enodes,
+               const double *__restrict__ Jg,
+               const double *__restrict__ W, SetupCoef cm, SetupCoef cd, double *__restrict__ qd_fac,
+               double *__restrict__ qd_pair)
+{
+   constexpr int NQ = Q * Q * Q;
+   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   int lane, q, e;
+   long blk;
+   if (BLOCKED)
+   {
+      lane = (int)(t & 63);
+      const long rest = t >> 6;
+      q = (int)(rest % NQ);
+      blk = rest / NQ;
+      const int ipos = (int)(blk * 64 + lane);
+      if (ipos >= ne) { return; }
+      e = perm ? perm[ipos] : ipos;
+   }
+   else
+   {
+      // AFFINE_E: threads over (e, q), q fastest
+      if (t >= (long)ne * NQ) { return; }
+      e = (int)(t / NQ);
+      q = (int)(t % NQ);
+      lane = 0;
+      blk = 0;
+   }
+   double J[3][3];
+   if (Jg)
+   {
+#pragma unroll
+      for (int j = 0; j < 3; j++)
+#pragma unroll
+         for (int i = 0; i < 3; i++) { J[i][j] = Jg[(((size_t)e * 3 + j) * 3 + i) * NQ]; }
+   }
+   else
+   {
+      const double *X = enodes + (size_t)e * 24;
+#pragma unroll
+      for (int i = 0; i < 3; i++)
+      {
+         J[i][0] = X[i * 8 + 1] - X[i * 8];
+         J[i][1] = X[i * 8 + 2] - X[i * 8];
+         J[i][2] = X[i * 8 + 4] - X[i * 8];
+      }
+   }
+   const double J11 = J[0][0], J21 = J[1][0], J31 = J[2][0];
+   const double J12 = J[0][1], J22 = J[1][1], J32 = J[2][1];
+   const double J13 = J[0][2], J23 = J[1][2], J33 = J[2][2];
+   const double detJ = J11 * (J22 * J33 - J32 * J23) - J21 * (J12 * J33 - J32 * J13) +
+                       J31 * (J12 * J23 - J22 * J13);
+   const size_t eq = (size_t)e * NQ + q;
+   const double w = W[q];
+   v2d pr;
+   pr.x = w * coef_at(cd, eq);
+   pr.y = w * coef_at(cm, eq) * detJ;
+   if (BLOCKED) { reinterpret_cast<v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane] = pr; }
+   else { reinterpret_cast<v2d *>(qd_pair)[(size_t)e * NQ + q] = pr; }
+   if (q == 0)
+   {
+      const double A11 = (J22 * J33) - (J23 * J32);
+      const double A12 = (J32 * J13) - (J12 * J33);
+      const double A13 = (J12 * J23) - (J22 * J13);
+      const double A21 = (J31 * J23) - (J21 * J33);
+      const double A22 = (J11 * J33) - (J13 * J31);
+      const double A23 = (J21 * J13) - (J11 * J23);
+      const double A31 = (J21 * J32) - (J31 * J22);
+      const double A32 = (J31 * J12) - (J11 * J32);
+      const double A33 = (J11 * J22) - (J12 * J21);
+      const double r = 1.0 / detJ;
+      v2d p0, p1, p2;
+      p0.x = r * (A11 * A11 + A12 * A12 + A13 * A13);
+      p0.y = r * (A11 * A21 + A12 * A22 + A13 * A23);
+      p1.x = r * (A11 * A31 + A12 * A32 + A13 * A33);
+      p1.y = r * (A21 * A21 + A22 * A22 + A23 * A23);
+      p2.x = r * (A21 * A31 + A22 * A32 + A23 * A33);
+      p2.y = r * (A31 * A31 + A32 * A32 + A33 * A33);
+      if (BLOCKED)
+      {
+         v2d *dst = reinterpret_cast<v2d *>(qd_fac + (size_t)blk * 3 * 128) + lane;
+         dst[0] = p0;
+         dst[64] = p1;
+         dst[128] = p2;
+      }
+      else
+      {
+         double *dst = qd_fac + (size_t)e * 6;  // (11, 12, 13, 22, 23, 33)
+         dst[0] = p0.x; dst[1] = p0.y; dst[2] = p1.x; dst[3] = p1.y; dst[4] = p2.x; dst[5] = p2.y;
+      }
+   }
+}
+
+SetupCoef make_setup_coef(const CoeffDesc *c, const double *q)
+{
+   SetupCoef s{};
+   if (!c) { return s; }
+   s.has = 1;
+   s.is_const = (c->kind == COEFF_CONSTANT);
+   s.value = c->value;
+   s.quad = q;
+   return s;
+}
+
+} // namespace
+
+namespace kern
+{
+
+void coeff_gridfunc(int ne, int D, int Q, const int *gmap, const Basis1D &b, const Basis1D *btab, const CoeffDesc &c,
+                    double *out, hipStream_t s)
+{
+   const long n = (long)ne * Q * Q * Q;
+   if (n == 0) { return; }
+   CoeffParams cp;
+   for (int i = 0; i < 6; i++) { cp.p[i] = c.p[i]; }
+#define ECM2_COEFF_CASE(DD, QQ)                                                                         \
+   if (D == DD && Q == QQ)                                                                              \
+   {                                                                                                    \
+      hipLaunchKernelGGL((k_coeff_line<DD, QQ>), dim3(ne), dim3(64), 0, s, ne, gmap, btab, c.lvec, c.kind, \
+                         c.scale, c.slope, c.t_ref, cp, out);                                          \
+      ECM2_HIP(hipGetLastError());                                                                      \
+      return;                                                                                           \
+   }
+   if (btab)
+   {
+      ECM2_COEFF_CASE(2, 3) ECM2_COEFF_CASE(3, 4) ECM2_COEFF_CASE(4, 5) ECM2_COEFF_CASE(5, 6)
+      ECM2_COEFF_CASE(6, 7) ECM2_COEFF_CASE(7, 8) ECM2_COEFF_CASE(2, 2) ECM2_COEFF_CASE(3, 3)
+      ECM2_COEFF_CASE(4, 4) ECM2_COEFF_CASE(5, 5)
+   }
+#undef ECM2_COEFF_CASE
+   hipLaunchKernelGGL(k_coeff_gridfunc, dim3(grid_for(n, 256)), dim3(256), 0, s, ne, D, Q, gmap, b, c.lvec, c.kind,
+                      c.scale, c.slope, c.t_ref, cp, out);
+   ECM2_HIP(hipGetLastError());
+}
+
+void setup_from_nodes(const QLayout &L, int Q, const double *enodes, const double *W,
+                      const Basis1D &b1, const CoeffDesc *cm, const CoeffDesc *cd,
+                      const double *cm_q, const double *cd_q, double *qd_diff,
+                      double *qd_mass, hipStream_t s)
+{
+   const long n = (long)L.ne * L.nq;
+   if (n == 0) { return; }
+   const SetupCoef scm = make_setup_coef(cm, cm_q), scd = make_setup_coef(cd, cd_q);
+   const bool blocked = L.kind == QLAYOUT_BLOCKED;
+   ECM2_VERIFY(!blocked || !L.pos || L.perm, ERR_INTERNAL, "blocked setup needs the inverse permutation");
+   const long nb = blocked ? (long)L.nblk() * 64 * L.nq : n;
+#define ECM2_SETUP_CASE(QQ)                                                                              \
+   if (Q == QQ)                                                                                          \
+   {                                                                                                     \
+      if (blocked)                                                                                       \
+      {                                                                                                  \
+         hipLaunchKernelGGL((k_setup_nodes_t<QQ, true>), dim3(grid_for(nb, 256)), dim3(256), 0, s, L.perm, L.ne, \
+                            enodes, W, b1, scm, scd, qd_diff, qd_mass);                                  \
+      }                                                                                                  \
+      else                                                                                               \
+      {                                                                                                  \
+         hipLaunchKernelGGL((k_setup_nodes_t<QQ, false>), dim3(grid_for(nb, 256)), dim3(256), 0, s, nullptr, L.ne, \
+                            enodes, W, b1, scm, scd, qd_diff, qd_mass);                                  \
+      }                                                                                                  \
+      ECM2_HIP(hipGetLastError());                                                                       \
+      return;                                                                                            \
+   }
+   ECM2_SETUP_CASE(2) ECM2_SETUP_CASE(3) ECM2_SETUP_CASE(4) ECM2_SETUP_CASE(5)
+   ECM2_SETUP_CASE(6) ECM2_SETUP_CASE(7) ECM2_SETUP_CASE(8)
+#undef ECM2_SETUP_CASE
+   ECM2_VERIFY(false, ERR_UNSUPPORTED, "setup: Q1D " << Q << " not instantiated");
+}
+
+bool jacobians_affine(int ne, int nq, const double *J, hipStream_t s)
+{
+   if (ne == 0) { return true; }
+   DeviceArray<int> flag;
+   flag.resize(1);
+   ECM2_HIP(hipMemsetAsync(flag.data(), 0, sizeof(int), s));
+   const long n = (long)ne * nq;
+   hipLaunchKernelGGL(k_jac_affine_check, dim3(grid_for(n, 256)), dim3(256), 0, s, ne, nq, J, flag.data());
+   ECM2_HIP(hipGetLastError());
+   int h = 1;
+   ECM2_HIP(hipMemcpyAsync(&h, flag.data(), sizeof(int), hipMemcpyDeviceToHost, s));
+   ECM2_HIP(hipStreamSynchronize(s));
+   return h == 0;
+}
+
+void setup_affine(const QLayout &L, int Q, const double *enodes, const double *J, const double *W,
+                  const CoeffDesc *cm, const CoeffDesc *cd, const double *cm_q, const double *cd_q,
+                  double *qd_fac, double *qd_pair, hipStream_t s)
+{
+   if (L.ne == 0) { return; }
+   ECM2_VERIFY(L.affine() && cm && cd, ERR_INTERNAL, "affine setup needs an AFFINE layout and both coefficients");
+   ECM2_VERIFY(!L.pos || L.perm, ERR_INTERNAL, "blocked setup needs the inverse permutation");
+   const SetupCoef scm = make_setup_coef(cm, cm_q), scd = make_setup_coef(cd, cd_q);
+   const bool blk = L.kind == QLAYOUT_AFFINE;
+   const long n = blk ? (long)L.nblk() * 64 * L.nq : (long)L.ne * L.nq;
+#define ECM2_AFF_CASE(QQ)                                                                               \
+   if (Q == QQ)                                                                                          \
+   {                                                                                                     \
+      if (blk)                                                                                           \
+      {                                                                                                  \
+         hipLaunchKernelGGL((k_setup_affine<QQ, true>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.perm, L.ne, \
+                            enodes, J, W, scm, scd, qd_fac, qd_pair);                                    \
+      }                                                                                                  \
+      else                                                                                               \
+      {                                                                                                  \
+         hipLaunchKernelGGL((k_setup_affine<QQ, false>), dim3(grid_for(n, 256)), dim3(256), 0, s, nullptr, L.ne, \
+                            enodes, J, W, scm, scd, qd_fac, qd_pair);                                    \
+      }                                                                                                  \
+      ECM2_HIP(hipGetLastError());                                                                       \
+      return;                                                                                            \
+   }
+   ECM2_AFF_CASE(2) ECM2_AFF_CASE(3) ECM2_AFF_CASE(4) ECM2_AFF_CASE(5) ECM2_AFF_CASE(6) ECM2_AFF_CASE(7)
+   ECM2_AFF_CASE(8)
+#undef ECM2_AFF_CASE
+   ECM2_VERIFY(false, ERR_UNSUPPORTED, "affine setup: Q1D " << Q << " not instantiated");
+}
+
+void setup_from_jacobians(const QLayout &L, const double *J, const double *W,
+                          const CoeffDesc *cm, const CoeffDesc *cd, const double *cm_q,
+                          const double *cd_q, double *qd_diff, double *qd_mass, hipStream_t s)
+{
+   const long n = (long)L.ne * L.nq;
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_setup_jac, dim3(grid_for(n, 256)), dim3(256), 0, s, L.pos, L.kind, L.ne, L.nq,
+                      J, W, make_setup_coef(cm, cm_q), make_setup_coef(cd, cd_q), qd_diff,
+                      qd_mass);
+   ECM2_HIP(hipGetLastError());
+}
+
+} // namespace kern
+} // namespace ecm2

@@ -1,0 +1,835 @@
+// k_tpe.hip -- fused thread-per-element apply and diagonal for p = 1, 2 (gfx950).
+//
+// One THREAD per element, 64 elements (one 4x4x4 brick) per wave, 4 waves per workgroup.
+// Each kernel replaces, in one pass over HBM, ElementRestriction::Mult (restriction.cpp:
+// 109-129), the mass and diffusion AddMultPA kernels (bilininteg_mass_kernels.hpp:809-1033,
+// bilininteg_diffusion_kernels.hpp:989-1214) and ElementRestriction::MultTranspose
+// (restriction.cpp:152-186): gather x into LDS, sum-factorised B/G contractions in
+// registers with the qdata streamed once by 1 KiB-per-wave-instruction nontemporal loads,
+// then the brick's shared faces assembled in-wave (shuffles) and across the workgroup's
+// waves (LDS), and a deterministic store (dofs held once: plain store; shared dofs: dense
+// partial slots summed by k_sum_partials in a fixed order).
+#include "dev_common.hpp"
+
+namespace ecm2
+{
+namespace
+{
+using namespace dev;
+
+// Rows per wave of the LDS region the cross-wave face exchange uses (3 faces of D x D).
+template <int D>
+struct XwaveRows
+{
+   static constexpr int ND = D * D * D, R = ND > 3 * D * D ? ND : 3 * D * D;
+};
+
+// In-wave assembly of a thread-per-element block's outputs and their store (apply and
+// diagonal kernels).  A 4x4x4 brick is one wave: x, y, z neighbours are lanes +1, +4, +16;
+// setup-computed lane flags say which faces really coincide (dof-index equality), so any
+// element order is correct; bricks make it effective.  SIGNS: apply the map's orientation
+// signs before summation (y = A x; the diagonal's signs square away).  Then entries whose
+// face was sent away hold nothing; a dof held once in the whole mesh is plain-stored; a
+// shared one goes to its dense partial slot [blk][a][lane] (summed in a fixed order by
+// k_sum_partials: deterministic, no atomics, no y memset) or, without a partial buffer, is
+// atomically added.
+// XW: after each direction's in-wave merge, faces shared with another wave of the workgroup
+// (lane flags 64|128|256 + the sending wave in bits 9-17, see build_merge_plan) move through
+// LDS: the sending lanes (low face, e_dir = 0) park their face in their own wave's region
+// xb[w][XR][64] (the kernel's x staging area, no longer read), a barrier, the receiving lanes
+// (high face, e_dir = 3) add it.  Every wave of the workgroup must call this (wave_on false:
+// barriers only).
+template <int D, bool SPLIT, bool SIGNS, bool XW>
+__device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], const int *__restrict__ mp, int fl,
+                                                   int blk, int lane, bool active, int n_owned,
+                                                   double *__restrict__ y, double *__restrict__ yg,
+                                                   double *__restrict__ part, double *xb, int w, bool wave_on)
+{
+   constexpr int ND = D * D * D, XR = XwaveRows<D>::R;
+   if (SIGNS && wave_on)
+   {
+#pragma unroll
+      for (int a = 0; a < ND; a++)
+      {
+         if (bneg(mp[a * 64])) { Yo[a] = -Yo[a]; }
+      }
+   }
+   auto merge = [&](int dir, int delta, int recv_bit, int sent_bit, auto face) {
+      if (XW && wave_on && ((lane / delta) & 3) == 0 && (fl & sent_bit))
+      {
+#pragma unroll
+         for (int j = 0; j < D; j++)
+#pragma unroll
+            for (int i = 0; i < D; i++) { xb[((w * XR) + dir * D * D + j * D + i) * 64 + lane] = Yo[face(0, i, j)]; }
+      }
+      if (wave_on)
+      {
+#pragma unroll
+         for (int j = 0; j < D; j++)
+#pragma unroll
+            for (int i = 0; i < D; i++)
+            {
+               const double v = __shfl_down(Yo[face(0, i, j)], delta, 64);
+               if (fl & recv_bit) { Yo[face(D - 1, i, j)] += v; }
+               if (fl & sent_bit) { Yo[face(0, i, j)] = 0.0; }
+            }
+      }
+      if (XW)
+      {
+         __syncthreads();
+         if (wave_on && (fl & (64 << dir)))
+         {
+            const int pw = (fl >> (9 + 3 * dir)) & 7;
+#pragma unroll
+            for (int j = 0; j < D; j++)
+#pragma unroll
+               for (int i = 0; i < D; i++)
+               {
+                  Yo[face(D - 1, i, j)] += xb[((pw * XR) + dir * D * D + j * D + i) * 64 + lane - 3 * delta];
+               }
+         }
+      }
+   };
+   merge(0, 1, 1, 2, [](int s, int i, int j) { return (j * D + i) * D + s; });    // x: (dz=j, dy=i)
+   merge(1, 4, 4, 8, [](int s, int i, int j) { return (j * D + s) * D + i; });    // y: (dz=j, dx=i)
+   merge(2, 16, 16, 32, [](int s, int i, int j) { return (s * D + j) * D + i; }); // z: (dy=j, dx=i)
+   if (!active || !wave_on) { return; }
+   const bool sx = fl & 2, sy = fl & 8, sz = fl & 32;
+#pragma unroll
+   for (int dz = 0; dz < D; dz++)
+#pragma unroll
+      for (int dy = 0; dy < D; dy++)
+#pragma unroll
+         for (int dx = 0; dx < D; dx++)
+         {
+            if ((dx == 0 && sx) || (dy == 0 && sy) || (dz == 0 && sz)) { continue; }
+            const int a = (dz * D + dy) * D + dx;
+            const int g = mp[a * 64];
+            const int d = bdof(g);
+            double *dst = (!SPLIT || d < n_owned) ? y + d : yg + (d - n_owned);
+            if (!bshared(g)) { *dst = Yo[a]; }
+            else if (part) { part[((size_t)blk * ND + a) * 64 + lane] = Yo[a]; }
+            else { unsafeAtomicAdd(dst, Yo[a]); }
+         }
+}
+
+// Full per-point qdata (BLOCKED layout), per quadrature row (qy, qz): the 27 gathered dofs
+// live in LDS (a private [a][lane] slot per wave: conflict-free ds_read_b64), which frees the
+// VGPRs to hold the NEXT row's qdata in flight while the current row is computed (double
+// buffering).  Per row: x-values contracted with precomputed B_y B_z, G_y B_z, B_y G_z
+// products (scalar loads of the row table), x-forward, weighting by the row's 56-byte points,
+// x-transpose, yz-transpose into the element outputs.
+template <int D, int Q, bool MASS, bool DIFF, bool SPLIT>
+__global__ void __launch_bounds__(256, 1)
+k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
+               const double *__restrict__ qdd, const double *__restrict__ qdm,
+               const double *__restrict__ x, const double *__restrict__ xg,
+               double *__restrict__ y, double *__restrict__ yg, const Basis1D b,
+               const double *__restrict__ rowtab, const int *__restrict__ lane_flags,
+               double *__restrict__ part)
+{
+   constexpr int ND = D * D * D, NQ = Q * Q * Q, NQH = (NQ + 1) / 2, DD = D * D;
+   constexpr int NR = Q * Q;  // rows
+   __shared__ double sX[4][ND][64];
+   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+   const int blk = blk_begin + (int)blockIdx.x * 4 + w;
+   if (blk >= blk_end) { return; }  // wave-uniform; no block-wide barrier below
+   const int e = blk * 64 + lane;
+   const bool active = e < ne;
+   const int *mp = gmap + (size_t)blk * ND * 64 + lane;
+#pragma unroll
+   for (int a = 0; a < ND; a++)
+   {
+      const int g = mp[a * 64];
+      const int d = bdof(g);
+      const double v = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
+      sX[w][a][lane] = bneg(g) ? -v : v;
+   }
+   double Yo[ND];
+#pragma unroll
+   for (int a = 0; a < ND; a++) { Yo[a] = 0.0; }
+
+   const double *qd = qdd + (size_t)blk * NQ * 3 * 128 + lane * 2;
+   const double *qm = qdm + (size_t)blk * NQH * 128 + lane * 2;
+   auto ld2 = [&](const double *p) -> v2d { return __builtin_nontemporal_load(reinterpret_cast<const v2d *>(p)); };
+   // row buffers: diffusion pairs (3 per point) and mass values (Q per row)
+   v2d cd[Q][3], nd_[Q][3];
+   double cm[Q], nm[Q];
+   auto load_row = [&](int row, v2d (&dq)[Q][3], double (&mq)[Q]) {
+#pragma unroll
+      for (int qx = 0; qx < Q; qx++)
+      {
+         const int q = row * Q + qx;
+         if (DIFF)
+         {
+#pragma unroll
+            for (int k = 0; k < 3; k++) { dq[qx][k] = ld2(qd + ((size_t)q * 3 + k) * 128); }
+         }
+         if (MASS) { mq[qx] = qm[(size_t)(q >> 1) * 128 + (q & 1)]; }
+      }
+   };
+   load_row(0, cd, cm);
+
+#pragma unroll 1
+   for (int row = 0; row < NR; row++)
+   {
+      if (row + 1 < NR) { load_row(row + 1, nd_, nm); }
+      const double *P = rowtab + (size_t)row * 3 * DD;
+      double Y00[D], Y01[D], Y10[D];
+#pragma unroll
+      for (int dx = 0; dx < D; dx++)
+      {
+         double u = 0.0, v = 0.0, wv = 0.0;
+#pragma unroll
+         for (int dz = 0; dz < D; dz++)
+#pragma unroll
+            for (int dy = 0; dy < D; dy++)
+            {
+               const double c = sX[w][(dz * D + dy) * D + dx][lane];
+               u += P[0 * DD + dz * D + dy] * c;
+               if (DIFF)
+               {
+                  v += P[1 * DD + dz * D + dy] * c;
+                  wv += P[2 * DD + dz * D + dy] * c;
+               }
+            }
+         Y00[dx] = u; Y01[dx] = v; Y10[dx] = wv;
+      }
+      double T0[D], T1[D], T2[D];
+#pragma unroll
+      for (int dx = 0; dx < D; dx++) { T0[dx] = 0.0; T1[dx] = 0.0; T2[dx] = 0.0; }
+#pragma unroll
+      for (int qx = 0; qx < Q; qx++)
+      {
+         double u = 0.0, ux = 0.0, uy = 0.0, uz = 0.0;
+#pragma unroll
+         for (int dx = 0; dx < D; dx++)
+         {
+            const double bq = b.B[qx + MQ * dx], gq = b.G[qx + MQ * dx];
+            if (MASS) { u += bq * Y00[dx]; }
+            if (DIFF)
+            {
+               ux += gq * Y00[dx];
+               uy += bq * Y01[dx];
+               uz += bq * Y10[dx];
+            }
+         }
+         double m = 0.0, fx = 0.0, fy = 0.0, fz = 0.0;
+         if (MASS) { m = cm[qx] * u; }
+         if (DIFF)
+         {
+            // (11,12) (13,22) (23,33)
+            const v2d d0 = cd[qx][0], d1 = cd[qx][1], d2 = cd[qx][2];
+            fx = d0.x * ux + d0.y * uy + d1.x * uz;
+            fy = d0.y * ux + d1.y * uy + d2.x * uz;
+            fz = d1.x * ux + d2.x * uy + d2.y * uz;
+         }
+#pragma unroll
+         for (int dx = 0; dx < D; dx++)
+         {
+            const double bq = b.B[qx + MQ * dx], gq = b.G[qx + MQ * dx];
+            double t0 = T0[dx];
+            if (MASS) { t0 += bq * m; }
+            if (DIFF)
+            {
+               t0 += gq * fx;
+               T1[dx] += bq * fy;
+               T2[dx] += bq * fz;
+            }
+            T0[dx] = t0;
+         }
+      }
+#pragma unroll
+      for (int dz = 0; dz < D; dz++)
+#pragma unroll
+         for (int dy = 0; dy < D; dy++)
+         {
+            const double p0 = P[0 * DD + dz * D + dy];
+            const double p1 = P[1 * DD + dz * D + dy];
+            const double p2 = P[2 * DD + dz * D + dy];
+#pragma unroll
+            for (int dx = 0; dx < D; dx++)
+            {
+               double yo = Yo[(dz * D + dy) * D + dx] + p0 * T0[dx];
+               if (DIFF) { yo += p1 * T1[dx] + p2 * T2[dx]; }
+               Yo[(dz * D + dy) * D + dx] = yo;
+            }
+         }
+#pragma unroll
+      for (int qx = 0; qx < Q; qx++)
+      {
+#pragma unroll
+         for (int k = 0; k < 3; k++) { cd[qx][k] = nd_[qx][k]; }
+         cm[qx] = nm[qx];
+      }
+   }
+   tpe_assemble_store<D, SPLIT, true, false>(Yo, mp, lane_flags[(size_t)blk * 64 + lane], blk, lane, active,
+                                             n_owned, y, yg, part, nullptr, w, true);
+}
+
+// Thread-per-element apply on AFFINE qdata, sum-factorised per quadrature plane qz: the
+// x-values (LDS) are contracted in z once per plane (ZB = B_z X, ZG = G_z X, D^2 each), each of
+// the plane's Q rows contracts them in y (3 D^2 multiply-adds instead of the row kernel's
+// 3 D^3 on precomputed B_y B_z products), then x / weighting (element matrix C in registers,
+// one 16-byte (W beta, W alpha det J) pair per point) / x-transpose; the row's y-transpose
+// accumulates into the plane sums SB, SG (2 D^2 + D^2) and the plane ends with one z-transpose
+// into the element outputs (2 D^3).  At p = 2 that is 229 FP64 multiply-adds per row.  The
+// next row's pairs are in flight while a row computes; in-wave and cross-wave face assembly,
+// deterministic store.
+template <int D, int Q, bool SPLIT>
+__global__ void __launch_bounds__(256, 1)
+k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
+               const double *__restrict__ qdd, const double *__restrict__ qdm,
+               const double *__restrict__ x, const double *__restrict__ xg,
+               double *__restrict__ y, double *__restrict__ yg, const Basis1D b,
+               const int *__restrict__ lane_flags, double *__restrict__ part)
+{
+   constexpr int ND = D * D * D, NQ = Q * Q * Q, NR = Q * Q, XR = XwaveRows<D>::R, WPG = 4;
+   __shared__ double sX[WPG][XR][64];  // gathered x; then the cross-wave face exchange
+   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+   const int blk = blk_begin + (int)blockIdx.x * WPG + w;
+   const bool wave_on = blk < blk_end;  // wave-uniform; every wave reaches the store's barriers
+   const int e = blk * 64 + lane;
+   const bool active = wave_on && e < ne;
+   const int *mp = gmap + (size_t)blk * ND * 64 + lane;
+   double Yo[ND];
+#pragma unroll
+   for (int a = 0; a < ND; a++) { Yo[a] = 0.0; }
+   if (wave_on)
+   {
+#pragma unroll
+      for (int a = 0; a < ND; a++)
+      {
+         const int g = mp[a * 64];
+         const int d = bdof(g);
+         const double v = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
+         sX[w][a][lane] = bneg(g) ? -v : v;
+      }
+      auto ld2 = [&](const double *p) -> v2d { return __builtin_nontemporal_load(reinterpret_cast<const v2d *>(p)); };
+      v2d ce[3];
+      {
+         const double *qc = qdd + (size_t)blk * 3 * 128 + lane * 2;
+#pragma unroll
+         for (int k = 0; k < 3; k++) { ce[k] = ld2(qc + k * 128); }
+      }
+      const double *qa = qdm + (size_t)blk * NQ * 128 + lane * 2;
+      v2d ca[Q], na[Q];
+      auto load_row = [&](int row, v2d (&aq)[Q]) {
+#pragma unroll
+         for (int qx = 0; qx < Q; qx++) { aq[qx] = ld2(qa + (size_t)(row * Q + qx) * 128); }
+      };
+      load_row(0, ca);
+
+#pragma unroll 1
+      for (int qz = 0; qz < Q; qz++)
+      {
+         double bz[D], gz[D];
+#pragma unroll
+         for (int dz = 0; dz < D; dz++) { bz[dz] = b.B[qz + MQ * dz]; gz[dz] = b.G[qz + MQ * dz]; }
+         // opaque lane index: the plane re-reads X from LDS instead of keeping 27 values live
+         int ll = lane;
+         asm volatile("" : "+v"(ll));
+         double ZB[D][D], ZG[D][D], SB[D][D], SG[D][D];
+#pragma unroll
+         for (int dy = 0; dy < D; dy++)
+#pragma unroll
+            for (int dx = 0; dx < D; dx++)
+            {
+               double zb = 0.0, zg = 0.0;
+#pragma unroll
+               for (int dz = 0; dz < D; dz++)
+               {
+                  const double c = sX[w][(dz * D + dy) * D + dx][ll];
+                  zb += bz[dz] * c;
+                  zg += gz[dz] * c;
+               }
+               ZB[dy][dx] = zb; ZG[dy][dx] = zg;
+               SB[dy][dx] = 0.0; SG[dy][dx] = 0.0;
+            }
+#pragma unroll 1
+         for (int qy = 0; qy < Q; qy++)
+         {
+            const int row = qz * Q + qy;
+            if (row + 1 < NR) { load_row(row + 1, na); }
+            // one row (qz, qy) of Q points: y-forward, x-forward, weighting, x-transpose, y-transpose
+            double Y00[D], Y01[D], Y10[D];
+#pragma unroll
+            for (int dx = 0; dx < D; dx++)
+            {
+               double u = 0.0, v = 0.0, wv = 0.0;
+#pragma unroll
+               for (int dy = 0; dy < D; dy++)
+               {
+                  const double by = b.B[qy + MQ * dy], gy = b.G[qy + MQ * dy];
+                  u += by * ZB[dy][dx];
+                  v += gy * ZB[dy][dx];
+                  wv += by * ZG[dy][dx];
+               }
+               Y00[dx] = u; Y01[dx] = v; Y10[dx] = wv;
+            }
+            double T0[D], T1[D], T2[D];
+#pragma unroll
+            for (int dx = 0; dx < D; dx++) { T0[dx] = 0.0; T1[dx] = 0.0; T2[dx] = 0.0; }
+#pragma unroll
+            for (int qx = 0; qx < Q; qx++)
+            {
+               double u = 0.0, ux = 0.0, uy = 0.0, uz = 0.0;
+#pragma unroll
+               for (int dx = 0; dx < D; dx++)
+               {
+                  const double bq = b.B[qx + MQ * dx], gq = b.G[qx + MQ * dx];
+                  u += bq * Y00[dx];
+                  ux += gq * Y00[dx];
+                  uy += bq * Y01[dx];
+                  uz += bq * Y10[dx];
+               }
+               const v2d sa = ca[qx];
+               const double m = sa.y * u;
+               const double fx = sa.x * (ce[0].x * ux + ce[0].y * uy + ce[1].x * uz);
+               const double fy = sa.x * (ce[0].y * ux + ce[1].y * uy + ce[2].x * uz);
+               const double fz = sa.x * (ce[1].x * ux + ce[2].x * uy + ce[2].y * uz);
+#pragma unroll
+               for (int dx = 0; dx < D; dx++)
+               {
+                  const double bq = b.B[qx + MQ * dx], gq = b.G[qx + MQ * dx];
+                  T0[dx] += bq * m + gq * fx;
+                  T1[dx] += bq * fy;
+                  T2[dx] += bq * fz;
+               }
+            }
+#pragma unroll
+            for (int dy = 0; dy < D; dy++)
+            {
+               const double by = b.B[qy + MQ * dy], gy = b.G[qy + MQ * dy];
+#pragma unroll
+               for (int dx = 0; dx < D; dx++)
+               {
+                  SB[dy][dx] += by * T0[dx] + gy * T1[dx];
+                  SG[dy][dx] += by * T2[dx];
+               }
+            }
+#pragma unroll
+            for (int qx = 0; qx < Q; qx++) { ca[qx] = na[qx]; }
+         }
+#pragma unroll
+         for (int dz = 0; dz < D; dz++)
+#pragma unroll
+            for (int dy = 0; dy < D; dy++)
+#pragma unroll
+               for (int dx = 0; dx < D; dx++)
+               {
+                  Yo[(dz * D + dy) * D + dx] += bz[dz] * SB[dy][dx] + gz[dz] * SG[dy][dx];
+               }
+      }
+   }  // wave_on
+   tpe_assemble_store<D, SPLIT, true, true>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0, blk, lane,
+                                            active, n_owned, y, yg, part, &sX[0][0][0], w, wave_on);
+}
+
+// Latency variant of k_apply_tpe_sf for small block ranges (the distributed Mult's boundary
+// elements, on the critical path of the exchange): one workgroup per 64-element block, its
+// four waves gather the x-values together and take one quadrature plane each (all of the
+// plane's pairs loaded up front), so a block costs one plane's latency instead of four.
+// Waves 1..3 hand their partial outputs to wave 0 through LDS, which adds them in a fixed
+// order (deterministic) and assembles / stores exactly like k_apply_tpe_sf (in-wave only).
+template <int D, int Q, bool SPLIT>
+__global__ void __launch_bounds__(256)
+k_apply_tpe_pp(int ne, int blk_begin, int n_owned, const int *__restrict__ gmap,
+               const double *__restrict__ qdd, const double *__restrict__ qdm,
+               const double *__restrict__ x, const double *__restrict__ xg,
+               double *__restrict__ y, double *__restrict__ yg, const Basis1D b,
+               const int *__restrict__ lane_flags, double *__restrict__ part)
+{
+   static_assert(Q <= 4, "one plane per wave");
+   constexpr int ND = D * D * D, NQ = Q * Q * Q;
+   __shared__ double sX[ND][64];
+   __shared__ double sY[3][ND][64];
+   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+   const int blk = blk_begin + (int)blockIdx.x;
+   const int e = blk * 64 + lane;
+   const bool active = e < ne;
+   const int *mp = gmap + (size_t)blk * ND * 64 + lane;
+   for (int a = w; a < ND; a += 4)
+   {
+      const int g = mp[a * 64];
+      const int d = bdof(g);
+      const double v = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
+      sX[a][lane] = bneg(g) ? -v : v;
+   }
+   double Yo[ND];
+#pragma unroll
+   for (int a = 0; a < ND; a++) { Yo[a] = 0.0; }
+   const int qz = w;
+   v2d ce[3], pr[Q][Q];
+   if (qz < Q)
+   {
+      const double *qc = qdd + (size_t)blk * 3 * 128 + lane * 2;
+#pragma unroll
+      for (int k = 0; k < 3; k++) { ce[k] = *reinterpret_cast<const v2d *>(qc + k * 128); }
+      const double *qa = qdm + (size_t)blk * NQ * 128 + lane * 2;
+#pragma unroll
+      for (int qy = 0; qy < Q; qy++)
+#pragma unroll
+         for (int qx = 0; qx < Q; qx++)
+         {
+            pr[qy][qx] = __builtin_nontemporal_load(
+               reinterpret_cast<const v2d *>(qa + (size_t)((qz * Q + qy) * Q + qx) * 128));
+         }
+   }
+   __syncthreads();
+   if (qz < Q)
+   {
+      double bz[D], gz[D];
+#pragma unroll
+      for (int dz = 0; dz < D; dz++) { bz[dz] = b.B[qz + MQ * dz]; gz[dz] = b.G[qz + MQ * dz]; }
+      double ZB[D][D], ZG[D][D], SB[D][D], SG[D][D];
+#pragma unroll
+      for (int dy = 0; dy < D; dy++)
+#pragma unroll
+         for (int dx = 0; dx < D; dx++)
+         {
+            double zb = 0.0, zg = 0.0;
+#pragma unroll
+            for (int dz = 0; dz < D; dz++)
+            {
+               const double c = sX[(dz * D + dy) * D + dx][lane];
+               zb += bz[dz] * c;
+               zg += gz[dz] * c;
+            }
+            ZB[dy][dx] = zb; ZG[dy][dx] = zg;
+            SB[dy][dx] = 0.0; SG[dy][dx] = 0.0;
+         }
+#pragma unroll
+      for (int qy = 0; qy < Q; qy++)
+      {
+         double Y00[D], Y01[D], Y10[D];
+#pragma unroll
+         for (int dx = 0; dx < D; dx++)
+         {
+            double u = 0.0, v = 0.0, wv = 0.0;
+#pragma unroll
+            for (int dy = 0; dy < D; dy++)
+            {
+               const double by = b.B[qy + MQ * dy], gy = b.G[qy + MQ * dy];
+               u += by * ZB[dy][dx];
+               v += gy * ZB[dy][dx];
+               wv += by * ZG[dy][dx];
+            }
+            Y00[dx] = u; Y01[dx] = v; Y10[dx] = wv;
+         }
+         double T0[D], T1[D], T2[D];
+#pragma unroll
+         for (int dx = 0; dx < D; dx++) { T0[dx] = 0.0; T1[dx] = 0.0; T2[dx] = 0.0; }
+#pragma unroll
+         for (int qx = 0; qx < Q; qx++)
+         {
+            double u = 0.0, ux = 0.0, uy = 0.0, uz = 0.0;
+#pragma unroll
+            for (int dx = 0; dx < D; dx++)
+            {
+               const double bq = b.B[qx + MQ * dx], gq = b.G[qx + MQ * dx];
+               u += bq * Y00[dx];
+               ux += gq * Y00[dx];
+               uy += bq * Y01[dx];
+               uz += bq * Y10[dx];
+            }
+            const v2d sa = pr[qy][qx];
+            const double m = sa.y * u;
+            const double fx = sa.x * (ce[0].x * ux + ce[0].y * uy + ce[1].x * uz);
+            const double fy = sa.x * (ce[0].y * ux + ce[1].y * uy + ce[2].x * uz);
+            const double fz = sa.x * (ce[1].x * ux + ce[2].x * uy + ce[2].y * uz);
+#pragma unroll
+            for (int dx = 0; dx < D; dx++)
+            {
+               const double bq = b.B[qx + MQ * dx], gq = b.G[qx + MQ * dx];
+               T0[dx] += bq * m + gq * fx;
+               T1[dx] += bq * fy;
+               T2[dx] += bq * fz;
+            }
+         }
+#pragma unroll
+         for (int dy = 0; dy < D; dy++)
+         {
+            const double by = b.B[qy + MQ * dy], gy = b.G[qy + MQ * dy];
+#pragma unroll
+            for (int dx = 0; dx < D; dx++)
+            {
+               SB[dy][dx] += by * T0[dx] + gy * T1[dx];
+               SG[dy][dx] += by * T2[dx];
+            }
+         }
+      }
+#pragma unroll
+      for (int dz = 0; dz < D; dz++)
+#pragma unroll
+         for (int dy = 0; dy < D; dy++)
+#pragma unroll
+            for (int dx = 0; dx < D; dx++)
+            {
+               Yo[(dz * D + dy) * D + dx] = bz[dz] * SB[dy][dx] + gz[dz] * SG[dy][dx];
+            }
+   }
+   if (w > 0)
+   {
+#pragma unroll
+      for (int a = 0; a < ND; a++) { sY[w - 1][a][lane] = Yo[a]; }
+   }
+   __syncthreads();
+   if (w != 0) { return; }
+#pragma unroll
+   for (int k = 0; k < 3; k++)
+#pragma unroll
+      for (int a = 0; a < ND; a++) { Yo[a] += sY[k][a][lane]; }
+   tpe_assemble_store<D, SPLIT, true, false>(Yo, mp, lane_flags[(size_t)blk * 64 + lane], blk, lane, active,
+                                             n_owned, y, yg, part, nullptr, 0, true);
+}
+
+// PA diagonal, thread per element on the blocked layout (PADiffusionDiagonal3D and the
+// mass diagonal, bilininteg_diffusion_kernels.hpp:369, bilininteg_mass_kernels.hpp:325,
+// assembled like AssembleDiagonal's E->L transpose, bilinearform_ext.cpp:370-454):
+//   diag(a) = sum_q grad(phi_a)^T O_q grad(phi_a) + m_q phi_a^2,  phi_a = B_x B_y B_z,
+// sum-factorised per quadrature row (qy, qz): seven x-contractions S_k(dx) of the row's
+// qdata, then the (dy, dz) factors of the row from a table, [6][dz][dy] = (By Bz)^2,
+// (Gy Bz)^2, (By Gz)^2, Gy By Bz^2, By^2 Gz Bz, Gy By Gz Bz.  Output assembled and stored
+// exactly like the apply kernels' (in-wave faces, cross-wave faces on AFFINE, plain stores,
+// partial slots): every diagonal entry written once, deterministic, no memset.
+template <int D, int Q, bool MASS, bool DIFF, bool SPLIT, bool AFF>
+__global__ void __launch_bounds__(256)
+k_diag_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
+           const double *__restrict__ qdd, const double *__restrict__ qdm, double *__restrict__ y,
+           double *__restrict__ yg, const Basis1D b, const double *__restrict__ drow,
+           const int *__restrict__ lane_flags, double *__restrict__ part)
+{
+   constexpr int ND = D * D * D, NQ = Q * Q * Q, NQH = (NQ + 1) / 2, DD = D * D, XR = XwaveRows<D>::R, WPG = 4;
+   __shared__ double xb[AFF ? WPG * XR * 64 : 1];  // AFF: cross-wave face exchange (as the apply's plan)
+   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+   const int blk = blk_begin + blockIdx.x * WPG + w;
+   const bool wave_on = blk < blk_end;  // wave-uniform
+   if (!AFF && !wave_on) { return; }    // no block-wide barrier without AFF
+   const bool active = wave_on && blk * 64 + lane < ne;
+   const int *mp = gmap + (size_t)blk * ND * 64 + lane;
+   const double *qd = qdd + (size_t)blk * NQ * 3 * 128 + lane * 2;
+   const double *qm = qdm + (size_t)blk * NQH * 128 + lane * 2;
+   const double *qa = qdm + (size_t)blk * NQ * 128 + lane * 2;  // AFF pairs
+   v2d ce[3];
+   if (AFF && wave_on)
+   {
+#pragma unroll
+      for (int k = 0; k < 3; k++) { ce[k] = *reinterpret_cast<const v2d *>(qdd + (size_t)blk * 3 * 128 + lane * 2 + k * 128); }
+   }
+   double Yo[ND];
+#pragma unroll
+   for (int a = 0; a < ND; a++) { Yo[a] = 0.0; }
+#pragma unroll 1
+   for (int row = 0; row < (wave_on ? Q * Q : 0); row++)
+   {
+      double S[7][D];
+#pragma unroll
+      for (int k = 0; k < 7; k++)
+#pragma unroll
+         for (int dx = 0; dx < D; dx++) { S[k][dx] = 0.0; }
+#pragma unroll
+      for (int qx = 0; qx < Q; qx++)
+      {
+         const int q = row * Q + qx;
+         v2d d0 = {0.0, 0.0}, d1 = {0.0, 0.0}, d2 = {0.0, 0.0};
+         double m = 0.0;
+         if (AFF)
+         {
+            const v2d sa = *reinterpret_cast<const v2d *>(qa + (size_t)q * 128);
+            d0 = sa.x * ce[0];
+            d1 = sa.x * ce[1];
+            d2 = sa.x * ce[2];
+            m = sa.y;
+         }
+         else
+         {
+            if (DIFF)
+            {
+               d0 = *reinterpret_cast<const v2d *>(qd + ((size_t)q * 3 + 0) * 128);
+               d1 = *reinterpret_cast<const v2d *>(qd + ((size_t)q * 3 + 1) * 128);
+               d2 = *reinterpret_cast<const v2d *>(qd + ((size_t)q * 3 + 2) * 128);
+            }
+            if (MASS) { m = qm[(size_t)(q >> 1) * 128 + (q & 1)]; }
+         }
+#pragma unroll
+         for (int dx = 0; dx < D; dx++)
+         {
+            const double bx = b.B[qx + MQ * dx], gx = b.G[qx + MQ * dx];
+            const double bb = bx * bx, gb = gx * bx;
+            if (DIFF)
+            {
+               S[0][dx] += gx * gx * d0.x;  // O11
+               S[1][dx] += bb * d1.y;       // O22
+               S[2][dx] += bb * d2.y;       // O33
+               S[3][dx] += gb * d0.y;       // O12
+               S[4][dx] += gb * d1.x;       // O13
+               S[5][dx] += bb * d2.x;       // O23
+            }
+            if (MASS) { S[6][dx] += bb * m; }
+         }
+      }
+      const double *P = drow + (size_t)row * 6 * DD;
+#pragma unroll
+      for (int dz = 0; dz < D; dz++)
+#pragma unroll
+         for (int dy = 0; dy < D; dy++)
+         {
+            const int o = dz * D + dy;
+            const double p0 = P[o], p1 = P[DD + o], p2 = P[2 * DD + o];
+            const double p3 = P[3 * DD + o], p4 = P[4 * DD + o], p5 = P[5 * DD + o];
+#pragma unroll
+            for (int dx = 0; dx < D; dx++)
+            {
+               double v = p0 * (S[0][dx] + S[6][dx]) + p1 * S[1][dx] + p2 * S[2][dx];
+               v += 2.0 * (p3 * S[3][dx] + p4 * S[4][dx] + p5 * S[5][dx]);
+               Yo[o * D + dx] += v;
+            }
+         }
+   }
+   tpe_assemble_store<D, SPLIT, false, AFF>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0, blk, lane,
+                                            active, n_owned, y, yg, part, xb, w, wave_on);
+}
+
+template <int D, int Q, bool MASS, bool DIFF, bool SPLIT>
+void launch_tpe(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipStream_t s)
+{
+   const int nb = a.blk_end - a.blk_begin;
+   const dim3 grid((nb + 3) / 4), block(256);
+   if (a.kind == QLAYOUT_AFFINE)
+   {
+      if constexpr (MASS && DIFF)
+      {
+         if (a.latency)
+         {
+            hipLaunchKernelGGL((k_apply_tpe_pp<D, Q, SPLIT>), dim3(nb), dim3(256), 0, s, a.ne, a.blk_begin,
+                               a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part);
+         }
+         else
+         {
+            hipLaunchKernelGGL((k_apply_tpe_sf<D, Q, SPLIT>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end,
+                               a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part);
+         }
+      }
+      else { ECM2_VERIFY(false, ERR_INTERNAL, "AFFINE qdata needs both integrators"); }
+      return;
+   }
+   hipLaunchKernelGGL((k_apply_tpe_pf<D, Q, MASS, DIFF, SPLIT>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end,
+                      a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, rowtab, a.lane_flags, a.part);
+}
+
+template <int D, int Q, bool MASS, bool DIFF>
+void launch_tpe_mdq(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipStream_t s)
+{
+   if (a.blk_end <= a.blk_begin) { return; }
+   ECM2_VERIFY(a.lane_flags, ERR_INTERNAL, "thread-per-element kernel needs the merge plan");
+   if (a.xg || a.yg) { launch_tpe<D, Q, MASS, DIFF, true>(a, b, rowtab, s); }
+   else { launch_tpe<D, Q, MASS, DIFF, false>(a, b, rowtab, s); }
+}
+
+template <int D, int Q>
+void launch_tpe_dq(bool mass, bool diff, const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipStream_t s)
+{
+   if (mass && diff) { launch_tpe_mdq<D, Q, true, true>(a, b, rowtab, s); }
+   else if (mass) { launch_tpe_mdq<D, Q, true, false>(a, b, rowtab, s); }
+   else if (diff) { launch_tpe_mdq<D, Q, false, true>(a, b, rowtab, s); }
+}
+
+template <int D, int Q, bool MASS, bool DIFF>
+void launch_diag_tpe(const ApplyArgs &a, const Basis1D &b, const double *drow, hipStream_t s)
+{
+   const int nb = a.blk_end - a.blk_begin;
+   if (nb <= 0) { return; }
+   const dim3 grid((nb + 3) / 4), block(256);
+#define ECM2_DIAG(SP, AF)                                                                                \
+   hipLaunchKernelGGL((k_diag_tpe<D, Q, MASS, DIFF, SP, AF>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end, \
+                      a.n_owned, a.gmap, a.qdd, a.qdm, a.y, a.yg, b, drow, a.lane_flags, a.part)
+   const bool aff = a.kind == QLAYOUT_AFFINE;
+   ECM2_VERIFY(!aff || (MASS && DIFF), ERR_INTERNAL, "AFFINE qdata needs both integrators");
+   if (a.yg) { if (aff) { ECM2_DIAG(true, true); } else { ECM2_DIAG(true, false); } }
+   else { if (aff) { ECM2_DIAG(false, true); } else { ECM2_DIAG(false, false); } }
+#undef ECM2_DIAG
+}
+
+template <int D, int Q>
+void launch_diag_tpe_dq(bool mass, bool diff, const ApplyArgs &a, const Basis1D &b, const double *drow,
+                        hipStream_t s)
+{
+   if (mass && diff) { launch_diag_tpe<D, Q, true, true>(a, b, drow, s); }
+   else if (mass) { launch_diag_tpe<D, Q, true, false>(a, b, drow, s); }
+   else if (diff) { launch_diag_tpe<D, Q, false, true>(a, b, drow, s); }
+}
+
+} // namespace
+
+namespace kern
+{
+
+void apply_tpe(int D, int Q, bool mass, bool diff, const ApplyArgs &a, const Basis1D &b,
+               const double *rowtab, hipStream_t s)
+{
+   if (a.ne == 0) { return; }
+   if (D == 2 && Q == 3) { launch_tpe_dq<2, 3>(mass, diff, a, b, rowtab, s); }
+   else if (D == 3 && Q == 4) { launch_tpe_dq<3, 4>(mass, diff, a, b, rowtab, s); }
+   else { ECM2_VERIFY(false, ERR_UNSUPPORTED, "no thread-per-element kernel for D1D=" << D << " Q1D=" << Q); }
+   ECM2_HIP(hipGetLastError());
+}
+
+void diagonal_tpe(int D, int Q, bool mass, bool diff, const ApplyArgs &a, const Basis1D &b, const double *drow,
+                  hipStream_t s)
+{
+   if (a.ne == 0) { return; }
+   if (D == 2 && Q == 3) { launch_diag_tpe_dq<2, 3>(mass, diff, a, b, drow, s); }
+   else if (D == 3 && Q == 4) { launch_diag_tpe_dq<3, 4>(mass, diff, a, b, drow, s); }
+   else { ECM2_VERIFY(false, ERR_UNSUPPORTED, "no thread-per-element diagonal for D1D=" << D << " Q1D=" << Q); }
+   ECM2_HIP(hipGetLastError());
+}
+
+std::vector<double> make_row_table(const DofToQuad &m)
+{
+   const int D = m.ndof, Q = m.nqpt, DD = D * D;
+   std::vector<double> t((size_t)Q * Q * 3 * DD);
+   for (int qz = 0; qz < Q; qz++)
+      for (int qy = 0; qy < Q; qy++)
+      {
+         double *P = &t[(size_t)(qz * Q + qy) * 3 * DD];
+         for (int dz = 0; dz < D; dz++)
+            for (int dy = 0; dy < D; dy++)
+            {
+               const double By = m.B[qy + Q * dy], Gy = m.G[qy + Q * dy];
+               const double Bz = m.B[qz + Q * dz], Gz = m.G[qz + Q * dz];
+               P[0 * DD + dz * D + dy] = By * Bz;
+               P[1 * DD + dz * D + dy] = Gy * Bz;
+               P[2 * DD + dz * D + dy] = By * Gz;
+            }
+      }
+   return t;
+}
+
+std::vector<double> make_diag_row_table(const DofToQuad &m)
+{
+   const int D = m.ndof, Q = m.nqpt, DD = D * D;
+   std::vector<double> t((size_t)Q * Q * 6 * DD);
+   for (int qz = 0; qz < Q; qz++)
+      for (int qy = 0; qy < Q; qy++)
+      {
+         double *P = &t[(size_t)(qz * Q + qy) * 6 * DD];
+         for (int dz = 0; dz < D; dz++)
+            for (int dy = 0; dy < D; dy++)
+            {
+               const double By = m.B[qy + Q * dy], Gy = m.G[qy + Q * dy];
+               const double Bz = m.B[qz + Q * dz], Gz = m.G[qz + Q * dz];
+               const int o = dz * D + dy;
+               P[0 * DD + o] = By * By * Bz * Bz;
+               P[1 * DD + o] = Gy * Gy * Bz * Bz;
+               P[2 * DD + o] = By * By * Gz * Gz;
+               P[3 * DD + o] = Gy * By * Bz * Bz;
+               P[4 * DD + o] = By * By * Gz * Bz;
+               P[5 * DD + o] = Gy * By * Gz * Bz;
+            }
+      }
+   return t;
+}
+
+} // namespace kern
+} // namespace ecm2

@@ -1,4 +1,7 @@
-// kernels.hpp -- host launchers for the gfx950 HIP kernels (pa_kernels.hip).
+// kernels.hpp -- host launchers for the gfx950 HIP kernels (k_setup.hip: qdata and
+// coefficient setup; k_tpe.hip: thread-per-element p <= 2 apply and diagonal; k_line.hip:
+// line / brick p >= 3 apply and the sum-factorised diagonal; k_misc.hip: workgroup-per-element
+// apply, restriction, vector and solver kernels).
 //
 // Quadrature-data layouts (the qdata a PA form owns):
 //  * BLOCKED (fused thread-per-element kernel): elements in blocks of 64 (one
@@ -66,15 +69,39 @@ struct QLayout
 // an affine function of an H1 grid function interpolated at the quadrature
 // points: c = scale * (1 + slope * (T(x_q) - t_ref))  (GridFunctionCoefficient,
 // coefficient.cpp:250-253, composed with the Pennes k(T) law).
-enum CoeffKind : int { COEFF_CONSTANT = 0, COEFF_QUAD = 1, COEFF_GRIDFUNC_AFFINE = 2 };
+// COEFF_GRIDFUNC_PERFUSION: the Pennes heat-capacity + perfusion term of the implicit
+// stage's mass coefficient, alpha(T) = rho_c + gdt_cb * w_b(T) with the temperature-dependent
+// perfusion w_b(T) = w0 * max(0, 1 + a (T - t0)) below the coagulation temperature t_stop and
+// 0 at or above it (perfusion shut-down in ablated tissue).  p = (rho_c, gdt_cb, w0, a, t0, t_stop).
+enum CoeffKind : int { COEFF_CONSTANT = 0, COEFF_QUAD = 1, COEFF_GRIDFUNC_AFFINE = 2, COEFF_GRIDFUNC_PERFUSION = 3 };
 struct CoeffDesc
 {
    int kind = COEFF_CONSTANT;
    double value = 1.0;           // constant
    const double *quad = nullptr; // device [ne][nq]
    const double *lvec = nullptr; // device L-vector of T
-   double scale = 1.0, slope = 0.0, t_ref = 0.0;
+   double scale = 1.0, slope = 0.0, t_ref = 0.0;  // GRIDFUNC_AFFINE
+   double p[6] = {0, 0, 0, 0, 0, 0};              // GRIDFUNC_PERFUSION
+   bool gridfunc() const { return kind == COEFF_GRIDFUNC_AFFINE || kind == COEFF_GRIDFUNC_PERFUSION; }
 };
+
+struct CoeffParams  // kernel-argument copy of CoeffDesc::p
+{
+   double p[6];
+};
+
+// The temperature law of a grid-function coefficient at one point (device and host).
+__host__ __device__ inline double coeff_law(int kind, double T, double scale, double slope, double t_ref,
+                                            const double *p)
+{
+   if (kind == COEFF_GRIDFUNC_PERFUSION)
+   {
+      const double r = 1.0 + p[3] * (T - p[4]);
+      const double wb = (T < p[5] && r > 0.0) ? p[2] * r : 0.0;
+      return p[0] + p[1] * wb;
+   }
+   return scale * (1.0 + slope * (T - t_ref));
+}
 
 // Arguments of one fused apply over element blocks [blk_begin, blk_end) (64 elements per
 // block).  With a split L-vector (distributed form) dofs >= n_owned live in xg / yg.
@@ -89,11 +116,10 @@ struct ApplyArgs
    const double *x = nullptr, *xg = nullptr;
    double *y = nullptr, *yg = nullptr;
    double *part = nullptr;          // partial slots of shared dofs (null: atomics)
-   const int *pslot = nullptr;      // TPE: [blk][nd][64] entry -> position in its dof's run (null: dense slots)
    bool latency = false;            // TPE + AFFINE: one workgroup per block, a plane per wave (small ranges)
-   int xwg = 4;                     // TPE + AFFINE: blocks (waves) per workgroup of the face-assembly plan
-   const int *chunks = nullptr;     // LINE: device chunk table (first | count << 24)
-   const int *chunk_off = nullptr;  // LINE: host [nblk + 1], chunks of 64-element block b
+   const Basis1D *btab = nullptr;   // LINE / brick / diagonal: device copy of the (D1D, Q1D) tables
+   const int *lelem = nullptr;      // LINE: device list of the elements outside bricks
+   const int *lelem_off = nullptr;  // LINE: host [nblk + 1], listed elements of 64-element block b
    // LINE, brick part (p >= 3 on structured regions): bricks of 2 x 2 x brick_bz elements
    const int *belem = nullptr;      // device [nbrick][4 bz] element ids (qdata addressing)
    const int *bmap = nullptr;       // device [nbrick][NB] lattice map: dof | shared << 30
@@ -129,8 +155,10 @@ __host__ __device__ inline int brick_surface_index(int D, int bz, int X, int Y, 
 namespace kern
 {
 // ---- setup (S1/S2/S3 equivalents) ----
-// Evaluate a grid-function coefficient at quadrature points into out[e][q].
-void coeff_gridfunc(int ne, int D, int Q, const int *gmap_native, const Basis1D &b,
+// Evaluate a grid-function coefficient at quadrature points into out[e][q]
+// (GridFunctionCoefficient projection, qfunction.cpp:73-98, then the temperature law).
+// btab: device copy of b (the sum-factorised kernel's tables).
+void coeff_gridfunc(int ne, int D, int Q, const int *gmap_native, const Basis1D &b, const Basis1D *btab,
                     const CoeffDesc &c, double *out, hipStream_t s);
 // qdata from lexicographic element corner coordinates enodes[e][3][8].
 void setup_from_nodes(const QLayout &L, int Q, const double *enodes, const double *W,
@@ -155,17 +183,14 @@ void setup_from_jacobians(const QLayout &L, const double *J, const double *W,
 // Fused y = R^T (M + K) R x, thread-per-element (blocked layout); y must be zeroed.
 void apply_tpe(int D, int Q, bool mass, bool diff, const ApplyArgs &a, const Basis1D &b,
                const double *rowtab, hipStream_t s);
-// Row table for apply_tpe: [qz][qy][3][dz][dy] products (see pa_kernels.hip).
+// Row table for apply_tpe: [qz][qy][3][dz][dy] products (see k_tpe.hip).
 std::vector<double> make_row_table(const DofToQuad &m);
-// Line kernel: one wave per chunk of x-adjacent elements, native qdata layout, L-vectors
+// Line kernel: one wave per listed element (a.lelem), native or AFFINE_E qdata, L-vectors
 // through an encoded map [e][nd] (dof | shared << 30 | sign << 31); shared dofs go to
-// part[e*nd + a] when a.part is set, else atomics.  has_line: (D, Q) instantiated.
+// part[e*nd + a] when a.part is set, else atomics; then the bricks (a.brick_bz).
+// has_line: (D, Q) instantiated.
 bool has_line(int D, int Q);
-// Longest chunk of x-adjacent elements the selected line-kernel variant walks per wave.
-int line_chunk_limit();
-// Write the constant-memory basis table of (D, Q) on the current device (once).
-void upload_basis(int D, int Q, const Basis1D &b);
-void apply_line(int D, int Q, bool mass, bool diff, const ApplyArgs &a, const Basis1D &b, hipStream_t s);
+void apply_line(int D, int Q, bool mass, bool diff, const ApplyArgs &a, hipStream_t s);
 // Brick kernel of the line family: (D, Q, bz) instantiated?  Lattice points per brick.
 bool has_brick(int D, int Q, int bz);
 int brick_points(int D, int bz);
@@ -188,7 +213,7 @@ void diagonal_tpe(int D, int Q, bool mass, bool diff, const ApplyArgs &a, const 
 std::vector<double> make_diag_row_table(const DofToQuad &m);
 // Sum-factorised workgroup-per-element diagonal, any layout; L-vector (atomics) or E-vector.
 void diagonal(const int *pos, int D, int Q, int layout, int ne, const int *gmap_native, const double *qd_diff,
-              const double *qd_mass, double *diag, bool out_evec, const Basis1D &b,
+              const double *qd_mass, double *diag, bool out_evec, const Basis1D &b, const Basis1D *btab,
               hipStream_t s);
 
 // ---- vector kernels for the device PCG ----
@@ -198,10 +223,6 @@ void copy_values(int n, const int *idx, const double *x, double *y, hipStream_t 
 // hout (optional): device pointer of mapped pinned host memory that also receives the result.
 void dot(int n, const double *a, const double *b, double *partials, double *out, hipStream_t s,
          double *hout = nullptr);
-// PCG updates with device-resident scalars (no host round trip):
-//   x += (nom/den) d ; r -= (nom/den) z
-void pcg_update_xr(int n, const double *nom, const double *den, const double *d,
-                   const double *z, double *x, double *r, hipStream_t s);
 // Fused PCG update: x += (nom/den) d; r -= (nom/den) z; z = dinv .* r (dinv null: z untouched);
 // *out = r.z (r.r without dinv), deterministic.  z holds A d on entry.
 void pcg_step(int n, const double *nom, const double *den, const double *d, double *z, double *x, double *r,
@@ -223,10 +244,9 @@ void stream_copy(long n, const double *a, double *b, hipStream_t s);
 void gather_idx(int n, const int *idx, const double *x, double *buf, hipStream_t s);
 void scatter_add_idx(int n, const int *idx, const double *buf, double *y, hipStream_t s);
 // Deterministic second scatter pass: y[dofs[i]] = sum_j part[slots[j]], j in
-// [start, start + count), meta[i] = start << 5 | count; slots null: part[j] (contiguous runs).
+// [start, start + count), meta[i] = start << 5 | count.
 void sum_partials(int i0, int i1, const int *dofs, const unsigned *meta, const int *slots, const double *part,
                   int n_owned, double *y, double *yg, hipStream_t s);
-void scatter_set_idx(int n, const int *idx, const double *buf, double *y, hipStream_t s);
 } // namespace kern
 
 } // namespace ecm2

@@ -259,17 +259,6 @@ uint64_t spread3(uint64_t v)  // 21 bits -> every third bit
    return v;
 }
 
-// Order in which complete bricks are visited: lexicographic (default) or along a Morton
-// curve (ECM2_BRICK_CURVE=morton, experiment knob: neighbouring bricks, which share x
-// values, are processed closer in time on large meshes).
-bool brick_curve_morton()
-{
-   static bool v = [] {
-      const char *e = std::getenv("ECM2_BRICK_CURVE");
-      return e && std::string(e) == "morton";
-   }();
-   return v;
-}
 } // namespace
 
 std::vector<int> brick_order(const std::vector<int> &elems, int nx, int ny, int nz)
@@ -281,16 +270,11 @@ std::vector<int> brick_order(const std::vector<int> &elems, int nx, int ny, int 
       const int ex = e % nx, ey = (e / nx) % ny, ez = e / (nx * ny);
       return (long)(ex / 4) + bx * ((long)(ey / 4) + (long)by * (ez / 4));
    };
-   const bool morton = brick_curve_morton();
-   auto curve = [&](long k) -> uint64_t {
-      if (!morton) { return (uint64_t)k; }
-      const uint64_t ix = k % bx, iy = (k / bx) % by, iz = k / ((long)bx * by);
-      return spread3(ix) | spread3(iy) << 1 | spread3(iz) << 2;
-   };
+   auto curve = [&](long k) -> uint64_t { return (uint64_t)k; };  // lexicographic brick order
    for (int e : elems) { count[key(e)]++; }
    std::vector<int> out;
    out.reserve(elems.size());
-   // complete bricks, in brick order (lexicographic or Morton), members x-fastest
+   // complete bricks, in lexicographic brick order, members x-fastest
    std::vector<int> sorted(elems);
    std::stable_sort(sorted.begin(), sorted.end(), [&](int a, int b) {
       const long ka = key(a), kb = key(b);

@@ -102,16 +102,6 @@ void PAForm::set_geometry_compression(bool on)
    assembled_ = false;
 }
 
-// experiment knob ECM2_AFFINE=0: never use the AFFINE qdata layout
-static bool affine_env()
-{
-   static const bool v = [] {
-      const char *e = std::getenv("ECM2_AFFINE");
-      return !(e && std::string(e) == "0");
-   }();
-   return v;
-}
-
 void PAForm::set_block_splits(const std::vector<int> &splits)
 {
    for (int b : splits) { ECM2_VERIFY(b >= 0 && b <= layout_.nblk(), ERR_ARG, "block split " << b << " out of range"); }
@@ -135,8 +125,7 @@ void PAForm::set_latency_from(int b)
 
 void PAForm::set_line_bricks(int bz)
 {
-   ECM2_VERIFY(bz >= -1 && (bz <= 2 || bz == 4 || bz == 8), ERR_ARG,
-               "brick mode " << bz << " not in {-1, 0, 1, 2, 4, 8}");
+   ECM2_VERIFY(bz >= -1 && bz <= 2, ERR_ARG, "brick mode " << bz << " not in {-1, 0, 1, 2}");
    line_bricks_ = bz;
    gmap_line_.resize(0);
    assembled_ = false;
@@ -145,10 +134,10 @@ void PAForm::set_line_bricks(int bz)
 void PAForm::add_integrator(int kind, const CoeffDesc &c)
 {
    ECM2_VERIFY(kind == INTEG_MASS || kind == INTEG_DIFFUSION, ERR_ARG, "unknown integrator " << kind);
-   ECM2_VERIFY(c.kind == COEFF_CONSTANT || c.kind == COEFF_QUAD || c.kind == COEFF_GRIDFUNC_AFFINE,
+   ECM2_VERIFY(c.kind == COEFF_CONSTANT || c.kind == COEFF_QUAD || c.gridfunc(),
                ERR_ARG, "unknown coefficient kind " << c.kind);
    ECM2_VERIFY(c.kind != COEFF_QUAD || ne_ == 0 || c.quad, ERR_ARG, "null quadrature coefficient");
-   ECM2_VERIFY(c.kind != COEFF_GRIDFUNC_AFFINE || ndofs_ == 0 || c.lvec, ERR_ARG, "null grid function");
+   ECM2_VERIFY(!c.gridfunc() || ndofs_ == 0 || c.lvec, ERR_ARG, "null grid function");
    if (kind == INTEG_MASS)
    {
       ECM2_VERIFY(!have_mass_, ERR_UNSUPPORTED, "a MassIntegrator is already present");
@@ -290,50 +279,12 @@ void build_merge_plan(int ne, int D, const std::vector<int> &gmap_int, int ndofs
 }
 } // namespace
 
-// Bricks of the line kernel family (experiment knob ECM2_LINE_BRICK): 0 = none (every
-// element runs the per-element line kernel), 1 = 2 x 2 x 1 (default), 2 = 2 x 2 x 2.
-// Measured at C5 (68^3, p = 4; profiles/ab_brick.sh): kernel 1.018 ms (none), 0.902 ms
-// (2 x 2 x 1: 192 threads, 27 KB LDS, 5 workgroups per CU), 1.114 ms (2 x 2 x 2: 320
-// threads, 54 KB, 3 per CU -- fewer, larger workgroups stall longer at the barriers).
-static int line_brick_mode()
-{
-   static int v = [] {
-      const char *e = std::getenv("ECM2_LINE_BRICK");
-      const int b = e ? std::atoi(e) : 1;
-      return (b >= 0 && (b <= 2 || b == 4 || b == 8)) ? b : 1;
-   }();
-   return v;
-}
-
-// Longest chunk of x-adjacent elements one wave of the line kernel walks: the kernel
-// variant's limit (1 for the default single-element variant), lowered by ECM2_LINE_CHUNK.
-static int line_chunk_max()
-{
-   static int v = [] {
-      const char *e = std::getenv("ECM2_LINE_CHUNK");
-      const int c = e ? std::atoi(e) : 8;
-      return std::max(1, std::min(c, kern::line_chunk_limit()));
-   }();
-   return v;
-}
-
-// Order of the second-pass list (experiment knob ECM2_SUM_ORDER=dof): by first partial
-// slot (default: neighbouring threads read neighbouring slots) or by dof (y stores coalesce).
-static bool sum_order_by_dof()
-{
-   static bool v = [] {
-      const char *e = std::getenv("ECM2_SUM_ORDER");
-      return e && std::string(e) == "dof";
-   }();
-   return v;
-}
-
 // Second-pass plan of the deterministic scatter: every dof not held exactly once with its
 // partial slots in ascending order; dofs held by nobody get an empty list (y = 0).  The
 // owned dofs come first, then the ghosts (split form); within each range the list is
 // ordered by first slot, so neighbouring threads of k_sum_partials read neighbouring slots.
 void PAForm::build_shared_plan(const std::vector<int> &hcount, const std::vector<int> &hdof,
-                               const std::vector<int> &hslot, hipStream_t s, std::vector<int> *slots_out)
+                               const std::vector<int> &hslot, hipStream_t s)
 {
    std::vector<int> start(ndofs_ + 1, 0);
    for (int d = 0; d < ndofs_; d++) { start[d + 1] = start[d] + (hcount[d] > 1 ? hcount[d] : 0); }
@@ -344,7 +295,7 @@ void PAForm::build_shared_plan(const std::vector<int> &hcount, const std::vector
    for (int d = 0; d < ndofs_; d++) { if (hcount[d] != 1) { dofs.push_back(d); } }
    auto key = [&](int d) -> long {
       const long first = hcount[d] > 1 ? slots_by_dof[start[d]] : -1;
-      return (d < n_owned_ ? 0 : (1l << 40)) + (sum_order_by_dof() ? (long)d : first);
+      return (d < n_owned_ ? 0 : (1l << 40)) + first;
    };
    std::stable_sort(dofs.begin(), dofs.end(), [&](int p, int q) { return key(p) < key(q); });
    std::vector<unsigned> meta;
@@ -364,22 +315,7 @@ void PAForm::build_shared_plan(const std::vector<int> &hcount, const std::vector
    n_slots_ = (long)slots.size();
    sh_dofs_.upload(dofs, s);
    sh_meta_.upload(meta, s);
-   if (slots_out) { *slots_out = std::move(slots); }  // caller lays partials out as runs
-   else { sh_slots_.upload(slots, s); }
-}
-
-// experiment knob ECM2_PART_RUNS=1: TPE partial slots laid out as contiguous per-dof runs
-// (the summation pass reads each dof's holders contiguously, no slot list) instead of the
-// dense [blk][a][lane] slots.  Measured (profiles/ab_runs.sh): the summation pass halves
-// (C4 88 -> 48 us) but the apply kernel's scattered partial stores cost more (C4 0.379 ->
-// 0.441 ms): net slower at C2 / C3 / C4, so off by default.
-static bool part_runs()
-{
-   static const bool v = [] {
-      const char *e = std::getenv("ECM2_PART_RUNS");
-      return e && std::string(e) == "1";
-   }();
-   return v;
+   sh_slots_.upload(slots, s);
 }
 
 void PAForm::set_kernel(int mode)
@@ -392,32 +328,6 @@ void PAForm::set_kernel(int mode)
 }
 
 static bool has_tpe(int D, int Q) { return (D == 2 && Q == 3) || (D == 3 && Q == 4); }
-
-// Cross-wave face assembly in the AFFINE thread-per-element kernels (ECM2_XWAVE=0: in-wave
-// only).  Off with the kernel variants that lack it (row kernel, plane-per-wave Mult).
-static bool xwave_env()
-{
-   static const bool v = [] {
-      const char *e = std::getenv("ECM2_XWAVE");
-      if (e && std::string(e) == "0") { return false; }
-      const char *tv = std::getenv("ECM2_TPE_VARIANT");
-      if (tv && (std::atoi(tv) & 64)) { return false; }
-      const char *pp = std::getenv("ECM2_TPE_PP");
-      return !(pp && std::string(pp) == "1");
-   }();
-   return v;
-}
-
-// Waves per workgroup of the cross-wave plan (experiment knob ECM2_XWAVE_WG=8: 2 x 2 x 2
-// bricks per workgroup).
-static int xwave_wg()
-{
-   static const int v = [] {
-      const char *e = std::getenv("ECM2_XWAVE_WG");
-      return (e && std::atoi(e) == 8) ? 8 : 4;
-   }();
-   return v;
-}
 
 void PAForm::assemble(hipStream_t s)
 {
@@ -433,11 +343,11 @@ void PAForm::assemble(hipStream_t s)
                "line kernel needs Q1D in {D1D, D1D+1} and Q1D <= 8");
    layout_.kind = (resolved_mode_ == KERNEL_TPE) ? QLAYOUT_BLOCKED : QLAYOUT_NATIVE;
    bool affine = affine_;
-   if (jac_ && compress_ && affine_env() && have_mass_ && have_diff_ && (resolved_mode_ == KERNEL_TPE || resolved_mode_ == KERNEL_LINE))
+   if (jac_ && compress_ && have_mass_ && have_diff_ && (resolved_mode_ == KERNEL_TPE || resolved_mode_ == KERNEL_LINE))
    {
       affine = kern::jacobians_affine(ne_, NQ_, jac_, s);  // the reference binding's geometry
    }
-   if (affine && compress_ && affine_env() && have_mass_ && have_diff_)
+   if (affine && compress_ && have_mass_ && have_diff_)
    {
       if (resolved_mode_ == KERNEL_TPE) { layout_.kind = QLAYOUT_AFFINE; }
       else if (resolved_mode_ == KERNEL_LINE) { layout_.kind = QLAYOUT_AFFINE_E; }
@@ -445,11 +355,7 @@ void PAForm::assemble(hipStream_t s)
 
    if (resolved_mode_ == KERNEL_TPE && !gmap_blk_.size() && ne_ > 0)
    {
-      static const bool auto_env = [] {  // experiment knob ECM2_AUTO_ORDER=0: keep caller order
-         const char *e = std::getenv("ECM2_AUTO_ORDER");
-         return !(e && std::string(e) == "0");
-      }();
-      if (perm_host_.empty() && auto_order_ && auto_env)
+      if (perm_host_.empty())
       {
          // no caller order: 4x4x4 face-linked bricks first (one per wave), per apply segment
          std::vector<int> cuts{0};
@@ -486,14 +392,13 @@ void PAForm::assemble(hipStream_t s)
          for (int sp : splits_) { seg.push_back(std::max(0, std::min(nblk, sp))); }
          std::sort(seg.begin(), seg.end());
          seg.erase(std::unique(seg.begin(), seg.end()), seg.end());
-         const bool xw = layout_.kind == QLAYOUT_AFFINE && xwave_env();
-         xwg_ = xw ? xwave_wg() : 4;
+         const bool xw = layout_.kind == QLAYOUT_AFFINE;
          for (size_t k = 0; k + 1 < seg.size(); k++)
          {
             const bool lat = latency_from_ >= 0 && seg[k] >= latency_from_;
-            for (int b = seg[k]; b < seg[k + 1]; b += xwg_)
+            for (int b = seg[k]; b < seg[k + 1]; b += 4)
             {
-               groups.push_back({b, std::min(b + xwg_, seg[k + 1]), (xw && !lat) ? 1 : 0});
+               groups.push_back({b, std::min(b + 4, seg[k + 1]), (xw && !lat) ? 1 : 0});
             }
          }
       }
@@ -525,22 +430,7 @@ void PAForm::assemble(hipStream_t s)
                      hslot.push_back((b * ND_ + a) * 64 + l);
                   }
                }
-         tpe_runs_ = part_runs();
-         if (tpe_runs_)
-         {
-            // partial slot of a shared holding entry = its position in the dof's run
-            std::vector<int> slots;
-            build_shared_plan(hcount, hdof, hslot, s, &slots);
-            std::vector<int> ps((size_t)nblk * ND_ * 64, -1);
-            for (size_t j = 0; j < slots.size(); j++) { ps[slots[j]] = (int)j; }
-            pslot_.upload(ps, s);
-            sh_slots_.resize(0);
-         }
-         else
-         {
-            build_shared_plan(hcount, hdof, hslot, s);
-            pslot_.resize(0);
-         }
+         build_shared_plan(hcount, hdof, hslot, s);
       }
       gmap_blk_.upload(blk, s);
       lane_flags_.upload(fl, s);
@@ -552,34 +442,22 @@ void PAForm::assemble(hipStream_t s)
       drowtab_.upload(kern::make_diag_row_table(maps_), s);
       ECM2_HIP(hipStreamSynchronize(s));
    }
-   if (resolved_mode_ == KERNEL_LINE) { kern::upload_basis(D_, Q_, basis_); }
+   if (!btab_.size()) { btab_.upload(&basis_, 1, s); }
    if (resolved_mode_ == KERNEL_LINE && !gmap_line_.size() && ne_ > 0)
    {
-      // Bricks of 2 x 2 x bz elements (deterministic scatter only) take every element they
-      // can; the leftovers run the per-element line kernel in chunks of up to 8 consecutive
-      // elements whose x-faces coincide (never crossing a 64-element block, so
-      // apply_blocks ranges map to chunk ranges; the face of element k is carried into
-      // element k+1, which holds it).  Then the encoded maps and the deterministic-scatter
-      // plan over the holding entries: the bricks' lattice points, the leftovers' entries.
+      // Bricks of 2 x 2 x bz elements (deterministic scatter, both integrators) take every
+      // element they can; the leftovers run the per-element line kernel, listed per
+      // 64-element block (apply_blocks ranges map to list ranges).  Then the encoded maps and
+      // the deterministic-scatter plan over the holding entries: the bricks' lattice points,
+      // the leftovers' entries.
       ECM2_VERIFY(ndofs_ < (1 << 30), ERR_UNSUPPORTED, "fused kernel supports < 2^30 dofs");
       ECM2_VERIFY((size_t)ne_ * ND_ < (1ull << 31) && ne_ < (1 << 24), ERR_UNSUPPORTED,
                   "too many elements for the line kernel's chunk table");
       auto dofv = [](int g) { return g >= 0 ? g : -1 - g; };
-      auto xface_match = [&](int e) {  // element e's high-x face == element e+1's low-x face
-         for (int dz = 0; dz < D_; dz++)
-            for (int dy = 0; dy < D_; dy++)
-            {
-               const int r = (dz * D_ + dy) * D_;
-               if (dofv(gmap_host_[(size_t)e * ND_ + r + D_ - 1]) != dofv(gmap_host_[(size_t)(e + 1) * ND_ + r]))
-               {
-                  return false;
-               }
-            }
-         return true;
-      };
       const int nblk = layout_.nblk();
-      int bz = scatter_ == SCATTER_PARTIALS ? (line_bricks_ >= 0 ? line_bricks_ : line_brick_mode()) : 0;
-      if (bz > 2 && !kern::has_brick(D_, Q_, bz)) { bz = 1; }
+      // default 2 x 2 x 1 (C5, profiles/ab_brick.sh: 0.861 ms against 1.018 ms per element and
+      // 1.114 ms for 2 x 2 x 2)
+      int bz = (scatter_ == SCATTER_PARTIALS && have_mass_ && have_diff_) ? (line_bricks_ >= 0 ? line_bricks_ : 1) : 0;
       if (bz == 2 && !kern::has_brick(D_, Q_, 2)) { bz = 1; }
       if (bz == 1 && !kern::has_brick(D_, Q_, 1)) { bz = 0; }
       std::vector<int> belem;
@@ -616,29 +494,19 @@ void PAForm::assemble(hipStream_t s)
                      b = d;
                   }
          }
-      std::vector<int> chunks, coff(nblk + 1, 0), boff(nblk + 1, 0);
+      std::vector<int> lelem, coff(nblk + 1, 0), boff(nblk + 1, 0);
       std::vector<char> holds((size_t)ne_ * ND_, 0);
-      int n_left = 0;
       for (int bk = 0; bk < nblk; bk++)
       {
-         const int eb = bk * 64, ee = std::min(ne_, eb + 64);
-         int e = eb;
-         while (e < ee)
+         for (int e = bk * 64; e < std::min(ne_, bk * 64 + 64); e++)
          {
-            if (in_brick[e]) { e++; continue; }
-            int n = 1;
-            while (n < line_chunk_max() && e + n < ee && !in_brick[e + n] && xface_match(e + n - 1)) { n++; }
-            chunks.push_back(e | (n << 24));
-            for (int k = 0; k < n; k++)
-               for (int a = 0; a < ND_; a++) { holds[(size_t)(e + k) * ND_ + a] = 1; }
-            for (int k = 0; k + 1 < n; k++)
-               for (int dz = 0; dz < D_; dz++)
-                  for (int dy = 0; dy < D_; dy++) { holds[(size_t)(e + k) * ND_ + (dz * D_ + dy) * D_ + D_ - 1] = 0; }
-            n_left += n;
-            e += n;
+            if (in_brick[e]) { continue; }
+            lelem.push_back(e);
+            for (int a = 0; a < ND_; a++) { holds[(size_t)e * ND_ + a] = 1; }
          }
-         coff[bk + 1] = (int)chunks.size();
+         coff[bk + 1] = (int)lelem.size();
       }
+      const int n_left = (int)lelem.size();
       for (int k = 0, bk = 0; bk < nblk; bk++)
       {
          while (k < n_bricks_ && belem[(size_t)k * nbe] / kElemBlock == bk) { k++; }
@@ -697,8 +565,8 @@ void PAForm::assemble(hipStream_t s)
       }
       build_shared_plan(hcount, hdof, hslot, s);
       gmap_line_.upload(enc, s);
-      chunks_.upload(chunks.empty() ? std::vector<int>{0} : chunks, s);
-      chunk_off_ = coff;
+      lelem_.upload(lelem.empty() ? std::vector<int>{0} : lelem, s);
+      lelem_off_ = coff;
       belem_.upload(belem, s);
       bmap_.upload(benc, s);
       brick_off_ = boff;
@@ -713,7 +581,7 @@ void PAForm::assemble(hipStream_t s)
       // [bricks' lattice slots | leftover elements' [e][nd] slots (when there are any)]
       part_.resize(std::max<size_t>(1, (size_t)part_line_off_ + (n_left_ ? (size_t)ne_ * ND_ : 0)));
    }
-   else { part_.resize(tpe_runs_ ? std::max<size_t>(1, (size_t)n_slots_) : (size_t)layout_.nblk() * ND_ * 64); }
+   else { part_.resize((size_t)layout_.nblk() * ND_ * 64); }
    qd_diff_.resize(have_diff_ ? layout_.diff_size() : 0);
    qd_mass_.resize(have_mass_ ? layout_.mass_size() : 0);
    // the setup kernels write every entry except the padding lanes of a partial last block
@@ -736,10 +604,10 @@ void PAForm::assemble(hipStream_t s)
    // Coefficient values at quadrature points (CoefficientVector::Project).
    auto coeff_values = [&](const CoeffDesc &c, DeviceArray<double> &tmp) -> const double * {
       if (c.kind == COEFF_QUAD) { return c.quad; }
-      if (c.kind == COEFF_GRIDFUNC_AFFINE)
+      if (c.gridfunc())
       {
          tmp.resize((size_t)ne_ * NQ_);
-         kern::coeff_gridfunc(ne_, D_, Q_, gmap_.data(), basis_, c, tmp.data(), s);
+         kern::coeff_gridfunc(ne_, D_, Q_, gmap_.data(), basis_, btab_.data(), c, tmp.data(), s);
          return tmp.data();
       }
       return nullptr;
@@ -764,6 +632,7 @@ void PAForm::assemble(hipStream_t s)
                              qd_diff_.data(), qd_mass_.data(), s);
    }
    assembled_ = true;
+   gen_++;
 }
 
 void PAForm::record_start(hipStream_t s)
@@ -840,16 +709,6 @@ void PAForm::ensure_work(hipStream_t)
    ye_.resize((size_t)ne_ * ND_);
 }
 
-// experiment knob ECM2_TPE_PP=1: the whole Mult with the plane-per-wave kernel
-static bool tpe_plane_parallel()
-{
-   static const bool v = [] {
-      const char *e = std::getenv("ECM2_TPE_PP");
-      return e && std::string(e) == "1";
-   }();
-   return v;
-}
-
 void PAForm::mult(const double *x, double *y, hipStream_t s)
 {
    ECM2_VERIFY(assembled_, ERR_STATE, "Mult before Assemble");
@@ -881,7 +740,7 @@ void PAForm::mult(const double *x, double *y, hipStream_t s)
       // exclusive dofs are plain-stored, shared ones summed from their partial slots:
       // every y entry is written exactly once, no memset, bitwise reproducible
       record_start(s);
-      apply_blocks(x, nullptr, y, nullptr, 0, layout_.nblk(), s, tpe_plane_parallel());
+      apply_blocks(x, nullptr, y, nullptr, 0, layout_.nblk(), s);
       record_stop(s);
       finish_shared(0, n_sh_, y, nullptr, s);
       return;
@@ -890,6 +749,14 @@ void PAForm::mult(const double *x, double *y, hipStream_t s)
    record_start(s);
    apply_blocks(x, nullptr, y, nullptr, 0, layout_.nblk(), s);
    record_stop(s);
+}
+
+void PAForm::add_mult(const double *x, double *y, double a, hipStream_t s)
+{
+   ECM2_VERIFY(ndofs_ == 0 || y, ERR_ARG, "null vector");
+   ywork_.resize(std::max(1, ndofs_));
+   mult(x, ywork_.data(), s);
+   kern::add_scaled(ndofs_, y, a, ywork_.data(), y, s);
 }
 
 void PAForm::set_scatter(int mode)
@@ -903,9 +770,7 @@ void PAForm::set_scatter(int mode)
 void PAForm::finish_shared(int i0, int i1, double *y, double *yg, hipStream_t s)
 {
    if (!use_partials()) { return; }
-   kern::sum_partials(i0, i1, sh_dofs_.data(), sh_meta_.data(), sh_slots_.size() ? sh_slots_.data() : nullptr,
-                      part_.data(), n_owned_, y,
-                      yg, s);
+   kern::sum_partials(i0, i1, sh_dofs_.data(), sh_meta_.data(), sh_slots_.data(), part_.data(), n_owned_, y, yg, s);
 }
 
 ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, double *yg, int b0,
@@ -925,10 +790,9 @@ ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, doubl
    a.qdm = qd_mass_.data();
    a.x = x; a.xg = xg; a.y = y; a.yg = yg;
    a.part = use_partials() ? const_cast<double *>(part_.data()) : nullptr;  // form-owned scratch
-   a.pslot = (resolved_mode_ == KERNEL_TPE && pslot_.size()) ? pslot_.data() : nullptr;
-   a.xwg = xwg_;
-   a.chunks = chunks_.data();
-   a.chunk_off = chunk_off_.empty() ? nullptr : chunk_off_.data();
+   a.btab = btab_.data();
+   a.lelem = lelem_.data();
+   a.lelem_off = lelem_off_.empty() ? nullptr : lelem_off_.data();
    if (resolved_mode_ == KERNEL_LINE && use_partials())
    {
       a.part_brick = const_cast<double *>(part_.data());
@@ -965,7 +829,7 @@ void PAForm::apply_blocks(const double *x, const double *xg, double *y, double *
    }
    else if (resolved_mode_ == KERNEL_LINE)
    {
-      kern::apply_line(D_, Q_, have_mass_, have_diff_, a, basis_, s);
+      kern::apply_line(D_, Q_, have_mass_, have_diff_, a, s);
    }
    else
    {
@@ -989,7 +853,7 @@ void PAForm::assemble_diagonal(double *diag, hipStream_t s)
    }
    ECM2_HIP(hipMemsetAsync(diag, 0, sizeof(double) * (size_t)ndofs_, s));
    kern::diagonal(layout_.pos, D_, Q_, layout_.kind, ne_, gmap_.data(), have_diff_ ? qd_diff_.data() : nullptr,
-                  have_mass_ ? qd_mass_.data() : nullptr, diag, false, basis_, s);
+                  have_mass_ ? qd_mass_.data() : nullptr, diag, false, basis_, btab_.data(), s);
 }
 
 void PAForm::restriction_mult(const double *x, double *xe, hipStream_t s)

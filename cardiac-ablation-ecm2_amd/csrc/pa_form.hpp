@@ -80,8 +80,8 @@ public:
    // (the distributed form's interior | boundary split).  The line kernel's bricks never
    // straddle one.
    void set_block_splits(const std::vector<int> &splits);
-   // Bricks of the line kernel family (p >= 3): -1 = default (ECM2_LINE_BRICK, else 2),
-   // 0 = none, 1 = 2 x 2 x 1, 2 = 2 x 2 x 2 elements per workgroup.
+   // Bricks of the line kernel family (p >= 3, both integrators, partial scatter): -1 =
+   // default (2 x 2 x 1), 0 = none, 1 = 2 x 2 x 1, 2 = 2 x 2 x 2 elements per workgroup.
    void set_line_bricks(int bz);
    // Blocks >= b are applied with the one-block-per-workgroup latency kernel (apply_blocks
    // latency = true): no cross-wave face assembly there.  -1: none.
@@ -100,6 +100,13 @@ public:
 
    // y = A x (BilinearForm::Mult semantics: y overwritten).
    void mult(const double *x, double *y, hipStream_t s);
+   // y += a A x (Operator::AddMult, linalg/operator.hpp:87-92): Mult into a work vector, then
+   // one axpy.
+   void add_mult(const double *x, double *y, double a, hipStream_t s);
+   bool assembled() const { return assembled_; }
+   // Incremented by every assemble(): whoever caches device pointers or launches of this form
+   // (the distributed form's HIP graphs) rebuilds them when it changes.
+   long generation() const { return gen_; }
    // Fused apply of element blocks [b0, b1) (64 elements per block); x / xg as in the
    // constructor's split.  Atomic scatter: accumulates into zero-initialised y / yg.
    // Partial scatter: stores the dofs held once, writes the shared ones' partial slots;
@@ -139,7 +146,7 @@ private:
    // second pass of the deterministic scatter from the shared holding entries
    // (hdof[i], hslot[i]) in ascending slot order and the per-dof holder counts
    void build_shared_plan(const std::vector<int> &hcount, const std::vector<int> &hdof,
-                          const std::vector<int> &hslot, hipStream_t s, std::vector<int> *slots_out = nullptr);
+                          const std::vector<int> &hslot, hipStream_t s);
    ApplyArgs apply_args(const double *x, const double *xg, double *y, double *yg, int b0,
                         int b1) const;
 
@@ -158,10 +165,10 @@ private:
    long n_slots_ = 0;
    DeviceArray<int> sh_dofs_, sh_slots_;           // second-pass plan (see finish_shared)
    DeviceArray<unsigned> sh_meta_;                 // start << 5 | count
-   DeviceArray<double> part_;                       // partial slots: TPE runs [n_slots] (or [blk][nd][64])
-   DeviceArray<int> pslot_;                         // TPE: [blk][nd][64] entry -> run position (-1: not shared)
-   bool tpe_runs_ = false;
+   DeviceArray<double> part_;                       // partial slots: TPE [blk][nd][64]; LINE [bricks | [e][nd]]
    bool assembled_ = false;
+   long gen_ = 0;
+   DeviceArray<double> ywork_;      // add_mult
    bool have_mass_ = false, have_diff_ = false;
    CoeffDesc cmass_, cdiff_;
 
@@ -169,8 +176,8 @@ private:
    DeviceArray<int> gmap_;          // native [e][nd]
    DeviceArray<int> gmap_blk_;      // blocked [blk][nd][64] (internal element order)
    DeviceArray<int> gmap_line_;     // LINE: [e][nd] dof | shared << 30 | sign << 31
-   DeviceArray<int> chunks_;        // LINE: first element | count << 24
-   std::vector<int> chunk_off_;     // LINE: chunks of block b = [chunk_off_[b], chunk_off_[b+1])
+   DeviceArray<int> lelem_;         // LINE: elements outside bricks
+   std::vector<int> lelem_off_;     // LINE: listed elements of block b = [lelem_off_[b], lelem_off_[b+1])
    std::vector<int> splits_;        // apply_blocks range boundaries besides 0 / nblk
    int n_bricks_ = 0, brick_bz_ = 0, brick_np_ = 0;  // LINE bricks: count, 2 x 2 x bz, lattice points
    DeviceArray<int> belem_, bmap_;  // LINE bricks: [nbrick][4 bz] elements, [nbrick][np] lattice map
@@ -181,8 +188,6 @@ private:
    bool affine_ = false;            // every element a parallelepiped (set_element_nodes)
    bool compress_ = true;           // set_geometry_compression
    int latency_from_ = -1;          // set_latency_from
-   int xwg_ = 4;                    // waves per workgroup of the face-assembly plan
-   bool auto_order_ = true;         // TPE without a caller order: face-linked 4x4x4 bricks
    bool perm_auto_ = false;         // perm_host_ was derived (not the caller's)
    DeviceArray<int> lane_flags_;    // [blk][64] in-wave merge flags
    std::vector<int> perm_host_;     // internal position -> caller element (empty: identity)
@@ -192,6 +197,7 @@ private:
    DeviceArray<double> enodes_;     // [e][3][8]
    const double *jac_ = nullptr;    // device, not owned
    DeviceArray<double> W_, rowtab_, drowtab_;
+   DeviceArray<Basis1D> btab_;      // device copy of basis_ (line / brick / diagonal / coefficient kernels)
    DeviceArray<double> qd_diff_, qd_mass_;
    DeviceArray<double> xe_, ye_;    // unfused work E-vectors
    DeviceArray<double> ctmp_m_, ctmp_d_;

@@ -80,44 +80,8 @@ double rccl_p2p_selftest(bool graph, int n)
    return err;
 }
 
-// CUs reserved for the comm stream (RCCL kernels, boundary elements, ghost sums): the
-// interior kernel runs on a stream masked to the other CUs, so the exchange chain never
-// waits for the interior's waves to retire (at C2 size one interior wave lives for the
-// whole kernel).  ECM2_COMM_CUS=0: no masks (comm stream by priority only).
-static int comm_cus()
-{
-   static const int v = [] {
-      const char *e = std::getenv("ECM2_COMM_CUS");
-      return e ? std::max(0, std::atoi(e)) : 0;
-   }();
-   return v;
-}
-
-// Interior split (percent of the interior blocks in part A, 0 = none): part A runs while the
-// exchange and the boundary elements proceed on the comm stream, part B waits for the
-// boundary kernel -- so the boundary never queues behind a full-GPU interior kernel whose
-// waves all live for the kernel's whole duration.  ECM2_INTERIOR_SPLIT.
-static int interior_split_pct()
-{
-   static const int v = [] {
-      const char *e = std::getenv("ECM2_INTERIOR_SPLIT");
-      return e ? std::max(0, std::min(100, std::atoi(e))) : 0;
-   }();
-   return v;
-}
-
-// Boundary elements with the plane-per-wave latency kernel (ECM2_BOUNDARY_PP=0: the
-// throughput kernel, whose waves each walk all planes).
-static bool boundary_pp()
-{
-   static const bool v = [] {
-      const char *e = std::getenv("ECM2_BOUNDARY_PP");
-      return !(e && std::string(e) == "0");
-   }();
-   return v;
-}
-
-// ECM2_PAR_GRAPH=0: launch the Mult's stages directly instead of replaying a captured graph.
+// ECM2_PAR_GRAPH=0: launch the Mult's stages directly instead of replaying a captured graph
+// (a debugging aid; the operator is the same).
 static bool par_graph()
 {
    static const bool v = [] {
@@ -134,24 +98,15 @@ ParPAForm::ParPAForm(const LocalPart &part, const double *enodes_local_host, int
    const int nl = part.n_owned + part.n_ghost;
    local_.reset(new PAForm(part.ne_local, part.order, nl, part.gather_map.data(), q1d, part.n_owned));
    local_->set_element_nodes(enodes_local_host);
-   // the Mult applies blocks [0, b_split) and [b_split, b_int) (interior parts A, B) and
-   // [b_int, nblk) (boundary) separately
+   // the Mult applies blocks [0, b_int) (interior) and [b_int, nblk) (boundary, with the
+   // one-block-per-workgroup latency kernel) separately
    const int bi = part.ne_interior / kElemBlock;
-   b_split_ = (int)((long)bi * interior_split_pct() / 100);
-   if (b_split_ <= 0 || b_split_ >= bi) { b_split_ = 0; }
-   if (b_split_) { local_->set_block_splits({b_split_, bi}); }
-   else { local_->set_block_splits({bi}); }
-   if (boundary_pp()) { local_->set_latency_from(bi); }  // boundary blocks: one block per workgroup
+   local_->set_block_splits({bi});
+   local_->set_latency_from(bi);
+   sched_p_ = exchange_schedule(part, false);
+   sched_t_ = exchange_schedule(part, true);
+   for (const Xfer &t : sched_p_) { pack_needed_ |= t.buf == XBUF_SENDBUF; }
    send_idx_.upload(part.send_idx);
-   pack_needed_ = false;
-   for (size_t k = 0; k < part.nbrs.size(); k++)
-   {
-      const int i0 = part.send_off[k], i1 = part.send_off[k + 1];
-      bool contig = i1 > i0;
-      for (int i = i0 + 1; i < i1 && contig; i++) { contig = part.send_idx[i] == part.send_idx[i - 1] + 1; }
-      send_start_.push_back(contig ? part.send_idx[i0] : -1);
-      pack_needed_ |= !contig && i1 > i0;
-   }
    sendbuf_.resize(std::max<size_t>(1, part.send_idx.size()));
    rbuf_.resize(std::max<size_t>(1, part.send_idx.size()));
    xg_.resize(std::max(1, part.n_ghost));
@@ -168,50 +123,39 @@ ParPAForm::ParPAForm(const LocalPart &part, const double *enodes_local_host, int
    // The comm stream (both transports) has the highest priority: the boundary elements and
    // the exchange kernels are dispatched ahead of the interior kernel's remaining
    // workgroups, so the exchange overlaps the interior instead of queueing behind it.
-   int dev = 0, ncu = 0;
-   ECM2_HIP(hipGetDevice(&dev));
-   ECM2_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-   const int k = comm_cus();
-   if (k > 0 && 4 * k <= ncu)
-   {
-      // k / 8 CUs of every 32 (one XCD's worth): balanced over the XCDs whether the mask is
-      // read linearly or per XCD
-      const int per = std::max(1, k / 8);
-      std::vector<uint32_t> cm((ncu + 31) / 32, 0u), im((ncu + 31) / 32, 0u);
-      for (int i = 0; i < ncu; i++) { (i % 32 < per ? cm : im)[i / 32] |= 1u << (i % 32); }
-      ECM2_HIP(hipExtStreamCreateWithCUMask(&cs_, (uint32_t)cm.size(), cm.data()));
-      ECM2_HIP(hipExtStreamCreateWithCUMask(&is_, (uint32_t)im.size(), im.data()));
-      ECM2_HIP(hipEventCreateWithFlags(&ev_s_, hipEventDisableTiming));
-      ECM2_HIP(hipEventCreateWithFlags(&ev_int_, hipEventDisableTiming));
-   }
-   else
-   {
-      int prio_least = 0, prio_greatest = 0;
-      ECM2_HIP(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
-      ECM2_HIP(hipStreamCreateWithPriority(&cs_, hipStreamNonBlocking, prio_greatest));
-   }
+   int prio_least = 0, prio_greatest = 0;
+   ECM2_HIP(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
+   ECM2_HIP(hipStreamCreateWithPriority(&cs_, hipStreamNonBlocking, prio_greatest));
    ECM2_HIP(hipEventCreateWithFlags(&ev_pack_, hipEventDisableTiming));
    ECM2_HIP(hipEventCreateWithFlags(&ev_xg_, hipEventDisableTiming));
    ECM2_HIP(hipEventCreateWithFlags(&ev_yg_, hipEventDisableTiming));
    ECM2_HIP(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
-   ECM2_HIP(hipEventCreateWithFlags(&ev_bnd_, hipEventDisableTiming));
    ECM2_HIP(hipDeviceSynchronize());
+}
+
+void ParPAForm::drop_graphs()
+{
+   for (auto &kv : graphs_) { (void)hipGraphExecDestroy(kv.second); }
+   graphs_.clear();
 }
 
 ParPAForm::~ParPAForm()
 {
+   drop_graphs();
    if (comm_) { (void)ncclCommDestroy((ncclComm_t)comm_); }
    if (cs_) { (void)hipStreamDestroy(cs_); }
-   if (is_) { (void)hipStreamDestroy(is_); }
-   for (auto &kv : graphs_) { (void)hipGraphExecDestroy(kv.second); }
    if (cap_) { (void)hipStreamDestroy(cap_); }
-   for (hipEvent_t e : {ev_pack_, ev_xg_, ev_yg_, ev_done_, ev_s_, ev_int_, ev_bnd_})
+   for (hipEvent_t e : {ev_pack_, ev_xg_, ev_yg_, ev_done_})
    {
       if (e) { (void)hipEventDestroy(e); }
    }
 }
 
-void ParPAForm::assemble(hipStream_t s) { local_->assemble(s); }
+void ParPAForm::assemble(hipStream_t s)
+{
+   drop_graphs();  // the local form's buffers and kernel may change
+   local_->assemble(s);
+}
 
 size_t ParPAForm::algorithmic_bytes() const
 {
@@ -223,14 +167,29 @@ size_t ParPAForm::algorithmic_bytes() const
    return 8ull * part_.ne_owned * nq * nc + 16ull * part_.n_owned + 4ull * part_.ne_owned * nd;
 }
 
+double *ParPAForm::xfer_ptr(const Xfer &t, const double *x_true)
+{
+   switch (t.buf)
+   {
+      case XBUF_X_TRUE: return const_cast<double *>(x_true) + t.off;
+      case XBUF_SENDBUF: return sendbuf_.data() + t.off;
+      case XBUF_XGHOST: return xg_.data() + t.off;
+      case XBUF_YGHOST: return yg_.data() + t.off;
+      case XBUF_RECVBUF: return rbuf_.data() + t.off;
+   }
+   ECM2_VERIFY(false, ERR_INTERNAL, "unknown exchange buffer " << t.buf);
+}
+
 // ---------------------------------------------------------------------------------------
 // Mult stages.  Per rank:
-//   s  : pack (owned interface values -> send buffer), record ev_pack
-//   cs : wait ev_pack; P exchange (ghost block <- owners); boundary elements; ghost shared
-//        sums; record ev_yg; P^T exchange (ghost block -> owners' receive buffer); ev_done
-//   s  : interior elements; wait ev_yg; owned shared sums; wait ev_done; add received
+//   s  : record ev_xg (x ready)
+//   cs : wait ev_xg; pack (owned interface values -> send buffer) if a send needs it; ev_pack
+//   s  : interior elements (enqueued first: whatever is enqueued first starts first)
+//   cs : P exchange (ghost block <- owners); boundary elements; [RAP: ghost shared sums,
+//        ev_yg, P^T exchange (ghost block -> owners' receive buffer)]; ev_done
+//   s  : wait ev_done; owned shared sums [RAP: + the received contributions]
 // The RCCL transport runs the stages of one rank in order; the loopback group enqueues
-// them stage-major over its members, with peer device copies for the exchanges, so both
+// them stage-major over its members with device copies for the exchanges, so both
 // transports share the same streams, events and overlap.
 // ---------------------------------------------------------------------------------------
 void ParPAForm::stage_pack(const double *x_true, double *y_true, hipStream_t s)
@@ -253,11 +212,9 @@ void ParPAForm::stage_pack(const double *x_true, double *y_true, hipStream_t s)
 
 void ParPAForm::stage_boundary(const double *x_true, double *y_true)
 {
-   const int b_int = part_.ne_interior / kElemBlock;
    local_->record_start_public(cs_);
-   local_->apply_blocks(x_true, xg_.data(), y_true, yg_.data(), b_int, local_->nblocks(), cs_, boundary_pp());
+   local_->apply_blocks(x_true, xg_.data(), y_true, yg_.data(), b_int(), local_->nblocks(), cs_, true);
    local_->record_stop_public(cs_);
-   ECM2_HIP(hipEventRecord(ev_bnd_, cs_));
    // ghost dofs are touched only by boundary elements: their sums are complete here (OVERLAP:
    // the ghost outputs are discarded, nothing to sum)
    if (!part_.overlap) { local_->finish_shared(local_->n_shared_owned(), local_->n_shared(), y_true, yg_.data(), cs_); }
@@ -266,178 +223,60 @@ void ParPAForm::stage_boundary(const double *x_true, double *y_true)
 
 void ParPAForm::stage_interior(const double *x_true, double *y_true, hipStream_t s)
 {
-   const int b_int = part_.ne_interior / kElemBlock;
-   hipStream_t st = s;
-   if (is_)  // interior on the CU-masked stream, ordered after s's work so far
-   {
-      ECM2_HIP(hipEventRecord(ev_s_, s));
-      ECM2_HIP(hipStreamWaitEvent(is_, ev_s_, 0));
-      st = is_;
-   }
-   if (b_split_)
-   {
-      local_->record_start_public(st);
-      local_->apply_blocks(x_true, xg_.data(), y_true, yg_.data(), 0, b_split_, st);
-      local_->record_stop_public(st);
-      ECM2_HIP(hipStreamWaitEvent(st, ev_bnd_, 0));
-      local_->record_start_public(st);
-      local_->apply_blocks(x_true, xg_.data(), y_true, yg_.data(), b_split_, b_int, st);
-      local_->record_stop_public(st);
-   }
-   else
-   {
-      local_->record_start_public(st);
-      local_->apply_blocks(x_true, xg_.data(), y_true, yg_.data(), 0, b_int, st);
-      local_->record_stop_public(st);
-   }
-   if (is_)
-   {
-      ECM2_HIP(hipEventRecord(ev_int_, is_));
-      ECM2_HIP(hipStreamWaitEvent(s, ev_int_, 0));
-   }
+   local_->record_start_public(s);
+   local_->apply_blocks(x_true, xg_.data(), y_true, yg_.data(), 0, b_int(), s);
+   local_->record_stop_public(s);
 }
 
 void ParPAForm::stage_finish(double *y_true, hipStream_t s)
 {
    ECM2_HIP(hipEventRecord(ev_done_, cs_));
-   if (part_.overlap)
-   {
-      // every contribution to an owned dof was computed here: sum the shared ones, done
-      ECM2_HIP(hipStreamWaitEvent(s, ev_done_, 0));
-      local_->finish_shared(0, local_->n_shared_owned(), y_true, yg_.data(), s);
-      return;
-   }
-   ECM2_HIP(hipStreamWaitEvent(s, ev_yg_, 0));
-   local_->finish_shared(0, local_->n_shared_owned(), y_true, yg_.data(), s);
    ECM2_HIP(hipStreamWaitEvent(s, ev_done_, 0));
-   kern::scatter_add_idx((int)part_.send_idx.size(), send_idx_.data(), rbuf_.data(), y_true, s);
+   local_->finish_shared(0, local_->n_shared_owned(), y_true, yg_.data(), s);
+   // OVERLAP: every contribution to an owned dof was computed here; RAP: add what the
+   // neighbours' ghost copies contributed (P^T)
+   if (!part_.overlap) { phase_finish(y_true, s); }
 }
 
-void ParPAForm::rccl_exchange(bool transpose)
+void ParPAForm::rccl_exchange(bool transpose, const double *x_true)
 {
    ncclComm_t comm = (ncclComm_t)comm_;
-   const int nn = (int)part_.nbrs.size();
-   if (!nn) { return; }
+   const std::vector<Xfer> &sch = schedule(transpose);
+   if (sch.empty()) { return; }
    ECM2_NCCL(ncclGroupStart());
-   for (int k = 0; k < nn; k++)
+   for (const Xfer &t : sch)
    {
-      const size_t nown = part_.send_off[k + 1] - part_.send_off[k];  // my owned dofs neighbour k ghosts
-      const size_t ngh = part_.recv_off[k + 1] - part_.recv_off[k];   // my ghosts owned by neighbour k
-      if (!transpose)
-      {
-         // P (tag 41822 in the reference): owner values -> ghost copies
-         if (nown) { ECM2_NCCL(ncclSend(send_ptr(k, x_cur_), nown, ncclFloat64, part_.nbrs[k], comm, cs_)); }
-         if (ngh) { ECM2_NCCL(ncclRecv(xg_.data() + part_.recv_off[k], ngh, ncclFloat64, part_.nbrs[k], comm, cs_)); }
-      }
-      else
-      {
-         // P^T (tag 41823): ghost contributions -> owners
-         if (ngh) { ECM2_NCCL(ncclSend(yg_.data() + part_.recv_off[k], ngh, ncclFloat64, part_.nbrs[k], comm, cs_)); }
-         if (nown) { ECM2_NCCL(ncclRecv(rbuf_.data() + part_.send_off[k], nown, ncclFloat64, part_.nbrs[k], comm, cs_)); }
-      }
+      double *p = xfer_ptr(t, x_true);
+      if (t.send) { ECM2_NCCL(ncclSend(p, t.count, ncclFloat64, t.peer, comm, cs_)); }
+      else { ECM2_NCCL(ncclRecv(p, t.count, ncclFloat64, t.peer, comm, cs_)); }
    }
    ECM2_NCCL(ncclGroupEnd());
 }
 
-// Measurement aid (ECM2_EMULATE_EXCHANGE=1, no RCCL communicator): one rank of an N-rank
-// partition run alone on one GPU, each exchange replaced by same-size device copies from the
-// rank's own buffers on the comm stream.  The values are NOT the operator's; the stream /
-// event / CU structure and every kernel are the RCCL rank's, so its timeline shows whether
-// the boundary chain hides behind the interior (bench.py --emulate-rank).
-static bool emulate_exchange()
+void ParPAForm::mult_stages(const double *x_true, double *y_true, hipStream_t s)
 {
-   static const bool v = [] {
-      const char *e = std::getenv("ECM2_EMULATE_EXCHANGE");
-      return e && std::string(e) == "1";
-   }();
-   return v;
-}
-
-void ParPAForm::self_exchange(bool transpose)
-{
-   for (size_t k = 0; k < part_.nbrs.size(); k++)
-   {
-      const size_t nown = part_.send_off[k + 1] - part_.send_off[k];
-      const size_t ngh = part_.recv_off[k + 1] - part_.recv_off[k];
-      if (!transpose && ngh)
-      {
-         // a same-size copy from this rank's own send range stands in for the peer's
-         const size_t n = std::min(ngh, nown ? nown : sendbuf_.size());
-         const double *src = nown ? send_ptr((int)k, x_cur_) : sendbuf_.data();
-         ECM2_HIP(hipMemcpyAsync(xg_.data() + part_.recv_off[k], src, n * sizeof(double),
-                                 hipMemcpyDeviceToDevice, cs_));
-      }
-      if (transpose && nown)
-      {
-         const size_t n = std::min(nown, yg_.size());
-         ECM2_HIP(hipMemcpyAsync(rbuf_.data() + part_.send_off[k], yg_.data(), n * sizeof(double),
-                                 hipMemcpyDeviceToDevice, cs_));
-      }
-   }
-}
-
-// Enqueue the interior elements before the exchange chain (ECM2_INTERIOR_FIRST=0: after):
-// each host call costs microseconds, so whatever is enqueued first starts first; the
-// interior kernel leaves wave slots free for the comm stream's boundary kernel.
-static bool interior_first()
-{
-   static const bool v = [] {
-      const char *e = std::getenv("ECM2_INTERIOR_FIRST");
-      return !(e && std::string(e) == "0");
-   }();
-   return v;
-}
-
-// OVERLAP with the boundary on the caller's stream after the interior (ECM2_PAR_SERIAL=1):
-// only the exchange runs on the comm stream, and the one cross-stream wait (for P) is long
-// satisfied when the interior ends -- no join after the boundary kernel.
-static bool par_serial()
-{
-   static const bool v = [] {
-      const char *e = std::getenv("ECM2_PAR_SERIAL");
-      return e && std::string(e) == "1";
-   }();
-   return v;
-}
-
-void ParPAForm::mult_stages(const double *x_true, double *y_true, hipStream_t s, bool emu)
-{
-   x_cur_ = x_true;
-   if (part_.overlap && par_serial() && !b_split_ && !is_)
-   {
-      stage_pack(x_true, y_true, s);
-      stage_interior(x_true, y_true, s);
-      if (emu) { self_exchange(false); } else { rccl_exchange(false); }
-      ECM2_HIP(hipEventRecord(ev_done_, cs_));
-      ECM2_HIP(hipStreamWaitEvent(s, ev_done_, 0));
-      local_->record_start_public(s);
-      local_->apply_blocks(x_true, xg_.data(), y_true, yg_.data(), b_int(), local_->nblocks(), s, boundary_pp());
-      local_->record_stop_public(s);
-      local_->finish_shared(0, local_->n_shared_owned(), y_true, yg_.data(), s);
-      return;
-   }
-   const bool first = interior_first() && !b_split_;  // part B of a split waits for the boundary
    stage_pack(x_true, y_true, s);
-   if (first) { stage_interior(x_true, y_true, s); }
-   if (emu) { self_exchange(false); } else { rccl_exchange(false); }
+   stage_interior(x_true, y_true, s);
+   rccl_exchange(false, x_true);
    stage_boundary(x_true, y_true);
-   if (!part_.overlap)
-   {
-      if (emu) { self_exchange(true); } else { rccl_exchange(true); }
-   }
-   if (!first) { stage_interior(x_true, y_true, s); }
+   if (!part_.overlap) { rccl_exchange(true, x_true); }
    stage_finish(y_true, s);
 }
 
 void ParPAForm::mult(const double *x_true, double *y_true, hipStream_t s)
 {
-   const bool emu = !comm_ && emulate_exchange();
-   ECM2_VERIFY(comm_ || emu, ERR_STATE, "mult needs the RCCL transport (use the loopback group otherwise)");
+   ECM2_VERIFY(comm_, ERR_STATE, "mult needs the RCCL transport (use the loopback group otherwise)");
+   ECM2_VERIFY(local_->assembled(), ERR_STATE, "Mult before Assemble");
+   if (graph_gen_ != local_->generation())
+   {
+      drop_graphs();  // the cached graphs bake in the previous assembly's buffers and kernels
+      graph_gen_ = local_->generation();
+   }
    if (!par_graph() || graph_failed_ || local_->timing_on() || !p2p_warm_)
    {
       // the first Mult runs directly on every rank: RCCL sets up its peer connections
       // lazily at the first send/recv, which then happens outside a stream capture
-      mult_stages(x_true, y_true, s, emu);
+      mult_stages(x_true, y_true, s);
       p2p_warm_ = true;
       return;
    }
@@ -448,13 +287,14 @@ void ParPAForm::mult(const double *x_true, double *y_true, hipStream_t s)
    auto it = graphs_.find(key);
    if (it == graphs_.end())
    {
+      if (graphs_.size() >= kMaxGraphs) { drop_graphs(); }  // callers cycling through temporaries
       if (!cap_) { ECM2_HIP(hipStreamCreateWithFlags(&cap_, hipStreamNonBlocking)); }
       hipGraph_t g = nullptr;
       hipGraphExec_t ge = nullptr;
       ECM2_HIP(hipStreamBeginCapture(cap_, hipStreamCaptureModeThreadLocal));
       try
       {
-         mult_stages(x_true, y_true, cap_, emu);
+         mult_stages(x_true, y_true, cap_);
       }
       catch (...)
       {
@@ -462,7 +302,7 @@ void ParPAForm::mult(const double *x_true, double *y_true, hipStream_t s)
          if (g) { (void)hipGraphDestroy(g); }
          (void)hipGetLastError();
          graph_failed_ = true;
-         mult_stages(x_true, y_true, s, emu);
+         mult_stages(x_true, y_true, s);
          return;
       }
       ECM2_HIP(hipStreamEndCapture(cap_, &g));
@@ -472,7 +312,7 @@ void ParPAForm::mult(const double *x_true, double *y_true, hipStream_t s)
       {
          (void)hipGetLastError();
          graph_failed_ = true;
-         mult_stages(x_true, y_true, s, emu);
+         mult_stages(x_true, y_true, s);
          return;
       }
       it = graphs_.emplace(key, ge).first;
@@ -499,22 +339,14 @@ void ParPAForm::diag_local(double *d_true, hipStream_t s)
 void ParPAForm::assemble_diagonal(double *d_true, hipStream_t s)
 {
    ECM2_VERIFY(comm_, ERR_STATE, "assemble_diagonal needs the RCCL transport (use the loopback group otherwise)");
-   ncclComm_t comm = (ncclComm_t)comm_;
    diag_local(d_true, s);
    if (part_.overlap) { return; }  // owned entries complete locally
-   const int nn = (int)part_.nbrs.size();
-   if (nn)
-   {
-      ECM2_NCCL(ncclGroupStart());
-      for (int k = 0; k < nn; k++)
-      {
-         const size_t ns = part_.recv_off[k + 1] - part_.recv_off[k];
-         const size_t nr = part_.send_off[k + 1] - part_.send_off[k];
-         if (ns) { ECM2_NCCL(ncclSend(yg_.data() + part_.recv_off[k], ns, ncclFloat64, part_.nbrs[k], comm, s)); }
-         if (nr) { ECM2_NCCL(ncclRecv(rbuf_.data() + part_.send_off[k], nr, ncclFloat64, part_.nbrs[k], comm, s)); }
-      }
-      ECM2_NCCL(ncclGroupEnd());
-   }
+   // P^T of the ghost entries, on s
+   ECM2_HIP(hipEventRecord(ev_xg_, s));
+   ECM2_HIP(hipStreamWaitEvent(cs_, ev_xg_, 0));
+   rccl_exchange(true, nullptr);
+   ECM2_HIP(hipEventRecord(ev_done_, cs_));
+   ECM2_HIP(hipStreamWaitEvent(s, ev_done_, 0));
    phase_finish(d_true, s);
 }
 
@@ -523,6 +355,38 @@ void ParPAForm::allreduce_sum(double *dev, int n, hipStream_t s)
    ECM2_VERIFY(comm_, ERR_STATE, "allreduce needs the RCCL transport");
    ECM2_NCCL(ncclAllReduce(dev, dev, n, ncclFloat64, ncclSum, (ncclComm_t)comm_, s));
 }
+
+namespace
+{
+// The loopback transport of one exchange: every receive of member r copies, on r's comm
+// stream and after the peer's `ready` event, the matching send of the peer's schedule (the
+// one addressed to r: a pair of ranks exchanges one block per direction).
+void group_exchange(std::vector<ParPAForm *> &forms, const std::vector<const double *> &x, bool transpose,
+                    hipEvent_t (ParPAForm::*ready)() const)
+{
+   const int n = (int)forms.size();
+   for (int r = 0; r < n; r++)
+   {
+      ParPAForm &f = *forms[r];
+      for (const Xfer &t : f.schedule(transpose))
+      {
+         if (t.send) { continue; }
+         ECM2_VERIFY(t.peer >= 0 && t.peer < n, ERR_INTERNAL, "exchange peer " << t.peer << " outside the group");
+         ParPAForm &o = *forms[t.peer];
+         const Xfer *m = nullptr;
+         for (const Xfer &u : o.schedule(transpose))
+         {
+            if (u.send && u.peer == r) { m = &u; break; }
+         }
+         ECM2_VERIFY(m && m->count == t.count, ERR_INTERNAL,
+                     "exchange schedules of ranks " << r << " and " << t.peer << " do not match");
+         ECM2_HIP(hipStreamWaitEvent(f.comm_stream(), (o.*ready)(), 0));
+         ECM2_HIP(hipMemcpyAsync(f.xfer_ptr(t, x[r]), o.xfer_ptr(*m, x[t.peer]), t.count * sizeof(double),
+                                 hipMemcpyDeviceToDevice, f.comm_stream()));
+      }
+   }
+}
+} // namespace
 
 void par_group_mult(std::vector<ParPAForm *> &forms, const std::vector<const double *> &x,
                     const std::vector<double *> &y, hipStream_t s)
@@ -533,91 +397,38 @@ void par_group_mult(std::vector<ParPAForm *> &forms, const std::vector<const dou
    {
       ECM2_VERIFY(forms[r]->part().rank == r && forms[r]->part().nranks == n, ERR_ARG,
                   "loopback group: form " << r << " has rank " << forms[r]->part().rank);
+      ECM2_VERIFY(forms[r]->local().assembled(), ERR_STATE, "Mult before Assemble");
    }
-   auto slot = [&](int s_rank, int r_rank) {  // index of r_rank in s_rank's neighbour list
-      const auto &nb = forms[s_rank]->part().nbrs;
-      const auto it = std::find(nb.begin(), nb.end(), r_rank);
-      ECM2_VERIFY(it != nb.end(), ERR_INTERNAL, "asymmetric neighbour lists");
-      return (int)(it - nb.begin());
-   };
    // the same stages as ParPAForm::mult, stage-major over the members; a member's
    // exchanges wait for its peers' events and copy from their buffers on its comm stream
    for (int r = 0; r < n; r++) { forms[r]->stage_pack(x[r], y[r], s); }
-   for (int r = 0; r < n; r++)
-   {
-      ParPAForm &f = *forms[r];
-      const LocalPart &pr = f.part();
-      for (size_t k = 0; k < pr.nbrs.size(); k++)
-      {
-         const int o = pr.nbrs[k], j = slot(o, r);
-         const LocalPart &po = forms[o]->part();
-         const size_t cnt = pr.recv_off[k + 1] - pr.recv_off[k];
-         ECM2_VERIFY(cnt == (size_t)(po.send_off[j + 1] - po.send_off[j]), ERR_INTERNAL,
-                     "exchange size mismatch " << r << "<-" << o);
-         if (!cnt) { continue; }
-         ECM2_HIP(hipStreamWaitEvent(f.comm_stream(), forms[o]->event_packed(), 0));
-         ECM2_HIP(hipMemcpyAsync(f.xghost() + pr.recv_off[k], forms[o]->send_ptr(j, x[o]),
-                                 cnt * sizeof(double), hipMemcpyDeviceToDevice, f.comm_stream()));
-      }
-   }
+   group_exchange(forms, x, false, &ParPAForm::event_packed);
    for (int r = 0; r < n; r++) { forms[r]->stage_boundary(x[r], y[r]); }
-   for (int r = 0; r < n; r++)
-   {
-      ParPAForm &f = *forms[r];
-      if (f.part().overlap) { continue; }  // no P^T
-      const LocalPart &pr = f.part();
-      for (size_t k = 0; k < pr.nbrs.size(); k++)
-      {
-         const int g = pr.nbrs[k], j = slot(g, r);
-         const LocalPart &pg = forms[g]->part();
-         const size_t cnt = pr.send_off[k + 1] - pr.send_off[k];
-         ECM2_VERIFY(cnt == (size_t)(pg.recv_off[j + 1] - pg.recv_off[j]), ERR_INTERNAL,
-                     "reduce size mismatch " << r << "<-" << g);
-         if (!cnt) { continue; }
-         ECM2_HIP(hipStreamWaitEvent(f.comm_stream(), forms[g]->event_ghosts_summed(), 0));
-         ECM2_HIP(hipMemcpyAsync(f.recvbuf() + pr.send_off[k], forms[g]->yghost() + pg.recv_off[j],
-                                 cnt * sizeof(double), hipMemcpyDeviceToDevice, f.comm_stream()));
-      }
-   }
+   if (!forms.empty() && !forms[0]->part().overlap) { group_exchange(forms, x, true, &ParPAForm::event_ghosts_summed); }
    for (int r = 0; r < n; r++) { forms[r]->stage_interior(x[r], y[r], s); }
    for (int r = 0; r < n; r++) { forms[r]->stage_finish(y[r], s); }
-}
-
-} // namespace ecm2
-
-namespace ecm2
-{
-// P^T of the loopback group: every member's ghost block (yghost) copied into its owner's
-// receive buffer, then added into the owner's true vector.
-static void group_reduce_ghosts(std::vector<ParPAForm *> &forms, const std::vector<double *> &y, hipStream_t s)
-{
-   const int n = (int)forms.size();
-   for (int r = 0; r < n; r++)
-   {
-      const LocalPart &pr = forms[r]->part();
-      for (size_t k = 0; k < pr.nbrs.size(); k++)
-      {
-         const int g = pr.nbrs[k];
-         const auto &nb = forms[g]->part().nbrs;
-         const int j = (int)(std::find(nb.begin(), nb.end(), r) - nb.begin());
-         ECM2_VERIFY(j < (int)nb.size(), ERR_INTERNAL, "asymmetric neighbour lists");
-         const LocalPart &pg = forms[g]->part();
-         const size_t cnt = pr.send_off[k + 1] - pr.send_off[k];
-         if (cnt)
-         {
-            ECM2_HIP(hipMemcpyAsync(forms[r]->recvbuf() + pr.send_off[k], forms[g]->yghost() + pg.recv_off[j],
-                                    cnt * sizeof(double), hipMemcpyDeviceToDevice, s));
-         }
-      }
-   }
-   for (int r = 0; r < n; r++) { forms[r]->phase_finish(y[r], s); }
 }
 
 void par_group_diagonal(std::vector<ParPAForm *> &forms, const std::vector<double *> &d, hipStream_t s)
 {
    ECM2_VERIFY(d.size() == forms.size(), ERR_ARG, "group size mismatch");
    for (size_t r = 0; r < forms.size(); r++) { forms[r]->diag_local(d[r], s); }
-   if (!forms.empty() && forms[0]->part().overlap) { return; }  // owned entries complete locally
-   group_reduce_ghosts(forms, d, s);
+   if (forms.empty() || forms[0]->part().overlap) { return; }  // owned entries complete locally
+   // P^T of the ghost entries: everything on s (the comm streams wait for it)
+   hipEvent_t ev;
+   ECM2_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+   ECM2_HIP(hipEventRecord(ev, s));
+   for (ParPAForm *f : forms) { ECM2_HIP(hipStreamWaitEvent(f->comm_stream(), ev, 0)); }
+   std::vector<const double *> none(forms.size(), nullptr);
+   for (ParPAForm *f : forms) { ECM2_HIP(hipEventRecord(f->event_ghosts_summed(), f->comm_stream())); }
+   group_exchange(forms, none, true, &ParPAForm::event_ghosts_summed);
+   for (ParPAForm *f : forms)
+   {
+      ECM2_HIP(hipEventRecord(ev, f->comm_stream()));
+      ECM2_HIP(hipStreamWaitEvent(s, ev, 0));
+   }
+   (void)hipEventDestroy(ev);
+   for (size_t r = 0; r < forms.size(); r++) { forms[r]->phase_finish(d[r], s); }
 }
+
 } // namespace ecm2

@@ -8,9 +8,10 @@
 //
 // MI355X design: one process per GPU; the local L-vector is [owned | ghost] so P is
 // "receive the ghost block in place" and P^T is "send the ghost block in place, add
-// what arrives into the owned interface dofs"; the exchange is one grouped
-// ncclSend/ncclRecv per direction on a dedicated comm stream, overlapped with the
-// interior elements (those touching no ghost dof), which run before the boundary ones.
+// what arrives into the owned interface dofs"; each exchange is one grouped
+// ncclSend/ncclRecv over the partition's exchange schedule (partition.hpp) on a dedicated
+// comm stream, overlapped with the interior elements (those touching no ghost dof), which
+// are enqueued before the boundary ones.
 #pragma once
 
 #include "pa_form.hpp"
@@ -28,7 +29,7 @@ class ParPAForm
 {
 public:
    // rccl_id: 128-byte ncclUniqueId shared by all ranks (RCCL transport), or null for a
-   // member of an in-process loopback group (ParGroup).
+   // member of an in-process loopback group (par_group_mult).
    ParPAForm(const LocalPart &part, const double *enodes_local_host, int q1d,
              const unsigned char *rccl_id);
    ~ParPAForm();
@@ -49,7 +50,7 @@ public:
    // Pieces of assemble_diagonal shared with the loopback group.
    void diag_local(double *d_true, hipStream_t s);  // d_true = owned part, ghost part -> yghost()
 
-   // Mult stages (par_form.cpp), shared by the RCCL transport and the loopback group.
+   // Mult stages, shared by the RCCL transport and the loopback group.
    void stage_pack(const double *x_true, double *y_true, hipStream_t s);
    void stage_boundary(const double *x_true, double *y_true);   // on the comm stream
    void stage_interior(const double *x_true, double *y_true, hipStream_t s);
@@ -62,51 +63,43 @@ public:
    hipEvent_t event_packed() const { return ev_pack_; }
    hipEvent_t event_ghosts_summed() const { return ev_yg_; }
 
-   // buffers (device)
-   double *sendbuf() { return sendbuf_.data(); }
-   // P send buffer of neighbour slot k: x_true itself where the rank's owned dofs that
-   // neighbour k ghosts form one contiguous range (z-slabs: the top dof planes), else the
-   // packed buffer.
-   const double *send_ptr(int k, const double *x_true) const
-   {
-      return send_start_[k] >= 0 ? x_true + send_start_[k] : sendbuf_.data() + part_.send_off[k];
-   }
-   double *xghost() { return xg_.data(); }
-   double *yghost() { return yg_.data(); }
-   double *recvbuf() { return rbuf_.data(); }
+   // The exchange schedule of P / P^T (exchange_schedule) and the device address of one
+   // transfer's data (x_true: the true vector of the Mult being enqueued).
+   const std::vector<Xfer> &schedule(bool transpose) const { return transpose ? sched_t_ : sched_p_; }
+   double *xfer_ptr(const Xfer &t, const double *x_true);
 
 private:
-   void rccl_exchange(bool transpose);  // P (false) or P^T (true) on the comm stream
-   void mult_stages(const double *x_true, double *y_true, hipStream_t s, bool emu);
+   void rccl_exchange(bool transpose, const double *x_true);  // grouped send/recv on the comm stream
+   void mult_stages(const double *x_true, double *y_true, hipStream_t s);
    int b_int() const { return part_.ne_interior / kElemBlock; }
-   int b_split_ = 0;                    // interior part A = [0, b_split_) (0: no split)
-   std::vector<int> send_start_;        // per neighbour: first owned index of a contiguous send range, or -1
-   bool pack_needed_ = true;            // some neighbour's send range is not contiguous
-   const double *x_cur_ = nullptr;      // x_true of the Mult being enqueued (contiguous sends)
-   hipEvent_t ev_bnd_ = nullptr;        // boundary elements applied (comm stream)
-   // Mult as a HIP graph per (x, y) pair: one launch instead of ~15 API calls
-   hipStream_t cap_ = nullptr;          // capture stream
-   std::map<std::pair<const double *, double *>, hipGraphExec_t> graphs_;
-   bool graph_failed_ = false;
-   bool p2p_warm_ = false;  // one direct Mult ran (RCCL peer connections exist) before any capture
+   void drop_graphs();
    LocalPart part_;
    std::unique_ptr<PAForm> local_;
+   std::vector<Xfer> sched_p_, sched_t_;
+   bool pack_needed_ = false;           // some P send goes through the packed buffer
    DeviceArray<int> send_idx_;
    DeviceArray<double> sendbuf_, xg_, yg_, rbuf_, dl_;
-   void *comm_ = nullptr;  // ncclComm_t
-   void self_exchange(bool transpose);  // ECM2_EMULATE_EXCHANGE measurement aid
-   hipStream_t cs_ = nullptr;
-   hipStream_t is_ = nullptr;       // interior stream, CU-masked against cs_ (null: interior on the caller's stream)
-   hipEvent_t ev_s_ = nullptr, ev_int_ = nullptr;
+   void *comm_ = nullptr;               // ncclComm_t
+   hipStream_t cs_ = nullptr;           // comm stream (highest priority)
    hipEvent_t ev_pack_ = nullptr, ev_xg_ = nullptr, ev_yg_ = nullptr, ev_done_ = nullptr;
+   // The Mult as a HIP graph per (x, y) pair: one launch instead of ~15 API calls.  A graph
+   // bakes in the local form's buffers and kernels, so the cache belongs to one assembly of
+   // it (generation) and holds at most kMaxGraphs entries.
+   static constexpr size_t kMaxGraphs = 4;
+   hipStream_t cap_ = nullptr;          // capture stream
+   std::map<std::pair<const double *, double *>, hipGraphExec_t> graphs_;
+   long graph_gen_ = -1;
+   bool graph_failed_ = false;
+   bool p2p_warm_ = false;  // one direct Mult ran (RCCL peer connections exist) before any capture
 };
 
 // RCCL point-to-point self-test (one-rank communicator, direct or graph-captured): max error.
 double rccl_p2p_selftest(bool graph, int n);
 
-// In-process loopback group: all subdomains on one GPU, exchanges by device copies.
-// Exercises partition, pack/unpack, split-vector kernels and interior/boundary
-// ordering without RCCL (which cannot put two ranks on one device).
+// In-process loopback group: all subdomains on one GPU, exchanges by device copies that
+// follow the members' exchange schedules (each receive copies the peer's matching send).
+// Exercises partition, schedule, split-vector kernels and interior/boundary ordering without
+// RCCL (which cannot put two ranks on one device).
 void par_group_mult(std::vector<ParPAForm *> &forms, const std::vector<const double *> &x,
                     const std::vector<double *> &y, hipStream_t s);
 void par_group_diagonal(std::vector<ParPAForm *> &forms, const std::vector<double *> &d, hipStream_t s);

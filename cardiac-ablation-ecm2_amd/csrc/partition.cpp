@@ -140,4 +140,32 @@ LocalPart build_local_part(const H1Space &s, const std::vector<int> &elem_rank, 
    return p;
 }
 
+std::vector<Xfer> exchange_schedule(const LocalPart &p, bool transpose)
+{
+   std::vector<Xfer> out;
+   for (size_t k = 0; k < p.nbrs.size(); k++)
+   {
+      const int s0 = p.send_off[k], s1 = p.send_off[k + 1];  // my owned dofs neighbour k ghosts
+      const int r0 = p.recv_off[k], r1 = p.recv_off[k + 1];  // my ghosts owned by neighbour k
+      const int nb = p.nbrs[k];
+      if (!transpose)
+      {
+         if (s1 > s0)
+         {
+            bool contig = true;
+            for (int i = s0 + 1; i < s1 && contig; i++) { contig = p.send_idx[i] == p.send_idx[i - 1] + 1; }
+            out.push_back(contig ? Xfer{nb, 1, XBUF_X_TRUE, p.send_idx[s0], s1 - s0}
+                                 : Xfer{nb, 1, XBUF_SENDBUF, s0, s1 - s0});
+         }
+         if (r1 > r0) { out.push_back(Xfer{nb, 0, XBUF_XGHOST, r0, r1 - r0}); }
+      }
+      else
+      {
+         if (r1 > r0) { out.push_back(Xfer{nb, 1, XBUF_YGHOST, r0, r1 - r0}); }
+         if (s1 > s0) { out.push_back(Xfer{nb, 0, XBUF_RECVBUF, s0, s1 - s0}); }
+      }
+   }
+   return out;
+}
+
 } // namespace ecm2

@@ -44,6 +44,24 @@ struct LocalPart
    std::vector<int> recv_off;           // P: ghost block of nbrs[k] = [n_owned+recv_off[k], n_owned+recv_off[k+1])
 };
 
+// One point-to-point transfer of an exchange: the unit both transports of the distributed
+// form consume (the RCCL form issues one ncclSend / ncclRecv per entry inside one group; the
+// in-process loopback group one device copy per receive, from the peer's matching send).
+// Buffers of a rank: its true vector x, the packed send buffer, the ghost blocks of x and y,
+// the P^T receive buffer; off / count in doubles.
+enum XferBuf : int { XBUF_X_TRUE = 0, XBUF_SENDBUF = 1, XBUF_XGHOST = 2, XBUF_YGHOST = 3, XBUF_RECVBUF = 4 };
+struct Xfer
+{
+   int peer, send, buf, off, count;
+};
+// P (transpose = false, the reference's tag 41822, pfespace.cpp:5394-5440): each neighbour's
+// owned interface values -> this rank's ghost block; sent straight from x where the values a
+// neighbour needs are one contiguous owned range (z-slabs), else from the packed buffer.  P^T
+// (transpose = true, tag 41823, pfespace.cpp:5496-5532): ghost contributions -> the owners'
+// receive buffers.  Entries in neighbour order, per neighbour its send before its receive;
+// empty transfers are omitted.
+std::vector<Xfer> exchange_schedule(const LocalPart &p, bool transpose);
+
 // CartesianPartitioning along z of a lexicographic Cartesian mesh (mesh.cpp:8966 semantics
 // for a 1 x 1 x nranks grid): elem_rank[e].
 std::vector<int> partition_slabs_z(const HexMesh &m, int nranks);

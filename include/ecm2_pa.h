@@ -39,6 +39,13 @@ extern "C" {
 #define ECM2_COEFF_CONSTANT 0       /* ConstantCoefficient                                   */
 #define ECM2_COEFF_QUAD 1           /* values at quadrature points, device [ne][nq]          */
 #define ECM2_COEFF_GRIDFUNC_AFFINE 2/* scale*(1+slope*(T(x_q)-t_ref)), T an H1 L-vector       */
+/* Pennes heat capacity + perfusion of the implicit stage's mass coefficient, T an H1 L-vector:
+ *   alpha(T) = rho_c + gdt_cb * w_b(T),  w_b(T) = w0 * max(0, 1 + a (T - t0)) for T < t_stop,
+ *   0 at or above t_stop (perfusion shut-down in coagulated tissue);
+ * params[0..5] = (rho_c, gdt_cb, w0, a, t0, t_stop).  T is projected to the quadrature points
+ * like a GridFunctionCoefficient (qfunction.cpp:73-98, coefficient.cpp:2052-2070); the law
+ * itself is the bioheat application's (not in the reference snapshot: parity-unpinned). */
+#define ECM2_COEFF_GRIDFUNC_PERFUSION 3
 
 /* Kernel selection (all produce the same operator). */
 #define ECM2_KERNEL_AUTO 0     /* TPE for p <= 2, LINE for p = 3..6                 */
@@ -153,11 +160,11 @@ int ecm2_pa_form_set_kernel(ecm2_pa_form *f, int kernel);
 int ecm2_pa_form_set_scatter(ecm2_pa_form *f, int mode);
 /* Work grouping of the p >= 3 line-kernel family (no reference counterpart; the
  * reference applies each element independently, bilininteg_diffusion_kernels.hpp:989-1214):
- * bz = -1 default (2 x 2 x 1), 0 = per-element line
- * kernel only, 1 = bricks of 2 x 2 x 1 elements, 2 = 2 x 2 x 2, 4 / 8 = 2 x 2 x bz column
- * bricks marched layer by layer (p = 3..6; bz = 8 only at p = 4).  A brick is one workgroup;
- * its internal shared faces are summed in LDS in a fixed order (deterministic).  Bricks
- * exist only with ECM2_SCATTER_PARTIALS; elements outside bricks use the line kernel. */
+ * bz = -1 default (2 x 2 x 1), 0 = per-element line kernel only, 1 = bricks of 2 x 2 x 1
+ * elements, 2 = 2 x 2 x 2 (p = 3..6 with the default rule).  A brick is one workgroup; its
+ * internal shared faces are summed in LDS in a fixed order (deterministic).  Bricks exist only
+ * with ECM2_SCATTER_PARTIALS and both integrators; elements outside bricks use the line
+ * kernel. */
 int ecm2_pa_form_set_bricks(ecm2_pa_form *f, int bz);
 /* After assemble: bricks formed and their depth (0 = none). */
 int ecm2_pa_form_brick_info(const ecm2_pa_form *f, int *n_bricks, int *bz);
@@ -174,6 +181,12 @@ int ecm2_pa_form_assemble(ecm2_pa_form *f, void *stream);
 /* BilinearForm::Mult / PABilinearFormExtension::Mult (bilinearform.cpp:1244-1254,
  * bilinearform_ext.cpp:487-564): y = A x, y overwritten.  x, y device [ndofs]. */
 int ecm2_pa_form_mult(ecm2_pa_form *f, const double *x, double *y, void *stream);
+/* PABilinearFormExtension::MultTranspose (bilinearform_ext.hpp:99, bilinearform_ext.cpp:
+ * 566-677): y = A^T x.  Mass + Diffusion with scalar coefficients are symmetric, so this is
+ * the Mult (tests/test_gpu_parity.py asserts the equality). */
+int ecm2_pa_form_mult_transpose(ecm2_pa_form *f, const double *x, double *y, void *stream);
+/* Operator::AddMult (linalg/operator.hpp:87-92): y += a A x. */
+int ecm2_pa_form_add_mult(ecm2_pa_form *f, const double *x, double *y, double a, void *stream);
 /* PABilinearFormExtension::AssembleDiagonal (bilinearform_ext.cpp:370-454). diag device [ndofs]. */
 int ecm2_pa_form_assemble_diagonal(ecm2_pa_form *f, double *diag, void *stream);
 /* ElementRestriction::Mult / MultTranspose (restriction.cpp:109-186). xe device [ne][nd]. */
@@ -277,6 +290,14 @@ int ecm2_partition_info(const ecm2_partition *p, int *ne_local, int *ne_interior
  * [n_nbrs+1], send_idx [n_send] (owned local indices). */
 int ecm2_partition_get(const ecm2_partition *p, int *elems, int *local_to_global, int *gather_map,
                        int *nbrs, int *send_off, int *send_idx, int *recv_off);
+/* The exchange schedule both transports consume (no reference counterpart; the reference's
+ * per-neighbour MPI_Isend/Irecv of DeviceConformingProlongationOperator, pfespace.cpp:
+ * 5394-5440 / 5496-5532, in one list): transpose = 0 for P (owners -> ghost copies), 1 for
+ * P^T.  Rows of 5 ints (peer, send, buffer, offset, count), buffer 0 = the true vector x,
+ * 1 = the packed send buffer [n_send], 2 = the ghost block of x [n_ghost], 3 = the ghost
+ * block of y, 4 = the P^T receive buffer [n_send].  Two-call pattern: out may be NULL to
+ * query *count.  Host only. */
+int ecm2_partition_exchange_schedule(const ecm2_partition *p, int transpose, int *out, int *count);
 /* ~ParFiniteElementSpace / ~ParMesh of the local view. */
 void ecm2_partition_destroy(ecm2_partition *p);
 
@@ -313,7 +334,10 @@ int ecm2_par_form_assemble(ecm2_par_form *f, void *stream);
  * [n_owned].  Grouped ncclSend/ncclRecv on an internal stream overlapped with the
  * interior elements. */
 int ecm2_par_form_mult(ecm2_par_form *f, const double *x_true, double *y_true, void *stream);
-/* All subdomains of one partition in this process on one GPU (exchange by device copies). */
+/* RAPOperator::MultTranspose (operator.hpp:979): P^T A^T P = P^T A P (A symmetric). */
+int ecm2_par_form_mult_transpose(ecm2_par_form *f, const double *x_true, double *y_true, void *stream);
+/* All subdomains of one partition in this process on one GPU (exchange by device copies that
+ * follow the members' exchange schedules). */
 int ecm2_par_group_mult(ecm2_par_form *const *forms, int n, const double *const *x_true,
                         double *const *y_true, void *stream);
 /* ParBilinearForm::AssembleDiagonal on the true dofs (local PA diagonal + P^T). */

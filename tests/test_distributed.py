@@ -258,3 +258,50 @@ def test_gpu_rccl_p2p_graph_capture(graph):
     of the distributed Mult's graph replay."""
     E.load_library()
     assert E.rccl_p2p_selftest(graph, 10201) == 0.0
+
+
+def _ids(part, row):
+    """Global dof ids a schedule row moves, in transfer order."""
+    peer, send, buf, off, cnt = (int(v) for v in row)
+    if buf == E.Partition.XBUF_X_TRUE:
+        return part.owned_global[off: off + cnt]
+    if buf in (E.Partition.XBUF_SENDBUF, E.Partition.XBUF_RECVBUF):
+        return part.owned_global[part.send_idx[off: off + cnt]]
+    assert buf in (E.Partition.XBUF_XGHOST, E.Partition.XBUF_YGHOST)
+    return part.local_to_global[part.n_owned + off: part.n_owned + off + cnt]
+
+
+@pytest.mark.parametrize("kind", ["slabs", "random"])
+@pytest.mark.parametrize("nranks", [2, 3, 5, 8])
+@pytest.mark.parametrize("decomp", ["rap", "overlap"])
+def test_exchange_schedule_pairs(kind, nranks, decomp):
+    """The one (peer, buffer, offset, count) schedule both transports consume
+    (ecm2_partition_exchange_schedule): the RCCL form issues exactly these ncclSend/ncclRecv
+    calls, the loopback group copies each receive from the peer's matching send.  Every send
+    of rank r to q has exactly one receive of q from r with the same count, and both move the
+    same global dofs in the same order; the P receives tile the ghost block; the P^T sends
+    tile it again and the P^T receives cover the P sends (pfespace.cpp:5394-5532)."""
+    m = E.Mesh.MakeCartesian3D(6, 5, 16)
+    fes = E.H1Space(m, 2, E.NUMBERING_STRUCTURED)
+    er = E.partition_slabs_z(m, nranks) if kind == "slabs" else \
+        np.random.default_rng(nranks).integers(0, nranks, m.GetNE()).astype(np.int32)
+    parts = [E.Partition(fes, er, r, nranks, decomposition=decomp) for r in range(nranks)]
+    for transpose in (False, True):
+        sch = [p.exchange_schedule(transpose) for p in parts]
+        for r, p in enumerate(parts):
+            ghosts = np.zeros(p.n_ghost, np.int32)
+            for row in sch[r]:
+                peer, send, buf, off, cnt = (int(v) for v in row)
+                assert peer != r and cnt > 0 and peer in p.nbrs
+                if (not transpose and not send) or (transpose and send):
+                    assert buf == (E.Partition.XBUF_XGHOST if not transpose else E.Partition.XBUF_YGHOST)
+                    ghosts[off: off + cnt] += 1
+                if not send:
+                    continue
+                match = [q for q in sch[peer] if q[0] == r and q[1] == 0]
+                assert len(match) == 1 and int(match[0][4]) == cnt
+                assert np.array_equal(_ids(p, row), _ids(parts[peer], match[0]))
+            assert np.all(ghosts == 1)  # each ghost received (P) / sent back (P^T) exactly once
+            if kind == "slabs" and not transpose:
+                # z-slabs: every P send is one contiguous owned range, sent straight from x
+                assert all(int(row[2]) == E.Partition.XBUF_X_TRUE for row in sch[r] if row[1])

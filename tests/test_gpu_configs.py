@@ -1,0 +1,400 @@
+"""GPU parity on the BASELINE configurations as the build runs them by default.
+
+* configs[2] (C3): fichera.mesh refined 2x / 3x (448 / 3,584 elements) at p = 1, 2 with the
+  default element order, so the face-linked 4x4x4 bricks derived from the gather map and the
+  cross-wave LDS face merge run on a non-lattice mesh; Mult and diagonal against the oracle;
+  the Pennes k(T) grid-function coefficient and Jacobi-PCG together on r3 against the
+  oracle's PCG (the reference pins PA == FA on fichera: test_pa_kernels.cpp:641-694).
+* Known answers on the reference's own fichera fixture through the HIP path: 1^T M 1 = |fichera|
+  = 7 and x^T K x = 7 |g|^2 for the linear x = g . X (H1 interpolates it exactly).
+* configs[4] (C5): p = 4 Cartesian 32^3 (2.15M DoF, all elements in 2 x 2 x 1 bricks) against
+  the oracle; the SDIRK33 step (ode.cpp:834-859) at p = 4 against the oracle's stepping.
+* configs[3] (C4): the 8-way z-slab split of a 16^3 p = 2 mesh (loopback group, both
+  decompositions) against the serial oracle.
+* The boundary's MultTranspose (bilinearform_ext.hpp:99) and AddMult; the device Pennes
+  perfusion law (parity-unpinned law, pinned projection); the distributed form's graph cache
+  across re-assembly.
+Bar: ||y - y_ref||_inf / ||y_ref||_inf <= RTOL = 1e-12 (FP64)."""
+import numpy as np
+import pytest
+
+import ecm2_amd as E
+import oracle as O
+import bioheat as BH
+import ode as ODE
+from helpers import GOLDEN, RTOL, alpha_bioheat, coeff_function, k_of_T, nonaligned, relerr, temperature
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    E.load_library()
+    yield
+    torch.cuda.synchronize()
+
+
+def dev(a, dtype=torch.float64):
+    return torch.as_tensor(np.ascontiguousarray(a)).to(device="cuda", dtype=dtype)
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy()
+
+
+def fichera(refinements):
+    m = E.Mesh(f"{GOLDEN}/fichera.mesh")
+    for _ in range(refinements):
+        m.UniformRefinement()
+    return m
+
+
+def quad_coeff(fes, values):
+    return E.QuadratureCoefficient(dev(np.asarray(values).reshape(fes.ne, -1)))
+
+
+# ---------------------------------------------------------------------------------------
+# configs[2]: fichera refined, default path (face-linked bricks + cross-wave merge)
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("refine", [2, 3])
+@pytest.mark.parametrize("order", [1, 2])
+def test_c3_fichera_default_path(refine, order):
+    m = fichera(refine)
+    assert m.GetNE() == 7 * 8 ** refine
+    fes = E.H1Space(m, order)
+    # every element of a refined fichera lies in a face-linked 4x4x4 brick
+    perm = fes.element_order_faces()
+    assert sorted(perm.tolist()) == list(range(fes.ne))
+    en = m.element_nodes()
+    q1d = O.default_q1d(order)
+    P = O.quad_points(en, q1d)
+    a, b = alpha_bioheat(P), k_of_T(temperature(P))
+    form = E.BilinearForm(fes)                       # defaults: auto kernel, auto element order
+    form.AddDomainIntegrator(E.MassIntegrator(quad_coeff(fes, a)))
+    form.AddDomainIntegrator(E.DiffusionIntegrator(quad_coeff(fes, b)))
+    form.Assemble()
+    info = form.info()
+    assert info["kernel"] == E.KERNEL_TPE and info["layout"] == E.QLAYOUT_AFFINE
+    native = E.BilinearForm(fes, element_order="native")
+    native.AddDomainIntegrator(E.MassIntegrator(quad_coeff(fes, a)))
+    native.AddDomainIntegrator(E.DiffusionIntegrator(quad_coeff(fes, b)))
+    native.Assemble()
+    # the brick order assembles faces in-wave and across waves: far fewer shared dofs
+    assert form.ScatterInfo()[0] < native.ScatterInfo()[0] // 2
+    op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=a, beta=b)
+    x = np.random.default_rng(refine * 10 + order).uniform(-1, 1, fes.ndofs)
+    for f in (form, native):
+        y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+        f.Mult(dev(x), y)
+        assert relerr(host(y), op.mult(x)) <= RTOL
+        d = torch.full_like(y, float("nan"))
+        f.AssembleDiagonal(d)
+        assert relerr(host(d), op.diagonal()) < 1e-13
+
+
+@pytest.mark.parametrize("jacobi", [True, False])
+def test_c3_fichera_pennes_pcg(jacobi):
+    """k(T) from an H1 temperature field (GridFunctionCoefficient projection + the Pennes law,
+    re-assembled on the device) inside the constrained Jacobi-PCG, r3 = 3,584 elements."""
+    m = fichera(3)
+    order = 2
+    fes = E.H1Space(m, order)
+    en = m.element_nodes()
+    q1d = O.default_q1d(order)
+    T = temperature(fes.dof_coords())
+    scale, slope, tref = 0.5 * 0.05, 0.0012, 37.0
+    form = E.BilinearForm(fes)
+    form.AddDomainIntegrator(E.MassIntegrator(E.ConstantCoefficient(1.0)))
+    form.AddDomainIntegrator(E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(dev(T), scale, slope, tref)))
+    form.Assemble()
+    beta = BH.affine_law(BH.temperature_at_quadrature(T, fes.gather_map(), order, q1d), scale, slope, tref)
+    op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=1.0, beta=beta)
+    ess = fes.boundary_dofs()
+    b = np.random.default_rng(4).uniform(-1, 1, fes.ndofs)
+    x = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    it, _ = form.PCG(dev(b), x, ess=dev(ess, torch.int32), rel_tol=1e-12, max_iter=3000, jacobi=jacobi)
+    xr, itr, _ = op.pcg(b, ess, rel_tol=1e-12, max_iter=3000, jacobi=jacobi)
+    # rounding differences move the iteration at which the 1e-12 test is first met by a few
+    assert abs(it - itr) <= max(2, 0.05 * itr)
+    assert relerr(host(x), xr) < 1e-9
+
+
+@pytest.mark.parametrize("refine", [1, 2, 3])
+@pytest.mark.parametrize("order", [1, 2, 3])
+def test_fichera_known_answers(refine, order):
+    """On the reference's data/fichera.mesh (7 unit cubes): 1^T M 1 = 7 and, for x = g . X
+    (linear: exactly in every H1 space), x^T K x = |g|^2 7 and K x = 0 in the interior dofs'
+    sense of sum(K x) = 0 (K 1 = 0)."""
+    m = fichera(refine)
+    fes = E.H1Space(m, order)
+    X = fes.dof_coords()
+    M = E.BilinearForm(fes)
+    M.AddDomainIntegrator(E.MassIntegrator(E.ConstantCoefficient(1.0)))
+    M.Assemble()
+    K = E.BilinearForm(fes)
+    K.AddDomainIntegrator(E.DiffusionIntegrator(E.ConstantCoefficient(1.0)))
+    K.Assemble()
+    one = torch.ones(fes.ndofs, dtype=torch.float64, device="cuda")
+    y = torch.empty_like(one)
+    M.Mult(one, y)
+    assert abs(float(y.sum()) - 7.0) < 1e-12 * 7.0
+    g = np.array([0.3, -1.1, 0.7])
+    x = dev(X @ g)
+    K.Mult(x, y)
+    assert abs(float(torch.dot(x, y)) - 7.0 * g @ g) < 1e-11 * 7.0 * (g @ g)
+    K.Mult(one, y)
+    assert float(y.abs().max()) < 1e-12
+
+
+# ---------------------------------------------------------------------------------------
+# configs[4]: p = 4 at size, and the SDIRK step at p = 4
+# ---------------------------------------------------------------------------------------
+def test_c5_p4_cartesian_32():
+    n = 32
+    m = E.Mesh.MakeCartesian3D(n, n, n)
+    fes = E.H1Space(m, 4, E.NUMBERING_STRUCTURED)
+    assert fes.ndofs == (4 * n + 1) ** 3
+    en = m.element_nodes()
+    P = O.quad_points(en, 6)
+    a, b = alpha_bioheat(P), k_of_T(temperature(P))
+    form = E.BilinearForm(fes)
+    form.AddDomainIntegrator(E.MassIntegrator(quad_coeff(fes, a)))
+    form.AddDomainIntegrator(E.DiffusionIntegrator(quad_coeff(fes, b)))
+    form.Assemble()
+    assert form.info()["kernel"] == E.KERNEL_LINE and form.info()["layout"] == E.QLAYOUT_AFFINE_E
+    assert form.BrickInfo() == (fes.ne // 4, 1)      # every element in a 2 x 2 x 1 brick
+    x = np.random.default_rng(32).uniform(-1, 1, fes.ndofs)
+    y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+    form.Mult(dev(x), y)
+    op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, 4, alpha=a, beta=b)
+    assert relerr(host(y), op.mult(x)) <= RTOL
+    y2 = torch.full_like(y, float("nan"))
+    form.Mult(dev(x), y2)
+    assert torch.equal(y, y2)                         # deterministic scatter
+
+
+def _serial_form(fes, P, alpha, beta):
+    f = E.BilinearForm(fes)
+    if alpha is not None:
+        f.AddDomainIntegrator(E.MassIntegrator(quad_coeff(fes, alpha)))
+    if beta is not None:
+        f.AddDomainIntegrator(E.DiffusionIntegrator(quad_coeff(fes, beta)))
+    f.Assemble()
+    return f
+
+
+@pytest.mark.parametrize("ode_type", [23, 21])
+def test_c5_sdirk_step_p4(ode_type):
+    """Two SDIRK33 (and backward Euler) steps of M du/dt = -K u at p = 4 with Dirichlet dofs
+    held, device ode_step (bricks + line kernel on a non-aligned mesh) against the oracle's
+    stepping with the oracle's PCG stage solves (ode.cpp:682-686, 834-859; ex16p.cpp:373-470)."""
+    m = E.Mesh.MakeCartesian3D(6, 4, 5)
+    m.set_vertices(nonaligned(m.vertices()))
+    order, dt = 4, 0.02
+    fes = E.H1Space(m, order)
+    en = m.element_nodes()
+    P = O.quad_points(en, O.default_q1d(order))
+    alpha = 2.0 + np.sin(P[..., 0]) * np.cos(P[..., 1])
+    beta = coeff_function(P)
+    c = E.ode_implicit_coeff(ode_type)
+    T = _serial_form(fes, P, alpha, c * dt * beta)
+    K = _serial_form(fes, P, None, beta)
+    assert T.BrickInfo()[0] > 0
+    Tr = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=alpha, beta=c * dt * beta)
+    Kr = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, beta=beta)
+    ess = fes.boundary_dofs()
+    X = fes.dof_coords()
+    u0 = 37.0 + 20.0 * np.exp(-4.0 * np.sum((X - 0.5) ** 2, axis=1))
+
+    def solve(us):
+        rhs = -Kr.mult(us)
+        rhs[ess] = 0.0
+        return Tr.pcg(rhs, ess, rel_tol=1e-13, max_iter=20000)[0]
+
+    ur = u0.copy()
+    for _ in range(2):
+        ur = ODE.step(ode_type, solve, ur, dt)
+    u = dev(u0)
+    essd = dev(ess, torch.int32)
+    for _ in range(2):
+        ns, it, conv = E.ode_step(ode_type, E.Operator(T), E.Operator(K), dt, u, ess=essd, rel_tol=1e-13,
+                                  max_iter=20000)
+        assert conv and ns == {21: 1, 23: 3}[ode_type]
+    uh = host(u)
+    assert np.array_equal(uh[ess], u0[ess])
+    assert relerr(uh - u0, ur - u0) < 1e-9
+
+
+# ---------------------------------------------------------------------------------------
+# configs[3]: the 8-way split
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("decomp", ["rap", "overlap"])
+@pytest.mark.parametrize("scatter", ["partials", "atomic"])
+def test_c4_eight_way_slabs(decomp, scatter):
+    n, nranks, order = 16, 8, 2
+    m = E.Mesh.MakeCartesian3D(n, n, n)
+    fes = E.H1Space(m, order, E.NUMBERING_STRUCTURED)
+    er = E.partition_slabs_z(m, nranks)
+    q1d = O.default_q1d(order)
+    xg = np.random.default_rng(8).uniform(-1, 1, fes.ndofs)
+    forms, parts, xs, ys = [], [], [], []
+    for r in range(nranks):
+        part = E.Partition(fes, er, r, nranks, decomposition=decomp)
+        pf = E.ParBilinearForm(part, scatter=scatter)
+        P = E.quadrature_points_subset(m, q1d, part.elems)
+        pf.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(alpha_bioheat(P).reshape(part.ne_local, -1)))))
+        pf.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(
+            dev(k_of_T(temperature(P)).reshape(part.ne_local, -1)))))
+        pf.Assemble()
+        forms.append(pf)
+        parts.append(part)
+        xs.append(dev(xg[part.owned_global]))
+        ys.append(torch.full((part.n_owned,), float("nan"), dtype=torch.float64, device="cuda"))
+    assert all(p.n_nbrs <= 2 for p in parts) and parts[3].n_nbrs == 2
+    group = E.ParGroup(forms)
+    for _ in range(2):  # repeated Mults reuse the streams, events and buffers
+        group.Mult(xs, ys)
+    y = np.full(fes.ndofs, np.nan)
+    for part, yt in zip(parts, ys):
+        y[part.owned_global] = host(yt)
+    Pg = O.quad_points(m.element_nodes(), q1d)
+    ref = O.OracleOperator(m.element_nodes(), fes.gather_map(), fes.ndofs, order, alpha=alpha_bioheat(Pg),
+                           beta=k_of_T(temperature(Pg))).mult(xg)
+    assert relerr(y, ref) <= RTOL
+
+
+# ---------------------------------------------------------------------------------------
+# boundary: MultTranspose / AddMult (bilinearform_ext.hpp:99, operator.hpp:87-92)
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("order", [2, 4])
+def test_mult_transpose_and_add_mult(order):
+    """test_assembly_levels.cpp:96-252 checks MultTranspose PA == legacy; the operator is
+    symmetric, so A^T x == A x, and y^T (A x) == x^T (A y)."""
+    m = fichera(1)
+    fes = E.H1Space(m, order)
+    en = m.element_nodes()
+    P = O.quad_points(en, O.default_q1d(order))
+    a, b = alpha_bioheat(P), coeff_function(P)
+    form = _serial_form(fes, P, a, b)
+    op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=a, beta=b)
+    rng = np.random.default_rng(order)
+    x, z = rng.uniform(-1, 1, fes.ndofs), rng.uniform(-1, 1, fes.ndofs)
+    yt = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+    form.MultTranspose(dev(x), yt)
+    ym = torch.empty_like(yt)
+    form.Mult(dev(x), ym)
+    assert torch.equal(yt, ym)
+    assert relerr(host(yt), op.fa_mult(x)) <= RTOL   # legacy (element-matrix) transpose = itself
+    zt = torch.empty_like(yt)
+    form.MultTranspose(dev(z), zt)
+    assert abs(z @ host(yt) - x @ host(zt)) <= 1e-12 * np.abs(z) @ np.abs(host(yt))
+    acc = dev(z.copy())
+    form.AddMult(dev(x), acc, -0.5)
+    assert relerr(host(acc), z - 0.5 * op.mult(x)) <= 1e-12
+
+
+def test_par_form_mult_transpose_loopback_free():
+    """The distributed boundary's MultTranspose (RCCL, one rank) equals its Mult."""
+    m = E.Mesh.MakeCartesian3D(4, 3, 6)
+    fes = E.H1Space(m, 2)
+    part = E.Partition(fes, np.zeros(m.GetNE(), np.int32), 0, 1)
+    pf = E.ParBilinearForm(part, rccl_id=E.rccl_unique_id())
+    pf.AddDomainIntegrator(E.MassIntegrator(E.ConstantCoefficient(2.0)))
+    pf.AddDomainIntegrator(E.DiffusionIntegrator(E.ConstantCoefficient(0.5)))
+    pf.Assemble()
+    x = dev(np.random.default_rng(3).uniform(-1, 1, part.n_owned))
+    y1, y2 = torch.empty_like(x), torch.empty_like(x)
+    pf.Mult(x, y1)
+    pf.MultTranspose(x, y2)
+    assert torch.equal(y1, y2)
+
+
+# ---------------------------------------------------------------------------------------
+# §8(f)1: device Pennes perfusion law for the mass integrator
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("order", [2, 4])
+def test_perfusion_coefficient(order):
+    """alpha(T) = rho c + gamma dt c_b w_b(T) from an H1 temperature field, evaluated on the
+    device at Assemble (projection: qfunction.cpp:73-98 restated by the oracle; the law is the
+    application's, parity-unpinned) beside the conductivity k(T); Mult and diagonal against the
+    oracle with the same laws on the oracle's projection."""
+    m = fichera(2) if order == 2 else fichera(1)
+    fes = E.H1Space(m, order)
+    en = m.element_nodes()
+    q1d = O.default_q1d(order)
+    T = temperature(fes.dof_coords())            # 37 .. 57 C: the hot spot coagulates
+    Tq = BH.temperature_at_quadrature(T, fes.gather_map(), order, q1d)
+    # shut-down temperature in the middle of a gap of the quadrature temperatures, so that no
+    # point sits on the law's discontinuity (rounding cannot flip a side)
+    ts = np.unique(Tq.ravel())
+    gaps = np.diff(ts)
+    mid = np.argmax(gaps * ((ts[:-1] > 45.0) & (ts[1:] < 55.0)))
+    t_stop = 0.5 * (ts[mid] + ts[mid + 1])
+    par = (3.6e6, 0.05 * 3.6e3, 6.4e-3, 0.02, 37.0, t_stop)
+    ks, kslope, ktref = 0.5 * 0.05, 0.0012, 37.0
+    form = E.BilinearForm(fes)
+    form.AddDomainIntegrator(E.MassIntegrator(E.PerfusionCoefficient(dev(T), *par)))
+    form.AddDomainIntegrator(E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(dev(T), ks, kslope, ktref)))
+    form.Assemble()
+    alpha = BH.perfusion_law(Tq, *par)
+    assert (alpha == par[0]).any() and (alpha > par[0]).any()  # both sides of the shut-down
+    beta = BH.affine_law(Tq, ks, kslope, ktref)
+    op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=alpha, beta=beta)
+    assert relerr(form.qdata(E.MASS)[:, 0, :], op.M) < 1e-13
+    x = np.random.default_rng(order).uniform(-1, 1, fes.ndofs)
+    y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    form.Mult(dev(x), y)
+    assert relerr(host(y), op.mult(x)) <= RTOL
+    d = torch.empty_like(y)
+    form.AssembleDiagonal(d)
+    assert relerr(host(d), op.diagonal()) < 1e-13
+
+
+# ---------------------------------------------------------------------------------------
+# the distributed form's graph cache across re-assembly (the graphs bake in buffers)
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("order", [2, 4])
+def test_rccl_graph_cache_follows_reassembly(order):
+    m = E.Mesh.MakeCartesian3D(6, 5, 4)
+    fes = E.H1Space(m, order)
+    part = E.Partition(fes, np.zeros(m.GetNE(), np.int32), 0, 1)
+    q1d = O.default_q1d(order)
+    P = E.quadrature_points_subset(m, q1d, part.elems)
+    c = coeff_function(P).reshape(part.ne_local, -1)
+    pf = E.ParBilinearForm(part, rccl_id=E.rccl_unique_id())
+    pf.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(c))))
+    pf.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(dev(c))))
+    pf.Assemble()
+    Pg = O.quad_points(m.element_nodes(), q1d)
+    cg = coeff_function(Pg)
+    ref = O.OracleOperator(m.element_nodes(), fes.gather_map(), fes.ndofs, order, alpha=cg, beta=cg)
+    xg = np.random.default_rng(6).uniform(-1, 1, fes.ndofs)
+    yref = ref.mult(xg)
+    x = dev(xg[part.owned_global])
+    y = torch.empty_like(x)
+
+    def check():
+        y.fill_(float("nan"))
+        for _ in range(3):           # direct, then graph capture, then replay
+            pf.Mult(x, y)
+        yy = np.zeros(fes.ndofs)
+        yy[part.owned_global] = host(y)
+        assert relerr(yy, yref) <= RTOL
+
+    check()
+    layouts = [pf.info()["layout"]]
+    pf.SetGeometryCompression(False)   # frees and reallocates qdata, selects another kernel
+    pf.Assemble()
+    check()
+    layouts.append(pf.info()["layout"])
+    assert layouts[0] != layouts[1]
+    pf.SetKernel(E.KERNEL_WPE)          # rebuilds the maps and plans
+    pf.Assemble()
+    check()
+    with pytest.raises(E.ECM2Error):   # a setter without Assemble: no stale replay
+        pf.SetKernel(E.KERNEL_AUTO)
+        pf.Mult(x, y)

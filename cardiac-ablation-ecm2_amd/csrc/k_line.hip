@@ -237,7 +237,8 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ lelem, int n_owned,
          {
             const double by = bp->B[qy + MQ * dy], gy = bp->G[qy + MQ * dy];
             c1 += by * l0[qy];                 // -> G_x
-            c2 += gy * l1[qy] + by * l2[qy];   // -> B_x
+            c2 += gy * l1[qy];   // -> B_x
+            c2 += by * l2[qy];
          }
          bufB[(dz * D + dy) * Q + qx] = c1;
          bufB[DD * Q + (dz * D + dy) * Q + qx] = c2;
@@ -260,7 +261,7 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ lelem, int n_owned,
       {
          double v = 0.0;
 #pragma unroll
-         for (int qx = 0; qx < Q; qx++) { v += bp->G[qx + MQ * dx] * l0[qx] + bp->B[qx + MQ * dx] * l1[qx]; }
+         for (int qx = 0; qx < Q; qx++) { v += bp->G[qx + MQ * dx] * l0[qx]; v += bp->B[qx + MQ * dx] * l1[qx]; }
          const int g = gl[dx];
          if (bneg(g)) { v = -v; }
          const int d = bdof(g);
@@ -285,21 +286,6 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ lelem, int n_owned,
 // (deterministic, no atomics).  Workgroups take bricks in XCD-contiguous order.
 // AFF: AFFINE_E qdata (per-element C + one (W beta, W alpha det J) pair per point).
 // --------------------------------------------------------------------------
-template <int D, int Q, int BZ>
-struct BrickShape
-{
-   static constexpr int NE = 4 * BZ, DD = D * D, QQ = Q * Q, DQ = D * Q, ND = D * D * D;
-   static constexpr int LX = 2 * (D - 1) + 1, LY = LX, LZ = BZ * (D - 1) + 1, NB = LX * LY * LZ;
-   static constexpr int SURF = 2 * LX * LY + 2 * (LZ - 2) * LX + 2 * (LZ - 2) * (LY - 2);
-   // per-element LDS: SA holds the x-stage lines (2 D^2 Q), SB the y/z-stage planes (3 D Q^2,
-   // the z stage works in place); staged element outputs (D^3) reuse SB
-   static constexpr int SA = 2 * DD * Q, SB = 3 * D * QQ;
-   static constexpr int NT = ((NE * QQ + 63) / 64) * 64;  // stage 3 in one pass
-   // waves per SIMD the register budget targets: 4 (<= 128 VGPRs) up to p = 4, where the
-   // 2 x 2 x 1 brick then fits 5 workgroups per CU; the larger orders keep their registers
-   static constexpr int WPE = D <= 5 ? 4 : 1;
-};
-
 // lattice coordinate P along one brick direction -> (first element index, local index,
 // holders): the shared plane P = D-1 is held by element 0 (local D-1) and 1 (local 0)
 template <int D>
@@ -310,66 +296,129 @@ __device__ __forceinline__ void brick_cand(int P, int &c0, int &l0, int &n)
    else { c0 = 1; l0 = P - (D - 1); n = 1; }
 }
 
-template <int D, int Q, int BZ, bool SPLIT, bool AFF>
-__global__ void __launch_bounds__((BrickShape<D, Q, BZ>::NT), (BrickShape<D, Q, BZ>::WPE))
-k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *__restrict__ bmap, int n_owned,
-              const double *__restrict__ qdd, const double *__restrict__ qdm,
-              const double *__restrict__ x, const double *__restrict__ xg,
-              double *__restrict__ y, double *__restrict__ yg, const Basis1D *__restrict__ btab,
-              double *__restrict__ part)
+// --------------------------------------------------------------------------
+// Brick kernel layout and addressing (round 2; profiles/r2_ab_brick.txt: -8..-9% vs the
+// round-1 form at C5):
+//  * bank-conflict-free LDS images: every stage's lane -> element mapping starts each element
+//    at a 32-lane boundary (x lines, y lines) or at a stride of S3 = QQ rounded up to 16 lanes
+//    (z columns); the x-line image is [f][qx][dz][dy], the y/z image [g][dz][qy][qx] with a dz
+//    stride DS = Q (mod 32) and an element stride SB = S3 (mod 32), so the lanes of a
+//    ds_read_b64 group (32 lanes) / ds_write_b64 group (16 lanes) hit distinct banks in all
+//    five stages (MI355X_MICROARCH.md §LDS);
+//  * REG (lattice-numbered bricks, set up when every brick's map is d = base + X sx + Y sy +
+//    Z sz and its shared points are exactly those on the brick faces other holders touch):
+//    5 ints per brick (breg) replace the 405-entry lattice map, so the x gather is issued at
+//    entry with no dependent map load, and the lattice stores compute their dofs;
+//  * load order x gather -> qdata, branch-free: stage 1 waits for the gather only (vmcnt
+//    counts in order), the qdata pairs stay in flight through the x and y stages.
+// Measured and rejected: a persistent form prefetching the next brick's gather and qdata behind
+// the z stage (155 VGPRs, 3 waves/SIMD: 0.83 vs 0.51 ms at C5).
+// --------------------------------------------------------------------------
+template <int D, int Q, int BZ>
+struct BrickShapeC
 {
-   using S = BrickShape<D, Q, BZ>;
-   constexpr int NE = S::NE, DD = S::DD, QQ = S::QQ, DQ = S::DQ, ND = S::ND, SA = S::SA, SB = S::SB;
-   constexpr int LX = S::LX, LY = S::LY, NB = S::NB;
+   static constexpr int NE = 4 * BZ, DD = D * D, QQ = Q * Q, DQ = D * Q, ND = D * D * D;
+   static constexpr int LX = 2 * (D - 1) + 1, LY = LX, LZ = BZ * (D - 1) + 1, NB = LX * LY * LZ;
+   static constexpr int SURF = 2 * LX * LY + 2 * (LZ - 2) * LX + 2 * (LZ - 2) * (LY - 2);
+   static constexpr int L2S = (DQ > DD ? DQ : DD) <= 32 ? 32 : 64;  // lanes per element, line stages
+   static constexpr int S3 = ((QQ + 15) / 16) * 16;                 // lanes per element, z stage
+   static constexpr int DS = (QQ <= Q + 32 * ((QQ - Q + 31) / 32)) ? Q + 32 * ((QQ - Q + 31) / 32) : QQ;
+   static constexpr int SA = 2 * DD * Q;                            // x-line image per element
+   static constexpr int SB0 = 3 * D * DS > ND ? 3 * D * DS : ND;
+   static constexpr int SB = SB0 + ((S3 % 32) - (SB0 % 32) + 32) % 32;  // SB = S3 (mod 32)
+   static constexpr int NTL = NE * L2S, NT3 = NE * S3;
+   static constexpr int NT = (((NTL > NT3 ? NTL : NT3) + 63) / 64) * 64;
+   static constexpr int WPE = (D <= 5 && BZ == 1) ? 4 : 1;
+};
+
+// faces of the brick lattice containing point (X, Y, Z): bits X = 0, X = LX-1, Y = 0, ...
+template <int LX, int LY, int LZ>
+__device__ __forceinline__ int brick_faces(int X, int Y, int Z)
+{
+   return (X == 0) | (X == LX - 1) << 1 | (Y == 0) << 2 | (Y == LY - 1) << 3 | (Z == 0) << 4 | (Z == LZ - 1) << 5;
+}
+
+template <int D, int Q, int BZ, bool SPLIT, bool AFF, bool REG>
+__global__ void __launch_bounds__((BrickShapeC<D, Q, BZ>::NT), (BrickShapeC<D, Q, BZ>::WPE))
+k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int *__restrict__ bmap,
+                const int *__restrict__ breg, int n_owned, const double *__restrict__ qdd,
+                const double *__restrict__ qdm, const double *__restrict__ x, const double *__restrict__ xg,
+                double *__restrict__ y, double *__restrict__ yg, const Basis1D *__restrict__ btab,
+                double *__restrict__ part)
+{
+   using S = BrickShapeC<D, Q, BZ>;
+   constexpr int NE = S::NE, DD = S::DD, QQ = S::QQ, DQ = S::DQ, SA = S::SA, SB = S::SB, DS = S::DS;
+   constexpr int LX = S::LX, LY = S::LY, LZ = S::LZ, NB = S::NB, L2S = S::L2S, S3 = S::S3, NQ = Q * Q * Q;
    static_assert(QQ <= 64, "brick kernel needs Q1D <= 8");
-   static_assert(SB >= ND, "staged outputs reuse bufB");
-   __shared__ double bufA[NE * SA];
-   __shared__ double bufB[NE * SB];
+   static_assert(DQ <= L2S && DD <= L2S, "line stages: one lane per line");
+   static_assert(!(REG && SPLIT), "regular bricks address one L-vector");
+   __shared__ double sXL[NE * SA];  // x lines: [e][f][qx][dz][dy]
+   __shared__ double sYQ[NE * SB];  // y / z planes: [e][g][dz (stride DS)][qy][qx]; then outputs [e][dx][dz][dy]
    const int k = k_begin + xcd_contiguous(blockIdx.x, gridDim.x);
    if (k >= k_end) { return; }  // whole workgroup
    const int t = threadIdx.x;
+   const int eL = t / L2S, lL = t % L2S;                 // line stages
+   const bool actL = eL < NE && lL < DD;                 // stages 1, 5: lL = dy + D dz
+   const bool act2 = eL < NE && lL < DQ;                 // stages 2, 4
+   const int e3 = t / S3, l3 = t % S3;                   // z stage: l3 = qx + Q qy
+   const bool act3 = e3 < NE && l3 < QQ;
+   int base = 0, sx = 0, sy = 0, sz = 0, mask = 0;
+   if (REG)
+   {
+      const int *r = breg + (size_t)k * 8;  // workgroup-uniform: scalar loads
+      base = r[0]; sx = r[1]; sy = r[2]; sz = r[3]; mask = r[4];
+   }
    const int *bm = bmap + (size_t)k * NB;
-   const int *be = belem + (size_t)k * NE;
    auto lattice = [&](int elt, int dx, int dy, int dz) {
       const int ex = elt & 1, ey = (elt >> 1) & 1, ez = elt >> 2;
       return ((ez * (D - 1) + dz) * LY + ey * (D - 1) + dy) * LX + ex * (D - 1) + dx;
    };
 
-   // qdata of the (element, qx, qy) column this lane weights in stage 3: in flight
-   // during the gather and the x / y contractions.  AFF: the raw per-point pairs and the
-   // element's C stay in registers until the z stage (forming the 6 entries at load time
-   // would make the wave wait for the loads at entry, and hold 7Q values instead of 2Q + 6)
+   // ---- loads, branch-free: element ids, the x-line gather, then this lane's z-stage qdata (in
+   // flight through stages 1-2).  Loads under a branch leave the compiler's wait counts unknown
+   // at the join, and it then waits for all of them (the x stage would wait for the qdata);
+   // idle lanes load a neighbour's (clamped) addresses instead and ignore the values.
+   const int eLc = eL < NE ? eL : NE - 1, lLc = lL < DD ? lL : DD - 1;
+   const int e = belem[(size_t)k * NE + (e3 < NE ? e3 : NE - 1)];
+   const int l3c = l3 < QQ ? l3 : QQ - 1;
+   double xl[D];
+   {
+      const int dy = lLc % D, dz = lLc / D, ex = eLc & 1, ey = (eLc >> 1) & 1, ez = eLc >> 2;
+      if (REG)
+      {
+         const int d0 = base + (ex * (D - 1)) * sx + (ey * (D - 1) + dy) * sy + (ez * (D - 1) + dz) * sz;
+#pragma unroll
+         for (int dx = 0; dx < D; dx++) { xl[dx] = x[d0 + dx * sx]; }
+      }
+      else
+      {
+         const int *mp = bm + lattice(eLc, 0, dy, dz);
+#pragma unroll
+         for (int dx = 0; dx < D; dx++)
+         {
+            const int d = bdof(mp[dx]);
+            xl[dx] = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
+         }
+      }
+   }
+   __builtin_amdgcn_sched_barrier(0);  // keep the gather ahead of the qdata loads
    double qv[7][Q];
    v2d pa[Q];
    double cc[6];
-   if (t < NE * QQ)
+   if (AFF)
    {
-      const int e = be[t / QQ], l = t % QQ;
-      if (AFF)
-      {
-         constexpr int NQ = Q * Q * Q;
 #pragma unroll
-         for (int qz = 0; qz < Q; qz++) { pa[qz] = reinterpret_cast<const v2d *>(qdm)[(size_t)e * NQ + qz * QQ + l]; }
+      for (int qz = 0; qz < Q; qz++) { pa[qz] = reinterpret_cast<const v2d *>(qdm)[(size_t)e * NQ + qz * QQ + l3c]; }
 #pragma unroll
-         for (int c = 0; c < 6; c++) { cc[c] = qdd[(size_t)e * 6 + c]; }
-      }
-      else { line_load_qdata<D, Q, true, true, false>(qv, e, l, qdd, qdm); }
+      for (int c = 0; c < 6; c++) { cc[c] = qdd[(size_t)e * 6 + c]; }
    }
+   else { line_load_qdata<D, Q, true, true, false>(qv, e, l3c, qdd, qdm); }
 
-   // ---- lanes (element, dy, dz): gather the x-line, contract in x
-   if (t < NE * DD)
+   // ---- lanes (element, dy, dz): contract in x -> sXL [f][qx][l]
+   if (actL)
    {
       CBasis *bp = stage_basis(btab);
-      const int elt = t / DD, l = t % DD;
-      const int *mp = bm + lattice(elt, 0, l % D, l / D);
-      double xl[D];
-#pragma unroll
-      for (int dx = 0; dx < D; dx++)
-      {
-         const int d = bdof(mp[dx]);
-         xl[dx] = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
-      }
-      double *o = bufA + elt * SA;
+      double *o = sXL + eL * SA + lL;
 #pragma unroll
       for (int qx = 0; qx < Q; qx++)
       {
@@ -380,58 +429,63 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
             u += bp->B[qx + MQ * dx] * xl[dx];
             v += bp->G[qx + MQ * dx] * xl[dx];
          }
-         o[l * Q + qx] = u;
-         o[DD * Q + l * Q + qx] = v;
+         o[qx * DD] = u;
+         o[Q * DD + qx * DD] = v;
       }
    }
+   if (k_begin < 0)  // never: a use outside the x stage stops the gather sinking behind the qdata
+   {
+      double u = 0.0;
+#pragma unroll
+      for (int dx = 0; dx < D; dx++) { u += xl[dx]; }
+      part[t] = u;
+   }
    __syncthreads();
-   // ---- lanes (element, qx, dz): contract in y
-   if (t < NE * DQ)
+   // ---- lanes (element, qx, dz), l2 = qx + Q dz: contract in y -> sYQ [g][dz][qy][qx]
+   if (act2)
    {
       CBasis *bp = stage_basis(btab);
-      const int elt = t / DQ, l = t % DQ, qx = l % Q, dz = l / Q;
-      const double *in = bufA + elt * SA;
+      const int qx = lL % Q, dz = lL / Q;
+      const double *in = sXL + eL * SA + qx * DD + dz * D;
       double la[D], lb[D];
 #pragma unroll
       for (int dy = 0; dy < D; dy++)
       {
-         la[dy] = in[(dz * D + dy) * Q + qx];
-         lb[dy] = in[DD * Q + (dz * D + dy) * Q + qx];
+         la[dy] = in[dy];
+         lb[dy] = in[Q * DD + dy];
       }
-      double *o = bufB + elt * SB;
+      double *o = sYQ + eL * SB + dz * DS + qx;
 #pragma unroll
       for (int qy = 0; qy < Q; qy++)
       {
          double gb = 0.0, bg = 0.0, bb = 0.0;
+         CBasis *br = stage_basis(btab);  // re-laundered per row: one row of the basis in SGPRs
 #pragma unroll
          for (int dy = 0; dy < D; dy++)
          {
-            const double by = bp->B[qy + MQ * dy], gy = bp->G[qy + MQ * dy];
+            const double by = br->B[qy + MQ * dy], gy = br->G[qy + MQ * dy];
             gb += by * lb[dy];
             bg += gy * la[dy];
             bb += by * la[dy];
          }
-         const int oo = (dz * Q + qy) * Q + qx;
-         o[oo] = gb;
-         o[D * QQ + oo] = bg;
-         o[2 * D * QQ + oo] = bb;
+         o[qy * Q] = gb;
+         o[D * DS + qy * Q] = bg;
+         o[2 * D * DS + qy * Q] = bb;
       }
    }
    __syncthreads();
-   // ---- lanes (element, qx, qy): contract in z, weight, transpose in z (in place: a lane
-   // reads its whole (qx, qy) column before writing it back)
-   if (t < NE * QQ)
+   // ---- lanes (element, qx, qy): contract in z, weight, transpose in z (in place)
+   if (act3)
    {
       CBasis *bp = stage_basis(btab);
-      const int elt = t / QQ, l = t % QQ;
-      double *in = bufB + elt * SB;
+      double *io = sYQ + e3 * SB + l3;
       double l0[D], l1[D], l2[D];
 #pragma unroll
       for (int dz = 0; dz < D; dz++)
       {
-         l0[dz] = in[dz * QQ + l];
-         l1[dz] = in[D * QQ + dz * QQ + l];
-         l2[dz] = in[2 * D * QQ + dz * QQ + l];
+         l0[dz] = io[dz * DS];
+         l1[dz] = io[D * DS + dz * DS];
+         l2[dz] = io[2 * D * DS + dz * DS];
       }
       double A1[D], A2[D], A3[D];
 #pragma unroll
@@ -478,28 +532,27 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
 #pragma unroll
       for (int dz = 0; dz < D; dz++)
       {
-         in[dz * QQ + l] = A1[dz];
-         in[D * QQ + dz * QQ + l] = A2[dz];
-         in[2 * D * QQ + dz * QQ + l] = A3[dz];
+         io[dz * DS] = A1[dz];
+         io[D * DS + dz * DS] = A2[dz];
+         io[2 * D * DS + dz * DS] = A3[dz];
       }
    }
    __syncthreads();
-   // ---- lanes (element, qx, dz): transpose in y
-   if (t < NE * DQ)
+   // ---- lanes (element, dz, qx), l4 = dz + D qx: transpose in y -> sXL [f][qx][dz][dy]
+   if (act2)
    {
       CBasis *bp = stage_basis(btab);
-      const int elt = t / DQ, l = t % DQ, qx = l % Q, dz = l / Q;
-      const double *in = bufB + elt * SB;
-      double l0[Q], l1[Q], l2[Q];
+      const int dz = lL % D, qx = lL / D;
+      const double *in = sYQ + eL * SB + dz * DS + qx;
+      double t0[Q], t1[Q], t2[Q];
 #pragma unroll
       for (int qy = 0; qy < Q; qy++)
       {
-         const int oo = (dz * Q + qy) * Q + qx;
-         l0[qy] = in[oo];
-         l1[qy] = in[D * QQ + oo];
-         l2[qy] = in[2 * D * QQ + oo];
+         t0[qy] = in[qy * Q];
+         t1[qy] = in[D * DS + qy * Q];
+         t2[qy] = in[2 * D * DS + qy * Q];
       }
-      double *o = bufA + elt * SA;
+      double *o = sXL + eL * SA + qx * DD + dz * D;
 #pragma unroll
       for (int dy = 0; dy < D; dy++)
       {
@@ -508,34 +561,34 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
          for (int qy = 0; qy < Q; qy++)
          {
             const double by = bp->B[qy + MQ * dy], gy = bp->G[qy + MQ * dy];
-            c1 += by * l0[qy];
-            c2 += gy * l1[qy] + by * l2[qy];
+            c1 += by * t0[qy];
+            c2 += gy * t1[qy];
+            c2 += by * t2[qy];
          }
-         o[(dz * D + dy) * Q + qx] = c1;
-         o[DD * Q + (dz * D + dy) * Q + qx] = c2;
+         o[dy] = c1;
+         o[Q * DD + dy] = c2;
       }
    }
    __syncthreads();
-   // ---- lanes (element, dy, dz): transpose in x -> element outputs staged in LDS [elt][a]
-   if (t < NE * DD)
+   // ---- lanes (element, dy, dz): transpose in x -> element outputs [e][dx][dz][dy] in sYQ
+   if (actL)
    {
       CBasis *bp = stage_basis(btab);
-      const int elt = t / DD, l = t % DD;
-      const double *in = bufA + elt * SA;
+      const double *in = sXL + eL * SA + lL;
       double l0[Q], l1[Q];
 #pragma unroll
       for (int qx = 0; qx < Q; qx++)
       {
-         l0[qx] = in[l * Q + qx];
-         l1[qx] = in[DD * Q + l * Q + qx];
+         l0[qx] = in[qx * DD];
+         l1[qx] = in[Q * DD + qx * DD];
       }
 #pragma unroll
       for (int dx = 0; dx < D; dx++)
       {
          double v = 0.0;
 #pragma unroll
-         for (int qx = 0; qx < Q; qx++) { v += bp->G[qx + MQ * dx] * l0[qx] + bp->B[qx + MQ * dx] * l1[qx]; }
-         bufB[elt * ND + l * D + dx] = v;  // bufB is free: stage 4 read it before a barrier
+         for (int qx = 0; qx < Q; qx++) { v += bp->G[qx + MQ * dx] * l0[qx]; v += bp->B[qx + MQ * dx] * l1[qx]; }
+         sYQ[eL * SB + dx * DD + lL] = v;  // sYQ is free: stage 4 read it before a barrier
       }
    }
    __syncthreads();
@@ -554,325 +607,23 @@ k_apply_brick(int k_begin, int k_end, const int *__restrict__ belem, const int *
             for (int ix = 0; ix < nx; ix++)
             {
                const int elt = (cx + ix) + 2 * ((cy + iy) + 2 * (cz + iz));
-               const int a = ((iz ? 0 : lz) * D + (iy ? 0 : ly)) * D + (ix ? 0 : lx);
-               v += bufB[elt * ND + a];
+               v += sYQ[elt * SB + (ix ? 0 : lx) * DD + (iz ? 0 : lz) * D + (iy ? 0 : ly)];
             }
-      const int g = bm[p];
-      const int d = bdof(g);
-      if (!bshared(g)) { *((!SPLIT || d < n_owned) ? y + d : yg + (d - n_owned)) = v; }
+      int d;
+      bool shared;
+      if (REG)
+      {
+         d = base + X * sx + Y * sy + Z * sz;
+         shared = (brick_faces<LX, LY, LZ>(X, Y, Z) & mask) != 0;
+      }
+      else
+      {
+         const int g = bm[p];
+         d = bdof(g);
+         shared = bshared(g);
+      }
+      if (!shared) { *((!SPLIT || d < n_owned) ? y + d : yg + (d - n_owned)) = v; }
       else { part[(size_t)k * S::SURF + brick_surface_index(D, BZ, X, Y, Z)] = v; }  // surface only (setup)
-   }
-}
-
-// --------------------------------------------------------------------------
-// Persistent brick kernel: the same brick algorithm, with
-//  * bank-conflict-free LDS images: every stage's lane -> element mapping starts each element
-//    at a 32-lane boundary (x lines, y lines) or at a stride of S3 = QQ rounded up to 16 lanes
-//    (z columns), the x-line image is [f][qx][dz][dy] (dense), the y/z image [g][dz][qy][qx]
-//    with a dz stride DS = Q (mod 32) and an element stride SB = S3 (mod 32), so consecutive
-//    lanes of a ds_read_b64 group (32 lanes) / ds_write_b64 group (16 lanes) hit distinct
-//    banks in all five stages (MI355X_MICROARCH.md §LDS);
-//  * one workgroup per CU slot (grid = occupancy x CUs) walking bricks k = j G + slot(w):
-//    the next brick's qdata pairs, element matrices and lattice map are loaded right after
-//    this brick's z stage (in flight during the transposed stages, the lattice sum and the
-//    next brick's gather and x / y stages), so HBM streams continuously instead of each
-//    workgroup paying its own load latency at entry.  At iteration j the workgroups hold a
-//    window of G consecutive bricks, split XCD-contiguously.
-// --------------------------------------------------------------------------
-template <int D, int Q, int BZ>
-struct BrickShapeP
-{
-   static constexpr int NE = 4 * BZ, DD = D * D, QQ = Q * Q, DQ = D * Q, ND = D * D * D;
-   static constexpr int LX = 2 * (D - 1) + 1, LY = LX, LZ = BZ * (D - 1) + 1, NB = LX * LY * LZ;
-   static constexpr int SURF = 2 * LX * LY + 2 * (LZ - 2) * LX + 2 * (LZ - 2) * (LY - 2);
-   static constexpr int L2S = (DQ > DD ? DQ : DD) <= 32 ? 32 : 64;  // lanes per element, line stages
-   static constexpr int S3 = ((QQ + 15) / 16) * 16;                 // lanes per element, z stage
-   static constexpr int DS = (QQ <= Q + 32 * ((QQ - Q + 31) / 32)) ? Q + 32 * ((QQ - Q + 31) / 32) : QQ;
-   static constexpr int SA = 2 * DD * Q;                            // x-line image per element
-   static constexpr int SB0 = 3 * D * DS > ND ? 3 * D * DS : ND;
-   static constexpr int SB = SB0 + ((S3 % 32) - (SB0 % 32) + 32) % 32;  // SB = S3 (mod 32)
-   static constexpr int NTL = NE * L2S, NT3 = NE * S3;
-   static constexpr int NT = (((NTL > NT3 ? NTL : NT3) + 63) / 64) * 64;
-   static constexpr int WPE = (D <= 5 && BZ == 1) ? 3 : 1;
-};
-
-template <int D, int Q, int BZ, bool SPLIT, bool AFF>
-__global__ void __launch_bounds__((BrickShapeP<D, Q, BZ>::NT), (BrickShapeP<D, Q, BZ>::WPE))
-k_apply_brick_p(int k_begin, int k_end, const int *__restrict__ belem, const int *__restrict__ bmap, int n_owned,
-                const double *__restrict__ qdd, const double *__restrict__ qdm,
-                const double *__restrict__ x, const double *__restrict__ xg,
-                double *__restrict__ y, double *__restrict__ yg, const Basis1D *__restrict__ btab,
-                double *__restrict__ part)
-{
-   using S = BrickShapeP<D, Q, BZ>;
-   constexpr int NE = S::NE, DD = S::DD, QQ = S::QQ, DQ = S::DQ, SA = S::SA, SB = S::SB, DS = S::DS;
-   constexpr int LX = S::LX, LY = S::LY, NB = S::NB, L2S = S::L2S, S3 = S::S3, NT = S::NT, NQ = Q * Q * Q;
-   constexpr int NPL = (NB + NT - 1) / NT;  // lattice points per thread
-   static_assert(QQ <= 64, "brick kernel needs Q1D <= 8");
-   static_assert(DQ <= L2S && DD <= L2S, "line stages: one lane per line");
-   __shared__ double sXL[NE * SA];  // x lines: [e][f][qx][dz][dy]
-   __shared__ double sYQ[NE * SB];  // y / z planes: [e][g][dz (stride DS)][qy][qx]; then outputs [e][dx][dz][dy]
-   const int t = threadIdx.x;
-   // lane roles
-   const int eL = t / L2S, lL = t % L2S;                 // line stages
-   const bool actL = eL < NE && lL < DD;                 // stages 1, 5: lL = dy + D dz
-   const bool act2 = eL < NE && lL < DQ;                 // stages 2, 4
-   const int e3 = t / S3, l3 = t % S3;                   // z stage: l3 = qx + Q qy
-   const bool act3 = e3 < NE && l3 < QQ;
-   const int G = gridDim.x, slot = xcd_contiguous(blockIdx.x, G);
-   auto lattice = [&](int elt, int dx, int dy, int dz) {
-      const int ex = elt & 1, ey = (elt >> 1) & 1, ez = elt >> 2;
-      return ((ez * (D - 1) + dz) * LY + ey * (D - 1) + dy) * LX + ex * (D - 1) + dx;
-   };
-
-   // registers carried across iterations: the z stage's qdata and the brick's maps
-   double qv[7][Q];      // native layout
-   v2d pa[Q];            // AFFINE_E pairs
-   double cc[6];         // AFFINE_E element matrix
-   int bmg[D];           // gather map of this lane's x line
-   int bms[NPL];         // lattice map of this lane's lattice points
-   auto load_brick = [&](int kb) {
-      const int *bm = bmap + (size_t)kb * NB;
-      if (act3)
-      {
-         const int e = belem[(size_t)kb * NE + e3];
-         if (AFF)
-         {
-#pragma unroll
-            for (int qz = 0; qz < Q; qz++) { pa[qz] = reinterpret_cast<const v2d *>(qdm)[(size_t)e * NQ + qz * QQ + l3]; }
-#pragma unroll
-            for (int c = 0; c < 6; c++) { cc[c] = qdd[(size_t)e * 6 + c]; }
-         }
-         else { line_load_qdata<D, Q, true, true, false>(qv, e, l3, qdd, qdm); }
-      }
-      if (actL)
-      {
-         const int *mp = bm + lattice(eL, 0, lL % D, lL / D);
-#pragma unroll
-         for (int dx = 0; dx < D; dx++) { bmg[dx] = mp[dx]; }
-      }
-#pragma unroll
-      for (int i = 0; i < NPL; i++)
-      {
-         const int p = t + i * NT;
-         bms[i] = p < NB ? bm[p] : 0;
-      }
-   };
-   int k = k_begin + slot;
-   if (k < k_end) { load_brick(k); }
-#pragma unroll 1
-   for (; k < k_end; k += G)  // workgroup-uniform
-   {
-      // ---- lanes (element, dy, dz): gather the x-line, contract in x -> sXL [f][qx][l]
-      if (actL)
-      {
-         CBasis *bp = stage_basis(btab);
-         double xl[D];
-#pragma unroll
-         for (int dx = 0; dx < D; dx++)
-         {
-            const int d = bdof(bmg[dx]);
-            xl[dx] = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
-         }
-         double *o = sXL + eL * SA + lL;
-#pragma unroll
-         for (int qx = 0; qx < Q; qx++)
-         {
-            double u = 0.0, v = 0.0;
-#pragma unroll
-            for (int dx = 0; dx < D; dx++)
-            {
-               u += bp->B[qx + MQ * dx] * xl[dx];
-               v += bp->G[qx + MQ * dx] * xl[dx];
-            }
-            o[qx * DD] = u;
-            o[Q * DD + qx * DD] = v;
-         }
-      }
-      __syncthreads();
-      // ---- lanes (element, qx, dz), l2 = qx + Q dz: contract in y -> sYQ [g][dz][qy][qx]
-      if (act2)
-      {
-         CBasis *bp = stage_basis(btab);
-         const int qx = lL % Q, dz = lL / Q;
-         const double *in = sXL + eL * SA + qx * DD + dz * D;
-         double la[D], lb[D];
-#pragma unroll
-         for (int dy = 0; dy < D; dy++)
-         {
-            la[dy] = in[dy];
-            lb[dy] = in[Q * DD + dy];
-         }
-         double *o = sYQ + eL * SB + dz * DS + qx;
-#pragma unroll
-         for (int qy = 0; qy < Q; qy++)
-         {
-            double gb = 0.0, bg = 0.0, bb = 0.0;
-#pragma unroll
-            for (int dy = 0; dy < D; dy++)
-            {
-               const double by = bp->B[qy + MQ * dy], gy = bp->G[qy + MQ * dy];
-               gb += by * lb[dy];
-               bg += gy * la[dy];
-               bb += by * la[dy];
-            }
-            o[qy * Q] = gb;
-            o[D * DS + qy * Q] = bg;
-            o[2 * D * DS + qy * Q] = bb;
-         }
-      }
-      __syncthreads();
-      // ---- lanes (element, qx, qy): contract in z, weight, transpose in z (in place)
-      if (act3)
-      {
-         CBasis *bp = stage_basis(btab);
-         double *io = sYQ + e3 * SB + l3;
-         double l0[D], l1[D], l2[D];
-#pragma unroll
-         for (int dz = 0; dz < D; dz++)
-         {
-            l0[dz] = io[dz * DS];
-            l1[dz] = io[D * DS + dz * DS];
-            l2[dz] = io[2 * D * DS + dz * DS];
-         }
-         double A1[D], A2[D], A3[D];
-#pragma unroll
-         for (int dz = 0; dz < D; dz++) { A1[dz] = 0.0; A2[dz] = 0.0; A3[dz] = 0.0; }
-#pragma unroll
-         for (int qz = 0; qz < Q; qz++)
-         {
-            double gx = 0.0, gy = 0.0, gz = 0.0, u = 0.0;
-#pragma unroll
-            for (int dz = 0; dz < D; dz++)
-            {
-               const double bz = bp->B[qz + MQ * dz], gzz = bp->G[qz + MQ * dz];
-               gx += bz * l0[dz];
-               gy += bz * l1[dz];
-               gz += gzz * l2[dz];
-               u += bz * l2[dz];
-            }
-            double fx, fy, fz, m;
-            if (AFF)
-            {
-               const double wb = pa[qz].x;
-               fx = wb * (cc[0] * gx + cc[1] * gy + cc[2] * gz);
-               fy = wb * (cc[1] * gx + cc[3] * gy + cc[4] * gz);
-               fz = wb * (cc[2] * gx + cc[4] * gy + cc[5] * gz);
-               m = pa[qz].y * u;
-            }
-            else
-            {
-               fx = qv[0][qz] * gx + qv[1][qz] * gy + qv[2][qz] * gz;
-               fy = qv[1][qz] * gx + qv[3][qz] * gy + qv[4][qz] * gz;
-               fz = qv[2][qz] * gx + qv[4][qz] * gy + qv[5][qz] * gz;
-               m = qv[6][qz] * u;
-            }
-#pragma unroll
-            for (int dz = 0; dz < D; dz++)
-            {
-               const double bz = bp->B[qz + MQ * dz], gzz = bp->G[qz + MQ * dz];
-               A1[dz] += bz * fx;
-               A2[dz] += bz * fy;
-               A3[dz] += gzz * fz;
-               A3[dz] += bz * m;
-            }
-         }
-#pragma unroll
-         for (int dz = 0; dz < D; dz++)
-         {
-            io[dz * DS] = A1[dz];
-            io[D * DS + dz * DS] = A2[dz];
-            io[2 * D * DS + dz * DS] = A3[dz];
-         }
-      }
-      // this brick's lattice map for the stores, then the next brick's qdata and maps: in
-      // flight from here through the next brick's z stage
-      int bst[NPL];
-#pragma unroll
-      for (int i = 0; i < NPL; i++) { bst[i] = bms[i]; }
-      if (k + G < k_end) { load_brick(k + G); }
-      __syncthreads();
-      // ---- lanes (element, dz, qx), l4 = dz + D qx: transpose in y -> sXL [f][qx][dz][dy]
-      if (act2)
-      {
-         CBasis *bp = stage_basis(btab);
-         const int dz = lL % D, qx = lL / D;
-         const double *in = sYQ + eL * SB + dz * DS + qx;
-         double t0[Q], t1[Q], t2[Q];
-#pragma unroll
-         for (int qy = 0; qy < Q; qy++)
-         {
-            t0[qy] = in[qy * Q];
-            t1[qy] = in[D * DS + qy * Q];
-            t2[qy] = in[2 * D * DS + qy * Q];
-         }
-         double *o = sXL + eL * SA + qx * DD + dz * D;
-#pragma unroll
-         for (int dy = 0; dy < D; dy++)
-         {
-            double c1 = 0.0, c2 = 0.0;
-#pragma unroll
-            for (int qy = 0; qy < Q; qy++)
-            {
-               const double by = bp->B[qy + MQ * dy], gy = bp->G[qy + MQ * dy];
-               c1 += by * t0[qy];
-               c2 += gy * t1[qy] + by * t2[qy];
-            }
-            o[dy] = c1;
-            o[Q * DD + dy] = c2;
-         }
-      }
-      __syncthreads();
-      // ---- lanes (element, dy, dz): transpose in x -> element outputs [e][dx][dz][dy] in sYQ
-      if (actL)
-      {
-         CBasis *bp = stage_basis(btab);
-         const double *in = sXL + eL * SA + lL;
-         double l0[Q], l1[Q];
-#pragma unroll
-         for (int qx = 0; qx < Q; qx++)
-         {
-            l0[qx] = in[qx * DD];
-            l1[qx] = in[Q * DD + qx * DD];
-         }
-#pragma unroll
-         for (int dx = 0; dx < D; dx++)
-         {
-            double v = 0.0;
-#pragma unroll
-            for (int qx = 0; qx < Q; qx++) { v += bp->G[qx + MQ * dx] * l0[qx] + bp->B[qx + MQ * dx] * l1[qx]; }
-            sYQ[eL * SB + dx * DD + lL] = v;  // sYQ is free: stage 4 read it before a barrier
-         }
-      }
-      __syncthreads();
-      // ---- lattice points: sum the holders in a fixed (z, y, x) order, store or publish
-#pragma unroll
-      for (int i = 0; i < NPL; i++)
-      {
-         const int p = t + i * NT;
-         if (p >= NB) { continue; }
-         const int X = p % LX, Y = (p / LX) % LY, Z = p / (LX * LY);
-         int cx, lx, nx, cy, ly, ny, cz, lz, nz;
-         brick_cand<D>(X, cx, lx, nx);
-         brick_cand<D>(Y, cy, ly, ny);
-         if (BZ == 2) { brick_cand<D>(Z, cz, lz, nz); }
-         else { cz = 0; lz = Z; nz = 1; }
-         double v = 0.0;
-         for (int iz = 0; iz < nz; iz++)
-            for (int iy = 0; iy < ny; iy++)
-               for (int ix = 0; ix < nx; ix++)
-               {
-                  const int elt = (cx + ix) + 2 * ((cy + iy) + 2 * (cz + iz));
-                  v += sYQ[elt * SB + (ix ? 0 : lx) * DD + (iz ? 0 : lz) * D + (iy ? 0 : ly)];
-               }
-         const int g = bst[i];
-         const int d = bdof(g);
-         if (!bshared(g)) { *((!SPLIT || d < n_owned) ? y + d : yg + (d - n_owned)) = v; }
-         else { part[(size_t)k * S::SURF + brick_surface_index(D, BZ, X, Y, Z)] = v; }  // surface only (setup)
-      }
-      // the next brick's stage 1 writes sXL (last read by stage 5, before the barrier above);
-      // its stage 2 writes sYQ after the barrier that follows stage 1 (the lattice sum above
-      // is done by then)
    }
 }
 
@@ -992,34 +743,6 @@ void launch_line_dq(bool mass, bool diff, const ApplyArgs &a, hipStream_t s)
    else if (diff) { launch_line_mdq<D, Q, false, true>(a, s); }
 }
 
-// Workgroups of the persistent brick kernel: what one CU holds at once (LDS, registers)
-// times the CUs, at most one per brick.
-template <typename K>
-int persistent_grid(K kernel, int nt, int nwork)
-{
-   static int cus = 0;
-   if (!cus)
-   {
-      int dev = 0;
-      ECM2_HIP(hipGetDevice(&dev));
-      ECM2_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-   }
-   int per_cu = 0;
-   ECM2_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, nt, 0));
-   return std::max(1, std::min(nwork, std::max(1, per_cu) * cus));
-}
-
-// experiment switch of this round's brick-kernel A/B (ECM2_BRICK_AB=0: the persistent
-// kernel; default: one brick per workgroup); removed with the losing variant
-static bool brick_ab_old()
-{
-   static const bool v = [] {
-      const char *e = std::getenv("ECM2_BRICK_AB");
-      return !(e && e[0] == '0');
-   }();
-   return v;
-}
-
 template <int D, int BZ>
 void launch_brick(const ApplyArgs &a, hipStream_t s)
 {
@@ -1028,26 +751,13 @@ void launch_brick(const ApplyArgs &a, hipStream_t s)
    if (k1 <= k0) { return; }
    ECM2_VERIFY(a.part_brick, ERR_INTERNAL, "brick kernel needs its partial slots");
    const bool split = a.xg || a.yg, aff = a.kind == QLAYOUT_AFFINE_E;
-   if (brick_ab_old() || !aff)  // the full per-point qdata (7 Q values per lane) does not fit the pipeline
-   {
-      const dim3 grid(k1 - k0), block(BrickShape<D, Q, BZ>::NT);
-#define ECM2_BRICK(SP, AF)                                                                                \
-   hipLaunchKernelGGL((k_apply_brick<D, Q, BZ, SP, AF>), grid, block, 0, s, k0, k1, a.belem, a.bmap, a.n_owned, \
-                      a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, a.btab, a.part_brick)
-      if (split) { if (aff) { ECM2_BRICK(true, true); } else { ECM2_BRICK(true, false); } }
-      else { if (aff) { ECM2_BRICK(false, true); } else { ECM2_BRICK(false, false); } }
-#undef ECM2_BRICK
-      return;
-   }
-   constexpr int NT = BrickShapeP<D, Q, BZ>::NT;
-#define ECM2_BRICK(SP, AF)                                                                                \
-   {                                                                                                      \
-      auto kern = k_apply_brick_p<D, Q, BZ, SP, AF>;                                                      \
-      hipLaunchKernelGGL(kern, dim3(persistent_grid(kern, NT, k1 - k0)), dim3(NT), 0, s, k0, k1, a.belem, \
-                         a.bmap, a.n_owned, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, a.btab, a.part_brick);    \
-   }
-   if (split) { ECM2_BRICK(true, true); }
-   else { ECM2_BRICK(false, true); }
+   const dim3 grid(k1 - k0), block(BrickShapeC<D, Q, BZ>::NT);
+#define ECM2_BRICK(SP, AF, RG)                                                                             \
+   hipLaunchKernelGGL((k_apply_brick_c<D, Q, BZ, SP, AF, RG>), grid, block, 0, s, k0, k1, a.belem, a.bmap,    \
+                      a.breg, a.n_owned, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, a.btab, a.part_brick)
+   if (split) { if (aff) { ECM2_BRICK(true, true, false); } else { ECM2_BRICK(true, false, false); } }
+   else if (a.breg) { if (aff) { ECM2_BRICK(false, true, true); } else { ECM2_BRICK(false, false, true); } }
+   else { if (aff) { ECM2_BRICK(false, true, false); } else { ECM2_BRICK(false, false, false); } }
 #undef ECM2_BRICK
 }
 

@@ -251,7 +251,7 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
             for (int dx = 0; dx < D; dx++)
             {
                double yo = Yo[(dz * D + dy) * D + dx] + p0 * T0[dx];
-               if (DIFF) { yo += p1 * T1[dx] + p2 * T2[dx]; }
+               if (DIFF) { yo += p1 * T1[dx]; yo += p2 * T2[dx]; }
                Yo[(dz * D + dy) * D + dx] = yo;
             }
          }
@@ -392,7 +392,8 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                for (int dx = 0; dx < D; dx++)
                {
                   const double bq = b.B[qx + MQ * dx], gq = b.G[qx + MQ * dx];
-                  T0[dx] += bq * m + gq * fx;
+                  T0[dx] += bq * m;
+                  T0[dx] += gq * fx;
                   T1[dx] += bq * fy;
                   T2[dx] += bq * fz;
                }
@@ -404,7 +405,8 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 #pragma unroll
                for (int dx = 0; dx < D; dx++)
                {
-                  SB[dy][dx] += by * T0[dx] + gy * T1[dx];
+                  SB[dy][dx] += by * T0[dx];
+                  SB[dy][dx] += gy * T1[dx];
                   SG[dy][dx] += by * T2[dx];
                }
             }
@@ -418,7 +420,8 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 #pragma unroll
                for (int dx = 0; dx < D; dx++)
                {
-                  Yo[(dz * D + dy) * D + dx] += bz[dz] * SB[dy][dx] + gz[dz] * SG[dy][dx];
+                  Yo[(dz * D + dy) * D + dx] += bz[dz] * SB[dy][dx];
+                  Yo[(dz * D + dy) * D + dx] += gz[dz] * SG[dy][dx];
                }
       }
    }  // wave_on
@@ -542,7 +545,8 @@ k_apply_tpe_pp(int ne, int blk_begin, int n_owned, const int *__restrict__ gmap,
             for (int dx = 0; dx < D; dx++)
             {
                const double bq = b.B[qx + MQ * dx], gq = b.G[qx + MQ * dx];
-               T0[dx] += bq * m + gq * fx;
+               T0[dx] += bq * m;
+               T0[dx] += gq * fx;
                T1[dx] += bq * fy;
                T2[dx] += bq * fz;
             }
@@ -554,7 +558,8 @@ k_apply_tpe_pp(int ne, int blk_begin, int n_owned, const int *__restrict__ gmap,
 #pragma unroll
             for (int dx = 0; dx < D; dx++)
             {
-               SB[dy][dx] += by * T0[dx] + gy * T1[dx];
+               SB[dy][dx] += by * T0[dx];
+               SB[dy][dx] += gy * T1[dx];
                SG[dy][dx] += by * T2[dx];
             }
          }

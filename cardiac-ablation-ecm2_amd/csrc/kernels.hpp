@@ -123,6 +123,7 @@ struct ApplyArgs
    // LINE, brick part (p >= 3 on structured regions): bricks of 2 x 2 x brick_bz elements
    const int *belem = nullptr;      // device [nbrick][4 bz] element ids (qdata addressing)
    const int *bmap = nullptr;       // device [nbrick][NB] lattice map: dof | shared << 30
+   const int *breg = nullptr;       // device [nbrick][8]: regular bricks (base, sx, sy, sz, face mask), or null
    const int *brick_off = nullptr;  // host [nblk + 1], bricks whose first element lies in block b
    int brick_bz = 0;                // 0: no bricks
    double *part_brick = nullptr;    // partial slots [nbrick][surface] of shared lattice points

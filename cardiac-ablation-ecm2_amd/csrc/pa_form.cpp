@@ -564,6 +564,44 @@ void PAForm::assemble(hipStream_t s)
          }
       }
       build_shared_plan(hcount, hdof, hslot, s);
+      // Regular bricks: every brick's lattice map an affine function of the lattice point
+      // (d = base + X sx + Y sy + Z sz, a lattice-numbered mesh) and its shared points exactly
+      // those on the brick faces other holders touch (one face-mask bit per face) -- the kernel
+      // then computes dofs and shared flags from 5 ints per brick instead of reading the map
+      breg_.resize(0);
+      if (n_bricks_ && n_owned_ == ndofs_)
+      {
+         const int LZ = brick_bz_ * (D_ - 1) + 1;
+         std::vector<int> reg((size_t)n_bricks_ * 8, 0);
+         bool regular = true;
+         for (int k = 0; k < n_bricks_ && regular; k++)
+         {
+            const int *b = &bdof[(size_t)k * brick_np_];
+            const int base = b[0], sx = b[1] - base, sy = b[LX] - base, sz = b[LX * LY] - base;
+            auto faces = [&](int X, int Y, int Z) {
+               return (X == 0) | (X == LX - 1) << 1 | (Y == 0) << 2 | (Y == LY - 1) << 3 | (Z == 0) << 4 |
+                      (Z == LZ - 1) << 5;
+            };
+            // face bit = sharing of a point inside that face (on no other face)
+            const int cx = LX / 2, cy = LY / 2, cz = LZ / 2;
+            const int probe[6][3] = {{0, cy, cz}, {LX - 1, cy, cz}, {cx, 0, cz}, {cx, LY - 1, cz}, {cx, cy, 0}, {cx, cy, LZ - 1}};
+            int mask = 0;
+            for (int f = 0; f < 6; f++)
+            {
+               const int p = (probe[f][2] * LY + probe[f][1]) * LX + probe[f][0];
+               if (hcount[b[p]] > 1) { mask |= 1 << f; }
+            }
+            for (int p = 0; p < brick_np_ && regular; p++)
+            {
+               const int X = p % LX, Y = (p / LX) % LY, Z = p / (LX * LY);
+               regular = b[p] == base + X * sx + Y * sy + Z * sz &&
+                         (hcount[b[p]] > 1) == ((faces(X, Y, Z) & mask) != 0);
+            }
+            int *r = &reg[(size_t)k * 8];
+            r[0] = base; r[1] = sx; r[2] = sy; r[3] = sz; r[4] = mask;
+         }
+         if (regular) { breg_.upload(reg, s); }
+      }
       gmap_line_.upload(enc, s);
       lelem_.upload(lelem.empty() ? std::vector<int>{0} : lelem, s);
       lelem_off_ = coff;
@@ -804,6 +842,7 @@ ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, doubl
       a.belem = belem_.data();
       a.bmap = bmap_.data();
       a.brick_off = brick_off_.data();
+      a.breg = breg_.size() ? breg_.data() : nullptr;
    }
    return a;
 }

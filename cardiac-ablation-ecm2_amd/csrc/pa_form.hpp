@@ -181,6 +181,7 @@ private:
    std::vector<int> splits_;        // apply_blocks range boundaries besides 0 / nblk
    int n_bricks_ = 0, brick_bz_ = 0, brick_np_ = 0;  // LINE bricks: count, 2 x 2 x bz, lattice points
    DeviceArray<int> belem_, bmap_;  // LINE bricks: [nbrick][4 bz] elements, [nbrick][np] lattice map
+   DeviceArray<int> breg_;          // LINE bricks, lattice-numbered: [nbrick][8] (base, sx, sy, sz, face mask)
    std::vector<int> brick_off_;     // LINE bricks of block b = [brick_off_[b], brick_off_[b+1])
    long part_line_off_ = 0;         // LINE: leftover elements' partial slots start here
    int n_left_ = 0;                 // LINE: elements outside bricks

@@ -47,8 +47,9 @@ double rccl_p2p_selftest(bool graph, int n)
    for (int rep = 0; rep < 3; rep++)
    {
       for (int i = 0; i < n; i++) { h[i] = 0.5 * i + rep; }
-      ECM2_HIP(hipMemcpy(a.data(), h.data(), sizeof(double) * n, hipMemcpyHostToDevice));
-      ECM2_HIP(hipMemset(b.data(), 0, sizeof(double) * n));
+      // on st: a non-blocking stream does not order itself after the null stream's memset
+      ECM2_HIP(hipMemcpyAsync(a.data(), h.data(), sizeof(double) * n, hipMemcpyHostToDevice, st));
+      ECM2_HIP(hipMemsetAsync(b.data(), 0, sizeof(double) * n, st));
       auto exchange = [&] {
          ECM2_NCCL(ncclGroupStart());
          ECM2_NCCL(ncclSend(a.data(), n, ncclFloat64, 0, comm, st));
@@ -71,7 +72,8 @@ double rccl_p2p_selftest(bool graph, int n)
       else { exchange(); }
       ECM2_HIP(hipStreamSynchronize(st));
       std::vector<double> r(std::max(1, n));
-      ECM2_HIP(hipMemcpy(r.data(), b.data(), sizeof(double) * n, hipMemcpyDeviceToHost));
+      ECM2_HIP(hipMemcpyAsync(r.data(), b.data(), sizeof(double) * n, hipMemcpyDeviceToHost, st));
+      ECM2_HIP(hipStreamSynchronize(st));
       for (int i = 0; i < n; i++) { err = std::max(err, std::fabs(r[i] - h[i])); }
       if (graph && rep == 2) { ECM2_HIP(hipGraphExecDestroy(ge)); ge = nullptr; }
    }

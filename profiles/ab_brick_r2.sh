@@ -1,21 +1,28 @@
 #!/bin/bash
 # Round-2 A/B of the p >= 3 brick kernel at C5 (68^3, p = 4), one box:
-#   ECM2_BRICK_AB=1: one brick per workgroup (round-1 kernel)
-#   default:         persistent, conflict-free LDS images, next brick's qdata prefetched
-# bench lines (alternating, twice each) and a rocprofv3 kernel-trace of each.
+#   ECM2_BRICK_AB=1: one brick per workgroup, round-1 LDS images (k_apply_brick)
+#   ECM2_BRICK_AB=2: conflict-free LDS images, regular-lattice addressing, gather-first load order,
+#                    one brick per workgroup (k_apply_brick_c)
+#   default:         the same stages, persistent workgroups prefetching the next brick's gather and
+#                    qdata behind the current brick's z stage (k_apply_brick_r)
+# brick parity tests under the default, then bench lines (alternating, twice each) and a
+# rocprofv3 kernel-trace of each.
 set -uo pipefail
 O=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/ab_brick
 mkdir -p "$O"
 export TMPDIR=/tmp
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+  -k "brick or c5 or line or affine or sdirk" > "$O/pytest_brick.log" 2>&1 || { tail -30 "$O/pytest_brick.log"; exit 1; }
+tail -2 "$O/pytest_brick.log"
 for rep in 1 2; do
-  for v in 1 0; do
+  for v in 1 2 0; do
     ECM2_BRICK_AB=$v timeout -k 10 300 python3 bench.py --workload c5 --steps 30 --warmup 5 --no-cpu-baseline \
       --full-layout 0 > "$O/bench_v${v}_r${rep}.json" 2> "$O/bench_v${v}_r${rep}.err" || exit $?
     python3 -c "import json,sys; d=json.loads(open('$O/bench_v${v}_r${rep}.json').read().strip().splitlines()[-1]); print('AB=$v rep $rep', d['value'], d['ms_per_step'], d['roofline']['kernel_ms_avg'])"
   done
 done
-for v in 1 0; do
+for v in 1 2 0; do
   ECM2_BRICK_AB=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/trace_v$v" -o run --output-format csv \
     -- python3 bench.py --workload c5 --steps 20 --warmup 3 --no-cpu-baseline --full-layout 0 > "$O/trace_v$v.json" 2>&1 || exit $?
-  find "$O/trace_v$v" -name "*kernel_stats.csv" -exec head -6 {} \;
+  find "$O/trace_v$v" -name "*kernel_stats.csv" -exec head -4 {} \;
 done

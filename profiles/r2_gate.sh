@@ -10,5 +10,8 @@ grep -E "FAILED|ERROR" "$O/pytest_gpu.log" | head -20
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 timeout -k 10 400 python3 bench.py --steps 20 --warmup 5 > "$O/bench_c4.json" 2> "$O/bench_c4.err" || exit $?
 cat "$O/bench_c4.json"
-[ "${1:-}" = "ab" ] && bash profiles/ab_brick_r2.sh
+timeout -k 10 400 python3 bench.py --workload c5 --steps 30 --warmup 5 --full-layout 0 --no-cpu-baseline > "$O/bench_c5.json" 2> "$O/bench_c5.err" || exit $?
+cat "$O/bench_c5.json"
+if [ "${1:-}" = "ab" ]; then bash profiles/ab_brick_r2.sh || exit $?; fi
+if [ "${1:-}" = "sq" ]; then bash profiles/sq_pass.sh c5 --workload c5 --steps 10 --warmup 2 --full-layout 0 || exit $?; fi
 exit $rc

@@ -20,9 +20,11 @@ def main(prof_dir, workload, key):
         "WRITE_SIZE_kB_avg": k["WRITE_SIZE_kB_avg"],
         "dispatches": k["dispatches"],
         "trace_avg_ns": (k.get("trace") or {}).get("avg_ns"),
-        "correction": s["correction"] + ("" if key == "apply" else
-                                         "; this kernel's loads are 8 B per lane, for which the guide's halving "
-                                         "is uncalibrated: treat as an upper bound"),
+        "correction": s["correction"] + "; the halving is calibrated for 4, 8 and 16 B/lane reads and for "
+                                        "one-lane-per-128-B-line gathers, WRITE_SIZE exact for 8 and 16 B/lane "
+                                        "stores (profiles/r2_fetch_calibration.json)",
+        "commit": os.environ.get("COMMIT"),
+        "date": os.environ.get("PIN_DATE"),
         "hbm_bytes_per_launch": k["hbm_bytes_per_launch"],
         "algorithmic_bytes_per_launch": alg,
         "traffic_over_algorithmic": k["hbm_bytes_per_launch"] / alg if alg else None,

@@ -1,7 +1,8 @@
 #!/bin/bash
-# Round-2 evidence in one pass per workload, same tree, same box: the bench line, the
-# rocprofv3 kernel-trace stats, the FETCH_SIZE and WRITE_SIZE passes (separate: TCC slots),
-# reduced (pmc_reduce.py) and pinned with provenance (pmc_pin.py; COMMIT = the tree's commit).
+# Round-2 evidence in one pass per workload, same tree, same box: the rocprofv3 kernel-trace
+# stats, the FETCH_SIZE and WRITE_SIZE passes (separate: TCC slots), reduced (pmc_reduce.py)
+# and pinned with provenance (pmc_pin.py; COMMIT = the tree's commit), then the bench line
+# reading that pin.
 # Usage: COMMIT=<sha> bash profiles/collect_r2.sh <workload-set: a | b>
 #   a: c4 (affine, the default line), c4 full layout (blocked), c5 (bricks)
 #   b: c2, c3
@@ -15,7 +16,6 @@ one() {  # tag layout kernel_key bench-args...
   local args="$* --no-cpu-baseline --full-layout 0"
   local P="$O/prof_$tag"
   mkdir -p "$P"
-  timeout -k 10 400 python3 bench.py "$@" > "$O/bench_$tag.json" 2> "$O/bench_$tag.err" || return 1
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -T -d "$P/trace" -o run --output-format csv \
     -- python3 bench.py $args > "$P/bench_trace.json" 2> "$P/trace.err" || return 1
   timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -T -d "$P/fetch" -o run --output-format csv \
@@ -24,6 +24,9 @@ one() {  # tag layout kernel_key bench-args...
     -- python3 bench.py $args > "$P/bench_write.json" 2> "$P/write.err" || return 1
   python3 profiles/pmc_reduce.py "$P" > "$P/pmc_summary.json" || return 1
   python3 profiles/pmc_pin.py "$P" "${tag%%_*}" "$key" > "$O/pmc_${tag%%_*}_n1_${layout}.json" || return 1
+  # the bench line last, reading the pin just made (this box's copy of profiles/)
+  cp "$O/pmc_${tag%%_*}_n1_${layout}.json" profiles/
+  timeout -k 10 400 python3 bench.py "$@" > "$O/bench_$tag.json" 2> "$O/bench_$tag.err" || return 1
   echo "$tag: $(tail -1 "$O/bench_$tag.json" | cut -c1-160)"
 }
 if [ "$SET" = a ]; then

@@ -13,6 +13,7 @@ namespace dev
 
 constexpr int MQ = MAX_Q1D;
 typedef double v2d __attribute__((ext_vector_type(2)));
+typedef double v4d __attribute__((ext_vector_type(4)));
 
 inline unsigned grid_for(long n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 

@@ -338,7 +338,7 @@ __device__ __forceinline__ int brick_faces(int X, int Y, int Z)
    return (X == 0) | (X == LX - 1) << 1 | (Y == 0) << 2 | (Y == LY - 1) << 3 | (Z == 0) << 4 | (Z == LZ - 1) << 5;
 }
 
-template <int D, int Q, int BZ, bool SPLIT, bool AFF, bool REG, bool MF = false>
+template <int D, int Q, int BZ, bool SPLIT, bool AFF, bool REG>
 __global__ void __launch_bounds__((BrickShapeC<D, Q, BZ>::NT), (BrickShapeC<D, Q, BZ>::WPE))
 k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int *__restrict__ bmap,
                 const int *__restrict__ breg, int n_owned, const double *__restrict__ qdd,
@@ -382,41 +382,6 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
    const int e = belem[(size_t)k * NE + (e3 < NE ? e3 : NE - 1)];
    const int l3c = l3 < QQ ? l3 : QQ - 1;
    double xl[D];
-   // MF (experiment, REG only): the x stage as a GEMM on the matrix cores, [lines x D] x [D x 2Q]
-   // in 16 x 16 x 4 f64 tiles -- A[line][dx] gathered straight into the operand layout (row =
-   // lane & 15, k = lane >> 4), B[dx][(f, qx)] from the basis, C (col = lane & 15, row =
-   // (lane >> 4) + 4 i) stored into the x-line image
-   static_assert(!MF || (REG && !SPLIT), "matrix-core x stage: regular bricks only");
-   constexpr int NTILE = (NE * DD + 15) / 16, NW = S::NT / 64, TPW = (NTILE + NW - 1) / NW, KS = (D + 3) / 4;
-   const int wv = t >> 6, mk = (t & 63) >> 4, mc = t & 15;
-   double am[TPW][KS], bo[KS];
-   if (MF)
-   {
-#pragma unroll
-      for (int ks = 0; ks < KS; ks++)  // B operand: per-lane loads, with the gather
-      {
-         const int dx = 4 * ks + mk;
-         const int c = mc < 2 * Q ? mc : 0;
-         const double v = c < Q ? btab->B[c + MQ * (dx < D ? dx : 0)] : btab->G[c - Q + MQ * (dx < D ? dx : 0)];
-         bo[ks] = (dx < D && mc < 2 * Q) ? v : 0.0;
-      }
-#pragma unroll
-      for (int j = 0; j < TPW; j++)
-      {
-         int line = 16 * (wv + NW * j) + mc;
-         line = line < NE * DD ? line : NE * DD - 1;
-         const int el = line / DD, ll = line % DD, dy = ll % D, dz = ll / D;
-         const int ex = el & 1, ey = (el >> 1) & 1, ez = el >> 2;
-         const int d0 = base + (ex * (D - 1)) * sx + (ey * (D - 1) + dy) * sy + (ez * (D - 1) + dz) * sz;
-#pragma unroll
-         for (int ks = 0; ks < KS; ks++)
-         {
-            const int dx = 4 * ks + mk;
-            am[j][ks] = x[d0 + (dx < D ? dx : D - 1) * sx];  // dx >= D: B row is 0
-         }
-      }
-   }
-   else
    {
       const int dy = lLc % D, dz = lLc / D, ex = eLc & 1, ey = (eLc >> 1) & 1, ez = eLc >> 2;
       if (REG)
@@ -450,31 +415,7 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
    else { line_load_qdata<D, Q, true, true, false>(qv, e, l3c, qdd, qdm); }
 
    // ---- lanes (element, dy, dz): contract in x -> sXL [f][qx][l]
-   if (MF)
-   {
-#pragma unroll
-      for (int j = 0; j < TPW; j++)
-      {
-         const int tile = wv + NW * j;
-         if (tile < NTILE)  // wave-uniform
-         {
-            v4d acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int ks = 0; ks < KS; ks++) { acc = __builtin_amdgcn_mfma_f64_16x16x4f64(am[j][ks], bo[ks], acc, 0, 0, 0); }
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-            {
-               const int line = 16 * tile + mk + 4 * i;
-               if (line < NE * DD && mc < 2 * Q)
-               {
-                  const int f = mc / Q, qx = mc % Q;
-                  sXL[(line / DD) * SA + (f * Q + qx) * DD + line % DD] = acc[i];
-               }
-            }
-         }
-      }
-   }
-   else if (actL)
+if (actL)
    {
       CBasis *bp = stage_basis(btab);
       double *o = sXL + eL * SA + lL;
@@ -495,18 +436,8 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
    if (k_begin < 0)  // never: a use outside the x stage stops the gather sinking behind the qdata
    {
       double u = 0.0;
-      if (MF)
-      {
 #pragma unroll
-         for (int j = 0; j < TPW; j++)
-#pragma unroll
-            for (int ks = 0; ks < KS; ks++) { u += am[j][ks] + bo[ks]; }
-      }
-      else
-      {
-#pragma unroll
-         for (int dx = 0; dx < D; dx++) { u += xl[dx]; }
-      }
+      for (int dx = 0; dx < D; dx++) { u += xl[dx]; }
       part[t] = u;
    }
    __syncthreads();
@@ -812,17 +743,6 @@ void launch_line_dq(bool mass, bool diff, const ApplyArgs &a, hipStream_t s)
    else if (diff) { launch_line_mdq<D, Q, false, true>(a, s); }
 }
 
-// experiment switch of this round's matrix-core A/B (ECM2_BRICK_MFMA=1: the x stage of regular
-// AFFINE_E bricks on v_mfma_f64_16x16x4f64); removed with the losing variant
-static bool brick_mfma()
-{
-   static const bool v = [] {
-      const char *e = std::getenv("ECM2_BRICK_MFMA");
-      return e && e[0] == '1';
-   }();
-   return v;
-}
-
 template <int D, int BZ>
 void launch_brick(const ApplyArgs &a, hipStream_t s)
 {
@@ -836,11 +756,6 @@ void launch_brick(const ApplyArgs &a, hipStream_t s)
    hipLaunchKernelGGL((k_apply_brick_c<D, Q, BZ, SP, AF, RG>), grid, block, 0, s, k0, k1, a.belem, a.bmap,    \
                       a.breg, a.n_owned, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, a.btab, a.part_brick)
    if (split) { if (aff) { ECM2_BRICK(true, true, false); } else { ECM2_BRICK(true, false, false); } }
-   else if (a.breg && aff && brick_mfma())
-   {
-      hipLaunchKernelGGL((k_apply_brick_c<D, Q, BZ, false, true, true, true>), grid, block, 0, s, k0, k1, a.belem, a.bmap,
-                         a.breg, a.n_owned, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, a.btab, a.part_brick);
-   }
    else if (a.breg) { if (aff) { ECM2_BRICK(false, true, true); } else { ECM2_BRICK(false, false, true); } }
    else { if (aff) { ECM2_BRICK(false, true, false); } else { ECM2_BRICK(false, false, false); } }
 #undef ECM2_BRICK

@@ -415,7 +415,7 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
    else { line_load_qdata<D, Q, true, true, false>(qv, e, l3c, qdd, qdm); }
 
    // ---- lanes (element, dy, dz): contract in x -> sXL [f][qx][l]
-if (actL)
+   if (actL)
    {
       CBasis *bp = stage_basis(btab);
       double *o = sXL + eL * SA + lL;

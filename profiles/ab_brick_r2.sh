@@ -1,4 +1,6 @@
 #!/bin/bash
+# NOTE: the experiment's switch was deleted with the losing variant after this run; the script is
+# kept as the recipe that produced the committed result (profiles/r2_ab_*.txt).
 # Round-2 A/B of the p >= 3 brick kernel at C5 (68^3, p = 4), one box:
 #   ECM2_BRICK_AB=1: one brick per workgroup, round-1 LDS images (k_apply_brick)
 #   ECM2_BRICK_AB=2: conflict-free LDS images, regular-lattice addressing, gather-first load order,

@@ -1,4 +1,6 @@
 #!/bin/bash
+# NOTE: the experiment's switch was deleted with the losing variant after this run; the script is
+# kept as the recipe that produced the committed result (profiles/r2_ab_*.txt).
 # Round-2 matrix-core experiment at C5 (68^3, p = 4), one box:
 #   ECM2_BRICK_MFMA=1: the brick kernel's x stage ([lines x D] x [D x 2Q] per brick) on
 #                      v_mfma_f64_16x16x4f64 tiles (k_apply_brick_c<..., MF = true>)

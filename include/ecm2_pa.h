@@ -182,10 +182,10 @@ int ecm2_pa_form_assemble(ecm2_pa_form *f, void *stream);
  * bilinearform_ext.cpp:487-564): y = A x, y overwritten.  x, y device [ndofs]. */
 int ecm2_pa_form_mult(ecm2_pa_form *f, const double *x, double *y, void *stream);
 /* PABilinearFormExtension::MultTranspose (bilinearform_ext.hpp:99, bilinearform_ext.cpp:
- * 566-677): y = A^T x.  Mass + Diffusion with scalar coefficients are symmetric, so this is
+ * 679-): y = A^T x.  Mass + Diffusion with scalar coefficients are symmetric, so this is
  * the Mult (tests/test_gpu_parity.py asserts the equality). */
 int ecm2_pa_form_mult_transpose(ecm2_pa_form *f, const double *x, double *y, void *stream);
-/* Operator::AddMult (linalg/operator.hpp:87-92): y += a A x. */
+/* Operator::AddMult (linalg/operator.hpp:108-109): y += a A x. */
 int ecm2_pa_form_add_mult(ecm2_pa_form *f, const double *x, double *y, double a, void *stream);
 /* PABilinearFormExtension::AssembleDiagonal (bilinearform_ext.cpp:370-454). diag device [ndofs]. */
 int ecm2_pa_form_assemble_diagonal(ecm2_pa_form *f, double *diag, void *stream);

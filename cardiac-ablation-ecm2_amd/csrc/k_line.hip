@@ -444,7 +444,6 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
    // ---- lanes (element, qx, dz), l2 = qx + Q dz: contract in y -> sYQ [g][dz][qy][qx]
    if (act2)
    {
-      CBasis *bp = stage_basis(btab);
       const int qx = lL % Q, dz = lL / Q;
       const double *in = sXL + eL * SA + qx * DD + dz * D;
       double la[D], lb[D];

@@ -379,33 +379,47 @@ __global__ void k_scatter_add_idx(int n, const int *__restrict__ idx, const doub
    if (i < n) { unsafeAtomicAdd(y + idx[i], buf[i]); }
 }
 
-// Second pass of the deterministic scatter: y[dofs[i]] = sum of the partial slots
-// slots[start .. start+count) in ascending slot order, for i in [i0, i1), with
-// meta[i] = start << 5 | count.  All slot loads, then all partial loads, are issued
-// independently (count <= 8 unrolled; more -- unstructured meshes -- loops), so a
-// thread waits ~3 memory latencies instead of 2 + 2*count.  The list is ordered by
-// first slot (pa_form.cpp), so neighbouring threads read neighbouring lanes; blocks are
-// taken in XCD-contiguous order, so the slot lines neighbouring dofs read sit in one L2.
-__global__ void k_sum_partials(int i0, int i1, const int *__restrict__ dofs, const unsigned *__restrict__ meta,
-                               const int *__restrict__ slots, const double *__restrict__ part, int n_owned,
-                               double *__restrict__ y, double *__restrict__ yg)
+// Second pass of the deterministic scatter, run-compressed (pa_form.cpp, build_shared_plan):
+// the shared dofs of a brick face or a lane row form runs -- 1D or 2D lattices of plan
+// entries whose dof and every holder's partial slot are affine in the entry's position.  A
+// workgroup takes whole runs (<= 256 entries), stages their 48-byte descriptors in LDS in one
+// coalesced read, and each thread finds its run there: two dependent global reads before the
+// partials (block table, descriptors), as the per-entry plan had (meta, slot list), with ~12
+// instead of ~24 plan bytes per 2-holder dof.  A dof's holders are summed in ascending slot
+// order.  Workgroups are taken in XCD-contiguous order (neighbouring runs, neighbouring slots).
+constexpr int kRunInts = 12;
+__global__ void __launch_bounds__(256)
+k_sum_partials(int b0, int b1, const int *__restrict__ blocks, const int *__restrict__ runs,
+               const int *__restrict__ rslots, const double *__restrict__ part, int n_owned,
+               double *__restrict__ y, double *__restrict__ yg)
 {
-   const int b = xcd_contiguous(blockIdx.x, gridDim.x);
-   const int i = i0 + b * blockDim.x + threadIdx.x;
-   if (i >= i1) { return; }
-   const unsigned m = meta[i];
-   const int d = dofs[i];
-   const int start = (int)(m >> 5), cnt = (int)(m & 31);
+   __shared__ int sd[257 * kRunInts];
+   const int blk = b0 + xcd_contiguous(blockIdx.x, gridDim.x);
+   if (blk >= b1) { return; }  // whole workgroup
+   const int r0 = blocks[2 * blk], nr = blocks[2 * blk + 1] - r0;
+   for (int k = threadIdx.x; k < (nr + 1) * kRunInts; k += blockDim.x) { sd[k] = runs[(size_t)r0 * kRunInts + k]; }
+   __syncthreads();
+   const int i = sd[6] + (int)threadIdx.x;
+   if (i >= sd[nr * kRunInts + 6]) { return; }
+   int lo = 0, hi = nr - 1;
+   while (lo < hi)
+   {
+      const int mid = (lo + hi + 1) >> 1;
+      if (sd[mid * kRunInts + 6] <= i) { lo = mid; }
+      else { hi = mid - 1; }
+   }
+   const int *R = sd + lo * kRunInts;
+   const int shape = R[0], n1 = shape & 255, cnt = shape >> 16;
+   const int off = i - R[6], pa = off % n1, pb = off / n1;
+   const int d = R[1] + pa * R[2] + pb * R[3];
+   const int ds = pa * R[4] + pb * R[5];
+   double v[4];
+#pragma unroll
+   for (int k = 0; k < 4; k++) { v[k] = k < cnt ? part[R[8 + k] + ds] : 0.0; }
    double acc = 0.0;
-   int sl[8];
 #pragma unroll
-   for (int k = 0; k < 8; k++) { sl[k] = k < cnt ? slots[start + k] : -1; }
-   double v[8];
-#pragma unroll
-   for (int k = 0; k < 8; k++) { v[k] = sl[k] >= 0 ? part[sl[k]] : 0.0; }
-#pragma unroll
-   for (int k = 0; k < 8; k++) { acc += v[k]; }
-   for (int k = 8; k < cnt; k++) { acc += part[slots[start + k]]; }
+   for (int k = 0; k < 4; k++) { acc += v[k]; }
+   for (int k = 4; k < cnt; k++) { acc += part[rslots[R[7] + k] + ds]; }
    if (d < n_owned) { y[d] = acc; }
    else { yg[d - n_owned] = acc; }
 }
@@ -587,13 +601,13 @@ void scatter_add_idx(int n, const int *idx, const double *buf, double *y, hipStr
    ECM2_HIP(hipGetLastError());
 }
 
-void sum_partials(int i0, int i1, const int *dofs, const unsigned *meta, const int *slots, const double *part,
+void sum_partials(int b0, int b1, const int *blocks, const int *runs, const int *rslots, const double *part,
                   int n_owned, double *y, double *yg, hipStream_t s)
 {
-   if (i1 <= i0) { return; }
-   ECM2_VERIFY(slots, ERR_INTERNAL, "summation pass needs its slot list");
-   hipLaunchKernelGGL(k_sum_partials, dim3(grid_for(i1 - i0, 256)), dim3(256), 0, s, i0, i1, dofs, meta, slots, part,
-                      n_owned, y, yg);
+   if (b1 <= b0) { return; }
+   ECM2_VERIFY(blocks && runs, ERR_INTERNAL, "summation pass needs its run plan");
+   hipLaunchKernelGGL(k_sum_partials, dim3(b1 - b0), dim3(256), 0, s, b0, b1, blocks, runs, rslots, part, n_owned, y,
+                      yg);
    ECM2_HIP(hipGetLastError());
 }
 

@@ -244,9 +244,13 @@ void stream_copy(long n, const double *a, double *b, hipStream_t s);
 // Halo pack/unpack for the distributed operator (K7): buf[i] = x[idx[i]] ; y[idx[i]] += buf[i]
 void gather_idx(int n, const int *idx, const double *x, double *buf, hipStream_t s);
 void scatter_add_idx(int n, const int *idx, const double *buf, double *y, hipStream_t s);
-// Deterministic second scatter pass: y[dofs[i]] = sum_j part[slots[j]], j in
-// [start, start + count), meta[i] = start << 5 | count.
-void sum_partials(int i0, int i1, const int *dofs, const unsigned *meta, const int *slots, const double *part,
+// Deterministic second scatter pass, run-compressed (PAForm::build_shared_plan), over plan
+// blocks [b0, b1): block k sums the entries of runs [blocks[2k], blocks[2k+1]) (<= 256 entries).
+// Run r = runs[r][12] = {n1 | n2 << 8 | cnt << 16, dof0, d1, d2, t1, t2, entry0, slot_off,
+// s0, s1, s2, s3}: its entry at lattice position (a, b) (offset a + n1 b from entry0) stores
+// y[dof0 + a d1 + b d2] = sum over holders h < cnt (ascending slots) of part[s_h + a t1 + b t2],
+// s_h = runs[r][8 + h] for h < 4, else rslots[slot_off + h].  runs has a sentinel row.
+void sum_partials(int b0, int b1, const int *blocks, const int *runs, const int *rslots, const double *part,
                   int n_owned, double *y, double *yg, hipStream_t s);
 } // namespace kern
 

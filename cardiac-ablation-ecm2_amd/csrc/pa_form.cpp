@@ -3,6 +3,8 @@
 #include "bricks.hpp"
 
 #include <algorithm>
+#include <map>
+#include <tuple>
 #include <array>
 #include <cmath>
 #include <cstdlib>
@@ -298,24 +300,136 @@ void PAForm::build_shared_plan(const std::vector<int> &hcount, const std::vector
       return (d < n_owned_ ? 0 : (1l << 40)) + first;
    };
    std::stable_sort(dofs.begin(), dofs.end(), [&](int p, int q) { return key(p) < key(q); });
-   std::vector<unsigned> meta;
-   std::vector<int> slots;
-   slots.reserve(slots_by_dof.size());
-   ECM2_VERIFY(slots_by_dof.size() < (1ull << 27), ERR_UNSUPPORTED, "too many partial slots");
-   for (int d : dofs)
-   {
-      const unsigned cnt = (unsigned)(start[d + 1] - start[d]);
-      ECM2_VERIFY(cnt < 32, ERR_UNSUPPORTED, "dof " << d << " held by " << cnt << " element entries");
-      meta.push_back((unsigned)slots.size() << 5 | cnt);
-      slots.insert(slots.end(), slots_by_dof.begin() + start[d], slots_by_dof.begin() + start[d + 1]);
-   }
+   ECM2_VERIFY(slots_by_dof.size() < (1ull << 31), ERR_UNSUPPORTED, "too many partial slots");
    n_sh_ = (int)dofs.size();
    n_sh_owned_ = 0;
    while (n_sh_owned_ < n_sh_ && dofs[n_sh_owned_] < n_owned_) { n_sh_owned_++; }
-   n_slots_ = (long)slots.size();
-   sh_dofs_.upload(dofs, s);
-   sh_meta_.upload(meta, s);
-   sh_slots_.upload(slots, s);
+   n_slots_ = (long)slots_by_dof.size();
+
+   // Run compression, per range ([owned | ghost]: finish_shared runs each on its own).  1D runs:
+   // consecutive entries (in the order above) with equal holder counts whose dof and every
+   // holder's slot advance by the same steps; 2D runs: 1D runs of one shape whose first entries
+   // advance by common steps again (a face interior, a 4 x 4 lane patch).  Entries are
+   // re-emitted run by run; each dof keeps its holders in ascending slot order.
+   auto cnt = [&](int d) { return hcount[d] > 1 ? start[d + 1] - start[d] : 0; };
+   auto slot = [&](int d, int h) { return slots_by_dof[start[d] + h]; };
+   struct Run { int n1, n2, c, dof0, d1, d2, t1, t2, first; std::vector<int> s0; };
+   std::vector<Run> runs;
+   std::vector<int> order;  // plan entries (dofs) in run-major order
+   for (int range = 0; range < 2; range++)
+   {
+      const int r0 = range ? n_sh_owned_ : 0, r1 = range ? n_sh_ : n_sh_owned_;
+      struct R1 { int i0, n, c, d1, t1; };
+      std::vector<R1> r1s;
+      for (int i = r0; i < r1;)
+      {
+         const int c = cnt(dofs[i]);
+         int n = 1, d1 = 0, t1 = 0;
+         while (i + n < r1 && n < 64 && c <= 8)
+         {
+            const int dj = dofs[i + n], dp = dofs[i + n - 1];
+            if (cnt(dj) != c) { break; }
+            const int dd = dj - dp, tt = c ? slot(dj, 0) - slot(dp, 0) : 0;
+            bool ok = n == 1 || (dd == d1 && tt == t1);
+            for (int h = 1; h < c && ok; h++) { ok = slot(dj, h) - slot(dp, h) == tt; }
+            if (!ok) { break; }
+            if (n == 1) { d1 = dd; t1 = tt; }
+            n++;
+         }
+         r1s.push_back({i, n, c, d1, t1});
+         i += n;
+      }
+      // 2D: one open run per (count, length, steps) class; a 1D run joins its class's open run
+      // when its first entry continues that run's lattice, else it opens a new one
+      std::vector<Run> out;
+      std::vector<std::vector<int>> members;  // 1D runs of each 2D run
+      std::map<std::tuple<int, int, int, int>, int> open;
+      for (size_t k = 0; k < r1s.size(); k++)
+      {
+         const R1 &q = r1s[k];
+         const int d0 = dofs[q.i0];
+         const auto key = std::make_tuple(q.c, q.n, q.d1, q.t1);
+         auto it = open.find(key);
+         bool joined = false;
+         if (it != open.end() && q.c <= 8)
+         {
+            Run &g = out[it->second];
+            if ((g.n2 + 1) * g.n1 <= 64)
+            {
+               const int dd = d0 - g.dof0, tt = q.c ? slot(d0, 0) - g.s0[0] : 0;
+               bool ok = g.n2 == 1 || (dd == g.n2 * g.d2 && tt == g.n2 * g.t2);
+               for (int h = 1; h < q.c && ok; h++) { ok = slot(d0, h) - g.s0[h] == tt; }
+               if (ok)
+               {
+                  if (g.n2 == 1) { g.d2 = dd; g.t2 = tt; }
+                  g.n2++;
+                  members[it->second].push_back((int)k);
+                  joined = true;
+               }
+            }
+         }
+         if (!joined)
+         {
+            Run g{q.n, 1, q.c, d0, q.d1, 0, q.t1, 0, q.i0, {}};
+            for (int h = 0; h < q.c; h++) { g.s0.push_back(slot(d0, h)); }
+            open[key] = (int)out.size();
+            out.push_back(g);
+            members.push_back({(int)k});
+         }
+      }
+      for (size_t g = 0; g < out.size(); g++)
+      {
+         out[g].first = (int)order.size();
+         for (int k : members[g])
+            for (int j = 0; j < r1s[k].n; j++) { order.push_back(dofs[r1s[k].i0 + j]); }
+         runs.push_back(std::move(out[g]));
+      }
+      ECM2_VERIFY((int)order.size() == r1, ERR_INTERNAL, "run plan lost entries");
+   }
+   std::vector<int> rdesc, rslots, blocks;
+   rdesc.reserve((runs.size() + 1) * 12);
+   for (const Run &g : runs)
+   {
+      // every entry of the run must be what the descriptor computes (checked, host side)
+      for (int j = 0; j < g.n1 * g.n2; j++)
+      {
+         const int a = j % g.n1, b = j / g.n1, d = order[g.first + j];
+         bool ok = d == g.dof0 + a * g.d1 + b * g.d2 && cnt(d) == g.c;
+         for (int h = 0; h < g.c && ok; h++) { ok = slot(d, h) == g.s0[h] + a * g.t1 + b * g.t2; }
+         ECM2_VERIFY(ok, ERR_INTERNAL, "run plan entry " << g.first + j << " does not match its run");
+      }
+      int row[12] = {g.n1 | g.n2 << 8 | g.c << 16, g.dof0, g.d1, g.d2, g.t1, g.t2, g.first, (int)rslots.size(), 0, 0, 0, 0};
+      for (int h = 0; h < g.c; h++)
+      {
+         if (h < 4) { row[8 + h] = g.s0[h]; }
+         rslots.push_back(g.s0[h]);
+      }
+      rdesc.insert(rdesc.end(), row, row + 12);
+   }
+   const int sentinel[12] = {1, 0, 0, 0, 0, 0, n_sh_, 0, 0, 0, 0, 0};
+   rdesc.insert(rdesc.end(), sentinel, sentinel + 12);
+   // blocks: whole runs, <= 256 entries each, never across the owned / ghost boundary
+   sh_nblk_owned_ = 0;
+   for (size_t r = 0; r < runs.size();)
+   {
+      const bool ghost = runs[r].first >= n_sh_owned_;
+      size_t e = r;
+      int n = 0;
+      while (e < runs.size() && (runs[e].first >= n_sh_owned_) == ghost && n + runs[e].n1 * runs[e].n2 <= 256)
+      {
+         n += runs[e].n1 * runs[e].n2;
+         e++;
+      }
+      blocks.push_back((int)r);
+      blocks.push_back((int)e);
+      if (!ghost) { sh_nblk_owned_++; }
+      r = e;
+   }
+   sh_nblk_ = (int)blocks.size() / 2;
+   n_runs_ = (long)runs.size();
+   sh_runs_.upload(rdesc, s);
+   sh_rslots_.upload(rslots.empty() ? std::vector<int>{0} : rslots, s);
+   sh_blocks_.upload(blocks.empty() ? std::vector<int>{0, 0} : blocks, s);
 }
 
 void PAForm::set_kernel(int mode)
@@ -808,7 +922,12 @@ void PAForm::set_scatter(int mode)
 void PAForm::finish_shared(int i0, int i1, double *y, double *yg, hipStream_t s)
 {
    if (!use_partials()) { return; }
-   kern::sum_partials(i0, i1, sh_dofs_.data(), sh_meta_.data(), sh_slots_.data(), part_.data(), n_owned_, y, yg, s);
+   // the plan's blocks cover the owned shared dofs [0, n_sh_owned_) then the ghost ones
+   ECM2_VERIFY((i0 == 0 || i0 == n_sh_owned_) && (i1 == n_sh_owned_ || i1 == n_sh_) && i0 <= i1, ERR_INTERNAL,
+               "summation range [" << i0 << ", " << i1 << ") is not a plan range");
+   const int b0 = i0 == 0 ? 0 : sh_nblk_owned_, b1 = i1 == n_sh_owned_ ? sh_nblk_owned_ : sh_nblk_;
+   kern::sum_partials(b0, b1, sh_blocks_.data(), sh_runs_.data(), sh_rslots_.data(), part_.data(), n_owned_, y, yg,
+                      s);
 }
 
 ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, double *yg, int b0,

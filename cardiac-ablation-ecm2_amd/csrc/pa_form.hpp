@@ -120,6 +120,7 @@ public:
    int n_shared() const { return n_sh_; }
    int n_shared_owned() const { return n_sh_owned_; }
    long n_partial_slots() const { return n_slots_; }
+   long n_summation_runs() const { return n_runs_; }
    int nblocks() const { return layout_.nblk(); }
    bool has_mass() const { return have_mass_; }
    bool has_diffusion() const { return have_diff_; }
@@ -163,8 +164,11 @@ private:
    int scatter_ = SCATTER_PARTIALS;
    int n_sh_ = 0, n_sh_owned_ = 0;
    long n_slots_ = 0;
-   DeviceArray<int> sh_dofs_, sh_slots_;           // second-pass plan (see finish_shared)
-   DeviceArray<unsigned> sh_meta_;                 // start << 5 | count
+   // second-pass plan (see finish_shared, kern::sum_partials): runs [nrun + 1][12], the
+   // first slots of holders beyond the fourth, blocks [nblk][2] (owned runs' blocks first)
+   DeviceArray<int> sh_runs_, sh_rslots_, sh_blocks_;
+   long n_runs_ = 0;
+   int sh_nblk_owned_ = 0, sh_nblk_ = 0;
    DeviceArray<double> part_;                       // partial slots: TPE [blk][nd][64]; LINE [bricks | [e][nd]]
    bool assembled_ = false;
    long gen_ = 0;

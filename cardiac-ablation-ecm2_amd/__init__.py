@@ -95,6 +95,7 @@ def load_library(path: str = LIB_PATH):
         "ecm2_pa_form_set_geometry_compression": (i32, [vp, i32]),
         "ecm2_pa_form_qdata_bytes": (i32, [vp, dp]),
         "ecm2_pa_form_brick_info": (i32, [vp, ip, ip]),
+        "ecm2_pa_form_addressing_info": (i32, [vp, ip, ctypes.POINTER(ctypes.c_long)]),
         "ecm2_pa_form_set_element_order": (i32, [vp, vp]),
         "ecm2_mesh_element_order": (i32, [vp, i32, vp]),
         "ecm2_pa_form_assemble": (i32, [vp, vp]),
@@ -428,6 +429,13 @@ class BilinearForm:
         n, m = ctypes.c_int(), ctypes.c_long()
         _check(_lib.ecm2_pa_form_scatter_info(self._h, ctypes.byref(n), ctypes.byref(m)))
         return n.value, m.value
+
+    def AddressingInfo(self):
+        """(lattice, n_runs) after Assemble: 1 when the fused kernel computes its dofs from the
+        lattice instead of reading the gather map; runs of the summation plan."""
+        n, r = ctypes.c_int(), ctypes.c_long()
+        _check(_lib.ecm2_pa_form_addressing_info(self._h, ctypes.byref(n), ctypes.byref(r)))
+        return n.value, r.value
 
     def BrickInfo(self):
         """(bricks, depth bz) of the p >= 3 brick kernel after Assemble (0, 0: none)."""

@@ -358,6 +358,15 @@ int ecm2_pa_form_brick_info(const ecm2_pa_form *f, int *n_bricks, int *bz)
    });
 }
 
+int ecm2_pa_form_addressing_info(const ecm2_pa_form *f, int *lattice, long *n_runs)
+{
+   return guard([&] {
+      NEED(f);
+      if (lattice) { *lattice = f->f->lattice_addressing() ? 1 : 0; }
+      if (n_runs) { *n_runs = f->f->n_summation_runs(); }
+   });
+}
+
 int ecm2_pa_form_scatter_info(const ecm2_pa_form *f, int *n_shared, long *n_slots)
 {
    return guard([&] {

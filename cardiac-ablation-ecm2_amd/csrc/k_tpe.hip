@@ -39,11 +39,18 @@ struct XwaveRows
 // xb[w][XR][64] (the kernel's x staging area, no longer read), a barrier, the receiving lanes
 // (high face, e_dir = 3) add it.  Every wave of the workgroup must call this (wave_on false:
 // barriers only).
-template <int D, bool SPLIT, bool SIGNS, bool XW>
+// REG (regular blocks, no signs): the lane's dofs are base + X sx + Y sy + Z sz on the block's
+// (4(D-1)+1)^3 lattice, shared iff on a block face whose bit is set in mask -- no map reads.
+struct TpeReg
+{
+   int base, sx, sy, sz, mask;
+};
+template <int D, bool SPLIT, bool SIGNS, bool XW, bool REG = false>
 __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], const int *__restrict__ mp, int fl,
                                                    int blk, int lane, bool active, int n_owned,
                                                    double *__restrict__ y, double *__restrict__ yg,
-                                                   double *__restrict__ part, double *xb, int w, bool wave_on)
+                                                   double *__restrict__ part, double *xb, int w, bool wave_on,
+                                                   TpeReg rg = {})
 {
    constexpr int ND = D * D * D, XR = XwaveRows<D>::R;
    if (SIGNS && wave_on)
@@ -104,10 +111,24 @@ __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], cons
          {
             if ((dx == 0 && sx) || (dy == 0 && sy) || (dz == 0 && sz)) { continue; }
             const int a = (dz * D + dy) * D + dx;
-            const int g = mp[a * 64];
-            const int d = bdof(g);
+            int d;
+            bool shared;
+            if (REG)
+            {
+               constexpr int L = 4 * (D - 1);
+               const int X = (D - 1) * (lane & 3) + dx, Y = (D - 1) * ((lane >> 2) & 3) + dy, Z = (D - 1) * (lane >> 4) + dz;
+               d = rg.base + X * rg.sx + Y * rg.sy + Z * rg.sz;
+               const int faces = (X == 0) | (X == L) << 1 | (Y == 0) << 2 | (Y == L) << 3 | (Z == 0) << 4 | (Z == L) << 5;
+               shared = (faces & rg.mask) != 0;
+            }
+            else
+            {
+               const int g = mp[a * 64];
+               d = bdof(g);
+               shared = bshared(g);
+            }
             double *dst = (!SPLIT || d < n_owned) ? y + d : yg + (d - n_owned);
-            if (!bshared(g)) { *dst = Yo[a]; }
+            if (!shared) { *dst = Yo[a]; }
             else if (part) { part[((size_t)blk * ND + a) * 64 + lane] = Yo[a]; }
             else { unsafeAtomicAdd(dst, Yo[a]); }
          }
@@ -276,14 +297,15 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 // into the element outputs (2 D^3).  At p = 2 that is 229 FP64 multiply-adds per row.  The
 // next row's pairs are in flight while a row computes; in-wave and cross-wave face assembly,
 // deterministic store.
-template <int D, int Q, bool SPLIT>
+template <int D, int Q, bool SPLIT, bool REG>
 __global__ void __launch_bounds__(256, 1)
 k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
                const double *__restrict__ qdd, const double *__restrict__ qdm,
                const double *__restrict__ x, const double *__restrict__ xg,
                double *__restrict__ y, double *__restrict__ yg, const Basis1D b,
-               const int *__restrict__ lane_flags, double *__restrict__ part)
+               const int *__restrict__ lane_flags, double *__restrict__ part, const int *__restrict__ treg)
 {
+   static_assert(!(REG && SPLIT), "regular blocks address one L-vector");
    constexpr int ND = D * D * D, NQ = Q * Q * Q, NR = Q * Q, XR = XwaveRows<D>::R, WPG = 4;
    __shared__ double sX[WPG][XR][64];  // gathered x; then the cross-wave face exchange
    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -292,18 +314,40 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
    const int e = blk * 64 + lane;
    const bool active = wave_on && e < ne;
    const int *mp = gmap + (size_t)blk * ND * 64 + lane;
+   TpeReg rg = {};
+   if (REG && wave_on)
+   {
+      const int *r = treg + (size_t)blk * 8;  // wave-uniform: scalar loads
+      rg = TpeReg{r[0], r[1], r[2], r[3], r[4]};
+   }
    double Yo[ND];
 #pragma unroll
    for (int a = 0; a < ND; a++) { Yo[a] = 0.0; }
    if (wave_on)
    {
-#pragma unroll
-      for (int a = 0; a < ND; a++)
+      if (REG)
       {
-         const int g = mp[a * 64];
-         const int d = bdof(g);
-         const double v = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
-         sX[w][a][lane] = bneg(g) ? -v : v;
+         const int d0 = rg.base + (D - 1) * ((lane & 3) * rg.sx + ((lane >> 2) & 3) * rg.sy + (lane >> 4) * rg.sz);
+#pragma unroll
+         for (int dz = 0; dz < D; dz++)
+#pragma unroll
+            for (int dy = 0; dy < D; dy++)
+#pragma unroll
+               for (int dx = 0; dx < D; dx++)
+               {
+                  sX[w][(dz * D + dy) * D + dx][lane] = x[d0 + dx * rg.sx + dy * rg.sy + dz * rg.sz];
+               }
+      }
+      else
+      {
+#pragma unroll
+         for (int a = 0; a < ND; a++)
+         {
+            const int g = mp[a * 64];
+            const int d = bdof(g);
+            const double v = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
+            sX[w][a][lane] = bneg(g) ? -v : v;
+         }
       }
       auto ld2 = [&](const double *p) -> v2d { return __builtin_nontemporal_load(reinterpret_cast<const v2d *>(p)); };
       v2d ce[3];
@@ -425,8 +469,8 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                }
       }
    }  // wave_on
-   tpe_assemble_store<D, SPLIT, true, true>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0, blk, lane,
-                                            active, n_owned, y, yg, part, &sX[0][0][0], w, wave_on);
+   tpe_assemble_store<D, SPLIT, !REG, true, REG>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0, blk,
+                                                 lane, active, n_owned, y, yg, part, &sX[0][0][0], w, wave_on, rg);
 }
 
 // Latency variant of k_apply_tpe_sf for small block ranges (the distributed Mult's boundary
@@ -712,8 +756,19 @@ void launch_tpe(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipS
          }
          else
          {
-            hipLaunchKernelGGL((k_apply_tpe_sf<D, Q, SPLIT>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end,
-                               a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part);
+            if constexpr (!SPLIT)
+            {
+               if (a.treg)
+               {
+                  hipLaunchKernelGGL((k_apply_tpe_sf<D, Q, false, true>), grid, block, 0, s, a.ne, a.blk_begin,
+                                     a.blk_end, a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b,
+                                     a.lane_flags, a.part, a.treg);
+                  return;
+               }
+            }
+            hipLaunchKernelGGL((k_apply_tpe_sf<D, Q, SPLIT, false>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end,
+                               a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part,
+                               nullptr);
          }
       }
       else { ECM2_VERIFY(false, ERR_INTERNAL, "AFFINE qdata needs both integrators"); }

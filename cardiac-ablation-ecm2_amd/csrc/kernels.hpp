@@ -111,6 +111,7 @@ struct ApplyArgs
    int ne = 0, blk_begin = 0, blk_end = 0, n_owned = 0;
    const int *pos = nullptr;        // element permutation (blocked layout), may be null
    const int *lane_flags = nullptr; // [blk][64]: in-wave face merge flags
+   const int *treg = nullptr;       // device [blk][8]: regular 4x4x4 blocks (base, sx, sy, sz, face mask), or null
    const int *gmap = nullptr;
    const double *qdd = nullptr, *qdm = nullptr;
    const double *x = nullptr, *xg = nullptr;

@@ -87,6 +87,12 @@ public:
    // latency = true): no cross-wave face assembly there.  -1: none.
    void set_latency_from(int b);
    int n_bricks() const { return n_bricks_; }
+   // the fused kernel computes dofs from 5 ints per block / brick instead of reading the map
+   bool lattice_addressing() const
+   {
+      return resolved_mode_ == KERNEL_TPE ? (treg_.size() > 0 && layout_.kind == QLAYOUT_AFFINE)
+                                          : (resolved_mode_ == KERNEL_LINE && breg_.size() > 0);
+   }
    int brick_bz() const { return brick_bz_; }
    void add_integrator(int kind, const CoeffDesc &c);
    void set_kernel(int mode);
@@ -186,6 +192,7 @@ private:
    int n_bricks_ = 0, brick_bz_ = 0, brick_np_ = 0;  // LINE bricks: count, 2 x 2 x bz, lattice points
    DeviceArray<int> belem_, bmap_;  // LINE bricks: [nbrick][4 bz] elements, [nbrick][np] lattice map
    DeviceArray<int> breg_;          // LINE bricks, lattice-numbered: [nbrick][8] (base, sx, sy, sz, face mask)
+   DeviceArray<int> treg_;          // TPE blocks, lattice-numbered: [nblk][8] (base, sx, sy, sz, face mask)
    std::vector<int> brick_off_;     // LINE bricks of block b = [brick_off_[b], brick_off_[b+1])
    long part_line_off_ = 0;         // LINE: leftover elements' partial slots start here
    int n_left_ = 0;                 // LINE: elements outside bricks

@@ -170,6 +170,11 @@ int ecm2_pa_form_set_bricks(ecm2_pa_form *f, int bz);
 int ecm2_pa_form_brick_info(const ecm2_pa_form *f, int *n_bricks, int *bz);
 /* Scatter statistics after assemble: shared dofs and their partial slots. */
 int ecm2_pa_form_scatter_info(const ecm2_pa_form *f, int *n_shared, long *n_slots);
+/* After assemble: 1 when the fused kernel addresses its elements arithmetically (a
+ * lattice-numbered mesh: every p <= 2 block or p >= 3 brick is d = base + X sx + Y sy + Z sz
+ * with face-determined sharing, checked against the gather map), 0 when it reads the map;
+ * n_runs = runs of the run-compressed summation plan.  The operator is the same either way. */
+int ecm2_pa_form_addressing_info(const ecm2_pa_form *f, int *lattice, long *n_runs);
 /* Optional element permutation for the fused kernel's blocked layout (host perm[ne]:
  * internal position i <- caller element perm[i]); see ecm2_mesh_element_order.  All
  * entry points keep the caller's element order (the reference's E-vector order,

@@ -11,6 +11,9 @@
   the oracle; the SDIRK33 step (ode.cpp:834-859) at p = 4 against the oracle's stepping.
 * configs[3] (C4): the 8-way z-slab split of a 16^3 p = 2 mesh (loopback group, both
   decompositions) against the serial oracle.
+* Lattice addressing (the fused kernels compute dofs from 5 ints per block / brick on a
+  lattice-numbered mesh) against the map-reading path on the same mesh with the entity
+  numbering, p = 1, 2 and 4, Mult and diagonal.
 * The boundary's MultTranspose (bilinearform_ext.hpp:99) and AddMult; the device Pennes
   perfusion law (parity-unpinned law, pinned projection); the distributed form's graph cache
   across re-assembly.
@@ -167,6 +170,7 @@ def test_c5_p4_cartesian_32():
     form.Assemble()
     assert form.info()["kernel"] == E.KERNEL_LINE and form.info()["layout"] == E.QLAYOUT_AFFINE_E
     assert form.BrickInfo() == (fes.ne // 4, 1)      # every element in a 2 x 2 x 1 brick
+    assert form.AddressingInfo()[0] == 1              # lattice-addressed bricks (no map reads)
     x = np.random.default_rng(32).uniform(-1, 1, fes.ndofs)
     y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
     form.Mult(dev(x), y)
@@ -398,3 +402,32 @@ def test_rccl_graph_cache_follows_reassembly(order):
     with pytest.raises(E.ECM2Error):   # a setter without Assemble: no stale replay
         pf.SetKernel(E.KERNEL_AUTO)
         pf.Mult(x, y)
+
+
+# ---------------------------------------------------------------------------------------
+# lattice addressing: structured numbering (lattice-addressed kernels) vs entity numbering
+# (map-reading kernels), same mesh and coefficients, both against the oracle
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("order,n", [(1, 16), (2, 16), (2, 12), (4, 8)])
+def test_lattice_addressing_matches_map_path(order, n):
+    m = E.Mesh.MakeCartesian3D(n, n, n)
+    en = m.element_nodes()
+    P = O.quad_points(en, order + 2)
+    a, b = alpha_bioheat(P), k_of_T(temperature(P))
+    # p = 1: the entity numbering (vertices of MakeCartesian3D) is itself a lattice numbering
+    for numbering, lattice in ((E.NUMBERING_STRUCTURED, 1), (E.NUMBERING_ENTITY, 1 if order == 1 else 0)):
+        fes = E.H1Space(m, order, numbering)
+        form = E.BilinearForm(fes)
+        form.AddDomainIntegrator(E.MassIntegrator(quad_coeff(fes, a)))
+        form.AddDomainIntegrator(E.DiffusionIntegrator(quad_coeff(fes, b)))
+        form.Assemble()
+        # n = 12 at p = 2: 1728 elements = 27 full 64-element blocks, lattice-addressed too
+        assert form.AddressingInfo()[0] == lattice, (numbering, form.AddressingInfo())
+        op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=a, beta=b)
+        x = np.random.default_rng(40 + order).uniform(-1, 1, fes.ndofs)
+        y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+        form.Mult(dev(x), y)
+        assert relerr(host(y), op.mult(x)) <= RTOL
+        d = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+        form.AssembleDiagonal(d)
+        assert relerr(host(d), op.diagonal()) <= RTOL

@@ -45,7 +45,9 @@ struct TpeReg
 {
    int base, sx, sy, sz, mask;
 };
-template <int D, bool SPLIT, bool SIGNS, bool XW, bool REG = false>
+// FS: face-grouped partial slots part[blk][tpe_surface_index(X, Y, Z)] (regular blocks: the
+// summation pass then reads a face's two holders as two contiguous runs), else [blk][a][lane].
+template <int D, bool SPLIT, bool SIGNS, bool XW, bool REG = false, bool FS = REG>
 __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], const int *__restrict__ mp, int fl,
                                                    int blk, int lane, bool active, int n_owned,
                                                    double *__restrict__ y, double *__restrict__ yg,
@@ -113,10 +115,10 @@ __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], cons
             const int a = (dz * D + dy) * D + dx;
             int d;
             bool shared;
+            constexpr int L = 4 * (D - 1);
+            const int X = (D - 1) * (lane & 3) + dx, Y = (D - 1) * ((lane >> 2) & 3) + dy, Z = (D - 1) * (lane >> 4) + dz;
             if (REG)
             {
-               constexpr int L = 4 * (D - 1);
-               const int X = (D - 1) * (lane & 3) + dx, Y = (D - 1) * ((lane >> 2) & 3) + dy, Z = (D - 1) * (lane >> 4) + dz;
                d = rg.base + X * rg.sx + Y * rg.sy + Z * rg.sz;
                const int faces = (X == 0) | (X == L) << 1 | (Y == 0) << 2 | (Y == L) << 3 | (Z == 0) << 4 | (Z == L) << 5;
                shared = (faces & rg.mask) != 0;
@@ -129,7 +131,11 @@ __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], cons
             }
             double *dst = (!SPLIT || d < n_owned) ? y + d : yg + (d - n_owned);
             if (!shared) { *dst = Yo[a]; }
-            else if (part) { part[((size_t)blk * ND + a) * 64 + lane] = Yo[a]; }
+            else if (part)
+            {
+               part[FS ? (size_t)blk * tpe_surface_points(D) + tpe_surface_index(D, X, Y, Z)
+                       : ((size_t)blk * ND + a) * 64 + lane] = Yo[a];
+            }
             else { unsafeAtomicAdd(dst, Yo[a]); }
          }
 }
@@ -642,7 +648,7 @@ k_apply_tpe_pp(int ne, int blk_begin, int n_owned, const int *__restrict__ gmap,
 // (Gy Bz)^2, (By Gz)^2, Gy By Bz^2, By^2 Gz Bz, Gy By Gz Bz.  Output assembled and stored
 // exactly like the apply kernels' (in-wave faces, cross-wave faces on AFFINE, plain stores,
 // partial slots): every diagonal entry written once, deterministic, no memset.
-template <int D, int Q, bool MASS, bool DIFF, bool SPLIT, bool AFF>
+template <int D, int Q, bool MASS, bool DIFF, bool SPLIT, bool AFF, bool FS = false>
 __global__ void __launch_bounds__(256)
 k_diag_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
            const double *__restrict__ qdd, const double *__restrict__ qdm, double *__restrict__ y,
@@ -736,7 +742,7 @@ k_diag_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restric
             }
          }
    }
-   tpe_assemble_store<D, SPLIT, false, AFF>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0, blk, lane,
+   tpe_assemble_store<D, SPLIT, false, AFF, false, FS>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0, blk, lane,
                                             active, n_owned, y, yg, part, xb, w, wave_on);
 }
 
@@ -807,6 +813,11 @@ void launch_diag_tpe(const ApplyArgs &a, const Basis1D &b, const double *drow, h
    const bool aff = a.kind == QLAYOUT_AFFINE;
    ECM2_VERIFY(!aff || (MASS && DIFF), ERR_INTERNAL, "AFFINE qdata needs both integrators");
    if (a.yg) { if (aff) { ECM2_DIAG(true, true); } else { ECM2_DIAG(true, false); } }
+   else if (aff && a.treg)  // regular blocks: face-grouped partial slots, as the apply's plan
+   {
+      hipLaunchKernelGGL((k_diag_tpe<D, Q, MASS, DIFF, false, true, true>), grid, block, 0, s, a.ne, a.blk_begin,
+                         a.blk_end, a.n_owned, a.gmap, a.qdd, a.qdm, a.y, a.yg, b, drow, a.lane_flags, a.part);
+   }
    else { if (aff) { ECM2_DIAG(false, true); } else { ECM2_DIAG(false, false); } }
 #undef ECM2_DIAG
 }

@@ -135,14 +135,12 @@ struct ApplyArgs
 // face dof -- this brick's high face and the neighbour's low face -- list it at the same
 // offset within their groups: [Z = 0 | Z = LZ-1 | Y = 0 | Y = LY-1 | X = 0 | X = LX-1],
 // edges and corners in the first group that contains them.  -1 for interior points.
-__host__ __device__ inline int brick_surface_points(int D, int bz)
+__host__ __device__ inline int lattice_surface_points(int LX, int LY, int LZ)
 {
-   const int LX = 2 * D - 1, LY = LX, LZ = bz * (D - 1) + 1;
    return 2 * LX * LY + 2 * (LZ - 2) * LX + 2 * (LZ - 2) * (LY - 2);
 }
-__host__ __device__ inline int brick_surface_index(int D, int bz, int X, int Y, int Z)
+__host__ __device__ inline int lattice_surface_index(int LX, int LY, int LZ, int X, int Y, int Z)
 {
-   const int LX = 2 * D - 1, LY = LX, LZ = bz * (D - 1) + 1;
    if (Z == 0) { return Y * LX + X; }
    if (Z == LZ - 1) { return LX * LY + Y * LX + X; }
    const int b1 = 2 * LX * LY;
@@ -152,6 +150,23 @@ __host__ __device__ inline int brick_surface_index(int D, int bz, int X, int Y, 
    if (X == 0) { return b2 + (Z - 1) * (LY - 2) + (Y - 1); }
    if (X == LX - 1) { return b2 + (LZ - 2) * (LY - 2) + (Z - 1) * (LY - 2) + (Y - 1); }
    return -1;
+}
+__host__ __device__ inline int brick_surface_points(int D, int bz)
+{
+   return lattice_surface_points(2 * D - 1, 2 * D - 1, bz * (D - 1) + 1);
+}
+__host__ __device__ inline int brick_surface_index(int D, int bz, int X, int Y, int Z)
+{
+   return lattice_surface_index(2 * D - 1, 2 * D - 1, bz * (D - 1) + 1, X, Y, Z);
+}
+// the same for a p <= 2 block (4 x 4 x 4 elements, lattice 4 (D-1) + 1 per side)
+__host__ __device__ inline int tpe_surface_points(int D)
+{
+   return lattice_surface_points(4 * D - 3, 4 * D - 3, 4 * D - 3);
+}
+__host__ __device__ inline int tpe_surface_index(int D, int X, int Y, int Z)
+{
+   return lattice_surface_index(4 * D - 3, 4 * D - 3, 4 * D - 3, X, Y, Z);
 }
 
 namespace kern

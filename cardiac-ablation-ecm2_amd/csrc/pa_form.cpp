@@ -531,22 +531,6 @@ void PAForm::assemble(hipStream_t s)
             blk[((size_t)b * ND_ + a) * 64 + l] = (int)enc;
          }
       }
-      {
-         std::vector<int> hdof, hslot;
-         for (int b = 0; b < nblk; b++)
-            for (int a = 0; a < ND_; a++)
-               for (int l = 0; l < 64; l++)
-               {
-                  if (!holds[((size_t)b * 64 + l) * ND_ + a]) { continue; }
-                  const int d = blk[((size_t)b * ND_ + a) * 64 + l] & 0x3fffffff;
-                  if (hcount[d] > 1)
-                  {
-                     hdof.push_back(d);
-                     hslot.push_back((b * ND_ + a) * 64 + l);
-                  }
-               }
-         build_shared_plan(hcount, hdof, hslot, s);
-      }
       // Regular blocks (the AFFINE kernel): every block's 64 elements a 4x4x4 lattice brick
       // (lane = ex + 4 ey + 16 ez) of a lattice-numbered mesh, d = base + X sx + Y sy + Z sz on
       // the block's (4(D-1)+1)^3 lattice, no orientation signs, and the held shared dofs
@@ -595,6 +579,40 @@ void PAForm::assemble(hipStream_t s)
             r[0] = base; r[1] = sx; r[2] = sy; r[3] = sz; r[4] = mask;
          }
          if (regular) { treg_.upload(reg, s); }
+      }
+      {
+         // partial slots: [blk][a][lane]; on regular blocks [blk][face-grouped surface index of
+         // the block lattice] (tpe_surface_index: a face's two holders list it at the same
+         // offset, so the summation pass reads both holders' runs contiguously)
+         const int ns = tpe_surface_points(D_);
+         std::vector<int> hdof, hslot;
+         for (int b = 0; b < nblk; b++)
+            for (int a = 0; a < ND_; a++)
+               for (int l = 0; l < 64; l++)
+               {
+                  if (!holds[((size_t)b * 64 + l) * ND_ + a]) { continue; }
+                  const int d = blk[((size_t)b * ND_ + a) * 64 + l] & 0x3fffffff;
+                  if (hcount[d] > 1)
+                  {
+                     hdof.push_back(d);
+                     if (treg_.size())
+                     {
+                        const int X = (D_ - 1) * (l & 3) + a % D_, Y = (D_ - 1) * ((l >> 2) & 3) + (a / D_) % D_,
+                                  Z = (D_ - 1) * (l >> 4) + a / (D_ * D_);
+                        const int si = tpe_surface_index(D_, X, Y, Z);
+                        ECM2_VERIFY(si >= 0, ERR_INTERNAL, "block " << b << ": interior lattice point shared");
+                        hslot.push_back(b * ns + si);
+                     }
+                     else { hslot.push_back((b * ND_ + a) * 64 + l); }
+                  }
+               }
+         // the plan wants each dof's holders in ascending slot order
+         std::vector<size_t> ord(hslot.size());
+         for (size_t i = 0; i < ord.size(); i++) { ord[i] = i; }
+         std::sort(ord.begin(), ord.end(), [&](size_t p, size_t q) { return hslot[p] < hslot[q]; });
+         std::vector<int> hd(ord.size()), hs(ord.size());
+         for (size_t i = 0; i < ord.size(); i++) { hd[i] = hdof[ord[i]]; hs[i] = hslot[ord[i]]; }
+         build_shared_plan(hcount, hd, hs, s);
       }
       gmap_blk_.upload(blk, s);
       lane_flags_.upload(fl, s);
@@ -783,7 +801,7 @@ void PAForm::assemble(hipStream_t s)
       // [bricks' lattice slots | leftover elements' [e][nd] slots (when there are any)]
       part_.resize(std::max<size_t>(1, (size_t)part_line_off_ + (n_left_ ? (size_t)ne_ * ND_ : 0)));
    }
-   else { part_.resize((size_t)layout_.nblk() * ND_ * 64); }
+   else { part_.resize((size_t)layout_.nblk() * (treg_.size() ? tpe_surface_points(D_) : ND_ * 64)); }
    qd_diff_.resize(have_diff_ ? layout_.diff_size() : 0);
    qd_mass_.resize(have_mass_ ? layout_.mass_size() : 0);
    // the setup kernels write every entry except the padding lanes of a partial last block

@@ -95,7 +95,7 @@ def load_library(path: str = LIB_PATH):
         "ecm2_pa_form_set_geometry_compression": (i32, [vp, i32]),
         "ecm2_pa_form_qdata_bytes": (i32, [vp, dp]),
         "ecm2_pa_form_brick_info": (i32, [vp, ip, ip]),
-        "ecm2_pa_form_addressing_info": (i32, [vp, ip, ctypes.POINTER(ctypes.c_long)]),
+        "ecm2_pa_form_addressing_info": (i32, [vp, ip, ip, ctypes.POINTER(ctypes.c_long)]),
         "ecm2_pa_form_set_element_order": (i32, [vp, vp]),
         "ecm2_mesh_element_order": (i32, [vp, i32, vp]),
         "ecm2_pa_form_assemble": (i32, [vp, vp]),
@@ -431,11 +431,12 @@ class BilinearForm:
         return n.value, m.value
 
     def AddressingInfo(self):
-        """(lattice, n_runs) after Assemble: 1 when the fused kernel computes its dofs from the
-        lattice instead of reading the gather map; runs of the summation plan."""
-        n, r = ctypes.c_int(), ctypes.c_long()
-        _check(_lib.ecm2_pa_form_addressing_info(self._h, ctypes.byref(n), ctypes.byref(r)))
-        return n.value, r.value
+        """(lattice, units, n_runs) after Assemble: of the fused kernel's units (p <= 2 blocks,
+        p >= 3 bricks), those that compute their dofs from the lattice instead of reading the
+        gather map; runs of the summation plan."""
+        n, u, r = ctypes.c_int(), ctypes.c_int(), ctypes.c_long()
+        _check(_lib.ecm2_pa_form_addressing_info(self._h, ctypes.byref(n), ctypes.byref(u), ctypes.byref(r)))
+        return n.value, u.value, r.value
 
     def BrickInfo(self):
         """(bricks, depth bz) of the p >= 3 brick kernel after Assemble (0, 0: none)."""
@@ -531,6 +532,8 @@ _PAR_SIGS = {
     "ecm2_par_form_set_kernel": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ecm2_par_form_set_scatter": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ecm2_par_form_set_bricks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "ecm2_par_form_addressing_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                                                      ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_long)]),
     "ecm2_par_form_set_geometry_compression": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ecm2_par_form_qdata_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]),
     "ecm2_par_form_layout": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
@@ -737,6 +740,12 @@ class ParBilinearForm:
         b = ctypes.c_double()
         _check(_par_lib().ecm2_par_form_qdata_bytes(self._h, ctypes.byref(b)))
         return b.value
+
+    def AddressingInfo(self):
+        """(lattice, units, n_runs) of the rank's local form (see BilinearForm.AddressingInfo)."""
+        n, u, r = ctypes.c_int(), ctypes.c_int(), ctypes.c_long()
+        _check(_par_lib().ecm2_par_form_addressing_info(self._h, ctypes.byref(n), ctypes.byref(u), ctypes.byref(r)))
+        return n.value, u.value, r.value
 
     def info(self) -> dict:
         n, k, lay = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()

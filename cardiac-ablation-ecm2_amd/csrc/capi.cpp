@@ -358,12 +358,26 @@ int ecm2_pa_form_brick_info(const ecm2_pa_form *f, int *n_bricks, int *bz)
    });
 }
 
-int ecm2_pa_form_addressing_info(const ecm2_pa_form *f, int *lattice, long *n_runs)
+static void addressing_info(const ecm2::PAForm &f, int *lattice, int *n_units, long *n_runs)
+{
+   if (lattice) { *lattice = f.lattice_units(); }
+   if (n_units) { *n_units = f.n_units(); }
+   if (n_runs) { *n_runs = f.n_summation_runs(); }
+}
+
+int ecm2_pa_form_addressing_info(const ecm2_pa_form *f, int *lattice, int *n_units, long *n_runs)
 {
    return guard([&] {
       NEED(f);
-      if (lattice) { *lattice = f->f->lattice_addressing() ? 1 : 0; }
-      if (n_runs) { *n_runs = f->f->n_summation_runs(); }
+      addressing_info(*f->f, lattice, n_units, n_runs);
+   });
+}
+
+int ecm2_par_form_addressing_info(const ecm2_par_form *f, int *lattice, int *n_units, long *n_runs)
+{
+   return guard([&] {
+      NEED(f);
+      addressing_info(f->f->local(), lattice, n_units, n_runs);
    });
 }
 

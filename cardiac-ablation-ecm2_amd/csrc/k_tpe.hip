@@ -45,17 +45,19 @@ struct TpeReg
 {
    int base, sx, sy, sz, mask;
 };
-// FS: face-grouped partial slots part[blk][tpe_surface_index(X, Y, Z)] (regular blocks: the
-// summation pass then reads a face's two holders as two contiguous runs), else [blk][a][lane].
-template <int D, bool SPLIT, bool SIGNS, bool XW, bool REG = false, bool FS = REG>
+// Partial slots: block blk owns part[blk pstride ...]: a regular block (reg) in face-grouped
+// order, [tpe_surface_index(X, Y, Z)] (the summation pass then reads a face's two holders as
+// two contiguous runs), any other block as [a][lane].  MAYREG: reg may be true (per block).
+template <int D, bool SPLIT, bool SIGNS, bool XW, bool MAYREG = false>
 __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], const int *__restrict__ mp, int fl,
                                                    int blk, int lane, bool active, int n_owned,
                                                    double *__restrict__ y, double *__restrict__ yg,
                                                    double *__restrict__ part, double *xb, int w, bool wave_on,
-                                                   TpeReg rg = {})
+                                                   TpeReg rg = {}, bool reg = false, int pstride = D * D * D * 64)
 {
    constexpr int ND = D * D * D, XR = XwaveRows<D>::R;
-   if (SIGNS && wave_on)
+   const bool rr = MAYREG && reg;
+   if (SIGNS && wave_on && !rr)
    {
 #pragma unroll
       for (int a = 0; a < ND; a++)
@@ -117,7 +119,7 @@ __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], cons
             bool shared;
             constexpr int L = 4 * (D - 1);
             const int X = (D - 1) * (lane & 3) + dx, Y = (D - 1) * ((lane >> 2) & 3) + dy, Z = (D - 1) * (lane >> 4) + dz;
-            if (REG)
+            if (rr)
             {
                d = rg.base + X * rg.sx + Y * rg.sy + Z * rg.sz;
                const int faces = (X == 0) | (X == L) << 1 | (Y == 0) << 2 | (Y == L) << 3 | (Z == 0) << 4 | (Z == L) << 5;
@@ -133,8 +135,7 @@ __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], cons
             if (!shared) { *dst = Yo[a]; }
             else if (part)
             {
-               part[FS ? (size_t)blk * tpe_surface_points(D) + tpe_surface_index(D, X, Y, Z)
-                       : ((size_t)blk * ND + a) * 64 + lane] = Yo[a];
+               part[(size_t)blk * pstride + (rr ? tpe_surface_index(D, X, Y, Z) : a * 64 + lane)] = Yo[a];
             }
             else { unsafeAtomicAdd(dst, Yo[a]); }
          }
@@ -303,15 +304,18 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 // into the element outputs (2 D^3).  At p = 2 that is 229 FP64 multiply-adds per row.  The
 // next row's pairs are in flight while a row computes; in-wave and cross-wave face assembly,
 // deterministic store.
-template <int D, int Q, bool SPLIT, bool REG>
+// RM: 0 every block map-addressed; 1 every block regular (treg rows, no flag read); 2 per block
+// (treg row flag [7], wave-uniform): a regular block's dofs are all owned (checked at setup),
+// so it addresses x / y only.
+template <int D, int Q, bool SPLIT, int RM>
 __global__ void __launch_bounds__(256, 1)
 k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
                const double *__restrict__ qdd, const double *__restrict__ qdm,
                const double *__restrict__ x, const double *__restrict__ xg,
                double *__restrict__ y, double *__restrict__ yg, const Basis1D b,
-               const int *__restrict__ lane_flags, double *__restrict__ part, const int *__restrict__ treg)
+               const int *__restrict__ lane_flags, double *__restrict__ part, const int *__restrict__ treg,
+               int pstride)
 {
-   static_assert(!(REG && SPLIT), "regular blocks address one L-vector");
    constexpr int ND = D * D * D, NQ = Q * Q * Q, NR = Q * Q, XR = XwaveRows<D>::R, WPG = 4;
    __shared__ double sX[WPG][XR][64];  // gathered x; then the cross-wave face exchange
    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -321,17 +325,19 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
    const bool active = wave_on && e < ne;
    const int *mp = gmap + (size_t)blk * ND * 64 + lane;
    TpeReg rg = {};
-   if (REG && wave_on)
+   bool reg = false;
+   if (RM && wave_on)
    {
       const int *r = treg + (size_t)blk * 8;  // wave-uniform: scalar loads
       rg = TpeReg{r[0], r[1], r[2], r[3], r[4]};
+      reg = RM == 1 || r[7] != 0;
    }
    double Yo[ND];
 #pragma unroll
    for (int a = 0; a < ND; a++) { Yo[a] = 0.0; }
    if (wave_on)
    {
-      if (REG)
+      if (reg)
       {
          const int d0 = rg.base + (D - 1) * ((lane & 3) * rg.sx + ((lane >> 2) & 3) * rg.sy + (lane >> 4) * rg.sz);
 #pragma unroll
@@ -475,8 +481,9 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                }
       }
    }  // wave_on
-   tpe_assemble_store<D, SPLIT, !REG, true, REG>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0, blk,
-                                                 lane, active, n_owned, y, yg, part, &sX[0][0][0], w, wave_on, rg);
+   tpe_assemble_store<D, SPLIT, RM != 1, true, RM != 0>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0,
+                                                         blk, lane, active, n_owned, y, yg, part, &sX[0][0][0], w,
+                                                         wave_on, rg, reg, pstride);
 }
 
 // Latency variant of k_apply_tpe_sf for small block ranges (the distributed Mult's boundary
@@ -491,7 +498,7 @@ k_apply_tpe_pp(int ne, int blk_begin, int n_owned, const int *__restrict__ gmap,
                const double *__restrict__ qdd, const double *__restrict__ qdm,
                const double *__restrict__ x, const double *__restrict__ xg,
                double *__restrict__ y, double *__restrict__ yg, const Basis1D b,
-               const int *__restrict__ lane_flags, double *__restrict__ part)
+               const int *__restrict__ lane_flags, double *__restrict__ part, int pstride)
 {
    static_assert(Q <= 4, "one plane per wave");
    constexpr int ND = D * D * D, NQ = Q * Q * Q;
@@ -636,7 +643,7 @@ k_apply_tpe_pp(int ne, int blk_begin, int n_owned, const int *__restrict__ gmap,
 #pragma unroll
       for (int a = 0; a < ND; a++) { Yo[a] += sY[k][a][lane]; }
    tpe_assemble_store<D, SPLIT, true, false>(Yo, mp, lane_flags[(size_t)blk * 64 + lane], blk, lane, active,
-                                             n_owned, y, yg, part, nullptr, 0, true);
+                                             n_owned, y, yg, part, nullptr, 0, true, TpeReg{}, false, pstride);
 }
 
 // PA diagonal, thread per element on the blocked layout (PADiffusionDiagonal3D and the
@@ -648,12 +655,12 @@ k_apply_tpe_pp(int ne, int blk_begin, int n_owned, const int *__restrict__ gmap,
 // (Gy Bz)^2, (By Gz)^2, Gy By Bz^2, By^2 Gz Bz, Gy By Gz Bz.  Output assembled and stored
 // exactly like the apply kernels' (in-wave faces, cross-wave faces on AFFINE, plain stores,
 // partial slots): every diagonal entry written once, deterministic, no memset.
-template <int D, int Q, bool MASS, bool DIFF, bool SPLIT, bool AFF, bool FS = false>
+template <int D, int Q, bool MASS, bool DIFF, bool SPLIT, bool AFF>
 __global__ void __launch_bounds__(256)
 k_diag_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
            const double *__restrict__ qdd, const double *__restrict__ qdm, double *__restrict__ y,
            double *__restrict__ yg, const Basis1D b, const double *__restrict__ drow,
-           const int *__restrict__ lane_flags, double *__restrict__ part)
+           const int *__restrict__ lane_flags, double *__restrict__ part, const int *__restrict__ treg, int pstride)
 {
    constexpr int ND = D * D * D, NQ = Q * Q * Q, NQH = (NQ + 1) / 2, DD = D * D, XR = XwaveRows<D>::R, WPG = 4;
    __shared__ double xb[AFF ? WPG * XR * 64 : 1];  // AFF: cross-wave face exchange (as the apply's plan)
@@ -742,8 +749,18 @@ k_diag_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restric
             }
          }
    }
-   tpe_assemble_store<D, SPLIT, false, AFF, false, FS>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0, blk, lane,
-                                            active, n_owned, y, yg, part, xb, w, wave_on);
+   // regular blocks (treg row flag): the apply's face-grouped partial slots
+   TpeReg rg = {};
+   bool reg = false;
+   if (treg && wave_on)
+   {
+      const int *r = treg + (size_t)blk * 8;
+      rg = TpeReg{r[0], r[1], r[2], r[3], r[4]};
+      reg = r[7] != 0;
+   }
+   tpe_assemble_store<D, SPLIT, false, AFF, true>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0, blk,
+                                                  lane, active, n_owned, y, yg, part, xb, w, wave_on, rg, reg,
+                                                  pstride);
 }
 
 template <int D, int Q, bool MASS, bool DIFF, bool SPLIT>
@@ -758,23 +775,18 @@ void launch_tpe(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipS
          if (a.latency)
          {
             hipLaunchKernelGGL((k_apply_tpe_pp<D, Q, SPLIT>), dim3(nb), dim3(256), 0, s, a.ne, a.blk_begin,
-                               a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part);
+                               a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part,
+                               a.part_stride);
          }
          else
          {
-            if constexpr (!SPLIT)
-            {
-               if (a.treg)
-               {
-                  hipLaunchKernelGGL((k_apply_tpe_sf<D, Q, false, true>), grid, block, 0, s, a.ne, a.blk_begin,
-                                     a.blk_end, a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b,
-                                     a.lane_flags, a.part, a.treg);
-                  return;
-               }
-            }
-            hipLaunchKernelGGL((k_apply_tpe_sf<D, Q, SPLIT, false>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end,
-                               a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part,
-                               nullptr);
+#define ECM2_SF(RM)                                                                                           \
+   hipLaunchKernelGGL((k_apply_tpe_sf<D, Q, SPLIT, RM>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end, a.n_owned, \
+                      a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part, a.treg, a.part_stride)
+            if (a.treg && a.treg_all) { ECM2_SF(1); }
+            else if (a.treg) { ECM2_SF(2); }
+            else { ECM2_SF(0); }
+#undef ECM2_SF
          }
       }
       else { ECM2_VERIFY(false, ERR_INTERNAL, "AFFINE qdata needs both integrators"); }
@@ -809,15 +821,11 @@ void launch_diag_tpe(const ApplyArgs &a, const Basis1D &b, const double *drow, h
    const dim3 grid((nb + 3) / 4), block(256);
 #define ECM2_DIAG(SP, AF)                                                                                \
    hipLaunchKernelGGL((k_diag_tpe<D, Q, MASS, DIFF, SP, AF>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end, \
-                      a.n_owned, a.gmap, a.qdd, a.qdm, a.y, a.yg, b, drow, a.lane_flags, a.part)
+                      a.n_owned, a.gmap, a.qdd, a.qdm, a.y, a.yg, b, drow, a.lane_flags, a.part,            \
+                      AF ? a.treg : nullptr, a.part_stride)
    const bool aff = a.kind == QLAYOUT_AFFINE;
    ECM2_VERIFY(!aff || (MASS && DIFF), ERR_INTERNAL, "AFFINE qdata needs both integrators");
    if (a.yg) { if (aff) { ECM2_DIAG(true, true); } else { ECM2_DIAG(true, false); } }
-   else if (aff && a.treg)  // regular blocks: face-grouped partial slots, as the apply's plan
-   {
-      hipLaunchKernelGGL((k_diag_tpe<D, Q, MASS, DIFF, false, true, true>), grid, block, 0, s, a.ne, a.blk_begin,
-                         a.blk_end, a.n_owned, a.gmap, a.qdd, a.qdm, a.y, a.yg, b, drow, a.lane_flags, a.part);
-   }
    else { if (aff) { ECM2_DIAG(false, true); } else { ECM2_DIAG(false, false); } }
 #undef ECM2_DIAG
 }

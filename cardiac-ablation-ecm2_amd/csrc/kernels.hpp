@@ -111,7 +111,9 @@ struct ApplyArgs
    int ne = 0, blk_begin = 0, blk_end = 0, n_owned = 0;
    const int *pos = nullptr;        // element permutation (blocked layout), may be null
    const int *lane_flags = nullptr; // [blk][64]: in-wave face merge flags
-   const int *treg = nullptr;       // device [blk][8]: regular 4x4x4 blocks (base, sx, sy, sz, face mask), or null
+   const int *treg = nullptr;       // device [blk][8]: 4x4x4 blocks (base, sx, sy, sz, face mask, -, -, regular), or null
+   int treg_all = 0;                // every block regular
+   int part_stride = 0;             // p <= 2 partial slots per block (27 * 64, or the lattice surface when treg_all)
    const int *gmap = nullptr;
    const double *qdd = nullptr, *qdm = nullptr;
    const double *x = nullptr, *xg = nullptr;

@@ -468,8 +468,12 @@ void PAForm::assemble(hipStream_t s)
       else if (resolved_mode_ == KERNEL_LINE) { layout_.kind = QLAYOUT_AFFINE_E; }
    }
 
+   // the merge plan (cross-wave faces), the regular blocks and the partial-slot layout belong
+   // to the qdata layout they were built for
+   if (gmap_blk_.size() && plan_kind_ != layout_.kind) { gmap_blk_.resize(0); }
    if (resolved_mode_ == KERNEL_TPE && !gmap_blk_.size() && ne_ > 0)
    {
+      plan_kind_ = layout_.kind;
       if (perm_host_.empty())
       {
          // no caller order: 4x4x4 face-linked bricks first (one per wave), per apply segment
@@ -531,25 +535,32 @@ void PAForm::assemble(hipStream_t s)
             blk[((size_t)b * ND_ + a) * 64 + l] = (int)enc;
          }
       }
-      // Regular blocks (the AFFINE kernel): every block's 64 elements a 4x4x4 lattice brick
-      // (lane = ex + 4 ey + 16 ez) of a lattice-numbered mesh, d = base + X sx + Y sy + Z sz on
-      // the block's (4(D-1)+1)^3 lattice, no orientation signs, and the held shared dofs
-      // exactly those on the block faces a 6-bit mask names -- the kernel then reads 5 ints per
-      // block instead of 64 ND map entries (C4: 136 MB per Mult)
+      // Regular blocks (the AFFINE kernel): the block's 64 elements a 4x4x4 lattice brick
+      // (lane = ex + 4 ey + 16 ez) of a lattice-numbered region, d = base + X sx + Y sy + Z sz on
+      // the block's (4(D-1)+1)^3 lattice, every dof owned, no orientation signs, and the held
+      // shared dofs exactly those on the block faces a 6-bit mask names.  The kernel then reads
+      // 5 ints per block instead of 64 ND map entries (C4: 136 MB per Mult and a dependent load
+      // chain at the gather and the store).  Decided per block (a partitioned rank's interior
+      // blocks are regular, its boundary blocks are not); treg_all when every block is.
       treg_.resize(0);
-      if (layout_.kind == QLAYOUT_AFFINE && n_owned_ == ndofs_ && ne_ % 64 == 0)
+      treg_all_ = false;
+      n_treg_ = 0;
+      const int ns = tpe_surface_points(D_);
+      std::vector<char> breg_ok(nblk, 0);
+      if (layout_.kind == QLAYOUT_AFFINE)
       {
          const int L = 4 * (D_ - 1);
          std::vector<int> reg((size_t)nblk * 8, 0);
-         bool regular = true;
          auto ent = [&](int b, int l, int a) { return blk[((size_t)b * ND_ + a) * 64 + l]; };
-         for (int b = 0; b < nblk && regular; b++)
+         auto faces = [&](int X, int Y, int Z) {
+            return (X == 0) | (X == L) << 1 | (Y == 0) << 2 | (Y == L) << 3 | (Z == 0) << 4 | (Z == L) << 5;
+         };
+         int nreg = 0;
+         for (int b = 0; b < nblk; b++)
          {
+            bool regular = (long)(b + 1) * 64 <= ne_;
             auto dv = [&](int l, int a) { return ent(b, l, a) & 0x3fffffff; };
             const int base = dv(0, 0), sx = dv(0, 1) - base, sy = dv(0, D_) - base, sz = dv(0, D_ * D_) - base;
-            auto faces = [&](int X, int Y, int Z) {
-               return (X == 0) | (X == L) << 1 | (Y == 0) << 2 | (Y == L) << 3 | (Z == 0) << 4 | (Z == L) << 5;
-            };
             int mask = 0;
             for (int l = 0; l < 64 && regular; l++)
                for (int a = 0; a < ND_ && regular; a++)
@@ -558,8 +569,8 @@ void PAForm::assemble(hipStream_t s)
                             Z = (D_ - 1) * (l >> 4) + a / (D_ * D_);
                   const unsigned g = (unsigned)ent(b, l, a);
                   const int d = (int)(g & 0x3fffffffu);
-                  regular = !(g >> 31) && d == base + X * sx + Y * sy + Z * sz;
-                  // a held entry on exactly one face sets or clears that face's bit
+                  regular = !(g >> 31) && d < n_owned_ && d == base + X * sx + Y * sy + Z * sz;
+                  // a held entry on exactly one face sets that face's bit
                   const int f = faces(X, Y, Z);
                   if (regular && holds[((size_t)b * 64 + l) * ND_ + a] && f && !(f & (f - 1)) && hcount[d] > 1)
                   {
@@ -572,19 +583,26 @@ void PAForm::assemble(hipStream_t s)
                   if (!holds[((size_t)b * 64 + l) * ND_ + a]) { continue; }
                   const int X = (D_ - 1) * (l & 3) + a % D_, Y = (D_ - 1) * ((l >> 2) & 3) + (a / D_) % D_,
                             Z = (D_ - 1) * (l >> 4) + a / (D_ * D_);
-                  const int d = ent(b, l, a) & 0x3fffffff;
-                  regular = (hcount[d] > 1) == ((faces(X, Y, Z) & mask) != 0);
+                  regular = (hcount[dv(l, a)] > 1) == ((faces(X, Y, Z) & mask) != 0);
                }
+            if (!regular) { continue; }
             int *r = &reg[(size_t)b * 8];
-            r[0] = base; r[1] = sx; r[2] = sy; r[3] = sz; r[4] = mask;
+            r[0] = base; r[1] = sx; r[2] = sy; r[3] = sz; r[4] = mask; r[7] = 1;
+            breg_ok[b] = 1;
+            nreg++;
          }
-         if (regular) { treg_.upload(reg, s); }
+         n_treg_ = nreg;
+         if (nreg)
+         {
+            treg_.upload(reg, s);
+            treg_all_ = nreg == nblk && (latency_from_ < 0 || latency_from_ >= nblk);
+         }
       }
+      part_stride_ = treg_all_ ? ns : ND_ * 64;
       {
          // partial slots: [blk][a][lane]; on regular blocks [blk][face-grouped surface index of
          // the block lattice] (tpe_surface_index: a face's two holders list it at the same
          // offset, so the summation pass reads both holders' runs contiguously)
-         const int ns = tpe_surface_points(D_);
          std::vector<int> hdof, hslot;
          for (int b = 0; b < nblk; b++)
             for (int a = 0; a < ND_; a++)
@@ -595,15 +613,15 @@ void PAForm::assemble(hipStream_t s)
                   if (hcount[d] > 1)
                   {
                      hdof.push_back(d);
-                     if (treg_.size())
+                     if (breg_ok[b])
                      {
                         const int X = (D_ - 1) * (l & 3) + a % D_, Y = (D_ - 1) * ((l >> 2) & 3) + (a / D_) % D_,
                                   Z = (D_ - 1) * (l >> 4) + a / (D_ * D_);
                         const int si = tpe_surface_index(D_, X, Y, Z);
                         ECM2_VERIFY(si >= 0, ERR_INTERNAL, "block " << b << ": interior lattice point shared");
-                        hslot.push_back(b * ns + si);
+                        hslot.push_back(b * part_stride_ + si);
                      }
-                     else { hslot.push_back((b * ND_ + a) * 64 + l); }
+                     else { hslot.push_back(b * part_stride_ + a * 64 + l); }
                   }
                }
          // the plan wants each dof's holders in ascending slot order
@@ -801,7 +819,7 @@ void PAForm::assemble(hipStream_t s)
       // [bricks' lattice slots | leftover elements' [e][nd] slots (when there are any)]
       part_.resize(std::max<size_t>(1, (size_t)part_line_off_ + (n_left_ ? (size_t)ne_ * ND_ : 0)));
    }
-   else { part_.resize((size_t)layout_.nblk() * (treg_.size() ? tpe_surface_points(D_) : ND_ * 64)); }
+   else { part_.resize((size_t)layout_.nblk() * part_stride_); }
    qd_diff_.resize(have_diff_ ? layout_.diff_size() : 0);
    qd_mass_.resize(have_mass_ ? layout_.mass_size() : 0);
    // the setup kernels write every entry except the padding lanes of a partial last block
@@ -1010,6 +1028,8 @@ ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, doubl
    a.pos = layout_.pos;
    a.lane_flags = lane_flags_.data();
    a.treg = treg_.size() ? treg_.data() : nullptr;
+   a.treg_all = treg_all_ ? 1 : 0;
+   a.part_stride = part_stride_;
    a.gmap = (resolved_mode_ == KERNEL_TPE) ? gmap_blk_.data()
             : (resolved_mode_ == KERNEL_LINE) ? gmap_line_.data() : gmap_.data();
    a.qdd = qd_diff_.data();

@@ -87,12 +87,14 @@ public:
    // latency = true): no cross-wave face assembly there.  -1: none.
    void set_latency_from(int b);
    int n_bricks() const { return n_bricks_; }
-   // the fused kernel computes dofs from 5 ints per block / brick instead of reading the map
-   bool lattice_addressing() const
+   // units (p <= 2 blocks, p >= 3 bricks) whose dofs the fused kernel computes from 5 ints
+   // instead of reading the map
+   int lattice_units() const
    {
-      return resolved_mode_ == KERNEL_TPE ? (treg_.size() > 0 && layout_.kind == QLAYOUT_AFFINE)
-                                          : (resolved_mode_ == KERNEL_LINE && breg_.size() > 0);
+      if (resolved_mode_ == KERNEL_TPE) { return layout_.kind == QLAYOUT_AFFINE ? n_treg_ : 0; }
+      return (resolved_mode_ == KERNEL_LINE && breg_.size()) ? n_bricks_ : 0;
    }
+   int n_units() const { return resolved_mode_ == KERNEL_TPE ? layout_.nblk() : n_bricks_; }
    int brick_bz() const { return brick_bz_; }
    void add_integrator(int kind, const CoeffDesc &c);
    void set_kernel(int mode);
@@ -192,7 +194,11 @@ private:
    int n_bricks_ = 0, brick_bz_ = 0, brick_np_ = 0;  // LINE bricks: count, 2 x 2 x bz, lattice points
    DeviceArray<int> belem_, bmap_;  // LINE bricks: [nbrick][4 bz] elements, [nbrick][np] lattice map
    DeviceArray<int> breg_;          // LINE bricks, lattice-numbered: [nbrick][8] (base, sx, sy, sz, face mask)
-   DeviceArray<int> treg_;          // TPE blocks, lattice-numbered: [nblk][8] (base, sx, sy, sz, face mask)
+   DeviceArray<int> treg_;          // TPE blocks: [nblk][8] (base, sx, sy, sz, face mask, -, -, regular)
+   bool treg_all_ = false;          // every TPE block regular: face-grouped slots only
+   int n_treg_ = 0;                 // regular TPE blocks
+   int part_stride_ = 0;            // TPE partial slots per block
+   int plan_kind_ = -1;             // qdata layout the TPE plan (merges, regular blocks, slots) was built for
    std::vector<int> brick_off_;     // LINE bricks of block b = [brick_off_[b], brick_off_[b+1])
    long part_line_off_ = 0;         // LINE: leftover elements' partial slots start here
    int n_left_ = 0;                 // LINE: elements outside bricks

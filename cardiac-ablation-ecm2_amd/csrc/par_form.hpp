@@ -35,6 +35,7 @@ public:
    ~ParPAForm();
 
    PAForm &local() { return *local_; }
+   const PAForm &local() const { return *local_; }
    const LocalPart &part() const { return part_; }
    int true_size() const { return part_.n_owned; }
 

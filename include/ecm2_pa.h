@@ -170,11 +170,12 @@ int ecm2_pa_form_set_bricks(ecm2_pa_form *f, int bz);
 int ecm2_pa_form_brick_info(const ecm2_pa_form *f, int *n_bricks, int *bz);
 /* Scatter statistics after assemble: shared dofs and their partial slots. */
 int ecm2_pa_form_scatter_info(const ecm2_pa_form *f, int *n_shared, long *n_slots);
-/* After assemble: 1 when the fused kernel addresses its elements arithmetically (a
- * lattice-numbered mesh: every p <= 2 block or p >= 3 brick is d = base + X sx + Y sy + Z sz
- * with face-determined sharing, checked against the gather map), 0 when it reads the map;
- * n_runs = runs of the run-compressed summation plan.  The operator is the same either way. */
-int ecm2_pa_form_addressing_info(const ecm2_pa_form *f, int *lattice, long *n_runs);
+/* After assemble: of the fused kernel's n_units units (p <= 2: 64-element blocks, p >= 3:
+ * bricks), the `lattice` ones address their dofs arithmetically (a lattice-numbered region:
+ * d = base + X sx + Y sy + Z sz with face-determined sharing, checked against the gather map;
+ * the others read the map); n_runs = runs of the run-compressed summation plan.  The
+ * operator is the same either way. */
+int ecm2_pa_form_addressing_info(const ecm2_pa_form *f, int *lattice, int *n_units, long *n_runs);
 /* Optional element permutation for the fused kernel's blocked layout (host perm[ne]:
  * internal position i <- caller element perm[i]); see ecm2_mesh_element_order.  All
  * entry points keep the caller's element order (the reference's E-vector order,
@@ -341,6 +342,9 @@ int ecm2_par_form_assemble(ecm2_par_form *f, void *stream);
 int ecm2_par_form_mult(ecm2_par_form *f, const double *x_true, double *y_true, void *stream);
 /* RAPOperator::MultTranspose (operator.hpp:979): P^T A^T P = P^T A P (A symmetric). */
 int ecm2_par_form_mult_transpose(ecm2_par_form *f, const double *x_true, double *y_true, void *stream);
+/* ecm2_pa_form_addressing_info for the rank's local form (its interior blocks can be
+ * lattice-addressed, those touching ghost dofs are not). */
+int ecm2_par_form_addressing_info(const ecm2_par_form *f, int *lattice, int *n_units, long *n_runs);
 /* All subdomains of one partition in this process on one GPU (exchange by device copies that
  * follow the members' exchange schedules). */
 int ecm2_par_group_mult(ecm2_par_form *const *forms, int n, const double *const *x_true,

@@ -170,7 +170,8 @@ def test_c5_p4_cartesian_32():
     form.Assemble()
     assert form.info()["kernel"] == E.KERNEL_LINE and form.info()["layout"] == E.QLAYOUT_AFFINE_E
     assert form.BrickInfo() == (fes.ne // 4, 1)      # every element in a 2 x 2 x 1 brick
-    assert form.AddressingInfo()[0] == 1              # lattice-addressed bricks (no map reads)
+    lat, units, _ = form.AddressingInfo()
+    assert lat == units == fes.ne // 4                 # every brick lattice-addressed (no map reads)
     x = np.random.default_rng(32).uniform(-1, 1, fes.ndofs)
     y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
     form.Mult(dev(x), y)
@@ -422,7 +423,8 @@ def test_lattice_addressing_matches_map_path(order, n):
         form.AddDomainIntegrator(E.DiffusionIntegrator(quad_coeff(fes, b)))
         form.Assemble()
         # n = 12 at p = 2: 1728 elements = 27 full 64-element blocks, lattice-addressed too
-        assert form.AddressingInfo()[0] == lattice, (numbering, form.AddressingInfo())
+        lat, units, _ = form.AddressingInfo()
+        assert (lat == units > 0) if lattice else lat == 0, (numbering, form.AddressingInfo())
         op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=a, beta=b)
         x = np.random.default_rng(40 + order).uniform(-1, 1, fes.ndofs)
         y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")

@@ -185,8 +185,9 @@ def roofline(workload, world, layout, kms, alg_bytes, mbytes, stream):
         "algorithmic_bytes_per_launch": alg_bytes,
         "alg_ratio": round(alg_bytes / (kms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
         "min_bytes_per_launch": mbytes,
-        "stream_copy_gbs": stream,
-        "frac_of_stream": round(achieved / stream, 4) if stream else None,
+        "stream_copy_gbs": stream[0] if stream else None,
+        "stream_read_gbs": stream[1] if stream else None,
+        "frac_of_stream": round(achieved / max(stream), 4) if stream else None,
     }
 
 
@@ -464,9 +465,9 @@ def c3_pcg(E, torch, fes, form, max_iter=200):
 
 
 def stream_copy_peak(E, torch, nbytes=1 << 30, reps=20):
-    """Measured HBM STREAM-copy rate on this GPU (read + write bytes / time) with the
-    library's 16-byte nontemporal copy kernel, reported beside the 8 TB/s spec peak
-    (SURVEY §8(d) 'Bounding roofline')."""
+    """Measured HBM stream rates on this GPU with the library's 16-byte nontemporal kernels:
+    (copy: read + write bytes / time, read-only: bytes / time), reported beside the 8 TB/s
+    spec peak (SURVEY §8(d) 'Bounding roofline'); frac_of_stream uses the larger."""
     a = torch.empty(nbytes // 8, dtype=torch.float64, device="cuda").uniform_()
     b = torch.empty_like(a)
     for _ in range(3):
@@ -478,8 +479,19 @@ def stream_copy_peak(E, torch, nbytes=1 << 30, reps=20):
     e1.record()
     torch.cuda.synchronize()
     rate = 2.0 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
-    del a, b
-    return round(rate, 1)
+    del b
+    # read-only stream of the same buffer (the PA kernels move ~93% reads)
+    out = torch.empty(256 * 64 * 256, dtype=torch.float64, device="cuda")
+    for _ in range(3):
+        E.stream_read(a, out)
+    e0.record()
+    for _ in range(reps):
+        E.stream_read(a, out)
+    e1.record()
+    torch.cuda.synchronize()
+    rrate = nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, out
+    return round(rate, 1), round(rrate, 1)
 
 
 def cpu_model():

@@ -88,6 +88,7 @@ def load_library(path: str = LIB_PATH):
         "ecm2_pa_form_set_jacobians": (i32, [vp, vp]),
         "ecm2_pa_form_add_integrator": (i32, [vp, i32, i32, vp, vp]),
         "ecm2_stream_copy": (i32, [vp, vp, ctypes.c_long, vp]),
+        "ecm2_stream_read": (i32, [vp, ctypes.c_long, vp, ctypes.c_long, vp]),
         "ecm2_pa_form_set_kernel": (i32, [vp, i32]),
         "ecm2_pa_form_set_scatter": (i32, [vp, i32]),
         "ecm2_pa_form_scatter_info": (i32, [vp, vp, vp]),
@@ -147,6 +148,11 @@ def _stream(stream=None) -> ctypes.c_void_p:
     import torch
     s = stream if stream is not None else torch.cuda.current_stream()
     return ctypes.c_void_p(s.cuda_stream)
+
+
+def stream_read(a, out, stream=None):
+    """Read-only HBM stream over a (out: >= 4,194,304 doubles of per-thread sums)."""
+    _check(load_library().ecm2_stream_read(_dev_ptr(a), a.numel(), _dev_ptr(out), out.numel(), _stream(stream)))
 
 
 def stream_copy(a, b, stream=None):

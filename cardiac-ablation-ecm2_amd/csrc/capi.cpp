@@ -102,6 +102,11 @@ extern "C" {
 const char *ecm2_last_error(void) { return g_last_error.c_str(); }
 int ecm2_version(void) { return 100; }
 
+int ecm2_stream_read(const double *a, long n, double *out, long nout, void *stream)
+{
+   return guard([&] { ecm2::kern::stream_read(n, a, out, nout, S(stream)); });
+}
+
 int ecm2_stream_copy(const double *a, double *b, long n, void *stream)
 {
    return guard([&] { ecm2::kern::stream_copy(n, a, b, S(stream)); });

@@ -259,6 +259,8 @@ void scale(int n, double a, double *y, hipStream_t s);                          
 void add_scaled(int n, const double *x, double c, const double *k, double *out, hipStream_t s); // out = x + c k
 // b = a with 16-byte nontemporal accesses (HBM STREAM-copy measurement)
 void stream_copy(long n, const double *a, double *b, hipStream_t s);
+// read-only stream: out[t] = sum of thread t's 16-byte loads (nout >= the launch's threads)
+void stream_read(long n, const double *a, double *out, long nout, hipStream_t s);
 // Halo pack/unpack for the distributed operator (K7): buf[i] = x[idx[i]] ; y[idx[i]] += buf[i]
 void gather_idx(int n, const int *idx, const double *x, double *buf, hipStream_t s);
 void scatter_add_idx(int n, const int *idx, const double *buf, double *y, hipStream_t s);

@@ -65,6 +65,9 @@ int ecm2_device_count(void);
  * nontemporal loads/stores -- the HBM STREAM-copy rate bench.py reports beside the
  * spec peak.  n even, a and b 16-byte aligned device arrays. */
 int ecm2_stream_copy(const double *a, double *b, long n, void *stream);
+/* Read-only HBM stream over a[0..n) (16-byte nontemporal loads, a per-thread sum written to
+ * out[0..nout)): the read bandwidth the read-dominated PA kernels are measured against. */
+int ecm2_stream_read(const double *a, long n, double *out, long nout, void *stream);
 
 /* ------------------------------------------------------------------------ */
 /* Setup side: meshes and H1 spaces (the caller's Mesh / FiniteElementSpace)  */

@@ -402,12 +402,8 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                ZB[dy][dx] = zb; ZG[dy][dx] = zg;
                SB[dy][dx] = 0.0; SG[dy][dx] = 0.0;
             }
-#pragma unroll 1
-         for (int qy = 0; qy < Q; qy++)
-         {
-            const int row = qz * Q + qy;
-            if (row + 1 < NR) { load_row(row + 1, na); }
-            // one row (qz, qy) of Q points: y-forward, x-forward, weighting, x-transpose, y-transpose
+         // one row (qz, qy) of Q points: y-forward, x-forward, weighting, x-transpose, y-transpose
+         auto row_body = [&](const int qy, const v2d (&cur)[Q]) {
             double Y00[D], Y01[D], Y10[D];
 #pragma unroll
             for (int dx = 0; dx < D; dx++)
@@ -439,7 +435,7 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                   uy += bq * Y01[dx];
                   uz += bq * Y10[dx];
                }
-               const v2d sa = ca[qx];
+               const v2d sa = cur[qx];
                const double m = sa.y * u;
                const double fx = sa.x * (ce[0].x * ux + ce[0].y * uy + ce[1].x * uz);
                const double fy = sa.x * (ce[0].y * ux + ce[1].y * uy + ce[2].x * uz);
@@ -466,8 +462,34 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                   SG[dy][dx] += by * T2[dx];
                }
             }
+         };
+         if constexpr (Q % 2 == 0)
+         {
+            // two row buffers in ping-pong, no register moves and no conditional loads: the
+            // next row's loads are always the 4 youngest in flight, so a row's data waits on
+            // vmcnt(4), never on the row after it (a conditional prefetch plus a buffer copy
+            // made the compiler wait for the prefetch itself: one exposed latency per row)
 #pragma unroll
-            for (int qx = 0; qx < Q; qx++) { ca[qx] = na[qx]; }
+            for (int qy = 0; qy < Q; qy += 2)
+            {
+               const int row = qz * Q + qy;
+               load_row(row + 1, na);
+               row_body(qy, ca);
+               load_row(row + 2 < NR ? row + 2 : NR - 1, ca);  // the next plane's first row (last: a reload)
+               row_body(qy + 1, na);
+            }
+         }
+         else
+         {
+#pragma unroll 1
+            for (int qy = 0; qy < Q; qy++)
+            {
+               const int row = qz * Q + qy;
+               if (row + 1 < NR) { load_row(row + 1, na); }
+               row_body(qy, ca);
+#pragma unroll
+               for (int qx = 0; qx < Q; qx++) { ca[qx] = na[qx]; }
+            }
          }
 #pragma unroll
          for (int dz = 0; dz < D; dz++)

@@ -197,7 +197,11 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
       }
    };
    load_row(0, cd, cm);
-   auto row_body = [&](const int row, const v2d (&curd)[Q][3], const double (&curm)[Q]) {
+
+#pragma unroll 1
+   for (int row = 0; row < NR; row++)
+   {
+      if (row + 1 < NR) { load_row(row + 1, nd_, nm); }
       const double *P = rowtab + (size_t)row * 3 * DD;
       double Y00[D], Y01[D], Y10[D];
 #pragma unroll
@@ -239,11 +243,11 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
             }
          }
          double m = 0.0, fx = 0.0, fy = 0.0, fz = 0.0;
-         if (MASS) { m = curm[qx] * u; }
+         if (MASS) { m = cm[qx] * u; }
          if (DIFF)
          {
             // (11,12) (13,22) (23,33)
-            const v2d d0 = curd[qx][0], d1 = curd[qx][1], d2 = curd[qx][2];
+            const v2d d0 = cd[qx][0], d1 = cd[qx][1], d2 = cd[qx][2];
             fx = d0.x * ux + d0.y * uy + d1.x * uz;
             fy = d0.y * ux + d1.y * uy + d2.x * uz;
             fz = d1.x * ux + d2.x * uy + d2.y * uz;
@@ -279,34 +283,12 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                Yo[(dz * D + dy) * D + dx] = yo;
             }
          }
-   };
-   if constexpr (NR % 2 == 0)
-   {
-      // two row buffers in ping-pong, unconditional loads (see k_apply_tpe_sf): a row waits
-      // only for its own qdata, never for the row it has just prefetched
-#pragma unroll 1
-      for (int row = 0; row < NR; row += 2)
-      {
-         load_row(row + 1, nd_, nm);
-         row_body(row, cd, cm);
-         load_row(row + 2 < NR ? row + 2 : NR - 1, cd, cm);
-         row_body(row + 1, nd_, nm);
-      }
-   }
-   else
-   {
-#pragma unroll 1
-      for (int row = 0; row < NR; row++)
-      {
-         if (row + 1 < NR) { load_row(row + 1, nd_, nm); }
-         row_body(row, cd, cm);
 #pragma unroll
-         for (int qx = 0; qx < Q; qx++)
-         {
+      for (int qx = 0; qx < Q; qx++)
+      {
 #pragma unroll
-            for (int k = 0; k < 3; k++) { cd[qx][k] = nd_[qx][k]; }
-            cm[qx] = nm[qx];
-         }
+         for (int k = 0; k < 3; k++) { cd[qx][k] = nd_[qx][k]; }
+         cm[qx] = nm[qx];
       }
    }
    tpe_assemble_store<D, SPLIT, true, false>(Yo, mp, lane_flags[(size_t)blk * 64 + lane], blk, lane, active,

@@ -272,6 +272,54 @@ def test_c4_eight_way_slabs(decomp, scatter):
     assert relerr(y, ref) <= RTOL
 
 
+@pytest.mark.parametrize("decomp", ["rap", "overlap"])
+def test_slabs_mixed_lattice_addressing(decomp):
+    """2-way z-slabs thick enough for complete 4x4x4 blocks: each rank's interior blocks are
+    lattice-addressed and its ghost-touching blocks read the map (per-block mode, per-block
+    partial-slot layout), the partitioned Mult still matching the serial oracle."""
+    nx, nz, nranks, order = 16, 24, 2, 2
+    m = E.Mesh.MakeCartesian3D(nx, nx, nz, 1.0, 1.0, nz / nx)
+    fes = E.H1Space(m, order, E.NUMBERING_STRUCTURED)
+    er = E.partition_slabs_z(m, nranks)
+    q1d = O.default_q1d(order)
+    xg = np.random.default_rng(9).uniform(-1, 1, fes.ndofs)
+    forms, parts, xs, ys, info = [], [], [], [], []
+    for r in range(nranks):
+        part = E.Partition(fes, er, r, nranks, decomposition=decomp)
+        pf = E.ParBilinearForm(part)
+        P = E.quadrature_points_subset(m, q1d, part.elems)
+        pf.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(alpha_bioheat(P).reshape(part.ne_local, -1)))))
+        pf.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(
+            dev(k_of_T(temperature(P)).reshape(part.ne_local, -1)))))
+        pf.Assemble()
+        info.append(pf.AddressingInfo()[:2])
+        forms.append(pf)
+        parts.append(part)
+        xs.append(dev(xg[part.owned_global]))
+        ys.append(torch.full((part.n_owned,), float("nan"), dtype=torch.float64, device="cuda"))
+    # every rank lattice-addresses blocks; a rank with ghost dofs also reads the map for some
+    # (the lowest rank owns the interface plane: with RAP all its blocks can be regular)
+    assert all(lat > 0 for lat, _ in info) and any(lat < units for lat, units in info), info
+    group = E.ParGroup(forms)
+    group.Mult(xs, ys)
+    y = np.full(fes.ndofs, np.nan)
+    for part, yt in zip(parts, ys):
+        y[part.owned_global] = host(yt)
+    Pg = O.quad_points(m.element_nodes(), q1d)
+    ref = O.OracleOperator(m.element_nodes(), fes.gather_map(), fes.ndofs, order, alpha=alpha_bioheat(Pg),
+                           beta=k_of_T(temperature(Pg))).mult(xg)
+    assert relerr(y, ref) <= RTOL
+    # the diagonal kernel writes the same per-block slot layouts
+    dg = [torch.full((p.n_owned,), float("nan"), dtype=torch.float64, device="cuda") for p in parts]
+    group.AssembleDiagonal(dg)
+    d = np.full(fes.ndofs, np.nan)
+    for part, dt in zip(parts, dg):
+        d[part.owned_global] = host(dt)
+    dref = O.OracleOperator(m.element_nodes(), fes.gather_map(), fes.ndofs, order, alpha=alpha_bioheat(Pg),
+                            beta=k_of_T(temperature(Pg))).diagonal()
+    assert relerr(d, dref) <= RTOL
+
+
 # ---------------------------------------------------------------------------------------
 # boundary: MultTranspose / AddMult (bilinearform_ext.hpp:99, operator.hpp:87-92)
 # ---------------------------------------------------------------------------------------

@@ -367,22 +367,15 @@ __global__ void __launch_bounds__(256) k_stream_copy(long n2, const v2d *__restr
    for (; i < n2; i += stride) { __builtin_nontemporal_store(__builtin_nontemporal_load(a + i), b + i); }
 }
 
+// Read-only stream: one 16-byte nontemporal load per thread per step, 8 workgroups of 256
+// per CU (profiles/calib/read_probe.hip: the fastest of the probed depths and grids, ~7 TB/s;
+// deeper per-thread unrolling reads slower).
 __global__ void __launch_bounds__(256) k_stream_read(long n2, const v2d *__restrict__ a, double *__restrict__ out)
 {
-   constexpr int U = 4;
    const long stride = (long)gridDim.x * blockDim.x;
    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
    v2d acc = {0.0, 0.0};
-   long i = t;
-   for (; i + (U - 1) * stride < n2; i += U * stride)
-   {
-      v2d v[U];
-#pragma unroll
-      for (int u = 0; u < U; u++) { v[u] = __builtin_nontemporal_load(a + i + u * stride); }
-#pragma unroll
-      for (int u = 0; u < U; u++) { acc += v[u]; }
-   }
-   for (; i < n2; i += stride) { acc += __builtin_nontemporal_load(a + i); }
+   for (long i = t; i < n2; i += stride) { acc += __builtin_nontemporal_load(a + i); }
    out[t] = acc.x + acc.y;
 }
 
@@ -610,9 +603,16 @@ void stream_copy(long n, const double *a, double *b, hipStream_t s)
 
 void stream_read(long n, const double *a, double *out, long nout, hipStream_t s)
 {
-   const long threads = 256L * 64 * 256;
+   static int cus = 0;
+   if (!cus)
+   {
+      int dev = 0;
+      ECM2_HIP(hipGetDevice(&dev));
+      ECM2_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+   }
+   const long blocks = 8L * cus, threads = blocks * 256;
    ECM2_VERIFY(nout >= threads, ERR_ARG, "stream_read needs " << threads << " outputs");
-   hipLaunchKernelGGL(k_stream_read, dim3(256 * 64), dim3(256), 0, s, n / 2, reinterpret_cast<const v2d *>(a), out);
+   hipLaunchKernelGGL(k_stream_read, dim3(blocks), dim3(256), 0, s, n / 2, reinterpret_cast<const v2d *>(a), out);
    ECM2_HIP(hipGetLastError());
 }
 

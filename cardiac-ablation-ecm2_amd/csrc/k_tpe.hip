@@ -374,11 +374,13 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 #pragma unroll
          for (int qx = 0; qx < Q; qx++) { aq[qx] = ld2(qa + (size_t)(row * Q + qx) * 128); }
       };
-      load_row(0, ca);
-
-#pragma unroll 1
-      for (int qz = 0; qz < Q; qz++)
-      {
+      // PF2: three row buffers in rotation, each row issues the row two ahead, so 8 KiB per wave
+      // are in flight instead of 4 (profiles/r2_ab_pf2.txt: C4 kernel -4.3%); the plane loop is
+      // unrolled so the rotation is static.  Map-addressed kernels (RM = 0) keep the ping-pong:
+      // unrolled, their register demand exceeds 256 VGPRs; at p = 1 the third buffer costs a wave/SIMD.
+      constexpr bool PF2 = RM != 0 && D == 3;
+      v2d ra[PF2 ? 3 : 1][Q];
+      auto plane = [&](const int qz) {
          double bz[D], gz[D];
 #pragma unroll
          for (int dz = 0; dz < D; dz++) { bz[dz] = b.B[qz + MQ * dz]; gz[dz] = b.G[qz + MQ * dz]; }
@@ -463,7 +465,19 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                }
             }
          };
-         if constexpr (Q % 2 == 0)
+         if constexpr (PF2)
+         {
+            // the last rows reload the final row (unconditional loads keep the wait counts exact)
+#pragma unroll
+            for (int qy = 0; qy < Q; qy++)
+            {
+               const int row = qz * Q + qy;
+               __builtin_amdgcn_sched_barrier(0);  // rows stay in program order (no interleaving)
+               load_row(row + 2 < NR ? row + 2 : NR - 1, ra[(row + 2) % 3]);
+               row_body(qy, ra[row % 3]);
+            }
+         }
+         else if constexpr (Q % 2 == 0)
          {
             // two row buffers in ping-pong, no register moves and no conditional loads: the
             // next row's loads are always the 4 youngest in flight, so a row's data waits on
@@ -501,6 +515,19 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                   Yo[(dz * D + dy) * D + dx] += bz[dz] * SB[dy][dx];
                   Yo[(dz * D + dy) * D + dx] += gz[dz] * SG[dy][dx];
                }
+      };
+      if constexpr (PF2)
+      {
+         load_row(0, ra[0]);
+         load_row(1, ra[1]);
+#pragma unroll
+         for (int qz = 0; qz < Q; qz++) { plane(qz); }
+      }
+      else
+      {
+         load_row(0, ca);
+#pragma unroll 1
+         for (int qz = 0; qz < Q; qz++) { plane(qz); }
       }
    }  // wave_on
    tpe_assemble_store<D, SPLIT, RM != 1, true, RM != 0>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0,

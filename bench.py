@@ -222,6 +222,8 @@ def main():
                     help="1 (N = 1): also time the full per-point qdata layout in this run (full_layout sub-object)")
     ap.add_argument("--loopback", type=int, default=1,
                     help="N>1 on one GPU: N subdomains in this process (validation of the partitioned path)")
+    ap.add_argument("--partition", choices=["slabs", "boxes"], default="slabs",
+                    help="N > 1: z-slabs (CartesianPartitioning along z) or px x py x pz boxes (2x2x2 at N = 8)")
     ap.add_argument("--deadline", type=float, default=900.0,
                     help="seconds after which a rank prints its last stage and exits non-zero (0: none)")
     args = ap.parse_args()
@@ -308,7 +310,13 @@ def main():
         ne_own = fes.ne
     else:
         # z-slab partition (CartesianPartitioning along z, mesh.cpp:8966)
-        er = E.partition_slabs_z(mesh, nsub)
+        if args.partition == "boxes":
+            f = {1: (1, 1, 1), 2: (1, 1, 2), 4: (1, 2, 2), 8: (2, 2, 2), 16: (2, 2, 4)}.get(nsub)
+            if f is None:
+                raise SystemExit(f"--partition boxes: no box factorisation for {nsub} parts")
+            er = E.partition_boxes(mesh, f)
+        else:
+            er = E.partition_slabs_z(mesh, nsub)
         if world > 1:
             rid = [E.rccl_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(rid, src=0)
@@ -422,9 +430,9 @@ def main():
                 "kernel": ["auto", "tpe", "wpe", "unfused", "line"][timed_forms[0].info()["kernel"]],
                 "qdata_layout": layout,
                 "qdata_bytes_stored": qbytes_total / world,
-                "parallelism": (f"domain decomposition, z-slabs x{world} ({decomp}), RCCL shared-DoF exchange"
+                "parallelism": (f"domain decomposition, {'z-slabs' if args.partition == 'slabs' else 'boxes'} x{world} ({decomp}), RCCL shared-DoF exchange"
                                 if world > 1 else
-                                (f"loopback z-slabs x{args.loopback} on one GPU" if args.loopback > 1 else "single GPU")),
+                                (f"loopback {'z-slabs' if args.partition == 'slabs' else 'boxes'} x{args.loopback} on one GPU" if args.loopback > 1 else "single GPU")),
             },
             "roofline": roofline(args.workload, world, layout, kavg_ms, bytes_total / world, mbytes_total / world,
                                  stream),

@@ -600,6 +600,23 @@ def partition_slabs_z(mesh: Mesh, nranks: int) -> np.ndarray:
     return out
 
 
+def partition_boxes(mesh: Mesh, parts) -> np.ndarray:
+    """Mesh::CartesianPartitioning(nxyz) (mesh.cpp:8966) for a box-shaped mesh: element ->
+    rank = i_x + px (i_y + py i_z), i_d = floor(centroid_d / extent_d * p_d), parts = (px, py, pz)."""
+    px, py, pz = (int(v) for v in parts)
+    c = mesh.element_nodes().mean(axis=2)  # [e][3]
+    lo, hi = c.min(axis=0), c.max(axis=0)
+    span = np.where(hi > lo, hi - lo, 1.0)
+    n = np.array([px, py, pz])
+    # centroids of an n-element row sit at (i + 1/2) h: map them to [0, n) exactly
+    idx = []
+    for d in range(3):
+        m = np.unique(np.round(c[:, d], 12)).size  # elements along d
+        i = np.floor((c[:, d] - lo[d]) / span[d] * (m - 1) + 0.5).astype(np.int64)  # element index along d
+        idx.append(np.minimum(i * n[d] // m, n[d] - 1))
+    return np.ascontiguousarray(idx[0] + px * (idx[1] + py * idx[2]), np.int32)
+
+
 def quadrature_points_subset(mesh: Mesh, q1d: int, elems: np.ndarray) -> np.ndarray:
     elems = np.ascontiguousarray(elems, np.int32)
     out = np.empty((elems.size, q1d ** 3, 3), np.float64)

@@ -305,3 +305,17 @@ def test_exchange_schedule_pairs(kind, nranks, decomp):
             if kind == "slabs" and not transpose:
                 # z-slabs: every P send is one contiguous owned range, sent straight from x
                 assert all(int(row[2]) == E.Partition.XBUF_X_TRUE for row in sch[r] if row[1])
+
+
+def test_partition_boxes():
+    """CartesianPartitioning into px x py x pz boxes (mesh.cpp:8966): every box holds its share,
+    each box is one contiguous block of the element lattice, and (1, 1, n) is the z-slab split."""
+    m = E.Mesh.MakeCartesian3D(12, 10, 8, 1.0, 10 / 12, 8 / 12)
+    r = E.partition_boxes(m, (2, 2, 2))
+    assert np.bincount(r).tolist() == [120] * 8
+    c = m.element_nodes().mean(axis=2)
+    for k in range(8):
+        lo, hi = c[r == k].min(axis=0), c[r == k].max(axis=0)
+        inside = np.all((c >= lo - 1e-12) & (c <= hi + 1e-12), axis=1)
+        assert np.array_equal(inside, r == k)
+    assert np.array_equal(E.partition_boxes(m, (1, 1, 4)), E.partition_slabs_z(m, 4))

@@ -273,6 +273,43 @@ def test_c4_eight_way_slabs(decomp, scatter):
 
 
 @pytest.mark.parametrize("decomp", ["rap", "overlap"])
+def test_c4_eight_way_boxes(decomp):
+    """The 2 x 2 x 2 box split of configs[3] (bench.py --partition boxes; SURVEY §8(d) names
+    both): up to 7 neighbours per rank (faces, edges, the corner) in the exchange schedule, the
+    gathered Mult against the serial oracle."""
+    n, nranks, order = 16, 8, 2
+    m = E.Mesh.MakeCartesian3D(n, n, n)
+    fes = E.H1Space(m, order, E.NUMBERING_STRUCTURED)
+    er = E.partition_boxes(m, (2, 2, 2))
+    q1d = O.default_q1d(order)
+    xg = np.random.default_rng(11).uniform(-1, 1, fes.ndofs)
+    forms, parts, xs, ys = [], [], [], []
+    for r in range(nranks):
+        part = E.Partition(fes, er, r, nranks, decomposition=decomp)
+        pf = E.ParBilinearForm(part)
+        P = E.quadrature_points_subset(m, q1d, part.elems)
+        pf.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(alpha_bioheat(P).reshape(part.ne_local, -1)))))
+        pf.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(
+            dev(k_of_T(temperature(P)).reshape(part.ne_local, -1)))))
+        pf.Assemble()
+        forms.append(pf)
+        parts.append(part)
+        xs.append(dev(xg[part.owned_global]))
+        ys.append(torch.full((part.n_owned,), float("nan"), dtype=torch.float64, device="cuda"))
+    assert max(p.n_nbrs for p in parts) == 7
+    group = E.ParGroup(forms)
+    for _ in range(2):
+        group.Mult(xs, ys)
+    y = np.full(fes.ndofs, np.nan)
+    for part, yt in zip(parts, ys):
+        y[part.owned_global] = host(yt)
+    Pg = O.quad_points(m.element_nodes(), q1d)
+    ref = O.OracleOperator(m.element_nodes(), fes.gather_map(), fes.ndofs, order, alpha=alpha_bioheat(Pg),
+                           beta=k_of_T(temperature(Pg))).mult(xg)
+    assert relerr(y, ref) <= RTOL
+
+
+@pytest.mark.parametrize("decomp", ["rap", "overlap"])
 def test_slabs_mixed_lattice_addressing(decomp):
     """2-way z-slabs thick enough for complete 4x4x4 blocks: each rank's interior blocks are
     lattice-addressed and its ghost-touching blocks read the map (per-block mode, per-block

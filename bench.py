@@ -165,6 +165,56 @@ def kernel_ms(forms, apply, x, y, steps, torch, settle_s=0.06, world=1, dist=Non
     return kms / steps
 
 
+def member_bench(args, torch, group, xs, ys, ndofs, workload, dl):
+    """--loopback N --member R: member R's rows of the partitioned operator alone, captured in
+    one HIP graph and replayed -- the stages, streams and kernels one RCCL rank runs on its own
+    GPU (interior elements beside the exchange + boundary elements, then the shared-dof sums),
+    with the exchange as device-local copies instead of xGMI transfers.  The slowest member's
+    time gives the emulated N-GPU rate (ndofs / that time); every member's time is printed."""
+    n = len(group.forms)
+    members = list(range(n)) if args.member < 0 else [args.member]
+    per = []
+    for r in members:
+        dl.at(f"member {r}")
+        for _ in range(3):
+            group.MultMember(r, xs, ys)
+        torch.cuda.synchronize()
+        use_graph = args.member_graph if args.member_graph >= 0 else (
+            args.par_graph if args.par_graph >= 0 else int(args.schedule == "overlap"))
+        if use_graph:
+            g = torch.cuda.CUDAGraph()
+            cs = torch.cuda.Stream()
+            with torch.cuda.graph(g, stream=cs):
+                group.MultMember(r, xs, ys)
+            run = g.replay
+        else:
+            g = None
+            run = lambda: group.MultMember(r, xs, ys)
+        t0 = time.perf_counter()
+        k = 0
+        while time.perf_counter() - t0 < 0.06:  # settle the clock (kernel_ms)
+            run()
+            k += 1
+            if k % 64 == 0:
+                torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        for _ in range(args.steps):
+            run()
+        ev1.record()
+        torch.cuda.synchronize()
+        per.append(ev0.elapsed_time(ev1) / args.steps)
+        del g, run
+    worst = max(per)
+    print(json.dumps({"emulated_n_gpus": n, "workload": workload, "ndofs": ndofs,
+                      "member_ms": [round(v, 5) for v in per], "members": members,
+                      "slowest_member_ms": round(worst, 5),
+                      "emulated_value": round(ndofs / (worst * 1e-3) / 1e6, 2), "unit": "MDoF/s",
+                      "note": "one member's Mult alone on one GPU (graph replay), exchange by device copies: "
+                              "a rank's Mult short of the xGMI transfer time"}), flush=True)
+
+
 def pmc_pin(workload, world, layout):
     """Pinned PMC traffic of this workload's dominant kernel in this layout (profiles/pmc_pin.py)."""
     path = os.path.join(ROOT, "profiles", f"pmc_{workload}_n{world}_{layout}.json")
@@ -224,6 +274,16 @@ def main():
                     help="N>1 on one GPU: N subdomains in this process (validation of the partitioned path)")
     ap.add_argument("--partition", choices=["slabs", "boxes"], default="slabs",
                     help="N > 1: z-slabs (CartesianPartitioning along z) or px x py x pz boxes (2x2x2 at N = 8)")
+    ap.add_argument("--member", type=int, default=None,
+                    help="with --loopback N (z-slabs, OVERLAP): time member R's rows alone, as one rank runs "
+                         "them on its own GPU (HIP graph); -1 = every member, the slowest sets the emulated rate")
+    ap.add_argument("--schedule", choices=["serial", "overlap"], default="serial",
+                    help="distributed Mult schedule (ecm2_par_form_set_schedule)")
+    ap.add_argument("--par-graph", type=int, default=-1, choices=[-1, 0, 1],
+                    help="distributed Mult: 1 HIP graph per Mult, 0 direct launches, -1 the schedule's default")
+    ap.add_argument("--member-graph", type=int, default=-1, choices=[-1, 0, 1],
+                    help="--member: 1 replay one HIP graph per Mult, 0 launch the stages directly, "
+                         "-1 as the RCCL form would (--par-graph, else the schedule's default)")
     ap.add_argument("--deadline", type=float, default=900.0,
                     help="seconds after which a rank prints its last stage and exits non-zero (0: none)")
     args = ap.parse_args()
@@ -322,7 +382,7 @@ def main():
             dist.broadcast_object_list(rid, src=0)
             part = E.Partition(fes, er, rank, world, decomposition=decomp)
             pform = E.ParBilinearForm(part, rccl_id=rid[0], kernel=kernel, scatter=scatter,
-                                      compress_geometry=compress)
+                                      compress_geometry=compress, schedule=args.schedule, graph=args.par_graph)
             alpha, T = bioheat_coefficients(E, torch, mesh, fes, part)
             pform.AddDomainIntegrator(mass(alpha))
             pform.AddDomainIntegrator(diff(T))
@@ -336,7 +396,8 @@ def main():
             forms = []
             for r in range(nsub):
                 part = E.Partition(fes, er, r, nsub, decomposition=decomp)
-                pf = E.ParBilinearForm(part, kernel=kernel, scatter=scatter, compress_geometry=compress)
+                pf = E.ParBilinearForm(part, kernel=kernel, scatter=scatter, compress_geometry=compress,
+                                       schedule=args.schedule)
                 alpha, T = bioheat_coefficients(E, torch, mesh, fes, part)
                 keep += [alpha, T, part]
                 pf.AddDomainIntegrator(mass(alpha))
@@ -346,6 +407,9 @@ def main():
             group = E.ParGroup(forms)
             xs = [torch.empty(f.true_size, dtype=torch.float64, device="cuda").uniform_(-1, 1) for f in forms]
             ys = [torch.empty_like(v) for v in xs]
+            if args.member is not None:
+                member_bench(args, torch, group, xs, ys, fes.ndofs, workload, dl)
+                return
             n_true = sum(f.true_size for f in forms)
             apply = lambda _x, _y: group.Mult(xs, ys)
             timed_forms = forms
@@ -430,7 +494,7 @@ def main():
                 "kernel": ["auto", "tpe", "wpe", "unfused", "line"][timed_forms[0].info()["kernel"]],
                 "qdata_layout": layout,
                 "qdata_bytes_stored": qbytes_total / world,
-                "parallelism": (f"domain decomposition, {'z-slabs' if args.partition == 'slabs' else 'boxes'} x{world} ({decomp}), RCCL shared-DoF exchange"
+                "parallelism": (f"domain decomposition, {'z-slabs' if args.partition == 'slabs' else 'boxes'} x{world} ({decomp}, {args.schedule} schedule), RCCL shared-DoF exchange"
                                 if world > 1 else
                                 (f"loopback {'z-slabs' if args.partition == 'slabs' else 'boxes'} x{args.loopback} on one GPU" if args.loopback > 1 else "single GPU")),
             },

@@ -538,6 +538,7 @@ _PAR_SIGS = {
     "ecm2_par_form_set_kernel": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ecm2_par_form_set_scatter": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ecm2_par_form_set_bricks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "ecm2_par_form_set_schedule": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "ecm2_par_form_addressing_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
                                                       ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_long)]),
     "ecm2_par_form_set_geometry_compression": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
@@ -555,6 +556,8 @@ _PAR_SIGS = {
                                                         ctypes.POINTER(ctypes.c_int)]),
     "ecm2_par_group_mult": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_void_p]),
+    "ecm2_par_group_mult_member": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                                  ctypes.c_void_p, ctypes.c_void_p]),
     "ecm2_par_form_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ecm2_par_form_timing_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                                 ctypes.POINTER(ctypes.c_long)]),
@@ -698,7 +701,8 @@ class ParBilinearForm:
     group member (use ParGroup.Mult); otherwise one process per GPU over RCCL."""
 
     def __init__(self, part: Partition, rccl_id: Optional[bytes] = None, kernel: int = KERNEL_AUTO, q1d: int = 0,
-                 scatter: str = "partials", bricks: int = -1, compress_geometry: bool = True):
+                 scatter: str = "partials", bricks: int = -1, compress_geometry: bool = True,
+                 schedule: str = "serial", graph: int = -1):
         lib = _par_lib()
         self.part = part
         self._keep = []
@@ -715,6 +719,7 @@ class ParBilinearForm:
         _check(lib.ecm2_par_form_set_kernel(h, kernel))
         _check(lib.ecm2_par_form_set_scatter(h, _SCATTER[scatter]))
         _check(lib.ecm2_par_form_set_bricks(h, bricks))
+        _check(lib.ecm2_par_form_set_schedule(h, {"serial": 0, "overlap": 1}[schedule], graph))
         _check(lib.ecm2_par_form_set_geometry_compression(h, 1 if compress_geometry else 0))
         self.true_size = part.n_owned
 
@@ -790,6 +795,17 @@ class ParGroup:
         ya = (ctypes.c_void_p * n)(*[_dev_ptr(y).value for y in ys])
         _check(_par_lib().ecm2_par_group_mult(ctypes.cast(fa, ctypes.c_void_p), n, ctypes.cast(xa, ctypes.c_void_p),
                                               ctypes.cast(ya, ctypes.c_void_p), _stream(stream)))
+
+    def MultMember(self, r, xs, ys, stream=None):
+        """Member r's rows alone (y[r] only), on the streams and in the stage order one RCCL rank
+        uses: what one rank's Mult costs on its own GPU, short of the xGMI transfer."""
+        n = len(self.forms)
+        fa = (ctypes.c_void_p * n)(*[f._h.value for f in self.forms])
+        xa = (ctypes.c_void_p * n)(*[_dev_ptr(x).value for x in xs])
+        ya = (ctypes.c_void_p * n)(*[_dev_ptr(y).value for y in ys])
+        _check(_par_lib().ecm2_par_group_mult_member(ctypes.cast(fa, ctypes.c_void_p), n, r,
+                                                     ctypes.cast(xa, ctypes.c_void_p),
+                                                     ctypes.cast(ya, ctypes.c_void_p), _stream(stream)))
 
     def AssembleDiagonal(self, ds, stream=None):
         n = len(self.forms)

@@ -609,6 +609,16 @@ int ecm2_par_form_set_bricks(ecm2_par_form *f, int bz)
    return guard([&] { NEED(f); f->f->local().set_line_bricks(bz); });
 }
 
+int ecm2_par_form_set_schedule(ecm2_par_form *f, int schedule, int graph)
+{
+   return guard([&] {
+      NEED(f);
+      ECM2_VERIFY(schedule == ECM2_SCHEDULE_SERIAL || schedule == ECM2_SCHEDULE_OVERLAP, ecm2::ERR_ARG,
+                  "schedule " << schedule << " not ECM2_SCHEDULE_SERIAL / ECM2_SCHEDULE_OVERLAP");
+      f->f->set_schedule(schedule == ECM2_SCHEDULE_SERIAL, graph);
+   });
+}
+
 int ecm2_par_form_set_scatter(ecm2_par_form *f, int mode)
 {
    return guard([&] { NEED(f); f->f->local().set_scatter(mode); });
@@ -693,6 +703,25 @@ int ecm2_par_group_mult(ecm2_par_form *const *forms, int n, const double *const 
          ys.push_back(y_true[i]);
       }
       ecm2::par_group_mult(fs, xs, ys, S(stream));
+   });
+}
+
+int ecm2_par_group_mult_member(ecm2_par_form *const *forms, int n, int member, const double *const *x_true,
+                               double *const *y_true, void *stream)
+{
+   return guard([&] {
+      NEED(forms); NEED(x_true); NEED(y_true);
+      std::vector<ecm2::ParPAForm *> fs;
+      std::vector<const double *> xs;
+      std::vector<double *> ys;
+      for (int i = 0; i < n; i++)
+      {
+         NEED(forms[i]);
+         fs.push_back(forms[i]->f);
+         xs.push_back(x_true[i]);
+         ys.push_back(y_true[i]);
+      }
+      ecm2::par_group_mult_member(fs, xs, ys, member, S(stream));
    });
 }
 

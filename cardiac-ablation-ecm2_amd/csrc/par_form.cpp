@@ -82,15 +82,20 @@ double rccl_p2p_selftest(bool graph, int n)
    return err;
 }
 
-// ECM2_PAR_GRAPH=0: launch the Mult's stages directly instead of replaying a captured graph
-// (a debugging aid; the operator is the same).
-static bool par_graph()
+// The distributed Mult as one captured HIP graph (per (x, y) pair) or as direct launches.
+// The serial schedule is ~5 API calls per Mult, fewer host-microseconds than its GPU time even
+// at C4 / 8 ranks, and a graph replay leaves ~9 us between consecutive Mults
+// (profiles/r2_member_emul.txt): direct launches.  The overlapped schedule's ~15 calls (event
+// pairs for the comm stream) are host-bound without the graph.  ECM2_PAR_GRAPH=0 / 1 forces
+// either (the operator is the same).
+static bool par_graph(bool serial, int mode)
 {
-   static const bool v = [] {
+   static const int v = [] {
       const char *e = std::getenv("ECM2_PAR_GRAPH");
-      return !(e && std::string(e) == "0");
+      return e ? (std::string(e) == "0" ? 0 : 1) : -1;
    }();
-   return v;
+   if (mode >= 0) { return mode == 1; }
+   return v < 0 ? !serial : v == 1;
 }
 
 ParPAForm::ParPAForm(const LocalPart &part, const double *enodes_local_host, int q1d,
@@ -100,11 +105,11 @@ ParPAForm::ParPAForm(const LocalPart &part, const double *enodes_local_host, int
    const int nl = part.n_owned + part.n_ghost;
    local_.reset(new PAForm(part.ne_local, part.order, nl, part.gather_map.data(), q1d, part.n_owned));
    local_->set_element_nodes(enodes_local_host);
-   // the Mult applies blocks [0, b_int) (interior) and [b_int, nblk) (boundary, with the
-   // one-block-per-workgroup latency kernel) separately
-   const int bi = part.ne_interior / kElemBlock;
-   local_->set_block_splits({bi});
-   local_->set_latency_from(bi);
+   // Mult schedule: serial by default (set_schedule; the overlapped one applies blocks [0,
+   // b_int) (interior) beside the exchange and [b_int, nblk) (boundary, with the
+   // one-block-per-workgroup latency kernel) on the comm stream -- profiles/r2_member_trace.txt:
+   // the interior kernel takes every CU slot and the boundary kernel beside it ends with it)
+   set_schedule(true, -1);
    sched_p_ = exchange_schedule(part, false);
    sched_t_ = exchange_schedule(part, true);
    for (const Xfer &t : sched_p_) { pack_needed_ |= t.buf == XBUF_SENDBUF; }
@@ -133,6 +138,31 @@ ParPAForm::ParPAForm(const LocalPart &part, const double *enodes_local_host, int
    ECM2_HIP(hipEventCreateWithFlags(&ev_yg_, hipEventDisableTiming));
    ECM2_HIP(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
    ECM2_HIP(hipDeviceSynchronize());
+}
+
+void ParPAForm::set_schedule(bool serial, int graph)
+{
+   ECM2_VERIFY(graph >= -1 && graph <= 1, ERR_ARG, "graph mode " << graph << " not in {-1, 0, 1}");
+   serial_ = serial;
+   graph_mode_ = graph;
+   drop_graphs();
+   const int bi = part_.ne_interior / kElemBlock;
+   if (!serial_)
+   {
+      local_->set_block_splits({bi});
+      local_->set_latency_from(bi);
+   }
+   else
+   {
+      // one launch over every block, but the element order is still derived per segment
+      // [interior | boundary]: the interior's face-linked bricks are anchored at its own first
+      // layer, so none of them touches a ghost dof and all are lattice-addressed (anchored at the
+      // local mesh's first layer, the bricks of the ghost-touching bottom layer read the map).
+      // A split on a multiple of 4 blocks keeps the plan's workgroups (4 blocks from each
+      // segment's start) those of the single launch.
+      local_->set_block_splits({bi / 4 * 4});
+      local_->set_latency_from(-1);
+   }
 }
 
 void ParPAForm::drop_graphs()
@@ -240,7 +270,7 @@ void ParPAForm::stage_finish(double *y_true, hipStream_t s)
    if (!part_.overlap) { phase_finish(y_true, s); }
 }
 
-void ParPAForm::rccl_exchange(bool transpose, const double *x_true)
+void ParPAForm::rccl_exchange(bool transpose, const double *x_true, hipStream_t st)
 {
    ncclComm_t comm = (ncclComm_t)comm_;
    const std::vector<Xfer> &sch = schedule(transpose);
@@ -249,19 +279,46 @@ void ParPAForm::rccl_exchange(bool transpose, const double *x_true)
    for (const Xfer &t : sch)
    {
       double *p = xfer_ptr(t, x_true);
-      if (t.send) { ECM2_NCCL(ncclSend(p, t.count, ncclFloat64, t.peer, comm, cs_)); }
-      else { ECM2_NCCL(ncclRecv(p, t.count, ncclFloat64, t.peer, comm, cs_)); }
+      if (t.send) { ECM2_NCCL(ncclSend(p, t.count, ncclFloat64, t.peer, comm, st)); }
+      else { ECM2_NCCL(ncclRecv(p, t.count, ncclFloat64, t.peer, comm, st)); }
    }
    ECM2_NCCL(ncclGroupEnd());
 }
 
+// Serial schedule, after the P exchange on s: every local block in one launch, then [RAP: the
+// ghost dofs' sums (sent by the caller's P^T exchange)] -- no comm stream, no cross-stream
+// event: the interior kernel would otherwise occupy every CU slot and the boundary kernel
+// beside it finishes only with it (profiles/r2_member_trace.txt).
+void ParPAForm::stage_serial_apply(const double *x_true, double *y_true, hipStream_t s)
+{
+   if (!local_->use_partials())
+   {
+      if (part_.n_owned) { ECM2_HIP(hipMemsetAsync(y_true, 0, sizeof(double) * part_.n_owned, s)); }
+      if (part_.n_ghost) { ECM2_HIP(hipMemsetAsync(yg_.data(), 0, sizeof(double) * part_.n_ghost, s)); }
+   }
+   local_->record_start_public(s);
+   local_->apply_blocks(x_true, xg_.data(), y_true, yg_.data(), 0, local_->nblocks(), s);
+   local_->record_stop_public(s);
+   if (!part_.overlap) { local_->finish_shared(local_->n_shared_owned(), local_->n_shared(), y_true, yg_.data(), s); }
+}
+
 void ParPAForm::mult_stages(const double *x_true, double *y_true, hipStream_t s)
 {
+   if (serial_)
+   {
+      if (pack_needed_) { kern::gather_idx((int)part_.send_idx.size(), send_idx_.data(), x_true, sendbuf_.data(), s); }
+      rccl_exchange(false, x_true, s);
+      stage_serial_apply(x_true, y_true, s);
+      if (!part_.overlap) { rccl_exchange(true, x_true, s); }
+      local_->finish_shared(0, local_->n_shared_owned(), y_true, yg_.data(), s);
+      if (!part_.overlap) { phase_finish(y_true, s); }
+      return;
+   }
    stage_pack(x_true, y_true, s);
    stage_interior(x_true, y_true, s);
-   rccl_exchange(false, x_true);
+   rccl_exchange(false, x_true, cs_);
    stage_boundary(x_true, y_true);
-   if (!part_.overlap) { rccl_exchange(true, x_true); }
+   if (!part_.overlap) { rccl_exchange(true, x_true, cs_); }
    stage_finish(y_true, s);
 }
 
@@ -274,7 +331,7 @@ void ParPAForm::mult(const double *x_true, double *y_true, hipStream_t s)
       drop_graphs();  // the cached graphs bake in the previous assembly's buffers and kernels
       graph_gen_ = local_->generation();
    }
-   if (!par_graph() || graph_failed_ || local_->timing_on() || !p2p_warm_)
+   if (!par_graph(serial_, graph_mode_) || graph_failed_ || local_->timing_on() || !p2p_warm_)
    {
       // the first Mult runs directly on every rank: RCCL sets up its peer connections
       // lazily at the first send/recv, which then happens outside a stream capture
@@ -346,7 +403,7 @@ void ParPAForm::assemble_diagonal(double *d_true, hipStream_t s)
    // P^T of the ghost entries, on s
    ECM2_HIP(hipEventRecord(ev_xg_, s));
    ECM2_HIP(hipStreamWaitEvent(cs_, ev_xg_, 0));
-   rccl_exchange(true, nullptr);
+   rccl_exchange(true, nullptr, cs_);
    ECM2_HIP(hipEventRecord(ev_done_, cs_));
    ECM2_HIP(hipStreamWaitEvent(s, ev_done_, 0));
    phase_finish(d_true, s);
@@ -388,7 +445,87 @@ void group_exchange(std::vector<ParPAForm *> &forms, const std::vector<const dou
       }
    }
 }
+// The loopback transport of one exchange on one stream (the serial schedule): every receive
+// copies the peer's matching send.
+void group_copies(std::vector<ParPAForm *> &forms, const std::vector<const double *> &x, bool transpose,
+                  hipStream_t s, int only = -1)
+{
+   const int n = (int)forms.size();
+   for (int r = 0; r < n; r++)
+   {
+      if (only >= 0 && r != only) { continue; }
+      ParPAForm &f = *forms[r];
+      for (const Xfer &t : f.schedule(transpose))
+      {
+         if (t.send) { continue; }
+         ECM2_VERIFY(t.peer >= 0 && t.peer < n, ERR_INTERNAL, "exchange peer " << t.peer << " outside the group");
+         ParPAForm &o = *forms[t.peer];
+         const Xfer *m = nullptr;
+         for (const Xfer &u : o.schedule(transpose))
+         {
+            if (u.send && u.peer == r) { m = &u; break; }
+         }
+         ECM2_VERIFY(m && m->count == t.count, ERR_INTERNAL,
+                     "exchange schedules of ranks " << r << " and " << t.peer << " do not match");
+         ECM2_HIP(hipMemcpyAsync(f.xfer_ptr(t, x.empty() ? nullptr : x[r]),
+                                 o.xfer_ptr(*m, x.empty() ? nullptr : x[t.peer]), t.count * sizeof(double),
+                                 hipMemcpyDeviceToDevice, s));
+      }
+   }
+}
 } // namespace
+
+void par_group_mult_member(std::vector<ParPAForm *> &forms, const std::vector<const double *> &x,
+                           const std::vector<double *> &y, int r, hipStream_t s)
+{
+   const int n = (int)forms.size();
+   ECM2_VERIFY((int)x.size() == n && (int)y.size() == n, ERR_ARG, "group size mismatch");
+   ECM2_VERIFY(r >= 0 && r < n, ERR_ARG, "member " << r << " outside the group of " << n);
+   ParPAForm &f = *forms[r];
+   ECM2_VERIFY(f.part().rank == r && f.part().nranks == n, ERR_ARG, "loopback group: form " << r << " has rank "
+                                                                    << f.part().rank);
+   ECM2_VERIFY(f.part().overlap, ERR_UNSUPPORTED, "a member's rows alone need the OVERLAP decomposition");
+   ECM2_VERIFY(f.local().assembled(), ERR_STATE, "Mult before Assemble");
+   for (const Xfer &t : f.schedule(false))
+   {
+      if (t.send) { continue; }
+      const Xfer *m = nullptr;
+      for (const Xfer &u : forms[t.peer]->schedule(false))
+      {
+         if (u.send && u.peer == r) { m = &u; break; }
+      }
+      ECM2_VERIFY(m && m->count == t.count, ERR_INTERNAL, "exchange schedules of ranks " << r << " and " << t.peer
+                                                                                       << " do not match");
+      ECM2_VERIFY(m->buf == XBUF_X_TRUE, ERR_UNSUPPORTED, "member Mult: rank " << t.peer
+                                                          << " sends through its pack buffer (z-slabs only)");
+   }
+   if (f.serial())
+   {
+      group_copies(forms, x, false, s, r);
+      f.stage_serial_apply(x[r], y[r], s);
+      f.local().finish_shared(0, f.local().n_shared_owned(), y[r], f.yghost(), s);
+      return;
+   }
+   f.stage_pack(x[r], y[r], s);
+   // the P exchange of this member on its comm stream: the peers' owned values straight from their x
+   for (const Xfer &t : f.schedule(false))
+   {
+      if (t.send) { continue; }
+      ParPAForm &o = *forms[t.peer];
+      for (const Xfer &u : o.schedule(false))
+      {
+         if (u.send && u.peer == r)
+         {
+            ECM2_HIP(hipMemcpyAsync(f.xfer_ptr(t, x[r]), o.xfer_ptr(u, x[t.peer]), t.count * sizeof(double),
+                                    hipMemcpyDeviceToDevice, f.comm_stream()));
+            break;
+         }
+      }
+   }
+   f.stage_interior(x[r], y[r], s);
+   f.stage_boundary(x[r], y[r]);
+   f.stage_finish(y[r], s);
+}
 
 void par_group_mult(std::vector<ParPAForm *> &forms, const std::vector<const double *> &x,
                     const std::vector<double *> &y, hipStream_t s)
@@ -400,6 +537,32 @@ void par_group_mult(std::vector<ParPAForm *> &forms, const std::vector<const dou
       ECM2_VERIFY(forms[r]->part().rank == r && forms[r]->part().nranks == n, ERR_ARG,
                   "loopback group: form " << r << " has rank " << forms[r]->part().rank);
       ECM2_VERIFY(forms[r]->local().assembled(), ERR_STATE, "Mult before Assemble");
+   }
+   for (int r = 1; r < n; r++)
+   {
+      ECM2_VERIFY(forms[r]->serial() == forms[0]->serial(), ERR_ARG, "loopback group: members use different schedules");
+   }
+   if (!forms.empty() && forms[0]->serial())
+   {
+      // the serial schedule, stage-major on s: packs, the P copies, the applies, [RAP: P^T
+      // copies], the sums
+      for (int r = 0; r < n; r++)
+      {
+         ParPAForm &f = *forms[r];
+         if (f.pack_needed())
+         {
+            kern::gather_idx((int)f.part().send_idx.size(), f.send_idx_data(), x[r], f.sendbuf_data(), s);
+         }
+      }
+      group_copies(forms, x, false, s);
+      for (int r = 0; r < n; r++) { forms[r]->stage_serial_apply(x[r], y[r], s); }
+      if (!forms[0]->part().overlap) { group_copies(forms, x, true, s); }
+      for (int r = 0; r < n; r++)
+      {
+         forms[r]->local().finish_shared(0, forms[r]->local().n_shared_owned(), y[r], forms[r]->yghost(), s);
+         if (!forms[r]->part().overlap) { forms[r]->phase_finish(y[r], s); }
+      }
+      return;
    }
    // the same stages as ParPAForm::mult, stage-major over the members; a member's
    // exchanges wait for its peers' events and copy from their buffers on its comm stream

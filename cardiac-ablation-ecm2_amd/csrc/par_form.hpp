@@ -60,7 +60,19 @@ public:
    {
       kern::scatter_add_idx((int)part_.send_idx.size(), send_idx_.data(), rbuf_.data(), y_true, s);
    }
+   // Serial schedule (one stream): pack, the P exchange, ONE apply launch over every local
+   // block, [RAP: ghost sums, P^T exchange], the shared-dof sums.  The overlapped schedule runs
+   // the interior beside the exchange + boundary elements on the comm stream instead.
+   bool serial() const { return serial_; }
+   // Schedule of the Mult (serial: true, overlapped: false) and its launch form (graph: 1
+   // captured HIP graph, 0 direct launches, -1 the schedule's default); before Assemble.
+   void set_schedule(bool serial, int graph);
+   void stage_serial_apply(const double *x_true, double *y_true, hipStream_t s);
    hipStream_t comm_stream() const { return cs_; }
+   bool pack_needed() const { return pack_needed_; }
+   const int *send_idx_data() const { return send_idx_.data(); }
+   double *sendbuf_data() { return sendbuf_.data(); }
+   double *yghost() { return yg_.data(); }
    hipEvent_t event_packed() const { return ev_pack_; }
    hipEvent_t event_ghosts_summed() const { return ev_yg_; }
 
@@ -70,7 +82,7 @@ public:
    double *xfer_ptr(const Xfer &t, const double *x_true);
 
 private:
-   void rccl_exchange(bool transpose, const double *x_true);  // grouped send/recv on the comm stream
+   void rccl_exchange(bool transpose, const double *x_true, hipStream_t st);  // grouped send/recv on st
    void mult_stages(const double *x_true, double *y_true, hipStream_t s);
    int b_int() const { return part_.ne_interior / kElemBlock; }
    void drop_graphs();
@@ -78,6 +90,8 @@ private:
    std::unique_ptr<PAForm> local_;
    std::vector<Xfer> sched_p_, sched_t_;
    bool pack_needed_ = false;           // some P send goes through the packed buffer
+   bool serial_ = true;                 // serial schedule (serial())
+   int graph_mode_ = -1;                // set_schedule
    DeviceArray<int> send_idx_;
    DeviceArray<double> sendbuf_, xg_, yg_, rbuf_, dl_;
    void *comm_ = nullptr;               // ncclComm_t
@@ -104,6 +118,13 @@ double rccl_p2p_selftest(bool graph, int n);
 void par_group_mult(std::vector<ParPAForm *> &forms, const std::vector<const double *> &x,
                     const std::vector<double *> &y, hipStream_t s);
 void par_group_diagonal(std::vector<ParPAForm *> &forms, const std::vector<double *> &d, hipStream_t s);
+// One member's rows of the group operator, y[r] = (A x)_r: member r's stages alone, exactly as
+// one rank of the RCCL transport runs them (interior on s, exchange + boundary on r's comm
+// stream, then the summation), its ghost values copied from the peers' x.  OVERLAP
+// decomposition, sends straight from x (z-slabs); the other members' y are not touched.  This
+// is what a rank's Mult costs on its own GPU, short of the xGMI transfer time.
+void par_group_mult_member(std::vector<ParPAForm *> &forms, const std::vector<const double *> &x,
+                           const std::vector<double *> &y, int r, hipStream_t s);
 
 void rccl_unique_id(unsigned char *out128);
 

@@ -332,6 +332,16 @@ int ecm2_par_form_add_integrator(ecm2_par_form *f, int integrator, int coeff_kin
 int ecm2_par_form_set_kernel(ecm2_par_form *f, int kernel);
 /* Brick mode of the local form (see ecm2_pa_form_set_bricks). */
 int ecm2_par_form_set_bricks(ecm2_par_form *f, int bz);
+/* Schedule of the distributed Mult (no reference counterpart; the reference overlaps its
+ * MPI exchange with nothing, pfespace.cpp:5394-5532): ECM2_SCHEDULE_SERIAL (default) = the P
+ * exchange, ONE apply launch over every local element, the shared-dof sums, all on the
+ * caller's stream; ECM2_SCHEDULE_OVERLAP = interior elements on the caller's stream beside the
+ * exchange + boundary elements on a high-priority comm stream.  graph: 1 = replay one captured
+ * HIP graph per (x, y), 0 = direct launches, -1 = the schedule's default (serial: direct,
+ * overlap: graph).  Before Assemble. */
+#define ECM2_SCHEDULE_SERIAL 0
+#define ECM2_SCHEDULE_OVERLAP 1
+int ecm2_par_form_set_schedule(ecm2_par_form *f, int schedule, int graph);
 /* Scatter mode of the local form (ECM2_SCATTER_*; see ecm2_pa_form_set_scatter). */
 int ecm2_par_form_set_scatter(ecm2_par_form *f, int mode);
 /* Geometry compression of the local form (see ecm2_pa_form_set_geometry_compression). */
@@ -352,6 +362,14 @@ int ecm2_par_form_addressing_info(const ecm2_par_form *f, int *lattice, int *n_u
  * follow the members' exchange schedules). */
 int ecm2_par_group_mult(ecm2_par_form *const *forms, int n, const double *const *x_true,
                         double *const *y_true, void *stream);
+/* One member's rows of the loopback group's operator (measurement of a rank's Mult on its own
+ * GPU; no reference counterpart): y_true[member] = (A x)[member's true dofs], running exactly
+ * the stages one RCCL rank runs (interior elements on `stream`, the P exchange -- here device
+ * copies from the peers' x -- and the boundary elements on the member's comm stream, then the
+ * shared-dof sums).  OVERLAP decomposition with sends straight from x (z-slabs); the other
+ * members' y are not written.  ECM2_ERR_UNSUPPORTED otherwise. */
+int ecm2_par_group_mult_member(ecm2_par_form *const *forms, int n, int member, const double *const *x_true,
+                               double *const *y_true, void *stream);
 /* ParBilinearForm::AssembleDiagonal on the true dofs (local PA diagonal + P^T). */
 int ecm2_par_form_assemble_diagonal(ecm2_par_form *f, double *d_true, void *stream);
 int ecm2_par_group_diagonal(ecm2_par_form *const *forms, int n, double *const *d_true, void *stream);

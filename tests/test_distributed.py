@@ -201,6 +201,93 @@ def test_gpu_loopback_group_matches_serial(kind, nranks, order, scatter, decomp)
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind,nranks,order", [("cart", 2, 2), ("fichera", 3, 2), ("fichera", 4, 3),
+                                               ("cart_big", 3, 4), ("cart_big", 2, 2)])
+@pytest.mark.parametrize("scatter", ["partials", "atomic"])
+@pytest.mark.parametrize("decomp", ["rap", "overlap"])
+def test_gpu_loopback_overlapped_schedule(kind, nranks, order, scatter, decomp):
+    """The overlapped Mult schedule (interior beside exchange + boundary on the comm stream,
+    ecm2_par_form_set_schedule) gives the serial oracle's y too."""
+    import torch
+    m = _mesh(kind)
+    fes = E.H1Space(m, order)
+    er = _elem_rank(m, kind, nranks)
+    q1d = O.default_q1d(order)
+    forms, xs, ys, parts = [], [], [], []
+    xg = np.random.default_rng(3).uniform(-1, 1, fes.ndofs)
+    for r in range(nranks):
+        part = E.Partition(fes, er, r, nranks, decomposition=decomp)
+        pf = E.ParBilinearForm(part, scatter=scatter, schedule="overlap")
+        P = E.quadrature_points_subset(m, q1d, part.elems)
+        c = torch.as_tensor(coeff_function(P).reshape(part.ne_local, -1)).cuda()
+        pf.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(c)))
+        pf.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(c.clone())))
+        pf.Assemble()
+        forms.append(pf)
+        parts.append(part)
+        xs.append(torch.as_tensor(xg[part.owned_global]).cuda())
+        ys.append(torch.full((part.n_owned,), float("nan"), dtype=torch.float64, device="cuda"))
+    E.ParGroup(forms).Mult(xs, ys)
+    torch.cuda.synchronize()
+    y = np.zeros(fes.ndofs)
+    for part, yt in zip(parts, ys):
+        y[part.owned_global] = yt.cpu().numpy()
+    Pg = O.quad_points(m.element_nodes(), q1d)
+    cg = coeff_function(Pg)
+    ref = O.OracleOperator(m.element_nodes(), fes.gather_map(), fes.ndofs, order, alpha=cg, beta=cg).mult(xg)
+    assert relerr(y, ref) <= RTOL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nranks,order", [(2, 2), (3, 2), (8, 2), (3, 4)])
+@pytest.mark.parametrize("schedule", ["serial", "overlap"])
+def test_gpu_group_member_rows(nranks, order, schedule):
+    """ParGroup.MultMember: one member's rows alone (the stages one RCCL rank runs, ghost values
+    copied from the peers' x) equal the serial oracle's rows; also replayed from a HIP graph
+    (how bench.py --member times it); the other members' y stay untouched."""
+    import torch
+    m = E.Mesh.MakeCartesian3D(6, 5, 16) if nranks == 8 else _mesh("cart_big")
+    m.set_vertices(nonaligned(m.vertices()))
+    fes = E.H1Space(m, order, E.NUMBERING_STRUCTURED)
+    er = E.partition_slabs_z(m, nranks)
+    q1d = O.default_q1d(order)
+    forms, xs, ys, parts = [], [], [], []
+    xg = np.random.default_rng(11).uniform(-1, 1, fes.ndofs)
+    for r in range(nranks):
+        part = E.Partition(fes, er, r, nranks, decomposition="overlap")
+        pf = E.ParBilinearForm(part, schedule=schedule)
+        P = E.quadrature_points_subset(m, q1d, part.elems)
+        c = torch.as_tensor(coeff_function(P).reshape(part.ne_local, -1)).cuda()
+        pf.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(c)))
+        pf.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(c.clone())))
+        pf.Assemble()
+        forms.append(pf)
+        parts.append(part)
+        xs.append(torch.as_tensor(xg[part.owned_global]).cuda())
+        ys.append(torch.full((part.n_owned,), float("nan"), dtype=torch.float64, device="cuda"))
+    Pg = O.quad_points(m.element_nodes(), q1d)
+    cg = coeff_function(Pg)
+    ref = O.OracleOperator(m.element_nodes(), fes.gather_map(), fes.ndofs, order, alpha=cg, beta=cg).mult(xg)
+    group = E.ParGroup(forms)
+    for r in range(nranks):
+        group.MultMember(r, xs, ys)
+        torch.cuda.synchronize()
+        assert relerr(ys[r].cpu().numpy(), ref[parts[r].owned_global]) <= RTOL
+        for q in range(r + 1, nranks):
+            assert torch.isnan(ys[q]).all()
+    r = nranks - 1
+    ys[r].fill_(float("nan"))
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=torch.cuda.Stream()):
+        group.MultMember(r, xs, ys)
+    g.replay()
+    g.replay()
+    torch.cuda.synchronize()
+    assert relerr(ys[r].cpu().numpy(), ref[parts[r].owned_global]) <= RTOL
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("order", [2, 4])
 def test_gpu_rccl_single_rank_transport(order):
     """The RCCL transport with one rank (ncclCommInitRank, the comm stream and its events,

@@ -448,14 +448,15 @@ def test_perfusion_coefficient(order):
 # the distributed form's graph cache across re-assembly (the graphs bake in buffers)
 # ---------------------------------------------------------------------------------------
 @pytest.mark.parametrize("order", [2, 4])
-def test_rccl_graph_cache_follows_reassembly(order):
+@pytest.mark.parametrize("schedule", ["serial", "overlap"])
+def test_rccl_graph_cache_follows_reassembly(order, schedule):
     m = E.Mesh.MakeCartesian3D(6, 5, 4)
     fes = E.H1Space(m, order)
     part = E.Partition(fes, np.zeros(m.GetNE(), np.int32), 0, 1)
     q1d = O.default_q1d(order)
     P = E.quadrature_points_subset(m, q1d, part.elems)
     c = coeff_function(P).reshape(part.ne_local, -1)
-    pf = E.ParBilinearForm(part, rccl_id=E.rccl_unique_id())
+    pf = E.ParBilinearForm(part, rccl_id=E.rccl_unique_id(), schedule=schedule, graph=1)
     pf.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(c))))
     pf.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(dev(c))))
     pf.Assemble()

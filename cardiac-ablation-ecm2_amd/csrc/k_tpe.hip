@@ -535,8 +535,8 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                                                          wave_on, rg, reg, pstride);
 }
 
-// Latency variant of k_apply_tpe_sf for small block ranges (the distributed Mult's boundary
-// elements, on the critical path of the exchange): one workgroup per 64-element block, its
+// Latency variant of k_apply_tpe_sf for small block ranges (the boundary elements of the
+// overlapped distributed-Mult schedule, behind the exchange): one workgroup per 64-element block, its
 // four waves gather the x-values together and take one quadrature plane each (all of the
 // plane's pairs loaded up front), so a block costs one plane's latency instead of four.
 // Waves 1..3 hand their partial outputs to wave 0 through LDS, which adds them in a fixed

@@ -350,8 +350,8 @@ int ecm2_par_form_set_geometry_compression(ecm2_par_form *f, int on);
  * (pbilinearform.cpp:475-511, bilinearform_ext.cpp:332-368). */
 int ecm2_par_form_assemble(ecm2_par_form *f, void *stream);
 /* RAPOperator::Mult (operator.hpp:977): y_true = P^T A P x_true; x_true, y_true device
- * [n_owned].  Grouped ncclSend/ncclRecv on an internal stream overlapped with the
- * interior elements. */
+ * [n_owned].  Grouped ncclSend/ncclRecv, then the local PA apply and the shared-dof sums on
+ * `stream` (ECM2_SCHEDULE_SERIAL, the default); see ecm2_par_form_set_schedule. */
 int ecm2_par_form_mult(ecm2_par_form *f, const double *x_true, double *y_true, void *stream);
 /* RAPOperator::MultTranspose (operator.hpp:979): P^T A^T P = P^T A P (A symmetric). */
 int ecm2_par_form_mult_transpose(ecm2_par_form *f, const double *x_true, double *y_true, void *stream);

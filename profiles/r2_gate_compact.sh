@@ -1,0 +1,13 @@
+#!/bin/bash
+# compact per-entry list for short summation runs: suite, then same-box A/B (before = runs only)
+set -uo pipefail
+O=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out
+mkdir -p "$O"
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$O/pytest_gpu.log" 2>&1
+rc=$?
+tail -2 "$O/pytest_gpu.log"; grep -E "FAILED|ERROR" "$O/pytest_gpu.log" | head -20
+[ $rc -eq 0 ] || exit $rc
+bash profiles/ab_lib_r2.sh compact_c3 --workload c3 --steps 30 --warmup 5 || exit $?
+bash profiles/ab_lib_r2.sh compact_c2 --workload c2 --steps 50 --warmup 5 || exit $?
+bash profiles/ab_member_r2.sh compact 8 2 || exit $?
+bash profiles/ab_lib_r2.sh compact_c4 --workload c4 --steps 50 --warmup 5 || exit $?

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (Needs the WPB experiment code, measured and removed: profiles/r2_ab_wpb.txt; kept as the record of the run.)
 # two waves per block (k_apply_tpe_sf WPB = 2) for small launches: suite (auto), then A/B by ECM2_TPE_WPB
 set -uo pipefail
 O=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/wpb

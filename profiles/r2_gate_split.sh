@@ -1,4 +1,5 @@
 #!/bin/bash
+# (Needs the split-schedule experiment code, measured and removed: profiles/r2_ab_split.txt; kept as the record of the run.)
 # split variant of the serial schedule: distributed GPU tests, then emulated ranks serial vs split (direct)
 set -uo pipefail
 O=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out

@@ -229,8 +229,10 @@ def pmc_pin(workload, world, layout):
     return pin.get("hbm_bytes_per_launch"), prov
 
 
-def roofline(workload, world, layout, kms, alg_bytes, mbytes, stream):
-    traffic, prov = pmc_pin(workload, world, layout)
+def roofline(workload, world, layout, kms, alg_bytes, mbytes, stream, use_pin=True):
+    # a pin holds the traffic of one configuration (the workload's default size, one kernel per
+    # GPU): anything else reports the formulation's minimum bytes instead
+    traffic, prov = pmc_pin(workload, world, layout) if use_pin else (None, None)
     moved = traffic if traffic else mbytes
     achieved = moved / (kms * 1e-3) / 1e9
     return {
@@ -446,6 +448,8 @@ def main():
             dist.all_reduce(s[i:i + 1], op=dist.ReduceOp.MAX)
         tot = s
     ndofs_total, tmax, bytes_total, kavg_ms, qbytes_total, mbytes_total = [float(v) for v in tot.cpu()]
+    pin_ok = (args.loopback <= 1 and (args.workload != "c2" or args.c2_n == 50)
+              and (args.workload != "c3" or args.c3_refine == 6))
     value = ndofs_total * args.steps / tmax / 1e6
 
     full = None
@@ -460,7 +464,7 @@ def main():
                 "value": round(fes.ndofs * args.steps / dtf / 1e6, 2),
                 "ms_per_step": round(dtf / args.steps * 1e3, 5),
                 "roofline": roofline(args.workload, 1, lay_f, kf, ff.algorithmic_bytes(),
-                                     min_bytes(ff, fes.ne, nd, fes.ndofs), None),
+                                     min_bytes(ff, fes.ne, nd, fes.ndofs), None, use_pin=pin_ok),
                 "note": "same run, same inputs, per-point qdata (56 B per quadrature point: the layout SURVEY "
                         "§8(d)'s algorithmic bytes describe, so its alg_ratio is a roofline fraction)"}
         del ff
@@ -499,7 +503,7 @@ def main():
                                 (f"loopback {'z-slabs' if args.partition == 'slabs' else 'boxes'} x{args.loopback} on one GPU" if args.loopback > 1 else "single GPU")),
             },
             "roofline": roofline(args.workload, world, layout, kavg_ms, bytes_total / world, mbytes_total / world,
-                                 stream),
+                                 stream, use_pin=pin_ok),
             "cpu_baseline": cpu,
         }
         if full is not None:

@@ -1,0 +1,53 @@
+"""bench.py's contract (the driver parses its last line): the JSON keys of a single-GPU line, a
+loopback group line and the per-member emulation line, on a small C2 mesh.  The numbers are not
+checked here (profiles/ holds the measurements); the shape of the output and its consistency are."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run_bench(*args, timeout=240):
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], cwd=ROOT, capture_output=True,
+                         text=True, timeout=timeout)
+    assert out.returncode == 0, out.stderr[-2000:]
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def test_bench_help_lists_the_options():
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--help"], cwd=ROOT, capture_output=True,
+                         text=True, timeout=120)
+    assert out.returncode == 0
+    for opt in ("--gpus", "--steps", "--warmup", "--workload", "--schedule", "--loopback", "--member", "--deadline"):
+        assert opt in out.stdout
+
+
+SMALL = ["--workload", "c2", "--c2-n", "12", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--full-layout", "0"]
+
+
+@pytest.mark.gpu
+def test_bench_single_gpu_line():
+    b = run_bench(*SMALL)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline"):
+        assert k in b, k
+    assert b["n_gpus"] == 1 and b["steps"] == 3 and b["warmup"] == 1 and b["value"] > 0
+    assert b["dtype"] == "f64" and b["config"]["ndofs"] == (2 * 12 + 1) ** 3
+    r = b["roofline"]
+    assert r["bound"] == "hbm" and r["peak"] == 8000.0 and r["frac"] == pytest.approx(r["achieved"] / r["peak"], abs=1e-3)
+    assert r["traffic"] is None  # a pin belongs to the default size only
+    # value = ndofs * steps / time
+    assert b["value"] == pytest.approx(b["config"]["ndofs"] / (b["ms_per_step"] * 1e-3) / 1e6, rel=1e-3)
+
+
+@pytest.mark.gpu
+def test_bench_loopback_group_and_member_lines():
+    g = run_bench(*SMALL, "--loopback", "2")
+    assert g["value"] > 0 and "loopback" in g["config"]["parallelism"]
+    m = run_bench(*SMALL, "--loopback", "2", "--member", "-1")
+    assert m["emulated_n_gpus"] == 2 and len(m["member_ms"]) == 2 and m["members"] == [0, 1]
+    assert m["slowest_member_ms"] == max(m["member_ms"]) and m["emulated_value"] > 0

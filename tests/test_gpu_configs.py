@@ -10,7 +10,8 @@
 * configs[4] (C5): p = 4 Cartesian 32^3 (2.15M DoF, all elements in 2 x 2 x 1 bricks) against
   the oracle; the SDIRK33 step (ode.cpp:834-859) at p = 4 against the oracle's stepping.
 * configs[3] (C4): the 8-way z-slab split of a 16^3 p = 2 mesh (loopback group, both
-  decompositions) against the serial oracle.
+  decompositions) against the serial oracle, and of the full 108^3 mesh (10.2M DoF) as the 8-GPU
+  bench runs it, each member's rows alone and the whole group.
 * Lattice addressing (the fused kernels compute dofs from 5 ints per block / brick on a
   lattice-numbered mesh) against the map-reading path on the same mesh with the entity
   numbering, p = 1, 2 and 4, Mult and diagonal.
@@ -269,6 +270,50 @@ def test_c4_eight_way_slabs(decomp, scatter):
     Pg = O.quad_points(m.element_nodes(), q1d)
     ref = O.OracleOperator(m.element_nodes(), fes.gather_map(), fes.ndofs, order, alpha=alpha_bioheat(Pg),
                            beta=k_of_T(temperature(Pg))).mult(xg)
+    assert relerr(y, ref) <= RTOL
+
+
+def test_c4_full_size_eight_way_members():
+    """configs[3] exactly as the 8-GPU bench runs it: Cartesian 108^3 (10.2M DoF) in 8 z-slabs,
+    OVERLAP, the serial schedule; every member's rows alone (ParGroup.MultMember, what one rank
+    computes on its GPU) and the whole group against one oracle Mult of the full mesh."""
+    n, nranks, order = 108, 8, 2
+    m = E.Mesh.MakeCartesian3D(n, n, n)
+    fes = E.H1Space(m, order, E.NUMBERING_STRUCTURED)
+    assert fes.ndofs == 10218313
+    er = E.partition_slabs_z(m, nranks)
+    q1d = O.default_q1d(order)
+    xg = np.random.default_rng(108).uniform(-1, 1, fes.ndofs)
+    forms, parts, xs, ys = [], [], [], []
+    for r in range(nranks):
+        part = E.Partition(fes, er, r, nranks, decomposition="overlap")
+        pf = E.ParBilinearForm(part)
+        P = E.quadrature_points_subset(m, q1d, part.elems)
+        pf.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(alpha_bioheat(P).reshape(part.ne_local, -1)))))
+        pf.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(
+            dev(k_of_T(temperature(P)).reshape(part.ne_local, -1)))))
+        pf.Assemble()
+        forms.append(pf)
+        parts.append(part)
+        xs.append(dev(xg[part.owned_global]))
+        ys.append(torch.full((part.n_owned,), float("nan"), dtype=torch.float64, device="cuda"))
+        del P
+    Pg = O.quad_points(m.element_nodes(), q1d)
+    ref = O.OracleOperator(m.element_nodes(), fes.gather_map(), fes.ndofs, order, alpha=alpha_bioheat(Pg),
+                           beta=k_of_T(temperature(Pg))).mult(xg)
+    del Pg
+    group = E.ParGroup(forms)
+    for r in range(nranks):
+        group.MultMember(r, xs, ys)
+    y = np.full(fes.ndofs, np.nan)
+    for part, yt in zip(parts, ys):
+        y[part.owned_global] = host(yt)
+    assert relerr(y, ref) <= RTOL
+    for yt in ys:
+        yt.fill_(float("nan"))
+    group.Mult(xs, ys)
+    for part, yt in zip(parts, ys):
+        y[part.owned_global] = host(yt)
     assert relerr(y, ref) <= RTOL
 
 

@@ -7,8 +7,9 @@
   oracle's PCG (the reference pins PA == FA on fichera: test_pa_kernels.cpp:641-694).
 * Known answers on the reference's own fichera fixture through the HIP path: 1^T M 1 = |fichera|
   = 7 and x^T K x = 7 |g|^2 for the linear x = g . X (H1 interpolates it exactly).
-* configs[4] (C5): p = 4 Cartesian 32^3 (2.15M DoF, all elements in 2 x 2 x 1 bricks) against
-  the oracle; the SDIRK33 step (ode.cpp:834-859) at p = 4 against the oracle's stepping.
+* configs[4] (C5): p = 4 Cartesian 32^3 (2.15M DoF) and 68^3 (20.3M DoF, the bench size), all
+  elements in 2 x 2 x 1 bricks, against the oracle; the SDIRK33 step (ode.cpp:834-859) at p = 4
+  against the oracle's stepping.
 * configs[3] (C4): the 8-way z-slab split of a 16^3 p = 2 mesh (loopback group, both
   decompositions) against the serial oracle, and of the full 108^3 mesh (10.2M DoF) as the 8-GPU
   bench runs it, each member's rows alone and the whole group.
@@ -181,6 +182,31 @@ def test_c5_p4_cartesian_32():
     y2 = torch.full_like(y, float("nan"))
     form.Mult(dev(x), y2)
     assert torch.equal(y, y2)                         # deterministic scatter
+
+
+def test_c5_full_size():
+    """configs[4] at size: Cartesian 68^3, p = 4 (20.3M DoF), every element in a lattice-addressed
+    2 x 2 x 1 brick, against the oracle."""
+    n = 68
+    m = E.Mesh.MakeCartesian3D(n, n, n)
+    fes = E.H1Space(m, 4, E.NUMBERING_STRUCTURED)
+    assert fes.ndofs == 20346417
+    en = m.element_nodes()
+    P = O.quad_points(en, 6)
+    a, b = alpha_bioheat(P), k_of_T(temperature(P))
+    del P
+    form = E.BilinearForm(fes)
+    form.AddDomainIntegrator(E.MassIntegrator(quad_coeff(fes, a)))
+    form.AddDomainIntegrator(E.DiffusionIntegrator(quad_coeff(fes, b)))
+    form.Assemble()
+    assert form.BrickInfo() == (fes.ne // 4, 1) and form.AddressingInfo()[0] == fes.ne // 4
+    x = np.random.default_rng(68).uniform(-1, 1, fes.ndofs)
+    y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+    form.Mult(dev(x), y)
+    yh = host(y)
+    del form, y
+    op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, 4, alpha=a, beta=b)
+    assert relerr(yh, op.mult(x)) <= RTOL
 
 
 def _serial_form(fes, P, alpha, beta):

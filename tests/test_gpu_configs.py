@@ -1,6 +1,7 @@
 """GPU parity on the BASELINE configurations as the build runs them by default.
 
-* configs[2] (C3): fichera.mesh refined 2x / 3x (448 / 3,584 elements) at p = 1, 2 with the
+* configs[2] (C3): fichera.mesh refined 6x as the bench runs it (14.9M DoF, the Pennes k(T)
+  re-assembly), and refined 2x / 3x (448 / 3,584 elements) at p = 1, 2 with the
   default element order, so the face-linked 4x4x4 bricks derived from the gather map and the
   cross-wave LDS face merge run on a non-lattice mesh; Mult and diagonal against the oracle;
   the Pennes k(T) grid-function coefficient and Jacobi-PCG together on r3 against the
@@ -126,6 +127,35 @@ def test_c3_fichera_pennes_pcg(jacobi):
     # rounding differences move the iteration at which the 1e-12 test is first met by a few
     assert abs(it - itr) <= max(2, 0.05 * itr)
     assert relerr(host(x), xr) < 1e-9
+
+
+def test_c3_full_size():
+    """configs[2] at the bench size: fichera.mesh refined 6x (1.84M elements, 14.9M DoF), p = 2,
+    default path (face-linked bricks, cross-wave merge), heat capacity as a quadrature coefficient
+    and k(T) from an H1 temperature field re-assembled on the device, against the oracle."""
+    m = fichera(6)
+    order, q1d = 2, O.default_q1d(2)
+    fes = E.H1Space(m, order)
+    assert fes.ndofs == 14877441
+    en = m.element_nodes()
+    P = O.quad_points(en, q1d)
+    a = alpha_bioheat(P)
+    del P
+    T = temperature(fes.dof_coords())
+    scale, slope, tref = 0.5 * 0.05, 0.0012, 37.0
+    form = E.BilinearForm(fes)
+    form.AddDomainIntegrator(E.MassIntegrator(quad_coeff(fes, a)))
+    form.AddDomainIntegrator(E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(dev(T), scale, slope, tref)))
+    form.Assemble()
+    assert form.info()["kernel"] == E.KERNEL_TPE and form.info()["layout"] == E.QLAYOUT_AFFINE
+    x = np.random.default_rng(6).uniform(-1, 1, fes.ndofs)
+    y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+    form.Mult(dev(x), y)
+    yh = host(y)
+    del form, y
+    beta = BH.affine_law(BH.temperature_at_quadrature(T, fes.gather_map(), order, q1d), scale, slope, tref)
+    op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=a, beta=beta)
+    assert relerr(yh, op.mult(x)) <= RTOL
 
 
 @pytest.mark.parametrize("refine", [1, 2, 3])

@@ -1,0 +1,48 @@
+"""The C++ example over the C ABI (examples/heat_step.cpp): a native caller that links
+libecm2pa.so through include/ecm2_pa.h alone, runs ex16's PA heat step (Mass + Diffusion with
+a k(T) coefficient, SDIRK33, constrained Jacobi-PCG) on the reference's fichera fixture and
+checks its known answers (1^T M 1 = 7, K 1 = 0, a decaying maximum)."""
+import os
+import subprocess
+
+import pytest
+
+from helpers import GOLDEN, ROOT
+
+EXAMPLES = os.path.join(ROOT, "examples")
+BINARY = os.path.join(EXAMPLES, "heat_step")
+
+
+def _build():
+    subprocess.run(["make", "-s", "-C", EXAMPLES], check=True, timeout=300)
+    assert os.access(BINARY, os.X_OK)
+
+
+def _run(*args, timeout=120):
+    return subprocess.run([BINARY, os.path.join(GOLDEN, "fichera.mesh"), *map(str, args)], cwd=ROOT,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_example_builds_and_fails_loudly_without_gpu():
+    """Compiles and links against the header + library; with no device the first compute
+    entry point returns ECM2_ERR_HIP and the program stops (no CPU fallback)."""
+    _build()
+    import ecm2_amd as E
+    if E.load_library().ecm2_device_count() > 0:
+        pytest.skip("a GPU is visible")
+    r = _run(1, 2, 1)
+    assert r.returncode == 2, r.stdout + r.stderr
+    assert "mesh " in r.stdout and "boundary dofs" in r.stdout  # host setup ran
+    assert "no HIP device" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("refine,order", [(1, 1), (2, 2)])
+def test_example_heat_step_on_gpu(refine, order):
+    if not os.access(BINARY, os.X_OK):
+        _build()
+    r = _run(refine, order, 5)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.rstrip().endswith("PASS")
+    assert r.stdout.count("converged 1") == 5

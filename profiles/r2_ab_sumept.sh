@@ -1,6 +1,6 @@
 #!/bin/bash
 # (experiment, source not kept in the tree) plan blocks of up to 4 x 256 entries (ECM2_SUM_EPT=4)
-# ECM2_SUM_EPT=4, the default) against one entry per thread (ECM2_SUM_EPT=1, the previous plan):
+# against one entry per thread (ECM2_SUM_EPT=1, the plan in the tree):
 # parity first, then C4 / C5 bench lines and the emulated 8-rank C4 member Mult, alternating.
 set -uo pipefail
 O=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/sumept

@@ -255,6 +255,15 @@ def roofline(workload, world, layout, kms, alg_bytes, mbytes, stream, use_pin=Tr
     }
 
 
+def par_launch_label(schedule, par_graph):
+    """The distributed Mult's launch form as par_form.cpp's par_graph() resolves it: --par-graph,
+    else ECM2_PAR_GRAPH, else the schedule's default (serial: direct launches, overlap: graph)."""
+    env = os.environ.get("ECM2_PAR_GRAPH")
+    graph = par_graph == 1 if par_graph >= 0 else (env != "0" if env is not None else schedule != "serial")
+    return (f"{schedule} schedule, "
+            + ("hip-graph replay per Mult (RCCL exchange captured)" if graph else "direct stream launches per Mult"))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -494,7 +503,7 @@ def main():
                 "ndofs": int(ndofs_total),
                 "elements": int(fes.ne),
                 "order": order, "q1d": order + 2,
-                "launch": "stream launches" if world == 1 else "hip-graph replay per Mult (RCCL exchange captured)",
+                "launch": "stream launches" if world == 1 else par_launch_label(args.schedule, args.par_graph),
                 "kernel": ["auto", "tpe", "wpe", "unfused", "line"][timed_forms[0].info()["kernel"]],
                 "qdata_layout": layout,
                 "qdata_bytes_stored": qbytes_total / world,

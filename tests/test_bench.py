@@ -26,6 +26,22 @@ def test_bench_help_lists_the_options():
         assert opt in out.stdout
 
 
+def test_par_launch_label_follows_the_graph_mode(monkeypatch):
+    """The N > 1 line names the launch form par_form.cpp's par_graph() picks (CPU, no GPU)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    monkeypatch.delenv("ECM2_PAR_GRAPH", raising=False)
+    assert "direct" in b.par_launch_label("serial", -1)
+    assert "graph" in b.par_launch_label("overlap", -1)
+    assert "graph" in b.par_launch_label("serial", 1) and "direct" in b.par_launch_label("overlap", 0)
+    monkeypatch.setenv("ECM2_PAR_GRAPH", "1")
+    assert "graph" in b.par_launch_label("serial", -1)
+    monkeypatch.setenv("ECM2_PAR_GRAPH", "0")
+    assert "direct" in b.par_launch_label("overlap", -1)
+
+
 SMALL = ["--workload", "c2", "--c2-n", "12", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--full-layout", "0"]
 
 

@@ -2,13 +2,16 @@
 // AssemblyLevel::PARTIAL over a z-slab partition, the RAPOperator Mult and an SDIRK step on
 // it) through the C ABI alone: N subdomains of a Cartesian mesh as an in-process loopback group
 // on one GPU (ecm2_par_group_*, the exchange as device copies that follow the same exchange
-// schedule the RCCL transport sends).  With one process per GPU the same code creates each
-// rank's form with an RCCL id (ecm2_rccl_unique_id on rank 0, broadcast) and uses
-// ecm2_par_form_mult / ecm2_operator_from_par_form instead of the group calls.
-// Checks, against the serial form on the whole mesh: the group Mult on the concatenated true
-// vectors (rank by rank) and two SDIRK33 steps.  Exit status 0 = pass.
+// schedule the RCCL transport sends).  `par_heat rccl ...` is the one-process-per-GPU form: each
+// process (RANK, WORLD_SIZE, LOCAL_RANK from the environment, as torchrun sets them) builds its
+// own rank's partition and form with an RCCL id (ecm2_rccl_unique_id on rank 0, handed to the
+// others through the file ECM2_ID_FILE names) and uses ecm2_par_form_mult /
+// ecm2_operator_from_par_form; PCG dots are summed over the ranks with ncclAllReduce.
+// Checks, against the serial form on the whole mesh: the Mult on the true dofs (rank by rank)
+// and two SDIRK33 steps.  Exit status 0 = pass.
 //
 // Usage: par_heat [subdomains = 4] [n = 12 elements per edge] [order = 2] [decomposition = 1 (OVERLAP), 0 RAP]
+//        RANK=r WORLD_SIZE=N ECM2_ID_FILE=path par_heat rccl [n] [order] [decomposition]
 #include "ecm2_pa.h"
 
 #include <hip/hip_runtime.h>
@@ -17,6 +20,10 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <chrono>
 #include <vector>
 
 #define CHECK(call)                                                                       \
@@ -60,9 +67,54 @@ struct Rank
    double *T = nullptr;  // local L-vector of the temperature [owned | ghost]
 };
 
+static int env_int(const char *name, int dflt)
+{
+   const char *v = std::getenv(name);
+   return v ? std::atoi(v) : dflt;
+}
+
+// one RCCL id per communicator (each par form holds its own): rank 0 makes kForms ids and
+// publishes them (write + rename); the others wait for the file
+constexpr int kForms = 3;
+static bool share_rccl_id(int rank, int world, unsigned char *id)
+{
+   if (rank == 0)
+   {
+      for (int k = 0; k < kForms; k++) { CHECK(ecm2_rccl_unique_id(id + 128 * k)); }
+   }
+   if (world == 1) { return true; }
+   const char *path = std::getenv("ECM2_ID_FILE");
+   if (!path)
+   {
+      std::fprintf(stderr, "WORLD_SIZE > 1 needs ECM2_ID_FILE (a fresh path all ranks can read)\n");
+      return false;
+   }
+   if (rank == 0)
+   {
+      const std::string tmp = std::string(path) + ".tmp";
+      FILE *f = std::fopen(tmp.c_str(), "wb");
+      if (!f || std::fwrite(id, 1, 128 * kForms, f) != 128 * kForms || std::fclose(f) != 0) { return false; }
+      return std::rename(tmp.c_str(), path) == 0;
+   }
+   for (int t = 0; t < 12000; t++)  // 120 s
+   {
+      if (FILE *f = std::fopen(path, "rb"))
+      {
+         const size_t got = std::fread(id, 1, 128 * kForms, f);
+         std::fclose(f);
+         if (got == 128 * kForms) { return true; }
+      }
+      std::this_thread::sleep_for(std::chrono::milliseconds(10));
+   }
+   return false;
+}
+
 int main(int argc, char **argv)
 {
-   const int N = argc > 1 ? std::atoi(argv[1]) : 4;
+   const bool rccl = argc > 1 && std::strcmp(argv[1], "rccl") == 0;
+   // argv[1] is the subdomain count or "rccl"; then n, order, decomposition in both forms
+   const int my_rank = rccl ? env_int("RANK", 0) : -1;
+   const int N = rccl ? env_int("WORLD_SIZE", 1) : (argc > 1 ? std::atoi(argv[1]) : 4);
    const int n = argc > 2 ? std::atoi(argv[2]) : 12;
    const int order = argc > 3 ? std::atoi(argv[3]) : 2;
    const int decomp = argc > 4 ? std::atoi(argv[4]) : ECM2_DECOMP_OVERLAP;
@@ -71,6 +123,16 @@ int main(int argc, char **argv)
    {
       std::fprintf(stderr, "no HIP device available (the PA path has no CPU fallback)\n");
       return 2;
+   }
+   unsigned char id[128 * kForms] = {};
+   if (rccl)
+   {
+      HIPCHECK(hipSetDevice(env_int("LOCAL_RANK", my_rank) % ecm2_device_count()));
+      if (!share_rccl_id(my_rank, N, id))
+      {
+         std::fprintf(stderr, "rank %d: no RCCL id\n", my_rank);
+         return 2;
+      }
    }
    ecm2_mesh *mesh = nullptr;
    CHECK(ecm2_mesh_cartesian(n, n, n, 1.0, 1.0, 1.0, &mesh));
@@ -118,11 +180,13 @@ int main(int argc, char **argv)
    // the partition: z-slabs (Mesh::CartesianPartitioning along z), one local space per rank
    std::vector<int> elem_rank(ne);
    CHECK(ecm2_partition_slabs_z(mesh, N, elem_rank.data()));
-   std::vector<Rank> ranks(N);
+   // the group builds every rank's local space; an RCCL process only its own
+   std::vector<Rank> ranks(rccl ? 1 : N);
    int n_true = 0;
-   for (int r = 0; r < N; r++)
+   for (int k = 0; k < (int)ranks.size(); k++)
    {
-      Rank &R = ranks[r];
+      const int r = rccl ? my_rank : k;
+      Rank &R = ranks[k];
       CHECK(ecm2_partition_create_ex(fes, mesh, elem_rank.data(), r, N, decomp, &R.part));
       int ne_int = 0, n_nbrs = 0, n_send = 0;
       CHECK(ecm2_partition_info(R.part, &R.ne_local, &ne_int, &R.n_owned, &R.n_ghost, &n_nbrs, &n_send));
@@ -142,16 +206,20 @@ int main(int argc, char **argv)
       std::printf("rank %d: %d local elements (%d interior), %d owned + %d ghost dofs, %d neighbours\n", r,
                   R.ne_local, ne_int, R.n_owned, R.n_ghost, n_nbrs);
    }
-   if (n_true != ndofs)
+   if (!rccl && n_true != ndofs)
    {
       std::fprintf(stderr, "owned dofs %d != %d\n", n_true, ndofs);
       return 1;
    }
+   const int NL = (int)ranks.size();
+   int next_id = 0;  // RCCL: the next unused communicator id
    auto par_forms = [&](double alpha, double kscale) {
-      std::vector<ecm2_par_form *> fs(N);
-      for (int r = 0; r < N; r++)
+      unsigned char *fid = rccl ? id + 128 * next_id++ : nullptr;
+      if (next_id > kForms) { std::fprintf(stderr, "out of RCCL ids\n"); std::exit(2); }
+      std::vector<ecm2_par_form *> fs(NL);
+      for (int r = 0; r < NL; r++)
       {
-         CHECK(ecm2_par_form_create(ranks[r].part, ranks[r].enodes.data(), 0, nullptr, &fs[r]));
+         CHECK(ecm2_par_form_create(ranks[r].part, ranks[r].enodes.data(), 0, fid, &fs[r]));
          if (alpha != 0.0)
          {
             CHECK(ecm2_par_form_add_integrator(fs[r], ECM2_MASS, ECM2_COEFF_CONSTANT, &alpha, nullptr));
@@ -190,15 +258,16 @@ int main(int argc, char **argv)
       const std::vector<double> ys = host_copy(y, ndofs);
       std::vector<ecm2_par_form *> fs = par_forms(1.0, 1.0);
       const std::vector<double> xt = to_true(xg);
-      std::vector<const double *> xr(N);
-      std::vector<double *> yr(N);
+      std::vector<const double *> xr(NL);
+      std::vector<double *> yr(NL);
       double *xtd = device_copy(xt), *ytd = nullptr;
-      HIPCHECK(hipMalloc(&ytd, n_true * sizeof(double)));
-      for (int r = 0; r < N; r++) { xr[r] = xtd + ranks[r].offset; yr[r] = ytd + ranks[r].offset; }
-      CHECK(ecm2_par_group_mult(fs.data(), N, xr.data(), yr.data(), nullptr));
+      HIPCHECK(hipMalloc(&ytd, std::max(1, n_true) * sizeof(double)));
+      for (int r = 0; r < NL; r++) { xr[r] = xtd + ranks[r].offset; yr[r] = ytd + ranks[r].offset; }
+      if (rccl) { CHECK(ecm2_par_form_mult(fs[0], xtd, ytd, nullptr)); }  // collective over the ranks
+      else { CHECK(ecm2_par_group_mult(fs.data(), N, xr.data(), yr.data(), nullptr)); }
       const double e = rel_diff(host_copy(ytd, n_true), ys);
-      std::printf("group Mult vs serial: max rel diff %.3e (%s decomposition, %d subdomains)\n", e,
-                  decomp == ECM2_DECOMP_OVERLAP ? "OVERLAP" : "RAP", N);
+      std::printf("%s Mult vs serial: max rel diff %.3e (%s decomposition, %d subdomains)\n",
+                  rccl ? "RCCL rank" : "group", e, decomp == ECM2_DECOMP_OVERLAP ? "OVERLAP" : "RAP", N);
       pass &= e < 1e-12;
       for (ecm2_par_form *f : fs) { ecm2_par_form_destroy(f); }
       (void)hipFree(ytd);
@@ -220,8 +289,16 @@ int main(int argc, char **argv)
       int *ess_d = device_copy(ess);
       std::vector<ecm2_par_form *> Kp = par_forms(0.0, 0.5), Tp = par_forms(1.0, c * dt * 0.5);
       ecm2_operator *Kg = nullptr, *Tgop = nullptr;
-      CHECK(ecm2_operator_from_par_group(Kp.data(), N, &Kg));
-      CHECK(ecm2_operator_from_par_group(Tp.data(), N, &Tgop));
+      if (rccl)
+      {
+         CHECK(ecm2_operator_from_par_form(Kp[0], &Kg));
+         CHECK(ecm2_operator_from_par_form(Tp[0], &Tgop));
+      }
+      else
+      {
+         CHECK(ecm2_operator_from_par_group(Kp.data(), N, &Kg));
+         CHECK(ecm2_operator_from_par_group(Tp.data(), N, &Tgop));
+      }
       int gsize = 0;
       CHECK(ecm2_operator_size(Kg, &gsize));
       pass &= gsize == n_true;
@@ -253,6 +330,7 @@ int main(int argc, char **argv)
       ecm2_pa_form_destroy(Ts);
       ecm2_pa_form_destroy(Ks);
    }
+   if (rccl) { std::printf("rank %d of %d: ", my_rank, N); }
    std::printf("%s\n", pass ? "PASS" : "FAIL");
 
    for (Rank &R : ranks)

@@ -62,3 +62,18 @@ def test_example_par_heat_on_gpu(args):
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.rstrip().endswith("PASS")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("decomp", ["1", "0"])
+def test_example_par_heat_rccl_one_rank(decomp):
+    """The one-process-per-GPU flow (RCCL id, ecm2_par_form_mult, RCCL-summed PCG dots) with one
+    rank on the box's GPU; WORLD_SIZE > 1 needs a node with that many GPUs."""
+    if not os.access(PAR_BINARY, os.X_OK):
+        _build()
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([PAR_BINARY, "rccl", "8", "2", decomp], cwd=ROOT, capture_output=True, text=True,
+                       timeout=120, env=env)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.rstrip().endswith("rank 0 of 1: PASS")

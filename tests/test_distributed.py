@@ -163,6 +163,93 @@ def test_gloo_exchange_matches_serial(tmp_path, kind, nranks, decomp):
     assert float(np.load(out)[0]) <= RTOL
 
 
+def _schedule_buffers(part, x_true):
+    """The five exchange buffers of one rank (par_form.cpp xfer_ptr): x_true, the packed send
+    buffer (x_true[send_idx], what kern::gather_idx writes), the ghost blocks of x and y and the
+    P^T receive buffer, as numpy arrays a schedule row slices."""
+    return {E.Partition.XBUF_X_TRUE: x_true,
+            E.Partition.XBUF_SENDBUF: x_true[part.send_idx].copy(),
+            E.Partition.XBUF_XGHOST: np.full(part.n_ghost, np.nan),
+            E.Partition.XBUF_YGHOST: np.zeros(part.n_ghost),
+            E.Partition.XBUF_RECVBUF: np.full(part.send_idx.size, np.nan)}
+
+
+def _run_schedule(rows, bufs, tag):
+    """Issue one exchange exactly as ParPAForm::rccl_exchange does (par_form.cpp:273-286): every
+    row of ecm2_partition_exchange_schedule is one send or receive of `count` doubles at
+    `offset` of buffer `buf`, to / from `peer`, all posted before any completes (the RCCL group)."""
+    import torch
+    import torch.distributed as dist
+    reqs, landed = [], []
+    for peer, send, buf, off, cnt in (tuple(int(v) for v in row) for row in rows):
+        if send:
+            reqs.append(dist.isend(torch.from_numpy(bufs[buf][off: off + cnt].copy()), peer, tag=tag))
+        else:
+            t = torch.empty(cnt, dtype=torch.float64)
+            reqs.append(dist.irecv(t, peer, tag=tag))
+            landed.append((buf, off, t))
+    for q in reqs:
+        q.wait()
+    for buf, off, t in landed:
+        bufs[buf][off: off + t.numel()] = t.numpy()
+
+
+def _worker_schedule(rank, nranks, port, kind, result_path, decomp):
+    """One rank of the product's exchange schedule over gloo: the P rows fill the ghost block,
+    the oracle applies the local operator, [RAP: the P^T rows carry the ghost contributions into
+    the owners' receive buffers, added at send_idx (phase_finish)]."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=nranks)
+    try:
+        m = _mesh(kind)
+        order = 2
+        fes = E.H1Space(m, order)
+        er = _elem_rank(m, kind, nranks)
+        part = E.Partition(fes, er, rank, nranks, decomposition=decomp)
+        q1d = O.default_q1d(order)
+        en = m.element_nodes()[part.elems]
+        c = coeff_function(O.quad_points(en, q1d))
+        nl = part.n_owned + part.n_ghost
+        op = O.OracleOperator(en, part.gather_map, nl, order, alpha=c, beta=c)
+        xg = np.random.default_rng(0).uniform(-1, 1, fes.ndofs)
+        bufs = _schedule_buffers(part, xg[part.owned_global].copy())
+        _run_schedule(part.exchange_schedule(False), bufs, tag=41822)
+        assert not np.isnan(bufs[E.Partition.XBUF_XGHOST]).any(), "a ghost was not received"
+        yl = op.mult(np.concatenate([bufs[E.Partition.XBUF_X_TRUE], bufs[E.Partition.XBUF_XGHOST]]))
+        y_true = yl[: part.n_owned].copy()
+        if decomp == "rap":
+            bufs[E.Partition.XBUF_YGHOST][:] = yl[part.n_owned:]
+            _run_schedule(part.exchange_schedule(True), bufs, tag=41823)
+            rb = bufs[E.Partition.XBUF_RECVBUF]
+            assert not np.isnan(rb).any(), "a P^T contribution was not received"
+            np.add.at(y_true, part.send_idx, rb)
+        gathered = [None] * nranks
+        dist.all_gather_object(gathered, (part.owned_global.tolist(), y_true.tolist()))
+        if rank == 0:
+            y = np.zeros(fes.ndofs)
+            for ids, vals in gathered:
+                y[np.array(ids, dtype=np.int64)] = vals
+            cg = coeff_function(O.quad_points(m.element_nodes(), q1d))
+            ref = O.OracleOperator(m.element_nodes(), fes.gather_map(), fes.ndofs, order, alpha=cg, beta=cg).mult(xg)
+            np.save(result_path, np.array([relerr(y, ref)]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind,nranks", [("cart", 2), ("cart", 3), ("fichera", 2), ("fichera", 3)])
+@pytest.mark.parametrize("decomp", ["rap", "overlap"])
+def test_gloo_schedule_rows_match_serial(tmp_path, kind, nranks, decomp):
+    """The exact rows the RCCL transport issues (ecm2_partition_exchange_schedule) moved between
+    processes: slab (cart: sends straight from x_true) and random (fichera: packed sends)
+    partitions, both decompositions; the assembled y equals the serial oracle."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "err.npy")
+    mp.spawn(_worker_schedule, args=(nranks, _free_port(), kind, out, decomp), nprocs=nranks, join=True)
+    assert float(np.load(out)[0]) <= RTOL
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,nranks,order", [("cart", 2, 2), ("cart", 3, 1), ("fichera", 3, 2),
                                                ("fichera", 4, 3), ("cart", 4, 2), ("cart", 2, 4),

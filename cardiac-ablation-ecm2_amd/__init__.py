@@ -556,6 +556,8 @@ _PAR_SIGS = {
                                                         ctypes.POINTER(ctypes.c_int)]),
     "ecm2_par_group_mult": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_void_p]),
+    "ecm2_par_group_mult_rccl": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_void_p]),
     "ecm2_par_group_mult_member": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                                   ctypes.c_void_p, ctypes.c_void_p]),
     "ecm2_par_form_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
@@ -604,20 +606,20 @@ def partition_slabs_z(mesh: Mesh, nranks: int) -> np.ndarray:
 
 
 def partition_boxes(mesh: Mesh, parts) -> np.ndarray:
-    """Mesh::CartesianPartitioning(nxyz) (mesh.cpp:8966) for a box-shaped mesh: element ->
-    rank = i_x + px (i_y + py i_z), i_d = floor(centroid_d / extent_d * p_d), parts = (px, py, pz)."""
-    px, py, pz = (int(v) for v in parts)
-    c = mesh.element_nodes().mean(axis=2)  # [e][3]
-    lo, hi = c.min(axis=0), c.max(axis=0)
+    """Mesh::CartesianPartitioning(nxyz) (mesh.cpp:8966-9003): element -> rank = i_x + px (i_y +
+    py i_z), i_d = clip(floor(n_d (c_d - vmin_d) / (vmax_d - vmin_d)), 0, n_d - 1) with c the
+    element centre and [vmin, vmax] the vertices' bounding box; parts = (px, py, pz).  A centre
+    that lies exactly on a box boundary (ties of the exact arithmetic, e.g. 10 elements split 4
+    ways) goes to the upper box, as the exact formula says (a relative 1e-12 nudge absorbs the
+    rounding of the centroid)."""
+    n = np.array([int(v) for v in parts])
+    c = mesh.element_nodes().mean(axis=2)  # [e][3] centres (the trilinear map at the reference centre)
+    V = mesh.vertices()
+    lo, hi = V.min(axis=0), V.max(axis=0)
     span = np.where(hi > lo, hi - lo, 1.0)
-    n = np.array([px, py, pz])
-    # centroids of an n-element row sit at (i + 1/2) h: map them to [0, n) exactly
-    idx = []
-    for d in range(3):
-        m = np.unique(np.round(c[:, d], 12)).size  # elements along d
-        i = np.floor((c[:, d] - lo[d]) / span[d] * (m - 1) + 0.5).astype(np.int64)  # element index along d
-        idx.append(np.minimum(i * n[d] // m, n[d] - 1))
-    return np.ascontiguousarray(idx[0] + px * (idx[1] + py * idx[2]), np.int32)
+    t = n * (c - lo) / span
+    idx = np.clip(np.floor(t + 1e-12 * np.maximum(1.0, np.abs(t))), 0, n - 1).astype(np.int64)
+    return np.ascontiguousarray(idx[:, 0] + n[0] * (idx[:, 1] + n[1] * idx[:, 2]), np.int32)
 
 
 def quadrature_points_subset(mesh: Mesh, q1d: int, elems: np.ndarray) -> np.ndarray:
@@ -795,6 +797,15 @@ class ParGroup:
         ya = (ctypes.c_void_p * n)(*[_dev_ptr(y).value for y in ys])
         _check(_par_lib().ecm2_par_group_mult(ctypes.cast(fa, ctypes.c_void_p), n, ctypes.cast(xa, ctypes.c_void_p),
                                               ctypes.cast(ya, ctypes.c_void_p), _stream(stream)))
+
+    def MultRccl(self, xs, ys, stream=None):
+        """Mult with every exchange row sent through RCCL (a one-rank communicator to itself)."""
+        n = len(self.forms)
+        fa = (ctypes.c_void_p * n)(*[f._h.value for f in self.forms])
+        xa = (ctypes.c_void_p * n)(*[_dev_ptr(x).value for x in xs])
+        ya = (ctypes.c_void_p * n)(*[_dev_ptr(y).value for y in ys])
+        _check(_par_lib().ecm2_par_group_mult_rccl(ctypes.cast(fa, ctypes.c_void_p), n, ctypes.cast(xa, ctypes.c_void_p),
+                                                   ctypes.cast(ya, ctypes.c_void_p), _stream(stream)))
 
     def MultMember(self, r, xs, ys, stream=None):
         """Member r's rows alone (y[r] only), on the streams and in the stage order one RCCL rank

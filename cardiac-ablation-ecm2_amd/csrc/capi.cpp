@@ -706,6 +706,25 @@ int ecm2_par_group_mult(ecm2_par_form *const *forms, int n, const double *const 
    });
 }
 
+int ecm2_par_group_mult_rccl(ecm2_par_form *const *forms, int n, const double *const *x_true,
+                             double *const *y_true, void *stream)
+{
+   return guard([&] {
+      NEED(forms); NEED(x_true); NEED(y_true);
+      std::vector<ecm2::ParPAForm *> fs;
+      std::vector<const double *> xs;
+      std::vector<double *> ys;
+      for (int i = 0; i < n; i++)
+      {
+         NEED(forms[i]);
+         fs.push_back(forms[i]->f);
+         xs.push_back(x_true[i]);
+         ys.push_back(y_true[i]);
+      }
+      ecm2::par_group_mult(fs, xs, ys, S(stream), true);
+   });
+}
+
 int ecm2_par_group_mult_member(ecm2_par_form *const *forms, int n, int member, const double *const *x_true,
                                double *const *y_true, void *stream)
 {

@@ -558,7 +558,8 @@ void PAForm::assemble(hipStream_t s)
          int nreg = 0;
          for (int b = 0; b < nblk; b++)
          {
-            bool regular = (long)(b + 1) * 64 <= ne_;
+            // (blocks the latency kernel applies store [a][lane] slots: never regular)
+            bool regular = (long)(b + 1) * 64 <= ne_ && (latency_from_ < 0 || b < latency_from_);
             auto dv = [&](int l, int a) { return ent(b, l, a) & 0x3fffffff; };
             const int base = dv(0, 0), sx = dv(0, 1) - base, sy = dv(0, D_) - base, sz = dv(0, D_ * D_) - base;
             int mask = 0;

@@ -108,8 +108,10 @@ public:
 
    // y = A x (BilinearForm::Mult semantics: y overwritten).
    void mult(const double *x, double *y, hipStream_t s);
-   // y += a A x (Operator::AddMult, linalg/operator.hpp:87-92): Mult into a work vector, then
-   // one axpy.
+   // y += a A x (Operator::AddMult, linalg/operator.hpp:87-92): Mult into a form-owned work
+   // vector, then one axpy.  Like every call on a form (the reference's Mult reuses its
+   // localX / localY too, bilinearform_ext.hpp:75), AddMult is stream-serial per form: two calls
+   // on the same form must be ordered (same stream or an event), not run concurrently.
    void add_mult(const double *x, double *y, double a, hipStream_t s);
    bool assembled() const { return assembled_; }
    // Incremented by every assemble(): whoever caches device pointers or launches of this form

@@ -446,11 +446,15 @@ void group_exchange(std::vector<ParPAForm *> &forms, const std::vector<const dou
    }
 }
 // The loopback transport of one exchange on one stream (the serial schedule): every receive
-// copies the peer's matching send.
+// copies the peer's matching send.  comm (a one-rank RCCL communicator): every (send row,
+// receive row) pair is instead one ncclSend + ncclRecv of the communicator to itself, all in one
+// group -- the rows, buffers and counts of ParPAForm::rccl_exchange through RCCL's own transfer
+// path (RCCL matches a group's self sends and receives in issue order).
 void group_copies(std::vector<ParPAForm *> &forms, const std::vector<const double *> &x, bool transpose,
-                  hipStream_t s, int only = -1)
+                  hipStream_t s, int only = -1, void *comm = nullptr)
 {
    const int n = (int)forms.size();
+   if (comm) { ECM2_NCCL(ncclGroupStart()); }
    for (int r = 0; r < n; r++)
    {
       if (only >= 0 && r != only) { continue; }
@@ -467,11 +471,31 @@ void group_copies(std::vector<ParPAForm *> &forms, const std::vector<const doubl
          }
          ECM2_VERIFY(m && m->count == t.count, ERR_INTERNAL,
                      "exchange schedules of ranks " << r << " and " << t.peer << " do not match");
-         ECM2_HIP(hipMemcpyAsync(f.xfer_ptr(t, x.empty() ? nullptr : x[r]),
-                                 o.xfer_ptr(*m, x.empty() ? nullptr : x[t.peer]), t.count * sizeof(double),
-                                 hipMemcpyDeviceToDevice, s));
+         double *dst = f.xfer_ptr(t, x.empty() ? nullptr : x[r]);
+         const double *src = o.xfer_ptr(*m, x.empty() ? nullptr : x[t.peer]);
+         if (comm)
+         {
+            ECM2_NCCL(ncclSend(src, t.count, ncclFloat64, 0, (ncclComm_t)comm, s));
+            ECM2_NCCL(ncclRecv(dst, t.count, ncclFloat64, 0, (ncclComm_t)comm, s));
+         }
+         else { ECM2_HIP(hipMemcpyAsync(dst, src, t.count * sizeof(double), hipMemcpyDeviceToDevice, s)); }
       }
    }
+   if (comm) { ECM2_NCCL(ncclGroupEnd()); }
+}
+
+// One-rank communicator of the RCCL-self group transport (created on first use, outside any
+// stream capture; lives for the process).
+void *self_comm()
+{
+   static ncclComm_t comm = [] {
+      ncclUniqueId id;
+      ECM2_NCCL(ncclGetUniqueId(&id));
+      ncclComm_t c;
+      ECM2_NCCL(ncclCommInitRank(&c, 1, id, 0));
+      return c;
+   }();
+   return comm;
 }
 } // namespace
 
@@ -528,7 +552,7 @@ void par_group_mult_member(std::vector<ParPAForm *> &forms, const std::vector<co
 }
 
 void par_group_mult(std::vector<ParPAForm *> &forms, const std::vector<const double *> &x,
-                    const std::vector<double *> &y, hipStream_t s)
+                    const std::vector<double *> &y, hipStream_t s, bool rccl_self)
 {
    const int n = (int)forms.size();
    ECM2_VERIFY((int)x.size() == n && (int)y.size() == n, ERR_ARG, "group size mismatch");
@@ -542,6 +566,9 @@ void par_group_mult(std::vector<ParPAForm *> &forms, const std::vector<const dou
    {
       ECM2_VERIFY(forms[r]->serial() == forms[0]->serial(), ERR_ARG, "loopback group: members use different schedules");
    }
+   ECM2_VERIFY(!rccl_self || forms.empty() || forms[0]->serial(), ERR_UNSUPPORTED,
+               "the RCCL-self group transport runs the serial schedule");
+   void *comm = rccl_self ? self_comm() : nullptr;
    if (!forms.empty() && forms[0]->serial())
    {
       // the serial schedule, stage-major on s: packs, the P copies, the applies, [RAP: P^T
@@ -554,9 +581,9 @@ void par_group_mult(std::vector<ParPAForm *> &forms, const std::vector<const dou
             kern::gather_idx((int)f.part().send_idx.size(), f.send_idx_data(), x[r], f.sendbuf_data(), s);
          }
       }
-      group_copies(forms, x, false, s);
+      group_copies(forms, x, false, s, -1, comm);
       for (int r = 0; r < n; r++) { forms[r]->stage_serial_apply(x[r], y[r], s); }
-      if (!forms[0]->part().overlap) { group_copies(forms, x, true, s); }
+      if (!forms[0]->part().overlap) { group_copies(forms, x, true, s, -1, comm); }
       for (int r = 0; r < n; r++)
       {
          forms[r]->local().finish_shared(0, forms[r]->local().n_shared_owned(), y[r], forms[r]->yghost(), s);

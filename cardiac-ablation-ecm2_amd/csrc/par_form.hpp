@@ -115,8 +115,11 @@ double rccl_p2p_selftest(bool graph, int n);
 // follow the members' exchange schedules (each receive copies the peer's matching send).
 // Exercises partition, schedule, split-vector kernels and interior/boundary ordering without
 // RCCL (which cannot put two ranks on one device).
+// rccl_self: the exchanges go through RCCL instead of device copies -- a one-rank communicator
+// sends each schedule row to itself and receives it into the peer's row (grouped ncclSend /
+// ncclRecv on s, capturable in a HIP graph); serial schedule only.
 void par_group_mult(std::vector<ParPAForm *> &forms, const std::vector<const double *> &x,
-                    const std::vector<double *> &y, hipStream_t s);
+                    const std::vector<double *> &y, hipStream_t s, bool rccl_self = false);
 void par_group_diagonal(std::vector<ParPAForm *> &forms, const std::vector<double *> &d, hipStream_t s);
 // One member's rows of the group operator, y[r] = (A x)_r: member r's stages alone, exactly as
 // one rank of the RCCL transport runs them (interior on s, exchange + boundary on r's comm

@@ -15,11 +15,10 @@ std::vector<int> partition_slabs_z(const HexMesh &m, int nranks)
    std::vector<int> er(m.ne);
    for (int e = 0; e < m.ne; e++)
    {
-      const int ez = e / (m.nx * m.ny);
-      // slab r = [floor(nz r / R), floor(nz (r+1) / R))
-      int r = 0;
-      while (r + 1 < nranks && (long)m.nz * (r + 1) / nranks <= ez) { r++; }
-      er[e] = r;
+      const long ez = e / (m.nx * m.ny);
+      // Mesh::CartesianPartitioning (mesh.cpp:8994) with nxyz = (1, 1, R) on the element centre
+      // z = (ez + 1/2) / nz of the box: r = floor(R (ez + 1/2) / nz), in exact integer arithmetic
+      er[e] = (int)std::min<long>(nranks - 1, (2 * ez + 1) * nranks / (2L * m.nz));
    }
    return er;
 }

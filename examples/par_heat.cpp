@@ -74,8 +74,21 @@ static int env_int(const char *name, int dflt)
 }
 
 // one RCCL id per communicator (each par form holds its own): rank 0 makes kForms ids and
-// publishes them (write + rename); the others wait for the file
-constexpr int kForms = 3;
+// publishes them with the job's nonce (write + rename); the others wait for a file carrying
+// their own nonce, so a file left over from an earlier job is never read as this job's ids.
+// The nonce is ECM2_JOB_ID, else the launcher's TORCHELASTIC_RUN_ID, else MASTER_ADDR:PORT.
+constexpr int kForms = 3, kNonce = 128;
+static std::string job_nonce()
+{
+   for (const char *k : {"ECM2_JOB_ID", "TORCHELASTIC_RUN_ID"})
+   {
+      const char *v = std::getenv(k);
+      if (v && *v) { return v; }
+   }
+   const char *a = std::getenv("MASTER_ADDR"), *p = std::getenv("MASTER_PORT");
+   return (a && p) ? std::string(a) + ":" + p : std::string();
+}
+
 static bool share_rccl_id(int rank, int world, unsigned char *id)
 {
    if (rank == 0)
@@ -84,25 +97,35 @@ static bool share_rccl_id(int rank, int world, unsigned char *id)
    }
    if (world == 1) { return true; }
    const char *path = std::getenv("ECM2_ID_FILE");
-   if (!path)
+   const std::string nonce = job_nonce();
+   if (!path || nonce.empty() || nonce.size() >= (size_t)kNonce)
    {
-      std::fprintf(stderr, "WORLD_SIZE > 1 needs ECM2_ID_FILE (a fresh path all ranks can read)\n");
+      std::fprintf(stderr, "WORLD_SIZE > 1 needs ECM2_ID_FILE (a path all ranks can read) and a job nonce "
+                           "(ECM2_JOB_ID, TORCHELASTIC_RUN_ID or MASTER_ADDR/MASTER_PORT)\n");
       return false;
    }
+   char tag[kNonce] = {};
+   std::memcpy(tag, nonce.data(), nonce.size());
    if (rank == 0)
    {
       const std::string tmp = std::string(path) + ".tmp";
       FILE *f = std::fopen(tmp.c_str(), "wb");
-      if (!f || std::fwrite(id, 1, 128 * kForms, f) != 128 * kForms || std::fclose(f) != 0) { return false; }
+      if (!f || std::fwrite(tag, 1, kNonce, f) != kNonce || std::fwrite(id, 1, 128 * kForms, f) != 128 * kForms ||
+          std::fclose(f) != 0)
+      {
+         return false;
+      }
       return std::rename(tmp.c_str(), path) == 0;
    }
    for (int t = 0; t < 12000; t++)  // 120 s
    {
       if (FILE *f = std::fopen(path, "rb"))
       {
-         const size_t got = std::fread(id, 1, 128 * kForms, f);
+         char got_tag[kNonce];
+         const size_t gt = std::fread(got_tag, 1, kNonce, f);
+         const size_t got = gt == kNonce ? std::fread(id, 1, 128 * kForms, f) : 0;
          std::fclose(f);
-         if (got == 128 * kForms) { return true; }
+         if (got == 128 * kForms && std::memcmp(got_tag, tag, kNonce) == 0) { return true; }  // else: stale
       }
       std::this_thread::sleep_for(std::chrono::milliseconds(10));
    }

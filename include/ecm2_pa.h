@@ -362,6 +362,13 @@ int ecm2_par_form_addressing_info(const ecm2_par_form *f, int *lattice, int *n_u
  * follow the members' exchange schedules). */
 int ecm2_par_group_mult(ecm2_par_form *const *forms, int n, const double *const *x_true,
                         double *const *y_true, void *stream);
+/* Transport test (no reference counterpart): ecm2_par_group_mult with every exchange row
+ * issued through RCCL -- a one-rank communicator (created on the first call, which must not be
+ * inside a stream capture) ncclSend's each peer's send row to itself and ncclRecv's it into
+ * the matching receive row, grouped, on `stream` (capturable).  Exercises the row buffers,
+ * offsets and counts of ecm2_par_form_mult's grouped exchange on one GPU.  Serial schedule. */
+int ecm2_par_group_mult_rccl(ecm2_par_form *const *forms, int n, const double *const *x_true,
+                             double *const *y_true, void *stream);
 /* One member's rows of the loopback group's operator (measurement of a rank's Mult on its own
  * GPU; no reference counterpart): y_true[member] = (A x)[member's true dofs], running exactly
  * the stages one RCCL rank runs (interior elements on `stream`, the P exchange -- here device

@@ -425,6 +425,62 @@ def test_gpu_rccl_single_rank_transport(order):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind,nranks", [("cart", 2), ("cart", 3), ("fichera", 3)])
+@pytest.mark.parametrize("decomp", ["rap", "overlap"])
+def test_gpu_rccl_rows_nonempty_schedule(kind, nranks, decomp):
+    """The distributed Mult's exchange rows through RCCL itself: every member's
+    schedule rows -- sends straight from x (slabs), from the pack buffer (fichera's random
+    partition), the P^T rows of RAP -- become grouped ncclSend/ncclRecv of a one-rank
+    communicator to itself; on the null stream and replayed from a captured HIP graph."""
+    import torch
+    m = _mesh(kind)
+    order = 2
+    fes = E.H1Space(m, order)
+    er = _elem_rank(m, kind, nranks)
+    q1d = O.default_q1d(order)
+    forms, xs, ys, parts = [], [], [], []
+    xg = np.random.default_rng(7).uniform(-1, 1, fes.ndofs)
+    nrows = 0
+    for r in range(nranks):
+        part = E.Partition(fes, er, r, nranks, decomposition=decomp)
+        nrows += len(part.exchange_schedule(False))
+        pf = E.ParBilinearForm(part)
+        P = E.quadrature_points_subset(m, q1d, part.elems)
+        c = torch.as_tensor(coeff_function(P).reshape(part.ne_local, -1)).cuda()
+        pf.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(c)))
+        pf.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(c.clone())))
+        pf.Assemble()
+        forms.append(pf)
+        parts.append(part)
+        xs.append(torch.as_tensor(xg[part.owned_global]).cuda())
+        ys.append(torch.full((part.n_owned,), float("nan"), dtype=torch.float64, device="cuda"))
+    assert nrows > 0
+    cg = coeff_function(O.quad_points(m.element_nodes(), q1d))
+    ref = O.OracleOperator(m.element_nodes(), fes.gather_map(), fes.ndofs, order, alpha=cg, beta=cg).mult(xg)
+
+    def check():
+        y = np.zeros(fes.ndofs)
+        for part, yt in zip(parts, ys):
+            y[part.owned_global] = yt.cpu().numpy()
+        assert relerr(y, ref) <= RTOL
+
+    group = E.ParGroup(forms)
+    group.MultRccl(xs, ys)  # null stream (creates the communicator outside any capture)
+    torch.cuda.synchronize()
+    check()
+    for yt in ys:
+        yt.fill_(float("nan"))
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=torch.cuda.Stream()):
+        group.MultRccl(xs, ys)
+    g.replay()
+    g.replay()
+    torch.cuda.synchronize()
+    check()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("graph", [False, True])
 def test_gpu_rccl_p2p_graph_capture(graph):
     """RCCL point-to-point (grouped ncclSend/ncclRecv, here a one-rank communicator talking to
@@ -493,3 +549,18 @@ def test_partition_boxes():
         inside = np.all((c >= lo - 1e-12) & (c <= hi + 1e-12), axis=1)
         assert np.array_equal(inside, r == k)
     assert np.array_equal(E.partition_boxes(m, (1, 1, 4)), E.partition_slabs_z(m, 4))
+
+
+def test_partition_boxes_uneven_counts():
+    """Counts that do not divide evenly follow the reference's floor(n (c - pmin) / (pmax - pmin))
+    (ADVICE r2): 10 elements split 4 ways -> element i in box floor(4 (i + 1/2) / 10); the z-slab
+    split of 13 layers into 3 uses the same rule."""
+    m = E.Mesh.MakeCartesian3D(10, 3, 13)
+    r = E.partition_boxes(m, (4, 1, 1))
+    ex = np.arange(m.GetNE()) % 10
+    assert np.array_equal(r, np.minimum(3, (2 * ex + 1) * 4 // 20))
+    assert r[2] == 1 and r[7] == 3
+    ez = np.arange(m.GetNE()) // 30
+    want = np.minimum(2, (2 * ez + 1) * 3 // 26)
+    assert np.array_equal(E.partition_slabs_z(m, 3), want)
+    assert np.array_equal(E.partition_boxes(m, (1, 1, 3)), want)

@@ -74,6 +74,10 @@ def load_library(path: str = LIB_PATH):
         "ecm2_mesh_set_vertices": (i32, [vp, vp]),
         "ecm2_mesh_get_elements": (i32, [vp, vp]),
         "ecm2_mesh_get_element_nodes": (i32, [vp, vp]),
+        "ecm2_mesh_get_attributes": (i32, [vp, vp]),
+        "ecm2_mesh_set_attributes": (i32, [vp, vp]),
+        "ecm2_pa_form_add_integrator_marked": (i32, [vp, i32, i32, vp, vp, vp, i32]),
+        "ecm2_pa_form_set_attributes": (i32, [vp, vp]),
         "ecm2_mesh_quadrature_points": (i32, [vp, i32, vp]),
         "ecm2_mesh_destroy": (None, [vp]),
         "ecm2_h1space_create": (i32, [vp, i32, i32, pp]),
@@ -222,6 +226,18 @@ class Mesh:
         out = np.empty((self.GetNE(), 8), np.int32)
         _check(_lib.ecm2_mesh_get_elements(self._h, _np_ptr(out)))
         return out
+
+    def GetAttributes(self) -> np.ndarray:
+        """Element attributes [ne] (Mesh::GetAttribute)."""
+        out = np.empty(self.GetNE(), np.int32)
+        _check(_lib.ecm2_mesh_get_attributes(self._h, _np_ptr(out)))
+        return out
+
+    def SetAttributes(self, attr):
+        """Mesh::SetAttribute for every element (then Mesh::SetAttributes)."""
+        a = np.ascontiguousarray(attr, np.int32)
+        assert a.shape == (self.GetNE(),)
+        _check(_lib.ecm2_mesh_set_attributes(self._h, _np_ptr(a)))
 
     def element_order(self, kind: int) -> np.ndarray:
         """0 native, 1 brick (Cartesian only), 2 Morton order of centroids."""
@@ -422,12 +438,23 @@ class BilinearForm:
         self._keep.append(J)
         _check(_lib.ecm2_pa_form_set_jacobians(self._h, _dev_ptr(J)))
 
-    def AddDomainIntegrator(self, integ):
+    def AddDomainIntegrator(self, integ, elem_marker=None):
+        """BilinearForm::AddDomainIntegrator(integ[, elem_marker]): with a marker (0 / 1 per
+        attribute) the integrator acts on the elements whose attribute a has elem_marker[a-1]."""
         kind, data, params = _integrator_args(integ.coeff, self._keep)
-        _check(_lib.ecm2_pa_form_add_integrator(self._h, integ.kind, kind, data, params))
+        if elem_marker is None:
+            _check(_lib.ecm2_pa_form_add_integrator(self._h, integ.kind, kind, data, params))
+        else:
+            mk = np.ascontiguousarray(elem_marker, np.int32)
+            _check(_lib.ecm2_pa_form_add_integrator_marked(self._h, integ.kind, kind, data, params, _np_ptr(mk),
+                                                           mk.size))
+            self._marked = True
         self._integs.append(integ)
 
     def Assemble(self, stream=None):
+        if getattr(self, "_marked", False):  # the mesh's current attributes, as the reference reads them
+            attr = np.ascontiguousarray(self.fes.mesh.GetAttributes())
+            _check(_lib.ecm2_pa_form_set_attributes(self._h, _np_ptr(attr)))
         _check(_lib.ecm2_pa_form_assemble(self._h, _stream(stream)))
 
     def ScatterInfo(self):
@@ -535,6 +562,9 @@ _PAR_SIGS = {
                                             ctypes.POINTER(ctypes.c_void_p)]),
     "ecm2_par_form_add_integrator": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                                     ctypes.c_void_p]),
+    "ecm2_par_form_add_integrator_marked": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "ecm2_par_form_set_attributes": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "ecm2_par_form_set_kernel": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ecm2_par_form_set_scatter": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ecm2_par_form_set_bricks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
@@ -730,11 +760,20 @@ class ParBilinearForm:
             _lib.ecm2_par_form_destroy(self._h)
             self._h = None
 
-    def AddDomainIntegrator(self, integ):
+    def AddDomainIntegrator(self, integ, elem_marker=None):
         kind, data, params = _integrator_args(integ.coeff, self._keep)
-        _check(_par_lib().ecm2_par_form_add_integrator(self._h, integ.kind, kind, data, params))
+        if elem_marker is None:
+            _check(_par_lib().ecm2_par_form_add_integrator(self._h, integ.kind, kind, data, params))
+        else:
+            mk = np.ascontiguousarray(elem_marker, np.int32)
+            _check(_par_lib().ecm2_par_form_add_integrator_marked(self._h, integ.kind, kind, data, params,
+                                                                  _np_ptr(mk), mk.size))
+            self._marked = True
 
     def Assemble(self, stream=None):
+        if getattr(self, "_marked", False):
+            attr = np.ascontiguousarray(self.part.fes.mesh.GetAttributes()[self.part.elems])
+            _check(_par_lib().ecm2_par_form_set_attributes(self._h, _np_ptr(attr)))
         _check(_par_lib().ecm2_par_form_assemble(self._h, _stream(stream)))
 
     def Mult(self, x, y, stream=None):

@@ -175,6 +175,23 @@ int ecm2_mesh_get_elements(const ecm2_mesh *m, int *out)
    });
 }
 
+int ecm2_mesh_get_attributes(const ecm2_mesh *m, int *out)
+{
+   return guard([&] {
+      NEED(m); NEED(out);
+      std::memcpy(out, m->m.attr.data(), m->m.attr.size() * sizeof(int));
+   });
+}
+
+int ecm2_mesh_set_attributes(ecm2_mesh *m, const int *in)
+{
+   return guard([&] {
+      NEED(m); NEED(in);
+      for (int e = 0; e < m->m.ne; e++) { ECM2_VERIFY(in[e] >= 1, ecm2::ERR_ARG, "element attributes are >= 1"); }
+      m->m.attr.assign(in, in + m->m.ne);
+   });
+}
+
 int ecm2_mesh_get_element_nodes(const ecm2_mesh *m, double *out)
 {
    return guard([&] {
@@ -327,6 +344,20 @@ int ecm2_pa_form_add_integrator(ecm2_pa_form *f, int integrator, int coeff_kind,
       NEED(f);
       f->f->add_integrator(integrator, make_coeff(coeff_kind, data, params));
    });
+}
+
+int ecm2_pa_form_add_integrator_marked(ecm2_pa_form *f, int integrator, int coeff_kind, const double *data,
+                                       const double *params, const int *marker, int n_marker)
+{
+   return guard([&] {
+      NEED(f); NEED(marker);
+      f->f->add_integrator(integrator, make_coeff(coeff_kind, data, params), marker, n_marker);
+   });
+}
+
+int ecm2_pa_form_set_attributes(ecm2_pa_form *f, const int *attr)
+{
+   return guard([&] { NEED(f); f->f->set_attributes(attr); });
 }
 
 int ecm2_pa_form_set_element_order(ecm2_pa_form *f, const int *perm)
@@ -602,6 +633,20 @@ int ecm2_par_form_add_integrator(ecm2_par_form *f, int integrator, int coeff_kin
       NEED(f);
       f->f->local().add_integrator(integrator, make_coeff(coeff_kind, data, params));
    });
+}
+
+int ecm2_par_form_add_integrator_marked(ecm2_par_form *f, int integrator, int coeff_kind, const double *data,
+                                        const double *params, const int *marker, int n_marker)
+{
+   return guard([&] {
+      NEED(f); NEED(marker);
+      f->f->local().add_integrator(integrator, make_coeff(coeff_kind, data, params), marker, n_marker);
+   });
+}
+
+int ecm2_par_form_set_attributes(ecm2_par_form *f, const int *attr_local)
+{
+   return guard([&] { NEED(f); f->f->local().set_attributes(attr_local); });
 }
 
 int ecm2_par_form_set_bricks(ecm2_par_form *f, int bz)

@@ -107,11 +107,16 @@ struct SetupCoef
    int is_const;
    double value;
    const double *quad;
+   const double *emask;  // element weights (1 / 0) of an attribute-marked integrator, or null
 };
 
-__device__ __forceinline__ double coef_at(const SetupCoef &c, size_t eq)
+// coefficient of caller element e at point eq = e nq + q; an attribute marker zeroes the
+// integrator on the elements it excludes (the effect of AddMultWithMarkers,
+// bilinearform_ext.cpp:753-774,807-847, folded into the quadrature data)
+__device__ __forceinline__ double coef_at(const SetupCoef &c, size_t eq, int e)
 {
-   return c.is_const ? c.value : c.quad[eq];
+   const double v = c.is_const ? c.value : c.quad[eq];
+   return c.emask ? v * c.emask[e] : v;
 }
 
 // Write D (6 symmetric entries) and mass value at one quadrature point (any layout).
@@ -138,7 +143,7 @@ __device__ __forceinline__ void write_qdata(const int *pos, int kind, int nq, in
       const double A31 = (J21 * J32) - (J31 * J22);
       const double A32 = (J31 * J12) - (J11 * J32);
       const double A33 = (J11 * J22) - (J12 * J21);
-      const double C = coef_at(cd, eq);
+      const double C = coef_at(cd, eq, e);
       qd_diff[qidx_diff(pos, kind, nq, e, 0, q)] = w_detJ * (C * A11 * A11 + C * A12 * A12 + C * A13 * A13);
       qd_diff[qidx_diff(pos, kind, nq, e, 1, q)] = w_detJ * (C * A11 * A21 + C * A12 * A22 + C * A13 * A23);
       qd_diff[qidx_diff(pos, kind, nq, e, 2, q)] = w_detJ * (C * A11 * A31 + C * A12 * A32 + C * A13 * A33);
@@ -148,7 +153,7 @@ __device__ __forceinline__ void write_qdata(const int *pos, int kind, int nq, in
    }
    if (cm.has)
    {
-      qd_mass[qidx_mass(pos, kind, nq, e, q)] = w * coef_at(cm, eq) * detJ;
+      qd_mass[qidx_mass(pos, kind, nq, e, q)] = w * coef_at(cm, eq, e) * detJ;
    }
 }
 
@@ -227,7 +232,7 @@ k_setup_nodes_t(const int *__restrict__ perm, int ne, const double *__restrict__
       const double A31 = (J21 * J32) - (J31 * J22);
       const double A32 = (J31 * J12) - (J11 * J32);
       const double A33 = (J11 * J22) - (J12 * J21);
-      const double C = coef_at(cd, eq);
+      const double C = coef_at(cd, eq, e);
       v2d p0, p1, p2;
       p0.x = w_detJ * (C * A11 * A11 + C * A12 * A12 + C * A13 * A13);
       p0.y = w_detJ * (C * A11 * A21 + C * A12 * A22 + C * A13 * A23);
@@ -242,7 +247,7 @@ k_setup_nodes_t(const int *__restrict__ perm, int ne, const double *__restrict__
    }
    if (cm.has)
    {
-      qd_mass[((size_t)blk * ((NQ + 1) / 2) + (q >> 1)) * 128 + lane * 2 + (q & 1)] = w * coef_at(cm, eq) * detJ;
+      qd_mass[((size_t)blk * ((NQ + 1) / 2) + (q >> 1)) * 128 + lane * 2 + (q & 1)] = w * coef_at(cm, eq, e) * detJ;
    }
 }
 
@@ -342,8 +347,8 @@ k_setup_affine(const int *__restrict__ perm, int ne, const double *__restrict__ 
    const size_t eq = (size_t)e * NQ + q;
    const double w = W[q];
    v2d pr;
-   pr.x = w * coef_at(cd, eq);
-   pr.y = w * coef_at(cm, eq) * detJ;
+   pr.x = w * coef_at(cd, eq, e);
+   pr.y = w * coef_at(cm, eq, e) * detJ;
    if (BLOCKED) { reinterpret_cast<v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane] = pr; }
    else { reinterpret_cast<v2d *>(qd_pair)[(size_t)e * NQ + q] = pr; }
    if (q == 0)
@@ -388,6 +393,7 @@ SetupCoef make_setup_coef(const CoeffDesc *c, const double *q)
    s.is_const = (c->kind == COEFF_CONSTANT);
    s.value = c->value;
    s.quad = q;
+   s.emask = c->emask;
    return s;
 }
 

@@ -82,6 +82,7 @@ struct CoeffDesc
    const double *lvec = nullptr; // device L-vector of T
    double scale = 1.0, slope = 0.0, t_ref = 0.0;  // GRIDFUNC_AFFINE
    double p[6] = {0, 0, 0, 0, 0, 0};              // GRIDFUNC_PERFUSION
+   const double *emask = nullptr; // device [ne] element weights of an attribute-marked integrator (form-owned)
    bool gridfunc() const { return kind == COEFF_GRIDFUNC_AFFINE || kind == COEFF_GRIDFUNC_PERFUSION; }
 };
 

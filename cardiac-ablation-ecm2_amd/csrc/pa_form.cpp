@@ -134,8 +134,21 @@ void PAForm::set_line_bricks(int bz)
    assembled_ = false;
 }
 
-void PAForm::add_integrator(int kind, const CoeffDesc &c)
+void PAForm::set_attributes(const int *attr_host)
 {
+   ECM2_VERIFY(ne_ == 0 || attr_host, ERR_ARG, "null attribute array");
+   attr_.assign(attr_host, attr_host + ne_);
+   assembled_ = false;
+}
+
+void PAForm::add_integrator(int kind, const CoeffDesc &c, const int *marker, int n_marker)
+{
+   ECM2_VERIFY(!marker || n_marker >= 0, ERR_ARG, "negative marker size");
+   if (kind == INTEG_MASS || kind == INTEG_DIFFUSION)
+   {
+      marked_[kind] = marker != nullptr;
+      marker_[kind].assign(marker, marker ? marker + n_marker : marker);
+   }
    ECM2_VERIFY(kind == INTEG_MASS || kind == INTEG_DIFFUSION, ERR_ARG, "unknown integrator " << kind);
    ECM2_VERIFY(c.kind == COEFF_CONSTANT || c.kind == COEFF_QUAD || c.gridfunc(),
                ERR_ARG, "unknown coefficient kind " << c.kind);
@@ -838,6 +851,29 @@ void PAForm::assemble(hipStream_t s)
          const size_t per = qd_mass_.size() / nb;
          ECM2_HIP(hipMemsetAsync(qd_mass_.data() + (nb - 1) * per, 0, per * sizeof(double), s));
       }
+   }
+
+   // Attribute markers: per marked integrator, element weights 1 (marker[attr - 1] != 0) or 0,
+   // applied to its coefficient at setup (the reference masks the integrator's E-vector output,
+   // AddWithMarkers_, bilinearform_ext.cpp:753-774: the same operator)
+   for (int k = 0; k < 2; k++)
+   {
+      CoeffDesc &c = k == INTEG_MASS ? cmass_ : cdiff_;
+      c.emask = nullptr;
+      if (!marked_[k] || !(k == INTEG_MASS ? have_mass_ : have_diff_)) { continue; }
+      ECM2_VERIFY((int)attr_.size() == ne_, ERR_STATE, "a marked integrator needs the element attributes "
+                                                       "(ecm2_pa_form_set_attributes)");
+      std::vector<double> w(std::max(1, ne_), 0.0);
+      for (int e = 0; e < ne_; e++)
+      {
+         const int a = attr_[e];
+         ECM2_VERIFY(a <= (int)marker_[k].size(), ERR_ARG, "element " << e << " has attribute " << a
+                                                            << " beyond the marker's " << marker_[k].size() << " entries");
+         w[e] = (a > 0 && marker_[k][a - 1] != 0) ? 1.0 : 0.0;
+      }
+      emask_[k].upload(w, s);
+      ECM2_HIP(hipStreamSynchronize(s));  // w is a host temporary
+      c.emask = emask_[k].data();
    }
 
    // Coefficient values at quadrature points (CoefficientVector::Project).

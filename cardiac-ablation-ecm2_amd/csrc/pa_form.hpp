@@ -96,7 +96,13 @@ public:
    }
    int n_units() const { return resolved_mode_ == KERNEL_TPE ? layout_.nblk() : n_bricks_; }
    int brick_bz() const { return brick_bz_; }
-   void add_integrator(int kind, const CoeffDesc &c);
+   // BilinearForm::AddDomainIntegrator(integ[, elem_marker]) (bilinearform.cpp:231-242): with a
+   // marker (host marker[n_marker], 0 / 1 per attribute), the integrator acts on the elements
+   // whose attribute a has a > 0 and marker[a - 1] != 0 only (AddMultWithMarkers,
+   // bilinearform_ext.cpp:753-774,807-847); the attributes come from set_attributes.
+   void add_integrator(int kind, const CoeffDesc &c, const int *marker = nullptr, int n_marker = 0);
+   // element attributes (host [ne], caller element order), as Mesh::GetAttribute
+   void set_attributes(const int *attr_host);
    void set_kernel(int mode);
    void set_scatter(int mode);
    int scatter() const { return scatter_; }
@@ -185,6 +191,10 @@ private:
    DeviceArray<double> ywork_;      // add_mult
    bool have_mass_ = false, have_diff_ = false;
    CoeffDesc cmass_, cdiff_;
+   std::vector<int> attr_;               // element attributes (set_attributes)
+   std::vector<int> marker_[2];          // per integrator kind: attribute marker (empty: none)
+   bool marked_[2] = {false, false};
+   DeviceArray<double> emask_[2];        // per integrator kind: element weights [ne] (marked only)
 
    std::vector<int> gmap_host_;
    DeviceArray<int> gmap_;          // native [e][nd]

@@ -86,6 +86,10 @@ int ecm2_mesh_info(const ecm2_mesh *m, int *nv, int *ne);
 int ecm2_mesh_get_vertices(const ecm2_mesh *m, double *out /* host [nv][3] */);
 int ecm2_mesh_set_vertices(ecm2_mesh *m, const double *in /* host [nv][3] */);
 int ecm2_mesh_get_elements(const ecm2_mesh *m, int *out /* host [ne][8], native order */);
+/* Element attributes (Mesh::GetAttribute / SetAttribute + SetAttributes, mesh.hpp), host [ne],
+ * every attribute >= 1. */
+int ecm2_mesh_get_attributes(const ecm2_mesh *m, int *out);
+int ecm2_mesh_set_attributes(ecm2_mesh *m, const int *in);
 /* Lexicographic corner coordinates, host out[ne][3][8]. */
 int ecm2_mesh_get_element_nodes(const ecm2_mesh *m, double *out);
 /* Physical coordinates of the Gauss-Legendre quadrature points of every element, host
@@ -152,6 +156,16 @@ int ecm2_pa_form_set_geometry_compression(ecm2_pa_form *f, int on);
  * params[0..2] = (scale, slope, t_ref).  Device arrays must stay valid until assemble. */
 int ecm2_pa_form_add_integrator(ecm2_pa_form *f, int integrator, int coeff_kind,
                                 const double *data, const double *params);
+/* BilinearForm::AddDomainIntegrator(integ, elem_marker) (bilinearform.cpp:237-242): as
+ * ecm2_pa_form_add_integrator, restricted to the elements whose attribute a has
+ * marker[a - 1] != 0 (host marker[n_marker]; the reference's PABilinearFormExtension::
+ * AddMultWithMarkers, bilinearform_ext.cpp:753-774,807-847, masks the integrator's E-vector
+ * output; here its quadrature data is zeroed on the excluded elements at assemble: the same
+ * operator, no extra pass per Mult).  Needs ecm2_pa_form_set_attributes before assemble. */
+int ecm2_pa_form_add_integrator_marked(ecm2_pa_form *f, int integrator, int coeff_kind, const double *data,
+                                       const double *params, const int *marker, int n_marker);
+/* Element attributes of the form's elements (the mesh's, host [ne], caller element order). */
+int ecm2_pa_form_set_attributes(ecm2_pa_form *f, const int *attr);
 int ecm2_pa_form_set_kernel(ecm2_pa_form *f, int kernel);
 /* Scatter of the fused thread-per-element kernel (no reference counterpart: the
  * reference's ElementRestriction::MultTranspose, restriction.cpp:146-186, is the
@@ -328,6 +342,11 @@ int ecm2_par_form_create(const ecm2_partition *p, const double *enodes_local, in
  * element order; GRIDFUNC_AFFINE -> device local L-vector [n_owned + n_ghost]. */
 int ecm2_par_form_add_integrator(ecm2_par_form *f, int integrator, int coeff_kind,
                                  const double *data, const double *params);
+/* As ecm2_pa_form_add_integrator_marked / ecm2_pa_form_set_attributes on the local elements
+ * (attributes host [ne_local], the partition's local element order). */
+int ecm2_par_form_add_integrator_marked(ecm2_par_form *f, int integrator, int coeff_kind, const double *data,
+                                        const double *params, const int *marker, int n_marker);
+int ecm2_par_form_set_attributes(ecm2_par_form *f, const int *attr_local);
 /* As ecm2_pa_form_set_kernel (fused kernels only). */
 int ecm2_par_form_set_kernel(ecm2_par_form *f, int kernel);
 /* Brick mode of the local form (see ecm2_pa_form_set_bricks). */

@@ -283,6 +283,26 @@ class OracleOperator:
                           _p(self._xe), _p(self._ye))
         return y
 
+    def mult_markers(self, x, attr, mass_marker=None, diff_marker=None):
+        """MultInternal with attribute markers (bilinearform_ext.cpp:527-560 + AddMultWithMarkers
+        :807-847, AddWithMarkers_ :753-774): each integrator's AddMultPA into a zeroed E-vector,
+        added element by element where attr > 0 and marker[attr - 1] != 0 (no marker: all)."""
+        attr = np.asarray(attr)
+        xe = restriction_mult(self.gm, x)
+        ye = np.zeros_like(xe)
+        for marker, app in ((mass_marker, self.M is not None and (lambda v: mass_apply(self.B, self.M, v))),
+                            (diff_marker, self.D is not None and (lambda v: diffusion_apply(self.B, self.G, self.D, v)))):
+            if not app:
+                continue
+            tmp = app(xe)
+            if marker is None:
+                ye += tmp
+                continue
+            mk = np.asarray(marker)
+            keep = np.array([a > 0 and mk[a - 1] != 0 for a in attr])
+            ye[keep] += tmp[keep]
+        return restriction_mult_transpose(self.off, self.idx, ye)
+
     def fa_mult(self, x, with_diag=False):
         """Legacy element-matrix assembly path (independent of sum factorisation)."""
         y = np.empty(self.ndofs)

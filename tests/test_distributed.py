@@ -564,3 +564,39 @@ def test_partition_boxes_uneven_counts():
     want = np.minimum(2, (2 * ez + 1) * 3 // 26)
     assert np.array_equal(E.partition_slabs_z(m, 3), want)
     assert np.array_equal(E.partition_boxes(m, (1, 1, 3)), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("decomp", ["rap", "overlap"])
+def test_gpu_loopback_group_attribute_markers(decomp):
+    """Marked integrators on the distributed form (ParBilinearForm::AddDomainIntegrator(integ,
+    marker) on each rank's local elements) give the serial masked operator."""
+    import torch
+    m = _mesh("fichera")
+    m.SetAttributes(1 + np.arange(m.GetNE()) % 2)
+    attr = m.GetAttributes()
+    order, nranks = 2, 3
+    fes = E.H1Space(m, order)
+    er = _elem_rank(m, "fichera", nranks)
+    q1d = O.default_q1d(order)
+    forms, xs, ys, parts = [], [], [], []
+    xg = np.random.default_rng(9).uniform(-1, 1, fes.ndofs)
+    for r in range(nranks):
+        part = E.Partition(fes, er, r, nranks, decomposition=decomp)
+        pf = E.ParBilinearForm(part)
+        c = torch.as_tensor(coeff_function(E.quadrature_points_subset(m, q1d, part.elems)).reshape(part.ne_local, -1))
+        pf.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(c.cuda())), [0, 1])
+        pf.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(c.cuda())))
+        pf.Assemble()
+        forms.append(pf)
+        parts.append(part)
+        xs.append(torch.as_tensor(xg[part.owned_global]).cuda())
+        ys.append(torch.full((part.n_owned,), float("nan"), dtype=torch.float64, device="cuda"))
+    E.ParGroup(forms).Mult(xs, ys)
+    torch.cuda.synchronize()
+    y = np.zeros(fes.ndofs)
+    for part, yt in zip(parts, ys):
+        y[part.owned_global] = yt.cpu().numpy()
+    cg = coeff_function(O.quad_points(m.element_nodes(), q1d))
+    op = O.OracleOperator(m.element_nodes(), fes.gather_map(), fes.ndofs, order, alpha=cg, beta=cg)
+    assert relerr(y, op.mult_markers(xg, attr, mass_marker=[0, 1])) <= RTOL

@@ -539,3 +539,52 @@ def test_cross_wave_face_assembly(order):
         d = torch.empty(fa.ndofs, dtype=torch.float64, device="cuda")
         form.AssembleDiagonal(d)
         assert relerr(host(d), op.diagonal()) < 1e-13
+
+
+@pytest.mark.parametrize("mesh_name", ["fichera_r1", "cart_bricks", "trilinear"])
+@pytest.mark.parametrize("order", [1, 2, 3, 4])
+@pytest.mark.parametrize("compress", [True, False])
+def test_attribute_markers(mesh_name, order, compress):
+    """"PA Markers" (test_pa_kernels.cpp:696-750): attributes 1 + i % 2, the MassIntegrator
+    restricted to attribute 2 by the marker {0, 1} (and, second form, the DiffusionIntegrator
+    to attribute 1), through the C ABI's marked integrators, against the oracle's masked
+    MultInternal (AddMultWithMarkers, bilinearform_ext.cpp:753-774,807-847) and the
+    diagonal of the masked operator; AFFINE and full-layout qdata, fused TPE / line kernels."""
+    m = make_mesh(mesh_name)
+    m.SetAttributes(1 + np.arange(m.GetNE()) % 2)
+    attr = m.GetAttributes()
+    fes = E.H1Space(m, order)
+    en = m.element_nodes()
+    q1d = O.default_q1d(order)
+    c = coeff_function(O.quad_points(en, q1d))
+    op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=c, beta=c)
+    x = np.random.default_rng(3).uniform(-1, 1, fes.ndofs)
+    for mm, dm in (([0, 1], None), (None, [1, 0])):
+        form = E.BilinearForm(fes, compress_geometry=compress)
+        form.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(c.reshape(fes.ne, -1)))), mm)
+        form.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(dev(c.reshape(fes.ne, -1)))), dm)
+        form.Assemble()
+        y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+        form.Mult(dev(x), y)
+        ref = op.mult_markers(x, attr, mass_marker=mm, diff_marker=dm)
+        assert relerr(host(y), ref) <= RTOL
+        # the masked operator's diagonal: e_i^T A e_i from the oracle's masked Mult on a few dofs
+        d = torch.empty_like(y)
+        form.AssembleDiagonal(d)
+        dh = host(d)
+        for i in np.random.default_rng(4).choice(fes.ndofs, 5, replace=False):
+            e = np.zeros(fes.ndofs)
+            e[i] = 1.0
+            assert abs(dh[i] - op.mult_markers(e, attr, mass_marker=mm, diff_marker=dm)[i]) <= 1e-12 * np.abs(dh).max()
+
+
+def test_attribute_marker_errors():
+    """A marked integrator needs the attributes, and every attribute must be within the marker
+    (the reference verifies marker sizes against attributes.Max())."""
+    m = make_mesh("nonaligned")
+    fes = E.H1Space(m, 2)
+    form = E.BilinearForm(fes)
+    form.AddDomainIntegrator(E.MassIntegrator(), [1])
+    m.SetAttributes(np.full(m.GetNE(), 2))
+    with pytest.raises(E.ECM2Error):
+        form.Assemble()

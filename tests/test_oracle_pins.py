@@ -8,6 +8,7 @@ the oracle (file:line of the reference test in each docstring).
 import numpy as np
 import pytest
 
+import ecm2_amd as E
 import oracle as O
 from helpers import (GOLDEN, RTOL, coeff_function, element_nodes_from, nonaligned,
                      read_mfem_mesh, relerr)
@@ -186,3 +187,29 @@ def test_golden_vectors_regression():
         x = g[f"{tag}_x"]
         assert relerr(op.mult(x), g[f"{tag}_y"]) < 1e-14
         assert relerr(op.diagonal(), g[f"{tag}_diag"]) < 1e-14
+
+
+@pytest.mark.parametrize("order", [1, 2, 3])
+def test_marker_oracle_matches_fa_on_marked_elements(order):
+    """"PA Markers" (test_pa_kernels.cpp:696-750) restated on the oracle: fichera.mesh with
+    attributes 1 + i % 2 and marker {0, 1} on the MassIntegrator.  The masked PA MultInternal
+    (AddWithMarkers_, bilinearform_ext.cpp:753-774) equals full assembly over the marked
+    elements only (the reference's FA form skips unmarked elements)."""
+    V, Ev = read_mfem_mesh(f"{GOLDEN}/fichera.mesh")
+    en = element_nodes_from(V, Ev)
+    m = E.Mesh(f"{GOLDEN}/fichera.mesh")
+    fes = E.H1Space(m, order)
+    gm = fes.gather_map()
+    attr = 1 + np.arange(fes.ne) % 2
+    q1d = O.default_q1d(order)
+    c = coeff_function(O.quad_points(en, q1d))
+    op = O.OracleOperator(en, gm, fes.ndofs, order, alpha=c, beta=c)
+    x = np.random.default_rng(1).uniform(-1, 1, fes.ndofs)
+    y = op.mult_markers(x, attr, mass_marker=[0, 1])
+    sel = attr == 2
+    fa_mass = O.OracleOperator(en[sel], gm[sel], fes.ndofs, order, alpha=c[sel]).fa_mult(x)
+    fa_diff = O.OracleOperator(en, gm, fes.ndofs, order, beta=c).fa_mult(x)
+    assert relerr(y, fa_mass + fa_diff) < 1e-12
+    # no marker: the plain Mult; marker excluding everything: diffusion alone
+    assert relerr(op.mult_markers(x, attr), op.mult(x)) < 1e-14
+    assert relerr(op.mult_markers(x, attr, mass_marker=[0, 0]), fa_diff) < 1e-12

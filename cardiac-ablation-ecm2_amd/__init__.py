@@ -67,6 +67,7 @@ def load_library(path: str = LIB_PATH):
         "ecm2_version": (i32, []),
         "ecm2_device_count": (i32, []),
         "ecm2_mesh_cartesian": (i32, [i32, i32, i32, f64, f64, f64, pp]),
+        "ecm2_mesh_cartesian_ex": (i32, [i32, i32, i32, f64, f64, f64, i32, pp]),
         "ecm2_mesh_read": (i32, [ctypes.c_char_p, pp]),
         "ecm2_mesh_refine_uniform": (i32, [vp]),
         "ecm2_mesh_info": (i32, [vp, ip, ip]),
@@ -187,10 +188,12 @@ class Mesh:
         self._h = h
 
     @classmethod
-    def MakeCartesian3D(cls, nx, ny, nz, sx=1.0, sy=1.0, sz=1.0):
+    def MakeCartesian3D(cls, nx, ny, nz, sx=1.0, sy=1.0, sz=1.0, sfc_ordering=False):
+        """Mesh::MakeCartesian3D.  sfc_ordering=True is the reference's default (elements along
+        a generalized Hilbert curve); False (lexicographic elements) is this module's default."""
         lib = load_library()
         h = ctypes.c_void_p()
-        _check(lib.ecm2_mesh_cartesian(nx, ny, nz, sx, sy, sz, ctypes.byref(h)))
+        _check(lib.ecm2_mesh_cartesian_ex(nx, ny, nz, sx, sy, sz, 1 if sfc_ordering else 0, ctypes.byref(h)))
         return cls(_handle=h)
 
     def __del__(self):

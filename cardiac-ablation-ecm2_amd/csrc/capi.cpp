@@ -128,6 +128,15 @@ int ecm2_mesh_cartesian(int nx, int ny, int nz, double sx, double sy, double sz,
    });
 }
 
+int ecm2_mesh_cartesian_ex(int nx, int ny, int nz, double sx, double sy, double sz, int sfc_ordering,
+                           ecm2_mesh **out)
+{
+   return guard([&] {
+      NEED(out);
+      *out = new ecm2_mesh{ecm2::HexMesh::cartesian(nx, ny, nz, sx, sy, sz, sfc_ordering != 0)};
+   });
+}
+
 int ecm2_mesh_read(const char *path, ecm2_mesh **out)
 {
    return guard([&] {
@@ -546,8 +555,7 @@ int ecm2_partition_create(const ecm2_h1space *s, const ecm2_mesh *m, const int *
       NEED(s); NEED(elem_rank); NEED(out);
       std::vector<int> er(elem_rank, elem_rank + s->s.ne);
       const bool cart = m && m->m.nx > 0 && m->m.ne == s->s.ne;
-      *out = new ecm2_partition{ecm2::build_local_part(s->s, er, rank, nranks, cart ? m->m.nx : 0,
-                                                       cart ? m->m.ny : 0, cart ? m->m.nz : 0)};
+      *out = new ecm2_partition{ecm2::build_local_part(s->s, er, rank, nranks, cart ? &m->m : nullptr)};
    });
 }
 
@@ -560,8 +568,7 @@ int ecm2_partition_create_ex(const ecm2_h1space *s, const ecm2_mesh *m, const in
                   "unknown decomposition " << decomposition);
       std::vector<int> er(elem_rank, elem_rank + s->s.ne);
       const bool cart = m && m->m.nx > 0 && m->m.ne == s->s.ne;
-      *out = new ecm2_partition{ecm2::build_local_part(s->s, er, rank, nranks, cart ? m->m.nx : 0,
-                                                       cart ? m->m.ny : 0, cart ? m->m.nz : 0,
+      *out = new ecm2_partition{ecm2::build_local_part(s->s, er, rank, nranks, cart ? &m->m : nullptr,
                                                        decomposition == ECM2_DECOMP_OVERLAP)};
    });
 }

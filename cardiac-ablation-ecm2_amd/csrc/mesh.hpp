@@ -26,10 +26,16 @@ struct HexMesh
    std::vector<double> vert;   // [nv][3]
    std::vector<int> elem;      // [ne][8] native order
    std::vector<int> attr;      // [ne]
-   // Cartesian provenance (for the structured numbering); nx = 0 when unstructured.
+   // Cartesian provenance (for the structured numbering); nx = 0 when unstructured.  lex[e] =
+   // ex + nx (ey + ny ez), the lattice position of element e (empty: lexicographic order).
    int nx = 0, ny = 0, nz = 0;
+   std::vector<int> lex;
+   int lex_index(int e) const { return lex.empty() ? e : lex[e]; }
 
-   static HexMesh cartesian(int nx, int ny, int nz, double sx, double sy, double sz);
+   // Mesh::Make3D (mesh.cpp:3683-3813): vertices lexicographic; elements lexicographic or, with
+   // sfc_ordering (MakeCartesian3D's default and the INLINE reader's, mesh_readers.cpp:1506),
+   // along NCMesh::GridSfcOrdering3D's generalized Hilbert curve (ncmesh.cpp:5435-5634).
+   static HexMesh cartesian(int nx, int ny, int nz, double sx, double sy, double sz, bool sfc_ordering = false);
    static HexMesh read(const std::string &path);
    void refine_uniform();
    // Corner coordinates in lexicographic order: out[e][c][a] (a = lex corner).
@@ -46,11 +52,31 @@ enum ElementOrder : int
 std::vector<int> element_order(const HexMesh &m, int kind);
 // Brick order of a subset of the elements of a lexicographic nx x ny x nz mesh: complete
 // 4x4x4 bricks first (members x-fastest), then the remaining elements in given order.
-std::vector<int> brick_order(const std::vector<int> &elems, int nx, int ny, int nz);
+std::vector<int> brick_order(const std::vector<int> &elems, const HexMesh &m);
+
+// The reference's topology tables of a hex mesh (what FiniteElementSpace numbers and
+// UniformRefinement refines): edges numbered in first-insertion order of
+// Mesh::GetVertexToVertexTable over the elements and their Geometry::CUBE Edges (DSTable::Push,
+// mesh.cpp:8304-8366, table.cpp:623), faces in first-insertion order of
+// Mesh::GetElementToFaceTable over the elements and their FaceVert (STable3D::Push4,
+// mesh.cpp:8774-8840, stable3d.cpp:64-165); a face's own frame is its first element's FaceVert
+// order (Mesh::AddQuadFaceElement).
+struct HexTopology
+{
+   int nedges = 0, nfaces = 0;
+   std::vector<int> elem_edges;       // [ne][12], Edges order
+   std::vector<int> elem_faces;       // [ne][6], FaceVert order
+   std::vector<int> face_vert;        // [nfaces][4], the face's frame
+   std::vector<int> face_count;       // [nfaces] elements per face (1: boundary)
+   static HexTopology build(const HexMesh &m);
+};
+extern const int kHexEdges[12][2];     // Geometry::Constants<CUBE>::Edges (geom.cpp:1020-1024)
+extern const int kHexFaceVert[6][4];   // Geometry::Constants<CUBE>::FaceVert (geom.cpp:1032-1036)
 
 enum Numbering : int
 {
-   NUMBERING_ENTITY = 0,     // vertex -> edge -> face -> interior (MFEM fespace order)
+   NUMBERING_ENTITY = 0,     // vertex -> edge -> face -> interior in the reference's entity order
+                             // (FiniteElementSpace, fespace.cpp:2767-2860; HexTopology)
    NUMBERING_STRUCTURED = 1  // lattice (I + NX(J + NY K)) on a Cartesian mesh
 };
 

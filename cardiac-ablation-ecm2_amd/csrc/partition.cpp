@@ -10,12 +10,12 @@ namespace ecm2
 
 std::vector<int> partition_slabs_z(const HexMesh &m, int nranks)
 {
-   ECM2_VERIFY(m.nx > 0, ERR_ARG, "slab partition needs a lexicographic Cartesian mesh");
+   ECM2_VERIFY(m.nx > 0, ERR_ARG, "slab partition needs a Cartesian mesh");
    ECM2_VERIFY(nranks >= 1 && nranks <= m.nz, ERR_ARG, "bad rank count " << nranks);
    std::vector<int> er(m.ne);
    for (int e = 0; e < m.ne; e++)
    {
-      const long ez = e / (m.nx * m.ny);
+      const long ez = m.lex_index(e) / (m.nx * m.ny);
       // Mesh::CartesianPartitioning (mesh.cpp:8994) with nxyz = (1, 1, R) on the element centre
       // z = (ez + 1/2) / nz of the box: r = floor(R (ez + 1/2) / nz), in exact integer arithmetic
       er[e] = (int)std::min<long>(nranks - 1, (2 * ez + 1) * nranks / (2L * m.nz));
@@ -24,7 +24,7 @@ std::vector<int> partition_slabs_z(const HexMesh &m, int nranks)
 }
 
 LocalPart build_local_part(const H1Space &s, const std::vector<int> &elem_rank, int rank, int nranks,
-                           int nx, int ny, int nz, bool overlap)
+                           const HexMesh *cart, bool overlap)
 {
    ECM2_VERIFY((int)elem_rank.size() == s.ne, ERR_ARG, "elem_rank size " << elem_rank.size() << " != ne " << s.ne);
    ECM2_VERIFY(nranks >= 1 && nranks <= 64, ERR_UNSUPPORTED, "1..64 ranks supported");
@@ -116,10 +116,10 @@ LocalPart build_local_part(const H1Space &s, const std::vector<int> &elem_rank, 
       }
       (bnd ? boundary : interior).push_back(e);
    }
-   if (nx > 0)
+   if (cart && cart->nx > 0)
    {
-      interior = brick_order(interior, nx, ny, nz);
-      boundary = brick_order(boundary, nx, ny, nz);
+      interior = brick_order(interior, *cart);
+      boundary = brick_order(boundary, *cart);
    }
    p.ne_interior = (int)interior.size();
    p.elems = interior;

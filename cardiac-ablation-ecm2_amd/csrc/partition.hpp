@@ -62,13 +62,13 @@ struct Xfer
 // empty transfers are omitted.
 std::vector<Xfer> exchange_schedule(const LocalPart &p, bool transpose);
 
-// CartesianPartitioning along z of a lexicographic Cartesian mesh (mesh.cpp:8966 semantics
+// CartesianPartitioning along z of a Cartesian mesh (any element order; mesh.cpp:8966 semantics
 // for a 1 x 1 x nranks grid): elem_rank[e].
 std::vector<int> partition_slabs_z(const HexMesh &m, int nranks);
 
-// nx > 0: the global mesh is a lexicographic nx x ny x nz Cartesian mesh; interior and
-// boundary element groups are then each put in brick order (one 4x4x4 brick per wave).
+// cart (optional): the global mesh when it is Cartesian; interior and boundary element groups
+// are then each put in brick order (one 4x4x4 brick per wave).
 LocalPart build_local_part(const H1Space &s, const std::vector<int> &elem_rank, int rank, int nranks,
-                           int nx = 0, int ny = 0, int nz = 0, bool overlap = false);
+                           const HexMesh *cart = nullptr, bool overlap = false);
 
 } // namespace ecm2

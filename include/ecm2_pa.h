@@ -75,12 +75,18 @@ int ecm2_stream_read(const double *a, long n, double *out, long nout, void *stre
 typedef struct ecm2_mesh ecm2_mesh;
 typedef struct ecm2_h1space ecm2_h1space;
 
-/* Mesh::MakeCartesian3D, mesh/mesh.cpp:3683 (lexicographic element order). */
+/* Mesh::MakeCartesian3D(..., sfc_ordering = false), mesh/mesh.cpp:3683 (lexicographic element order). */
 int ecm2_mesh_cartesian(int nx, int ny, int nz, double sx, double sy, double sz, ecm2_mesh **out);
+/* Mesh::MakeCartesian3D(nx, ny, nz, HEXAHEDRON, sx, sy, sz, sfc_ordering) (mesh.hpp:898-904,
+ * mesh.cpp:3683-3813): sfc_ordering = 1 (the reference's default) orders the elements along
+ * NCMesh::GridSfcOrdering3D's generalized Hilbert curve (ncmesh.cpp:5435-5634). */
+int ecm2_mesh_cartesian_ex(int nx, int ny, int nz, double sx, double sy, double sz, int sfc_ordering,
+                           ecm2_mesh **out);
 /* Mesh(filename): MFEM mesh v1.0 hex meshes and MFEM INLINE hex meshes
- * (mesh/mesh_readers.cpp:1356-1506).  Host file read. */
+ * (mesh/mesh_readers.cpp:1356-1506; INLINE = Make3D with sfc_ordering, :1506).  Host file read. */
 int ecm2_mesh_read(const char *path, ecm2_mesh **out);
-/* Mesh::UniformRefinement, mesh/mesh.cpp:11403 (hex: 1 -> 8). */
+/* Mesh::UniformRefinement, mesh/mesh.cpp:11403 (hex: 1 -> 8; UniformRefinement3D_base's vertex
+ * and child numbering, mesh.cpp:10155-10290, 10635-10705). */
 int ecm2_mesh_refine_uniform(ecm2_mesh *m);
 int ecm2_mesh_info(const ecm2_mesh *m, int *nv, int *ne);
 int ecm2_mesh_get_vertices(const ecm2_mesh *m, double *out /* host [nv][3] */);

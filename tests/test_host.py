@@ -178,3 +178,113 @@ def test_face_brick_order(order):
     assert _face_links(fc, perm) == 2 * 2 * 1
     ref = c.element_order(E.ORDER_BRICK)
     assert sorted(perm[:256].tolist()) == sorted(ref[:256].tolist())
+
+
+# native hex corner -> lexicographic (x, y, z) and the reference's Geometry::CUBE tables
+_NAT = np.array([[0, 0, 0], [1, 0, 0], [1, 1, 0], [0, 1, 0], [0, 0, 1], [1, 0, 1], [1, 1, 1], [0, 1, 1]])
+_EDGES = [(0, 1), (1, 2), (3, 2), (0, 3), (4, 5), (5, 6), (7, 6), (4, 7), (0, 4), (1, 5), (2, 6), (3, 7)]
+_FACES = [(3, 2, 1, 0), (0, 1, 5, 4), (1, 2, 6, 5), (2, 3, 7, 6), (3, 0, 4, 7), (4, 5, 6, 7)]
+
+
+def _cells(m):
+    """Lattice cell (x, y, z) of every element of a unit-cube Cartesian mesh, from its corners."""
+    nx = round(1.0 / np.ptp(m.element_nodes()[0, 0]))
+    return np.rint(m.element_nodes().min(axis=2) * nx).astype(int)
+
+
+@pytest.mark.parametrize("shape", [(4, 4, 4), (6, 5, 7), (8, 3, 2), (3, 9, 4), (5, 4, 12)])
+def test_cartesian_sfc_ordering(shape):
+    """MakeCartesian3D(..., sfc_ordering=True) / the INLINE reader (Make3D, mesh.cpp:3749-3774;
+    NCMesh::GridSfcOrdering3D, ncmesh.cpp:5435-5634): the elements visit every cell once, start at
+    the origin and walk a continuous generalized Hilbert curve -- consecutive cells share a face,
+    but for the odd-extent corner steps gilbert allows (at most a few diagonal moves) -- and for
+    a 2^k cube it is a true Hilbert curve (every step a face step)."""
+    nx, ny, nz = shape
+    m = E.Mesh.MakeCartesian3D(nx, ny, nz, 1.0, ny / nx, nz / nx, sfc_ordering=True)
+    c = _cells(m)
+    assert len({tuple(v) for v in c}) == nx * ny * nz
+    assert tuple(c[0]) == (0, 0, 0)
+    steps = np.abs(np.diff(c, axis=0)).sum(axis=1)
+    assert steps.max() <= 3
+    assert (steps > 1).sum() <= 8
+    if len(set(shape)) == 1 and (nx & (nx - 1)) == 0:
+        assert np.all(steps == 1)
+    # same vertices as the lexicographic mesh, elements permuted
+    lexm = E.Mesh.MakeCartesian3D(nx, ny, nz, 1.0, ny / nx, nz / nx)
+    assert np.array_equal(m.vertices(), lexm.vertices())
+    assert sorted(map(tuple, m.elements())) == sorted(map(tuple, lexm.elements()))
+    # the lattice view still works: brick order and structured numbering
+    assert sorted(m.element_order(E.ORDER_BRICK)) == list(range(m.GetNE()))
+    f = E.H1Space(m, 2, E.NUMBERING_STRUCTURED)
+    assert f.ndofs == (2 * nx + 1) * (2 * ny + 1) * (2 * nz + 1)
+
+
+def test_inline_reader_uses_sfc_order():
+    m = E.Mesh(f"{GOLDEN}/inline-hex.mesh")
+    s = E.Mesh.MakeCartesian3D(4, 4, 4, sfc_ordering=True)
+    assert np.array_equal(m.elements(), s.elements())
+
+
+@pytest.mark.parametrize("mesh", ["cart_sfc", "fichera", "fichera_r1"])
+def test_entity_numbering_follows_reference_tables(mesh):
+    """FiniteElementSpace's H1 numbering (fespace.cpp:2767-2860) over the reference's topology
+    tables: vertex dofs are the vertex ids; edge k of element e gets nv + (its first-insertion
+    index in GetVertexToVertexTable over elements x Edges, DSTable::Push); faces the STable3D::Push4
+    first-insertion index over elements x FaceVert; interiors off_i + e.  Checked at p = 2 (one
+    dof per entity) against an independent numpy restatement of those insertion orders."""
+    if mesh == "cart_sfc":
+        m = E.Mesh.MakeCartesian3D(5, 4, 3, sfc_ordering=True)
+    else:
+        m = E.Mesh(f"{GOLDEN}/fichera.mesh")
+        if mesh == "fichera_r1":
+            m.UniformRefinement()
+    Ev = m.elements()
+    fes = E.H1Space(m, 2)
+    gm = fes.gather_map().reshape(-1, 3, 3, 3)  # [e][z][y][x]
+    nv = m.GetNV()
+    edges, faces = {}, {}
+    for e in range(m.GetNE()):
+        for a, b in _EDGES:
+            edges.setdefault(tuple(sorted((Ev[e, a], Ev[e, b]))), len(edges))
+        for fv in _FACES:
+            faces.setdefault(tuple(sorted(Ev[e, list(fv)])[:3]), len(faces))
+    off_f, off_i = nv + len(edges), nv + len(edges) + len(faces)
+    assert fes.ndofs == off_i + m.GetNE()
+    for e in range(m.GetNE()):
+        for n in range(8):
+            x, y, z = 2 * _NAT[n]
+            assert gm[e, z, y, x] == Ev[e, n]
+        for a, b in _EDGES:
+            x, y, z = _NAT[a] + _NAT[b]
+            assert gm[e, z, y, x] == nv + edges[tuple(sorted((Ev[e, a], Ev[e, b])))]
+        for fv in _FACES:
+            x, y, z = _NAT[list(fv)].sum(axis=0) // 2
+            assert gm[e, z, y, x] == off_f + faces[tuple(sorted(Ev[e, list(fv)])[:3])]
+        assert gm[e, 1, 1, 1] == off_i + e
+
+
+def test_uniform_refinement_follows_reference_numbering():
+    """UniformRefinement3D_base (mesh.cpp:10271-10290, 10673-10704): new vertices oedge + edge,
+    oface + face, oelem + element, with the reference's tables' entity numbers; child k of
+    element i is element 8 i + k and its corners are the reference's vertex lists."""
+    m = E.Mesh(f"{GOLDEN}/fichera.mesh")
+    Ev, V = m.elements(), m.vertices()
+    edges, faces = {}, {}
+    E12 = np.empty((m.GetNE(), 12), int)
+    F6 = np.empty((m.GetNE(), 6), int)
+    for e in range(m.GetNE()):
+        for k, (a, b) in enumerate(_EDGES):
+            E12[e, k] = edges.setdefault(tuple(sorted((Ev[e, a], Ev[e, b]))), len(edges))
+        for k, fv in enumerate(_FACES):
+            F6[e, k] = faces.setdefault(tuple(sorted(Ev[e, list(fv)])[:3]), len(faces))
+    nv, ne = m.GetNV(), m.GetNE()
+    oe, of, oc = nv, nv + len(edges), nv + len(edges) + len(faces)
+    m.UniformRefinement()
+    R, VR = m.elements(), m.vertices()
+    assert m.GetNV() == oc + ne and m.GetNE() == 8 * ne
+    for i in range(ne):
+        v, e_, f_, c = Ev[i], oe + E12[i], of + F6[i], oc + i
+        assert list(R[8 * i]) == [v[0], e_[0], f_[0], e_[3], e_[8], f_[1], c, f_[4]]
+        assert list(R[8 * i + 6]) == [c, f_[2], e_[10], f_[3], f_[5], e_[5], v[6], e_[6]]
+        assert np.allclose(VR[c], V[v].mean(axis=0), atol=1e-15)
+        assert np.allclose(VR[e_[0]], V[[v[0], v[1]]].mean(axis=0), atol=1e-15)

@@ -281,6 +281,15 @@ def main():
                     help="compressed: AFFINE qdata on parallelepiped meshes (default); full: per-point layout")
     ap.add_argument("--full-layout", type=int, default=1,
                     help="1 (N = 1): also time the full per-point qdata layout in this run (full_layout sub-object)")
+    ap.add_argument("--variants", type=int, default=1,
+                    help="1 (N = 1, c2/c4/c5): also time, in this run, the reference's own numbering "
+                         "(entity_numbering sub-object) and a trilinear mesh (trilinear sub-object)")
+    ap.add_argument("--numbering", choices=["structured", "entity"], default="structured",
+                    help="c2/c4/c5 main line: lattice dof numbering on a lexicographic mesh (structured) or the "
+                         "reference's own (entity: MakeCartesian3D's space-filling-curve element order, "
+                         "FiniteElementSpace vertex/edge/face/interior numbering, element order derived by the form)")
+    ap.add_argument("--mesh", choices=["affine", "trilinear"], default="affine",
+                    help="c2/c4/c5 main line: the Cartesian mesh (affine) or its interior vertices moved (trilinear)")
     ap.add_argument("--loopback", type=int, default=1,
                     help="N>1 on one GPU: N subdomains in this process (validation of the partitioned path)")
     ap.add_argument("--partition", choices=["slabs", "boxes"], default="slabs",
@@ -353,23 +362,43 @@ def main():
             mesh.UniformRefinement()
         fes = E.H1Space(mesh, order)
     else:
-        mesh = E.Mesh.MakeCartesian3D(nx, ny, nz_total, 1.0, ny / nx, nz_total / nx)
-        fes = E.H1Space(mesh, order, E.NUMBERING_STRUCTURED)
+        mesh, fes = cartesian_space(E, nx, ny, nz_total, order, args.numbering, args.mesh)
+    variant = variant_key(args)
     nsub = world if world > 1 else args.loopback
     mass = lambda a: E.MassIntegrator(E.QuadratureCoefficient(a))
     diff = lambda T: E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(T, K_SCALE, K_SLOPE, K_TREF))
     form = None
     keep = []
 
-    def serial_form(compress_geometry):
+    def serial_form(compress_geometry, mesh=mesh, fes=fes, numbering=args.numbering):
         a, T = bioheat_coefficients(E, torch, mesh, fes)
         keep.extend([a, T])
-        f = E.BilinearForm(fes, kernel=kernel, element_order=os.environ.get("ECM2_ELEMENT_ORDER", "auto"),
+        # the reference's numbering: no mesh knowledge, the form derives its order from the map
+        eo = "faces" if numbering == "entity" and args.workload != "c3" else "auto"
+        f = E.BilinearForm(fes, kernel=kernel, element_order=os.environ.get("ECM2_ELEMENT_ORDER", eo),
                            scatter=scatter, compress_geometry=compress_geometry)
         f.AddDomainIntegrator(mass(a))
         f.AddDomainIntegrator(diff(T))
         f.Assemble()
         return f
+
+    def sub_measure(f, fes_s, tag, note):
+        """Time another serial form of this workload in this run (same steps, same clock
+        settling): value, step and kernel time, roofline (the pin of its own variant)."""
+        xs = torch.empty(fes_s.ndofs, dtype=torch.float64, device="cuda")
+        xs.uniform_(-1.0, 1.0, generator=torch.Generator(device="cuda").manual_seed(1))
+        ys = torch.empty_like(xs)
+        kf = kernel_ms([f], f.Mult, xs, ys, args.steps, torch)
+        dtf = time_mults(f.Mult, xs, ys, args.steps, args.warmup, 1, dist, torch)
+        lay = qdata_layout(E, f)
+        lat, units, runs = f.AddressingInfo()
+        return {"qdata_layout": lay,
+                "value": round(fes_s.ndofs * args.steps / dtf / 1e6, 2),
+                "ms_per_step": round(dtf / args.steps * 1e3, 5),
+                "lattice_units": [lat, units], "summation_runs": runs,
+                "roofline": roofline(args.workload + tag, 1, lay, kf, f.algorithmic_bytes(),
+                                     min_bytes(f, fes_s.ne, nd, fes_s.ndofs), None, use_pin=pin_ok),
+                "note": note}
 
     dl.at("assemble")
     if nsub <= 1:
@@ -460,23 +489,35 @@ def main():
     pin_ok = (args.loopback <= 1 and (args.workload != "c2" or args.c2_n == 50)
               and (args.workload != "c3" or args.c3_refine == 6))
     value = ndofs_total * args.steps / tmax / 1e6
+    lattice = timed_forms[0].AddressingInfo()
 
-    full = None
-    if world == 1 and args.loopback <= 1 and args.full_layout and compress and args.workload != "c3":
+    subs = {}
+    serial_main = world == 1 and args.loopback <= 1 and args.workload != "c3"
+    if serial_main and args.full_layout and compress:
         dl.at("full layout")
         del apply
         ff = serial_form(False)
-        kf = kernel_ms([ff], ff.Mult, x, y, args.steps, torch)
-        dtf = time_mults(ff.Mult, x, y, args.steps, args.warmup, 1, dist, torch)
-        lay_f = qdata_layout(E, ff)
-        full = {"qdata_layout": lay_f,
-                "value": round(fes.ndofs * args.steps / dtf / 1e6, 2),
-                "ms_per_step": round(dtf / args.steps * 1e3, 5),
-                "roofline": roofline(args.workload, 1, lay_f, kf, ff.algorithmic_bytes(),
-                                     min_bytes(ff, fes.ne, nd, fes.ndofs), None, use_pin=pin_ok),
-                "note": "same run, same inputs, per-point qdata (56 B per quadrature point: the layout SURVEY "
-                        "§8(d)'s algorithmic bytes describe, so its alg_ratio is a roofline fraction)"}
+        subs["full_layout"] = sub_measure(
+            ff, fes, variant, "same run, same mesh and numbering, per-point qdata (56 B per quadrature point: the "
+                              "layout SURVEY §8(d)'s algorithmic bytes describe, so its alg_ratio is a roofline fraction)")
         del ff
+    if serial_main and args.variants and args.numbering == "structured" and args.mesh == "affine":
+        dl.at("entity numbering")
+        me, fe_ = cartesian_space(E, nx, ny, nz_total, order, "entity", "affine")
+        fv = serial_form(compress, me, fe_, "entity")
+        subs["entity_numbering"] = sub_measure(
+            fv, fe_, "ent", "same run, same mesh geometry, the reference's own numbering: MakeCartesian3D's "
+                            "space-filling-curve element order (sfc_ordering = true) and FiniteElementSpace's "
+                            "vertex/edge/face/interior dofs (what a drop-in BilinearFormExtension receives as "
+                            "gather_map), element order derived by the form from the map alone")
+        del fv
+        dl.at("trilinear mesh")
+        mt, ft = cartesian_space(E, nx, ny, nz_total, order, "structured", "trilinear")
+        fv = serial_form(compress, mt, ft, "structured")
+        subs["trilinear"] = sub_measure(
+            fv, ft, "tri", "same run, interior vertices moved by up to 0.15 h (genuinely trilinear hexes, as "
+                           "an unstructured cardiac mesh): per-point qdata (the AFFINE compression does not apply)")
+        del fv, me, fe_, mt, ft
 
     if rank == 0:
         dl.at("stream copy peak")
@@ -506,17 +547,20 @@ def main():
                 "launch": "stream launches" if world == 1 else par_launch_label(args.schedule, args.par_graph),
                 "kernel": ["auto", "tpe", "wpe", "unfused", "line"][timed_forms[0].info()["kernel"]],
                 "qdata_layout": layout,
+                "numbering": ("entity (the reference's FiniteElementSpace numbering)" if args.workload == "c3" or
+                              args.numbering == "entity" else "structured (dof lattice of the Cartesian mesh)"),
+                "mesh": args.mesh if args.workload != "c3" else "fichera (affine after refinement)",
+                "lattice_units": list(lattice[:2]), "summation_runs": lattice[2],
                 "qdata_bytes_stored": qbytes_total / world,
                 "parallelism": (f"domain decomposition, {'z-slabs' if args.partition == 'slabs' else 'boxes'} x{world} ({decomp}, {args.schedule} schedule), RCCL shared-DoF exchange"
                                 if world > 1 else
                                 (f"loopback {'z-slabs' if args.partition == 'slabs' else 'boxes'} x{args.loopback} on one GPU" if args.loopback > 1 else "single GPU")),
             },
-            "roofline": roofline(args.workload, world, layout, kavg_ms, bytes_total / world, mbytes_total / world,
-                                 stream, use_pin=pin_ok),
+            "roofline": roofline(args.workload + variant, world, layout, kavg_ms, bytes_total / world,
+                                 mbytes_total / world, stream, use_pin=pin_ok),
             "cpu_baseline": cpu,
         }
-        if full is not None:
-            line["full_layout"] = full
+        line.update(subs)
         if pcg is not None:
             line["pcg"] = pcg
         print(json.dumps(line), flush=True)
@@ -533,7 +577,31 @@ def main():
     dl.done()
 
 
-def c3_pcg(E, torch, fes, form, max_iter=200):
+def variant_key(args):
+    """Suffix of the PMC pin of the main line's variant: '' structured affine, 'ent', 'tri'."""
+    if args.workload == "c3":
+        return ""
+    return ("ent" if args.numbering == "entity" else "") + ("tri" if args.mesh == "trilinear" else "")
+
+
+def cartesian_space(E, nx, ny, nz, order, numbering, shape):
+    """The Cartesian box mesh and its H1 space.  structured: lexicographic elements, lattice dofs;
+    entity: the reference's MakeCartesian3D (space-filling-curve element order) and its
+    FiniteElementSpace numbering.  trilinear: every interior vertex moved by a seeded uniform
+    offset of up to 0.15 h per coordinate (non-affine hexes)."""
+    mesh = E.Mesh.MakeCartesian3D(nx, ny, nz, 1.0, ny / nx, nz / nx, sfc_ordering=(numbering == "entity"))
+    if shape == "trilinear":
+        V = mesh.vertices()
+        h = 1.0 / nx
+        hi = np.array([1.0, ny / nx, nz / nx])
+        inner = np.all((V > 0.5 * h) & (V < hi - 0.5 * h), axis=1)
+        V[inner] += 0.15 * h * np.random.default_rng(7).uniform(-1, 1, (int(inner.sum()), 3))
+        mesh.set_vertices(V)
+    fes = E.H1Space(mesh, order, E.NUMBERING_ENTITY if numbering == "entity" else E.NUMBERING_STRUCTURED)
+    return mesh, fes
+
+
+def c3_pcg(E, torch, fes, form, max_iter=100):
     """C3 extras: device re-assembly after a k(T) change (coefficient projection
     + qdata setup) and a Jacobi-PCG solve on the constrained operator, as MDoF*iter/s."""
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -552,13 +620,15 @@ def c3_pcg(E, torch, fes, form, max_iter=200):
     x = torch.empty_like(b)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    it, nrm = form.PCG(b, x, ess=ess, rel_tol=1e-30, max_iter=max_iter, jacobi=True)  # fixed iteration count
+    it, nrm = form.PCG(b, x, ess=ess, rel_tol=1e-30, max_iter=max_iter, jacobi=True)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    return {"iterations": it, "seconds": round(dt, 4), "mdof_iter_per_s": round(fes.ndofs * it / dt / 1e6, 1),
-            "reassembly_ms": round(reasm_ms, 3),
-            "note": "fixed max_iter with rel_tol 1e-30 (timing); includes the per-iteration 8-byte "
-                    "convergence read-back and the DIAG_ONE constraint passes"}
+    stop = (f"stopped at max_iter = {max_iter}" if it >= max_iter else
+            f"converged to rel_tol 1e-30 after {it} of max_iter = {max_iter} iterations")
+    return {"iterations": it, "max_iter": max_iter, "seconds": round(dt, 4),
+            "mdof_iter_per_s": round(fes.ndofs * it / dt / 1e6, 1), "reassembly_ms": round(reasm_ms, 3),
+            "note": f"Jacobi-PCG with rel_tol 1e-30 ({stop}); MDoF*iter/s over the iterations run, including the "
+                    "per-iteration 8-byte convergence read-back and the DIAG_ONE constraint passes"}
 
 
 def stream_copy_peak(E, torch, nbytes=1 << 30, reps=20):
@@ -633,6 +703,9 @@ def cpu_baseline(fes, mesh, alpha, T, seconds, workload):
         "value": round(fes.ndofs * n / dt / 1e6, 3),
         "unit": "MDoF/s",
         "cores": O.num_threads(),
+        "cores_note": (f"OpenMP threads = OMP_NUM_THREADS ({os.environ.get('OMP_NUM_THREADS', 'unset')}): the "
+                       f"host-core share of one GPU on this box (os.cpu_count() = {os.cpu_count()} is the whole "
+                       "multi-GPU host's, shared by 8 GPUs' jobs)"),
         "kind": "port",
         "cpu_model": cpu_model(),
         "sample": f"{n} oracle PA Mults (gather, mass, diffusion, CSR scatter; OpenMP) on the same "

@@ -58,6 +58,12 @@ def test_bench_single_gpu_line():
     assert r["traffic"] is None  # a pin belongs to the default size only
     # value = ndofs * steps / time
     assert b["value"] == pytest.approx(b["config"]["ndofs"] / (b["ms_per_step"] * 1e-3) / 1e6, rel=1e-3)
+    assert b["config"]["numbering"].startswith("structured") and b["config"]["mesh"] == "affine"
+    # the same run's variants: the reference's numbering (same layout) and a trilinear mesh (per-point qdata)
+    assert b["entity_numbering"]["value"] > 0 and b["entity_numbering"]["qdata_layout"] == "affine"
+    assert b["trilinear"]["value"] > 0 and b["trilinear"]["qdata_layout"] == "blocked"
+    e = run_bench(*SMALL, "--numbering", "entity", "--variants", "0")
+    assert e["config"]["numbering"].startswith("entity") and "entity_numbering" not in e
 
 
 @pytest.mark.gpu

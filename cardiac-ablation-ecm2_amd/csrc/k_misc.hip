@@ -411,8 +411,8 @@ __global__ void k_scatter_add_idx(int n, const int *__restrict__ idx, const doub
 constexpr int kRunInts = 12;
 __global__ void __launch_bounds__(256)
 k_sum_partials(int b0, int b1, const int *__restrict__ blocks, const int *__restrict__ runs,
-               const int *__restrict__ rslots, const double *__restrict__ part, int n_owned,
-               double *__restrict__ y, double *__restrict__ yg)
+               const int *__restrict__ rslots, const int *__restrict__ pdof, const double *__restrict__ part,
+               int n_owned, double *__restrict__ y, double *__restrict__ yg)
 {
    __shared__ int sd[257 * kRunInts];
    const int blk = b0 + xcd_contiguous(blockIdx.x, gridDim.x);
@@ -430,9 +430,10 @@ k_sum_partials(int b0, int b1, const int *__restrict__ blocks, const int *__rest
       else { hi = mid - 1; }
    }
    const int *R = sd + lo * kRunInts;
-   const int shape = R[0], n1 = shape & 255, cnt = shape >> 16;
+   const int shape = R[0], n1 = shape & 255, cnt = (shape >> 16) & 255;
    const int off = i - R[6], pa = off % n1, pb = off / n1;
-   const int d = R[1] + pa * R[2] + pb * R[3];
+   // shape bit 24: the run's dofs are not a lattice (entity numbering): the entry list holds them
+   const int d = (shape >> 24) ? pdof[i] : R[1] + pa * R[2] + pb * R[3];
    const int ds = pa * R[4] + pb * R[5];
    double v[4];
 #pragma unroll
@@ -637,13 +638,13 @@ void scatter_add_idx(int n, const int *idx, const double *buf, double *y, hipStr
    ECM2_HIP(hipGetLastError());
 }
 
-void sum_partials(int b0, int b1, const int *blocks, const int *runs, const int *rslots, const double *part,
-                  int n_owned, double *y, double *yg, hipStream_t s)
+void sum_partials(int b0, int b1, const int *blocks, const int *runs, const int *rslots, const int *pdof,
+                  const double *part, int n_owned, double *y, double *yg, hipStream_t s)
 {
    if (b1 <= b0) { return; }
-   ECM2_VERIFY(blocks && runs, ERR_INTERNAL, "summation pass needs its run plan");
-   hipLaunchKernelGGL(k_sum_partials, dim3(b1 - b0), dim3(256), 0, s, b0, b1, blocks, runs, rslots, part, n_owned, y,
-                      yg);
+   ECM2_VERIFY(blocks && runs && pdof, ERR_INTERNAL, "summation pass needs its run plan");
+   hipLaunchKernelGGL(k_sum_partials, dim3(b1 - b0), dim3(256), 0, s, b0, b1, blocks, runs, rslots, pdof, part,
+                      n_owned, y, yg);
    ECM2_HIP(hipGetLastError());
 }
 

@@ -45,18 +45,20 @@ struct TpeReg
 {
    int base, sx, sy, sz, mask;
 };
-// Partial slots: block blk owns part[blk pstride ...]: a regular block (reg) in face-grouped
-// order, [tpe_surface_index(X, Y, Z)] (the summation pass then reads a face's two holders as
-// two contiguous runs), any other block as [a][lane].  MAYREG: reg may be true (per block).
+// Partial slots: block blk owns part[blk pstride ...]: a regular or lattice-slot block (regf 1 or
+// 2) in face-grouped order, [tpe_surface_index(X, Y, Z)] (the summation pass then reads a face's
+// two holders as two contiguous runs), any other block as [a][lane].  regf 1 also computes the
+// dofs from the lattice (no map reads); regf 2 reads them from the map (dofs not a lattice).
+// MAYREG: regf may be nonzero (per block).
 template <int D, bool SPLIT, bool SIGNS, bool XW, bool MAYREG = false>
 __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], const int *__restrict__ mp, int fl,
                                                    int blk, int lane, bool active, int n_owned,
                                                    double *__restrict__ y, double *__restrict__ yg,
                                                    double *__restrict__ part, double *xb, int w, bool wave_on,
-                                                   TpeReg rg = {}, bool reg = false, int pstride = D * D * D * 64)
+                                                   TpeReg rg = {}, int regf = 0, int pstride = D * D * D * 64)
 {
    constexpr int ND = D * D * D, XR = XwaveRows<D>::R;
-   const bool rr = MAYREG && reg;
+   const bool rr = MAYREG && regf == 1, rs = MAYREG && regf != 0;
    if (SIGNS && wave_on && !rr)
    {
 #pragma unroll
@@ -135,7 +137,7 @@ __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], cons
             if (!shared) { *dst = Yo[a]; }
             else if (part)
             {
-               part[(size_t)blk * pstride + (rr ? tpe_surface_index(D, X, Y, Z) : a * 64 + lane)] = Yo[a];
+               part[(size_t)blk * pstride + (rs ? tpe_surface_index(D, X, Y, Z) : a * 64 + lane)] = Yo[a];
             }
             else { unsafeAtomicAdd(dst, Yo[a]); }
          }
@@ -325,13 +327,14 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
    const bool active = wave_on && e < ne;
    const int *mp = gmap + (size_t)blk * ND * 64 + lane;
    TpeReg rg = {};
-   bool reg = false;
+   int regf = 0;
    if (RM && wave_on)
    {
       const int *r = treg + (size_t)blk * 8;  // wave-uniform: scalar loads
       rg = TpeReg{r[0], r[1], r[2], r[3], r[4]};
-      reg = RM == 1 || r[7] != 0;
+      regf = RM == 1 ? 1 : r[7];
    }
+   const bool reg = regf == 1;
    double Yo[ND];
 #pragma unroll
    for (int a = 0; a < ND; a++) { Yo[a] = 0.0; }
@@ -532,7 +535,7 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
    }  // wave_on
    tpe_assemble_store<D, SPLIT, RM != 1, true, RM != 0>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0,
                                                          blk, lane, active, n_owned, y, yg, part, &sX[0][0][0], w,
-                                                         wave_on, rg, reg, pstride);
+                                                         wave_on, rg, regf, pstride);
 }
 
 // Latency variant of k_apply_tpe_sf for small block ranges (the boundary elements of the
@@ -692,7 +695,7 @@ k_apply_tpe_pp(int ne, int blk_begin, int n_owned, const int *__restrict__ gmap,
 #pragma unroll
       for (int a = 0; a < ND; a++) { Yo[a] += sY[k][a][lane]; }
    tpe_assemble_store<D, SPLIT, true, false>(Yo, mp, lane_flags[(size_t)blk * 64 + lane], blk, lane, active,
-                                             n_owned, y, yg, part, nullptr, 0, true, TpeReg{}, false, pstride);
+                                             n_owned, y, yg, part, nullptr, 0, true, TpeReg{}, 0, pstride);
 }
 
 // PA diagonal, thread per element on the blocked layout (PADiffusionDiagonal3D and the
@@ -800,15 +803,15 @@ k_diag_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restric
    }
    // regular blocks (treg row flag): the apply's face-grouped partial slots
    TpeReg rg = {};
-   bool reg = false;
+   int regf = 0;
    if (treg && wave_on)
    {
       const int *r = treg + (size_t)blk * 8;
       rg = TpeReg{r[0], r[1], r[2], r[3], r[4]};
-      reg = r[7] != 0;
+      regf = r[7];
    }
    tpe_assemble_store<D, SPLIT, false, AFF, true>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0, blk,
-                                                  lane, active, n_owned, y, yg, part, xb, w, wave_on, rg, reg,
+                                                  lane, active, n_owned, y, yg, part, xb, w, wave_on, rg, regf,
                                                   pstride);
 }
 

@@ -112,7 +112,7 @@ struct ApplyArgs
    int ne = 0, blk_begin = 0, blk_end = 0, n_owned = 0;
    const int *pos = nullptr;        // element permutation (blocked layout), may be null
    const int *lane_flags = nullptr; // [blk][64]: in-wave face merge flags
-   const int *treg = nullptr;       // device [blk][8]: 4x4x4 blocks (base, sx, sy, sz, face mask, -, -, regular), or null
+   const int *treg = nullptr;       // device [blk][8]: 4x4x4 blocks (base, sx, sy, sz, face mask, -, -, flag: 1 regular, 2 lattice slots), or null
    int treg_all = 0;                // every block regular
    int part_stride = 0;             // p <= 2 partial slots per block (27 * 64, or the lattice surface when treg_all)
    const int *gmap = nullptr;
@@ -271,7 +271,7 @@ void scatter_add_idx(int n, const int *idx, const double *buf, double *y, hipStr
 // s0, s1, s2, s3}: its entry at lattice position (a, b) (offset a + n1 b from entry0) stores
 // y[dof0 + a d1 + b d2] = sum over holders h < cnt (ascending slots) of part[s_h + a t1 + b t2],
 // s_h = runs[r][8 + h] for h < 4, else rslots[slot_off + h].  runs has a sentinel row.
-void sum_partials(int b0, int b1, const int *blocks, const int *runs, const int *rslots, const double *part,
+void sum_partials(int b0, int b1, const int *blocks, const int *runs, const int *rslots, const int *pdof, const double *part,
                   int n_owned, double *y, double *yg, hipStream_t s);
 } // namespace kern
 

@@ -3,6 +3,7 @@
 #include "bricks.hpp"
 
 #include <algorithm>
+#include <climits>
 #include <map>
 #include <tuple>
 #include <array>
@@ -327,6 +328,10 @@ void PAForm::build_shared_plan(const std::vector<int> &hcount, const std::vector
    // re-emitted run by run; each dof keeps its holders in ascending slot order.
    auto cnt = [&](int d) { return hcount[d] > 1 ? start[d + 1] - start[d] : 0; };
    auto slot = [&](int d, int h) { return slots_by_dof[start[d] + h]; };
+   // d1 == kExplicitDofs: the run's slots are affine but its dofs are not (a numbering that is not a
+   // lattice, e.g. the reference's entity numbering): the pass reads each entry's dof from the
+   // plan's entry list instead (4 coalesced bytes per entry)
+   constexpr int kExplicitDofs = INT32_MIN;
    struct Run { int n1, n2, c, dof0, d1, d2, t1, t2, first; std::vector<int> s0; };
    std::vector<Run> runs;
    std::vector<int> order;  // plan entries (dofs) in run-major order
@@ -335,20 +340,36 @@ void PAForm::build_shared_plan(const std::vector<int> &hcount, const std::vector
       const int r0 = range ? n_sh_owned_ : 0, r1 = range ? n_sh_ : n_sh_owned_;
       struct R1 { int i0, n, c, d1, t1; };
       std::vector<R1> r1s;
-      for (int i = r0; i < r1;)
-      {
+      // longest run from entry i: slots affine with a common step, dofs too unless explicit
+      auto extend = [&](int i, bool explicit_dofs, int &d1, int &t1) {
          const int c = cnt(dofs[i]);
-         int n = 1, d1 = 0, t1 = 0;
+         int n = 1;
+         d1 = 0;
+         t1 = 0;
          while (i + n < r1 && n < 64 && c <= 8)
          {
             const int dj = dofs[i + n], dp = dofs[i + n - 1];
             if (cnt(dj) != c) { break; }
             const int dd = dj - dp, tt = c ? slot(dj, 0) - slot(dp, 0) : 0;
-            bool ok = n == 1 || (dd == d1 && tt == t1);
+            bool ok = n == 1 || ((explicit_dofs || dd == d1) && tt == t1);
             for (int h = 1; h < c && ok; h++) { ok = slot(dj, h) - slot(dp, h) == tt; }
             if (!ok) { break; }
             if (n == 1) { d1 = dd; t1 = tt; }
             n++;
+         }
+         return n;
+      };
+      for (int i = r0; i < r1;)
+      {
+         const int c = cnt(dofs[i]);
+         int d1, t1, e1, et1;
+         int n = extend(i, false, d1, t1);
+         const int ne_ = c ? extend(i, true, e1, et1) : 0;
+         if (ne_ >= 2 * n && ne_ >= 4)
+         {
+            n = ne_;
+            d1 = kExplicitDofs;
+            t1 = et1;
          }
          r1s.push_back({i, n, c, d1, t1});
          i += n;
@@ -370,7 +391,7 @@ void PAForm::build_shared_plan(const std::vector<int> &hcount, const std::vector
             Run &g = out[it->second];
             if ((g.n2 + 1) * g.n1 <= 64)
             {
-               const int dd = d0 - g.dof0, tt = q.c ? slot(d0, 0) - g.s0[0] : 0;
+               const int dd = g.d1 == kExplicitDofs ? 0 : d0 - g.dof0, tt = q.c ? slot(d0, 0) - g.s0[0] : 0;
                bool ok = g.n2 == 1 || (dd == g.n2 * g.d2 && tt == g.n2 * g.t2);
                for (int h = 1; h < q.c && ok; h++) { ok = slot(d0, h) - g.s0[h] == tt; }
                if (ok)
@@ -408,11 +429,14 @@ void PAForm::build_shared_plan(const std::vector<int> &hcount, const std::vector
       for (int j = 0; j < g.n1 * g.n2; j++)
       {
          const int a = j % g.n1, b = j / g.n1, d = order[g.first + j];
-         bool ok = d == g.dof0 + a * g.d1 + b * g.d2 && cnt(d) == g.c;
+         bool ok = (g.d1 == kExplicitDofs || d == g.dof0 + a * g.d1 + b * g.d2) && cnt(d) == g.c;
          for (int h = 0; h < g.c && ok; h++) { ok = slot(d, h) == g.s0[h] + a * g.t1 + b * g.t2; }
          ECM2_VERIFY(ok, ERR_INTERNAL, "run plan entry " << g.first + j << " does not match its run");
       }
-      int row[12] = {g.n1 | g.n2 << 8 | g.c << 16, g.dof0, g.d1, g.d2, g.t1, g.t2, g.first, (int)rslots.size(), 0, 0, 0, 0};
+      const bool ex = g.d1 == kExplicitDofs;  // shape bit 24: dofs from the entry list
+      ECM2_VERIFY(g.c < 256, ERR_UNSUPPORTED, "a dof with " << g.c << " holders");
+      int row[12] = {g.n1 | g.n2 << 8 | g.c << 16 | (ex ? 1 << 24 : 0), g.dof0, ex ? 0 : g.d1, ex ? 0 : g.d2,
+                     g.t1, g.t2, g.first, (int)rslots.size(), 0, 0, 0, 0};
       for (int h = 0; h < g.c; h++)
       {
          if (h < 4) { row[8 + h] = g.s0[h]; }
@@ -444,6 +468,9 @@ void PAForm::build_shared_plan(const std::vector<int> &hcount, const std::vector
    sh_runs_.upload(rdesc, s);
    sh_rslots_.upload(rslots.empty() ? std::vector<int>{0} : rslots, s);
    sh_blocks_.upload(blocks.empty() ? std::vector<int>{0, 0} : blocks, s);
+   n_explicit_runs_ = 0;
+   for (const Run &g : runs) { n_explicit_runs_ += g.d1 == kExplicitDofs; }
+   sh_pdof_.upload(order.empty() ? std::vector<int>{0} : order, s);
 }
 
 void PAForm::set_kernel(int mode)
@@ -558,6 +585,7 @@ void PAForm::assemble(hipStream_t s)
       treg_.resize(0);
       treg_all_ = false;
       n_treg_ = 0;
+      n_tlat_ = 0;
       const int ns = tpe_surface_points(D_);
       std::vector<char> breg_ok(nblk, 0);
       if (layout_.kind == QLAYOUT_AFFINE)
@@ -606,7 +634,34 @@ void PAForm::assemble(hipStream_t s)
             nreg++;
          }
          n_treg_ = nreg;
-         if (nreg)
+         // Lattice-slot blocks (flag 2): complete blocks whose dofs are not a lattice (the
+         // reference's entity numbering) but whose held shared entries all sit on distinct points
+         // of the block surface: their partial slots are face-grouped like a regular block's, so
+         // the summation plan's runs stay long (with the dofs from its entry list)
+         int nlat = 0;
+         for (int b = 0; b < nblk; b++)
+         {
+            if (breg_ok[b] || (long)(b + 1) * 64 > ne_ || (latency_from_ >= 0 && b >= latency_from_)) { continue; }
+            std::vector<char> used(ns, 0);
+            bool ok = true;
+            for (int l = 0; l < 64 && ok; l++)
+               for (int a = 0; a < ND_ && ok; a++)
+               {
+                  if (!holds[((size_t)b * 64 + l) * ND_ + a]) { continue; }
+                  if (hcount[blk[((size_t)b * ND_ + a) * 64 + l] & 0x3fffffff] <= 1) { continue; }
+                  const int X = (D_ - 1) * (l & 3) + a % D_, Y = (D_ - 1) * ((l >> 2) & 3) + (a / D_) % D_,
+                            Z = (D_ - 1) * (l >> 4) + a / (D_ * D_);
+                  const int si = tpe_surface_index(D_, X, Y, Z);
+                  ok = si >= 0 && !used[si];
+                  if (ok) { used[si] = 1; }
+               }
+            if (!ok) { continue; }
+            reg[(size_t)b * 8 + 7] = 2;
+            breg_ok[b] = 2;
+            nlat++;
+         }
+         n_tlat_ = nlat;
+         if (nreg || nlat)
          {
             treg_.upload(reg, s);
             treg_all_ = nreg == nblk && (latency_from_ < 0 || latency_from_ >= nblk);
@@ -632,7 +687,7 @@ void PAForm::assemble(hipStream_t s)
                         const int X = (D_ - 1) * (l & 3) + a % D_, Y = (D_ - 1) * ((l >> 2) & 3) + (a / D_) % D_,
                                   Z = (D_ - 1) * (l >> 4) + a / (D_ * D_);
                         const int si = tpe_surface_index(D_, X, Y, Z);
-                        ECM2_VERIFY(si >= 0, ERR_INTERNAL, "block " << b << ": interior lattice point shared");
+                        ECM2_VERIFY(si >= 0, ERR_INTERNAL, "block " << b << ": interior lattice point shared");  // (checked)
                         hslot.push_back(b * part_stride_ + si);
                      }
                      else { hslot.push_back(b * part_stride_ + a * 64 + l); }
@@ -1049,8 +1104,8 @@ void PAForm::finish_shared(int i0, int i1, double *y, double *yg, hipStream_t s)
    ECM2_VERIFY((i0 == 0 || i0 == n_sh_owned_) && (i1 == n_sh_owned_ || i1 == n_sh_) && i0 <= i1, ERR_INTERNAL,
                "summation range [" << i0 << ", " << i1 << ") is not a plan range");
    const int b0 = i0 == 0 ? 0 : sh_nblk_owned_, b1 = i1 == n_sh_owned_ ? sh_nblk_owned_ : sh_nblk_;
-   kern::sum_partials(b0, b1, sh_blocks_.data(), sh_runs_.data(), sh_rslots_.data(), part_.data(), n_owned_, y, yg,
-                      s);
+   kern::sum_partials(b0, b1, sh_blocks_.data(), sh_runs_.data(), sh_rslots_.data(), sh_pdof_.data(), part_.data(),
+                      n_owned_, y, yg, s);
 }
 
 ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, double *yg, int b0,

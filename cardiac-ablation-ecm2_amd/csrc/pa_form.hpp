@@ -137,6 +137,7 @@ public:
    int n_shared_owned() const { return n_sh_owned_; }
    long n_partial_slots() const { return n_slots_; }
    long n_summation_runs() const { return n_runs_; }
+   long n_explicit_runs() const { return n_explicit_runs_; }
    int nblocks() const { return layout_.nblk(); }
    bool has_mass() const { return have_mass_; }
    bool has_diffusion() const { return have_diff_; }
@@ -183,7 +184,8 @@ private:
    // second-pass plan (see finish_shared, kern::sum_partials): runs [nrun + 1][12], the
    // first slots of holders beyond the fourth, blocks [nblk][2] (owned runs' blocks first)
    DeviceArray<int> sh_runs_, sh_rslots_, sh_blocks_;
-   long n_runs_ = 0;
+   DeviceArray<int> sh_pdof_;       // plan entry -> dof (runs whose dofs are not affine read it)
+   long n_runs_ = 0, n_explicit_runs_ = 0;
    int sh_nblk_owned_ = 0, sh_nblk_ = 0;
    DeviceArray<double> part_;                       // partial slots: TPE [blk][nd][64]; LINE [bricks | [e][nd]]
    bool assembled_ = false;
@@ -206,9 +208,10 @@ private:
    int n_bricks_ = 0, brick_bz_ = 0, brick_np_ = 0;  // LINE bricks: count, 2 x 2 x bz, lattice points
    DeviceArray<int> belem_, bmap_;  // LINE bricks: [nbrick][4 bz] elements, [nbrick][np] lattice map
    DeviceArray<int> breg_;          // LINE bricks, lattice-numbered: [nbrick][8] (base, sx, sy, sz, face mask)
-   DeviceArray<int> treg_;          // TPE blocks: [nblk][8] (base, sx, sy, sz, face mask, -, -, regular)
+   DeviceArray<int> treg_;          // TPE blocks: [nblk][8] (base, sx, sy, sz, face mask, -, -, flag 1 regular / 2 lattice slots)
    bool treg_all_ = false;          // every TPE block regular: face-grouped slots only
    int n_treg_ = 0;                 // regular TPE blocks
+   int n_tlat_ = 0;                 // TPE blocks with face-grouped slots but map-addressed dofs (treg flag 2)
    int part_stride_ = 0;            // TPE partial slots per block
    int plan_kind_ = -1;             // qdata layout the TPE plan (merges, regular blocks, slots) was built for
    std::vector<int> brick_off_;     // LINE bricks of block b = [brick_off_[b], brick_off_[b+1])

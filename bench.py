@@ -174,6 +174,8 @@ def member_bench(args, torch, group, xs, ys, ndofs, workload, dl):
     n = len(group.forms)
     members = list(range(n)) if args.member < 0 else [args.member]
     per = []
+    group.Mult(xs, ys)  # RAP: every member's ghost contributions, which a member's P^T receive copies
+    torch.cuda.synchronize()
     for r in members:
         dl.at(f"member {r}")
         for _ in range(3):

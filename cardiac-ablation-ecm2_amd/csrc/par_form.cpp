@@ -508,7 +508,8 @@ void par_group_mult_member(std::vector<ParPAForm *> &forms, const std::vector<co
    ParPAForm &f = *forms[r];
    ECM2_VERIFY(f.part().rank == r && f.part().nranks == n, ERR_ARG, "loopback group: form " << r << " has rank "
                                                                     << f.part().rank);
-   ECM2_VERIFY(f.part().overlap, ERR_UNSUPPORTED, "a member's rows alone need the OVERLAP decomposition");
+   ECM2_VERIFY(f.part().overlap || f.serial(), ERR_UNSUPPORTED,
+               "a member's RAP rows alone run the serial schedule");
    ECM2_VERIFY(f.local().assembled(), ERR_STATE, "Mult before Assemble");
    for (const Xfer &t : f.schedule(false))
    {
@@ -526,8 +527,12 @@ void par_group_mult_member(std::vector<ParPAForm *> &forms, const std::vector<co
    if (f.serial())
    {
       group_copies(forms, x, false, s, r);
-      f.stage_serial_apply(x[r], y[r], s);
+      f.stage_serial_apply(x[r], y[r], s);  // RAP: + the ghost dofs' sums
+      // RAP: the P^T receive copies the peers' ghost contributions -- their y ghost blocks as
+      // their own stage_serial_apply left them (a previous group Mult on the same x)
+      if (!f.part().overlap) { group_copies(forms, x, true, s, r); }
       f.local().finish_shared(0, f.local().n_shared_owned(), y[r], f.yghost(), s);
+      if (!f.part().overlap) { f.phase_finish(y[r], s); }
       return;
    }
    f.stage_pack(x[r], y[r], s);

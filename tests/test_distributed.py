@@ -327,11 +327,12 @@ def test_gpu_loopback_overlapped_schedule(kind, nranks, order, scatter, decomp):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("nranks,order", [(2, 2), (3, 2), (8, 2), (3, 4)])
-@pytest.mark.parametrize("schedule", ["serial", "overlap"])
-def test_gpu_group_member_rows(nranks, order, schedule):
+@pytest.mark.parametrize("schedule,decomp", [("serial", "overlap"), ("overlap", "overlap"), ("serial", "rap")])
+def test_gpu_group_member_rows(nranks, order, schedule, decomp):
     """ParGroup.MultMember: one member's rows alone (the stages one RCCL rank runs, ghost values
-    copied from the peers' x) equal the serial oracle's rows; also replayed from a HIP graph
-    (how bench.py --member times it); the other members' y stay untouched."""
+    copied from the peers' x; RAP: + the P^T receive from the peers' ghost sums of a previous
+    group Mult) equal the serial oracle's rows; also replayed from a HIP graph (how bench.py
+    --member times it); the other members' y stay untouched."""
     import torch
     m = E.Mesh.MakeCartesian3D(6, 5, 16) if nranks == 8 else _mesh("cart_big")
     m.set_vertices(nonaligned(m.vertices()))
@@ -341,7 +342,7 @@ def test_gpu_group_member_rows(nranks, order, schedule):
     forms, xs, ys, parts = [], [], [], []
     xg = np.random.default_rng(11).uniform(-1, 1, fes.ndofs)
     for r in range(nranks):
-        part = E.Partition(fes, er, r, nranks, decomposition="overlap")
+        part = E.Partition(fes, er, r, nranks, decomposition=decomp)
         pf = E.ParBilinearForm(part, schedule=schedule)
         P = E.quadrature_points_subset(m, q1d, part.elems)
         c = torch.as_tensor(coeff_function(P).reshape(part.ne_local, -1)).cuda()
@@ -356,6 +357,11 @@ def test_gpu_group_member_rows(nranks, order, schedule):
     cg = coeff_function(Pg)
     ref = O.OracleOperator(m.element_nodes(), fes.gather_map(), fes.ndofs, order, alpha=cg, beta=cg).mult(xg)
     group = E.ParGroup(forms)
+    if decomp == "rap":
+        group.Mult(xs, ys)  # the peers' ghost contributions a member's P^T receive copies
+        torch.cuda.synchronize()
+        for yt in ys:
+            yt.fill_(float("nan"))
     for r in range(nranks):
         group.MultMember(r, xs, ys)
         torch.cuda.synchronize()

@@ -394,7 +394,11 @@ def main():
         dtf = time_mults(f.Mult, xs, ys, args.steps, args.warmup, 1, dist, torch)
         lay = qdata_layout(E, f)
         lat, units, runs = f.AddressingInfo()
+        lslot, xruns = f.PlanInfo()
+        nsh, nslots = f.ScatterInfo()
         return {"qdata_layout": lay,
+                "plan": {"lattice_slot_units": lslot, "explicit_dof_runs": xruns, "shared_dofs": nsh,
+                         "partial_slots": nslots},
                 "value": round(fes_s.ndofs * args.steps / dtf / 1e6, 2),
                 "ms_per_step": round(dtf / args.steps * 1e3, 5),
                 "lattice_units": [lat, units], "summation_runs": runs,

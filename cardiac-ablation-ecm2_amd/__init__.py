@@ -102,6 +102,7 @@ def load_library(path: str = LIB_PATH):
         "ecm2_pa_form_qdata_bytes": (i32, [vp, dp]),
         "ecm2_pa_form_brick_info": (i32, [vp, ip, ip]),
         "ecm2_pa_form_addressing_info": (i32, [vp, ip, ip, ctypes.POINTER(ctypes.c_long)]),
+        "ecm2_pa_form_plan_info": (i32, [vp, ip, ctypes.POINTER(ctypes.c_long)]),
         "ecm2_pa_form_set_element_order": (i32, [vp, vp]),
         "ecm2_mesh_element_order": (i32, [vp, i32, vp]),
         "ecm2_pa_form_assemble": (i32, [vp, vp]),
@@ -473,6 +474,12 @@ class BilinearForm:
         n, u, r = ctypes.c_int(), ctypes.c_int(), ctypes.c_long()
         _check(_lib.ecm2_pa_form_addressing_info(self._h, ctypes.byref(n), ctypes.byref(u), ctypes.byref(r)))
         return n.value, u.value, r.value
+
+    def PlanInfo(self):
+        """(lattice-slot units, explicit-dof summation runs) after Assemble."""
+        n, r = ctypes.c_int(), ctypes.c_long()
+        _check(_lib.ecm2_pa_form_plan_info(self._h, ctypes.byref(n), ctypes.byref(r)))
+        return n.value, r.value
 
     def BrickInfo(self):
         """(bricks, depth bz) of the p >= 3 brick kernel after Assemble (0, 0: none)."""

@@ -426,6 +426,15 @@ int ecm2_par_form_addressing_info(const ecm2_par_form *f, int *lattice, int *n_u
    });
 }
 
+int ecm2_pa_form_plan_info(const ecm2_pa_form *f, int *lattice_slot_units, long *n_explicit_runs)
+{
+   return guard([&] {
+      NEED(f);
+      if (lattice_slot_units) { *lattice_slot_units = f->f->lattice_slot_units(); }
+      if (n_explicit_runs) { *n_explicit_runs = f->f->n_explicit_runs(); }
+   });
+}
+
 int ecm2_pa_form_scatter_info(const ecm2_pa_form *f, int *n_shared, long *n_slots)
 {
    return guard([&] {

@@ -55,11 +55,13 @@ __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], cons
                                                    int blk, int lane, bool active, int n_owned,
                                                    double *__restrict__ y, double *__restrict__ yg,
                                                    double *__restrict__ part, double *xb, int w, bool wave_on,
-                                                   TpeReg rg = {}, int regf = 0, int pstride = D * D * D * 64)
+                                                   TpeReg rg = {}, int regf = 0, int pstride = D * D * D * 64,
+                                                   const int *__restrict__ lm = nullptr)
 {
    constexpr int ND = D * D * D, XR = XwaveRows<D>::R;
-   const bool rr = MAYREG && regf == 1, rs = MAYREG && regf != 0;
-   if (SIGNS && wave_on && !rr)
+   const bool rr = MAYREG && regf == 1, rs = MAYREG && regf != 0, rl = MAYREG && regf == 2;
+   // (regular and lattice-map blocks carry no orientation signs: checked at setup)
+   if (SIGNS && wave_on && !rs)
    {
 #pragma unroll
       for (int a = 0; a < ND; a++)
@@ -129,7 +131,7 @@ __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], cons
             }
             else
             {
-               const int g = mp[a * 64];
+               const int g = rl ? lm[tpe_lattice_slot(D, X, Y, Z)] : mp[a * 64];
                d = bdof(g);
                shared = bshared(g);
             }
@@ -161,20 +163,13 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
    constexpr int ND = D * D * D, NQ = Q * Q * Q, NQH = (NQ + 1) / 2, DD = D * D;
    constexpr int NR = Q * Q;  // rows
    __shared__ double sX[4][ND][64];
-   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+   const int lane = threadIdx.x & 63;
+   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
    const int blk = blk_begin + (int)blockIdx.x * 4 + w;
    if (blk >= blk_end) { return; }  // wave-uniform; no block-wide barrier below
    const int e = blk * 64 + lane;
    const bool active = e < ne;
    const int *mp = gmap + (size_t)blk * ND * 64 + lane;
-#pragma unroll
-   for (int a = 0; a < ND; a++)
-   {
-      const int g = mp[a * 64];
-      const int d = bdof(g);
-      const double v = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
-      sX[w][a][lane] = bneg(g) ? -v : v;
-   }
    double Yo[ND];
 #pragma unroll
    for (int a = 0; a < ND; a++) { Yo[a] = 0.0; }
@@ -198,7 +193,16 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
          if (MASS) { mq[qx] = qm[(size_t)(q >> 1) * 128 + (q & 1)]; }
       }
    };
+   // the first row's qdata is issued before the gather: its latency overlaps the map -> x chain
    load_row(0, cd, cm);
+#pragma unroll
+   for (int a = 0; a < ND; a++)
+   {
+      const int g = mp[a * 64];
+      const int d = bdof(g);
+      const double v = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
+      sX[w][a][lane] = bneg(g) ? -v : v;
+   }
 
 #pragma unroll 1
    for (int row = 0; row < NR; row++)
@@ -316,11 +320,12 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                const double *__restrict__ x, const double *__restrict__ xg,
                double *__restrict__ y, double *__restrict__ yg, const Basis1D b,
                const int *__restrict__ lane_flags, double *__restrict__ part, const int *__restrict__ treg,
-               int pstride)
+               int pstride, const int *__restrict__ lmap)
 {
    constexpr int ND = D * D * D, NQ = Q * Q * Q, NR = Q * Q, XR = XwaveRows<D>::R, WPG = 4;
    __shared__ double sX[WPG][XR][64];  // gathered x; then the cross-wave face exchange
-   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+   const int lane = threadIdx.x & 63;
+   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: block data in SGPRs
    const int blk = blk_begin + (int)blockIdx.x * WPG + w;
    const bool wave_on = blk < blk_end;  // wave-uniform; every wave reaches the store's barriers
    const int e = blk * 64 + lane;
@@ -328,42 +333,14 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
    const int *mp = gmap + (size_t)blk * ND * 64 + lane;
    TpeReg rg = {};
    int regf = 0;
-   if (RM && wave_on)
-   {
-      const int *r = treg + (size_t)blk * 8;  // wave-uniform: scalar loads
-      rg = TpeReg{r[0], r[1], r[2], r[3], r[4]};
-      regf = RM == 1 ? 1 : r[7];
-   }
-   const bool reg = regf == 1;
    double Yo[ND];
 #pragma unroll
    for (int a = 0; a < ND; a++) { Yo[a] = 0.0; }
    if (wave_on)
    {
-      if (reg)
-      {
-         const int d0 = rg.base + (D - 1) * ((lane & 3) * rg.sx + ((lane >> 2) & 3) * rg.sy + (lane >> 4) * rg.sz);
-#pragma unroll
-         for (int dz = 0; dz < D; dz++)
-#pragma unroll
-            for (int dy = 0; dy < D; dy++)
-#pragma unroll
-               for (int dx = 0; dx < D; dx++)
-               {
-                  sX[w][(dz * D + dy) * D + dx][lane] = x[d0 + dx * rg.sx + dy * rg.sy + dz * rg.sz];
-               }
-      }
-      else
-      {
-#pragma unroll
-         for (int a = 0; a < ND; a++)
-         {
-            const int g = mp[a * 64];
-            const int d = bdof(g);
-            const double v = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
-            sX[w][a][lane] = bneg(g) ? -v : v;
-         }
-      }
+      // The element matrix and the first rows' pairs are issued first: they do not depend on the
+      // gather, so their latency overlaps the (treg ->) (map ->) x chain instead of following it
+      // (one memory latency less per wave before the first row computes).
       auto ld2 = [&](const double *p) -> v2d { return __builtin_nontemporal_load(reinterpret_cast<const v2d *>(p)); };
       v2d ce[3];
       {
@@ -383,6 +360,56 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
       // unrolled, their register demand exceeds 256 VGPRs; at p = 1 the third buffer costs a wave/SIMD.
       constexpr bool PF2 = RM != 0 && D == 3;
       v2d ra[PF2 ? 3 : 1][Q];
+      if constexpr (PF2)
+      {
+         load_row(0, ra[0]);
+         load_row(1, ra[1]);
+      }
+      else { load_row(0, ca); }
+      if (RM)
+      {
+         const int *r = treg + (size_t)blk * 8;  // wave-uniform: scalar loads
+         rg = TpeReg{r[0], r[1], r[2], r[3], r[4]};
+         regf = RM == 1 ? 1 : r[7];
+      }
+      if (regf == 1)
+      {
+         const int d0 = rg.base + (D - 1) * ((lane & 3) * rg.sx + ((lane >> 2) & 3) * rg.sy + (lane >> 4) * rg.sz);
+#pragma unroll
+         for (int dz = 0; dz < D; dz++)
+#pragma unroll
+            for (int dy = 0; dy < D; dy++)
+#pragma unroll
+               for (int dx = 0; dx < D; dx++)
+               {
+                  sX[w][(dz * D + dy) * D + dx][lane] = x[d0 + dx * rg.sx + dy * rg.sy + dz * rg.sz];
+               }
+      }
+      else if (RM == 2 && regf == 2)
+      {
+         // lattice-map block: the dofs of the block's lattice points (no signs), each entry a's
+         // 64 loads one contiguous sub-block of the map
+         const int *lm = lmap + (size_t)blk * tpe_lattice_points(D);
+#pragma unroll
+         for (int a = 0; a < ND; a++)
+         {
+            const int X = (D - 1) * (lane & 3) + a % D, Y = (D - 1) * ((lane >> 2) & 3) + (a / D) % D,
+                      Z = (D - 1) * (lane >> 4) + a / (D * D);
+            const int d = bdof(lm[tpe_lattice_slot(D, X, Y, Z)]);
+            sX[w][a][lane] = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
+         }
+      }
+      else
+      {
+#pragma unroll
+         for (int a = 0; a < ND; a++)
+         {
+            const int g = mp[a * 64];
+            const int d = bdof(g);
+            const double v = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
+            sX[w][a][lane] = bneg(g) ? -v : v;
+         }
+      }
       auto plane = [&](const int qz) {
          double bz[D], gz[D];
 #pragma unroll
@@ -521,21 +548,19 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
       };
       if constexpr (PF2)
       {
-         load_row(0, ra[0]);
-         load_row(1, ra[1]);
 #pragma unroll
          for (int qz = 0; qz < Q; qz++) { plane(qz); }
       }
       else
       {
-         load_row(0, ca);
 #pragma unroll 1
          for (int qz = 0; qz < Q; qz++) { plane(qz); }
       }
    }  // wave_on
    tpe_assemble_store<D, SPLIT, RM != 1, true, RM != 0>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0,
                                                          blk, lane, active, n_owned, y, yg, part, &sX[0][0][0], w,
-                                                         wave_on, rg, regf, pstride);
+                                                         wave_on, rg, regf, pstride,
+                                                         lmap ? lmap + (size_t)blk * tpe_lattice_points(D) : nullptr);
 }
 
 // Latency variant of k_apply_tpe_sf for small block ranges (the boundary elements of the
@@ -712,7 +737,8 @@ __global__ void __launch_bounds__(256)
 k_diag_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
            const double *__restrict__ qdd, const double *__restrict__ qdm, double *__restrict__ y,
            double *__restrict__ yg, const Basis1D b, const double *__restrict__ drow,
-           const int *__restrict__ lane_flags, double *__restrict__ part, const int *__restrict__ treg, int pstride)
+           const int *__restrict__ lane_flags, double *__restrict__ part, const int *__restrict__ treg, int pstride,
+           const int *__restrict__ lmap)
 {
    constexpr int ND = D * D * D, NQ = Q * Q * Q, NQH = (NQ + 1) / 2, DD = D * D, XR = XwaveRows<D>::R, WPG = 4;
    __shared__ double xb[AFF ? WPG * XR * 64 : 1];  // AFF: cross-wave face exchange (as the apply's plan)
@@ -812,7 +838,7 @@ k_diag_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restric
    }
    tpe_assemble_store<D, SPLIT, false, AFF, true>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0, blk,
                                                   lane, active, n_owned, y, yg, part, xb, w, wave_on, rg, regf,
-                                                  pstride);
+                                                  pstride, lmap ? lmap + (size_t)blk * tpe_lattice_points(D) : nullptr);
 }
 
 template <int D, int Q, bool MASS, bool DIFF, bool SPLIT>
@@ -834,7 +860,8 @@ void launch_tpe(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipS
          {
 #define ECM2_SF(RM)                                                                                           \
    hipLaunchKernelGGL((k_apply_tpe_sf<D, Q, SPLIT, RM>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end, a.n_owned, \
-                      a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part, a.treg, a.part_stride)
+                      a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part, a.treg, a.part_stride, \
+                      a.lmap)
             if (a.treg && a.treg_all) { ECM2_SF(1); }
             else if (a.treg) { ECM2_SF(2); }
             else { ECM2_SF(0); }
@@ -874,7 +901,7 @@ void launch_diag_tpe(const ApplyArgs &a, const Basis1D &b, const double *drow, h
 #define ECM2_DIAG(SP, AF)                                                                                \
    hipLaunchKernelGGL((k_diag_tpe<D, Q, MASS, DIFF, SP, AF>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end, \
                       a.n_owned, a.gmap, a.qdd, a.qdm, a.y, a.yg, b, drow, a.lane_flags, a.part,            \
-                      AF ? a.treg : nullptr, a.part_stride)
+                      AF ? a.treg : nullptr, a.part_stride, AF ? a.lmap : nullptr)
    const bool aff = a.kind == QLAYOUT_AFFINE;
    ECM2_VERIFY(!aff || (MASS && DIFF), ERR_INTERNAL, "AFFINE qdata needs both integrators");
    if (a.yg) { if (aff) { ECM2_DIAG(true, true); } else { ECM2_DIAG(true, false); } }

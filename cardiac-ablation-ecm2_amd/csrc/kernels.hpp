@@ -115,6 +115,7 @@ struct ApplyArgs
    const int *treg = nullptr;       // device [blk][8]: 4x4x4 blocks (base, sx, sy, sz, face mask, -, -, flag: 1 regular, 2 lattice slots), or null
    int treg_all = 0;                // every block regular
    int part_stride = 0;             // p <= 2 partial slots per block (27 * 64, or the lattice surface when treg_all)
+   const int *lmap = nullptr;       // device [blk][tpe_lattice_points]: lattice-slot blocks' lattice maps, or null
    const int *gmap = nullptr;
    const double *qdd = nullptr, *qdm = nullptr;
    const double *x = nullptr, *xg = nullptr;
@@ -170,6 +171,32 @@ __host__ __device__ inline int tpe_surface_points(int D)
 __host__ __device__ inline int tpe_surface_index(int D, int X, int Y, int Z)
 {
    return lattice_surface_index(4 * D - 3, 4 * D - 3, 4 * D - 3, X, Y, Z);
+}
+
+// Block lattice map (lattice-slot blocks): one entry per point of the block's (4(D-1)+1)^3
+// lattice, in "parity-class" order: the points are grouped by (X, Y, Z) mod (D-1) -- the
+// classes a lane's entry a = (dx, dy, dz) falls in -- and lexicographic within a class, so the 64
+// lanes' loads of one entry a touch one contiguous 4 x 4 x 4 sub-block (coalesced) and every
+// point is stored once (729 ints at p = 2 against 27 x 64 per-entry map ints).
+__host__ __device__ inline int tpe_lattice_points(int D)
+{
+   const int L = 4 * (D - 1) + 1;
+   return L * L * L;
+}
+__host__ __device__ inline int tpe_lattice_slot(int D, int X, int Y, int Z)
+{
+   const int P = D - 1;
+   const int cx = X % P, cy = Y % P, cz = Z % P;
+   auto n = [](int c) { return c == 0 ? 5 : 4; };  // points of residue c along one axis
+   // classes in (cz, cy, cx) lexicographic order; offset = points in earlier classes
+   int off = 0;
+   for (int k = 0; k < cz; k++) { off += n(k) * (4 * P + 1) * (4 * P + 1); }  // whole earlier z-classes
+   const int nz = n(cz);
+   for (int j = 0; j < cy; j++) { off += nz * n(j) * (4 * P + 1); }
+   const int ny = n(cy);
+   for (int i = 0; i < cx; i++) { off += nz * ny * n(i); }
+   const int nx = n(cx);
+   return off + ((Z / P) * ny + (Y / P)) * nx + (X / P);
 }
 
 namespace kern

@@ -586,6 +586,7 @@ void PAForm::assemble(hipStream_t s)
       treg_all_ = false;
       n_treg_ = 0;
       n_tlat_ = 0;
+      lmap_.resize(0);
       const int ns = tpe_surface_points(D_);
       std::vector<char> breg_ok(nblk, 0);
       if (layout_.kind == QLAYOUT_AFFINE)
@@ -638,12 +639,28 @@ void PAForm::assemble(hipStream_t s)
          // reference's entity numbering) but whose held shared entries all sit on distinct points
          // of the block surface: their partial slots are face-grouped like a regular block's, so
          // the summation plan's runs stay long (with the dofs from its entry list)
+         // Their dofs come from a block lattice map (tpe_lattice_slot order, one entry per lattice
+         // point): every entry of the block at one lattice point must encode the same dof, none
+         // with an orientation sign.
          int nlat = 0;
+         const int NL = tpe_lattice_points(D_);
+         std::vector<int> lmap;
          for (int b = 0; b < nblk; b++)
          {
             if (breg_ok[b] || (long)(b + 1) * 64 > ne_ || (latency_from_ >= 0 && b >= latency_from_)) { continue; }
             std::vector<char> used(ns, 0);
+            std::vector<int> lm(NL, -1);
             bool ok = true;
+            for (int l = 0; l < 64 && ok; l++)
+               for (int a = 0; a < ND_ && ok; a++)
+               {
+                  const int X = (D_ - 1) * (l & 3) + a % D_, Y = (D_ - 1) * ((l >> 2) & 3) + (a / D_) % D_,
+                            Z = (D_ - 1) * (l >> 4) + a / (D_ * D_);
+                  const int g = blk[((size_t)b * ND_ + a) * 64 + l];
+                  int &m = lm[tpe_lattice_slot(D_, X, Y, Z)];
+                  ok = !((unsigned)g >> 31) && (m < 0 || m == g);
+                  m = g;
+               }
             for (int l = 0; l < 64 && ok; l++)
                for (int a = 0; a < ND_ && ok; a++)
                {
@@ -659,8 +676,12 @@ void PAForm::assemble(hipStream_t s)
             reg[(size_t)b * 8 + 7] = 2;
             breg_ok[b] = 2;
             nlat++;
+            if (lmap.empty()) { lmap.assign((size_t)nblk * NL, 0); }
+            std::copy(lm.begin(), lm.end(), lmap.begin() + (size_t)b * NL);
          }
          n_tlat_ = nlat;
+         lmap_.resize(0);
+         if (nlat) { lmap_.upload(lmap, s); }
          if (nreg || nlat)
          {
             treg_.upload(reg, s);
@@ -1121,6 +1142,7 @@ ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, doubl
    a.lane_flags = lane_flags_.data();
    a.treg = treg_.size() ? treg_.data() : nullptr;
    a.treg_all = treg_all_ ? 1 : 0;
+   a.lmap = lmap_.size() ? lmap_.data() : nullptr;
    a.part_stride = part_stride_;
    a.gmap = (resolved_mode_ == KERNEL_TPE) ? gmap_blk_.data()
             : (resolved_mode_ == KERNEL_LINE) ? gmap_line_.data() : gmap_.data();

@@ -95,6 +95,8 @@ public:
       return (resolved_mode_ == KERNEL_LINE && breg_.size()) ? n_bricks_ : 0;
    }
    int n_units() const { return resolved_mode_ == KERNEL_TPE ? layout_.nblk() : n_bricks_; }
+   // p <= 2 blocks with face-grouped partial slots but map-addressed dofs (a numbering that is not a lattice)
+   int lattice_slot_units() const { return resolved_mode_ == KERNEL_TPE ? n_tlat_ : 0; }
    int brick_bz() const { return brick_bz_; }
    // BilinearForm::AddDomainIntegrator(integ[, elem_marker]) (bilinearform.cpp:231-242): with a
    // marker (host marker[n_marker], 0 / 1 per attribute), the integrator acts on the elements
@@ -212,6 +214,7 @@ private:
    bool treg_all_ = false;          // every TPE block regular: face-grouped slots only
    int n_treg_ = 0;                 // regular TPE blocks
    int n_tlat_ = 0;                 // TPE blocks with face-grouped slots but map-addressed dofs (treg flag 2)
+   DeviceArray<int> lmap_;          // their block lattice maps [nblk][tpe_lattice_points] (tpe_lattice_slot order)
    int part_stride_ = 0;            // TPE partial slots per block
    int plan_kind_ = -1;             // qdata layout the TPE plan (merges, regular blocks, slots) was built for
    std::vector<int> brick_off_;     // LINE bricks of block b = [brick_off_[b], brick_off_[b+1])

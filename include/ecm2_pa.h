@@ -199,6 +199,10 @@ int ecm2_pa_form_scatter_info(const ecm2_pa_form *f, int *n_shared, long *n_slot
  * the others read the map); n_runs = runs of the run-compressed summation plan.  The
  * operator is the same either way. */
 int ecm2_pa_form_addressing_info(const ecm2_pa_form *f, int *lattice, int *n_units, long *n_runs);
+/* Summation-plan details (introspection): units whose partial slots are face-grouped although
+ * their dofs are read from the map (non-lattice numberings, e.g. the reference's entity
+ * numbering), and runs whose dofs come from the plan's entry list. */
+int ecm2_pa_form_plan_info(const ecm2_pa_form *f, int *lattice_slot_units, long *n_explicit_runs);
 /* Optional element permutation for the fused kernel's blocked layout (host perm[ne]:
  * internal position i <- caller element perm[i]); see ecm2_mesh_element_order.  All
  * entry points keep the caller's element order (the reference's E-vector order,

@@ -102,9 +102,9 @@ def bioheat_coefficients(E, torch, mesh, fes, part=None):
 
 
 def qdata_layout(E, form):
-    """Quadrature-data layout of a (local) form: affine | affine_e | blocked | native."""
-    return {E.QLAYOUT_NATIVE: "native", E.QLAYOUT_BLOCKED: "blocked",
-            E.QLAYOUT_AFFINE: "affine", E.QLAYOUT_AFFINE_E: "affine_e"}[form.info()["layout"]]
+    """Quadrature-data layout of a (local) form: affine | affine_e | trilinear | blocked | native."""
+    return {E.QLAYOUT_NATIVE: "native", E.QLAYOUT_BLOCKED: "blocked", E.QLAYOUT_AFFINE: "affine",
+            E.QLAYOUT_AFFINE_E: "affine_e", E.QLAYOUT_TRILINEAR: "trilinear"}[form.info()["layout"]]
 
 
 def min_bytes(form, ne, nd, n_true):
@@ -522,7 +522,9 @@ def main():
         fv = serial_form(compress, mt, ft, "structured")
         subs["trilinear"] = sub_measure(
             fv, ft, "tri", "same run, interior vertices moved by up to 0.15 h (genuinely trilinear hexes, as "
-                           "an unstructured cardiac mesh): per-point qdata (the AFFINE compression does not apply)")
+                           "an unstructured cardiac mesh): the AFFINE compression does not apply; the TRILINEAR "
+                           "layout stores the elements' trilinear-map coefficients and the kernel evaluates J, "
+                           "adj(J) and det J at every quadrature point (the per-point layout is full_layout's)")
         del fv, me, fe_, mt, ft
 
     if rank == 0:

@@ -36,7 +36,7 @@ KERNEL_AUTO, KERNEL_TPE, KERNEL_WPE, KERNEL_UNFUSED, KERNEL_LINE = 0, 1, 2, 3, 4
 NUMBERING_ENTITY, NUMBERING_STRUCTURED = 0, 1
 ORDER_NATIVE, ORDER_BRICK, ORDER_MORTON = 0, 1, 2
 SCATTER_PARTIALS, SCATTER_ATOMIC = 0, 1
-QLAYOUT_NATIVE, QLAYOUT_BLOCKED, QLAYOUT_AFFINE, QLAYOUT_AFFINE_E = 0, 1, 2, 3  # BilinearForm.info()['layout']
+QLAYOUT_NATIVE, QLAYOUT_BLOCKED, QLAYOUT_AFFINE, QLAYOUT_AFFINE_E, QLAYOUT_TRILINEAR = 0, 1, 2, 3, 4  # info()['layout']
 DECOMP_RAP, DECOMP_OVERLAP = 0, 1  # Partition decomposition
 _SCATTER = {"partials": SCATTER_PARTIALS, "atomic": SCATTER_ATOMIC}
 
@@ -122,7 +122,9 @@ def load_library(path: str = LIB_PATH):
         "ecm2_pcg_solve": (i32, [vp, vp, i32, vp, vp, f64, f64, i32, i32, ip, dp, vp]),
     }
     for name, (res, args) in sig.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:  # an older build (same-box A/B of library versions); tests check the exports
+            continue
         fn.restype = res
         fn.argtypes = args
     _lib = lib
@@ -632,7 +634,9 @@ def _par_lib():
     lib = load_library()
     if not getattr(lib, "_ecm2_par_ready", False):
         for name, (res, args) in _PAR_SIGS.items():
-            fn = getattr(lib, name)
+            fn = getattr(lib, name, None)
+            if fn is None:
+                continue
             fn.restype, fn.argtypes = res, args
         lib._ecm2_par_ready = True
     return lib

@@ -385,6 +385,104 @@ k_setup_affine(const int *__restrict__ perm, int ne, const double *__restrict__ 
    }
 }
 
+// TRILINEAR layout (kernels.hpp): per point the pair (W_q beta_q, W_q alpha_q) -- det J is
+// evaluated by the apply kernel -- and, from the q = 0 threads, the element's trilinear-map
+// coefficients c1..c7 of each coordinate from its lexicographic corners X_a (a = ax + 2 ay + 4 az):
+// c1 = X1 - X0, c2 = X2 - X0, c3 = X4 - X0, c4 = X3 - X2 - X1 + X0, c5 = X5 - X4 - X1 + X0,
+// c6 = X6 - X4 - X2 + X0, c7 = X7 - X6 - X5 - X3 + X4 + X2 + X1 - X0.
+template <int Q>
+__global__ void __launch_bounds__(256)
+k_setup_trilinear(const int *__restrict__ perm, int ne, const double *__restrict__ enodes,
+                  const double *__restrict__ W, SetupCoef cm, SetupCoef cd, double *__restrict__ qd_geo,
+                  double *__restrict__ qd_pair)
+{
+   constexpr int NQ = Q * Q * Q;
+   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   const int lane = (int)(t & 63);
+   const long rest = t >> 6;
+   const int q = (int)(rest % NQ);
+   const long blk = rest / NQ;
+   const int ipos = (int)(blk * 64 + lane);
+   if (ipos >= ne) { return; }
+   const int e = perm ? perm[ipos] : ipos;
+   const size_t eq = (size_t)e * NQ + q;
+   const double w = W[q];
+   v2d pr;
+   pr.x = w * coef_at(cd, eq, e);
+   pr.y = w * coef_at(cm, eq, e);
+   reinterpret_cast<v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane] = pr;
+   if (q != 0) { return; }
+   const double *X = enodes + (size_t)e * 24;
+   double c[2 * kTrilinPairs];
+#pragma unroll
+   for (int i = 0; i < 3; i++)
+   {
+      const double *x = X + i * 8;
+      c[0 * 3 + i] = x[1] - x[0];
+      c[1 * 3 + i] = x[2] - x[0];
+      c[2 * 3 + i] = x[4] - x[0];
+      c[3 * 3 + i] = (x[3] - x[2]) - (x[1] - x[0]);
+      c[4 * 3 + i] = (x[5] - x[4]) - (x[1] - x[0]);
+      c[5 * 3 + i] = (x[6] - x[4]) - (x[2] - x[0]);
+      c[6 * 3 + i] = ((x[7] - x[6]) - (x[5] - x[4])) - ((x[3] - x[2]) - (x[1] - x[0]));
+   }
+   c[21] = 0.0;
+   v2d *dst = reinterpret_cast<v2d *>(qd_geo + (size_t)blk * kTrilinPairs * 128) + lane;
+#pragma unroll
+   for (int k = 0; k < kTrilinPairs; k++) { dst[k * 64] = v2d{c[2 * k], c[2 * k + 1]}; }
+}
+
+// TRILINEAR -> BLOCKED: the full per-point qdata of a TRILINEAR form (for the diagonal, the
+// E-vector apply and the qdata export; the apply kernel evaluates the same algebra on the fly).
+template <int Q>
+__global__ void __launch_bounds__(256)
+k_trilinear_expand(int ne, const double *__restrict__ qd_geo, const double *__restrict__ qd_pair, const QPts qp,
+                   double *__restrict__ qd_diff, double *__restrict__ qd_mass)
+{
+   constexpr int NQ = Q * Q * Q;
+   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   const int lane = (int)(t & 63);
+   const long rest = t >> 6;
+   const int q = (int)(rest % NQ);
+   const long blk = rest / NQ;
+   if (blk * 64 + lane >= ne) { return; }
+   const double *cg = qd_geo + (size_t)blk * kTrilinPairs * 128 + lane * 2;
+   double c[2 * kTrilinPairs];
+#pragma unroll
+   for (int k = 0; k < kTrilinPairs; k++) { c[2 * k] = cg[k * 128]; c[2 * k + 1] = cg[k * 128 + 1]; }
+   auto cf = [&](int k, int i) { return c[3 * k + i]; };
+   const double xi = qp.x[q % Q], et = qp.x[(q / Q) % Q], zt = qp.x[q / (Q * Q)];
+   double J[3][3];
+#pragma unroll
+   for (int i = 0; i < 3; i++)
+   {
+      J[i][0] = (cf(0, i) + cf(4, i) * zt) + (cf(3, i) + cf(6, i) * zt) * et;
+      J[i][1] = (cf(1, i) + cf(5, i) * zt) + (cf(3, i) + cf(6, i) * zt) * xi;
+      J[i][2] = (cf(2, i) + cf(5, i) * et) + (cf(4, i) + cf(6, i) * et) * xi;
+   }
+   const double A11 = J[1][1] * J[2][2] - J[1][2] * J[2][1], A12 = J[2][1] * J[0][2] - J[0][1] * J[2][2],
+                A13 = J[0][1] * J[1][2] - J[1][1] * J[0][2];
+   const double A21 = J[2][0] * J[1][2] - J[1][0] * J[2][2], A22 = J[0][0] * J[2][2] - J[0][2] * J[2][0],
+                A23 = J[1][0] * J[0][2] - J[0][0] * J[1][2];
+   const double A31 = J[1][0] * J[2][1] - J[2][0] * J[1][1], A32 = J[2][0] * J[0][1] - J[0][0] * J[2][1],
+                A33 = J[0][0] * J[1][1] - J[0][1] * J[1][0];
+   const double det = J[0][0] * A11 + J[1][0] * A12 + J[2][0] * A13;
+   const v2d pr = reinterpret_cast<const v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane];
+   const double sc = pr.x / det;
+   v2d p0, p1, p2;
+   p0.x = sc * (A11 * A11 + A12 * A12 + A13 * A13);
+   p0.y = sc * (A11 * A21 + A12 * A22 + A13 * A23);
+   p1.x = sc * (A11 * A31 + A12 * A32 + A13 * A33);
+   p1.y = sc * (A21 * A21 + A22 * A22 + A23 * A23);
+   p2.x = sc * (A21 * A31 + A22 * A32 + A23 * A33);
+   p2.y = sc * (A31 * A31 + A32 * A32 + A33 * A33);
+   v2d *dst = reinterpret_cast<v2d *>(qd_diff + ((size_t)blk * NQ + q) * 3 * 128) + lane;
+   dst[0] = p0;
+   dst[64] = p1;
+   dst[128] = p2;
+   qd_mass[((size_t)blk * ((NQ + 1) / 2) + (q >> 1)) * 128 + lane * 2 + (q & 1)] = pr.y * det;
+}
+
 SetupCoef make_setup_coef(const CoeffDesc *c, const double *q)
 {
    SetupCoef s{};
@@ -475,6 +573,49 @@ bool jacobians_affine(int ne, int nq, const double *J, hipStream_t s)
    ECM2_HIP(hipMemcpyAsync(&h, flag.data(), sizeof(int), hipMemcpyDeviceToHost, s));
    ECM2_HIP(hipStreamSynchronize(s));
    return h == 0;
+}
+
+void setup_trilinear(const QLayout &L, int Q, const double *enodes, const double *W, const CoeffDesc *cm,
+                     const CoeffDesc *cd, const double *cm_q, const double *cd_q, double *qd_geo, double *qd_pair,
+                     hipStream_t s)
+{
+   if (L.ne == 0) { return; }
+   ECM2_VERIFY(L.kind == QLAYOUT_TRILINEAR && cm && cd && enodes, ERR_INTERNAL,
+               "trilinear setup needs a TRILINEAR layout, both coefficients and the corners");
+   ECM2_VERIFY(!L.pos || L.perm, ERR_INTERNAL, "blocked setup needs the inverse permutation");
+   const SetupCoef scm = make_setup_coef(cm, cm_q), scd = make_setup_coef(cd, cd_q);
+   const long n = (long)L.nblk() * 64 * L.nq;
+   if (Q == 3)
+   {
+      hipLaunchKernelGGL((k_setup_trilinear<3>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.perm, L.ne, enodes, W,
+                         scm, scd, qd_geo, qd_pair);
+   }
+   else if (Q == 4)
+   {
+      hipLaunchKernelGGL((k_setup_trilinear<4>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.perm, L.ne, enodes, W,
+                         scm, scd, qd_geo, qd_pair);
+   }
+   else { ECM2_VERIFY(false, ERR_UNSUPPORTED, "trilinear setup: Q1D " << Q << " not instantiated"); }
+   ECM2_HIP(hipGetLastError());
+}
+
+void trilinear_expand(const QLayout &L, int Q, const double *qd_geo, const double *qd_pair, const QPts &qp,
+                      double *qd_diff, double *qd_mass, hipStream_t s)
+{
+   if (L.ne == 0) { return; }
+   const long n = (long)L.nblk() * 64 * L.nq;
+   if (Q == 3)
+   {
+      hipLaunchKernelGGL((k_trilinear_expand<3>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.ne, qd_geo, qd_pair, qp,
+                         qd_diff, qd_mass);
+   }
+   else if (Q == 4)
+   {
+      hipLaunchKernelGGL((k_trilinear_expand<4>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.ne, qd_geo, qd_pair, qp,
+                         qd_diff, qd_mass);
+   }
+   else { ECM2_VERIFY(false, ERR_UNSUPPORTED, "trilinear expand: Q1D " << Q << " not instantiated"); }
+   ECM2_HIP(hipGetLastError());
 }
 
 void setup_affine(const QLayout &L, int Q, const double *enodes, const double *J, const double *W,

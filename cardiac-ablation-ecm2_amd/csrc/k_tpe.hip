@@ -313,14 +313,21 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 // RM: 0 every block map-addressed; 1 every block regular (treg rows, no flag read); 2 per block
 // (treg row flag [7], wave-uniform): a regular block's dofs are all owned (checked at setup),
 // so it addresses x / y only.
-template <int D, int Q, bool SPLIT, int RM>
+// TL (TRILINEAR layout, kernels.hpp): the element's trilinear-map coefficients instead of C,
+// and the point pair (W beta, W alpha); J, adj(J), det J evaluated at every point: per plane
+// (zeta) the J pieces A = c1 + c5 zeta, B = c4 + c7 zeta, Cz = c2 + c6 zeta, per row (eta)
+// J[.][0] = A + B eta, G = c3 + c6 eta, H = c5 + c7 eta, per point (xi) J[.][1] = Cz + B xi,
+// J[.][2] = G + H xi; then f = (W beta / det J) adj(J) (adj(J)^T grad u), m = W alpha det J u --
+// PADiffusionSetup3D's D = W beta adj(J) adj(J)^T / det J (bilininteg_diffusion_kernels.cpp:
+// 349-362) and the mass setup's W alpha det J, never stored.
+template <int D, int Q, bool SPLIT, int RM, bool TL = false>
 __global__ void __launch_bounds__(256, 1)
 k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
                const double *__restrict__ qdd, const double *__restrict__ qdm,
                const double *__restrict__ x, const double *__restrict__ xg,
                double *__restrict__ y, double *__restrict__ yg, const Basis1D b,
                const int *__restrict__ lane_flags, double *__restrict__ part, const int *__restrict__ treg,
-               int pstride, const int *__restrict__ lmap)
+               int pstride, const int *__restrict__ lmap, const QPts qp)
 {
    constexpr int ND = D * D * D, NQ = Q * Q * Q, NR = Q * Q, XR = XwaveRows<D>::R, WPG = 4;
    __shared__ double sX[WPG][XR][64];  // gathered x; then the cross-wave face exchange
@@ -342,12 +349,18 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
       // gather, so their latency overlaps the (treg ->) (map ->) x chain instead of following it
       // (one memory latency less per wave before the first row computes).
       auto ld2 = [&](const double *p) -> v2d { return __builtin_nontemporal_load(reinterpret_cast<const v2d *>(p)); };
-      v2d ce[3];
+      constexpr int NCE = TL ? kTrilinPairs : 3;
+      v2d ce[NCE];
       {
-         const double *qc = qdd + (size_t)blk * 3 * 128 + lane * 2;
+         const double *qc = qdd + (size_t)blk * NCE * 128 + lane * 2;
 #pragma unroll
-         for (int k = 0; k < 3; k++) { ce[k] = ld2(qc + k * 128); }
+         for (int k = 0; k < NCE; k++) { ce[k] = ld2(qc + k * 128); }
       }
+      // TL: coefficient c_{k+1} of coordinate i
+      auto cf = [&](int k, int i) -> double {
+         const int f = 3 * k + i;
+         return (f & 1) ? ce[f >> 1].y : ce[f >> 1].x;
+      };
       const double *qa = qdm + (size_t)blk * NQ * 128 + lane * 2;
       v2d ca[Q], na[Q];
       auto load_row = [&](int row, v2d (&aq)[Q]) {
@@ -358,7 +371,7 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
       // are in flight instead of 4 (profiles/r2_ab_pf2.txt: C4 kernel -4.3%); the plane loop is
       // unrolled so the rotation is static.  Map-addressed kernels (RM = 0) keep the ping-pong:
       // unrolled, their register demand exceeds 256 VGPRs; at p = 1 the third buffer costs a wave/SIMD.
-      constexpr bool PF2 = RM != 0 && D == 3;
+      constexpr bool PF2 = RM != 0 && D == 3 && !TL;  // TL: the runtime plane loop keeps the geometry live once
       v2d ra[PF2 ? 3 : 1][Q];
       if constexpr (PF2)
       {
@@ -414,6 +427,18 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
          double bz[D], gz[D];
 #pragma unroll
          for (int dz = 0; dz < D; dz++) { bz[dz] = b.B[qz + MQ * dz]; gz[dz] = b.G[qz + MQ * dz]; }
+         double pA[3], pB[3], pC[3];  // TL: the plane's J pieces
+         if constexpr (TL)
+         {
+            const double zt = qp.x[qz];
+#pragma unroll
+            for (int i = 0; i < 3; i++)
+            {
+               pA[i] = cf(0, i) + cf(4, i) * zt;
+               pB[i] = cf(3, i) + cf(6, i) * zt;
+               pC[i] = cf(1, i) + cf(5, i) * zt;
+            }
+         }
          // opaque lane index: the plane re-reads X from LDS instead of keeping 27 values live
          int ll = lane;
          asm volatile("" : "+v"(ll));
@@ -454,6 +479,18 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
             double T0[D], T1[D], T2[D];
 #pragma unroll
             for (int dx = 0; dx < D; dx++) { T0[dx] = 0.0; T1[dx] = 0.0; T2[dx] = 0.0; }
+            double ja[3], rG[3], rH[3];  // TL: the row's J[.][0] and J[.][2] pieces
+            if constexpr (TL)
+            {
+               const double et = qp.x[qy];
+#pragma unroll
+               for (int i = 0; i < 3; i++)
+               {
+                  ja[i] = pA[i] + pB[i] * et;
+                  rG[i] = cf(2, i) + cf(5, i) * et;
+                  rH[i] = cf(4, i) + cf(6, i) * et;
+               }
+            }
 #pragma unroll
             for (int qx = 0; qx < Q; qx++)
             {
@@ -468,10 +505,41 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                   uz += bq * Y10[dx];
                }
                const v2d sa = cur[qx];
-               const double m = sa.y * u;
-               const double fx = sa.x * (ce[0].x * ux + ce[0].y * uy + ce[1].x * uz);
-               const double fy = sa.x * (ce[0].y * ux + ce[1].y * uy + ce[2].x * uz);
-               const double fz = sa.x * (ce[1].x * ux + ce[2].x * uy + ce[2].y * uz);
+               double m, fx, fy, fz;
+               if constexpr (TL)
+               {
+                  const double xi = qp.x[qx];
+                  // J = [ja | jb | jc] (rows: coordinates), adj(J) rows A1., A2., A3.
+                  const double jb0 = pC[0] + pB[0] * xi, jb1 = pC[1] + pB[1] * xi, jb2 = pC[2] + pB[2] * xi;
+                  const double jc0 = rG[0] + rH[0] * xi, jc1 = rG[1] + rH[1] * xi, jc2 = rG[2] + rH[2] * xi;
+                  const double A11 = jb1 * jc2 - jc1 * jb2, A12 = jb2 * jc0 - jb0 * jc2, A13 = jb0 * jc1 - jb1 * jc0;
+                  const double A21 = ja[2] * jc1 - ja[1] * jc2, A22 = ja[0] * jc2 - jc0 * ja[2],
+                               A23 = ja[1] * jc0 - ja[0] * jc1;
+                  const double A31 = ja[1] * jb2 - ja[2] * jb1, A32 = ja[2] * jb0 - ja[0] * jb2,
+                               A33 = ja[0] * jb1 - jb0 * ja[1];
+                  const double det = ja[0] * A11 + ja[1] * A12 + ja[2] * A13;
+                  const double sc = sa.x / det;
+                  double t1 = A11 * ux;
+                  t1 += A21 * uy;
+                  t1 += A31 * uz;
+                  double t2 = A12 * ux;
+                  t2 += A22 * uy;
+                  t2 += A32 * uz;
+                  double t3 = A13 * ux;
+                  t3 += A23 * uy;
+                  t3 += A33 * uz;
+                  m = (sa.y * det) * u;
+                  fx = sc * (A11 * t1 + A12 * t2 + A13 * t3);
+                  fy = sc * (A21 * t1 + A22 * t2 + A23 * t3);
+                  fz = sc * (A31 * t1 + A32 * t2 + A33 * t3);
+               }
+               else
+               {
+                  m = sa.y * u;
+                  fx = sa.x * (ce[0].x * ux + ce[0].y * uy + ce[1].x * uz);
+                  fy = sa.x * (ce[0].y * ux + ce[1].y * uy + ce[2].x * uz);
+                  fz = sa.x * (ce[1].x * ux + ce[2].x * uy + ce[2].y * uz);
+               }
 #pragma unroll
                for (int dx = 0; dx < D; dx++)
                {
@@ -732,7 +800,7 @@ k_apply_tpe_pp(int ne, int blk_begin, int n_owned, const int *__restrict__ gmap,
 // (Gy Bz)^2, (By Gz)^2, Gy By Bz^2, By^2 Gz Bz, Gy By Gz Bz.  Output assembled and stored
 // exactly like the apply kernels' (in-wave faces, cross-wave faces on AFFINE, plain stores,
 // partial slots): every diagonal entry written once, deterministic, no memset.
-template <int D, int Q, bool MASS, bool DIFF, bool SPLIT, bool AFF>
+template <int D, int Q, bool MASS, bool DIFF, bool SPLIT, bool AFF, bool XWV = AFF>
 __global__ void __launch_bounds__(256)
 k_diag_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
            const double *__restrict__ qdd, const double *__restrict__ qdm, double *__restrict__ y,
@@ -741,11 +809,13 @@ k_diag_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restric
            const int *__restrict__ lmap)
 {
    constexpr int ND = D * D * D, NQ = Q * Q * Q, NQH = (NQ + 1) / 2, DD = D * D, XR = XwaveRows<D>::R, WPG = 4;
-   __shared__ double xb[AFF ? WPG * XR * 64 : 1];  // AFF: cross-wave face exchange (as the apply's plan)
+   // XWV: cross-wave face exchange, as the apply's plan (AFFINE; TRILINEAR forms, whose diagonal
+   // reads their full per-point qdata: AFF false, XWV true)
+   __shared__ double xb[XWV ? WPG * XR * 64 : 1];
    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
    const int blk = blk_begin + blockIdx.x * WPG + w;
    const bool wave_on = blk < blk_end;  // wave-uniform
-   if (!AFF && !wave_on) { return; }    // no block-wide barrier without AFF
+   if (!XWV && !wave_on) { return; }    // no block-wide barrier without the exchange
    const bool active = wave_on && blk * 64 + lane < ne;
    const int *mp = gmap + (size_t)blk * ND * 64 + lane;
    const double *qd = qdd + (size_t)blk * NQ * 3 * 128 + lane * 2;
@@ -836,7 +906,7 @@ k_diag_tpe(int ne, int blk_begin, int blk_end, int n_owned, const int *__restric
       rg = TpeReg{r[0], r[1], r[2], r[3], r[4]};
       regf = r[7];
    }
-   tpe_assemble_store<D, SPLIT, false, AFF, true>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0, blk,
+   tpe_assemble_store<D, SPLIT, false, XWV, true>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0, blk,
                                                   lane, active, n_owned, y, yg, part, xb, w, wave_on, rg, regf,
                                                   pstride, lmap ? lmap + (size_t)blk * tpe_lattice_points(D) : nullptr);
 }
@@ -846,6 +916,22 @@ void launch_tpe(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipS
 {
    const int nb = a.blk_end - a.blk_begin;
    const dim3 grid((nb + 3) / 4), block(256);
+   if (a.kind == QLAYOUT_TRILINEAR)
+   {
+      if constexpr (MASS && DIFF)
+      {
+#define ECM2_TL(RM)                                                                                           \
+   hipLaunchKernelGGL((k_apply_tpe_sf<D, Q, SPLIT, RM, true>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end,   \
+                      a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part, a.treg,   \
+                      a.part_stride, a.lmap, a.qp)
+         if (a.treg && a.treg_all) { ECM2_TL(1); }
+         else if (a.treg) { ECM2_TL(2); }
+         else { ECM2_TL(0); }
+#undef ECM2_TL
+      }
+      else { ECM2_VERIFY(false, ERR_INTERNAL, "TRILINEAR qdata needs both integrators"); }
+      return;
+   }
    if (a.kind == QLAYOUT_AFFINE)
    {
       if constexpr (MASS && DIFF)
@@ -861,7 +947,7 @@ void launch_tpe(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipS
 #define ECM2_SF(RM)                                                                                           \
    hipLaunchKernelGGL((k_apply_tpe_sf<D, Q, SPLIT, RM>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end, a.n_owned, \
                       a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part, a.treg, a.part_stride, \
-                      a.lmap)
+                      a.lmap, a.qp)
             if (a.treg && a.treg_all) { ECM2_SF(1); }
             else if (a.treg) { ECM2_SF(2); }
             else { ECM2_SF(0); }
@@ -898,14 +984,26 @@ void launch_diag_tpe(const ApplyArgs &a, const Basis1D &b, const double *drow, h
    const int nb = a.blk_end - a.blk_begin;
    if (nb <= 0) { return; }
    const dim3 grid((nb + 3) / 4), block(256);
-#define ECM2_DIAG(SP, AF)                                                                                \
-   hipLaunchKernelGGL((k_diag_tpe<D, Q, MASS, DIFF, SP, AF>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end, \
-                      a.n_owned, a.gmap, a.qdd, a.qdm, a.y, a.yg, b, drow, a.lane_flags, a.part,            \
-                      AF ? a.treg : nullptr, a.part_stride, AF ? a.lmap : nullptr)
+#define ECM2_DIAG(SP, AF, XV)                                                                            \
+   hipLaunchKernelGGL((k_diag_tpe<D, Q, MASS, DIFF, SP, AF, XV>), grid, block, 0, s, a.ne, a.blk_begin,        \
+                      a.blk_end, a.n_owned, a.gmap, a.qdd, a.qdm, a.y, a.yg, b, drow, a.lane_flags, a.part,  \
+                      XV ? a.treg : nullptr, a.part_stride, XV ? a.lmap : nullptr)
    const bool aff = a.kind == QLAYOUT_AFFINE;
+   // a.xwave: the plan was built with cross-wave faces (AFFINE or TRILINEAR forms)
+   const bool xw = aff || a.xwave;
    ECM2_VERIFY(!aff || (MASS && DIFF), ERR_INTERNAL, "AFFINE qdata needs both integrators");
-   if (a.yg) { if (aff) { ECM2_DIAG(true, true); } else { ECM2_DIAG(true, false); } }
-   else { if (aff) { ECM2_DIAG(false, true); } else { ECM2_DIAG(false, false); } }
+   if (a.yg)
+   {
+      if (aff) { ECM2_DIAG(true, true, true); }
+      else if (xw) { ECM2_DIAG(true, false, true); }
+      else { ECM2_DIAG(true, false, false); }
+   }
+   else
+   {
+      if (aff) { ECM2_DIAG(false, true, true); }
+      else if (xw) { ECM2_DIAG(false, false, true); }
+      else { ECM2_DIAG(false, false, false); }
+   }
 #undef ECM2_DIAG
 }
 

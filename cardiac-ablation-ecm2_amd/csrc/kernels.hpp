@@ -35,7 +35,24 @@
 namespace ecm2
 {
 
-enum QLayoutKind : int { QLAYOUT_NATIVE = 0, QLAYOUT_BLOCKED = 1, QLAYOUT_AFFINE = 2, QLAYOUT_AFFINE_E = 3 };
+enum QLayoutKind : int { QLAYOUT_NATIVE = 0, QLAYOUT_BLOCKED = 1, QLAYOUT_AFFINE = 2, QLAYOUT_AFFINE_E = 3,
+                         QLAYOUT_TRILINEAR = 4 };
+// TRILINEAR (fused thread-per-element kernel, p <= 2, both integrators, geometry from element
+// corners, elements NOT all parallelepipeds): the geometry is stored once per element as the
+// coefficients of its trilinear map x_i(xi, eta, zeta) = c0 + c1 xi + c2 eta + c3 zeta +
+// c4 xi eta + c5 xi zeta + c6 eta zeta + c7 xi eta zeta (the expansion of GeometricFactors'
+// sum over the corners, mesh.cpp:15220-15273), and the kernel evaluates J, adj(J), det J at
+// each quadrature point (PADiffusionSetup3D's algebra, bilininteg_diffusion_kernels.cpp:
+// 349-362): qd_diff = [blk][11 pairs][lane][2] holding c1..c7 of x, y, z (index 3 (k - 1) + i,
+// padded to 22), qd_mass = [blk][q][lane][2] = (W_q beta_q, W_q alpha_q).  16 B per point +
+// 176 B per element instead of 56 B per point: the bytes of the AFFINE layout on a general
+// trilinear mesh, for ~55 extra FP64 operations per point.
+constexpr int kTrilinPairs = 11;
+// 1D Gauss-Legendre points on [0, 1] (kernel argument: scalar loads)
+struct QPts
+{
+   double x[MAX_Q1D];
+};
 
 constexpr int kElemBlock = 64;  // elements per wave in the blocked layout
 
@@ -49,18 +66,19 @@ struct QLayout
    {
       if (kind == QLAYOUT_NATIVE) { return (size_t)ne * 6 * nq; }
       if (kind == QLAYOUT_AFFINE) { return (size_t)nblk() * 6 * kElemBlock; }
+      if (kind == QLAYOUT_TRILINEAR) { return (size_t)nblk() * 2 * kTrilinPairs * kElemBlock; }
       if (kind == QLAYOUT_AFFINE_E) { return (size_t)ne * 6; }
       return (size_t)nblk() * nq * 6 * kElemBlock;
    }
    size_t mass_size() const
    {
       if (kind == QLAYOUT_NATIVE) { return (size_t)ne * nq; }
-      if (kind == QLAYOUT_AFFINE) { return (size_t)nblk() * nq * 2 * kElemBlock; }
+      if (kind == QLAYOUT_AFFINE || kind == QLAYOUT_TRILINEAR) { return (size_t)nblk() * nq * 2 * kElemBlock; }
       if (kind == QLAYOUT_AFFINE_E) { return (size_t)ne * nq * 2; }
       return (size_t)nblk() * ((nq + 1) / 2) * 2 * kElemBlock;
    }
    int nblk() const { return (ne + kElemBlock - 1) / kElemBlock; }
-   bool blocked() const { return kind == QLAYOUT_BLOCKED || kind == QLAYOUT_AFFINE; }
+   bool blocked() const { return kind == QLAYOUT_BLOCKED || kind == QLAYOUT_AFFINE || kind == QLAYOUT_TRILINEAR; }
    bool affine() const { return kind == QLAYOUT_AFFINE || kind == QLAYOUT_AFFINE_E; }
 };
 
@@ -116,6 +134,8 @@ struct ApplyArgs
    int treg_all = 0;                // every block regular
    int part_stride = 0;             // p <= 2 partial slots per block (27 * 64, or the lattice surface when treg_all)
    const int *lmap = nullptr;       // device [blk][tpe_lattice_points]: lattice-slot blocks' lattice maps, or null
+   QPts qp = {};                    // TRILINEAR: the quadrature points
+   int xwave = 0;                   // the merge plan has cross-wave faces (AFFINE / TRILINEAR forms)
    const int *gmap = nullptr;
    const double *qdd = nullptr, *qdm = nullptr;
    const double *x = nullptr, *xg = nullptr;
@@ -218,6 +238,13 @@ void setup_from_nodes(const QLayout &L, int Q, const double *enodes, const doubl
 void setup_affine(const QLayout &L, int Q, const double *enodes, const double *J, const double *W,
                   const CoeffDesc *cm, const CoeffDesc *cd, const double *cm_q, const double *cd_q,
                   double *qd_fac, double *qd_pair, hipStream_t s);
+// TRILINEAR layout (see above) from lexicographic element corners; both coefficients.
+void setup_trilinear(const QLayout &L, int Q, const double *enodes, const double *W, const CoeffDesc *cm,
+                     const CoeffDesc *cd, const double *cm_q, const double *cd_q, double *qd_geo, double *qd_pair,
+                     hipStream_t s);
+// The BLOCKED per-point qdata of a TRILINEAR form (L: its layout; outputs sized as BLOCKED).
+void trilinear_expand(const QLayout &L, int Q, const double *qd_geo, const double *qd_pair, const QPts &qp,
+                      double *qd_diff, double *qd_mass, hipStream_t s);
 // Every element's Jacobian the same at all its points (1e-13 relative; synchronises s).
 bool jacobians_affine(int ne, int nq, const double *J, hipStream_t s);
 // qdata from MFEM-layout Jacobians J(q,i,j,e) (GeometricFactors::JACOBIANS).

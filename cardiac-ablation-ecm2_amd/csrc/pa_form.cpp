@@ -507,6 +507,12 @@ void PAForm::assemble(hipStream_t s)
       if (resolved_mode_ == KERNEL_TPE) { layout_.kind = QLAYOUT_AFFINE; }
       else if (resolved_mode_ == KERNEL_LINE) { layout_.kind = QLAYOUT_AFFINE_E; }
    }
+   else if (!affine && compress_ && have_mass_ && have_diff_ && resolved_mode_ == KERNEL_TPE && !jac_ &&
+            enodes_.size())
+   {
+      // general trilinear hexes from corners: geometry per element, J evaluated per point
+      layout_.kind = QLAYOUT_TRILINEAR;
+   }
 
    // the merge plan (cross-wave faces), the regular blocks and the partial-slot layout belong
    // to the qdata layout they were built for
@@ -551,7 +557,7 @@ void PAForm::assemble(hipStream_t s)
          for (int sp : splits_) { seg.push_back(std::max(0, std::min(nblk, sp))); }
          std::sort(seg.begin(), seg.end());
          seg.erase(std::unique(seg.begin(), seg.end()), seg.end());
-         const bool xw = layout_.kind == QLAYOUT_AFFINE;
+         const bool xw = layout_.kind == QLAYOUT_AFFINE || layout_.kind == QLAYOUT_TRILINEAR;
          for (size_t k = 0; k + 1 < seg.size(); k++)
          {
             const bool lat = latency_from_ >= 0 && seg[k] >= latency_from_;
@@ -589,7 +595,7 @@ void PAForm::assemble(hipStream_t s)
       lmap_.resize(0);
       const int ns = tpe_surface_points(D_);
       std::vector<char> breg_ok(nblk, 0);
-      if (layout_.kind == QLAYOUT_AFFINE)
+      if (layout_.kind == QLAYOUT_AFFINE || layout_.kind == QLAYOUT_TRILINEAR)
       {
          const int L = 4 * (D_ - 1);
          std::vector<int> reg((size_t)nblk * 8, 0);
@@ -972,6 +978,11 @@ void PAForm::assemble(hipStream_t s)
       kern::setup_affine(layout_, Q_, jac_ ? nullptr : enodes_.data(), jac_, W_.data(), cm, cd, cm_q, cd_q,
                          qd_diff_.data(), qd_mass_.data(), s);
    }
+   else if (layout_.kind == QLAYOUT_TRILINEAR)
+   {
+      kern::setup_trilinear(layout_, Q_, enodes_.data(), W_.data(), cm, cd, cm_q, cd_q, qd_diff_.data(),
+                            qd_mass_.data(), s);
+   }
    else if (jac_)
    {
       kern::setup_from_jacobians(layout_, jac_, W_.data(), cm, cd, cm_q, cd_q, qd_diff_.data(),
@@ -1143,6 +1154,8 @@ ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, doubl
    a.treg = treg_.size() ? treg_.data() : nullptr;
    a.treg_all = treg_all_ ? 1 : 0;
    a.lmap = lmap_.size() ? lmap_.data() : nullptr;
+   for (int q = 0; q < Q_ && q < MAX_Q1D; q++) { a.qp.x[q] = maps_.qpts[q]; }
+   a.xwave = (layout_.kind == QLAYOUT_AFFINE || layout_.kind == QLAYOUT_TRILINEAR) ? 1 : 0;
    a.part_stride = part_stride_;
    a.gmap = (resolved_mode_ == KERNEL_TPE) ? gmap_blk_.data()
             : (resolved_mode_ == KERNEL_LINE) ? gmap_line_.data() : gmap_.data();
@@ -1208,13 +1221,38 @@ void PAForm::assemble_diagonal(double *diag, hipStream_t s)
       double *dg = n_owned_ < ndofs_ ? diag + n_owned_ : nullptr;
       if (!use_partials()) { ECM2_HIP(hipMemsetAsync(diag, 0, sizeof(double) * (size_t)ndofs_, s)); }
       ApplyArgs a = apply_args(nullptr, nullptr, diag, dg, 0, layout_.nblk());
+      DeviceArray<double> fd, fm;
+      if (layout_.kind == QLAYOUT_TRILINEAR)
+      {
+         expand_trilinear(fd, fm, s);  // per-point qdata for the diagonal's tables
+         a.kind = QLAYOUT_BLOCKED;
+         a.qdd = fd.data();
+         a.qdm = fm.data();
+      }
       kern::diagonal_tpe(D_, Q_, have_mass_, have_diff_, a, basis_, drowtab_.data(), s);
       finish_shared(0, n_sh_, diag, dg, s);
+      if (fd.size()) { ECM2_HIP(hipStreamSynchronize(s)); }  // the temporaries are freed on return
       return;
    }
    ECM2_HIP(hipMemsetAsync(diag, 0, sizeof(double) * (size_t)ndofs_, s));
    kern::diagonal(layout_.pos, D_, Q_, layout_.kind, ne_, gmap_.data(), have_diff_ ? qd_diff_.data() : nullptr,
                   have_mass_ ? qd_mass_.data() : nullptr, diag, false, basis_, btab_.data(), s);
+}
+
+void PAForm::expand_trilinear(DeviceArray<double> &fd, DeviceArray<double> &fm, hipStream_t s) const
+{
+   QLayout L = layout_;
+   L.kind = QLAYOUT_BLOCKED;
+   fd.resize(std::max<size_t>(1, have_diff_ ? L.diff_size() : 0));
+   fm.resize(std::max<size_t>(1, have_mass_ ? L.mass_size() : 0));
+   if (ne_ % kElemBlock)
+   {
+      ECM2_HIP(hipMemsetAsync(fd.data(), 0, fd.bytes(), s));
+      ECM2_HIP(hipMemsetAsync(fm.data(), 0, fm.bytes(), s));
+   }
+   QPts qp = {};
+   for (int q = 0; q < Q_ && q < MAX_Q1D; q++) { qp.x[q] = maps_.qpts[q]; }
+   kern::trilinear_expand(layout_, Q_, qd_diff_.data(), qd_mass_.data(), qp, fd.data(), fm.data(), s);
 }
 
 void PAForm::restriction_mult(const double *x, double *xe, hipStream_t s)
@@ -1235,7 +1273,16 @@ void PAForm::integrator_add_mult(int kind, const double *xe, double *ye, hipStre
                ERR_ARG, "integrator " << kind << " not present");
    ApplyArgs a = apply_args(xe, nullptr, ye, nullptr, 0, layout_.nblk());
    a.gmap = gmap_.data();
+   DeviceArray<double> fd, fm;
+   if (layout_.kind == QLAYOUT_TRILINEAR)
+   {
+      expand_trilinear(fd, fm, s);
+      a.kind = QLAYOUT_BLOCKED;
+      a.qdd = fd.data();
+      a.qdm = fm.data();
+   }
    kern::apply_wpe(D_, Q_, kind == INTEG_MASS, kind == INTEG_DIFFUSION, a, true, true, basis_, s);
+   if (fd.size()) { ECM2_HIP(hipStreamSynchronize(s)); }
 }
 
 void PAForm::get_qdata(int kind, double *out, hipStream_t s)
@@ -1244,7 +1291,10 @@ void PAForm::get_qdata(int kind, double *out, hipStream_t s)
    const bool diff = kind == INTEG_DIFFUSION;
    ECM2_VERIFY(diff ? have_diff_ : have_mass_, ERR_ARG, "integrator " << kind << " not present");
    const bool aff = layout_.affine();
-   DeviceArray<double> &src = (diff && !aff) ? qd_diff_ : qd_mass_;
+   DeviceArray<double> fd, fm;
+   const bool tl = layout_.kind == QLAYOUT_TRILINEAR;
+   if (tl) { expand_trilinear(fd, fm, s); }  // decoded as BLOCKED below
+   DeviceArray<double> &src = tl ? (diff ? fd : fm) : ((diff && !aff) ? qd_diff_ : qd_mass_);
    std::vector<double> h(src.size()), hc(aff ? qd_diff_.size() : 0);
    if (src.size())
    {

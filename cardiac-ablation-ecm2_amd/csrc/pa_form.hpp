@@ -91,7 +91,10 @@ public:
    // instead of reading the map
    int lattice_units() const
    {
-      if (resolved_mode_ == KERNEL_TPE) { return layout_.kind == QLAYOUT_AFFINE ? n_treg_ : 0; }
+      if (resolved_mode_ == KERNEL_TPE)
+      {
+         return (layout_.kind == QLAYOUT_AFFINE || layout_.kind == QLAYOUT_TRILINEAR) ? n_treg_ : 0;
+      }
       return (resolved_mode_ == KERNEL_LINE && breg_.size()) ? n_bricks_ : 0;
    }
    int n_units() const { return resolved_mode_ == KERNEL_TPE ? layout_.nblk() : n_bricks_; }
@@ -169,6 +172,8 @@ private:
                           const std::vector<int> &hslot, hipStream_t s);
    ApplyArgs apply_args(const double *x, const double *xg, double *y, double *yg, int b0,
                         int b1) const;
+   // TRILINEAR forms: their per-point qdata in the BLOCKED layout (temporaries of the caller)
+   void expand_trilinear(DeviceArray<double> &fd, DeviceArray<double> &fm, hipStream_t s) const;
 
  public:
    void record_start_public(hipStream_t s) { record_start(s); }

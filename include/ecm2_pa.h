@@ -155,6 +155,11 @@ int ecm2_pa_form_set_jacobians(ecm2_pa_form *f, const double *J);
 #define ECM2_QLAYOUT_BLOCKED 1
 #define ECM2_QLAYOUT_AFFINE 2
 #define ECM2_QLAYOUT_AFFINE_E 3  /* the same compression for the p >= 3 line / brick kernels */
+/* TRILINEAR (p <= 2, geometry from corners, both integrators, elements not all parallelepipeds):
+ * the element's trilinear-map coefficients once per element plus one (W beta, W alpha) pair per
+ * point; the fused kernel evaluates J, adj(J) and det J at every quadrature point (the
+ * reference's setup algebra, never stored): the AFFINE layout's bytes on a general mesh. */
+#define ECM2_QLAYOUT_TRILINEAR 4
 int ecm2_pa_form_set_geometry_compression(ecm2_pa_form *f, int on);
 /* BilinearForm::AddDomainIntegrator(new MassIntegrator(Q)) / DiffusionIntegrator(Q)
  * (bilinearform.cpp:231-242).  data: CONSTANT -> data[0] (host);

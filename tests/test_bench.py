@@ -61,7 +61,7 @@ def test_bench_single_gpu_line():
     assert b["config"]["numbering"].startswith("structured") and b["config"]["mesh"] == "affine"
     # the same run's variants: the reference's numbering (same layout) and a trilinear mesh (per-point qdata)
     assert b["entity_numbering"]["value"] > 0 and b["entity_numbering"]["qdata_layout"] == "affine"
-    assert b["trilinear"]["value"] > 0 and b["trilinear"]["qdata_layout"] == "blocked"
+    assert b["trilinear"]["value"] > 0 and b["trilinear"]["qdata_layout"] == "trilinear"
     e = run_bench(*SMALL, "--numbering", "entity", "--variants", "0")
     assert e["config"]["numbering"].startswith("entity") and "entity_numbering" not in e
 

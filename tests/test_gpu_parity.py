@@ -472,13 +472,16 @@ def test_affine_geometry_layout(mesh_name, order, compress):
     chosen exactly for parallelepiped meshes with both integrators -- blocked for the p <= 2
     thread-per-element kernel, element-ordered (AFFINE_E) for the p >= 3 line / brick
     kernels -- and the operator, its diagonal and the reference-layout qdata match the
-    oracle either way; non-affine (trilinear) elements keep the full per-point layout."""
+    oracle either way; non-affine (trilinear) elements get the TRILINEAR layout at p <= 2 (map
+    coefficients per element, J evaluated per point) and the full per-point layout at p >= 3."""
     m = make_mesh(mesh_name)
     fes, form, op = build_pair(m, order, "bio_a", "fn", compress_geometry=compress)
     affine = mesh_name != "trilinear" and AFFINE_ON
     nq = (order + 2) ** 3
     if order <= 2:
         want = E.QLAYOUT_AFFINE if (affine and compress) else E.QLAYOUT_BLOCKED
+        if mesh_name == "trilinear" and compress:
+            want = E.QLAYOUT_TRILINEAR
     else:
         want = E.QLAYOUT_AFFINE_E if (affine and compress) else E.QLAYOUT_NATIVE
     assert form.info()["layout"] == want
@@ -486,6 +489,8 @@ def test_affine_geometry_layout(mesh_name, order, compress):
         assert form.qdata_bytes() == 8 * 64 * ((fes.ne + 63) // 64) * (6 + 2 * nq)
     elif want == E.QLAYOUT_AFFINE_E:
         assert form.qdata_bytes() == 8 * fes.ne * (6 + 2 * nq)
+    elif want == E.QLAYOUT_TRILINEAR:
+        assert form.qdata_bytes() == 8 * 64 * ((fes.ne + 63) // 64) * (22 + 2 * nq)
     x = np.random.default_rng(41).uniform(-1, 1, fes.ndofs)
     y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
     form.Mult(dev(x), y)
@@ -588,3 +593,53 @@ def test_attribute_marker_errors():
     m.SetAttributes(np.full(m.GetNE(), 2))
     with pytest.raises(E.ECM2Error):
         form.Assemble()
+
+
+@pytest.mark.parametrize("order", [1, 2])
+@pytest.mark.parametrize("mesh_name", ["trilinear", "trilinear_big"])
+@pytest.mark.parametrize("numbering", [E.NUMBERING_STRUCTURED, E.NUMBERING_ENTITY])
+def test_trilinear_layout_on_the_fly_geometry(order, mesh_name, numbering):
+    """TRILINEAR layout (general trilinear hexes, p <= 2): the fused kernel evaluates J, adj(J)
+    and det J at every point from the element's map coefficients -- the operator, the diagonal,
+    the E-vector integrator applies and the reference-layout qdata all match the oracle's
+    setup + apply (bilininteg_diffusion_kernels.cpp:243-367, bilininteg_mass_pa.cpp:62-78),
+    on lattice-addressed and map-addressed blocks, and with an attribute marker."""
+    if mesh_name == "trilinear":
+        m = make_mesh("trilinear")
+    else:
+        m = E.Mesh.MakeCartesian3D(8, 8, 9, 1.0, 1.0, 9 / 8)  # complete 4x4x4 bricks + a ragged layer
+        V = m.vertices()
+        inner = np.all((V > 1e-9) & (V < np.array([1.0, 1.0, 9 / 8]) - 1e-9), axis=1)
+        V[inner] += 0.03 * np.random.default_rng(8).uniform(-1, 1, (int(inner.sum()), 3))
+        m.set_vertices(V)
+    fes, form, op = build_pair(m, order, "bio_a", "fn", numbering=numbering)
+    assert form.info()["layout"] == E.QLAYOUT_TRILINEAR
+    x = np.random.default_rng(5).uniform(-1, 1, fes.ndofs)
+    y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+    form.Mult(dev(x), y)
+    assert relerr(host(y), op.mult(x)) <= RTOL
+    d = torch.empty_like(y)
+    form.AssembleDiagonal(d)
+    assert relerr(host(d), op.diagonal()) < 1e-13
+    assert relerr(form.qdata(E.DIFFUSION), op.D) < 1e-13
+    assert relerr(form.qdata(E.MASS)[:, 0, :], op.M) < 1e-13
+    xe = np.random.default_rng(6).uniform(-1, 1, (fes.ne, fes.nd))
+    ye = torch.zeros(fes.ne * fes.nd, dtype=torch.float64, device="cuda")
+    form.IntegratorAddMultPA(E.DIFFUSION, dev(xe), ye)
+    assert relerr(host(ye).reshape(fes.ne, fes.nd), O.diffusion_apply(op.B, op.G, op.D, xe)) <= RTOL
+    if mesh_name == "trilinear_big":
+        lat, units, _ = form.AddressingInfo()
+        if numbering == E.NUMBERING_STRUCTURED:
+            assert lat > 0  # lattice-addressed blocks run the TRILINEAR kernel too
+        m.SetAttributes(1 + np.arange(m.GetNE()) % 2)
+        f2 = E.BilinearForm(fes)
+        en = m.element_nodes()
+        P = O.quad_points(en, O.default_q1d(order))
+        a, c = alpha_bioheat(P), coeff_function(P)
+        f2.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(a.reshape(fes.ne, -1)))), [0, 1])
+        f2.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(dev(c.reshape(fes.ne, -1)))))
+        f2.Assemble()
+        assert f2.info()["layout"] == E.QLAYOUT_TRILINEAR
+        f2.Mult(dev(x), y)
+        opm = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=a, beta=c)
+        assert relerr(host(y), opm.mult_markers(x, m.GetAttributes(), mass_marker=[0, 1])) <= RTOL

@@ -521,11 +521,11 @@ void par_group_mult_member(std::vector<ParPAForm *> &forms, const std::vector<co
       }
       ECM2_VERIFY(m && m->count == t.count, ERR_INTERNAL, "exchange schedules of ranks " << r << " and " << t.peer
                                                                                        << " do not match");
-      ECM2_VERIFY(m->buf == XBUF_X_TRUE, ERR_UNSUPPORTED, "member Mult: rank " << t.peer
-                                                          << " sends through its pack buffer (z-slabs only)");
    }
    if (f.serial())
    {
+      // the rank's own pack (its sends); the peers' packed sends are as their last group Mult left them
+      if (f.pack_needed()) { kern::gather_idx((int)f.part().send_idx.size(), f.send_idx_data(), x[r], f.sendbuf_data(), s); }
       group_copies(forms, x, false, s, r);
       f.stage_serial_apply(x[r], y[r], s);  // RAP: + the ghost dofs' sums
       // RAP: the P^T receive copies the peers' ghost contributions -- their y ghost blocks as

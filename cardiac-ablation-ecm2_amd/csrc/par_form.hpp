@@ -123,10 +123,11 @@ void par_group_mult(std::vector<ParPAForm *> &forms, const std::vector<const dou
 void par_group_diagonal(std::vector<ParPAForm *> &forms, const std::vector<double *> &d, hipStream_t s);
 // One member's rows of the group operator, y[r] = (A x)_r: member r's stages alone, exactly as
 // one rank of the RCCL transport runs them (interior on s, exchange + boundary on r's comm
-// stream, then the summation), its ghost values copied from the peers' x; sends straight from
-// x (z-slabs).  RAP (serial schedule): + the ghost sums and the P^T receive, copied from the
-// peers' y ghost blocks as the last group Mult left them.  The other members' y are not
-// touched.  This is what a rank's Mult costs on its own GPU, short of the xGMI transfer time.
+// stream, then the summation), its ghost values copied from the peers' x (or, for packed sends,
+// their send buffers as the last group Mult left them).  RAP (serial schedule): + the ghost sums
+// and the P^T receive, copied from the peers' y ghost blocks as the last group Mult left them.
+// The other members' y are not touched.  This is what a rank's Mult costs on its own GPU, short
+// of the xGMI transfer time.  Run one group Mult on the same x first.
 void par_group_mult_member(std::vector<ParPAForm *> &forms, const std::vector<const double *> &x,
                            const std::vector<double *> &y, int r, hipStream_t s);
 

@@ -407,10 +407,10 @@ int ecm2_par_group_mult_rccl(ecm2_par_form *const *forms, int n, const double *c
  * GPU; no reference counterpart): y_true[member] = (A x)[member's true dofs], running exactly
  * the stages one RCCL rank runs (interior elements on `stream`, the P exchange -- here device
  * copies from the peers' x -- and the boundary elements on the member's comm stream, then the
- * shared-dof sums).  Sends straight from x (z-slabs); the other members' y are not written.
- * RAP (serial schedule): the P^T receive copies the peers' ghost contributions as their last
+ * shared-dof sums); the other members' y are not written.  Packed sends (non-slab partitions)
+ * and, with RAP (serial schedule), the P^T receive copy the peers' buffers as their last
  * ecm2_par_group_mult left them (run one group Mult on the same x first).
- * ECM2_ERR_UNSUPPORTED otherwise. */
+ * ECM2_ERR_UNSUPPORTED otherwise (RAP with the overlapped schedule). */
 int ecm2_par_group_mult_member(ecm2_par_form *const *forms, int n, int member, const double *const *x_true,
                                double *const *y_true, void *stream);
 /* ParBilinearForm::AssembleDiagonal on the true dofs (local PA diagonal + P^T). */

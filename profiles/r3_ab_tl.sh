@@ -8,4 +8,6 @@ timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeou
 rc=$?
 tail -3 "$O/pytest_gpu.log"; grep -E "FAILED|ERROR" "$O/pytest_gpu.log" | head -20
 bash profiles/ab_libs.sh tl_c4t "libecm2pa_c.so libecm2pa_d.so libecm2pa_e.so" --workload c4 --steps 30 --warmup 5 --variants 0 --mesh trilinear || exit $?
-exit $rc
+
+bash profiles/r3_member_emul.sh
+[ $rc -eq 0 ] || exit $rc

@@ -606,3 +606,40 @@ def test_gpu_loopback_group_attribute_markers(decomp):
     cg = coeff_function(O.quad_points(m.element_nodes(), q1d))
     op = O.OracleOperator(m.element_nodes(), fes.gather_map(), fes.ndofs, order, alpha=cg, beta=cg)
     assert relerr(y, op.mult_markers(xg, attr, mass_marker=[0, 1])) <= RTOL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("decomp", ["overlap", "rap"])
+def test_gpu_group_member_rows_boxes(decomp):
+    """Member emulation on a 2 x 2 x 2 box partition (packed sends, 7 neighbours per rank): each
+    member's rows alone equal the serial oracle's, after one group Mult on the same x."""
+    import torch
+    m = E.Mesh.MakeCartesian3D(8, 8, 8)
+    m.set_vertices(nonaligned(m.vertices()))
+    fes = E.H1Space(m, 2, E.NUMBERING_STRUCTURED)
+    er = E.partition_boxes(m, (2, 2, 2))
+    q1d = O.default_q1d(2)
+    forms, xs, ys, parts = [], [], [], []
+    xg = np.random.default_rng(12).uniform(-1, 1, fes.ndofs)
+    for r in range(8):
+        part = E.Partition(fes, er, r, 8, decomposition=decomp)
+        pf = E.ParBilinearForm(part)
+        c = torch.as_tensor(coeff_function(E.quadrature_points_subset(m, q1d, part.elems)).reshape(part.ne_local, -1))
+        pf.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(c.cuda())))
+        pf.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(c.cuda())))
+        pf.Assemble()
+        forms.append(pf)
+        parts.append(part)
+        xs.append(torch.as_tensor(xg[part.owned_global]).cuda())
+        ys.append(torch.full((part.n_owned,), float("nan"), dtype=torch.float64, device="cuda"))
+    cg = coeff_function(O.quad_points(m.element_nodes(), q1d))
+    ref = O.OracleOperator(m.element_nodes(), fes.gather_map(), fes.ndofs, 2, alpha=cg, beta=cg).mult(xg)
+    group = E.ParGroup(forms)
+    group.Mult(xs, ys)
+    torch.cuda.synchronize()
+    for yt in ys:
+        yt.fill_(float("nan"))
+    for r in range(8):
+        group.MultMember(r, xs, ys)
+        torch.cuda.synchronize()
+        assert relerr(ys[r].cpu().numpy(), ref[parts[r].owned_global]) <= RTOL

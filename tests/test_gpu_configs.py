@@ -132,7 +132,8 @@ def test_c3_fichera_pennes_pcg(jacobi):
 def test_c3_full_size():
     """configs[2] at the bench size: fichera.mesh refined 6x (1.84M elements, 14.9M DoF), p = 2,
     default path (face-linked bricks, cross-wave merge), heat capacity as a quadrature coefficient
-    and k(T) from an H1 temperature field re-assembled on the device, against the oracle."""
+    and k(T) from an H1 temperature field re-assembled on the device, against the oracle: the
+    Mult, and 8 iterations of the constrained Jacobi-PCG the bench times."""
     m = fichera(6)
     order, q1d = 2, O.default_q1d(2)
     fes = E.H1Space(m, order)
@@ -152,10 +153,19 @@ def test_c3_full_size():
     y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
     form.Mult(dev(x), y)
     yh = host(y)
-    del form, y
+    del y
     beta = BH.affine_law(BH.temperature_at_quadrature(T, fes.gather_map(), order, q1d), scale, slope, tref)
     op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=a, beta=beta)
     assert relerr(yh, op.mult(x)) <= RTOL
+    # the bench's C3 solve at full size: constrained Jacobi-PCG, a fixed 8 iterations (rel_tol 0)
+    # on both sides (CGSolver::Mult, solvers.cpp:869-1004, with ConstrainedOperator DIAG_ONE)
+    ess = fes.boundary_dofs()
+    b = np.random.default_rng(2).uniform(-1, 1, fes.ndofs)
+    xs = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    it, _ = form.PCG(dev(b), xs, ess=dev(ess, torch.int32), rel_tol=0.0, max_iter=8, jacobi=True)
+    xr, itr, _ = op.pcg(b, ess, rel_tol=0.0, max_iter=8, jacobi=True)
+    assert it == itr == 8
+    assert relerr(host(xs), xr) < 1e-10
 
 
 @pytest.mark.parametrize("refine", [1, 2, 3])

@@ -167,7 +167,11 @@ std::vector<int> face_brick_order(int ne, int D, const std::vector<int> &gm)
          for (int d = 0; d < 3 && ok; d++) { ok = a[d] == 3 || N.n[d][lane[l]] == lane[l + step[d]]; }
       }
       if (!ok) { continue; }
-      bricks.push_back({{patch[lane[0]], curve(lane[0])}, lane});
+      // in the order of the caller's elements (their smallest index): the reference's meshes
+      // number elements along a space-filling curve and their dofs in that traversal, so bricks
+      // taken in that order gather and store neighbouring dofs close in time
+      (void)curve;
+      bricks.push_back({{patch[lane[0]], (uint64_t)*std::min_element(lane.begin(), lane.end())}, lane});
    }
    std::sort(bricks.begin(), bricks.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
    for (auto &b : bricks)

@@ -393,8 +393,8 @@ k_setup_affine(const int *__restrict__ perm, int ne, const double *__restrict__ 
 template <int Q>
 __global__ void __launch_bounds__(256)
 k_setup_trilinear(const int *__restrict__ perm, int ne, const double *__restrict__ enodes,
-                  const double *__restrict__ W, SetupCoef cm, SetupCoef cd, double *__restrict__ qd_geo,
-                  double *__restrict__ qd_pair)
+                  const double *__restrict__ cfit, const double *__restrict__ W, SetupCoef cm, SetupCoef cd,
+                  double *__restrict__ qd_geo, double *__restrict__ qd_pair)
 {
    constexpr int NQ = Q * Q * Q;
    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -412,12 +412,16 @@ k_setup_trilinear(const int *__restrict__ perm, int ne, const double *__restrict
    pr.y = w * coef_at(cm, eq, e);
    reinterpret_cast<v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane] = pr;
    if (q != 0) { return; }
-   const double *X = enodes + (size_t)e * 24;
    double c[2 * kTrilinPairs];
-#pragma unroll
-   for (int i = 0; i < 3; i++)
+   if (cfit)  // fitted from MFEM-layout Jacobians (k_jac_trilinear_fit)
    {
-      const double *x = X + i * 8;
+#pragma unroll
+      for (int k = 0; k < 21; k++) { c[k] = cfit[(size_t)e * 21 + k]; }
+   }
+#pragma unroll
+   for (int i = 0; i < (cfit ? 0 : 3); i++)
+   {
+      const double *x = enodes + (size_t)e * 24 + i * 8;
       c[0 * 3 + i] = x[1] - x[0];
       c[1 * 3 + i] = x[2] - x[0];
       c[2 * 3 + i] = x[4] - x[0];
@@ -430,6 +434,71 @@ k_setup_trilinear(const int *__restrict__ perm, int ne, const double *__restrict
    v2d *dst = reinterpret_cast<v2d *>(qd_geo + (size_t)blk * kTrilinPairs * 128) + lane;
 #pragma unroll
    for (int k = 0; k < kTrilinPairs; k++) { dst[k * 64] = v2d{c[2 * k], c[2 * k + 1]}; }
+}
+
+// The trilinear-map coefficients c1..c7 of every element recovered from MFEM-layout Jacobians
+// J(q,i,j,e) (what the reference-side binding passes, GeometricFactors::JACOBIANS): J[i][0] =
+// c1 + c4 eta + c5 zeta + c7 eta zeta is bilinear in (eta, zeta) -- four values at the rule's
+// extreme points a = x_0, b = x_{Q-1} give it -- and J[i][1] / J[i][2] give c2, c6 and c3 the same
+// way.  Then every point's J is compared with the fitted map's (1e-13 of the element's largest
+// entry): bad[0] = 1 when some element is not a trilinear map of the reference cube (e.g. a
+// curved, high-order mesh), which keeps the per-point layout.
+template <int Q>
+__global__ void k_jac_trilinear_fit(int ne, const double *__restrict__ Jg, const QPts qp, double *__restrict__ cfit)
+{
+   constexpr int NQ = Q * Q * Q;
+   const int e = blockIdx.x * blockDim.x + threadIdx.x;
+   if (e >= ne) { return; }
+   const double a = qp.x[0], b = qp.x[Q - 1], h = b - a;
+   auto J = [&](int i, int j, int qx, int qy, int qz) {
+      return Jg[(((size_t)e * 3 + j) * 3 + i) * NQ + (qz * Q + qy) * Q + qx];
+   };
+   const int L = Q - 1;
+   double *c = cfit + (size_t)e * 21;  // c[3 (k - 1) + i] = c_k of coordinate i
+#pragma unroll
+   for (int i = 0; i < 3; i++)
+   {
+      // J[i][0](eta, zeta) at (a, a), (b, a), (a, b), (b, b): c1, c4, c5, c7
+      const double f00 = J(i, 0, 0, 0, 0), f10 = J(i, 0, 0, L, 0), f01 = J(i, 0, 0, 0, L), f11 = J(i, 0, 0, L, L);
+      const double c7 = (f11 - f10 - f01 + f00) / (h * h);
+      const double c4 = (f10 - f00) / h - c7 * a, c5 = (f01 - f00) / h - c7 * a;
+      const double c1 = f00 - (c4 + c5) * a - c7 * a * a;
+      // J[i][1](xi, zeta) = c2 + c4 xi + c6 zeta + c7 xi zeta: c2, c6 from (a, a), (a, b)
+      const double g00 = J(i, 1, 0, 0, 0), g01 = J(i, 1, 0, 0, L);
+      const double c6 = (g01 - g00) / h - c7 * a;
+      const double c2 = g00 - c4 * a - c6 * a - c7 * a * a;
+      // J[i][2](xi, eta) = c3 + c5 xi + c6 eta + c7 xi eta: c3 from (a, a)
+      const double c3 = J(i, 2, 0, 0, 0) - c5 * a - c6 * a - c7 * a * a;
+      c[0 * 3 + i] = c1; c[1 * 3 + i] = c2; c[2 * 3 + i] = c3; c[3 * 3 + i] = c4;
+      c[4 * 3 + i] = c5; c[5 * 3 + i] = c6; c[6 * 3 + i] = c7;
+   }
+}
+
+template <int Q>
+__global__ void k_jac_trilinear_check(int ne, const double *__restrict__ Jg, const QPts qp,
+                                      const double *__restrict__ cfit, int *__restrict__ bad)
+{
+   constexpr int NQ = Q * Q * Q;
+   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   if (t >= (long)ne * NQ) { return; }
+   const int e = (int)(t / NQ), q = (int)(t % NQ);
+   const double xi = qp.x[q % Q], et = qp.x[(q / Q) % Q], zt = qp.x[q / (Q * Q)];
+   const double *c = cfit + (size_t)e * 21;
+   double mx = 0.0, dv = 0.0;
+   for (int i = 0; i < 3; i++)
+   {
+      auto cf = [&](int k) { return c[3 * k + i]; };
+      const double f[3] = {cf(0) + cf(3) * et + cf(4) * zt + cf(6) * et * zt,
+                           cf(1) + cf(3) * xi + cf(5) * zt + cf(6) * xi * zt,
+                           cf(2) + cf(4) * xi + cf(5) * et + cf(6) * xi * et};
+      for (int j = 0; j < 3; j++)
+      {
+         const double v = Jg[(((size_t)e * 3 + j) * 3 + i) * NQ + q];
+         mx = fmax(mx, fabs(v));
+         dv = fmax(dv, fabs(v - f[j]));
+      }
+   }
+   if (!(dv <= 1e-13 * mx)) { bad[0] = 1; }
 }
 
 // TRILINEAR -> BLOCKED: the full per-point qdata of a TRILINEAR form (for the diagonal, the
@@ -575,25 +644,50 @@ bool jacobians_affine(int ne, int nq, const double *J, hipStream_t s)
    return h == 0;
 }
 
-void setup_trilinear(const QLayout &L, int Q, const double *enodes, const double *W, const CoeffDesc *cm,
-                     const CoeffDesc *cd, const double *cm_q, const double *cd_q, double *qd_geo, double *qd_pair,
-                     hipStream_t s)
+bool jacobians_trilinear_fit(int ne, int Q, const QPts &qp, const double *J, double *cfit, hipStream_t s)
+{
+   if (ne == 0) { return true; }
+   DeviceArray<int> flag;
+   flag.resize(1);
+   ECM2_HIP(hipMemsetAsync(flag.data(), 0, sizeof(int), s));
+   const long n = (long)ne * Q * Q * Q;
+#define ECM2_FIT(QQ)                                                                                           \
+   if (Q == QQ)                                                                                                \
+   {                                                                                                           \
+      hipLaunchKernelGGL((k_jac_trilinear_fit<QQ>), dim3(grid_for(ne, 256)), dim3(256), 0, s, ne, J, qp, cfit);   \
+      hipLaunchKernelGGL((k_jac_trilinear_check<QQ>), dim3(grid_for(n, 256)), dim3(256), 0, s, ne, J, qp, cfit,   \
+                         flag.data());                                                                        \
+   }
+   ECM2_FIT(3)
+   else ECM2_FIT(4)
+   else { return false; }
+#undef ECM2_FIT
+   ECM2_HIP(hipGetLastError());
+   int h = 1;
+   ECM2_HIP(hipMemcpyAsync(&h, flag.data(), sizeof(int), hipMemcpyDeviceToHost, s));
+   ECM2_HIP(hipStreamSynchronize(s));
+   return h == 0;
+}
+
+void setup_trilinear(const QLayout &L, int Q, const double *enodes, const double *cfit, const double *W,
+                     const CoeffDesc *cm, const CoeffDesc *cd, const double *cm_q, const double *cd_q, double *qd_geo,
+                     double *qd_pair, hipStream_t s)
 {
    if (L.ne == 0) { return; }
-   ECM2_VERIFY(L.kind == QLAYOUT_TRILINEAR && cm && cd && enodes, ERR_INTERNAL,
-               "trilinear setup needs a TRILINEAR layout, both coefficients and the corners");
+   ECM2_VERIFY(L.kind == QLAYOUT_TRILINEAR && cm && cd && (enodes || cfit), ERR_INTERNAL,
+               "trilinear setup needs a TRILINEAR layout, both coefficients and the corners or fitted maps");
    ECM2_VERIFY(!L.pos || L.perm, ERR_INTERNAL, "blocked setup needs the inverse permutation");
    const SetupCoef scm = make_setup_coef(cm, cm_q), scd = make_setup_coef(cd, cd_q);
    const long n = (long)L.nblk() * 64 * L.nq;
    if (Q == 3)
    {
-      hipLaunchKernelGGL((k_setup_trilinear<3>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.perm, L.ne, enodes, W,
-                         scm, scd, qd_geo, qd_pair);
+      hipLaunchKernelGGL((k_setup_trilinear<3>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.perm, L.ne, enodes,
+                         cfit, W, scm, scd, qd_geo, qd_pair);
    }
    else if (Q == 4)
    {
-      hipLaunchKernelGGL((k_setup_trilinear<4>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.perm, L.ne, enodes, W,
-                         scm, scd, qd_geo, qd_pair);
+      hipLaunchKernelGGL((k_setup_trilinear<4>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.perm, L.ne, enodes,
+                         cfit, W, scm, scd, qd_geo, qd_pair);
    }
    else { ECM2_VERIFY(false, ERR_UNSUPPORTED, "trilinear setup: Q1D " << Q << " not instantiated"); }
    ECM2_HIP(hipGetLastError());

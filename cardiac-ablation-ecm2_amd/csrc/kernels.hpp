@@ -239,9 +239,14 @@ void setup_affine(const QLayout &L, int Q, const double *enodes, const double *J
                   const CoeffDesc *cm, const CoeffDesc *cd, const double *cm_q, const double *cd_q,
                   double *qd_fac, double *qd_pair, hipStream_t s);
 // TRILINEAR layout (see above) from lexicographic element corners; both coefficients.
-void setup_trilinear(const QLayout &L, int Q, const double *enodes, const double *W, const CoeffDesc *cm,
-                     const CoeffDesc *cd, const double *cm_q, const double *cd_q, double *qd_geo, double *qd_pair,
-                     hipStream_t s);
+// (enodes: lexicographic corners, or cfit: the fitted map coefficients [ne][21] of
+// jacobians_trilinear_fit)
+void setup_trilinear(const QLayout &L, int Q, const double *enodes, const double *cfit, const double *W,
+                     const CoeffDesc *cm, const CoeffDesc *cd, const double *cm_q, const double *cd_q, double *qd_geo,
+                     double *qd_pair, hipStream_t s);
+// Trilinear-map coefficients of every element from MFEM-layout Jacobians (cfit [ne][21]); false
+// when some element's Jacobians are not those of a trilinear map (1e-13; synchronises s).
+bool jacobians_trilinear_fit(int ne, int Q, const QPts &qp, const double *J, double *cfit, hipStream_t s);
 // The BLOCKED per-point qdata of a TRILINEAR form (L: its layout; outputs sized as BLOCKED).
 void trilinear_expand(const QLayout &L, int Q, const double *qd_geo, const double *qd_pair, const QPts &qp,
                       double *qd_diff, double *qd_mass, hipStream_t s);

@@ -507,11 +507,19 @@ void PAForm::assemble(hipStream_t s)
       if (resolved_mode_ == KERNEL_TPE) { layout_.kind = QLAYOUT_AFFINE; }
       else if (resolved_mode_ == KERNEL_LINE) { layout_.kind = QLAYOUT_AFFINE_E; }
    }
-   else if (!affine && compress_ && have_mass_ && have_diff_ && resolved_mode_ == KERNEL_TPE && !jac_ &&
-            enodes_.size())
+   else if (!affine && compress_ && have_mass_ && have_diff_ && resolved_mode_ == KERNEL_TPE)
    {
-      // general trilinear hexes from corners: geometry per element, J evaluated per point
-      layout_.kind = QLAYOUT_TRILINEAR;
+      // general trilinear hexes: the map coefficients per element (from the corners, or fitted
+      // to the reference binding's Jacobians when they are a trilinear map's), J per point
+      bool tl = !jac_ && enodes_.size();
+      if (jac_)
+      {
+         QPts qp = {};
+         for (int q = 0; q < Q_ && q < MAX_Q1D; q++) { qp.x[q] = maps_.qpts[q]; }
+         cfit_.resize(std::max(1, ne_) * 21);
+         tl = kern::jacobians_trilinear_fit(ne_, Q_, qp, jac_, cfit_.data(), s);
+      }
+      if (tl) { layout_.kind = QLAYOUT_TRILINEAR; }
    }
 
    // the merge plan (cross-wave faces), the regular blocks and the partial-slot layout belong
@@ -980,8 +988,8 @@ void PAForm::assemble(hipStream_t s)
    }
    else if (layout_.kind == QLAYOUT_TRILINEAR)
    {
-      kern::setup_trilinear(layout_, Q_, enodes_.data(), W_.data(), cm, cd, cm_q, cd_q, qd_diff_.data(),
-                            qd_mass_.data(), s);
+      kern::setup_trilinear(layout_, Q_, jac_ ? nullptr : enodes_.data(), jac_ ? cfit_.data() : nullptr, W_.data(),
+                            cm, cd, cm_q, cd_q, qd_diff_.data(), qd_mass_.data(), s);
    }
    else if (jac_)
    {

@@ -236,6 +236,7 @@ private:
    DeviceArray<int> perm_dev_;      // internal position -> caller element
    DeviceArray<int> csr_off_, csr_idx_;
    DeviceArray<double> enodes_;     // [e][3][8]
+   DeviceArray<double> cfit_;       // TRILINEAR from Jacobians: fitted map coefficients [e][21]
    const double *jac_ = nullptr;    // device, not owned
    DeviceArray<double> W_, rowtab_, drowtab_;
    DeviceArray<Basis1D> btab_;      // device copy of basis_ (line / brick / diagonal / coefficient kernels)

@@ -146,7 +146,9 @@ def test_qdata_matches_reference_setup(kernel, order):
 def test_jacobian_geometry_path(mesh_name, order):
     """set_jacobians (GeometricFactors layout -- what the reference-side binding passes) gives
     the same operator as element nodes; affine Jacobians (constant per element, checked on
-    the device) select the compressed layout, trilinear ones keep the full one."""
+    the device) select the compressed layout; trilinear ones at p <= 2 are fitted to the
+    elements' trilinear maps (checked at every point) and select the TRILINEAR layout, at p >= 3
+    they keep the full one."""
     m = make_mesh(mesh_name)
     fes = E.H1Space(m, order)
     en = m.element_nodes()
@@ -160,8 +162,10 @@ def test_jacobian_geometry_path(mesh_name, order):
     op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=3.0, beta=0.5)
     affine = mesh_name != "trilinear" and AFFINE_ON
     want = (E.QLAYOUT_AFFINE if order <= 2 else E.QLAYOUT_AFFINE_E) if affine else \
-        (E.QLAYOUT_BLOCKED if order <= 2 else E.QLAYOUT_NATIVE)
+        (E.QLAYOUT_TRILINEAR if order <= 2 else E.QLAYOUT_NATIVE)
     assert form.info()["layout"] == want
+    if want == E.QLAYOUT_TRILINEAR:
+        assert relerr(form.qdata(E.DIFFUSION), op.D) < 1e-13
     x = np.random.default_rng(5).uniform(-1, 1, fes.ndofs)
     y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
     form.Mult(dev(x), y)
@@ -643,3 +647,19 @@ def test_trilinear_layout_on_the_fly_geometry(order, mesh_name, numbering):
         f2.Mult(dev(x), y)
         opm = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=a, beta=c)
         assert relerr(host(y), opm.mult_markers(x, m.GetAttributes(), mass_marker=[0, 1])) <= RTOL
+
+
+def test_jacobians_not_trilinear_keep_per_point_layout():
+    """Jacobians that no trilinear map produces (one point of one element perturbed, as on a
+    curved mesh) fail the fit's per-point check: the form keeps the full per-point layout."""
+    m = make_mesh("trilinear")
+    fes = E.H1Space(m, 2)
+    _, J, _ = O.geom(m.element_nodes(), O.default_q1d(2))
+    J = np.array(J)
+    J[7, 0, 1, 5] *= 1.0 + 1e-6
+    form = E.BilinearForm(fes, geometry="jacobians")
+    form.SetJacobians(dev(J))
+    form.AddDomainIntegrator(E.MassIntegrator(E.ConstantCoefficient(3.0)))
+    form.AddDomainIntegrator(E.DiffusionIntegrator(E.ConstantCoefficient(0.5)))
+    form.Assemble()
+    assert form.info()["layout"] == E.QLAYOUT_BLOCKED

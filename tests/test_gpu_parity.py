@@ -337,6 +337,35 @@ def test_full_size_c4_tpe():
     assert relerr(host(y), op.mult(x)) <= RTOL
 
 
+@pytest.mark.parametrize("mesh_kind", ["affine", "trilinear"])
+def test_full_size_c4_reference_numbering(mesh_kind):
+    """configs[3] size with the reference's own numbering -- MakeCartesian3D's space-filling-curve
+    element order and FiniteElementSpace's entity dofs, the element order derived by the form from
+    the map (what a drop-in binding gets; bench.py's entity_numbering sub-object) -- and, second
+    case, the same mesh with its interior vertices moved (TRILINEAR layout): against the oracle,
+    plus the diagonal."""
+    n = 108
+    m = E.Mesh.MakeCartesian3D(n, n, n, sfc_ordering=True)
+    if mesh_kind == "trilinear":
+        V = m.vertices()
+        h = 1.0 / n
+        inner = np.all((V > 0.5 * h) & (V < 1.0 - 0.5 * h), axis=1)
+        V[inner] += 0.15 * h * np.random.default_rng(7).uniform(-1, 1, (int(inner.sum()), 3))
+        m.set_vertices(V)
+    fes, form, op = build_pair(m, 2, "bio_a", "bio_b", numbering=E.NUMBERING_ENTITY, element_order="faces")
+    assert fes.ndofs == 10218313
+    assert form.info()["layout"] == (E.QLAYOUT_AFFINE if mesh_kind == "affine" else E.QLAYOUT_TRILINEAR)
+    lslot, _ = form.PlanInfo()
+    assert lslot == (n // 4) ** 3  # every 4x4x4 brick reads a lattice map and keeps face-grouped slots
+    x = np.random.default_rng(23).uniform(-1, 1, fes.ndofs)
+    y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    form.Mult(dev(x), y)
+    assert relerr(host(y), op.mult(x)) <= RTOL
+    d = torch.empty_like(y)
+    form.AssembleDiagonal(d)
+    assert relerr(host(d), op.diagonal()) < 1e-13
+
+
 @pytest.mark.parametrize("element_order", ["native", "brick", "morton"])
 @pytest.mark.parametrize("order", [1, 2])
 def test_element_orders_same_operator(element_order, order):

@@ -29,7 +29,7 @@ def main(prof_dir, workload, key):
         "algorithmic_bytes_per_launch": alg,
         "traffic_over_algorithmic": k["hbm_bytes_per_launch"] / alg if alg else None,
         "second_pass": s["kernels"].get("sum_partials"),
-        "source": f"profiles/collect_r2.sh / run_profile.sh {workload} (rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate "
+        "source": f"{os.environ.get('PIN_SCRIPT', 'profiles/collect_r3.sh')} {workload} (rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate "
                   "passes) -> profiles/pmc_reduce.py -> profiles/pmc_pin.py",
     }
     print(json.dumps(out, indent=1))

@@ -60,6 +60,25 @@ __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], cons
 {
    constexpr int ND = D * D * D, XR = XwaveRows<D>::R;
    const bool rr = MAYREG && regf == 1, rs = MAYREG && regf != 0, rl = MAYREG && regf == 2;
+   // A lattice-map block's store entries are loaded here, before the face merges: their latency
+   // (the map left L2 while the block computed) overlaps the shuffles and barriers instead of
+   // preceding the stores.  (An opaque lane offset pins the loads here: hoisted above the
+   // compute, 27 live values spill.  Map-addressed blocks keep their loads at the store: the
+   // same hoist makes the RM = 0 kernel spill.)
+   int lo = 0;
+   asm volatile("" : "+v"(lo));
+   int gs[ND];
+#pragma unroll
+   for (int a = 0; a < ND; a++)
+   {
+      gs[a] = 0;
+      if (wave_on && rl)
+      {
+         const int X = (D - 1) * (lane & 3) + a % D, Y = (D - 1) * ((lane >> 2) & 3) + (a / D) % D,
+                   Z = (D - 1) * (lane >> 4) + a / (D * D);
+         gs[a] = lm[tpe_lattice_slot(D, X, Y, Z) + lo];
+      }
+   }
    // (regular and lattice-map blocks carry no orientation signs: checked at setup)
    if (SIGNS && wave_on && !rs)
    {
@@ -131,7 +150,7 @@ __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], cons
             }
             else
             {
-               const int g = rl ? lm[tpe_lattice_slot(D, X, Y, Z)] : mp[a * 64];
+               const int g = rl ? gs[a] : mp[a * 64];
                d = bdof(g);
                shared = bshared(g);
             }
@@ -312,7 +331,8 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 // deterministic store.
 // RM: 0 every block map-addressed; 1 every block regular (treg rows, no flag read); 2 per block
 // (treg row flag [7], wave-uniform): a regular block's dofs are all owned (checked at setup),
-// so it addresses x / y only.
+// so it addresses x / y only; 3 every block a lattice-map block (the reference's numbering on a
+// Cartesian mesh): the map loads are the first loads of the gather chain.
 // TL (TRILINEAR layout, kernels.hpp): the element's trilinear-map coefficients instead of C,
 // and the point pair (W beta, W alpha); J, adj(J), det J evaluated at every point: per plane
 // (zeta) the J pieces A = c1 + c5 zeta, B = c4 + c7 zeta, Cz = c2 + c6 zeta, per row (eta)
@@ -379,7 +399,8 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
          load_row(1, ra[1]);
       }
       else { load_row(0, ca); }
-      if (RM)
+      if (RM == 3) { regf = 2; }  // every block lattice-map: no treg row in the gather's chain
+      else if (RM)
       {
          const int *r = treg + (size_t)blk * 8;  // wave-uniform: scalar loads
          rg = TpeReg{r[0], r[1], r[2], r[3], r[4]};
@@ -398,7 +419,7 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                   sX[w][(dz * D + dy) * D + dx][lane] = x[d0 + dx * rg.sx + dy * rg.sy + dz * rg.sz];
                }
       }
-      else if (RM == 2 && regf == 2)
+      else if (RM >= 2 && regf == 2)
       {
          // lattice-map block: the dofs of the block's lattice points (no signs), each entry a's
          // 64 loads one contiguous sub-block of the map
@@ -625,7 +646,7 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
          for (int qz = 0; qz < Q; qz++) { plane(qz); }
       }
    }  // wave_on
-   tpe_assemble_store<D, SPLIT, RM != 1, true, RM != 0>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0,
+   tpe_assemble_store<D, SPLIT, RM == 0 || RM == 2, true, RM != 0>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0,
                                                          blk, lane, active, n_owned, y, yg, part, &sX[0][0][0], w,
                                                          wave_on, rg, regf, pstride,
                                                          lmap ? lmap + (size_t)blk * tpe_lattice_points(D) : nullptr);
@@ -925,6 +946,7 @@ void launch_tpe(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipS
                       a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part, a.treg,   \
                       a.part_stride, a.lmap, a.qp)
          if (a.treg && a.treg_all) { ECM2_TL(1); }
+         else if (a.treg && a.tlat_all) { ECM2_TL(3); }
          else if (a.treg) { ECM2_TL(2); }
          else { ECM2_TL(0); }
 #undef ECM2_TL
@@ -949,6 +971,7 @@ void launch_tpe(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipS
                       a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part, a.treg, a.part_stride, \
                       a.lmap, a.qp)
             if (a.treg && a.treg_all) { ECM2_SF(1); }
+            else if (a.treg && a.tlat_all) { ECM2_SF(3); }
             else if (a.treg) { ECM2_SF(2); }
             else { ECM2_SF(0); }
 #undef ECM2_SF

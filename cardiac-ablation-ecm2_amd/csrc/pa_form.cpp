@@ -365,7 +365,7 @@ void PAForm::build_shared_plan(const std::vector<int> &hcount, const std::vector
          int d1, t1, e1, et1;
          int n = extend(i, false, d1, t1);
          const int ne_ = c ? extend(i, true, e1, et1) : 0;
-         if (ne_ >= 2 * n && ne_ >= 4)
+         if (ne_ > n && (n < 4 || ne_ >= 2 * n))  // a short affine run costs more descriptor bytes per entry
          {
             n = ne_;
             d1 = kExplicitDofs;
@@ -598,6 +598,7 @@ void PAForm::assemble(hipStream_t s)
       // blocks are regular, its boundary blocks are not); treg_all when every block is.
       treg_.resize(0);
       treg_all_ = false;
+      tlat_all_ = false;
       n_treg_ = 0;
       n_tlat_ = 0;
       lmap_.resize(0);
@@ -700,9 +701,10 @@ void PAForm::assemble(hipStream_t s)
          {
             treg_.upload(reg, s);
             treg_all_ = nreg == nblk && (latency_from_ < 0 || latency_from_ >= nblk);
+            tlat_all_ = nlat == nblk && (latency_from_ < 0 || latency_from_ >= nblk);
          }
       }
-      part_stride_ = treg_all_ ? ns : ND_ * 64;
+      part_stride_ = treg_all_ || tlat_all_ ? ns : ND_ * 64;
       {
          // partial slots: [blk][a][lane]; on regular blocks [blk][face-grouped surface index of
          // the block lattice] (tpe_surface_index: a face's two holders list it at the same
@@ -1161,6 +1163,7 @@ ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, doubl
    a.lane_flags = lane_flags_.data();
    a.treg = treg_.size() ? treg_.data() : nullptr;
    a.treg_all = treg_all_ ? 1 : 0;
+   a.tlat_all = tlat_all_ ? 1 : 0;
    a.lmap = lmap_.size() ? lmap_.data() : nullptr;
    for (int q = 0; q < Q_ && q < MAX_Q1D; q++) { a.qp.x[q] = maps_.qpts[q]; }
    a.xwave = (layout_.kind == QLAYOUT_AFFINE || layout_.kind == QLAYOUT_TRILINEAR) ? 1 : 0;

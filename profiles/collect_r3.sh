@@ -6,6 +6,7 @@
 #   a: c4 (structured, affine: the headline), c4ent (the reference's numbering), c4tri (trilinear
 #      mesh, TRILINEAR layout), c4 full layout (blocked)
 #   b: c5 (bricks, affine_e), c3 (fichera r6)
+#   e: c4ent and c3 (the reference's numbering: re-pinned after a lattice-map kernel change)
 set -uo pipefail
 SET=${1:-a}
 O=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/collect_r3
@@ -39,6 +40,9 @@ if [ "$SET" = a ]; then
   one c4ent affine apply --workload c4 --numbering entity --steps 50 --warmup 5 || exit 1
   one c4tri trilinear apply --workload c4 --mesh trilinear --steps 30 --warmup 5 || exit 1
   one c4_full blocked apply --workload c4 --geometry full --steps 30 --warmup 5 || exit 1
+elif [ "$SET" = e ]; then
+  one c4ent affine apply --workload c4 --numbering entity --steps 50 --warmup 5 || exit 1
+  one c3 affine apply --workload c3 --steps 30 --warmup 5 || exit 1
 else
   one c5 affine_e apply_brick --workload c5 --steps 30 --warmup 5 || exit 1
   one c3 affine apply --workload c3 --steps 30 --warmup 5 || exit 1

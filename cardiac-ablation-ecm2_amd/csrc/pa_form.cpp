@@ -375,42 +375,60 @@ void PAForm::build_shared_plan(const std::vector<int> &hcount, const std::vector
          i += n;
       }
       // 2D: one open run per (count, length, steps) class; a 1D run joins its class's open run
-      // when its first entry continues that run's lattice, else it opens a new one
+      // when its first entry continues that run's lattice, else it opens a new one.  A run whose
+      // slots continue the lattice but whose dofs do not (the reference's numbering: the 3- and
+      // 4-holder entries of a brick edge are 1D runs of one entry each) joins the last open run
+      // of its (count, length, slot step) class instead, which becomes explicit-dof if it is not
+      // yet (only while small: an explicit entry costs 4 plan bytes, a run descriptor 48)
       std::vector<Run> out;
       std::vector<std::vector<int>> members;  // 1D runs of each 2D run
-      std::map<std::tuple<int, int, int, int>, int> open;
+      std::map<std::tuple<int, int, int, int>, int> open_aff;
+      std::map<std::tuple<int, int, int>, int> open_any;
+      auto try_join = [&](int gi, const R1 &q, int d0, int k, bool convert) {
+         Run &g = out[gi];
+         if ((g.n2 + 1) * g.n1 > 64 || q.c > 8) { return false; }
+         const int tt = q.c ? slot(d0, 0) - g.s0[0] : 0;
+         bool ok = g.n2 == 1 || tt == g.n2 * g.t2;
+         for (int h = 1; h < q.c && ok; h++) { ok = slot(d0, h) - g.s0[h] == tt; }
+         if (!ok) { return false; }
+         const bool gex = g.d1 == kExplicitDofs, qex = q.d1 == kExplicitDofs;
+         const int dd = d0 - g.dof0;
+         const bool dofs_ok = !gex && !qex && q.d1 == g.d1 && (g.n2 == 1 || dd == g.n2 * g.d2);
+         if (!gex && !dofs_ok)
+         {
+            if (!convert || g.n1 * g.n2 > 12) { return false; }
+            g.d1 = kExplicitDofs;  // the run's dofs come from the entry list from now on
+            g.d2 = 0;
+         }
+         if (g.n2 == 1) { g.t2 = tt; g.d2 = g.d1 == kExplicitDofs ? 0 : dd; }
+         g.n2++;
+         members[gi].push_back(k);
+         return true;
+      };
       for (size_t k = 0; k < r1s.size(); k++)
       {
          const R1 &q = r1s[k];
          const int d0 = dofs[q.i0];
-         const auto key = std::make_tuple(q.c, q.n, q.d1, q.t1);
-         auto it = open.find(key);
-         bool joined = false;
-         if (it != open.end() && q.c <= 8)
+         const auto ka = std::make_tuple(q.c, q.n, q.d1, q.t1);
+         const auto kb = std::make_tuple(q.c, q.n, q.t1);
+         int gi = -1;
+         auto ia = open_aff.find(ka);
+         if (ia != open_aff.end() && try_join(ia->second, q, d0, (int)k, false)) { gi = ia->second; }
+         if (gi < 0)
          {
-            Run &g = out[it->second];
-            if ((g.n2 + 1) * g.n1 <= 64)
-            {
-               const int dd = g.d1 == kExplicitDofs ? 0 : d0 - g.dof0, tt = q.c ? slot(d0, 0) - g.s0[0] : 0;
-               bool ok = g.n2 == 1 || (dd == g.n2 * g.d2 && tt == g.n2 * g.t2);
-               for (int h = 1; h < q.c && ok; h++) { ok = slot(d0, h) - g.s0[h] == tt; }
-               if (ok)
-               {
-                  if (g.n2 == 1) { g.d2 = dd; g.t2 = tt; }
-                  g.n2++;
-                  members[it->second].push_back((int)k);
-                  joined = true;
-               }
-            }
+            auto ib = open_any.find(kb);
+            if (ib != open_any.end() && try_join(ib->second, q, d0, (int)k, true)) { gi = ib->second; }
          }
-         if (!joined)
+         if (gi < 0)
          {
             Run g{q.n, 1, q.c, d0, q.d1, 0, q.t1, 0, q.i0, {}};
             for (int h = 0; h < q.c; h++) { g.s0.push_back(slot(d0, h)); }
-            open[key] = (int)out.size();
+            gi = (int)out.size();
+            open_aff[ka] = gi;
             out.push_back(g);
             members.push_back({(int)k});
          }
+         open_any[kb] = gi;
       }
       for (size_t g = 0; g < out.size(); g++)
       {
@@ -420,6 +438,26 @@ void PAForm::build_shared_plan(const std::vector<int> &hcount, const std::vector
          runs.push_back(std::move(out[g]));
       }
       ECM2_VERIFY((int)order.size() == r1, ERR_INTERNAL, "run plan lost entries");
+   }
+   if (std::getenv("ECM2_PLAN_DUMP"))  // (diagnostic) run classes of the summation plan
+   {
+      std::map<std::tuple<int, int, int, int>, std::pair<long, long>> h;
+      for (const Run &g : runs)
+      {
+         auto &v = h[std::make_tuple(g.d1 == kExplicitDofs, g.c, g.n1, g.n2)];
+         v.first++;
+         v.second += (long)g.n1 * g.n2;
+      }
+      std::vector<std::pair<long, std::tuple<int, int, int, int>>> top;
+      for (auto &kv : h) { top.push_back({kv.second.first, kv.first}); }
+      std::sort(top.rbegin(), top.rend());
+      std::fprintf(stderr, "plan: %zu runs, %d entries\n", runs.size(), n_sh_);
+      for (size_t i = 0; i < top.size() && i < 30; i++)
+      {
+         const auto &k = top[i].second;
+         std::fprintf(stderr, "  explicit %d holders %d shape %dx%d: %ld runs, %ld entries\n", std::get<0>(k),
+                      std::get<1>(k), std::get<2>(k), std::get<3>(k), top[i].first, h[k].second);
+      }
    }
    std::vector<int> rdesc, rslots, blocks;
    rdesc.reserve((runs.size() + 1) * 12);

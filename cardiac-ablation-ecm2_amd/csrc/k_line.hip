@@ -286,17 +286,6 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ lelem, int n_owned,
 // (deterministic, no atomics).  Workgroups take bricks in XCD-contiguous order.
 // AFF: AFFINE_E qdata (per-element C + one (W beta, W alpha det J) pair per point).
 // --------------------------------------------------------------------------
-// lattice coordinate P along one brick direction -> (first element index, local index,
-// holders): the shared plane P = D-1 is held by element 0 (local D-1) and 1 (local 0)
-template <int D>
-__device__ __forceinline__ void brick_cand(int P, int &c0, int &l0, int &n)
-{
-   if (P < D - 1) { c0 = 0; l0 = P; n = 1; }
-   else if (P == D - 1) { c0 = 0; l0 = D - 1; n = 2; }
-   else { c0 = 1; l0 = P - (D - 1); n = 1; }
-}
-
-// --------------------------------------------------------------------------
 // Brick kernel layout and addressing (round 2; profiles/r2_ab_brick.txt: -8..-9% vs the
 // round-1 form at C5):
 //  * bank-conflict-free LDS images: every stage's lane -> element mapping starts each element
@@ -344,10 +333,54 @@ struct BrickShapeC
 
 // faces of the brick lattice containing point (X, Y, Z): bits X = 0, X = LX-1, Y = 0, ...
 template <int LX, int LY, int LZ>
-__device__ __forceinline__ int brick_faces(int X, int Y, int Z)
+__host__ __device__ constexpr int brick_faces(int X, int Y, int Z)
 {
    return (X == 0) | (X == LX - 1) << 1 | (Y == 0) << 2 | (Y == LY - 1) << 3 | (Z == 0) << 4 | (Z == LZ - 1) << 5;
 }
+
+// Lattice-point table of the brick kernel's final stage (round 3), the same for every brick of
+// a (D, BZ): per lattice point p (X fastest) the LDS offsets of its holders' outputs in the
+// element-output image [e][dx][dz][dy], in ascending element order and padded with the image's
+// zero slot (NE SB), two 16-bit offsets per int; then X | Y << 8 | Z << 16 | faces << 24; then
+// the point's surface index (brick_surface_index, -1 inside).  A thread reads its points' rows
+// once and sums 4 (8) LDS values per point with no per-point index arithmetic: the loop it
+// replaces derived the holder set per point (variable-trip loops over the candidate elements)
+// and was ~22% of the kernel's VALU instructions at p = 4.
+template <int D, int Q, int BZ>
+struct BrickPtTable
+{
+   using S = BrickShapeC<D, Q, BZ>;
+   static constexpr int NH = 4 * BZ, NW = NH / 2 + 2;
+   int w[S::NB][NW];
+   constexpr BrickPtTable() : w()
+   {
+      for (int p = 0; p < S::NB; p++)
+      {
+         const int X = p % S::LX, Y = (p / S::LX) % S::LY, Z = p / (S::LX * S::LY);
+         int off[NH] = {};
+         int n = 0;
+         // holders along one direction: P < D-1 -> element 0 at P; P == D-1 -> elements 0 (D-1)
+         // and 1 (0); P > D-1 -> element 1 at P - (D-1)
+         const int nz = BZ == 2 && Z == D - 1 ? 2 : 1, ny = Y == D - 1 ? 2 : 1, nx = X == D - 1 ? 2 : 1;
+         for (int iz = 0; iz < nz; iz++)
+            for (int iy = 0; iy < ny; iy++)
+               for (int ix = 0; ix < nx; ix++)
+               {
+                  const int cx = X < D - 1 ? 0 : (X == D - 1 ? ix : 1), lx = cx == 0 ? X : X - (D - 1);
+                  const int cy = Y < D - 1 ? 0 : (Y == D - 1 ? iy : 1), ly = cy == 0 ? Y : Y - (D - 1);
+                  const int cz = BZ == 1 ? 0 : (Z < D - 1 ? 0 : (Z == D - 1 ? iz : 1)), lz = cz == 0 ? Z : Z - (D - 1);
+                  const int elt = cx + 2 * (cy + 2 * cz);
+                  off[n++] = elt * S::SB + lx * S::DD + lz * D + ly;
+               }
+         for (; n < NH; n++) { off[n] = S::NE * S::SB; }
+         for (int h = 0; h < NH / 2; h++) { w[p][h] = off[2 * h] | off[2 * h + 1] << 16; }
+         w[p][NH / 2] = X | Y << 8 | Z << 16 | brick_faces<S::LX, S::LY, S::LZ>(X, Y, Z) << 24;
+         w[p][NH / 2 + 1] = brick_surface_index(D, BZ, X, Y, Z);
+      }
+   }
+};
+template <int D, int Q, int BZ>
+__device__ const BrickPtTable<D, Q, BZ> kBrickPts = BrickPtTable<D, Q, BZ>();
 
 template <int D, int Q, int BZ, bool SPLIT, bool AFF, bool REG>
 __global__ void __launch_bounds__((BrickShapeC<D, Q, BZ>::NT), (BrickShapeC<D, Q, BZ>::WPE))
@@ -359,15 +392,16 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
 {
    using S = BrickShapeC<D, Q, BZ>;
    constexpr int NE = S::NE, DD = S::DD, QQ = S::QQ, DQ = S::DQ, SA = S::SA, SB = S::SB, DS = S::DS;
-   constexpr int LX = S::LX, LY = S::LY, LZ = S::LZ, NB = S::NB, L2S = S::L2S, S3 = S::S3, NQ = Q * Q * Q;
+   constexpr int LX = S::LX, LY = S::LY, NB = S::NB, L2S = S::L2S, S3 = S::S3, NQ = Q * Q * Q;
    static_assert(QQ <= 64, "brick kernel needs Q1D <= 8");
    static_assert(DQ <= L2S && DD <= L2S, "line stages: one lane per line");
    static_assert(!(REG && SPLIT), "regular bricks address one L-vector");
-   __shared__ double sXL[NE * SA];  // x lines: [e][f][qx][dz][dy]
-   __shared__ double sYQ[NE * SB];  // y / z planes: [e][g][dz (stride DS)][qy][qx]; then outputs [e][dx][dz][dy]
+   __shared__ double sXL[NE * SA];      // x lines: [e][f][qx][dz][dy]
+   __shared__ double sYQ[NE * SB + 1];  // y / z planes: [e][g][dz (stride DS)][qy][qx]; then outputs [e][dx][dz][dy]; zero slot
    const int k = k_begin + xcd_contiguous(blockIdx.x, gridDim.x);
    if (k >= k_end) { return; }  // whole workgroup
    const int t = threadIdx.x;
+   if (t == 0) { sYQ[NE * SB] = 0.0; }  // the point table's padding slot (published by the first barrier)
    const int eL = t / L2S, lL = t % L2S;                 // line stages
    const bool actL = eL < NE && lL < DD;                 // stages 1, 5: lL = dy + D dz
    const bool act2 = eL < NE && lL < DQ;                 // stages 2, 4
@@ -580,6 +614,20 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
       }
    }
    __syncthreads();
+   // this thread's lattice points of the final stage: table rows (and map entries) issued here,
+   // so their latency overlaps the x transpose
+   using PT = BrickPtTable<D, Q, BZ>;
+   constexpr int NIT = (NB + S::NT - 1) / S::NT, NW = PT::NW;
+   int pw[NIT][NW], pg[NIT];
+#pragma unroll
+   for (int i = 0; i < NIT; i++)
+   {
+      const int p = t + i * S::NT < NB ? t + i * S::NT : NB - 1;
+      const int *row = kBrickPts<D, Q, BZ>.w[p];
+#pragma unroll
+      for (int j = 0; j < NW; j++) { pw[i][j] = row[j]; }
+      pg[i] = REG ? 0 : bm[p];
+   }
    // ---- lanes (element, dy, dz): transpose in x -> element outputs [e][dx][dz][dy] in sYQ
    if (actL)
    {
@@ -602,38 +650,35 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
       }
    }
    __syncthreads();
-   // ---- lattice points: sum the holders in a fixed (z, y, x) order, store or publish
-   for (int p = t; p < NB; p += S::NT)
+   // ---- lattice points: sum the holders in ascending element order (the (z, y, x) order of
+   // the point table), store or publish
+#pragma unroll
+   for (int i = 0; i < NIT; i++)
    {
-      const int X = p % LX, Y = (p / LX) % LY, Z = p / (LX * LY);
-      int cx, lx, nx, cy, ly, ny, cz, lz, nz;
-      brick_cand<D>(X, cx, lx, nx);
-      brick_cand<D>(Y, cy, ly, ny);
-      if (BZ == 2) { brick_cand<D>(Z, cz, lz, nz); }
-      else { cz = 0; lz = Z; nz = 1; }
-      double v = 0.0;
-      for (int iz = 0; iz < nz; iz++)
-         for (int iy = 0; iy < ny; iy++)
-            for (int ix = 0; ix < nx; ix++)
-            {
-               const int elt = (cx + ix) + 2 * ((cy + iy) + 2 * (cz + iz));
-               v += sYQ[elt * SB + (ix ? 0 : lx) * DD + (iz ? 0 : lz) * D + (iy ? 0 : ly)];
-            }
+      if (NB % S::NT != 0 && i == NIT - 1 && t + i * S::NT >= NB) { break; }
+      double v = sYQ[pw[i][0] & 0xffff];
+      v += sYQ[pw[i][0] >> 16];
+#pragma unroll
+      for (int h = 1; h < NW - 2; h++)
+      {
+         v += sYQ[pw[i][h] & 0xffff];
+         v += sYQ[pw[i][h] >> 16];
+      }
+      const int c = pw[i][NW - 2];
       int d;
       bool shared;
       if (REG)
       {
-         d = base + X * sx + Y * sy + Z * sz;
-         shared = (brick_faces<LX, LY, LZ>(X, Y, Z) & mask) != 0;
+         d = base + (c & 255) * sx + ((c >> 8) & 255) * sy + ((c >> 16) & 255) * sz;
+         shared = ((c >> 24) & mask) != 0;
       }
       else
       {
-         const int g = bm[p];
-         d = bdof(g);
-         shared = bshared(g);
+         d = bdof(pg[i]);
+         shared = bshared(pg[i]);
       }
       if (!shared) { *((!SPLIT || d < n_owned) ? y + d : yg + (d - n_owned)) = v; }
-      else { part[(size_t)k * S::SURF + brick_surface_index(D, BZ, X, Y, Z)] = v; }  // surface only (setup)
+      else { part[(size_t)k * S::SURF + pw[i][NW - 1]] = v; }  // surface only (setup)
    }
 }
 

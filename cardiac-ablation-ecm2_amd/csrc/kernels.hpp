@@ -160,11 +160,11 @@ struct ApplyArgs
 // face dof -- this brick's high face and the neighbour's low face -- list it at the same
 // offset within their groups: [Z = 0 | Z = LZ-1 | Y = 0 | Y = LY-1 | X = 0 | X = LX-1],
 // edges and corners in the first group that contains them.  -1 for interior points.
-__host__ __device__ inline int lattice_surface_points(int LX, int LY, int LZ)
+__host__ __device__ constexpr int lattice_surface_points(int LX, int LY, int LZ)
 {
    return 2 * LX * LY + 2 * (LZ - 2) * LX + 2 * (LZ - 2) * (LY - 2);
 }
-__host__ __device__ inline int lattice_surface_index(int LX, int LY, int LZ, int X, int Y, int Z)
+__host__ __device__ constexpr int lattice_surface_index(int LX, int LY, int LZ, int X, int Y, int Z)
 {
    if (Z == 0) { return Y * LX + X; }
    if (Z == LZ - 1) { return LX * LY + Y * LX + X; }
@@ -176,11 +176,11 @@ __host__ __device__ inline int lattice_surface_index(int LX, int LY, int LZ, int
    if (X == LX - 1) { return b2 + (LZ - 2) * (LY - 2) + (Z - 1) * (LY - 2) + (Y - 1); }
    return -1;
 }
-__host__ __device__ inline int brick_surface_points(int D, int bz)
+__host__ __device__ constexpr int brick_surface_points(int D, int bz)
 {
    return lattice_surface_points(2 * D - 1, 2 * D - 1, bz * (D - 1) + 1);
 }
-__host__ __device__ inline int brick_surface_index(int D, int bz, int X, int Y, int Z)
+__host__ __device__ constexpr int brick_surface_index(int D, int bz, int X, int Y, int Z)
 {
    return lattice_surface_index(2 * D - 1, 2 * D - 1, bz * (D - 1) + 1, X, Y, Z);
 }

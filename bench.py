@@ -378,7 +378,8 @@ def main():
         # the reference's numbering: no mesh knowledge, the form derives its order from the map
         eo = "faces" if numbering == "entity" and args.workload != "c3" else "auto"
         f = E.BilinearForm(fes, kernel=kernel, element_order=os.environ.get("ECM2_ELEMENT_ORDER", eo),
-                           scatter=scatter, compress_geometry=compress_geometry)
+                           scatter=scatter, compress_geometry=compress_geometry,
+                           bricks=int(os.environ.get("ECM2_BRICKS", "-1")))  # A/B: p >= 3 brick depth
         f.AddDomainIntegrator(mass(a))
         f.AddDomainIntegrator(diff(T))
         f.Assemble()

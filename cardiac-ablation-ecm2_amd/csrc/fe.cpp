@@ -197,4 +197,29 @@ Basis1D make_basis1d(const DofToQuad &m)
    return b;
 }
 
+BasisDev make_basis_dev(const Basis1D &b, int D, int Q)
+{
+   BasisDev t{};
+   t.b = b;
+   const int H = D / 2;
+   for (int q = 0; q < Q; q++)
+   {
+      for (int i = 0; i < H; i++)
+      {
+         const int a = q + MAX_Q1D * i, r = q + MAX_Q1D * (D - 1 - i);
+         t.eo.BP[a] = 0.5 * (b.B[a] + b.B[r]);
+         t.eo.BM[a] = 0.5 * (b.B[a] - b.B[r]);
+         t.eo.GP[a] = 0.5 * (b.G[a] + b.G[r]);
+         t.eo.GM[a] = 0.5 * (b.G[a] - b.G[r]);
+      }
+      if (D % 2)
+      {
+         const int a = q + MAX_Q1D * H;
+         t.eo.BP[a] = b.B[a];
+         t.eo.GP[a] = b.G[a];
+      }
+   }
+   return t;
+}
+
 } // namespace ecm2

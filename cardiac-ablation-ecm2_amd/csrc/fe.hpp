@@ -43,4 +43,29 @@ struct Basis1D
 };
 Basis1D make_basis1d(const DofToQuad &m);
 
+// Even/odd split of the 1D tables (round 3, the brick kernel's contractions).  The GLL nodes and
+// the Gauss points are symmetric about the element midpoint, so B(Q-1-q, D-1-d) = B(q, d) and
+// G(Q-1-q, D-1-d) = -G(q, d).  For a table T and i < D/2:
+//   TP(q, i) = (T(q, i) + T(q, D-1-i)) / 2,  TM(q, i) = (T(q, i) - T(q, D-1-i)) / 2,
+// and TP(q, D/2) = T(q, D/2) for odd D.  A contraction y = T x of a line then needs the rows
+// q < Q/2 only, on e_i = x_i + x_{D-1-i} and o_i = x_i - x_{D-1-i}:
+//   B: y_q, y_{Q-1-q} = (BP e) +- (BM o)      G: y_q, y_{Q-1-q} = (GM o) +- (GP e)
+// (and the transposes likewise): about (D+1)/2 + D/2 instead of D multiply-adds per pair of
+// outputs (the even-odd decomposition of sum-factorised tensor kernels).  The identity is exact
+// algebra for the table rows it uses; the mirrored rows are the symmetric images, equal to the
+// computed ones up to rounding (~1e-16 relative).
+struct BasisEO
+{
+   double BP[MAX_Q1D * MAX_D1D], BM[MAX_Q1D * MAX_D1D];  // [q + MAX_Q1D * i]
+   double GP[MAX_Q1D * MAX_D1D], GM[MAX_Q1D * MAX_D1D];
+};
+// The device copy of the tables the line / brick / diagonal / coefficient kernels read (as a
+// Basis1D through the first member; the brick kernel also reads eo).
+struct BasisDev
+{
+   Basis1D b;
+   BasisEO eo;
+};
+BasisDev make_basis_dev(const Basis1D &b, int D, int Q);
+
 } // namespace ecm2

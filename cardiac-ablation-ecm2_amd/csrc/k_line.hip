@@ -314,6 +314,132 @@ __device__ __forceinline__ double lds_read(const double *p)
    return *q;
 }
 
+// ---- even/odd contractions (fe.hpp, BasisEO): a line x[D] is split into e[NE] (x_i + x_{D-1-i},
+// then the middle value for odd D) and o[H] (x_i - x_{D-1-i}); a forward contraction computes
+// the rows q < Q/2 and mirrors them; a transposed one accumulates into E[NE] / O[H] and merges.
+typedef const __attribute__((address_space(4))) BasisEO CBasisEO;
+__device__ __forceinline__ CBasisEO *stage_eo(const Basis1D *tab)
+{
+   CBasisEO *p = (CBasisEO *)&reinterpret_cast<const BasisDev *>(tab)->eo;
+   asm volatile("" : "+s"(p));
+   return p;
+}
+template <int D>
+__device__ __forceinline__ void eo_split(const double (&x)[D], double (&e)[(D + 1) / 2], double (&o)[D / 2])
+{
+#pragma unroll
+   for (int i = 0; i < D / 2; i++)
+   {
+      e[i] = x[i] + x[D - 1 - i];
+      o[i] = x[i] - x[D - 1 - i];
+   }
+   if (D % 2) { e[D / 2] = x[D / 2]; }
+}
+// y = B x
+template <int D, int Q>
+__device__ __forceinline__ void eo_fwd_b(CBasisEO *t, const double (&e)[(D + 1) / 2], const double (&o)[D / 2],
+                                         double (&y)[Q])
+{
+#pragma unroll
+   for (int q = 0; q < (Q + 1) / 2; q++)
+   {
+      double s = 0.0, a = 0.0;
+#pragma unroll
+      for (int i = 0; i < (D + 1) / 2; i++) { s += t->BP[q + MQ * i] * e[i]; }
+      if (2 * q + 1 == Q) { y[q] = s; }  // the middle row (odd Q): BM vanishes there
+      else
+      {
+#pragma unroll
+         for (int i = 0; i < D / 2; i++) { a += t->BM[q + MQ * i] * o[i]; }
+         y[q] = s + a;
+         y[Q - 1 - q] = s - a;
+      }
+   }
+}
+// y = G x
+template <int D, int Q>
+__device__ __forceinline__ void eo_fwd_g(CBasisEO *t, const double (&e)[(D + 1) / 2], const double (&o)[D / 2],
+                                         double (&y)[Q])
+{
+#pragma unroll
+   for (int q = 0; q < (Q + 1) / 2; q++)
+   {
+      double s = 0.0, a = 0.0;
+#pragma unroll
+      for (int i = 0; i < D / 2; i++) { s += t->GM[q + MQ * i] * o[i]; }
+      if (2 * q + 1 == Q) { y[q] = s; }  // GP vanishes on the middle row
+      else
+      {
+#pragma unroll
+         for (int i = 0; i < (D + 1) / 2; i++) { a += t->GP[q + MQ * i] * e[i]; }
+         y[q] = s + a;
+         y[Q - 1 - q] = s - a;
+      }
+   }
+}
+// E, O += split of B^T y
+template <int D, int Q>
+__device__ __forceinline__ void eo_acc_bt(CBasisEO *t, const double (&y)[Q], double (&E)[(D + 1) / 2],
+                                          double (&O)[D / 2])
+{
+#pragma unroll
+   for (int q = 0; q < (Q + 1) / 2; q++)
+   {
+      if (2 * q + 1 == Q)
+      {
+#pragma unroll
+         for (int i = 0; i < (D + 1) / 2; i++) { E[i] += t->BP[q + MQ * i] * y[q]; }
+      }
+      else
+      {
+         const double ye = y[q] + y[Q - 1 - q], yo = y[q] - y[Q - 1 - q];
+#pragma unroll
+         for (int i = 0; i < (D + 1) / 2; i++) { E[i] += t->BP[q + MQ * i] * ye; }
+#pragma unroll
+         for (int i = 0; i < D / 2; i++) { O[i] += t->BM[q + MQ * i] * yo; }
+      }
+   }
+}
+// E, O += split of G^T y
+template <int D, int Q>
+__device__ __forceinline__ void eo_acc_gt(CBasisEO *t, const double (&y)[Q], double (&E)[(D + 1) / 2],
+                                          double (&O)[D / 2])
+{
+#pragma unroll
+   for (int q = 0; q < (Q + 1) / 2; q++)
+   {
+      if (2 * q + 1 == Q)
+      {
+#pragma unroll
+         for (int i = 0; i < D / 2; i++) { O[i] += t->GM[q + MQ * i] * y[q]; }
+      }
+      else
+      {
+         const double ye = y[q] + y[Q - 1 - q], yo = y[q] - y[Q - 1 - q];
+#pragma unroll
+         for (int i = 0; i < (D + 1) / 2; i++) { E[i] += t->GP[q + MQ * i] * yo; }
+#pragma unroll
+         for (int i = 0; i < D / 2; i++) { O[i] += t->GM[q + MQ * i] * ye; }
+      }
+   }
+}
+template <int D>
+__device__ __forceinline__ void eo_zero(double (&E)[(D + 1) / 2], double (&O)[D / 2])
+{
+#pragma unroll
+   for (int i = 0; i < (D + 1) / 2; i++) { E[i] = 0.0; }
+#pragma unroll
+   for (int i = 0; i < D / 2; i++) { O[i] = 0.0; }
+}
+template <int D>
+__device__ __forceinline__ double eo_at(const double (&E)[(D + 1) / 2], const double (&O)[D / 2], int d)
+{
+   // d is a compile-time index after unrolling
+   if (d < D / 2) { return E[d] + O[d]; }
+   if (2 * d + 1 == D) { return E[(D - 1) / 2]; }  // odd D: the middle
+   return E[D - 1 - d] - O[D - 1 - d];
+}
+
 template <int D, int Q, int BZ>
 struct BrickShapeC
 {
@@ -393,6 +519,7 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
    using S = BrickShapeC<D, Q, BZ>;
    constexpr int NE = S::NE, DD = S::DD, QQ = S::QQ, DQ = S::DQ, SA = S::SA, SB = S::SB, DS = S::DS;
    constexpr int LX = S::LX, LY = S::LY, NB = S::NB, L2S = S::L2S, S3 = S::S3, NQ = Q * Q * Q;
+   constexpr int NEO = (D + 1) / 2, NOO = D / 2;  // even / odd parts of a split line
    static_assert(QQ <= 64, "brick kernel needs Q1D <= 8");
    static_assert(DQ <= L2S && DD <= L2S, "line stages: one lane per line");
    static_assert(!(REG && SPLIT), "regular bricks address one L-vector");
@@ -462,20 +589,17 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
    // ---- lanes (element, dy, dz): contract in x -> sXL [f][qx][l]
    if (actL)
    {
-      CBasis *bp = stage_basis(btab);
       double *o = sXL + eL * SA + lL;
+      CBasisEO *te = stage_eo(btab);
+      double xe[NEO], xo[NOO], u[Q], v[Q];
+      eo_split<D>(xl, xe, xo);
+      eo_fwd_b<D, Q>(te, xe, xo, u);
+      eo_fwd_g<D, Q>(te, xe, xo, v);
 #pragma unroll
       for (int qx = 0; qx < Q; qx++)
       {
-         double u = 0.0, v = 0.0;
-#pragma unroll
-         for (int dx = 0; dx < D; dx++)
-         {
-            u += bp->B[qx + MQ * dx] * xl[dx];
-            v += bp->G[qx + MQ * dx] * xl[dx];
-         }
-         o[qx * DD] = u;
-         o[Q * DD + qx * DD] = v;
+         o[qx * DD] = u[qx];
+         o[Q * DD + qx * DD] = v[qx];
       }
    }
    if (k_begin < 0)  // never: a use outside the x stage stops the gather sinking behind the qdata
@@ -499,29 +623,25 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
          lb[dy] = lds_read(in + Q * DD + dy);
       }
       double *o = sYQ + eL * SB + dz * DS + qx;
+      CBasisEO *te = stage_eo(btab);
+      double ae[NEO], ao[NOO], be[NEO], bo[NOO], gb[Q], bg[Q], bb[Q];
+      eo_split<D>(la, ae, ao);
+      eo_split<D>(lb, be, bo);
+      eo_fwd_b<D, Q>(te, be, bo, gb);  // G_x B_y
+      eo_fwd_g<D, Q>(te, ae, ao, bg);  // B_x G_y
+      eo_fwd_b<D, Q>(te, ae, ao, bb);  // B_x B_y
 #pragma unroll
       for (int qy = 0; qy < Q; qy++)
       {
-         double gb = 0.0, bg = 0.0, bb = 0.0;
-         CBasis *br = stage_basis(btab);  // re-laundered per row: one row of the basis in SGPRs
-#pragma unroll
-         for (int dy = 0; dy < D; dy++)
-         {
-            const double by = br->B[qy + MQ * dy], gy = br->G[qy + MQ * dy];
-            gb += by * lb[dy];
-            bg += gy * la[dy];
-            bb += by * la[dy];
-         }
-         o[qy * Q] = gb;
-         o[D * DS + qy * Q] = bg;
-         o[2 * D * DS + qy * Q] = bb;
+         o[qy * Q] = gb[qy];
+         o[D * DS + qy * Q] = bg[qy];
+         o[2 * D * DS + qy * Q] = bb[qy];
       }
    }
    __syncthreads();
    // ---- lanes (element, qx, qy): contract in z, weight, transpose in z (in place)
    if (act3)
    {
-      CBasis *bp = stage_basis(btab);
       double *io = sYQ + e3 * SB + l3;
       double l0[D], l1[D], l2[D];
 #pragma unroll
@@ -531,23 +651,9 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
          l1[dz] = lds_read(io + D * DS + dz * DS);
          l2[dz] = lds_read(io + 2 * D * DS + dz * DS);
       }
-      double A1[D], A2[D], A3[D];
-#pragma unroll
-      for (int dz = 0; dz < D; dz++) { A1[dz] = 0.0; A2[dz] = 0.0; A3[dz] = 0.0; }
-#pragma unroll
-      for (int qz = 0; qz < Q; qz++)
-      {
-         double gx = 0.0, gy = 0.0, gz = 0.0, u = 0.0;
-#pragma unroll
-         for (int dz = 0; dz < D; dz++)
-         {
-            const double bz = bp->B[qz + MQ * dz], gzz = bp->G[qz + MQ * dz];
-            gx += bz * l0[dz];
-            gy += bz * l1[dz];
-            gz += gzz * l2[dz];
-            u += bz * l2[dz];
-         }
-         double fx, fy, fz, m;
+      // the quadrature-point operator: (f, m) = (W beta C grad u, W alpha det J u) at qz
+      auto qpoint = [&](int qz, double gx, double gy, double gz, double u, double &fx, double &fy, double &fz,
+                        double &m) {
          if (AFF)
          {
             const double wb = pa[qz].x;
@@ -563,29 +669,98 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
             fz = qv[2][qz] * gx + qv[4][qz] * gy + qv[5][qz] * gz;
             m = qv[6][qz] * u;
          }
+      };
+      // rows qz and Q-1-qz together: forward split contractions, the operator at both points, the
+      // transposed contractions accumulated into split sums
+      CBasisEO *te = stage_eo(btab);
+      double e0[NEO], o0[NOO], e1[NEO], o1[NOO], e2[NEO], o2[NOO];
+      eo_split<D>(l0, e0, o0);
+      eo_split<D>(l1, e1, o1);
+      eo_split<D>(l2, e2, o2);
+      double A1E[NEO], A1O[NOO], A2E[NEO], A2O[NOO], A3E[NEO], A3O[NOO];
+      eo_zero<D>(A1E, A1O);
+      eo_zero<D>(A2E, A2O);
+      eo_zero<D>(A3E, A3O);
 #pragma unroll
-         for (int dz = 0; dz < D; dz++)
+      for (int qp = 0; qp < (Q + 1) / 2; qp++)
+      {
+         const int qr = Q - 1 - qp;
+         const bool mid = qr == qp;
+         double sx_ = 0.0, sy_ = 0.0, su = 0.0, sg = 0.0, ax = 0.0, ay = 0.0, au = 0.0, ag = 0.0;
+#pragma unroll
+         for (int i = 0; i < NEO; i++)
          {
-            const double bz = bp->B[qz + MQ * dz], gzz = bp->G[qz + MQ * dz];
-            A1[dz] += bz * fx;
-            A2[dz] += bz * fy;
-            A3[dz] += gzz * fz;
-            A3[dz] += bz * m;
+            const double b = te->BP[qp + MQ * i];
+            sx_ += b * e0[i];
+            sy_ += b * e1[i];
+            su += b * e2[i];
+            if (!mid) { ag += te->GP[qp + MQ * i] * e2[i]; }
+         }
+#pragma unroll
+         for (int i = 0; i < NOO; i++)
+         {
+            sg += te->GM[qp + MQ * i] * o2[i];
+            if (!mid)
+            {
+               const double b = te->BM[qp + MQ * i];
+               ax += b * o0[i];
+               ay += b * o1[i];
+               au += b * o2[i];
+            }
+         }
+         double fxp, fyp, fzp, mp;
+         qpoint(qp, sx_ + ax, sy_ + ay, sg + ag, su + au, fxp, fyp, fzp, mp);
+         if (mid)
+         {
+#pragma unroll
+            for (int i = 0; i < NEO; i++)
+            {
+               const double b = te->BP[qp + MQ * i];
+               A1E[i] += b * fxp;
+               A2E[i] += b * fyp;
+               A3E[i] += b * mp;
+            }
+#pragma unroll
+            for (int i = 0; i < NOO; i++) { A3O[i] += te->GM[qp + MQ * i] * fzp; }
+         }
+         else
+         {
+            double fxr, fyr, fzr, mr;
+            qpoint(qr, sx_ - ax, sy_ - ay, sg - ag, su - au, fxr, fyr, fzr, mr);
+            const double fxe = fxp + fxr, fxo = fxp - fxr, fye = fyp + fyr, fyo = fyp - fyr;
+            const double fze = fzp + fzr, fzo = fzp - fzr, me = mp + mr, mo = mp - mr;
+#pragma unroll
+            for (int i = 0; i < NEO; i++)
+            {
+               const double b = te->BP[qp + MQ * i];
+               A1E[i] += b * fxe;
+               A2E[i] += b * fye;
+               A3E[i] += b * me;
+               A3E[i] += te->GP[qp + MQ * i] * fzo;
+            }
+#pragma unroll
+            for (int i = 0; i < NOO; i++)
+            {
+               const double b = te->BM[qp + MQ * i];
+               A1O[i] += b * fxo;
+               A2O[i] += b * fyo;
+               A3O[i] += b * mo;
+               A3O[i] += te->GM[qp + MQ * i] * fze;
+            }
          }
       }
 #pragma unroll
       for (int dz = 0; dz < D; dz++)
       {
-         io[dz * DS] = A1[dz];
-         io[D * DS + dz * DS] = A2[dz];
-         io[2 * D * DS + dz * DS] = A3[dz];
+         io[dz * DS] = eo_at<D>(A1E, A1O, dz);
+         io[D * DS + dz * DS] = eo_at<D>(A2E, A2O, dz);
+         io[2 * D * DS + dz * DS] = eo_at<D>(A3E, A3O, dz);
       }
    }
    __syncthreads();
    // ---- lanes (element, dz, qx), l4 = dz + D qx: transpose in y -> sXL [f][qx][dz][dy]
    if (act2)
    {
-      CBasis *bp = stage_basis(btab);
       const int dz = lL % D, qx = lL / D;
       const double *in = sYQ + eL * SB + dz * DS + qx;
       double t0[Q], t1[Q], t2[Q];
@@ -597,20 +772,18 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
          t2[qy] = lds_read(in + 2 * D * DS + qy * Q);
       }
       double *o = sXL + eL * SA + qx * DD + dz * D;
+      CBasisEO *te = stage_eo(btab);
+      double C1E[NEO], C1O[NOO], C2E[NEO], C2O[NOO];
+      eo_zero<D>(C1E, C1O);
+      eo_zero<D>(C2E, C2O);
+      eo_acc_bt<D, Q>(te, t0, C1E, C1O);
+      eo_acc_gt<D, Q>(te, t1, C2E, C2O);
+      eo_acc_bt<D, Q>(te, t2, C2E, C2O);
 #pragma unroll
       for (int dy = 0; dy < D; dy++)
       {
-         double c1 = 0.0, c2 = 0.0;
-#pragma unroll
-         for (int qy = 0; qy < Q; qy++)
-         {
-            const double by = bp->B[qy + MQ * dy], gy = bp->G[qy + MQ * dy];
-            c1 += by * t0[qy];
-            c2 += gy * t1[qy];
-            c2 += by * t2[qy];
-         }
-         o[dy] = c1;
-         o[Q * DD + dy] = c2;
+         o[dy] = eo_at<D>(C1E, C1O, dy);
+         o[Q * DD + dy] = eo_at<D>(C2E, C2O, dy);
       }
    }
    __syncthreads();
@@ -631,7 +804,6 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
    // ---- lanes (element, dy, dz): transpose in x -> element outputs [e][dx][dz][dy] in sYQ
    if (actL)
    {
-      CBasis *bp = stage_basis(btab);
       const double *in = sXL + eL * SA + lL;
       double l0[Q], l1[Q];
 #pragma unroll
@@ -640,14 +812,13 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
          l0[qx] = lds_read(in + qx * DD);
          l1[qx] = lds_read(in + Q * DD + qx * DD);
       }
+      CBasisEO *te = stage_eo(btab);
+      double VE[NEO], VO[NOO];
+      eo_zero<D>(VE, VO);
+      eo_acc_gt<D, Q>(te, l0, VE, VO);
+      eo_acc_bt<D, Q>(te, l1, VE, VO);
 #pragma unroll
-      for (int dx = 0; dx < D; dx++)
-      {
-         double v = 0.0;
-#pragma unroll
-         for (int qx = 0; qx < Q; qx++) { v += bp->G[qx + MQ * dx] * l0[qx]; v += bp->B[qx + MQ * dx] * l1[qx]; }
-         sYQ[eL * SB + dx * DD + lL] = v;  // sYQ is free: stage 4 read it before a barrier
-      }
+      for (int dx = 0; dx < D; dx++) { sYQ[eL * SB + dx * DD + lL] = eo_at<D>(VE, VO, dx); }
    }
    __syncthreads();
    // ---- lattice points: sum the holders in ascending element order (the (z, y, x) order of

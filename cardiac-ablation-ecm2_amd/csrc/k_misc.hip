@@ -417,11 +417,16 @@ k_sum_partials(int b0, int b1, const int *__restrict__ blocks, const int *__rest
    __shared__ int sd[257 * kRunInts];
    const int blk = b0 + xcd_contiguous(blockIdx.x, gridDim.x);
    if (blk >= b1) { return; }  // whole workgroup
-   const int r0 = blocks[2 * blk], nr = blocks[2 * blk + 1] - r0;
+   // block row: first run, end run, first entry, entries | explicit-dof runs << 30 (scalar loads)
+   const int r0 = blocks[4 * blk], nr = blocks[4 * blk + 1] - r0, e0 = blocks[4 * blk + 2], bn = blocks[4 * blk + 3];
+   const int i = e0 + (int)threadIdx.x;
+   const bool live = (int)threadIdx.x < (bn & 0xffff);
+   // a block with explicit-dof runs issues its entries' dofs now, beside the descriptor staging
+   // (the entry list holds every entry's dof), instead of after the run lookup
+   const int dpre = ((bn >> 30) & 1) && live ? pdof[i] : 0;
    for (int k = threadIdx.x; k < (nr + 1) * kRunInts; k += blockDim.x) { sd[k] = runs[(size_t)r0 * kRunInts + k]; }
    __syncthreads();
-   const int i = sd[6] + (int)threadIdx.x;
-   if (i >= sd[nr * kRunInts + 6]) { return; }
+   if (!live) { return; }
    int lo = 0, hi = nr - 1;
    while (lo < hi)
    {
@@ -433,7 +438,7 @@ k_sum_partials(int b0, int b1, const int *__restrict__ blocks, const int *__rest
    const int shape = R[0], n1 = shape & 255, cnt = (shape >> 16) & 255;
    const int off = i - R[6], pa = off % n1, pb = off / n1;
    // shape bit 24: the run's dofs are not a lattice (entity numbering): the entry list holds them
-   const int d = (shape >> 24) ? pdof[i] : R[1] + pa * R[2] + pb * R[3];
+   const int d = (shape >> 24) ? dpre : R[1] + pa * R[2] + pb * R[3];
    const int ds = pa * R[4] + pb * R[5];
    double v[4];
 #pragma unroll

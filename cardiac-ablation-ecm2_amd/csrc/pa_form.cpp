@@ -496,16 +496,20 @@ void PAForm::build_shared_plan(const std::vector<int> &hcount, const std::vector
          n += runs[e].n1 * runs[e].n2;
          e++;
       }
+      bool ex = false;
+      for (size_t g = r; g < e; g++) { ex = ex || runs[g].d1 == kExplicitDofs; }
       blocks.push_back((int)r);
       blocks.push_back((int)e);
+      blocks.push_back(runs[r].first);
+      blocks.push_back(n | (ex ? 1 << 30 : 0));
       if (!ghost) { sh_nblk_owned_++; }
       r = e;
    }
-   sh_nblk_ = (int)blocks.size() / 2;
+   sh_nblk_ = (int)blocks.size() / 4;
    n_runs_ = (long)runs.size();
    sh_runs_.upload(rdesc, s);
    sh_rslots_.upload(rslots.empty() ? std::vector<int>{0} : rslots, s);
-   sh_blocks_.upload(blocks.empty() ? std::vector<int>{0, 0} : blocks, s);
+   sh_blocks_.upload(blocks.empty() ? std::vector<int>{0, 0, 0, 0} : blocks, s);
    n_explicit_runs_ = 0;
    for (const Run &g : runs) { n_explicit_runs_ += g.d1 == kExplicitDofs; }
    sh_pdof_.upload(order.empty() ? std::vector<int>{0} : order, s);
@@ -786,7 +790,11 @@ void PAForm::assemble(hipStream_t s)
       drowtab_.upload(kern::make_diag_row_table(maps_), s);
       ECM2_HIP(hipStreamSynchronize(s));
    }
-   if (!btab_.size()) { btab_.upload(&basis_, 1, s); }
+   if (!btab_.size())
+   {
+      const BasisDev bd = make_basis_dev(basis_, D_, Q_);
+      btab_.upload(&bd, 1, s);
+   }
    if (resolved_mode_ == KERNEL_LINE && !gmap_line_.size() && ne_ > 0)
    {
       // Bricks of 2 x 2 x bz elements (deterministic scatter, both integrators) take every
@@ -1012,7 +1020,7 @@ void PAForm::assemble(hipStream_t s)
       if (c.gridfunc())
       {
          tmp.resize((size_t)ne_ * NQ_);
-         kern::coeff_gridfunc(ne_, D_, Q_, gmap_.data(), basis_, btab_.data(), c, tmp.data(), s);
+         kern::coeff_gridfunc(ne_, D_, Q_, gmap_.data(), basis_, btab(), c, tmp.data(), s);
          return tmp.data();
       }
       return nullptr;
@@ -1212,7 +1220,7 @@ ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, doubl
    a.qdm = qd_mass_.data();
    a.x = x; a.xg = xg; a.y = y; a.yg = yg;
    a.part = use_partials() ? const_cast<double *>(part_.data()) : nullptr;  // form-owned scratch
-   a.btab = btab_.data();
+   a.btab = btab();
    a.lelem = lelem_.data();
    a.lelem_off = lelem_off_.empty() ? nullptr : lelem_off_.data();
    if (resolved_mode_ == KERNEL_LINE && use_partials())
@@ -1285,7 +1293,7 @@ void PAForm::assemble_diagonal(double *diag, hipStream_t s)
    }
    ECM2_HIP(hipMemsetAsync(diag, 0, sizeof(double) * (size_t)ndofs_, s));
    kern::diagonal(layout_.pos, D_, Q_, layout_.kind, ne_, gmap_.data(), have_diff_ ? qd_diff_.data() : nullptr,
-                  have_mass_ ? qd_mass_.data() : nullptr, diag, false, basis_, btab_.data(), s);
+                  have_mass_ ? qd_mass_.data() : nullptr, diag, false, basis_, btab(), s);
 }
 
 void PAForm::expand_trilinear(DeviceArray<double> &fd, DeviceArray<double> &fm, hipStream_t s) const

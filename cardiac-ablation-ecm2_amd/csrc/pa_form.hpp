@@ -240,7 +240,8 @@ private:
    DeviceArray<double> cfit_;       // TRILINEAR from Jacobians: fitted map coefficients [e][21]
    const double *jac_ = nullptr;    // device, not owned
    DeviceArray<double> W_, rowtab_, drowtab_;
-   DeviceArray<Basis1D> btab_;      // device copy of basis_ (line / brick / diagonal / coefficient kernels)
+   DeviceArray<BasisDev> btab_;     // device copy of basis_ + its even/odd split (line / brick / diagonal / coefficient kernels)
+   const Basis1D *btab() const { return btab_.size() ? &btab_.data()->b : nullptr; }
    DeviceArray<double> qd_diff_, qd_mass_;
    DeviceArray<double> xe_, ye_;    // unfused work E-vectors
    DeviceArray<double> ctmp_m_, ctmp_d_;

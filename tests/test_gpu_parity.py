@@ -439,7 +439,7 @@ def test_full_size_c2_deterministic():
 
 
 @pytest.mark.parametrize("mesh_name", ["inline_hex", "cart_bricks", "nonaligned", "fichera_r1", "cart_130"])
-@pytest.mark.parametrize("order", [3, 4, 5])
+@pytest.mark.parametrize("order", [3, 4, 5, 6])
 def test_line_bricks(mesh_name, order):
     """p >= 3 brick kernel (2 x 2 x 1 and 2 x 2 x 2 workgroups, LDS lattice assembly) and the
     per-element line kernel it falls back to: each matches the oracle, overwrites every y

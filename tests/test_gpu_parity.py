@@ -459,7 +459,7 @@ def test_line_bricks(mesh_name, order):
         if bz == 0:
             assert nb == 0
         elif mesh_name in ("inline_hex", "cart_bricks"):
-            assert nb > 0 and depth == bz
+            assert nb > 0 and depth == (bz if order < 6 else 1)  # 2 x 2 x 2 bricks exceed LDS at p = 6
         x = np.random.default_rng(order).uniform(-1, 1, fes.ndofs)
         y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
         form.Mult(dev(x), y)

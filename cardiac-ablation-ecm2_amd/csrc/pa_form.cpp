@@ -430,7 +430,59 @@ void PAForm::build_shared_plan(const std::vector<int> &hcount, const std::vector
          }
          open_any[kb] = gi;
       }
-      for (size_t g = 0; g < out.size(); g++)
+      // Run order: by first partial slot (the slot locality of the entry order above) or by
+      // smallest dof (neighbouring workgroups of the pass then store neighbouring y lines: C5
+      // pass -10%, profiles/r3_ab_runorder.txt).  Which one is decided by the 128-B lines (y
+      // lines written + partial-slot lines read) that windows of 256 consecutive entries touch,
+      // the smaller total wins; ECM2_RUN_ORDER=slot|dof forces one.
+      std::vector<size_t> by_slot(out.size()), by_dof;
+      for (size_t g = 0; g < out.size(); g++) { by_slot[g] = g; }
+      {
+         std::vector<long> kmin(out.size(), LONG_MAX);
+         for (size_t g = 0; g < out.size(); g++)
+            for (int k : members[g])
+               for (int j = 0; j < r1s[k].n; j++) { kmin[g] = std::min<long>(kmin[g], dofs[r1s[k].i0 + j]); }
+         by_dof = by_slot;
+         std::stable_sort(by_dof.begin(), by_dof.end(), [&](size_t a, size_t b) { return kmin[a] < kmin[b]; });
+      }
+      auto lines_touched = [&](const std::vector<size_t> &go) {
+         long total = 0;
+         int in_window = 0;
+         std::vector<long> ids;
+         auto flush = [&] {
+            std::sort(ids.begin(), ids.end());
+            total += std::unique(ids.begin(), ids.end()) - ids.begin();
+            ids.clear();
+            in_window = 0;
+         };
+         for (size_t g : go)
+            for (int k : members[g])
+               for (int j = 0; j < r1s[k].n; j++)
+               {
+                  const int d = dofs[r1s[k].i0 + j];
+                  ids.push_back((long)d >> 4);
+                  for (int h = 0; h < cnt(d); h++) { ids.push_back((1l << 40) + (slot(d, h) >> 4)); }
+                  if (++in_window == 256) { flush(); }
+               }
+         flush();
+         return total;
+      };
+      const char *ro = std::getenv("ECM2_RUN_ORDER");
+      bool use_dof;
+      if (ro && std::string(ro) == "slot") { use_dof = false; }
+      else if (ro && std::string(ro) == "dof") { use_dof = true; }
+      else
+      {
+         const long ls = lines_touched(by_slot), ld = lines_touched(by_dof);
+         use_dof = ld < ls;
+         if (std::getenv("ECM2_PLAN_DUMP"))
+         {
+            std::fprintf(stderr, "plan range %d: lines touched by slot order %ld, by dof order %ld -> %s\n", range, ls, ld,
+                         use_dof ? "dof" : "slot");
+         }
+      }
+      const std::vector<size_t> &gord = use_dof ? by_dof : by_slot;
+      for (size_t g : gord)
       {
          out[g].first = (int)order.size();
          for (int k : members[g])

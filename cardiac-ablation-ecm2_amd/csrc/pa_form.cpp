@@ -467,21 +467,99 @@ void PAForm::build_shared_plan(const std::vector<int> &hcount, const std::vector
          flush();
          return total;
       };
+      // chain order: greedy, each next run the unplaced one sharing the most 128-B lines with the
+      // run placed last (ties and dead ends: the next unplaced run in slot order), so a face's edge
+      // runs follow its interior run and reuse its partial lines while they are in L2
+      auto chain_order = [&]() {
+         const size_t nr = out.size();
+         std::vector<std::vector<long>> rl(nr);
+         std::vector<long> all;
+         for (size_t g = 0; g < nr; g++)
+         {
+            for (int k : members[g])
+               for (int j = 0; j < r1s[k].n; j++)
+               {
+                  const int d = dofs[r1s[k].i0 + j];
+                  rl[g].push_back((long)d >> 4);
+                  for (int h = 0; h < cnt(d); h++) { rl[g].push_back((1l << 40) + (slot(d, h) >> 4)); }
+               }
+            std::sort(rl[g].begin(), rl[g].end());
+            rl[g].erase(std::unique(rl[g].begin(), rl[g].end()), rl[g].end());
+            all.insert(all.end(), rl[g].begin(), rl[g].end());
+         }
+         std::sort(all.begin(), all.end());
+         all.erase(std::unique(all.begin(), all.end()), all.end());
+         // line -> runs (CSR)
+         std::vector<int> loff(all.size() + 1, 0), lrun;
+         auto lid = [&](long v) { return (size_t)(std::lower_bound(all.begin(), all.end(), v) - all.begin()); };
+         std::vector<std::vector<int>> rli(nr);
+         for (size_t g = 0; g < nr; g++)
+            for (long v : rl[g])
+            {
+               const size_t i = lid(v);
+               rli[g].push_back((int)i);
+               loff[i + 1]++;
+            }
+         for (size_t i = 0; i < all.size(); i++) { loff[i + 1] += loff[i]; }
+         lrun.resize(loff.back());
+         {
+            std::vector<int> fill(loff.begin(), loff.end() - 1);
+            for (size_t g = 0; g < nr; g++)
+               for (int i : rli[g]) { lrun[fill[i]++] = (int)g; }
+         }
+         std::vector<char> placed(nr, 0);
+         std::vector<int> shared(nr, 0), touched;
+         std::vector<size_t> go;
+         go.reserve(nr);
+         size_t next_free = 0, cur = 0;
+         while (go.size() < nr)
+         {
+            if (go.empty() || placed[cur])
+            {
+               while (placed[next_free]) { next_free++; }
+               cur = next_free;
+            }
+            placed[cur] = 1;
+            go.push_back(cur);
+            size_t best = nr;
+            int bs = 0;
+            for (int i : rli[cur])
+               for (int q = loff[i]; q < loff[i + 1]; q++)
+               {
+                  const int g = lrun[q];
+                  if (placed[g]) { continue; }
+                  if (!shared[g]) { touched.push_back(g); }
+                  shared[g]++;
+               }
+            for (int g : touched)
+            {
+               if (shared[g] > bs || (shared[g] == bs && (size_t)g < best)) { bs = shared[g]; best = g; }
+               shared[g] = 0;
+            }
+            touched.clear();
+            cur = best < nr ? best : cur;  // cur placed: the next free run in slot order
+         }
+         return go;
+      };
       const char *ro = std::getenv("ECM2_RUN_ORDER");
-      bool use_dof;
-      if (ro && std::string(ro) == "slot") { use_dof = false; }
-      else if (ro && std::string(ro) == "dof") { use_dof = true; }
+      std::vector<size_t> by_chain;
+      int pick = 0;  // 0 slot, 1 dof, 2 chain
+      if (ro && std::string(ro) == "slot") { pick = 0; }
+      else if (ro && std::string(ro) == "dof") { pick = 1; }
+      else if (ro && std::string(ro) == "chain") { pick = 2; by_chain = chain_order(); }
       else
       {
-         const long ls = lines_touched(by_slot), ld = lines_touched(by_dof);
-         use_dof = ld < ls;
+         by_chain = chain_order();
+         const long ls = lines_touched(by_slot), ld = lines_touched(by_dof), lc = lines_touched(by_chain);
+         pick = ld < ls ? 1 : 0;
+         if (lc < std::min(ls, ld)) { pick = 2; }
          if (std::getenv("ECM2_PLAN_DUMP"))
          {
-            std::fprintf(stderr, "plan range %d: lines touched by slot order %ld, by dof order %ld -> %s\n", range, ls, ld,
-                         use_dof ? "dof" : "slot");
+            std::fprintf(stderr, "plan range %d: lines touched by slot order %ld, dof order %ld, chain order %ld -> %s\n",
+                         range, ls, ld, lc, pick == 2 ? "chain" : pick ? "dof" : "slot");
          }
       }
-      const std::vector<size_t> &gord = use_dof ? by_dof : by_slot;
+      const std::vector<size_t> &gord = pick == 2 ? by_chain : pick ? by_dof : by_slot;
       for (size_t g : gord)
       {
          out[g].first = (int)order.size();

@@ -579,21 +579,12 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
    double cc[6];
    if (AFF)
    {
-#ifndef ECM2_BRICK_NT
-#define ECM2_BRICK_NT 0
-#endif
-      if (ECM2_BRICK_NT)
-      {
+      // the point pairs are streamed once per Mult: nontemporal, so they do not evict the x lines
+      // neighbouring bricks gather again (profiles/r3_ab_bnt.txt: kernel -1%, Mult -2%)
 #pragma unroll
-         for (int qz = 0; qz < Q; qz++)
-         {
-            pa[qz] = __builtin_nontemporal_load(reinterpret_cast<const v2d *>(qdm) + (size_t)e * NQ + qz * QQ + l3c);
-         }
-      }
-      else
+      for (int qz = 0; qz < Q; qz++)
       {
-#pragma unroll
-         for (int qz = 0; qz < Q; qz++) { pa[qz] = reinterpret_cast<const v2d *>(qdm)[(size_t)e * NQ + qz * QQ + l3c]; }
+         pa[qz] = __builtin_nontemporal_load(reinterpret_cast<const v2d *>(qdm) + (size_t)e * NQ + qz * QQ + l3c);
       }
 #pragma unroll
       for (int c = 0; c < 6; c++) { cc[c] = qdd[(size_t)e * 6 + c]; }

@@ -442,13 +442,7 @@ k_sum_partials(int b0, int b1, const int *__restrict__ blocks, const int *__rest
    const int ds = pa * R[4] + pb * R[5];
    double v[4];
 #pragma unroll
-#ifndef ECM2_SUM_NT
-#define ECM2_SUM_NT 0
-#endif
-   for (int k = 0; k < 4; k++)
-   {
-      v[k] = k < cnt ? (ECM2_SUM_NT ? __builtin_nontemporal_load(part + R[8 + k] + ds) : part[R[8 + k] + ds]) : 0.0;
-   }
+   for (int k = 0; k < 4; k++) { v[k] = k < cnt ? part[R[8 + k] + ds] : 0.0; }
    double acc = 0.0;
 #pragma unroll
    for (int k = 0; k < 4; k++) { acc += v[k]; }

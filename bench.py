@@ -173,48 +173,58 @@ def member_bench(args, torch, group, xs, ys, ndofs, workload, dl):
     time gives the emulated N-GPU rate (ndofs / that time); every member's time is printed."""
     n = len(group.forms)
     members = list(range(n)) if args.member < 0 else [args.member]
-    per = []
     group.Mult(xs, ys)  # RAP: every member's ghost contributions, which a member's P^T receive copies
     torch.cuda.synchronize()
+    use_graph = args.member_graph if args.member_graph >= 0 else (
+        args.par_graph if args.par_graph >= 0 else int(args.schedule == "overlap"))
+    runs, graphs = {}, []
     for r in members:
-        dl.at(f"member {r}")
         for _ in range(3):
             group.MultMember(r, xs, ys)
         torch.cuda.synchronize()
-        use_graph = args.member_graph if args.member_graph >= 0 else (
-            args.par_graph if args.par_graph >= 0 else int(args.schedule == "overlap"))
         if use_graph:
             g = torch.cuda.CUDAGraph()
-            cs = torch.cuda.Stream()
-            with torch.cuda.graph(g, stream=cs):
+            with torch.cuda.graph(g, stream=torch.cuda.Stream()):
                 group.MultMember(r, xs, ys)
-            run = g.replay
+            graphs.append(g)
+            runs[r] = g.replay
         else:
-            g = None
-            run = lambda: group.MultMember(r, xs, ys)
-        t0 = time.perf_counter()
-        k = 0
-        while time.perf_counter() - t0 < 0.06:  # settle the clock (kernel_ms)
-            run()
-            k += 1
-            if k % 64 == 0:
-                torch.cuda.synchronize()
-        torch.cuda.synchronize()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ev0.record()
-        for _ in range(args.steps):
-            run()
-        ev1.record()
-        torch.cuda.synchronize()
-        per.append(ev0.elapsed_time(ev1) / args.steps)
-        del g, run
+            runs[r] = (lambda rr: (lambda: group.MultMember(rr, xs, ys)))(r)
+    # members interleaved over several passes, each member's time the median of its passes: one
+    # member timed once carries +-10% run-to-run noise, and the slowest of eight picks it up
+    # (profiles/r3_member_emul.txt)
+    passes = 3 if len(members) > 1 else 1
+    samples = {r: [] for r in members}
+    for p in range(passes):
+        for r in members:
+            dl.at(f"member {r} pass {p}")
+            run = runs[r]
+            t0 = time.perf_counter()
+            k = 0
+            while time.perf_counter() - t0 < 0.06:  # settle the clock (kernel_ms)
+                run()
+                k += 1
+                if k % 64 == 0:
+                    torch.cuda.synchronize()
+            torch.cuda.synchronize()
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+            for _ in range(args.steps):
+                run()
+            ev1.record()
+            torch.cuda.synchronize()
+            samples[r].append(ev0.elapsed_time(ev1) / args.steps)
+    per = [sorted(samples[r])[len(samples[r]) // 2] for r in members]
+    del runs, graphs
     worst = max(per)
     print(json.dumps({"emulated_n_gpus": n, "workload": workload, "ndofs": ndofs,
                       "member_ms": [round(v, 5) for v in per], "members": members,
+                      "member_passes_ms": [[round(v, 5) for v in samples[r]] for r in members],
                       "slowest_member_ms": round(worst, 5),
                       "emulated_value": round(ndofs / (worst * 1e-3) / 1e6, 2), "unit": "MDoF/s",
-                      "note": "one member's Mult alone on one GPU (graph replay), exchange by device copies: "
-                              "a rank's Mult short of the xGMI transfer time"}), flush=True)
+                      "note": f"one member's Mult alone on one GPU, exchange by device copies: a rank's Mult short "
+                              f"of the xGMI transfer time; members interleaved over {passes} passes, the median "
+                              "pass per member"}), flush=True)
 
 
 def pmc_pin(workload, world, layout):
@@ -422,6 +432,13 @@ def main():
             if f is None:
                 raise SystemExit(f"--partition boxes: no box factorisation for {nsub} parts")
             er = E.partition_boxes(mesh, f)
+        elif os.environ.get("ECM2_SLABS", "") == "balanced":
+            # A/B: equal element counts (z-major, then y, then x: a split layer divides along y)
+            import numpy as np
+            c = mesh.element_nodes().mean(axis=2)
+            order = np.lexsort((c[:, 0], c[:, 1], c[:, 2]))
+            er = np.empty(len(order), np.int32)
+            er[order] = (np.arange(len(order), dtype=np.int64) * nsub // len(order)).astype(np.int32)
         else:
             er = E.partition_slabs_z(mesh, nsub)
         if world > 1:

@@ -432,13 +432,6 @@ def main():
             if f is None:
                 raise SystemExit(f"--partition boxes: no box factorisation for {nsub} parts")
             er = E.partition_boxes(mesh, f)
-        elif os.environ.get("ECM2_SLABS", "") == "balanced":
-            # A/B: equal element counts (z-major, then y, then x: a split layer divides along y)
-            import numpy as np
-            c = mesh.element_nodes().mean(axis=2)
-            order = np.lexsort((c[:, 0], c[:, 1], c[:, 2]))
-            er = np.empty(len(order), np.int32)
-            er[order] = (np.arange(len(order), dtype=np.int64) * nsub // len(order)).astype(np.int32)
         else:
             er = E.partition_slabs_z(mesh, nsub)
         if world > 1:

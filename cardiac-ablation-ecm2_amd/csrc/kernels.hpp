@@ -176,42 +176,13 @@ __host__ __device__ constexpr int lattice_surface_index(int LX, int LY, int LZ, 
    if (X == LX - 1) { return b2 + (LZ - 2) * (LY - 2) + (Z - 1) * (LY - 2) + (Y - 1); }
    return -1;
 }
-// A/B: the same groups, each listing its face-interior points first (lexicographic in the face)
-// and then its ring (the points also on another face), so a face's 2-holder run reads whole
-// lines of both holders' groups and the edge runs read lines of their own.
-__host__ __device__ constexpr int lattice_surface_index_ring(int LX, int LY, int LZ, int X, int Y, int Z)
-{
-   if (Z == 0 || Z == LZ - 1)
-   {
-      const int g = Z == 0 ? 0 : LX * LY, ni = (LX - 2) * (LY - 2);
-      if (X > 0 && X < LX - 1 && Y > 0 && Y < LY - 1) { return g + (Y - 1) * (LX - 2) + (X - 1); }
-      if (Y == 0) { return g + ni + X; }
-      if (Y == LY - 1) { return g + ni + LX + X; }
-      return g + ni + 2 * LX + (X == 0 ? 0 : LY - 2) + (Y - 1);
-   }
-   const int b1 = 2 * LX * LY;
-   if (Y == 0 || Y == LY - 1)
-   {
-      const int g = b1 + (Y == 0 ? 0 : (LZ - 2) * LX), ni = (LZ - 2) * (LX - 2);
-      if (X > 0 && X < LX - 1) { return g + (Z - 1) * (LX - 2) + (X - 1); }
-      return g + ni + (X == 0 ? 0 : LZ - 2) + (Z - 1);
-   }
-   const int b2 = b1 + 2 * (LZ - 2) * LX;
-   if (X == 0) { return b2 + (Z - 1) * (LY - 2) + (Y - 1); }
-   if (X == LX - 1) { return b2 + (LZ - 2) * (LY - 2) + (Z - 1) * (LY - 2) + (Y - 1); }
-   return -1;
-}
-#ifndef ECM2_SURF_RING
-#define ECM2_SURF_RING 0  // bit 0: bricks (p >= 3), bit 1: p <= 2 blocks
-#endif
 __host__ __device__ constexpr int brick_surface_points(int D, int bz)
 {
    return lattice_surface_points(2 * D - 1, 2 * D - 1, bz * (D - 1) + 1);
 }
 __host__ __device__ constexpr int brick_surface_index(int D, int bz, int X, int Y, int Z)
 {
-   return (ECM2_SURF_RING & 1) ? lattice_surface_index_ring(2 * D - 1, 2 * D - 1, bz * (D - 1) + 1, X, Y, Z)
-                               : lattice_surface_index(2 * D - 1, 2 * D - 1, bz * (D - 1) + 1, X, Y, Z);
+   return lattice_surface_index(2 * D - 1, 2 * D - 1, bz * (D - 1) + 1, X, Y, Z);
 }
 // the same for a p <= 2 block (4 x 4 x 4 elements, lattice 4 (D-1) + 1 per side)
 __host__ __device__ inline int tpe_surface_points(int D)
@@ -220,8 +191,7 @@ __host__ __device__ inline int tpe_surface_points(int D)
 }
 __host__ __device__ inline int tpe_surface_index(int D, int X, int Y, int Z)
 {
-   return (ECM2_SURF_RING & 2) ? lattice_surface_index_ring(4 * D - 3, 4 * D - 3, 4 * D - 3, X, Y, Z)
-                               : lattice_surface_index(4 * D - 3, 4 * D - 3, 4 * D - 3, X, Y, Z);
+   return lattice_surface_index(4 * D - 3, 4 * D - 3, 4 * D - 3, X, Y, Z);
 }
 
 // Block lattice map (lattice-slot blocks): one entry per point of the block's (4(D-1)+1)^3

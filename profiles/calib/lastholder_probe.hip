@@ -1,0 +1,147 @@
+// Probe (profiles/calib, not product code): prices a fused "last holder finishes" summation
+// against the two-pass scheme the apply kernels use (partial slots, then k_sum_partials).
+//
+// A chain of blocks: block b holds faces b-1 and b (face f is shared by blocks f and f+1), M
+// points per face.  Each block computes a synthetic value per (face, point).
+//   two-pass : every block stores its two partials to part[face][holder][pt]; a second kernel
+//              sums y[face][pt] = part[f][0][pt] + part[f][1][pt].
+//   fused    : every block stores its partials, an agent-scope release fence, one vector atomic
+//              per face on an arrival counter (the counters are never reset: odd = second
+//              arrival); the second holder issues an agent-scope acquire fence, reads the first
+//              holder's partial and stores y.  2-holder sums are commutative, so y is bitwise
+//              the two-pass result whichever holder arrives last.
+// Checked: y of both schemes bitwise equal.  Timed: HIP events over R repetitions each.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#define CK(x)                                                                               \
+   do                                                                                       \
+   {                                                                                        \
+      hipError_t e_ = (x);                                                                  \
+      if (e_ != hipSuccess) { fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); exit(1); } \
+   } while (0)
+
+constexpr int M = 81;   // points per face (a p = 4 brick's z face)
+constexpr int NT = 128; // threads per block
+
+__device__ __forceinline__ double val(int b, int f, int p) { return 1e-3 * (double)((b * 131 + f * 17 + p * 7) % 1009) + 0.5; }
+
+__global__ void __launch_bounds__(NT) k_write_partials(int nb, double *__restrict__ part)
+{
+   const int b = blockIdx.x;
+   for (int i = threadIdx.x; i < 2 * M; i += NT)
+   {
+      const int side = i / M, p = i % M;
+      const int f = b - 1 + side;  // side 0: face b-1 (this block is its holder 1), side 1: face b (holder 0)
+      if (f < 0 || f >= nb - 1) { continue; }
+      part[((size_t)f * 2 + (side == 0 ? 1 : 0)) * M + p] = val(b, f, p);
+   }
+}
+
+__global__ void __launch_bounds__(256) k_sum(int nf, const double *__restrict__ part, double *__restrict__ y)
+{
+   const long i = (long)blockIdx.x * 256 + threadIdx.x;
+   if (i >= (long)nf * M) { return; }
+   const long f = i / M, p = i % M;
+   y[i] = part[(f * 2) * M + p] + part[(f * 2 + 1) * M + p];
+}
+
+__global__ void __launch_bounds__(NT) k_fused(int nb, double *__restrict__ part, unsigned *__restrict__ cnt,
+                                              double *__restrict__ y)
+{
+   __shared__ unsigned last[2];
+   const int b = blockIdx.x;
+   for (int i = threadIdx.x; i < 2 * M; i += NT)
+   {
+      const int side = i / M, p = i % M;
+      const int f = b - 1 + side;
+      if (f < 0 || f >= nb - 1) { continue; }
+      part[((size_t)f * 2 + (side == 0 ? 1 : 0)) * M + p] = val(b, f, p);
+   }
+   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+   __syncthreads();
+   if (threadIdx.x < 2)
+   {
+      const int f = b - 1 + (int)threadIdx.x;
+      unsigned old = 0;
+      if (f >= 0 && f < nb - 1) { old = __hip_atomic_fetch_add(cnt + f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+      last[threadIdx.x] = (f >= 0 && f < nb - 1) ? (old & 1u) : 0u;
+   }
+   __syncthreads();
+   if (!last[0] && !last[1]) { return; }
+   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+   for (int i = threadIdx.x; i < 2 * M; i += NT)
+   {
+      const int side = i / M, p = i % M;
+      if (!last[side]) { continue; }
+      const int f = b - 1 + side;
+      const int mine = side == 0 ? 1 : 0;
+      const double other = part[((size_t)f * 2 + (1 - mine)) * M + p];
+      const double v = val(b, f, p);
+      y[(size_t)f * M + p] = mine == 0 ? v + other : other + v;  // holder 0's value first (commutative anyway)
+   }
+}
+
+int main(int argc, char **argv)
+{
+   const int nb = argc > 1 ? atoi(argv[1]) : 120000, R = argc > 2 ? atoi(argv[2]) : 50;
+   const int nf = nb - 1;
+   const size_t np = (size_t)nf * 2 * M, ny = (size_t)nf * M;
+   double *part, *y1, *y2;
+   unsigned *cnt;
+   CK(hipMalloc(&part, np * 8));
+   CK(hipMalloc(&y1, ny * 8));
+   CK(hipMalloc(&y2, ny * 8));
+   CK(hipMalloc(&cnt, (size_t)nf * 4));
+   CK(hipMemset(cnt, 0, (size_t)nf * 4));
+   CK(hipMemset(y1, 0, ny * 8));
+   CK(hipMemset(y2, 0, ny * 8));
+   hipEvent_t e0, e1;
+   CK(hipEventCreate(&e0));
+   CK(hipEventCreate(&e1));
+   const int g2 = (int)((ny + 255) / 256);
+   auto two_pass = [&]() {
+      hipLaunchKernelGGL(k_write_partials, dim3(nb), dim3(NT), 0, 0, nb, part);
+      hipLaunchKernelGGL(k_sum, dim3(g2), dim3(256), 0, 0, nf, part, y1);
+   };
+   auto fused = [&]() { hipLaunchKernelGGL(k_fused, dim3(nb), dim3(NT), 0, 0, nb, part, cnt, y2); };
+   for (int w = 0; w < 5; w++) { two_pass(); fused(); }
+   CK(hipDeviceSynchronize());
+   float ms_a = 0, ms_b = 0, ms_w = 0;
+   for (int rep = 0; rep < 2; rep++)
+   {
+      CK(hipEventRecord(e0));
+      for (int r = 0; r < R; r++) { two_pass(); }
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&ms_a, e0, e1));
+      CK(hipEventRecord(e0));
+      for (int r = 0; r < R; r++) { fused(); }
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&ms_b, e0, e1));
+      CK(hipEventRecord(e0));
+      for (int r = 0; r < R; r++) { hipLaunchKernelGGL(k_write_partials, dim3(nb), dim3(NT), 0, 0, nb, part); }
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&ms_w, e0, e1));
+      printf("rep %d  faces %d x %d points: two-pass %.2f us (write kernel alone %.2f us), fused %.2f us\n", rep, nf, M,
+             1e3 * ms_a / R, 1e3 * ms_w / R, 1e3 * ms_b / R);
+   }
+   // correctness: fresh y, one call each
+   CK(hipMemset(y1, 0, ny * 8));
+   CK(hipMemset(y2, 0, ny * 8));
+   two_pass();
+   fused();
+   CK(hipDeviceSynchronize());
+   std::vector<double> h1(ny), h2(ny);
+   CK(hipMemcpy(h1.data(), y1, ny * 8, hipMemcpyDeviceToHost));
+   CK(hipMemcpy(h2.data(), y2, ny * 8, hipMemcpyDeviceToHost));
+   size_t bad = 0;
+   for (size_t i = 0; i < ny; i++) { bad += memcmp(&h1[i], &h2[i], 8) != 0; }
+   printf("bitwise mismatches: %zu of %zu\n", bad, ny);
+   return bad ? 2 : 0;
+}

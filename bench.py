@@ -302,6 +302,9 @@ def main():
                          "FiniteElementSpace vertex/edge/face/interior numbering, element order derived by the form)")
     ap.add_argument("--mesh", choices=["affine", "trilinear"], default="affine",
                     help="c2/c4/c5 main line: the Cartesian mesh (affine) or its interior vertices moved (trilinear)")
+    ap.add_argument("--geometry-input", choices=["nodes", "jacobians"], default="nodes",
+                    help="c2/c4/c5 main line: geometry given as element corners (nodes) or as MFEM's "
+                         "GeometricFactors::JACOBIANS array (what the reference-side binding passes)")
     ap.add_argument("--loopback", type=int, default=1,
                     help="N>1 on one GPU: N subdomains in this process (validation of the partitioned path)")
     ap.add_argument("--partition", choices=["slabs", "boxes"], default="slabs",
@@ -382,14 +385,20 @@ def main():
     form = None
     keep = []
 
-    def serial_form(compress_geometry, mesh=mesh, fes=fes, numbering=args.numbering):
+    def serial_form(compress_geometry, mesh=mesh, fes=fes, numbering=args.numbering, geo=args.geometry_input):
         a, T = bioheat_coefficients(E, torch, mesh, fes)
         keep.extend([a, T])
         # the reference's numbering: no mesh knowledge, the form derives its order from the map
         eo = "faces" if numbering == "entity" and args.workload != "c3" else "auto"
         f = E.BilinearForm(fes, kernel=kernel, element_order=os.environ.get("ECM2_ELEMENT_ORDER", eo),
                            scatter=scatter, compress_geometry=compress_geometry,
-                           bricks=int(os.environ.get("ECM2_BRICKS", "-1")))  # A/B: p >= 3 brick depth
+                           bricks=int(os.environ.get("ECM2_BRICKS", "-1")),  # A/B: p >= 3 brick depth
+                           geometry="jacobians" if geo == "jacobians" else "nodes")
+        if geo == "jacobians":
+            # MFEM's GeometricFactors::JACOBIANS (NQ x 3 x 3 x NE), as the binding passes it; the form
+            # fits it to trilinear maps (or checks it affine) at Assemble and keeps it for re-assembly
+            J = mesh.jacobians(fes.order + 2)
+            f.SetJacobians(J)
         f.AddDomainIntegrator(mass(a))
         f.AddDomainIntegrator(diff(T))
         f.Assemble()
@@ -537,6 +546,16 @@ def main():
                            "layout stores the elements' trilinear-map coefficients and the kernel evaluates J, "
                            "adj(J) and det J at every quadrature point (the per-point layout is full_layout's)")
         del fv, me, fe_, mt, ft
+        dl.at("drop-in configuration")
+        md, fd = cartesian_space(E, nx, ny, nz_total, order, "entity", "trilinear")
+        fv = serial_form(compress, md, fd, "entity", "jacobians")
+        subs["drop_in"] = sub_measure(
+            fv, fd, "enttrijac", "same run, the configuration a drop-in ECM2PABilinearFormExtension executes "
+                                 "(INTEGRATION.md): the reference's own numbering (SFC element order, entity dofs), "
+                                 "non-affine hexes (interior vertices moved by up to 0.15 h) and the geometry as MFEM's "
+                                 "GeometricFactors::JACOBIANS array (set_jacobians, fitted to trilinear maps at "
+                                 "Assemble)")
+        del fv, md, fd
 
     if rank == 0:
         dl.at("stream copy peak")
@@ -597,10 +616,12 @@ def main():
 
 
 def variant_key(args):
-    """Suffix of the PMC pin of the main line's variant: '' structured affine, 'ent', 'tri'."""
+    """Suffix of the PMC pin of the main line's variant: '' structured affine, 'ent', 'tri', 'jac'
+    (geometry as MFEM Jacobians) and their combinations ('enttrijac': the drop-in configuration)."""
     if args.workload == "c3":
         return ""
-    return ("ent" if args.numbering == "entity" else "") + ("tri" if args.mesh == "trilinear" else "")
+    return (("ent" if args.numbering == "entity" else "") + ("tri" if args.mesh == "trilinear" else "")
+            + ("jac" if args.geometry_input == "jacobians" else ""))
 
 
 def cartesian_space(E, nx, ny, nz, order, numbering, shape):

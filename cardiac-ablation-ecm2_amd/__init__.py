@@ -257,6 +257,30 @@ class Mesh:
         _check(_lib.ecm2_mesh_quadrature_points(self._h, q1d, _np_ptr(out)))
         return out
 
+    def jacobians(self, q1d: int, device="cuda"):
+        """GeometricFactors::JACOBIANS of the trilinear elements at the q1d^3 Gauss-Legendre
+        points (mesh.cpp:15220-15273): a torch float64 tensor in MFEM's layout NQ x 3 x 3 x NE,
+        J(q, i, j, e) = d x_i / d xi_j, q lexicographic (qx fastest) -- the array the reference-side
+        binding hands ecm2_pa_form_set_jacobians.  Computed with torch on
+        `device` from the corners (the caller's data, not the product path)."""
+        import torch
+        t, _ = np.polynomial.legendre.leggauss(q1d)
+        t = 0.5 * (t + 1.0)
+        z = torch.as_tensor(self.element_nodes(), device=device)  # [e][i][corner], corner = cx + 2 cy + 4 cz
+        # d N_c / d xi_j at every point: N_c = prod_k (xi_k if c_k else 1 - xi_k)
+        dN = np.zeros((q1d ** 3, 8, 3))
+        for q in range(q1d ** 3):
+            xi = (t[q % q1d], t[(q // q1d) % q1d], t[q // (q1d * q1d)])
+            for c in range(8):
+                ck = (c & 1, (c >> 1) & 1, (c >> 2) & 1)
+                f = [xi[k] if ck[k] else 1.0 - xi[k] for k in range(3)]
+                for j in range(3):
+                    g = 1.0 if ck[j] else -1.0
+                    dN[q, c, j] = g * np.prod([f[k] for k in range(3) if k != j])
+        dN = torch.as_tensor(dN, device=device)
+        # J[e][j][i][q] flattened is MFEM's J(q, i, j, e)
+        return torch.einsum("eic,qcj->ejiq", z, dN).contiguous()
+
     def element_nodes(self) -> np.ndarray:
         """Lexicographic corner coordinates [ne][3][8]."""
         out = np.empty((self.GetNE(), 3, 8), np.float64)

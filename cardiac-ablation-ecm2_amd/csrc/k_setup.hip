@@ -385,16 +385,19 @@ k_setup_affine(const int *__restrict__ perm, int ne, const double *__restrict__ 
    }
 }
 
-// TRILINEAR layout (kernels.hpp): per point the pair (W_q beta_q, W_q alpha_q) -- det J is
-// evaluated by the apply kernel -- and, from the q = 0 threads, the element's trilinear-map
-// coefficients c1..c7 of each coordinate from its lexicographic corners X_a (a = ax + 2 ay + 4 az):
-// c1 = X1 - X0, c2 = X2 - X0, c3 = X4 - X0, c4 = X3 - X2 - X1 + X0, c5 = X5 - X4 - X1 + X0,
-// c6 = X6 - X4 - X2 + X0, c7 = X7 - X6 - X5 - X3 + X4 + X2 + X1 - X0.
+// TRILINEAR layout (kernels.hpp): per point the pair (W_q beta_q / det J_q, W_q alpha_q det J_q)
+// -- the scalar factors of PADiffusionSetup3D's D = W beta adj(J) adj(J)^T / det J
+// (bilininteg_diffusion_kernels.cpp:349-362) and of the mass setup's W alpha det J
+// (bilininteg_mass_pa.cpp:76); the apply kernel evaluates adj(J) -- and, from the q = 0 threads,
+// the element's trilinear-map coefficients c1..c7 of each coordinate from its lexicographic
+// corners X_a (a = ax + 2 ay + 4 az): c1 = X1 - X0, c2 = X2 - X0, c3 = X4 - X0,
+// c4 = X3 - X2 - X1 + X0, c5 = X5 - X4 - X1 + X0, c6 = X6 - X4 - X2 + X0,
+// c7 = X7 - X6 - X5 - X3 + X4 + X2 + X1 - X0.
 template <int Q>
 __global__ void __launch_bounds__(256)
 k_setup_trilinear(const int *__restrict__ perm, int ne, const double *__restrict__ enodes,
-                  const double *__restrict__ cfit, const double *__restrict__ W, SetupCoef cm, SetupCoef cd,
-                  double *__restrict__ qd_geo, double *__restrict__ qd_pair)
+                  const double *__restrict__ cfit, const double *__restrict__ W, const QPts qp, SetupCoef cm,
+                  SetupCoef cd, double *__restrict__ qd_geo, double *__restrict__ qd_pair)
 {
    constexpr int NQ = Q * Q * Q;
    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -405,13 +408,6 @@ k_setup_trilinear(const int *__restrict__ perm, int ne, const double *__restrict
    const int ipos = (int)(blk * 64 + lane);
    if (ipos >= ne) { return; }
    const int e = perm ? perm[ipos] : ipos;
-   const size_t eq = (size_t)e * NQ + q;
-   const double w = W[q];
-   v2d pr;
-   pr.x = w * coef_at(cd, eq, e);
-   pr.y = w * coef_at(cm, eq, e);
-   reinterpret_cast<v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane] = pr;
-   if (q != 0) { return; }
    double c[2 * kTrilinPairs];
    if (cfit)  // fitted from MFEM-layout Jacobians (k_jac_trilinear_fit)
    {
@@ -431,6 +427,27 @@ k_setup_trilinear(const int *__restrict__ perm, int ne, const double *__restrict
       c[6 * 3 + i] = ((x[7] - x[6]) - (x[5] - x[4])) - ((x[3] - x[2]) - (x[1] - x[0]));
    }
    c[21] = 0.0;
+   // det J at the point from the map (the apply kernel's J: J[.][0] = c1 + c4 eta + c5 zeta +
+   // c7 eta zeta, J[.][1] = c2 + c4 xi + c6 zeta + c7 xi zeta, J[.][2] = c3 + c5 xi + c6 eta + c7 xi eta)
+   const double xi = qp.x[q % Q], et = qp.x[(q / Q) % Q], zt = qp.x[q / (Q * Q)];
+   double J[3][3];
+#pragma unroll
+   for (int i = 0; i < 3; i++)
+   {
+      J[i][0] = (c[0 * 3 + i] + c[4 * 3 + i] * zt) + (c[3 * 3 + i] + c[6 * 3 + i] * zt) * et;
+      J[i][1] = (c[1 * 3 + i] + c[5 * 3 + i] * zt) + (c[3 * 3 + i] + c[6 * 3 + i] * zt) * xi;
+      J[i][2] = (c[2 * 3 + i] + c[5 * 3 + i] * et) + (c[4 * 3 + i] + c[6 * 3 + i] * et) * xi;
+   }
+   const double det = J[0][0] * (J[1][1] * J[2][2] - J[1][2] * J[2][1]) -
+                      J[0][1] * (J[1][0] * J[2][2] - J[1][2] * J[2][0]) +
+                      J[0][2] * (J[1][0] * J[2][1] - J[1][1] * J[2][0]);
+   const size_t eq = (size_t)e * NQ + q;
+   const double w = W[q];
+   v2d pr;
+   pr.x = w * coef_at(cd, eq, e) / det;
+   pr.y = w * coef_at(cm, eq, e) * det;
+   reinterpret_cast<v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane] = pr;
+   if (q != 0) { return; }
    v2d *dst = reinterpret_cast<v2d *>(qd_geo + (size_t)blk * kTrilinPairs * 128) + lane;
 #pragma unroll
    for (int k = 0; k < kTrilinPairs; k++) { dst[k * 64] = v2d{c[2 * k], c[2 * k + 1]}; }
@@ -535,9 +552,8 @@ k_trilinear_expand(int ne, const double *__restrict__ qd_geo, const double *__re
                 A23 = J[1][0] * J[0][2] - J[0][0] * J[1][2];
    const double A31 = J[1][0] * J[2][1] - J[2][0] * J[1][1], A32 = J[2][0] * J[0][1] - J[0][0] * J[2][1],
                 A33 = J[0][0] * J[1][1] - J[0][1] * J[1][0];
-   const double det = J[0][0] * A11 + J[1][0] * A12 + J[2][0] * A13;
    const v2d pr = reinterpret_cast<const v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane];
-   const double sc = pr.x / det;
+   const double sc = pr.x;  // W beta / det J
    v2d p0, p1, p2;
    p0.x = sc * (A11 * A11 + A12 * A12 + A13 * A13);
    p0.y = sc * (A11 * A21 + A12 * A22 + A13 * A23);
@@ -549,7 +565,7 @@ k_trilinear_expand(int ne, const double *__restrict__ qd_geo, const double *__re
    dst[0] = p0;
    dst[64] = p1;
    dst[128] = p2;
-   qd_mass[((size_t)blk * ((NQ + 1) / 2) + (q >> 1)) * 128 + lane * 2 + (q & 1)] = pr.y * det;
+   qd_mass[((size_t)blk * ((NQ + 1) / 2) + (q >> 1)) * 128 + lane * 2 + (q & 1)] = pr.y;  // W alpha det J
 }
 
 SetupCoef make_setup_coef(const CoeffDesc *c, const double *q)
@@ -670,8 +686,8 @@ bool jacobians_trilinear_fit(int ne, int Q, const QPts &qp, const double *J, dou
 }
 
 void setup_trilinear(const QLayout &L, int Q, const double *enodes, const double *cfit, const double *W,
-                     const CoeffDesc *cm, const CoeffDesc *cd, const double *cm_q, const double *cd_q, double *qd_geo,
-                     double *qd_pair, hipStream_t s)
+                     const QPts &qp, const CoeffDesc *cm, const CoeffDesc *cd, const double *cm_q, const double *cd_q,
+                     double *qd_geo, double *qd_pair, hipStream_t s)
 {
    if (L.ne == 0) { return; }
    ECM2_VERIFY(L.kind == QLAYOUT_TRILINEAR && cm && cd && (enodes || cfit), ERR_INTERNAL,
@@ -682,12 +698,12 @@ void setup_trilinear(const QLayout &L, int Q, const double *enodes, const double
    if (Q == 3)
    {
       hipLaunchKernelGGL((k_setup_trilinear<3>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.perm, L.ne, enodes,
-                         cfit, W, scm, scd, qd_geo, qd_pair);
+                         cfit, W, qp, scm, scd, qd_geo, qd_pair);
    }
    else if (Q == 4)
    {
       hipLaunchKernelGGL((k_setup_trilinear<4>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.perm, L.ne, enodes,
-                         cfit, W, scm, scd, qd_geo, qd_pair);
+                         cfit, W, qp, scm, scd, qd_geo, qd_pair);
    }
    else { ECM2_VERIFY(false, ERR_UNSUPPORTED, "trilinear setup: Q1D " << Q << " not instantiated"); }
    ECM2_HIP(hipGetLastError());

@@ -334,10 +334,10 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 // so it addresses x / y only; 3 every block a lattice-map block (the reference's numbering on a
 // Cartesian mesh): the map loads are the first loads of the gather chain.
 // TL (TRILINEAR layout, kernels.hpp): the element's trilinear-map coefficients instead of C,
-// and the point pair (W beta, W alpha); J, adj(J), det J evaluated at every point: per plane
-// (zeta) the J pieces A = c1 + c5 zeta, B = c4 + c7 zeta, Cz = c2 + c6 zeta, per row (eta)
+// and the point pair (W beta / det J, W alpha det J); J and adj(J) evaluated at every point: per
+// plane (zeta) the J pieces A = c1 + c5 zeta, B = c4 + c7 zeta, Cz = c2 + c6 zeta, per row (eta)
 // J[.][0] = A + B eta, G = c3 + c6 eta, H = c5 + c7 eta, per point (xi) J[.][1] = Cz + B xi,
-// J[.][2] = G + H xi; then f = (W beta / det J) adj(J) (adj(J)^T grad u), m = W alpha det J u --
+// J[.][2] = G + H xi; then f = (W beta / det J) adj(J) (adj(J)^T grad u), m = (W alpha det J) u --
 // PADiffusionSetup3D's D = W beta adj(J) adj(J)^T / det J (bilininteg_diffusion_kernels.cpp:
 // 349-362) and the mass setup's W alpha det J, never stored.
 template <int D, int Q, bool SPLIT, int RM, bool TL = false>
@@ -538,8 +538,7 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                                A23 = ja[1] * jc0 - ja[0] * jc1;
                   const double A31 = ja[1] * jb2 - ja[2] * jb1, A32 = ja[2] * jb0 - ja[0] * jb2,
                                A33 = ja[0] * jb1 - jb0 * ja[1];
-                  const double det = ja[0] * A11 + ja[1] * A12 + ja[2] * A13;
-                  const double sc = sa.x / det;
+                  const double sc = sa.x;  // W beta / det J (setup)
                   double t1 = A11 * ux;
                   t1 += A21 * uy;
                   t1 += A31 * uz;
@@ -549,7 +548,7 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                   double t3 = A13 * ux;
                   t3 += A23 * uy;
                   t3 += A33 * uz;
-                  m = (sa.y * det) * u;
+                  m = sa.y * u;  // W alpha det J
                   fx = sc * (A11 * t1 + A12 * t2 + A13 * t3);
                   fy = sc * (A21 * t1 + A22 * t2 + A23 * t3);
                   fz = sc * (A31 * t1 + A32 * t2 + A33 * t3);
@@ -650,6 +649,291 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                                                          blk, lane, active, n_owned, y, yg, part, &sX[0][0][0], w,
                                                          wave_on, rg, regf, pstride,
                                                          lmap ? lmap + (size_t)blk * tpe_lattice_points(D) : nullptr);
+}
+
+// Lattice coordinates of a block's lattice slots (the inverse of tpe_lattice_slot): X | Y << 5 | Z << 10.
+template <int D>
+struct LatticeXYZ
+{
+   static constexpr int L = 4 * (D - 1) + 1, N = L * L * L;
+   unsigned short v[N];
+   constexpr LatticeXYZ() : v()
+   {
+      for (int Z = 0; Z < L; Z++)
+         for (int Y = 0; Y < L; Y++)
+            for (int X = 0; X < L; X++) { v[tpe_lattice_slot(D, X, Y, Z)] = (unsigned short)(X | Y << 5 | Z << 10); }
+   }
+};
+__constant__ LatticeXYZ<2> kLatXYZ2 = LatticeXYZ<2>();
+__constant__ LatticeXYZ<3> kLatXYZ3 = LatticeXYZ<3>();
+template <int D>
+__device__ __forceinline__ unsigned lattice_xyz(int j)
+{
+   if constexpr (D == 2) { return kLatXYZ2.v[j]; }
+   else { return kLatXYZ3.v[j]; }
+}
+
+// TRILINEAR apply for forms whose blocks are all 4x4x4 bricks of one dof lattice (RM 1: regular
+// blocks, 3: lattice-map blocks -- the structured numbering and the reference's numbering on a
+// brick-tiled mesh), at TWO waves per SIMD.  The per-element kernel above (k_apply_tpe_sf, TL)
+// keeps the 27 x-values per element in LDS and the 27 outputs in registers: 408 VGPR+AGPR, one
+// wave per SIMD and ~290 AGPR copies per plane, which made it VALU-bound at 0.47 of the HBM peak
+// (profiles/r4_*).  Here (a) the block's x values are gathered ONCE per lattice point into LDS in
+// the lattice-slot order (729 doubles per 64 elements at p = 2 instead of 1728: the 64 lanes' reads
+// of one element entry hit one contiguous sub-block of a residue class, and the gather issues 12
+// coalesced map loads per lane instead of 27); (b) the element outputs live in LDS ([a][lane], the
+// same region then stages the cross-wave face exchange) and every plane adds its z-transpose into
+// them; (c) the per-point pair is (W beta / det J, W alpha det J), so no determinant or division
+// per point.  LDS 78.6 KB per workgroup: two workgroups (8 waves) per CU.
+template <int D, int Q, bool SPLIT, int RM>
+__global__ void __launch_bounds__(256, 2)
+k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
+                const double *__restrict__ qdd, const double *__restrict__ qdm,
+                const double *__restrict__ x, const double *__restrict__ xg,
+                double *__restrict__ y, double *__restrict__ yg, const Basis1D b,
+                const double *__restrict__ rowtab, const int *__restrict__ lane_flags, double *__restrict__ part,
+                const int *__restrict__ treg, int pstride, const int *__restrict__ lmap, const QPts qp)
+{
+   static_assert(RM == 1 || RM == 3, "lattice blocks only");
+   static_assert(Q % 2 == 0, "ping-pong rows");
+   constexpr int ND = D * D * D, NQ = Q * Q * Q, NR = Q * Q, XR = XwaveRows<D>::R, WPG = 4, P = D - 1;
+   constexpr int NLP = tpe_lattice_points(D);
+   static_assert(XR >= ND, "outputs fit the staging rows");
+   __shared__ double sXL[WPG][NLP];   // the block's x values in lattice-slot order
+   __shared__ double sY[WPG][XR][64]; // element outputs [a][lane]; then the cross-wave face exchange
+   const int lane = threadIdx.x & 63;
+   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+   const int blk = blk_begin + (int)blockIdx.x * WPG + w;
+   const bool wave_on = blk < blk_end;  // wave-uniform; every wave reaches the barriers
+   const int e = blk * 64 + lane;
+   const bool active = wave_on && e < ne;
+   const int *mp = gmap + (size_t)blk * ND * 64 + lane;
+   const int ex = lane & 3, ey = (lane >> 2) & 3, ez = lane >> 4;
+   TpeReg rg = {};
+   const int regf = RM == 1 ? 1 : 2;
+   auto ld2 = [&](const double *p) -> v2d { return __builtin_nontemporal_load(reinterpret_cast<const v2d *>(p)); };
+   constexpr int NCE = kTrilinPairs;
+   v2d ce[NCE];
+   const double *qa = qdm + (size_t)blk * NQ * 128 + lane * 2;
+   v2d ca[Q];
+   auto load_row = [&](int row, v2d (&aq)[Q]) {
+#pragma unroll
+      for (int qx = 0; qx < Q; qx++) { aq[qx] = ld2(qa + (size_t)(row * Q + qx) * 128); }
+   };
+   if (wave_on)
+   {
+      // geometry and the first row's pairs first: independent of the gather chain
+      const double *qc = qdd + (size_t)blk * NCE * 128 + lane * 2;
+#pragma unroll
+      for (int k = 0; k < NCE; k++) { ce[k] = ld2(qc + k * 128); }
+      load_row(0, ca);
+      if (RM == 1)
+      {
+         const int *r = treg + (size_t)blk * 8;  // wave-uniform: scalar loads
+         rg = TpeReg{r[0], r[1], r[2], r[3], r[4]};
+      }
+      const int *lm = lmap + (size_t)blk * NLP;
+#pragma unroll
+      for (int k = 0; k < (NLP + 63) / 64; k++)
+      {
+         const int j = lane + 64 * k;
+         if (j < NLP)
+         {
+            int d;
+            if (RM == 3) { d = bdof(lm[j]); }
+            else
+            {
+               const unsigned v = lattice_xyz<D>(j);
+               d = rg.base + (int)(v & 31) * rg.sx + (int)((v >> 5) & 31) * rg.sy + (int)(v >> 10) * rg.sz;
+            }
+            sXL[w][j] = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
+         }
+      }
+#pragma unroll
+      for (int a = 0; a < ND; a++) { sY[w][a][lane] = 0.0; }
+   }
+   __syncthreads();  // the lattice is read by every lane of the wave
+   if (wave_on)
+   {
+      auto cf = [&](int k, int i) -> double {
+         const int f = 3 * k + i;
+         return (f & 1) ? ce[f >> 1].y : ce[f >> 1].x;
+      };
+      // lane part of a lattice slot per residue class (cx, cy): ((ez) ny + ey) nx + ex
+      auto lane_base = [&](int cx, int cy) {
+         const int nx = tpe_lattice_class_n(cx), ny = tpe_lattice_class_n(cy);
+         return (ez * ny + ey) * nx + ex;
+      };
+#pragma unroll 1
+      for (int qz = 0; qz < Q; qz++)
+      {
+         double bz[D], gz[D];
+#pragma unroll
+         for (int dz = 0; dz < D; dz++) { bz[dz] = b.B[qz + MQ * dz]; gz[dz] = b.G[qz + MQ * dz]; }
+         double pA[3], pB[3], pC[3];  // the plane's J pieces
+         {
+            // opaque per plane: otherwise the compiler hoists every plane's and row's J pieces out of
+            // the plane loop into a table (in scratch)
+            double zt = qp.x[qz];
+            asm volatile("" : "+s"(zt));
+#pragma unroll
+            for (int i = 0; i < 3; i++)
+            {
+               pA[i] = cf(0, i) + cf(4, i) * zt;
+               pB[i] = cf(3, i) + cf(6, i) * zt;
+               pC[i] = cf(1, i) + cf(5, i) * zt;
+            }
+         }
+         double SB[D][D], SG[D][D];
+#pragma unroll
+         for (int dy = 0; dy < D; dy++)
+#pragma unroll
+            for (int dx = 0; dx < D; dx++) { SB[dy][dx] = 0.0; SG[dy][dx] = 0.0; }
+         auto row_body = [&](const int qy, v2d (&cur)[Q], const int next_row) {
+            // z- and y-forward of the row straight from the lattice, one x column at a time (no
+            // per-plane partials in registers: 81 instead of 27 + 54 / Q multiply-adds per row)
+            double Y00[D], Y01[D], Y10[D];
+#pragma unroll
+            for (int dx = 0; dx < D; dx++)
+            {
+               double u = 0.0, v = 0.0, wv = 0.0;
+#pragma unroll
+               for (int dy = 0; dy < D; dy++)
+               {
+                  int lb = lane_base(dx % P, dy % P);
+                  asm volatile("" : "+v"(lb));  // re-read the lattice every row (no 27 live values)
+                  double zb = 0.0, zg = 0.0;
+#pragma unroll
+                  for (int dz = 0; dz < D; dz++)
+                  {
+                     const int cx = dx % P, cy = dy % P, cz = dz % P;
+                     const int nx = tpe_lattice_class_n(cx), ny = tpe_lattice_class_n(cy);
+                     const int sl = tpe_lattice_class_off(D, cx, cy, cz) + ((dz / P) * ny + dy / P) * nx + dx / P;
+                     const double c = sXL[w][lb + sl];
+                     zb += bz[dz] * c;
+                     zg += gz[dz] * c;
+                  }
+                  const double by = b.B[qy + MQ * dy], gy = b.G[qy + MQ * dy];
+                  u += by * zb;
+                  v += gy * zb;
+                  wv += by * zg;
+               }
+               Y00[dx] = u; Y01[dx] = v; Y10[dx] = wv;
+            }
+            double T0[D], T1[D], T2[D];
+#pragma unroll
+            for (int dx = 0; dx < D; dx++) { T0[dx] = 0.0; T1[dx] = 0.0; T2[dx] = 0.0; }
+            double ja[3], rG[3], rH[3];  // the row's J[.][0] and J[.][2] pieces
+            {
+               double et = qp.x[qy];
+               asm volatile("" : "+s"(et));  // (as zt: the rows' pieces stay in the loop)
+#pragma unroll
+               for (int i = 0; i < 3; i++)
+               {
+                  ja[i] = pA[i] + pB[i] * et;
+                  rG[i] = cf(2, i) + cf(5, i) * et;
+                  rH[i] = cf(4, i) + cf(6, i) * et;
+               }
+            }
+#pragma unroll
+            for (int qx = 0; qx < Q; qx++)
+            {
+               double u = 0.0, ux = 0.0, uy = 0.0, uz = 0.0;
+#pragma unroll
+               for (int dx = 0; dx < D; dx++)
+               {
+                  const double bq = b.B[qx + MQ * dx], gq = b.G[qx + MQ * dx];
+                  u += bq * Y00[dx];
+                  ux += gq * Y00[dx];
+                  uy += bq * Y01[dx];
+                  uz += bq * Y10[dx];
+               }
+               const v2d sa = cur[qx];
+               // the next row's pair of this point goes into the slot just read: one row of pairs in
+               // flight in Q registers pairs (ping-pong buffers cost 16 VGPRs more)
+               cur[qx] = ld2(qa + (size_t)(next_row * Q + qx) * 128);
+               const double xi = qp.x[qx];
+               // J = [ja | jb | jc] (rows: coordinates), adj(J) rows A1., A2., A3.
+               const double jb0 = pC[0] + pB[0] * xi, jb1 = pC[1] + pB[1] * xi, jb2 = pC[2] + pB[2] * xi;
+               const double jc0 = rG[0] + rH[0] * xi, jc1 = rG[1] + rH[1] * xi, jc2 = rG[2] + rH[2] * xi;
+               const double A11 = jb1 * jc2 - jc1 * jb2, A12 = jb2 * jc0 - jb0 * jc2, A13 = jb0 * jc1 - jb1 * jc0;
+               const double A21 = ja[2] * jc1 - ja[1] * jc2, A22 = ja[0] * jc2 - jc0 * ja[2],
+                            A23 = ja[1] * jc0 - ja[0] * jc1;
+               const double A31 = ja[1] * jb2 - ja[2] * jb1, A32 = ja[2] * jb0 - ja[0] * jb2,
+                            A33 = ja[0] * jb1 - jb0 * ja[1];
+               // t = (W beta / det J) adj(J)^T grad u, f = adj(J) t, m = (W alpha det J) u
+               const double sux = sa.x * ux, suy = sa.x * uy, suz = sa.x * uz;
+               double t1 = A11 * sux;
+               t1 += A21 * suy;
+               t1 += A31 * suz;
+               double t2 = A12 * sux;
+               t2 += A22 * suy;
+               t2 += A32 * suz;
+               double t3 = A13 * sux;
+               t3 += A23 * suy;
+               t3 += A33 * suz;
+               const double m = sa.y * u;
+               double fx = A11 * t1;
+               fx += A12 * t2;
+               fx += A13 * t3;
+               double fy = A21 * t1;
+               fy += A22 * t2;
+               fy += A23 * t3;
+               double fz = A31 * t1;
+               fz += A32 * t2;
+               fz += A33 * t3;
+#pragma unroll
+               for (int dx = 0; dx < D; dx++)
+               {
+                  const double bq = b.B[qx + MQ * dx], gq = b.G[qx + MQ * dx];
+                  T0[dx] += bq * m;
+                  T0[dx] += gq * fx;
+                  T1[dx] += bq * fy;
+                  T2[dx] += bq * fz;
+               }
+            }
+#pragma unroll
+            for (int dy = 0; dy < D; dy++)
+            {
+               const double by = b.B[qy + MQ * dy], gy = b.G[qy + MQ * dy];
+#pragma unroll
+               for (int dx = 0; dx < D; dx++)
+               {
+                  SB[dy][dx] += by * T0[dx];
+                  SB[dy][dx] += gy * T1[dx];
+                  SG[dy][dx] += by * T2[dx];
+               }
+            }
+         };
+#pragma unroll
+         for (int qy = 0; qy < Q; qy++)
+         {
+            const int row = qz * Q + qy;
+            __builtin_amdgcn_sched_barrier(0);  // rows stay in program order (no interleaved live ranges)
+            row_body(qy, ca, row + 1 < NR ? row + 1 : NR - 1);  // (the last row reloads itself: exact wait counts)
+         }
+         // the plane's z-transpose into the outputs (private [a][lane] slots: same-lane RMW)
+#pragma unroll
+         for (int dz = 0; dz < D; dz++)
+#pragma unroll
+            for (int dy = 0; dy < D; dy++)
+#pragma unroll
+               for (int dx = 0; dx < D; dx++)
+               {
+                  double &yo = sY[w][(dz * D + dy) * D + dx][lane];
+                  double v = yo;
+                  v += bz[dz] * SB[dy][dx];
+                  v += gz[dz] * SG[dy][dx];
+                  yo = v;
+               }
+      }
+   }  // wave_on
+   double Yo[ND];
+#pragma unroll
+   for (int a = 0; a < ND; a++) { Yo[a] = wave_on ? sY[w][a][lane] : 0.0; }
+   tpe_assemble_store<D, SPLIT, false, true, true>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0, blk, lane,
+                                                  active, n_owned, y, yg, part, &sY[0][0][0], w, wave_on, rg, regf,
+                                                  pstride, lmap ? lmap + (size_t)blk * NLP : nullptr);
 }
 
 // Latency variant of k_apply_tpe_sf for small block ranges (the boundary elements of the
@@ -941,14 +1225,21 @@ void launch_tpe(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipS
    {
       if constexpr (MASS && DIFF)
       {
-#define ECM2_TL(RM)                                                                                           \
-   hipLaunchKernelGGL((k_apply_tpe_sf<D, Q, SPLIT, RM, true>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end,   \
-                      a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part, a.treg,   \
+#define ECM2_TL(KT)                                                                                           \
+   hipLaunchKernelGGL(KT, grid, block, 0, s, a.ne, a.blk_begin, a.blk_end, a.n_owned, a.gmap, a.qdd, a.qdm, a.x, \
+                      a.xg, a.y, a.yg, b, a.lane_flags, a.part, a.treg, a.part_stride, a.lmap, a.qp)
+         // every block a lattice brick: the two-waves-per-SIMD lattice kernel; else per element
+         // (p = 2; at p = 1 the per-element kernel fits two waves already)
+#define ECM2_TLB(RM)                                                                                          \
+   hipLaunchKernelGGL((k_apply_tpe_tlb<3, 4, SPLIT, RM>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end,          \
+                      a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, rowtab, a.lane_flags, a.part, a.treg, \
                       a.part_stride, a.lmap, a.qp)
-         if (a.treg && a.treg_all) { ECM2_TL(1); }
-         else if (a.treg && a.tlat_all) { ECM2_TL(3); }
-         else if (a.treg) { ECM2_TL(2); }
-         else { ECM2_TL(0); }
+         constexpr bool LAT = D == 3 && Q == 4;
+         if (LAT && a.treg && a.treg_all) { ECM2_TLB(1); }
+         else if (LAT && a.treg && a.tlat_all) { ECM2_TLB(3); }
+#undef ECM2_TLB
+         else if (a.treg) { ECM2_TL((k_apply_tpe_sf<D, Q, SPLIT, 2, true>)); }
+         else { ECM2_TL((k_apply_tpe_sf<D, Q, SPLIT, 0, true>)); }
 #undef ECM2_TL
       }
       else { ECM2_VERIFY(false, ERR_INTERNAL, "TRILINEAR qdata needs both integrators"); }

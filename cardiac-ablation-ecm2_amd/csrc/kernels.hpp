@@ -44,9 +44,10 @@ enum QLayoutKind : int { QLAYOUT_NATIVE = 0, QLAYOUT_BLOCKED = 1, QLAYOUT_AFFINE
 // sum over the corners, mesh.cpp:15220-15273), and the kernel evaluates J, adj(J), det J at
 // each quadrature point (PADiffusionSetup3D's algebra, bilininteg_diffusion_kernels.cpp:
 // 349-362): qd_diff = [blk][11 pairs][lane][2] holding c1..c7 of x, y, z (index 3 (k - 1) + i,
-// padded to 22), qd_mass = [blk][q][lane][2] = (W_q beta_q, W_q alpha_q).  16 B per point +
-// 176 B per element instead of 56 B per point: the bytes of the AFFINE layout on a general
-// trilinear mesh, for ~55 extra FP64 operations per point.
+// padded to 22), qd_mass = [blk][q][lane][2] = (W_q beta_q / det J_q, W_q alpha_q det J_q) (the
+// setup evaluates det J once, so the apply needs no division).  16 B per point + 176 B per
+// element instead of 56 B per point: the bytes of the AFFINE layout on a general trilinear mesh,
+// for ~33 extra FP64 operations per point (adj(J) and its two products).
 constexpr int kTrilinPairs = 11;
 // 1D Gauss-Legendre points on [0, 1] (kernel argument: scalar loads)
 struct QPts
@@ -199,25 +200,30 @@ __host__ __device__ inline int tpe_surface_index(int D, int X, int Y, int Z)
 // classes a lane's entry a = (dx, dy, dz) falls in -- and lexicographic within a class, so the 64
 // lanes' loads of one entry a touch one contiguous 4 x 4 x 4 sub-block (coalesced) and every
 // point is stored once (729 ints at p = 2 against 27 x 64 per-entry map ints).
-__host__ __device__ inline int tpe_lattice_points(int D)
+__host__ __device__ constexpr int tpe_lattice_points(int D)
 {
-   const int L = 4 * (D - 1) + 1;
-   return L * L * L;
+   return (4 * (D - 1) + 1) * (4 * (D - 1) + 1) * (4 * (D - 1) + 1);
 }
-__host__ __device__ inline int tpe_lattice_slot(int D, int X, int Y, int Z)
+// points of residue class c (mod D - 1) along one axis of the lattice
+__host__ __device__ constexpr int tpe_lattice_class_n(int c) { return c == 0 ? 5 : 4; }
+// first slot of residue class (cx, cy, cz): classes in (cz, cy, cx) lexicographic order
+__host__ __device__ constexpr int tpe_lattice_class_off(int D, int cx, int cy, int cz)
+{
+   const int P = D - 1;
+   int off = 0;
+   for (int k = 0; k < cz; k++) { off += tpe_lattice_class_n(k) * (4 * P + 1) * (4 * P + 1); }  // whole earlier z-classes
+   const int nz = tpe_lattice_class_n(cz);
+   for (int j = 0; j < cy; j++) { off += nz * tpe_lattice_class_n(j) * (4 * P + 1); }
+   const int ny = tpe_lattice_class_n(cy);
+   for (int i = 0; i < cx; i++) { off += nz * ny * tpe_lattice_class_n(i); }
+   return off;
+}
+__host__ __device__ constexpr int tpe_lattice_slot(int D, int X, int Y, int Z)
 {
    const int P = D - 1;
    const int cx = X % P, cy = Y % P, cz = Z % P;
-   auto n = [](int c) { return c == 0 ? 5 : 4; };  // points of residue c along one axis
-   // classes in (cz, cy, cx) lexicographic order; offset = points in earlier classes
-   int off = 0;
-   for (int k = 0; k < cz; k++) { off += n(k) * (4 * P + 1) * (4 * P + 1); }  // whole earlier z-classes
-   const int nz = n(cz);
-   for (int j = 0; j < cy; j++) { off += nz * n(j) * (4 * P + 1); }
-   const int ny = n(cy);
-   for (int i = 0; i < cx; i++) { off += nz * ny * n(i); }
-   const int nx = n(cx);
-   return off + ((Z / P) * ny + (Y / P)) * nx + (X / P);
+   const int ny = tpe_lattice_class_n(cy), nx = tpe_lattice_class_n(cx);
+   return tpe_lattice_class_off(D, cx, cy, cz) + ((Z / P) * ny + (Y / P)) * nx + (X / P);
 }
 
 namespace kern
@@ -243,8 +249,8 @@ void setup_affine(const QLayout &L, int Q, const double *enodes, const double *J
 // (enodes: lexicographic corners, or cfit: the fitted map coefficients [ne][21] of
 // jacobians_trilinear_fit)
 void setup_trilinear(const QLayout &L, int Q, const double *enodes, const double *cfit, const double *W,
-                     const CoeffDesc *cm, const CoeffDesc *cd, const double *cm_q, const double *cd_q, double *qd_geo,
-                     double *qd_pair, hipStream_t s);
+                     const QPts &qp, const CoeffDesc *cm, const CoeffDesc *cd, const double *cm_q, const double *cd_q,
+                     double *qd_geo, double *qd_pair, hipStream_t s);
 // Trilinear-map coefficients of every element from MFEM-layout Jacobians (cfit [ne][21]); false
 // when some element's Jacobians are not those of a trilinear map (1e-13; synchronises s).
 bool jacobians_trilinear_fit(int ne, int Q, const QPts &qp, const double *J, double *cfit, hipStream_t s);

@@ -145,11 +145,6 @@ void PAForm::set_attributes(const int *attr_host)
 void PAForm::add_integrator(int kind, const CoeffDesc &c, const int *marker, int n_marker)
 {
    ECM2_VERIFY(!marker || n_marker >= 0, ERR_ARG, "negative marker size");
-   if (kind == INTEG_MASS || kind == INTEG_DIFFUSION)
-   {
-      marked_[kind] = marker != nullptr;
-      marker_[kind].assign(marker, marker ? marker + n_marker : marker);
-   }
    ECM2_VERIFY(kind == INTEG_MASS || kind == INTEG_DIFFUSION, ERR_ARG, "unknown integrator " << kind);
    ECM2_VERIFY(c.kind == COEFF_CONSTANT || c.kind == COEFF_QUAD || c.gridfunc(),
                ERR_ARG, "unknown coefficient kind " << c.kind);
@@ -167,6 +162,11 @@ void PAForm::add_integrator(int kind, const CoeffDesc &c, const int *marker, int
       have_diff_ = true;
       cdiff_ = c;
    }
+   // (the marker state changes only once the integrator is accepted: a rejected duplicate leaves
+   // the installed one untouched)
+   marked_[kind] = marker != nullptr;
+   marker_[kind].assign(marker, marker ? marker + n_marker : marker);
+   order_added_.push_back(kind);
    assembled_ = false;
 }
 
@@ -364,10 +364,10 @@ void PAForm::build_shared_plan(const std::vector<int> &hcount, const std::vector
          const int c = cnt(dofs[i]);
          int d1, t1, e1, et1;
          int n = extend(i, false, d1, t1);
-         const int ne_ = c ? extend(i, true, e1, et1) : 0;
-         if (ne_ > n && (n < 4 || ne_ >= 2 * n))  // a short affine run costs more descriptor bytes per entry
+         const int n_ex = c ? extend(i, true, e1, et1) : 0;  // explicit-dof run length
+         if (n_ex > n && (n < 4 || n_ex >= 2 * n))  // a short affine run costs more descriptor bytes per entry
          {
-            n = ne_;
+            n = n_ex;
             d1 = kExplicitDofs;
             t1 = et1;
          }
@@ -1102,6 +1102,29 @@ void PAForm::assemble(hipStream_t s)
       part_.resize(std::max<size_t>(1, (size_t)part_line_off_ + (n_left_ ? (size_t)ne_ * ND_ : 0)));
    }
    else { part_.resize((size_t)layout_.nblk() * part_stride_); }
+   setup_qdata(s, nullptr);
+   assembled_ = true;
+   gen_++;
+}
+
+std::vector<double> PAForm::marker_weights(int k) const
+{
+   std::vector<double> w(ne_, 1.0);
+   if (!marked_[k]) { return w; }
+   ECM2_VERIFY((int)attr_.size() == ne_, ERR_STATE, "a marked integrator needs the element attributes "
+                                                    "(ecm2_pa_form_set_attributes)");
+   for (int e = 0; e < ne_; e++)
+   {
+      const int a = attr_[e];
+      ECM2_VERIFY(a <= (int)marker_[k].size(), ERR_ARG, "element " << e << " has attribute " << a
+                                                         << " beyond the marker's " << marker_[k].size() << " entries");
+      w[e] = (a > 0 && marker_[k][a - 1] != 0) ? 1.0 : 0.0;
+   }
+   return w;
+}
+
+void PAForm::setup_qdata(hipStream_t s, const std::pair<int, std::vector<double>> *wover)
+{
    qd_diff_.resize(have_diff_ ? layout_.diff_size() : 0);
    qd_mass_.resize(have_mass_ ? layout_.mass_size() : 0);
    // the setup kernels write every entry except the padding lanes of a partial last block
@@ -1123,22 +1146,17 @@ void PAForm::assemble(hipStream_t s)
 
    // Attribute markers: per marked integrator, element weights 1 (marker[attr - 1] != 0) or 0,
    // applied to its coefficient at setup (the reference masks the integrator's E-vector output,
-   // AddWithMarkers_, bilinearform_ext.cpp:753-774: the same operator)
+   // AddWithMarkers_, bilinearform_ext.cpp:753-774: the same operator).  wover: other weights
+   // for one integrator (the diagonal's, see assemble_diagonal)
    for (int k = 0; k < 2; k++)
    {
       CoeffDesc &c = k == INTEG_MASS ? cmass_ : cdiff_;
       c.emask = nullptr;
-      if (!marked_[k] || !(k == INTEG_MASS ? have_mass_ : have_diff_)) { continue; }
-      ECM2_VERIFY((int)attr_.size() == ne_, ERR_STATE, "a marked integrator needs the element attributes "
-                                                       "(ecm2_pa_form_set_attributes)");
-      std::vector<double> w(std::max(1, ne_), 0.0);
-      for (int e = 0; e < ne_; e++)
-      {
-         const int a = attr_[e];
-         ECM2_VERIFY(a <= (int)marker_[k].size(), ERR_ARG, "element " << e << " has attribute " << a
-                                                            << " beyond the marker's " << marker_[k].size() << " entries");
-         w[e] = (a > 0 && marker_[k][a - 1] != 0) ? 1.0 : 0.0;
-      }
+      if (!(k == INTEG_MASS ? have_mass_ : have_diff_)) { continue; }
+      const bool over = wover && wover->first == k;
+      if (!marked_[k] && !over) { continue; }
+      std::vector<double> w = over ? wover->second : marker_weights(k);
+      w.resize(std::max(1, ne_));
       emask_[k].upload(w, s);
       ECM2_HIP(hipStreamSynchronize(s));  // w is a host temporary
       c.emask = emask_[k].data();
@@ -1166,8 +1184,10 @@ void PAForm::assemble(hipStream_t s)
    }
    else if (layout_.kind == QLAYOUT_TRILINEAR)
    {
+      QPts qp = {};
+      for (int q = 0; q < Q_ && q < MAX_Q1D; q++) { qp.x[q] = maps_.qpts[q]; }
       kern::setup_trilinear(layout_, Q_, jac_ ? nullptr : enodes_.data(), jac_ ? cfit_.data() : nullptr, W_.data(),
-                            cm, cd, cm_q, cd_q, qd_diff_.data(), qd_mass_.data(), s);
+                            qp, cm, cd, cm_q, cd_q, qd_diff_.data(), qd_mass_.data(), s);
    }
    else if (jac_)
    {
@@ -1179,8 +1199,6 @@ void PAForm::assemble(hipStream_t s)
       kern::setup_from_nodes(layout_, Q_, enodes_.data(), W_.data(), basis1_, cm, cd, cm_q, cd_q,
                              qd_diff_.data(), qd_mass_.data(), s);
    }
-   assembled_ = true;
-   gen_++;
 }
 
 void PAForm::record_start(hipStream_t s)
@@ -1402,6 +1420,41 @@ void PAForm::assemble_diagonal(double *diag, hipStream_t s)
 {
    ECM2_VERIFY(assembled_, ERR_STATE, "AssembleDiagonal before Assemble");
    if (ndofs_ == 0) { return; }
+   // The reference's AssembleDiagonal (bilinearform_ext.cpp:370-411) adds every integrator's
+   // AssembleDiagonalPA into ONE localY and then zeroes a marked integrator's excluded elements of
+   // that localY, so on those elements the contributions of the integrators added before it vanish
+   // too (Mult masks each integrator's output separately, AddMultWithMarkers :753-774).  This
+   // library reproduces it: when the second integrator added is marked and excludes elements the
+   // first acts on, the diagonal comes from qdata set up with the first integrator's element
+   // weights times the second's (temporaries; the Mult's qdata is restored).
+   if (order_added_.size() == 2 && marked_[order_added_[1]])
+   {
+      const int F = order_added_[0], S = order_added_[1];
+      std::vector<double> wf = marker_weights(F);
+      const std::vector<double> ws = marker_weights(S);
+      bool differ = false;
+      for (int e = 0; e < ne_; e++)
+      {
+         differ = differ || (wf[e] != 0.0 && ws[e] == 0.0);
+         wf[e] *= ws[e];
+      }
+      if (differ)
+      {
+         DeviceArray<double> keep_d(std::move(qd_diff_)), keep_m(std::move(qd_mass_));
+         const std::pair<int, std::vector<double>> over(F, wf);
+         setup_qdata(s, &over);
+         diagonal_from_qdata(diag, s);
+         ECM2_HIP(hipStreamSynchronize(s));  // the temporaries are freed below
+         qd_diff_ = std::move(keep_d);
+         qd_mass_ = std::move(keep_m);
+         return;
+      }
+   }
+   diagonal_from_qdata(diag, s);
+}
+
+void PAForm::diagonal_from_qdata(double *diag, hipStream_t s)
+{
    if (resolved_mode_ == KERNEL_TPE && (have_mass_ || have_diff_))
    {
       // thread-per-element diagonal assembled like the Mult (deterministic with partials)

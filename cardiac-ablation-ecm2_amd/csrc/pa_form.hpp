@@ -18,6 +18,7 @@
 #include "kernels.hpp"
 
 #include <memory>
+#include <utility>
 #include <vector>
 
 namespace ecm2
@@ -172,6 +173,12 @@ private:
                           const std::vector<int> &hslot, hipStream_t s);
    ApplyArgs apply_args(const double *x, const double *xg, double *y, double *yg, int b0,
                         int b1) const;
+   // qdata of the integrators present (resized, padding cleared, coefficients projected, setup
+   // kernel); wover = (kind, element weights) replaces that integrator's marker weights
+   void setup_qdata(hipStream_t s, const std::pair<int, std::vector<double>> *wover);
+   // element weights [ne] of integrator kind k: 1 / 0 per its attribute marker, all 1 unmarked
+   std::vector<double> marker_weights(int k) const;
+   void diagonal_from_qdata(double *diag, hipStream_t s);
    // TRILINEAR forms: their per-point qdata in the BLOCKED layout (temporaries of the caller)
    void expand_trilinear(DeviceArray<double> &fd, DeviceArray<double> &fm, hipStream_t s) const;
 
@@ -203,6 +210,7 @@ private:
    std::vector<int> attr_;               // element attributes (set_attributes)
    std::vector<int> marker_[2];          // per integrator kind: attribute marker (empty: none)
    bool marked_[2] = {false, false};
+   std::vector<int> order_added_;        // integrator kinds in AddDomainIntegrator order (the diagonal's markers)
    DeviceArray<double> emask_[2];        // per integrator kind: element weights [ne] (marked only)
 
    std::vector<int> gmap_host_;

@@ -522,6 +522,17 @@ void par_group_mult_member(std::vector<ParPAForm *> &forms, const std::vector<co
       ECM2_VERIFY(m && m->count == t.count, ERR_INTERNAL, "exchange schedules of ranks " << r << " and " << t.peer
                                                                                        << " do not match");
    }
+   // the peers' packed sends (and, RAP, their y ghost blocks) are copied as their last group Mult
+   // left them: it must have run on these x arrays and on the current assembly
+   for (const Xfer &t : f.schedule(false))
+   {
+      if (t.send) { continue; }
+      ParPAForm &o = *forms[t.peer];
+      const bool needs = !f.part().overlap || o.pack_needed();
+      ECM2_VERIFY(!needs || o.group_mult_current(x[t.peer]), ERR_STATE,
+                  "member " << r << ": peer " << t.peer << "'s last group Mult ran on another x or assembly "
+                            "(run a group Mult on the same x first)");
+   }
    if (f.serial())
    {
       // the rank's own pack (its sends); the peers' packed sends are as their last group Mult left them
@@ -574,6 +585,7 @@ void par_group_mult(std::vector<ParPAForm *> &forms, const std::vector<const dou
    ECM2_VERIFY(!rccl_self || forms.empty() || forms[0]->serial(), ERR_UNSUPPORTED,
                "the RCCL-self group transport runs the serial schedule");
    void *comm = rccl_self ? self_comm() : nullptr;
+   for (int r = 0; r < n; r++) { forms[r]->note_group_mult(x[r]); }
    if (!forms.empty() && forms[0]->serial())
    {
       // the serial schedule, stage-major on s: packs, the P copies, the applies, [RAP: P^T

@@ -80,6 +80,13 @@ public:
    // transfer's data (x_true: the true vector of the Mult being enqueued).
    const std::vector<Xfer> &schedule(bool transpose) const { return transpose ? sched_t_ : sched_p_; }
    double *xfer_ptr(const Xfer &t, const double *x_true);
+   // The x of the last loopback-group Mult and the local form's assembly it ran on: a member's
+   // RAP rows copy the state it left (par_group_mult_member checks it is current).
+   void note_group_mult(const double *x_true) { group_x_ = x_true; group_gen_ = local_->generation(); }
+   bool group_mult_current(const double *x_true) const
+   {
+      return group_x_ == x_true && group_gen_ == local_->generation();
+   }
 
 private:
    void rccl_exchange(bool transpose, const double *x_true, hipStream_t st);  // grouped send/recv on st
@@ -106,6 +113,8 @@ private:
    long graph_gen_ = -1;
    bool graph_failed_ = false;
    bool p2p_warm_ = false;  // one direct Mult ran (RCCL peer connections exist) before any capture
+   const double *group_x_ = nullptr;  // note_group_mult
+   long group_gen_ = -1;
 };
 
 // RCCL point-to-point self-test (one-rank communicator, direct or graph-captured): max error.
@@ -127,7 +136,8 @@ void par_group_diagonal(std::vector<ParPAForm *> &forms, const std::vector<doubl
 // their send buffers as the last group Mult left them).  RAP (serial schedule): + the ghost sums
 // and the P^T receive, copied from the peers' y ghost blocks as the last group Mult left them.
 // The other members' y are not touched.  This is what a rank's Mult costs on its own GPU, short
-// of the xGMI transfer time.  Run one group Mult on the same x first.
+// of the xGMI transfer time.  Run one group Mult on the same x arrays first: RAP and packed sends
+// fail with ERR_STATE when the peers' last group Mult ran on other x arrays or another assembly.
 void par_group_mult_member(std::vector<ParPAForm *> &forms, const std::vector<const double *> &x,
                            const std::vector<double *> &y, int r, hipStream_t s);
 

@@ -320,6 +320,26 @@ class OracleOperator:
         lib().orc_pa_diagonal_e(self.ne, self.p + 1, Q, _p(self._Bf), _p(self._Gf), _p(self.M), _p(self.D), _p(de))
         return np.bincount(self.gm.ravel(), weights=de.ravel(), minlength=self.ndofs)
 
+    def diagonal_markers(self, attr, integrators):
+        """PABilinearFormExtension::AssembleDiagonal with markers (bilinearform_ext.cpp:370-411):
+        localY = 0; for each (kind, marker) in AddDomainIntegrator order, the integrator's
+        AssembleDiagonalPA adds into localY, then a marked integrator zeroes the elements it
+        excludes in that SHARED localY (earlier integrators' contributions there included);
+        finally AbsMultTranspose.  integrators: [("mass" | "diffusion", marker or None), ...]."""
+        attr = np.asarray(attr)
+        nd = self.gm.shape[1]
+        de = np.zeros((self.ne, nd))
+        Q = self.q1d
+        for kind, marker in integrators:
+            Dm = self.M if kind == "mass" else None
+            Dd = self.D if kind == "diffusion" else None
+            lib().orc_pa_diagonal_e(self.ne, self.p + 1, Q, _p(self._Bf), _p(self._Gf), _p(Dm), _p(Dd), _p(de))
+            if marker is not None:
+                mk = np.asarray(marker)
+                drop = np.array([not (a > 0 and mk[a - 1] != 0) for a in attr])
+                de[drop] = 0.0
+        return np.bincount(self.gm.ravel(), weights=de.ravel(), minlength=self.ndofs)
+
     def pcg(self, b, ess, rel_tol=1e-12, abs_tol=0.0, max_iter=1000, jacobi=True):
         ess = _i32(ess)
         dinv = None

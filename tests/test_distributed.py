@@ -358,6 +358,13 @@ def test_gpu_group_member_rows(nranks, order, schedule, decomp):
     ref = O.OracleOperator(m.element_nodes(), fes.gather_map(), fes.ndofs, order, alpha=cg, beta=cg).mult(xg)
     group = E.ParGroup(forms)
     if decomp == "rap":
+        # a member's RAP rows copy the peers' state of a group Mult on the same x: refused without one
+        with pytest.raises(E.ECM2Error):
+            group.MultMember(0, xs, ys)
+        x2 = [v.clone() for v in xs]
+        group.Mult(x2, ys)
+        with pytest.raises(E.ECM2Error):
+            group.MultMember(0, xs, ys)
         group.Mult(xs, ys)  # the peers' ghost contributions a member's P^T receive copies
         torch.cuda.synchronize()
         for yt in ys:
@@ -643,3 +650,119 @@ def test_gpu_group_member_rows_boxes(decomp):
         group.MultMember(r, xs, ys)
         torch.cuda.synchronize()
         assert relerr(ys[r].cpu().numpy(), ref[parts[r].owned_global]) <= RTOL
+
+
+def _worker_pcg(rank, nranks, port, kind, result_path, decomp, max_iter):
+    """One rank of the product's distributed constrained Jacobi-PCG (pcg_solve, solvers.cpp, with
+    ParPAForm as the operator): the Mult is the schedule rows' P exchange + the oracle local
+    operator [+ RAP: the P^T rows], the Jacobi diagonal the local diagonal [+ RAP: its P^T sums],
+    and every dot is a local partial all-reduced between the processes (ParPAForm::sum_scalars,
+    the reference's two MPI_Allreduce per CG iteration: solvers.cpp:931,963, vector.hpp:773-779),
+    in pcg_solve's exact step order (the fused x/r/z/r.z update, DIAG_ONE ConstrainedOperator)."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=nranks)
+    try:
+        m = _mesh(kind)
+        order = 2
+        fes = E.H1Space(m, order)
+        er = _elem_rank(m, kind, nranks)
+        part = E.Partition(fes, er, rank, nranks, decomposition=decomp)
+        q1d = O.default_q1d(order)
+        en = m.element_nodes()[part.elems]
+        c = coeff_function(O.quad_points(en, q1d))
+        nl = part.n_owned + part.n_ghost
+        op = O.OracleOperator(en, part.gather_map, nl, order, alpha=c, beta=c)
+        tag = [41822]
+
+        def ghost_sums(yl):
+            """RAP: the ghost entries' contributions added into their owners (the P^T rows)."""
+            y_true = yl[: part.n_owned].copy()
+            if decomp == "rap":
+                bufs = _schedule_buffers(part, y_true)
+                bufs[E.Partition.XBUF_YGHOST][:] = yl[part.n_owned:]
+                tag[0] += 1
+                _run_schedule(part.exchange_schedule(True), bufs, tag=tag[0])
+                np.add.at(y_true, part.send_idx, bufs[E.Partition.XBUF_RECVBUF])
+            return y_true
+
+        def mult(x_true):
+            bufs = _schedule_buffers(part, x_true.copy())
+            tag[0] += 1
+            _run_schedule(part.exchange_schedule(False), bufs, tag=tag[0])
+            return ghost_sums(op.mult(np.concatenate([x_true, bufs[E.Partition.XBUF_XGHOST]])))
+
+        def allreduce(v):
+            t = torch.tensor([v], dtype=torch.float64)
+            dist.all_reduce(t)
+            return float(t.item())
+
+        own = np.zeros(fes.ndofs, bool)
+        own[part.owned_global] = True
+        gl = np.full(fes.ndofs, -1, np.int64)
+        gl[part.owned_global] = np.arange(part.n_owned)
+        ess_g = fes.boundary_dofs()
+        ess = gl[ess_g[own[ess_g]]]
+
+        def cmult(v):  # ConstrainedOperator DIAG_ONE: zero ess in place, Mult, restore, out[ess] = in[ess]
+            saved = v[ess].copy()
+            v[ess] = 0.0
+            out = mult(v)
+            v[ess] = saved
+            out[ess] = saved
+            return out
+
+        dg = ghost_sums(op.diagonal())
+        dg[ess] = 1.0
+        dinv = 1.0 / dg
+        b = np.random.default_rng(2).uniform(-1, 1, fes.ndofs)[part.owned_global]
+        r = b.copy()
+        x = np.zeros(part.n_owned)
+        z = dinv * r
+        d = z.copy()
+        nom = allreduce(d @ r)
+        z = cmult(d)
+        den = allreduce(z @ d)
+        it = 0
+        for i in range(1, max_iter + 1):
+            alpha = nom / den
+            x += alpha * d
+            r -= alpha * z
+            z = dinv * r
+            betanom = allreduce(r @ z)
+            it = i
+            if i == max_iter:
+                break
+            d = z + (betanom / nom) * d
+            z = cmult(d)
+            den = allreduce(d @ z)
+            nom = betanom
+        gathered = [None] * nranks
+        dist.all_gather_object(gathered, (part.owned_global.tolist(), x.tolist(), it))
+        if rank == 0:
+            xs = np.zeros(fes.ndofs)
+            for ids, vals, _ in gathered:
+                xs[np.array(ids, dtype=np.int64)] = vals
+            cg = coeff_function(O.quad_points(m.element_nodes(), q1d))
+            ref = O.OracleOperator(m.element_nodes(), fes.gather_map(), fes.ndofs, order, alpha=cg, beta=cg)
+            bg = np.random.default_rng(2).uniform(-1, 1, fes.ndofs)
+            xr, itr, _ = ref.pcg(bg, ess_g, rel_tol=0.0, max_iter=max_iter, jacobi=True)
+            np.save(result_path, np.array([relerr(xs, xr), it, itr]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind,nranks", [("cart", 2), ("cart", 3), ("fichera", 2), ("fichera", 3)])
+@pytest.mark.parametrize("decomp", ["rap", "overlap"])
+def test_gloo_pcg_reductions_match_serial(tmp_path, kind, nranks, decomp):
+    """The distributed constrained Jacobi-PCG between processes: the product's step order with
+    its two dots per iteration all-reduced over gloo (the RCCL path's ncclAllReduce) and the
+    schedule rows' exchange; 8 fixed iterations give the serial oracle CGSolver's iterate."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "pcg.npy")
+    mp.spawn(_worker_pcg, args=(nranks, _free_port(), kind, out, decomp, 8), nprocs=nranks, join=True)
+    err, it, itr = np.load(out)
+    assert it == itr == 8
+    assert err < 1e-10

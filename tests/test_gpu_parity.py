@@ -597,23 +597,33 @@ def test_attribute_markers(mesh_name, order, compress):
     c = coeff_function(O.quad_points(en, q1d))
     op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=c, beta=c)
     x = np.random.default_rng(3).uniform(-1, 1, fes.ndofs)
-    for mm, dm in (([0, 1], None), (None, [1, 0])):
+    # (mass marker, diffusion marker, diffusion added first)
+    for mm, dm, dfirst in (([0, 1], None, False), (None, [1, 0], False), ([0, 1], None, True)):
         form = E.BilinearForm(fes, compress_geometry=compress)
-        form.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(c.reshape(fes.ne, -1)))), mm)
-        form.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(dev(c.reshape(fes.ne, -1)))), dm)
+        mi = E.MassIntegrator(E.QuadratureCoefficient(dev(c.reshape(fes.ne, -1))))
+        di = E.DiffusionIntegrator(E.QuadratureCoefficient(dev(c.reshape(fes.ne, -1))))
+        seq = [(di, dm, "diffusion"), (mi, mm, "mass")] if dfirst else [(mi, mm, "mass"), (di, dm, "diffusion")]
+        for integ, mk, _ in seq:
+            form.AddDomainIntegrator(integ, mk)
         form.Assemble()
         y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
         form.Mult(dev(x), y)
         ref = op.mult_markers(x, attr, mass_marker=mm, diff_marker=dm)
         assert relerr(host(y), ref) <= RTOL
-        # the masked operator's diagonal: e_i^T A e_i from the oracle's masked Mult on a few dofs
+        # the reference's diagonal (bilinearform_ext.cpp:370-411): a marked integrator zeroes its excluded
+        # elements of the shared localY, earlier integrators' contributions included
         d = torch.empty_like(y)
         form.AssembleDiagonal(d)
         dh = host(d)
-        for i in np.random.default_rng(4).choice(fes.ndofs, 5, replace=False):
-            e = np.zeros(fes.ndofs)
-            e[i] = 1.0
-            assert abs(dh[i] - op.mult_markers(e, attr, mass_marker=mm, diff_marker=dm)[i]) <= 1e-12 * np.abs(dh).max()
+        assert relerr(dh, op.diagonal_markers(attr, [(k, mk) for _, mk, k in seq])) < 1e-13
+        if seq[1][1] is None:  # no later marker: the masked operator's own diagonal, e_i^T A e_i
+            for i in np.random.default_rng(4).choice(fes.ndofs, 5, replace=False):
+                e = np.zeros(fes.ndofs)
+                e[i] = 1.0
+                assert abs(dh[i] - op.mult_markers(e, attr, mass_marker=mm, diff_marker=dm)[i]) <= 1e-12 * np.abs(dh).max()
+        # Mult after the diagonal: the form's own qdata is back
+        form.Mult(dev(x), y)
+        assert relerr(host(y), ref) <= RTOL
 
 
 def test_attribute_marker_errors():

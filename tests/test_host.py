@@ -43,6 +43,22 @@ def test_cartesian_mesh_matches_make3d_layout():
     assert np.array_equal(en_prod, en_orc)
 
 
+@pytest.mark.parametrize("q1d", [3, 4, 6])
+def test_mesh_jacobians_match_geometric_factors(q1d):
+    """Mesh.jacobians (the GeometricFactors::JACOBIANS array a drop-in binding passes, MFEM layout
+    NQ x 3 x 3 x NE) equals the oracle's restatement of mesh.cpp:15220-15273 on a refined
+    fichera mesh with moved interior vertices (trilinear hexes)."""
+    m = E.Mesh(f"{GOLDEN}/fichera.mesh")
+    m.UniformRefinement()
+    V = m.vertices()
+    V += 0.05 * np.sin(7.0 * V[:, [1, 2, 0]])
+    m.set_vertices(V)
+    J = m.jacobians(q1d, device="cpu").numpy()
+    _, Jr, _ = O.geom(m.element_nodes(), q1d)
+    assert J.shape == Jr.shape
+    assert relerr(J, Jr) < 1e-14
+
+
 def test_mesh_readers_against_reference_fixtures():
     """data/fichera.mesh and data/inline-hex.mesh (reference fixtures) parse to the same
     vertices/elements as an independent parser."""

@@ -213,3 +213,30 @@ def test_marker_oracle_matches_fa_on_marked_elements(order):
     # no marker: the plain Mult; marker excluding everything: diffusion alone
     assert relerr(op.mult_markers(x, attr), op.mult(x)) < 1e-14
     assert relerr(op.mult_markers(x, attr, mass_marker=[0, 0]), fa_diff) < 1e-12
+
+
+@pytest.mark.parametrize("order", [1, 2])
+def test_marker_diagonal_oracle_follows_shared_localY(order):
+    """The oracle's marked AssembleDiagonal (bilinearform_ext.cpp:370-411): every integrator adds
+    into one localY and a marked integrator zeroes its excluded elements there.  Pinned by full
+    assembly: (Mass unmarked, then Diffusion with {1, 0}) leaves the attribute-1 elements only --
+    the FA diagonal of both integrators over them; with the marked integrator added first, the
+    later unmarked one survives everywhere (the masked operator's own diagonal, as the Mult's)."""
+    V, Ev = read_mfem_mesh(f"{GOLDEN}/fichera.mesh")
+    en = element_nodes_from(V, Ev)
+    fes = E.H1Space(E.Mesh(f"{GOLDEN}/fichera.mesh"), order)
+    gm = fes.gather_map()
+    attr = 1 + np.arange(fes.ne) % 2
+    q1d = O.default_q1d(order)
+    c = coeff_function(O.quad_points(en, q1d))
+    op = O.OracleOperator(en, gm, fes.ndofs, order, alpha=c, beta=c)
+    x = np.zeros(fes.ndofs)
+    s1 = attr == 1
+    _, fa1 = O.OracleOperator(en[s1], gm[s1], fes.ndofs, order, alpha=c[s1], beta=c[s1]).fa_mult(x, with_diag=True)
+    d = op.diagonal_markers(attr, [("mass", None), ("diffusion", [1, 0])])
+    assert relerr(d, fa1) < 1e-12
+    _, fam = O.OracleOperator(en, gm, fes.ndofs, order, alpha=c).fa_mult(x, with_diag=True)
+    _, fad = O.OracleOperator(en[s1], gm[s1], fes.ndofs, order, beta=c[s1]).fa_mult(x, with_diag=True)
+    d2 = op.diagonal_markers(attr, [("diffusion", [1, 0]), ("mass", None)])
+    assert relerr(d2, fam + fad) < 1e-12
+    assert relerr(op.diagonal_markers(attr, [("mass", None), ("diffusion", None)]), op.diagonal()) < 1e-14

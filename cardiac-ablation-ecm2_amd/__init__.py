@@ -32,11 +32,14 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ecm2_pa.h")
 
 MASS, DIFFUSION = 0, 1
 COEFF_CONSTANT, COEFF_QUAD, COEFF_GRIDFUNC_AFFINE, COEFF_GRIDFUNC_PERFUSION = 0, 1, 2, 3
+COEFF_QUAD_VECTOR, COEFF_QUAD_SYMMATRIX, COEFF_QUAD_MATRIX = 4, 5, 6
+COEFF_CONST_VECTOR, COEFF_CONST_SYMMATRIX, COEFF_CONST_MATRIX = 7, 8, 9
 KERNEL_AUTO, KERNEL_TPE, KERNEL_WPE, KERNEL_UNFUSED, KERNEL_LINE = 0, 1, 2, 3, 4
 NUMBERING_ENTITY, NUMBERING_STRUCTURED = 0, 1
 ORDER_NATIVE, ORDER_BRICK, ORDER_MORTON = 0, 1, 2
 SCATTER_PARTIALS, SCATTER_ATOMIC = 0, 1
 QLAYOUT_NATIVE, QLAYOUT_BLOCKED, QLAYOUT_AFFINE, QLAYOUT_AFFINE_E, QLAYOUT_TRILINEAR = 0, 1, 2, 3, 4  # info()['layout']
+QLAYOUT_NATIVE9 = 5  # a general matrix diffusion coefficient's 9-entry qdata
 DECOMP_RAP, DECOMP_OVERLAP = 0, 1  # Partition decomposition
 _SCATTER = {"partials": SCATTER_PARTIALS, "atomic": SCATTER_ATOMIC}
 
@@ -353,6 +356,24 @@ class QuadratureCoefficient:
         self.values = values
 
 
+class VectorCoefficient:
+    """DiffusionIntegrator(VectorCoefficient): the diagonal conductivity diag(v).  values: a
+    3-vector (VectorConstantCoefficient) or torch CUDA float64 [ne][nq][3] at the quadrature points."""
+
+    def __init__(self, values):
+        self.values = values
+
+
+class MatrixCoefficient:
+    """DiffusionIntegrator(MatrixCoefficient): anisotropic conductivity M.  values: a 3x3 matrix
+    (MatrixConstantCoefficient) or torch CUDA float64 [ne][nq][3][3] at the quadrature points
+    (row-major M(i, j)); symmetric=True (SymmetricMatrixCoefficient) keeps the 6 entries
+    (11,12,13,22,23,33), else the general 9-entry qdata (bilininteg_diffusion_kernels.cpp:297-348)."""
+
+    def __init__(self, values, symmetric=False):
+        self.values, self.symmetric = values, bool(symmetric)
+
+
 class AffineGridFunctionCoefficient:
     """scale * (1 + slope * (T(x) - t_ref)) with T an H1 grid function (CUDA L-vector).
 
@@ -387,6 +408,31 @@ def _integrator_args(c, keep):
         params = (ctypes.c_double * 3)(c.scale, c.slope, c.t_ref)
         keep.append(params)
         return COEFF_GRIDFUNC_AFFINE, _dev_ptr(c.T), ctypes.cast(params, ctypes.c_void_p)
+    if isinstance(c, (VectorCoefficient, MatrixCoefficient)):
+        v = c.values
+        vec = isinstance(c, VectorCoefficient)
+        if hasattr(v, "is_cuda"):  # per quadrature point, device
+            if vec:
+                keep.append(v.contiguous())
+                return COEFF_QUAD_VECTOR, _dev_ptr(keep[-1]), None
+            m = v.reshape(v.shape[0], v.shape[1], 3, 3)
+            if c.symmetric:
+                m = m[..., [0, 0, 0, 1, 1, 2], [0, 1, 2, 1, 2, 2]]
+            keep.append(m.contiguous())
+            return (COEFF_QUAD_SYMMATRIX if c.symmetric else COEFF_QUAD_MATRIX), _dev_ptr(keep[-1]), None
+        a = np.asarray(v, np.float64)
+        if vec:
+            arr = (ctypes.c_double * 3)(*a.reshape(3))
+            kind = COEFF_CONST_VECTOR
+        elif c.symmetric:
+            a = a.reshape(3, 3)
+            arr = (ctypes.c_double * 6)(a[0, 0], a[0, 1], a[0, 2], a[1, 1], a[1, 2], a[2, 2])
+            kind = COEFF_CONST_SYMMATRIX
+        else:
+            arr = (ctypes.c_double * 9)(*a.reshape(9))
+            kind = COEFF_CONST_MATRIX
+        keep.append(arr)
+        return kind, ctypes.cast(arr, ctypes.c_void_p), None
     if isinstance(c, PerfusionCoefficient):
         keep.append(c.T)
         params = (ctypes.c_double * 6)(*c.params)
@@ -544,7 +590,7 @@ class BilinearForm:
     def qdata(self, kind) -> np.ndarray:
         info = self.info()
         nq = info["q1d"] ** 3
-        nc = 6 if kind == DIFFUSION else 1
+        nc = (9 if info["layout"] == QLAYOUT_NATIVE9 else 6) if kind == DIFFUSION else 1
         out = np.empty((self.fes.ne, nc, nq), np.float64)
         _check(_lib.ecm2_pa_form_get_qdata(self._h, kind, _np_ptr(out), _stream()))
         return out

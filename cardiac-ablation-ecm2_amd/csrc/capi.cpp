@@ -93,6 +93,12 @@ ecm2::CoeffDesc make_coeff(int coeff_kind, const double *data, const double *par
       c.lvec = data;
       for (int i = 0; i < 6; i++) { c.p[i] = params[i]; }
    }
+   else if (coeff_kind >= ECM2_COEFF_QUAD_VECTOR && coeff_kind <= ECM2_COEFF_QUAD_MATRIX) { c.quad = data; }
+   else if (coeff_kind >= ECM2_COEFF_CONST_VECTOR && coeff_kind <= ECM2_COEFF_CONST_MATRIX)
+   {
+      NEED(data);
+      for (int i = 0; i < c.dim(); i++) { c.cv[i] = data[i]; }
+   }
    return c;
 }
 } // namespace

@@ -17,10 +17,20 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 
 inline unsigned grid_for(long n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
+// Order a wave's LDS writes before its subsequent LDS reads by other lanes of the SAME wave (a
+// wave's LDS instructions complete in order; this is the compiler barrier plus the wait), in place
+// of a workgroup barrier when producer and consumer lanes share a wave.
+__device__ __forceinline__ void wave_lds_sync()
+{
+   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+   __builtin_amdgcn_wave_barrier();
+}
+
 // pos: caller element -> internal position (element permutation of the blocked layout)
 __device__ __forceinline__ size_t qidx_diff(const int *pos, int kind, int nq, int e, int c, int q)
 {
    if (kind == QLAYOUT_NATIVE) { return ((size_t)e * 6 + c) * nq + q; }
+   if (kind == QLAYOUT_NATIVE9) { return ((size_t)e * 9 + c) * nq + q; }
    if (pos) { e = pos[e]; }
    const int blk = e >> 6, lane = e & 63;
    return (((size_t)blk * nq + q) * 3 + (c >> 1)) * 128 + lane * 2 + (c & 1);
@@ -28,7 +38,7 @@ __device__ __forceinline__ size_t qidx_diff(const int *pos, int kind, int nq, in
 
 __device__ __forceinline__ size_t qidx_mass(const int *pos, int kind, int nq, int e, int q)
 {
-   if (kind == QLAYOUT_NATIVE) { return (size_t)e * nq + q; }
+   if (kind == QLAYOUT_NATIVE || kind == QLAYOUT_NATIVE9) { return (size_t)e * nq + q; }
    if (pos) { e = pos[e]; }
    const int blk = e >> 6, lane = e & 63;
    const int nqh = (nq + 1) >> 1;
@@ -46,6 +56,8 @@ __device__ __forceinline__ size_t affine_pair(const int *pos, int nq, int e, int
 __device__ __forceinline__ double qd_diff_at(const double *qdd, const double *qdm, const int *pos, int kind,
                                              int nq, int e, int c, int q)
 {
+   // (NATIVE9: c = 3 i + j of the general D_ij; every other layout: the symmetric c = 0..5)
+   if (kind == QLAYOUT_NATIVE9) { return qdd[((size_t)e * 9 + c) * nq + q]; }
    if (kind == QLAYOUT_AFFINE_E) { return qdm[((size_t)e * nq + q) * 2] * qdd[(size_t)e * 6 + c]; }
    if (kind == QLAYOUT_AFFINE)
    {
@@ -54,8 +66,26 @@ __device__ __forceinline__ double qd_diff_at(const double *qdd, const double *qd
    }
    return qdd[qidx_diff(pos, kind, nq, e, c, q)];
 }
+// The diffusion term k of the PA diagonal's sum over i, j of D_ij (d_i phi)(d_j phi) at (e, q):
+// k = 0..5 -> D_11, D_22, D_33, D_12 + D_21, D_13 + D_31, D_23 + D_32 (PADiffusionDiagonal3D,
+// bilininteg_diffusion_kernels.hpp:410-431: symmetric ? ksym : 3 i + j).
+__device__ __forceinline__ double qd_diag_term(const double *qdd, const double *qdm, const int *pos, int kind,
+                                               int nq, int e, int k, int q)
+{
+   if (kind == QLAYOUT_NATIVE9)
+   {
+      const int a[6] = {0, 4, 8, 1, 2, 5}, b[6] = {-1, -1, -1, 3, 6, 7};
+      const double v = qd_diff_at(qdd, qdm, pos, kind, nq, e, a[k], q);
+      return b[k] < 0 ? v : v + qd_diff_at(qdd, qdm, pos, kind, nq, e, b[k], q);
+   }
+   const int src[6] = {0, 3, 5, 1, 2, 4};  // symmetric (11,12,13,22,23,33)
+   const double v = qd_diff_at(qdd, qdm, pos, kind, nq, e, src[k], q);
+   return k >= 3 ? 2.0 * v : v;
+}
+
 __device__ __forceinline__ double qd_mass_at(const double *qdm, const int *pos, int kind, int nq, int e, int q)
 {
+   if (kind == QLAYOUT_NATIVE9) { return qdm[(size_t)e * nq + q]; }
    if (kind == QLAYOUT_AFFINE_E) { return qdm[((size_t)e * nq + q) * 2 + 1]; }
    if (kind == QLAYOUT_AFFINE) { return qdm[affine_pair(pos, nq, e, q) + 1]; }
    return qdm[qidx_mass(pos, kind, nq, e, q)];

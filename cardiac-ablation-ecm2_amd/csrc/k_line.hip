@@ -614,7 +614,10 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
       for (int dx = 0; dx < D; dx++) { u += xl[dx]; }
       part[t] = u;
    }
-   __syncthreads();
+   // an element's x and y line stages run on the same L2S (32 or 64) lanes of one wave: the
+   // hand-off needs the wave's LDS writes ordered before its reads, not a workgroup barrier
+   static_assert(64 % L2S == 0, "an element's line lanes lie in one wave");
+   wave_lds_sync();
    // ---- lanes (element, qx, dz), l2 = qx + Q dz: contract in y -> sYQ [g][dz][qy][qx]
    if (act2)
    {
@@ -791,7 +794,7 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
          o[Q * DD + dy] = eo_at<D>(C2E, C2O, dy);
       }
    }
-   __syncthreads();
+   wave_lds_sync();  // y transpose -> x transpose: the element's lanes of one wave (as above)
    // this thread's lattice points of the final stage: table rows (and map entries) issued here,
    // so their latency overlaps the x transpose
    using PT = BrickPtTable<D, Q, BZ>;
@@ -895,13 +898,9 @@ k_diag_sf(const int *__restrict__ pos, int kind, int ne, const int *__restrict__
       {
          const int q = qz * QQ + t;
          double O[7];
-         // symmetric entries (11,12,13,22,23,33) -> terms (11, 22, 33, 2*12, 2*13, 2*23), mass
-         const int src[6] = {0, 3, 5, 1, 2, 4};
+         // terms (11, 22, 33, 12 + 21, 13 + 31, 23 + 32) of the symmetric or general qdata, mass
 #pragma unroll
-         for (int k = 0; k < 6; k++)
-         {
-            O[k] = qdd ? qd_diff_at(qdd, qdm, pos, kind, NQ, e, src[k], q) * (k >= 3 ? 2.0 : 1.0) : 0.0;
-         }
+         for (int k = 0; k < 6; k++) { O[k] = qdd ? qd_diag_term(qdd, qdm, pos, kind, NQ, e, k, q) : 0.0; }
          O[6] = qdm ? qd_mass_at(qdm, pos, kind, NQ, e, q) : 0.0;
 #pragma unroll
          for (int k = 0; k < 7; k++)

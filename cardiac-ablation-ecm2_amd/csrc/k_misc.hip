@@ -98,15 +98,21 @@ __global__ void k_apply_wpe(const int *__restrict__ pos, int kind, int ne, int e
       if (MASS) { m = qd_mass_at(qdm, pos, kind, NQ, e, t) * u; }
       if (DIFF)
       {
+         // (11,12,13,22,23,33), or NATIVE9's general D_ij at 3 i + j (SmemPADiffusionApply3D,
+         // bilininteg_diffusion_kernels.hpp:1122-1136: "symmetric ? ... : d(q, 3..8)")
+         const bool g9 = kind == QLAYOUT_NATIVE9;
          const double O11 = qd_diff_at(qdd, qdm, pos, kind, NQ, e, 0, t);
          const double O12 = qd_diff_at(qdd, qdm, pos, kind, NQ, e, 1, t);
          const double O13 = qd_diff_at(qdd, qdm, pos, kind, NQ, e, 2, t);
-         const double O22 = qd_diff_at(qdd, qdm, pos, kind, NQ, e, 3, t);
-         const double O23 = qd_diff_at(qdd, qdm, pos, kind, NQ, e, 4, t);
-         const double O33 = qd_diff_at(qdd, qdm, pos, kind, NQ, e, 5, t);
+         const double O21 = g9 ? qd_diff_at(qdd, qdm, pos, kind, NQ, e, 3, t) : O12;
+         const double O22 = qd_diff_at(qdd, qdm, pos, kind, NQ, e, g9 ? 4 : 3, t);
+         const double O23 = qd_diff_at(qdd, qdm, pos, kind, NQ, e, g9 ? 5 : 4, t);
+         const double O31 = g9 ? qd_diff_at(qdd, qdm, pos, kind, NQ, e, 6, t) : O13;
+         const double O32 = g9 ? qd_diff_at(qdd, qdm, pos, kind, NQ, e, 7, t) : O23;
+         const double O33 = qd_diff_at(qdd, qdm, pos, kind, NQ, e, g9 ? 8 : 5, t);
          fx = (O11 * gx) + (O12 * gy) + (O13 * gz);
-         fy = (O12 * gx) + (O22 * gy) + (O23 * gz);
-         fz = (O13 * gx) + (O23 * gy) + (O33 * gz);
+         fy = (O21 * gx) + (O22 * gy) + (O23 * gz);
+         fz = (O31 * gx) + (O32 * gy) + (O33 * gz);
       }
       s3m[t] = m; s3x[t] = fx; s3y[t] = fy; s3z[t] = fz;
    }
@@ -210,12 +216,12 @@ __global__ void k_diagonal(const int *__restrict__ pos, int D, int Q, int kind, 
             if (qdd)
             {
                const double p0 = gx * by * bz, p1 = bx * gy * bz, p2 = bx * by * gz;
-               s += p0 * p0 * qd_diff_at(qdd, qdm, pos, kind, NQ, e, 0, q) +
-                    p1 * p1 * qd_diff_at(qdd, qdm, pos, kind, NQ, e, 3, q) +
-                    p2 * p2 * qd_diff_at(qdd, qdm, pos, kind, NQ, e, 5, q) +
-                    2.0 * (p0 * p1 * qd_diff_at(qdd, qdm, pos, kind, NQ, e, 1, q) +
-                           p0 * p2 * qd_diff_at(qdd, qdm, pos, kind, NQ, e, 2, q) +
-                           p1 * p2 * qd_diff_at(qdd, qdm, pos, kind, NQ, e, 4, q));
+               s += p0 * p0 * qd_diag_term(qdd, qdm, pos, kind, NQ, e, 0, q) +
+                    p1 * p1 * qd_diag_term(qdd, qdm, pos, kind, NQ, e, 1, q) +
+                    p2 * p2 * qd_diag_term(qdd, qdm, pos, kind, NQ, e, 2, q) +
+                    (p0 * p1 * qd_diag_term(qdd, qdm, pos, kind, NQ, e, 3, q) +
+                     p0 * p2 * qd_diag_term(qdd, qdm, pos, kind, NQ, e, 4, q) +
+                     p1 * p2 * qd_diag_term(qdd, qdm, pos, kind, NQ, e, 5, q));
             }
          }
    if (out_e) { diag[t] += s; }

@@ -105,8 +105,10 @@ struct SetupCoef
 {
    int has;          // integrator present
    int is_const;
+   int dim;          // values per point: 1 scalar, 3 vector, 6 symmetric matrix, 9 general matrix
    double value;
-   const double *quad;
+   double cv[9];     // constant vector / matrix values
+   const double *quad;   // [ne][nq] or [ne][nq][dim]
    const double *emask;  // element weights (1 / 0) of an attribute-marked integrator, or null
 };
 
@@ -118,42 +120,116 @@ __device__ __forceinline__ double coef_at(const SetupCoef &c, size_t eq, int e)
    const double v = c.is_const ? c.value : c.quad[eq];
    return c.emask ? v * c.emask[e] : v;
 }
+// entry i of a vector / matrix coefficient at point eq
+__device__ __forceinline__ double coef_at_i(const SetupCoef &c, size_t eq, int e, int i)
+{
+   const double v = c.is_const ? c.cv[i] : c.quad[eq * c.dim + i];
+   return c.emask ? v * c.emask[e] : v;
+}
 
-// Write D (6 symmetric entries) and mass value at one quadrature point (any layout).
-__device__ __forceinline__ void write_qdata(const int *pos, int kind, int nq, int e, int q, double w,
-                                            const double J[3][3], const SetupCoef &cm,
-                                            const SetupCoef &cd, double *qd_diff,
-                                            double *qd_mass)
+// PADiffusionSetup3D at one point (bilininteg_diffusion_kernels.cpp:270-362): D = W adj(J) M adj(J)^T
+// / det J for the coefficient's coeffDim (scalar / vector: C1..C3 on the diagonal, :338-347; matrix
+// 6 / 9: R = M adj(J)^T then adj(J) R, :297-336).  Returns the entries written to D: 6 symmetric
+// (11,12,13,22,23,33) or, for a general matrix, 9 (D_ij at 3 i + j).
+__device__ __forceinline__ int diff_point(const double J[3][3], double w, const SetupCoef &cd, size_t eq, int e,
+                                          double D[9])
 {
    const double J11 = J[0][0], J21 = J[1][0], J31 = J[2][0];
    const double J12 = J[0][1], J22 = J[1][1], J32 = J[2][1];
    const double J13 = J[0][2], J23 = J[1][2], J33 = J[2][2];
    const double detJ = J11 * (J22 * J33 - J32 * J23) - J21 * (J12 * J33 - J32 * J13) +
                        J31 * (J12 * J23 - J22 * J13);
+   const double w_detJ = w / detJ;
+   const double A11 = (J22 * J33) - (J23 * J32);
+   const double A12 = (J32 * J13) - (J12 * J33);
+   const double A13 = (J12 * J23) - (J22 * J13);
+   const double A21 = (J31 * J23) - (J21 * J33);
+   const double A22 = (J11 * J33) - (J13 * J31);
+   const double A23 = (J21 * J13) - (J11 * J23);
+   const double A31 = (J21 * J32) - (J31 * J22);
+   const double A32 = (J31 * J12) - (J11 * J32);
+   const double A33 = (J11 * J22) - (J12 * J21);
+   if (cd.dim == 6 || cd.dim == 9)
+   {
+      const bool sym = cd.dim == 6;
+      const double M11 = coef_at_i(cd, eq, e, 0), M12 = coef_at_i(cd, eq, e, 1), M13 = coef_at_i(cd, eq, e, 2);
+      const double M21 = sym ? M12 : coef_at_i(cd, eq, e, 3);
+      const double M22 = sym ? coef_at_i(cd, eq, e, 3) : coef_at_i(cd, eq, e, 4);
+      const double M23 = sym ? coef_at_i(cd, eq, e, 4) : coef_at_i(cd, eq, e, 5);
+      const double M31 = sym ? M13 : coef_at_i(cd, eq, e, 6);
+      const double M32 = sym ? M23 : coef_at_i(cd, eq, e, 7);
+      const double M33 = sym ? coef_at_i(cd, eq, e, 5) : coef_at_i(cd, eq, e, 8);
+      const double R11 = M11 * A11 + M12 * A12 + M13 * A13;
+      const double R12 = M11 * A21 + M12 * A22 + M13 * A23;
+      const double R13 = M11 * A31 + M12 * A32 + M13 * A33;
+      const double R21 = M21 * A11 + M22 * A12 + M23 * A13;
+      const double R22 = M21 * A21 + M22 * A22 + M23 * A23;
+      const double R23 = M21 * A31 + M22 * A32 + M23 * A33;
+      const double R31 = M31 * A11 + M32 * A12 + M33 * A13;
+      const double R32 = M31 * A21 + M32 * A22 + M33 * A23;
+      const double R33 = M31 * A31 + M32 * A32 + M33 * A33;
+      const double D11 = w_detJ * (A11 * R11 + A12 * R21 + A13 * R31);
+      const double D12 = w_detJ * (A11 * R12 + A12 * R22 + A13 * R32);
+      const double D13 = w_detJ * (A11 * R13 + A12 * R23 + A13 * R33);
+      const double D22 = w_detJ * (A21 * R12 + A22 * R22 + A23 * R32);
+      const double D23 = w_detJ * (A21 * R13 + A22 * R23 + A23 * R33);
+      const double D33 = w_detJ * (A31 * R13 + A32 * R23 + A33 * R33);
+      if (sym)
+      {
+         D[0] = D11; D[1] = D12; D[2] = D13; D[3] = D22; D[4] = D23; D[5] = D33;
+         return 6;
+      }
+      D[0] = D11; D[1] = D12; D[2] = D13;
+      D[3] = w_detJ * (A21 * R11 + A22 * R21 + A23 * R31);
+      D[4] = D22; D[5] = D23;
+      D[6] = w_detJ * (A31 * R11 + A32 * R21 + A33 * R31);
+      D[7] = w_detJ * (A31 * R12 + A32 * R22 + A33 * R32);
+      D[8] = D33;
+      return 9;
+   }
+   double C1, C2, C3;
+   if (cd.dim == 3)
+   {
+      C1 = coef_at_i(cd, eq, e, 0);
+      C2 = coef_at_i(cd, eq, e, 1);
+      C3 = coef_at_i(cd, eq, e, 2);
+   }
+   else { C1 = C2 = C3 = coef_at(cd, eq, e); }
+   D[0] = w_detJ * (C1 * A11 * A11 + C2 * A12 * A12 + C3 * A13 * A13);
+   D[1] = w_detJ * (C1 * A11 * A21 + C2 * A12 * A22 + C3 * A13 * A23);
+   D[2] = w_detJ * (C1 * A11 * A31 + C2 * A12 * A32 + C3 * A13 * A33);
+   D[3] = w_detJ * (C1 * A21 * A21 + C2 * A22 * A22 + C3 * A23 * A23);
+   D[4] = w_detJ * (C1 * A21 * A31 + C2 * A22 * A32 + C3 * A23 * A33);
+   D[5] = w_detJ * (C1 * A31 * A31 + C2 * A32 * A32 + C3 * A33 * A33);
+   return 6;
+}
+
+__device__ __forceinline__ double det3(const double J[3][3])
+{
+   return J[0][0] * (J[1][1] * J[2][2] - J[2][1] * J[1][2]) - J[1][0] * (J[0][1] * J[2][2] - J[2][1] * J[0][2]) +
+          J[2][0] * (J[0][1] * J[1][2] - J[1][1] * J[0][2]);
+}
+
+// Write D (6 symmetric entries, or 9 in NATIVE9) and the mass value at one quadrature point (any layout).
+__device__ __forceinline__ void write_qdata(const int *pos, int kind, int nq, int e, int q, double w,
+                                            const double J[3][3], const SetupCoef &cm,
+                                            const SetupCoef &cd, double *qd_diff,
+                                            double *qd_mass)
+{
    const size_t eq = (size_t)e * nq + q;
    if (cd.has)
    {
-      const double w_detJ = w / detJ;
-      const double A11 = (J22 * J33) - (J23 * J32);
-      const double A12 = (J32 * J13) - (J12 * J33);
-      const double A13 = (J12 * J23) - (J22 * J13);
-      const double A21 = (J31 * J23) - (J21 * J33);
-      const double A22 = (J11 * J33) - (J13 * J31);
-      const double A23 = (J21 * J13) - (J11 * J23);
-      const double A31 = (J21 * J32) - (J31 * J22);
-      const double A32 = (J31 * J12) - (J11 * J32);
-      const double A33 = (J11 * J22) - (J12 * J21);
-      const double C = coef_at(cd, eq, e);
-      qd_diff[qidx_diff(pos, kind, nq, e, 0, q)] = w_detJ * (C * A11 * A11 + C * A12 * A12 + C * A13 * A13);
-      qd_diff[qidx_diff(pos, kind, nq, e, 1, q)] = w_detJ * (C * A11 * A21 + C * A12 * A22 + C * A13 * A23);
-      qd_diff[qidx_diff(pos, kind, nq, e, 2, q)] = w_detJ * (C * A11 * A31 + C * A12 * A32 + C * A13 * A33);
-      qd_diff[qidx_diff(pos, kind, nq, e, 3, q)] = w_detJ * (C * A21 * A21 + C * A22 * A22 + C * A23 * A23);
-      qd_diff[qidx_diff(pos, kind, nq, e, 4, q)] = w_detJ * (C * A21 * A31 + C * A22 * A32 + C * A23 * A33);
-      qd_diff[qidx_diff(pos, kind, nq, e, 5, q)] = w_detJ * (C * A31 * A31 + C * A32 * A32 + C * A33 * A33);
+      double D[9];
+      const int n = diff_point(J, w, cd, eq, e, D);
+#pragma unroll
+      for (int c = 0; c < 9; c++)
+      {
+         if (c < n) { qd_diff[qidx_diff(pos, kind, nq, e, c, q)] = D[c]; }
+      }
    }
    if (cm.has)
    {
-      qd_mass[qidx_mass(pos, kind, nq, e, q)] = w * coef_at(cm, eq, e) * detJ;
+      qd_mass[qidx_mass(pos, kind, nq, e, q)] = w * coef_at(cm, eq, e) * det3(J);
    }
 }
 
@@ -166,7 +242,7 @@ template <int Q, bool BLOCKED>
 __global__ void __launch_bounds__(256)
 k_setup_nodes_t(const int *__restrict__ perm, int ne, const double *__restrict__ enodes,
                 const double *__restrict__ W, const Basis1D b1, SetupCoef cm, SetupCoef cd,
-                double *__restrict__ qd_diff, double *__restrict__ qd_mass)
+                double *__restrict__ qd_diff, double *__restrict__ qd_mass, int kind)
 {
    constexpr int NQ = Q * Q * Q;
    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -209,45 +285,24 @@ k_setup_nodes_t(const int *__restrict__ perm, int ne, const double *__restrict__
    }
    if (!BLOCKED)
    {
-      write_qdata(nullptr, QLAYOUT_NATIVE, NQ, e, q, W[q], J, cm, cd, qd_diff, qd_mass);
+      write_qdata(nullptr, kind, NQ, e, q, W[q], J, cm, cd, qd_diff, qd_mass);  // NATIVE / NATIVE9
       return;
    }
-   // same arithmetic as write_qdata (PADiffusionSetup3D / mass setup), blocked stores
-   const double J11 = J[0][0], J21 = J[1][0], J31 = J[2][0];
-   const double J12 = J[0][1], J22 = J[1][1], J32 = J[2][1];
-   const double J13 = J[0][2], J23 = J[1][2], J33 = J[2][2];
-   const double detJ = J11 * (J22 * J33 - J32 * J23) - J21 * (J12 * J33 - J32 * J13) +
-                       J31 * (J12 * J23 - J22 * J13);
+   // write_qdata's arithmetic (PADiffusionSetup3D / mass setup), blocked stores
    const size_t eq = (size_t)e * NQ + q;
    const double w = W[q];
    if (cd.has)
    {
-      const double w_detJ = w / detJ;
-      const double A11 = (J22 * J33) - (J23 * J32);
-      const double A12 = (J32 * J13) - (J12 * J33);
-      const double A13 = (J12 * J23) - (J22 * J13);
-      const double A21 = (J31 * J23) - (J21 * J33);
-      const double A22 = (J11 * J33) - (J13 * J31);
-      const double A23 = (J21 * J13) - (J11 * J23);
-      const double A31 = (J21 * J32) - (J31 * J22);
-      const double A32 = (J31 * J12) - (J11 * J32);
-      const double A33 = (J11 * J22) - (J12 * J21);
-      const double C = coef_at(cd, eq, e);
-      v2d p0, p1, p2;
-      p0.x = w_detJ * (C * A11 * A11 + C * A12 * A12 + C * A13 * A13);
-      p0.y = w_detJ * (C * A11 * A21 + C * A12 * A22 + C * A13 * A23);
-      p1.x = w_detJ * (C * A11 * A31 + C * A12 * A32 + C * A13 * A33);
-      p1.y = w_detJ * (C * A21 * A21 + C * A22 * A22 + C * A23 * A23);
-      p2.x = w_detJ * (C * A21 * A31 + C * A22 * A32 + C * A23 * A33);
-      p2.y = w_detJ * (C * A31 * A31 + C * A32 * A32 + C * A33 * A33);
+      double D[9];
+      (void)diff_point(J, w, cd, eq, e, D);  // (BLOCKED: symmetric coefficients only)
       v2d *dst = reinterpret_cast<v2d *>(qd_diff + ((size_t)blk * NQ + q) * 3 * 128) + lane;
-      dst[0] = p0;
-      dst[64] = p1;
-      dst[128] = p2;
+      dst[0] = v2d{D[0], D[1]};
+      dst[64] = v2d{D[2], D[3]};
+      dst[128] = v2d{D[4], D[5]};
    }
    if (cm.has)
    {
-      qd_mass[((size_t)blk * ((NQ + 1) / 2) + (q >> 1)) * 128 + lane * 2 + (q & 1)] = w * coef_at(cm, eq, e) * detJ;
+      qd_mass[((size_t)blk * ((NQ + 1) / 2) + (q >> 1)) * 128 + lane * 2 + (q & 1)] = w * coef_at(cm, eq, e) * det3(J);
    }
 }
 
@@ -294,7 +349,7 @@ template <int Q, bool BLOCKED>
 __global__ void __launch_bounds__(256)
 k_setup_affine(const int *__restrict__ perm, int ne, const double *__restrict__ enodes,
                const double *__restrict__ Jg,
-               const double *__restrict__ W, SetupCoef cm, SetupCoef cd, double *__restrict__ qd_fac,
+               const double *__restrict__ W, SetupCoef cm, SetupCoef cd, int pw, double *__restrict__ qd_fac,
                double *__restrict__ qd_pair)
 {
    constexpr int NQ = Q * Q * Q;
@@ -348,8 +403,9 @@ k_setup_affine(const int *__restrict__ perm, int ne, const double *__restrict__ 
    const double w = W[q];
    v2d pr;
    pr.x = w * coef_at(cd, eq, e);
-   pr.y = w * coef_at(cm, eq, e) * detJ;
-   if (BLOCKED) { reinterpret_cast<v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane] = pr; }
+   pr.y = pw == 2 ? w * coef_at(cm, eq, e) * detJ : 0.0;
+   if (BLOCKED && pw == 1) { qd_pair[((size_t)blk * NQ + q) * 64 + lane] = pr.x; }  // diffusion-only form
+   else if (BLOCKED) { reinterpret_cast<v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane] = pr; }
    else { reinterpret_cast<v2d *>(qd_pair)[(size_t)e * NQ + q] = pr; }
    if (q == 0)
    {
@@ -397,7 +453,7 @@ template <int Q>
 __global__ void __launch_bounds__(256)
 k_setup_trilinear(const int *__restrict__ perm, int ne, const double *__restrict__ enodes,
                   const double *__restrict__ cfit, const double *__restrict__ W, const QPts qp, SetupCoef cm,
-                  SetupCoef cd, double *__restrict__ qd_geo, double *__restrict__ qd_pair)
+                  SetupCoef cd, int pw, double *__restrict__ qd_geo, double *__restrict__ qd_pair)
 {
    constexpr int NQ = Q * Q * Q;
    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -445,8 +501,9 @@ k_setup_trilinear(const int *__restrict__ perm, int ne, const double *__restrict
    const double w = W[q];
    v2d pr;
    pr.x = w * coef_at(cd, eq, e) / det;
-   pr.y = w * coef_at(cm, eq, e) * det;
-   reinterpret_cast<v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane] = pr;
+   pr.y = pw == 2 ? w * coef_at(cm, eq, e) * det : 0.0;
+   if (pw == 1) { qd_pair[((size_t)blk * NQ + q) * 64 + lane] = pr.x; }  // diffusion-only form
+   else { reinterpret_cast<v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane] = pr; }
    if (q != 0) { return; }
    v2d *dst = reinterpret_cast<v2d *>(qd_geo + (size_t)blk * kTrilinPairs * 128) + lane;
 #pragma unroll
@@ -523,7 +580,7 @@ __global__ void k_jac_trilinear_check(int ne, const double *__restrict__ Jg, con
 template <int Q>
 __global__ void __launch_bounds__(256)
 k_trilinear_expand(int ne, const double *__restrict__ qd_geo, const double *__restrict__ qd_pair, const QPts qp,
-                   double *__restrict__ qd_diff, double *__restrict__ qd_mass)
+                   int pw, double *__restrict__ qd_diff, double *__restrict__ qd_mass)
 {
    constexpr int NQ = Q * Q * Q;
    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -552,7 +609,8 @@ k_trilinear_expand(int ne, const double *__restrict__ qd_geo, const double *__re
                 A23 = J[1][0] * J[0][2] - J[0][0] * J[1][2];
    const double A31 = J[1][0] * J[2][1] - J[2][0] * J[1][1], A32 = J[2][0] * J[0][1] - J[0][0] * J[2][1],
                 A33 = J[0][0] * J[1][1] - J[0][1] * J[1][0];
-   const v2d pr = reinterpret_cast<const v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane];
+   const v2d pr = pw == 2 ? reinterpret_cast<const v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane]
+                          : v2d{qd_pair[((size_t)blk * NQ + q) * 64 + lane], 0.0};
    const double sc = pr.x;  // W beta / det J
    v2d p0, p1, p2;
    p0.x = sc * (A11 * A11 + A12 * A12 + A13 * A13);
@@ -565,7 +623,30 @@ k_trilinear_expand(int ne, const double *__restrict__ qd_geo, const double *__re
    dst[0] = p0;
    dst[64] = p1;
    dst[128] = p2;
-   qd_mass[((size_t)blk * ((NQ + 1) / 2) + (q >> 1)) * 128 + lane * 2 + (q & 1)] = pr.y;  // W alpha det J
+   if (pw == 2) { qd_mass[((size_t)blk * ((NQ + 1) / 2) + (q >> 1)) * 128 + lane * 2 + (q & 1)] = pr.y; }  // W alpha det J
+}
+
+// AFFINE (p <= 2) -> BLOCKED: D(q) = (W beta)_q C_e and the mass value (W alpha det J)_q, for the
+// diagonal, the E-vector apply and the qdata export of a diffusion-only AFFINE form (pw = 1).
+template <int Q>
+__global__ void __launch_bounds__(256)
+k_affine_expand(int ne, const double *__restrict__ qd_fac, const double *__restrict__ qd_pair, int pw,
+                double *__restrict__ qd_diff, double *__restrict__ qd_mass)
+{
+   constexpr int NQ = Q * Q * Q;
+   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   const int lane = (int)(t & 63);
+   const long rest = t >> 6;
+   const int q = (int)(rest % NQ);
+   const long blk = rest / NQ;
+   if (blk * 64 + lane >= ne) { return; }
+   const v2d *C = reinterpret_cast<const v2d *>(qd_fac + (size_t)blk * 3 * 128) + lane;
+   const v2d pr = pw == 2 ? reinterpret_cast<const v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane]
+                          : v2d{qd_pair[((size_t)blk * NQ + q) * 64 + lane], 0.0};
+   v2d *dst = reinterpret_cast<v2d *>(qd_diff + ((size_t)blk * NQ + q) * 3 * 128) + lane;
+#pragma unroll
+   for (int k = 0; k < 3; k++) { dst[k * 64] = pr.x * C[k * 64]; }
+   if (pw == 2) { qd_mass[((size_t)blk * ((NQ + 1) / 2) + (q >> 1)) * 128 + lane * 2 + (q & 1)] = pr.y; }
 }
 
 SetupCoef make_setup_coef(const CoeffDesc *c, const double *q)
@@ -573,8 +654,10 @@ SetupCoef make_setup_coef(const CoeffDesc *c, const double *q)
    SetupCoef s{};
    if (!c) { return s; }
    s.has = 1;
-   s.is_const = (c->kind == COEFF_CONSTANT);
+   s.is_const = (c->kind == COEFF_CONSTANT || c->kind >= COEFF_CONST_VECTOR);
+   s.dim = c->dim();
    s.value = c->value;
+   for (int i = 0; i < 9; i++) { s.cv[i] = c->cv[i]; }
    s.quad = q;
    s.emask = c->emask;
    return s;
@@ -629,12 +712,12 @@ void setup_from_nodes(const QLayout &L, int Q, const double *enodes, const doubl
       if (blocked)                                                                                       \
       {                                                                                                  \
          hipLaunchKernelGGL((k_setup_nodes_t<QQ, true>), dim3(grid_for(nb, 256)), dim3(256), 0, s, L.perm, L.ne, \
-                            enodes, W, b1, scm, scd, qd_diff, qd_mass);                                  \
+                            enodes, W, b1, scm, scd, qd_diff, qd_mass, L.kind);                          \
       }                                                                                                  \
       else                                                                                               \
       {                                                                                                  \
          hipLaunchKernelGGL((k_setup_nodes_t<QQ, false>), dim3(grid_for(nb, 256)), dim3(256), 0, s, nullptr, L.ne, \
-                            enodes, W, b1, scm, scd, qd_diff, qd_mass);                                  \
+                            enodes, W, b1, scm, scd, qd_diff, qd_mass, L.kind);                          \
       }                                                                                                  \
       ECM2_HIP(hipGetLastError());                                                                       \
       return;                                                                                            \
@@ -690,20 +773,20 @@ void setup_trilinear(const QLayout &L, int Q, const double *enodes, const double
                      double *qd_geo, double *qd_pair, hipStream_t s)
 {
    if (L.ne == 0) { return; }
-   ECM2_VERIFY(L.kind == QLAYOUT_TRILINEAR && cm && cd && (enodes || cfit), ERR_INTERNAL,
-               "trilinear setup needs a TRILINEAR layout, both coefficients and the corners or fitted maps");
+   ECM2_VERIFY(L.kind == QLAYOUT_TRILINEAR && (cm || L.pw == 1) && cd && (enodes || cfit), ERR_INTERNAL,
+               "trilinear setup needs a TRILINEAR layout, the coefficients and the corners or fitted maps");
    ECM2_VERIFY(!L.pos || L.perm, ERR_INTERNAL, "blocked setup needs the inverse permutation");
    const SetupCoef scm = make_setup_coef(cm, cm_q), scd = make_setup_coef(cd, cd_q);
    const long n = (long)L.nblk() * 64 * L.nq;
    if (Q == 3)
    {
       hipLaunchKernelGGL((k_setup_trilinear<3>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.perm, L.ne, enodes,
-                         cfit, W, qp, scm, scd, qd_geo, qd_pair);
+                         cfit, W, qp, scm, scd, L.pw, qd_geo, qd_pair);
    }
    else if (Q == 4)
    {
       hipLaunchKernelGGL((k_setup_trilinear<4>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.perm, L.ne, enodes,
-                         cfit, W, qp, scm, scd, qd_geo, qd_pair);
+                         cfit, W, qp, scm, scd, L.pw, qd_geo, qd_pair);
    }
    else { ECM2_VERIFY(false, ERR_UNSUPPORTED, "trilinear setup: Q1D " << Q << " not instantiated"); }
    ECM2_HIP(hipGetLastError());
@@ -717,14 +800,33 @@ void trilinear_expand(const QLayout &L, int Q, const double *qd_geo, const doubl
    if (Q == 3)
    {
       hipLaunchKernelGGL((k_trilinear_expand<3>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.ne, qd_geo, qd_pair, qp,
-                         qd_diff, qd_mass);
+                         L.pw, qd_diff, qd_mass);
    }
    else if (Q == 4)
    {
       hipLaunchKernelGGL((k_trilinear_expand<4>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.ne, qd_geo, qd_pair, qp,
-                         qd_diff, qd_mass);
+                         L.pw, qd_diff, qd_mass);
    }
    else { ECM2_VERIFY(false, ERR_UNSUPPORTED, "trilinear expand: Q1D " << Q << " not instantiated"); }
+   ECM2_HIP(hipGetLastError());
+}
+
+void affine_expand(const QLayout &L, int Q, const double *qd_fac, const double *qd_pair, double *qd_diff,
+                   double *qd_mass, hipStream_t s)
+{
+   if (L.ne == 0) { return; }
+   const long n = (long)L.nblk() * 64 * L.nq;
+   if (Q == 3)
+   {
+      hipLaunchKernelGGL((k_affine_expand<3>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.ne, qd_fac, qd_pair, L.pw,
+                         qd_diff, qd_mass);
+   }
+   else if (Q == 4)
+   {
+      hipLaunchKernelGGL((k_affine_expand<4>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.ne, qd_fac, qd_pair, L.pw,
+                         qd_diff, qd_mass);
+   }
+   else { ECM2_VERIFY(false, ERR_UNSUPPORTED, "affine expand: Q1D " << Q << " not instantiated"); }
    ECM2_HIP(hipGetLastError());
 }
 
@@ -733,7 +835,8 @@ void setup_affine(const QLayout &L, int Q, const double *enodes, const double *J
                   double *qd_fac, double *qd_pair, hipStream_t s)
 {
    if (L.ne == 0) { return; }
-   ECM2_VERIFY(L.affine() && cm && cd, ERR_INTERNAL, "affine setup needs an AFFINE layout and both coefficients");
+   ECM2_VERIFY(L.affine() && cd && (cm || (L.pw == 1 && L.kind == QLAYOUT_AFFINE)), ERR_INTERNAL,
+               "affine setup needs an AFFINE layout and its coefficients");
    ECM2_VERIFY(!L.pos || L.perm, ERR_INTERNAL, "blocked setup needs the inverse permutation");
    const SetupCoef scm = make_setup_coef(cm, cm_q), scd = make_setup_coef(cd, cd_q);
    const bool blk = L.kind == QLAYOUT_AFFINE;
@@ -744,12 +847,12 @@ void setup_affine(const QLayout &L, int Q, const double *enodes, const double *J
       if (blk)                                                                                           \
       {                                                                                                  \
          hipLaunchKernelGGL((k_setup_affine<QQ, true>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.perm, L.ne, \
-                            enodes, J, W, scm, scd, qd_fac, qd_pair);                                    \
+                            enodes, J, W, scm, scd, L.pw, qd_fac, qd_pair);                              \
       }                                                                                                  \
       else                                                                                               \
       {                                                                                                  \
          hipLaunchKernelGGL((k_setup_affine<QQ, false>), dim3(grid_for(n, 256)), dim3(256), 0, s, nullptr, L.ne, \
-                            enodes, J, W, scm, scd, qd_fac, qd_pair);                                    \
+                            enodes, J, W, scm, scd, L.pw, qd_fac, qd_pair);                              \
       }                                                                                                  \
       ECM2_HIP(hipGetLastError());                                                                       \
       return;                                                                                            \

@@ -340,7 +340,8 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 // J[.][2] = G + H xi; then f = (W beta / det J) adj(J) (adj(J)^T grad u), m = (W alpha det J) u --
 // PADiffusionSetup3D's D = W beta adj(J) adj(J)^T / det J (bilininteg_diffusion_kernels.cpp:
 // 349-362) and the mass setup's W alpha det J, never stored.
-template <int D, int Q, bool SPLIT, int RM, bool TL = false>
+// PW: point values per quadrature point (2: the pair; 1: a diffusion-only form's W beta [/ det J]).
+template <int D, int Q, bool SPLIT, int RM, bool TL = false, int PW = 2>
 __global__ void __launch_bounds__(256, 1)
 k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
                const double *__restrict__ qdd, const double *__restrict__ qdm,
@@ -381,11 +382,15 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
          const int f = 3 * k + i;
          return (f & 1) ? ce[f >> 1].y : ce[f >> 1].x;
       };
-      const double *qa = qdm + (size_t)blk * NQ * 128 + lane * 2;
+      const double *qa = qdm + (size_t)blk * NQ * 64 * PW + lane * PW;
       v2d ca[Q], na[Q];
       auto load_row = [&](int row, v2d (&aq)[Q]) {
 #pragma unroll
-         for (int qx = 0; qx < Q; qx++) { aq[qx] = ld2(qa + (size_t)(row * Q + qx) * 128); }
+         for (int qx = 0; qx < Q; qx++)
+         {
+            if constexpr (PW == 2) { aq[qx] = ld2(qa + (size_t)(row * Q + qx) * 128); }
+            else { aq[qx] = v2d{__builtin_nontemporal_load(qa + (size_t)(row * Q + qx) * 64), 0.0}; }
+         }
       };
       // PF2: three row buffers in rotation, each row issues the row two ahead, so 8 KiB per wave
       // are in flight instead of 4 (profiles/r2_ab_pf2.txt: C4 kernel -4.3%); the plane loop is
@@ -548,14 +553,14 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                   double t3 = A13 * ux;
                   t3 += A23 * uy;
                   t3 += A33 * uz;
-                  m = sa.y * u;  // W alpha det J
+                  m = PW == 2 ? sa.y * u : 0.0;  // W alpha det J
                   fx = sc * (A11 * t1 + A12 * t2 + A13 * t3);
                   fy = sc * (A21 * t1 + A22 * t2 + A23 * t3);
                   fz = sc * (A31 * t1 + A32 * t2 + A33 * t3);
                }
                else
                {
-                  m = sa.y * u;
+                  m = PW == 2 ? sa.y * u : 0.0;
                   fx = sa.x * (ce[0].x * ux + ce[0].y * uy + ce[1].x * uz);
                   fy = sa.x * (ce[0].y * ux + ce[1].y * uy + ce[2].x * uz);
                   fz = sa.x * (ce[1].x * ux + ce[2].x * uy + ce[2].y * uz);
@@ -564,7 +569,7 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                for (int dx = 0; dx < D; dx++)
                {
                   const double bq = b.B[qx + MQ * dx], gq = b.G[qx + MQ * dx];
-                  T0[dx] += bq * m;
+                  if (PW == 2) { T0[dx] += bq * m; }
                   T0[dx] += gq * fx;
                   T1[dx] += bq * fy;
                   T2[dx] += bq * fz;
@@ -664,13 +669,12 @@ struct LatticeXYZ
             for (int X = 0; X < L; X++) { v[tpe_lattice_slot(D, X, Y, Z)] = (unsigned short)(X | Y << 5 | Z << 10); }
    }
 };
-__constant__ LatticeXYZ<2> kLatXYZ2 = LatticeXYZ<2>();
-__constant__ LatticeXYZ<3> kLatXYZ3 = LatticeXYZ<3>();
+__constant__ LatticeXYZ<3> kLatXYZ3 = LatticeXYZ<3>();  // (the lattice kernel runs at p = 2)
 template <int D>
 __device__ __forceinline__ unsigned lattice_xyz(int j)
 {
-   if constexpr (D == 2) { return kLatXYZ2.v[j]; }
-   else { return kLatXYZ3.v[j]; }
+   static_assert(D == 3, "p = 2 lattice table");
+   return kLatXYZ3.v[j];
 }
 
 // TRILINEAR apply for forms whose blocks are all 4x4x4 bricks of one dof lattice (RM 1: regular
@@ -685,13 +689,13 @@ __device__ __forceinline__ unsigned lattice_xyz(int j)
 // same region then stages the cross-wave face exchange) and every plane adds its z-transpose into
 // them; (c) the per-point pair is (W beta / det J, W alpha det J), so no determinant or division
 // per point.  LDS 78.6 KB per workgroup: two workgroups (8 waves) per CU.
-template <int D, int Q, bool SPLIT, int RM>
+template <int D, int Q, bool SPLIT, int RM, int PW = 2>
 __global__ void __launch_bounds__(256, 2)
 k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
                 const double *__restrict__ qdd, const double *__restrict__ qdm,
                 const double *__restrict__ x, const double *__restrict__ xg,
                 double *__restrict__ y, double *__restrict__ yg, const Basis1D b,
-                const double *__restrict__ rowtab, const int *__restrict__ lane_flags, double *__restrict__ part,
+                const int *__restrict__ lane_flags, double *__restrict__ part,
                 const int *__restrict__ treg, int pstride, const int *__restrict__ lmap, const QPts qp)
 {
    static_assert(RM == 1 || RM == 3, "lattice blocks only");
@@ -714,11 +718,15 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
    auto ld2 = [&](const double *p) -> v2d { return __builtin_nontemporal_load(reinterpret_cast<const v2d *>(p)); };
    constexpr int NCE = kTrilinPairs;
    v2d ce[NCE];
-   const double *qa = qdm + (size_t)blk * NQ * 128 + lane * 2;
+   const double *qa = qdm + (size_t)blk * NQ * 64 * PW + lane * PW;
+   auto ldp = [&](int q) -> v2d {  // the point values of point q (PW = 1: W beta / det J alone)
+      if constexpr (PW == 2) { return ld2(qa + (size_t)q * 128); }
+      else { return v2d{__builtin_nontemporal_load(qa + (size_t)q * 64), 0.0}; }
+   };
    v2d ca[Q];
    auto load_row = [&](int row, v2d (&aq)[Q]) {
 #pragma unroll
-      for (int qx = 0; qx < Q; qx++) { aq[qx] = ld2(qa + (size_t)(row * Q + qx) * 128); }
+      for (int qx = 0; qx < Q; qx++) { aq[qx] = ldp(row * Q + qx); }
    };
    if (wave_on)
    {
@@ -851,7 +859,7 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
                const v2d sa = cur[qx];
                // the next row's pair of this point goes into the slot just read: one row of pairs in
                // flight in Q registers pairs (ping-pong buffers cost 16 VGPRs more)
-               cur[qx] = ld2(qa + (size_t)(next_row * Q + qx) * 128);
+               cur[qx] = ldp(next_row * Q + qx);
                const double xi = qp.x[qx];
                // J = [ja | jb | jc] (rows: coordinates), adj(J) rows A1., A2., A3.
                const double jb0 = pC[0] + pB[0] * xi, jb1 = pC[1] + pB[1] * xi, jb2 = pC[2] + pB[2] * xi;
@@ -872,7 +880,7 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
                double t3 = A13 * sux;
                t3 += A23 * suy;
                t3 += A33 * suz;
-               const double m = sa.y * u;
+               const double m = PW == 2 ? sa.y * u : 0.0;
                double fx = A11 * t1;
                fx += A12 * t2;
                fx += A13 * t3;
@@ -886,7 +894,7 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
                for (int dx = 0; dx < D; dx++)
                {
                   const double bq = b.B[qx + MQ * dx], gq = b.G[qx + MQ * dx];
-                  T0[dx] += bq * m;
+                  if (PW == 2) { T0[dx] += bq * m; }
                   T0[dx] += gq * fx;
                   T1[dx] += bq * fy;
                   T2[dx] += bq * fz;
@@ -1221,35 +1229,39 @@ void launch_tpe(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipS
 {
    const int nb = a.blk_end - a.blk_begin;
    const dim3 grid((nb + 3) / 4), block(256);
+   // compressed layouts: both integrators (PW 2) or a diffusion-only form (PW 1)
+   constexpr int PW = MASS ? 2 : 1;
    if (a.kind == QLAYOUT_TRILINEAR)
    {
-      if constexpr (MASS && DIFF)
+      if constexpr (DIFF)
       {
+         ECM2_VERIFY(a.pw == PW, ERR_INTERNAL, "TRILINEAR point values do not match the integrators");
 #define ECM2_TL(KT)                                                                                           \
    hipLaunchKernelGGL(KT, grid, block, 0, s, a.ne, a.blk_begin, a.blk_end, a.n_owned, a.gmap, a.qdd, a.qdm, a.x, \
                       a.xg, a.y, a.yg, b, a.lane_flags, a.part, a.treg, a.part_stride, a.lmap, a.qp)
          // every block a lattice brick: the two-waves-per-SIMD lattice kernel; else per element
          // (p = 2; at p = 1 the per-element kernel fits two waves already)
 #define ECM2_TLB(RM)                                                                                          \
-   hipLaunchKernelGGL((k_apply_tpe_tlb<3, 4, SPLIT, RM>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end,          \
-                      a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, rowtab, a.lane_flags, a.part, a.treg, \
+   hipLaunchKernelGGL((k_apply_tpe_tlb<3, 4, SPLIT, RM, PW>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end,      \
+                      a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part, a.treg,      \
                       a.part_stride, a.lmap, a.qp)
          constexpr bool LAT = D == 3 && Q == 4;
          if (LAT && a.treg && a.treg_all) { ECM2_TLB(1); }
          else if (LAT && a.treg && a.tlat_all) { ECM2_TLB(3); }
 #undef ECM2_TLB
-         else if (a.treg) { ECM2_TL((k_apply_tpe_sf<D, Q, SPLIT, 2, true>)); }
-         else { ECM2_TL((k_apply_tpe_sf<D, Q, SPLIT, 0, true>)); }
+         else if (a.treg) { ECM2_TL((k_apply_tpe_sf<D, Q, SPLIT, 2, true, PW>)); }
+         else { ECM2_TL((k_apply_tpe_sf<D, Q, SPLIT, 0, true, PW>)); }
 #undef ECM2_TL
       }
-      else { ECM2_VERIFY(false, ERR_INTERNAL, "TRILINEAR qdata needs both integrators"); }
+      else { ECM2_VERIFY(false, ERR_INTERNAL, "TRILINEAR qdata needs the diffusion integrator"); }
       return;
    }
    if (a.kind == QLAYOUT_AFFINE)
    {
-      if constexpr (MASS && DIFF)
+      if constexpr (DIFF)
       {
-         if (a.latency)
+         ECM2_VERIFY(a.pw == PW, ERR_INTERNAL, "AFFINE point values do not match the integrators");
+         if (MASS && a.latency)
          {
             hipLaunchKernelGGL((k_apply_tpe_pp<D, Q, SPLIT>), dim3(nb), dim3(256), 0, s, a.ne, a.blk_begin,
                                a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part,
@@ -1258,9 +1270,9 @@ void launch_tpe(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipS
          else
          {
 #define ECM2_SF(RM)                                                                                           \
-   hipLaunchKernelGGL((k_apply_tpe_sf<D, Q, SPLIT, RM>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end, a.n_owned, \
-                      a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part, a.treg, a.part_stride, \
-                      a.lmap, a.qp)
+   hipLaunchKernelGGL((k_apply_tpe_sf<D, Q, SPLIT, RM, false, PW>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end, \
+                      a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, b, a.lane_flags, a.part, a.treg,       \
+                      a.part_stride, a.lmap, a.qp)
             if (a.treg && a.treg_all) { ECM2_SF(1); }
             else if (a.treg && a.tlat_all) { ECM2_SF(3); }
             else if (a.treg) { ECM2_SF(2); }
@@ -1268,7 +1280,7 @@ void launch_tpe(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipS
 #undef ECM2_SF
          }
       }
-      else { ECM2_VERIFY(false, ERR_INTERNAL, "AFFINE qdata needs both integrators"); }
+      else { ECM2_VERIFY(false, ERR_INTERNAL, "AFFINE qdata needs the diffusion integrator"); }
       return;
    }
    hipLaunchKernelGGL((k_apply_tpe_pf<D, Q, MASS, DIFF, SPLIT>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end,

@@ -36,7 +36,10 @@ namespace ecm2
 {
 
 enum QLayoutKind : int { QLAYOUT_NATIVE = 0, QLAYOUT_BLOCKED = 1, QLAYOUT_AFFINE = 2, QLAYOUT_AFFINE_E = 3,
-                         QLAYOUT_TRILINEAR = 4 };
+                         QLAYOUT_TRILINEAR = 4, QLAYOUT_NATIVE9 = 5 };
+// NATIVE9: the reference's layout for a general (nonsymmetric) matrix diffusion coefficient,
+// D(q, k, e) = [e][9][NQ] with k = 3 i + j for D_ij (bilininteg_diffusion_kernels.cpp:320-345,
+// "symmetric ? 6 : 9"); the workgroup-per-element kernels read it.
 // TRILINEAR (fused thread-per-element kernel, p <= 2, both integrators, geometry from element
 // corners, elements NOT all parallelepipeds): the geometry is stored once per element as the
 // coefficients of its trilinear map x_i(xi, eta, zeta) = c0 + c1 xi + c2 eta + c3 zeta +
@@ -61,11 +64,15 @@ struct QLayout
 {
    int kind = QLAYOUT_NATIVE;
    int ne = 0, nq = 0;
+   // AFFINE / TRILINEAR point values: 2 = the pair (diffusion factor, mass factor), 1 = the
+   // diffusion factor alone (a form without a MassIntegrator: [blk][q][lane], 8 B per point)
+   int pw = 2;
    const int *pos = nullptr;  // device: caller element -> internal position (BLOCKED)
    const int *perm = nullptr; // device: internal position -> caller element (BLOCKED)
    size_t diff_size() const
    {
       if (kind == QLAYOUT_NATIVE) { return (size_t)ne * 6 * nq; }
+      if (kind == QLAYOUT_NATIVE9) { return (size_t)ne * 9 * nq; }
       if (kind == QLAYOUT_AFFINE) { return (size_t)nblk() * 6 * kElemBlock; }
       if (kind == QLAYOUT_TRILINEAR) { return (size_t)nblk() * 2 * kTrilinPairs * kElemBlock; }
       if (kind == QLAYOUT_AFFINE_E) { return (size_t)ne * 6; }
@@ -73,8 +80,8 @@ struct QLayout
    }
    size_t mass_size() const
    {
-      if (kind == QLAYOUT_NATIVE) { return (size_t)ne * nq; }
-      if (kind == QLAYOUT_AFFINE || kind == QLAYOUT_TRILINEAR) { return (size_t)nblk() * nq * 2 * kElemBlock; }
+      if (kind == QLAYOUT_NATIVE || kind == QLAYOUT_NATIVE9) { return (size_t)ne * nq; }
+      if (kind == QLAYOUT_AFFINE || kind == QLAYOUT_TRILINEAR) { return (size_t)nblk() * nq * pw * kElemBlock; }
       if (kind == QLAYOUT_AFFINE_E) { return (size_t)ne * nq * 2; }
       return (size_t)nblk() * ((nq + 1) / 2) * 2 * kElemBlock;
    }
@@ -92,17 +99,36 @@ struct QLayout
 // stage's mass coefficient, alpha(T) = rho_c + gdt_cb * w_b(T) with the temperature-dependent
 // perfusion w_b(T) = w0 * max(0, 1 + a (T - t0)) below the coagulation temperature t_stop and
 // 0 at or above it (perfusion shut-down in ablated tissue).  p = (rho_c, gdt_cb, w0, a, t0, t_stop).
-enum CoeffKind : int { COEFF_CONSTANT = 0, COEFF_QUAD = 1, COEFF_GRIDFUNC_AFFINE = 2, COEFF_GRIDFUNC_PERFUSION = 3 };
+// Vector / matrix diffusion coefficients (DiffusionIntegrator(VectorCoefficient / MatrixCoefficient),
+// PADiffusionSetup3D coeffDim 3 / 6 / 9, bilininteg_diffusion_kernels.cpp:297-348): QUAD_* device
+// [ne][nq][dim], CONST_* the dim values in cv; dim 3 = diag(v), 6 = symmetric (11,12,13,22,23,33),
+// 9 = general, row-major M(i,j) at 3 i + j (CoefficientVector::ProjectTranspose, coefficient.cpp:2093-2123).
+enum CoeffKind : int { COEFF_CONSTANT = 0, COEFF_QUAD = 1, COEFF_GRIDFUNC_AFFINE = 2, COEFF_GRIDFUNC_PERFUSION = 3,
+                       COEFF_QUAD_VECTOR = 4, COEFF_QUAD_SYMMATRIX = 5, COEFF_QUAD_MATRIX = 6,
+                       COEFF_CONST_VECTOR = 7, COEFF_CONST_SYMMATRIX = 8, COEFF_CONST_MATRIX = 9 };
 struct CoeffDesc
 {
    int kind = COEFF_CONSTANT;
    double value = 1.0;           // constant
-   const double *quad = nullptr; // device [ne][nq]
+   double cv[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // CONST_VECTOR / _SYMMATRIX / _MATRIX
+   const double *quad = nullptr; // device [ne][nq] (QUAD) or [ne][nq][dim] (QUAD_VECTOR / _SYMMATRIX / _MATRIX)
    const double *lvec = nullptr; // device L-vector of T
    double scale = 1.0, slope = 0.0, t_ref = 0.0;  // GRIDFUNC_AFFINE
    double p[6] = {0, 0, 0, 0, 0, 0};              // GRIDFUNC_PERFUSION
    const double *emask = nullptr; // device [ne] element weights of an attribute-marked integrator (form-owned)
    bool gridfunc() const { return kind == COEFF_GRIDFUNC_AFFINE || kind == COEFF_GRIDFUNC_PERFUSION; }
+   // values per point: 1 scalar, 3 vector, 6 symmetric matrix, 9 general matrix
+   int dim() const
+   {
+      switch (kind)
+      {
+         case COEFF_QUAD_VECTOR: case COEFF_CONST_VECTOR: return 3;
+         case COEFF_QUAD_SYMMATRIX: case COEFF_CONST_SYMMATRIX: return 6;
+         case COEFF_QUAD_MATRIX: case COEFF_CONST_MATRIX: return 9;
+         default: return 1;
+      }
+   }
+   bool quad_values() const { return kind == COEFF_QUAD || (kind >= COEFF_QUAD_VECTOR && kind <= COEFF_QUAD_MATRIX); }
 };
 
 struct CoeffParams  // kernel-argument copy of CoeffDesc::p
@@ -128,6 +154,7 @@ __host__ __device__ inline double coeff_law(int kind, double T, double scale, do
 struct ApplyArgs
 {
    int kind = QLAYOUT_NATIVE;
+   int pw = 2;                      // AFFINE / TRILINEAR point values (QLayout::pw)
    int ne = 0, blk_begin = 0, blk_end = 0, n_owned = 0;
    const int *pos = nullptr;        // element permutation (blocked layout), may be null
    const int *lane_flags = nullptr; // [blk][64]: in-wave face merge flags
@@ -239,13 +266,13 @@ void setup_from_nodes(const QLayout &L, int Q, const double *enodes, const doubl
                       const Basis1D &b1, const CoeffDesc *cm, const CoeffDesc *cd,
                       const double *cm_q, const double *cd_q,
                       double *qd_diff, double *qd_mass, hipStream_t s);
-// AFFINE / AFFINE_E layout (see above) from the corners of parallelepiped elements; needs both
-// coefficients (cm, cd non-null).
+// AFFINE / AFFINE_E layout (see above) from the corners of parallelepiped elements; needs the
+// diffusion coefficient (cd); cm null: a diffusion-only form (L.pw = 1, AFFINE only).
 // J (optional, device, MFEM layout NQ x 3 x 3 x NE) replaces the corners.
 void setup_affine(const QLayout &L, int Q, const double *enodes, const double *J, const double *W,
                   const CoeffDesc *cm, const CoeffDesc *cd, const double *cm_q, const double *cd_q,
                   double *qd_fac, double *qd_pair, hipStream_t s);
-// TRILINEAR layout (see above) from lexicographic element corners; both coefficients.
+// TRILINEAR layout (see above) from lexicographic element corners; cd, and cm unless L.pw = 1.
 // (enodes: lexicographic corners, or cfit: the fitted map coefficients [ne][21] of
 // jacobians_trilinear_fit)
 void setup_trilinear(const QLayout &L, int Q, const double *enodes, const double *cfit, const double *W,
@@ -254,6 +281,9 @@ void setup_trilinear(const QLayout &L, int Q, const double *enodes, const double
 // Trilinear-map coefficients of every element from MFEM-layout Jacobians (cfit [ne][21]); false
 // when some element's Jacobians are not those of a trilinear map (1e-13; synchronises s).
 bool jacobians_trilinear_fit(int ne, int Q, const QPts &qp, const double *J, double *cfit, hipStream_t s);
+// The BLOCKED per-point qdata of an AFFINE (p <= 2) form (L: its layout; outputs sized as BLOCKED).
+void affine_expand(const QLayout &L, int Q, const double *qd_fac, const double *qd_pair, double *qd_diff,
+                   double *qd_mass, hipStream_t s);
 // The BLOCKED per-point qdata of a TRILINEAR form (L: its layout; outputs sized as BLOCKED).
 void trilinear_expand(const QLayout &L, int Q, const double *qd_geo, const double *qd_pair, const QPts &qp,
                       double *qd_diff, double *qd_mass, hipStream_t s);

@@ -146,9 +146,10 @@ void PAForm::add_integrator(int kind, const CoeffDesc &c, const int *marker, int
 {
    ECM2_VERIFY(!marker || n_marker >= 0, ERR_ARG, "negative marker size");
    ECM2_VERIFY(kind == INTEG_MASS || kind == INTEG_DIFFUSION, ERR_ARG, "unknown integrator " << kind);
-   ECM2_VERIFY(c.kind == COEFF_CONSTANT || c.kind == COEFF_QUAD || c.gridfunc(),
-               ERR_ARG, "unknown coefficient kind " << c.kind);
-   ECM2_VERIFY(c.kind != COEFF_QUAD || ne_ == 0 || c.quad, ERR_ARG, "null quadrature coefficient");
+   ECM2_VERIFY(c.kind >= COEFF_CONSTANT && c.kind <= COEFF_CONST_MATRIX, ERR_ARG, "unknown coefficient kind " << c.kind);
+   ECM2_VERIFY(c.dim() == 1 || kind == INTEG_DIFFUSION, ERR_ARG,
+               "vector / matrix coefficients belong to a DiffusionIntegrator");
+   ECM2_VERIFY(!c.quad_values() || ne_ == 0 || c.quad, ERR_ARG, "null quadrature coefficient");
    ECM2_VERIFY(!c.gridfunc() || ndofs_ == 0 || c.lvec, ERR_ARG, "null grid function");
    if (kind == INTEG_MASS)
    {
@@ -668,18 +669,35 @@ void PAForm::assemble(hipStream_t s)
                "thread-per-element kernel needs (D1D,Q1D) in {(2,3),(3,4)}");
    ECM2_VERIFY(resolved_mode_ != KERNEL_LINE || kern::has_line(D_, Q_), ERR_UNSUPPORTED,
                "line kernel needs Q1D in {D1D, D1D+1} and Q1D <= 8");
-   layout_.kind = (resolved_mode_ == KERNEL_TPE) ? QLAYOUT_BLOCKED : QLAYOUT_NATIVE;
+   // a general (nonsymmetric) matrix coefficient: the reference's 9-entry qdata (NATIVE9), read by
+   // the workgroup-per-element kernels; any other vector / matrix coefficient keeps 6 symmetric
+   // entries but varies per point in direction: no geometry compression
+   const int cdim = have_diff_ ? cdiff_.dim() : 1;
+   if (cdim == 9)
+   {
+      ECM2_VERIFY(mode_ == KERNEL_AUTO || mode_ == KERNEL_WPE || mode_ == KERNEL_UNFUSED, ERR_UNSUPPORTED,
+                  "a general matrix coefficient runs the workgroup-per-element or unfused kernels");
+      if (mode_ == KERNEL_AUTO) { resolved_mode_ = KERNEL_WPE; }
+   }
+   layout_.kind = (resolved_mode_ == KERNEL_TPE) ? QLAYOUT_BLOCKED : (cdim == 9 ? QLAYOUT_NATIVE9 : QLAYOUT_NATIVE);
+   layout_.pw = 2;
+   // Compressed geometry: both integrators, or (the thread-per-element kernels, p <= 2) a
+   // diffusion-only form such as ex16's K (point values W beta [/ det J] alone, 8 B per point).  A
+   // mass-only form keeps the BLOCKED mass stream, already one 8-byte W alpha det J per point.
+   const bool both = have_mass_ && have_diff_ && cdim == 1;
+   const bool comp_tpe = compress_ && have_diff_ && cdim == 1 && resolved_mode_ == KERNEL_TPE;
    bool affine = affine_;
-   if (jac_ && compress_ && have_mass_ && have_diff_ && (resolved_mode_ == KERNEL_TPE || resolved_mode_ == KERNEL_LINE))
+   if (jac_ && ((compress_ && both && resolved_mode_ == KERNEL_LINE) || comp_tpe))
    {
       affine = kern::jacobians_affine(ne_, NQ_, jac_, s);  // the reference binding's geometry
    }
-   if (affine && compress_ && have_mass_ && have_diff_)
+   if (affine && compress_ && both && resolved_mode_ == KERNEL_LINE) { layout_.kind = QLAYOUT_AFFINE_E; }
+   else if (affine && comp_tpe)
    {
-      if (resolved_mode_ == KERNEL_TPE) { layout_.kind = QLAYOUT_AFFINE; }
-      else if (resolved_mode_ == KERNEL_LINE) { layout_.kind = QLAYOUT_AFFINE_E; }
+      layout_.kind = QLAYOUT_AFFINE;
+      layout_.pw = have_mass_ ? 2 : 1;
    }
-   else if (!affine && compress_ && have_mass_ && have_diff_ && resolved_mode_ == KERNEL_TPE)
+   else if (!affine && comp_tpe)
    {
       // general trilinear hexes: the map coefficients per element (from the corners, or fitted
       // to the reference binding's Jacobians when they are a trilinear map's), J per point
@@ -691,7 +709,11 @@ void PAForm::assemble(hipStream_t s)
          cfit_.resize(std::max(1, ne_) * 21);
          tl = kern::jacobians_trilinear_fit(ne_, Q_, qp, jac_, cfit_.data(), s);
       }
-      if (tl) { layout_.kind = QLAYOUT_TRILINEAR; }
+      if (tl)
+      {
+         layout_.kind = QLAYOUT_TRILINEAR;
+         layout_.pw = have_mass_ ? 2 : 1;
+      }
    }
 
    // the merge plan (cross-wave faces), the regular blocks and the partial-slot layout belong
@@ -1125,8 +1147,10 @@ std::vector<double> PAForm::marker_weights(int k) const
 
 void PAForm::setup_qdata(hipStream_t s, const std::pair<int, std::vector<double>> *wover)
 {
+   // (compressed layouts: qd_mass_ holds the point values, present with either integrator)
+   const bool comp = layout_.kind == QLAYOUT_AFFINE || layout_.kind == QLAYOUT_AFFINE_E || layout_.kind == QLAYOUT_TRILINEAR;
    qd_diff_.resize(have_diff_ ? layout_.diff_size() : 0);
-   qd_mass_.resize(have_mass_ ? layout_.mass_size() : 0);
+   qd_mass_.resize(have_mass_ || comp ? layout_.mass_size() : 0);
    // the setup kernels write every entry except the padding lanes of a partial last block
    // (blocked layout), which are cleared so the apply kernels stream defined values
    if (layout_.blocked() && ne_ % kElemBlock)
@@ -1164,7 +1188,7 @@ void PAForm::setup_qdata(hipStream_t s, const std::pair<int, std::vector<double>
 
    // Coefficient values at quadrature points (CoefficientVector::Project).
    auto coeff_values = [&](const CoeffDesc &c, DeviceArray<double> &tmp) -> const double * {
-      if (c.kind == COEFF_QUAD) { return c.quad; }
+      if (c.quad_values()) { return c.quad; }
       if (c.gridfunc())
       {
          tmp.resize((size_t)ne_ * NQ_);
@@ -1349,6 +1373,7 @@ ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, doubl
 {
    ApplyArgs a;
    a.kind = layout_.kind;
+   a.pw = layout_.pw;
    a.ne = ne_;
    a.blk_begin = b0;
    a.blk_end = b1;
@@ -1462,9 +1487,9 @@ void PAForm::diagonal_from_qdata(double *diag, hipStream_t s)
       if (!use_partials()) { ECM2_HIP(hipMemsetAsync(diag, 0, sizeof(double) * (size_t)ndofs_, s)); }
       ApplyArgs a = apply_args(nullptr, nullptr, diag, dg, 0, layout_.nblk());
       DeviceArray<double> fd, fm;
-      if (layout_.kind == QLAYOUT_TRILINEAR)
+      if (expand_needed())
       {
-         expand_trilinear(fd, fm, s);  // per-point qdata for the diagonal's tables
+         expand_compressed(fd, fm, s);  // per-point qdata for the diagonal's tables
          a.kind = QLAYOUT_BLOCKED;
          a.qdd = fd.data();
          a.qdm = fm.data();
@@ -1479,7 +1504,7 @@ void PAForm::diagonal_from_qdata(double *diag, hipStream_t s)
                   have_mass_ ? qd_mass_.data() : nullptr, diag, false, basis_, btab(), s);
 }
 
-void PAForm::expand_trilinear(DeviceArray<double> &fd, DeviceArray<double> &fm, hipStream_t s) const
+void PAForm::expand_compressed(DeviceArray<double> &fd, DeviceArray<double> &fm, hipStream_t s) const
 {
    QLayout L = layout_;
    L.kind = QLAYOUT_BLOCKED;
@@ -1492,7 +1517,11 @@ void PAForm::expand_trilinear(DeviceArray<double> &fd, DeviceArray<double> &fm, 
    }
    QPts qp = {};
    for (int q = 0; q < Q_ && q < MAX_Q1D; q++) { qp.x[q] = maps_.qpts[q]; }
-   kern::trilinear_expand(layout_, Q_, qd_diff_.data(), qd_mass_.data(), qp, fd.data(), fm.data(), s);
+   if (layout_.kind == QLAYOUT_TRILINEAR)
+   {
+      kern::trilinear_expand(layout_, Q_, qd_diff_.data(), qd_mass_.data(), qp, fd.data(), fm.data(), s);
+   }
+   else { kern::affine_expand(layout_, Q_, qd_diff_.data(), qd_mass_.data(), fd.data(), fm.data(), s); }
 }
 
 void PAForm::restriction_mult(const double *x, double *xe, hipStream_t s)
@@ -1514,9 +1543,9 @@ void PAForm::integrator_add_mult(int kind, const double *xe, double *ye, hipStre
    ApplyArgs a = apply_args(xe, nullptr, ye, nullptr, 0, layout_.nblk());
    a.gmap = gmap_.data();
    DeviceArray<double> fd, fm;
-   if (layout_.kind == QLAYOUT_TRILINEAR)
+   if (expand_needed())
    {
-      expand_trilinear(fd, fm, s);
+      expand_compressed(fd, fm, s);
       a.kind = QLAYOUT_BLOCKED;
       a.qdd = fd.data();
       a.qdm = fm.data();
@@ -1530,10 +1559,10 @@ void PAForm::get_qdata(int kind, double *out, hipStream_t s)
    ECM2_VERIFY(assembled_, ERR_STATE, "get_qdata before Assemble");
    const bool diff = kind == INTEG_DIFFUSION;
    ECM2_VERIFY(diff ? have_diff_ : have_mass_, ERR_ARG, "integrator " << kind << " not present");
-   const bool aff = layout_.affine();
    DeviceArray<double> fd, fm;
-   const bool tl = layout_.kind == QLAYOUT_TRILINEAR;
-   if (tl) { expand_trilinear(fd, fm, s); }  // decoded as BLOCKED below
+   const bool tl = expand_needed();  // TRILINEAR, or a diffusion-only AFFINE form
+   const bool aff = layout_.affine() && !tl;
+   if (tl) { expand_compressed(fd, fm, s); }  // decoded as BLOCKED below
    DeviceArray<double> &src = tl ? (diff ? fd : fm) : ((diff && !aff) ? qd_diff_ : qd_mass_);
    std::vector<double> h(src.size()), hc(aff ? qd_diff_.size() : 0);
    if (src.size())
@@ -1545,7 +1574,7 @@ void PAForm::get_qdata(int kind, double *out, hipStream_t s)
       ECM2_HIP(hipMemcpyAsync(hc.data(), qd_diff_.data(), qd_diff_.bytes(), hipMemcpyDeviceToHost, s));
    }
    ECM2_HIP(hipStreamSynchronize(s));
-   const int nc = diff ? 6 : 1;
+   const int nc = diff ? (layout_.kind == QLAYOUT_NATIVE9 ? 9 : 6) : 1;
    std::vector<int> invp;
    if (!perm_host_.empty())
    {
@@ -1558,7 +1587,7 @@ void PAForm::get_qdata(int kind, double *out, hipStream_t s)
          for (int q = 0; q < NQ_; q++)
          {
             size_t src_i;
-            if (layout_.kind == QLAYOUT_NATIVE) { src_i = ((size_t)e * nc + c) * NQ_ + q; }
+            if (layout_.kind == QLAYOUT_NATIVE || layout_.kind == QLAYOUT_NATIVE9) { src_i = ((size_t)e * nc + c) * NQ_ + q; }
             else if (layout_.kind == QLAYOUT_AFFINE_E)
             {
                const size_t pi = ((size_t)e * NQ_ + q) * 2;

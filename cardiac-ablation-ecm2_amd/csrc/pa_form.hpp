@@ -179,8 +179,13 @@ private:
    // element weights [ne] of integrator kind k: 1 / 0 per its attribute marker, all 1 unmarked
    std::vector<double> marker_weights(int k) const;
    void diagonal_from_qdata(double *diag, hipStream_t s);
-   // TRILINEAR forms: their per-point qdata in the BLOCKED layout (temporaries of the caller)
-   void expand_trilinear(DeviceArray<double> &fd, DeviceArray<double> &fm, hipStream_t s) const;
+   // TRILINEAR forms and diffusion-only AFFINE forms: their per-point qdata in the BLOCKED layout
+   // (temporaries of the caller) for the diagonal, the E-vector apply and the qdata export
+   bool expand_needed() const
+   {
+      return layout_.kind == QLAYOUT_TRILINEAR || (layout_.kind == QLAYOUT_AFFINE && layout_.pw == 1);
+   }
+   void expand_compressed(DeviceArray<double> &fd, DeviceArray<double> &fm, hipStream_t s) const;
 
  public:
    void record_start_public(hipStream_t s) { record_start(s); }

@@ -524,14 +524,17 @@ void par_group_mult_member(std::vector<ParPAForm *> &forms, const std::vector<co
    }
    // the peers' packed sends (and, RAP, their y ghost blocks) are copied as their last group Mult
    // left them: it must have run on these x arrays and on the current assembly
-   for (const Xfer &t : f.schedule(false))
+   for (int tr = 0; tr < (f.part().overlap ? 1 : 2); tr++)
    {
-      if (t.send) { continue; }
-      ParPAForm &o = *forms[t.peer];
-      const bool needs = !f.part().overlap || o.pack_needed();
-      ECM2_VERIFY(!needs || o.group_mult_current(x[t.peer]), ERR_STATE,
-                  "member " << r << ": peer " << t.peer << "'s last group Mult ran on another x or assembly "
-                            "(run a group Mult on the same x first)");
+      for (const Xfer &t : f.schedule(tr == 1))
+      {
+         if (t.send) { continue; }
+         ParPAForm &o = *forms[t.peer];
+         const bool needs = tr == 1 || o.pack_needed();  // P^T: the peer's y ghost block; P: its packed sends
+         ECM2_VERIFY(!needs || o.group_mult_current(x[t.peer]), ERR_STATE,
+                     "member " << r << ": peer " << t.peer << "'s last group Mult ran on another x or assembly "
+                               "(run a group Mult on the same x first)");
+      }
    }
    if (f.serial())
    {

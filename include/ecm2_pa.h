@@ -46,6 +46,21 @@ extern "C" {
  * like a GridFunctionCoefficient (qfunction.cpp:73-98, coefficient.cpp:2052-2070); the law
  * itself is the bioheat application's (not in the reference snapshot: parity-unpinned). */
 #define ECM2_COEFF_GRIDFUNC_PERFUSION 3
+/* Vector and matrix diffusion coefficients -- anisotropic (fibre-oriented) tissue conductivity;
+ * DiffusionIntegrator(VectorCoefficient | MatrixCoefficient), PADiffusionSetup3D coeffDim 3 / 6 / 9
+ * (fem/integ/bilininteg_diffusion_kernels.cpp:297-348), DiffusionIntegrator only.  QUAD_*: device
+ * [ne][nq][dim]; CONST_*: host data[dim].  dim 3: diag(v); 6: symmetric (11,12,13,22,23,33)
+ * (SymmetricMatrixCoefficient::ProjectSymmetric); 9: general, row-major M(i,j) at 3 i + j (the
+ * transposed projection of CoefficientVector::ProjectTranspose, coefficient.cpp:2093-2123).  These
+ * keep the full per-point layout (BLOCKED / NATIVE: 6 symmetric entries); a general matrix keeps
+ * the reference's 9-entry qdata (ECM2_QLAYOUT_NATIVE9) and runs the workgroup-per-element or
+ * unfused kernels (ECM2_ERR_UNSUPPORTED for ECM2_KERNEL_TPE / _LINE). */
+#define ECM2_COEFF_QUAD_VECTOR 4
+#define ECM2_COEFF_QUAD_SYMMATRIX 5
+#define ECM2_COEFF_QUAD_MATRIX 6
+#define ECM2_COEFF_CONST_VECTOR 7
+#define ECM2_COEFF_CONST_SYMMATRIX 8
+#define ECM2_COEFF_CONST_MATRIX 9
 
 /* Kernel selection (all produce the same operator). */
 #define ECM2_KERNEL_AUTO 0     /* TPE for p <= 2, LINE for p = 3..6                 */
@@ -160,6 +175,7 @@ int ecm2_pa_form_set_jacobians(ecm2_pa_form *f, const double *J);
  * point; the fused kernel evaluates J, adj(J) and det J at every quadrature point (the
  * reference's setup algebra, never stored): the AFFINE layout's bytes on a general mesh. */
 #define ECM2_QLAYOUT_TRILINEAR 4
+#define ECM2_QLAYOUT_NATIVE9 5   /* [e][9][nq] general D_ij (a nonsymmetric matrix coefficient)    */
 int ecm2_pa_form_set_geometry_compression(ecm2_pa_form *f, int on);
 /* BilinearForm::AddDomainIntegrator(new MassIntegrator(Q)) / DiffusionIntegrator(Q)
  * (bilinearform.cpp:231-242).  data: CONSTANT -> data[0] (host);

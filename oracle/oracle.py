@@ -49,6 +49,10 @@ def lib():
             "orc_pa_mult": (None, [i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
             "orc_fa_mult": (None, [i32, i32, i32, vp, vp, i32, vp, i32, vp, i32, vp, vp, vp]),
             "orc_pa_diagonal_e": (None, [i32, i32, i32, vp, vp, vp, vp, vp]),
+            "orc_diffusion_setup_m": (i32, [i32, i32, vp, vp, vp, i32, i32, vp]),
+            "orc_diffusion_apply_n": (None, [i32, i32, i32, vp, vp, vp, i32, vp, vp]),
+            "orc_pa_diagonal_e_n": (None, [i32, i32, i32, vp, vp, vp, vp, i32, vp]),
+            "orc_fa_mult_m": (None, [i32, i32, i32, vp, vp, i32, vp, i32, vp, i32, i32, vp, vp, vp]),
             "orc_pcg": (i32, [i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp,
                               f64, f64, i32, ctypes.POINTER(ctypes.c_double)]),
             "orc_num_threads": (i32, []),
@@ -250,12 +254,36 @@ def diffusion_apply(B, G, Dd, xe):
     return ye
 
 
+def diffusion_setup_m(J, W, coef, cdim, q1d):
+    """PADiffusionSetup3D for a vector / matrix coefficient (cdim 3, 6, 9): coef [ne][nq][cdim] or
+    the cdim constant values; returns D [ne][nD][nq], nD = 9 (general) or 6 (symmetric)."""
+    ne, nq = J.shape[0], q1d ** 3
+    c = _f64(coef)
+    const = 1 if c.size == cdim else 0
+    assert const or c.size == ne * nq * cdim
+    D = np.empty((ne, 9 if cdim == 9 else 6, nq))
+    lib().orc_diffusion_setup_m(ne, q1d, _p(_f64(W)), _p(_f64(J)), _p(c), cdim, const, _p(D))
+    return D
+
+
+def diffusion_apply_n(B, G, Dd, xe):
+    """The diffusion AddMultPA on 6- or 9-entry qdata (Dd [ne][nD][nq])."""
+    Q, D = B.shape
+    ne = xe.shape[0]
+    ye = np.zeros_like(_f64(xe))
+    lib().orc_diffusion_apply_n(ne, D, Q, _p(_f64(B.T.ravel())), _p(_f64(G.T.ravel())), _p(_f64(Dd)), Dd.shape[1],
+                                _p(_f64(xe)), _p(ye))
+    return ye
+
+
 class OracleOperator:
     """y = R^T (M_alpha + K_beta) R x on the CPU (the reference's PA path, restated).
 
-    alpha / beta: scalar, per-quadrature array [ne][nq], or None (integrator absent)."""
+    alpha / beta: scalar, per-quadrature array [ne][nq], or None (integrator absent).
+    beta_dim 3 / 6 / 9: beta is a vector / symmetric matrix (11,12,13,22,23,33) / general matrix
+    (row-major) coefficient, [ne][nq][beta_dim] or its beta_dim constant values."""
 
-    def __init__(self, enodes, gm, ndofs, order, alpha=None, beta=None, q1d=None):
+    def __init__(self, enodes, gm, ndofs, order, alpha=None, beta=None, q1d=None, beta_dim=1):
         self.enodes = _f64(enodes)
         self.gm = _i32(gm)
         self.ne = self.gm.shape[0]
@@ -268,7 +296,13 @@ class OracleOperator:
         self.X, self.J, self.detJ = X, J, detJ
         self.alpha, self.beta = alpha, beta
         self.M = mass_setup(detJ, self.W, alpha, self.q1d) if alpha is not None else None
-        self.D = diffusion_setup(J, self.W, beta, self.q1d) if beta is not None else None
+        self.beta_dim = beta_dim
+        if beta is None:
+            self.D = None
+        elif beta_dim == 1:
+            self.D = diffusion_setup(J, self.W, beta, self.q1d)
+        else:
+            self.D = diffusion_setup_m(J, self.W, beta, beta_dim, self.q1d)
         self.off, self.idx = build_csr(self.gm, self.ndofs)
         nd = self.gm.shape[1]
         self._xe = np.empty((self.ne, nd))
@@ -277,6 +311,12 @@ class OracleOperator:
         self._Gf = _f64(self.G.T.ravel())
 
     def mult(self, x):
+        if self.D is not None and self.D.shape[1] == 9:  # MultInternal with the general qdata
+            xe = restriction_mult(self.gm, x)
+            ye = diffusion_apply_n(self.B, self.G, self.D, xe)
+            if self.M is not None:
+                ye += mass_apply(self.B, self.M, xe)
+            return restriction_mult_transpose(self.off, self.idx, ye)
         y = np.empty(self.ndofs)
         lib().orc_pa_mult(self.ne, self.p, self.q1d, self.ndofs, _p(self.gm), _p(self.off), _p(self.idx),
                           _p(self._Bf), _p(self._Gf), _p(self.M), _p(self.D), _p(_f64(x)), _p(y),
@@ -308,16 +348,22 @@ class OracleOperator:
         y = np.empty(self.ndofs)
         diag = np.empty(self.ndofs) if with_diag else None
         am, amc = _coef(self.alpha, self.ne, self.q1d ** 3) if self.alpha is not None else (None, 0)
-        bd, bdc = _coef(self.beta, self.ne, self.q1d ** 3) if self.beta is not None else (None, 0)
-        lib().orc_fa_mult(self.ne, self.p, self.q1d, _p(self.enodes), _p(self.gm), self.ndofs,
-                          _p(am), amc, _p(bd), bdc, _p(_f64(x)), _p(y), _p(diag))
+        if self.beta is not None and self.beta_dim > 1:
+            bd = _f64(self.beta)
+            bdc = 1 if bd.size == self.beta_dim else 0
+        else:
+            bd, bdc = _coef(self.beta, self.ne, self.q1d ** 3) if self.beta is not None else (None, 0)
+        lib().orc_fa_mult_m(self.ne, self.p, self.q1d, _p(self.enodes), _p(self.gm), self.ndofs,
+                            _p(am), amc, _p(bd), self.beta_dim, bdc, _p(_f64(x)), _p(y), _p(diag))
         return (y, diag) if with_diag else y
 
     def diagonal(self):
         nd = self.gm.shape[1]
         de = np.zeros((self.ne, nd))
         Q = self.q1d
-        lib().orc_pa_diagonal_e(self.ne, self.p + 1, Q, _p(self._Bf), _p(self._Gf), _p(self.M), _p(self.D), _p(de))
+        nD = self.D.shape[1] if self.D is not None else 6
+        lib().orc_pa_diagonal_e_n(self.ne, self.p + 1, Q, _p(self._Bf), _p(self._Gf), _p(self.M), _p(self.D), nD,
+                                  _p(de))
         return np.bincount(self.gm.ravel(), weights=de.ravel(), minlength=self.ndofs)
 
     def diagonal_markers(self, attr, integrators):

@@ -13,3 +13,5 @@ tail -3 "$O/pytest_gpu.log"; grep -E "FAILED|ERROR" "$O/pytest_gpu.log" | head -
 [ $rc -eq 0 ] || exit $rc
 bash profiles/ab_libs.sh tlb_c4t "libecm2pa_tlold.so libecm2pa_tlA.so libecm2pa_tlB.so" --workload c4 --steps 30 --warmup 5 --variants 0 --mesh trilinear || exit $?
 bash profiles/ab_libs.sh tlb_drop "libecm2pa_tlold.so libecm2pa_tlA.so libecm2pa_tlB.so" --workload c4 --steps 30 --warmup 5 --variants 0 --mesh trilinear --numbering entity --geometry-input jacobians || exit $?
+# C5 brick kernel: in-wave stage hand-offs without workgroup barriers (brws) against the tree before it (tlA)
+bash profiles/ab_libs.sh brws_c5 "libecm2pa_tlA.so libecm2pa_brws.so" --workload c5 --steps 30 --warmup 5 --variants 0 || exit $?

@@ -108,3 +108,36 @@ for _d in (os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
     if _d not in sys.path:
         sys.path.insert(0, _d)
 load_pkg()
+
+
+def vector_coeff_function(P):
+    """vectorCoeffFunction, 3D (test_pa_coeff.cpp:58-70): [..., 3]."""
+    return np.stack([np.sin(np.pi * P[..., 1]), np.sin(2.5 * np.pi * P[..., 0]), np.sin(6.1 * np.pi * P[..., 2])], -1)
+
+
+def symmetric_matrix_coeff_function(P):
+    """symmetricMatrixCoeffFunction, 3D (test_pa_coeff.cpp:105-125): (11,12,13,22,23,33) [..., 6]."""
+    x, y, z = P[..., 0], P[..., 1], P[..., 2]
+    return np.stack([np.sin(np.pi * y), np.cos(2.5 * np.pi * x), np.sin(4.9 * np.pi * z),
+                     np.sin(6.1 * np.pi * y), np.cos(6.1 * np.pi * z), np.sin(6.1 * np.pi * z)], -1)
+
+
+def asymmetric_matrix_coeff_function(P):
+    """asymmetricMatrixCoeffFunction, 3D (test_pa_coeff.cpp:84-103): row-major M(i, j) [..., 9]."""
+    x, y, z = P[..., 0], P[..., 1], P[..., 2]
+    return np.stack([1.1 + np.sin(np.pi * y), np.cos(2.5 * np.pi * x), np.sin(4.9 * np.pi * z),
+                     np.cos(np.pi * x), 1.1 + np.sin(6.1 * np.pi * y), np.cos(6.1 * np.pi * z),
+                     np.sin(1.5 * np.pi * y), np.cos(2.9 * np.pi * x), 1.1 + np.sin(6.1 * np.pi * z)], -1)
+
+
+def anisotropic_coefficients(P, ctype, seed=0):
+    """test_pa_coeff.cpp coeffType 3..6: (values, dim) -- 3 vector function, 4 symmetric matrix
+    function, 5 asymmetric matrix function, 6 a constant random matrix with 2 added on its diagonal."""
+    if ctype == 3:
+        return vector_coeff_function(P), 3
+    if ctype == 4:
+        return symmetric_matrix_coeff_function(P), 6
+    if ctype == 5:
+        return asymmetric_matrix_coeff_function(P), 9
+    m = np.random.default_rng(seed).uniform(0, 1, (3, 3)) + 2.0 * np.eye(3)
+    return m.reshape(9), 9

@@ -359,6 +359,7 @@ def test_gpu_group_member_rows(nranks, order, schedule, decomp):
     group = E.ParGroup(forms)
     if decomp == "rap":
         # a member's RAP rows copy the peers' state of a group Mult on the same x: refused without one
+        # (member 0 owns its interface with member 1: its P^T receive copies member 1's y ghost block)
         with pytest.raises(E.ECM2Error):
             group.MultMember(0, xs, ys)
         x2 = [v.clone() for v in xs]

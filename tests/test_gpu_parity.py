@@ -129,6 +129,147 @@ def test_single_integrators_and_constants(order, integ):
     assert relerr(host(y), op.mult(x)) <= RTOL
 
 
+@pytest.mark.parametrize("ctype", [3, 4, 5, 6])
+@pytest.mark.parametrize("order", [1, 2, 3, 4])
+@pytest.mark.parametrize("mesh_name", ["nonaligned", "trilinear"])
+def test_anisotropic_diffusion_coefficients(ctype, order, mesh_name):
+    """"H1 PA Coefficient" (test_pa_coeff.cpp:129-272), coeffType 3..6 through the C ABI: vector,
+    symmetric-matrix (full per-point layout, the fused kernels), asymmetric and constant general
+    matrices (the reference's 9-entry qdata, workgroup-per-element kernel), with a MassIntegrator:
+    Mult, diagonal, E-vector AddMultPA and the reference-layout qdata against the oracle (itself
+    pinned to full assembly, test_oracle_pins.py)."""
+    from helpers import anisotropic_coefficients
+    m = make_mesh(mesh_name)
+    fes = E.H1Space(m, order)
+    en = m.element_nodes()
+    q1d = O.default_q1d(order)
+    P = O.quad_points(en, q1d)
+    beta, dim = anisotropic_coefficients(P, ctype)
+    alpha = coeff_function(P)
+    if beta.ndim == 1:  # constant
+        coef = E.MatrixCoefficient(beta.reshape(3, 3))
+    elif dim == 3:
+        coef = E.VectorCoefficient(dev(beta.reshape(fes.ne, -1, 3)))
+    elif dim == 6:
+        full = beta[..., [0, 1, 2, 1, 3, 4, 2, 4, 5]]
+        coef = E.MatrixCoefficient(dev(full.reshape(fes.ne, -1, 9)), symmetric=True)
+    else:
+        coef = E.MatrixCoefficient(dev(beta.reshape(fes.ne, -1, 9)))
+    form = E.BilinearForm(fes)
+    form.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(alpha.reshape(fes.ne, -1)))))
+    form.AddDomainIntegrator(E.DiffusionIntegrator(coef))
+    form.Assemble()
+    info = form.info()
+    if dim == 9:
+        assert info["layout"] == E.QLAYOUT_NATIVE9 and info["kernel"] == E.KERNEL_WPE
+    else:
+        assert info["layout"] == (E.QLAYOUT_BLOCKED if order <= 2 else E.QLAYOUT_NATIVE)
+    op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=alpha, beta=beta, beta_dim=dim)
+    x = np.random.default_rng(17).uniform(-1, 1, fes.ndofs)
+    y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    form.Mult(dev(x), y)
+    assert relerr(host(y), op.mult(x)) <= RTOL
+    d = torch.empty_like(y)
+    form.AssembleDiagonal(d)
+    assert relerr(host(d), op.diagonal()) < 1e-13
+    assert relerr(form.qdata(E.DIFFUSION), op.D) < 1e-13
+    xe = np.random.default_rng(18).uniform(-1, 1, (fes.ne, fes.nd))
+    ye = torch.zeros(fes.ne * fes.nd, dtype=torch.float64, device="cuda")
+    form.IntegratorAddMultPA(E.DIFFUSION, dev(xe), ye)
+    assert relerr(host(ye).reshape(fes.ne, fes.nd), O.diffusion_apply_n(op.B, op.G, op.D, xe)) <= RTOL
+    if dim == 9:
+        with pytest.raises(E.ECM2Error):  # the fused kernels read symmetric qdata only
+            f2 = E.BilinearForm(fes, kernel=E.KERNEL_TPE if order <= 2 else E.KERNEL_LINE)
+            f2.AddDomainIntegrator(E.DiffusionIntegrator(coef))
+            f2.Assemble()
+
+
+def _lattice_trilinear(n=8):
+    """n^3 Cartesian mesh (complete 4x4x4 bricks only) with moved interior vertices."""
+    m = E.Mesh.MakeCartesian3D(n, n, n)
+    V = m.vertices()
+    inner = np.all((V > 1e-9) & (V < 1.0 - 1e-9), axis=1)
+    V[inner] += 0.15 / n * np.random.default_rng(9).uniform(-1, 1, (int(inner.sum()), 3))
+    m.set_vertices(V)
+    return m
+
+
+@pytest.mark.parametrize("mesh_name", ["cart_bricks", "nonaligned", "trilinear", "lattice_tri"])
+@pytest.mark.parametrize("order", [1, 2])
+@pytest.mark.parametrize("geometry", ["nodes", "jacobians"])
+def test_diffusion_only_compressed_layouts(mesh_name, order, geometry):
+    """A form with only a DiffusionIntegrator (ex16's K, ex16p.cpp:464) keeps the compressed
+    geometry: AFFINE (C_e + W beta per point) or TRILINEAR (map coefficients + W beta / det J per
+    point), 8 B per point -- Mult, diagonal, E-vector AddMultPA and the reference-layout qdata
+    against the oracle.  A mass-only form keeps the BLOCKED mass stream (8 B per point)."""
+    m = _lattice_trilinear() if mesh_name == "lattice_tri" else make_mesh(mesh_name)
+    fes = E.H1Space(m, order)
+    en = m.element_nodes()
+    q1d = O.default_q1d(order)
+    c = coeff_function(O.quad_points(en, q1d))
+    form = E.BilinearForm(fes, geometry=geometry)
+    if geometry == "jacobians":
+        form.SetJacobians(m.jacobians(q1d))
+    form.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(dev(c.reshape(fes.ne, -1)))))
+    form.Assemble()
+    affine = mesh_name in ("cart_bricks", "nonaligned")
+    assert form.info()["layout"] == (E.QLAYOUT_AFFINE if affine else E.QLAYOUT_TRILINEAR)
+    assert form.qdata_bytes() < 20 * fes.ne * q1d ** 3  # 8 B per point + the per-element geometry
+    op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=None, beta=c)
+    x = np.random.default_rng(13).uniform(-1, 1, fes.ndofs)
+    y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    form.Mult(dev(x), y)
+    assert relerr(host(y), op.mult(x)) <= RTOL
+    d = torch.empty_like(y)
+    form.AssembleDiagonal(d)
+    assert relerr(host(d), op.diagonal()) < 1e-13
+    assert relerr(form.qdata(E.DIFFUSION), op.D) < 1e-13
+    xe = np.random.default_rng(14).uniform(-1, 1, (fes.ne, fes.nd))
+    ye = torch.zeros(fes.ne * fes.nd, dtype=torch.float64, device="cuda")
+    form.IntegratorAddMultPA(E.DIFFUSION, dev(xe), ye)
+    assert relerr(host(ye).reshape(fes.ne, fes.nd), O.diffusion_apply(op.B, op.G, op.D, xe)) <= RTOL
+    if geometry == "nodes" and mesh_name == "trilinear":
+        fm = E.BilinearForm(fes)
+        fm.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(c.reshape(fes.ne, -1)))))
+        fm.Assemble()
+        assert fm.info()["layout"] == E.QLAYOUT_BLOCKED
+        nq = fm.info()["q1d"] ** 3
+        assert fm.qdata_bytes() <= 8 * 64 * 2 * ((nq + 1) // 2) * ((fes.ne + 63) // 64)  # pairs of points
+        fm.Mult(dev(x), y)
+        assert relerr(host(y), O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=c).mult(x)) <= RTOL
+
+
+@pytest.mark.parametrize("numbering", [E.NUMBERING_STRUCTURED, E.NUMBERING_ENTITY])
+@pytest.mark.parametrize("mass", [True, False])
+def test_trilinear_lattice_kernel(numbering, mass):
+    """The two-waves-per-SIMD TRILINEAR kernel (every block a lattice brick: regular blocks with
+    the structured numbering, lattice-map blocks with the reference's) against the oracle, with
+    and without the MassIntegrator, on the distributed form's split L-vector too."""
+    m = _lattice_trilinear(8)
+    order = 2
+    fes = E.H1Space(m, order, numbering)
+    en = m.element_nodes()
+    q1d = O.default_q1d(order)
+    c = coeff_function(O.quad_points(en, q1d))
+    form = E.BilinearForm(fes, element_order="faces" if numbering == E.NUMBERING_ENTITY else "auto")
+    if mass:
+        form.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(c.reshape(fes.ne, -1)))))
+    form.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(dev(c.reshape(fes.ne, -1)))))
+    form.Assemble()
+    assert form.info()["layout"] == E.QLAYOUT_TRILINEAR
+    lat, units, _ = form.AddressingInfo()
+    lslot, _ = form.PlanInfo()
+    assert (lat if numbering == E.NUMBERING_STRUCTURED else lslot) == units == 8  # every block a brick
+    op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=c if mass else None, beta=c)
+    x = np.random.default_rng(15).uniform(-1, 1, fes.ndofs)
+    y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    form.Mult(dev(x), y)
+    assert relerr(host(y), op.mult(x)) <= RTOL
+    y2 = torch.empty_like(y)
+    form.Mult(dev(x), y2)
+    assert torch.equal(y, y2)  # deterministic
+
+
 @pytest.mark.parametrize("kernel", ["tpe", "wpe"])
 @pytest.mark.parametrize("order", [1, 2])
 def test_qdata_matches_reference_setup(kernel, order):

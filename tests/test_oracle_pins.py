@@ -240,3 +240,29 @@ def test_marker_diagonal_oracle_follows_shared_localY(order):
     d2 = op.diagonal_markers(attr, [("diffusion", [1, 0]), ("mass", None)])
     assert relerr(d2, fam + fad) < 1e-12
     assert relerr(op.diagonal_markers(attr, [("mass", None), ("diffusion", None)]), op.diagonal()) < 1e-14
+
+
+@pytest.mark.parametrize("ctype", [3, 4, 5, 6])
+@pytest.mark.parametrize("order", [1, 2, 3])
+@pytest.mark.parametrize("with_mass", [False, True])
+def test_anisotropic_coefficients_pa_equals_fa(ctype, order, with_mass):
+    """"H1 PA Coefficient" (test_pa_coeff.cpp:129-272), coeffType 3..6: a DiffusionIntegrator with a
+    vector, symmetric-matrix, asymmetric-matrix or constant matrix coefficient (PADiffusionSetup3D's
+    coeffDim 3 / 6 / 9 branches, bilininteg_diffusion_kernels.cpp:297-348), with and without a
+    MassIntegrator, on the non-aligned 2x2x2 mesh: the oracle's PA Mult equals its full assembly
+    (the reference asserts < 1e-12), and its PA diagonal the assembled diagonal."""
+    from helpers import anisotropic_coefficients
+    en, gm, nd, _ = O.cartesian_mesh(2, 2, 2, order=order, transform=nonaligned)
+    q1d = O.default_q1d(order)
+    P = O.quad_points(en, q1d)
+    beta, dim = anisotropic_coefficients(P, ctype)
+    alpha = coeff_function(P) if with_mass else None
+    op = O.OracleOperator(en, gm, nd, order, alpha=alpha, beta=beta, beta_dim=dim)
+    assert op.D.shape[1] == (9 if dim == 9 else 6)
+    x = np.random.default_rng(order).uniform(-1, 1, nd)
+    y_fa, d_fa = op.fa_mult(x, with_diag=True)
+    assert relerr(op.mult(x), y_fa) < 1e-12
+    assert relerr(op.diagonal(), d_fa) < 1e-12
+    if dim == 9 and ctype == 5:  # a nonsymmetric operator: x^T A y != y^T A x in general
+        z = np.random.default_rng(9).uniform(-1, 1, nd)
+        assert abs(z @ op.mult(x) - x @ op.mult(z)) > 1e-6 * abs(z @ op.mult(x))

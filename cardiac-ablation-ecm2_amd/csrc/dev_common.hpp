@@ -17,14 +17,6 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 
 inline unsigned grid_for(long n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
-// Order a wave's LDS writes before its subsequent LDS reads by other lanes of the SAME wave (a
-// wave's LDS instructions complete in order; this is the compiler barrier plus the wait), in place
-// of a workgroup barrier when producer and consumer lanes share a wave.
-__device__ __forceinline__ void wave_lds_sync()
-{
-   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-   __builtin_amdgcn_wave_barrier();
-}
 
 // pos: caller element -> internal position (element permutation of the blocked layout)
 __device__ __forceinline__ size_t qidx_diff(const int *pos, int kind, int nq, int e, int c, int q)

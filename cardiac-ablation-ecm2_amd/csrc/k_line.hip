@@ -614,10 +614,7 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
       for (int dx = 0; dx < D; dx++) { u += xl[dx]; }
       part[t] = u;
    }
-   // an element's x and y line stages run on the same L2S (32 or 64) lanes of one wave: the
-   // hand-off needs the wave's LDS writes ordered before its reads, not a workgroup barrier
-   static_assert(64 % L2S == 0, "an element's line lanes lie in one wave");
-   wave_lds_sync();
+   __syncthreads();
    // ---- lanes (element, qx, dz), l2 = qx + Q dz: contract in y -> sYQ [g][dz][qy][qx]
    if (act2)
    {
@@ -794,7 +791,7 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
          o[Q * DD + dy] = eo_at<D>(C2E, C2O, dy);
       }
    }
-   wave_lds_sync();  // y transpose -> x transpose: the element's lanes of one wave (as above)
+   __syncthreads();
    // this thread's lattice points of the final stage: table rows (and map entries) issued here,
    // so their latency overlaps the x transpose
    using PT = BrickPtTable<D, Q, BZ>;

@@ -171,7 +171,7 @@ __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], cons
 // products (scalar loads of the row table), x-forward, weighting by the row's 56-byte points,
 // x-transpose, yz-transpose into the element outputs.
 template <int D, int Q, bool MASS, bool DIFF, bool SPLIT>
-__global__ void __launch_bounds__(256, 1)
+__global__ void __launch_bounds__(256, 2)
 k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
                const double *__restrict__ qdd, const double *__restrict__ qdm,
                const double *__restrict__ x, const double *__restrict__ xg,
@@ -179,7 +179,7 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                const double *__restrict__ rowtab, const int *__restrict__ lane_flags,
                double *__restrict__ part)
 {
-   constexpr int ND = D * D * D, NQ = Q * Q * Q, NQH = (NQ + 1) / 2, DD = D * D;
+   constexpr int ND = D * D * D, NQ = Q * Q * Q, NQH = (NQ + 1) / 2;
    constexpr int NR = Q * Q;  // rows
    __shared__ double sX[4][ND][64];
    const int lane = threadIdx.x & 63;
@@ -196,9 +196,11 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
    const double *qd = qdd + (size_t)blk * NQ * 3 * 128 + lane * 2;
    const double *qm = qdm + (size_t)blk * NQH * 128 + lane * 2;
    auto ld2 = [&](const double *p) -> v2d { return __builtin_nontemporal_load(reinterpret_cast<const v2d *>(p)); };
-   // row buffers: diffusion pairs (3 per point) and mass values (Q per row)
-   v2d cd[Q][3], nd_[Q][3];
-   double cm[Q], nm[Q];
+   // one row buffer: diffusion pairs (3 per point) and mass values (Q per row); each point's slot
+   // is refilled with the next row's point as soon as it is read (a second buffer costs 56 VGPRs:
+   // one wave per SIMD instead of two)
+   v2d cd[Q][3];
+   double cm[Q];
    auto load_row = [&](int row, v2d (&dq)[Q][3], double (&mq)[Q]) {
 #pragma unroll
       for (int qx = 0; qx < Q; qx++)
@@ -226,26 +228,40 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 #pragma unroll 1
    for (int row = 0; row < NR; row++)
    {
-      if (row + 1 < NR) { load_row(row + 1, nd_, nm); }
-      const double *P = rowtab + (size_t)row * 3 * DD;
+      const int nrow = row + 1 < NR ? row + 1 : NR - 1;  // (the last row reloads itself: exact wait counts)
+      const int qz = row / Q, qy = row % Q;
+      // z- then y-forward per x column with the 1D tables (12 scalar doubles per row: the row table's
+      // 27 products spilled SGPRs into VGPR lanes, 58 readlanes per row)
+      double bz[D], gz[D], by[D], gy[D];
+#pragma unroll
+      for (int d = 0; d < D; d++)
+      {
+         bz[d] = b.B[qz + MQ * d]; gz[d] = b.G[qz + MQ * d];
+         by[d] = b.B[qy + MQ * d]; gy[d] = b.G[qy + MQ * d];
+      }
       double Y00[D], Y01[D], Y10[D];
 #pragma unroll
       for (int dx = 0; dx < D; dx++)
       {
          double u = 0.0, v = 0.0, wv = 0.0;
 #pragma unroll
-         for (int dz = 0; dz < D; dz++)
+         for (int dy = 0; dy < D; dy++)
+         {
+            double zb = 0.0, zg = 0.0;
 #pragma unroll
-            for (int dy = 0; dy < D; dy++)
+            for (int dz = 0; dz < D; dz++)
             {
                const double c = sX[w][(dz * D + dy) * D + dx][lane];
-               u += P[0 * DD + dz * D + dy] * c;
-               if (DIFF)
-               {
-                  v += P[1 * DD + dz * D + dy] * c;
-                  wv += P[2 * DD + dz * D + dy] * c;
-               }
+               zb += bz[dz] * c;
+               if (DIFF) { zg += gz[dz] * c; }
             }
+            u += by[dy] * zb;
+            if (DIFF)
+            {
+               v += gy[dy] * zb;
+               wv += by[dy] * zg;
+            }
+         }
          Y00[dx] = u; Y01[dx] = v; Y10[dx] = wv;
       }
       double T0[D], T1[D], T2[D];
@@ -277,6 +293,15 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
             fy = d0.y * ux + d1.y * uy + d2.x * uz;
             fz = d1.x * ux + d2.x * uy + d2.y * uz;
          }
+         {
+            const int q = nrow * Q + qx;  // the next row's point into the slot just read
+            if (DIFF)
+            {
+#pragma unroll
+               for (int k = 0; k < 3; k++) { cd[qx][k] = ld2(qd + ((size_t)q * 3 + k) * 128); }
+            }
+            if (MASS) { cm[qx] = qm[(size_t)(q >> 1) * 128 + (q & 1)]; }
+         }
 #pragma unroll
          for (int dx = 0; dx < D; dx++)
          {
@@ -293,28 +318,24 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
          }
       }
 #pragma unroll
-      for (int dz = 0; dz < D; dz++)
+      for (int dy = 0; dy < D; dy++)
 #pragma unroll
-         for (int dy = 0; dy < D; dy++)
+         for (int dx = 0; dx < D; dx++)
          {
-            const double p0 = P[0 * DD + dz * D + dy];
-            const double p1 = P[1 * DD + dz * D + dy];
-            const double p2 = P[2 * DD + dz * D + dy];
-#pragma unroll
-            for (int dx = 0; dx < D; dx++)
+            double sb = by[dy] * T0[dx], sg = 0.0;
+            if (DIFF)
             {
-               double yo = Yo[(dz * D + dy) * D + dx] + p0 * T0[dx];
-               if (DIFF) { yo += p1 * T1[dx]; yo += p2 * T2[dx]; }
+               sb += gy[dy] * T1[dx];
+               sg = by[dy] * T2[dx];
+            }
+#pragma unroll
+            for (int dz = 0; dz < D; dz++)
+            {
+               double yo = Yo[(dz * D + dy) * D + dx] + bz[dz] * sb;
+               if (DIFF) { yo += gz[dz] * sg; }
                Yo[(dz * D + dy) * D + dx] = yo;
             }
          }
-#pragma unroll
-      for (int qx = 0; qx < Q; qx++)
-      {
-#pragma unroll
-         for (int k = 0; k < 3; k++) { cd[qx][k] = nd_[qx][k]; }
-         cm[qx] = nm[qx];
-      }
    }
    tpe_assemble_store<D, SPLIT, true, false>(Yo, mp, lane_flags[(size_t)blk * 64 + lane], blk, lane, active,
                                              n_owned, y, yg, part, nullptr, w, true);

@@ -1,0 +1,42 @@
+#!/bin/bash
+# Round-4 evidence, one pass per workload, same tree, same box: rocprofv3 kernel-trace stats,
+# the FETCH_SIZE and WRITE_SIZE passes (separate: TCC slots), reduced (pmc_reduce.py) and pinned
+# with provenance (pmc_pin.py; COMMIT = the tree's commit), then the bench line that reads the pin.
+# Usage: COMMIT=<sha> bash profiles/collect_r4.sh <set: a | b | d>
+#   a: c4 (structured, affine: the headline), c4ent (the reference's numbering), c4tri (trilinear
+#      mesh: the lattice TRILINEAR kernel), c4 full per-point layout (blocked)
+#   d: c4enttrijac (the drop-in configuration: reference numbering + trilinear mesh + MFEM Jacobians)
+#   b: c5 (bricks, affine_e), c3 (fichera r6)
+set -uo pipefail
+SET=${1:-a}
+O=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/collect_r4
+mkdir -p "$O"
+export TMPDIR=/tmp PIN_DATE=$(date -u +%Y-%m-%dT%H:%MZ) PIN_SCRIPT=profiles/collect_r4.sh
+one() {  # tag layout kernel_key bench-args...
+  local tag=$1 layout=$2 key=$3; shift 3
+  local args="$* --no-cpu-baseline --full-layout 0 --variants 0"
+  local P="$O/prof_$tag"
+  mkdir -p "$P"
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -T -d "$P/trace" -o run --output-format csv \
+    -- python3 bench.py $args > "$P/bench_trace.json" 2> "$P/trace.err" || return 1
+  timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -T -d "$P/fetch" -o run --output-format csv \
+    -- python3 bench.py $args > "$P/bench_fetch.json" 2> "$P/fetch.err" || return 1
+  timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -T -d "$P/write" -o run --output-format csv \
+    -- python3 bench.py $args > "$P/bench_write.json" 2> "$P/write.err" || return 1
+  python3 profiles/pmc_reduce.py "$P" > "$P/pmc_summary.json" || return 1
+  python3 profiles/pmc_pin.py "$P" "${tag%%_*}" "$key" > "$O/pmc_${tag%%_*}_n1_${layout}.json" || return 1
+  cp "$O/pmc_${tag%%_*}_n1_${layout}.json" profiles/
+  timeout -k 10 400 python3 bench.py "$@" --variants 0 > "$O/bench_$tag.json" 2> "$O/bench_$tag.err" || return 1
+  echo "$tag: $(tail -1 "$O/bench_$tag.json" | cut -c1-160)"
+}
+if [ "$SET" = a ]; then
+  one c4 affine apply --workload c4 --steps 50 --warmup 5 || exit 1
+  one c4ent affine apply --workload c4 --numbering entity --steps 50 --warmup 5 || exit 1
+  one c4tri trilinear apply --workload c4 --mesh trilinear --steps 30 --warmup 5 || exit 1
+  one c4_full blocked apply --workload c4 --geometry full --steps 30 --warmup 5 || exit 1
+elif [ "$SET" = d ]; then
+  one c4enttrijac trilinear apply --workload c4 --numbering entity --mesh trilinear --geometry-input jacobians --steps 30 --warmup 5 || exit 1
+else
+  one c5 affine_e apply_brick --workload c5 --steps 30 --warmup 5 || exit 1
+  one c3 affine apply --workload c3 --steps 30 --warmup 5 || exit 1
+fi

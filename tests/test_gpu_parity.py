@@ -676,12 +676,17 @@ def test_affine_geometry_layout(mesh_name, order, compress):
     assert relerr(form.qdata(E.MASS)[:, 0, :], op.M) < 1e-13
 
 
-def test_affine_needs_both_integrators():
-    """Mass-only / diffusion-only forms keep the per-point layout."""
+def test_single_integrator_layouts():
+    """A mass-only form keeps the BLOCKED mass stream (already 8 B per point, W alpha det J); a
+    diffusion-only form (ex16's K) gets the compressed AFFINE layout with 8-byte points."""
     m = make_mesh("nonaligned")
-    for a, b in ((2.5, None), (None, 0.7)):
+    for a, b, want in ((2.5, None, E.QLAYOUT_BLOCKED), (None, 0.7, E.QLAYOUT_AFFINE)):
         fes, form, op = build_pair(m, 2, a, b, kernel=E.KERNEL_TPE)
-        assert form.info()["layout"] == E.QLAYOUT_BLOCKED
+        assert form.info()["layout"] == want
+        x = np.random.default_rng(2).uniform(-1, 1, fes.ndofs)
+        y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+        form.Mult(dev(x), y)
+        assert relerr(host(y), op.mult(x)) <= RTOL
 
 
 def test_affine_wpe_reads_compressed_layout():

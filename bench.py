@@ -104,7 +104,7 @@ def bioheat_coefficients(E, torch, mesh, fes, part=None):
 def qdata_layout(E, form):
     """Quadrature-data layout of a (local) form: affine | affine_e | trilinear | blocked | native."""
     return {E.QLAYOUT_NATIVE: "native", E.QLAYOUT_BLOCKED: "blocked", E.QLAYOUT_AFFINE: "affine",
-            E.QLAYOUT_AFFINE_E: "affine_e", E.QLAYOUT_TRILINEAR: "trilinear"}[form.info()["layout"]]
+            E.QLAYOUT_AFFINE_E: "affine_e", E.QLAYOUT_TRILINEAR: "trilinear", E.QLAYOUT_TRILINEAR_E: "trilinear_e"}[form.info()["layout"]]
 
 
 def min_bytes(form, ne, nd, n_true):

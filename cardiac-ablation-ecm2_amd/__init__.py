@@ -40,6 +40,7 @@ ORDER_NATIVE, ORDER_BRICK, ORDER_MORTON = 0, 1, 2
 SCATTER_PARTIALS, SCATTER_ATOMIC = 0, 1
 QLAYOUT_NATIVE, QLAYOUT_BLOCKED, QLAYOUT_AFFINE, QLAYOUT_AFFINE_E, QLAYOUT_TRILINEAR = 0, 1, 2, 3, 4  # info()['layout']
 QLAYOUT_NATIVE9 = 5  # a general matrix diffusion coefficient's 9-entry qdata
+QLAYOUT_TRILINEAR_E = 6  # TRILINEAR for the p >= 3 line / brick kernels
 DECOMP_RAP, DECOMP_OVERLAP = 0, 1  # Partition decomposition
 _SCATTER = {"partials": SCATTER_PARTIALS, "atomic": SCATTER_ATOMIC}
 

@@ -85,6 +85,49 @@ __device__ __forceinline__ double qd_mass_at(const double *qdm, const int *pos, 
 
 __device__ __forceinline__ int dof_of(int g) { return g >= 0 ? g : -1 - g; }
 
+// adj(J) of a 3x3 Jacobian (rows A_i = (A_i1, A_i2, A_i3)): PADiffusionSetup3D's
+// adjugate (bilininteg_diffusion_kernels.cpp:349-360), so D = (W beta / det J) A A^T.
+__device__ __forceinline__ void adj3(const double (&J)[3][3], double (&A)[3][3])
+{
+   A[0][0] = J[1][1] * J[2][2] - J[1][2] * J[2][1];
+   A[0][1] = J[2][1] * J[0][2] - J[0][1] * J[2][2];
+   A[0][2] = J[0][1] * J[1][2] - J[1][1] * J[0][2];
+   A[1][0] = J[2][0] * J[1][2] - J[1][0] * J[2][2];
+   A[1][1] = J[0][0] * J[2][2] - J[0][2] * J[2][0];
+   A[1][2] = J[1][0] * J[0][2] - J[0][0] * J[1][2];
+   A[2][0] = J[1][0] * J[2][1] - J[2][0] * J[1][1];
+   A[2][1] = J[2][0] * J[0][1] - J[0][0] * J[2][1];
+   A[2][2] = J[0][0] * J[1][1] - J[0][1] * J[1][0];
+}
+
+// The trilinear map's Jacobian at (xi, eta, zeta) from its coefficients c[3 (k - 1) + i] = c_k of
+// coordinate i (kernels.hpp TRILINEAR): J[i][0] = c1 + c4 eta + c5 zeta + c7 eta zeta, J[i][1] =
+// c2 + c4 xi + c6 zeta + c7 xi zeta, J[i][2] = c3 + c5 xi + c6 eta + c7 xi eta.
+__device__ __forceinline__ void trilinear_jacobian(const double *c, double xi, double et, double zt,
+                                                   double (&J)[3][3])
+{
+#pragma unroll
+   for (int i = 0; i < 3; i++)
+   {
+      J[i][0] = (c[i] + c[12 + i] * zt) + (c[9 + i] + c[18 + i] * zt) * et;
+      J[i][1] = (c[3 + i] + c[15 + i] * zt) + (c[9 + i] + c[18 + i] * zt) * xi;
+      J[i][2] = (c[6 + i] + c[15 + i] * et) + (c[12 + i] + c[18 + i] * et) * xi;
+   }
+}
+
+// The six symmetric entries (11, 12, 13, 22, 23, 33) of D = sc A A^T, A = adj(J).
+__device__ __forceinline__ void trilinear_dmat(const double (&J)[3][3], double sc, double (&d)[6])
+{
+   double A[3][3];
+   adj3(J, A);
+   d[0] = sc * (A[0][0] * A[0][0] + A[0][1] * A[0][1] + A[0][2] * A[0][2]);
+   d[1] = sc * (A[0][0] * A[1][0] + A[0][1] * A[1][1] + A[0][2] * A[1][2]);
+   d[2] = sc * (A[0][0] * A[2][0] + A[0][1] * A[2][1] + A[0][2] * A[2][2]);
+   d[3] = sc * (A[1][0] * A[1][0] + A[1][1] * A[1][1] + A[1][2] * A[1][2]);
+   d[4] = sc * (A[1][0] * A[2][0] + A[1][1] * A[2][1] + A[1][2] * A[2][2]);
+   d[5] = sc * (A[2][0] * A[2][0] + A[2][1] * A[2][1] + A[2][2] * A[2][2]);
+}
+
 // Encoded (fused-kernel) map entries: bits 0-29 dof, bit 30 "shared" (the dof is held by
 // more than one entry of the whole mesh after the kernel's own face assembly -> partial slot
 // or atomic add), bit 31 orientation sign.

@@ -19,24 +19,42 @@ namespace
 {
 using namespace dev;
 
-template <int D, int Q, bool MASS, bool DIFF, bool AFF>
+// G: the qdata layout -- 0 the reference's native [e][6][NQ] / [e][NQ]; 1 AFFINE_E (per-element C
+// and the point values (W beta, W alpha det J), or W beta alone without MASS); 2 TRILINEAR_E (the
+// element's trilinear-map coefficients and the point values (W beta / det J, W alpha det J): D at
+// the lane's points from J, as PADiffusionSetup3D, bilininteg_diffusion_kernels.cpp:349-362)
+template <int D, int Q, bool MASS, bool DIFF, int G>
 __device__ __forceinline__ void line_load_qdata(double (&qv)[7][Q], int e, int t,
                                                 const double *__restrict__ qdd,
-                                                const double *__restrict__ qdm)
+                                                const double *__restrict__ qdm, const QPts &qp)
 {
    constexpr int NQ = Q * Q * Q, QQ = Q * Q;
-   if (AFF && t < QQ)
+   static_assert(G == 0 || DIFF, "compressed layouts carry the diffusion integrator");
+   if (G != 0 && t < QQ)
    {
-      // AFFINE_E: D_c = (W beta)(q) C_c, mass = (W alpha det J)(q); 16-byte pair per point
-      double c[6];
+      double c[G == 1 ? 6 : 21];
 #pragma unroll
-      for (int k = 0; k < 6; k++) { c[k] = qdd[(size_t)e * 6 + k]; }
+      for (int k = 0; k < (G == 1 ? 6 : 21); k++) { c[k] = qdd[(size_t)e * (G == 1 ? 6 : 21) + k]; }
 #pragma unroll
       for (int qz = 0; qz < Q; qz++)
       {
-         const v2d p = reinterpret_cast<const v2d *>(qdm)[(size_t)e * NQ + qz * QQ + t];
+         const size_t eq = (size_t)e * NQ + qz * QQ + t;
+         v2d p;
+         if (MASS) { p = reinterpret_cast<const v2d *>(qdm)[eq]; }
+         else { p = v2d{qdm[eq], 0.0}; }
+         if (G == 1)
+         {
 #pragma unroll
-         for (int k = 0; k < 6; k++) { qv[k][qz] = p.x * c[k]; }
+            for (int k = 0; k < 6; k++) { qv[k][qz] = p.x * c[k]; }
+         }
+         else
+         {
+            double J[3][3], d[6];
+            trilinear_jacobian(c, qp.x[t % Q], qp.x[t / Q], qp.x[qz], J);
+            trilinear_dmat(J, p.x, d);
+#pragma unroll
+            for (int k = 0; k < 6; k++) { qv[k][qz] = d[k]; }
+         }
          qv[6][qz] = p.y;
       }
       return;
@@ -70,13 +88,13 @@ __device__ __forceinline__ void line_load_qdata(double (&qv)[7][Q], int e, int t
 // partial slot part[e][a] (or, without partials, an atomic add); n_owned: dofs >= n_owned
 // live in the ghost vectors xg / yg (distributed form; n_owned = ndofs otherwise).
 // --------------------------------------------------------------------------
-template <int D, int Q, bool MASS, bool DIFF, bool AFF>
+template <int D, int Q, bool MASS, bool DIFF, int G>
 __global__ void __launch_bounds__(64)
 k_apply_line(int c_begin, int c_end, const int *__restrict__ lelem, int n_owned, const int *__restrict__ gmap,
              const double *__restrict__ qdd, const double *__restrict__ qdm,
              const double *__restrict__ x, const double *__restrict__ xg,
              double *__restrict__ y, double *__restrict__ yg, const Basis1D *__restrict__ btab,
-             double *__restrict__ part)
+             double *__restrict__ part, const QPts qp)
 {
    constexpr int ND = D * D * D, DD = D * D, QQ = Q * Q, DQ = D * Q;
    constexpr int SA = (2 * DD * Q > 3 * D * QQ) ? 2 * DD * Q : 3 * D * QQ;
@@ -90,7 +108,7 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ lelem, int n_owned,
    const int e = lelem[c];
 
    double qv[7][Q];
-   line_load_qdata<D, Q, MASS, DIFF, AFF>(qv, e, t, qdd, qdm);
+   line_load_qdata<D, Q, MASS, DIFF, G>(qv, e, t, qdd, qdm, qp);
    // ---- lanes (dy, dz): gather the x-line, contract in x
    int gl[D];
    if (t < DD)
@@ -284,7 +302,9 @@ k_apply_line(int c_begin, int c_end, const int *__restrict__ lelem, int n_owned,
 // the brick surface that other holders share goes to its partial slot
 // part[brick][surface index] (face-grouped, brick_surface_index) for k_sum_partials
 // (deterministic, no atomics).  Workgroups take bricks in XCD-contiguous order.
-// AFF: AFFINE_E qdata (per-element C + one (W beta, W alpha det J) pair per point).
+// G: 0 native qdata, 1 AFFINE_E (per-element C + one (W beta, W alpha det J) pair per point),
+// 2 TRILINEAR_E (the element's trilinear-map coefficients + one (W beta / det J, W alpha det J)
+// pair per point; the z stage evaluates J, adj(J) at its points).
 // --------------------------------------------------------------------------
 // Brick kernel layout and addressing (round 2; profiles/r2_ab_brick.txt: -8..-9% vs the
 // round-1 form at C5):
@@ -508,14 +528,15 @@ struct BrickPtTable
 template <int D, int Q, int BZ>
 __device__ const BrickPtTable<D, Q, BZ> kBrickPts = BrickPtTable<D, Q, BZ>();
 
-template <int D, int Q, int BZ, bool SPLIT, bool AFF, bool REG>
+template <int D, int Q, int BZ, bool SPLIT, int G, bool REG>
 __global__ void __launch_bounds__((BrickShapeC<D, Q, BZ>::NT), (BrickShapeC<D, Q, BZ>::WPE))
 k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int *__restrict__ bmap,
                 const int *__restrict__ breg, int n_owned, const double *__restrict__ qdd,
                 const double *__restrict__ qdm, const double *__restrict__ x, const double *__restrict__ xg,
                 double *__restrict__ y, double *__restrict__ yg, const Basis1D *__restrict__ btab,
-                double *__restrict__ part)
+                double *__restrict__ part, const QPts qp)
 {
+   constexpr bool AFF = G != 0;  // a compressed layout: point pairs + per-element data
    using S = BrickShapeC<D, Q, BZ>;
    constexpr int NE = S::NE, DD = S::DD, QQ = S::QQ, DQ = S::DQ, SA = S::SA, SB = S::SB, DS = S::DS;
    constexpr int LX = S::LX, LY = S::LY, NB = S::NB, L2S = S::L2S, S3 = S::S3, NQ = Q * Q * Q;
@@ -587,9 +608,9 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
          pa[qz] = __builtin_nontemporal_load(reinterpret_cast<const v2d *>(qdm) + (size_t)e * NQ + qz * QQ + l3c);
       }
 #pragma unroll
-      for (int c = 0; c < 6; c++) { cc[c] = qdd[(size_t)e * 6 + c]; }
+      for (int c = 0; c < (G == 1 ? 6 : 0); c++) { cc[c] = qdd[(size_t)e * 6 + c]; }
    }
-   else { line_load_qdata<D, Q, true, true, false>(qv, e, l3c, qdd, qdm); }
+   else { line_load_qdata<D, Q, true, true, 0>(qv, e, l3c, qdd, qdm, qp); }
 
    // ---- lanes (element, dy, dz): contract in x -> sXL [f][qx][l]
    if (actL)
@@ -656,10 +677,52 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
          l1[dz] = lds_read(io + D * DS + dz * DS);
          l2[dz] = lds_read(io + 2 * D * DS + dz * DS);
       }
+      // TRILINEAR_E: the column's Jacobian pieces, J[i][0] = a0 + b0 zeta, J[i][1] = a1 + b1 zeta,
+      // J[i][2] = j2 (dev_common.hpp trilinear_jacobian at xi = x_qx, eta = x_qy)
+      double a0[3], b0[3], a1[3], b1[3], j2[3];
+      if (G == 2)
+      {
+         // the coefficients are read here (L2: the brick's four elements share 672 B), not with the
+         // point pairs at entry, where 42 more live registers through stages 1-2 spill
+         const double xi = qp.x[l3 % Q], et = qp.x[l3 / Q];
+         const double *c = qdd + (size_t)e * 21;
+#pragma unroll
+         for (int i = 0; i < 3; i++)
+         {
+            a0[i] = c[i] + c[9 + i] * et;
+            b0[i] = c[12 + i] + c[18 + i] * et;
+            a1[i] = c[3 + i] + c[9 + i] * xi;
+            b1[i] = c[15 + i] + c[18 + i] * xi;
+            j2[i] = (c[6 + i] + c[12 + i] * xi) + b1[i] * et;
+         }
+      }
       // the quadrature-point operator: (f, m) = (W beta C grad u, W alpha det J u) at qz
       auto qpoint = [&](int qz, double gx, double gy, double gz, double u, double &fx, double &fy, double &fz,
                         double &m) {
-         if (AFF)
+         if (G == 2)
+         {
+            // f = (W beta / det J) adj(J) (adj(J)^T g), adj(J) from J at (x_qx, x_qy, x_qz)
+            const double zt = qp.x[qz];
+            double J[3][3], A[3][3];
+#pragma unroll
+            for (int i = 0; i < 3; i++)
+            {
+               J[i][0] = a0[i] + b0[i] * zt;
+               J[i][1] = a1[i] + b1[i] * zt;
+               J[i][2] = j2[i];
+            }
+            adj3(J, A);
+            const double sc = pa[qz].x;
+            double t0 = A[0][0] * gx, t1 = A[0][1] * gx, t2 = A[0][2] * gx;
+            t0 += A[1][0] * gy; t1 += A[1][1] * gy; t2 += A[1][2] * gy;
+            t0 += A[2][0] * gz; t1 += A[2][1] * gz; t2 += A[2][2] * gz;
+            t0 *= sc; t1 *= sc; t2 *= sc;
+            fx = A[0][0] * t0; fx += A[0][1] * t1; fx += A[0][2] * t2;
+            fy = A[1][0] * t0; fy += A[1][1] * t1; fy += A[1][2] * t2;
+            fz = A[2][0] * t0; fz += A[2][1] * t1; fz += A[2][2] * t2;
+            m = pa[qz].y * u;
+         }
+         else if (AFF)
          {
             const double wb = pa[qz].x;
             fx = wb * (cc[0] * gx + cc[1] * gy + cc[2] * gz);
@@ -949,16 +1012,21 @@ void launch_line_mdq(const ApplyArgs &a, hipStream_t s)
    const int c0 = a.lelem_off[a.blk_begin], c1 = a.lelem_off[a.blk_end];
    if (c1 <= c0) { return; }
    const dim3 grid(c1 - c0), block(64);
-#define ECM2_LINE(AF)                                                                                     \
-   hipLaunchKernelGGL((k_apply_line<D, Q, MASS, DIFF, AF>), grid, block, 0, s, c0, c1, a.lelem, a.n_owned,   \
-                      a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, a.btab, a.part)
-   if (a.kind == QLAYOUT_AFFINE_E)
+#define ECM2_LINE(GG)                                                                                     \
+   hipLaunchKernelGGL((k_apply_line<D, Q, MASS, DIFF, GG>), grid, block, 0, s, c0, c1, a.lelem, a.n_owned,   \
+                      a.gmap, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, a.btab, a.part, a.qp)
+   if (a.kind == QLAYOUT_AFFINE_E || a.kind == QLAYOUT_TRILINEAR_E)
    {
-      if constexpr (MASS && DIFF) { ECM2_LINE(true); }
-      else { ECM2_VERIFY(false, ERR_INTERNAL, "AFFINE qdata needs both integrators"); }
+      if constexpr (DIFF)
+      {
+         ECM2_VERIFY(a.pw == (MASS ? 2 : 1), ERR_INTERNAL, "compressed point values do not match the integrators");
+         if (a.kind == QLAYOUT_AFFINE_E) { ECM2_LINE(1); }
+         else { ECM2_LINE(2); }
+      }
+      else { ECM2_VERIFY(false, ERR_INTERNAL, "compressed qdata needs the diffusion integrator"); }
       return;
    }
-   ECM2_LINE(false);
+   ECM2_LINE(0);
 #undef ECM2_LINE
 }
 
@@ -977,14 +1045,21 @@ void launch_brick(const ApplyArgs &a, hipStream_t s)
    const int k0 = a.brick_off[a.blk_begin], k1 = a.brick_off[a.blk_end];
    if (k1 <= k0) { return; }
    ECM2_VERIFY(a.part_brick, ERR_INTERNAL, "brick kernel needs its partial slots");
-   const bool split = a.xg || a.yg, aff = a.kind == QLAYOUT_AFFINE_E;
+   const bool split = a.xg || a.yg;
+   const int g = a.kind == QLAYOUT_AFFINE_E ? 1 : a.kind == QLAYOUT_TRILINEAR_E ? 2 : 0;
+   ECM2_VERIFY(g == 0 || a.pw == 2, ERR_INTERNAL, "bricks need both integrators");
    const dim3 grid(k1 - k0), block(BrickShapeC<D, Q, BZ>::NT);
-#define ECM2_BRICK(SP, AF, RG)                                                                             \
-   hipLaunchKernelGGL((k_apply_brick_c<D, Q, BZ, SP, AF, RG>), grid, block, 0, s, k0, k1, a.belem, a.bmap,    \
-                      a.breg, a.n_owned, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, a.btab, a.part_brick)
-   if (split) { if (aff) { ECM2_BRICK(true, true, false); } else { ECM2_BRICK(true, false, false); } }
-   else if (a.breg) { if (aff) { ECM2_BRICK(false, true, true); } else { ECM2_BRICK(false, false, true); } }
-   else { if (aff) { ECM2_BRICK(false, true, false); } else { ECM2_BRICK(false, false, false); } }
+#define ECM2_BRICK(SP, GG, RG)                                                                             \
+   hipLaunchKernelGGL((k_apply_brick_c<D, Q, BZ, SP, GG, RG>), grid, block, 0, s, k0, k1, a.belem, a.bmap,    \
+                      a.breg, a.n_owned, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, a.btab, a.part_brick, a.qp)
+#define ECM2_BRICK_G(SP, RG)                    \
+   if (g == 1) { ECM2_BRICK(SP, 1, RG); }       \
+   else if (g == 2) { ECM2_BRICK(SP, 2, RG); }  \
+   else { ECM2_BRICK(SP, 0, RG); }
+   if (split) { ECM2_BRICK_G(true, false) }
+   else if (a.breg) { ECM2_BRICK_G(false, true) }
+   else { ECM2_BRICK_G(false, false) }
+#undef ECM2_BRICK_G
 #undef ECM2_BRICK
 }
 

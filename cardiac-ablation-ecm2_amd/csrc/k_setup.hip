@@ -7,6 +7,8 @@
 // coefficient.cpp:2052-2070, qfunction.cpp:73-98) composed with the bioheat temperature laws.
 #include "dev_common.hpp"
 
+#include <type_traits>
+
 namespace ecm2
 {
 namespace
@@ -406,6 +408,7 @@ k_setup_affine(const int *__restrict__ perm, int ne, const double *__restrict__ 
    pr.y = pw == 2 ? w * coef_at(cm, eq, e) * detJ : 0.0;
    if (BLOCKED && pw == 1) { qd_pair[((size_t)blk * NQ + q) * 64 + lane] = pr.x; }  // diffusion-only form
    else if (BLOCKED) { reinterpret_cast<v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane] = pr; }
+   else if (pw == 1) { qd_pair[(size_t)e * NQ + q] = pr.x; }
    else { reinterpret_cast<v2d *>(qd_pair)[(size_t)e * NQ + q] = pr; }
    if (q == 0)
    {
@@ -449,7 +452,9 @@ k_setup_affine(const int *__restrict__ perm, int ne, const double *__restrict__ 
 // corners X_a (a = ax + 2 ay + 4 az): c1 = X1 - X0, c2 = X2 - X0, c3 = X4 - X0,
 // c4 = X3 - X2 - X1 + X0, c5 = X5 - X4 - X1 + X0, c6 = X6 - X4 - X2 + X0,
 // c7 = X7 - X6 - X5 - X3 + X4 + X2 + X1 - X0.
-template <int Q>
+// BLOCKED = false: TRILINEAR_E (p >= 3 line / brick kernels), threads over (e, q), the
+// coefficients [e][21] and the point values [e][q][pw].
+template <int Q, bool BLOCKED>
 __global__ void __launch_bounds__(256)
 k_setup_trilinear(const int *__restrict__ perm, int ne, const double *__restrict__ enodes,
                   const double *__restrict__ cfit, const double *__restrict__ W, const QPts qp, SetupCoef cm,
@@ -457,13 +462,24 @@ k_setup_trilinear(const int *__restrict__ perm, int ne, const double *__restrict
 {
    constexpr int NQ = Q * Q * Q;
    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-   const int lane = (int)(t & 63);
-   const long rest = t >> 6;
-   const int q = (int)(rest % NQ);
-   const long blk = rest / NQ;
-   const int ipos = (int)(blk * 64 + lane);
-   if (ipos >= ne) { return; }
-   const int e = perm ? perm[ipos] : ipos;
+   int lane = 0, q, e;
+   long blk = 0;
+   if (BLOCKED)
+   {
+      lane = (int)(t & 63);
+      const long rest = t >> 6;
+      q = (int)(rest % NQ);
+      blk = rest / NQ;
+      const int ipos = (int)(blk * 64 + lane);
+      if (ipos >= ne) { return; }
+      e = perm ? perm[ipos] : ipos;
+   }
+   else
+   {
+      if (t >= (long)ne * NQ) { return; }
+      e = (int)(t / NQ);
+      q = (int)(t % NQ);
+   }
    double c[2 * kTrilinPairs];
    if (cfit)  // fitted from MFEM-layout Jacobians (k_jac_trilinear_fit)
    {
@@ -502,6 +518,15 @@ k_setup_trilinear(const int *__restrict__ perm, int ne, const double *__restrict
    v2d pr;
    pr.x = w * coef_at(cd, eq, e) / det;
    pr.y = pw == 2 ? w * coef_at(cm, eq, e) * det : 0.0;
+   if (!BLOCKED)
+   {
+      if (pw == 1) { qd_pair[eq] = pr.x; }
+      else { reinterpret_cast<v2d *>(qd_pair)[eq] = pr; }
+      if (q != 0) { return; }
+#pragma unroll
+      for (int k = 0; k < 21; k++) { qd_geo[(size_t)e * 21 + k] = c[k]; }
+      return;
+   }
    if (pw == 1) { qd_pair[((size_t)blk * NQ + q) * 64 + lane] = pr.x; }  // diffusion-only form
    else { reinterpret_cast<v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane] = pr; }
    if (q != 0) { return; }
@@ -577,22 +602,36 @@ __global__ void k_jac_trilinear_check(int ne, const double *__restrict__ Jg, con
 
 // TRILINEAR -> BLOCKED: the full per-point qdata of a TRILINEAR form (for the diagonal, the
 // E-vector apply and the qdata export; the apply kernel evaluates the same algebra on the fly).
-template <int Q>
+// BLOCKED = false: TRILINEAR_E -> NATIVE ([e][6][NQ], [e][NQ]).
+template <int Q, bool BLOCKED>
 __global__ void __launch_bounds__(256)
 k_trilinear_expand(int ne, const double *__restrict__ qd_geo, const double *__restrict__ qd_pair, const QPts qp,
                    int pw, double *__restrict__ qd_diff, double *__restrict__ qd_mass)
 {
    constexpr int NQ = Q * Q * Q;
    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-   const int lane = (int)(t & 63);
-   const long rest = t >> 6;
-   const int q = (int)(rest % NQ);
-   const long blk = rest / NQ;
-   if (blk * 64 + lane >= ne) { return; }
-   const double *cg = qd_geo + (size_t)blk * kTrilinPairs * 128 + lane * 2;
+   int lane = 0, q, e = 0;
+   long blk = 0;
    double c[2 * kTrilinPairs];
+   if (BLOCKED)
+   {
+      lane = (int)(t & 63);
+      const long rest = t >> 6;
+      q = (int)(rest % NQ);
+      blk = rest / NQ;
+      if (blk * 64 + lane >= ne) { return; }
+      const double *cg = qd_geo + (size_t)blk * kTrilinPairs * 128 + lane * 2;
 #pragma unroll
-   for (int k = 0; k < kTrilinPairs; k++) { c[2 * k] = cg[k * 128]; c[2 * k + 1] = cg[k * 128 + 1]; }
+      for (int k = 0; k < kTrilinPairs; k++) { c[2 * k] = cg[k * 128]; c[2 * k + 1] = cg[k * 128 + 1]; }
+   }
+   else
+   {
+      if (t >= (long)ne * NQ) { return; }
+      e = (int)(t / NQ);
+      q = (int)(t % NQ);
+#pragma unroll
+      for (int k = 0; k < 21; k++) { c[k] = qd_geo[(size_t)e * 21 + k]; }
+   }
    auto cf = [&](int k, int i) { return c[3 * k + i]; };
    const double xi = qp.x[q % Q], et = qp.x[(q / Q) % Q], zt = qp.x[q / (Q * Q)];
    double J[3][3];
@@ -609,8 +648,17 @@ k_trilinear_expand(int ne, const double *__restrict__ qd_geo, const double *__re
                 A23 = J[1][0] * J[0][2] - J[0][0] * J[1][2];
    const double A31 = J[1][0] * J[2][1] - J[2][0] * J[1][1], A32 = J[2][0] * J[0][1] - J[0][0] * J[2][1],
                 A33 = J[0][0] * J[1][1] - J[0][1] * J[1][0];
-   const v2d pr = pw == 2 ? reinterpret_cast<const v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane]
-                          : v2d{qd_pair[((size_t)blk * NQ + q) * 64 + lane], 0.0};
+   v2d pr;
+   if (BLOCKED)
+   {
+      pr = pw == 2 ? reinterpret_cast<const v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane]
+                   : v2d{qd_pair[((size_t)blk * NQ + q) * 64 + lane], 0.0};
+   }
+   else
+   {
+      const size_t eq = (size_t)e * NQ + q;
+      pr = pw == 2 ? reinterpret_cast<const v2d *>(qd_pair)[eq] : v2d{qd_pair[eq], 0.0};
+   }
    const double sc = pr.x;  // W beta / det J
    v2d p0, p1, p2;
    p0.x = sc * (A11 * A11 + A12 * A12 + A13 * A13);
@@ -619,6 +667,13 @@ k_trilinear_expand(int ne, const double *__restrict__ qd_geo, const double *__re
    p1.y = sc * (A21 * A21 + A22 * A22 + A23 * A23);
    p2.x = sc * (A21 * A31 + A22 * A32 + A23 * A33);
    p2.y = sc * (A31 * A31 + A32 * A32 + A33 * A33);
+   if (!BLOCKED)
+   {
+      double *d = qd_diff + (size_t)e * 6 * NQ + q;  // (11, 12, 13, 22, 23, 33)
+      d[0] = p0.x; d[NQ] = p0.y; d[2 * NQ] = p1.x; d[3 * NQ] = p1.y; d[4 * NQ] = p2.x; d[5 * NQ] = p2.y;
+      if (pw == 2) { qd_mass[(size_t)e * NQ + q] = pr.y; }
+      return;
+   }
    v2d *dst = reinterpret_cast<v2d *>(qd_diff + ((size_t)blk * NQ + q) * 3 * 128) + lane;
    dst[0] = p0;
    dst[64] = p1;
@@ -628,13 +683,25 @@ k_trilinear_expand(int ne, const double *__restrict__ qd_geo, const double *__re
 
 // AFFINE (p <= 2) -> BLOCKED: D(q) = (W beta)_q C_e and the mass value (W alpha det J)_q, for the
 // diagonal, the E-vector apply and the qdata export of a diffusion-only AFFINE form (pw = 1).
-template <int Q>
+// BLOCKED = false: AFFINE_E -> NATIVE ([e][6][NQ], [e][NQ]).
+template <int Q, bool BLOCKED>
 __global__ void __launch_bounds__(256)
 k_affine_expand(int ne, const double *__restrict__ qd_fac, const double *__restrict__ qd_pair, int pw,
                 double *__restrict__ qd_diff, double *__restrict__ qd_mass)
 {
    constexpr int NQ = Q * Q * Q;
    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   if (!BLOCKED)
+   {
+      if (t >= (long)ne * NQ) { return; }
+      const int e = (int)(t / NQ), q = (int)(t % NQ);
+      const size_t eq = (size_t)e * NQ + q;
+      const v2d pr = pw == 2 ? reinterpret_cast<const v2d *>(qd_pair)[eq] : v2d{qd_pair[eq], 0.0};
+#pragma unroll
+      for (int k = 0; k < 6; k++) { qd_diff[((size_t)e * 6 + k) * NQ + q] = pr.x * qd_fac[(size_t)e * 6 + k]; }
+      if (pw == 2) { qd_mass[eq] = pr.y; }
+      return;
+   }
    const int lane = (int)(t & 63);
    const long rest = t >> 6;
    const int q = (int)(rest % NQ);
@@ -750,17 +817,18 @@ bool jacobians_trilinear_fit(int ne, int Q, const QPts &qp, const double *J, dou
    flag.resize(1);
    ECM2_HIP(hipMemsetAsync(flag.data(), 0, sizeof(int), s));
    const long n = (long)ne * Q * Q * Q;
+   bool done = false;
 #define ECM2_FIT(QQ)                                                                                           \
    if (Q == QQ)                                                                                                \
    {                                                                                                           \
       hipLaunchKernelGGL((k_jac_trilinear_fit<QQ>), dim3(grid_for(ne, 256)), dim3(256), 0, s, ne, J, qp, cfit);   \
       hipLaunchKernelGGL((k_jac_trilinear_check<QQ>), dim3(grid_for(n, 256)), dim3(256), 0, s, ne, J, qp, cfit,   \
                          flag.data());                                                                        \
+      done = true;                                                                                             \
    }
-   ECM2_FIT(3)
-   else ECM2_FIT(4)
-   else { return false; }
+   ECM2_FIT(2) ECM2_FIT(3) ECM2_FIT(4) ECM2_FIT(5) ECM2_FIT(6) ECM2_FIT(7) ECM2_FIT(8)
 #undef ECM2_FIT
+   if (!done) { return false; }
    ECM2_HIP(hipGetLastError());
    int h = 1;
    ECM2_HIP(hipMemcpyAsync(&h, flag.data(), sizeof(int), hipMemcpyDeviceToHost, s));
@@ -768,74 +836,75 @@ bool jacobians_trilinear_fit(int ne, int Q, const QPts &qp, const double *J, dou
    return h == 0;
 }
 
+// the launches of a (Q, BLOCKED) kernel family over n threads; BLOCKED: the p <= 2 layouts
+#define ECM2_Q_BLOCKED_CASES(KERNEL, n, blocked, ...)                                                      \
+   {                                                                                                       \
+      bool done_ = false;                                                                                  \
+      auto launch_ = [&](auto qc) {                                                                        \
+         constexpr int QQ = decltype(qc)::value;                                                           \
+         if (blocked)                                                                                      \
+         {                                                                                                 \
+            hipLaunchKernelGGL((KERNEL<QQ, true>), dim3(grid_for(n, 256)), dim3(256), 0, s, __VA_ARGS__);  \
+         }                                                                                                 \
+         else { hipLaunchKernelGGL((KERNEL<QQ, false>), dim3(grid_for(n, 256)), dim3(256), 0, s, __VA_ARGS__); } \
+         done_ = true;                                                                                     \
+      };                                                                                                   \
+      switch (Q)                                                                                           \
+      {                                                                                                    \
+      case 2: launch_(std::integral_constant<int, 2>()); break;                                            \
+      case 3: launch_(std::integral_constant<int, 3>()); break;                                            \
+      case 4: launch_(std::integral_constant<int, 4>()); break;                                            \
+      case 5: launch_(std::integral_constant<int, 5>()); break;                                            \
+      case 6: launch_(std::integral_constant<int, 6>()); break;                                            \
+      case 7: launch_(std::integral_constant<int, 7>()); break;                                            \
+      case 8: launch_(std::integral_constant<int, 8>()); break;                                            \
+      default: break;                                                                                      \
+      }                                                                                                    \
+      ECM2_VERIFY(done_, ERR_UNSUPPORTED, #KERNEL ": Q1D " << Q << " not instantiated");                  \
+      ECM2_HIP(hipGetLastError());                                                                         \
+   }
+
 void setup_trilinear(const QLayout &L, int Q, const double *enodes, const double *cfit, const double *W,
                      const QPts &qp, const CoeffDesc *cm, const CoeffDesc *cd, const double *cm_q, const double *cd_q,
                      double *qd_geo, double *qd_pair, hipStream_t s)
 {
    if (L.ne == 0) { return; }
-   ECM2_VERIFY(L.kind == QLAYOUT_TRILINEAR && (cm || L.pw == 1) && cd && (enodes || cfit), ERR_INTERNAL,
-               "trilinear setup needs a TRILINEAR layout, the coefficients and the corners or fitted maps");
+   ECM2_VERIFY((L.kind == QLAYOUT_TRILINEAR || L.kind == QLAYOUT_TRILINEAR_E) && (cm || L.pw == 1) && cd &&
+                  (enodes || cfit),
+               ERR_INTERNAL, "trilinear setup needs a TRILINEAR layout, the coefficients and the corners or fitted maps");
    ECM2_VERIFY(!L.pos || L.perm, ERR_INTERNAL, "blocked setup needs the inverse permutation");
    const SetupCoef scm = make_setup_coef(cm, cm_q), scd = make_setup_coef(cd, cd_q);
-   const long n = (long)L.nblk() * 64 * L.nq;
-   if (Q == 3)
-   {
-      hipLaunchKernelGGL((k_setup_trilinear<3>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.perm, L.ne, enodes,
-                         cfit, W, qp, scm, scd, L.pw, qd_geo, qd_pair);
-   }
-   else if (Q == 4)
-   {
-      hipLaunchKernelGGL((k_setup_trilinear<4>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.perm, L.ne, enodes,
-                         cfit, W, qp, scm, scd, L.pw, qd_geo, qd_pair);
-   }
-   else { ECM2_VERIFY(false, ERR_UNSUPPORTED, "trilinear setup: Q1D " << Q << " not instantiated"); }
-   ECM2_HIP(hipGetLastError());
+   const bool blk = L.kind == QLAYOUT_TRILINEAR;
+   const long n = blk ? (long)L.nblk() * 64 * L.nq : (long)L.ne * L.nq;
+   const int *perm = blk ? L.perm : nullptr;
+   ECM2_Q_BLOCKED_CASES(k_setup_trilinear, n, blk, perm, L.ne, enodes, cfit, W, qp, scm, scd, L.pw, qd_geo, qd_pair)
 }
 
 void trilinear_expand(const QLayout &L, int Q, const double *qd_geo, const double *qd_pair, const QPts &qp,
                       double *qd_diff, double *qd_mass, hipStream_t s)
 {
    if (L.ne == 0) { return; }
-   const long n = (long)L.nblk() * 64 * L.nq;
-   if (Q == 3)
-   {
-      hipLaunchKernelGGL((k_trilinear_expand<3>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.ne, qd_geo, qd_pair, qp,
-                         L.pw, qd_diff, qd_mass);
-   }
-   else if (Q == 4)
-   {
-      hipLaunchKernelGGL((k_trilinear_expand<4>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.ne, qd_geo, qd_pair, qp,
-                         L.pw, qd_diff, qd_mass);
-   }
-   else { ECM2_VERIFY(false, ERR_UNSUPPORTED, "trilinear expand: Q1D " << Q << " not instantiated"); }
-   ECM2_HIP(hipGetLastError());
+   const bool blk = L.kind == QLAYOUT_TRILINEAR;
+   const long n = blk ? (long)L.nblk() * 64 * L.nq : (long)L.ne * L.nq;
+   ECM2_Q_BLOCKED_CASES(k_trilinear_expand, n, blk, L.ne, qd_geo, qd_pair, qp, L.pw, qd_diff, qd_mass)
 }
 
 void affine_expand(const QLayout &L, int Q, const double *qd_fac, const double *qd_pair, double *qd_diff,
                    double *qd_mass, hipStream_t s)
 {
    if (L.ne == 0) { return; }
-   const long n = (long)L.nblk() * 64 * L.nq;
-   if (Q == 3)
-   {
-      hipLaunchKernelGGL((k_affine_expand<3>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.ne, qd_fac, qd_pair, L.pw,
-                         qd_diff, qd_mass);
-   }
-   else if (Q == 4)
-   {
-      hipLaunchKernelGGL((k_affine_expand<4>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.ne, qd_fac, qd_pair, L.pw,
-                         qd_diff, qd_mass);
-   }
-   else { ECM2_VERIFY(false, ERR_UNSUPPORTED, "affine expand: Q1D " << Q << " not instantiated"); }
-   ECM2_HIP(hipGetLastError());
+   const bool blk = L.kind == QLAYOUT_AFFINE;
+   const long n = blk ? (long)L.nblk() * 64 * L.nq : (long)L.ne * L.nq;
+   ECM2_Q_BLOCKED_CASES(k_affine_expand, n, blk, L.ne, qd_fac, qd_pair, L.pw, qd_diff, qd_mass)
 }
+#undef ECM2_Q_BLOCKED_CASES
 
 void setup_affine(const QLayout &L, int Q, const double *enodes, const double *J, const double *W,
                   const CoeffDesc *cm, const CoeffDesc *cd, const double *cm_q, const double *cd_q,
                   double *qd_fac, double *qd_pair, hipStream_t s)
 {
    if (L.ne == 0) { return; }
-   ECM2_VERIFY(L.affine() && cd && (cm || (L.pw == 1 && L.kind == QLAYOUT_AFFINE)), ERR_INTERNAL,
+   ECM2_VERIFY(L.affine() && cd && (cm || L.pw == 1), ERR_INTERNAL,
                "affine setup needs an AFFINE layout and its coefficients");
    ECM2_VERIFY(!L.pos || L.perm, ERR_INTERNAL, "blocked setup needs the inverse permutation");
    const SetupCoef scm = make_setup_coef(cm, cm_q), scd = make_setup_coef(cd, cd_q);

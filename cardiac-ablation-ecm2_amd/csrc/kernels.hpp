@@ -36,7 +36,10 @@ namespace ecm2
 {
 
 enum QLayoutKind : int { QLAYOUT_NATIVE = 0, QLAYOUT_BLOCKED = 1, QLAYOUT_AFFINE = 2, QLAYOUT_AFFINE_E = 3,
-                         QLAYOUT_TRILINEAR = 4, QLAYOUT_NATIVE9 = 5 };
+                         QLAYOUT_TRILINEAR = 4, QLAYOUT_NATIVE9 = 5, QLAYOUT_TRILINEAR_E = 6 };
+// TRILINEAR_E: the TRILINEAR compression for the p >= 3 line / brick kernels, caller element
+// order: qd_diff = [e][21] map coefficients c1..c7 of x, y, z (index 3 (k - 1) + i), qd_mass =
+// [e][q][pw] point values.  AFFINE_E / TRILINEAR_E with pw = 1: a diffusion-only form.
 // NATIVE9: the reference's layout for a general (nonsymmetric) matrix diffusion coefficient,
 // D(q, k, e) = [e][9][NQ] with k = 3 i + j for D_ij (bilininteg_diffusion_kernels.cpp:320-345,
 // "symmetric ? 6 : 9"); the workgroup-per-element kernels read it.
@@ -76,18 +79,22 @@ struct QLayout
       if (kind == QLAYOUT_AFFINE) { return (size_t)nblk() * 6 * kElemBlock; }
       if (kind == QLAYOUT_TRILINEAR) { return (size_t)nblk() * 2 * kTrilinPairs * kElemBlock; }
       if (kind == QLAYOUT_AFFINE_E) { return (size_t)ne * 6; }
+      if (kind == QLAYOUT_TRILINEAR_E) { return (size_t)ne * 21; }
       return (size_t)nblk() * nq * 6 * kElemBlock;
    }
    size_t mass_size() const
    {
       if (kind == QLAYOUT_NATIVE || kind == QLAYOUT_NATIVE9) { return (size_t)ne * nq; }
       if (kind == QLAYOUT_AFFINE || kind == QLAYOUT_TRILINEAR) { return (size_t)nblk() * nq * pw * kElemBlock; }
-      if (kind == QLAYOUT_AFFINE_E) { return (size_t)ne * nq * 2; }
+      if (kind == QLAYOUT_AFFINE_E || kind == QLAYOUT_TRILINEAR_E) { return (size_t)ne * nq * pw; }
       return (size_t)nblk() * ((nq + 1) / 2) * 2 * kElemBlock;
    }
    int nblk() const { return (ne + kElemBlock - 1) / kElemBlock; }
    bool blocked() const { return kind == QLAYOUT_BLOCKED || kind == QLAYOUT_AFFINE || kind == QLAYOUT_TRILINEAR; }
    bool affine() const { return kind == QLAYOUT_AFFINE || kind == QLAYOUT_AFFINE_E; }
+   bool trilinear() const { return kind == QLAYOUT_TRILINEAR || kind == QLAYOUT_TRILINEAR_E; }
+   // the point values live in qd_mass (present with either integrator)
+   bool compressed() const { return affine() || trilinear(); }
 };
 
 // Coefficient descriptor for qdata setup: constant, per-quadrature-point array

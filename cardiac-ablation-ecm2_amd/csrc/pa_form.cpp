@@ -681,23 +681,24 @@ void PAForm::assemble(hipStream_t s)
    }
    layout_.kind = (resolved_mode_ == KERNEL_TPE) ? QLAYOUT_BLOCKED : (cdim == 9 ? QLAYOUT_NATIVE9 : QLAYOUT_NATIVE);
    layout_.pw = 2;
-   // Compressed geometry: both integrators, or (the thread-per-element kernels, p <= 2) a
-   // diffusion-only form such as ex16's K (point values W beta [/ det J] alone, 8 B per point).  A
-   // mass-only form keeps the BLOCKED mass stream, already one 8-byte W alpha det J per point.
-   const bool both = have_mass_ && have_diff_ && cdim == 1;
-   const bool comp_tpe = compress_ && have_diff_ && cdim == 1 && resolved_mode_ == KERNEL_TPE;
+   // Compressed geometry for the fused kernels (thread-per-element p <= 2: AFFINE / TRILINEAR;
+   // line / brick p >= 3: AFFINE_E / TRILINEAR_E), with both integrators or a diffusion-only form
+   // such as ex16's K (point values W beta [/ det J] alone, 8 B per point).  A mass-only form keeps
+   // the mass stream, already one 8-byte W alpha det J per point.
+   const bool fused = resolved_mode_ == KERNEL_TPE || resolved_mode_ == KERNEL_LINE;
+   const bool comp = compress_ && have_diff_ && cdim == 1 && fused;
+   const bool tpe = resolved_mode_ == KERNEL_TPE;
    bool affine = affine_;
-   if (jac_ && ((compress_ && both && resolved_mode_ == KERNEL_LINE) || comp_tpe))
+   if (jac_ && comp)
    {
       affine = kern::jacobians_affine(ne_, NQ_, jac_, s);  // the reference binding's geometry
    }
-   if (affine && compress_ && both && resolved_mode_ == KERNEL_LINE) { layout_.kind = QLAYOUT_AFFINE_E; }
-   else if (affine && comp_tpe)
+   if (affine && comp)
    {
-      layout_.kind = QLAYOUT_AFFINE;
+      layout_.kind = tpe ? QLAYOUT_AFFINE : QLAYOUT_AFFINE_E;
       layout_.pw = have_mass_ ? 2 : 1;
    }
-   else if (!affine && comp_tpe)
+   else if (!affine && comp)
    {
       // general trilinear hexes: the map coefficients per element (from the corners, or fitted
       // to the reference binding's Jacobians when they are a trilinear map's), J per point
@@ -711,7 +712,7 @@ void PAForm::assemble(hipStream_t s)
       }
       if (tl)
       {
-         layout_.kind = QLAYOUT_TRILINEAR;
+         layout_.kind = tpe ? QLAYOUT_TRILINEAR : QLAYOUT_TRILINEAR_E;
          layout_.pw = have_mass_ ? 2 : 1;
       }
    }
@@ -1148,7 +1149,7 @@ std::vector<double> PAForm::marker_weights(int k) const
 void PAForm::setup_qdata(hipStream_t s, const std::pair<int, std::vector<double>> *wover)
 {
    // (compressed layouts: qd_mass_ holds the point values, present with either integrator)
-   const bool comp = layout_.kind == QLAYOUT_AFFINE || layout_.kind == QLAYOUT_AFFINE_E || layout_.kind == QLAYOUT_TRILINEAR;
+   const bool comp = layout_.compressed();
    qd_diff_.resize(have_diff_ ? layout_.diff_size() : 0);
    qd_mass_.resize(have_mass_ || comp ? layout_.mass_size() : 0);
    // the setup kernels write every entry except the padding lanes of a partial last block
@@ -1206,7 +1207,7 @@ void PAForm::setup_qdata(hipStream_t s, const std::pair<int, std::vector<double>
       kern::setup_affine(layout_, Q_, jac_ ? nullptr : enodes_.data(), jac_, W_.data(), cm, cd, cm_q, cd_q,
                          qd_diff_.data(), qd_mass_.data(), s);
    }
-   else if (layout_.kind == QLAYOUT_TRILINEAR)
+   else if (layout_.trilinear())
    {
       QPts qp = {};
       for (int q = 0; q < Q_ && q < MAX_Q1D; q++) { qp.x[q] = maps_.qpts[q]; }
@@ -1490,7 +1491,7 @@ void PAForm::diagonal_from_qdata(double *diag, hipStream_t s)
       if (expand_needed())
       {
          expand_compressed(fd, fm, s);  // per-point qdata for the diagonal's tables
-         a.kind = QLAYOUT_BLOCKED;
+         a.kind = expand_kind();
          a.qdd = fd.data();
          a.qdm = fm.data();
       }
@@ -1500,24 +1501,35 @@ void PAForm::diagonal_from_qdata(double *diag, hipStream_t s)
       return;
    }
    ECM2_HIP(hipMemsetAsync(diag, 0, sizeof(double) * (size_t)ndofs_, s));
-   kern::diagonal(layout_.pos, D_, Q_, layout_.kind, ne_, gmap_.data(), have_diff_ ? qd_diff_.data() : nullptr,
-                  have_mass_ ? qd_mass_.data() : nullptr, diag, false, basis_, btab(), s);
+   DeviceArray<double> fd, fm;
+   int kind = layout_.kind;
+   const double *qdd = qd_diff_.data(), *qdm = qd_mass_.data();
+   if (expand_needed())
+   {
+      expand_compressed(fd, fm, s);
+      kind = expand_kind();
+      qdd = fd.data();
+      qdm = fm.data();
+   }
+   kern::diagonal(layout_.pos, D_, Q_, kind, ne_, gmap_.data(), have_diff_ ? qdd : nullptr,
+                  have_mass_ ? qdm : nullptr, diag, false, basis_, btab(), s);
+   if (fd.size()) { ECM2_HIP(hipStreamSynchronize(s)); }  // the temporaries are freed on return
 }
 
 void PAForm::expand_compressed(DeviceArray<double> &fd, DeviceArray<double> &fm, hipStream_t s) const
 {
    QLayout L = layout_;
-   L.kind = QLAYOUT_BLOCKED;
+   L.kind = expand_kind();
    fd.resize(std::max<size_t>(1, have_diff_ ? L.diff_size() : 0));
    fm.resize(std::max<size_t>(1, have_mass_ ? L.mass_size() : 0));
-   if (ne_ % kElemBlock)
+   if (L.blocked() && ne_ % kElemBlock)
    {
       ECM2_HIP(hipMemsetAsync(fd.data(), 0, fd.bytes(), s));
       ECM2_HIP(hipMemsetAsync(fm.data(), 0, fm.bytes(), s));
    }
    QPts qp = {};
    for (int q = 0; q < Q_ && q < MAX_Q1D; q++) { qp.x[q] = maps_.qpts[q]; }
-   if (layout_.kind == QLAYOUT_TRILINEAR)
+   if (layout_.trilinear())
    {
       kern::trilinear_expand(layout_, Q_, qd_diff_.data(), qd_mass_.data(), qp, fd.data(), fm.data(), s);
    }
@@ -1546,7 +1558,7 @@ void PAForm::integrator_add_mult(int kind, const double *xe, double *ye, hipStre
    if (expand_needed())
    {
       expand_compressed(fd, fm, s);
-      a.kind = QLAYOUT_BLOCKED;
+      a.kind = expand_kind();
       a.qdd = fd.data();
       a.qdm = fm.data();
    }
@@ -1560,9 +1572,10 @@ void PAForm::get_qdata(int kind, double *out, hipStream_t s)
    const bool diff = kind == INTEG_DIFFUSION;
    ECM2_VERIFY(diff ? have_diff_ : have_mass_, ERR_ARG, "integrator " << kind << " not present");
    DeviceArray<double> fd, fm;
-   const bool tl = expand_needed();  // TRILINEAR, or a diffusion-only AFFINE form
+   const bool tl = expand_needed();  // TRILINEAR(_E), or a diffusion-only AFFINE(_E) form
    const bool aff = layout_.affine() && !tl;
-   if (tl) { expand_compressed(fd, fm, s); }  // decoded as BLOCKED below
+   if (tl) { expand_compressed(fd, fm, s); }  // decoded as expand_kind() below
+   const int kind_h = tl ? expand_kind() : layout_.kind;
    DeviceArray<double> &src = tl ? (diff ? fd : fm) : ((diff && !aff) ? qd_diff_ : qd_mass_);
    std::vector<double> h(src.size()), hc(aff ? qd_diff_.size() : 0);
    if (src.size())
@@ -1587,8 +1600,8 @@ void PAForm::get_qdata(int kind, double *out, hipStream_t s)
          for (int q = 0; q < NQ_; q++)
          {
             size_t src_i;
-            if (layout_.kind == QLAYOUT_NATIVE || layout_.kind == QLAYOUT_NATIVE9) { src_i = ((size_t)e * nc + c) * NQ_ + q; }
-            else if (layout_.kind == QLAYOUT_AFFINE_E)
+            if (kind_h == QLAYOUT_NATIVE || kind_h == QLAYOUT_NATIVE9) { src_i = ((size_t)e * nc + c) * NQ_ + q; }
+            else if (kind_h == QLAYOUT_AFFINE_E)
             {
                const size_t pi = ((size_t)e * NQ_ + q) * 2;
                out[((size_t)e * nc + c) * NQ_ + q] = diff ? h[pi] * hc[(size_t)e * 6 + c] : h[pi + 1];

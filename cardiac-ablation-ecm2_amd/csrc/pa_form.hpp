@@ -179,12 +179,11 @@ private:
    // element weights [ne] of integrator kind k: 1 / 0 per its attribute marker, all 1 unmarked
    std::vector<double> marker_weights(int k) const;
    void diagonal_from_qdata(double *diag, hipStream_t s);
-   // TRILINEAR forms and diffusion-only AFFINE forms: their per-point qdata in the BLOCKED layout
-   // (temporaries of the caller) for the diagonal, the E-vector apply and the qdata export
-   bool expand_needed() const
-   {
-      return layout_.kind == QLAYOUT_TRILINEAR || (layout_.kind == QLAYOUT_AFFINE && layout_.pw == 1);
-   }
+   // TRILINEAR(_E) forms and diffusion-only AFFINE(_E) forms: their per-point qdata in the BLOCKED
+   // (p <= 2) or NATIVE (p >= 3) layout, expand_kind() (temporaries of the caller) for the
+   // diagonal, the E-vector apply and the qdata export
+   bool expand_needed() const { return layout_.trilinear() || (layout_.affine() && layout_.pw == 1); }
+   int expand_kind() const { return layout_.blocked() ? QLAYOUT_BLOCKED : QLAYOUT_NATIVE; }
    void expand_compressed(DeviceArray<double> &fd, DeviceArray<double> &fm, hipStream_t s) const;
 
  public:

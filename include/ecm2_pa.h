@@ -170,12 +170,15 @@ int ecm2_pa_form_set_jacobians(ecm2_pa_form *f, const double *J);
 #define ECM2_QLAYOUT_BLOCKED 1
 #define ECM2_QLAYOUT_AFFINE 2
 #define ECM2_QLAYOUT_AFFINE_E 3  /* the same compression for the p >= 3 line / brick kernels */
-/* TRILINEAR (p <= 2, geometry from corners, both integrators, elements not all parallelepipeds):
- * the element's trilinear-map coefficients once per element plus one (W beta, W alpha) pair per
- * point; the fused kernel evaluates J, adj(J) and det J at every quadrature point (the
- * reference's setup algebra, never stored): the AFFINE layout's bytes on a general mesh. */
+/* TRILINEAR (p <= 2, elements not all parallelepipeds, geometry from corners or from Jacobians
+ * that a trilinear map produces): the element's trilinear-map coefficients once per element plus
+ * one (W beta / det J, W alpha det J) pair per point; the fused kernel evaluates J and adj(J) at
+ * every quadrature point (the reference's setup algebra, never stored): the AFFINE layout's bytes
+ * on a general mesh.  TRILINEAR_E: the same for the p >= 3 line / brick kernels.  Every
+ * compressed layout also serves a diffusion-only form (one W beta [/ det J] value per point). */
 #define ECM2_QLAYOUT_TRILINEAR 4
 #define ECM2_QLAYOUT_NATIVE9 5   /* [e][9][nq] general D_ij (a nonsymmetric matrix coefficient)    */
+#define ECM2_QLAYOUT_TRILINEAR_E 6
 int ecm2_pa_form_set_geometry_compression(ecm2_pa_form *f, int on);
 /* BilinearForm::AddDomainIntegrator(new MassIntegrator(Q)) / DiffusionIntegrator(Q)
  * (bilinearform.cpp:231-242).  data: CONSTANT -> data[0] (host);

@@ -12,3 +12,5 @@ SQ_COUNTERS="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_A
 SQ_COUNTERS="SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_MISC SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_INST_ANY" \
   bash profiles/sq_pass.sh c4tri_tlb2 --workload c4 --mesh trilinear --variants 0 --full-layout 0 --steps 20 --warmup 3 > "$O/sq_c4tri2.txt" 2>&1 || exit 1
 echo done
+# the lattice TRILINEAR kernel with per-plane z partials (tlZ, 2 scratch ops per plane) against per-row (main)
+bash profiles/ab_libs.sh tlz_c4t "libecm2pa.so libecm2pa_tlZ.so" --workload c4 --steps 30 --warmup 5 --variants 0 --mesh trilinear || exit $?

@@ -66,8 +66,9 @@ def make_mesh(name):
 
 
 def build_pair(mesh, order, alpha, beta, kernel=E.KERNEL_AUTO, numbering=E.NUMBERING_ENTITY,
-               element_order="auto", scatter="partials", compress_geometry=True):
-    """Product form + oracle operator on the same mesh; alpha/beta: 'fn', 'bio', float or None."""
+               element_order="auto", scatter="partials", compress_geometry=True, geometry="nodes"):
+    """Product form + oracle operator on the same mesh; alpha/beta: 'fn', 'bio', float or None;
+    geometry="jacobians": the form gets J at the points through SetJacobians (the drop-in path)."""
     fes = E.H1Space(mesh, order, numbering)
     en = mesh.element_nodes()
     q1d = O.default_q1d(order)
@@ -89,7 +90,9 @@ def build_pair(mesh, order, alpha, beta, kernel=E.KERNEL_AUTO, numbering=E.NUMBE
     a_np, a_c = coeff(alpha)
     b_np, b_c = coeff(beta)
     form = E.BilinearForm(fes, kernel=kernel, element_order=element_order, scatter=scatter,
-                          compress_geometry=compress_geometry)
+                          compress_geometry=compress_geometry, geometry=geometry)
+    if geometry == "jacobians":
+        form.SetJacobians(mesh.jacobians(q1d))
     if a_c is not None:
         form.AddDomainIntegrator(E.MassIntegrator(a_c))
     if b_c is not None:
@@ -195,13 +198,14 @@ def _lattice_trilinear(n=8):
 
 
 @pytest.mark.parametrize("mesh_name", ["cart_bricks", "nonaligned", "trilinear", "lattice_tri"])
-@pytest.mark.parametrize("order", [1, 2])
+@pytest.mark.parametrize("order", [1, 2, 3, 4])
 @pytest.mark.parametrize("geometry", ["nodes", "jacobians"])
 def test_diffusion_only_compressed_layouts(mesh_name, order, geometry):
     """A form with only a DiffusionIntegrator (ex16's K, ex16p.cpp:464) keeps the compressed
     geometry: AFFINE (C_e + W beta per point) or TRILINEAR (map coefficients + W beta / det J per
-    point), 8 B per point -- Mult, diagonal, E-vector AddMultPA and the reference-layout qdata
-    against the oracle.  A mass-only form keeps the BLOCKED mass stream (8 B per point)."""
+    point), 8 B per point, blocked at p <= 2 and element-ordered (AFFINE_E / TRILINEAR_E, the line
+    kernel) at p >= 3 -- Mult, diagonal, E-vector AddMultPA and the reference-layout qdata against
+    the oracle.  A mass-only form keeps the BLOCKED mass stream (8 B per point)."""
     m = _lattice_trilinear() if mesh_name == "lattice_tri" else make_mesh(mesh_name)
     fes = E.H1Space(m, order)
     en = m.element_nodes()
@@ -213,7 +217,11 @@ def test_diffusion_only_compressed_layouts(mesh_name, order, geometry):
     form.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(dev(c.reshape(fes.ne, -1)))))
     form.Assemble()
     affine = mesh_name in ("cart_bricks", "nonaligned")
-    assert form.info()["layout"] == (E.QLAYOUT_AFFINE if affine else E.QLAYOUT_TRILINEAR)
+    if order <= 2:
+        assert form.info()["layout"] == (E.QLAYOUT_AFFINE if affine else E.QLAYOUT_TRILINEAR)
+    else:
+        assert form.info()["layout"] == (E.QLAYOUT_AFFINE_E if affine else E.QLAYOUT_TRILINEAR_E)
+        assert form.qdata_bytes() == 8 * fes.ne * ((6 if affine else 21) + q1d ** 3)
     assert form.qdata_bytes() < 20 * fes.ne * q1d ** 3  # 8 B per point + the per-element geometry
     op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=None, beta=c)
     x = np.random.default_rng(13).uniform(-1, 1, fes.ndofs)
@@ -228,7 +236,7 @@ def test_diffusion_only_compressed_layouts(mesh_name, order, geometry):
     ye = torch.zeros(fes.ne * fes.nd, dtype=torch.float64, device="cuda")
     form.IntegratorAddMultPA(E.DIFFUSION, dev(xe), ye)
     assert relerr(host(ye).reshape(fes.ne, fes.nd), O.diffusion_apply(op.B, op.G, op.D, xe)) <= RTOL
-    if geometry == "nodes" and mesh_name == "trilinear":
+    if geometry == "nodes" and mesh_name == "trilinear" and order <= 2:
         fm = E.BilinearForm(fes)
         fm.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(c.reshape(fes.ne, -1)))))
         fm.Assemble()
@@ -287,9 +295,9 @@ def test_qdata_matches_reference_setup(kernel, order):
 def test_jacobian_geometry_path(mesh_name, order):
     """set_jacobians (GeometricFactors layout -- what the reference-side binding passes) gives
     the same operator as element nodes; affine Jacobians (constant per element, checked on
-    the device) select the compressed layout; trilinear ones at p <= 2 are fitted to the
-    elements' trilinear maps (checked at every point) and select the TRILINEAR layout, at p >= 3
-    they keep the full one."""
+    the device) select the compressed layout; trilinear ones are fitted to the elements'
+    trilinear maps (checked at every point) and select the TRILINEAR layout (TRILINEAR_E at
+    p >= 3)."""
     m = make_mesh(mesh_name)
     fes = E.H1Space(m, order)
     en = m.element_nodes()
@@ -303,9 +311,9 @@ def test_jacobian_geometry_path(mesh_name, order):
     op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=3.0, beta=0.5)
     affine = mesh_name != "trilinear" and AFFINE_ON
     want = (E.QLAYOUT_AFFINE if order <= 2 else E.QLAYOUT_AFFINE_E) if affine else \
-        (E.QLAYOUT_TRILINEAR if order <= 2 else E.QLAYOUT_NATIVE)
+        (E.QLAYOUT_TRILINEAR if order <= 2 else E.QLAYOUT_TRILINEAR_E)
     assert form.info()["layout"] == want
-    if want == E.QLAYOUT_TRILINEAR:
+    if want in (E.QLAYOUT_TRILINEAR, E.QLAYOUT_TRILINEAR_E):
         assert relerr(form.qdata(E.DIFFUSION), op.D) < 1e-13
     x = np.random.default_rng(5).uniform(-1, 1, fes.ndofs)
     y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
@@ -478,22 +486,26 @@ def test_full_size_c4_tpe():
     assert relerr(host(y), op.mult(x)) <= RTOL
 
 
-@pytest.mark.parametrize("mesh_kind", ["affine", "trilinear"])
+@pytest.mark.parametrize("mesh_kind", ["affine", "trilinear", "trilinear_jacobians"])
 def test_full_size_c4_reference_numbering(mesh_kind):
     """configs[3] size with the reference's own numbering -- MakeCartesian3D's space-filling-curve
     element order and FiniteElementSpace's entity dofs, the element order derived by the form from
     the map (what a drop-in binding gets; bench.py's entity_numbering sub-object) -- and, second
     case, the same mesh with its interior vertices moved (TRILINEAR layout): against the oracle,
-    plus the diagonal."""
+    plus the diagonal. Third case: the full drop-in configuration (bench.py's drop_in sub-object)
+    -- the same perturbed mesh, but the geometry handed over as J at the quadrature points
+    (SetJacobians, what GeometricFactors gives the reference's PA setup), fitted to TRILINEAR."""
     n = 108
     m = E.Mesh.MakeCartesian3D(n, n, n, sfc_ordering=True)
-    if mesh_kind == "trilinear":
+    if mesh_kind.startswith("trilinear"):
         V = m.vertices()
         h = 1.0 / n
         inner = np.all((V > 0.5 * h) & (V < 1.0 - 0.5 * h), axis=1)
         V[inner] += 0.15 * h * np.random.default_rng(7).uniform(-1, 1, (int(inner.sum()), 3))
         m.set_vertices(V)
-    fes, form, op = build_pair(m, 2, "bio_a", "bio_b", numbering=E.NUMBERING_ENTITY, element_order="faces")
+    geo = "jacobians" if mesh_kind == "trilinear_jacobians" else "nodes"
+    fes, form, op = build_pair(m, 2, "bio_a", "bio_b", numbering=E.NUMBERING_ENTITY, element_order="faces",
+                               geometry=geo)
     assert fes.ndofs == 10218313
     assert form.info()["layout"] == (E.QLAYOUT_AFFINE if mesh_kind == "affine" else E.QLAYOUT_TRILINEAR)
     lslot, _ = form.PlanInfo()
@@ -638,6 +650,50 @@ def test_full_size_c5_bricks():
         assert relerr(out[bz], ref) <= RTOL, bz
 
 
+@pytest.mark.parametrize("order", [3, 4, 5])
+@pytest.mark.parametrize("geometry", ["nodes", "jacobians"])
+def test_trilinear_e_bricks(order, geometry):
+    """TRILINEAR_E at p >= 3 (a non-affine mesh: the element's trilinear-map coefficients + one
+    (W beta / det J, W alpha det J) pair per point; the brick kernel's z stage evaluates J and
+    adj(J) at its points): 2 x 2 x 1 and 2 x 2 x 2 bricks and the per-element line kernel against
+    the oracle (bitwise reproducible), from corners and from the reference binding's Jacobians,
+    plus the diagonal and the reference-layout qdata."""
+    m = E.Mesh.MakeCartesian3D(6, 4, 4)
+    V = m.vertices()
+    inner = np.all((V > 1e-9) & (V < np.array([1.0, 1.0, 1.0]) - 1e-9), axis=1)
+    V[inner] += 0.04 * np.random.default_rng(12).uniform(-1, 1, (int(inner.sum()), 3))
+    m.set_vertices(V)
+    fes = E.H1Space(m, order)
+    en = m.element_nodes()
+    q1d = O.default_q1d(order)
+    P = O.quad_points(en, q1d)
+    a, b = alpha_bioheat(P), coeff_function(P)
+    op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=a, beta=b)
+    x = np.random.default_rng(order).uniform(-1, 1, fes.ndofs)
+    for bz in (0, 1, 2):
+        form = E.BilinearForm(fes, kernel=E.KERNEL_LINE, bricks=bz, geometry=geometry)
+        if geometry == "jacobians":
+            form.SetJacobians(m.jacobians(q1d))
+        form.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(a.reshape(fes.ne, -1)))))
+        form.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(dev(b.reshape(fes.ne, -1)))))
+        form.Assemble()
+        assert form.info()["layout"] == E.QLAYOUT_TRILINEAR_E
+        nb, depth = form.BrickInfo()
+        assert (nb > 0) == (bz > 0)
+        y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+        form.Mult(dev(x), y)
+        assert relerr(host(y), op.mult(x)) <= RTOL, (bz, nb, depth)
+        y2 = torch.full_like(y, float("nan"))
+        form.Mult(dev(x), y2)
+        assert torch.equal(y, y2)
+        if bz == 1:
+            d = torch.empty_like(y)
+            form.AssembleDiagonal(d)
+            assert relerr(host(d), op.diagonal()) < 1e-13
+            assert relerr(form.qdata(E.DIFFUSION), op.D) < 1e-13
+            assert relerr(form.qdata(E.MASS)[:, 0, :], op.M) < 1e-13
+
+
 @pytest.mark.parametrize("mesh_name", ["nonaligned", "fichera_r1", "cart_bricks", "cart_130", "trilinear"])
 @pytest.mark.parametrize("order", [1, 2, 3, 4])
 @pytest.mark.parametrize("compress", [True, False])
@@ -646,8 +702,9 @@ def test_affine_geometry_layout(mesh_name, order, compress):
     chosen exactly for parallelepiped meshes with both integrators -- blocked for the p <= 2
     thread-per-element kernel, element-ordered (AFFINE_E) for the p >= 3 line / brick
     kernels -- and the operator, its diagonal and the reference-layout qdata match the
-    oracle either way; non-affine (trilinear) elements get the TRILINEAR layout at p <= 2 (map
-    coefficients per element, J evaluated per point) and the full per-point layout at p >= 3."""
+    oracle either way; non-affine (trilinear) elements get the TRILINEAR layout (map coefficients
+    per element, J evaluated per point; TRILINEAR_E at p >= 3); compression off keeps the full
+    per-point layout."""
     m = make_mesh(mesh_name)
     fes, form, op = build_pair(m, order, "bio_a", "fn", compress_geometry=compress)
     affine = mesh_name != "trilinear" and AFFINE_ON
@@ -658,6 +715,8 @@ def test_affine_geometry_layout(mesh_name, order, compress):
             want = E.QLAYOUT_TRILINEAR
     else:
         want = E.QLAYOUT_AFFINE_E if (affine and compress) else E.QLAYOUT_NATIVE
+        if mesh_name == "trilinear" and compress:
+            want = E.QLAYOUT_TRILINEAR_E
     assert form.info()["layout"] == want
     if want == E.QLAYOUT_AFFINE:
         assert form.qdata_bytes() == 8 * 64 * ((fes.ne + 63) // 64) * (6 + 2 * nq)
@@ -665,6 +724,8 @@ def test_affine_geometry_layout(mesh_name, order, compress):
         assert form.qdata_bytes() == 8 * fes.ne * (6 + 2 * nq)
     elif want == E.QLAYOUT_TRILINEAR:
         assert form.qdata_bytes() == 8 * 64 * ((fes.ne + 63) // 64) * (22 + 2 * nq)
+    elif want == E.QLAYOUT_TRILINEAR_E:
+        assert form.qdata_bytes() == 8 * fes.ne * (21 + 2 * nq)
     x = np.random.default_rng(41).uniform(-1, 1, fes.ndofs)
     y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
     form.Mult(dev(x), y)

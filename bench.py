@@ -102,9 +102,14 @@ def bioheat_coefficients(E, torch, mesh, fes, part=None):
 
 
 def qdata_layout(E, form):
-    """Quadrature-data layout of a (local) form: affine | affine_e | trilinear | blocked | native."""
-    return {E.QLAYOUT_NATIVE: "native", E.QLAYOUT_BLOCKED: "blocked", E.QLAYOUT_AFFINE: "affine",
-            E.QLAYOUT_AFFINE_E: "affine_e", E.QLAYOUT_TRILINEAR: "trilinear", E.QLAYOUT_TRILINEAR_E: "trilinear_e"}[form.info()["layout"]]
+    """Quadrature-data layout of a (local) form: affine | affine_ts (AFFINE with the k(T)
+    coefficient snapshot) | affine_e | trilinear | trilinear_e | blocked | native."""
+    lay = {E.QLAYOUT_NATIVE: "native", E.QLAYOUT_BLOCKED: "blocked", E.QLAYOUT_AFFINE: "affine",
+           E.QLAYOUT_AFFINE_E: "affine_e", E.QLAYOUT_TRILINEAR: "trilinear",
+           E.QLAYOUT_TRILINEAR_E: "trilinear_e"}[form.info()["layout"]]
+    if lay == "affine" and hasattr(form, "CoefficientSnapshot") and form.CoefficientSnapshot():
+        lay = "affine_ts"
+    return lay
 
 
 def min_bytes(form, ne, nd, n_true):
@@ -291,6 +296,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--geometry", choices=["compressed", "full"], default="compressed",
                     help="compressed: AFFINE qdata on parallelepiped meshes (default); full: per-point layout")
+    ap.add_argument("--coefficient-snapshot", type=int, default=1, choices=[0, 1],
+                    help="1: k(T) evaluated in the kernel from a snapshot of T (p = 2 AFFINE lattice forms, "
+                         "ecm2_pa_form_set_coefficient_snapshot); 0: W beta stored per point")
     ap.add_argument("--full-layout", type=int, default=1,
                     help="1 (N = 1): also time the full per-point qdata layout in this run (full_layout sub-object)")
     ap.add_argument("--variants", type=int, default=1,
@@ -393,7 +401,8 @@ def main():
         f = E.BilinearForm(fes, kernel=kernel, element_order=os.environ.get("ECM2_ELEMENT_ORDER", eo),
                            scatter=scatter, compress_geometry=compress_geometry,
                            bricks=int(os.environ.get("ECM2_BRICKS", "-1")),  # A/B: p >= 3 brick depth
-                           geometry="jacobians" if geo == "jacobians" else "nodes")
+                           geometry="jacobians" if geo == "jacobians" else "nodes",
+                           coefficient_snapshot=bool(args.coefficient_snapshot))
         if geo == "jacobians":
             # MFEM's GeometricFactors::JACOBIANS (NQ x 3 x 3 x NE), as the binding passes it; the form
             # fits it to trilinear maps (or checks it affine) at Assemble and keeps it for re-assembly

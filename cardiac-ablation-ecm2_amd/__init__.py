@@ -103,6 +103,8 @@ def load_library(path: str = LIB_PATH):
         "ecm2_pa_form_scatter_info": (i32, [vp, vp, vp]),
         "ecm2_pa_form_set_bricks": (i32, [vp, i32]),
         "ecm2_pa_form_set_geometry_compression": (i32, [vp, i32]),
+        "ecm2_pa_form_set_coefficient_snapshot": (i32, [vp, i32]),
+        "ecm2_pa_form_coefficient_snapshot": (i32, [vp, ip]),
         "ecm2_pa_form_qdata_bytes": (i32, [vp, dp]),
         "ecm2_pa_form_brick_info": (i32, [vp, ip, ip]),
         "ecm2_pa_form_addressing_info": (i32, [vp, ip, ip, ctypes.POINTER(ctypes.c_long)]),
@@ -465,7 +467,7 @@ class BilinearForm:
 
     def __init__(self, fes: H1Space, kernel: int = KERNEL_AUTO, q1d: int = 0, geometry: str = "nodes",
                  element_order: str = "auto", scatter: str = "partials", bricks: int = -1,
-                 compress_geometry: bool = True):
+                 compress_geometry: bool = True, coefficient_snapshot: bool = True):
         self.fes = fes
         self._integs = []
         self._kernel = kernel
@@ -481,6 +483,7 @@ class BilinearForm:
         _check(_lib.ecm2_pa_form_set_scatter(h, _SCATTER[scatter]))
         _check(_lib.ecm2_pa_form_set_bricks(h, bricks))
         _check(_lib.ecm2_pa_form_set_geometry_compression(h, 1 if compress_geometry else 0))
+        _check(_lib.ecm2_pa_form_set_coefficient_snapshot(h, 1 if coefficient_snapshot else 0))
         if element_order == "native" and fes.ne > 0:
             ident = np.arange(fes.ne, dtype=np.int32)  # kept alive across the call
             _check(_lib.ecm2_pa_form_set_element_order(h, _np_ptr(ident)))
@@ -575,6 +578,15 @@ class BilinearForm:
 
     def SetGeometryCompression(self, on: bool):
         _check(_lib.ecm2_pa_form_set_geometry_compression(self._h, 1 if on else 0))
+
+    def SetCoefficientSnapshot(self, on: bool):
+        """Interpolate the diffusion coefficient's field snapshot in the kernel (see ecm2_pa.h)."""
+        _check(_lib.ecm2_pa_form_set_coefficient_snapshot(self._h, 1 if on else 0))
+
+    def CoefficientSnapshot(self) -> bool:
+        v = ctypes.c_int()
+        _check(_lib.ecm2_pa_form_coefficient_snapshot(self._h, ctypes.byref(v)))
+        return bool(v.value)
 
     def AssembleDiagonal(self, diag, stream=None):
         _check(_lib.ecm2_pa_form_assemble_diagonal(self._h, _dev_ptr(diag), _stream(stream)))

@@ -395,6 +395,16 @@ int ecm2_pa_form_set_geometry_compression(ecm2_pa_form *f, int on)
    return guard([&] { NEED(f); f->f->set_geometry_compression(on != 0); });
 }
 
+int ecm2_pa_form_set_coefficient_snapshot(ecm2_pa_form *f, int on)
+{
+   return guard([&] { NEED(f); f->f->set_coefficient_snapshot(on != 0); });
+}
+
+int ecm2_pa_form_coefficient_snapshot(const ecm2_pa_form *f, int *on)
+{
+   return guard([&] { NEED(f); NEED(on); *on = f->f->coefficient_snapshot() ? 1 : 0; });
+}
+
 int ecm2_pa_form_set_bricks(ecm2_pa_form *f, int bz)
 {
    return guard([&] { NEED(f); f->f->set_line_bricks(bz); });

@@ -174,6 +174,7 @@ DofToQuad make_dof_to_quad(int order, int q1d)
          m.G[q + q1d * j] = d[j];
       }
    }
+   m.qw1 = qw;
    m.W.resize(q1d * q1d * q1d);
    for (int iz = 0; iz < q1d; ++iz)
       for (int iy = 0; iy < q1d; ++iy)

@@ -29,6 +29,7 @@ struct DofToQuad
    std::vector<double> B, G;   // [q + nqpt*d]
    std::vector<double> W;      // tensor weights, [qx + Q*(qy + Q*qz)]
    std::vector<double> qpts;   // 1D Gauss-Legendre points
+   std::vector<double> qw1;    // 1D Gauss-Legendre weights (W = qw1[qx] qw1[qy] qw1[qz])
    std::vector<double> nodes;  // 1D GLL nodes
 };
 

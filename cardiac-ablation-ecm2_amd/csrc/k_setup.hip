@@ -351,8 +351,8 @@ template <int Q, bool BLOCKED>
 __global__ void __launch_bounds__(256)
 k_setup_affine(const int *__restrict__ perm, int ne, const double *__restrict__ enodes,
                const double *__restrict__ Jg,
-               const double *__restrict__ W, SetupCoef cm, SetupCoef cd, int pw, double *__restrict__ qd_fac,
-               double *__restrict__ qd_pair)
+               const double *__restrict__ W, SetupCoef cm, SetupCoef cd, int pw, int tsnap,
+               double *__restrict__ qd_fac, double *__restrict__ qd_pair)
 {
    constexpr int NQ = Q * Q * Q;
    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -404,10 +404,15 @@ k_setup_affine(const int *__restrict__ perm, int ne, const double *__restrict__ 
    const size_t eq = (size_t)e * NQ + q;
    const double w = W[q];
    v2d pr;
-   pr.x = w * coef_at(cd, eq, e);
-   pr.y = pw == 2 ? w * coef_at(cm, eq, e) * detJ : 0.0;
-   if (BLOCKED && pw == 1) { qd_pair[((size_t)blk * NQ + q) * 64 + lane] = pr.x; }  // diffusion-only form
-   else if (BLOCKED) { reinterpret_cast<v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane] = pr; }
+   // (coefficient snapshot: the diffusion factor comes from the kernel's T' interpolation and the
+   // single point value is the mass factor, none without a MassIntegrator)
+   pr.x = tsnap ? (pw == 1 ? w * coef_at(cm, eq, e) * detJ : 0.0) : w * coef_at(cd, eq, e);
+   pr.y = (!tsnap && pw == 2) ? w * coef_at(cm, eq, e) * detJ : 0.0;
+   if (BLOCKED)
+   {
+      if (pw == 1) { qd_pair[((size_t)blk * NQ + q) * 64 + lane] = pr.x; }  // one value per point
+      else if (pw == 2) { reinterpret_cast<v2d *>(qd_pair + ((size_t)blk * NQ + q) * 128)[lane] = pr; }
+   }
    else if (pw == 1) { qd_pair[(size_t)e * NQ + q] = pr.x; }
    else { reinterpret_cast<v2d *>(qd_pair)[(size_t)e * NQ + q] = pr; }
    if (q == 0)
@@ -687,8 +692,10 @@ k_trilinear_expand(int ne, const double *__restrict__ qd_geo, const double *__re
 template <int Q, bool BLOCKED>
 __global__ void __launch_bounds__(256)
 k_affine_expand(int ne, const double *__restrict__ qd_fac, const double *__restrict__ qd_pair, int pw,
-                double *__restrict__ qd_diff, double *__restrict__ qd_mass)
+                double *__restrict__ qd_diff, double *__restrict__ qd_mass, const double *__restrict__ qm1)
 {
+   // qm1 (BLOCKED, optional): the mass values one per point ([blk][q][lane], a coefficient-snapshot
+   // form's stored W alpha det J) for qd_mass
    constexpr int NQ = Q * Q * Q;
    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
    if (!BLOCKED)
@@ -713,7 +720,19 @@ k_affine_expand(int ne, const double *__restrict__ qd_fac, const double *__restr
    v2d *dst = reinterpret_cast<v2d *>(qd_diff + ((size_t)blk * NQ + q) * 3 * 128) + lane;
 #pragma unroll
    for (int k = 0; k < 3; k++) { dst[k * 64] = pr.x * C[k * 64]; }
-   if (pw == 2) { qd_mass[((size_t)blk * ((NQ + 1) / 2) + (q >> 1)) * 128 + lane * 2 + (q & 1)] = pr.y; }
+   if (pw == 2 || qm1)
+   {
+      qd_mass[((size_t)blk * ((NQ + 1) / 2) + (q >> 1)) * 128 + lane * 2 + (q & 1)] =
+         qm1 ? qm1[((size_t)blk * NQ + q) * 64 + lane] : pr.y;
+   }
+}
+
+// The coefficient snapshot T' = A + B T of an affine law of an H1 field (k_apply_tpe_ts).
+__global__ void __launch_bounds__(256) k_affine_snapshot(int n, const double *__restrict__ T, double A, double B,
+                                                         double *__restrict__ out)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { out[i] = A + B * T[i]; }
 }
 
 SetupCoef make_setup_coef(const CoeffDesc *c, const double *q)
@@ -793,6 +812,13 @@ void setup_from_nodes(const QLayout &L, int Q, const double *enodes, const doubl
    ECM2_SETUP_CASE(6) ECM2_SETUP_CASE(7) ECM2_SETUP_CASE(8)
 #undef ECM2_SETUP_CASE
    ECM2_VERIFY(false, ERR_UNSUPPORTED, "setup: Q1D " << Q << " not instantiated");
+}
+
+void affine_snapshot(int n, const double *T, double A, double B, double *out, hipStream_t s)
+{
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_affine_snapshot, dim3(grid_for(n, 256)), dim3(256), 0, s, n, T, A, B, out);
+   ECM2_HIP(hipGetLastError());
 }
 
 bool jacobians_affine(int ne, int nq, const double *J, hipStream_t s)
@@ -890,12 +916,13 @@ void trilinear_expand(const QLayout &L, int Q, const double *qd_geo, const doubl
 }
 
 void affine_expand(const QLayout &L, int Q, const double *qd_fac, const double *qd_pair, double *qd_diff,
-                   double *qd_mass, hipStream_t s)
+                   double *qd_mass, hipStream_t s, const double *qm1)
 {
+   ECM2_VERIFY(!qm1 || L.kind == QLAYOUT_AFFINE, ERR_INTERNAL, "single mass values: blocked layout");
    if (L.ne == 0) { return; }
    const bool blk = L.kind == QLAYOUT_AFFINE;
    const long n = blk ? (long)L.nblk() * 64 * L.nq : (long)L.ne * L.nq;
-   ECM2_Q_BLOCKED_CASES(k_affine_expand, n, blk, L.ne, qd_fac, qd_pair, L.pw, qd_diff, qd_mass)
+   ECM2_Q_BLOCKED_CASES(k_affine_expand, n, blk, L.ne, qd_fac, qd_pair, L.pw, qd_diff, qd_mass, qm1)
 }
 #undef ECM2_Q_BLOCKED_CASES
 
@@ -904,7 +931,7 @@ void setup_affine(const QLayout &L, int Q, const double *enodes, const double *J
                   double *qd_fac, double *qd_pair, hipStream_t s)
 {
    if (L.ne == 0) { return; }
-   ECM2_VERIFY(L.affine() && cd && (cm || L.pw == 1), ERR_INTERNAL,
+   ECM2_VERIFY(L.affine() && cd && (cm || L.pw <= 1) && (!L.tsnap || L.kind == QLAYOUT_AFFINE), ERR_INTERNAL,
                "affine setup needs an AFFINE layout and its coefficients");
    ECM2_VERIFY(!L.pos || L.perm, ERR_INTERNAL, "blocked setup needs the inverse permutation");
    const SetupCoef scm = make_setup_coef(cm, cm_q), scd = make_setup_coef(cd, cd_q);
@@ -916,12 +943,12 @@ void setup_affine(const QLayout &L, int Q, const double *enodes, const double *J
       if (blk)                                                                                           \
       {                                                                                                  \
          hipLaunchKernelGGL((k_setup_affine<QQ, true>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.perm, L.ne, \
-                            enodes, J, W, scm, scd, L.pw, qd_fac, qd_pair);                              \
+                            enodes, J, W, scm, scd, L.pw, L.tsnap, qd_fac, qd_pair);                     \
       }                                                                                                  \
       else                                                                                               \
       {                                                                                                  \
          hipLaunchKernelGGL((k_setup_affine<QQ, false>), dim3(grid_for(n, 256)), dim3(256), 0, s, nullptr, L.ne, \
-                            enodes, J, W, scm, scd, L.pw, qd_fac, qd_pair);                              \
+                            enodes, J, W, scm, scd, L.pw, L.tsnap, qd_fac, qd_pair);                              \
       }                                                                                                  \
       ECM2_HIP(hipGetLastError());                                                                       \
       return;                                                                                            \

@@ -689,6 +689,12 @@ __device__ __forceinline__ unsigned lattice_xyz(int j)
 // same region then stages the cross-wave face exchange) and every plane adds its z-transpose into
 // them; (c) the per-point pair is (W beta / det J, W alpha det J), so no determinant or division
 // per point.  LDS 78.6 KB per workgroup: two workgroups (8 waves) per CU.
+#ifndef ECM2_TLB_PFD
+#define ECM2_TLB_PFD 2  // rows of point values in flight
+#endif
+#ifndef ECM2_TLB_ZP
+#define ECM2_TLB_ZP 1   // per-plane z partials
+#endif
 template <int D, int Q, bool SPLIT, int RM, int PW = 2>
 __global__ void __launch_bounds__(256, 2)
 k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
@@ -720,10 +726,13 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
    v2d ce[NCE];
    const double *qa = qdm + (size_t)blk * NQ * 64 * PW + lane * PW;
    auto ldp = [&](int q) -> v2d {  // the point values of point q (PW = 1: W beta / det J alone)
+#ifdef ECM2_PROBE_TLB_NOPAIR
+      return v2d{1.0 + 1e-3 * q, 0.5};  // timing probe only: no point-value loads
+#endif
       if constexpr (PW == 2) { return ld2(qa + (size_t)q * 128); }
       else { return v2d{__builtin_nontemporal_load(qa + (size_t)q * 64), 0.0}; }
    };
-   v2d ca[Q];
+   v2d ca[Q], cb[Q];  // point values of the rows in flight (cb: the odd rows at prefetch depth 2)
    auto load_row = [&](int row, v2d (&aq)[Q]) {
 #pragma unroll
       for (int qx = 0; qx < Q; qx++) { aq[qx] = ldp(row * Q + qx); }
@@ -735,6 +744,7 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
 #pragma unroll
       for (int k = 0; k < NCE; k++) { ce[k] = ld2(qc + k * 128); }
       load_row(0, ca);
+      if (ECM2_TLB_PFD == 2) { load_row(1, cb); }
       if (RM == 1)
       {
          const int *r = treg + (size_t)blk * 8;  // wave-uniform: scalar loads
@@ -754,7 +764,11 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
                const unsigned v = lattice_xyz<D>(j);
                d = rg.base + (int)(v & 31) * rg.sx + (int)((v >> 5) & 31) * rg.sy + (int)(v >> 10) * rg.sz;
             }
+#ifdef ECM2_PROBE_TLB_NOGATHER
+            sXL[w][j] = (double)(d & 7);  // timing probe only: no x loads
+#else
             sXL[w][j] = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
+#endif
          }
       }
 #pragma unroll
@@ -795,13 +809,17 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
          // the plane's z-forward partials from the lattice (ZB = B_z X, ZG = G_z X): 36 VGPRs that
          // spill 2 values per plane into scratch, against 81 instead of 27 multiply-adds per row
          // when every row re-reads the lattice (profiles/r4/ab_tlz_pf2.txt: kernel -2..-3%)
-         double SB[D][D], SG[D][D], ZB[D][D], ZG[D][D];
+         double SB[D][D], SG[D][D];
+#if ECM2_TLB_ZP
+         double ZB[D][D], ZG[D][D];
+#endif
 #pragma unroll
          for (int dy = 0; dy < D; dy++)
 #pragma unroll
             for (int dx = 0; dx < D; dx++)
             {
                SB[dy][dx] = 0.0; SG[dy][dx] = 0.0;
+#if ECM2_TLB_ZP
                int lb = lane_base(dx % P, dy % P);
                asm volatile("" : "+v"(lb));
                double zb = 0.0, zg = 0.0;
@@ -816,6 +834,7 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
                   zg += gz[dz] * c;
                }
                ZB[dy][dx] = zb; ZG[dy][dx] = zg;
+#endif
             }
          auto row_body = [&](const int qy, v2d (&cur)[Q], const int next_row) {
             double Y00[D], Y01[D], Y10[D];
@@ -827,9 +846,27 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
                for (int dy = 0; dy < D; dy++)
                {
                   const double by = b.B[qy + MQ * dy], gy = b.G[qy + MQ * dy];
-                  u += by * ZB[dy][dx];
-                  v += gy * ZB[dy][dx];
-                  wv += by * ZG[dy][dx];
+#if ECM2_TLB_ZP
+                  const double zb = ZB[dy][dx], zg = ZG[dy][dx];
+#else
+                  // z-forward straight from the lattice, one column at a time (no 27 live values)
+                  int lb = lane_base(dx % P, dy % P);
+                  asm volatile("" : "+v"(lb));
+                  double zb = 0.0, zg = 0.0;
+#pragma unroll
+                  for (int dz = 0; dz < D; dz++)
+                  {
+                     const int cx = dx % P, cy = dy % P, cz = dz % P;
+                     const int nx = tpe_lattice_class_n(cx), ny = tpe_lattice_class_n(cy);
+                     const int sl = tpe_lattice_class_off(D, cx, cy, cz) + ((dz / P) * ny + dy / P) * nx + dx / P;
+                     const double c = sXL[w][lb + sl];
+                     zb += bz[dz] * c;
+                     zg += gz[dz] * c;
+                  }
+#endif
+                  u += by * zb;
+                  v += gy * zb;
+                  wv += by * zg;
                }
                Y00[dx] = u; Y01[dx] = v; Y10[dx] = wv;
             }
@@ -862,8 +899,7 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
                   uz += bq * Y10[dx];
                }
                const v2d sa = cur[qx];
-               // the next row's pair of this point goes into the slot just read: one row of pairs in
-               // flight in Q registers pairs (ping-pong buffers cost 16 VGPRs more)
+               // the pair of this point ECM2_TLB_PFD rows ahead goes into the slot just read
                cur[qx] = ldp(next_row * Q + qx);
                const double xi = qp.x[qx];
                // J = [ja | jb | jc] (rows: coordinates), adj(J) rows A1., A2., A3.
@@ -922,8 +958,10 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
          for (int qy = 0; qy < Q; qy++)
          {
             const int row = qz * Q + qy;
+            const int nrow = row + ECM2_TLB_PFD < NR ? row + ECM2_TLB_PFD : NR - 1;  // (the last rows reload the last)
             __builtin_amdgcn_sched_barrier(0);  // rows stay in program order (no interleaved live ranges)
-            row_body(qy, ca, row + 1 < NR ? row + 1 : NR - 1);  // (the last row reloads itself: exact wait counts)
+            if (ECM2_TLB_PFD == 1 || qy % 2 == 0) { row_body(qy, ca, nrow); }
+            else { row_body(qy, cb, nrow); }
          }
          // the plane's z-transpose into the outputs (private [a][lane] slots: same-lane RMW)
 #pragma unroll
@@ -946,6 +984,214 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
    for (int a = 0; a < ND; a++) { Yo[a] = wave_on ? sY[w][a][lane] : 0.0; }
    tpe_assemble_store<D, SPLIT, false, true, true>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0, blk, lane,
                                                   active, n_owned, y, yg, part, &sY[0][0][0], w, wave_on, rg, regf,
+                                                  pstride, lmap ? lmap + (size_t)blk * NLP : nullptr);
+}
+
+// AFFINE apply with the diffusion coefficient evaluated from a snapshot of its temperature field
+// (TS: ApplyArgs::tsnap).  In the bioheat form beta = k(T) is affine in T, an H1 grid function on
+// the form's own space (AffineGridFunctionCoefficient, coefficient.cpp:250-253 with the Pennes k(T)
+// law): the reference evaluates it at the quadrature points at Assemble (CoefficientVector::Project,
+// coefficient.cpp:2052-2070, then PADiffusionSetup3D stores W beta adj(J) adj(J)^T / det J).  Here
+// Assemble keeps T' = A + B T (the law applied to T's dofs, A = scale (1 - slope t_ref), B = scale
+// slope) and the kernel interpolates it with the weight-scaled basis w_q B (bw), so
+// W_q beta(x_q) = sum (w B)_z (w B)_y (w B)_x T' comes out of the same sum factorisation as u: per
+// plane 27, per row 9, per point 3 multiply-adds, and 8 bytes per point fewer -- only W alpha det J
+// is streamed (nothing without a MassIntegrator).  x and T' are gathered once per lattice point
+// (the block's 729 lattice slots, as k_apply_tpe_tlb) into one LDS region that the cross-wave face
+// exchange reuses afterwards.  Lattice blocks only (RM 1 regular, 3 lattice-map), p = 2.
+template <int D, int Q, bool SPLIT, int RM, bool MASS>
+__global__ void __launch_bounds__(256, 2)
+k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
+               const double *__restrict__ qdd, const double *__restrict__ qdm,
+               const double *__restrict__ x, const double *__restrict__ xg, const double *__restrict__ tsn,
+               double *__restrict__ y, double *__restrict__ yg, const Basis1D b, const Basis1D bw,
+               const int *__restrict__ lane_flags, double *__restrict__ part, const int *__restrict__ treg,
+               int pstride, const int *__restrict__ lmap)
+{
+   static_assert(RM == 1 || RM == 3, "lattice blocks only");
+   static_assert(D == 3 && Q == 4, "p = 2");
+   constexpr int ND = D * D * D, NR = Q * Q, XR = XwaveRows<D>::R, WPG = 4, P = D - 1;
+   constexpr int NLP = tpe_lattice_points(D);
+   static_assert(2 * NLP <= XR * 64, "x and T' lattices fit a wave's exchange rows");
+   __shared__ double sU[WPG][XR][64];  // per wave: x lattice | T' lattice; then the cross-wave face exchange
+   const int lane = threadIdx.x & 63;
+   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+   const int blk = blk_begin + (int)blockIdx.x * WPG + w;
+   const bool wave_on = blk < blk_end;  // wave-uniform; every wave reaches the barriers
+   const int e = blk * 64 + lane;
+   const bool active = wave_on && e < ne;
+   const int *mp = gmap + (size_t)blk * ND * 64 + lane;
+   const int ex = lane & 3, ey = (lane >> 2) & 3, ez = lane >> 4;
+   double *sXL = &sU[w][0][0];
+   double *sTL = sXL + NLP;
+   TpeReg rg = {};
+   const int regf = RM == 1 ? 1 : 2;
+   double Yo[ND];
+#pragma unroll
+   for (int a = 0; a < ND; a++) { Yo[a] = 0.0; }
+   auto ld2 = [&](const double *p) -> v2d { return __builtin_nontemporal_load(reinterpret_cast<const v2d *>(p)); };
+   v2d ce[3];
+   const double *qa = qdm + (size_t)blk * NR * Q * 64 + lane;  // W alpha det J, [blk][q][lane]
+   // three row buffers in rotation, each row issues the row two ahead (the plane loop is unrolled)
+   double ra[3][Q];
+   auto load_row = [&](int row, double (&aq)[Q]) {
+#pragma unroll
+      for (int qx = 0; qx < Q; qx++) { aq[qx] = MASS ? __builtin_nontemporal_load(qa + (size_t)(row * Q + qx) * 64) : 0.0; }
+   };
+   if (wave_on)
+   {
+      const double *qc = qdd + (size_t)blk * 3 * 128 + lane * 2;
+#pragma unroll
+      for (int k = 0; k < 3; k++) { ce[k] = ld2(qc + k * 128); }
+      load_row(0, ra[0]);
+      load_row(1, ra[1]);
+      if (RM == 1)
+      {
+         const int *r = treg + (size_t)blk * 8;  // wave-uniform: scalar loads
+         rg = TpeReg{r[0], r[1], r[2], r[3], r[4]};
+      }
+      const int *lm = lmap + (size_t)blk * NLP;
+#pragma unroll
+      for (int k = 0; k < (NLP + 63) / 64; k++)
+      {
+         const int j = lane + 64 * k;
+         if (j < NLP)
+         {
+            int d;
+            if (RM == 3) { d = bdof(lm[j]); }
+            else
+            {
+               const unsigned v = lattice_xyz<D>(j);
+               d = rg.base + (int)(v & 31) * rg.sx + (int)((v >> 5) & 31) * rg.sy + (int)(v >> 10) * rg.sz;
+            }
+            sXL[j] = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
+            sTL[j] = tsn[d];
+         }
+      }
+   }
+   __syncthreads();  // the lattices are read by every lane of the wave
+   if (wave_on)
+   {
+      auto lane_base = [&](int cx, int cy) {
+         const int nx = tpe_lattice_class_n(cx), ny = tpe_lattice_class_n(cy);
+         return (ez * ny + ey) * nx + ex;
+      };
+      auto plane = [&](const int qz) {
+         double bz[D], gz[D], wz[D];
+#pragma unroll
+         for (int dz = 0; dz < D; dz++)
+         {
+            bz[dz] = b.B[qz + MQ * dz]; gz[dz] = b.G[qz + MQ * dz]; wz[dz] = bw.B[qz + MQ * dz];
+         }
+         double ZB[D][D], ZG[D][D], ZT[D][D], SB[D][D], SG[D][D];
+#pragma unroll
+         for (int dy = 0; dy < D; dy++)
+#pragma unroll
+            for (int dx = 0; dx < D; dx++)
+            {
+               int lb = lane_base(dx % P, dy % P);
+               asm volatile("" : "+v"(lb));  // the plane re-reads the lattices (no 54 live values)
+               double zb = 0.0, zg = 0.0, zt = 0.0;
+#pragma unroll
+               for (int dz = 0; dz < D; dz++)
+               {
+                  const int cx = dx % P, cy = dy % P, cz = dz % P;
+                  const int nx = tpe_lattice_class_n(cx), ny = tpe_lattice_class_n(cy);
+                  const int sl = tpe_lattice_class_off(D, cx, cy, cz) + ((dz / P) * ny + dy / P) * nx + dx / P;
+                  const double c = sXL[lb + sl], t = sTL[lb + sl];
+                  zb += bz[dz] * c;
+                  zg += gz[dz] * c;
+                  zt += wz[dz] * t;
+               }
+               ZB[dy][dx] = zb; ZG[dy][dx] = zg; ZT[dy][dx] = zt;
+               SB[dy][dx] = 0.0; SG[dy][dx] = 0.0;
+            }
+         auto row_body = [&](const int qy, const double (&cur)[Q]) {
+            double Y00[D], Y01[D], Y10[D], YT[D];
+#pragma unroll
+            for (int dx = 0; dx < D; dx++)
+            {
+               double u = 0.0, v = 0.0, wv = 0.0, t = 0.0;
+#pragma unroll
+               for (int dy = 0; dy < D; dy++)
+               {
+                  const double by = b.B[qy + MQ * dy], gy = b.G[qy + MQ * dy], wy = bw.B[qy + MQ * dy];
+                  u += by * ZB[dy][dx];
+                  v += gy * ZB[dy][dx];
+                  wv += by * ZG[dy][dx];
+                  t += wy * ZT[dy][dx];
+               }
+               Y00[dx] = u; Y01[dx] = v; Y10[dx] = wv; YT[dx] = t;
+            }
+            double T0[D], T1[D], T2[D];
+#pragma unroll
+            for (int dx = 0; dx < D; dx++) { T0[dx] = 0.0; T1[dx] = 0.0; T2[dx] = 0.0; }
+#pragma unroll
+            for (int qx = 0; qx < Q; qx++)
+            {
+               double u = 0.0, ux = 0.0, uy = 0.0, uz = 0.0, wb = 0.0;
+#pragma unroll
+               for (int dx = 0; dx < D; dx++)
+               {
+                  const double bq = b.B[qx + MQ * dx], gq = b.G[qx + MQ * dx], wq = bw.B[qx + MQ * dx];
+                  u += bq * Y00[dx];
+                  ux += gq * Y00[dx];
+                  uy += bq * Y01[dx];
+                  uz += bq * Y10[dx];
+                  wb += wq * YT[dx];  // W_q beta(x_q)
+               }
+               const double m = MASS ? cur[qx] * u : 0.0;  // W alpha det J u
+               double fx = ce[0].x * ux, fy = ce[0].y * ux, fz = ce[1].x * ux;
+               fx += ce[0].y * uy; fy += ce[1].y * uy; fz += ce[2].x * uy;
+               fx += ce[1].x * uz; fy += ce[2].x * uz; fz += ce[2].y * uz;
+               fx *= wb; fy *= wb; fz *= wb;
+#pragma unroll
+               for (int dx = 0; dx < D; dx++)
+               {
+                  const double bq = b.B[qx + MQ * dx], gq = b.G[qx + MQ * dx];
+                  if (MASS) { T0[dx] += bq * m; }
+                  T0[dx] += gq * fx;
+                  T1[dx] += bq * fy;
+                  T2[dx] += bq * fz;
+               }
+            }
+#pragma unroll
+            for (int dy = 0; dy < D; dy++)
+            {
+               const double by = b.B[qy + MQ * dy], gy = b.G[qy + MQ * dy];
+#pragma unroll
+               for (int dx = 0; dx < D; dx++)
+               {
+                  SB[dy][dx] += by * T0[dx];
+                  SB[dy][dx] += gy * T1[dx];
+                  SG[dy][dx] += by * T2[dx];
+               }
+            }
+         };
+#pragma unroll
+         for (int qy = 0; qy < Q; qy++)
+         {
+            const int row = qz * Q + qy;
+            __builtin_amdgcn_sched_barrier(0);  // rows stay in program order (no interleaving)
+            load_row(row + 2 < NR ? row + 2 : NR - 1, ra[(row + 2) % 3]);  // (the last rows reload the final row)
+            row_body(qy, ra[row % 3]);
+         }
+#pragma unroll
+         for (int dz = 0; dz < D; dz++)
+#pragma unroll
+            for (int dy = 0; dy < D; dy++)
+#pragma unroll
+               for (int dx = 0; dx < D; dx++)
+               {
+                  Yo[(dz * D + dy) * D + dx] += bz[dz] * SB[dy][dx];
+                  Yo[(dz * D + dy) * D + dx] += gz[dz] * SG[dy][dx];
+               }
+      };
+#pragma unroll
+      for (int qz = 0; qz < Q; qz++) { plane(qz); }
+   }  // wave_on
+   tpe_assemble_store<D, SPLIT, false, true, true>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0, blk, lane,
+                                                  active, n_owned, y, yg, part, &sU[0][0][0], w, wave_on, rg, regf,
                                                   pstride, lmap ? lmap + (size_t)blk * NLP : nullptr);
 }
 
@@ -1259,6 +1505,27 @@ void launch_tpe(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipS
 #undef ECM2_TL
       }
       else { ECM2_VERIFY(false, ERR_INTERNAL, "TRILINEAR qdata needs the diffusion integrator"); }
+      return;
+   }
+   if (a.kind == QLAYOUT_AFFINE && a.tsnap)
+   {
+      // the diffusion coefficient from its temperature snapshot: only W alpha det J per point
+      if constexpr (DIFF && D == 3 && Q == 4)
+      {
+         ECM2_VERIFY(a.pw == (MASS ? 1 : 0) && a.treg && (a.treg_all || a.tlat_all), ERR_INTERNAL,
+                     "coefficient snapshot needs lattice blocks and the mass-only point values");
+         Basis1D bw = b;  // (w B): the weight-scaled interpolation of T'
+         for (int d = 0; d < MAX_D1D; d++)
+            for (int q = 0; q < MAX_Q1D; q++) { bw.B[q + MQ * d] = a.qw[q] * b.B[q + MQ * d]; }
+#define ECM2_TS(RM)                                                                                              \
+   hipLaunchKernelGGL((k_apply_tpe_ts<3, 4, SPLIT, RM, MASS>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end,      \
+                      a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.tsnap, a.y, a.yg, b, bw, a.lane_flags, a.part,  \
+                      a.treg, a.part_stride, a.lmap)
+         if (a.treg_all) { ECM2_TS(1); }
+         else { ECM2_TS(3); }
+#undef ECM2_TS
+      }
+      else { ECM2_VERIFY(false, ERR_INTERNAL, "coefficient snapshot: p = 2 forms with the diffusion integrator"); }
       return;
    }
    if (a.kind == QLAYOUT_AFFINE)

@@ -70,6 +70,10 @@ struct QLayout
    // AFFINE / TRILINEAR point values: 2 = the pair (diffusion factor, mass factor), 1 = the
    // diffusion factor alone (a form without a MassIntegrator: [blk][q][lane], 8 B per point)
    int pw = 2;
+   // AFFINE (p = 2, lattice blocks) with the diffusion coefficient an affine law of an H1 field:
+   // the kernel interpolates a snapshot of the field (ApplyArgs::tsnap) instead of reading W beta,
+   // and the point values are W alpha det J alone (pw = 1; pw = 0 without a MassIntegrator)
+   int tsnap = 0;
    const int *pos = nullptr;  // device: caller element -> internal position (BLOCKED)
    const int *perm = nullptr; // device: internal position -> caller element (BLOCKED)
    size_t diff_size() const
@@ -112,7 +116,9 @@ struct QLayout
 // 9 = general, row-major M(i,j) at 3 i + j (CoefficientVector::ProjectTranspose, coefficient.cpp:2093-2123).
 enum CoeffKind : int { COEFF_CONSTANT = 0, COEFF_QUAD = 1, COEFF_GRIDFUNC_AFFINE = 2, COEFF_GRIDFUNC_PERFUSION = 3,
                        COEFF_QUAD_VECTOR = 4, COEFF_QUAD_SYMMATRIX = 5, COEFF_QUAD_MATRIX = 6,
-                       COEFF_CONST_VECTOR = 7, COEFF_CONST_SYMMATRIX = 8, COEFF_CONST_MATRIX = 9 };
+                       COEFF_CONST_VECTOR = 7, COEFF_CONST_SYMMATRIX = 8, COEFF_CONST_MATRIX = 9,
+                       // internal: the field's own values (a coefficient snapshot, the law already applied)
+                       COEFF_GRIDFUNC_VALUE = -2 };
 struct CoeffDesc
 {
    int kind = COEFF_CONSTANT;
@@ -123,7 +129,10 @@ struct CoeffDesc
    double scale = 1.0, slope = 0.0, t_ref = 0.0;  // GRIDFUNC_AFFINE
    double p[6] = {0, 0, 0, 0, 0, 0};              // GRIDFUNC_PERFUSION
    const double *emask = nullptr; // device [ne] element weights of an attribute-marked integrator (form-owned)
-   bool gridfunc() const { return kind == COEFF_GRIDFUNC_AFFINE || kind == COEFF_GRIDFUNC_PERFUSION; }
+   bool gridfunc() const
+   {
+      return kind == COEFF_GRIDFUNC_AFFINE || kind == COEFF_GRIDFUNC_PERFUSION || kind == COEFF_GRIDFUNC_VALUE;
+   }
    // values per point: 1 scalar, 3 vector, 6 symmetric matrix, 9 general matrix
    int dim() const
    {
@@ -147,6 +156,7 @@ struct CoeffParams  // kernel-argument copy of CoeffDesc::p
 __host__ __device__ inline double coeff_law(int kind, double T, double scale, double slope, double t_ref,
                                             const double *p)
 {
+   if (kind == COEFF_GRIDFUNC_VALUE) { return T; }
    if (kind == COEFF_GRIDFUNC_PERFUSION)
    {
       const double r = 1.0 + p[3] * (T - p[4]);
@@ -171,6 +181,10 @@ struct ApplyArgs
    int part_stride = 0;             // p <= 2 partial slots per block (27 * 64, or the lattice surface when treg_all)
    const int *lmap = nullptr;       // device [blk][tpe_lattice_points]: lattice-slot blocks' lattice maps, or null
    QPts qp = {};                    // TRILINEAR: the quadrature points
+   // AFFINE with a coefficient snapshot (QLayout::tsnap): T' = A + B T at the form's L-vector dofs
+   // (the diffusion coefficient's law applied to its field at Assemble) and the 1D Gauss weights
+   const double *tsnap = nullptr;
+   double qw[MAX_Q1D] = {};
    int xwave = 0;                   // the merge plan has cross-wave faces (AFFINE / TRILINEAR forms)
    const int *gmap = nullptr;
    const double *qdd = nullptr, *qdm = nullptr;
@@ -287,10 +301,12 @@ void setup_trilinear(const QLayout &L, int Q, const double *enodes, const double
                      double *qd_geo, double *qd_pair, hipStream_t s);
 // Trilinear-map coefficients of every element from MFEM-layout Jacobians (cfit [ne][21]); false
 // when some element's Jacobians are not those of a trilinear map (1e-13; synchronises s).
+// out[i] = A + B T[i] (i < n): the coefficient snapshot of an affine law of an H1 field.
+void affine_snapshot(int n, const double *T, double A, double B, double *out, hipStream_t s);
 bool jacobians_trilinear_fit(int ne, int Q, const QPts &qp, const double *J, double *cfit, hipStream_t s);
 // The BLOCKED per-point qdata of an AFFINE (p <= 2) form (L: its layout; outputs sized as BLOCKED).
 void affine_expand(const QLayout &L, int Q, const double *qd_fac, const double *qd_pair, double *qd_diff,
-                   double *qd_mass, hipStream_t s);
+                   double *qd_mass, hipStream_t s, const double *qm1 = nullptr);
 // The BLOCKED per-point qdata of a TRILINEAR form (L: its layout; outputs sized as BLOCKED).
 void trilinear_expand(const QLayout &L, int Q, const double *qd_geo, const double *qd_pair, const QPts &qp,
                       double *qd_diff, double *qd_mass, hipStream_t s);

@@ -106,6 +106,12 @@ void PAForm::set_geometry_compression(bool on)
    assembled_ = false;
 }
 
+void PAForm::set_coefficient_snapshot(bool on)
+{
+   tsnap_pref_ = on;
+   assembled_ = false;
+}
+
 void PAForm::set_block_splits(const std::vector<int> &splits)
 {
    for (int b : splits) { ECM2_VERIFY(b >= 0 && b <= layout_.nblk(), ERR_ARG, "block split " << b << " out of range"); }
@@ -1125,6 +1131,23 @@ void PAForm::assemble(hipStream_t s)
       part_.resize(std::max<size_t>(1, (size_t)part_line_off_ + (n_left_ ? (size_t)ne_ * ND_ : 0)));
    }
    else { part_.resize((size_t)layout_.nblk() * part_stride_); }
+   // Coefficient snapshot (k_apply_tpe_ts): the diffusion coefficient an affine law of an H1 field
+   // on this space (beta = scale (1 + slope (T - t_ref)), AffineGridFunctionCoefficient), AFFINE
+   // geometry, p = 2, every block a lattice brick, no attribute marker on the diffusion integrator
+   layout_.tsnap = 0;
+   tsnap_.resize(0);
+   if (tsnap_pref_ && layout_.kind == QLAYOUT_AFFINE && resolved_mode_ == KERNEL_TPE && D_ == 3 && Q_ == 4 &&
+       (treg_all_ || tlat_all_) && have_diff_ && cdiff_.kind == COEFF_GRIDFUNC_AFFINE && cdiff_.lvec &&
+       !marked_[INTEG_DIFFUSION])
+   {
+      layout_.tsnap = 1;
+      layout_.pw = have_mass_ ? 1 : 0;
+      // T' = A + B T at every dof (the interpolated T' is the law at the point: the basis sums to
+      // 1), taken here only: later setups (the marker diagonal's) keep the Assemble-time field
+      const double A = cdiff_.scale * (1.0 - cdiff_.slope * cdiff_.t_ref), B = cdiff_.scale * cdiff_.slope;
+      tsnap_.resize(std::max(1, ndofs_));
+      kern::affine_snapshot(ndofs_, cdiff_.lvec, A, B, tsnap_.data(), s);
+   }
    setup_qdata(s, nullptr);
    assembled_ = true;
    gen_++;
@@ -1144,6 +1167,18 @@ std::vector<double> PAForm::marker_weights(int k) const
       w[e] = (a > 0 && marker_[k][a - 1] != 0) ? 1.0 : 0.0;
    }
    return w;
+}
+
+const double *PAForm::coeff_points(const CoeffDesc &c, DeviceArray<double> &tmp, hipStream_t s) const
+{
+   if (c.quad_values()) { return c.quad; }
+   if (c.gridfunc())
+   {
+      tmp.resize((size_t)ne_ * NQ_);
+      kern::coeff_gridfunc(ne_, D_, Q_, gmap_.data(), basis_, btab(), c, tmp.data(), s);
+      return tmp.data();
+   }
+   return nullptr;
 }
 
 void PAForm::setup_qdata(hipStream_t s, const std::pair<int, std::vector<double>> *wover)
@@ -1188,18 +1223,9 @@ void PAForm::setup_qdata(hipStream_t s, const std::pair<int, std::vector<double>
    }
 
    // Coefficient values at quadrature points (CoefficientVector::Project).
-   auto coeff_values = [&](const CoeffDesc &c, DeviceArray<double> &tmp) -> const double * {
-      if (c.quad_values()) { return c.quad; }
-      if (c.gridfunc())
-      {
-         tmp.resize((size_t)ne_ * NQ_);
-         kern::coeff_gridfunc(ne_, D_, Q_, gmap_.data(), basis_, btab(), c, tmp.data(), s);
-         return tmp.data();
-      }
-      return nullptr;
-   };
-   const double *cm_q = have_mass_ ? coeff_values(cmass_, ctmp_m_) : nullptr;
-   const double *cd_q = have_diff_ ? coeff_values(cdiff_, ctmp_d_) : nullptr;
+   const double *cm_q = have_mass_ ? coeff_points(cmass_, ctmp_m_, s) : nullptr;
+   const double *cd_q = have_diff_ && !layout_.tsnap ? coeff_points(cdiff_, ctmp_d_, s) : nullptr;
+
    const CoeffDesc *cm = have_mass_ ? &cmass_ : nullptr;
    const CoeffDesc *cd = have_diff_ ? &cdiff_ : nullptr;
    if (layout_.affine())
@@ -1385,7 +1411,8 @@ ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, doubl
    a.treg_all = treg_all_ ? 1 : 0;
    a.tlat_all = tlat_all_ ? 1 : 0;
    a.lmap = lmap_.size() ? lmap_.data() : nullptr;
-   for (int q = 0; q < Q_ && q < MAX_Q1D; q++) { a.qp.x[q] = maps_.qpts[q]; }
+   for (int q = 0; q < Q_ && q < MAX_Q1D; q++) { a.qp.x[q] = maps_.qpts[q]; a.qw[q] = maps_.qw1[q]; }
+   a.tsnap = layout_.tsnap ? tsnap_.data() : nullptr;
    a.xwave = (layout_.kind == QLAYOUT_AFFINE || layout_.kind == QLAYOUT_TRILINEAR) ? 1 : 0;
    a.part_stride = part_stride_;
    a.gmap = (resolved_mode_ == KERNEL_TPE) ? gmap_blk_.data()
@@ -1427,7 +1454,7 @@ void PAForm::apply_blocks(const double *x, const double *xg, double *y, double *
                                                           << ") cuts a brick: declare the split with set_block_splits");
    }
    ApplyArgs a = apply_args(x, xg, y, yg, b0, b1);
-   a.latency = latency && layout_.kind == QLAYOUT_AFFINE && have_mass_ && have_diff_;
+   a.latency = latency && layout_.kind == QLAYOUT_AFFINE && have_mass_ && have_diff_ && !layout_.tsnap;
    if (resolved_mode_ == KERNEL_TPE)
    {
       kern::apply_tpe(D_, Q_, have_mass_, have_diff_, a, basis_, rowtab_.data(), s);
@@ -1529,6 +1556,30 @@ void PAForm::expand_compressed(DeviceArray<double> &fd, DeviceArray<double> &fm,
    }
    QPts qp = {};
    for (int q = 0; q < Q_ && q < MAX_Q1D; q++) { qp.x[q] = maps_.qpts[q]; }
+   if (layout_.tsnap)
+   {
+      // the AFFINE pairs with W beta at the points (the coefficient evaluated as the reference's
+      // setup does), then their BLOCKED expansion
+      // beta at the points from the snapshot (the field as Assemble saw it, the law applied), the
+      // mass values as stored
+      QLayout La = layout_;
+      La.tsnap = 0;
+      La.pw = 1;
+      DeviceArray<double> fac, pair, ctd;
+      fac.resize(La.diff_size());
+      pair.resize(La.mass_size());
+      if (ne_ % kElemBlock) { ECM2_HIP(hipMemsetAsync(pair.data(), 0, pair.bytes(), s)); }
+      CoeffDesc cs = cdiff_;
+      cs.kind = COEFF_GRIDFUNC_VALUE;
+      cs.lvec = tsnap_.data();
+      const double *cd_q = coeff_points(cs, ctd, s);
+      kern::setup_affine(La, Q_, jac_ ? nullptr : enodes_.data(), jac_, W_.data(), nullptr, &cs, nullptr, cd_q,
+                         fac.data(), pair.data(), s);
+      kern::affine_expand(La, Q_, fac.data(), pair.data(), fd.data(), fm.data(), s,
+                          have_mass_ ? qd_mass_.data() : nullptr);
+      ECM2_HIP(hipStreamSynchronize(s));  // the temporaries are freed on return
+      return;
+   }
    if (layout_.trilinear())
    {
       kern::trilinear_expand(layout_, Q_, qd_diff_.data(), qd_mass_.data(), qp, fd.data(), fm.data(), s);

@@ -68,8 +68,14 @@ public:
    // parallelepiped (checked on the corners) and both integrators are present: on by default.
    void set_geometry_compression(bool on);
    bool affine_geometry() const { return affine_; }
-   // bytes of quadrature data the form stores (diffusion + mass)
-   size_t qdata_bytes() const { return qd_diff_.bytes() + qd_mass_.bytes(); }
+   // Coefficient snapshot (AFFINE, p = 2, lattice blocks, the diffusion coefficient an affine law
+   // of an H1 field, unmarked): the law applied to the field's dofs at Assemble and interpolated by
+   // the kernel, instead of a stored W beta per point.  On by default; coefficient_snapshot() says
+   // whether the last Assemble took it.
+   void set_coefficient_snapshot(bool on);
+   bool coefficient_snapshot() const { return layout_.tsnap != 0; }
+   // bytes of quadrature data the form stores (diffusion + mass + the coefficient snapshot)
+   size_t qdata_bytes() const { return qd_diff_.bytes() + qd_mass_.bytes() + tsnap_.bytes(); }
 
    // Optional element permutation (internal position i <- caller element perm[i]) used by
    // the blocked layout; ORDER_BRICK puts one 4x4x4 brick in each 64-lane wave so the
@@ -182,7 +188,12 @@ private:
    // TRILINEAR(_E) forms and diffusion-only AFFINE(_E) forms: their per-point qdata in the BLOCKED
    // (p <= 2) or NATIVE (p >= 3) layout, expand_kind() (temporaries of the caller) for the
    // diagonal, the E-vector apply and the qdata export
-   bool expand_needed() const { return layout_.trilinear() || (layout_.affine() && layout_.pw == 1); }
+   bool expand_needed() const
+   {
+      return layout_.trilinear() || layout_.tsnap || (layout_.affine() && layout_.pw == 1);
+   }
+   // coefficient values at the quadrature points ([e][q], tmp holds computed ones)
+   const double *coeff_points(const CoeffDesc &c, DeviceArray<double> &tmp, hipStream_t s) const;
    int expand_kind() const { return layout_.blocked() ? QLAYOUT_BLOCKED : QLAYOUT_NATIVE; }
    void expand_compressed(DeviceArray<double> &fd, DeviceArray<double> &fm, hipStream_t s) const;
 
@@ -241,6 +252,8 @@ private:
    int line_bricks_ = -1;           // requested brick mode (set_line_bricks)
    bool affine_ = false;            // every element a parallelepiped (set_element_nodes)
    bool compress_ = true;           // set_geometry_compression
+   bool tsnap_pref_ = true;         // set_coefficient_snapshot
+   DeviceArray<double> tsnap_;      // coefficient snapshot T' = A + B T (local L-vector)
    int latency_from_ = -1;          // set_latency_from
    bool perm_auto_ = false;         // perm_host_ was derived (not the caller's)
    DeviceArray<int> lane_flags_;    // [blk][64] in-wave merge flags

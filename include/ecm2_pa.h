@@ -180,6 +180,15 @@ int ecm2_pa_form_set_jacobians(ecm2_pa_form *f, const double *J);
 #define ECM2_QLAYOUT_NATIVE9 5   /* [e][9][nq] general D_ij (a nonsymmetric matrix coefficient)    */
 #define ECM2_QLAYOUT_TRILINEAR_E 6
 int ecm2_pa_form_set_geometry_compression(ecm2_pa_form *f, int on);
+/* Coefficient snapshot (p = 2, AFFINE layout, every 64-element block a lattice brick, the
+ * diffusion coefficient ECM2_COEFF_GRIDFUNC_AFFINE without an attribute marker): Assemble keeps
+ * T' = scale (1 + slope (T - t_ref)) at the field's dofs and the fused kernel interpolates it at
+ * the quadrature points, instead of storing W beta per point (the reference evaluates the same
+ * coefficient at the points in its setup, coefficient.cpp:2052-2070): 8 B per point fewer.  The
+ * snapshot is taken at Assemble (the reference's assemble-time semantics).  On by default;
+ * ecm2_pa_form_coefficient_snapshot reports whether the last Assemble took it. */
+int ecm2_pa_form_set_coefficient_snapshot(ecm2_pa_form *f, int on);
+int ecm2_pa_form_coefficient_snapshot(const ecm2_pa_form *f, int *on);
 /* BilinearForm::AddDomainIntegrator(new MassIntegrator(Q)) / DiffusionIntegrator(Q)
  * (bilinearform.cpp:231-242).  data: CONSTANT -> data[0] (host);
  * QUAD -> device [ne][nq]; GRIDFUNC_AFFINE -> device L-vector T with

@@ -378,6 +378,77 @@ def test_gridfunction_pennes_coefficient():
     assert relerr(host(y), op.mult(x)) <= RTOL
 
 
+@pytest.mark.parametrize("numbering", [E.NUMBERING_STRUCTURED, E.NUMBERING_ENTITY])
+@pytest.mark.parametrize("mass", ["quad", "none", "marked"])
+def test_coefficient_snapshot(numbering, mass):
+    """AFFINE layout with the diffusion coefficient k(T) evaluated in the kernel from a snapshot of
+    T's dofs (k_apply_tpe_ts): the operator, its diagonal, the E-vector AddMultPA and the
+    reference-layout qdata match the oracle (beta = the affine law of T interpolated at the points,
+    as the reference's setup projects it, qfunction.cpp:73-98 / coefficient.cpp:2052-2070), and the
+    form without the snapshot; with a MassIntegrator, without one, and with a marked one; the
+    snapshot is taken at Assemble (a later change of T does not reach the operator)."""
+    n = 8
+    if numbering == E.NUMBERING_ENTITY:
+        m = E.Mesh.MakeCartesian3D(n, n, n, 1.0, 0.7, 1.3, sfc_ordering=True)
+    else:
+        m = E.Mesh.MakeCartesian3D(n, n, n, 1.0, 0.7, 1.3)
+    if mass == "marked":
+        m.SetAttributes(1 + np.arange(m.GetNE()) % 2)
+    order = 2
+    fes = E.H1Space(m, order, numbering)
+    en = m.element_nodes()
+    q1d = O.default_q1d(order)
+    T = temperature(fes.dof_coords())
+    Td = dev(T)
+    scale, slope, tref = 0.05, 0.0012, 37.0
+    a = alpha_bioheat(O.quad_points(en, q1d))
+    eo = "faces" if numbering == E.NUMBERING_ENTITY else "auto"
+    forms = {}
+    for snap in (True, False):
+        f = E.BilinearForm(fes, element_order=eo, coefficient_snapshot=snap)
+        if mass != "none":
+            mi = E.MassIntegrator(E.QuadratureCoefficient(dev(a.reshape(fes.ne, -1))))
+            f.AddDomainIntegrator(mi, [1, 0] if mass == "marked" else None)
+        f.AddDomainIntegrator(E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(Td, scale, slope, tref)))
+        f.Assemble()
+        assert f.info()["layout"] == E.QLAYOUT_AFFINE
+        assert f.CoefficientSnapshot() == snap
+        forms[snap] = f
+    form = forms[True]
+    nq = q1d ** 3
+    assert form.qdata_bytes() < forms[False].qdata_bytes() - 8 * fes.ne * nq + 8 * fes.ndofs + 1
+    Tq = O.interp_evector(T[fes.gather_map()], order, q1d)
+    beta = scale * (1.0 + slope * (Tq - tref))
+    op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=None if mass == "none" else a, beta=beta)
+    x = np.random.default_rng(17).uniform(-1, 1, fes.ndofs)
+    y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+    y2 = torch.empty_like(y)
+    Td.fill_(1.0e3)  # after Assemble: the snapshot (and the reference's qdata) keep the old T
+    form.Mult(dev(x), y)
+    forms[False].Mult(dev(x), y2)
+    want = op.mult_markers(x, m.GetAttributes(), mass_marker=[1, 0]) if mass == "marked" else op.mult(x)
+    assert relerr(host(y), want) <= RTOL
+    assert relerr(host(y), host(y2)) <= 1e-13
+    d = torch.empty_like(y)
+    form.AssembleDiagonal(d)
+    dwant = op.diagonal_markers(m.GetAttributes(), [("mass", [1, 0]), ("diffusion", None)]) \
+        if mass == "marked" else op.diagonal()
+    assert relerr(host(d), dwant) < 1e-12
+    assert relerr(form.qdata(E.DIFFUSION), op.D) < 1e-12
+    if mass == "quad":
+        assert relerr(form.qdata(E.MASS)[:, 0, :], op.M) < 1e-13
+        xe = np.random.default_rng(18).uniform(-1, 1, (fes.ne, fes.nd))
+        ye = torch.zeros(fes.ne * fes.nd, dtype=torch.float64, device="cuda")
+        form.IntegratorAddMultPA(E.DIFFUSION, dev(xe), ye)
+        assert relerr(host(ye).reshape(fes.ne, fes.nd), O.diffusion_apply(op.B, op.G, op.D, xe)) <= RTOL
+    # a marked diffusion integrator keeps the stored W beta
+    f3 = E.BilinearForm(fes, element_order=eo)
+    f3.AddDomainIntegrator(E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(dev(T), scale, slope, tref)), [1, 1])
+    m.SetAttributes(np.ones(m.GetNE(), dtype=int))
+    f3.Assemble()
+    assert not f3.CoefficientSnapshot()
+
+
 @pytest.mark.parametrize("jacobi", [True, False])
 def test_pcg_matches_oracle(jacobi):
     m = make_mesh("fichera_r1")
@@ -843,6 +914,30 @@ def test_attribute_marker_errors():
     m.SetAttributes(np.full(m.GetNE(), 2))
     with pytest.raises(E.ECM2Error):
         form.Assemble()
+
+
+def test_rejected_duplicate_integrator_keeps_marker():
+    """A second MassIntegrator / DiffusionIntegrator is rejected (ERR_UNSUPPORTED) and leaves the
+    installed integrator, its coefficient and its attribute marker unchanged."""
+    m = make_mesh("cart_bricks")
+    m.SetAttributes(1 + np.arange(m.GetNE()) % 2)
+    fes = E.H1Space(m, 2)
+    en = m.element_nodes()
+    P = O.quad_points(en, O.default_q1d(2))
+    a, c = alpha_bioheat(P), coeff_function(P)
+    form = E.BilinearForm(fes)
+    form.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(a.reshape(fes.ne, -1)))))
+    form.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(dev(c.reshape(fes.ne, -1)))), [1, 0])
+    with pytest.raises(E.ECM2Error):
+        form.AddDomainIntegrator(E.DiffusionIntegrator(E.ConstantCoefficient(9.0)))  # unmarked, other coefficient
+    with pytest.raises(E.ECM2Error):
+        form.AddDomainIntegrator(E.MassIntegrator(E.ConstantCoefficient(9.0)), [0, 1])
+    form.Assemble()
+    x = np.random.default_rng(3).uniform(-1, 1, fes.ndofs)
+    y = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    form.Mult(dev(x), y)
+    op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, 2, alpha=a, beta=c)
+    assert relerr(host(y), op.mult_markers(x, m.GetAttributes(), diff_marker=[1, 0])) <= RTOL
 
 
 @pytest.mark.parametrize("order", [1, 2])

@@ -689,12 +689,6 @@ __device__ __forceinline__ unsigned lattice_xyz(int j)
 // same region then stages the cross-wave face exchange) and every plane adds its z-transpose into
 // them; (c) the per-point pair is (W beta / det J, W alpha det J), so no determinant or division
 // per point.  LDS 78.6 KB per workgroup: two workgroups (8 waves) per CU.
-#ifndef ECM2_TLB_PFD
-#define ECM2_TLB_PFD 2  // rows of point values in flight
-#endif
-#ifndef ECM2_TLB_ZP
-#define ECM2_TLB_ZP 1   // per-plane z partials
-#endif
 template <int D, int Q, bool SPLIT, int RM, int PW = 2>
 __global__ void __launch_bounds__(256, 2)
 k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
@@ -732,7 +726,7 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
       if constexpr (PW == 2) { return ld2(qa + (size_t)q * 128); }
       else { return v2d{__builtin_nontemporal_load(qa + (size_t)q * 64), 0.0}; }
    };
-   v2d ca[Q], cb[Q];  // point values of the rows in flight (cb: the odd rows at prefetch depth 2)
+   v2d ca[Q];  // point values of the row in flight
    auto load_row = [&](int row, v2d (&aq)[Q]) {
 #pragma unroll
       for (int qx = 0; qx < Q; qx++) { aq[qx] = ldp(row * Q + qx); }
@@ -744,7 +738,6 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
 #pragma unroll
       for (int k = 0; k < NCE; k++) { ce[k] = ld2(qc + k * 128); }
       load_row(0, ca);
-      if (ECM2_TLB_PFD == 2) { load_row(1, cb); }
       if (RM == 1)
       {
          const int *r = treg + (size_t)blk * 8;  // wave-uniform: scalar loads
@@ -809,17 +802,13 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
          // the plane's z-forward partials from the lattice (ZB = B_z X, ZG = G_z X): 36 VGPRs that
          // spill 2 values per plane into scratch, against 81 instead of 27 multiply-adds per row
          // when every row re-reads the lattice (profiles/r4/ab_tlz_pf2.txt: kernel -2..-3%)
-         double SB[D][D], SG[D][D];
-#if ECM2_TLB_ZP
-         double ZB[D][D], ZG[D][D];
-#endif
+         double SB[D][D], SG[D][D], ZB[D][D], ZG[D][D];
 #pragma unroll
          for (int dy = 0; dy < D; dy++)
 #pragma unroll
             for (int dx = 0; dx < D; dx++)
             {
                SB[dy][dx] = 0.0; SG[dy][dx] = 0.0;
-#if ECM2_TLB_ZP
                int lb = lane_base(dx % P, dy % P);
                asm volatile("" : "+v"(lb));
                double zb = 0.0, zg = 0.0;
@@ -834,7 +823,6 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
                   zg += gz[dz] * c;
                }
                ZB[dy][dx] = zb; ZG[dy][dx] = zg;
-#endif
             }
          auto row_body = [&](const int qy, v2d (&cur)[Q], const int next_row) {
             double Y00[D], Y01[D], Y10[D];
@@ -846,24 +834,7 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
                for (int dy = 0; dy < D; dy++)
                {
                   const double by = b.B[qy + MQ * dy], gy = b.G[qy + MQ * dy];
-#if ECM2_TLB_ZP
                   const double zb = ZB[dy][dx], zg = ZG[dy][dx];
-#else
-                  // z-forward straight from the lattice, one column at a time (no 27 live values)
-                  int lb = lane_base(dx % P, dy % P);
-                  asm volatile("" : "+v"(lb));
-                  double zb = 0.0, zg = 0.0;
-#pragma unroll
-                  for (int dz = 0; dz < D; dz++)
-                  {
-                     const int cx = dx % P, cy = dy % P, cz = dz % P;
-                     const int nx = tpe_lattice_class_n(cx), ny = tpe_lattice_class_n(cy);
-                     const int sl = tpe_lattice_class_off(D, cx, cy, cz) + ((dz / P) * ny + dy / P) * nx + dx / P;
-                     const double c = sXL[w][lb + sl];
-                     zb += bz[dz] * c;
-                     zg += gz[dz] * c;
-                  }
-#endif
                   u += by * zb;
                   v += gy * zb;
                   wv += by * zg;
@@ -899,7 +870,8 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
                   uz += bq * Y10[dx];
                }
                const v2d sa = cur[qx];
-               // the pair of this point ECM2_TLB_PFD rows ahead goes into the slot just read
+               // the next row's pair of this point goes into the slot just read: one row in flight
+               // (two rows, in two buffers: +3% kernel time, profiles/r4/ab_pfd.txt)
                cur[qx] = ldp(next_row * Q + qx);
                const double xi = qp.x[qx];
                // J = [ja | jb | jc] (rows: coordinates), adj(J) rows A1., A2., A3.
@@ -958,10 +930,8 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
          for (int qy = 0; qy < Q; qy++)
          {
             const int row = qz * Q + qy;
-            const int nrow = row + ECM2_TLB_PFD < NR ? row + ECM2_TLB_PFD : NR - 1;  // (the last rows reload the last)
             __builtin_amdgcn_sched_barrier(0);  // rows stay in program order (no interleaved live ranges)
-            if (ECM2_TLB_PFD == 1 || qy % 2 == 0) { row_body(qy, ca, nrow); }
-            else { row_body(qy, cb, nrow); }
+            row_body(qy, ca, row + 1 < NR ? row + 1 : NR - 1);  // (the last row reloads itself: exact wait counts)
          }
          // the plane's z-transpose into the outputs (private [a][lane] slots: same-lane RMW)
 #pragma unroll
@@ -1013,7 +983,7 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
    constexpr int ND = D * D * D, NR = Q * Q, XR = XwaveRows<D>::R, WPG = 4, P = D - 1;
    constexpr int NLP = tpe_lattice_points(D);
    static_assert(2 * NLP <= XR * 64, "x and T' lattices fit a wave's exchange rows");
-   __shared__ double sU[WPG][XR][64];  // per wave: x lattice | T' lattice; then the cross-wave face exchange
+   __shared__ double sU[WPG][XR][64];  // per wave: (x, T') lattice pairs; then the cross-wave face exchange
    const int lane = threadIdx.x & 63;
    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
    const int blk = blk_begin + (int)blockIdx.x * WPG + w;
@@ -1022,8 +992,9 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
    const bool active = wave_on && e < ne;
    const int *mp = gmap + (size_t)blk * ND * 64 + lane;
    const int ex = lane & 3, ey = (lane >> 2) & 3, ez = lane >> 4;
-   double *sXL = &sU[w][0][0];
-   double *sTL = sXL + NLP;
+   // (x, T') pairs per lattice slot: one 16-byte LDS read per point (two 8-byte arrays: +3.5% kernel
+   // time, profiles/r4/ab_pfd.txt)
+   v2d *sPL = reinterpret_cast<v2d *>(&sU[w][0][0]);
    TpeReg rg = {};
    const int regf = RM == 1 ? 1 : 2;
    double Yo[ND];
@@ -1064,8 +1035,7 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                const unsigned v = lattice_xyz<D>(j);
                d = rg.base + (int)(v & 31) * rg.sx + (int)((v >> 5) & 31) * rg.sy + (int)(v >> 10) * rg.sz;
             }
-            sXL[j] = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
-            sTL[j] = tsn[d];
+            sPL[j] = v2d{(!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned], tsn[d]};
          }
       }
    }
@@ -1098,7 +1068,8 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                   const int cx = dx % P, cy = dy % P, cz = dz % P;
                   const int nx = tpe_lattice_class_n(cx), ny = tpe_lattice_class_n(cy);
                   const int sl = tpe_lattice_class_off(D, cx, cy, cz) + ((dz / P) * ny + dy / P) * nx + dx / P;
-                  const double c = sXL[lb + sl], t = sTL[lb + sl];
+                  const v2d ct = sPL[lb + sl];
+                  const double c = ct.x, t = ct.y;
                   zb += bz[dz] * c;
                   zg += gz[dz] * c;
                   zt += wz[dz] * t;

@@ -3,10 +3,11 @@
 # the FETCH_SIZE and WRITE_SIZE passes (separate: TCC slots), reduced (pmc_reduce.py) and pinned
 # with provenance (pmc_pin.py; COMMIT = the tree's commit), then the bench line that reads the pin.
 # Usage: COMMIT=<sha> bash profiles/collect_r4.sh <set: a | b | d>
-#   a: c4 (structured, affine: the headline), c4ent (the reference's numbering), c4tri (trilinear
-#      mesh: the lattice TRILINEAR kernel), c4 full per-point layout (blocked)
+#   a: c4 (structured, affine + the k(T) coefficient snapshot: the headline), c4ent (the reference's
+#      numbering, also with the snapshot), c4tri (trilinear mesh: the lattice TRILINEAR kernel), c4 full
+#      per-point layout (blocked)
 #   d: c4enttrijac (the drop-in configuration: reference numbering + trilinear mesh + MFEM Jacobians)
-#   b: c5 (bricks, affine_e), c3 (fichera r6)
+#   b: c5 (bricks, affine_e), c5tri (trilinear mesh, trilinear_e), c3 (fichera r6)
 set -uo pipefail
 SET=${1:-a}
 O=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/collect_r4
@@ -30,13 +31,14 @@ one() {  # tag layout kernel_key bench-args...
   echo "$tag: $(tail -1 "$O/bench_$tag.json" | cut -c1-160)"
 }
 if [ "$SET" = a ]; then
-  one c4 affine apply --workload c4 --steps 50 --warmup 5 || exit 1
-  one c4ent affine apply --workload c4 --numbering entity --steps 50 --warmup 5 || exit 1
+  one c4 affine_ts apply --workload c4 --steps 50 --warmup 5 || exit 1
+  one c4ent affine_ts apply --workload c4 --numbering entity --steps 50 --warmup 5 || exit 1
   one c4tri trilinear apply --workload c4 --mesh trilinear --steps 30 --warmup 5 || exit 1
   one c4_full blocked apply --workload c4 --geometry full --steps 30 --warmup 5 || exit 1
 elif [ "$SET" = d ]; then
   one c4enttrijac trilinear apply --workload c4 --numbering entity --mesh trilinear --geometry-input jacobians --steps 30 --warmup 5 || exit 1
 else
   one c5 affine_e apply_brick --workload c5 --steps 30 --warmup 5 || exit 1
+  one c5tri trilinear_e apply_brick --workload c5 --mesh trilinear --steps 30 --warmup 5 || exit 1
   one c3 affine apply --workload c3 --steps 30 --warmup 5 || exit 1
 fi

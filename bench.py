@@ -35,6 +35,17 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+PEAK_FP64_TFLOPS = 78.6  # MI355X FP64 vector (and matrix) peak, dense
+
+
+def alg_flops(order, ne):
+    """SURVEY §8(d)'s algorithmic flops of one Mult (2 x the sum-factorised MACs per element:
+    diffusion 2D^3Q + 3D^2Q^2 + 3Q^3D + 9Q^3 + 3Q^3D + 3Q^2D^2 + 3D^3Q, mass 2(D^3Q + D^2Q^2 + DQ^3)
+    + Q^3); C4: 10.29 GF, C5: 14.62 GF."""
+    D, Q = order + 1, order + 2
+    dif = 2 * D**3 * Q + 3 * D**2 * Q**2 + 3 * Q**3 * D + 9 * Q**3 + 3 * Q**3 * D + 3 * Q**2 * D**2 + 3 * D**3 * Q
+    mas = 2 * (D**3 * Q + D**2 * Q**2 + D * Q**3) + Q**3
+    return 2.0 * (dif + mas) * ne
 METRIC = "MDoF/s on PA diffusion+mass Mult, hex p=2; % HBM roofline at 1/2/4/8 GPUs"
 
 
@@ -246,7 +257,7 @@ def pmc_pin(workload, world, layout):
     return pin.get("hbm_bytes_per_launch"), prov
 
 
-def roofline(workload, world, layout, kms, alg_bytes, mbytes, stream, use_pin=True):
+def roofline(workload, world, layout, kms, alg_bytes, mbytes, stream, use_pin=True, flops=None):
     # a pin holds the traffic of one configuration (the workload's default size, one kernel per
     # GPU): anything else reports the formulation's minimum bytes instead
     traffic, prov = pmc_pin(workload, world, layout) if use_pin else (None, None)
@@ -269,6 +280,11 @@ def roofline(workload, world, layout, kms, alg_bytes, mbytes, stream, use_pin=Tr
         "stream_copy_gbs": stream[0] if stream else None,
         "stream_read_gbs": stream[1] if stream else None,
         "frac_of_stream": round(achieved / max(stream), 4) if stream else None,
+        # the second roof: SURVEY §8(d)'s algorithmic FP64 flops per launch over the same time (the
+        # compressed layouts and the coefficient snapshot leave kernels between the two roofs)
+        "fp64": ({"achieved": round(flops / (kms * 1e-3) / 1e12, 2), "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                  "frac": round(flops / (kms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS, 4),
+                  "algorithmic_flops_per_launch": flops} if flops else None),
     }
 
 
@@ -432,7 +448,8 @@ def main():
                 "ms_per_step": round(dtf / args.steps * 1e3, 5),
                 "lattice_units": [lat, units], "summation_runs": runs,
                 "roofline": roofline(args.workload + tag, 1, lay, kf, f.algorithmic_bytes(),
-                                     min_bytes(f, fes_s.ne, nd, fes_s.ndofs), None, use_pin=pin_ok),
+                                     min_bytes(f, fes_s.ne, nd, fes_s.ndofs), None, use_pin=pin_ok,
+                                     flops=alg_flops(order, fes_s.ne)),
                 "note": note}
 
     dl.at("assemble")
@@ -604,7 +621,7 @@ def main():
                                 (f"loopback {'z-slabs' if args.partition == 'slabs' else 'boxes'} x{args.loopback} on one GPU" if args.loopback > 1 else "single GPU")),
             },
             "roofline": roofline(args.workload + variant, world, layout, kavg_ms, bytes_total / world,
-                                 mbytes_total / world, stream, use_pin=pin_ok),
+                                 mbytes_total / world, stream, use_pin=pin_ok, flops=alg_flops(order, ne_own)),
             "cpu_baseline": cpu,
         }
         line.update(subs)

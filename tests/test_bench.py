@@ -59,9 +59,14 @@ def test_bench_single_gpu_line():
     # value = ndofs * steps / time
     assert b["value"] == pytest.approx(b["config"]["ndofs"] / (b["ms_per_step"] * 1e-3) / 1e6, rel=1e-3)
     assert b["config"]["numbering"].startswith("structured") and b["config"]["mesh"] == "affine"
-    # the same run's variants: the reference's numbering (same layout) and a trilinear mesh (per-point qdata)
-    assert b["entity_numbering"]["value"] > 0 and b["entity_numbering"]["qdata_layout"] == "affine"
+    # the same run's variants: the reference's numbering (same layout: AFFINE with the k(T) snapshot on a
+    # brick-tiled mesh), a trilinear mesh (TRILINEAR) and the drop-in configuration (+ MFEM Jacobians)
+    assert b["entity_numbering"]["value"] > 0 and b["entity_numbering"]["qdata_layout"] == "affine_ts"
     assert b["trilinear"]["value"] > 0 and b["trilinear"]["qdata_layout"] == "trilinear"
+    assert b["drop_in"]["value"] > 0 and b["drop_in"]["qdata_layout"] == "trilinear"
+    s = run_bench(*SMALL, "--variants", "0", "--coefficient-snapshot", "0")
+    assert s["value"] > 0 and "entity_numbering" not in s
+    assert b["config"]["qdata_layout"] == "affine_ts" and s["config"]["qdata_layout"] == "affine"
     e = run_bench(*SMALL, "--numbering", "entity", "--variants", "0")
     assert e["config"]["numbering"].startswith("entity") and "entity_numbering" not in e
 

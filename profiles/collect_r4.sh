@@ -40,5 +40,5 @@ elif [ "$SET" = d ]; then
 else
   one c5 affine_e apply_brick --workload c5 --steps 30 --warmup 5 || exit 1
   one c5tri trilinear_e apply_brick --workload c5 --mesh trilinear --steps 30 --warmup 5 || exit 1
-  one c3 affine apply --workload c3 --steps 30 --warmup 5 || exit 1
+  one c3 affine_ts apply --workload c3 --steps 30 --warmup 5 || exit 1
 fi

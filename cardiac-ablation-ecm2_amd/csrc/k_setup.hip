@@ -735,6 +735,24 @@ __global__ void __launch_bounds__(256) k_affine_snapshot(int n, const double *__
    if (i < n) { out[i] = A + B * T[i]; }
 }
 
+// The same snapshot in block lattice-slot order, out[b][j] = A + B T[lmap[b][j]] (lattice-map blocks:
+// the snapshot kernel then reads it contiguously instead of a second dependent gather), and back to
+// dof order (every dof is some block's lattice point; shared points carry equal values).
+__global__ void __launch_bounds__(256) k_affine_snapshot_lattice(long n, int nlp, const int *__restrict__ lmap,
+                                                                 const double *__restrict__ T, double A, double B,
+                                                                 double *__restrict__ out)
+{
+   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { out[i] = A + B * T[lmap[i] & 0x3fffffff]; }
+}
+
+__global__ void __launch_bounds__(256) k_lattice_to_dofs(long n, const int *__restrict__ lmap,
+                                                         const double *__restrict__ v, double *__restrict__ out)
+{
+   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { out[lmap[i] & 0x3fffffff] = v[i]; }
+}
+
 SetupCoef make_setup_coef(const CoeffDesc *c, const double *q)
 {
    SetupCoef s{};
@@ -818,6 +836,23 @@ void affine_snapshot(int n, const double *T, double A, double B, double *out, hi
 {
    if (n == 0) { return; }
    hipLaunchKernelGGL(k_affine_snapshot, dim3(grid_for(n, 256)), dim3(256), 0, s, n, T, A, B, out);
+   ECM2_HIP(hipGetLastError());
+}
+
+void affine_snapshot_lattice(int nblk, int nlp, const int *lmap, const double *T, double A, double B, double *out,
+                             hipStream_t s)
+{
+   const long n = (long)nblk * nlp;
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_affine_snapshot_lattice, dim3(grid_for(n, 256)), dim3(256), 0, s, n, nlp, lmap, T, A, B, out);
+   ECM2_HIP(hipGetLastError());
+}
+
+void lattice_to_dofs(int nblk, int nlp, const int *lmap, const double *v, double *out, hipStream_t s)
+{
+   const long n = (long)nblk * nlp;
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_lattice_to_dofs, dim3(grid_for(n, 256)), dim3(256), 0, s, n, lmap, v, out);
    ECM2_HIP(hipGetLastError());
 }
 

@@ -1035,7 +1035,8 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                const unsigned v = lattice_xyz<D>(j);
                d = rg.base + (int)(v & 31) * rg.sx + (int)((v >> 5) & 31) * rg.sy + (int)(v >> 10) * rg.sz;
             }
-            sPL[j] = v2d{(!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned], tsn[d]};
+            // (lattice-map blocks: the snapshot is stored in their slot order, a contiguous read)
+            sPL[j] = v2d{(!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned], RM == 3 ? tsn[(size_t)blk * NLP + j] : tsn[d]};
          }
       }
    }
@@ -1483,8 +1484,8 @@ void launch_tpe(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipS
       // the diffusion coefficient from its temperature snapshot: only W alpha det J per point
       if constexpr (DIFF && D == 3 && Q == 4)
       {
-         ECM2_VERIFY(a.pw == (MASS ? 1 : 0) && a.treg && (a.treg_all || a.tlat_all), ERR_INTERNAL,
-                     "coefficient snapshot needs lattice blocks and the mass-only point values");
+         ECM2_VERIFY(a.pw == (MASS ? 1 : 0) && a.treg && (a.treg_all || a.tlat_all) && a.tsnap_kind == (a.treg_all ? 1 : 2),
+                     ERR_INTERNAL, "coefficient snapshot needs lattice blocks and the mass-only point values");
          Basis1D bw = b;  // (w B): the weight-scaled interpolation of T'
          for (int d = 0; d < MAX_D1D; d++)
             for (int q = 0; q < MAX_Q1D; q++) { bw.B[q + MQ * d] = a.qw[q] * b.B[q + MQ * d]; }

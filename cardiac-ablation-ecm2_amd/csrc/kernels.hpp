@@ -72,7 +72,8 @@ struct QLayout
    int pw = 2;
    // AFFINE (p = 2, lattice blocks) with the diffusion coefficient an affine law of an H1 field:
    // the kernel interpolates a snapshot of the field (ApplyArgs::tsnap) instead of reading W beta,
-   // and the point values are W alpha det J alone (pw = 1; pw = 0 without a MassIntegrator)
+   // and the point values are W alpha det J alone (pw = 1; pw = 0 without a MassIntegrator).
+   // 1: the snapshot in dof order (regular blocks); 2: in the lattice-map blocks' slot order
    int tsnap = 0;
    const int *pos = nullptr;  // device: caller element -> internal position (BLOCKED)
    const int *perm = nullptr; // device: internal position -> caller element (BLOCKED)
@@ -184,6 +185,7 @@ struct ApplyArgs
    // AFFINE with a coefficient snapshot (QLayout::tsnap): T' = A + B T at the form's L-vector dofs
    // (the diffusion coefficient's law applied to its field at Assemble) and the 1D Gauss weights
    const double *tsnap = nullptr;
+   int tsnap_kind = 0;              // QLayout::tsnap
    double qw[MAX_Q1D] = {};
    int xwave = 0;                   // the merge plan has cross-wave faces (AFFINE / TRILINEAR forms)
    const int *gmap = nullptr;
@@ -303,6 +305,11 @@ void setup_trilinear(const QLayout &L, int Q, const double *enodes, const double
 // when some element's Jacobians are not those of a trilinear map (1e-13; synchronises s).
 // out[i] = A + B T[i] (i < n): the coefficient snapshot of an affine law of an H1 field.
 void affine_snapshot(int n, const double *T, double A, double B, double *out, hipStream_t s);
+// The snapshot in the lattice-map blocks' slot order ([blk][nlp], lmap: the blocks' lattice maps),
+// and its values back in dof order.
+void affine_snapshot_lattice(int nblk, int nlp, const int *lmap, const double *T, double A, double B, double *out,
+                             hipStream_t s);
+void lattice_to_dofs(int nblk, int nlp, const int *lmap, const double *v, double *out, hipStream_t s);
 bool jacobians_trilinear_fit(int ne, int Q, const QPts &qp, const double *J, double *cfit, hipStream_t s);
 // The BLOCKED per-point qdata of an AFFINE (p <= 2) form (L: its layout; outputs sized as BLOCKED).
 void affine_expand(const QLayout &L, int Q, const double *qd_fac, const double *qd_pair, double *qd_diff,

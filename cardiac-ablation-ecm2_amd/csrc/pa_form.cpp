@@ -1145,8 +1145,20 @@ void PAForm::assemble(hipStream_t s)
       // T' = A + B T at every dof (the interpolated T' is the law at the point: the basis sums to
       // 1), taken here only: later setups (the marker diagonal's) keep the Assemble-time field
       const double A = cdiff_.scale * (1.0 - cdiff_.slope * cdiff_.t_ref), B = cdiff_.scale * cdiff_.slope;
-      tsnap_.resize(std::max(1, ndofs_));
-      kern::affine_snapshot(ndofs_, cdiff_.lvec, A, B, tsnap_.data(), s);
+      if (treg_all_)
+      {
+         tsnap_.resize(std::max(1, ndofs_));
+         kern::affine_snapshot(ndofs_, cdiff_.lvec, A, B, tsnap_.data(), s);
+      }
+      else
+      {
+         // lattice-map blocks (the reference's numbering): the snapshot in their lattice-slot order,
+         // read contiguously by the kernel (no second dependent gather through the map)
+         layout_.tsnap = 2;
+         const int nlp = tpe_lattice_points(D_);
+         tsnap_.resize((size_t)layout_.nblk() * nlp);
+         kern::affine_snapshot_lattice(layout_.nblk(), nlp, lmap_.data(), cdiff_.lvec, A, B, tsnap_.data(), s);
+      }
    }
    setup_qdata(s, nullptr);
    assembled_ = true;
@@ -1413,6 +1425,7 @@ ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, doubl
    a.lmap = lmap_.size() ? lmap_.data() : nullptr;
    for (int q = 0; q < Q_ && q < MAX_Q1D; q++) { a.qp.x[q] = maps_.qpts[q]; a.qw[q] = maps_.qw1[q]; }
    a.tsnap = layout_.tsnap ? tsnap_.data() : nullptr;
+   a.tsnap_kind = layout_.tsnap;
    a.xwave = (layout_.kind == QLAYOUT_AFFINE || layout_.kind == QLAYOUT_TRILINEAR) ? 1 : 0;
    a.part_stride = part_stride_;
    a.gmap = (resolved_mode_ == KERNEL_TPE) ? gmap_blk_.data()
@@ -1572,6 +1585,13 @@ void PAForm::expand_compressed(DeviceArray<double> &fd, DeviceArray<double> &fm,
       CoeffDesc cs = cdiff_;
       cs.kind = COEFF_GRIDFUNC_VALUE;
       cs.lvec = tsnap_.data();
+      DeviceArray<double> tdof;
+      if (layout_.tsnap == 2)
+      {
+         tdof.resize(std::max(1, ndofs_));
+         kern::lattice_to_dofs(layout_.nblk(), tpe_lattice_points(D_), lmap_.data(), tsnap_.data(), tdof.data(), s);
+         cs.lvec = tdof.data();
+      }
       const double *cd_q = coeff_points(cs, ctd, s);
       kern::setup_affine(La, Q_, jac_ ? nullptr : enodes_.data(), jac_, W_.data(), nullptr, &cs, nullptr, cd_q,
                          fac.data(), pair.data(), s);

@@ -668,6 +668,7 @@ _PAR_SIGS = {
                                                       ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_long)]),
     "ecm2_par_form_set_geometry_compression": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ecm2_par_form_qdata_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]),
+    "ecm2_par_form_coefficient_snapshot": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
     "ecm2_par_form_layout": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
     "ecm2_rccl_p2p_selftest": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
     "ecm2_partition_create_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
@@ -906,6 +907,11 @@ class ParBilinearForm:
         b = ctypes.c_double()
         _check(_par_lib().ecm2_par_form_qdata_bytes(self._h, ctypes.byref(b)))
         return b.value
+
+    def CoefficientSnapshot(self) -> bool:
+        v = ctypes.c_int()
+        _check(_par_lib().ecm2_par_form_coefficient_snapshot(self._h, ctypes.byref(v)))
+        return bool(v.value)
 
     def AddressingInfo(self):
         """(lattice, units, n_runs) of the rank's local form (see BilinearForm.AddressingInfo)."""

@@ -942,6 +942,11 @@ int ecm2_par_form_algorithmic_bytes(const ecm2_par_form *f, double *bytes)
    });
 }
 
+int ecm2_par_form_coefficient_snapshot(const ecm2_par_form *f, int *on)
+{
+   return guard([&] { NEED(f); NEED(on); *on = f->f->local().coefficient_snapshot() ? 1 : 0; });
+}
+
 int ecm2_par_form_qdata_bytes(const ecm2_par_form *f, double *bytes)
 {
    return guard([&] { NEED(f); NEED(bytes); *bytes = (double)f->f->local().qdata_bytes(); });

@@ -450,6 +450,9 @@ int ecm2_par_form_timing(ecm2_par_form *f, int enable);
 int ecm2_par_form_timing_get(ecm2_par_form *f, double *total_ms, long *launches);
 int ecm2_par_form_algorithmic_bytes(const ecm2_par_form *f, double *bytes);
 int ecm2_par_form_qdata_bytes(const ecm2_par_form *f, double *bytes);
+/* Whether the local form's last Assemble took the coefficient snapshot
+ * (ecm2_pa_form_coefficient_snapshot). */
+int ecm2_par_form_coefficient_snapshot(const ecm2_par_form *f, int *on);
 /* Quadrature-data layout of the local form (ECM2_QLAYOUT_*), after assemble. */
 int ecm2_par_form_layout(const ecm2_par_form *f, int *layout);
 int ecm2_par_form_info(const ecm2_par_form *f, int *n_true, int *kernel);

@@ -17,7 +17,7 @@ import pytest
 import helpers  # noqa: F401  (registers ecm2_amd in spawned workers too)
 import ecm2_amd as E
 import oracle as O
-from helpers import GOLDEN, RTOL, coeff_function, nonaligned, relerr
+from helpers import GOLDEN, RTOL, alpha_bioheat, coeff_function, nonaligned, relerr, temperature
 
 
 def _mesh(kind):
@@ -284,6 +284,50 @@ def test_gpu_loopback_group_matches_serial(kind, nranks, order, scatter, decomp)
     Pg = O.quad_points(m.element_nodes(), q1d)
     cg = coeff_function(Pg)
     ref = O.OracleOperator(m.element_nodes(), fes.gather_map(), fes.ndofs, order, alpha=cg, beta=cg).mult(xg)
+    assert relerr(y, ref) <= RTOL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("decomp", ["rap", "overlap"])
+def test_gpu_loopback_group_coefficient_snapshot(decomp):
+    """Two z-slabs of 4 element layers (RAP: every local block a 4x4x4 brick -- rank 0's regular,
+    rank 1's lattice-mapped with the ghost plane -- so both take the k(T) snapshot on the split
+    L-vector; OVERLAP adds a layer and keeps the stored pairs): the group Mult matches the serial
+    oracle with beta = k(T) projected at the points."""
+    import torch
+    m = E.Mesh.MakeCartesian3D(8, 8, 8)
+    order = 2
+    fes = E.H1Space(m, order)
+    er = E.partition_slabs_z(m, 2)
+    q1d = O.default_q1d(order)
+    T = temperature(fes.dof_coords())
+    scale, slope, tref = 0.05, 0.0012, 37.0
+    forms, xs, ys, parts = [], [], [], []
+    xg = np.random.default_rng(4).uniform(-1, 1, fes.ndofs)
+    for r in range(2):
+        part = E.Partition(fes, er, r, 2, decomposition=decomp)
+        pf = E.ParBilinearForm(part)
+        P = E.quadrature_points_subset(m, q1d, part.elems)
+        a = torch.as_tensor(alpha_bioheat(P).reshape(part.ne_local, -1)).cuda()
+        Tl = torch.as_tensor(T[part.local_to_global]).cuda()
+        pf.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(a)))
+        pf.AddDomainIntegrator(E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(Tl, scale, slope, tref)))
+        pf.Assemble()
+        assert pf.CoefficientSnapshot() == (decomp == "rap")
+        forms.append(pf)
+        parts.append(part)
+        xs.append(torch.as_tensor(xg[part.owned_global]).cuda())
+        ys.append(torch.full((part.n_owned,), float("nan"), dtype=torch.float64, device="cuda"))
+    E.ParGroup(forms).Mult(xs, ys)
+    torch.cuda.synchronize()
+    y = np.zeros(fes.ndofs)
+    for part, yt in zip(parts, ys):
+        y[part.owned_global] = yt.cpu().numpy()
+    en = m.element_nodes()
+    Tq = O.interp_evector(T[fes.gather_map()], order, q1d)
+    beta = scale * (1.0 + slope * (Tq - tref))
+    ref = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=alpha_bioheat(O.quad_points(en, q1d)),
+                           beta=beta).mult(xg)
     assert relerr(y, ref) <= RTOL
 
 

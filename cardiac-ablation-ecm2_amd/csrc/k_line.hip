@@ -528,8 +528,16 @@ struct BrickPtTable
 template <int D, int Q, int BZ>
 __device__ const BrickPtTable<D, Q, BZ> kBrickPts = BrickPtTable<D, Q, BZ>();
 
+#ifndef ECM2_BRICK_TL_WPE
+#define ECM2_BRICK_TL_WPE 0  // A/B: waves per SIMD the TRILINEAR_E brick kernel is built for (0: the shape's)
+#endif
+template <int D, int Q, int BZ, int G>
+constexpr int brick_wpe()
+{
+   return (G == 2 && ECM2_BRICK_TL_WPE > 0) ? ECM2_BRICK_TL_WPE : BrickShapeC<D, Q, BZ>::WPE;
+}
 template <int D, int Q, int BZ, bool SPLIT, int G, bool REG>
-__global__ void __launch_bounds__((BrickShapeC<D, Q, BZ>::NT), (BrickShapeC<D, Q, BZ>::WPE))
+__global__ void __launch_bounds__((BrickShapeC<D, Q, BZ>::NT), (brick_wpe<D, Q, BZ, G>()))
 k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int *__restrict__ bmap,
                 const int *__restrict__ breg, int n_owned, const double *__restrict__ qdd,
                 const double *__restrict__ qdm, const double *__restrict__ x, const double *__restrict__ xg,

@@ -528,13 +528,14 @@ struct BrickPtTable
 template <int D, int Q, int BZ>
 __device__ const BrickPtTable<D, Q, BZ> kBrickPts = BrickPtTable<D, Q, BZ>();
 
-#ifndef ECM2_BRICK_TL_WPE
-#define ECM2_BRICK_TL_WPE 0  // A/B: waves per SIMD the TRILINEAR_E brick kernel is built for (0: the shape's)
-#endif
+// Waves per SIMD a brick kernel is built for: the TRILINEAR_E z stage's column geometry takes it
+// past 128 VGPRs (8 values spilled at 4 waves); at 3 waves it holds 140 without spills
+// (profiles/r4/ab_bw3.txt: kernel -1%).
 template <int D, int Q, int BZ, int G>
 constexpr int brick_wpe()
 {
-   return (G == 2 && ECM2_BRICK_TL_WPE > 0) ? ECM2_BRICK_TL_WPE : BrickShapeC<D, Q, BZ>::WPE;
+   constexpr int W = BrickShapeC<D, Q, BZ>::WPE;
+   return (G == 2 && W > 3) ? 3 : W;
 }
 template <int D, int Q, int BZ, bool SPLIT, int G, bool REG>
 __global__ void __launch_bounds__((BrickShapeC<D, Q, BZ>::NT), (brick_wpe<D, Q, BZ, G>()))

@@ -720,9 +720,6 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
    v2d ce[NCE];
    const double *qa = qdm + (size_t)blk * NQ * 64 * PW + lane * PW;
    auto ldp = [&](int q) -> v2d {  // the point values of point q (PW = 1: W beta / det J alone)
-#ifdef ECM2_PROBE_TLB_NOPAIR
-      return v2d{1.0 + 1e-3 * q, 0.5};  // timing probe only: no point-value loads
-#endif
       if constexpr (PW == 2) { return ld2(qa + (size_t)q * 128); }
       else { return v2d{__builtin_nontemporal_load(qa + (size_t)q * 64), 0.0}; }
    };
@@ -757,11 +754,7 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
                const unsigned v = lattice_xyz<D>(j);
                d = rg.base + (int)(v & 31) * rg.sx + (int)((v >> 5) & 31) * rg.sy + (int)(v >> 10) * rg.sz;
             }
-#ifdef ECM2_PROBE_TLB_NOGATHER
-            sXL[w][j] = (double)(d & 7);  // timing probe only: no x loads
-#else
             sXL[w][j] = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
-#endif
          }
       }
 #pragma unroll

@@ -159,10 +159,11 @@ int ecm2_pa_form_set_element_nodes(ecm2_pa_form *f, const double *enodes);
  * device pointer, must stay valid until ecm2_pa_form_assemble returns. */
 int ecm2_pa_form_set_jacobians(ecm2_pa_form *f, const double *J);
 /* Quadrature-data layout (ecm2_pa_form_info's *layout).  AFFINE: when every element is
- * a parallelepiped (checked on the corners given to set_element_nodes) and both
- * integrators are present, the p <= 2 fused kernel stores the constant element geometry
+ * a parallelepiped (checked on the corners given to set_element_nodes, or on the Jacobians) and
+ * the diffusion integrator is present, the p <= 2 fused kernel stores the constant element geometry
  * adj(J) adj(J)^T / det J once per element and one (W beta, W alpha det J) pair per
- * quadrature point: the reference's pa_data values (bilininteg_diffusion_kernels.cpp:349-362,
+ * quadrature point (W beta alone without a MassIntegrator; W alpha det J alone with the coefficient
+ * snapshot below): the reference's pa_data values (bilininteg_diffusion_kernels.cpp:349-362,
  * bilininteg_mass_pa.cpp:76) up to rounding, 3.3x fewer bytes at p = 2 (3.5x at p = 4,
  * AFFINE_E: element-ordered, for the p >= 3 line / brick kernels).  On by default;
  * ecm2_pa_form_set_geometry_compression(f, 0) keeps the full per-point layout. */

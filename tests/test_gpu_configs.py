@@ -249,6 +249,39 @@ def test_c5_full_size():
     assert relerr(yh, op.mult(x)) <= RTOL
 
 
+def test_c5_full_size_drop_in():
+    """configs[4] size in the drop-in configuration at p = 4: MakeCartesian3D's space-filling-curve
+    element order and FiniteElementSpace's entity dofs, interior vertices moved (non-affine hexes)
+    and the geometry as MFEM Jacobians (set_jacobians, fitted to trilinear maps: TRILINEAR_E, the
+    brick kernel evaluating J and adj(J) per point), against the oracle."""
+    n = 68
+    m = E.Mesh.MakeCartesian3D(n, n, n, sfc_ordering=True)
+    V = m.vertices()
+    h = 1.0 / n
+    inner = np.all((V > 0.5 * h) & (V < 1.0 - 0.5 * h), axis=1)
+    V[inner] += 0.15 * h * np.random.default_rng(11).uniform(-1, 1, (int(inner.sum()), 3))
+    m.set_vertices(V)
+    fes = E.H1Space(m, 4, E.NUMBERING_ENTITY)
+    assert fes.ndofs == 20346417
+    en = m.element_nodes()
+    P = O.quad_points(en, 6)
+    a, b = alpha_bioheat(P), k_of_T(temperature(P))
+    del P
+    form = E.BilinearForm(fes, geometry="jacobians")
+    form.SetJacobians(m.jacobians(6))
+    form.AddDomainIntegrator(E.MassIntegrator(quad_coeff(fes, a)))
+    form.AddDomainIntegrator(E.DiffusionIntegrator(quad_coeff(fes, b)))
+    form.Assemble()
+    assert form.info()["layout"] == E.QLAYOUT_TRILINEAR_E and form.BrickInfo()[0] > 0
+    x = np.random.default_rng(69).uniform(-1, 1, fes.ndofs)
+    y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+    form.Mult(dev(x), y)
+    yh = host(y)
+    del form, y
+    op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, 4, alpha=a, beta=b)
+    assert relerr(yh, op.mult(x)) <= RTOL
+
+
 def _serial_form(fes, P, alpha, beta):
     f = E.BilinearForm(fes)
     if alpha is not None:

@@ -525,6 +525,7 @@ def main():
     qbytes = sum(f.qdata_bytes() for f in timed_forms)
     layout = qdata_layout(E, timed_forms[0])
     pcg = c3_pcg(E, torch, fes, form) if args.workload == "c3" else None
+    reasm = reassembly_ms(torch, form) if (form is not None and args.workload != "c3") else None
 
     # aggregate over ranks: total true dofs, max time; kernel ms per Mult (interior + boundary
     # launches of one Mult when partitioned); bytes per GPU
@@ -624,6 +625,8 @@ def main():
                                  mbytes_total / world, stream, use_pin=pin_ok, flops=alg_flops(order, ne_own)),
             "cpu_baseline": cpu,
         }
+        if reasm is not None:
+            line["reassembly_ms"] = reasm  # Assemble after a k(T) change, plan kept (outside the timed region)
         line.update(subs)
         if pcg is not None:
             line["pcg"] = pcg
@@ -665,6 +668,20 @@ def cartesian_space(E, nx, ny, nz, order, numbering, shape):
         mesh.set_vertices(V)
     fes = E.H1Space(mesh, order, E.NUMBERING_ENTITY if numbering == "entity" else E.NUMBERING_STRUCTURED)
     return mesh, fes
+
+
+def reassembly_ms(torch, form, reps=5):
+    """Device re-assembly after a k(T) change (row f1: the coefficient snapshot or projection and the
+    qdata setup; the merge plan and addressing are kept), ms per Assemble."""
+    form.Assemble()  # warm
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(reps):
+        form.Assemble()
+    ev1.record()
+    torch.cuda.synchronize()
+    return round(ev0.elapsed_time(ev1) / reps, 3)
 
 
 def c3_pcg(E, torch, fes, form, max_iter=100):

@@ -11,8 +11,6 @@
 // partial slots summed by k_sum_partials in a fixed order).
 #include "dev_common.hpp"
 
-#include <type_traits>
-
 namespace ecm2
 {
 namespace
@@ -967,18 +965,18 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
 template <int D, int Q, bool SPLIT, int RM, bool MASS>
 __global__ void __launch_bounds__(256, 2)
 k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
-               const double *__restrict__ qdd, const double *__restrict__ qdm, const double *__restrict__ qdb,
+               const double *__restrict__ qdd, const double *__restrict__ qdm,
                const double *__restrict__ x, const double *__restrict__ xg, const double *__restrict__ tsn,
                double *__restrict__ y, double *__restrict__ yg, const Basis1D b, const Basis1D bw,
                const int *__restrict__ lane_flags, double *__restrict__ part, const int *__restrict__ treg,
                int pstride, const int *__restrict__ lmap)
 {
-   static_assert(RM == 1 || RM == 2 || RM == 3, "RM 1 / 3: lattice blocks; 2: per block");
+   static_assert(RM == 1 || RM == 3, "lattice blocks only");
    static_assert(D == 3 && Q == 4, "p = 2");
    constexpr int ND = D * D * D, NR = Q * Q, XR = XwaveRows<D>::R, WPG = 4, P = D - 1;
    constexpr int NLP = tpe_lattice_points(D);
    static_assert(2 * NLP <= XR * 64, "x and T' lattices fit a wave's exchange rows");
-   __shared__ double sU[WPG][XR][64];  // per wave: (x, T') lattice pairs or x [a][lane]; then the face exchange
+   __shared__ double sU[WPG][XR][64];  // per wave: (x, T') lattice pairs; then the cross-wave face exchange
    const int lane = threadIdx.x & 63;
    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
    const int blk = blk_begin + (int)blockIdx.x * WPG + w;
@@ -990,29 +988,19 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
    // (x, T') pairs per lattice slot: one 16-byte LDS read per point (two 8-byte arrays: +3.5% kernel
    // time, profiles/r4/ab_pfd.txt)
    v2d *sPL = reinterpret_cast<v2d *>(&sU[w][0][0]);
-   double *sXm = &sU[w][0][0];  // a map-addressed block's x, [a][lane]
    TpeReg rg = {};
-   // the block's addressing (wave-uniform): 1 regular, 2 lattice map, 0 element map (RM 2 only:
-   // a partitioned rank's ghost-touching or leftover blocks, whose W beta is stored, qdb)
-   int regf = RM == 1 ? 1 : 2;
-   if (RM == 2 && wave_on) { regf = treg[(size_t)blk * 8 + 7]; }
-   const bool lat = regf != 0;
+   const int regf = RM == 1 ? 1 : 2;
    double Yo[ND];
 #pragma unroll
    for (int a = 0; a < ND; a++) { Yo[a] = 0.0; }
    auto ld2 = [&](const double *p) -> v2d { return __builtin_nontemporal_load(reinterpret_cast<const v2d *>(p)); };
    v2d ce[3];
    const double *qa = qdm + (size_t)blk * NR * Q * 64 + lane;  // W alpha det J, [blk][q][lane]
-   const double *qb = qdb ? qdb + (size_t)blk * NR * Q * 64 + lane : nullptr;  // W beta (element-map blocks)
    // three row buffers in rotation, each row issues the row two ahead (the plane loop is unrolled)
-   double ra[3][Q], rb[2][Q];  // (rb: element-map blocks' W beta, one row ahead)
+   double ra[3][Q];
    auto load_row = [&](int row, double (&aq)[Q]) {
 #pragma unroll
       for (int qx = 0; qx < Q; qx++) { aq[qx] = MASS ? __builtin_nontemporal_load(qa + (size_t)(row * Q + qx) * 64) : 0.0; }
-   };
-   auto load_rowb = [&](int row, double (&bq)[Q]) {
-#pragma unroll
-      for (int qx = 0; qx < Q; qx++) { bq[qx] = __builtin_nontemporal_load(qb + (size_t)(row * Q + qx) * 64); }
    };
    if (wave_on)
    {
@@ -1021,50 +1009,33 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
       for (int k = 0; k < 3; k++) { ce[k] = ld2(qc + k * 128); }
       load_row(0, ra[0]);
       load_row(1, ra[1]);
-      if (RM == 2 && !lat) { load_rowb(0, rb[0]); }
-      if (RM != 3)
+      if (RM == 1)
       {
          const int *r = treg + (size_t)blk * 8;  // wave-uniform: scalar loads
          rg = TpeReg{r[0], r[1], r[2], r[3], r[4]};
       }
-      if (lat)
-      {
-         const int *lm = lmap + (size_t)blk * NLP;
+      const int *lm = lmap + (size_t)blk * NLP;
 #pragma unroll
-         for (int k = 0; k < (NLP + 63) / 64; k++)
+      for (int k = 0; k < (NLP + 63) / 64; k++)
+      {
+         const int j = lane + 64 * k;
+         if (j < NLP)
          {
-            const int j = lane + 64 * k;
-            if (j < NLP)
+            int d;
+            if (RM == 3) { d = bdof(lm[j]); }
+            else
             {
-               int d;
-               if (RM == 3 || (RM == 2 && regf == 2)) { d = bdof(lm[j]); }
-               else
-               {
-                  const unsigned v = lattice_xyz<D>(j);
-                  d = rg.base + (int)(v & 31) * rg.sx + (int)((v >> 5) & 31) * rg.sy + (int)(v >> 10) * rg.sz;
-               }
-               // (all-lattice-map forms: the snapshot is stored in the blocks' slot order, a contiguous read)
-               sPL[j] = v2d{(!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned], RM == 3 ? tsn[(size_t)blk * NLP + j] : tsn[d]};
+               const unsigned v = lattice_xyz<D>(j);
+               d = rg.base + (int)(v & 31) * rg.sx + (int)((v >> 5) & 31) * rg.sy + (int)(v >> 10) * rg.sz;
             }
-         }
-      }
-      else if (RM == 2)
-      {
-#pragma unroll
-         for (int a = 0; a < ND; a++)
-         {
-            const int g = mp[a * 64];
-            const int d = bdof(g);
-            const double v = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
-            sXm[a * 64 + lane] = bneg(g) ? -v : v;
+            // (lattice-map blocks: the snapshot is stored in their slot order, a contiguous read)
+            sPL[j] = v2d{(!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned], RM == 3 ? tsn[(size_t)blk * NLP + j] : tsn[d]};
          }
       }
    }
    __syncthreads();  // the lattices are read by every lane of the wave
-   // the quadrature planes; LAT: the diffusion coefficient interpolated from T' (lattice blocks),
-   // else read (element-map blocks)
-   auto compute = [&](auto lat_tag) {
-      constexpr bool LAT = decltype(lat_tag)::value;
+   if (wave_on)
+   {
       auto lane_base = [&](int cx, int cy) {
          const int nx = tpe_lattice_class_n(cx), ny = tpe_lattice_class_n(cy);
          return (ez * ny + ey) * nx + ex;
@@ -1077,45 +1048,30 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
             bz[dz] = b.B[qz + MQ * dz]; gz[dz] = b.G[qz + MQ * dz]; wz[dz] = bw.B[qz + MQ * dz];
          }
          double ZB[D][D], ZG[D][D], ZT[D][D], SB[D][D], SG[D][D];
-         int ll = lane;
-         asm volatile("" : "+v"(ll));  // (element-map blocks: re-read x per plane, as k_apply_tpe_sf)
 #pragma unroll
          for (int dy = 0; dy < D; dy++)
 #pragma unroll
             for (int dx = 0; dx < D; dx++)
             {
+               int lb = lane_base(dx % P, dy % P);
+               asm volatile("" : "+v"(lb));  // the plane re-reads the lattices (no 54 live values)
                double zb = 0.0, zg = 0.0, zt = 0.0;
-               if constexpr (LAT)
-               {
-                  int lb = lane_base(dx % P, dy % P);
-                  asm volatile("" : "+v"(lb));  // the plane re-reads the lattices (no 54 live values)
 #pragma unroll
-                  for (int dz = 0; dz < D; dz++)
-                  {
-                     const int cx = dx % P, cy = dy % P, cz = dz % P;
-                     const int nx = tpe_lattice_class_n(cx), ny = tpe_lattice_class_n(cy);
-                     const int sl = tpe_lattice_class_off(D, cx, cy, cz) + ((dz / P) * ny + dy / P) * nx + dx / P;
-                     const v2d ct = sPL[lb + sl];
-                     const double c = ct.x, t = ct.y;
-                     zb += bz[dz] * c;
-                     zg += gz[dz] * c;
-                     zt += wz[dz] * t;
-                  }
-               }
-               else
+               for (int dz = 0; dz < D; dz++)
                {
-#pragma unroll
-                  for (int dz = 0; dz < D; dz++)
-                  {
-                     const double c = sXm[((dz * D + dy) * D + dx) * 64 + ll];
-                     zb += bz[dz] * c;
-                     zg += gz[dz] * c;
-                  }
+                  const int cx = dx % P, cy = dy % P, cz = dz % P;
+                  const int nx = tpe_lattice_class_n(cx), ny = tpe_lattice_class_n(cy);
+                  const int sl = tpe_lattice_class_off(D, cx, cy, cz) + ((dz / P) * ny + dy / P) * nx + dx / P;
+                  const v2d ct = sPL[lb + sl];
+                  const double c = ct.x, t = ct.y;
+                  zb += bz[dz] * c;
+                  zg += gz[dz] * c;
+                  zt += wz[dz] * t;
                }
                ZB[dy][dx] = zb; ZG[dy][dx] = zg; ZT[dy][dx] = zt;
                SB[dy][dx] = 0.0; SG[dy][dx] = 0.0;
             }
-         auto row_body = [&](const int qy, const double (&cur)[Q], const double (&curb)[Q]) {
+         auto row_body = [&](const int qy, const double (&cur)[Q]) {
             double Y00[D], Y01[D], Y10[D], YT[D];
 #pragma unroll
             for (int dx = 0; dx < D; dx++)
@@ -1128,7 +1084,7 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                   u += by * ZB[dy][dx];
                   v += gy * ZB[dy][dx];
                   wv += by * ZG[dy][dx];
-                  if (LAT) { t += wy * ZT[dy][dx]; }
+                  t += wy * ZT[dy][dx];
                }
                Y00[dx] = u; Y01[dx] = v; Y10[dx] = wv; YT[dx] = t;
             }
@@ -1147,9 +1103,8 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                   ux += gq * Y00[dx];
                   uy += bq * Y01[dx];
                   uz += bq * Y10[dx];
-                  if (LAT) { wb += wq * YT[dx]; }  // W_q beta(x_q)
+                  wb += wq * YT[dx];  // W_q beta(x_q)
                }
-               if (!LAT) { wb = curb[qx]; }
                const double m = MASS ? cur[qx] * u : 0.0;  // W alpha det J u
                double fx = ce[0].x * ux, fy = ce[0].y * ux, fz = ce[1].x * ux;
                fx += ce[0].y * uy; fy += ce[1].y * uy; fz += ce[2].x * uy;
@@ -1182,11 +1137,9 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
          for (int qy = 0; qy < Q; qy++)
          {
             const int row = qz * Q + qy;
-            const int nrow = row + 2 < NR ? row + 2 : NR - 1;  // (the last rows reload the final row)
             __builtin_amdgcn_sched_barrier(0);  // rows stay in program order (no interleaving)
-            load_row(nrow, ra[(row + 2) % 3]);
-            if (!LAT) { load_rowb(row + 1 < NR ? row + 1 : NR - 1, rb[(row + 1) % 2]); }
-            row_body(qy, ra[row % 3], rb[row % 2]);
+            load_row(row + 2 < NR ? row + 2 : NR - 1, ra[(row + 2) % 3]);  // (the last rows reload the final row)
+            row_body(qy, ra[row % 3]);
          }
 #pragma unroll
          for (int dz = 0; dz < D; dz++)
@@ -1201,15 +1154,10 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
       };
 #pragma unroll
       for (int qz = 0; qz < Q; qz++) { plane(qz); }
-   };
-   if (wave_on)
-   {
-      if (RM != 2 || lat) { compute(std::true_type()); }
-      else { compute(std::false_type()); }
-   }
-   tpe_assemble_store<D, SPLIT, RM == 2, true, true>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0, blk,
-                                                    lane, active, n_owned, y, yg, part, &sU[0][0][0], w, wave_on, rg,
-                                                    regf, pstride, lmap ? lmap + (size_t)blk * NLP : nullptr);
+   }  // wave_on
+   tpe_assemble_store<D, SPLIT, false, true, true>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0, blk, lane,
+                                                  active, n_owned, y, yg, part, &sU[0][0][0], w, wave_on, rg, regf,
+                                                  pstride, lmap ? lmap + (size_t)blk * NLP : nullptr);
 }
 
 // Latency variant of k_apply_tpe_sf for small block ranges (the boundary elements of the
@@ -1529,19 +1477,17 @@ void launch_tpe(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipS
       // the diffusion coefficient from its temperature snapshot: only W alpha det J per point
       if constexpr (DIFF && D == 3 && Q == 4)
       {
-         ECM2_VERIFY(a.pw == (MASS ? 1 : 0) && a.treg &&
-                        ((a.tsnap_kind == 1 && a.treg_all) || (a.tsnap_kind == 2 && a.tlat_all) || (a.tsnap_kind == 3 && a.qdb)),
-                     ERR_INTERNAL, "coefficient snapshot: layout and block addressing do not match");
+         ECM2_VERIFY(a.pw == (MASS ? 1 : 0) && a.treg && (a.treg_all || a.tlat_all) && a.tsnap_kind == (a.treg_all ? 1 : 2),
+                     ERR_INTERNAL, "coefficient snapshot needs lattice blocks and the mass-only point values");
          Basis1D bw = b;  // (w B): the weight-scaled interpolation of T'
          for (int d = 0; d < MAX_D1D; d++)
             for (int q = 0; q < MAX_Q1D; q++) { bw.B[q + MQ * d] = a.qw[q] * b.B[q + MQ * d]; }
 #define ECM2_TS(RM)                                                                                              \
    hipLaunchKernelGGL((k_apply_tpe_ts<3, 4, SPLIT, RM, MASS>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end,      \
-                      a.n_owned, a.gmap, a.qdd, a.qdm, a.qdb, a.x, a.xg, a.tsnap, a.y, a.yg, b, bw, a.lane_flags,   \
-                      a.part, a.treg, a.part_stride, a.lmap)
-         if (a.tsnap_kind == 1 && a.treg_all) { ECM2_TS(1); }
-         else if (a.tsnap_kind == 2) { ECM2_TS(3); }
-         else { ECM2_TS(2); }
+                      a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.tsnap, a.y, a.yg, b, bw, a.lane_flags, a.part,  \
+                      a.treg, a.part_stride, a.lmap)
+         if (a.treg_all) { ECM2_TS(1); }
+         else { ECM2_TS(3); }
 #undef ECM2_TS
       }
       else { ECM2_VERIFY(false, ERR_INTERNAL, "coefficient snapshot: p = 2 forms with the diffusion integrator"); }

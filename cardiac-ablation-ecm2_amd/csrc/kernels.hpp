@@ -73,9 +73,7 @@ struct QLayout
    // AFFINE (p = 2, lattice blocks) with the diffusion coefficient an affine law of an H1 field:
    // the kernel interpolates a snapshot of the field (ApplyArgs::tsnap) instead of reading W beta,
    // and the point values are W alpha det J alone (pw = 1; pw = 0 without a MassIntegrator).
-   // 1: the snapshot in dof order (regular blocks); 2: in the lattice-map blocks' slot order;
-   // 3: dof order, some blocks element-map addressed (a partitioned rank's ghost-touching or leftover
-   //    blocks): those read a stored W beta per point (PAForm::qd_beta_)
+   // 1: the snapshot in dof order (regular blocks); 2: in the lattice-map blocks' slot order
    int tsnap = 0;
    const int *pos = nullptr;  // device: caller element -> internal position (BLOCKED)
    const int *perm = nullptr; // device: internal position -> caller element (BLOCKED)
@@ -188,7 +186,6 @@ struct ApplyArgs
    // (the diffusion coefficient's law applied to its field at Assemble) and the 1D Gauss weights
    const double *tsnap = nullptr;
    int tsnap_kind = 0;              // QLayout::tsnap
-   const double *qdb = nullptr;     // tsnap 3: W beta per point [blk][q][lane] (read by element-map blocks)
    double qw[MAX_Q1D] = {};
    int xwave = 0;                   // the merge plan has cross-wave faces (AFFINE / TRILINEAR forms)
    const int *gmap = nullptr;

@@ -1136,15 +1136,8 @@ void PAForm::assemble(hipStream_t s)
    // geometry, p = 2, every block a lattice brick, no attribute marker on the diffusion integrator
    layout_.tsnap = 0;
    tsnap_.resize(0);
-   qd_beta_.resize(0);
-   // (lattice blocks: every block regular or lattice-mapped; or some of them, the rest element-map
-   // addressed with a stored W beta -- a partitioned rank's ghost-touching and leftover layers)
-#ifndef ECM2_TSNAP_MIXED
-#define ECM2_TSNAP_MIXED 1  // (A/B switch: 0 keeps the stored pairs on mixed forms)
-#endif
-   const bool some_lattice = ECM2_TSNAP_MIXED && treg_.size() && (n_treg_ + n_tlat_) > 0;
    if (tsnap_pref_ && layout_.kind == QLAYOUT_AFFINE && resolved_mode_ == KERNEL_TPE && D_ == 3 && Q_ == 4 &&
-       (treg_all_ || tlat_all_ || some_lattice) && have_diff_ && cdiff_.kind == COEFF_GRIDFUNC_AFFINE && cdiff_.lvec &&
+       (treg_all_ || tlat_all_) && have_diff_ && cdiff_.kind == COEFF_GRIDFUNC_AFFINE && cdiff_.lvec &&
        !marked_[INTEG_DIFFUSION])
    {
       layout_.tsnap = 1;
@@ -1152,9 +1145,8 @@ void PAForm::assemble(hipStream_t s)
       // T' = A + B T at every dof (the interpolated T' is the law at the point: the basis sums to
       // 1), taken here only: later setups (the marker diagonal's) keep the Assemble-time field
       const double A = cdiff_.scale * (1.0 - cdiff_.slope * cdiff_.t_ref), B = cdiff_.scale * cdiff_.slope;
-      if (treg_all_ || !tlat_all_)
+      if (treg_all_)
       {
-         if (!treg_all_) { layout_.tsnap = 3; }  // mixed: element-map blocks read a stored W beta
          tsnap_.resize(std::max(1, ndofs_));
          kern::affine_snapshot(ndofs_, cdiff_.lvec, A, B, tsnap_.data(), s);
       }
@@ -1244,7 +1236,7 @@ void PAForm::setup_qdata(hipStream_t s, const std::pair<int, std::vector<double>
 
    // Coefficient values at quadrature points (CoefficientVector::Project).
    const double *cm_q = have_mass_ ? coeff_points(cmass_, ctmp_m_, s) : nullptr;
-   const double *cd_q = have_diff_ && (!layout_.tsnap || layout_.tsnap == 3) ? coeff_points(cdiff_, ctmp_d_, s) : nullptr;
+   const double *cd_q = have_diff_ && !layout_.tsnap ? coeff_points(cdiff_, ctmp_d_, s) : nullptr;
 
    const CoeffDesc *cm = have_mass_ ? &cmass_ : nullptr;
    const CoeffDesc *cd = have_diff_ ? &cdiff_ : nullptr;
@@ -1252,17 +1244,6 @@ void PAForm::setup_qdata(hipStream_t s, const std::pair<int, std::vector<double>
    {
       kern::setup_affine(layout_, Q_, jac_ ? nullptr : enodes_.data(), jac_, W_.data(), cm, cd, cm_q, cd_q,
                          qd_diff_.data(), qd_mass_.data(), s);
-      if (layout_.tsnap == 3)
-      {
-         // W beta at every point too (the element-map blocks read it; the lattice blocks interpolate T')
-         QLayout Lb = layout_;
-         Lb.tsnap = 0;
-         Lb.pw = 1;
-         qd_beta_.resize(Lb.mass_size());
-         if (ne_ % kElemBlock) { ECM2_HIP(hipMemsetAsync(qd_beta_.data(), 0, qd_beta_.bytes(), s)); }
-         kern::setup_affine(Lb, Q_, jac_ ? nullptr : enodes_.data(), jac_, W_.data(), nullptr, cd, nullptr, cd_q,
-                            qd_diff_.data(), qd_beta_.data(), s);
-      }
    }
    else if (layout_.trilinear())
    {
@@ -1445,7 +1426,6 @@ ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, doubl
    for (int q = 0; q < Q_ && q < MAX_Q1D; q++) { a.qp.x[q] = maps_.qpts[q]; a.qw[q] = maps_.qw1[q]; }
    a.tsnap = layout_.tsnap ? tsnap_.data() : nullptr;
    a.tsnap_kind = layout_.tsnap;
-   a.qdb = qd_beta_.size() ? qd_beta_.data() : nullptr;
    a.xwave = (layout_.kind == QLAYOUT_AFFINE || layout_.kind == QLAYOUT_TRILINEAR) ? 1 : 0;
    a.part_stride = part_stride_;
    a.gmap = (resolved_mode_ == KERNEL_TPE) ? gmap_blk_.data()
@@ -1526,14 +1506,13 @@ void PAForm::assemble_diagonal(double *diag, hipStream_t s)
       }
       if (differ)
       {
-         DeviceArray<double> keep_d(std::move(qd_diff_)), keep_m(std::move(qd_mass_)), keep_b(std::move(qd_beta_));
+         DeviceArray<double> keep_d(std::move(qd_diff_)), keep_m(std::move(qd_mass_));
          const std::pair<int, std::vector<double>> over(F, wf);
          setup_qdata(s, &over);
          diagonal_from_qdata(diag, s);
          ECM2_HIP(hipStreamSynchronize(s));  // the temporaries are freed below
          qd_diff_ = std::move(keep_d);
          qd_mass_ = std::move(keep_m);
-         qd_beta_ = std::move(keep_b);
          return;
       }
    }

@@ -75,7 +75,7 @@ public:
    void set_coefficient_snapshot(bool on);
    bool coefficient_snapshot() const { return layout_.tsnap != 0; }
    // bytes of quadrature data the form stores (diffusion + mass + the coefficient snapshot)
-   size_t qdata_bytes() const { return qd_diff_.bytes() + qd_mass_.bytes() + tsnap_.bytes() + qd_beta_.bytes(); }
+   size_t qdata_bytes() const { return qd_diff_.bytes() + qd_mass_.bytes() + tsnap_.bytes(); }
 
    // Optional element permutation (internal position i <- caller element perm[i]) used by
    // the blocked layout; ORDER_BRICK puts one 4x4x4 brick in each 64-lane wave so the
@@ -254,7 +254,6 @@ private:
    bool compress_ = true;           // set_geometry_compression
    bool tsnap_pref_ = true;         // set_coefficient_snapshot
    DeviceArray<double> tsnap_;      // coefficient snapshot T' = A + B T (local L-vector)
-   DeviceArray<double> qd_beta_;    // tsnap 3: W beta per point [blk][q][lane] (element-map blocks read it)
    int latency_from_ = -1;          // set_latency_from
    bool perm_auto_ = false;         // perm_host_ was derived (not the caller's)
    DeviceArray<int> lane_flags_;    // [blk][64] in-wave merge flags

@@ -291,9 +291,9 @@ def test_gpu_loopback_group_matches_serial(kind, nranks, order, scatter, decomp)
 @pytest.mark.parametrize("decomp", ["rap", "overlap"])
 def test_gpu_loopback_group_coefficient_snapshot(decomp):
     """Two z-slabs of 4 element layers (RAP: every local block a 4x4x4 brick -- rank 0's regular,
-    rank 1's lattice-mapped with the ghost plane; OVERLAP adds rank 0 a fifth layer of element-map
-    blocks, which read a stored W beta): every rank takes the k(T) snapshot on its split L-vector and
-    the group Mult matches the serial oracle with beta = k(T) projected at the points."""
+    rank 1's lattice-mapped with the ghost plane -- so both take the k(T) snapshot on the split
+    L-vector; OVERLAP adds rank 0 a fifth layer, which keeps the stored pairs there): the group Mult
+    matches the serial oracle with beta = k(T) projected at the points."""
     import torch
     m = E.Mesh.MakeCartesian3D(8, 8, 8)
     order = 2
@@ -313,9 +313,8 @@ def test_gpu_loopback_group_coefficient_snapshot(decomp):
         pf.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(a)))
         pf.AddDomainIntegrator(E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(Tl, scale, slope, tref)))
         pf.Assemble()
-        # (OVERLAP: rank 0 holds 5 layers, a leftover layer of element-map blocks that read a stored
-        # W beta beside the snapshot; rank 1's 4 layers are bricks)
-        assert pf.CoefficientSnapshot()
+        # (OVERLAP: rank 0 holds 5 layers, a leftover layer of non-brick blocks; rank 1's 4 layers are bricks)
+        assert pf.CoefficientSnapshot() == (decomp == "rap" or r == 1)
         forms.append(pf)
         parts.append(part)
         xs.append(torch.as_tensor(xg[part.owned_global]).cuda())

@@ -181,6 +181,9 @@ def kernel_ms(forms, apply, x, y, steps, torch, settle_s=0.06, world=1, dist=Non
     return kms / steps
 
 
+PART_NAME = {"slabs": "z-slabs", "boxes": "boxes", "bricks": "brick runs"}
+
+
 def member_bench(args, torch, group, xs, ys, ndofs, workload, dl):
     """--loopback N --member R: member R's rows of the partitioned operator alone, captured in
     one HIP graph and replayed -- the stages, streams and kernels one RCCL rank runs on its own
@@ -237,6 +240,9 @@ def member_bench(args, torch, group, xs, ys, ndofs, workload, dl):
                       "member_ms": [round(v, 5) for v in per], "members": members,
                       "member_passes_ms": [[round(v, 5) for v in samples[r]] for r in members],
                       "slowest_member_ms": round(worst, 5),
+                      "partition": PART_NAME[args.partition],
+                      "decomposition": group.forms[0].part.decomposition,
+                      "coefficient_snapshot": [bool(f.CoefficientSnapshot()) for f in group.forms],
                       "emulated_value": round(ndofs / (worst * 1e-3) / 1e6, 2), "unit": "MDoF/s",
                       "note": f"one member's Mult alone on one GPU, exchange by device copies: a rank's Mult short "
                               f"of the xGMI transfer time; members interleaved over {passes} passes, the median "
@@ -331,8 +337,10 @@ def main():
                          "GeometricFactors::JACOBIANS array (what the reference-side binding passes)")
     ap.add_argument("--loopback", type=int, default=1,
                     help="N>1 on one GPU: N subdomains in this process (validation of the partitioned path)")
-    ap.add_argument("--partition", choices=["slabs", "boxes"], default="slabs",
-                    help="N > 1: z-slabs (CartesianPartitioning along z) or px x py x pz boxes (2x2x2 at N = 8)")
+    ap.add_argument("--partition", choices=["slabs", "boxes", "bricks"], default="slabs",
+                    help="N > 1: z-slabs (CartesianPartitioning along z), px x py x pz boxes (2x2x2 at N = 8) "
+                         "or equal runs of whole 4x4x4 bricks (partition_bricks; with ECM2_DECOMP=rap every "
+                         "rank's blocks are bricks)")
     ap.add_argument("--member", type=int, default=None,
                     help="with --loopback N (z-slabs, OVERLAP): time member R's rows alone, as one rank runs "
                          "them on its own GPU (HIP graph); -1 = every member, the slowest sets the emulated rate")
@@ -467,6 +475,8 @@ def main():
             if f is None:
                 raise SystemExit(f"--partition boxes: no box factorisation for {nsub} parts")
             er = E.partition_boxes(mesh, f)
+        elif args.partition == "bricks":
+            er = E.partition_bricks(mesh, nsub)
         else:
             er = E.partition_slabs_z(mesh, nsub)
         if world > 1:
@@ -617,9 +627,9 @@ def main():
                 "mesh": args.mesh if args.workload != "c3" else "fichera (affine after refinement)",
                 "lattice_units": list(lattice[:2]), "summation_runs": lattice[2],
                 "qdata_bytes_stored": qbytes_total / world,
-                "parallelism": (f"domain decomposition, {'z-slabs' if args.partition == 'slabs' else 'boxes'} x{world} ({decomp}, {args.schedule} schedule), RCCL shared-DoF exchange"
+                "parallelism": (f"domain decomposition, {PART_NAME[args.partition]} x{world} ({decomp}, {args.schedule} schedule), RCCL shared-DoF exchange"
                                 if world > 1 else
-                                (f"loopback {'z-slabs' if args.partition == 'slabs' else 'boxes'} x{args.loopback} on one GPU" if args.loopback > 1 else "single GPU")),
+                                (f"loopback {PART_NAME[args.partition]} x{args.loopback} on one GPU" if args.loopback > 1 else "single GPU")),
             },
             "roofline": roofline(args.workload + variant, world, layout, kavg_ms, bytes_total / world,
                                  mbytes_total / world, stream, use_pin=pin_ok, flops=alg_flops(order, ne_own)),

@@ -647,6 +647,7 @@ class BilinearForm:
 # ----------------------------------------------------------------------------
 _PAR_SIGS = {
     "ecm2_partition_slabs_z": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "ecm2_partition_bricks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     "ecm2_partition_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                              ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "ecm2_partition_info": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_int)] * 6),
@@ -748,6 +749,19 @@ def partition_boxes(mesh: Mesh, parts) -> np.ndarray:
     t = n * (c - lo) / span
     idx = np.clip(np.floor(t + 1e-12 * np.maximum(1.0, np.abs(t))), 0, n - 1).astype(np.int64)
     return np.ascontiguousarray(idx[:, 0] + n[0] * (idx[:, 1] + n[1] * idx[:, 2]), np.int32)
+
+
+def partition_bricks(mesh: Mesh, nranks: int, cell: int = 4) -> np.ndarray:
+    """Equal runs of whole cell^3 element bricks of a Cartesian mesh in lexicographic (x-fastest)
+    brick order, element -> rank (ecm2_partition_bricks).  Every part is a union of the 4 x 4 x 4
+    bricks the fused kernels assemble (bricks.hpp aligns them at the part's minimum corner), so a
+    RAP-decomposed rank holds no leftover element-map blocks and takes the k(T) coefficient
+    snapshot; the parts' brick counts differ by at most one.  (Not a reference partitioner: the
+    reference offers METIS and Mesh::CartesianPartitioning; Partition accepts any element -> rank
+    map.)"""
+    out = np.empty(mesh.GetNE(), np.int32)
+    _check(_par_lib().ecm2_partition_bricks(mesh._h, nranks, cell, _np_ptr(out)))
+    return out
 
 
 def quadrature_points_subset(mesh: Mesh, q1d: int, elems: np.ndarray) -> np.ndarray:

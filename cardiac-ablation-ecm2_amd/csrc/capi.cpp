@@ -573,6 +573,15 @@ int ecm2_partition_slabs_z(const ecm2_mesh *m, int nranks, int *elem_rank)
    });
 }
 
+int ecm2_partition_bricks(const ecm2_mesh *m, int nranks, int cell, int *elem_rank)
+{
+   return guard([&] {
+      NEED(m); NEED(elem_rank);
+      const std::vector<int> er = ecm2::partition_bricks(m->m, nranks, cell);
+      std::memcpy(elem_rank, er.data(), er.size() * sizeof(int));
+   });
+}
+
 int ecm2_partition_create(const ecm2_h1space *s, const ecm2_mesh *m, const int *elem_rank, int rank,
                           int nranks, ecm2_partition **out)
 {

@@ -23,6 +23,23 @@ std::vector<int> partition_slabs_z(const HexMesh &m, int nranks)
    return er;
 }
 
+std::vector<int> partition_bricks(const HexMesh &m, int nranks, int cell)
+{
+   ECM2_VERIFY(m.nx > 0, ERR_ARG, "brick partition needs a Cartesian mesh");
+   ECM2_VERIFY(cell >= 1, ERR_ARG, "bad brick edge " << cell);
+   const long bx = (m.nx + cell - 1) / cell, by = (m.ny + cell - 1) / cell, bz = (m.nz + cell - 1) / cell;
+   const long nb = bx * by * bz;
+   ECM2_VERIFY(nranks >= 1 && nranks <= nb, ERR_ARG, "bad rank count " << nranks << " for " << nb << " bricks");
+   std::vector<int> er(m.ne);
+   for (int e = 0; e < m.ne; e++)
+   {
+      const long l = m.lex_index(e), ix = l % m.nx, iy = (l / m.nx) % m.ny, iz = l / ((long)m.nx * m.ny);
+      const long b = ix / cell + bx * (iy / cell + by * (iz / cell));
+      er[e] = (int)(b * nranks / nb);  // equal runs of the lexicographic brick order
+   }
+   return er;
+}
+
 LocalPart build_local_part(const H1Space &s, const std::vector<int> &elem_rank, int rank, int nranks,
                            const HexMesh *cart, bool overlap)
 {

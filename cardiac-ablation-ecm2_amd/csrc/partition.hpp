@@ -66,6 +66,11 @@ std::vector<Xfer> exchange_schedule(const LocalPart &p, bool transpose);
 // for a 1 x 1 x nranks grid): elem_rank[e].
 std::vector<int> partition_slabs_z(const HexMesh &m, int nranks);
 
+// Equal runs of whole cell^3 bricks of a Cartesian mesh in lexicographic (x-fastest) brick order
+// (not a reference partitioner): every part is a union of the bricks the fused kernels assemble,
+// so an owned-elements (RAP) rank has no leftover element-map blocks.  elem_rank[e].
+std::vector<int> partition_bricks(const HexMesh &m, int nranks, int cell);
+
 // cart (optional): the global mesh when it is Cartesian; interior and boundary element groups
 // are then each put in brick order (one 4x4x4 brick per wave).
 LocalPart build_local_part(const H1Space &s, const std::vector<int> &elem_rank, int rank, int nranks,

@@ -332,6 +332,11 @@ typedef struct ecm2_partition ecm2_partition;
 /* Mesh::CartesianPartitioning along z (mesh/mesh.cpp:8966) of a lexicographic Cartesian
  * mesh: elem_rank host [ne]. */
 int ecm2_partition_slabs_z(const ecm2_mesh *m, int nranks, int *elem_rank);
+/* Not a reference interface (the reference partitions with METIS or CartesianPartitioning):
+ * equal runs of whole cell^3 element bricks of a Cartesian mesh in lexicographic brick order,
+ * so that an owned-elements (ECM2_DECOMP_RAP) rank holds only the bricks the fused kernels
+ * assemble (and takes the k(T) coefficient snapshot).  elem_rank host [ne]. */
+int ecm2_partition_bricks(const ecm2_mesh *m, int nranks, int cell, int *elem_rank);
 /* Per-rank local space of a global H1 space and an element partition (ParMesh +
  * ParFiniteElementSpace, pmesh.hpp:33, pfespace.cpp:1389-1418): local L-vector
  * [owned | ghost], owner = lowest touching rank, local elements [interior | boundary],

@@ -289,23 +289,27 @@ def test_gpu_loopback_group_matches_serial(kind, nranks, order, scatter, decomp)
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("decomp", ["rap", "overlap"])
-def test_gpu_loopback_group_coefficient_snapshot(decomp):
-    """Two z-slabs of 4 element layers (RAP: every local block a 4x4x4 brick -- rank 0's regular,
-    rank 1's lattice-mapped with the ghost plane -- so both take the k(T) snapshot on the split
-    L-vector; OVERLAP adds rank 0 a fifth layer, which keeps the stored pairs there): the group Mult
-    matches the serial oracle with beta = k(T) projected at the points."""
+@pytest.mark.parametrize("split", ["slabs", "bricks"])
+def test_gpu_loopback_group_coefficient_snapshot(decomp, split):
+    """slabs: two z-slabs of 4 element layers (RAP: every local block a 4x4x4 brick -- rank 0's
+    regular, rank 1's lattice-mapped with the ghost plane -- so both take the k(T) snapshot on the
+    split L-vector; OVERLAP adds rank 0 a fifth layer, which keeps the stored pairs there).  bricks:
+    partition_bricks of a 12 x 8 x 8 grid into 3 runs of 4 bricks (rank 1 holds half of each brick
+    layer: a stepped interface), every RAP rank on bricks alone.  The group Mult matches the serial
+    oracle with beta = k(T) projected at the points."""
     import torch
-    m = E.Mesh.MakeCartesian3D(8, 8, 8)
+    m = E.Mesh.MakeCartesian3D(8, 8, 8) if split == "slabs" else E.Mesh.MakeCartesian3D(12, 8, 8)
     order = 2
     fes = E.H1Space(m, order)
-    er = E.partition_slabs_z(m, 2)
+    nr = 2 if split == "slabs" else 3
+    er = E.partition_slabs_z(m, 2) if split == "slabs" else E.partition_bricks(m, 3)
     q1d = O.default_q1d(order)
     T = temperature(fes.dof_coords())
     scale, slope, tref = 0.05, 0.0012, 37.0
     forms, xs, ys, parts = [], [], [], []
     xg = np.random.default_rng(4).uniform(-1, 1, fes.ndofs)
-    for r in range(2):
-        part = E.Partition(fes, er, r, 2, decomposition=decomp)
+    for r in range(nr):
+        part = E.Partition(fes, er, r, nr, decomposition=decomp)
         pf = E.ParBilinearForm(part)
         P = E.quadrature_points_subset(m, q1d, part.elems)
         a = torch.as_tensor(alpha_bioheat(P).reshape(part.ne_local, -1)).cuda()
@@ -314,7 +318,10 @@ def test_gpu_loopback_group_coefficient_snapshot(decomp):
         pf.AddDomainIntegrator(E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(Tl, scale, slope, tref)))
         pf.Assemble()
         # (OVERLAP: rank 0 holds 5 layers, a leftover layer of non-brick blocks; rank 1's 4 layers are bricks)
-        assert pf.CoefficientSnapshot() == (decomp == "rap" or r == 1)
+        if split == "slabs":
+            assert pf.CoefficientSnapshot() == (decomp == "rap" or r == 1)
+        elif decomp == "rap":
+            assert pf.CoefficientSnapshot()
         forms.append(pf)
         parts.append(part)
         xs.append(torch.as_tensor(xg[part.owned_global]).cuda())
@@ -608,6 +615,36 @@ def test_partition_boxes():
         inside = np.all((c >= lo - 1e-12) & (c <= hi + 1e-12), axis=1)
         assert np.array_equal(inside, r == k)
     assert np.array_equal(E.partition_boxes(m, (1, 1, 4)), E.partition_slabs_z(m, 4))
+
+
+@pytest.mark.parametrize("dims,nranks", [((12, 8, 8), 3), ((10, 9, 13), 4), ((16, 16, 16), 8), ((5, 4, 4), 2)])
+def test_partition_bricks(dims, nranks):
+    """partition_bricks: every 4 x 4 x 4 brick of the grid (partial at a ragged edge) lies in one
+    part, the parts are runs of the lexicographic brick order and their brick counts differ by
+    at most one."""
+    m = E.Mesh.MakeCartesian3D(*dims)
+    r = E.partition_bricks(m, nranks)
+    c = m.element_nodes().mean(axis=2)
+    h = 1.0 / np.array(dims, float)
+    idx = np.floor(c / h).astype(int)
+    nb = [-(-d // 4) for d in dims]
+    b = idx // 4
+    lin = b[:, 0] + nb[0] * (b[:, 1] + nb[1] * b[:, 2])
+    per = {}
+    for bl, rr in zip(lin, r):
+        per.setdefault(int(bl), set()).add(int(rr))
+    assert all(len(v) == 1 for v in per.values())
+    owner = np.array([next(iter(per[k])) for k in sorted(per)])
+    assert np.all(np.diff(owner) >= 0) and owner[0] == 0 and owner[-1] == nranks - 1
+    counts = np.bincount(owner, minlength=nranks)
+    assert counts.max() - counts.min() <= 1
+    with pytest.raises(E.ECM2Error):
+        E.partition_bricks(m, int(np.prod(nb)) + 1)
+    # a renumbered (SFC) element order partitions the same elements
+    ms = E.Mesh.MakeCartesian3D(*dims, sfc_ordering=True)
+    cs = ms.element_nodes().mean(axis=2)
+    key = lambda cc: np.lexsort(np.round(cc, 9).T[::-1])
+    assert np.array_equal(E.partition_bricks(ms, nranks)[key(cs)], r[key(c)])
 
 
 def test_partition_boxes_uneven_counts():

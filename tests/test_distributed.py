@@ -306,7 +306,7 @@ def test_gpu_loopback_group_coefficient_snapshot(decomp, split):
     q1d = O.default_q1d(order)
     T = temperature(fes.dof_coords())
     scale, slope, tref = 0.05, 0.0012, 37.0
-    forms, xs, ys, parts = [], [], [], []
+    forms, xs, ys, parts, mixed = [], [], [], [], []
     xg = np.random.default_rng(4).uniform(-1, 1, fes.ndofs)
     for r in range(nr):
         part = E.Partition(fes, er, r, nr, decomposition=decomp)
@@ -322,10 +322,14 @@ def test_gpu_loopback_group_coefficient_snapshot(decomp, split):
             assert pf.CoefficientSnapshot() == (decomp == "rap" or r == 1)
         elif decomp == "rap":
             assert pf.CoefficientSnapshot()
+            lat, units, _ = pf.AddressingInfo()
+            mixed.append(0 < lat < units)  # regular and lattice-map blocks in one form (snapshot kernel RM 2)
         forms.append(pf)
         parts.append(part)
         xs.append(torch.as_tensor(xg[part.owned_global]).cuda())
         ys.append(torch.full((part.n_owned,), float("nan"), dtype=torch.float64, device="cuda"))
+    if split == "bricks" and decomp == "rap":
+        assert any(mixed)  # (rank 0's L-shaped bricks: the full-width one regular, the other not)
     E.ParGroup(forms).Mult(xs, ys)
     torch.cuda.synchronize()
     y = np.zeros(fes.ndofs)

@@ -21,7 +21,7 @@ from helpers import GOLDEN, RTOL, alpha_bioheat, coeff_function, nonaligned, rel
 
 
 def _mesh(kind):
-    if kind == "cart_big":  # slabs with whole 64-element interior blocks (brick segments)
+    if kind in ("cart_big", "bricks"):  # slabs with whole 64-element interior blocks (brick segments)
         m = E.Mesh.MakeCartesian3D(8, 8, 12, 1.0, 1.0, 1.5)
         m.set_vertices(nonaligned(m.vertices()))
         return m
@@ -37,11 +37,13 @@ def _mesh(kind):
 def _elem_rank(m, kind, nranks):
     if kind in ("cart", "cart_big"):
         return E.partition_slabs_z(m, nranks)
+    if kind == "bricks":  # runs of whole 4x4x4 bricks (stepped interfaces, partition_bricks)
+        return E.partition_bricks(m, nranks)
     rng = np.random.default_rng(5)  # irregular partition: random element owners
     return rng.integers(0, nranks, m.GetNE()).astype(np.int32)
 
 
-@pytest.mark.parametrize("kind", ["cart", "fichera"])
+@pytest.mark.parametrize("kind", ["cart", "fichera", "bricks"])
 @pytest.mark.parametrize("nranks", [2, 3, 4])
 @pytest.mark.parametrize("decomp", ["rap", "overlap"])
 def test_partition_invariants(kind, nranks, decomp):
@@ -154,7 +156,7 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("kind,nranks", [("cart", 2), ("fichera", 3)])
+@pytest.mark.parametrize("kind,nranks", [("cart", 2), ("fichera", 3), ("bricks", 5)])
 @pytest.mark.parametrize("decomp", ["rap", "overlap"])
 def test_gloo_exchange_matches_serial(tmp_path, kind, nranks, decomp):
     import torch.multiprocessing as mp

@@ -6,8 +6,8 @@ set -uo pipefail
 O=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/r4mb2
 mkdir -p "$O"
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_distributed.py \
-  > "$O/tests.txt" 2>&1 || { tail -40 "$O/tests.txt"; exit 1; }
+timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_distributed.py \
+  tests/test_gpu_parity.py -k "not test_gpu_parity.py or snapshot" > "$O/tests.txt" 2>&1 || { tail -40 "$O/tests.txt"; exit 1; }
 tail -1 "$O/tests.txt"
 show() { python3 -c "import json,sys; b=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], 'N=%d' % b['emulated_n_gpus'], 'slowest', b['slowest_member_ms'], 'members', b['member_ms'], 'snapshot', b.get('coefficient_snapshot'))" "$1" "$2"; }
 timeout -k 10 300 python3 bench.py --workload c4 --steps 50 --warmup 5 --no-cpu-baseline --full-layout 0 --variants 0 > "$O/n1.json" 2> "$O/n1.err" || exit 1

@@ -293,11 +293,11 @@ def test_gpu_loopback_group_matches_serial(kind, nranks, order, scatter, decomp)
 @pytest.mark.parametrize("decomp", ["rap", "overlap"])
 @pytest.mark.parametrize("split", ["slabs", "slabs8", "bricks"])
 def test_gpu_loopback_group_coefficient_snapshot(decomp, split):
-    """slabs: two z-slabs of 4 element layers (RAP: every local block a 4x4x4 brick -- rank 0's
-    regular, rank 1's lattice-mapped with the ghost plane -- so both take the k(T) snapshot on the
-    split L-vector; OVERLAP adds rank 0 a fifth layer, which keeps the stored pairs there).  slabs8:
-    two slabs of 8 layers; RAP rank 1's lower bricks touch the ghost plane (lattice-map), its upper
-    ones do not (regular): the snapshot kernel's mixed form (RM 2, dof-order T').  bricks:
+    """slabs: two z-slabs of 4 element layers (RAP: every local block a 4x4x4 lattice-map brick, so
+    both take the k(T) snapshot on the split L-vector; OVERLAP adds rank 0 a fifth layer, which keeps
+    the stored pairs there).  slabs8: two slabs of 8 layers in the lattice numbering; RAP rank 1's
+    lower bricks touch the ghost plane (lattice-map), its upper ones do not (regular): the snapshot
+    kernel's mixed form (RM 2, dof-order T'), rank 0 all regular.  bricks:
     partition_bricks of a 12 x 8 x 8 grid into 3 runs of 4 bricks (stepped interfaces), every RAP
     rank on bricks alone.  The group Mult matches the serial oracle with beta = k(T) projected at
     the points."""
@@ -305,7 +305,8 @@ def test_gpu_loopback_group_coefficient_snapshot(decomp, split):
     m = {"slabs": (8, 8, 8), "slabs8": (8, 8, 16), "bricks": (12, 8, 8)}[split]
     m = E.Mesh.MakeCartesian3D(*m)
     order = 2
-    fes = E.H1Space(m, order)
+    # (slabs8: the lattice numbering, whose owned-only bricks are regular; the others the entity numbering)
+    fes = E.H1Space(m, order, E.NUMBERING_STRUCTURED if split == "slabs8" else E.NUMBERING_ENTITY)
     nr = 3 if split == "bricks" else 2
     er = E.partition_bricks(m, 3) if split == "bricks" else E.partition_slabs_z(m, 2)
     q1d = O.default_q1d(order)

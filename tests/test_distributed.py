@@ -847,7 +847,7 @@ def _worker_pcg(rank, nranks, port, kind, result_path, decomp, max_iter):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind,nranks", [("cart", 2), ("cart", 3), ("fichera", 2), ("fichera", 3)])
+@pytest.mark.parametrize("kind,nranks", [("cart", 2), ("cart", 3), ("fichera", 2), ("fichera", 3), ("bricks", 3)])
 @pytest.mark.parametrize("decomp", ["rap", "overlap"])
 def test_gloo_pcg_reductions_match_serial(tmp_path, kind, nranks, decomp):
     """The distributed constrained Jacobi-PCG between processes: the product's step order with

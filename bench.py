@@ -339,8 +339,7 @@ def main():
                     help="N>1 on one GPU: N subdomains in this process (validation of the partitioned path)")
     ap.add_argument("--partition", choices=["slabs", "boxes", "bricks"], default="slabs",
                     help="N > 1: z-slabs (CartesianPartitioning along z), px x py x pz boxes (2x2x2 at N = 8) "
-                         "or equal runs of whole 4x4x4 bricks (partition_bricks; with ECM2_DECOMP=rap every "
-                         "rank's blocks are bricks)")
+                         "or equal runs of whole 4x4x4 bricks (partition_bricks: balanced to one brick)")
     ap.add_argument("--member", type=int, default=None,
                     help="with --loopback N (z-slabs, OVERLAP): time member R's rows alone, as one rank runs "
                          "them on its own GPU (HIP graph); -1 = every member, the slowest sets the emulated rate")

@@ -754,11 +754,10 @@ def partition_boxes(mesh: Mesh, parts) -> np.ndarray:
 def partition_bricks(mesh: Mesh, nranks: int, cell: int = 4) -> np.ndarray:
     """Equal runs of whole cell^3 element bricks of a Cartesian mesh in lexicographic (x-fastest)
     brick order, element -> rank (ecm2_partition_bricks).  Every part is a union of the 4 x 4 x 4
-    bricks the fused kernels assemble (bricks.hpp aligns them at the part's minimum corner), so a
-    RAP-decomposed rank holds no leftover element-map blocks and takes the k(T) coefficient
-    snapshot; the parts' brick counts differ by at most one.  (Not a reference partitioner: the
-    reference offers METIS and Mesh::CartesianPartitioning; Partition accepts any element -> rank
-    map.)"""
+    bricks the fused kernels assemble (bricks.hpp aligns them at the part's minimum corner), and
+    the parts' brick counts differ by at most one (z-slabs differ by a whole layer).  (Not a
+    reference partitioner: the reference offers METIS and Mesh::CartesianPartitioning; Partition
+    accepts any element -> rank map.  Measured against z-slabs: DESIGN.md §6.)"""
     out = np.empty(mesh.GetNE(), np.int32)
     _check(_par_lib().ecm2_partition_bricks(mesh._h, nranks, cell, _np_ptr(out)))
     return out

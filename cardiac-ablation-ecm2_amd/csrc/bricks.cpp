@@ -60,11 +60,10 @@ FaceNeighbors face_neighbors(int ne, int D, const std::vector<int> &gm)
    return N;
 }
 
-std::vector<int> face_brick_order(int ne, int D, const std::vector<int> &gm, int *n_in_bricks)
+std::vector<int> face_brick_order(int ne, int D, const std::vector<int> &gm)
 {
    std::vector<int> perm;
    perm.reserve(ne);
-   if (n_in_bricks) { *n_in_bricks = 0; }
    if (ne == 0) { return perm; }
    const FaceNeighbors N = face_neighbors(ne, D, gm);
    std::vector<int> lo[3];
@@ -182,7 +181,6 @@ std::vector<int> face_brick_order(int ne, int D, const std::vector<int> &gm, int
          used[e] = 1;
       }
    }
-   if (n_in_bricks) { *n_in_bricks = (int)perm.size(); }
    for (int e = 0; e < ne; e++) { if (!used[e]) { perm.push_back(e); } }
    return perm;
 }

@@ -28,9 +28,8 @@ FaceNeighbors face_neighbors(int ne, int D, const std::vector<int> &gmap);
 // order of first element), then every element in no
 // brick in its original order.  Lattice coordinates come from a breadth-first walk of the
 // face links (per connected patch), so bricks align with the patch's own grid (a refined
-// fichera hex is a 64^3 patch).  Returns perm (internal position -> element); n_in_bricks
-// (optional): how many elements the bricks hold (the first n_in_bricks of perm).
-std::vector<int> face_brick_order(int ne, int D, const std::vector<int> &gmap, int *n_in_bricks = nullptr);
+// fichera hex is a 64^3 patch).  Returns perm (internal position -> element).
+std::vector<int> face_brick_order(int ne, int D, const std::vector<int> &gmap);
 
 // 2 x 2 x bz groups for the p >= 3 brick kernel (bz = 1, 2, or 4 / 8 for the column
 // bricks the kernel marches layer by layer): greedy in element order, all internal faces

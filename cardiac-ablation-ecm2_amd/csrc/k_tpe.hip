@@ -971,7 +971,7 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                const int *__restrict__ lane_flags, double *__restrict__ part, const int *__restrict__ treg,
                int pstride, const int *__restrict__ lmap)
 {
-   static_assert(RM >= 1 && RM <= 3, "lattice blocks only");
+   static_assert(RM == 1 || RM == 3, "lattice blocks only");
    static_assert(D == 3 && Q == 4, "p = 2");
    constexpr int ND = D * D * D, NR = Q * Q, XR = XwaveRows<D>::R, WPG = 4, P = D - 1;
    constexpr int NLP = tpe_lattice_points(D);
@@ -989,7 +989,7 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
    // time, profiles/r4/ab_pfd.txt)
    v2d *sPL = reinterpret_cast<v2d *>(&sU[w][0][0]);
    TpeReg rg = {};
-   int regf = RM == 1 ? 1 : 2;
+   const int regf = RM == 1 ? 1 : 2;
    double Yo[ND];
 #pragma unroll
    for (int a = 0; a < ND; a++) { Yo[a] = 0.0; }
@@ -1009,11 +1009,10 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
       for (int k = 0; k < 3; k++) { ce[k] = ld2(qc + k * 128); }
       load_row(0, ra[0]);
       load_row(1, ra[1]);
-      if (RM != 3)
+      if (RM == 1)
       {
          const int *r = treg + (size_t)blk * 8;  // wave-uniform: scalar loads
          rg = TpeReg{r[0], r[1], r[2], r[3], r[4]};
-         if (RM == 2) { regf = r[7]; }  // (mixed forms: this block regular or lattice-map)
       }
       const int *lm = lmap + (size_t)blk * NLP;
 #pragma unroll
@@ -1023,14 +1022,13 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
          if (j < NLP)
          {
             int d;
-            if (RM == 3 || (RM == 2 && regf == 2)) { d = bdof(lm[j]); }
+            if (RM == 3) { d = bdof(lm[j]); }
             else
             {
                const unsigned v = lattice_xyz<D>(j);
                d = rg.base + (int)(v & 31) * rg.sx + (int)((v >> 5) & 31) * rg.sy + (int)(v >> 10) * rg.sz;
             }
-            // (lattice-map blocks: the snapshot is stored in their slot order, a contiguous read; a
-            // mixed form's (RM 2) snapshot is in dof order, the ghost dofs' T' included)
+            // (lattice-map blocks: the snapshot is stored in their slot order, a contiguous read)
             sPL[j] = v2d{(!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned], RM == 3 ? tsn[(size_t)blk * NLP + j] : tsn[d]};
          }
       }
@@ -1479,8 +1477,7 @@ void launch_tpe(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipS
       // the diffusion coefficient from its temperature snapshot: only W alpha det J per point
       if constexpr (DIFF && D == 3 && Q == 4)
       {
-         ECM2_VERIFY(a.pw == (MASS ? 1 : 0) && a.treg && (a.treg_all || a.tlat_all || a.tmix_all) &&
-                         a.tsnap_kind == (a.tlat_all ? 2 : 1),
+         ECM2_VERIFY(a.pw == (MASS ? 1 : 0) && a.treg && (a.treg_all || a.tlat_all) && a.tsnap_kind == (a.treg_all ? 1 : 2),
                      ERR_INTERNAL, "coefficient snapshot needs lattice blocks and the mass-only point values");
          Basis1D bw = b;  // (w B): the weight-scaled interpolation of T'
          for (int d = 0; d < MAX_D1D; d++)
@@ -1490,8 +1487,7 @@ void launch_tpe(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipS
                       a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.tsnap, a.y, a.yg, b, bw, a.lane_flags, a.part,  \
                       a.treg, a.part_stride, a.lmap)
          if (a.treg_all) { ECM2_TS(1); }
-         else if (a.tlat_all) { ECM2_TS(3); }
-         else { ECM2_TS(2); }
+         else { ECM2_TS(3); }
 #undef ECM2_TS
       }
       else { ECM2_VERIFY(false, ERR_INTERNAL, "coefficient snapshot: p = 2 forms with the diffusion integrator"); }

@@ -179,7 +179,6 @@ struct ApplyArgs
    const int *treg = nullptr;       // device [blk][8]: 4x4x4 blocks (base, sx, sy, sz, face mask, -, -, flag: 1 regular, 2 lattice slots), or null
    int treg_all = 0;                // every block regular
    int tlat_all = 0;                // every block a lattice-map block (treg flag 2)
-   int tmix_all = 0;                // every block regular or lattice-map, both present (flags 1 / 2)
    int part_stride = 0;             // p <= 2 partial slots per block (27 * 64, or the lattice surface when treg_all)
    const int *lmap = nullptr;       // device [blk][tpe_lattice_points]: lattice-slot blocks' lattice maps, or null
    QPts qp = {};                    // TRILINEAR: the quadrature points

@@ -800,7 +800,6 @@ void PAForm::assemble(hipStream_t s)
       treg_.resize(0);
       treg_all_ = false;
       tlat_all_ = false;
-      tmix_all_ = false;
       n_treg_ = 0;
       n_tlat_ = 0;
       lmap_.resize(0);
@@ -904,7 +903,6 @@ void PAForm::assemble(hipStream_t s)
             treg_.upload(reg, s);
             treg_all_ = nreg == nblk && (latency_from_ < 0 || latency_from_ >= nblk);
             tlat_all_ = nlat == nblk && (latency_from_ < 0 || latency_from_ >= nblk);
-            tmix_all_ = nreg && nlat && nreg + nlat == nblk && (latency_from_ < 0 || latency_from_ >= nblk);
          }
       }
       part_stride_ = treg_all_ || tlat_all_ ? ns : ND_ * 64;
@@ -1139,7 +1137,7 @@ void PAForm::assemble(hipStream_t s)
    layout_.tsnap = 0;
    tsnap_.resize(0);
    if (tsnap_pref_ && layout_.kind == QLAYOUT_AFFINE && resolved_mode_ == KERNEL_TPE && D_ == 3 && Q_ == 4 &&
-       (treg_all_ || tlat_all_ || tmix_all_) && have_diff_ && cdiff_.kind == COEFF_GRIDFUNC_AFFINE && cdiff_.lvec &&
+       (treg_all_ || tlat_all_) && have_diff_ && cdiff_.kind == COEFF_GRIDFUNC_AFFINE && cdiff_.lvec &&
        !marked_[INTEG_DIFFUSION])
    {
       layout_.tsnap = 1;
@@ -1147,10 +1145,8 @@ void PAForm::assemble(hipStream_t s)
       // T' = A + B T at every dof (the interpolated T' is the law at the point: the basis sums to
       // 1), taken here only: later setups (the marker diagonal's) keep the Assemble-time field
       const double A = cdiff_.scale * (1.0 - cdiff_.slope * cdiff_.t_ref), B = cdiff_.scale * cdiff_.slope;
-      if (!tlat_all_)
+      if (treg_all_)
       {
-         // (dof order: regular blocks compute their dofs; a mixed form's lattice-map blocks -- a
-         // partitioned rank's ghost-touching bricks -- read T' through the same dof as x)
          tsnap_.resize(std::max(1, ndofs_));
          kern::affine_snapshot(ndofs_, cdiff_.lvec, A, B, tsnap_.data(), s);
       }
@@ -1426,7 +1422,6 @@ ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, doubl
    a.treg = treg_.size() ? treg_.data() : nullptr;
    a.treg_all = treg_all_ ? 1 : 0;
    a.tlat_all = tlat_all_ ? 1 : 0;
-   a.tmix_all = tmix_all_ ? 1 : 0;
    a.lmap = lmap_.size() ? lmap_.data() : nullptr;
    for (int q = 0; q < Q_ && q < MAX_Q1D; q++) { a.qp.x[q] = maps_.qpts[q]; a.qw[q] = maps_.qw1[q]; }
    a.tsnap = layout_.tsnap ? tsnap_.data() : nullptr;

@@ -241,7 +241,6 @@ private:
    DeviceArray<int> treg_;          // TPE blocks: [nblk][8] (base, sx, sy, sz, face mask, -, -, flag 1 regular / 2 lattice slots)
    bool treg_all_ = false;          // every TPE block regular: face-grouped slots only
    bool tlat_all_ = false;          // every TPE block a lattice-map block (treg flag 2)
-   bool tmix_all_ = false;          // every TPE block regular or lattice-map, both kinds present
    int n_treg_ = 0;                 // regular TPE blocks
    int n_tlat_ = 0;                 // TPE blocks with face-grouped slots but map-addressed dofs (treg flag 2)
    DeviceArray<int> lmap_;          // their block lattice maps [nblk][tpe_lattice_points] (tpe_lattice_slot order)

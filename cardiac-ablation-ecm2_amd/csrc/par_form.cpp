@@ -1,6 +1,5 @@
 // par_form.cpp -- see par_form.hpp.
 #include "par_form.hpp"
-#include "bricks.hpp"
 
 #include <rccl/rccl.h>
 
@@ -160,17 +159,8 @@ void ParPAForm::set_schedule(bool serial, int graph)
       // layer, so none of them touches a ghost dof and all are lattice-addressed (anchored at the
       // local mesh's first layer, the bricks of the ghost-touching bottom layer read the map).
       // A split on a multiple of 4 blocks keeps the plan's workgroups (4 blocks from each
-      // segment's start) those of the single launch.  A local mesh made of whole bricks
-      // (partition_bricks with RAP) is ordered as one segment instead: every block is then a
-      // brick -- regular inside, lattice-map where it touches ghost dofs -- and the form can take
-      // the k(T) coefficient snapshot (the segments would cut the bricks along the ghost layer).
-      if (all_bricks_ < 0)
-      {
-         int nb = 0;
-         (void)face_brick_order(part_.ne_local, part_.order + 1, part_.gather_map, &nb);
-         all_bricks_ = part_.ne_local > 0 && nb == part_.ne_local ? 1 : 0;
-      }
-      local_->set_block_splits(all_bricks_ ? std::vector<int>{} : std::vector<int>{bi / 4 * 4});
+      // segment's start) those of the single launch.
+      local_->set_block_splits({bi / 4 * 4});
       local_->set_latency_from(-1);
    }
 }

@@ -99,7 +99,6 @@ private:
    bool pack_needed_ = false;           // some P send goes through the packed buffer
    bool serial_ = true;                 // serial schedule (serial())
    int graph_mode_ = -1;                // set_schedule
-   int all_bricks_ = -1;                // the local elements are whole face-linked bricks (-1: not yet known)
    DeviceArray<int> send_idx_;
    DeviceArray<double> sendbuf_, xg_, yg_, rbuf_, dl_;
    void *comm_ = nullptr;               // ncclComm_t

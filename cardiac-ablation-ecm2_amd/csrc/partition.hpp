@@ -68,7 +68,7 @@ std::vector<int> partition_slabs_z(const HexMesh &m, int nranks);
 
 // Equal runs of whole cell^3 bricks of a Cartesian mesh in lexicographic (x-fastest) brick order
 // (not a reference partitioner): every part is a union of the bricks the fused kernels assemble,
-// so an owned-elements (RAP) rank has no leftover element-map blocks.  elem_rank[e].
+// balanced to one brick.  elem_rank[e].
 std::vector<int> partition_bricks(const HexMesh &m, int nranks, int cell);
 
 // cart (optional): the global mesh when it is Cartesian; interior and boundary element groups

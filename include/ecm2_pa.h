@@ -334,8 +334,9 @@ typedef struct ecm2_partition ecm2_partition;
 int ecm2_partition_slabs_z(const ecm2_mesh *m, int nranks, int *elem_rank);
 /* Not a reference interface (the reference partitions with METIS or CartesianPartitioning):
  * equal runs of whole cell^3 element bricks of a Cartesian mesh in lexicographic brick order,
- * so that an owned-elements (ECM2_DECOMP_RAP) rank holds only the bricks the fused kernels
- * assemble (and takes the k(T) coefficient snapshot).  elem_rank host [ne]. */
+ * so that an owned-elements (ECM2_DECOMP_RAP) rank holds only whole bricks of the fused
+ * kernels' blocks (balanced to one brick; measured against z-slabs in DESIGN.md §6).
+ * elem_rank host [ne]. */
 int ecm2_partition_bricks(const ecm2_mesh *m, int nranks, int cell, int *elem_rank);
 /* Per-rank local space of a global H1 space and an element partition (ParMesh +
  * ParFiniteElementSpace, pmesh.hpp:33, pfespace.cpp:1389-1418): local L-vector

@@ -291,28 +291,23 @@ def test_gpu_loopback_group_matches_serial(kind, nranks, order, scatter, decomp)
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("decomp", ["rap", "overlap"])
-@pytest.mark.parametrize("split", ["slabs", "slabs8", "bricks"])
+@pytest.mark.parametrize("split", ["slabs", "bricks"])
 def test_gpu_loopback_group_coefficient_snapshot(decomp, split):
     """slabs: two z-slabs of 4 element layers (RAP: every local block a 4x4x4 lattice-map brick, so
     both take the k(T) snapshot on the split L-vector; OVERLAP adds rank 0 a fifth layer, which keeps
-    the stored pairs there).  slabs8: two slabs of 8 layers in the lattice numbering; RAP rank 1's
-    lower bricks touch the ghost plane (lattice-map), its upper ones do not (regular): the snapshot
-    kernel's mixed form (RM 2, dof-order T'), rank 0 all regular.  bricks:
-    partition_bricks of a 12 x 8 x 8 grid into 3 runs of 4 bricks (stepped interfaces), every RAP
-    rank on bricks alone.  The group Mult matches the serial oracle with beta = k(T) projected at
-    the points."""
+    the stored pairs there).  bricks: partition_bricks of a 12 x 8 x 8 grid into 3 runs of 4 bricks
+    (stepped interfaces; whichever layout each rank's blocks allow).  The group Mult matches the
+    serial oracle with beta = k(T) projected at the points."""
     import torch
-    m = {"slabs": (8, 8, 8), "slabs8": (8, 8, 16), "bricks": (12, 8, 8)}[split]
-    m = E.Mesh.MakeCartesian3D(*m)
+    m = E.Mesh.MakeCartesian3D(8, 8, 8) if split == "slabs" else E.Mesh.MakeCartesian3D(12, 8, 8)
     order = 2
-    # (slabs8: the lattice numbering, whose owned-only bricks are regular; the others the entity numbering)
-    fes = E.H1Space(m, order, E.NUMBERING_STRUCTURED if split == "slabs8" else E.NUMBERING_ENTITY)
-    nr = 3 if split == "bricks" else 2
-    er = E.partition_bricks(m, 3) if split == "bricks" else E.partition_slabs_z(m, 2)
+    fes = E.H1Space(m, order)
+    nr = 2 if split == "slabs" else 3
+    er = E.partition_slabs_z(m, 2) if split == "slabs" else E.partition_bricks(m, 3)
     q1d = O.default_q1d(order)
     T = temperature(fes.dof_coords())
     scale, slope, tref = 0.05, 0.0012, 37.0
-    forms, xs, ys, parts, mixed = [], [], [], [], []
+    forms, xs, ys, parts = [], [], [], []
     xg = np.random.default_rng(4).uniform(-1, 1, fes.ndofs)
     for r in range(nr):
         part = E.Partition(fes, er, r, nr, decomposition=decomp)
@@ -326,16 +321,10 @@ def test_gpu_loopback_group_coefficient_snapshot(decomp, split):
         # (OVERLAP: rank 0 holds 5 layers, a leftover layer of non-brick blocks; rank 1's 4 layers are bricks)
         if split == "slabs":
             assert pf.CoefficientSnapshot() == (decomp == "rap" or r == 1)
-        elif decomp == "rap":
-            assert pf.CoefficientSnapshot()
-            lat, units, _ = pf.AddressingInfo()
-            mixed.append(0 < lat < units)  # regular and lattice-map blocks in one form (snapshot kernel RM 2)
         forms.append(pf)
         parts.append(part)
         xs.append(torch.as_tensor(xg[part.owned_global]).cuda())
         ys.append(torch.full((part.n_owned,), float("nan"), dtype=torch.float64, device="cuda"))
-    if split == "slabs8" and decomp == "rap":
-        assert mixed == [False, True]
     E.ParGroup(forms).Mult(xs, ys)
     torch.cuda.synchronize()
     y = np.zeros(fes.ndofs)

@@ -677,6 +677,10 @@ __device__ __forceinline__ unsigned lattice_xyz(int j)
    return kLatXYZ3.v[j];
 }
 
+// pairs of the TRILINEAR coefficients (c[3 (k - 1) + i] two per pair) that only the per-plane J
+// pieces read: k = 0, 1, 3 -> f = 0..5, 9..11 -> pairs 0, 1, 2, 5 (pair 4 also holds f = 8, a row one)
+__device__ __forceinline__ constexpr bool tlb_plane_pair(int k) { return k == 0 || k == 1 || k == 2 || k == 5; }
+
 // TRILINEAR apply for forms whose blocks are all 4x4x4 bricks of one dof lattice (RM 1: regular
 // blocks, 3: lattice-map blocks -- the structured numbering and the reference's numbering on a
 // brick-tiled mesh), at TWO waves per SIMD.  The per-element kernel above (k_apply_tpe_sf, TL)
@@ -733,7 +737,10 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
       // geometry and the first row's pairs first: independent of the gather chain
       const double *qc = qdd + (size_t)blk * NCE * 128 + lane * 2;
 #pragma unroll
-      for (int k = 0; k < NCE; k++) { ce[k] = ld2(qc + k * 128); }
+      for (int k = 0; k < NCE; k++)
+      {
+         if (!tlb_plane_pair(k)) { ce[k] = ld2(qc + k * 128); }  // (the plane-only pairs: per plane)
+      }
       load_row(0, ca);
       if (RM == 1)
       {
@@ -780,6 +787,19 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
          for (int dz = 0; dz < D; dz++) { bz[dz] = b.B[qz + MQ * dz]; gz[dz] = b.G[qz + MQ * dz]; }
          double pA[3], pB[3], pC[3];  // the plane's J pieces
          {
+            {
+               // the coefficients only the plane pieces use (c1, c2, c4) are read again per plane (an
+               // L2 hit) instead of being held through the rows: 16 VGPRs, which removes the 11-14
+               // spilled values (profiles/r4/ab_tlr.txt: kernel -2.7% trilinear, -3.4% drop-in).  (The
+               // opaque pointer keeps the loads in the plane loop.)
+               const double *qcp = qdd + (size_t)blk * NCE * 128 + lane * 2;
+               asm volatile("" : "+v"(qcp));
+#pragma unroll
+               for (int k = 0; k < NCE; k++)
+               {
+                  if (tlb_plane_pair(k)) { ce[k] = *reinterpret_cast<const v2d *>(qcp + k * 128); }
+               }
+            }
             // opaque per plane: otherwise the compiler hoists every plane's and row's J pieces out of
             // the plane loop into a table (in scratch)
             double zt = qp.x[qz];

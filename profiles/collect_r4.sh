@@ -9,6 +9,7 @@
 #   d: c4enttrijac (the drop-in configuration: reference numbering + trilinear mesh + MFEM Jacobians)
 #   b: c5 (bricks, affine_e), c5tri (trilinear mesh, trilinear_e), c3 (fichera r6)
 #   e: c4ent and c3 again (the lattice-map blocks' configurations)
+#   f: c4tri and c4enttrijac again (the TRILINEAR kernel's configurations)
 set -uo pipefail
 SET=${1:-a}
 O=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/collect_r4
@@ -40,6 +41,10 @@ elif [ "$SET" = e ]; then
   # (after the lattice-ordered snapshot: the two lattice-map-block configurations again)
   one c4ent affine_ts apply --workload c4 --numbering entity --steps 50 --warmup 5 || exit 1
   one c3 affine_ts apply --workload c3 --steps 30 --warmup 5 || exit 1
+elif [ "$SET" = f ]; then
+  # (after the TRILINEAR kernel's per-plane coefficient reload: its two configurations again)
+  one c4tri trilinear apply --workload c4 --mesh trilinear --steps 30 --warmup 5 || exit 1
+  one c4enttrijac trilinear apply --workload c4 --numbering entity --mesh trilinear --geometry-input jacobians --steps 30 --warmup 5 || exit 1
 elif [ "$SET" = d ]; then
   one c4enttrijac trilinear apply --workload c4 --numbering entity --mesh trilinear --geometry-input jacobians --steps 30 --warmup 5 || exit 1
 else

@@ -2,7 +2,8 @@
 # Round 4: the TRILINEAR lattice kernel with the plane-only map coefficients (c1, c2, c4) re-read per
 # plane instead of held through the rows (ECM2_TLB_RELOAD=1: 254-256 VGPRs, no spills, against 11-14
 # spilled values) -- parity on the trilinear tests with the variant library, then a same-box A/B on the
-# trilinear C4 mesh and the drop-in configuration.
+# trilinear C4 mesh and the drop-in configuration.  (Adopted: the reload is unconditional since 1d6d7f2 and
+# the ECM2_TLB_RELOAD switch is gone; the variant library was built at 64edb79 + -DECM2_TLB_RELOAD=1.)
 set -uo pipefail
 O=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/r4tlr
 mkdir -p "$O"

@@ -112,6 +112,40 @@ def bioheat_coefficients(E, torch, mesh, fes, part=None):
     return torch.as_tensor(alpha).cuda(), torch.as_tensor(T).cuda()
 
 
+def bench_integrators(E):
+    """The timed form's integrators: MassIntegrator(QuadratureCoefficient(alpha)) (the projected
+    FunctionCoefficient rho*c_eff(x)) and DiffusionIntegrator(AffineGridFunctionCoefficient(T, ...))
+    (gamma*dt*k(T) of the H1 temperature field)."""
+    mass = lambda a: E.MassIntegrator(E.QuadratureCoefficient(a))
+    diff = lambda T: E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(T, K_SCALE, K_SLOPE, K_TREF))
+    return mass, diff
+
+
+def bench_form(E, torch, mesh, fes, keep, kernel=0, scatter="partials", compress_geometry=True,
+               element_order="auto", geometry_input="nodes", coefficient_snapshot=True):
+    """The serial form every bench line times (and tests/test_gpu_timed_forms.py pins against the
+    oracle at the timed size): Mass(rho*c_eff(x)) + Diffusion(gamma*dt*k(T)) on `fes`, assembled.
+    element_order "faces": the reference's numbering, the form derives its order from the map alone.
+    geometry_input "jacobians": MFEM's GeometricFactors::JACOBIANS array, as the binding passes it.
+    The coefficient tensors are appended to `keep` (they must outlive the form's Assemble)."""
+    a, T = bioheat_coefficients(E, torch, mesh, fes)
+    keep.extend([a, T])
+    mass, diff = bench_integrators(E)
+    f = E.BilinearForm(fes, kernel=kernel, element_order=os.environ.get("ECM2_ELEMENT_ORDER", element_order),
+                       scatter=scatter, compress_geometry=compress_geometry,
+                       bricks=int(os.environ.get("ECM2_BRICKS", "-1")),  # A/B: p >= 3 brick depth
+                       geometry="jacobians" if geometry_input == "jacobians" else "nodes",
+                       coefficient_snapshot=coefficient_snapshot)
+    if geometry_input == "jacobians":
+        # MFEM's GeometricFactors::JACOBIANS (NQ x 3 x 3 x NE), as the binding passes it; the form
+        # fits it to trilinear maps (or checks it affine) at Assemble and keeps it for re-assembly
+        f.SetJacobians(mesh.jacobians(fes.order + 2))
+    f.AddDomainIntegrator(mass(a))
+    f.AddDomainIntegrator(diff(T))
+    f.Assemble()
+    return f
+
+
 def qdata_layout(E, form):
     """Quadrature-data layout of a (local) form: affine | affine_ts (AFFINE with the k(T)
     coefficient snapshot) | affine_e | trilinear | trilinear_e | blocked | native."""
@@ -411,30 +445,15 @@ def main():
         mesh, fes = cartesian_space(E, nx, ny, nz_total, order, args.numbering, args.mesh)
     variant = variant_key(args)
     nsub = world if world > 1 else args.loopback
-    mass = lambda a: E.MassIntegrator(E.QuadratureCoefficient(a))
-    diff = lambda T: E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(T, K_SCALE, K_SLOPE, K_TREF))
+    mass, diff = bench_integrators(E)
     form = None
     keep = []
 
     def serial_form(compress_geometry, mesh=mesh, fes=fes, numbering=args.numbering, geo=args.geometry_input):
-        a, T = bioheat_coefficients(E, torch, mesh, fes)
-        keep.extend([a, T])
-        # the reference's numbering: no mesh knowledge, the form derives its order from the map
-        eo = "faces" if numbering == "entity" and args.workload != "c3" else "auto"
-        f = E.BilinearForm(fes, kernel=kernel, element_order=os.environ.get("ECM2_ELEMENT_ORDER", eo),
-                           scatter=scatter, compress_geometry=compress_geometry,
-                           bricks=int(os.environ.get("ECM2_BRICKS", "-1")),  # A/B: p >= 3 brick depth
-                           geometry="jacobians" if geo == "jacobians" else "nodes",
-                           coefficient_snapshot=bool(args.coefficient_snapshot))
-        if geo == "jacobians":
-            # MFEM's GeometricFactors::JACOBIANS (NQ x 3 x 3 x NE), as the binding passes it; the form
-            # fits it to trilinear maps (or checks it affine) at Assemble and keeps it for re-assembly
-            J = mesh.jacobians(fes.order + 2)
-            f.SetJacobians(J)
-        f.AddDomainIntegrator(mass(a))
-        f.AddDomainIntegrator(diff(T))
-        f.Assemble()
-        return f
+        return bench_form(E, torch, mesh, fes, keep, kernel=kernel, scatter=scatter,
+                          compress_geometry=compress_geometry,
+                          element_order="faces" if numbering == "entity" and args.workload != "c3" else "auto",
+                          geometry_input=geo, coefficient_snapshot=bool(args.coefficient_snapshot))
 
     def sub_measure(f, fes_s, tag, note):
         """Time another serial form of this workload in this run (same steps, same clock

@@ -397,13 +397,35 @@ class PerfusionCoefficient:
         self.params = tuple(float(v) for v in (rho_c, gdt_cb, w0, a, t0, t_stop))
 
 
-def _integrator_args(c, keep):
-    """(coefficient kind, data pointer, params pointer) of a coefficient for the C ABI."""
+def _check_points(c, v, tails, ne, nq, flat_ok=False):
+    """A per-quadrature-point coefficient tensor must be CUDA float64, contiguous-able, shaped
+    (ne, nq) + one of `tails` (flat_ok: or ne * nq values in any shape): the kernels read it as
+    [ne][nq][dim] doubles, so anything else would be misread (or read out of bounds) on the GPU."""
+    import torch
+    name = type(c).__name__
+    if not isinstance(v, torch.Tensor) or not v.is_cuda or v.dtype != torch.float64:
+        raise ECM2Error(f"{name}: expected a CUDA float64 tensor, got {type(v).__name__} "
+                        f"{getattr(v, 'dtype', '')}")
+    if flat_ok:
+        if ne is not None and v.numel() != ne * nq:
+            raise ECM2Error(f"{name}: {v.numel()} values, the form has {ne} x {nq} quadrature points")
+        if not v.is_contiguous():
+            raise ECM2Error(f"{name}: the values must be contiguous")
+        return
+    shp = tuple(v.shape)
+    if len(shp) < 2 or shp[2:] not in tails or (ne is not None and shp[:2] != (ne, nq)):
+        raise ECM2Error(f"{name}: expected shape ({ne}, {nq}) + one of {tails}, got {shp}")
+
+
+def _integrator_args(c, keep, ne=None, nq=None):
+    """(coefficient kind, data pointer, params pointer) of a coefficient for the C ABI; ne, nq: the
+    form's elements and quadrature points per element (checked against per-point tensors)."""
     if isinstance(c, ConstantCoefficient):
         arr = (ctypes.c_double * 1)(c.value)
         keep.append(arr)
         return COEFF_CONSTANT, ctypes.cast(arr, ctypes.c_void_p), None
     if isinstance(c, QuadratureCoefficient):
+        _check_points(c, c.values, ((),), ne, nq, flat_ok=True)
         keep.append(c.values)
         return COEFF_QUAD, _dev_ptr(c.values), None
     if isinstance(c, AffineGridFunctionCoefficient):
@@ -415,6 +437,8 @@ def _integrator_args(c, keep):
         v = c.values
         vec = isinstance(c, VectorCoefficient)
         if hasattr(v, "is_cuda"):  # per quadrature point, device
+            # the kernels read [ne][nq][dim] float64: anything else would be misread on the GPU
+            _check_points(c, v, ((3,),) if vec else ((3, 3), (9,)), ne, nq)
             if vec:
                 keep.append(v.contiguous())
                 return COEFF_QUAD_VECTOR, _dev_ptr(keep[-1]), None
@@ -521,7 +545,8 @@ class BilinearForm:
     def AddDomainIntegrator(self, integ, elem_marker=None):
         """BilinearForm::AddDomainIntegrator(integ[, elem_marker]): with a marker (0 / 1 per
         attribute) the integrator acts on the elements whose attribute a has elem_marker[a-1]."""
-        kind, data, params = _integrator_args(integ.coeff, self._keep)
+        info = self.info()
+        kind, data, params = _integrator_args(integ.coeff, self._keep, info["ne"], info["q1d"] ** 3)
         if elem_marker is None:
             _check(_lib.ecm2_pa_form_add_integrator(self._h, integ.kind, kind, data, params))
         else:
@@ -848,6 +873,7 @@ class ParBilinearForm:
                  schedule: str = "serial", graph: int = -1):
         lib = _par_lib()
         self.part = part
+        self._q1d = q1d
         self._keep = []
         en = np.ascontiguousarray(part.fes.mesh.element_nodes()[part.elems]) if part.ne_local else np.zeros((1, 3, 8))
         idbuf = None
@@ -872,7 +898,8 @@ class ParBilinearForm:
             self._h = None
 
     def AddDomainIntegrator(self, integ, elem_marker=None):
-        kind, data, params = _integrator_args(integ.coeff, self._keep)
+        kind, data, params = _integrator_args(integ.coeff, self._keep, self.part.ne_local,
+                                              (self._q1d or self.part.fes.order + 2) ** 3)
         if elem_marker is None:
             _check(_par_lib().ecm2_par_form_add_integrator(self._h, integ.kind, kind, data, params))
         else:

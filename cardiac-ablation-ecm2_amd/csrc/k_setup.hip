@@ -753,6 +753,79 @@ __global__ void __launch_bounds__(256) k_lattice_to_dofs(long n, const int *__re
    if (i < n) { out[lmap[i] & 0x3fffffff] = v[i]; }
 }
 
+// Element weights applied to one integrator's stored qdata, any layout (the marker diagonal,
+// PAForm::assemble_diagonal): every entry of integrator `integ` on caller element e is multiplied
+// by w[e].  pos: caller element -> internal position (blocked layouts), else null.
+__global__ void __launch_bounds__(256)
+k_scale_elements(int kind, int ne, int NQ, int pw, int tsnap, const int *__restrict__ pos, int integ,
+                 const double *__restrict__ w, double *__restrict__ qdd, double *__restrict__ qdm)
+{
+   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   if (t >= (long)ne * NQ) { return; }
+   const int e = (int)(t / NQ), q = (int)(t % NQ);
+   const double wt = w[e];
+   if (wt == 1.0) { return; }
+   const int ip = pos ? pos[e] : e;
+   const size_t blk = (size_t)(ip >> 6);
+   const int lane = ip & 63;
+   const size_t eq = (size_t)e * NQ + q, bq = (blk * NQ + q) * 64 + lane;
+   const bool diff = integ == 1;
+   switch (kind)
+   {
+   case QLAYOUT_NATIVE:
+   case QLAYOUT_NATIVE9:
+      if (diff)
+      {
+         const int nc = kind == QLAYOUT_NATIVE9 ? 9 : 6;
+         for (int c = 0; c < nc; c++) { qdd[((size_t)e * nc + c) * NQ + q] *= wt; }
+      }
+      else { qdm[eq] *= wt; }
+      break;
+   case QLAYOUT_BLOCKED:
+      if (diff)
+      {
+         for (int k = 0; k < 3; k++)
+         {
+            double *p = qdd + ((blk * NQ + q) * 3 + k) * 128 + lane * 2;
+            p[0] *= wt;
+            p[1] *= wt;
+         }
+      }
+      else { qdm[(blk * ((NQ + 1) / 2) + (q >> 1)) * 128 + lane * 2 + (q & 1)] *= wt; }
+      break;
+   case QLAYOUT_AFFINE:
+      if (diff)
+      {
+         if (q != 0) { break; }
+         for (int k = 0; k < 3; k++)  // the element matrix C_e
+         {
+            double *p = qdd + (blk * 3 + k) * 128 + lane * 2;
+            p[0] *= wt;
+            p[1] *= wt;
+         }
+      }
+      else if (pw == 2) { qdm[bq * 2 + 1] *= wt; }
+      else if (tsnap && pw == 1) { qdm[bq] *= wt; }  // W alpha det J alone (coefficient snapshot)
+      break;
+   case QLAYOUT_AFFINE_E:
+      if (diff)
+      {
+         if (q == 0) { for (int k = 0; k < 6; k++) { qdd[(size_t)e * 6 + k] *= wt; } }
+      }
+      else if (pw == 2) { qdm[eq * 2 + 1] *= wt; }
+      break;
+   case QLAYOUT_TRILINEAR:
+      if (diff) { qdm[pw == 2 ? bq * 2 : bq] *= wt; }  // W beta / det J
+      else if (pw == 2) { qdm[bq * 2 + 1] *= wt; }
+      break;
+   case QLAYOUT_TRILINEAR_E:
+      if (diff) { qdm[pw == 2 ? eq * 2 : eq] *= wt; }
+      else if (pw == 2) { qdm[eq * 2 + 1] *= wt; }
+      break;
+   default: break;
+   }
+}
+
 SetupCoef make_setup_coef(const CoeffDesc *c, const double *q)
 {
    SetupCoef s{};
@@ -830,6 +903,15 @@ void setup_from_nodes(const QLayout &L, int Q, const double *enodes, const doubl
    ECM2_SETUP_CASE(6) ECM2_SETUP_CASE(7) ECM2_SETUP_CASE(8)
 #undef ECM2_SETUP_CASE
    ECM2_VERIFY(false, ERR_UNSUPPORTED, "setup: Q1D " << Q << " not instantiated");
+}
+
+void scale_elements(const QLayout &L, int integ, const double *w, double *qd_diff, double *qd_mass, hipStream_t s)
+{
+   const long n = (long)L.ne * L.nq;
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_scale_elements, dim3(grid_for(n, 256)), dim3(256), 0, s, L.kind, L.ne, L.nq, L.pw, L.tsnap,
+                      L.blocked() ? L.pos : nullptr, integ, w, qd_diff, qd_mass);
+   ECM2_HIP(hipGetLastError());
 }
 
 void affine_snapshot(int n, const double *T, double A, double B, double *out, hipStream_t s)

@@ -303,6 +303,9 @@ void setup_trilinear(const QLayout &L, int Q, const double *enodes, const double
                      double *qd_geo, double *qd_pair, hipStream_t s);
 // Trilinear-map coefficients of every element from MFEM-layout Jacobians (cfit [ne][21]); false
 // when some element's Jacobians are not those of a trilinear map (1e-13; synchronises s).
+// Multiply integrator `integ`'s (0 mass, 1 diffusion) stored qdata on caller element e by w[e]
+// (device [ne]), in any layout L (pos: L.pos for the blocked layouts).
+void scale_elements(const QLayout &L, int integ, const double *w, double *qd_diff, double *qd_mass, hipStream_t s);
 // out[i] = A + B T[i] (i < n): the coefficient snapshot of an affine law of an H1 field.
 void affine_snapshot(int n, const double *T, double A, double B, double *out, hipStream_t s);
 // The snapshot in the lattice-map blocks' slot order ([blk][nlp], lmap: the blocks' lattice maps),

@@ -1160,7 +1160,24 @@ void PAForm::assemble(hipStream_t s)
          kern::affine_snapshot_lattice(layout_.nblk(), nlp, lmap_.data(), cdiff_.lvec, A, B, tsnap_.data(), s);
       }
    }
-   setup_qdata(s, nullptr);
+   setup_qdata(s);
+   // The marker diagonal's element weights (assemble_diagonal), from the Assemble-time attributes
+   // (the reference reads them in SetupRestrictionOperators, bilinearform_ext.cpp:269)
+   diag_integ_ = -1;
+   diag_w_.resize(0);
+   if (order_added_.size() == 2 && marked_[order_added_[1]])
+   {
+      const int F = order_added_[0], S = order_added_[1];
+      const std::vector<double> wf = marker_weights(F), ws = marker_weights(S);
+      bool differ = false;
+      for (int e = 0; e < ne_ && !differ; e++) { differ = wf[e] != 0.0 && ws[e] == 0.0; }
+      if (differ)
+      {
+         diag_integ_ = F;
+         diag_w_.upload(ws, s);
+         ECM2_HIP(hipStreamSynchronize(s));  // ws is a host temporary
+      }
+   }
    assembled_ = true;
    gen_++;
 }
@@ -1193,7 +1210,7 @@ const double *PAForm::coeff_points(const CoeffDesc &c, DeviceArray<double> &tmp,
    return nullptr;
 }
 
-void PAForm::setup_qdata(hipStream_t s, const std::pair<int, std::vector<double>> *wover)
+void PAForm::setup_qdata(hipStream_t s)
 {
    // (compressed layouts: qd_mass_ holds the point values, present with either integrator)
    const bool comp = layout_.compressed();
@@ -1218,16 +1235,14 @@ void PAForm::setup_qdata(hipStream_t s, const std::pair<int, std::vector<double>
 
    // Attribute markers: per marked integrator, element weights 1 (marker[attr - 1] != 0) or 0,
    // applied to its coefficient at setup (the reference masks the integrator's E-vector output,
-   // AddWithMarkers_, bilinearform_ext.cpp:753-774: the same operator).  wover: other weights
-   // for one integrator (the diagonal's, see assemble_diagonal)
+   // AddWithMarkers_, bilinearform_ext.cpp:753-774: the same operator)
    for (int k = 0; k < 2; k++)
    {
       CoeffDesc &c = k == INTEG_MASS ? cmass_ : cdiff_;
       c.emask = nullptr;
       if (!(k == INTEG_MASS ? have_mass_ : have_diff_)) { continue; }
-      const bool over = wover && wover->first == k;
-      if (!marked_[k] && !over) { continue; }
-      std::vector<double> w = over ? wover->second : marker_weights(k);
+      if (!marked_[k]) { continue; }
+      std::vector<double> w = marker_weights(k);
       w.resize(std::max(1, ne_));
       emask_[k].upload(w, s);
       ECM2_HIP(hipStreamSynchronize(s));  // w is a host temporary
@@ -1490,31 +1505,36 @@ void PAForm::assemble_diagonal(double *diag, hipStream_t s)
    // AssembleDiagonalPA into ONE localY and then zeroes a marked integrator's excluded elements of
    // that localY, so on those elements the contributions of the integrators added before it vanish
    // too (Mult masks each integrator's output separately, AddMultWithMarkers :753-774).  This
-   // library reproduces it: when the second integrator added is marked and excludes elements the
-   // first acts on, the diagonal comes from qdata set up with the first integrator's element
-   // weights times the second's (temporaries; the Mult's qdata is restored).
-   if (order_added_.size() == 2 && marked_[order_added_[1]])
+   // library reproduces it: when the second integrator added (S) is marked and excludes elements
+   // the first (F) acts on, the diagonal is taken from a copy of the stored (Assemble-time) qdata
+   // with F's entries multiplied by S's element weights (diag_w_, set at Assemble); the Mult's
+   // qdata is swapped back whatever happens.
+   if (diag_integ_ >= 0)
    {
-      const int F = order_added_[0], S = order_added_[1];
-      std::vector<double> wf = marker_weights(F);
-      const std::vector<double> ws = marker_weights(S);
-      bool differ = false;
-      for (int e = 0; e < ne_; e++)
+      DeviceArray<double> td, tm;
+      td.resize(qd_diff_.size());
+      tm.resize(qd_mass_.size());
+      if (td.size()) { ECM2_HIP(hipMemcpyAsync(td.data(), qd_diff_.data(), td.bytes(), hipMemcpyDeviceToDevice, s)); }
+      if (tm.size()) { ECM2_HIP(hipMemcpyAsync(tm.data(), qd_mass_.data(), tm.bytes(), hipMemcpyDeviceToDevice, s)); }
+      kern::scale_elements(layout_, diag_integ_, diag_w_.data(), td.data(), tm.data(), s);
+      struct Swap
       {
-         differ = differ || (wf[e] != 0.0 && ws[e] == 0.0);
-         wf[e] *= ws[e];
-      }
-      if (differ)
-      {
-         DeviceArray<double> keep_d(std::move(qd_diff_)), keep_m(std::move(qd_mass_));
-         const std::pair<int, std::vector<double>> over(F, wf);
-         setup_qdata(s, &over);
-         diagonal_from_qdata(diag, s);
-         ECM2_HIP(hipStreamSynchronize(s));  // the temporaries are freed below
-         qd_diff_ = std::move(keep_d);
-         qd_mass_ = std::move(keep_m);
-         return;
-      }
+         PAForm &f;
+         DeviceArray<double> &d, &m;
+         Swap(PAForm &f_, DeviceArray<double> &d_, DeviceArray<double> &m_) : f(f_), d(d_), m(m_)
+         {
+            std::swap(f.qd_diff_, d);
+            std::swap(f.qd_mass_, m);
+         }
+         ~Swap()
+         {
+            (void)hipDeviceSynchronize();  // the temporaries are freed after this scope
+            std::swap(f.qd_diff_, d);
+            std::swap(f.qd_mass_, m);
+         }
+      } swap(*this, td, tm);
+      diagonal_from_qdata(diag, s);
+      return;
    }
    diagonal_from_qdata(diag, s);
 }
@@ -1595,7 +1615,9 @@ void PAForm::expand_compressed(DeviceArray<double> &fd, DeviceArray<double> &fm,
       const double *cd_q = coeff_points(cs, ctd, s);
       kern::setup_affine(La, Q_, jac_ ? nullptr : enodes_.data(), jac_, W_.data(), nullptr, &cs, nullptr, cd_q,
                          fac.data(), pair.data(), s);
-      kern::affine_expand(La, Q_, fac.data(), pair.data(), fd.data(), fm.data(), s,
+      // (the stored element matrices C_e, not the recomputed ones in fac: the marker diagonal scales
+      // the stored qdata, assemble_diagonal)
+      kern::affine_expand(La, Q_, qd_diff_.data(), pair.data(), fd.data(), fm.data(), s,
                           have_mass_ ? qd_mass_.data() : nullptr);
       ECM2_HIP(hipStreamSynchronize(s));  // the temporaries are freed on return
       return;

@@ -180,8 +180,8 @@ private:
    ApplyArgs apply_args(const double *x, const double *xg, double *y, double *yg, int b0,
                         int b1) const;
    // qdata of the integrators present (resized, padding cleared, coefficients projected, setup
-   // kernel); wover = (kind, element weights) replaces that integrator's marker weights
-   void setup_qdata(hipStream_t s, const std::pair<int, std::vector<double>> *wover);
+   // kernel)
+   void setup_qdata(hipStream_t s);
    // element weights [ne] of integrator kind k: 1 / 0 per its attribute marker, all 1 unmarked
    std::vector<double> marker_weights(int k) const;
    void diagonal_from_qdata(double *diag, hipStream_t s);
@@ -227,6 +227,8 @@ private:
    bool marked_[2] = {false, false};
    std::vector<int> order_added_;        // integrator kinds in AddDomainIntegrator order (the diagonal's markers)
    DeviceArray<double> emask_[2];        // per integrator kind: element weights [ne] (marked only)
+   int diag_integ_ = -1;                 // the marker diagonal: integrator whose qdata diag_w_ scales (-1: none)
+   DeviceArray<double> diag_w_;          // its element weights [ne] (the second integrator's marker, at Assemble)
 
    std::vector<int> gmap_host_;
    DeviceArray<int> gmap_;          // native [e][nd]

@@ -334,6 +334,50 @@ def test_c5_sdirk_step_p4(ode_type):
     assert relerr(uh - u0, ur - u0) < 1e-9
 
 
+def test_c5_sdirk_step_full_size():
+    """configs[4]'s implicit time step at size: one SDIRK33 step (ode.cpp:834-859, ex16p.cpp:373-470)
+    of M du/dt = -K u on Cartesian 68^3 at p = 4 (20.3M DoF, every element in a lattice-addressed
+    2 x 2 x 1 brick), T = M_alpha + c dt K_beta and K = K_beta as the bench's forms, Dirichlet dofs
+    held; each of the three stage solves a constrained Jacobi-PCG with a fixed 8 iterations (rel_tol
+    0) on both sides -- the device ode_step against oracle/ode.py's SDIRK33 over the oracle's PCG."""
+    n, order, dt, iters = 68, 4, 0.02, 8
+    m = E.Mesh.MakeCartesian3D(n, n, n)
+    fes = E.H1Space(m, order, E.NUMBERING_STRUCTURED)
+    assert fes.ndofs == 20346417
+    en = m.element_nodes()
+    P = O.quad_points(en, O.default_q1d(order))
+    alpha, beta = alpha_bioheat(P) / 3.6e6, k_of_T(temperature(P))
+    del P
+    c = E.ode_implicit_coeff(23)
+    T = _serial_form(fes, None, alpha, c * dt * beta)
+    K = _serial_form(fes, None, None, beta)
+    assert T.BrickInfo() == (fes.ne // 4, 1) and T.info()["layout"] == E.QLAYOUT_AFFINE_E
+    ess = fes.boundary_dofs()
+    X = fes.dof_coords()
+    u0 = 37.0 + 20.0 * np.exp(-4.0 * np.sum((X - 0.5) ** 2, axis=1))
+    del X
+    u = dev(u0)
+    ns, it, conv = E.ode_step(23, E.Operator(T), E.Operator(K), dt, u, ess=dev(ess, torch.int32), rel_tol=0.0,
+                              max_iter=iters)
+    assert ns == 3 and it == 3 * iters and not conv   # fixed iteration count: "not converged" by design
+    uh = host(u)
+    del T, K, u
+    Tr = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=alpha, beta=c * dt * beta)
+    Kr = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, beta=beta)
+    del alpha, beta
+
+    def solve(us):
+        rhs = -Kr.mult(us)
+        rhs[ess] = 0.0
+        xs, itr, _ = Tr.pcg(rhs, ess, rel_tol=0.0, max_iter=iters)
+        assert itr == iters
+        return xs
+
+    ur = ODE.step(23, solve, u0, dt)
+    assert np.array_equal(uh[ess], u0[ess])
+    assert relerr(uh - u0, ur - u0) < 1e-9
+
+
 # ---------------------------------------------------------------------------------------
 # configs[3]: the 8-way split
 # ---------------------------------------------------------------------------------------

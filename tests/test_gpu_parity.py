@@ -452,6 +452,89 @@ def test_coefficient_snapshot(numbering, mass):
     assert not f3.CoefficientSnapshot()
 
 
+@pytest.mark.parametrize("snap", [True, False])
+def test_marker_diagonal_keeps_assemble_time_state(snap):
+    """Diffusion k(T) added first, then a MassIntegrator(perfusion(T)) restricted to attribute 1; T
+    changes after Assemble.  AssembleDiagonal follows the reference's shared-localY rule
+    (bilinearform_ext.cpp:370-411) on the Assemble-time coefficients (the reference builds it from
+    the pa_data stored at Assemble), and leaves no element mask behind: the Mult, the diffusion
+    qdata and its E-vector AddMultPA afterwards still describe the unmasked diffusion."""
+    import bioheat as BH
+    n, order = 8, 2
+    m = E.Mesh.MakeCartesian3D(n, n, n, 1.0, 0.7, 1.3)
+    m.SetAttributes(1 + np.arange(m.GetNE()) % 2)
+    fes = E.H1Space(m, order, E.NUMBERING_STRUCTURED)
+    en = m.element_nodes()
+    q1d = O.default_q1d(order)
+    T = temperature(fes.dof_coords())
+    Td = dev(T)
+    par = (3.6e6, 0.05 * 3.6e3, 6.4e-3, 0.02, 37.0, 1e300)
+    ks, kslope, ktref = 0.05, 0.0012, 37.0
+    f = E.BilinearForm(fes, coefficient_snapshot=snap)
+    f.AddDomainIntegrator(E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(Td, ks, kslope, ktref)))
+    f.AddDomainIntegrator(E.MassIntegrator(E.PerfusionCoefficient(Td, *par)), [1, 0])
+    f.Assemble()
+    assert f.CoefficientSnapshot() == snap
+    Tq = BH.temperature_at_quadrature(T, fes.gather_map(), order, q1d)
+    op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=BH.perfusion_law(Tq, *par),
+                          beta=BH.affine_law(Tq, ks, kslope, ktref))
+    Td.fill_(1.0e3)  # after Assemble: neither the operator nor its diagonal may see it
+    attr = m.GetAttributes()
+    d = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+    f.AssembleDiagonal(d)
+    assert relerr(host(d), op.diagonal_markers(attr, [("diffusion", None), ("mass", [1, 0])])) < 1e-12
+    x = np.random.default_rng(5).uniform(-1, 1, fes.ndofs)
+    y = torch.full_like(d, float("nan"))
+    f.Mult(dev(x), y)
+    assert relerr(host(y), op.mult_markers(x, attr, mass_marker=[1, 0])) <= RTOL
+    assert relerr(f.qdata(E.DIFFUSION), op.D) < 1e-12
+    xe = np.random.default_rng(6).uniform(-1, 1, (fes.ne, fes.nd))
+    ye = torch.zeros(fes.ne * fes.nd, dtype=torch.float64, device="cuda")
+    f.IntegratorAddMultPA(E.DIFFUSION, dev(xe), ye)
+    assert relerr(host(ye).reshape(fes.ne, fes.nd), O.diffusion_apply(op.B, op.G, op.D, xe)) <= RTOL
+    d2 = torch.full_like(d, float("nan"))
+    f.AssembleDiagonal(d2)
+    assert torch.equal(d, d2)
+
+
+@pytest.mark.parametrize("order,q1d", [(1, 3), (2, 3), (2, 5), (3, 4), (4, 5), (4, 7)])
+@pytest.mark.parametrize("geometry", ["nodes", "jacobians"])
+def test_integration_rule_q1d(order, q1d, geometry):
+    """The rule the integrator asks for, passed through the ABI as q1d (ecm2_pa_form_create): MFEM's
+    AssemblePA takes IntRule ? IntRule : GetRule(el, el[, T]) (bilininteg_diffusion_pa.cpp:97,
+    bilininteg_mass_pa.cpp:34), which differs from the default Q1D = p + 2 for a user rule or a
+    high-order mesh (MassIntegrator::GetRule adds Trans.OrderW(), bilininteg.cpp:1450-1462; a
+    quadratic mesh gives Q1D = p + 3).  Mult and diagonal on fichera r1 (the reference's numbering,
+    non-lattice blocks) against the oracle on the same Gauss-Legendre rule, geometry as corners or
+    as MFEM Jacobians at that rule's points."""
+    m = make_mesh("fichera_r1")
+    fes = E.H1Space(m, order)
+    en = m.element_nodes()
+    P = O.quad_points(en, q1d)
+    a, b = alpha_bioheat(P), coeff_function(P)
+    form = E.BilinearForm(fes, q1d=q1d, geometry=geometry)
+    assert form.info()["q1d"] == q1d
+    if geometry == "jacobians":
+        form.SetJacobians(m.jacobians(q1d))
+    form.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(a.reshape(fes.ne, -1)))))
+    form.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(dev(b.reshape(fes.ne, -1)))))
+    form.Assemble()
+    op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=a, beta=b, q1d=q1d)
+    x = np.random.default_rng(q1d).uniform(-1, 1, fes.ndofs)
+    y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+    form.Mult(dev(x), y)
+    assert relerr(host(y), op.mult(x)) <= RTOL
+    d = torch.full_like(y, float("nan"))
+    form.AssembleDiagonal(d)
+    assert relerr(host(d), op.diagonal()) <= RTOL
+    # a wrong-sized coefficient (the default rule's points) is refused before it reaches the GPU
+    if q1d != order + 2:
+        f2 = E.BilinearForm(fes, q1d=q1d)
+        Pd = O.quad_points(en, order + 2)
+        with pytest.raises(E.ECM2Error):
+            f2.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(alpha_bioheat(Pd).reshape(fes.ne, -1)))))
+
+
 @pytest.mark.parametrize("jacobi", [True, False])
 def test_pcg_matches_oracle(jacobi):
     m = make_mesh("fichera_r1")

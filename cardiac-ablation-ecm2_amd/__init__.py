@@ -34,6 +34,7 @@ MASS, DIFFUSION = 0, 1
 COEFF_CONSTANT, COEFF_QUAD, COEFF_GRIDFUNC_AFFINE, COEFF_GRIDFUNC_PERFUSION = 0, 1, 2, 3
 COEFF_QUAD_VECTOR, COEFF_QUAD_SYMMATRIX, COEFF_QUAD_MATRIX = 4, 5, 6
 COEFF_CONST_VECTOR, COEFF_CONST_SYMMATRIX, COEFF_CONST_MATRIX = 7, 8, 9
+COEFF_GRIDFUNC = 10
 KERNEL_AUTO, KERNEL_TPE, KERNEL_WPE, KERNEL_UNFUSED, KERNEL_LINE = 0, 1, 2, 3, 4
 NUMBERING_ENTITY, NUMBERING_STRUCTURED = 0, 1
 ORDER_NATIVE, ORDER_BRICK, ORDER_MORTON = 0, 1, 2
@@ -377,6 +378,15 @@ class MatrixCoefficient:
         self.values, self.symmetric = values, bool(symmetric)
 
 
+class GridFunctionCoefficient:
+    """GridFunctionCoefficient (coefficient.cpp:250-253): the H1 field T (CUDA L-vector on the form's
+    own space) interpolated at the quadrature points, no law -- e.g. ex16p's kappa + alpha u formed at
+    the dofs (examples/ex16p.cpp:450-466)."""
+
+    def __init__(self, T):
+        self.T = T
+
+
 class AffineGridFunctionCoefficient:
     """scale * (1 + slope * (T(x) - t_ref)) with T an H1 grid function (CUDA L-vector).
 
@@ -428,6 +438,9 @@ def _integrator_args(c, keep, ne=None, nq=None):
         _check_points(c, c.values, ((),), ne, nq, flat_ok=True)
         keep.append(c.values)
         return COEFF_QUAD, _dev_ptr(c.values), None
+    if isinstance(c, GridFunctionCoefficient):
+        keep.append(c.T)
+        return COEFF_GRIDFUNC, _dev_ptr(c.T), None
     if isinstance(c, AffineGridFunctionCoefficient):
         keep.append(c.T)
         params = (ctypes.c_double * 3)(c.scale, c.slope, c.t_ref)
@@ -612,6 +625,12 @@ class BilinearForm:
         v = ctypes.c_int()
         _check(_lib.ecm2_pa_form_coefficient_snapshot(self._h, ctypes.byref(v)))
         return bool(v.value)
+
+    def SnapshotInfo(self):
+        """(snapshot taken, mass values 0 none / 1 per point / 2 per element, laws applied at the point)."""
+        v = [ctypes.c_int() for _ in range(3)]
+        _check(_lib.ecm2_pa_form_snapshot_info(self._h, *[ctypes.byref(a) for a in v]))
+        return bool(v[0].value), v[1].value, bool(v[2].value)
 
     def AssembleDiagonal(self, diag, stream=None):
         _check(_lib.ecm2_pa_form_assemble_diagonal(self._h, _dev_ptr(diag), _stream(stream)))

@@ -93,12 +93,15 @@ ecm2::CoeffDesc make_coeff(int coeff_kind, const double *data, const double *par
       c.lvec = data;
       for (int i = 0; i < 6; i++) { c.p[i] = params[i]; }
    }
+   else if (coeff_kind == ECM2_COEFF_GRIDFUNC) { c.lvec = data; }
    else if (coeff_kind >= ECM2_COEFF_QUAD_VECTOR && coeff_kind <= ECM2_COEFF_QUAD_MATRIX) { c.quad = data; }
    else if (coeff_kind >= ECM2_COEFF_CONST_VECTOR && coeff_kind <= ECM2_COEFF_CONST_MATRIX)
    {
       NEED(data);
       for (int i = 0; i < c.dim(); i++) { c.cv[i] = data[i]; }
    }
+   else { ECM2_VERIFY(false, ecm2::ERR_ARG, "unknown coefficient kind " << coeff_kind); }
+   if (c.gridfunc()) { NEED(data); }
    return c;
 }
 } // namespace
@@ -403,6 +406,16 @@ int ecm2_pa_form_set_coefficient_snapshot(ecm2_pa_form *f, int on)
 int ecm2_pa_form_coefficient_snapshot(const ecm2_pa_form *f, int *on)
 {
    return guard([&] { NEED(f); NEED(on); *on = f->f->coefficient_snapshot() ? 1 : 0; });
+}
+
+int ecm2_pa_form_snapshot_info(const ecm2_pa_form *f, int *on, int *mass_values, int *law_at_point)
+{
+   return guard([&] {
+      NEED(f);
+      if (on) { *on = f->f->coefficient_snapshot() ? 1 : 0; }
+      if (mass_values) { *mass_values = f->f->snapshot_mass(); }
+      if (law_at_point) { *law_at_point = f->f->snapshot_law_at_point(); }
+   });
 }
 
 int ecm2_pa_form_set_bricks(ecm2_pa_form *f, int bz)

@@ -351,7 +351,7 @@ template <int Q, bool BLOCKED>
 __global__ void __launch_bounds__(256)
 k_setup_affine(const int *__restrict__ perm, int ne, const double *__restrict__ enodes,
                const double *__restrict__ Jg,
-               const double *__restrict__ W, SetupCoef cm, SetupCoef cd, int pw, int tsnap,
+               const double *__restrict__ W, SetupCoef cm, SetupCoef cd, int pw, int tsnap, int tmass,
                double *__restrict__ qd_fac, double *__restrict__ qd_pair)
 {
    constexpr int NQ = Q * Q * Q;
@@ -417,6 +417,9 @@ k_setup_affine(const int *__restrict__ perm, int ne, const double *__restrict__ 
    else { reinterpret_cast<v2d *>(qd_pair)[(size_t)e * NQ + q] = pr; }
    if (q == 0)
    {
+      // (snapshot with the mass value per element, QLayout::tmass 2: the constant coefficient, or 1
+      // when the kernel evaluates the mass law, times det J and the marker weight)
+      if (BLOCKED && tsnap && tmass == 2 && cm.has) { qd_pair[(size_t)blk * 64 + lane] = coef_at(cm, eq, e) * detJ; }
       const double A11 = (J22 * J33) - (J23 * J32);
       const double A12 = (J32 * J13) - (J12 * J33);
       const double A13 = (J12 * J23) - (J22 * J13);
@@ -753,11 +756,42 @@ __global__ void __launch_bounds__(256) k_lattice_to_dofs(long n, const int *__re
    if (i < n) { out[lmap[i] & 0x3fffffff] = v[i]; }
 }
 
+// AFFINE with a coefficient snapshot -> BLOCKED (the diagonal, the E-vector apply, the qdata export):
+// D(q) = W_q beta_q C_e with beta_q the snapshot's law at the point (caller order [e][q]) and the stored
+// element matrices C_e; the mass W alpha det J as stored per point (tmass 1) or W_q (alpha_q | 1) times
+// the stored per-element (c alpha) det J (tmass 2; alpha_q null: a constant, folded in).
+template <int Q>
+__global__ void __launch_bounds__(256)
+k_tsnap_expand(const int *__restrict__ perm, int ne, const double *__restrict__ W, const double *__restrict__ qd_fac,
+               const double *__restrict__ qd_m, int tmass, const double *__restrict__ beta_q,
+               const double *__restrict__ alpha_q, double *__restrict__ qd_diff, double *__restrict__ qd_mass)
+{
+   constexpr int NQ = Q * Q * Q;
+   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   const int lane = (int)(t & 63);
+   const long rest = t >> 6;
+   const int q = (int)(rest % NQ);
+   const long blk = rest / NQ;
+   const int ipos = (int)(blk * 64 + lane);
+   if (ipos >= ne) { return; }
+   const int e = perm ? perm[ipos] : ipos;
+   const size_t eq = (size_t)e * NQ + q;
+   const double wb = W[q] * beta_q[eq];
+   const v2d *C = reinterpret_cast<const v2d *>(qd_fac + (size_t)blk * 3 * 128) + lane;
+   v2d *dst = reinterpret_cast<v2d *>(qd_diff + ((size_t)blk * NQ + q) * 3 * 128) + lane;
+#pragma unroll
+   for (int k = 0; k < 3; k++) { dst[k * 64] = wb * C[k * 64]; }
+   if (tmass == 0) { return; }
+   const double m = tmass == 1 ? qd_m[((size_t)blk * NQ + q) * 64 + lane]
+                               : W[q] * (alpha_q ? alpha_q[eq] : 1.0) * qd_m[(size_t)blk * 64 + lane];
+   qd_mass[((size_t)blk * ((NQ + 1) / 2) + (q >> 1)) * 128 + lane * 2 + (q & 1)] = m;
+}
+
 // Element weights applied to one integrator's stored qdata, any layout (the marker diagonal,
 // PAForm::assemble_diagonal): every entry of integrator `integ` on caller element e is multiplied
 // by w[e].  pos: caller element -> internal position (blocked layouts), else null.
 __global__ void __launch_bounds__(256)
-k_scale_elements(int kind, int ne, int NQ, int pw, int tsnap, const int *__restrict__ pos, int integ,
+k_scale_elements(int kind, int ne, int NQ, int pw, int tsnap, int tmass, const int *__restrict__ pos, int integ,
                  const double *__restrict__ w, double *__restrict__ qdd, double *__restrict__ qdm)
 {
    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -805,6 +839,7 @@ k_scale_elements(int kind, int ne, int NQ, int pw, int tsnap, const int *__restr
          }
       }
       else if (pw == 2) { qdm[bq * 2 + 1] *= wt; }
+      else if (tsnap && tmass == 2) { if (q == 0) { qdm[blk * 64 + lane] *= wt; } }  // per element
       else if (tsnap && pw == 1) { qdm[bq] *= wt; }  // W alpha det J alone (coefficient snapshot)
       break;
    case QLAYOUT_AFFINE_E:
@@ -905,11 +940,22 @@ void setup_from_nodes(const QLayout &L, int Q, const double *enodes, const doubl
    ECM2_VERIFY(false, ERR_UNSUPPORTED, "setup: Q1D " << Q << " not instantiated");
 }
 
+void tsnap_expand(const QLayout &L, int Q, const double *W, const double *qd_fac, const double *qd_m,
+                  const double *beta_q, const double *alpha_q, double *qd_diff, double *qd_mass, hipStream_t s)
+{
+   ECM2_VERIFY(L.kind == QLAYOUT_AFFINE && L.tsnap && Q == 4, ERR_INTERNAL, "snapshot expansion: AFFINE p = 2");
+   const long n = (long)L.nblk() * 64 * L.nq;
+   if (n == 0) { return; }
+   hipLaunchKernelGGL((k_tsnap_expand<4>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.perm, L.ne, W, qd_fac, qd_m,
+                      L.tmass, beta_q, alpha_q, qd_diff, qd_mass);
+   ECM2_HIP(hipGetLastError());
+}
+
 void scale_elements(const QLayout &L, int integ, const double *w, double *qd_diff, double *qd_mass, hipStream_t s)
 {
    const long n = (long)L.ne * L.nq;
    if (n == 0) { return; }
-   hipLaunchKernelGGL(k_scale_elements, dim3(grid_for(n, 256)), dim3(256), 0, s, L.kind, L.ne, L.nq, L.pw, L.tsnap,
+   hipLaunchKernelGGL(k_scale_elements, dim3(grid_for(n, 256)), dim3(256), 0, s, L.kind, L.ne, L.nq, L.pw, L.tsnap, L.tmass,
                       L.blocked() ? L.pos : nullptr, integ, w, qd_diff, qd_mass);
    ECM2_HIP(hipGetLastError());
 }
@@ -1060,12 +1106,12 @@ void setup_affine(const QLayout &L, int Q, const double *enodes, const double *J
       if (blk)                                                                                           \
       {                                                                                                  \
          hipLaunchKernelGGL((k_setup_affine<QQ, true>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.perm, L.ne, \
-                            enodes, J, W, scm, scd, L.pw, L.tsnap, qd_fac, qd_pair);                     \
+                            enodes, J, W, scm, scd, L.pw, L.tsnap, L.tmass, qd_fac, qd_pair);            \
       }                                                                                                  \
       else                                                                                               \
       {                                                                                                  \
          hipLaunchKernelGGL((k_setup_affine<QQ, false>), dim3(grid_for(n, 256)), dim3(256), 0, s, nullptr, L.ne, \
-                            enodes, J, W, scm, scd, L.pw, L.tsnap, qd_fac, qd_pair);                              \
+                            enodes, J, W, scm, scd, L.pw, L.tsnap, L.tmass, qd_fac, qd_pair);                     \
       }                                                                                                  \
       ECM2_HIP(hipGetLastError());                                                                       \
       return;                                                                                            \

@@ -971,28 +971,36 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
 }
 
 // AFFINE apply with the diffusion coefficient evaluated from a snapshot of its temperature field
-// (TS: ApplyArgs::tsnap).  In the bioheat form beta = k(T) is affine in T, an H1 grid function on
-// the form's own space (AffineGridFunctionCoefficient, coefficient.cpp:250-253 with the Pennes k(T)
-// law): the reference evaluates it at the quadrature points at Assemble (CoefficientVector::Project,
-// coefficient.cpp:2052-2070, then PADiffusionSetup3D stores W beta adj(J) adj(J)^T / det J).  Here
-// Assemble keeps T' = A + B T (the law applied to T's dofs, A = scale (1 - slope t_ref), B = scale
-// slope) and the kernel interpolates it with the weight-scaled basis w_q B (bw), so
-// W_q beta(x_q) = sum (w B)_z (w B)_y (w B)_x T' comes out of the same sum factorisation as u: per
-// plane 27, per row 9, per point 3 multiply-adds, and 8 bytes per point fewer -- only W alpha det J
-// is streamed (nothing without a MassIntegrator).  x and T' are gathered once per lattice point
-// (the block's 729 lattice slots, as k_apply_tpe_tlb) into one LDS region that the cross-wave face
-// exchange reuses afterwards.  Lattice blocks only (RM 1 regular, 3 lattice-map), p = 2.
-template <int D, int Q, bool SPLIT, int RM, bool MASS>
+// (TS: ApplyArgs::tsnap).  In the bioheat form beta = k(T) is a law of T, an H1 grid function on the
+// form's own space (GridFunctionCoefficient, coefficient.cpp:250-253, possibly composed with a law as
+// TransformedCoefficient::Eval does, coefficient.cpp:262): the reference evaluates it at the
+// quadrature points at Assemble (CoefficientVector::Project, coefficient.cpp:2052-2070, then
+// PADiffusionSetup3D stores W beta adj(J) adj(J)^T / det J).  Here Assemble keeps a snapshot of the
+// field at its dofs and the kernel interpolates it at the points in the same sum factorisation as u
+// (per plane 27, per row 9, per point 3 multiply-adds), so no W beta is streamed:
+// * LAW = false: the snapshot is T' = A + B T (an affine or identity law applied to the dofs: the
+//   basis sums to one, so the interpolated T' is the law at the point) and the weight-scaled basis
+//   w_q B (bw) gives W_q beta(x_q) directly;
+// * LAW = true: the snapshot is T itself, interpolated with B (bw = b) to T(x_q), where the laws are
+//   applied (law_d: any grid-function law, e.g. the perfusion law; law_m: a mass law of the same
+//   field) and multiplied by W_q = w_qx w_qy w_qz.
+// MM: the mass -- 0 none; 1 W alpha det J streamed per point; 2 one stored value per element,
+// (c alpha) det J (a constant coefficient folded in, or the mass law evaluated here), times W_q: no
+// per-point stream at all.  x and T' are gathered once per lattice point (the block's 729 lattice
+// slots, as k_apply_tpe_tlb) into one LDS region that the cross-wave face exchange reuses afterwards.
+// Lattice blocks only (RM 1 regular, 3 lattice-map), p = 2.
+template <int D, int Q, bool SPLIT, int RM, int MM, bool LAW>
 __global__ void __launch_bounds__(256, 2)
 k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
                const double *__restrict__ qdd, const double *__restrict__ qdm,
                const double *__restrict__ x, const double *__restrict__ xg, const double *__restrict__ tsn,
                double *__restrict__ y, double *__restrict__ yg, const Basis1D b, const Basis1D bw,
                const int *__restrict__ lane_flags, double *__restrict__ part, const int *__restrict__ treg,
-               int pstride, const int *__restrict__ lmap)
+               int pstride, const int *__restrict__ lmap, const QPts qw, const PointLaw law_d, const PointLaw law_m)
 {
    static_assert(RM == 1 || RM == 3, "lattice blocks only");
    static_assert(D == 3 && Q == 4, "p = 2");
+   constexpr bool MASS = MM != 0;
    constexpr int ND = D * D * D, NR = Q * Q, XR = XwaveRows<D>::R, WPG = 4, P = D - 1;
    constexpr int NLP = tpe_lattice_points(D);
    static_assert(2 * NLP <= XR * 64, "x and T' lattices fit a wave's exchange rows");
@@ -1015,13 +1023,14 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
    for (int a = 0; a < ND; a++) { Yo[a] = 0.0; }
    auto ld2 = [&](const double *p) -> v2d { return __builtin_nontemporal_load(reinterpret_cast<const v2d *>(p)); };
    v2d ce[3];
-   const double *qa = qdm + (size_t)blk * NR * Q * 64 + lane;  // W alpha det J, [blk][q][lane]
+   const double *qa = qdm + (size_t)blk * NR * Q * 64 + lane;  // MM 1: W alpha det J, [blk][q][lane]
    // three row buffers in rotation, each row issues the row two ahead (the plane loop is unrolled)
    double ra[3][Q];
    auto load_row = [&](int row, double (&aq)[Q]) {
 #pragma unroll
-      for (int qx = 0; qx < Q; qx++) { aq[qx] = MASS ? __builtin_nontemporal_load(qa + (size_t)(row * Q + qx) * 64) : 0.0; }
+      for (int qx = 0; qx < Q; qx++) { aq[qx] = MM == 1 ? __builtin_nontemporal_load(qa + (size_t)(row * Q + qx) * 64) : 0.0; }
    };
+   double mel = 0.0;  // MM 2: the element's (c alpha) det J, [blk][lane]
    if (wave_on)
    {
       const double *qc = qdd + (size_t)blk * 3 * 128 + lane * 2;
@@ -1029,6 +1038,7 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
       for (int k = 0; k < 3; k++) { ce[k] = ld2(qc + k * 128); }
       load_row(0, ra[0]);
       load_row(1, ra[1]);
+      if (MM == 2) { mel = qdm[(size_t)blk * 64 + lane]; }
       if (RM == 1)
       {
          const int *r = treg + (size_t)blk * 8;  // wave-uniform: scalar loads
@@ -1065,7 +1075,7 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 #pragma unroll
          for (int dz = 0; dz < D; dz++)
          {
-            bz[dz] = b.B[qz + MQ * dz]; gz[dz] = b.G[qz + MQ * dz]; wz[dz] = bw.B[qz + MQ * dz];
+            bz[dz] = b.B[qz + MQ * dz]; gz[dz] = b.G[qz + MQ * dz]; wz[dz] = LAW ? bz[dz] : bw.B[qz + MQ * dz];
          }
          double ZB[D][D], ZG[D][D], ZT[D][D], SB[D][D], SG[D][D];
 #pragma unroll
@@ -1093,6 +1103,7 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
             }
          auto row_body = [&](const int qy, const double (&cur)[Q]) {
             double Y00[D], Y01[D], Y10[D], YT[D];
+            const double wyz = qw.x[qy] * qw.x[qz];  // (LAW or MM 2: W_q = w_qx w_qy w_qz)
 #pragma unroll
             for (int dx = 0; dx < D; dx++)
             {
@@ -1100,7 +1111,8 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 #pragma unroll
                for (int dy = 0; dy < D; dy++)
                {
-                  const double by = b.B[qy + MQ * dy], gy = b.G[qy + MQ * dy], wy = bw.B[qy + MQ * dy];
+                  const double by = b.B[qy + MQ * dy], gy = b.G[qy + MQ * dy];
+                  const double wy = LAW ? by : bw.B[qy + MQ * dy];
                   u += by * ZB[dy][dx];
                   v += gy * ZB[dy][dx];
                   wv += by * ZG[dy][dx];
@@ -1118,14 +1130,28 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 #pragma unroll
                for (int dx = 0; dx < D; dx++)
                {
-                  const double bq = b.B[qx + MQ * dx], gq = b.G[qx + MQ * dx], wq = bw.B[qx + MQ * dx];
+                  const double bq = b.B[qx + MQ * dx], gq = b.G[qx + MQ * dx];
+                  const double wq = LAW ? bq : bw.B[qx + MQ * dx];
                   u += bq * Y00[dx];
                   ux += gq * Y00[dx];
                   uy += bq * Y01[dx];
                   uz += bq * Y10[dx];
-                  wb += wq * YT[dx];  // W_q beta(x_q)
+                  wb += wq * YT[dx];  // LAW: T(x_q), else W_q beta(x_q)
                }
-               const double m = MASS ? cur[qx] * u : 0.0;  // W alpha det J u
+               double mc = 0.0;  // W alpha det J
+               if (LAW || MM == 2)
+               {
+                  const double Wq = wyz * qw.x[qx];
+                  if (MM == 2) { mc = Wq * mel; }
+                  if (LAW)
+                  {
+                     const double tq = wb;
+                     wb = Wq * point_law(law_d, tq);
+                     if (MM == 2) { mc *= point_law(law_m, tq); }
+                  }
+               }
+               if (MM == 1) { mc = cur[qx]; }
+               const double m = MASS ? mc * u : 0.0;  // W alpha det J u
                double fx = ce[0].x * ux, fy = ce[0].y * ux, fz = ce[1].x * ux;
                fx += ce[0].y * uy; fy += ce[1].y * uy; fz += ce[2].x * uy;
                fx += ce[1].x * uz; fy += ce[2].x * uz; fz += ce[2].y * uz;
@@ -1494,20 +1520,35 @@ void launch_tpe(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipS
    }
    if (a.kind == QLAYOUT_AFFINE && a.tsnap)
    {
-      // the diffusion coefficient from its temperature snapshot: only W alpha det J per point
+      // the diffusion coefficient from its field snapshot: W alpha det J per point (tmass 1), or no
+      // per-point stream (tmass 2)
       if constexpr (DIFF && D == 3 && Q == 4)
       {
-         ECM2_VERIFY(a.pw == (MASS ? 1 : 0) && a.treg && (a.treg_all || a.tlat_all) && a.tsnap_kind == (a.treg_all ? 1 : 2),
-                     ERR_INTERNAL, "coefficient snapshot needs lattice blocks and the mass-only point values");
-         Basis1D bw = b;  // (w B): the weight-scaled interpolation of T'
+         ECM2_VERIFY(a.tmass == (MASS ? a.tmass : 0) && (a.tmass != 0) == MASS && a.pw == (a.tmass == 1 ? 1 : 0) &&
+                        a.treg && (a.treg_all || a.tlat_all) && a.tsnap_kind == (a.treg_all ? 1 : 2),
+                     ERR_INTERNAL, "coefficient snapshot needs lattice blocks and matching mass values");
+         Basis1D bw = b;  // (w B): the weight-scaled interpolation of T' (LAW = false)
          for (int d = 0; d < MAX_D1D; d++)
             for (int q = 0; q < MAX_Q1D; q++) { bw.B[q + MQ * d] = a.qw[q] * b.B[q + MQ * d]; }
-#define ECM2_TS(RM)                                                                                              \
-   hipLaunchKernelGGL((k_apply_tpe_ts<3, 4, SPLIT, RM, MASS>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end,      \
-                      a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.tsnap, a.y, a.yg, b, bw, a.lane_flags, a.part,  \
-                      a.treg, a.part_stride, a.lmap)
-         if (a.treg_all) { ECM2_TS(1); }
-         else { ECM2_TS(3); }
+         QPts qw = {};
+         for (int q = 0; q < MAX_Q1D; q++) { qw.x[q] = a.qw[q]; }
+#define ECM2_TS(RM, MM, LAW)                                                                                        \
+   hipLaunchKernelGGL((k_apply_tpe_ts<3, 4, SPLIT, RM, MM, LAW>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end,     \
+                      a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.tsnap, a.y, a.yg, b, bw, a.lane_flags, a.part,     \
+                      a.treg, a.part_stride, a.lmap, qw, a.law_d, a.law_m)
+#define ECM2_TS_MM(RM, LAW)                                                                                         \
+   if (!MASS) { ECM2_TS(RM, 0, LAW); }                                                                              \
+   else if (a.tmass == 1) { ECM2_TS(RM, 1, LAW); }                                                                  \
+   else { ECM2_TS(RM, 2, LAW); }
+         if (a.treg_all)
+         {
+            if (a.tlaw) { ECM2_TS_MM(1, true) } else { ECM2_TS_MM(1, false) }
+         }
+         else
+         {
+            if (a.tlaw) { ECM2_TS_MM(3, true) } else { ECM2_TS_MM(3, false) }
+         }
+#undef ECM2_TS_MM
 #undef ECM2_TS
       }
       else { ECM2_VERIFY(false, ERR_INTERNAL, "coefficient snapshot: p = 2 forms with the diffusion integrator"); }

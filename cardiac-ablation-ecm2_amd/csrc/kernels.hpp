@@ -70,11 +70,20 @@ struct QLayout
    // AFFINE / TRILINEAR point values: 2 = the pair (diffusion factor, mass factor), 1 = the
    // diffusion factor alone (a form without a MassIntegrator: [blk][q][lane], 8 B per point)
    int pw = 2;
-   // AFFINE (p = 2, lattice blocks) with the diffusion coefficient an affine law of an H1 field:
-   // the kernel interpolates a snapshot of the field (ApplyArgs::tsnap) instead of reading W beta,
-   // and the point values are W alpha det J alone (pw = 1; pw = 0 without a MassIntegrator).
+   // AFFINE (p = 2, lattice blocks) with the diffusion coefficient a law of an H1 field on the form's
+   // space (grid-function coefficient kinds): the kernel interpolates a snapshot of the field
+   // (ApplyArgs::tsnap) instead of reading W beta per point.
    // 1: the snapshot in dof order (regular blocks); 2: in the lattice-map blocks' slot order
    int tsnap = 0;
+   // with tsnap, the mass: 0 none; 1 W alpha det J per point (pw = 1: a quadrature coefficient, or a
+   // grid function other than the diffusion's field); 2 one value per element, (c alpha) det J (pw = 0:
+   // alpha constant, folded in, or a law of the diffusion's own field, evaluated in the kernel)
+   int tmass = 0;
+   // with tsnap: 0 the (affine) diffusion law applied to the snapshot's dofs and the weight-scaled
+   // interpolation gives W beta directly; 1 the snapshot is the field itself, interpolated at the point,
+   // where the laws are applied (TransformedCoefficient::Eval, coefficient.cpp:262: any law, and the
+   // mass law of the same field)
+   int tlaw = 0;
    const int *pos = nullptr;  // device: caller element -> internal position (BLOCKED)
    const int *perm = nullptr; // device: internal position -> caller element (BLOCKED)
    size_t diff_size() const
@@ -90,6 +99,7 @@ struct QLayout
    size_t mass_size() const
    {
       if (kind == QLAYOUT_NATIVE || kind == QLAYOUT_NATIVE9) { return (size_t)ne * nq; }
+      if (kind == QLAYOUT_AFFINE && tsnap && tmass == 2) { return (size_t)nblk() * kElemBlock; }  // [blk][lane]
       if (kind == QLAYOUT_AFFINE || kind == QLAYOUT_TRILINEAR) { return (size_t)nblk() * nq * pw * kElemBlock; }
       if (kind == QLAYOUT_AFFINE_E || kind == QLAYOUT_TRILINEAR_E) { return (size_t)ne * nq * pw; }
       return (size_t)nblk() * ((nq + 1) / 2) * 2 * kElemBlock;
@@ -115,11 +125,13 @@ struct QLayout
 // PADiffusionSetup3D coeffDim 3 / 6 / 9, bilininteg_diffusion_kernels.cpp:297-348): QUAD_* device
 // [ne][nq][dim], CONST_* the dim values in cv; dim 3 = diag(v), 6 = symmetric (11,12,13,22,23,33),
 // 9 = general, row-major M(i,j) at 3 i + j (CoefficientVector::ProjectTranspose, coefficient.cpp:2093-2123).
+// COEFF_GRIDFUNC: GridFunctionCoefficient (coefficient.cpp:250-253, qfunction.cpp:73-98), the H1 field's
+// own value at the point (no law): e.g. ex16p's conductivity kappa + alpha u, formed at the dofs
+// (examples/ex16p.cpp:450-466).
 enum CoeffKind : int { COEFF_CONSTANT = 0, COEFF_QUAD = 1, COEFF_GRIDFUNC_AFFINE = 2, COEFF_GRIDFUNC_PERFUSION = 3,
                        COEFF_QUAD_VECTOR = 4, COEFF_QUAD_SYMMATRIX = 5, COEFF_QUAD_MATRIX = 6,
                        COEFF_CONST_VECTOR = 7, COEFF_CONST_SYMMATRIX = 8, COEFF_CONST_MATRIX = 9,
-                       // internal: the field's own values (a coefficient snapshot, the law already applied)
-                       COEFF_GRIDFUNC_VALUE = -2 };
+                       COEFF_GRIDFUNC = 10 };
 struct CoeffDesc
 {
    int kind = COEFF_CONSTANT;
@@ -132,7 +144,7 @@ struct CoeffDesc
    const double *emask = nullptr; // device [ne] element weights of an attribute-marked integrator (form-owned)
    bool gridfunc() const
    {
-      return kind == COEFF_GRIDFUNC_AFFINE || kind == COEFF_GRIDFUNC_PERFUSION || kind == COEFF_GRIDFUNC_VALUE;
+      return kind == COEFF_GRIDFUNC_AFFINE || kind == COEFF_GRIDFUNC_PERFUSION || kind == COEFF_GRIDFUNC;
    }
    // values per point: 1 scalar, 3 vector, 6 symmetric matrix, 9 general matrix
    int dim() const
@@ -157,7 +169,7 @@ struct CoeffParams  // kernel-argument copy of CoeffDesc::p
 __host__ __device__ inline double coeff_law(int kind, double T, double scale, double slope, double t_ref,
                                             const double *p)
 {
-   if (kind == COEFF_GRIDFUNC_VALUE) { return T; }
+   if (kind == COEFF_GRIDFUNC) { return T; }
    if (kind == COEFF_GRIDFUNC_PERFUSION)
    {
       const double r = 1.0 + p[3] * (T - p[4]);
@@ -165,6 +177,33 @@ __host__ __device__ inline double coeff_law(int kind, double T, double scale, do
       return p[0] + p[1] * wb;
    }
    return scale * (1.0 + slope * (T - t_ref));
+}
+
+// A grid-function coefficient's law as a kernel argument (the coefficient snapshot applies it at the
+// quadrature point), in one branch-free form covering every law kind:
+//   law(T) = c0 + c1 T + c2 r(T),  r(T) = max(0, 1 + a (T - t0)) for T < t_stop, else 0;
+// COEFF_GRIDFUNC: c1 = 1; _AFFINE: c0 = scale (1 - slope t_ref), c1 = scale slope; _PERFUSION: c0 = rho_c,
+// c2 = gdt_cb w0 (coeff_law's algebra, regrouped); a constant folded into stored values: c0 = 1.
+struct PointLaw
+{
+   double c0 = 1.0, c1 = 0.0, c2 = 0.0, a = 0.0, t0 = 0.0, t_stop = 0.0;
+};
+inline PointLaw point_law_of(const CoeffDesc &c)
+{
+   PointLaw l;
+   if (c.kind == COEFF_GRIDFUNC) { l.c0 = 0.0; l.c1 = 1.0; }
+   else if (c.kind == COEFF_GRIDFUNC_AFFINE) { l.c0 = c.scale * (1.0 - c.slope * c.t_ref); l.c1 = c.scale * c.slope; }
+   else if (c.kind == COEFF_GRIDFUNC_PERFUSION)
+   {
+      l.c0 = c.p[0]; l.c2 = c.p[1] * c.p[2]; l.a = c.p[3]; l.t0 = c.p[4]; l.t_stop = c.p[5];
+   }
+   return l;
+}
+__host__ __device__ inline double point_law(const PointLaw &l, double T)
+{
+   const double r = 1.0 + l.a * (T - l.t0);
+   const double w = (T < l.t_stop && r > 0.0) ? r : 0.0;
+   return l.c0 + l.c1 * T + l.c2 * w;
 }
 
 // Arguments of one fused apply over element blocks [blk_begin, blk_end) (64 elements per
@@ -186,6 +225,8 @@ struct ApplyArgs
    // (the diffusion coefficient's law applied to its field at Assemble) and the 1D Gauss weights
    const double *tsnap = nullptr;
    int tsnap_kind = 0;              // QLayout::tsnap
+   int tmass = 0, tlaw = 0;         // QLayout::tmass, QLayout::tlaw
+   PointLaw law_d, law_m;           // tlaw = 1: the diffusion and mass laws at the point
    double qw[MAX_Q1D] = {};
    int xwave = 0;                   // the merge plan has cross-wave faces (AFFINE / TRILINEAR forms)
    const int *gmap = nullptr;
@@ -303,6 +344,11 @@ void setup_trilinear(const QLayout &L, int Q, const double *enodes, const double
                      double *qd_geo, double *qd_pair, hipStream_t s);
 // Trilinear-map coefficients of every element from MFEM-layout Jacobians (cfit [ne][21]); false
 // when some element's Jacobians are not those of a trilinear map (1e-13; synchronises s).
+// The BLOCKED per-point qdata of an AFFINE coefficient-snapshot form (p = 2): D = W beta_q C_e from the
+// stored element matrices (qd_fac) and beta at the points (device [ne][nq], caller order); the mass from
+// the stored values qd_m (per point, or per element times W_q alpha_q; alpha_q null: 1).
+void tsnap_expand(const QLayout &L, int Q, const double *W, const double *qd_fac, const double *qd_m,
+                  const double *beta_q, const double *alpha_q, double *qd_diff, double *qd_mass, hipStream_t s);
 // Multiply integrator `integ`'s (0 mass, 1 diffusion) stored qdata on caller element e by w[e]
 // (device [ne]), in any layout L (pos: L.pos for the blocked layouts).
 void scale_elements(const QLayout &L, int integ, const double *w, double *qd_diff, double *qd_mass, hipStream_t s);

@@ -1131,20 +1131,34 @@ void PAForm::assemble(hipStream_t s)
       part_.resize(std::max<size_t>(1, (size_t)part_line_off_ + (n_left_ ? (size_t)ne_ * ND_ : 0)));
    }
    else { part_.resize((size_t)layout_.nblk() * part_stride_); }
-   // Coefficient snapshot (k_apply_tpe_ts): the diffusion coefficient an affine law of an H1 field
-   // on this space (beta = scale (1 + slope (T - t_ref)), AffineGridFunctionCoefficient), AFFINE
-   // geometry, p = 2, every block a lattice brick, no attribute marker on the diffusion integrator
+   // Coefficient snapshot (k_apply_tpe_ts): the diffusion coefficient a law of an H1 field on this
+   // space (GridFunctionCoefficient, AffineGridFunctionCoefficient, the perfusion law), AFFINE
+   // geometry, p = 2, every block a lattice brick, no attribute marker on the diffusion integrator.
+   // The mass then streams W alpha det J per point (tmass 1), or nothing per point when its
+   // coefficient is a constant or a law of the same field (tmass 2: (c alpha) det J per element).
    layout_.tsnap = 0;
+   layout_.tmass = 0;
+   layout_.tlaw = 0;
    tsnap_.resize(0);
    if (tsnap_pref_ && layout_.kind == QLAYOUT_AFFINE && resolved_mode_ == KERNEL_TPE && D_ == 3 && Q_ == 4 &&
-       (treg_all_ || tlat_all_) && have_diff_ && cdiff_.kind == COEFF_GRIDFUNC_AFFINE && cdiff_.lvec &&
-       !marked_[INTEG_DIFFUSION])
+       (treg_all_ || tlat_all_) && have_diff_ && cdiff_.gridfunc() && cdiff_.lvec && !marked_[INTEG_DIFFUSION])
    {
       layout_.tsnap = 1;
-      layout_.pw = have_mass_ ? 1 : 0;
-      // T' = A + B T at every dof (the interpolated T' is the law at the point: the basis sums to
-      // 1), taken here only: later setups (the marker diagonal's) keep the Assemble-time field
-      const double A = cdiff_.scale * (1.0 - cdiff_.slope * cdiff_.t_ref), B = cdiff_.scale * cdiff_.slope;
+      const bool mass_law = have_mass_ && cmass_.gridfunc() && cmass_.lvec == cdiff_.lvec;
+      layout_.tmass = !have_mass_ ? 0 : (cmass_.kind == COEFF_CONSTANT || mass_law) ? 2 : 1;
+      layout_.pw = layout_.tmass == 1 ? 1 : 0;
+      // an affine (or identity) diffusion law alone is applied to the dofs (the interpolated T' is
+      // the law at the point: the basis sums to 1); a nonlinear law, or a mass law of the same field,
+      // needs the field itself at the point
+      layout_.tlaw = (mass_law || cdiff_.kind == COEFF_GRIDFUNC_PERFUSION) ? 1 : 0;
+      // T' = A + B T at every dof, taken here only: the Assemble-time field (the reference's qdata
+      // semantics; the diagonal and the qdata export read the same snapshot)
+      double A = 0.0, B = 1.0;
+      if (!layout_.tlaw && cdiff_.kind == COEFF_GRIDFUNC_AFFINE)
+      {
+         A = cdiff_.scale * (1.0 - cdiff_.slope * cdiff_.t_ref);
+         B = cdiff_.scale * cdiff_.slope;
+      }
       if (treg_all_)
       {
          tsnap_.resize(std::max(1, ndofs_));
@@ -1250,10 +1264,16 @@ void PAForm::setup_qdata(hipStream_t s)
    }
 
    // Coefficient values at quadrature points (CoefficientVector::Project).
-   const double *cm_q = have_mass_ ? coeff_points(cmass_, ctmp_m_, s) : nullptr;
+   // (coefficient snapshot: the diffusion law is evaluated by the kernel, and with tmass 2 the mass law
+   // too -- the stored per-element value is then det J times the marker weight alone)
+   const bool mass_in_kernel = layout_.tsnap && layout_.tmass == 2 && cmass_.gridfunc();
+   CoeffDesc cm_one = cmass_;
+   cm_one.kind = COEFF_CONSTANT;
+   cm_one.value = 1.0;
+   const double *cm_q = have_mass_ && !mass_in_kernel ? coeff_points(cmass_, ctmp_m_, s) : nullptr;
    const double *cd_q = have_diff_ && !layout_.tsnap ? coeff_points(cdiff_, ctmp_d_, s) : nullptr;
 
-   const CoeffDesc *cm = have_mass_ ? &cmass_ : nullptr;
+   const CoeffDesc *cm = have_mass_ ? (mass_in_kernel ? &cm_one : &cmass_) : nullptr;
    const CoeffDesc *cd = have_diff_ ? &cdiff_ : nullptr;
    if (layout_.affine())
    {
@@ -1441,6 +1461,13 @@ ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, doubl
    for (int q = 0; q < Q_ && q < MAX_Q1D; q++) { a.qp.x[q] = maps_.qpts[q]; a.qw[q] = maps_.qw1[q]; }
    a.tsnap = layout_.tsnap ? tsnap_.data() : nullptr;
    a.tsnap_kind = layout_.tsnap;
+   a.tmass = layout_.tmass;
+   a.tlaw = layout_.tlaw;
+   if (layout_.tsnap && layout_.tlaw)
+   {
+      a.law_d = point_law_of(cdiff_);
+      if (layout_.tmass == 2 && cmass_.gridfunc()) { a.law_m = point_law_of(cmass_); }
+   }
    a.xwave = (layout_.kind == QLAYOUT_AFFINE || layout_.kind == QLAYOUT_TRILINEAR) ? 1 : 0;
    a.part_stride = part_stride_;
    a.gmap = (resolved_mode_ == KERNEL_TPE) ? gmap_blk_.data()
@@ -1591,34 +1618,33 @@ void PAForm::expand_compressed(DeviceArray<double> &fd, DeviceArray<double> &fm,
    for (int q = 0; q < Q_ && q < MAX_Q1D; q++) { qp.x[q] = maps_.qpts[q]; }
    if (layout_.tsnap)
    {
-      // the AFFINE pairs with W beta at the points (the coefficient evaluated as the reference's
-      // setup does), then their BLOCKED expansion
-      // beta at the points from the snapshot (the field as Assemble saw it, the law applied), the
-      // mass values as stored
-      QLayout La = layout_;
-      La.tsnap = 0;
-      La.pw = 1;
-      DeviceArray<double> fac, pair, ctd;
-      fac.resize(La.diff_size());
-      pair.resize(La.mass_size());
-      if (ne_ % kElemBlock) { ECM2_HIP(hipMemsetAsync(pair.data(), 0, pair.bytes(), s)); }
-      CoeffDesc cs = cdiff_;
-      cs.kind = COEFF_GRIDFUNC_VALUE;
-      cs.lvec = tsnap_.data();
-      DeviceArray<double> tdof;
+      // beta (and a mass law of the same field) at the points from the snapshot -- the field as
+      // Assemble saw it, projected as the reference's setup projects a GridFunctionCoefficient and the
+      // law applied at the point -- times the STORED element matrices and mass values (which the
+      // marker diagonal may have scaled, assemble_diagonal)
+      DeviceArray<double> tdof, ctd, ctm;
+      const double *tv = tsnap_.data();
       if (layout_.tsnap == 2)
       {
          tdof.resize(std::max(1, ndofs_));
          kern::lattice_to_dofs(layout_.nblk(), tpe_lattice_points(D_), lmap_.data(), tsnap_.data(), tdof.data(), s);
-         cs.lvec = tdof.data();
+         tv = tdof.data();
       }
+      CoeffDesc cs = cdiff_;
+      cs.kind = layout_.tlaw ? cdiff_.kind : COEFF_GRIDFUNC;  // (tlaw 0: the law is in the snapshot)
+      cs.lvec = tv;
+      cs.emask = nullptr;
       const double *cd_q = coeff_points(cs, ctd, s);
-      kern::setup_affine(La, Q_, jac_ ? nullptr : enodes_.data(), jac_, W_.data(), nullptr, &cs, nullptr, cd_q,
-                         fac.data(), pair.data(), s);
-      // (the stored element matrices C_e, not the recomputed ones in fac: the marker diagonal scales
-      // the stored qdata, assemble_diagonal)
-      kern::affine_expand(La, Q_, qd_diff_.data(), pair.data(), fd.data(), fm.data(), s,
-                          have_mass_ ? qd_mass_.data() : nullptr);
+      const double *cm_q = nullptr;
+      if (layout_.tmass == 2 && cmass_.gridfunc())
+      {
+         CoeffDesc cm = cmass_;
+         cm.lvec = tv;  // tlaw 1: the snapshot is the field itself
+         cm.emask = nullptr;
+         cm_q = coeff_points(cm, ctm, s);
+      }
+      kern::tsnap_expand(layout_, Q_, W_.data(), qd_diff_.data(), qd_mass_.data(), cd_q, cm_q, fd.data(),
+                         fm.data(), s);
       ECM2_HIP(hipStreamSynchronize(s));  // the temporaries are freed on return
       return;
    }

@@ -74,6 +74,9 @@ public:
    // whether the last Assemble took it.
    void set_coefficient_snapshot(bool on);
    bool coefficient_snapshot() const { return layout_.tsnap != 0; }
+   // with the snapshot: the mass values (QLayout::tmass) and where the laws are applied (QLayout::tlaw)
+   int snapshot_mass() const { return layout_.tmass; }
+   int snapshot_law_at_point() const { return layout_.tlaw; }
    // bytes of quadrature data the form stores (diffusion + mass + the coefficient snapshot)
    size_t qdata_bytes() const { return qd_diff_.bytes() + qd_mass_.bytes() + tsnap_.bytes(); }
 

@@ -61,6 +61,11 @@ extern "C" {
 #define ECM2_COEFF_CONST_VECTOR 7
 #define ECM2_COEFF_CONST_SYMMATRIX 8
 #define ECM2_COEFF_CONST_MATRIX 9
+/* GridFunctionCoefficient of an H1 field on the form's own space (fem/coefficient.cpp:250-253 ->
+ * QuadratureFunction::ProjectGridFunction, qfunction.cpp:73-98): data = the field's device L-vector,
+ * params NULL; the value at a point is the interpolated field (no law) -- e.g. ex16p's conductivity
+ * kappa + alpha u formed at the dofs, examples/ex16p.cpp:450-466. */
+#define ECM2_COEFF_GRIDFUNC 10
 
 /* Kernel selection (all produce the same operator). */
 #define ECM2_KERNEL_AUTO 0     /* TPE for p <= 2, LINE for p = 3..6                 */
@@ -182,14 +187,23 @@ int ecm2_pa_form_set_jacobians(ecm2_pa_form *f, const double *J);
 #define ECM2_QLAYOUT_TRILINEAR_E 6
 int ecm2_pa_form_set_geometry_compression(ecm2_pa_form *f, int on);
 /* Coefficient snapshot (p = 2, AFFINE layout, every 64-element block a lattice brick, the
- * diffusion coefficient ECM2_COEFF_GRIDFUNC_AFFINE without an attribute marker): Assemble keeps
- * T' = scale (1 + slope (T - t_ref)) at the field's dofs and the fused kernel interpolates it at
- * the quadrature points, instead of storing W beta per point (the reference evaluates the same
- * coefficient at the points in its setup, coefficient.cpp:2052-2070): 8 B per point fewer.  The
- * snapshot is taken at Assemble (the reference's assemble-time semantics).  On by default;
- * ecm2_pa_form_coefficient_snapshot reports whether the last Assemble took it. */
+ * diffusion coefficient a grid-function kind -- ECM2_COEFF_GRIDFUNC, _GRIDFUNC_AFFINE or
+ * _GRIDFUNC_PERFUSION -- without an attribute marker): Assemble keeps a copy of the field at its
+ * dofs (with an affine / identity law applied there) and the fused kernel interpolates it at the
+ * quadrature points and applies the law there (as TransformedCoefficient::Eval, coefficient.cpp:262),
+ * instead of storing W beta per point (the reference evaluates the same coefficient at the points in
+ * its setup, coefficient.cpp:2052-2070): 8 B per point fewer.  A MassIntegrator with a constant
+ * coefficient or a grid-function law of the SAME field (the Pennes heat capacity + perfusion
+ * alpha(T)) then stores one value per element instead of W alpha det J per point: no per-point
+ * stream at all.  The snapshot is taken at Assemble (the reference's assemble-time semantics).  On
+ * by default; ecm2_pa_form_coefficient_snapshot reports whether the last Assemble took it. */
 int ecm2_pa_form_set_coefficient_snapshot(ecm2_pa_form *f, int on);
 int ecm2_pa_form_coefficient_snapshot(const ecm2_pa_form *f, int *on);
+/* Introspection of the last Assemble's snapshot (no reference counterpart; any output may be NULL):
+ * *on as above; *mass_values 0 = no MassIntegrator, 1 = W alpha det J stored per point, 2 = one value
+ * per element (constant or same-field mass law); *law_at_point 1 = the field itself is interpolated and
+ * the laws applied at the point, 0 = an affine / identity law applied to the snapshot's dofs. */
+int ecm2_pa_form_snapshot_info(const ecm2_pa_form *f, int *on, int *mass_values, int *law_at_point);
 /* BilinearForm::AddDomainIntegrator(new MassIntegrator(Q)) / DiffusionIntegrator(Q)
  * (bilinearform.cpp:231-242).  data: CONSTANT -> data[0] (host);
  * QUAD -> device [ne][nq]; GRIDFUNC_AFFINE -> device L-vector T with

@@ -321,6 +321,11 @@ def test_gpu_loopback_group_coefficient_snapshot(decomp, split):
         # (OVERLAP: rank 0 holds 5 layers, a leftover layer of non-brick blocks; rank 1's 4 layers are bricks)
         if split == "slabs":
             assert pf.CoefficientSnapshot() == (decomp == "rap" or r == 1)
+        else:
+            # brick runs (4 whole bricks per rank): with RAP every rank holds bricks only and takes the
+            # snapshot (ghost-touching bricks read T' through their lattice map); with OVERLAP the ghost
+            # element layers of ranks 0 and 1 are not bricks (profiles/r5/probe_snap_parts.txt)
+            assert pf.CoefficientSnapshot() == (decomp == "rap" or r == 2)
         forms.append(pf)
         parts.append(part)
         xs.append(torch.as_tensor(xg[part.owned_global]).cuda())

@@ -353,9 +353,9 @@ def test_c5_sdirk_step_full_size():
     K = _serial_form(fes, None, None, beta)
     assert T.BrickInfo() == (fes.ne // 4, 1) and T.info()["layout"] == E.QLAYOUT_AFFINE_E
     ess = fes.boundary_dofs()
-    X = fes.dof_coords()
-    u0 = 37.0 + 20.0 * np.exp(-4.0 * np.sum((X - 0.5) ** 2, axis=1))
-    del X
+    # a rough state (uniform random): K u0 without cancellation, so the comparison measures the step's
+    # algebra rather than the rounding of a near-zero Laplacian amplified by 24 unconverged CG iterations
+    u0 = np.random.default_rng(68).uniform(-1.0, 1.0, fes.ndofs)
     u = dev(u0)
     ns, it, conv = E.ode_step(23, E.Operator(T), E.Operator(K), dt, u, ess=dev(ess, torch.int32), rel_tol=0.0,
                               max_iter=iters)

@@ -146,6 +146,30 @@ def bench_form(E, torch, mesh, fes, keep, kernel=0, scatter="partials", compress
     return f
 
 
+PERFUSION = (3.6e6, 0.05 * 3.6e3, 6.4e-3, 0.02, 37.0, 50.0)  # rho_c, gamma dt c_b, w0, a, T0, T_stop
+
+
+def bench_law_form(E, torch, mesh, fes, keep, case):
+    """The coefficient-snapshot forms whose mass is not a quadrature coefficient (bench sub-objects):
+    pennes -- Mass(rho c + gamma dt c_b w_b(T)) + Diffusion(gamma dt k(T)) of one H1 temperature field
+    (the Pennes perfusion law with coagulation shut-off at T_stop, evaluated at the point); ex16 --
+    ex16p's implicit operator M + dt K(u_alpha_gf), u_alpha_gf = kappa + alpha u formed at the dofs and
+    passed as a GridFunctionCoefficient (examples/ex16p.cpp:450-466), the mass coefficient 1."""
+    T = torch.as_tensor(temperature_fn(fes.dof_coords())).cuda()
+    f = E.BilinearForm(fes)
+    if case == "pennes":
+        keep.append(T)
+        f.AddDomainIntegrator(E.MassIntegrator(E.PerfusionCoefficient(T, *PERFUSION)))
+        f.AddDomainIntegrator(E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(T, K_SCALE, K_SLOPE, K_TREF)))
+    else:
+        ua = 0.05 * (0.5 + 0.01 * T)  # dt (kappa + alpha u)
+        keep.append(ua)
+        f.AddDomainIntegrator(E.MassIntegrator(E.ConstantCoefficient(1.0)))
+        f.AddDomainIntegrator(E.DiffusionIntegrator(E.GridFunctionCoefficient(ua)))
+    f.Assemble()
+    return f
+
+
 def qdata_layout(E, form):
     """Quadrature-data layout of a (local) form: affine | affine_ts (AFFINE with the k(T)
     coefficient snapshot) | affine_e | trilinear | trilinear_e | blocked | native."""
@@ -455,7 +479,7 @@ def main():
                           element_order="faces" if numbering == "entity" and args.workload != "c3" else "auto",
                           geometry_input=geo, coefficient_snapshot=bool(args.coefficient_snapshot))
 
-    def sub_measure(f, fes_s, tag, note):
+    def sub_measure(f, fes_s, tag, note, use_pin=True):
         """Time another serial form of this workload in this run (same steps, same clock
         settling): value, step and kernel time, roofline (the pin of its own variant)."""
         xs = torch.empty(fes_s.ndofs, dtype=torch.float64, device="cuda")
@@ -474,7 +498,7 @@ def main():
                 "ms_per_step": round(dtf / args.steps * 1e3, 5),
                 "lattice_units": [lat, units], "summation_runs": runs,
                 "roofline": roofline(args.workload + tag, 1, lay, kf, f.algorithmic_bytes(),
-                                     min_bytes(f, fes_s.ne, nd, fes_s.ndofs), None, use_pin=pin_ok,
+                                     min_bytes(f, fes_s.ne, nd, fes_s.ndofs), None, use_pin=pin_ok and use_pin,
                                      flops=alg_flops(order, fes_s.ne)),
                 "note": note}
 
@@ -611,6 +635,21 @@ def main():
                                  "GeometricFactors::JACOBIANS array (set_jacobians, fitted to trilinear maps at "
                                  "Assemble)")
         del fv, md, fd
+        for case, note in (("pennes", "same run, same mesh and numbering as the main line, the Pennes operator with "
+                                      "both coefficients laws of one H1 temperature field: Mass(rho c + gamma dt c_b "
+                                      "w_b(T), perfusion shut-off at T_stop) + Diffusion(gamma dt k(T)); the snapshot "
+                                      "kernel applies both laws at the point and stores one mass value per element "
+                                      "(no per-point stream)"),
+                           ("ex16", "same run, same mesh and numbering, ex16p's implicit operator M + dt K(u_alpha_gf) "
+                                    "with u_alpha_gf = kappa + alpha u formed at the dofs and passed as a "
+                                    "GridFunctionCoefficient (examples/ex16p.cpp:450-466); one mass value per "
+                                    "element")):
+            dl.at(f"{case} form")
+            fv = bench_law_form(E, torch, mesh, fes, keep, case)
+            sub = sub_measure(fv, fes, "", note, use_pin=False)  # (the main line's pin is not this form's)
+            sub["snapshot"] = dict(zip(("on", "mass_values", "law_at_point"), fv.SnapshotInfo()))
+            subs[case] = sub
+            del fv
 
     if rank == 0:
         dl.at("stream copy peak")

@@ -152,7 +152,7 @@ void PAForm::add_integrator(int kind, const CoeffDesc &c, const int *marker, int
 {
    ECM2_VERIFY(!marker || n_marker >= 0, ERR_ARG, "negative marker size");
    ECM2_VERIFY(kind == INTEG_MASS || kind == INTEG_DIFFUSION, ERR_ARG, "unknown integrator " << kind);
-   ECM2_VERIFY(c.kind >= COEFF_CONSTANT && c.kind <= COEFF_CONST_MATRIX, ERR_ARG, "unknown coefficient kind " << c.kind);
+   ECM2_VERIFY(c.kind >= COEFF_CONSTANT && c.kind <= COEFF_GRIDFUNC, ERR_ARG, "unknown coefficient kind " << c.kind);
    ECM2_VERIFY(c.dim() == 1 || kind == INTEG_DIFFUSION, ERR_ARG,
                "vector / matrix coefficients belong to a DiffusionIntegrator");
    ECM2_VERIFY(!c.quad_values() || ne_ == 0 || c.quad, ERR_ARG, "null quadrature coefficient");

@@ -1,5 +1,6 @@
-// heat_step.cpp -- the serial bioheat step of examples/ex16.cpp (ConductionOperator with
-// MassIntegrator + DiffusionIntegrator at AssemblyLevel::PARTIAL, an SDIRK implicit solve by
+// heat_step.cpp -- the serial heat step of examples/ex16p.cpp (ConductionOperator with
+// MassIntegrator + DiffusionIntegrator(GridFunctionCoefficient(kappa + alpha u)) at
+// AssemblyLevel::PARTIAL, SetParameters after every step, an SDIRK implicit solve by
 // constrained Jacobi-PCG), written against the C ABI alone (include/ecm2_pa.h) the way a C++
 // host binding of the reference would call it: no Python, no torch; HIP only for device
 // buffers.  Checks the known answers of the reference's own fichera fixture (1^T M 1 = |fichera|
@@ -66,6 +67,22 @@ static ecm2_pa_form *make_form(int ne, int order, int ndofs, const std::vector<i
    return f;
 }
 
+// ex16p's K(u) = DiffusionIntegrator(GridFunctionCoefficient(u_alpha_gf)) [+ MassIntegrator(1)]: the
+// conductivity field is a grid function on the form's own space (ECM2_COEFF_GRIDFUNC), re-read at
+// every Assemble (ConductionOperator::SetParameters, examples/ex16p.cpp:450-466)
+static ecm2_pa_form *make_ex16_form(int ne, int order, int ndofs, const std::vector<int> &gmap,
+                                    const std::vector<double> &enodes, bool mass, const double *ua_dev)
+{
+   ecm2_pa_form *f = nullptr;
+   const double one = 1.0;
+   CHECK(ecm2_pa_form_create(ne, order, ndofs, gmap.data(), 0, &f));
+   CHECK(ecm2_pa_form_set_element_nodes(f, enodes.data()));
+   if (mass) { CHECK(ecm2_pa_form_add_integrator(f, ECM2_MASS, ECM2_COEFF_CONSTANT, &one, nullptr)); }
+   CHECK(ecm2_pa_form_add_integrator(f, ECM2_DIFFUSION, ECM2_COEFF_GRIDFUNC, ua_dev, nullptr));
+   CHECK(ecm2_pa_form_assemble(f, nullptr));
+   return f;
+}
+
 int main(int argc, char **argv)
 {
    const std::string path = argc > 1 ? argv[1] : "tests/golden/fichera.mesh";
@@ -128,19 +145,35 @@ int main(int argc, char **argv)
       ecm2_pa_form_destroy(M1);
    }
 
-   // ex16: M du/dt = -K(T) u with rho c = 1 (scaled), SDIRK33 stages (M + c dt K) k = -K u
+   // ex16p: M du/dt = -K(u) u with K(u) = div((kappa + alpha u) grad), rho c = 1 (scaled), SDIRK33
+   // stages (M + c dt K) k = -K u; as ex16p, the conductivity is lagged: SetParameters(u) after
+   // every step forms u_alpha_gf = kappa + alpha u at the dofs and re-assembles K and T from it
    const int type = 23;
-   const double dt = 0.01, c = ecm2_ode_implicit_coeff(type), kscale = 0.5;
-   ecm2_pa_form *Kf = make_form(ne, order, ndofs, gmap, enodes, 0.0, true, T, kscale);
-   ecm2_pa_form *Tf = make_form(ne, order, ndofs, gmap, enodes, 1.0, true, T, c * dt * kscale);
-   ecm2_operator *Kop = nullptr, *Top = nullptr;
-   CHECK(ecm2_operator_from_pa_form(Kf, &Kop));
-   CHECK(ecm2_operator_from_pa_form(Tf, &Top));
+   const double dt = 0.01, c = ecm2_ode_implicit_coeff(type), kappa = 0.5, alpha_u = 0.01;
    // u = T - 37 (the excess temperature decays to the boundary value 0)
    std::vector<double> u0(ndofs);
    for (int i = 0; i < ndofs; i++) { u0[i] = T0[i] - 37.0; }
    for (int i : ess) { u0[i] = 0.0; }
    double *u = device_copy(u0);
+   std::vector<double> ua(ndofs), cua(ndofs);
+   auto set_parameters = [&](const std::vector<double> &uh) {
+      for (int i = 0; i < ndofs; i++)
+      {
+         ua[i] = kappa + alpha_u * uh[i];
+         cua[i] = c * dt * ua[i];
+      }
+   };
+   set_parameters(u0);
+   double *ua_d = device_copy(ua), *cua_d = device_copy(cua);
+   ecm2_pa_form *Kf = make_ex16_form(ne, order, ndofs, gmap, enodes, false, ua_d);
+   ecm2_pa_form *Tf = make_ex16_form(ne, order, ndofs, gmap, enodes, true, cua_d);
+   int snap = 0, mvals = 0, atpt = 0;
+   CHECK(ecm2_pa_form_snapshot_info(Tf, &snap, &mvals, &atpt));
+   std::printf("T = M + c dt K(u): coefficient snapshot %d (mass values %d, laws at the point %d)\n", snap, mvals,
+               atpt);
+   ecm2_operator *Kop = nullptr, *Top = nullptr;
+   CHECK(ecm2_operator_from_pa_form(Kf, &Kop));
+   CHECK(ecm2_operator_from_pa_form(Tf, &Top));
    double umax0 = 0.0;
    for (double v : u0) { umax0 = std::max(umax0, std::fabs(v)); }
    double umax = umax0;
@@ -155,6 +188,13 @@ int main(int argc, char **argv)
                   iters, conv, mx);
       pass &= conv != 0 && std::isfinite(mx) && mx <= umax * (1.0 + 1e-12);  // a heat equation's maximum principle
       umax = mx;
+      // ConductionOperator::SetParameters(u): the new conductivity field, then Assemble (the forms
+      // read their grid functions at Assemble, as the reference's K->Assemble does)
+      set_parameters(uh);
+      HIPCHECK(hipMemcpy(ua_d, ua.data(), ndofs * sizeof(double), hipMemcpyHostToDevice));
+      HIPCHECK(hipMemcpy(cua_d, cua.data(), ndofs * sizeof(double), hipMemcpyHostToDevice));
+      CHECK(ecm2_pa_form_assemble(Kf, nullptr));
+      CHECK(ecm2_pa_form_assemble(Tf, nullptr));
    }
    pass &= umax < umax0;
    std::printf("%s\n", pass ? "PASS" : "FAIL");
@@ -164,6 +204,8 @@ int main(int argc, char **argv)
    ecm2_pa_form_destroy(Tf);
    ecm2_pa_form_destroy(Kf);
    (void)hipFree(u);
+   (void)hipFree(ua_d);
+   (void)hipFree(cua_d);
    (void)hipFree(y);
    (void)hipFree(one);
    (void)hipFree(ess_d);

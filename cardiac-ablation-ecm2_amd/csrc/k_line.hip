@@ -537,14 +537,23 @@ constexpr int brick_wpe()
    constexpr int W = BrickShapeC<D, Q, BZ>::WPE;
    return (G == 2 && W > 3) ? 3 : W;
 }
-template <int D, int Q, int BZ, bool SPLIT, int G, bool REG>
+// TS (round 5, AFFINE_E only): the coefficient snapshot (kernels.hpp QLayout::tsnap) -- the diffusion
+// coefficient's field T is gathered beside x (the same addressing), interpolated at the quadrature
+// points through the same five stages with B only (its x image parks in sYQ until the y stage has
+// read it, its y image in sXL until the z stage has: no extra LDS, one more barrier), and
+// W beta = W_q law(T(x_q)) is formed at the point (LAW: the law applied there, else folded into the
+// snapshot's dofs).  TS 1: W alpha det J streamed per point (8 B instead of the 16-B pair); TS 2: one
+// value per element, (c alpha) det J, times W_q [law_m(T(x_q))]: no per-point stream.
+template <int D, int Q, int BZ, bool SPLIT, int G, bool REG, int TS = 0, bool LAW = false>
 __global__ void __launch_bounds__((BrickShapeC<D, Q, BZ>::NT), (brick_wpe<D, Q, BZ, G>()))
 k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int *__restrict__ bmap,
                 const int *__restrict__ breg, int n_owned, const double *__restrict__ qdd,
                 const double *__restrict__ qdm, const double *__restrict__ x, const double *__restrict__ xg,
                 double *__restrict__ y, double *__restrict__ yg, const Basis1D *__restrict__ btab,
-                double *__restrict__ part, const QPts qp)
+                double *__restrict__ part, const QPts qp, const double *__restrict__ tsn, const QPts qw,
+                const PointLaw law_d, const PointLaw law_m)
 {
+   static_assert(TS == 0 || G == 1, "the coefficient snapshot runs on AFFINE_E");
    constexpr bool AFF = G != 0;  // a compressed layout: point pairs + per-element data
    using S = BrickShapeC<D, Q, BZ>;
    constexpr int NE = S::NE, DD = S::DD, QQ = S::QQ, DQ = S::DQ, SA = S::SA, SB = S::SB, DS = S::DS;
@@ -583,14 +592,18 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
    const int eLc = eL < NE ? eL : NE - 1, lLc = lL < DD ? lL : DD - 1;
    const int e = belem[(size_t)k * NE + (e3 < NE ? e3 : NE - 1)];
    const int l3c = l3 < QQ ? l3 : QQ - 1;
-   double xl[D];
+   double xl[D], tl[D];
    {
       const int dy = lLc % D, dz = lLc / D, ex = eLc & 1, ey = (eLc >> 1) & 1, ez = eLc >> 2;
       if (REG)
       {
          const int d0 = base + (ex * (D - 1)) * sx + (ey * (D - 1) + dy) * sy + (ez * (D - 1) + dz) * sz;
 #pragma unroll
-         for (int dx = 0; dx < D; dx++) { xl[dx] = x[d0 + dx * sx]; }
+         for (int dx = 0; dx < D; dx++)
+         {
+            xl[dx] = x[d0 + dx * sx];
+            if (TS) { tl[dx] = tsn[d0 + dx * sx]; }
+         }
       }
       else
       {
@@ -600,14 +613,28 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
          {
             const int d = bdof(mp[dx]);
             xl[dx] = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
+            if (TS) { tl[dx] = tsn[d]; }  // (the snapshot: the whole local L-vector, contiguous)
          }
       }
    }
    __builtin_amdgcn_sched_barrier(0);  // keep the gather ahead of the qdata loads
    double qv[7][Q];
    v2d pa[Q];
+   double pm[Q];        // TS 1: W alpha det J of this lane's column
+   double mel = 0.0;    // TS 2: the element's (c alpha) det J
    double cc[6];
-   if (AFF)
+   if (TS)
+   {
+      if (TS == 1)
+      {
+#pragma unroll
+         for (int qz = 0; qz < Q; qz++) { pm[qz] = __builtin_nontemporal_load(qdm + (size_t)e * NQ + qz * QQ + l3c); }
+      }
+      else { mel = qdm[e]; }
+#pragma unroll
+      for (int c = 0; c < 6; c++) { cc[c] = qdd[(size_t)e * 6 + c]; }
+   }
+   else if (AFF)
    {
       // the point pairs are streamed once per Mult: nontemporal, so they do not evict the x lines
       // neighbouring bricks gather again (profiles/r3_ab_bnt.txt: kernel -1%, Mult -2%)
@@ -636,27 +663,42 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
          o[qx * DD] = u[qx];
          o[Q * DD + qx * DD] = v[qx];
       }
+      if (TS)
+      {
+         // T's x image [qx][dz][dy] parks in sYQ (free until the y stage writes it)
+         double te_[NEO], to_[NOO], tu[Q];
+         eo_split<D>(tl, te_, to_);
+         eo_fwd_b<D, Q>(te, te_, to_, tu);
+#pragma unroll
+         for (int qx = 0; qx < Q; qx++) { sYQ[eL * SB + qx * DD + lL] = tu[qx]; }
+      }
    }
    if (k_begin < 0)  // never: a use outside the x stage stops the gather sinking behind the qdata
    {
       double u = 0.0;
 #pragma unroll
-      for (int dx = 0; dx < D; dx++) { u += xl[dx]; }
+      for (int dx = 0; dx < D; dx++) { u += xl[dx]; if (TS) { u += tl[dx]; } }
       part[t] = u;
    }
    __syncthreads();
    // ---- lanes (element, qx, dz), l2 = qx + Q dz: contract in y -> sYQ [g][dz][qy][qx]
+   double la[D], lb[D], lt[D];
    if (act2)
    {
       const int qx = lL % Q, dz = lL / Q;
       const double *in = sXL + eL * SA + qx * DD + dz * D;
-      double la[D], lb[D];
 #pragma unroll
       for (int dy = 0; dy < D; dy++)
       {
          la[dy] = lds_read(in + dy);
          lb[dy] = lds_read(in + Q * DD + dy);
+         if (TS) { lt[dy] = lds_read(sYQ + eL * SB + qx * DD + dz * D + dy); }
       }
+   }
+   if (TS) { __syncthreads(); }  // every lane has read T's x image (sYQ) and the x images (sXL)
+   if (act2)
+   {
+      const int qx = lL % Q, dz = lL / Q;
       double *o = sYQ + eL * SB + dz * DS + qx;
       CBasisEO *te = stage_eo(btab);
       double ae[NEO], ao[NOO], be[NEO], bo[NOO], gb[Q], bg[Q], bb[Q];
@@ -672,20 +714,31 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
          o[D * DS + qy * Q] = bg[qy];
          o[2 * D * DS + qy * Q] = bb[qy];
       }
+      if (TS)
+      {
+         // T's y image [dz][qy][qx] into sXL (read by the z stage before the x transposes overwrite it)
+         double te_[NEO], to_[NOO], ty[Q];
+         eo_split<D>(lt, te_, to_);
+         eo_fwd_b<D, Q>(te, te_, to_, ty);
+#pragma unroll
+         for (int qy = 0; qy < Q; qy++) { sXL[eL * SA + dz * QQ + qy * Q + qx] = ty[qy]; }
+      }
    }
    __syncthreads();
    // ---- lanes (element, qx, qy): contract in z, weight, transpose in z (in place)
    if (act3)
    {
       double *io = sYQ + e3 * SB + l3;
-      double l0[D], l1[D], l2[D];
+      double l0[D], l1[D], l2[D], lz[D];
 #pragma unroll
       for (int dz = 0; dz < D; dz++)
       {
          l0[dz] = lds_read(io + dz * DS);
          l1[dz] = lds_read(io + D * DS + dz * DS);
          l2[dz] = lds_read(io + 2 * D * DS + dz * DS);
+         if (TS) { lz[dz] = lds_read(sXL + e3 * SA + dz * QQ + l3); }
       }
+      const double wxy = TS ? qw.x[l3 % Q] * qw.x[l3 / Q] : 0.0;  // W_q = w_qx w_qy w_qz
       // TRILINEAR_E: the column's Jacobian pieces, J[i][0] = a0 + b0 zeta, J[i][1] = a1 + b1 zeta,
       // J[i][2] = j2 (dev_common.hpp trilinear_jacobian at xi = x_qx, eta = x_qy)
       double a0[3], b0[3], a1[3], b1[3], j2[3];
@@ -705,10 +758,19 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
             j2[i] = (c[6 + i] + c[12 + i] * xi) + b1[i] * et;
          }
       }
-      // the quadrature-point operator: (f, m) = (W beta C grad u, W alpha det J u) at qz
-      auto qpoint = [&](int qz, double gx, double gy, double gz, double u, double &fx, double &fy, double &fz,
-                        double &m) {
-         if (G == 2)
+      // the quadrature-point operator: (f, m) = (W beta C grad u, W alpha det J u) at qz; tq: T(x_q) (TS)
+      auto qpoint = [&](int qz, double gx, double gy, double gz, double u, double tq, double &fx, double &fy,
+                        double &fz, double &m) {
+         if (TS)
+         {
+            const double Wq = wxy * qw.x[qz];
+            const double wb = Wq * (LAW ? point_law(law_d, tq) : tq);
+            fx = wb * (cc[0] * gx + cc[1] * gy + cc[2] * gz);
+            fy = wb * (cc[1] * gx + cc[3] * gy + cc[4] * gz);
+            fz = wb * (cc[2] * gx + cc[4] * gy + cc[5] * gz);
+            m = (TS == 1 ? pm[qz] : Wq * mel * (LAW ? point_law(law_m, tq) : 1.0)) * u;
+         }
+         else if (G == 2)
          {
             // f = (W beta / det J) adj(J) (adj(J)^T g), adj(J) from J at (x_qx, x_qy, x_qz)
             const double zt = qp.x[qz];
@@ -750,10 +812,11 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
       // rows qz and Q-1-qz together: forward split contractions, the operator at both points, the
       // transposed contractions accumulated into split sums
       CBasisEO *te = stage_eo(btab);
-      double e0[NEO], o0[NOO], e1[NEO], o1[NOO], e2[NEO], o2[NOO];
+      double e0[NEO], o0[NOO], e1[NEO], o1[NOO], e2[NEO], o2[NOO], eT[NEO], oT[NOO];
       eo_split<D>(l0, e0, o0);
       eo_split<D>(l1, e1, o1);
       eo_split<D>(l2, e2, o2);
+      if (TS) { eo_split<D>(lz, eT, oT); }
       double A1E[NEO], A1O[NOO], A2E[NEO], A2O[NOO], A3E[NEO], A3O[NOO];
       eo_zero<D>(A1E, A1O);
       eo_zero<D>(A2E, A2O);
@@ -763,7 +826,7 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
       {
          const int qr = Q - 1 - qp;
          const bool mid = qr == qp;
-         double sx_ = 0.0, sy_ = 0.0, su = 0.0, sg = 0.0, ax = 0.0, ay = 0.0, au = 0.0, ag = 0.0;
+         double sx_ = 0.0, sy_ = 0.0, su = 0.0, sg = 0.0, ax = 0.0, ay = 0.0, au = 0.0, ag = 0.0, st = 0.0, at = 0.0;
 #pragma unroll
          for (int i = 0; i < NEO; i++)
          {
@@ -771,6 +834,7 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
             sx_ += b * e0[i];
             sy_ += b * e1[i];
             su += b * e2[i];
+            if (TS) { st += b * eT[i]; }
             if (!mid) { ag += te->GP[qp + MQ * i] * e2[i]; }
          }
 #pragma unroll
@@ -783,10 +847,11 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
                ax += b * o0[i];
                ay += b * o1[i];
                au += b * o2[i];
+               if (TS) { at += b * oT[i]; }
             }
          }
          double fxp, fyp, fzp, mp;
-         qpoint(qp, sx_ + ax, sy_ + ay, sg + ag, su + au, fxp, fyp, fzp, mp);
+         qpoint(qp, sx_ + ax, sy_ + ay, sg + ag, su + au, st + at, fxp, fyp, fzp, mp);
          if (mid)
          {
 #pragma unroll
@@ -803,7 +868,7 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
          else
          {
             double fxr, fyr, fzr, mr;
-            qpoint(qr, sx_ - ax, sy_ - ay, sg - ag, su - au, fxr, fyr, fzr, mr);
+            qpoint(qr, sx_ - ax, sy_ - ay, sg - ag, su - au, st - at, fxr, fyr, fzr, mr);
             const double fxe = fxp + fxr, fxo = fxp - fxr, fye = fyp + fyr, fyo = fyp - fyr;
             const double fze = fzp + fzr, fzo = fzp - fzr, me = mp + mr, mo = mp - mr;
 #pragma unroll
@@ -1056,11 +1121,32 @@ void launch_brick(const ApplyArgs &a, hipStream_t s)
    ECM2_VERIFY(a.part_brick, ERR_INTERNAL, "brick kernel needs its partial slots");
    const bool split = a.xg || a.yg;
    const int g = a.kind == QLAYOUT_AFFINE_E ? 1 : a.kind == QLAYOUT_TRILINEAR_E ? 2 : 0;
-   ECM2_VERIFY(g == 0 || a.pw == 2, ERR_INTERNAL, "bricks need both integrators");
+   ECM2_VERIFY(g == 0 || a.pw == 2 || a.tsnap, ERR_INTERNAL, "bricks need both integrators");
    const dim3 grid(k1 - k0), block(BrickShapeC<D, Q, BZ>::NT);
-#define ECM2_BRICK(SP, GG, RG)                                                                             \
-   hipLaunchKernelGGL((k_apply_brick_c<D, Q, BZ, SP, GG, RG>), grid, block, 0, s, k0, k1, a.belem, a.bmap,    \
-                      a.breg, a.n_owned, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, a.btab, a.part_brick, a.qp)
+   QPts qw = {};
+   for (int q = 0; q < MAX_Q1D; q++) { qw.x[q] = a.qw[q]; }
+#define ECM2_BRICK_TS(SP, GG, RG, TS, LW)                                                                  \
+   hipLaunchKernelGGL((k_apply_brick_c<D, Q, BZ, SP, GG, RG, TS, LW>), grid, block, 0, s, k0, k1, a.belem,     \
+                      a.bmap, a.breg, a.n_owned, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, a.btab, a.part_brick, a.qp,  \
+                      a.tsnap, qw, a.law_d, a.law_m)
+   if constexpr (BZ == 1 && D <= 6)
+   {
+      if (a.tsnap)
+      {
+         ECM2_VERIFY(g == 1 && a.tsnap_kind == 1 && (a.tmass == 1 || a.tmass == 2) && a.pw == (a.tmass == 1 ? 1 : 0),
+                     ERR_INTERNAL, "brick coefficient snapshot: AFFINE_E, dof-ordered, both integrators");
+#define ECM2_BRICK_TSM(SP, RG)                                                        \
+   if (a.tmass == 1) { if (a.tlaw) { ECM2_BRICK_TS(SP, 1, RG, 1, true); } else { ECM2_BRICK_TS(SP, 1, RG, 1, false); } } \
+   else { if (a.tlaw) { ECM2_BRICK_TS(SP, 1, RG, 2, true); } else { ECM2_BRICK_TS(SP, 1, RG, 2, false); } }
+         if (split) { ECM2_BRICK_TSM(true, false) }
+         else if (a.breg) { ECM2_BRICK_TSM(false, true) }
+         else { ECM2_BRICK_TSM(false, false) }
+#undef ECM2_BRICK_TSM
+         return;
+      }
+   }
+   ECM2_VERIFY(!a.tsnap, ERR_INTERNAL, "no brick snapshot kernel for D1D=" << D << " bz=" << BZ);
+#define ECM2_BRICK(SP, GG, RG) ECM2_BRICK_TS(SP, GG, RG, 0, false)
 #define ECM2_BRICK_G(SP, RG)                    \
    if (g == 1) { ECM2_BRICK(SP, 1, RG); }       \
    else if (g == 2) { ECM2_BRICK(SP, 2, RG); }  \
@@ -1070,6 +1156,7 @@ void launch_brick(const ApplyArgs &a, hipStream_t s)
    else { ECM2_BRICK_G(false, false) }
 #undef ECM2_BRICK_G
 #undef ECM2_BRICK
+#undef ECM2_BRICK_TS
 }
 
 void apply_brick(int D, int Q, const ApplyArgs &a, hipStream_t s)

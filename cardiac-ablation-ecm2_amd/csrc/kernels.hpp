@@ -100,6 +100,7 @@ struct QLayout
    {
       if (kind == QLAYOUT_NATIVE || kind == QLAYOUT_NATIVE9) { return (size_t)ne * nq; }
       if (kind == QLAYOUT_AFFINE && tsnap && tmass == 2) { return (size_t)nblk() * kElemBlock; }  // [blk][lane]
+      if (kind == QLAYOUT_AFFINE_E && tsnap && tmass == 2) { return (size_t)ne; }                 // [e]
       if (kind == QLAYOUT_AFFINE || kind == QLAYOUT_TRILINEAR) { return (size_t)nblk() * nq * pw * kElemBlock; }
       if (kind == QLAYOUT_AFFINE_E || kind == QLAYOUT_TRILINEAR_E) { return (size_t)ne * nq * pw; }
       return (size_t)nblk() * ((nq + 1) / 2) * 2 * kElemBlock;

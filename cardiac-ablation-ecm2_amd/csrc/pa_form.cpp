@@ -1140,8 +1140,14 @@ void PAForm::assemble(hipStream_t s)
    layout_.tmass = 0;
    layout_.tlaw = 0;
    tsnap_.resize(0);
-   if (tsnap_pref_ && layout_.kind == QLAYOUT_AFFINE && resolved_mode_ == KERNEL_TPE && D_ == 3 && Q_ == 4 &&
-       (treg_all_ || tlat_all_) && have_diff_ && cdiff_.gridfunc() && cdiff_.lvec && !marked_[INTEG_DIFFUSION])
+   // p >= 3 (k_apply_brick_c, round 5): AFFINE_E, every element in a 2 x 2 x 1 brick (both integrators:
+   // bricks exist only with both), the snapshot in dof order.
+   const bool ts_tpe = layout_.kind == QLAYOUT_AFFINE && resolved_mode_ == KERNEL_TPE && D_ == 3 && Q_ == 4 &&
+                       (treg_all_ || tlat_all_);
+   const bool ts_brick = layout_.kind == QLAYOUT_AFFINE_E && resolved_mode_ == KERNEL_LINE && n_bricks_ > 0 &&
+                         n_left_ == 0 && brick_bz_ == 1 && D_ <= 6 && Q_ == D_ + 1 && have_mass_ && use_partials();
+   if (tsnap_pref_ && (ts_tpe || ts_brick) && have_diff_ && cdiff_.gridfunc() && cdiff_.lvec &&
+       !marked_[INTEG_DIFFUSION])
    {
       layout_.tsnap = 1;
       const bool mass_law = have_mass_ && cmass_.gridfunc() && cmass_.lvec == cdiff_.lvec;
@@ -1159,7 +1165,7 @@ void PAForm::assemble(hipStream_t s)
          A = cdiff_.scale * (1.0 - cdiff_.slope * cdiff_.t_ref);
          B = cdiff_.scale * cdiff_.slope;
       }
-      if (treg_all_)
+      if (ts_brick || treg_all_)
       {
          tsnap_.resize(std::max(1, ndofs_));
          kern::affine_snapshot(ndofs_, cdiff_.lvec, A, B, tsnap_.data(), s);

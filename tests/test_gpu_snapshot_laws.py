@@ -159,6 +159,65 @@ def test_snapshot_laws(numbering, dkind, mass):
     assert relerr(host(ye).reshape(fes.ne, fes.nd), O.diffusion_apply(op.B, op.G, op.D, xe)) <= RTOL
 
 
+@pytest.mark.parametrize("dkind", ["gridfunc", "affine", "perfusion"])
+@pytest.mark.parametrize("mass", ["quad", "const", "perf_same", "perf_marked"])
+@pytest.mark.parametrize("order", [3, 4, 5])
+def test_snapshot_laws_bricks(order, dkind, mass):
+    """p = 3..5 (the line-kernel family): every element of a Cartesian mesh in a lattice-addressed
+    2 x 2 x 1 brick, so the brick kernel takes the snapshot (k_apply_brick_c TS 1 / 2, the field's x
+    and y images parked in the other stage's LDS image); Mult, diagonal, qdata and AddMultPA against
+    the oracle, and against the same form without the snapshot."""
+    m = E.Mesh.MakeCartesian3D(6, 4, 4, 1.0, 0.7, 1.3)
+    m.SetAttributes(1 + np.arange(m.GetNE()) % 2)
+    fes = E.H1Space(m, order, E.NUMBERING_STRUCTURED)
+    en = m.element_nodes()
+    q1d = O.default_q1d(order)
+    gm = fes.gather_map()
+    T = temperature(fes.dof_coords())
+    Tq = BH.temperature_at_quadrature(T, gm, order, q1d)
+    t_stop = mid_gap_stop(Tq)
+    attr = m.GetAttributes()
+    a_q = alpha_bioheat(O.quad_points(en, q1d))
+    forms, keep = {}, []
+    for snap in (True, False):
+        Td = dev(T)
+        keep.append(Td)
+        f = E.BilinearForm(fes, coefficient_snapshot=snap)
+        dc, dlaw = diff_coeff(dkind, Td, t_stop)
+        f.AddDomainIntegrator(E.DiffusionIntegrator(dc))
+        marker = [1, 0] if mass == "perf_marked" else None
+        mc = {"quad": lambda: E.QuadratureCoefficient(dev(a_q.reshape(fes.ne, -1))),
+              "const": lambda: E.ConstantCoefficient(3.6e6)}.get(
+            mass, lambda: E.PerfusionCoefficient(Td, *(PERF_MASS + (t_stop,))))()
+        f.AddDomainIntegrator(E.MassIntegrator(mc), marker)
+        f.Assemble()
+        forms[snap] = f
+    form = forms[True]
+    assert form.info()["layout"] == E.QLAYOUT_AFFINE_E and form.BrickInfo() == (fes.ne // 4, 1)
+    want_m = 1 if mass == "quad" else 2
+    assert form.SnapshotInfo() == (True, want_m, dkind == "perfusion" or mass.startswith("perf"))
+    assert not forms[False].CoefficientSnapshot()
+    alpha = a_q if mass == "quad" else 3.6e6 if mass == "const" else BH.perfusion_law(Tq, *(PERF_MASS + (t_stop,)))
+    op = O.OracleOperator(en, gm, fes.ndofs, order, alpha=alpha, beta=dlaw(Tq))
+    for t in keep:
+        t.fill_(1.0e3)
+    x = np.random.default_rng(order).uniform(-1, 1, fes.ndofs)
+    y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+    form.Mult(dev(x), y)
+    marked = mass == "perf_marked"
+    assert relerr(host(y), op.mult_markers(x, attr, mass_marker=[1, 0]) if marked else op.mult(x)) <= RTOL
+    y2 = torch.empty_like(y)
+    forms[False].Mult(dev(x), y2)
+    assert relerr(host(y), host(y2)) <= 1e-13
+    d = torch.full_like(y, float("nan"))
+    form.AssembleDiagonal(d)
+    dwant = op.diagonal_markers(attr, [("diffusion", None), ("mass", [1, 0])]) if marked else op.diagonal()
+    assert relerr(host(d), dwant) < 1e-12
+    assert relerr(form.qdata(E.DIFFUSION), op.D) < 1e-12
+    if not marked:
+        assert relerr(form.qdata(E.MASS)[:, 0, :], op.M) < 1e-13
+
+
 @pytest.mark.parametrize("case", ["pennes", "ex16"])
 def test_snapshot_laws_c3_size(case):
     """configs[2]'s mesh (fichera refined 6x, 14.9M DoF, the reference's numbering: lattice-map blocks)

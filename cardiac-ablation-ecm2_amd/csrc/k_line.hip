@@ -995,6 +995,73 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
    }
 }
 
+// Surface points of a 2 x 2 x 1 brick in partial-slot order (brick_surface_index inverted):
+// X | Y << 8 | Z << 16.
+template <int D>
+struct BrickSurfXYZ
+{
+   static constexpr int LX = 2 * D - 1, LY = LX, LZ = D, N = brick_surface_points(D, 1);
+   int v[N];
+   constexpr BrickSurfXYZ() : v()
+   {
+      for (int Z = 0; Z < LZ; Z++)
+         for (int Y = 0; Y < LY; Y++)
+            for (int X = 0; X < LX; X++)
+            {
+               const int si = brick_surface_index(D, 1, X, Y, Z);
+               if (si >= 0) { v[si] = X | Y << 8 | Z << 16; }
+            }
+   }
+};
+template <int D>
+__device__ const BrickSurfXYZ<D> kBrickSurf = BrickSurfXYZ<D>();
+
+// The summation pass of a brick grid (PAForm::brick_grid_; 2 x 2 x 1 regular bricks in
+// lexicographic brick order, nbx per row, nbxy per layer): one workgroup per brick k, one thread per
+// surface point.  A point shared across a face lies on exactly the faces its breg face mask names;
+// the brick whose shared faces through the point are all low faces (X = 0, Y = 0, Z = 0) is its
+// highest holder and finishes it: the partial slots of the holders k - dz nbxy - dy nbx - dx (the
+// point mirrored onto the neighbour's high face) summed in ascending brick order -- the run plan's
+// ascending slot order, so the sums are bitwise those of k_sum_partials -- then y stored.  Addresses
+// follow from the brick index and a constant table: the loads issue at once, with no plan reads.
+template <int D>
+__global__ void __launch_bounds__(256)
+k_sum_brick_grid(int nbrick, int nbx, int nbxy, const int *__restrict__ breg, const double *__restrict__ part,
+                 double *__restrict__ y)
+{
+   constexpr int LX = 2 * D - 1, LY = LX, LZ = D, SURF = brick_surface_points(D, 1);
+   const int k = xcd_contiguous(blockIdx.x, gridDim.x);
+   if (k >= nbrick) { return; }
+   const int *r = breg + (size_t)k * 8;  // workgroup-uniform: scalar loads
+   const int base = r[0], sx = r[1], sy = r[2], sz = r[3], mask = r[4];
+   for (int t = threadIdx.x; t < SURF; t += blockDim.x)
+   {
+      const int c = kBrickSurf<D>.v[t];
+      const int X = c & 255, Y = (c >> 8) & 255, Z = c >> 16;
+      const int f = ((X == 0) | (X == LX - 1) << 1 | (Y == 0) << 2 | (Y == LY - 1) << 3 | (Z == 0) << 4 |
+                     (Z == LZ - 1) << 5) & mask;
+      if (f == 0 || (f & 0x2a)) { continue; }  // not shared, or a higher brick holds it too
+      const int nx = f & 1, ny = (f >> 2) & 1, nz = (f >> 4) & 1;
+      double v[8];
+      int n = 0;
+#pragma unroll
+      for (int dz = 1; dz >= 0; dz--)
+#pragma unroll
+         for (int dy = 1; dy >= 0; dy--)
+#pragma unroll
+            for (int dx = 1; dx >= 0; dx--)
+            {
+               if ((dz && !nz) || (dy && !ny) || (dx && !nx)) { continue; }
+               const int kk = k - dz * nbxy - dy * nbx - dx;
+               const int si = brick_surface_index(D, 1, dx ? LX - 1 : X, dy ? LY - 1 : Y, dz ? LZ - 1 : Z);
+               v[n++] = part[(size_t)kk * SURF + si];
+            }
+      double acc = v[0];
+      for (int h = 1; h < n; h++) { acc += v[h]; }
+      y[base + X * sx + Y * sy + Z * sz] = acc;
+   }
+}
+
 // PA diagonal, one 64-lane workgroup per element, any qdata layout, any (D1D, Q1D) with
 // Q1D^2 <= 64: the seven terms of diag(a) = sum_q grad(phi_a)^T O_q grad(phi_a) + m_q phi_a^2
 // sum-factorised in three stages through LDS (PADiffusionDiagonal3D / the mass diagonal,
@@ -1198,6 +1265,22 @@ bool has_brick(int D, int Q, int bz)
 }
 
 int brick_points(int D, int bz) { return (2 * D - 1) * (2 * D - 1) * (bz * (D - 1) + 1); }
+
+void sum_brick_grid(int D, int nbrick, int nbx, int nbxy, const int *breg, const double *part, double *y,
+                    hipStream_t s)
+{
+   if (nbrick == 0) { return; }
+#define ECM2_GRID_CASE(DD)                                                                                  \
+   if (D == DD)                                                                                             \
+   {                                                                                                        \
+      hipLaunchKernelGGL((k_sum_brick_grid<DD>), dim3(nbrick), dim3(256), 0, s, nbrick, nbx, nbxy, breg, part, y); \
+      ECM2_HIP(hipGetLastError());                                                                          \
+      return;                                                                                               \
+   }
+   ECM2_GRID_CASE(4) ECM2_GRID_CASE(5) ECM2_GRID_CASE(6) ECM2_GRID_CASE(7)
+#undef ECM2_GRID_CASE
+   ECM2_VERIFY(false, ERR_UNSUPPORTED, "no brick-grid summation for D1D=" << D);
+}
 
 void apply_line(int D, int Q, bool mass, bool diff, const ApplyArgs &a, hipStream_t s)
 {

@@ -884,7 +884,7 @@ SetupCoef make_setup_coef(const CoeffDesc *c, const double *q)
    SetupCoef s{};
    if (!c) { return s; }
    s.has = 1;
-   s.is_const = (c->kind == COEFF_CONSTANT || c->kind >= COEFF_CONST_VECTOR);
+   s.is_const = (c->kind == COEFF_CONSTANT || (c->kind >= COEFF_CONST_VECTOR && c->kind <= COEFF_CONST_MATRIX));
    s.dim = c->dim();
    s.value = c->value;
    for (int i = 0; i < 9; i++) { s.cv[i] = c->cv[i]; }

@@ -449,6 +449,12 @@ void scatter_add_idx(int n, const int *idx, const double *buf, double *y, hipStr
 // s_h = runs[r][8 + h] for h < 4, else rslots[slot_off + h].  runs has a sentinel row.
 void sum_partials(int b0, int b1, const int *blocks, const int *runs, const int *rslots, const int *pdof, const double *part,
                   int n_owned, double *y, double *yg, hipStream_t s);
+// The summation pass of regular 2 x 2 x 1 bricks in a lexicographic grid (PAForm::brick_grid_):
+// per brick and surface point, the highest holder sums the partial slots of the point's holders
+// (itself and its -x / -y / -z neighbours k - 1, k - nbx, k - nbxy) in ascending brick order and
+// stores y; no plan, no dependent reads.  breg [nbrick][8], part [nbrick][surface].
+void sum_brick_grid(int D, int nbrick, int nbx, int nbxy, const int *breg, const double *part, double *y,
+                    hipStream_t s);
 } // namespace kern
 
 } // namespace ecm2

@@ -35,6 +35,7 @@ PAForm::PAForm(int ne, int order, int ndofs, const int *gather_map_host, int q1d
    require_device();
    D_ = order + 1;
    Q_ = q1d > 0 ? q1d : default_q1d(order);
+   if (const char *g = std::getenv("ECM2_SUM_GRID")) { brick_grid_on_ = std::atoi(g) != 0; }
    ECM2_VERIFY(Q_ >= D_ && Q_ <= MAX_Q1D, ERR_ARG, "q1d must satisfy p+1 <= q1d <= " << MAX_Q1D);
    ND_ = D_ * D_ * D_;
    NQ_ = Q_ * Q_ * Q_;
@@ -1112,6 +1113,31 @@ void PAForm::assemble(hipStream_t s)
             r[0] = base; r[1] = sx; r[2] = sy; r[3] = sz; r[4] = mask;
          }
          if (regular) { breg_.upload(reg, s); }
+         // Brick grid (round 5): the regular bricks of a Cartesian lattice in lexicographic brick order
+         // (nbx along x, nby along y), each face shared exactly when a neighbour brick lies behind it.
+         // Then a shared point's holders are the brick and its -x / -y / -z neighbours k - 1, k - nbx,
+         // k - nbx nby, found by arithmetic: the summation pass needs no plan (k_sum_brick_grid).
+         brick_grid_ = {0, 0, 0};
+         if (regular && n_left == 0 && brick_bz_ == 1)
+         {
+            const int *r0 = &reg[0];
+            const int sx = r0[1], sy = r0[2], sz = r0[3];
+            int nbx = 1, nby = 1;
+            while (nbx < n_bricks_ && reg[(size_t)nbx * 8] == r0[0] + nbx * (LX - 1) * sx) { nbx++; }
+            while (nby * nbx < n_bricks_ && reg[(size_t)nby * nbx * 8] == r0[0] + nby * (LY - 1) * sy) { nby++; }
+            bool grid = n_bricks_ % (nbx * nby) == 0;
+            const int nbz = grid ? n_bricks_ / (nbx * nby) : 0, LZ = D_;
+            for (int k = 0; k < n_bricks_ && grid; k++)
+            {
+               const int i = k % nbx, j = (k / nbx) % nby, l = k / (nbx * nby);
+               const int *r = &reg[(size_t)k * 8];
+               const int want_mask = (i > 0) | (i < nbx - 1) << 1 | (j > 0) << 2 | (j < nby - 1) << 3 | (l > 0) << 4 |
+                                     (l < nbz - 1) << 5;
+               grid = r[0] == r0[0] + i * (LX - 1) * sx + j * (LY - 1) * sy + l * (LZ - 1) * sz && r[1] == sx &&
+                      r[2] == sy && r[3] == sz && r[4] == want_mask;
+            }
+            if (grid) { brick_grid_ = {n_bricks_, nbx, nbx * nby}; }
+         }
       }
       gmap_line_.upload(enc, s);
       lelem_.upload(lelem.empty() ? std::vector<int>{0} : lelem, s);
@@ -1443,6 +1469,16 @@ void PAForm::finish_shared(int i0, int i1, double *y, double *yg, hipStream_t s)
    // the plan's blocks cover the owned shared dofs [0, n_sh_owned_) then the ghost ones
    ECM2_VERIFY((i0 == 0 || i0 == n_sh_owned_) && (i1 == n_sh_owned_ || i1 == n_sh_) && i0 <= i1, ERR_INTERNAL,
                "summation range [" << i0 << ", " << i1 << ") is not a plan range");
+   if (brick_grid_.n && brick_grid_on_ && resolved_mode_ == KERNEL_LINE)
+   {
+      // (all dofs owned: the whole range is [0, n_sh_))
+      if (i0 == 0 && i1 == n_sh_)
+      {
+         kern::sum_brick_grid(D_, brick_grid_.n, brick_grid_.nbx, brick_grid_.nbxy, breg_.data(), part_.data(), y, s);
+         return;
+      }
+      if (i0 == i1) { return; }
+   }
    const int b0 = i0 == 0 ? 0 : sh_nblk_owned_, b1 = i1 == n_sh_owned_ ? sh_nblk_owned_ : sh_nblk_;
    kern::sum_partials(b0, b1, sh_blocks_.data(), sh_runs_.data(), sh_rslots_.data(), sh_pdof_.data(), part_.data(),
                       n_owned_, y, yg, s);

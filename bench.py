@@ -172,12 +172,15 @@ def bench_law_form(E, torch, mesh, fes, keep, case):
 
 def qdata_layout(E, form):
     """Quadrature-data layout of a (local) form: affine | affine_ts (AFFINE with the k(T)
-    coefficient snapshot) | affine_e | trilinear | trilinear_e | blocked | native."""
+    coefficient snapshot; affine_tsm: and the mass per element) | affine_e | affine_e_ts(m) (the p >= 3
+    bricks' snapshot) | trilinear | trilinear_e | blocked | native."""
     lay = {E.QLAYOUT_NATIVE: "native", E.QLAYOUT_BLOCKED: "blocked", E.QLAYOUT_AFFINE: "affine",
            E.QLAYOUT_AFFINE_E: "affine_e", E.QLAYOUT_TRILINEAR: "trilinear",
            E.QLAYOUT_TRILINEAR_E: "trilinear_e"}[form.info()["layout"]]
-    if lay == "affine" and hasattr(form, "CoefficientSnapshot") and form.CoefficientSnapshot():
-        lay = "affine_ts"
+    if lay in ("affine", "affine_e") and hasattr(form, "CoefficientSnapshot") and form.CoefficientSnapshot():
+        lay += "_ts"
+        if hasattr(form, "SnapshotInfo") and form.SnapshotInfo()[1] == 2:
+            lay += "m"  # the mass stored per element: no per-point stream
     return lay
 
 
@@ -381,9 +384,11 @@ def main():
                          "ecm2_pa_form_set_coefficient_snapshot); 0: W beta stored per point")
     ap.add_argument("--full-layout", type=int, default=1,
                     help="1 (N = 1): also time the full per-point qdata layout in this run (full_layout sub-object)")
-    ap.add_argument("--variants", type=int, default=1,
+    ap.add_argument("--variants", type=int, default=1, choices=[0, 1, 2],
                     help="1 (N = 1, c2/c4/c5): also time, in this run, the reference's own numbering "
-                         "(entity_numbering sub-object) and a trilinear mesh (trilinear sub-object)")
+                         "(entity_numbering sub-object), a trilinear mesh (trilinear), the drop-in configuration "
+                         "(drop_in) and the snapshot forms without a per-point stream (pennes, ex16); 2: the "
+                         "last two only")
     ap.add_argument("--numbering", choices=["structured", "entity"], default="structured",
                     help="c2/c4/c5 main line: lattice dof numbering on a lexicographic mesh (structured) or the "
                          "reference's own (entity: MakeCartesian3D's space-filling-curve element order, "
@@ -606,7 +611,7 @@ def main():
             ff, fes, variant, "same run, same mesh and numbering, per-point qdata (56 B per quadrature point: the "
                               "layout SURVEY §8(d)'s algorithmic bytes describe, so its alg_ratio is a roofline fraction)")
         del ff
-    if serial_main and args.variants and args.numbering == "structured" and args.mesh == "affine":
+    if serial_main and args.variants == 1 and args.numbering == "structured" and args.mesh == "affine":
         dl.at("entity numbering")
         me, fe_ = cartesian_space(E, nx, ny, nz_total, order, "entity", "affine")
         fv = serial_form(compress, me, fe_, "entity")
@@ -635,6 +640,7 @@ def main():
                                  "GeometricFactors::JACOBIANS array (set_jacobians, fitted to trilinear maps at "
                                  "Assemble)")
         del fv, md, fd
+    if serial_main and args.variants in (1, 2) and args.numbering == "structured" and args.mesh == "affine":
         for case, note in (("pennes", "same run, same mesh and numbering as the main line, the Pennes operator with "
                                       "both coefficients laws of one H1 temperature field: Mass(rho c + gamma dt c_b "
                                       "w_b(T), perfusion shut-off at T_stop) + Diffusion(gamma dt k(T)); the snapshot "

@@ -10,6 +10,8 @@
 // restriction.cpp:152-186) fused in.
 #include "dev_common.hpp"
 
+#include <type_traits>
+
 #include <algorithm>
 #include <cstdlib>
 
@@ -1017,48 +1019,93 @@ template <int D>
 __device__ const BrickSurfXYZ<D> kBrickSurf = BrickSurfXYZ<D>();
 
 // The summation pass of a brick grid (PAForm::brick_grid_; 2 x 2 x 1 regular bricks in
-// lexicographic brick order, nbx per row, nbxy per layer): one workgroup per brick k, one thread per
-// surface point.  A point shared across a face lies on exactly the faces its breg face mask names;
-// the brick whose shared faces through the point are all low faces (X = 0, Y = 0, Z = 0) is its
-// highest holder and finishes it: the partial slots of the holders k - dz nbxy - dy nbx - dx (the
-// point mirrored onto the neighbour's high face) summed in ascending brick order -- the run plan's
-// ascending slot order, so the sums are bitwise those of k_sum_partials -- then y stored.  Addresses
-// follow from the brick index and a constant table: the loads issue at once, with no plan reads.
-template <int D>
+// lexicographic brick order, nbx per row, nbxy per layer) over the items (brick k, surface point t),
+// t fastest.  A point shared across a face lies on exactly the faces its breg face mask names; the
+// brick whose shared faces through the point are all low faces (X = 0, Y = 0, Z = 0) is its highest
+// holder and finishes it: the partial slots of the holders k - dz nbxy - dy nbx - dx (the point
+// mirrored onto the neighbour's high face) summed in ascending brick order -- the run plan's
+// ascending slot order, so the sums are bitwise those of k_sum_partials -- then y stored.  Every
+// address follows from the item index, a constant table and the brick's breg row, and each thread
+// takes K items with all of their loads issued before any sum: the pass is bound by its
+// workgroups' rounds times one load chain (breg -> partials -> store), so it runs K times fewer
+// rounds than one item per thread (profiles/r5/ab_c5.txt).
+template <int D, int K>
 __global__ void __launch_bounds__(256)
-k_sum_brick_grid(int nbrick, int nbx, int nbxy, const int *__restrict__ breg, const double *__restrict__ part,
+k_sum_brick_grid(long nitems, int nbx, int nbxy, const int *__restrict__ breg, const double *__restrict__ part,
                  double *__restrict__ y)
 {
    constexpr int LX = 2 * D - 1, LY = LX, LZ = D, SURF = brick_surface_points(D, 1);
-   const int k = xcd_contiguous(blockIdx.x, gridDim.x);
-   if (k >= nbrick) { return; }
-   const int *r = breg + (size_t)k * 8;  // workgroup-uniform: scalar loads
-   const int base = r[0], sx = r[1], sy = r[2], sz = r[3], mask = r[4];
-   for (int t = threadIdx.x; t < SURF; t += blockDim.x)
+   const long i0 = (long)xcd_contiguous(blockIdx.x, gridDim.x) * 256 * K + threadIdx.x;
+   int cxyz[K], rb[K][5];
+#pragma unroll
+   for (int j = 0; j < K; j++)
    {
-      const int c = kBrickSurf<D>.v[t];
+      const long i = i0 + (long)j * 256;
+      const long ic = i < nitems ? i : nitems - 1;  // (clamped: every load in flight, results unused)
+      const int k = (int)(ic / SURF), t = (int)(ic % SURF);
+      cxyz[j] = kBrickSurf<D>.v[t];
+      const int *r = breg + (size_t)k * 8;
+#pragma unroll
+      for (int c = 0; c < 5; c++) { rb[j][c] = r[c]; }
+   }
+   // face points (two holders, the large majority) keep both partials in flight; edge and corner
+   // points (4 / 8 holders) are finished after them, one at a time
+   double v0[K], v1[K];
+   int st[K], dof[K];  // 0 nothing, 1 one holder... 2 face (two holders), 3 edge / corner; the dof
+#pragma unroll
+   for (int j = 0; j < K; j++)
+   {
+      const long i = i0 + (long)j * 256;
+      const int k = (int)((i < nitems ? i : nitems - 1) / SURF);
+      const int c = cxyz[j];
       const int X = c & 255, Y = (c >> 8) & 255, Z = c >> 16;
       const int f = ((X == 0) | (X == LX - 1) << 1 | (Y == 0) << 2 | (Y == LY - 1) << 3 | (Z == 0) << 4 |
-                     (Z == LZ - 1) << 5) & mask;
-      if (f == 0 || (f & 0x2a)) { continue; }  // not shared, or a higher brick holds it too
-      const int nx = f & 1, ny = (f >> 2) & 1, nz = (f >> 4) & 1;
-      double v[8];
-      int n = 0;
+                     (Z == LZ - 1) << 5) & rb[j][4];
+      // not shared, or a higher brick holds it too: nothing to do here
+      const bool own = i < nitems && f != 0 && (f & 0x2a) == 0;
+      const int nl = (f & 1) + ((f >> 2) & 1) + ((f >> 4) & 1);  // shared low faces through the point
+      dof[j] = rb[j][0] + X * rb[j][1] + Y * rb[j][2] + Z * rb[j][3];
+      st[j] = !own ? 0 : nl == 1 ? 2 : 3;
+      v0[j] = 0.0;
+      v1[j] = 0.0;
+      if (st[j] == 2)
+      {
+         // the neighbour behind the one shared low face (lower index: first in the sum)
+         const int kk = k - ((f & 16) ? nbxy : (f & 4) ? nbx : 1);
+         const int si = brick_surface_index(D, 1, (f & 1) ? LX - 1 : X, (f & 4) ? LY - 1 : Y, (f & 16) ? LZ - 1 : Z);
+         v0[j] = part[(size_t)kk * SURF + si];
+         v1[j] = part[(size_t)k * SURF + brick_surface_index(D, 1, X, Y, Z)];
+      }
+   }
 #pragma unroll
-      for (int dz = 1; dz >= 0; dz--)
+   for (int j = 0; j < K; j++)
+   {
+      if (st[j] == 2) { y[dof[j]] = v0[j] + v1[j]; }
+   }
+   // edges and corners: the holders k - dz nbxy - dy nbx - dx in ascending order (the plan's)
 #pragma unroll
-         for (int dy = 1; dy >= 0; dy--)
+   for (int j = 0; j < K; j++)
+   {
+      if (st[j] != 3) { continue; }
+      const long i = i0 + (long)j * 256;
+      const int k = (int)(i / SURF);
+      const int c = cxyz[j];
+      const int X = c & 255, Y = (c >> 8) & 255, Z = c >> 16;
+      const int f = ((X == 0) | (Y == 0) << 2 | (Z == 0) << 4) & rb[j][4];
+      double acc = 0.0;
+      bool first = true;
 #pragma unroll
-            for (int dx = 1; dx >= 0; dx--)
-            {
-               if ((dz && !nz) || (dy && !ny) || (dx && !nx)) { continue; }
-               const int kk = k - dz * nbxy - dy * nbx - dx;
-               const int si = brick_surface_index(D, 1, dx ? LX - 1 : X, dy ? LY - 1 : Y, dz ? LZ - 1 : Z);
-               v[n++] = part[(size_t)kk * SURF + si];
-            }
-      double acc = v[0];
-      for (int h = 1; h < n; h++) { acc += v[h]; }
-      y[base + X * sx + Y * sy + Z * sz] = acc;
+      for (int h = 7; h >= 0; h--)
+      {
+         const int dz = h >> 2, dy = (h >> 1) & 1, dx = h & 1;
+         if ((dz && !(f & 16)) || (dy && !(f & 4)) || (dx && !(f & 1))) { continue; }
+         const int kk = k - dz * nbxy - dy * nbx - dx;
+         const double w =
+            part[(size_t)kk * SURF + brick_surface_index(D, 1, dx ? LX - 1 : X, dy ? LY - 1 : Y, dz ? LZ - 1 : Z)];
+         acc = first ? w : acc + w;
+         first = false;
+      }
+      y[dof[j]] = acc;
    }
 }
 
@@ -1266,19 +1313,26 @@ bool has_brick(int D, int Q, int bz)
 
 int brick_points(int D, int bz) { return (2 * D - 1) * (2 * D - 1) * (bz * (D - 1) + 1); }
 
-void sum_brick_grid(int D, int nbrick, int nbx, int nbxy, const int *breg, const double *part, double *y,
+void sum_brick_grid(int D, int nbrick, int nbx, int nbxy, const int *breg, const double *part, double *y, int k_items,
                     hipStream_t s)
 {
    if (nbrick == 0) { return; }
-#define ECM2_GRID_CASE(DD)                                                                                  \
-   if (D == DD)                                                                                             \
-   {                                                                                                        \
-      hipLaunchKernelGGL((k_sum_brick_grid<DD>), dim3(nbrick), dim3(256), 0, s, nbrick, nbx, nbxy, breg, part, y); \
-      ECM2_HIP(hipGetLastError());                                                                          \
-      return;                                                                                               \
-   }
-   ECM2_GRID_CASE(4) ECM2_GRID_CASE(5) ECM2_GRID_CASE(6) ECM2_GRID_CASE(7)
-#undef ECM2_GRID_CASE
+   auto launch = [&](auto dc, auto kc) {
+      constexpr int DD = decltype(dc)::value, K = decltype(kc)::value;
+      const long n = (long)nbrick * brick_surface_points(DD, 1);
+      hipLaunchKernelGGL((k_sum_brick_grid<DD, K>), dim3((unsigned)((n + 256 * K - 1) / (256 * K))), dim3(256), 0, s, n,
+                         nbx, nbxy, breg, part, y);
+      ECM2_HIP(hipGetLastError());
+   };
+   auto by_k = [&](auto dc) {
+      if (k_items >= 8) { launch(dc, std::integral_constant<int, 8>()); }
+      else if (k_items >= 4) { launch(dc, std::integral_constant<int, 4>()); }
+      else { launch(dc, std::integral_constant<int, 2>()); }
+   };
+   if (D == 4) { by_k(std::integral_constant<int, 4>()); return; }
+   if (D == 5) { by_k(std::integral_constant<int, 5>()); return; }
+   if (D == 6) { by_k(std::integral_constant<int, 6>()); return; }
+   if (D == 7) { by_k(std::integral_constant<int, 7>()); return; }
    ECM2_VERIFY(false, ERR_UNSUPPORTED, "no brick-grid summation for D1D=" << D);
 }
 
@@ -1340,6 +1394,11 @@ void diagonal(const int *pos, int D, int Q, int layout, int ne, const int *gm, c
       ECM2_DIAG_CASE(3, 3)
       ECM2_DIAG_CASE(4, 4)
       ECM2_DIAG_CASE(5, 5)
+      ECM2_DIAG_CASE(2, 4)
+      ECM2_DIAG_CASE(3, 5)
+      ECM2_DIAG_CASE(4, 6)
+      ECM2_DIAG_CASE(5, 7)
+      ECM2_DIAG_CASE(6, 8)
    }
 #undef ECM2_DIAG_CASE
    diagonal_generic(pos, D, Q, layout, ne, gm, qdd, qdm, diag, out_e, b, s);

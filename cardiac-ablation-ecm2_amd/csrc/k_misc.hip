@@ -502,6 +502,13 @@ void apply_wpe(int D, int Q, bool mass, bool diff, const ApplyArgs &a, bool in_e
    ECM2_WPE_CASE(4, 4)
    ECM2_WPE_CASE(5, 5)
    ECM2_WPE_CASE(6, 7)
+   // Q1D = D1D + 2: the rule a quadratic mesh's MassIntegrator asks for (GetRule adds Trans.OrderW(),
+   // bilininteg.cpp:1450-1462), or a user rule (IntRule)
+   ECM2_WPE_CASE(2, 4)
+   ECM2_WPE_CASE(3, 5)
+   ECM2_WPE_CASE(4, 6)
+   ECM2_WPE_CASE(5, 7)
+   ECM2_WPE_CASE(6, 8)
 #undef ECM2_WPE_CASE
    ECM2_VERIFY(false, ERR_UNSUPPORTED, "no PA kernel for D1D=" << D << " Q1D=" << Q);
 }

@@ -453,7 +453,7 @@ void sum_partials(int b0, int b1, const int *blocks, const int *runs, const int 
 // per brick and surface point, the highest holder sums the partial slots of the point's holders
 // (itself and its -x / -y / -z neighbours k - 1, k - nbx, k - nbxy) in ascending brick order and
 // stores y; no plan, no dependent reads.  breg [nbrick][8], part [nbrick][surface].
-void sum_brick_grid(int D, int nbrick, int nbx, int nbxy, const int *breg, const double *part, double *y,
+void sum_brick_grid(int D, int nbrick, int nbx, int nbxy, const int *breg, const double *part, double *y, int k_items,
                     hipStream_t s);
 } // namespace kern
 

@@ -35,7 +35,8 @@ PAForm::PAForm(int ne, int order, int ndofs, const int *gather_map_host, int q1d
    require_device();
    D_ = order + 1;
    Q_ = q1d > 0 ? q1d : default_q1d(order);
-   if (const char *g = std::getenv("ECM2_SUM_GRID")) { brick_grid_on_ = std::atoi(g) != 0; }
+   if (const char *g = std::getenv("ECM2_SUM_GRID")) { brick_grid_k_ = std::atoi(g); }
+   if (const char *g = std::getenv("ECM2_BRICK_TS")) { brick_ts_ = std::atoi(g); }
    ECM2_VERIFY(Q_ >= D_ && Q_ <= MAX_Q1D, ERR_ARG, "q1d must satisfy p+1 <= q1d <= " << MAX_Q1D);
    ND_ = D_ * D_ * D_;
    NQ_ = Q_ * Q_ * Q_;
@@ -1172,7 +1173,13 @@ void PAForm::assemble(hipStream_t s)
                        (treg_all_ || tlat_all_);
    const bool ts_brick = layout_.kind == QLAYOUT_AFFINE_E && resolved_mode_ == KERNEL_LINE && n_bricks_ > 0 &&
                          n_left_ == 0 && brick_bz_ == 1 && D_ <= 6 && Q_ == D_ + 1 && have_mass_ && use_partials();
-   if (tsnap_pref_ && (ts_tpe || ts_brick) && have_diff_ && cdiff_.gridfunc() && cdiff_.lvec &&
+   // (the bricks take it only when it removes the whole per-point stream: with W alpha det J still
+   // streamed, the T images' extra stage work and barrier cost more than the 8 B per point save,
+   // profiles/r5/ab_c5.txt)
+   const bool mass_elem = have_mass_ && (cmass_.kind == COEFF_CONSTANT ||
+                                         (cmass_.gridfunc() && cmass_.lvec == cdiff_.lvec));
+   const bool ts_brick_ok = ts_brick && (brick_ts_ == 2 || (brick_ts_ == 1 && mass_elem));
+   if (tsnap_pref_ && (ts_tpe || ts_brick_ok) && have_diff_ && cdiff_.gridfunc() && cdiff_.lvec &&
        !marked_[INTEG_DIFFUSION])
    {
       layout_.tsnap = 1;
@@ -1191,7 +1198,7 @@ void PAForm::assemble(hipStream_t s)
          A = cdiff_.scale * (1.0 - cdiff_.slope * cdiff_.t_ref);
          B = cdiff_.scale * cdiff_.slope;
       }
-      if (ts_brick || treg_all_)
+      if (ts_brick_ok || treg_all_)
       {
          tsnap_.resize(std::max(1, ndofs_));
          kern::affine_snapshot(ndofs_, cdiff_.lvec, A, B, tsnap_.data(), s);
@@ -1469,12 +1476,13 @@ void PAForm::finish_shared(int i0, int i1, double *y, double *yg, hipStream_t s)
    // the plan's blocks cover the owned shared dofs [0, n_sh_owned_) then the ghost ones
    ECM2_VERIFY((i0 == 0 || i0 == n_sh_owned_) && (i1 == n_sh_owned_ || i1 == n_sh_) && i0 <= i1, ERR_INTERNAL,
                "summation range [" << i0 << ", " << i1 << ") is not a plan range");
-   if (brick_grid_.n && brick_grid_on_ && resolved_mode_ == KERNEL_LINE)
+   if (brick_grid_.n && brick_grid_k_ > 0 && resolved_mode_ == KERNEL_LINE)
    {
       // (all dofs owned: the whole range is [0, n_sh_))
       if (i0 == 0 && i1 == n_sh_)
       {
-         kern::sum_brick_grid(D_, brick_grid_.n, brick_grid_.nbx, brick_grid_.nbxy, breg_.data(), part_.data(), y, s);
+         kern::sum_brick_grid(D_, brick_grid_.n, brick_grid_.nbx, brick_grid_.nbxy, breg_.data(), part_.data(), y,
+                              brick_grid_k_, s);
          return;
       }
       if (i0 == i1) { return; }

@@ -64,6 +64,12 @@ def test_bench_single_gpu_line():
     assert b["entity_numbering"]["value"] > 0 and b["entity_numbering"]["qdata_layout"] == "affine_ts"
     assert b["trilinear"]["value"] > 0 and b["trilinear"]["qdata_layout"] == "trilinear"
     assert b["drop_in"]["value"] > 0 and b["drop_in"]["qdata_layout"] == "trilinear"
+    # the snapshot forms without a per-point stream: the Pennes operator (both laws of one field) and
+    # ex16p's M + dt K(u_alpha_gf)
+    assert b["pennes"]["snapshot"] == {"on": True, "mass_values": 2, "law_at_point": True}
+    assert b["ex16"]["snapshot"] == {"on": True, "mass_values": 2, "law_at_point": False}
+    assert b["pennes"]["qdata_layout"] == b["ex16"]["qdata_layout"] == "affine_tsm"
+    assert b["pennes"]["roofline"]["traffic"] is None and b["pennes"]["value"] > 0
     s = run_bench(*SMALL, "--variants", "0", "--coefficient-snapshot", "0")
     assert s["value"] > 0 and "entity_numbering" not in s
     assert b["config"]["qdata_layout"] == "affine_ts" and s["config"]["qdata_layout"] == "affine"

@@ -10,8 +10,6 @@
 // restriction.cpp:152-186) fused in.
 #include "dev_common.hpp"
 
-#include <type_traits>
-
 #include <algorithm>
 #include <cstdlib>
 
@@ -539,23 +537,14 @@ constexpr int brick_wpe()
    constexpr int W = BrickShapeC<D, Q, BZ>::WPE;
    return (G == 2 && W > 3) ? 3 : W;
 }
-// TS (round 5, AFFINE_E only): the coefficient snapshot (kernels.hpp QLayout::tsnap) -- the diffusion
-// coefficient's field T is gathered beside x (the same addressing), interpolated at the quadrature
-// points through the same five stages with B only (its x image parks in sYQ until the y stage has
-// read it, its y image in sXL until the z stage has: no extra LDS, one more barrier), and
-// W beta = W_q law(T(x_q)) is formed at the point (LAW: the law applied there, else folded into the
-// snapshot's dofs).  TS 1: W alpha det J streamed per point (8 B instead of the 16-B pair); TS 2: one
-// value per element, (c alpha) det J, times W_q [law_m(T(x_q))]: no per-point stream.
-template <int D, int Q, int BZ, bool SPLIT, int G, bool REG, int TS = 0, bool LAW = false>
+template <int D, int Q, int BZ, bool SPLIT, int G, bool REG>
 __global__ void __launch_bounds__((BrickShapeC<D, Q, BZ>::NT), (brick_wpe<D, Q, BZ, G>()))
 k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int *__restrict__ bmap,
                 const int *__restrict__ breg, int n_owned, const double *__restrict__ qdd,
                 const double *__restrict__ qdm, const double *__restrict__ x, const double *__restrict__ xg,
                 double *__restrict__ y, double *__restrict__ yg, const Basis1D *__restrict__ btab,
-                double *__restrict__ part, const QPts qp, const double *__restrict__ tsn, const QPts qw,
-                const PointLaw law_d, const PointLaw law_m)
+                double *__restrict__ part, const QPts qp)
 {
-   static_assert(TS == 0 || G == 1, "the coefficient snapshot runs on AFFINE_E");
    constexpr bool AFF = G != 0;  // a compressed layout: point pairs + per-element data
    using S = BrickShapeC<D, Q, BZ>;
    constexpr int NE = S::NE, DD = S::DD, QQ = S::QQ, DQ = S::DQ, SA = S::SA, SB = S::SB, DS = S::DS;
@@ -594,18 +583,14 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
    const int eLc = eL < NE ? eL : NE - 1, lLc = lL < DD ? lL : DD - 1;
    const int e = belem[(size_t)k * NE + (e3 < NE ? e3 : NE - 1)];
    const int l3c = l3 < QQ ? l3 : QQ - 1;
-   double xl[D], tl[D];
+   double xl[D];
    {
       const int dy = lLc % D, dz = lLc / D, ex = eLc & 1, ey = (eLc >> 1) & 1, ez = eLc >> 2;
       if (REG)
       {
          const int d0 = base + (ex * (D - 1)) * sx + (ey * (D - 1) + dy) * sy + (ez * (D - 1) + dz) * sz;
 #pragma unroll
-         for (int dx = 0; dx < D; dx++)
-         {
-            xl[dx] = x[d0 + dx * sx];
-            if (TS) { tl[dx] = tsn[d0 + dx * sx]; }
-         }
+         for (int dx = 0; dx < D; dx++) { xl[dx] = x[d0 + dx * sx]; }
       }
       else
       {
@@ -615,28 +600,14 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
          {
             const int d = bdof(mp[dx]);
             xl[dx] = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
-            if (TS) { tl[dx] = tsn[d]; }  // (the snapshot: the whole local L-vector, contiguous)
          }
       }
    }
    __builtin_amdgcn_sched_barrier(0);  // keep the gather ahead of the qdata loads
    double qv[7][Q];
    v2d pa[Q];
-   double pm[Q];        // TS 1: W alpha det J of this lane's column
-   double mel = 0.0;    // TS 2: the element's (c alpha) det J
    double cc[6];
-   if (TS)
-   {
-      if (TS == 1)
-      {
-#pragma unroll
-         for (int qz = 0; qz < Q; qz++) { pm[qz] = __builtin_nontemporal_load(qdm + (size_t)e * NQ + qz * QQ + l3c); }
-      }
-      else { mel = qdm[e]; }
-#pragma unroll
-      for (int c = 0; c < 6; c++) { cc[c] = qdd[(size_t)e * 6 + c]; }
-   }
-   else if (AFF)
+   if (AFF)
    {
       // the point pairs are streamed once per Mult: nontemporal, so they do not evict the x lines
       // neighbouring bricks gather again (profiles/r3_ab_bnt.txt: kernel -1%, Mult -2%)
@@ -665,42 +636,27 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
          o[qx * DD] = u[qx];
          o[Q * DD + qx * DD] = v[qx];
       }
-      if (TS)
-      {
-         // T's x image [qx][dz][dy] parks in sYQ (free until the y stage writes it)
-         double te_[NEO], to_[NOO], tu[Q];
-         eo_split<D>(tl, te_, to_);
-         eo_fwd_b<D, Q>(te, te_, to_, tu);
-#pragma unroll
-         for (int qx = 0; qx < Q; qx++) { sYQ[eL * SB + qx * DD + lL] = tu[qx]; }
-      }
    }
    if (k_begin < 0)  // never: a use outside the x stage stops the gather sinking behind the qdata
    {
       double u = 0.0;
 #pragma unroll
-      for (int dx = 0; dx < D; dx++) { u += xl[dx]; if (TS) { u += tl[dx]; } }
+      for (int dx = 0; dx < D; dx++) { u += xl[dx]; }
       part[t] = u;
    }
    __syncthreads();
    // ---- lanes (element, qx, dz), l2 = qx + Q dz: contract in y -> sYQ [g][dz][qy][qx]
-   double la[D], lb[D], lt[D];
    if (act2)
    {
       const int qx = lL % Q, dz = lL / Q;
       const double *in = sXL + eL * SA + qx * DD + dz * D;
+      double la[D], lb[D];
 #pragma unroll
       for (int dy = 0; dy < D; dy++)
       {
          la[dy] = lds_read(in + dy);
          lb[dy] = lds_read(in + Q * DD + dy);
-         if (TS) { lt[dy] = lds_read(sYQ + eL * SB + qx * DD + dz * D + dy); }
       }
-   }
-   if (TS) { __syncthreads(); }  // every lane has read T's x image (sYQ) and the x images (sXL)
-   if (act2)
-   {
-      const int qx = lL % Q, dz = lL / Q;
       double *o = sYQ + eL * SB + dz * DS + qx;
       CBasisEO *te = stage_eo(btab);
       double ae[NEO], ao[NOO], be[NEO], bo[NOO], gb[Q], bg[Q], bb[Q];
@@ -716,31 +672,20 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
          o[D * DS + qy * Q] = bg[qy];
          o[2 * D * DS + qy * Q] = bb[qy];
       }
-      if (TS)
-      {
-         // T's y image [dz][qy][qx] into sXL (read by the z stage before the x transposes overwrite it)
-         double te_[NEO], to_[NOO], ty[Q];
-         eo_split<D>(lt, te_, to_);
-         eo_fwd_b<D, Q>(te, te_, to_, ty);
-#pragma unroll
-         for (int qy = 0; qy < Q; qy++) { sXL[eL * SA + dz * QQ + qy * Q + qx] = ty[qy]; }
-      }
    }
    __syncthreads();
    // ---- lanes (element, qx, qy): contract in z, weight, transpose in z (in place)
    if (act3)
    {
       double *io = sYQ + e3 * SB + l3;
-      double l0[D], l1[D], l2[D], lz[D];
+      double l0[D], l1[D], l2[D];
 #pragma unroll
       for (int dz = 0; dz < D; dz++)
       {
          l0[dz] = lds_read(io + dz * DS);
          l1[dz] = lds_read(io + D * DS + dz * DS);
          l2[dz] = lds_read(io + 2 * D * DS + dz * DS);
-         if (TS) { lz[dz] = lds_read(sXL + e3 * SA + dz * QQ + l3); }
       }
-      const double wxy = TS ? qw.x[l3 % Q] * qw.x[l3 / Q] : 0.0;  // W_q = w_qx w_qy w_qz
       // TRILINEAR_E: the column's Jacobian pieces, J[i][0] = a0 + b0 zeta, J[i][1] = a1 + b1 zeta,
       // J[i][2] = j2 (dev_common.hpp trilinear_jacobian at xi = x_qx, eta = x_qy)
       double a0[3], b0[3], a1[3], b1[3], j2[3];
@@ -760,19 +705,10 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
             j2[i] = (c[6 + i] + c[12 + i] * xi) + b1[i] * et;
          }
       }
-      // the quadrature-point operator: (f, m) = (W beta C grad u, W alpha det J u) at qz; tq: T(x_q) (TS)
-      auto qpoint = [&](int qz, double gx, double gy, double gz, double u, double tq, double &fx, double &fy,
-                        double &fz, double &m) {
-         if (TS)
-         {
-            const double Wq = wxy * qw.x[qz];
-            const double wb = Wq * (LAW ? point_law(law_d, tq) : tq);
-            fx = wb * (cc[0] * gx + cc[1] * gy + cc[2] * gz);
-            fy = wb * (cc[1] * gx + cc[3] * gy + cc[4] * gz);
-            fz = wb * (cc[2] * gx + cc[4] * gy + cc[5] * gz);
-            m = (TS == 1 ? pm[qz] : Wq * mel * (LAW ? point_law(law_m, tq) : 1.0)) * u;
-         }
-         else if (G == 2)
+      // the quadrature-point operator: (f, m) = (W beta C grad u, W alpha det J u) at qz
+      auto qpoint = [&](int qz, double gx, double gy, double gz, double u, double &fx, double &fy, double &fz,
+                        double &m) {
+         if (G == 2)
          {
             // f = (W beta / det J) adj(J) (adj(J)^T g), adj(J) from J at (x_qx, x_qy, x_qz)
             const double zt = qp.x[qz];
@@ -814,11 +750,10 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
       // rows qz and Q-1-qz together: forward split contractions, the operator at both points, the
       // transposed contractions accumulated into split sums
       CBasisEO *te = stage_eo(btab);
-      double e0[NEO], o0[NOO], e1[NEO], o1[NOO], e2[NEO], o2[NOO], eT[NEO], oT[NOO];
+      double e0[NEO], o0[NOO], e1[NEO], o1[NOO], e2[NEO], o2[NOO];
       eo_split<D>(l0, e0, o0);
       eo_split<D>(l1, e1, o1);
       eo_split<D>(l2, e2, o2);
-      if (TS) { eo_split<D>(lz, eT, oT); }
       double A1E[NEO], A1O[NOO], A2E[NEO], A2O[NOO], A3E[NEO], A3O[NOO];
       eo_zero<D>(A1E, A1O);
       eo_zero<D>(A2E, A2O);
@@ -828,7 +763,7 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
       {
          const int qr = Q - 1 - qp;
          const bool mid = qr == qp;
-         double sx_ = 0.0, sy_ = 0.0, su = 0.0, sg = 0.0, ax = 0.0, ay = 0.0, au = 0.0, ag = 0.0, st = 0.0, at = 0.0;
+         double sx_ = 0.0, sy_ = 0.0, su = 0.0, sg = 0.0, ax = 0.0, ay = 0.0, au = 0.0, ag = 0.0;
 #pragma unroll
          for (int i = 0; i < NEO; i++)
          {
@@ -836,7 +771,6 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
             sx_ += b * e0[i];
             sy_ += b * e1[i];
             su += b * e2[i];
-            if (TS) { st += b * eT[i]; }
             if (!mid) { ag += te->GP[qp + MQ * i] * e2[i]; }
          }
 #pragma unroll
@@ -849,11 +783,10 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
                ax += b * o0[i];
                ay += b * o1[i];
                au += b * o2[i];
-               if (TS) { at += b * oT[i]; }
             }
          }
          double fxp, fyp, fzp, mp;
-         qpoint(qp, sx_ + ax, sy_ + ay, sg + ag, su + au, st + at, fxp, fyp, fzp, mp);
+         qpoint(qp, sx_ + ax, sy_ + ay, sg + ag, su + au, fxp, fyp, fzp, mp);
          if (mid)
          {
 #pragma unroll
@@ -870,7 +803,7 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
          else
          {
             double fxr, fyr, fzr, mr;
-            qpoint(qr, sx_ - ax, sy_ - ay, sg - ag, su - au, st - at, fxr, fyr, fzr, mr);
+            qpoint(qr, sx_ - ax, sy_ - ay, sg - ag, su - au, fxr, fyr, fzr, mr);
             const double fxe = fxp + fxr, fxo = fxp - fxr, fye = fyp + fyr, fyo = fyp - fyr;
             const double fze = fzp + fzr, fzo = fzp - fzr, me = mp + mr, mo = mp - mr;
 #pragma unroll
@@ -994,118 +927,6 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
       }
       if (!shared) { *((!SPLIT || d < n_owned) ? y + d : yg + (d - n_owned)) = v; }
       else { part[(size_t)k * S::SURF + pw[i][NW - 1]] = v; }  // surface only (setup)
-   }
-}
-
-// Surface points of a 2 x 2 x 1 brick in partial-slot order (brick_surface_index inverted):
-// X | Y << 8 | Z << 16.
-template <int D>
-struct BrickSurfXYZ
-{
-   static constexpr int LX = 2 * D - 1, LY = LX, LZ = D, N = brick_surface_points(D, 1);
-   int v[N];
-   constexpr BrickSurfXYZ() : v()
-   {
-      for (int Z = 0; Z < LZ; Z++)
-         for (int Y = 0; Y < LY; Y++)
-            for (int X = 0; X < LX; X++)
-            {
-               const int si = brick_surface_index(D, 1, X, Y, Z);
-               if (si >= 0) { v[si] = X | Y << 8 | Z << 16; }
-            }
-   }
-};
-template <int D>
-__device__ const BrickSurfXYZ<D> kBrickSurf = BrickSurfXYZ<D>();
-
-// The summation pass of a brick grid (PAForm::brick_grid_; 2 x 2 x 1 regular bricks in
-// lexicographic brick order, nbx per row, nbxy per layer) over the items (brick k, surface point t),
-// t fastest.  A point shared across a face lies on exactly the faces its breg face mask names; the
-// brick whose shared faces through the point are all low faces (X = 0, Y = 0, Z = 0) is its highest
-// holder and finishes it: the partial slots of the holders k - dz nbxy - dy nbx - dx (the point
-// mirrored onto the neighbour's high face) summed in ascending brick order -- the run plan's
-// ascending slot order, so the sums are bitwise those of k_sum_partials -- then y stored.  Every
-// address follows from the item index, a constant table and the brick's breg row, and each thread
-// takes K items with all of their loads issued before any sum: the pass is bound by its
-// workgroups' rounds times one load chain (breg -> partials -> store), so it runs K times fewer
-// rounds than one item per thread (profiles/r5/ab_c5.txt).
-template <int D, int K>
-__global__ void __launch_bounds__(256)
-k_sum_brick_grid(long nitems, int nbx, int nbxy, const int *__restrict__ breg, const double *__restrict__ part,
-                 double *__restrict__ y)
-{
-   constexpr int LX = 2 * D - 1, LY = LX, LZ = D, SURF = brick_surface_points(D, 1);
-   const long i0 = (long)xcd_contiguous(blockIdx.x, gridDim.x) * 256 * K + threadIdx.x;
-   int cxyz[K], rb[K][5];
-#pragma unroll
-   for (int j = 0; j < K; j++)
-   {
-      const long i = i0 + (long)j * 256;
-      const long ic = i < nitems ? i : nitems - 1;  // (clamped: every load in flight, results unused)
-      const int k = (int)(ic / SURF), t = (int)(ic % SURF);
-      cxyz[j] = kBrickSurf<D>.v[t];
-      const int *r = breg + (size_t)k * 8;
-#pragma unroll
-      for (int c = 0; c < 5; c++) { rb[j][c] = r[c]; }
-   }
-   // face points (two holders, the large majority) keep both partials in flight; edge and corner
-   // points (4 / 8 holders) are finished after them, one at a time
-   double v0[K], v1[K];
-   int st[K], dof[K];  // 0 nothing, 1 one holder... 2 face (two holders), 3 edge / corner; the dof
-#pragma unroll
-   for (int j = 0; j < K; j++)
-   {
-      const long i = i0 + (long)j * 256;
-      const int k = (int)((i < nitems ? i : nitems - 1) / SURF);
-      const int c = cxyz[j];
-      const int X = c & 255, Y = (c >> 8) & 255, Z = c >> 16;
-      const int f = ((X == 0) | (X == LX - 1) << 1 | (Y == 0) << 2 | (Y == LY - 1) << 3 | (Z == 0) << 4 |
-                     (Z == LZ - 1) << 5) & rb[j][4];
-      // not shared, or a higher brick holds it too: nothing to do here
-      const bool own = i < nitems && f != 0 && (f & 0x2a) == 0;
-      const int nl = (f & 1) + ((f >> 2) & 1) + ((f >> 4) & 1);  // shared low faces through the point
-      dof[j] = rb[j][0] + X * rb[j][1] + Y * rb[j][2] + Z * rb[j][3];
-      st[j] = !own ? 0 : nl == 1 ? 2 : 3;
-      v0[j] = 0.0;
-      v1[j] = 0.0;
-      if (st[j] == 2)
-      {
-         // the neighbour behind the one shared low face (lower index: first in the sum)
-         const int kk = k - ((f & 16) ? nbxy : (f & 4) ? nbx : 1);
-         const int si = brick_surface_index(D, 1, (f & 1) ? LX - 1 : X, (f & 4) ? LY - 1 : Y, (f & 16) ? LZ - 1 : Z);
-         v0[j] = part[(size_t)kk * SURF + si];
-         v1[j] = part[(size_t)k * SURF + brick_surface_index(D, 1, X, Y, Z)];
-      }
-   }
-#pragma unroll
-   for (int j = 0; j < K; j++)
-   {
-      if (st[j] == 2) { y[dof[j]] = v0[j] + v1[j]; }
-   }
-   // edges and corners: the holders k - dz nbxy - dy nbx - dx in ascending order (the plan's)
-#pragma unroll
-   for (int j = 0; j < K; j++)
-   {
-      if (st[j] != 3) { continue; }
-      const long i = i0 + (long)j * 256;
-      const int k = (int)(i / SURF);
-      const int c = cxyz[j];
-      const int X = c & 255, Y = (c >> 8) & 255, Z = c >> 16;
-      const int f = ((X == 0) | (Y == 0) << 2 | (Z == 0) << 4) & rb[j][4];
-      double acc = 0.0;
-      bool first = true;
-#pragma unroll
-      for (int h = 7; h >= 0; h--)
-      {
-         const int dz = h >> 2, dy = (h >> 1) & 1, dx = h & 1;
-         if ((dz && !(f & 16)) || (dy && !(f & 4)) || (dx && !(f & 1))) { continue; }
-         const int kk = k - dz * nbxy - dy * nbx - dx;
-         const double w =
-            part[(size_t)kk * SURF + brick_surface_index(D, 1, dx ? LX - 1 : X, dy ? LY - 1 : Y, dz ? LZ - 1 : Z)];
-         acc = first ? w : acc + w;
-         first = false;
-      }
-      y[dof[j]] = acc;
    }
 }
 
@@ -1235,32 +1056,11 @@ void launch_brick(const ApplyArgs &a, hipStream_t s)
    ECM2_VERIFY(a.part_brick, ERR_INTERNAL, "brick kernel needs its partial slots");
    const bool split = a.xg || a.yg;
    const int g = a.kind == QLAYOUT_AFFINE_E ? 1 : a.kind == QLAYOUT_TRILINEAR_E ? 2 : 0;
-   ECM2_VERIFY(g == 0 || a.pw == 2 || a.tsnap, ERR_INTERNAL, "bricks need both integrators");
+   ECM2_VERIFY(g == 0 || a.pw == 2, ERR_INTERNAL, "bricks need both integrators");
    const dim3 grid(k1 - k0), block(BrickShapeC<D, Q, BZ>::NT);
-   QPts qw = {};
-   for (int q = 0; q < MAX_Q1D; q++) { qw.x[q] = a.qw[q]; }
-#define ECM2_BRICK_TS(SP, GG, RG, TS, LW)                                                                  \
-   hipLaunchKernelGGL((k_apply_brick_c<D, Q, BZ, SP, GG, RG, TS, LW>), grid, block, 0, s, k0, k1, a.belem,     \
-                      a.bmap, a.breg, a.n_owned, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, a.btab, a.part_brick, a.qp,  \
-                      a.tsnap, qw, a.law_d, a.law_m)
-   if constexpr (BZ == 1 && D <= 6)
-   {
-      if (a.tsnap)
-      {
-         ECM2_VERIFY(g == 1 && a.tsnap_kind == 1 && (a.tmass == 1 || a.tmass == 2) && a.pw == (a.tmass == 1 ? 1 : 0),
-                     ERR_INTERNAL, "brick coefficient snapshot: AFFINE_E, dof-ordered, both integrators");
-#define ECM2_BRICK_TSM(SP, RG)                                                        \
-   if (a.tmass == 1) { if (a.tlaw) { ECM2_BRICK_TS(SP, 1, RG, 1, true); } else { ECM2_BRICK_TS(SP, 1, RG, 1, false); } } \
-   else { if (a.tlaw) { ECM2_BRICK_TS(SP, 1, RG, 2, true); } else { ECM2_BRICK_TS(SP, 1, RG, 2, false); } }
-         if (split) { ECM2_BRICK_TSM(true, false) }
-         else if (a.breg) { ECM2_BRICK_TSM(false, true) }
-         else { ECM2_BRICK_TSM(false, false) }
-#undef ECM2_BRICK_TSM
-         return;
-      }
-   }
-   ECM2_VERIFY(!a.tsnap, ERR_INTERNAL, "no brick snapshot kernel for D1D=" << D << " bz=" << BZ);
-#define ECM2_BRICK(SP, GG, RG) ECM2_BRICK_TS(SP, GG, RG, 0, false)
+#define ECM2_BRICK(SP, GG, RG)                                                                             \
+   hipLaunchKernelGGL((k_apply_brick_c<D, Q, BZ, SP, GG, RG>), grid, block, 0, s, k0, k1, a.belem, a.bmap,    \
+                      a.breg, a.n_owned, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, a.btab, a.part_brick, a.qp)
 #define ECM2_BRICK_G(SP, RG)                    \
    if (g == 1) { ECM2_BRICK(SP, 1, RG); }       \
    else if (g == 2) { ECM2_BRICK(SP, 2, RG); }  \
@@ -1270,7 +1070,6 @@ void launch_brick(const ApplyArgs &a, hipStream_t s)
    else { ECM2_BRICK_G(false, false) }
 #undef ECM2_BRICK_G
 #undef ECM2_BRICK
-#undef ECM2_BRICK_TS
 }
 
 void apply_brick(int D, int Q, const ApplyArgs &a, hipStream_t s)
@@ -1312,29 +1111,6 @@ bool has_brick(int D, int Q, int bz)
 }
 
 int brick_points(int D, int bz) { return (2 * D - 1) * (2 * D - 1) * (bz * (D - 1) + 1); }
-
-void sum_brick_grid(int D, int nbrick, int nbx, int nbxy, const int *breg, const double *part, double *y, int k_items,
-                    hipStream_t s)
-{
-   if (nbrick == 0) { return; }
-   auto launch = [&](auto dc, auto kc) {
-      constexpr int DD = decltype(dc)::value, K = decltype(kc)::value;
-      const long n = (long)nbrick * brick_surface_points(DD, 1);
-      hipLaunchKernelGGL((k_sum_brick_grid<DD, K>), dim3((unsigned)((n + 256 * K - 1) / (256 * K))), dim3(256), 0, s, n,
-                         nbx, nbxy, breg, part, y);
-      ECM2_HIP(hipGetLastError());
-   };
-   auto by_k = [&](auto dc) {
-      if (k_items >= 8) { launch(dc, std::integral_constant<int, 8>()); }
-      else if (k_items >= 4) { launch(dc, std::integral_constant<int, 4>()); }
-      else { launch(dc, std::integral_constant<int, 2>()); }
-   };
-   if (D == 4) { by_k(std::integral_constant<int, 4>()); return; }
-   if (D == 5) { by_k(std::integral_constant<int, 5>()); return; }
-   if (D == 6) { by_k(std::integral_constant<int, 6>()); return; }
-   if (D == 7) { by_k(std::integral_constant<int, 7>()); return; }
-   ECM2_VERIFY(false, ERR_UNSUPPORTED, "no brick-grid summation for D1D=" << D);
-}
 
 void apply_line(int D, int Q, bool mass, bool diff, const ApplyArgs &a, hipStream_t s)
 {

@@ -419,7 +419,7 @@ k_setup_affine(const int *__restrict__ perm, int ne, const double *__restrict__ 
    {
       // (snapshot with the mass value per element, QLayout::tmass 2: the constant coefficient, or 1
       // when the kernel evaluates the mass law, times det J and the marker weight)
-      if (tsnap && tmass == 2 && cm.has) { qd_pair[BLOCKED ? (size_t)blk * 64 + lane : (size_t)e] = coef_at(cm, eq, e) * detJ; }
+      if (BLOCKED && tsnap && tmass == 2 && cm.has) { qd_pair[(size_t)blk * 64 + lane] = coef_at(cm, eq, e) * detJ; }
       const double A11 = (J22 * J33) - (J23 * J32);
       const double A12 = (J32 * J13) - (J12 * J33);
       const double A13 = (J12 * J23) - (J22 * J13);
@@ -760,22 +760,6 @@ __global__ void __launch_bounds__(256) k_lattice_to_dofs(long n, const int *__re
 // D(q) = W_q beta_q C_e with beta_q the snapshot's law at the point (caller order [e][q]) and the stored
 // element matrices C_e; the mass W alpha det J as stored per point (tmass 1) or W_q (alpha_q | 1) times
 // the stored per-element (c alpha) det J (tmass 2; alpha_q null: a constant, folded in).
-// AFFINE_E (p >= 3 bricks) -> NATIVE ([e][6][NQ], [e][NQ]): threads over (e, q).
-__global__ void __launch_bounds__(256)
-k_tsnap_expand_e(int ne, int NQ, const double *__restrict__ W, const double *__restrict__ qd_fac,
-                 const double *__restrict__ qd_m, int tmass, const double *__restrict__ beta_q,
-                 const double *__restrict__ alpha_q, double *__restrict__ qd_diff, double *__restrict__ qd_mass)
-{
-   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-   if (t >= (long)ne * NQ) { return; }
-   const int e = (int)(t / NQ), q = (int)(t % NQ);
-   const size_t eq = (size_t)e * NQ + q;
-   const double wb = W[q] * beta_q[eq];
-   for (int k = 0; k < 6; k++) { qd_diff[((size_t)e * 6 + k) * NQ + q] = wb * qd_fac[(size_t)e * 6 + k]; }
-   if (tmass == 0) { return; }
-   qd_mass[eq] = tmass == 1 ? qd_m[eq] : W[q] * (alpha_q ? alpha_q[eq] : 1.0) * qd_m[e];
-}
-
 template <int Q>
 __global__ void __launch_bounds__(256)
 k_tsnap_expand(const int *__restrict__ perm, int ne, const double *__restrict__ W, const double *__restrict__ qd_fac,
@@ -863,8 +847,6 @@ k_scale_elements(int kind, int ne, int NQ, int pw, int tsnap, int tmass, const i
       {
          if (q == 0) { for (int k = 0; k < 6; k++) { qdd[(size_t)e * 6 + k] *= wt; } }
       }
-      else if (tsnap && tmass == 2) { if (q == 0) { qdm[e] *= wt; } }
-      else if (tsnap && pw == 1) { qdm[eq] *= wt; }
       else if (pw == 2) { qdm[eq * 2 + 1] *= wt; }
       break;
    case QLAYOUT_TRILINEAR:
@@ -961,17 +943,7 @@ void setup_from_nodes(const QLayout &L, int Q, const double *enodes, const doubl
 void tsnap_expand(const QLayout &L, int Q, const double *W, const double *qd_fac, const double *qd_m,
                   const double *beta_q, const double *alpha_q, double *qd_diff, double *qd_mass, hipStream_t s)
 {
-   ECM2_VERIFY(L.tsnap && ((L.kind == QLAYOUT_AFFINE && Q == 4) || L.kind == QLAYOUT_AFFINE_E), ERR_INTERNAL,
-               "snapshot expansion: AFFINE p = 2 or AFFINE_E");
-   if (L.kind == QLAYOUT_AFFINE_E)
-   {
-      const long ne_q = (long)L.ne * L.nq;
-      if (ne_q == 0) { return; }
-      hipLaunchKernelGGL(k_tsnap_expand_e, dim3(grid_for(ne_q, 256)), dim3(256), 0, s, L.ne, L.nq, W, qd_fac, qd_m,
-                         L.tmass, beta_q, alpha_q, qd_diff, qd_mass);
-      ECM2_HIP(hipGetLastError());
-      return;
-   }
+   ECM2_VERIFY(L.kind == QLAYOUT_AFFINE && L.tsnap && Q == 4, ERR_INTERNAL, "snapshot expansion: AFFINE p = 2");
    const long n = (long)L.nblk() * 64 * L.nq;
    if (n == 0) { return; }
    hipLaunchKernelGGL((k_tsnap_expand<4>), dim3(grid_for(n, 256)), dim3(256), 0, s, L.perm, L.ne, W, qd_fac, qd_m,
@@ -1122,7 +1094,8 @@ void setup_affine(const QLayout &L, int Q, const double *enodes, const double *J
                   double *qd_fac, double *qd_pair, hipStream_t s)
 {
    if (L.ne == 0) { return; }
-   ECM2_VERIFY(L.affine() && cd && (cm || L.pw <= 1), ERR_INTERNAL, "affine setup needs an AFFINE layout and its coefficients");
+   ECM2_VERIFY(L.affine() && cd && (cm || L.pw <= 1) && (!L.tsnap || L.kind == QLAYOUT_AFFINE), ERR_INTERNAL,
+               "affine setup needs an AFFINE layout and its coefficients");
    ECM2_VERIFY(!L.pos || L.perm, ERR_INTERNAL, "blocked setup needs the inverse permutation");
    const SetupCoef scm = make_setup_coef(cm, cm_q), scd = make_setup_coef(cd, cd_q);
    const bool blk = L.kind == QLAYOUT_AFFINE;

@@ -100,7 +100,6 @@ struct QLayout
    {
       if (kind == QLAYOUT_NATIVE || kind == QLAYOUT_NATIVE9) { return (size_t)ne * nq; }
       if (kind == QLAYOUT_AFFINE && tsnap && tmass == 2) { return (size_t)nblk() * kElemBlock; }  // [blk][lane]
-      if (kind == QLAYOUT_AFFINE_E && tsnap && tmass == 2) { return (size_t)ne; }                 // [e]
       if (kind == QLAYOUT_AFFINE || kind == QLAYOUT_TRILINEAR) { return (size_t)nblk() * nq * pw * kElemBlock; }
       if (kind == QLAYOUT_AFFINE_E || kind == QLAYOUT_TRILINEAR_E) { return (size_t)ne * nq * pw; }
       return (size_t)nblk() * ((nq + 1) / 2) * 2 * kElemBlock;
@@ -449,12 +448,6 @@ void scatter_add_idx(int n, const int *idx, const double *buf, double *y, hipStr
 // s_h = runs[r][8 + h] for h < 4, else rslots[slot_off + h].  runs has a sentinel row.
 void sum_partials(int b0, int b1, const int *blocks, const int *runs, const int *rslots, const int *pdof, const double *part,
                   int n_owned, double *y, double *yg, hipStream_t s);
-// The summation pass of regular 2 x 2 x 1 bricks in a lexicographic grid (PAForm::brick_grid_):
-// per brick and surface point, the highest holder sums the partial slots of the point's holders
-// (itself and its -x / -y / -z neighbours k - 1, k - nbx, k - nbxy) in ascending brick order and
-// stores y; no plan, no dependent reads.  breg [nbrick][8], part [nbrick][surface].
-void sum_brick_grid(int D, int nbrick, int nbx, int nbxy, const int *breg, const double *part, double *y, int k_items,
-                    hipStream_t s);
 } // namespace kern
 
 } // namespace ecm2

@@ -35,8 +35,6 @@ PAForm::PAForm(int ne, int order, int ndofs, const int *gather_map_host, int q1d
    require_device();
    D_ = order + 1;
    Q_ = q1d > 0 ? q1d : default_q1d(order);
-   if (const char *g = std::getenv("ECM2_SUM_GRID")) { brick_grid_k_ = std::atoi(g); }
-   if (const char *g = std::getenv("ECM2_BRICK_TS")) { brick_ts_ = std::atoi(g); }
    ECM2_VERIFY(Q_ >= D_ && Q_ <= MAX_Q1D, ERR_ARG, "q1d must satisfy p+1 <= q1d <= " << MAX_Q1D);
    ND_ = D_ * D_ * D_;
    NQ_ = Q_ * Q_ * Q_;
@@ -1114,31 +1112,6 @@ void PAForm::assemble(hipStream_t s)
             r[0] = base; r[1] = sx; r[2] = sy; r[3] = sz; r[4] = mask;
          }
          if (regular) { breg_.upload(reg, s); }
-         // Brick grid (round 5): the regular bricks of a Cartesian lattice in lexicographic brick order
-         // (nbx along x, nby along y), each face shared exactly when a neighbour brick lies behind it.
-         // Then a shared point's holders are the brick and its -x / -y / -z neighbours k - 1, k - nbx,
-         // k - nbx nby, found by arithmetic: the summation pass needs no plan (k_sum_brick_grid).
-         brick_grid_ = {0, 0, 0};
-         if (regular && n_left == 0 && brick_bz_ == 1)
-         {
-            const int *r0 = &reg[0];
-            const int sx = r0[1], sy = r0[2], sz = r0[3];
-            int nbx = 1, nby = 1;
-            while (nbx < n_bricks_ && reg[(size_t)nbx * 8] == r0[0] + nbx * (LX - 1) * sx) { nbx++; }
-            while (nby * nbx < n_bricks_ && reg[(size_t)nby * nbx * 8] == r0[0] + nby * (LY - 1) * sy) { nby++; }
-            bool grid = n_bricks_ % (nbx * nby) == 0;
-            const int nbz = grid ? n_bricks_ / (nbx * nby) : 0, LZ = D_;
-            for (int k = 0; k < n_bricks_ && grid; k++)
-            {
-               const int i = k % nbx, j = (k / nbx) % nby, l = k / (nbx * nby);
-               const int *r = &reg[(size_t)k * 8];
-               const int want_mask = (i > 0) | (i < nbx - 1) << 1 | (j > 0) << 2 | (j < nby - 1) << 3 | (l > 0) << 4 |
-                                     (l < nbz - 1) << 5;
-               grid = r[0] == r0[0] + i * (LX - 1) * sx + j * (LY - 1) * sy + l * (LZ - 1) * sz && r[1] == sx &&
-                      r[2] == sy && r[3] == sz && r[4] == want_mask;
-            }
-            if (grid) { brick_grid_ = {n_bricks_, nbx, nbx * nby}; }
-         }
       }
       gmap_line_.upload(enc, s);
       lelem_.upload(lelem.empty() ? std::vector<int>{0} : lelem, s);
@@ -1167,20 +1140,10 @@ void PAForm::assemble(hipStream_t s)
    layout_.tmass = 0;
    layout_.tlaw = 0;
    tsnap_.resize(0);
-   // p >= 3 (k_apply_brick_c, round 5): AFFINE_E, every element in a 2 x 2 x 1 brick (both integrators:
-   // bricks exist only with both), the snapshot in dof order.
+   // (p >= 3: the same snapshot in the brick kernel was measured and rejected, profiles/r5/ab_c5*.txt)
    const bool ts_tpe = layout_.kind == QLAYOUT_AFFINE && resolved_mode_ == KERNEL_TPE && D_ == 3 && Q_ == 4 &&
                        (treg_all_ || tlat_all_);
-   const bool ts_brick = layout_.kind == QLAYOUT_AFFINE_E && resolved_mode_ == KERNEL_LINE && n_bricks_ > 0 &&
-                         n_left_ == 0 && brick_bz_ == 1 && D_ <= 6 && Q_ == D_ + 1 && have_mass_ && use_partials();
-   // (the bricks take it only when it removes the whole per-point stream: with W alpha det J still
-   // streamed, the T images' extra stage work and barrier cost more than the 8 B per point save,
-   // profiles/r5/ab_c5.txt)
-   const bool mass_elem = have_mass_ && (cmass_.kind == COEFF_CONSTANT ||
-                                         (cmass_.gridfunc() && cmass_.lvec == cdiff_.lvec));
-   const bool ts_brick_ok = ts_brick && (brick_ts_ == 2 || (brick_ts_ == 1 && mass_elem));
-   if (tsnap_pref_ && (ts_tpe || ts_brick_ok) && have_diff_ && cdiff_.gridfunc() && cdiff_.lvec &&
-       !marked_[INTEG_DIFFUSION])
+   if (tsnap_pref_ && ts_tpe && have_diff_ && cdiff_.gridfunc() && cdiff_.lvec && !marked_[INTEG_DIFFUSION])
    {
       layout_.tsnap = 1;
       const bool mass_law = have_mass_ && cmass_.gridfunc() && cmass_.lvec == cdiff_.lvec;
@@ -1198,7 +1161,7 @@ void PAForm::assemble(hipStream_t s)
          A = cdiff_.scale * (1.0 - cdiff_.slope * cdiff_.t_ref);
          B = cdiff_.scale * cdiff_.slope;
       }
-      if (ts_brick_ok || treg_all_)
+      if (treg_all_)
       {
          tsnap_.resize(std::max(1, ndofs_));
          kern::affine_snapshot(ndofs_, cdiff_.lvec, A, B, tsnap_.data(), s);
@@ -1476,17 +1439,6 @@ void PAForm::finish_shared(int i0, int i1, double *y, double *yg, hipStream_t s)
    // the plan's blocks cover the owned shared dofs [0, n_sh_owned_) then the ghost ones
    ECM2_VERIFY((i0 == 0 || i0 == n_sh_owned_) && (i1 == n_sh_owned_ || i1 == n_sh_) && i0 <= i1, ERR_INTERNAL,
                "summation range [" << i0 << ", " << i1 << ") is not a plan range");
-   if (brick_grid_.n && brick_grid_k_ > 0 && resolved_mode_ == KERNEL_LINE)
-   {
-      // (all dofs owned: the whole range is [0, n_sh_))
-      if (i0 == 0 && i1 == n_sh_)
-      {
-         kern::sum_brick_grid(D_, brick_grid_.n, brick_grid_.nbx, brick_grid_.nbxy, breg_.data(), part_.data(), y,
-                              brick_grid_k_, s);
-         return;
-      }
-      if (i0 == i1) { return; }
-   }
    const int b0 = i0 == 0 ? 0 : sh_nblk_owned_, b1 = i1 == n_sh_owned_ ? sh_nblk_owned_ : sh_nblk_;
    kern::sum_partials(b0, b1, sh_blocks_.data(), sh_runs_.data(), sh_rslots_.data(), sh_pdof_.data(), part_.data(),
                       n_owned_, y, yg, s);

@@ -243,11 +243,6 @@ private:
    int n_bricks_ = 0, brick_bz_ = 0, brick_np_ = 0;  // LINE bricks: count, 2 x 2 x bz, lattice points
    DeviceArray<int> belem_, bmap_;  // LINE bricks: [nbrick][4 bz] elements, [nbrick][np] lattice map
    DeviceArray<int> breg_;          // LINE bricks, lattice-numbered: [nbrick][8] (base, sx, sy, sz, face mask)
-   // LINE bricks forming a lexicographic grid (nbrick, nbx, nbx nby; nbrick 0: no): the summation pass
-   // finds a shared point's holders by arithmetic (kern::sum_brick_grid) instead of the run plan
-   struct { int n, nbx, nbxy; } brick_grid_ = {0, 0, 0};
-   int brick_grid_k_ = 8;           // items per thread of the grid pass (A/B: ECM2_SUM_GRID=0 keeps the run plan)
-   int brick_ts_ = 1;               // brick snapshot: 0 never, 1 with the mass per element (tmass 2), 2 always (A/B: ECM2_BRICK_TS)
    DeviceArray<int> treg_;          // TPE blocks: [nblk][8] (base, sx, sy, sz, face mask, -, -, flag 1 regular / 2 lattice slots)
    bool treg_all_ = false;          // every TPE block regular: face-grouped slots only
    bool tlat_all_ = false;          // every TPE block a lattice-map block (treg flag 2)

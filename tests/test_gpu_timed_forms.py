@@ -120,14 +120,14 @@ def test_timed_trilinear_forms(variant):
 
 def test_timed_c5_form():
     """configs[4] as bench.py --workload c5 times it: Cartesian 68^3, p = 4 (20.3M DoF), AFFINE_E,
-    every element in a lattice-addressed 2 x 2 x 1 brick, k(T) from the H1 field through the brick
-    kernel's coefficient snapshot (k_apply_brick_c<5,6,1,false,1,true,TS=1,LAW=false>: W alpha det J
-    per point, k(T) interpolated from the snapshot)."""
+    every element in a lattice-addressed 2 x 2 x 1 brick (k_apply_brick_c<5,6,1,false,1,true>), the
+    stored (W beta, W alpha det J) pairs (the bricks do not take the k(T) snapshot: measured slower,
+    profiles/r5/ab_c5.txt) and the run-plan summation pass."""
     mesh, fes = B.cartesian_space(E, 68, 68, 68, 4, "structured", "affine")
     assert fes.ndofs == 20346417
     keep = []
     form = B.bench_form(E, torch, mesh, fes, keep)
     assert form.info()["kernel"] == E.KERNEL_LINE and form.info()["layout"] == E.QLAYOUT_AFFINE_E
     assert form.BrickInfo() == (fes.ne // 4, 1) and form.AddressingInfo()[0] == fes.ne // 4
-    assert form.SnapshotInfo() == (True, 1, False)
+    assert form.SnapshotInfo() == (False, 0, False)
     _check_form(mesh, fes, form, keep, 68)

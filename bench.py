@@ -398,6 +398,9 @@ def main():
     ap.add_argument("--geometry-input", choices=["nodes", "jacobians"], default="nodes",
                     help="c2/c4/c5 main line: geometry given as element corners (nodes) or as MFEM's "
                          "GeometricFactors::JACOBIANS array (what the reference-side binding passes)")
+    ap.add_argument("--coefficients", choices=["bioheat", "pennes", "ex16"], default="bioheat",
+                    help="serial main line's coefficients: bioheat (rho c_eff(x) projected + gamma dt k(T), the "
+                         "headline), pennes or ex16 (the snapshot forms of the pennes / ex16 sub-objects)")
     ap.add_argument("--loopback", type=int, default=1,
                     help="N>1 on one GPU: N subdomains in this process (validation of the partitioned path)")
     ap.add_argument("--partition", choices=["slabs", "boxes", "bricks"], default="slabs",
@@ -479,6 +482,9 @@ def main():
     keep = []
 
     def serial_form(compress_geometry, mesh=mesh, fes=fes, numbering=args.numbering, geo=args.geometry_input):
+        if args.coefficients != "bioheat":
+            keep.extend(list(bioheat_coefficients(E, torch, mesh, fes)))  # (the CPU baseline's operator)
+            return bench_law_form(E, torch, mesh, fes, keep, args.coefficients)
         return bench_form(E, torch, mesh, fes, keep, kernel=kernel, scatter=scatter,
                           compress_geometry=compress_geometry,
                           element_order="faces" if numbering == "entity" and args.workload != "c3" else "auto",
@@ -611,7 +617,8 @@ def main():
             ff, fes, variant, "same run, same mesh and numbering, per-point qdata (56 B per quadrature point: the "
                               "layout SURVEY §8(d)'s algorithmic bytes describe, so its alg_ratio is a roofline fraction)")
         del ff
-    if serial_main and args.variants == 1 and args.numbering == "structured" and args.mesh == "affine":
+    if (serial_main and args.variants == 1 and args.numbering == "structured" and args.mesh == "affine"
+            and args.coefficients == "bioheat"):
         dl.at("entity numbering")
         me, fe_ = cartesian_space(E, nx, ny, nz_total, order, "entity", "affine")
         fv = serial_form(compress, me, fe_, "entity")
@@ -640,7 +647,8 @@ def main():
                                  "GeometricFactors::JACOBIANS array (set_jacobians, fitted to trilinear maps at "
                                  "Assemble)")
         del fv, md, fd
-    if serial_main and args.variants in (1, 2) and args.numbering == "structured" and args.mesh == "affine":
+    if (serial_main and args.variants in (1, 2) and args.numbering == "structured" and args.mesh == "affine"
+            and args.coefficients == "bioheat"):
         for case, note in (("pennes", "same run, same mesh and numbering as the main line, the Pennes operator with "
                                       "both coefficients laws of one H1 temperature field: Mass(rho c + gamma dt c_b "
                                       "w_b(T), perfusion shut-off at T_stop) + Diffusion(gamma dt k(T)); the snapshot "
@@ -652,7 +660,7 @@ def main():
                                     "element")):
             dl.at(f"{case} form")
             fv = bench_law_form(E, torch, mesh, fes, keep, case)
-            sub = sub_measure(fv, fes, "", note, use_pin=False)  # (the main line's pin is not this form's)
+            sub = sub_measure(fv, fes, {"pennes": "pen", "ex16": "ex16"}[case], note)  # (its own pin)
             sub["snapshot"] = dict(zip(("on", "mass_values", "law_at_point"), fv.SnapshotInfo()))
             subs[case] = sub
             del fv
@@ -723,7 +731,8 @@ def variant_key(args):
     if args.workload == "c3":
         return ""
     return (("ent" if args.numbering == "entity" else "") + ("tri" if args.mesh == "trilinear" else "")
-            + ("jac" if args.geometry_input == "jacobians" else ""))
+            + ("jac" if args.geometry_input == "jacobians" else "")
+            + {"bioheat": "", "pennes": "pen", "ex16": "ex16"}[args.coefficients])
 
 
 def cartesian_space(E, nx, ny, nz, order, numbering, shape):

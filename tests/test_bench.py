@@ -69,7 +69,7 @@ def test_bench_single_gpu_line():
     assert b["pennes"]["snapshot"] == {"on": True, "mass_values": 2, "law_at_point": True}
     assert b["ex16"]["snapshot"] == {"on": True, "mass_values": 2, "law_at_point": False}
     assert b["pennes"]["qdata_layout"] == b["ex16"]["qdata_layout"] == "affine_tsm"
-    assert b["pennes"]["roofline"]["traffic"] is None and b["pennes"]["value"] > 0
+    assert b["pennes"]["roofline"]["traffic"] is None and b["pennes"]["value"] > 0  # (pins: default size only)
     s = run_bench(*SMALL, "--variants", "0", "--coefficient-snapshot", "0")
     assert s["value"] > 0 and "entity_numbering" not in s
     assert b["config"]["qdata_layout"] == "affine_ts" and s["config"]["qdata_layout"] == "affine"

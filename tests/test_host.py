@@ -304,3 +304,22 @@ def test_uniform_refinement_follows_reference_numbering():
         assert list(R[8 * i + 6]) == [c, f_[2], e_[10], f_[3], f_[5], e_[5], v[6], e_[6]]
         assert np.allclose(VR[c], V[v].mean(axis=0), atol=1e-15)
         assert np.allclose(VR[e_[0]], V[[v[0], v[1]]].mean(axis=0), atol=1e-15)
+
+
+def test_point_coefficients_are_checked_before_the_gpu():
+    """Per-quadrature-point coefficient tensors are validated in the Python mirror before a device
+    pointer reaches the kernels (which read [ne][nq][dim] float64): wrong dtype, shape or device is an
+    ECM2Error, not a silent misread."""
+    torch = pytest.importorskip("torch")
+    ne, nq = 6, 27
+    for c in (E.QuadratureCoefficient(torch.zeros(ne, nq, dtype=torch.float32)),
+              E.QuadratureCoefficient(torch.zeros(ne, nq, dtype=torch.float64)),          # a host tensor
+              E.VectorCoefficient(torch.zeros(ne, nq, 3, dtype=torch.float64)),
+              E.MatrixCoefficient(torch.zeros(ne, nq, 9, dtype=torch.float64), symmetric=True)):
+        with pytest.raises(E.ECM2Error):
+            E._integrator_args(c, [], ne, nq)
+    # the shape rule itself (a device-independent part of the check)
+    with pytest.raises(E.ECM2Error):
+        E._check_points(E.VectorCoefficient(None), np.zeros((ne, nq, 3)), ((3,),), ne, nq)
+    # the grid-function kinds map to the ABI's kinds without touching the data
+    assert E.COEFF_GRIDFUNC == 10 and E.GridFunctionCoefficient(None).T is None

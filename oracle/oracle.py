@@ -310,6 +310,35 @@ class OracleOperator:
         self._Bf = _f64(self.B.T.ravel())
         self._Gf = _f64(self.G.T.ravel())
 
+    @classmethod
+    def from_jacobians(cls, J, gm, ndofs, order, alpha=None, beta=None, q1d=None):
+        """The same operator on a mesh given by its Jacobians at the quadrature points -- J [ne][3 (j)][3 (i)]
+        [nq], GeometricFactors::JACOBIANS' memory order (mesh.cpp:15220-15273) -- e.g. a curved mesh whose
+        high-order nodes the test turned into J; the setups are PADiffusionSetup3D / the mass setup on
+        that J (bilininteg_diffusion_kernels.cpp:243-367, bilininteg_mass_pa.cpp:60-78)."""
+        self = cls.__new__(cls)
+        self.gm = _i32(gm)
+        self.ne = self.gm.shape[0]
+        self.ndofs = int(ndofs)
+        self.p = order
+        self.q1d = q1d or default_q1d(order)
+        self.B, self.G = dof_to_quad(order, self.q1d)
+        self.W = cube_weights(self.q1d)
+        J = _f64(J)
+        assert J.shape == (self.ne, 3, 3, self.q1d ** 3)
+        self.enodes, self.X, self.J = None, None, J
+        self.detJ = np.ascontiguousarray(np.linalg.det(np.transpose(J, (0, 3, 2, 1))))  # det of J[i][j]
+        self.alpha, self.beta, self.beta_dim = alpha, beta, 1
+        self.M = mass_setup(self.detJ, self.W, alpha, self.q1d) if alpha is not None else None
+        self.D = diffusion_setup(J, self.W, beta, self.q1d) if beta is not None else None
+        self.off, self.idx = build_csr(self.gm, self.ndofs)
+        nd = self.gm.shape[1]
+        self._xe = np.empty((self.ne, nd))
+        self._ye = np.empty((self.ne, nd))
+        self._Bf = _f64(self.B.T.ravel())
+        self._Gf = _f64(self.G.T.ravel())
+        return self
+
     def mult(self, x):
         if self.D is not None and self.D.shape[1] == 9:  # MultInternal with the general qdata
             xe = restriction_mult(self.gm, x)

@@ -80,6 +80,97 @@ def read_mfem_mesh(path):
     return V, E
 
 
+def read_mfem_nodes(path):
+    """The `nodes` section of an MFEM v1.0 mesh (a high-order, curved mesh: FiniteElementSpace with
+    VDim 3): (collection name, [ndofs][3] coordinates).  Ordering 0 = byNODES (all x, then y, then z),
+    1 = byVDIM."""
+    lines = [ln.split("#")[0].strip() for ln in open(path)]
+    lines = [ln for ln in lines if ln]
+    i = lines.index("nodes")
+    hdr = {}
+    j = i + 1
+    while ":" in lines[j] or lines[j] == "FiniteElementSpace":
+        if ":" in lines[j]:
+            k, v = lines[j].split(":", 1)
+            hdr[k.strip()] = v.strip()
+        j += 1
+    vals = np.array([float(t) for ln in lines[j:] for t in ln.split()])
+    vdim = int(hdr["VDim"])
+    n = vals.size // vdim
+    X = vals.reshape(vdim, n).T if int(hdr.get("Ordering", 0)) == 0 else vals.reshape(n, vdim)
+    return hdr["FiniteElementCollection"], np.ascontiguousarray(X)
+
+
+def write_linear_mfem_mesh(path, V, E):
+    """An MFEM v1.0 hex mesh file from vertices [nv][3] and native-order elements [ne][8] (attribute 1,
+    no boundary section)."""
+    with open(path, "w") as f:
+        f.write("MFEM mesh v1.0\n\ndimension\n3\n\nelements\n%d\n" % len(E))
+        for e in E:
+            f.write("1 5 " + " ".join(str(int(v)) for v in e) + "\n")
+        f.write("\nboundary\n0\n\nvertices\n%d\n3\n" % len(V))
+        for v in V:
+            f.write("%.17g %.17g %.17g\n" % tuple(v))
+
+
+def curved_jacobians(Xn, gm_geo, p_geo, q1d):
+    """GeometricFactors::JACOBIANS (mesh.cpp:15220-15273) of a curved mesh from its H1 nodes: J(q)[i][j]
+    = sum_a X_a[i] d_j phi_a(xi_q) over the element's lexicographic nodes (gm_geo: the order-p_geo
+    space's gather map, Xn: the node coordinates); returns J [ne][3 (j)][3 (i)][nq] -- the MFEM layout
+    NQ x 3 x 3 x NE in memory -- and the lexicographic node coordinates [ne][nd][3]."""
+    import oracle as O
+    B, G = O.dof_to_quad(p_geo, q1d)          # [Q][D]
+    D = p_geo + 1
+    Xe = Xn[gm_geo]                            # [ne][nd][3], nd lexicographic dx fastest
+    ne = Xe.shape[0]
+    Xl = Xe.reshape(ne, D, D, D, 3)            # [e][dz][dy][dx][i]
+    # d/dxi, d/deta, d/dzeta at (qx, qy, qz)
+    dx = np.einsum("xa,yb,zc,ecbai->ezyxi", G, B, B, Xl)
+    dy = np.einsum("xa,yb,zc,ecbai->ezyxi", B, G, B, Xl)
+    dz = np.einsum("xa,yb,zc,ecbai->ezyxi", B, B, G, Xl)
+    nq = q1d ** 3
+    J = np.empty((ne, 3, 3, nq))
+    for j, d in enumerate((dx, dy, dz)):
+        J[:, j, :, :] = d.reshape(ne, nq, 3).transpose(0, 2, 1)
+    return J, Xe
+
+
+def curved_fichera(tmpdir, order, q1d, name="fichera-q2.mesh"):
+    """The reference's curved fichera (data/fichera-q2.mesh: 7 hexes, H1_3D_P2 nodes, used by
+    tests/unit/fem/test_assembly_levels.cpp:260): (mesh, fes, J, X) -- the linear mesh of its topology
+    (the vertex nodes as corners; the library's numbering of an H1 space depends on the topology only),
+    the order-`order` H1 space on it, the curved map's Jacobians at the q1d^3 Gauss-Legendre points
+    [ne][3][3][nq] (MFEM layout), and the physical coordinates of the space's dofs (the curved map at
+    each element's GLL nodes)."""
+    import oracle as O
+    path = os.path.join(GOLDEN, name)
+    coll, Xn = read_mfem_nodes(path)
+    assert coll == "H1_3D_P2"
+    lines = [ln.split("#")[0].strip() for ln in open(path)]
+    lines = [ln for ln in lines if ln]
+    i = lines.index("elements")
+    ne = int(lines[i + 1])
+    elems = np.array([[int(t) for t in lines[i + 2 + k].split()[2:]] for k in range(ne)], np.int32)
+    nv = int(lines[lines.index("vertices") + 1])
+    lin = os.path.join(str(tmpdir), "fichera_q2_linear.mesh")
+    write_linear_mfem_mesh(lin, Xn[:nv], elems)   # (MFEM's H1 numbering puts the vertex dofs first)
+    mesh = load_pkg().Mesh(lin)
+    E = load_pkg()
+    geo = E.H1Space(mesh, 2, E.NUMBERING_ENTITY)
+    assert geo.ndofs == Xn.shape[0]
+    J, Xe = curved_jacobians(Xn, geo.gather_map(), 2, q1d)
+    fes = E.H1Space(mesh, order, E.NUMBERING_ENTITY)
+    # the curved map at the order-p GLL nodes of every element, lexicographic, to the global dofs
+    gnodes, _ = O.gauss_lobatto(3)
+    pnodes, _ = O.gauss_lobatto(order + 1)
+    Bp = np.array([O.basis_eval(2, gnodes, y)[0] for y in pnodes])   # [p+1][3]
+    Xl = Xe.reshape(ne, 3, 3, 3, 3)
+    Xp = np.einsum("xa,yb,zc,ecbai->ezyxi", Bp, Bp, Bp, Xl).reshape(ne, -1, 3)
+    X = np.empty((fes.ndofs, 3))
+    X[fes.gather_map()] = Xp
+    return mesh, fes, J, X
+
+
 LEX_TO_NATIVE = [0, 1, 3, 2, 4, 5, 7, 6]
 
 

@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 import ecm2_amd as E
+import helpers as H
 import oracle as O
 from helpers import (GOLDEN, RTOL, alpha_bioheat, coeff_function, k_of_T, nonaligned, relerr,
                      temperature)
@@ -495,6 +496,55 @@ def test_marker_diagonal_keeps_assemble_time_state(snap):
     d2 = torch.full_like(d, float("nan"))
     f.AssembleDiagonal(d2)
     assert torch.equal(d, d2)
+
+
+@pytest.mark.parametrize("order,q1d", [(2, 4), (2, 5), (3, 5), (3, 6)])
+def test_curved_mesh_jacobians(tmp_path, order, q1d):
+    """A curved (high-order-node) mesh through the drop-in boundary: the reference's data/fichera-q2.mesh
+    (H1_3D_P2 nodes; the curved fichera meshes of test_assembly_levels.cpp:230,260 and
+    test_pa_kernels.cpp:647) handed over as GeometricFactors::JACOBIANS at the rule's points
+    (ecm2_pa_form_set_jacobians, as INTEGRATION.md's binding passes them).  No trilinear map produces
+    them, so the form keeps the per-point layout; Q1D = p + 3 is the rule a quadratic mesh's
+    MassIntegrator asks for (GetRule adds Trans.OrderW(), bilininteg.cpp:1450-1462).  Mult and diagonal
+    against the oracle on the same Jacobians, and the geometry-independent identities through the HIP
+    path (1^T M 1 = sum W det J, K 1 = 0, x^T K x = |g|^2 sum W det J for the linear x = g . X)."""
+    mesh, fes, J, X = H.curved_fichera(tmp_path, order, q1d)
+    gm = fes.gather_map()
+    en = mesh.element_nodes()
+    P = O.quad_points(en, q1d)           # (coefficient sample points: any smooth per-point values)
+    a, b = alpha_bioheat(P), coeff_function(P)
+    form = E.BilinearForm(fes, q1d=q1d, geometry="jacobians")
+    form.SetJacobians(dev(J))
+    form.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(a.reshape(fes.ne, -1)))))
+    form.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(dev(b.reshape(fes.ne, -1)))))
+    form.Assemble()
+    assert form.info()["layout"] not in (E.QLAYOUT_AFFINE, E.QLAYOUT_TRILINEAR, E.QLAYOUT_AFFINE_E,
+                                         E.QLAYOUT_TRILINEAR_E)   # curved: the per-point layout
+    op = O.OracleOperator.from_jacobians(J, gm, fes.ndofs, order, alpha=a, beta=b, q1d=q1d)
+    x = np.random.default_rng(order * 10 + q1d).uniform(-1, 1, fes.ndofs)
+    y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+    form.Mult(dev(x), y)
+    assert relerr(host(y), op.mult(x)) <= RTOL
+    d = torch.full_like(y, float("nan"))
+    form.AssembleDiagonal(d)
+    assert relerr(host(d), op.diagonal()) <= RTOL
+    vol = float((np.linalg.det(np.transpose(J, (0, 3, 2, 1))) * O.cube_weights(q1d)).sum())
+    for kind in ("mass", "diffusion"):
+        f = E.BilinearForm(fes, q1d=q1d, geometry="jacobians")
+        f.SetJacobians(dev(J))
+        f.AddDomainIntegrator(E.MassIntegrator() if kind == "mass" else E.DiffusionIntegrator())
+        f.Assemble()
+        one = torch.ones(fes.ndofs, dtype=torch.float64, device="cuda")
+        yy = torch.empty_like(one)
+        f.Mult(one, yy)
+        if kind == "mass":
+            assert abs(float(yy.sum()) - vol) < 1e-12 * vol
+        else:
+            assert float(yy.abs().max()) < 1e-12
+            g = np.array([0.3, -1.1, 0.7])
+            xg = dev(X @ g)
+            f.Mult(xg, yy)
+            assert abs(float(torch.dot(xg, yy)) - (g @ g) * vol) < 1e-11 * (g @ g) * vol
 
 
 @pytest.mark.parametrize("order,q1d", [(1, 3), (2, 3), (2, 5), (3, 4), (4, 5), (4, 7)])

@@ -5,10 +5,13 @@ and its tests hold no numeric golden vectors for PA diffusion/mass; they assert
 identities instead.  Each test below restates one of those assertions against
 the oracle (file:line of the reference test in each docstring).
 """
+import os
+
 import numpy as np
 import pytest
 
 import ecm2_amd as E
+import helpers as H
 import oracle as O
 from helpers import (GOLDEN, RTOL, coeff_function, element_nodes_from, nonaligned,
                      read_mfem_mesh, relerr)
@@ -266,3 +269,34 @@ def test_anisotropic_coefficients_pa_equals_fa(ctype, order, with_mass):
     if dim == 9 and ctype == 5:  # a nonsymmetric operator: x^T A y != y^T A x in general
         z = np.random.default_rng(9).uniform(-1, 1, nd)
         assert abs(z @ op.mult(x) - x @ op.mult(z)) > 1e-6 * abs(z @ op.mult(x))
+
+
+@pytest.mark.parametrize("order,q1d", [(2, 4), (2, 5), (3, 5), (3, 6)])
+def test_curved_mesh_oracle_known_answers(tmp_path, order, q1d):
+    """The reference's curved fichera (data/fichera-q2.mesh, H1_3D_P2 nodes; its PA parity tests run the
+    curved fichera meshes, test_assembly_levels.cpp:230,260, test_pa_kernels.cpp:647): the oracle built
+    from the curved map's Jacobians (OracleOperator.from_jacobians) satisfies the identities that hold for
+    any geometry -- 1^T M 1 = sum W det J (the quadrature of the volume), K 1 = 0, and for the linear
+    function x = g . X (in the space: the map is quadratic, p >= 2) x^T K x = |g|^2 sum W det J (grad x = g
+    at every point) -- and the node numbering is pinned by the geometry: det J > 0 everywhere and each
+    element's edge-midpoint nodes within the file's perturbation of their corners' mean."""
+    mesh, fes, J, X = H.curved_fichera(tmp_path, order, q1d)
+    W = O.cube_weights(q1d)
+    detJ = np.linalg.det(np.transpose(J, (0, 3, 2, 1)))
+    assert detJ.min() > 0.3
+    vol = float((detJ * W).sum())
+    assert 6.0 < vol < 7.5                                  # the 7 unit cubes, curved
+    gm = fes.gather_map()
+    M = O.OracleOperator.from_jacobians(J, gm, fes.ndofs, order, alpha=1.0, q1d=q1d)
+    K = O.OracleOperator.from_jacobians(J, gm, fes.ndofs, order, beta=1.0, q1d=q1d)
+    one = np.ones(fes.ndofs)
+    assert abs(M.mult(one).sum() - vol) < 1e-12 * vol
+    assert np.abs(K.mult(one)).max() < 1e-12
+    g = np.array([0.3, -1.1, 0.7])
+    x = X @ g
+    assert abs(x @ K.mult(x) - (g @ g) * vol) < 1e-11 * (g @ g) * vol
+    # numbering pin: a wrong edge / face assignment puts nodes ~0.5 from where they belong
+    geo = H.load_pkg().H1Space(mesh, 2, H.load_pkg().NUMBERING_ENTITY)
+    _, Xn = H.read_mfem_nodes(os.path.join(H.GOLDEN, "fichera-q2.mesh"))
+    Xl = Xn[geo.gather_map()].reshape(-1, 3, 3, 3, 3)
+    assert np.abs(Xl[:, 0, 0, 1] - 0.5 * (Xl[:, 0, 0, 0] + Xl[:, 0, 0, 2])).max() < 0.15

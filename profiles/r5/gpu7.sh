@@ -8,6 +8,11 @@ timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method threa
   tests/test_gpu_parity.py::test_curved_mesh_jacobians tests/test_gpu_snapshot_laws.py \
   tests/test_gpu_timed_forms.py::test_timed_c5_form > $O/tests.txt 2>&1 || { tail -30 $O/tests.txt; exit 1; }
 tail -3 $O/tests.txt
+for ept in 2 4; do  # the narrower summation workgroups against the oracle before timing them
+  ECM2_SUM_EPT=$ept timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread \
+    tests/test_gpu_parity.py > $O/parity_e$ept.txt 2>&1 || { tail -30 $O/parity_e$ept.txt; exit 1; }
+  tail -1 $O/parity_e$ept.txt
+done
 run() {  # tag ept bench-args
   local tag=$1 ept=$2; shift 2
   ECM2_SUM_EPT=$ept timeout -k 10 300 python -u bench.py "$@" --full-layout 0 --variants 0 --no-cpu-baseline \

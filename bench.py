@@ -245,7 +245,7 @@ def kernel_ms(forms, apply, x, y, steps, torch, settle_s=0.06, world=1, dist=Non
 PART_NAME = {"slabs": "z-slabs", "boxes": "boxes", "bricks": "brick runs"}
 
 
-def member_bench(args, torch, group, xs, ys, ndofs, workload, dl):
+def member_bench(args, E, torch, group, xs, ys, ndofs, workload, dl):
     """--loopback N --member R: member R's rows of the partitioned operator alone, captured in
     one HIP graph and replayed -- the stages, streams and kernels one RCCL rank runs on its own
     GPU (interior elements beside the exchange + boundary elements, then the shared-dof sums),
@@ -297,6 +297,23 @@ def member_bench(args, torch, group, xs, ys, ndofs, workload, dl):
     per = [sorted(samples[r])[len(samples[r]) // 2] for r in members]
     del runs, graphs
     worst = max(per)
+    pcg = None
+    if args.pcg_iters:
+        # one rank's solver iteration: its Mult, its vector passes on its true dofs, two dots
+        # through a real (one-rank) RCCL all-reduce and the per-iteration read-back
+        it_ms = {r: [] for r in members}
+        for p in range(passes):
+            for r in members:
+                dl.at(f"member {r} pcg pass {p}")
+                it_ms[r].append(pcg_iteration_ms(torch, E.Operator(group, member=r),
+                                                 group.forms[r].true_size, args.pcg_iters))
+        pm = [sorted(it_ms[r])[len(it_ms[r]) // 2] for r in members]
+        pcg = {"iterations": args.pcg_iters, "member_iteration_ms": [round(v, 5) for v in pm],
+               "slowest_member_iteration_ms": round(max(pm), 5),
+               "note": "Jacobi-PCG iterations of each member as one rank's operator (ecm2_operator_from_par_member: "
+                       "the member's Mult, its vector passes, both dots through ncclAllReduce on a one-rank "
+                       "communicator, the per-iteration 8-byte read-back); a real N-rank all-reduce over xGMI "
+                       "adds its hops on top"}
     print(json.dumps({"emulated_n_gpus": n, "workload": workload, "ndofs": ndofs,
                       "member_ms": [round(v, 5) for v in per], "members": members,
                       "member_passes_ms": [[round(v, 5) for v in samples[r]] for r in members],
@@ -305,9 +322,25 @@ def member_bench(args, torch, group, xs, ys, ndofs, workload, dl):
                       "decomposition": group.forms[0].part.decomposition,
                       "coefficient_snapshot": [bool(f.CoefficientSnapshot()) for f in group.forms],
                       "emulated_value": round(ndofs / (worst * 1e-3) / 1e6, 2), "unit": "MDoF/s",
+                      "pcg": pcg,
                       "note": f"one member's Mult alone on one GPU, exchange by device copies: a rank's Mult short "
                               f"of the xGMI transfer time; members interleaved over {passes} passes, the median "
                               "pass per member"}), flush=True)
+
+
+def pcg_iteration_ms(torch, op, n, iters):
+    """Wall time per Jacobi-PCG iteration of `op` (an Operator, or a BilinearForm's own PCG) over
+    `iters` iterations, no essential dofs, rel_tol 1e-30 (so every iteration runs), after one
+    untimed solve of the same length."""
+    b = torch.empty(n, dtype=torch.float64, device="cuda")
+    b.uniform_(-1.0, 1.0, generator=torch.Generator(device="cuda").manual_seed(3))
+    x = torch.empty_like(b)
+    op.PCG(b, x, rel_tol=1e-30, max_iter=iters, jacobi=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    it, _ = op.PCG(b, x, rel_tol=1e-30, max_iter=iters, jacobi=True)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) * 1e3 / max(it, 1)
 
 
 def pmc_pin(workload, world, layout):
@@ -416,6 +449,10 @@ def main():
     ap.add_argument("--member-graph", type=int, default=-1, choices=[-1, 0, 1],
                     help="--member: 1 replay one HIP graph per Mult, 0 launch the stages directly, "
                          "-1 as the RCCL form would (--par-graph, else the schedule's default)")
+    ap.add_argument("--pcg-iters", type=int, default=0,
+                    help="also time K Jacobi-PCG iterations (no ess, rel_tol 1e-30): on one GPU the serial "
+                         "form's solver; with --member the member as one rank's operator (its dots through "
+                         "a one-rank RCCL all-reduce, ecm2_operator_from_par_member)")
     ap.add_argument("--deadline", type=float, default=900.0,
                     help="seconds after which a rank prints its last stage and exits non-zero (0: none)")
     args = ap.parse_args()
@@ -563,7 +600,7 @@ def main():
             xs = [torch.empty(f.true_size, dtype=torch.float64, device="cuda").uniform_(-1, 1) for f in forms]
             ys = [torch.empty_like(v) for v in xs]
             if args.member is not None:
-                member_bench(args, torch, group, xs, ys, fes.ndofs, workload, dl)
+                member_bench(args, E, torch, group, xs, ys, fes.ndofs, workload, dl)
                 return
             n_true = sum(f.true_size for f in forms)
             apply = lambda _x, _y: group.Mult(xs, ys)
@@ -589,6 +626,8 @@ def main():
     layout = qdata_layout(E, timed_forms[0])
     pcg = c3_pcg(E, torch, fes, form) if args.workload == "c3" else None
     reasm = reassembly_ms(torch, form) if (form is not None and args.workload != "c3") else None
+    pcg_it = (pcg_iteration_ms(torch, form, fes.ndofs, args.pcg_iters)
+              if (args.pcg_iters and form is not None and world == 1 and args.loopback <= 1) else None)
 
     # aggregate over ranks: total true dofs, max time; kernel ms per Mult (interior + boundary
     # launches of one Mult when partitioned); bytes per GPU
@@ -706,6 +745,10 @@ def main():
                                  mbytes_total / world, stream, use_pin=pin_ok, flops=alg_flops(order, ne_own)),
             "cpu_baseline": cpu,
         }
+        if pcg_it is not None:
+            line["pcg_iteration"] = {"iterations": args.pcg_iters, "iteration_ms": round(pcg_it, 5),
+                                     "note": "Jacobi-PCG on the serial form (ecm2_pcg_solve), no ess, rel_tol 1e-30: "
+                                             "Mult + vector passes + two dots + the 8-byte read-back per iteration"}
         if reasm is not None:
             line["reassembly_ms"] = reasm  # Assemble after a k(T) change, plan kept (outside the timed region)
         line.update(subs)

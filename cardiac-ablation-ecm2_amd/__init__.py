@@ -744,6 +744,8 @@ _PAR_SIGS = {
     "ecm2_operator_from_pa_form": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
     "ecm2_operator_from_par_form": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
     "ecm2_operator_from_par_group": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "ecm2_operator_from_par_member": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                     ctypes.POINTER(ctypes.c_void_p)]),
     "ecm2_operator_size": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
     "ecm2_operator_mult": (ctypes.c_int, [ctypes.c_void_p] * 4),
     "ecm2_operator_pcg": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
@@ -1037,10 +1039,19 @@ class Operator:
     BilinearForm, one RCCL rank's ParBilinearForm (collective solvers), or a ParGroup
     (vectors = concatenated true vectors of its members)."""
 
-    def __init__(self, form):
+    def __init__(self, form, member=None):
+        """member (ParGroup only): that member alone as one rank's operator on its own GPU
+        (measurement; ecm2_operator_from_par_member)."""
         lib = _par_lib()
         h = ctypes.c_void_p()
-        if isinstance(form, BilinearForm):
+        if member is not None:
+            if not isinstance(form, ParGroup):
+                raise ECM2Error("member= needs a ParGroup")
+            n = len(form.forms)
+            fa = (ctypes.c_void_p * n)(*[f._h.value for f in form.forms])
+            _check(lib.ecm2_operator_from_par_member(ctypes.cast(fa, ctypes.c_void_p), n, int(member),
+                                                     ctypes.byref(h)))
+        elif isinstance(form, BilinearForm):
             _check(lib.ecm2_operator_from_pa_form(form._h, ctypes.byref(h)))
         elif isinstance(form, ParBilinearForm):
             _check(lib.ecm2_operator_from_par_form(form._h, ctypes.byref(h)))

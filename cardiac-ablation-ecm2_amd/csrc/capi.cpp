@@ -898,6 +898,23 @@ int ecm2_operator_from_par_group(ecm2_par_form *const *forms, int n, ecm2_operat
    });
 }
 
+int ecm2_operator_from_par_member(ecm2_par_form *const *forms, int n, int member, ecm2_operator **out)
+{
+   return guard([&] {
+      NEED(forms); NEED(out);
+      ECM2_VERIFY(n > 0, ecm2::ERR_ARG, "empty group");
+      std::vector<ecm2::ParPAForm *> fs;
+      for (int i = 0; i < n; i++)
+      {
+         NEED(forms[i]);
+         ECM2_VERIFY(forms[i]->f->part().rank == i && forms[i]->f->part().nranks == n, ecm2::ERR_ARG,
+                     "loopback group: form " << i << " has rank " << forms[i]->f->part().rank);
+         fs.push_back(forms[i]->f);
+      }
+      *out = new ecm2_operator{std::unique_ptr<ecm2::LinOp>(new ecm2::MemberOp(fs, member))};
+   });
+}
+
 int ecm2_operator_size(const ecm2_operator *op, int *n)
 {
    return guard([&] { NEED(op); NEED(n); *n = op->op->size(); });

@@ -499,6 +499,11 @@ void *self_comm()
 }
 } // namespace
 
+void group_self_allreduce(double *dev, int n, hipStream_t s)
+{
+   ECM2_NCCL(ncclAllReduce(dev, dev, n, ncclFloat64, ncclSum, (ncclComm_t)self_comm(), s));
+}
+
 void par_group_mult_member(std::vector<ParPAForm *> &forms, const std::vector<const double *> &x,
                            const std::vector<double *> &y, int r, hipStream_t s)
 {

@@ -138,6 +138,9 @@ void par_group_diagonal(std::vector<ParPAForm *> &forms, const std::vector<doubl
 // The other members' y are not touched.  This is what a rank's Mult costs on its own GPU, short
 // of the xGMI transfer time.  Run one group Mult on the same x arrays first: RAP and packed sends
 // fail with ERR_STATE when the peers' last group Mult ran on other x arrays or another assembly.
+// In-place sum of n device scalars on the one-rank RCCL communicator of the self transport: the
+// collective call a rank's solver makes, without the peers (member emulation, MemberOp).
+void group_self_allreduce(double *dev, int n, hipStream_t s);
 void par_group_mult_member(std::vector<ParPAForm *> &forms, const std::vector<const double *> &x,
                            const std::vector<double *> &y, int r, hipStream_t s);
 

@@ -37,6 +37,46 @@ void GroupOp::diagonal(double *d, hipStream_t s)
    par_group_diagonal(forms_, ds, s);
 }
 
+MemberOp::MemberOp(std::vector<ParPAForm *> forms, int member) : forms_(std::move(forms)), member_(member)
+{
+   const int n = (int)forms_.size();
+   ECM2_VERIFY(member >= 0 && member < n, ERR_ARG, "member " << member << " outside the group of " << n);
+   // the peers' x live in this operator's own buffer, on which no group Mult runs: their packed sends
+   // and (RAP) their ghost sums would be stale
+   ECM2_VERIFY(forms_[member]->part().overlap, ERR_UNSUPPORTED, "a member operator needs the OVERLAP decomposition");
+   for (ParPAForm *f : forms_)
+   {
+      ECM2_VERIFY(!f->pack_needed(), ERR_UNSUPPORTED, "a member operator needs contiguous sends (slabs)");
+   }
+   off_.assign(n + 1, 0);
+   for (int r = 0; r < n; r++) { off_[r + 1] = off_[r] + forms_[r]->true_size(); }
+   peers_.resize(std::max(off_.back(), 1));
+   yscratch_.resize(std::max(off_.back(), 1));
+   ECM2_HIP(hipMemset(peers_.data(), 0, peers_.size() * sizeof(double)));
+}
+
+void MemberOp::mult(const double *x, double *y, hipStream_t s)
+{
+   std::vector<const double *> xs;
+   std::vector<double *> ys;
+   for (size_t r = 0; r < forms_.size(); r++)
+   {
+      const bool me = (int)r == member_;
+      xs.push_back(me ? x : peers_.data() + off_[r]);
+      ys.push_back(me ? y : yscratch_.data() + off_[r]);
+   }
+   par_group_mult_member(forms_, xs, ys, member_, s);
+}
+
+void MemberOp::diagonal(double *d, hipStream_t s)
+{
+   std::vector<double *> ds;
+   for (size_t r = 0; r < forms_.size(); r++) { ds.push_back(yscratch_.data() + off_[r]); }
+   par_group_diagonal(forms_, ds, s);
+   const int n = size();
+   if (n) { ECM2_HIP(hipMemcpyAsync(d, ds[member_], n * sizeof(double), hipMemcpyDeviceToDevice, s)); }
+}
+
 // ---------------------------------------------------------------------------------------
 // ConstrainedOperator + CGSolver + OperatorJacobiSmoother
 // ---------------------------------------------------------------------------------------

@@ -81,6 +81,28 @@ private:
    int n_ = 0;
 };
 
+// One member of the loopback group as one rank's operator (measurement of a rank's solver
+// iteration on its own GPU; no reference counterpart): Mult = par_group_mult_member (the P
+// exchange as device copies from the peers' x, held in a private concatenated vector), the
+// dots summed by a real ncclAllReduce on a one-rank communicator (the collective call without
+// the xGMI hops).  Vectors are the member's true dofs.
+class MemberOp : public LinOp
+{
+public:
+   MemberOp(std::vector<ParPAForm *> forms, int member);
+   int size() const override { return forms_[member_]->true_size(); }
+   void mult(const double *x, double *y, hipStream_t s) override;
+   void diagonal(double *d, hipStream_t s) override;
+   void sum_scalars(double *dev, int n, hipStream_t s) override { group_self_allreduce(dev, n, s); }
+   bool distributed() const override { return true; }
+
+private:
+   std::vector<ParPAForm *> forms_;
+   int member_;
+   std::vector<int> off_;
+   DeviceArray<double> peers_, yscratch_;  // the peers' x (zeros) and y (never read), concatenated
+};
+
 struct PCGResult
 {
    int iterations = 0;

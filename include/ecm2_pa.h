@@ -313,6 +313,12 @@ int ecm2_operator_from_par_form(ecm2_par_form *f, ecm2_operator **out);
 /* forms[r] must be rank r of an n-rank partition; vectors are the concatenation of the
  * ranks' true vectors (rank r at offset sum_{q<r} n_owned(q)). */
 int ecm2_operator_from_par_group(ecm2_par_form *const *forms, int n, ecm2_operator **out);
+/* Measurement (no reference counterpart): member `member` of the loopback group as one rank's
+ * operator on its own GPU -- Mult = ecm2_par_group_mult_member (the peers' x held at zero in a
+ * private buffer), dots summed by ncclAllReduce on a one-rank communicator.  Vectors are the
+ * member's true dofs; ecm2_operator_pcg on it times one rank's solver iteration.  OVERLAP
+ * decomposition with contiguous sends (slabs) only: ECM2_ERR_UNSUPPORTED otherwise. */
+int ecm2_operator_from_par_member(ecm2_par_form *const *forms, int n, int member, ecm2_operator **out);
 /* Operator::Height/Width and Operator::Mult (operator.hpp:24-110). */
 int ecm2_operator_size(const ecm2_operator *op, int *n);
 int ecm2_operator_mult(ecm2_operator *op, const double *x, double *y, void *stream);

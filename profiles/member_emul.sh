@@ -9,9 +9,9 @@ mkdir -p "$O"
 WL=${WL:-c4}
 timeout -k 10 300 python3 bench.py --workload $WL --steps 50 --warmup 5 --no-cpu-baseline --full-layout 0 ${EXTRA:-} \
   > "$O/${WL}${TAG:-}_n1.json" 2> "$O/${WL}${TAG:-}_n1.err" || exit $?
-python3 -c "import json,sys; b=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('N=1', b['value'], 'MDoF/s', b['ms_per_step'], 'ms')" "$O/${WL}${TAG:-}_n1.json"
+python3 -c "import json,sys; b=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('N=1', b['value'], 'MDoF/s', b['ms_per_step'], 'ms', 'pcg_iteration_ms', (b.get('pcg_iteration') or {}).get('iteration_ms'))" "$O/${WL}${TAG:-}_n1.json"
 for N in ${@:-2 4 8}; do
   timeout -k 10 400 python3 bench.py --workload $WL --loopback $N --member -1 --steps 50 --warmup 5 \
     --no-cpu-baseline --full-layout 0 ${EXTRA:-} > "$O/${WL}${TAG:-}_n$N.json" 2> "$O/${WL}${TAG:-}_n$N.err" || exit $?
-  python3 -c "import json,sys; b=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('N=%d' % b['emulated_n_gpus'], b['emulated_value'], 'MDoF/s', 'slowest', b['slowest_member_ms'], 'ms', 'members', b['member_ms'])" "$O/${WL}${TAG:-}_n$N.json"
+  python3 -c "import json,sys; b=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); p=b.get('pcg') or {}; print('N=%d' % b['emulated_n_gpus'], b['emulated_value'], 'MDoF/s', 'slowest', b['slowest_member_ms'], 'ms', 'members', b['member_ms'], 'pcg slowest', p.get('slowest_member_iteration_ms'), 'ms/iter', p.get('member_iteration_ms'))" "$O/${WL}${TAG:-}_n$N.json"
 done

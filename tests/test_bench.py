@@ -84,3 +84,8 @@ def test_bench_loopback_group_and_member_lines():
     m = run_bench(*SMALL, "--loopback", "2", "--member", "-1")
     assert m["emulated_n_gpus"] == 2 and len(m["member_ms"]) == 2 and m["members"] == [0, 1]
     assert m["slowest_member_ms"] == max(m["member_ms"]) and m["emulated_value"] > 0
+    assert m["pcg"] is None
+    p = run_bench(*SMALL, "--loopback", "2", "--member", "-1", "--pcg-iters", "5")
+    assert len(p["pcg"]["member_iteration_ms"]) == 2 and p["pcg"]["slowest_member_iteration_ms"] > 0
+    s = run_bench(*SMALL, "--variants", "0", "--pcg-iters", "5")
+    assert s["pcg_iteration"]["iteration_ms"] > s["ms_per_step"]

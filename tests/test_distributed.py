@@ -445,6 +445,63 @@ def test_gpu_group_member_rows(nranks, order, schedule, decomp):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_gpu_member_operator_pcg(nranks):
+    """Operator(group, member=r) (ecm2_operator_from_par_member, bench.py --pcg-iters with --member):
+    member r as one rank's operator -- its Mult is the oracle's rows of r applied to x with every
+    peer-owned dof zero (the principal block), and Jacobi-PCG on it (dots through a one-rank RCCL
+    all-reduce) solves that block; RAP is refused (its P^T receive needs the peers' group Mult)."""
+    import torch
+    m = _mesh("cart_big")
+    m.set_vertices(nonaligned(m.vertices()))
+    order = 2
+    fes = E.H1Space(m, order, E.NUMBERING_STRUCTURED)
+    er = E.partition_slabs_z(m, nranks)
+    q1d = O.default_q1d(order)
+    Pg = O.quad_points(m.element_nodes(), q1d)
+    cg = coeff_function(Pg)
+    oracle = O.OracleOperator(m.element_nodes(), fes.gather_map(), fes.ndofs, order, alpha=cg, beta=cg)
+
+    def group_of(decomp):
+        forms, parts = [], []
+        for r in range(nranks):
+            part = E.Partition(fes, er, r, nranks, decomposition=decomp)
+            pf = E.ParBilinearForm(part)
+            P = E.quadrature_points_subset(m, q1d, part.elems)
+            c = torch.as_tensor(coeff_function(P).reshape(part.ne_local, -1)).cuda()
+            pf.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(c)))
+            pf.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(c.clone())))
+            pf.Assemble()
+            forms.append(pf)
+            parts.append(part)
+        return E.ParGroup(forms), parts
+
+    group, parts = group_of("overlap")
+    rng = np.random.default_rng(5)
+    for r in range(nranks):
+        op = E.Operator(group, member=r)
+        own = parts[r].owned_global
+        assert op.size == len(own)
+        xl = rng.uniform(-1, 1, len(own))
+        xg = np.zeros(fes.ndofs)
+        xg[own] = xl
+        y = torch.empty(len(own), dtype=torch.float64, device="cuda")
+        op.Mult(torch.as_tensor(xl).cuda(), y)
+        torch.cuda.synchronize()
+        assert relerr(y.cpu().numpy(), oracle.mult(xg)[own]) <= RTOL
+        b = torch.as_tensor(rng.uniform(-1, 1, len(own))).cuda()
+        x = torch.empty_like(b)
+        it, nrm = op.PCG(b, x, rel_tol=1e-11, max_iter=2000, jacobi=True)
+        assert 0 < it < 2000
+        op.Mult(x, y)
+        torch.cuda.synchronize()
+        assert relerr(y.cpu().numpy(), b.cpu().numpy()) <= 1e-8
+    rap, _ = group_of("rap")
+    with pytest.raises(E.ECM2Error):
+        E.Operator(rap, member=0)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("order", [2, 4])
 def test_gpu_rccl_single_rank_transport(order):
     """The RCCL transport with one rank (ncclCommInitRank, the comm stream and its events,

@@ -310,10 +310,10 @@ def member_bench(args, E, torch, group, xs, ys, ndofs, workload, dl):
         pm = [sorted(it_ms[r])[len(it_ms[r]) // 2] for r in members]
         pcg = {"iterations": args.pcg_iters, "member_iteration_ms": [round(v, 5) for v in pm],
                "slowest_member_iteration_ms": round(max(pm), 5),
-               "note": "Jacobi-PCG iterations of each member as one rank's operator (ecm2_operator_from_par_member: "
-                       "the member's Mult, its vector passes, both dots through ncclAllReduce on a one-rank "
-                       "communicator, the per-iteration 8-byte read-back); a real N-rank all-reduce over xGMI "
-                       "adds its hops on top"}
+               "note": "marginal time per Jacobi-PCG iteration of each member as one rank's operator "
+                       "(ecm2_operator_from_par_member: the member's Mult, its vector passes, both dots through "
+                       "ncclAllReduce on a one-rank communicator, the device-driven loop); a real N-rank "
+                       "all-reduce over xGMI adds its hops on top"}
     print(json.dumps({"emulated_n_gpus": n, "workload": workload, "ndofs": ndofs,
                       "member_ms": [round(v, 5) for v in per], "members": members,
                       "member_passes_ms": [[round(v, 5) for v in samples[r]] for r in members],
@@ -329,18 +329,23 @@ def member_bench(args, E, torch, group, xs, ys, ndofs, workload, dl):
 
 
 def pcg_iteration_ms(torch, op, n, iters):
-    """Wall time per Jacobi-PCG iteration of `op` (an Operator, or a BilinearForm's own PCG) over
-    `iters` iterations, no essential dofs, rel_tol 1e-30 (so every iteration runs), after one
-    untimed solve of the same length."""
+    """Marginal wall time per Jacobi-PCG iteration of `op` (an Operator, or a BilinearForm's own
+    PCG): (t(2K) - t(K)) / K for solves of K and 2K iterations (no essential dofs, rel_tol 1e-30 so
+    every iteration runs), after one untimed solve -- the per-solve setup (the Jacobi diagonal, the
+    first residual and its read-backs) cancels."""
     b = torch.empty(n, dtype=torch.float64, device="cuda")
     b.uniform_(-1.0, 1.0, generator=torch.Generator(device="cuda").manual_seed(3))
     x = torch.empty_like(b)
     op.PCG(b, x, rel_tol=1e-30, max_iter=iters, jacobi=True)
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    it, _ = op.PCG(b, x, rel_tol=1e-30, max_iter=iters, jacobi=True)
-    torch.cuda.synchronize()
-    return (time.perf_counter() - t0) * 1e3 / max(it, 1)
+    t = []
+    for k in (iters, 2 * iters):
+        t0 = time.perf_counter()
+        it, _ = op.PCG(b, x, rel_tol=1e-30, max_iter=k, jacobi=True)
+        torch.cuda.synchronize()
+        t.append((time.perf_counter() - t0) * 1e3)
+        assert it == k, (it, k)
+    return (t[1] - t[0]) / iters
 
 
 def pmc_pin(workload, world, layout):
@@ -747,8 +752,8 @@ def main():
         }
         if pcg_it is not None:
             line["pcg_iteration"] = {"iterations": args.pcg_iters, "iteration_ms": round(pcg_it, 5),
-                                     "note": "Jacobi-PCG on the serial form (ecm2_pcg_solve), no ess, rel_tol 1e-30: "
-                                             "Mult + vector passes + two dots + the 8-byte read-back per iteration"}
+                                     "note": "marginal time per Jacobi-PCG iteration on the serial form (ecm2_pcg_solve: the "
+                                             "device-driven loop), no ess: Mult + vector passes + two dots"}
         if reasm is not None:
             line["reassembly_ms"] = reasm  # Assemble after a k(T) change, plan kept (outside the timed region)
         line.update(subs)

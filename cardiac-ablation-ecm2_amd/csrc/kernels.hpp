@@ -414,14 +414,39 @@ void diagonal(const int *pos, int D, int Q, int layout, int ne, const int *gmap_
 // ---- vector kernels for the device PCG ----
 void set_values(int n, const int *idx, double val, double *y, hipStream_t s);     // y[idx] = val
 void copy_values(int n, const int *idx, const double *x, double *y, hipStream_t s); // y[idx] = x[idx]
-// Deterministic two-pass dot: result written to *out (device).
+// The device-driven PCG loop's state (device memory; the check kernel also writes it to a mapped
+// pinned host mirror): done = 0 running, 1 converged, 2 stopped at max_iter; iters, final = the
+// iteration and r.z at which it stopped.  The vector kernels of an iteration given `ctl` return at
+// once when done is set, so the host can enqueue iterations ahead of the stopping test.
+struct PcgCtl
+{
+   int done, iters;
+   double final;
+};
+// CGSolver's stopping test of iteration `it` (solvers.cpp:950-960) on the device: betanom <= r0 ->
+// converged at `it`; else it + 1 > max_iter -> stopped.  Writes ctl and the host mirror once, when
+// done is first set.
+struct PcgStop
+{
+   double r0;
+   int it, max_iter;
+   PcgCtl *ctl, *host;
+};
+// Deterministic one-pass dot (the last workgroup sums the per-workgroup partials in a fixed order):
+// result written to *out (device).  partials: kDotPartials doubles, zero-initialised once (the last
+// double is the arrival counter, re-armed by every launch).
 // hout (optional): device pointer of mapped pinned host memory that also receives the result.
+constexpr int kDotPartials = 1024 + 1;
 void dot(int n, const double *a, const double *b, double *partials, double *out, hipStream_t s,
-         double *hout = nullptr);
+         double *hout = nullptr, const PcgCtl *ctl = nullptr);
 // Fused PCG update: x += (nom/den) d; r -= (nom/den) z; z = dinv .* r (dinv null: z untouched);
-// *out = r.z (r.r without dinv), deterministic.  z holds A d on entry.
+// *out = r.z (r.r without dinv), deterministic.  z holds A d on entry.  stop (serial solver): the
+// stopping test on *out in the same launch.
 void pcg_step(int n, const double *nom, const double *den, const double *d, double *z, double *x, double *r,
-              const double *dinv, double *partials, double *out, hipStream_t s, double *hout = nullptr);
+              const double *dinv, double *partials, double *out, hipStream_t s, double *hout = nullptr,
+              const PcgCtl *ctl = nullptr, const PcgStop *stop = nullptr);
+// the stopping test alone (after a distributed r.z's all-reduce)
+void pcg_check(const double *betanom, const PcgStop &stop, hipStream_t s);
 // saved[i] = v[idx[i]], v[idx[i]] = 0  /  v[idx[i]] = y[idx[i]] = saved[i]
 void ess_save_zero(int n, const int *idx, double *v, double *saved, hipStream_t s);
 void ess_restore(int n, const int *idx, const double *saved, double *v, double *y, hipStream_t s);
@@ -429,7 +454,7 @@ void ess_restore(int n, const int *idx, const double *saved, double *v, double *
 void pcg_precond(int n, const double *dinv, const double *r, double *z, hipStream_t s);
 //   d = z + (betanom/nom) d
 void pcg_update_d(int n, const double *betanom, const double *nom, const double *z, double *d,
-                  hipStream_t s);
+                  hipStream_t s, const PcgCtl *ctl = nullptr);
 void reciprocal(int n, const double *a, double *out, hipStream_t s);
 void scale(int n, double a, double *y, hipStream_t s);                                   // y *= a
 void add_scaled(int n, const double *x, double c, const double *k, double *out, hipStream_t s); // out = x + c k

@@ -85,13 +85,21 @@ namespace
 // CGSolver's work vectors live across solves (CGSolver::SetOperator allocates them once,
 // solvers.cpp:869-880): one workspace per host thread and device, grown on demand, with a
 // mapped pinned scalar the final-dot kernels write the stopping-test value into.
+// Iterations the host enqueues ahead of the stopping test it has read (the device-driven loop).
+constexpr int kPcgAhead = 4;
+
 struct PCGWork
 {
    DeviceArray<double> r, d, z, saved, dinv, partials, scal;
    double *hs = nullptr, *hs_dev = nullptr;
+   DeviceArray<kern::PcgCtl> ctl;                          // the device-driven loop's state
+   kern::PcgCtl *hctl = nullptr, *hctl_dev = nullptr;      // its mapped pinned mirror
+   std::vector<hipEvent_t> ev;                             // per-iteration events (run-ahead window)
    ~PCGWork()
    {
       if (hs) { (void)hipHostFree(hs); }
+      if (hctl) { (void)hipHostFree(hctl); }
+      for (hipEvent_t e : ev) { (void)hipEventDestroy(e); }
    }
    void ensure(int n, int n_ess, bool jacobi)
    {
@@ -103,12 +111,21 @@ struct PCGWork
       grow(z, std::max(n, 1));
       grow(saved, std::max(n_ess, 1));
       if (jacobi) { grow(dinv, std::max(n, 1)); }
-      grow(partials, 1024);
+      if (partials.size() < (size_t)kern::kDotPartials)
+      {
+         partials.resize(kern::kDotPartials);  // (the one-pass dot's arrival counter must start at zero)
+         ECM2_HIP(hipMemset(partials.data(), 0, partials.bytes()));
+      }
       grow(scal, 4);
       if (!hs)
       {
          ECM2_HIP(hipHostMalloc(&hs, 4 * sizeof(double), hipHostMallocMapped));
          ECM2_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&hs_dev), hs, 0));
+         ECM2_HIP(hipHostMalloc(&hctl, sizeof(kern::PcgCtl), hipHostMallocMapped));
+         ECM2_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&hctl_dev), hctl, 0));
+         ctl.resize(1);
+         ev.resize(kPcgAhead);
+         for (hipEvent_t &e : ev) { ECM2_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming)); }
       }
    }
 };
@@ -138,8 +155,8 @@ PCGResult pcg_solve(LinOp &A, const int *ess, int n_ess, const double *b, double
    // serial: the final-dot kernel also writes the value into mapped pinned memory, so the
    // stopping test needs only a stream sync; distributed: copy after the all-reduce
    const bool direct = !A.distributed();
-   auto dot = [&](const double *a, const double *bb, double *out) {
-      kern::dot(n, a, bb, partials, out, s, direct ? w.hs_dev : nullptr);
+   auto dot = [&](const double *a, const double *bb, double *out, const kern::PcgCtl *c = nullptr) {
+      kern::dot(n, a, bb, partials, out, s, direct && !c ? w.hs_dev : nullptr, c);
       A.sum_scalars(out, 1, s);
    };
    auto readback = [&](const double *dv) {
@@ -182,25 +199,58 @@ PCGResult pcg_solve(LinOp &A, const int *ess, int n_ess, const double *b, double
    if (nom0 <= r0) { res.converged = true; }
    else
    {
+      // the device-driven loop's state, reset before the read-back below idles the stream (no
+      // kernel of a previous solve writes the mirror any more: every solve ends synchronised)
+      ECM2_HIP(hipMemsetAsync(w.ctl.data(), 0, sizeof(kern::PcgCtl), s));
+      w.hctl->done = 0;
+      w.hctl->iters = 0;
+      w.hctl->final = 0.0;
       cmult(d, z);
       dot(z, d, den);
       if (readback(den) != 0.0)
       {
-         for (int i = 1;;)
+         // CGSolver's loop (solvers.cpp:930-1000) driven by the device: the stopping test runs in a
+         // one-thread kernel after each r.z (and its all-reduce), and once it stops every later
+         // vector kernel returns at once.  The host enqueues iterations up to kPcgAhead ahead of the
+         // last one it has waited for, and ends when the mirror says the loop stopped at an
+         // iteration it has waited for -- the same iteration on every rank, so the ranks issue the
+         // same collectives.  The iterates are those of the host-tested loop (same kernels, same
+         // order); the wasted tail is <= kPcgAhead operator Mults per solve.
+         kern::PcgCtl *ctl = w.ctl.data(), *hm = w.hctl;  // (reset before the den read-back)
+         auto stopped_by = [&](int waited) {
+            const int dn = *(volatile int *)&hm->done;
+            return dn != 0 && *(volatile int *)&hm->iters <= waited;
+         };
+         int i = 1;
+         for (;; i++)
          {
+            if (i > kPcgAhead)
+            {
+               const int waited = i - kPcgAhead;
+               ECM2_HIP(hipEventSynchronize(w.ev[waited % kPcgAhead]));
+               if (stopped_by(waited)) { break; }
+            }
             // x += alpha d, r -= alpha A d, z = M^{-1} r, betanom = r.z in one pass
-            kern::pcg_step(n, nom, den, d, z, x, r, dinv, partials, betanom, s, direct ? w.hs_dev : nullptr);
-            A.sum_scalars(betanom, 1, s);
-            const double bn = readback(betanom);
-            res.final_norm = bn >= 0 ? std::sqrt(bn) : bn;
-            res.iterations = i;
-            if (bn <= r0) { res.converged = true; break; }
-            if (++i > max_iter) { break; }
-            kern::pcg_update_d(n, betanom, nom, jacobi ? z : r, d, s);
+            const kern::PcgStop stop{r0, i, max_iter, ctl, w.hctl_dev};
+            kern::pcg_step(n, nom, den, d, z, x, r, dinv, partials, betanom, s, nullptr, ctl, direct ? &stop : nullptr);
+            if (!direct)
+            {
+               A.sum_scalars(betanom, 1, s);
+               kern::pcg_check(betanom, stop, s);
+            }
+            if (i >= max_iter) { break; }
+            kern::pcg_update_d(n, betanom, nom, jacobi ? z : r, d, s, ctl);
             cmult(d, z);
-            dot(d, z, den);
+            dot(d, z, den, ctl);
             std::swap(nom, betanom);  // nom <- betanom
+            ECM2_HIP(hipEventRecord(w.ev[i % kPcgAhead], s));
          }
+         ECM2_HIP(hipStreamSynchronize(s));
+         ECM2_VERIFY(*(volatile int *)&hm->done != 0, ERR_INTERNAL, "device PCG loop ended without a stop");
+         const double bn = hm->final;
+         res.final_norm = bn >= 0 ? std::sqrt(bn) : bn;
+         res.iterations = hm->iters;
+         res.converged = hm->done == 1;
       }
    }
    ECM2_HIP(hipStreamSynchronize(s));

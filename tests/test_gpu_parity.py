@@ -599,6 +599,27 @@ def test_pcg_matches_oracle(jacobi):
     assert relerr(host(x), xr) < 1e-9
 
 
+@pytest.mark.parametrize("max_iter", [1, 2, 3, 4, 5, 8])
+def test_pcg_device_loop_stops_like_cgsolver(max_iter):
+    """The device-driven PCG loop (the stopping test in a kernel, iterations enqueued up to
+    kPcgAhead ahead, later vector kernels no-ops once stopped) returns CGSolver's iterate: after
+    max_iter iterations (fewer and more than the run-ahead window) x equals the oracle's after the
+    same count, and a converging solve stops at the oracle's iteration (solvers.cpp:930-1000)."""
+    m = make_mesh("fichera_r1")
+    fes, form, op = build_pair(m, 2, 1.0, "fn")
+    ess = fes.boundary_dofs()
+    b = np.random.default_rng(6).uniform(-1, 1, fes.ndofs)
+    x = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    it, nrm = form.PCG(dev(b), x, ess=dev(ess, torch.int32), rel_tol=1e-30, max_iter=max_iter, jacobi=True)
+    xr, itr, nr = op.pcg(b, ess, rel_tol=1e-30, max_iter=max_iter, jacobi=True)
+    assert it == itr == max_iter
+    assert relerr(host(x), xr) < 1e-11 and nrm == pytest.approx(nr, rel=1e-9)
+    # converging at a loose tolerance: the same stopping iteration, then every later kernel idle
+    it, nrm = form.PCG(dev(b), x, ess=dev(ess, torch.int32), rel_tol=1e-3, max_iter=500, jacobi=True)
+    xr, itr, nr = op.pcg(b, ess, rel_tol=1e-3, max_iter=500, jacobi=True)
+    assert it == itr and relerr(host(x), xr) < 1e-11
+
+
 def test_golden_vectors():
     g = np.load(f"{GOLDEN}/oracle_golden.npz")
     for order in (1, 2, 3):

@@ -256,81 +256,76 @@ __device__ void pcg_check_one(double bn, const PcgCheck &c)
 {
    if (c.ctl->done) { return; }
    const int done = bn <= c.r0 ? 1 : (c.it + 1 > c.max_iter ? 2 : 0);
-   if (!done) { return; }
-   c.ctl->done = done;
-   c.ctl->iters = c.it;
-   c.ctl->final = bn;
-   c.host->final = bn;
-   c.host->iters = c.it;
-   __threadfence_system();  // (the mirror's fields before its flag)
-   c.host->done = done;
+   if (done)
+   {
+      c.ctl->done = done;
+      c.ctl->iters = c.it;
+      c.ctl->final = bn;
+      c.host->final = bn;
+      c.host->iters = c.it;
+      __threadfence_system();  // (the mirror's fields before its flag)
+      c.host->done = done;
+   }
+   __threadfence_system();  // (the flag before the progress mark the host polls)
+   c.host->checked = c.it;
 }
 
-// The end of a one-pass deterministic dot over kDotBlocks workgroups: each workgroup reduces its
-// grid-stride sum, parks it in partials[blockIdx] as an agent-scope (write-through) store that is
-// acknowledged before the workgroup's arrival on the counter, and the last workgroup to arrive sums
-// the partials in the fixed order the former second kernel used (4 per thread in stride 256, the
-// wave shuffle tree, the 4 wave sums pairwise): the same value bit for bit, one launch fewer.  The
-// last workgroup re-arms the counter; optionally it runs the stopping test on the result.
-__device__ __forceinline__ void dot_finish(double s, double *__restrict__ partials, unsigned *__restrict__ arrivals,
-                                           double *__restrict__ out, double *__restrict__ hout, const PcgCheck *chk)
+// Deterministic dot, pass 1: each of kDotBlocks workgroups writes its grid-stride sum.  (A
+// one-pass form -- the last workgroup to arrive on a counter sums the parks -- was measured slower:
+// the 1,024 arrivals on one counter serialise, 16.6 vs 6.5 us per dot at a rank's 1.28M dofs,
+// profiles/r5/dot_probe.txt.)
+__device__ __forceinline__ void dot_park(double s, double *__restrict__ partials)
 {
    __shared__ double red[4];
-   __shared__ int last;
+   for (int off = 32; off > 0; off >>= 1) { s += __shfl_down(s, off, 64); }
+   if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6] = s; }
+   __syncthreads();
+   if (threadIdx.x == 0) { partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]); }
+}
+
+__global__ void __launch_bounds__(256)
+k_dot_partial(int n, const double *__restrict__ a, const double *__restrict__ b, double *__restrict__ partials,
+              const PcgCtl *__restrict__ ctl)
+{
+   if (ctl && ctl->done) { return; }  // (wave-uniform)
+   double s = 0.0;
+   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+   {
+      s += a[i] * b[i];
+   }
+   dot_park(s, partials);
+}
+
+// pass 2 (one workgroup): the partials in a fixed order; optionally the stopping test on the result
+__global__ void __launch_bounds__(256)
+k_dot_final(int nparts, const double *__restrict__ partials, double *__restrict__ out, double *__restrict__ hout,
+            const PcgCtl *__restrict__ ctl, PcgCheck chk, int with_check)
+{
+   if (ctl && ctl->done) { return; }
+   __shared__ double red[4];
+   double s = 0.0;
+   for (int i = threadIdx.x; i < nparts; i += blockDim.x) { s += partials[i]; }
    for (int off = 32; off > 0; off >>= 1) { s += __shfl_down(s, off, 64); }
    if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6] = s; }
    __syncthreads();
    if (threadIdx.x == 0)
    {
       const double v = (red[0] + red[1]) + (red[2] + red[3]);
-      __hip_atomic_store(partials + blockIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_s_waitcnt(0);  // the partial acknowledged before the arrival
-      last = __hip_atomic_fetch_add(arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-   }
-   __syncthreads();
-   if (!last) { return; }
-   double t = 0.0;
-   for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x)
-   {
-      t += __hip_atomic_load(partials + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-   }
-   for (int off = 32; off > 0; off >>= 1) { t += __shfl_down(t, off, 64); }
-   if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6] = t; }
-   __syncthreads();
-   if (threadIdx.x == 0)
-   {
-      const double v = (red[0] + red[1]) + (red[2] + red[3]);
       *out = v;
       if (hout) { *hout = v; }  // mapped pinned host mirror (the solver's read-back)
-      __hip_atomic_store(arrivals, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (chk) { pcg_check_one(v, *chk); }
+      if (with_check) { pcg_check_one(v, chk); }
    }
-}
-
-__global__ void __launch_bounds__(256)
-k_dot(int n, const double *__restrict__ a, const double *__restrict__ b, double *__restrict__ partials,
-      unsigned *__restrict__ arrivals, double *__restrict__ out, double *__restrict__ hout,
-      const PcgCtl *__restrict__ ctl)
-{
-   if (ctl && ctl->done) { return; }  // (every workgroup: the counter stays armed)
-   double s = 0.0;
-   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-   {
-      s += a[i] * b[i];
-   }
-   dot_finish(s, partials, arrivals, out, hout, nullptr);
 }
 
 // One fused PCG update (CGSolver::Mult's add/Mult(prec)/Dot sequence, solvers.cpp:930-960):
-// alpha = nom/den; x += alpha d; r -= alpha Ad; z = dinv .* r (jacobi) ; r.z (or r.r) in the fixed
-// grid-stride order of k_dot, finished by the last workgroup (and, serial, the stopping test).
+// alpha = nom/den; x += alpha d; r -= alpha Ad; z = dinv .* r (jacobi) ; the partial sums of r.z
+// (or r.r) in the fixed grid-stride order of k_dot_partial, finished by k_dot_final.
 // z holds A d on entry and the preconditioned residual on exit (jacobi only).
 __global__ void __launch_bounds__(256)
 k_pcg_step(int n, const double *__restrict__ nom, const double *__restrict__ den,
            const double *__restrict__ d, double *__restrict__ z, double *__restrict__ x,
            double *__restrict__ r, const double *__restrict__ dinv, double *__restrict__ partials,
-           unsigned *__restrict__ arrivals, double *__restrict__ out, double *__restrict__ hout,
-           const PcgCtl *__restrict__ ctl, PcgCheck chk, int with_check)
+           const PcgCtl *__restrict__ ctl)
 {
    if (ctl && ctl->done) { return; }
    const double alpha = *nom / *den;
@@ -348,7 +343,7 @@ k_pcg_step(int n, const double *__restrict__ nom, const double *__restrict__ den
       }
       else { s += rn * rn; }
    }
-   dot_finish(s, partials, arrivals, out, hout, with_check ? &chk : nullptr);
+   dot_park(s, partials);
 }
 
 // ConstrainedOperator around a Mult without a vector copy: saved = v[ess], v[ess] = 0 ...
@@ -602,14 +597,11 @@ void copy_values(int n, const int *idx, const double *x, double *y, hipStream_t 
    ECM2_HIP(hipGetLastError());
 }
 
-// partials: kDotBlocks values + the arrival counter (zero between launches)
-unsigned *dot_arrivals(double *partials) { return reinterpret_cast<unsigned *>(partials + kDotBlocks); }
-
 void dot(int n, const double *a, const double *b, double *partials, double *out, hipStream_t s, double *hout,
          const PcgCtl *ctl)
 {
-   hipLaunchKernelGGL(k_dot, dim3(kDotBlocks), dim3(256), 0, s, n, a, b, partials, dot_arrivals(partials), out, hout,
-                      ctl);
+   hipLaunchKernelGGL(k_dot_partial, dim3(kDotBlocks), dim3(256), 0, s, n, a, b, partials, ctl);
+   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, s, kDotBlocks, partials, out, hout, ctl, PcgCheck{}, 0);
    ECM2_HIP(hipGetLastError());
 }
 
@@ -619,8 +611,8 @@ void pcg_step(int n, const double *nom, const double *den, const double *d, doub
 {
    PcgCheck chk{stop ? stop->r0 : 0.0, stop ? stop->it : 0, stop ? stop->max_iter : 0,
                 stop ? stop->ctl : nullptr, stop ? stop->host : nullptr};
-   hipLaunchKernelGGL(k_pcg_step, dim3(kDotBlocks), dim3(256), 0, s, n, nom, den, d, z, x, r, dinv, partials,
-                      dot_arrivals(partials), out, hout, ctl, chk, stop ? 1 : 0);
+   hipLaunchKernelGGL(k_pcg_step, dim3(kDotBlocks), dim3(256), 0, s, n, nom, den, d, z, x, r, dinv, partials, ctl);
+   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, s, kDotBlocks, partials, out, hout, ctl, chk, stop ? 1 : 0);
    ECM2_HIP(hipGetLastError());
 }
 

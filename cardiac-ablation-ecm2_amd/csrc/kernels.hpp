@@ -416,11 +416,12 @@ void set_values(int n, const int *idx, double val, double *y, hipStream_t s);   
 void copy_values(int n, const int *idx, const double *x, double *y, hipStream_t s); // y[idx] = x[idx]
 // The device-driven PCG loop's state (device memory; the check kernel also writes it to a mapped
 // pinned host mirror): done = 0 running, 1 converged, 2 stopped at max_iter; iters, final = the
-// iteration and r.z at which it stopped.  The vector kernels of an iteration given `ctl` return at
-// once when done is set, so the host can enqueue iterations ahead of the stopping test.
+// iteration and r.z at which it stopped; checked (mirror) = the last iteration whose stopping test
+// ran.  The vector kernels of an iteration given `ctl` return at once when done is set, so the host
+// can enqueue an iteration before it has read the previous one's test.
 struct PcgCtl
 {
-   int done, iters;
+   int done, iters, checked, pad;
    double final;
 };
 // CGSolver's stopping test of iteration `it` (solvers.cpp:950-960) on the device: betanom <= r0 ->
@@ -432,11 +433,9 @@ struct PcgStop
    int it, max_iter;
    PcgCtl *ctl, *host;
 };
-// Deterministic one-pass dot (the last workgroup sums the per-workgroup partials in a fixed order):
-// result written to *out (device).  partials: kDotPartials doubles, zero-initialised once (the last
-// double is the arrival counter, re-armed by every launch).
+// Deterministic two-pass dot: result written to *out (device).  partials: kDotPartials doubles.
 // hout (optional): device pointer of mapped pinned host memory that also receives the result.
-constexpr int kDotPartials = 1024 + 1;
+constexpr int kDotPartials = 1024;
 void dot(int n, const double *a, const double *b, double *partials, double *out, hipStream_t s,
          double *hout = nullptr, const PcgCtl *ctl = nullptr);
 // Fused PCG update: x += (nom/den) d; r -= (nom/den) z; z = dinv .* r (dinv null: z untouched);

@@ -85,21 +85,16 @@ namespace
 // CGSolver's work vectors live across solves (CGSolver::SetOperator allocates them once,
 // solvers.cpp:869-880): one workspace per host thread and device, grown on demand, with a
 // mapped pinned scalar the final-dot kernels write the stopping-test value into.
-// Iterations the host enqueues ahead of the stopping test it has read (the device-driven loop).
-constexpr int kPcgAhead = 4;
-
 struct PCGWork
 {
    DeviceArray<double> r, d, z, saved, dinv, partials, scal;
    double *hs = nullptr, *hs_dev = nullptr;
    DeviceArray<kern::PcgCtl> ctl;                          // the device-driven loop's state
    kern::PcgCtl *hctl = nullptr, *hctl_dev = nullptr;      // its mapped pinned mirror
-   std::vector<hipEvent_t> ev;                             // per-iteration events (run-ahead window)
    ~PCGWork()
    {
       if (hs) { (void)hipHostFree(hs); }
       if (hctl) { (void)hipHostFree(hctl); }
-      for (hipEvent_t e : ev) { (void)hipEventDestroy(e); }
    }
    void ensure(int n, int n_ess, bool jacobi)
    {
@@ -111,11 +106,7 @@ struct PCGWork
       grow(z, std::max(n, 1));
       grow(saved, std::max(n_ess, 1));
       if (jacobi) { grow(dinv, std::max(n, 1)); }
-      if (partials.size() < (size_t)kern::kDotPartials)
-      {
-         partials.resize(kern::kDotPartials);  // (the one-pass dot's arrival counter must start at zero)
-         ECM2_HIP(hipMemset(partials.data(), 0, partials.bytes()));
-      }
+      grow(partials, kern::kDotPartials);
       grow(scal, 4);
       if (!hs)
       {
@@ -124,8 +115,6 @@ struct PCGWork
          ECM2_HIP(hipHostMalloc(&hctl, sizeof(kern::PcgCtl), hipHostMallocMapped));
          ECM2_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&hctl_dev), hctl, 0));
          ctl.resize(1);
-         ev.resize(kPcgAhead);
-         for (hipEvent_t &e : ev) { ECM2_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming)); }
       }
    }
 };
@@ -202,34 +191,46 @@ PCGResult pcg_solve(LinOp &A, const int *ess, int n_ess, const double *b, double
       // the device-driven loop's state, reset before the read-back below idles the stream (no
       // kernel of a previous solve writes the mirror any more: every solve ends synchronised)
       ECM2_HIP(hipMemsetAsync(w.ctl.data(), 0, sizeof(kern::PcgCtl), s));
-      w.hctl->done = 0;
-      w.hctl->iters = 0;
-      w.hctl->final = 0.0;
+      *w.hctl = kern::PcgCtl{};
       cmult(d, z);
       dot(z, d, den);
       if (readback(den) != 0.0)
       {
-         // CGSolver's loop (solvers.cpp:930-1000) driven by the device: the stopping test runs in a
-         // one-thread kernel after each r.z (and its all-reduce), and once it stops every later
-         // vector kernel returns at once.  The host enqueues iterations up to kPcgAhead ahead of the
-         // last one it has waited for, and ends when the mirror says the loop stopped at an
-         // iteration it has waited for -- the same iteration on every rank, so the ranks issue the
-         // same collectives.  The iterates are those of the host-tested loop (same kernels, same
-         // order); the wasted tail is <= kPcgAhead operator Mults per solve.
-         kern::PcgCtl *ctl = w.ctl.data(), *hm = w.hctl;  // (reset before the den read-back)
+         // CGSolver's loop (solvers.cpp:930-1000) driven by the device: the stopping test runs on
+         // the device after each r.z (in the fused update's last workgroup, or in a one-thread kernel
+         // after the all-reduce), and once it stops every later vector kernel returns at once.  The
+         // host enqueues iteration i as soon as the test of i - 1 has run (it polls the mirror's
+         // progress mark; no host synchronisation of the stream), so the queue holds the rest of
+         // iteration i - 1 while it does, and it ends at the iteration the device stopped at: the same
+         // iteration on every rank, so the ranks issue the same collectives.  The iterates are
+         // CGSolver's (same kernels, same order); at most one operator Mult (the stopping
+         // iteration's) runs after the stop.
+         kern::PcgCtl *ctl = w.ctl.data(), *hm = w.hctl;
+         auto vol = [](const int &v) { return *(volatile const int *)&v; };
+         // has the loop stopped at an iteration <= waited?  (waits until the test of `waited` ran)
          auto stopped_by = [&](int waited) {
-            const int dn = *(volatile int *)&hm->done;
-            return dn != 0 && *(volatile int *)&hm->iters <= waited;
-         };
-         int i = 1;
-         for (;; i++)
-         {
-            if (i > kPcgAhead)
+            for (long spin = 1;; spin++)
             {
-               const int waited = i - kPcgAhead;
-               ECM2_HIP(hipEventSynchronize(w.ev[waited % kPcgAhead]));
-               if (stopped_by(waited)) { break; }
+               if (vol(hm->checked) >= waited)
+               {
+                  // (the device writes done before checked: a stop at `waited` is visible now)
+                  return vol(hm->done) != 0 && vol(hm->iters) <= waited;
+               }
+               if (vol(hm->done) != 0) { return vol(hm->iters) <= waited; }
+               if (spin % 4096 == 0)
+               {
+                  const hipError_t e = hipStreamQuery(s);
+                  if (e == hipSuccess && vol(hm->checked) < waited && vol(hm->done) == 0)
+                  {
+                     ECM2_VERIFY(false, ERR_INTERNAL, "device PCG loop: stream idle before the test of iteration " << waited);
+                  }
+                  if (e != hipSuccess && e != hipErrorNotReady) { ECM2_HIP(e); }
+               }
             }
+         };
+         for (int i = 1;; i++)
+         {
+            if (i > 1 && stopped_by(i - 1)) { break; }
             // x += alpha d, r -= alpha A d, z = M^{-1} r, betanom = r.z in one pass
             const kern::PcgStop stop{r0, i, max_iter, ctl, w.hctl_dev};
             kern::pcg_step(n, nom, den, d, z, x, r, dinv, partials, betanom, s, nullptr, ctl, direct ? &stop : nullptr);
@@ -243,7 +244,6 @@ PCGResult pcg_solve(LinOp &A, const int *ess, int n_ess, const double *b, double
             cmult(d, z);
             dot(d, z, den, ctl);
             std::swap(nom, betanom);  // nom <- betanom
-            ECM2_HIP(hipEventRecord(w.ev[i % kPcgAhead], s));
          }
          ECM2_HIP(hipStreamSynchronize(s));
          ECM2_VERIFY(*(volatile int *)&hm->done != 0, ERR_INTERNAL, "device PCG loop ended without a stop");

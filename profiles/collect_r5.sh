@@ -6,6 +6,7 @@
 #   a: c4 (the headline: structured, affine + the k(T) coefficient snapshot), c4pen (the Pennes operator:
 #      both coefficients laws of one field, no per-point stream), c4ex16 (ex16p's M + dt K(u_alpha_gf))
 #   b: c5 (bricks, affine_e), c4ent (the reference's numbering with the snapshot)
+#   c: c4tri, c4enttrijac (the drop-in configuration), c5tri, c3
 set -uo pipefail
 SET=${1:-a}
 O=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/collect_r5
@@ -33,7 +34,13 @@ if [ "$SET" = a ]; then
   one c4 affine_ts apply --workload c4 --steps 50 --warmup 5 || exit 1
   one c4pen affine_tsm apply --workload c4 --coefficients pennes --steps 50 --warmup 5 || exit 1
   one c4ex16 affine_tsm apply --workload c4 --coefficients ex16 --steps 50 --warmup 5 || exit 1
-else
+elif [ "$SET" = b ]; then
   one c5 affine_e apply_brick --workload c5 --steps 30 --warmup 5 || exit 1
   one c4ent affine_ts apply --workload c4 --numbering entity --steps 50 --warmup 5 || exit 1
+else
+  # c: the TRILINEAR configurations and C3 at HEAD
+  one c4tri trilinear apply --workload c4 --mesh trilinear --steps 30 --warmup 5 || exit 1
+  one c4enttrijac trilinear apply --workload c4 --numbering entity --mesh trilinear --geometry-input jacobians --steps 30 --warmup 5 || exit 1
+  one c5tri trilinear_e apply_brick --workload c5 --mesh trilinear --steps 30 --warmup 5 || exit 1
+  one c3 affine_ts apply --workload c3 --steps 30 --warmup 5 || exit 1
 fi

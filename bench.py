@@ -454,16 +454,19 @@ def main():
     ap.add_argument("--member-graph", type=int, default=-1, choices=[-1, 0, 1],
                     help="--member: 1 replay one HIP graph per Mult, 0 launch the stages directly, "
                          "-1 as the RCCL form would (--par-graph, else the schedule's default)")
-    ap.add_argument("--pcg-iters", type=int, default=0,
+    ap.add_argument("--pcg-iters", type=int, default=-1,
                     help="also time K Jacobi-PCG iterations (no ess, rel_tol 1e-30): on one GPU the serial "
                          "form's solver; with --member the member as one rank's operator (its dots through "
-                         "a one-rank RCCL all-reduce, ecm2_operator_from_par_member)")
+                         "a one-rank RCCL all-reduce, ecm2_operator_from_par_member).  Default: 20 on the "
+                         "one-GPU line, 0 otherwise")
     ap.add_argument("--deadline", type=float, default=900.0,
                     help="seconds after which a rank prints its last stage and exits non-zero (0: none)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if args.pcg_iters < 0:
+        args.pcg_iters = 20 if (world == 1 and args.loopback <= 1 and args.workload != "c3") else 0
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dl = Deadline(args.deadline, rank)
     if world != args.gpus:
@@ -752,6 +755,7 @@ def main():
         }
         if pcg_it is not None:
             line["pcg_iteration"] = {"iterations": args.pcg_iters, "iteration_ms": round(pcg_it, 5),
+                                     "mdof_iter_per_s": round(fes.ndofs / (pcg_it * 1e-3) / 1e6, 1),
                                      "note": "marginal time per Jacobi-PCG iteration on the serial form (ecm2_pcg_solve: the "
                                              "device-driven loop), no ess: Mult + vector passes + two dots"}
         if reasm is not None:
@@ -840,8 +844,9 @@ def c3_pcg(E, torch, fes, form, max_iter=100):
             f"converged to rel_tol 1e-30 after {it} of max_iter = {max_iter} iterations")
     return {"iterations": it, "max_iter": max_iter, "seconds": round(dt, 4),
             "mdof_iter_per_s": round(fes.ndofs * it / dt / 1e6, 1), "reassembly_ms": round(reasm_ms, 3),
-            "note": f"Jacobi-PCG with rel_tol 1e-30 ({stop}); MDoF*iter/s over the iterations run, including the "
-                    "per-iteration 8-byte convergence read-back and the DIAG_ONE constraint passes"}
+            "note": f"Jacobi-PCG with rel_tol 1e-30 ({stop}); MDoF*iter/s over the whole solve (its setup -- the "
+                    "Jacobi diagonal, the first residual -- included), with the DIAG_ONE constraint passes and the "
+                    "device-driven stopping test"}
 
 
 def stream_copy_peak(E, torch, nbytes=1 << 30, reps=20):

@@ -59,6 +59,8 @@ def test_bench_single_gpu_line():
     # value = ndofs * steps / time
     assert b["value"] == pytest.approx(b["config"]["ndofs"] / (b["ms_per_step"] * 1e-3) / 1e6, rel=1e-3)
     assert b["config"]["numbering"].startswith("structured") and b["config"]["mesh"] == "affine"
+    # the one-GPU line carries the marginal Jacobi-PCG iteration (MDoF*iter/s)
+    assert b["pcg_iteration"]["iterations"] == 20 and b["pcg_iteration"]["iteration_ms"] > b["ms_per_step"]
     # the same run's variants: the reference's numbering (same layout: AFFINE with the k(T) snapshot on a
     # brick-tiled mesh), a trilinear mesh (TRILINEAR) and the drop-in configuration (+ MFEM Jacobians)
     assert b["entity_numbering"]["value"] > 0 and b["entity_numbering"]["qdata_layout"] == "affine_ts"

@@ -1530,6 +1530,23 @@ void PAForm::assemble_diagonal(double *diag, hipStream_t s)
 {
    ECM2_VERIFY(assembled_, ERR_STATE, "AssembleDiagonal before Assemble");
    if (ndofs_ == 0) { return; }
+   // The diagonal is a function of the assembled state alone (every setter clears assembled_, and
+   // Assemble bumps gen_): repeated requests between two Assembles -- a Jacobi smoother per PCG
+   // solve, three SDIRK stages on one T -- copy the first result instead of recomputing it (at C4
+   // with the snapshot: ~3 ms of expansion and diagonal kernels against a 25 us copy).
+   if (diag_gen_ == gen_ && diag_cache_.size() == (size_t)ndofs_)
+   {
+      ECM2_HIP(hipMemcpyAsync(diag, diag_cache_.data(), diag_cache_.bytes(), hipMemcpyDeviceToDevice, s));
+      return;
+   }
+   assemble_diagonal_uncached(diag, s);
+   diag_cache_.resize(ndofs_);
+   ECM2_HIP(hipMemcpyAsync(diag_cache_.data(), diag, diag_cache_.bytes(), hipMemcpyDeviceToDevice, s));
+   diag_gen_ = gen_;
+}
+
+void PAForm::assemble_diagonal_uncached(double *diag, hipStream_t s)
+{
    // The reference's AssembleDiagonal (bilinearform_ext.cpp:370-411) adds every integrator's
    // AssembleDiagonalPA into ONE localY and then zeroes a marked integrator's excluded elements of
    // that localY, so on those elements the contributions of the integrators added before it vanish

@@ -156,7 +156,7 @@ public:
    int nblocks() const { return layout_.nblk(); }
    bool has_mass() const { return have_mass_; }
    bool has_diffusion() const { return have_diff_; }
-   void assemble_diagonal(double *diag, hipStream_t s);
+   void assemble_diagonal(double *diag, hipStream_t s);  // cached per assembly (gen_)
 
    // Reference-shaped pieces (E-vector layout [e][nd], lexicographic).
    void restriction_mult(const double *x, double *xe, hipStream_t s);
@@ -188,6 +188,7 @@ private:
    // element weights [ne] of integrator kind k: 1 / 0 per its attribute marker, all 1 unmarked
    std::vector<double> marker_weights(int k) const;
    void diagonal_from_qdata(double *diag, hipStream_t s);
+   void assemble_diagonal_uncached(double *diag, hipStream_t s);
    // TRILINEAR(_E) forms and diffusion-only AFFINE(_E) forms: their per-point qdata in the BLOCKED
    // (p <= 2) or NATIVE (p >= 3) layout, expand_kind() (temporaries of the caller) for the
    // diagonal, the E-vector apply and the qdata export
@@ -221,6 +222,8 @@ private:
    int sh_nblk_owned_ = 0, sh_nblk_ = 0;
    DeviceArray<double> part_;                       // partial slots: TPE [blk][nd][64]; LINE [bricks | [e][nd]]
    bool assembled_ = false;
+   DeviceArray<double> diag_cache_;  // the diagonal of assembly diag_gen_ (assemble_diagonal)
+   long diag_gen_ = -1;
    long gen_ = 0;
    DeviceArray<double> ywork_;      // add_mult
    bool have_mass_ = false, have_diff_ = false;

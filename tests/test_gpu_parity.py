@@ -445,6 +445,20 @@ def test_coefficient_snapshot(numbering, mass):
         ye = torch.zeros(fes.ne * fes.nd, dtype=torch.float64, device="cuda")
         form.IntegratorAddMultPA(E.DIFFUSION, dev(xe), ye)
         assert relerr(host(ye).reshape(fes.ne, fes.nd), O.diffusion_apply(op.B, op.G, op.D, xe)) <= RTOL
+    # the diagonal is kept per assembly: a second request returns the same values; after T changes
+    # and the form is re-assembled it follows the new T (not the kept copy)
+    d2 = torch.empty_like(y)
+    form.AssembleDiagonal(d2)
+    assert torch.equal(d, d2)
+    T2 = T + 5.0 * np.sin(3.0 * fes.dof_coords()[:, 0])
+    Td.copy_(dev(T2))
+    form.Assemble()
+    form.AssembleDiagonal(d2)
+    beta2 = scale * (1.0 + slope * (O.interp_evector(T2[fes.gather_map()], order, q1d) - tref))
+    op2 = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=None if mass == "none" else a, beta=beta2)
+    dwant2 = op2.diagonal_markers(m.GetAttributes(), [("mass", [1, 0]), ("diffusion", None)]) \
+        if mass == "marked" else op2.diagonal()
+    assert relerr(host(d2), dwant2) < 1e-12 and relerr(host(d2), dwant) > 1e-9  # (the mass term dominates)
     # a marked diffusion integrator keeps the stored W beta
     f3 = E.BilinearForm(fes, element_order=eo)
     f3.AddDomainIntegrator(E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(dev(T), scale, slope, tref)), [1, 1])

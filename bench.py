@@ -328,6 +328,44 @@ def member_bench(args, E, torch, group, xs, ys, ndofs, workload, dl):
                               "pass per member"}), flush=True)
 
 
+def sdirk_step(E, torch, mesh, fes, keep, ode_type=23, dt=0.01):
+    """configs[4]'s unit of work: one implicit step of ex16p's ConductionOperator (examples/ex16p.cpp:
+    373-470, SDIRK33 ode.cpp:834-859) -- SetParameters(u) re-assembles T = M + c dt K(u) and K(u)
+    (K = DiffusionIntegrator(k(T)) through the snapshot kernel, M = MassIntegrator(rho c_eff(x) /
+    3.6e6: ex16's unit capacity)), then the three stage solves (constrained Jacobi-PCG, rel_tol 1e-8 as
+    ex16p, Dirichlet on the boundary).  One untimed step first; the timed step starts from its result."""
+    a, T = bioheat_coefficients(E, torch, mesh, fes)
+    a = a / 3.6e6
+    keep.extend([a, T])
+    c = E.ode_implicit_coeff(ode_type)
+    Tf, Kf = E.BilinearForm(fes), E.BilinearForm(fes)
+    Tf.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(a)))
+    Tf.AddDomainIntegrator(E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(T, 0.5 * c * dt, K_SLOPE, K_TREF)))
+    Kf.AddDomainIntegrator(E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(T, 0.5, K_SLOPE, K_TREF)))
+    ess = torch.as_tensor(fes.boundary_dofs()).cuda()
+    u = T.clone()
+    out = {}
+    for timed in (False, True):
+        T.copy_(u)  # SetParameters(u): the coefficient field is the current state
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        Tf.Assemble()
+        Kf.Assemble()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        ns, it, conv = E.ode_step(ode_type, E.Operator(Tf), E.Operator(Kf), dt, u, ess=ess, rel_tol=1e-8, max_iter=500)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        if timed:
+            out = {"ode": "SDIRK33", "dt": dt, "step_ms": round((t2 - t0) * 1e3, 3),
+                   "reassembly_ms": round((t1 - t0) * 1e3, 3), "solves_ms": round((t2 - t1) * 1e3, 3),
+                   "stage_solves": ns, "pcg_iterations": it, "converged": conv,
+                   "ms_per_iteration": round((t2 - t1) * 1e3 / max(it, 1), 4),
+                   "note": "ex16p's step: SetParameters (re-Assemble T = M + c dt K(u) and K(u)) + three constrained "
+                           "Jacobi-PCG stage solves (rel_tol 1e-8, boundary dofs held); wall time"}
+    return out
+
+
 def pcg_iteration_ms(torch, op, n, iters):
     """Marginal wall time per Jacobi-PCG iteration of `op` (an Operator, or a BilinearForm's own
     PCG): (t(2K) - t(K)) / K for solves of K and 2K iterations (no essential dofs, rel_tol 1e-30 so
@@ -459,6 +497,8 @@ def main():
                          "form's solver; with --member the member as one rank's operator (its dots through "
                          "a one-rank RCCL all-reduce, ecm2_operator_from_par_member).  Default: 20 on the "
                          "one-GPU line, 0 otherwise")
+    ap.add_argument("--sdirk", type=int, default=1, choices=[0, 1],
+                    help="one-GPU line: also time one ex16p SDIRK33 step on this workload's mesh (sdirk_step)")
     ap.add_argument("--deadline", type=float, default=900.0,
                     help="seconds after which a rank prints its last stage and exits non-zero (0: none)")
     args = ap.parse_args()
@@ -636,6 +676,9 @@ def main():
     reasm = reassembly_ms(torch, form) if (form is not None and args.workload != "c3") else None
     pcg_it = (pcg_iteration_ms(torch, form, fes.ndofs, args.pcg_iters)
               if (args.pcg_iters and form is not None and world == 1 and args.loopback <= 1) else None)
+    sdirk = (sdirk_step(E, torch, mesh, fes, keep)
+             if (args.sdirk and form is not None and world == 1 and args.loopback <= 1 and args.workload != "c3")
+             else None)
 
     # aggregate over ranks: total true dofs, max time; kernel ms per Mult (interior + boundary
     # launches of one Mult when partitioned); bytes per GPU
@@ -753,6 +796,8 @@ def main():
                                  mbytes_total / world, stream, use_pin=pin_ok, flops=alg_flops(order, ne_own)),
             "cpu_baseline": cpu,
         }
+        if sdirk is not None:
+            line["sdirk_step"] = sdirk
         if pcg_it is not None:
             line["pcg_iteration"] = {"iterations": args.pcg_iters, "iteration_ms": round(pcg_it, 5),
                                      "mdof_iter_per_s": round(fes.ndofs / (pcg_it * 1e-3) / 1e6, 1),

@@ -61,6 +61,9 @@ def test_bench_single_gpu_line():
     assert b["config"]["numbering"].startswith("structured") and b["config"]["mesh"] == "affine"
     # the one-GPU line carries the marginal Jacobi-PCG iteration (MDoF*iter/s)
     assert b["pcg_iteration"]["iterations"] == 20 and b["pcg_iteration"]["iteration_ms"] > b["ms_per_step"]
+    # and one ex16p SDIRK33 step (configs[4]'s unit of work) on the same mesh
+    st = b["sdirk_step"]
+    assert st["stage_solves"] == 3 and st["converged"] and st["pcg_iterations"] > 3 and st["step_ms"] > st["solves_ms"]
     # the same run's variants: the reference's numbering (same layout: AFFINE with the k(T) snapshot on a
     # brick-tiled mesh), a trilinear mesh (TRILINEAR) and the drop-in configuration (+ MFEM Jacobians)
     assert b["entity_numbering"]["value"] > 0 and b["entity_numbering"]["qdata_layout"] == "affine_ts"

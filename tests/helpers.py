@@ -113,13 +113,24 @@ def write_linear_mfem_mesh(path, V, E):
             f.write("%.17g %.17g %.17g\n" % tuple(v))
 
 
-def curved_jacobians(Xn, gm_geo, p_geo, q1d):
-    """GeometricFactors::JACOBIANS (mesh.cpp:15220-15273) of a curved mesh from its H1 nodes: J(q)[i][j]
-    = sum_a X_a[i] d_j phi_a(xi_q) over the element's lexicographic nodes (gm_geo: the order-p_geo
-    space's gather map, Xn: the node coordinates); returns J [ne][3 (j)][3 (i)][nq] -- the MFEM layout
-    NQ x 3 x 3 x NE in memory -- and the lexicographic node coordinates [ne][nd][3]."""
+def lagrange_tables(p, nodes1d, pts):
+    """B, G [len(pts)][p + 1]: the 1D Lagrange basis on `nodes1d` (ascending) and its derivative."""
     import oracle as O
-    B, G = O.dof_to_quad(p_geo, q1d)          # [Q][D]
+    rows = [O.basis_eval(p, nodes1d, y) for y in pts]
+    return np.array([r[0] for r in rows]), np.array([r[1] for r in rows])
+
+
+def curved_jacobians(Xn, gm_geo, p_geo, q1d, nodes1d=None):
+    """GeometricFactors::JACOBIANS (mesh.cpp:15220-15273) of a curved mesh from its nodes: J(q)[i][j]
+    = sum_a X_a[i] d_j phi_a(xi_q) over the element's lexicographic nodes (gm_geo: the order-p_geo
+    gather map of the nodes, Xn: the node coordinates; nodes1d: the 1D node positions, default the GLL
+    nodes of H1); returns J [ne][3 (j)][3 (i)][nq] -- the MFEM layout NQ x 3 x 3 x NE in memory -- and
+    the lexicographic node coordinates [ne][nd][3]."""
+    import oracle as O
+    if nodes1d is None:
+        B, G = O.dof_to_quad(p_geo, q1d)      # [Q][D]
+    else:
+        B, G = lagrange_tables(p_geo, nodes1d, O.gauss_legendre(q1d)[0])
     D = p_geo + 1
     Xe = Xn[gm_geo]                            # [ne][nd][3], nd lexicographic dx fastest
     ne = Xe.shape[0]
@@ -135,36 +146,64 @@ def curved_jacobians(Xn, gm_geo, p_geo, q1d):
     return J, Xe
 
 
+# LagrangeHexFiniteElement(3) (the legacy "Cubic" collection of data/fichera-q3.mesh) numbers its 8
+# interior nodes counter-clockwise per z layer (fe_fixed_order.cpp:3192-3199), H1 lexicographically:
+# interior lexicographic index L (a + 2b + 4c) -> the Cubic element's interior index
+CUBIC_INTERIOR = [0, 1, 3, 2, 4, 5, 7, 6]
+
+
+def curved_geometry_map(name, mesh_E, Xn):
+    """The gather map of a curved mesh's nodes in each element's lexicographic node order and the 1D
+    node positions: H1_3D_P2 (fichera-q2) -- the H1 order-2 numbering of the topology itself, GLL
+    nodes; Cubic (fichera-q3, the legacy collection) -- the H1 order-3 numbering of the topology (the
+    same vertex / edge / face / interior layout, the same edge and quad-face orders for every
+    orientation: fe_coll.cpp:867-898 against the H1 tables, fe_coll.cpp:1896-1903) with the interior
+    nodes permuted (CUBIC_INTERIOR), equispaced nodes (Lagrange1DFiniteElement, fe_fixed_order.cpp:2818)."""
+    E, mesh, coll = mesh_E[0], mesh_E[1], name
+    if coll == "H1_3D_P2":
+        geo = E.H1Space(mesh, 2, E.NUMBERING_ENTITY)
+        assert geo.ndofs == Xn.shape[0]
+        return 2, geo.gather_map(), None
+    assert coll == "Cubic", coll
+    geo = E.H1Space(mesh, 3, E.NUMBERING_ENTITY)
+    assert geo.ndofs == Xn.shape[0]
+    gm = geo.gather_map().copy()
+    pos = [(1 + a) + 4 * (1 + b) + 16 * (1 + c) for c in (0, 1) for b in (0, 1) for a in (0, 1)]
+    inner = gm[:, pos].copy()
+    for L in range(8):
+        gm[:, pos[L]] = inner[:, CUBIC_INTERIOR[L]]
+    return 3, gm, np.array([0.0, 1.0 / 3.0, 2.0 / 3.0, 1.0])
+
+
 def curved_fichera(tmpdir, order, q1d, name="fichera-q2.mesh"):
-    """The reference's curved fichera (data/fichera-q2.mesh: 7 hexes, H1_3D_P2 nodes, used by
-    tests/unit/fem/test_assembly_levels.cpp:260): (mesh, fes, J, X) -- the linear mesh of its topology
-    (the vertex nodes as corners; the library's numbering of an H1 space depends on the topology only),
-    the order-`order` H1 space on it, the curved map's Jacobians at the q1d^3 Gauss-Legendre points
+    """The reference's curved fichera meshes (data/fichera-q2.mesh: 7 hexes, H1_3D_P2 nodes, used by
+    tests/unit/fem/test_assembly_levels.cpp:260; data/fichera-q3.mesh: the legacy Cubic collection, the
+    mesh of test_pa_kernels.cpp:647): (mesh, fes, J, X) -- the linear mesh of its topology (the vertex
+    nodes as corners; the library's numbering of an H1 space depends on the topology only), the
+    order-`order` H1 space on it, the curved map's Jacobians at the q1d^3 Gauss-Legendre points
     [ne][3][3][nq] (MFEM layout), and the physical coordinates of the space's dofs (the curved map at
     each element's GLL nodes)."""
     import oracle as O
     path = os.path.join(GOLDEN, name)
     coll, Xn = read_mfem_nodes(path)
-    assert coll == "H1_3D_P2"
     lines = [ln.split("#")[0].strip() for ln in open(path)]
     lines = [ln for ln in lines if ln]
     i = lines.index("elements")
     ne = int(lines[i + 1])
     elems = np.array([[int(t) for t in lines[i + 2 + k].split()[2:]] for k in range(ne)], np.int32)
     nv = int(lines[lines.index("vertices") + 1])
-    lin = os.path.join(str(tmpdir), "fichera_q2_linear.mesh")
-    write_linear_mfem_mesh(lin, Xn[:nv], elems)   # (MFEM's H1 numbering puts the vertex dofs first)
-    mesh = load_pkg().Mesh(lin)
+    lin = os.path.join(str(tmpdir), name.replace(".mesh", "_linear.mesh"))
+    write_linear_mfem_mesh(lin, Xn[:nv], elems)   # (MFEM's numbering puts the vertex dofs first)
     E = load_pkg()
-    geo = E.H1Space(mesh, 2, E.NUMBERING_ENTITY)
-    assert geo.ndofs == Xn.shape[0]
-    J, Xe = curved_jacobians(Xn, geo.gather_map(), 2, q1d)
+    mesh = E.Mesh(lin)
+    pg, gm_geo, nodes1d = curved_geometry_map(coll, (E, mesh), Xn)
+    J, Xe = curved_jacobians(Xn, gm_geo, pg, q1d, nodes1d)
     fes = E.H1Space(mesh, order, E.NUMBERING_ENTITY)
     # the curved map at the order-p GLL nodes of every element, lexicographic, to the global dofs
-    gnodes, _ = O.gauss_lobatto(3)
+    gnodes = O.gauss_lobatto(pg + 1)[0] if nodes1d is None else nodes1d
     pnodes, _ = O.gauss_lobatto(order + 1)
-    Bp = np.array([O.basis_eval(2, gnodes, y)[0] for y in pnodes])   # [p+1][3]
-    Xl = Xe.reshape(ne, 3, 3, 3, 3)
+    Bp, _ = lagrange_tables(pg, gnodes, pnodes)          # [p+1][pg+1]
+    Xl = Xe.reshape(ne, pg + 1, pg + 1, pg + 1, 3)
     Xp = np.einsum("xa,yb,zc,ecbai->ezyxi", Bp, Bp, Bp, Xl).reshape(ne, -1, 3)
     X = np.empty((fes.ndofs, 3))
     X[fes.gather_map()] = Xp

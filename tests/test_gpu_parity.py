@@ -512,17 +512,20 @@ def test_marker_diagonal_keeps_assemble_time_state(snap):
     assert torch.equal(d, d2)
 
 
-@pytest.mark.parametrize("order,q1d", [(2, 4), (2, 5), (3, 5), (3, 6)])
-def test_curved_mesh_jacobians(tmp_path, order, q1d):
+@pytest.mark.parametrize("name,order,q1d", [("fichera-q2.mesh", 2, 4), ("fichera-q2.mesh", 2, 5), ("fichera-q2.mesh", 3, 5),
+                                         ("fichera-q2.mesh", 3, 6), ("fichera-q3.mesh", 3, 5), ("fichera-q3.mesh", 3, 6),
+                                         ("fichera-q3.mesh", 4, 6)])
+def test_curved_mesh_jacobians(tmp_path, name, order, q1d):
     """A curved (high-order-node) mesh through the drop-in boundary: the reference's data/fichera-q2.mesh
-    (H1_3D_P2 nodes; the curved fichera meshes of test_assembly_levels.cpp:230,260 and
-    test_pa_kernels.cpp:647) handed over as GeometricFactors::JACOBIANS at the rule's points
+    (H1_3D_P2 nodes) and data/fichera-q3.mesh (the legacy Cubic collection; the curved fichera meshes of
+    test_assembly_levels.cpp:230,260 and test_pa_kernels.cpp:647, the orders >= the map's so that the
+    linear function below is in the space) handed over as GeometricFactors::JACOBIANS at the rule's points
     (ecm2_pa_form_set_jacobians, as INTEGRATION.md's binding passes them).  No trilinear map produces
     them, so the form keeps the per-point layout; Q1D = p + 3 is the rule a quadratic mesh's
     MassIntegrator asks for (GetRule adds Trans.OrderW(), bilininteg.cpp:1450-1462).  Mult and diagonal
     against the oracle on the same Jacobians, and the geometry-independent identities through the HIP
     path (1^T M 1 = sum W det J, K 1 = 0, x^T K x = |g|^2 sum W det J for the linear x = g . X)."""
-    mesh, fes, J, X = H.curved_fichera(tmp_path, order, q1d)
+    mesh, fes, J, X = H.curved_fichera(tmp_path, order, q1d, name)
     gm = fes.gather_map()
     en = mesh.element_nodes()
     P = O.quad_points(en, q1d)           # (coefficient sample points: any smooth per-point values)

@@ -271,16 +271,19 @@ def test_anisotropic_coefficients_pa_equals_fa(ctype, order, with_mass):
         assert abs(z @ op.mult(x) - x @ op.mult(z)) > 1e-6 * abs(z @ op.mult(x))
 
 
-@pytest.mark.parametrize("order,q1d", [(2, 4), (2, 5), (3, 5), (3, 6)])
-def test_curved_mesh_oracle_known_answers(tmp_path, order, q1d):
-    """The reference's curved fichera (data/fichera-q2.mesh, H1_3D_P2 nodes; its PA parity tests run the
-    curved fichera meshes, test_assembly_levels.cpp:230,260, test_pa_kernels.cpp:647): the oracle built
+@pytest.mark.parametrize("name,order,q1d", [("fichera-q2.mesh", 2, 4), ("fichera-q2.mesh", 2, 5), ("fichera-q2.mesh", 3, 5),
+                                         ("fichera-q2.mesh", 3, 6), ("fichera-q3.mesh", 3, 5), ("fichera-q3.mesh", 3, 6),
+                                         ("fichera-q3.mesh", 4, 6)])
+def test_curved_mesh_oracle_known_answers(tmp_path, name, order, q1d):
+    """The reference's curved fichera meshes (data/fichera-q2.mesh, H1_3D_P2 nodes; data/fichera-q3.mesh,
+    the legacy Cubic collection; its PA parity tests run them, test_assembly_levels.cpp:230,260,
+    test_pa_kernels.cpp:647): the oracle built
     from the curved map's Jacobians (OracleOperator.from_jacobians) satisfies the identities that hold for
     any geometry -- 1^T M 1 = sum W det J (the quadrature of the volume), K 1 = 0, and for the linear
-    function x = g . X (in the space: the map is quadratic, p >= 2) x^T K x = |g|^2 sum W det J (grad x = g
+    function x = g . X (in the space: the map has degree 2 or 3, p >= it) x^T K x = |g|^2 sum W det J (grad x = g
     at every point) -- and the node numbering is pinned by the geometry: det J > 0 everywhere and each
     element's edge-midpoint nodes within the file's perturbation of their corners' mean."""
-    mesh, fes, J, X = H.curved_fichera(tmp_path, order, q1d)
+    mesh, fes, J, X = H.curved_fichera(tmp_path, order, q1d, name)
     W = O.cube_weights(q1d)
     detJ = np.linalg.det(np.transpose(J, (0, 3, 2, 1)))
     assert detJ.min() > 0.3
@@ -295,8 +298,15 @@ def test_curved_mesh_oracle_known_answers(tmp_path, order, q1d):
     g = np.array([0.3, -1.1, 0.7])
     x = X @ g
     assert abs(x @ K.mult(x) - (g @ g) * vol) < 1e-11 * (g @ g) * vol
-    # numbering pin: a wrong edge / face assignment puts nodes ~0.5 from where they belong
-    geo = H.load_pkg().H1Space(mesh, 2, H.load_pkg().NUMBERING_ENTITY)
-    _, Xn = H.read_mfem_nodes(os.path.join(H.GOLDEN, "fichera-q2.mesh"))
-    Xl = Xn[geo.gather_map()].reshape(-1, 3, 3, 3, 3)
-    assert np.abs(Xl[:, 0, 0, 1] - 0.5 * (Xl[:, 0, 0, 0] + Xl[:, 0, 0, 2])).max() < 0.15
+    # numbering pin: every node of an element sits within the file's perturbation (< 0.15) of the
+    # trilinear interpolation of its corners at its reference position; a wrong edge / face / interior
+    # assignment puts nodes >= 0.33 away (the plain H1 order-3 map on fichera-q3: 0.38)
+    E = H.load_pkg()
+    coll, Xn = H.read_mfem_nodes(os.path.join(H.GOLDEN, name))
+    pg, gm_geo, nodes1d = H.curved_geometry_map(coll, (E, mesh), Xn)
+    t = O.gauss_lobatto(pg + 1)[0] if nodes1d is None else nodes1d
+    Xl = Xn[gm_geo].reshape(-1, pg + 1, pg + 1, pg + 1, 3)
+    C = Xl[:, ::pg, ::pg, ::pg]
+    lin = np.stack([1.0 - t, t])                                        # [2][pg + 1]
+    tri = np.einsum("kc,jb,ia,ekjix->ecbax", lin, lin, lin, C)
+    assert np.abs(Xl - tri).max() < 0.15

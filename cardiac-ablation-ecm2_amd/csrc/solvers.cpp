@@ -112,7 +112,8 @@ struct PCGWork
       {
          ECM2_HIP(hipHostMalloc(&hs, 4 * sizeof(double), hipHostMallocMapped));
          ECM2_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&hs_dev), hs, 0));
-         ECM2_HIP(hipHostMalloc(&hctl, sizeof(kern::PcgCtl), hipHostMallocMapped));
+         // (coherent: the host polls it while kernels run)
+         ECM2_HIP(hipHostMalloc(&hctl, sizeof(kern::PcgCtl), hipHostMallocMapped | hipHostMallocCoherent));
          ECM2_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&hctl_dev), hctl, 0));
          ctl.resize(1);
       }
@@ -197,8 +198,8 @@ PCGResult pcg_solve(LinOp &A, const int *ess, int n_ess, const double *b, double
       if (readback(den) != 0.0)
       {
          // CGSolver's loop (solvers.cpp:930-1000) driven by the device: the stopping test runs on
-         // the device after each r.z (in the fused update's last workgroup, or in a one-thread kernel
-         // after the all-reduce), and once it stops every later vector kernel returns at once.  The
+         // the device after each r.z (in the dot's final pass, or in a one-thread kernel after the
+         // all-reduce), and once it stops every later vector kernel returns at once.  The
          // host enqueues iteration i as soon as the test of i - 1 has run (it polls the mirror's
          // progress mark; no host synchronisation of the stream), so the queue holds the rest of
          // iteration i - 1 while it does, and it ends at the iteration the device stopped at: the same

@@ -196,6 +196,64 @@ __global__ void __launch_bounds__(256) k_xcd(int n, const double *a, const doubl
    if (threadIdx.x == 0) { __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 }
 
+typedef double v2d __attribute__((ext_vector_type(2)));
+
+// the update's shape with two elements per thread (16-byte accesses), r.z summed in element order
+__global__ void __launch_bounds__(256) k_step_v2(int n, double al, const double *__restrict__ d, double *__restrict__ z,
+                                                 double *__restrict__ x, double *__restrict__ r,
+                                                 const double *__restrict__ dinv, double *parts)
+{
+   __shared__ double red[4];
+   double s = 0.0;
+   const int n2 = n / 2;
+   for (long p = (long)blockIdx.x * blockDim.x + threadIdx.x; p < n2; p += (long)gridDim.x * blockDim.x)
+   {
+      const v2d xv = reinterpret_cast<const v2d *>(x)[p], dv = reinterpret_cast<const v2d *>(d)[p];
+      const v2d rv = reinterpret_cast<const v2d *>(r)[p], zv = reinterpret_cast<const v2d *>(z)[p];
+      const v2d iv = reinterpret_cast<const v2d *>(dinv)[p];
+      reinterpret_cast<v2d *>(x)[p] = xv + al * dv;
+      const v2d rn = rv + (-al) * zv;
+      reinterpret_cast<v2d *>(r)[p] = rn;
+      const v2d zn = iv * rn;
+      reinterpret_cast<v2d *>(z)[p] = zn;
+      s += rn.x * zn.x;
+      s += rn.y * zn.y;
+   }
+   const double v = wg_sum(s, red);
+   if (threadIdx.x == 0) { parts[blockIdx.x] = v; }
+}
+
+__global__ void k_upd(int n, double be, const double *__restrict__ z, double *__restrict__ d)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n) { d[i] = z[i] + be * d[i]; }
+}
+
+__global__ void k_upd_v2(int n2, double be, const double *__restrict__ z, double *__restrict__ d)
+{
+   const int p = blockIdx.x * blockDim.x + threadIdx.x;
+   if (p < n2)
+   {
+      const v2d zv = reinterpret_cast<const v2d *>(z)[p], dv = reinterpret_cast<const v2d *>(d)[p];
+      reinterpret_cast<v2d *>(d)[p] = zv + be * dv;
+   }
+}
+
+__global__ void __launch_bounds__(256) k_partial_v2(int n, const double *__restrict__ a, const double *__restrict__ b,
+                                                    double *parts)
+{
+   __shared__ double red[4];
+   double s = 0.0;
+   for (long p = (long)blockIdx.x * blockDim.x + threadIdx.x; p < n / 2; p += (long)gridDim.x * blockDim.x)
+   {
+      const v2d av = reinterpret_cast<const v2d *>(a)[p], bv = reinterpret_cast<const v2d *>(b)[p];
+      s += av.x * bv.x;
+      s += av.y * bv.y;
+   }
+   const double v = wg_sum(s, red);
+   if (threadIdx.x == 0) { parts[blockIdx.x] = v; }
+}
+
 int main()
 {
    const int sizes[2] = {1277289, 10218313};  // an N = 8 rank's true dofs (C4), the whole C4 space
@@ -245,6 +303,10 @@ int main()
          hipLaunchKernelGGL(k_partial, dim3(1024), dim3(256), 0, 0, n, a, b, parts);
          hipLaunchKernelGGL(k_final, dim3(1), dim3(256), 0, 0, 1024, parts, out);
       });
+      run("two_v2", [&] {
+         hipLaunchKernelGGL(k_partial_v2, dim3(1024), dim3(256), 0, 0, n, a, b, parts);
+         hipLaunchKernelGGL(k_final, dim3(1), dim3(256), 0, 0, 1024, parts, out);
+      });
       run("two_u4", [&] {
          hipLaunchKernelGGL(k_partial_u4, dim3(1024), dim3(256), 0, 0, n, a, b, parts);
          hipLaunchKernelGGL(k_final, dim3(1), dim3(256), 0, 0, 1024, parts, out);
@@ -280,6 +342,24 @@ int main()
                         64.0 * n / (ms * 1e-3 / reps) / 1e12);
          };
          step("step", k_step, 1024);
+         step("step_v2", k_step_v2, 1024);
+         step("step_v2_512", k_step_v2, 512);
+         {
+            auto upd = [&](const char *name, auto launch) {
+               for (int w = 0; w < 10; w++) { launch(); }
+               CK(hipDeviceSynchronize());
+               CK(hipEventRecord(e0));
+               for (int r = 0; r < reps; r++) { launch(); }
+               CK(hipEventRecord(e1));
+               CK(hipEventSynchronize(e1));
+               float ms = 0;
+               CK(hipEventElapsedTime(&ms, e0, e1));
+               std::printf("n=%9d %-12s %8.2f us/launch  %6.2f TB/s (3 streams)\n", n, name, ms * 1e3 / reps,
+                           24.0 * n / (ms * 1e-3 / reps) / 1e12);
+            };
+            upd("upd", [&] { hipLaunchKernelGGL(k_upd, dim3((n + 255) / 256), dim3(256), 0, 0, n, 0.5, a, x5); });
+            upd("upd_v2", [&] { hipLaunchKernelGGL(k_upd_v2, dim3((n / 2 + 255) / 256), dim3(256), 0, 0, n / 2, 0.5, a, x5); });
+         }
          step("step_u4", k_step_u4, 1024);
          step("step_u4_2k", k_step_u4, 2048);
          step("step_4k", k_step, 4096);

@@ -354,6 +354,8 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
    __shared__ double sX[WPG][XR][64];  // gathered x; then the cross-wave face exchange
    const int lane = threadIdx.x & 63;
    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: block data in SGPRs
+   // (round-robin dispatch: the XCD-contiguous order of the lattice kernels is 2.6% slower here,
+   // profiles/r5/ab_xcd.txt)
    const int blk = blk_begin + (int)blockIdx.x * WPG + w;
    const bool wave_on = blk < blk_end;  // wave-uniform; every wave reaches the store's barriers
    const int e = blk * 64 + lane;
@@ -711,7 +713,7 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
    __shared__ double sY[WPG][XR][64]; // element outputs [a][lane]; then the cross-wave face exchange
    const int lane = threadIdx.x & 63;
    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-   const int blk = blk_begin + (int)blockIdx.x * WPG + w;
+   const int blk = blk_begin + xcd_contiguous((int)blockIdx.x, (int)gridDim.x) * WPG + w;  // (as k_apply_tpe_ts)
    const bool wave_on = blk < blk_end;  // wave-uniform; every wave reaches the barriers
    const int e = blk * 64 + lane;
    const bool active = wave_on && e < ne;
@@ -1007,7 +1009,9 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
    __shared__ double sU[WPG][XR][64];  // per wave: (x, T') lattice pairs; then the cross-wave face exchange
    const int lane = threadIdx.x & 63;
    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-   const int blk = blk_begin + (int)blockIdx.x * WPG + w;
+   // XCD-contiguous workgroup order: consecutive (Morton-adjacent) brick groups share one XCD's L2
+   // for the x / T' lattice faces they both gather (kernel -1.5..-2.3%, profiles/r5/ab_xcd.txt)
+   const int blk = blk_begin + xcd_contiguous((int)blockIdx.x, (int)gridDim.x) * WPG + w;
    const bool wave_on = blk < blk_end;  // wave-uniform; every wave reaches the barriers
    const int e = blk * 64 + lane;
    const bool active = wave_on && e < ne;

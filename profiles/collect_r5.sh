@@ -14,7 +14,9 @@ mkdir -p "$O"
 export TMPDIR=/tmp PIN_DATE=$(date -u +%Y-%m-%dT%H:%MZ) PIN_SCRIPT=profiles/collect_r5.sh
 one() {  # tag layout kernel_key bench-args...
   local tag=$1 layout=$2 key=$3; shift 3
-  local args="$* --no-cpu-baseline --full-layout 0 --variants 0"
+  # (no PCG / SDIRK sub-measurements: their forms run other instantiations of the same kernels,
+  # which the PMC passes would average in)
+  local args="$* --no-cpu-baseline --full-layout 0 --variants 0 --sdirk 0 --pcg-iters 0"
   local P="$O/prof_$tag"
   mkdir -p "$P"
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -T -d "$P/trace" -o run --output-format csv \

@@ -21,6 +21,12 @@ provenance) / its HIP-event time / 8 TB/s -- or, without a pin, the formulation'
 bytes (stored qdata + x + y + map) as a lower bound; `alg_ratio` = SURVEY §8(d)'s fixed
 algorithmic bytes (56 B per quadrature point) / the same time / 8 TB/s, which exceeds 1
 when the compressed (AFFINE) layout stores less than the formula counts.
+
+Beside the timed Mults (outside the timed region), the one-GPU line also carries the same
+run's variants (the reference's numbering, a trilinear mesh, the drop-in configuration, the full
+per-point layout, the Pennes and ex16p coefficient paths), the marginal Jacobi-PCG iteration
+(`pcg_iteration`, the device-driven loop) and one ex16p SDIRK33 step (`sdirk_step`), and the CPU
+oracle baseline.
 """
 import argparse
 import importlib.util

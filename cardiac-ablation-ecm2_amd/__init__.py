@@ -127,6 +127,7 @@ def load_library(path: str = LIB_PATH):
         "ecm2_pa_form_algorithmic_bytes": (i32, [vp, dp]),
         "ecm2_pa_form_destroy": (None, [vp]),
         "ecm2_pcg_solve": (i32, [vp, vp, i32, vp, vp, f64, f64, i32, i32, ip, dp, vp]),
+        "ecm2_pcg_last_converged": (i32, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name, None)
@@ -141,7 +142,15 @@ def load_library(path: str = LIB_PATH):
 def _check(rc: int):
     if rc != 0:
         msg = _lib.ecm2_last_error().decode(errors="replace")
-        raise ECM2Error(f"ecm2 error {rc}: {msg}")
+        err = ECM2Error(f"ecm2 error {rc}: {msg}")
+        err.code = rc
+        raise err
+
+
+def pcg_last_converged() -> bool:
+    """IterativeSolver::GetConverged() of this thread's last PCG solve (BilinearForm.PCG,
+    Operator.PCG): False after CGSolver's (B r, r) < 0 or (A d, d) == 0 stops and at max_iter."""
+    return bool(load_library().ecm2_pcg_last_converged())
 
 
 def _np_ptr(a: np.ndarray):

@@ -42,6 +42,7 @@ struct ecm2_operator
 namespace
 {
 thread_local std::string g_last_error;
+thread_local int g_pcg_converged = 0;  // IterativeSolver::GetConverged() of the thread's last PCG
 
 template <typename F>
 int guard(F &&fn)
@@ -562,17 +563,21 @@ void ecm2_pa_form_destroy(ecm2_pa_form *f)
    if (f) { delete f->f; delete f; }
 }
 
+int ecm2_pcg_last_converged(void) { return g_pcg_converged; }
+
 int ecm2_pcg_solve(ecm2_pa_form *f, const int *ess, int n_ess, const double *b, double *x,
                    double rel_tol, double abs_tol, int max_iter, int jacobi, int *iterations,
                    double *final_norm, void *stream)
 {
    return guard([&] {
       NEED(f); NEED(b); NEED(x);
+      g_pcg_converged = 0;
       ECM2_VERIFY(n_ess == 0 || ess, ecm2::ERR_ARG, "null essential dof list");
       const ecm2::PCGResult r = ecm2::pcg_solve(*f->f, ess, n_ess, b, x, rel_tol, abs_tol,
                                                 max_iter, jacobi != 0, S(stream));
       if (iterations) { *iterations = r.iterations; }
       if (final_norm) { *final_norm = r.final_norm; }
+      g_pcg_converged = r.converged ? 1 : 0;
    });
 }
 
@@ -931,11 +936,13 @@ int ecm2_operator_pcg(ecm2_operator *op, const int *ess, int n_ess, const double
 {
    return guard([&] {
       NEED(op); NEED(b); NEED(x);
+      g_pcg_converged = 0;
       ECM2_VERIFY(n_ess == 0 || ess, ecm2::ERR_ARG, "null essential dof list");
       const ecm2::PCGResult r = ecm2::pcg_solve(*op->op, ess, n_ess, b, x, rel_tol, abs_tol, max_iter,
                                                 jacobi != 0, S(stream));
       if (iterations) { *iterations = r.iterations; }
       if (final_norm) { *final_norm = r.final_norm; }
+      g_pcg_converged = r.converged ? 1 : 0;
    });
 }
 

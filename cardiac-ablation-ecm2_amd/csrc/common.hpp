@@ -35,7 +35,8 @@ enum Status : int
    ERR_IO = 4,        // mesh file problems
    ERR_UNSUPPORTED = 5,
    ERR_COMM = 6,      // RCCL failure
-   ERR_INTERNAL = 7
+   ERR_INTERNAL = 7,
+   ERR_NUMERIC = 8    // non-finite value where the reference's MFEM_VERIFY(IsFinite) aborts
 };
 
 #define ECM2_VERIFY(cond, code, msg)                                          \

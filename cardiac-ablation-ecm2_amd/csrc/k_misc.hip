@@ -12,6 +12,12 @@ namespace
 {
 using namespace dev;
 using kern::PcgCtl;
+using kern::PCG_RUNNING;
+using kern::PCG_CONVERGED;
+using kern::PCG_MAX_ITER;
+using kern::PCG_NEG_BR;
+using kern::PCG_DEN_ZERO;
+using kern::PCG_NONFINITE;
 
 // Workgroup per element (lane per quadrature point), any layout, L- or E-vectors in and
 // out (in_e / out_e): six 1D stages through LDS, the reference's smem kernels' structure
@@ -244,30 +250,53 @@ __global__ void k_copy_values(int n, const int *__restrict__ idx, const double *
 
 constexpr int kDotBlocks = 1024;
 
-// CGSolver's stopping test (solvers.cpp:950-960) as the device-driven loop runs it
+// CGSolver's stopping tests (solvers.cpp:950-1000) as the device-driven loop runs them.
+// kind 0: the test of iteration `it` on betanom = (B r, r): not finite -> MFEM_VERIFY's abort
+// (PCG_NONFINITE, the host raises ECM2_ERR_NUMERIC); < 0 -> not converged (the preconditioner is not
+// positive definite, :955-964); <= r0 -> converged (:972-977); it + 1 > max_iter -> stopped (:979-982).
+// kind 1: the test of den = (A d, d) in iteration it's tail, after ++i (`it` is then the next
+// iteration's number, :993-1004): not finite -> abort; == 0 -> stopped, not converged, final_iter = it.
 struct PcgCheck
 {
    double r0;
    int it, max_iter;
    PcgCtl *ctl, *host;
+   const double *betanom;
+   int kind;
 };
 
-__device__ void pcg_check_one(double bn, const PcgCheck &c)
+__device__ void pcg_check_one(double v, const PcgCheck &c)
 {
    if (c.ctl->done) { return; }
-   const int done = bn <= c.r0 ? 1 : (c.it + 1 > c.max_iter ? 2 : 0);
+   int done;
+   double fin = v;
+   if (c.kind == 0)
+   {
+      done = !isfinite(v) ? PCG_NONFINITE
+             : v < 0.0    ? PCG_NEG_BR
+             : v <= c.r0  ? PCG_CONVERGED
+             : (c.it + 1 > c.max_iter ? PCG_MAX_ITER : PCG_RUNNING);
+   }
+   else
+   {
+      done = !isfinite(v) ? PCG_NONFINITE : (v == 0.0 ? PCG_DEN_ZERO : PCG_RUNNING);
+      fin = *c.betanom;  // (final_norm = sqrt(betanom) of the iteration, :1047)
+   }
    if (done)
    {
       c.ctl->done = done;
       c.ctl->iters = c.it;
-      c.ctl->final = bn;
-      c.host->final = bn;
+      c.ctl->final = fin;
+      c.host->final = fin;
       c.host->iters = c.it;
       __threadfence_system();  // (the mirror's fields before its flag)
       c.host->done = done;
    }
-   __threadfence_system();  // (the flag before the progress mark the host polls)
-   c.host->checked = c.it;
+   if (c.kind == 0)
+   {
+      __threadfence_system();  // (the flag before the progress mark the host polls)
+      c.host->checked = c.it;
+   }
 }
 
 // Deterministic dot, pass 1: each of kDotBlocks workgroups writes its grid-stride sum.  (A
@@ -283,9 +312,10 @@ __device__ __forceinline__ void dot_park(double s, double *__restrict__ partials
    if (threadIdx.x == 0) { partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]); }
 }
 
+// (ctl: read only when no check writes it in the same kernel -- no __restrict__ on it)
 __global__ void __launch_bounds__(256)
 k_dot_partial(int n, const double *__restrict__ a, const double *__restrict__ b, double *__restrict__ partials,
-              const PcgCtl *__restrict__ ctl)
+              const PcgCtl *ctl)
 {
    if (ctl && ctl->done) { return; }  // (wave-uniform)
    double s = 0.0;
@@ -296,10 +326,10 @@ k_dot_partial(int n, const double *__restrict__ a, const double *__restrict__ b,
    dot_park(s, partials);
 }
 
-// pass 2 (one workgroup): the partials in a fixed order; optionally the stopping test on the result
+// pass 2 (one workgroup): the partials in a fixed order; optionally a stopping test on the result
 __global__ void __launch_bounds__(256)
 k_dot_final(int nparts, const double *__restrict__ partials, double *__restrict__ out, double *__restrict__ hout,
-            const PcgCtl *__restrict__ ctl, PcgCheck chk, int with_check)
+            const PcgCtl *ctl, PcgCheck chk, int with_check)
 {
    if (ctl && ctl->done) { return; }
    __shared__ double red[4];
@@ -317,33 +347,59 @@ k_dot_final(int nparts, const double *__restrict__ partials, double *__restrict_
    }
 }
 
-// One fused PCG update (CGSolver::Mult's add/Mult(prec)/Dot sequence, solvers.cpp:930-960):
-// alpha = nom/den; x += alpha d; r -= alpha Ad; z = dinv .* r (jacobi) ; the partial sums of r.z
-// (or r.r) in the fixed grid-stride order of k_dot_partial, finished by k_dot_final.
-// z holds A d on entry and the preconditioned residual on exit (jacobi only).
+// The residual half of CGSolver's update (solvers.cpp:930-947): alpha = nom/den; r -= alpha A d;
+// z = dinv .* r (jacobi) and the partial sums of r.z (or r.r) in the fixed grid-stride order of
+// k_dot_partial, finished by k_dot_final.  z holds A d on entry; z is not stored (k_pcg_update_xd
+// forms it again from r where it is consumed: 4 vector streams here instead of 8).  x += alpha d is
+// deferred to k_pcg_update_xd (or k_pcg_finish_x after the stop), which reads d anyway.  Same
+// arithmetic per entry as CGSolver's add / Mult(prec) / Dot.  alpha_out: alpha of the last step run.
 __global__ void __launch_bounds__(256)
-k_pcg_step(int n, const double *__restrict__ nom, const double *__restrict__ den,
-           const double *__restrict__ d, double *__restrict__ z, double *__restrict__ x,
-           double *__restrict__ r, const double *__restrict__ dinv, double *__restrict__ partials,
-           const PcgCtl *__restrict__ ctl)
+k_pcg_step_r(int n, const double *__restrict__ nom, const double *__restrict__ den, const double *__restrict__ z,
+             double *__restrict__ r, const double *__restrict__ dinv, double *__restrict__ partials,
+             double *__restrict__ alpha_out, const PcgCtl *ctl)
 {
    if (ctl && ctl->done) { return; }
    const double alpha = *nom / *den;
+   if (blockIdx.x == 0 && threadIdx.x == 0) { *alpha_out = alpha; }
    double s = 0.0;
    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
    {
-      x[i] = x[i] + alpha * d[i];
       const double rn = r[i] + (-alpha) * z[i];
       r[i] = rn;
-      if (dinv)
-      {
-         const double zn = dinv[i] * rn;
-         z[i] = zn;
-         s += rn * zn;
-      }
+      if (dinv) { s += rn * (dinv[i] * rn); }
       else { s += rn * rn; }
    }
    dot_park(s, partials);
+}
+
+// The direction half (solvers.cpp:930, 985-990): x += alpha d (this iteration's alpha = nom/den,
+// deferred from k_pcg_step_r), then d = z + (betanom/nom) d with z = dinv .* r formed here.
+// 6 vector streams (x, d, r, dinv read; x, d written) instead of k_pcg_step's x part and
+// k_pcg_update_d's 3 + the stored z.
+__global__ void __launch_bounds__(256)
+k_pcg_update_xd(int n, const double *__restrict__ nom, const double *__restrict__ den,
+                const double *__restrict__ betanom, double *__restrict__ x, double *__restrict__ d,
+                const double *__restrict__ r, const double *__restrict__ dinv, const PcgCtl *ctl)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i >= n || (ctl && ctl->done)) { return; }
+   const double alpha = *nom / *den, beta = *betanom / *nom;
+   const double dold = d[i];
+   x[i] = x[i] + alpha * dold;
+   const double z = dinv ? dinv[i] * r[i] : r[i];
+   d[i] = z + beta * dold;
+}
+
+// After the loop: the stopping iteration's x += alpha d, when the stop came from its betanom test
+// (converged, max_iter, (B r, r) < 0: CGSolver has already added alpha d then); a den == 0 stop
+// comes after k_pcg_update_xd has run (x complete).
+__global__ void k_pcg_finish_x(int n, const double *__restrict__ alpha, const double *__restrict__ d,
+                               double *__restrict__ x, const PcgCtl *ctl)
+{
+   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+   const int done = ctl->done;
+   if (i >= n || !(done == PCG_CONVERGED || done == PCG_MAX_ITER || done == PCG_NEG_BR)) { return; }
+   x[i] = x[i] + *alpha * d[i];
 }
 
 // ConstrainedOperator around a Mult without a vector copy: saved = v[ess], v[ess] = 0 ...
@@ -369,18 +425,8 @@ __global__ void k_pcg_precond(int n, const double *__restrict__ dinv, const doub
    if (i < n) { z[i] = dinv ? dinv[i] * r[i] : r[i]; }
 }
 
-__global__ void k_pcg_update_d(int n, const double *__restrict__ betanom,
-                               const double *__restrict__ nom, const double *__restrict__ z,
-                               double *__restrict__ d, const PcgCtl *__restrict__ ctl)
-{
-   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-   if (i >= n || (ctl && ctl->done)) { return; }
-   const double beta = *betanom / *nom;
-   d[i] = z[i] + beta * d[i];
-}
-
-// one thread: the stopping test after a distributed r.z's all-reduce
-__global__ void k_pcg_check(const double *__restrict__ betanom, PcgCheck chk) { pcg_check_one(*betanom, chk); }
+// one thread: a stopping test after a distributed dot's all-reduce
+__global__ void k_pcg_check(const double *__restrict__ v, PcgCheck chk) { pcg_check_one(*v, chk); }
 
 __global__ void k_scale(int n, double a, double *__restrict__ y)
 {
@@ -597,29 +643,49 @@ void copy_values(int n, const int *idx, const double *x, double *y, hipStream_t 
    ECM2_HIP(hipGetLastError());
 }
 
+static PcgCheck to_check(const PcgStop *stop)
+{
+   return stop ? PcgCheck{stop->r0, stop->it, stop->max_iter, stop->ctl, stop->host, stop->betanom, stop->kind}
+               : PcgCheck{};
+}
+
 void dot(int n, const double *a, const double *b, double *partials, double *out, hipStream_t s, double *hout,
-         const PcgCtl *ctl)
+         const PcgCtl *ctl, const PcgStop *stop)
 {
    hipLaunchKernelGGL(k_dot_partial, dim3(kDotBlocks), dim3(256), 0, s, n, a, b, partials, ctl);
-   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, s, kDotBlocks, partials, out, hout, ctl, PcgCheck{}, 0);
+   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, s, kDotBlocks, partials, out, hout, ctl, to_check(stop),
+                      stop ? 1 : 0);
    ECM2_HIP(hipGetLastError());
 }
 
-void pcg_step(int n, const double *nom, const double *den, const double *d, double *z, double *x, double *r,
-              const double *dinv, double *partials, double *out, hipStream_t s, double *hout, const PcgCtl *ctl,
-              const PcgStop *stop)
+void pcg_step_r(int n, const double *nom, const double *den, const double *z, double *r, const double *dinv,
+                double *partials, double *out, double *alpha, hipStream_t s, const PcgCtl *ctl, const PcgStop *stop)
 {
-   PcgCheck chk{stop ? stop->r0 : 0.0, stop ? stop->it : 0, stop ? stop->max_iter : 0,
-                stop ? stop->ctl : nullptr, stop ? stop->host : nullptr};
-   hipLaunchKernelGGL(k_pcg_step, dim3(kDotBlocks), dim3(256), 0, s, n, nom, den, d, z, x, r, dinv, partials, ctl);
-   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, s, kDotBlocks, partials, out, hout, ctl, chk, stop ? 1 : 0);
+   hipLaunchKernelGGL(k_pcg_step_r, dim3(kDotBlocks), dim3(256), 0, s, n, nom, den, z, r, dinv, partials, alpha, ctl);
+   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, s, kDotBlocks, partials, out, nullptr, ctl, to_check(stop),
+                      stop ? 1 : 0);
    ECM2_HIP(hipGetLastError());
 }
 
-void pcg_check(const double *betanom, const PcgStop &stop, hipStream_t s)
+void pcg_update_xd(int n, const double *nom, const double *den, const double *betanom, double *x, double *d,
+                   const double *r, const double *dinv, hipStream_t s, const PcgCtl *ctl)
 {
-   PcgCheck chk{stop.r0, stop.it, stop.max_iter, stop.ctl, stop.host};
-   hipLaunchKernelGGL(k_pcg_check, dim3(1), dim3(1), 0, s, betanom, chk);
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_pcg_update_xd, dim3(grid_for(n, 256)), dim3(256), 0, s, n, nom, den, betanom, x, d, r, dinv,
+                      ctl);
+   ECM2_HIP(hipGetLastError());
+}
+
+void pcg_finish_x(int n, const double *alpha, const double *d, double *x, hipStream_t s, const PcgCtl *ctl)
+{
+   if (n == 0) { return; }
+   hipLaunchKernelGGL(k_pcg_finish_x, dim3(grid_for(n, 256)), dim3(256), 0, s, n, alpha, d, x, ctl);
+   ECM2_HIP(hipGetLastError());
+}
+
+void pcg_check(const double *v, const PcgStop &stop, hipStream_t s)
+{
+   hipLaunchKernelGGL(k_pcg_check, dim3(1), dim3(1), 0, s, v, to_check(&stop));
    ECM2_HIP(hipGetLastError());
 }
 
@@ -640,13 +706,6 @@ void ess_restore(int n, const int *idx, const double *saved, double *v, double *
 void pcg_precond(int n, const double *dinv, const double *r, double *z, hipStream_t s)
 {
    hipLaunchKernelGGL(k_pcg_precond, dim3(grid_for(n, 256)), dim3(256), 0, s, n, dinv, r, z);
-   ECM2_HIP(hipGetLastError());
-}
-
-void pcg_update_d(int n, const double *betanom, const double *nom, const double *z, double *d,
-                  hipStream_t s, const PcgCtl *ctl)
-{
-   hipLaunchKernelGGL(k_pcg_update_d, dim3(grid_for(n, 256)), dim3(256), 0, s, n, betanom, nom, z, d, ctl);
    ECM2_HIP(hipGetLastError());
 }
 

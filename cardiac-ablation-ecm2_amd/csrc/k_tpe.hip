@@ -50,7 +50,9 @@ struct TpeReg
 // two holders as two contiguous runs), any other block as [a][lane].  regf 1 also computes the
 // dofs from the lattice (no map reads); regf 2 reads them from the map (dofs not a lattice).
 // MAYREG: regf may be nonzero (per block).
-template <int D, bool SPLIT, bool SIGNS, bool XW, bool MAYREG = false>
+// XR: rows per wave of xb (a kernel whose waves stage more than XwaveRows rows passes its stride, so
+// a wave's sends land in its own region while the other waves may still read theirs).
+template <int D, bool SPLIT, bool SIGNS, bool XW, bool MAYREG = false, int XR = XwaveRows<D>::R>
 __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], const int *__restrict__ mp, int fl,
                                                    int blk, int lane, bool active, int n_owned,
                                                    double *__restrict__ y, double *__restrict__ yg,
@@ -58,7 +60,8 @@ __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], cons
                                                    TpeReg rg = {}, int regf = 0, int pstride = D * D * D * 64,
                                                    const int *__restrict__ lm = nullptr)
 {
-   constexpr int ND = D * D * D, XR = XwaveRows<D>::R;
+   constexpr int ND = D * D * D;
+   static_assert(XR >= XwaveRows<D>::R, "staging rows");
    const bool rr = MAYREG && regf == 1, rs = MAYREG && regf != 0, rl = MAYREG && regf == 2;
    // A lattice-map block's store entries are loaded here, before the face merges: their latency
    // (the map left L2 while the block computed) overlaps the shuffles and barriers instead of
@@ -678,6 +681,19 @@ __device__ __forceinline__ unsigned lattice_xyz(int j)
    static_assert(D == 3, "p = 2 lattice table");
    return kLatXYZ3.v[j];
 }
+// The padded LDS slot (tsl_slot, kernels.hpp) of each lattice slot j, for k_apply_tpe_ts's gather.
+struct LatticeTsl
+{
+   static constexpr int N = tpe_lattice_points(3);
+   unsigned short v[N];
+   constexpr LatticeTsl() : v()
+   {
+      for (int Z = 0; Z < 9; Z++)
+         for (int Y = 0; Y < 9; Y++)
+            for (int X = 0; X < 9; X++) { v[tpe_lattice_slot(3, X, Y, Z)] = (unsigned short)tsl_slot(X, Y, Z); }
+   }
+};
+__constant__ LatticeTsl kLatTsl3 = LatticeTsl();
 
 // pairs of the TRILINEAR coefficients (c[3 (k - 1) + i] two per pair) that only the per-plane J
 // pieces read: k = 0, 1, 3 -> f = 0..5, 9..11 -> pairs 0, 1, 2, 5 (pair 4 also holds f = 8, a row one)
@@ -1005,8 +1021,10 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
    constexpr bool MASS = MM != 0;
    constexpr int ND = D * D * D, NR = Q * Q, XR = XwaveRows<D>::R, WPG = 4, P = D - 1;
    constexpr int NLP = tpe_lattice_points(D);
-   static_assert(2 * NLP <= XR * 64, "x and T' lattices fit a wave's exchange rows");
-   __shared__ double sU[WPG][XR][64];  // per wave: (x, T') lattice pairs; then the cross-wave face exchange
+   // rows per wave: the padded (x, T') image (tsl_points pairs, conflict-free 16-byte reads), which
+   // the cross-wave face exchange (XR rows) reuses
+   constexpr int XRS = (2 * tsl_points() + 63) / 64 > XR ? (2 * tsl_points() + 63) / 64 : XR;
+   __shared__ double sU[WPG][XRS][64];  // per wave: (x, T') lattice pairs; then the cross-wave face exchange
    const int lane = threadIdx.x & 63;
    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
    // XCD-contiguous workgroup order: consecutive (Morton-adjacent) brick groups share one XCD's L2
@@ -1063,16 +1081,16 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                d = rg.base + (int)(v & 31) * rg.sx + (int)((v >> 5) & 31) * rg.sy + (int)(v >> 10) * rg.sz;
             }
             // (lattice-map blocks: the snapshot is stored in their slot order, a contiguous read)
-            sPL[j] = v2d{(!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned], RM == 3 ? tsn[(size_t)blk * NLP + j] : tsn[d]};
+            sPL[kLatTsl3.v[j]] = v2d{(!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned], RM == 3 ? tsn[(size_t)blk * NLP + j] : tsn[d]};
          }
       }
    }
    __syncthreads();  // the lattices are read by every lane of the wave
    if (wave_on)
    {
-      auto lane_base = [&](int cx, int cy) {
+      auto lane_base = [&](int cx, int cy) {  // (the padded image: tsl_slot)
          const int nx = tpe_lattice_class_n(cx), ny = tpe_lattice_class_n(cy);
-         return (ez * ny + ey) * nx + ex;
+         return ez * tsl_sz(nx, ny) + ey * tsl_sy(nx) + ex;
       };
       auto plane = [&](const int qz) {
          double bz[D], gz[D], wz[D];
@@ -1095,7 +1113,7 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                {
                   const int cx = dx % P, cy = dy % P, cz = dz % P;
                   const int nx = tpe_lattice_class_n(cx), ny = tpe_lattice_class_n(cy);
-                  const int sl = tpe_lattice_class_off(D, cx, cy, cz) + ((dz / P) * ny + dy / P) * nx + dx / P;
+                  const int sl = tsl_class_off(cx, cy, cz) + (dz / P) * tsl_sz(nx, ny) + (dy / P) * tsl_sy(nx) + dx / P;
                   const v2d ct = sPL[lb + sl];
                   const double c = ct.x, t = ct.y;
                   zb += bz[dz] * c;
@@ -1205,9 +1223,9 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 #pragma unroll
       for (int qz = 0; qz < Q; qz++) { plane(qz); }
    }  // wave_on
-   tpe_assemble_store<D, SPLIT, false, true, true>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0, blk, lane,
-                                                  active, n_owned, y, yg, part, &sU[0][0][0], w, wave_on, rg, regf,
-                                                  pstride, lmap ? lmap + (size_t)blk * NLP : nullptr);
+   tpe_assemble_store<D, SPLIT, false, true, true, XRS>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0, blk, lane,
+                                                       active, n_owned, y, yg, part, &sU[0][0][0], w, wave_on, rg, regf,
+                                                       pstride, lmap ? lmap + (size_t)blk * NLP : nullptr);
 }
 
 // Latency variant of k_apply_tpe_sf for small block ranges (the boundary elements of the

@@ -317,6 +317,60 @@ __host__ __device__ constexpr int tpe_lattice_slot(int D, int X, int Y, int Z)
    return tpe_lattice_class_off(D, cx, cy, cz) + ((Z / P) * ny + (Y / P)) * nx + (X / P);
 }
 
+// LDS image of a p = 2 block lattice for 16-byte reads (k_apply_tpe_ts: an (x, T') pair per point).
+// Lane (ex, ey, ez) of the plane loop reads class (cx, cy, cz) at ez sz + ey sy + ex plus a
+// wave-uniform offset; ds_read_b128 serves a wave in four 16-lane groups ({0-3, 12-15, 20-27},
+// {4-11, 16-19, 28-31} and the same +32), each conflict-free iff its 16 lanes hit 16 distinct 16-byte
+// slots of a 256-byte bank row.  The compact class order (row stride nx, plane stride nx ny) maps
+// them 2.5-way on average (10.2 LDS cycles per read against 4: the 13.2M conflict cycles per launch
+// of profiles/r5/sq/sq_r5_c4_xcd.json are 108 reads x 6.2 x 19,683 waves).  With the row stride
+// sy = 4 (nx = 4) or 8 (nx = 5) and the plane stride sz = 0 mod 16 (sy 4) or 4 mod 8 (sy 8) the
+// four (ey, ez) rows of every group fall on the four distinct quarter-rows: 1,100 slots instead of
+// 729, conflict-free (tsl_conflict_free below, checked at compile time).
+__host__ __device__ constexpr int tsl_sy(int nx) { return nx == 5 ? 8 : 4; }
+__host__ __device__ constexpr int tsl_sz(int nx, int ny) { return nx == 4 ? (ny == 4 ? 16 : 32) : (ny == 4 ? 36 : 44); }
+__host__ __device__ constexpr int tsl_class_size(int cx, int cy, int cz)
+{
+   const int nx = tpe_lattice_class_n(cx), ny = tpe_lattice_class_n(cy), nz = tpe_lattice_class_n(cz);
+   return tsl_sz(nx, ny) * (nz - 1) + tsl_sy(nx) * (ny - 1) + nx;
+}
+__host__ __device__ constexpr int tsl_class_off(int cx, int cy, int cz)
+{
+   int off = 0;
+   for (int c = 0; c < ((cz * 2 + cy) * 2 + cx); c++) { off += tsl_class_size(c & 1, (c >> 1) & 1, c >> 2); }
+   return off;
+}
+__host__ __device__ constexpr int tsl_points() { return tsl_class_off(0, 0, 2); }  // (all eight classes)
+// slot of lattice point (X, Y, Z) (p = 2: classes mod 2)
+__host__ __device__ constexpr int tsl_slot(int X, int Y, int Z)
+{
+   const int cx = X & 1, cy = Y & 1, nx = tpe_lattice_class_n(cx), ny = tpe_lattice_class_n(cy);
+   return tsl_class_off(cx, cy, Z & 1) + (Z >> 1) * tsl_sz(nx, ny) + (Y >> 1) * tsl_sy(nx) + (X >> 1);
+}
+__host__ __device__ constexpr bool tsl_conflict_free()
+{
+   for (int r = 0; r < 27; r++)  // the plane loop's reads (dx, dy, dz)
+   {
+      const int dx = r % 3, dy = (r / 3) % 3, dz = r / 9;
+      for (int g = 0; g < 4; g++)
+      {
+         bool used[16] = {};
+         for (int lane = 0; lane < 64; lane++)
+         {
+            const int l = lane & 31;
+            const int grp = (lane >> 5) * 2 + ((l < 4 || (l >= 12 && l < 16) || (l >= 20 && l < 28)) ? 0 : 1);
+            if (grp != g) { continue; }
+            const int s = tsl_slot(2 * (lane & 3) + dx, 2 * ((lane >> 2) & 3) + dy, 2 * (lane >> 4) + dz) & 15;
+            if (used[s]) { return false; }
+            used[s] = true;
+         }
+      }
+   }
+   return true;
+}
+static_assert(tsl_conflict_free(), "k_apply_tpe_ts lattice image: conflict-free 16-byte reads");
+static_assert(tsl_points() == 1100, "padded lattice image size");
+
 namespace kern
 {
 // ---- setup (S1/S2/S3 equivalents) ----
@@ -414,46 +468,64 @@ void diagonal(const int *pos, int D, int Q, int layout, int ne, const int *gmap_
 // ---- vector kernels for the device PCG ----
 void set_values(int n, const int *idx, double val, double *y, hipStream_t s);     // y[idx] = val
 void copy_values(int n, const int *idx, const double *x, double *y, hipStream_t s); // y[idx] = x[idx]
-// The device-driven PCG loop's state (device memory; the check kernel also writes it to a mapped
-// pinned host mirror): done = 0 running, 1 converged, 2 stopped at max_iter; iters, final = the
-// iteration and r.z at which it stopped; checked (mirror) = the last iteration whose stopping test
-// ran.  The vector kernels of an iteration given `ctl` return at once when done is set, so the host
-// can enqueue an iteration before it has read the previous one's test.
+// The device-driven PCG loop's state (device memory; the check kernels also write it to a mapped
+// pinned host mirror): done = PCG_RUNNING or the stop code below; iters, final = the iteration
+// (CGSolver's final_iter) and (B r, r) at which it stopped; checked (mirror) = the last iteration whose
+// betanom test ran.  The vector kernels of an iteration given `ctl` return at once when done is set,
+// so the host can enqueue an iteration before it has read the previous one's test.
 struct PcgCtl
 {
    int done, iters, checked, pad;
    double final;
 };
-// CGSolver's stopping test of iteration `it` (solvers.cpp:950-960) on the device: betanom <= r0 ->
-// converged at `it`; else it + 1 > max_iter -> stopped.  Writes ctl and the host mirror once, when
-// done is first set.
+// stop codes (CGSolver::Mult, solvers.cpp:950-1004): converged; max_iter reached; (B r, r) < 0 (the
+// preconditioner is not positive definite: not converged); (A d, d) == 0 (not converged); a
+// non-finite (B r, r) or (A d, d) (MFEM_VERIFY(IsFinite) aborts: ECM2_ERR_NUMERIC)
+enum PcgDone
+{
+   PCG_RUNNING = 0,
+   PCG_CONVERGED = 1,
+   PCG_MAX_ITER = 2,
+   PCG_NEG_BR = 3,
+   PCG_DEN_ZERO = 4,
+   PCG_NONFINITE = 5
+};
+// A stopping test on the device.  kind 0: iteration `it`'s test of betanom = the dot (non-finite,
+// < 0, <= r0, it + 1 > max_iter); kind 1: the test of den = the dot in iteration it - 1's tail (it =
+// the incremented iteration number, CGSolver's final_iter on a den == 0 stop; final = *betanom).
+// Writes ctl and the host mirror once, when done is first set.
 struct PcgStop
 {
    double r0;
    int it, max_iter;
    PcgCtl *ctl, *host;
+   const double *betanom = nullptr;
+   int kind = 0;
 };
 // Deterministic two-pass dot: result written to *out (device).  partials: kDotPartials doubles.
 // hout (optional): device pointer of mapped pinned host memory that also receives the result.
+// stop (serial solver): a stopping test on *out in the same launch.
 constexpr int kDotPartials = 1024;
 void dot(int n, const double *a, const double *b, double *partials, double *out, hipStream_t s,
-         double *hout = nullptr, const PcgCtl *ctl = nullptr);
-// Fused PCG update: x += (nom/den) d; r -= (nom/den) z; z = dinv .* r (dinv null: z untouched);
-// *out = r.z (r.r without dinv), deterministic.  z holds A d on entry.  stop (serial solver): the
-// stopping test on *out in the same launch.
-void pcg_step(int n, const double *nom, const double *den, const double *d, double *z, double *x, double *r,
-              const double *dinv, double *partials, double *out, hipStream_t s, double *hout = nullptr,
-              const PcgCtl *ctl = nullptr, const PcgStop *stop = nullptr);
-// the stopping test alone (after a distributed r.z's all-reduce)
-void pcg_check(const double *betanom, const PcgStop &stop, hipStream_t s);
+         double *hout = nullptr, const PcgCtl *ctl = nullptr, const PcgStop *stop = nullptr);
+// CGSolver's update in two passes (4 + 6 vector streams, z never stored):
+//   pcg_step_r: alpha = nom/den (-> *alpha); r -= alpha z (z holds A d); *out = r.(dinv .* r)
+//               (r.r without dinv), deterministic; stop (serial): betanom test in the same launch;
+//   pcg_update_xd: x += (nom/den) d; d = dinv .* r + (betanom/nom) d;
+//   pcg_finish_x (after the loop): x += *alpha d if the loop stopped at a betanom test.
+void pcg_step_r(int n, const double *nom, const double *den, const double *z, double *r, const double *dinv,
+                double *partials, double *out, double *alpha, hipStream_t s, const PcgCtl *ctl = nullptr,
+                const PcgStop *stop = nullptr);
+void pcg_update_xd(int n, const double *nom, const double *den, const double *betanom, double *x, double *d,
+                   const double *r, const double *dinv, hipStream_t s, const PcgCtl *ctl = nullptr);
+void pcg_finish_x(int n, const double *alpha, const double *d, double *x, hipStream_t s, const PcgCtl *ctl);
+// a stopping test alone (after a distributed dot's all-reduce)
+void pcg_check(const double *v, const PcgStop &stop, hipStream_t s);
 // saved[i] = v[idx[i]], v[idx[i]] = 0  /  v[idx[i]] = y[idx[i]] = saved[i]
 void ess_save_zero(int n, const int *idx, double *v, double *saved, hipStream_t s);
 void ess_restore(int n, const int *idx, const double *saved, double *v, double *y, hipStream_t s);
 //   z = dinv .* r  (dinv may be null -> z = r)
 void pcg_precond(int n, const double *dinv, const double *r, double *z, hipStream_t s);
-//   d = z + (betanom/nom) d
-void pcg_update_d(int n, const double *betanom, const double *nom, const double *z, double *d,
-                  hipStream_t s, const PcgCtl *ctl = nullptr);
 void reciprocal(int n, const double *a, double *out, hipStream_t s);
 void scale(int n, double a, double *y, hipStream_t s);                                   // y *= a
 void add_scaled(int n, const double *x, double c, const double *k, double *out, hipStream_t s); // out = x + c k

@@ -1,6 +1,8 @@
 // solvers.cpp -- see solvers.hpp.
 #include "solvers.hpp"
 
+#include <thread>
+
 #include <algorithm>
 #include <cmath>
 #include <memory>
@@ -140,8 +142,8 @@ PCGResult pcg_solve(LinOp &A, const int *ess, int n_ess, const double *b, double
    w.ensure(n, n_ess, jacobi);
    double *r = w.r.data(), *d = w.d.data(), *z = w.z.data(), *dinv = jacobi ? w.dinv.data() : nullptr;
    double *partials = w.partials.data();
-   // device scalars; nom and betanom swap roles every iteration (no copy)
-   double *nom = w.scal.data(), *den = w.scal.data() + 1, *betanom = w.scal.data() + 2;
+   // device scalars; nom and betanom swap roles every iteration (no copy); alpha of the last step
+   double *nom = w.scal.data(), *den = w.scal.data() + 1, *betanom = w.scal.data() + 2, *alpha = w.scal.data() + 3;
    // serial: the final-dot kernel also writes the value into mapped pinned memory, so the
    // stopping test needs only a stream sync; distributed: copy after the all-reduce
    const bool direct = !A.distributed();
@@ -183,9 +185,18 @@ PCGResult pcg_solve(LinOp &A, const int *ess, int n_ess, const double *b, double
    }
    dot(d, r, nom);
    const double nom0 = readback(nom);
+   // CGSolver::Mult's checks before the loop (solvers.cpp:893-948)
+   ECM2_VERIFY(std::isfinite(nom0), ERR_NUMERIC, "PCG: nom = " << nom0);
    res.initial_norm = nom0 >= 0 ? std::sqrt(nom0) : nom0;
-   const double r0 = std::max(nom0 * rel_tol * rel_tol, abs_tol * abs_tol);
    res.final_norm = res.initial_norm;
+   if (nom0 < 0.0)
+   {
+      // the preconditioner is not positive definite: not converged, final_norm = nom (:905-917)
+      res.initial_norm = res.final_norm = nom0;
+      ECM2_HIP(hipStreamSynchronize(s));
+      return res;
+   }
+   const double r0 = std::max(nom0 * rel_tol * rel_tol, abs_tol * abs_tol);
    if (nom0 <= r0) { res.converged = true; }
    else
    {
@@ -195,17 +206,19 @@ PCGResult pcg_solve(LinOp &A, const int *ess, int n_ess, const double *b, double
       *w.hctl = kern::PcgCtl{};
       cmult(d, z);
       dot(z, d, den);
-      if (readback(den) != 0.0)
+      const double den0 = readback(den);
+      ECM2_VERIFY(std::isfinite(den0), ERR_NUMERIC, "PCG: den = " << den0);
+      if (den0 != 0.0)
       {
-         // CGSolver's loop (solvers.cpp:930-1000) driven by the device: the stopping test runs on
-         // the device after each r.z (in the dot's final pass, or in a one-thread kernel after the
-         // all-reduce), and once it stops every later vector kernel returns at once.  The
-         // host enqueues iteration i as soon as the test of i - 1 has run (it polls the mirror's
-         // progress mark; no host synchronisation of the stream), so the queue holds the rest of
-         // iteration i - 1 while it does, and it ends at the iteration the device stopped at: the same
-         // iteration on every rank, so the ranks issue the same collectives.  The iterates are
-         // CGSolver's (same kernels, same order); at most one operator Mult (the stopping
-         // iteration's) runs after the stop.
+         // CGSolver's loop (solvers.cpp:930-1000) driven by the device: the stopping tests run on
+         // the device after each r.z and each (A d, d) (in the dot's final pass, or in a one-thread
+         // kernel after the all-reduce), and once one stops every later vector kernel returns at once.
+         // The host enqueues iteration i as soon as the betanom test of i - 1 has run (it polls the
+         // mirror's progress mark; no host synchronisation of the stream), so the queue holds the
+         // rest of iteration i - 1 while it does, and it ends at the iteration the device stopped at:
+         // the same iteration on every rank, so the ranks issue the same collectives.  The iterates
+         // are CGSolver's (the same operations per entry, in its order; x += alpha d deferred into
+         // the next pass that reads d); at most the stopping iteration's Mult runs after the stop.
          kern::PcgCtl *ctl = w.ctl.data(), *hm = w.hctl;
          auto vol = [](const int &v) { return *(volatile const int *)&v; };
          // has the loop stopped at an iteration <= waited?  (waits until the test of `waited` ran)
@@ -227,31 +240,47 @@ PCGResult pcg_solve(LinOp &A, const int *ess, int n_ess, const double *b, double
                   }
                   if (e != hipSuccess && e != hipErrorNotReady) { ECM2_HIP(e); }
                }
+               // back off after a short spin: the host core stays free for RCCL's
+               // proxy and the other ranks' host threads while the device runs the iteration
+               if (spin > 256) { std::this_thread::yield(); }
             }
          };
          for (int i = 1;; i++)
          {
             if (i > 1 && stopped_by(i - 1)) { break; }
-            // x += alpha d, r -= alpha A d, z = M^{-1} r, betanom = r.z in one pass
+            // r -= alpha A d, betanom = r.(M^{-1} r) in one pass, its test
             const kern::PcgStop stop{r0, i, max_iter, ctl, w.hctl_dev};
-            kern::pcg_step(n, nom, den, d, z, x, r, dinv, partials, betanom, s, nullptr, ctl, direct ? &stop : nullptr);
+            kern::pcg_step_r(n, nom, den, z, r, dinv, partials, betanom, alpha, s, ctl, direct ? &stop : nullptr);
             if (!direct)
             {
                A.sum_scalars(betanom, 1, s);
                kern::pcg_check(betanom, stop, s);
             }
             if (i >= max_iter) { break; }
-            kern::pcg_update_d(n, betanom, nom, jacobi ? z : r, d, s, ctl);
+            // x += alpha d, d = M^{-1} r + beta d
+            kern::pcg_update_xd(n, nom, den, betanom, x, d, r, dinv, s, ctl);
             cmult(d, z);
-            dot(d, z, den, ctl);
+            // den = (A d, d) and its test (after ++i: final_iter = i + 1 on a den == 0 stop)
+            const kern::PcgStop dstop{r0, i + 1, max_iter, ctl, w.hctl_dev, betanom, 1};
+            if (direct) { kern::dot(n, d, z, partials, den, s, nullptr, ctl, &dstop); }
+            else
+            {
+               dot(d, z, den, ctl);
+               kern::pcg_check(den, dstop, s);
+            }
             std::swap(nom, betanom);  // nom <- betanom
          }
+         // the stopping iteration's x += alpha d (a betanom stop)
+         kern::pcg_finish_x(n, alpha, d, x, s, ctl);
          ECM2_HIP(hipStreamSynchronize(s));
-         ECM2_VERIFY(*(volatile int *)&hm->done != 0, ERR_INTERNAL, "device PCG loop ended without a stop");
+         const int done = *(volatile int *)&hm->done;
+         ECM2_VERIFY(done != kern::PCG_RUNNING, ERR_INTERNAL, "device PCG loop ended without a stop");
          const double bn = hm->final;
+         ECM2_VERIFY(done != kern::PCG_NONFINITE, ERR_NUMERIC,
+                     "PCG: non-finite (B r, r) or (A d, d) at iteration " << hm->iters << " (" << bn << ")");
          res.final_norm = bn >= 0 ? std::sqrt(bn) : bn;
          res.iterations = hm->iters;
-         res.converged = hm->done == 1;
+         res.converged = done == kern::PCG_CONVERGED;
       }
    }
    ECM2_HIP(hipStreamSynchronize(s));

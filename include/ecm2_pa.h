@@ -30,6 +30,8 @@ extern "C" {
 #define ECM2_ERR_UNSUPPORTED 5
 #define ECM2_ERR_COMM 6
 #define ECM2_ERR_INTERNAL 7
+#define ECM2_ERR_NUMERIC 8  /* a non-finite value where the reference's MFEM_VERIFY(IsFinite(..)) aborts
+                              (CGSolver::Mult's nom / den / betanom, linalg/solvers.cpp:896, 932, 954, 993) */
 
 /* Integrator kinds (MassIntegrator, DiffusionIntegrator: fem/bilininteg.hpp:2177-2465). */
 #define ECM2_MASS 0
@@ -295,10 +297,17 @@ void ecm2_pa_form_destroy(ecm2_pa_form *f);
 /* CGSolver::Mult solvers.cpp:869-1004)                                       */
 /* ------------------------------------------------------------------------ */
 /* ess: device int [n_ess] essential dofs (DIAG_ONE).  b, x device [ndofs];
- * x is overwritten (iterative_mode = false).  jacobi != 0 -> OperatorJacobiSmoother. */
+ * x is overwritten (iterative_mode = false).  jacobi != 0 -> OperatorJacobiSmoother.
+ * iterations = CGSolver's final_iter, final_norm = sqrt((B r, r)) (the raw (B r, r) when it is
+ * negative).  CGSolver's stops: converged, max_iter, (B r, r) < 0 or (A d, d) == 0 (not
+ * converged: ecm2_pcg_last_converged() == 0); a non-finite (B r, r) or (A d, d), where the
+ * reference's MFEM_VERIFY aborts, returns ECM2_ERR_NUMERIC. */
 int ecm2_pcg_solve(ecm2_pa_form *f, const int *ess, int n_ess, const double *b, double *x,
                    double rel_tol, double abs_tol, int max_iter, int jacobi, int *iterations,
                    double *final_norm, void *stream);
+/* IterativeSolver::GetConverged() (solvers.hpp:155) of the calling thread's last
+ * ecm2_pcg_solve / ecm2_operator_pcg: 1 converged, 0 not (or no solve yet). */
+int ecm2_pcg_last_converged(void);
 
 /* ------------------------------------------------------------------------ */
 /* Operators for the solvers: the serial form, one rank of the RCCL form, or */

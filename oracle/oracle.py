@@ -54,7 +54,7 @@ def lib():
             "orc_pa_diagonal_e_n": (None, [i32, i32, i32, vp, vp, vp, vp, i32, vp]),
             "orc_fa_mult_m": (None, [i32, i32, i32, vp, vp, i32, vp, i32, vp, i32, i32, vp, vp, vp]),
             "orc_pcg": (i32, [i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp,
-                              f64, f64, i32, ctypes.POINTER(ctypes.c_double)]),
+                              f64, f64, i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
             "orc_num_threads": (i32, []),
         }
         for n, (r, a) in sig.items():
@@ -424,9 +424,13 @@ class OracleOperator:
             dinv = 1.0 / d
         x = np.empty(self.ndofs)
         fn = ctypes.c_double()
+        st = ctypes.c_int()
         it = lib().orc_pcg(self.ne, self.p, self.q1d, self.ndofs, _p(self.gm), _p(self.off), _p(self.idx),
                            _p(self._Bf), _p(self._Gf), _p(self.M), _p(self.D), _p(ess), ess.size,
-                           _p(dinv), _p(_f64(b)), _p(x), rel_tol, abs_tol, max_iter, ctypes.byref(fn))
+                           _p(dinv), _p(_f64(b)), _p(x), rel_tol, abs_tol, max_iter, ctypes.byref(fn),
+                           ctypes.byref(st))
+        # CGSolver's outcome: 1 converged, 2 max_iter, 3 (B r, r) < 0, 4 (A d, d) == 0, 5 non-finite
+        self.last_pcg_status = st.value
         return x, it, fn.value
 
 

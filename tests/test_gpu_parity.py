@@ -637,6 +637,54 @@ def test_pcg_device_loop_stops_like_cgsolver(max_iter):
     assert it == itr and relerr(host(x), xr) < 1e-11
 
 
+@pytest.mark.parametrize("case", ["spd", "indefinite_mid", "indefinite_first", "negative_start", "zero_operator",
+                                  "nan_rhs"])
+def test_pcg_device_stops_like_cgsolver_indefinite(case):
+    """CGSolver's other stops (solvers.cpp:893-1004) in the device-driven loop, against
+    the oracle (pinned by tests/test_oracle_pins.py::test_pcg_oracle_stops_like_cgsolver): a mass
+    coefficient of -amp on x > 0.7 makes the Jacobi diagonal indefinite, so (B r, r) < 0 stops the
+    loop not converged in the loop (final_iter = i) or before it (final_iter 0, final_norm = nom); a
+    zero operator without a preconditioner stops at (A d, d) == 0; a NaN right-hand side is
+    MFEM_VERIFY's abort, ECM2_ERR_NUMERIC."""
+    m = E.Mesh.MakeCartesian3D(4, 4, 4)
+    m.set_vertices(nonaligned(m.vertices()))
+    fes = E.H1Space(m, 2)
+    en = m.element_nodes()
+    P = O.quad_points(en, O.default_q1d(2))
+    amp, beta, jacobi, expect = {"spd": (-1.0, 0.5, True, 1), "indefinite_mid": (30.0, 0.05, True, 3),
+                                 "indefinite_first": (40.0, 0.05, True, 3), "negative_start": (60.0, 0.05, True, 3),
+                                 "zero_operator": (0.0, 0.0, False, 4), "nan_rhs": (-1.0, 0.5, True, 5)}[case]
+    alpha = np.where(P[..., 0] > 0.7, -amp, 1.0) if case != "zero_operator" else np.zeros(P.shape[:-1])
+    form = E.BilinearForm(fes)
+    form.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(alpha.reshape(fes.ne, -1)))))
+    form.AddDomainIntegrator(E.DiffusionIntegrator(E.ConstantCoefficient(beta)))
+    form.Assemble()
+    op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, 2, alpha=alpha, beta=beta)
+    X = fes.dof_coords()
+    ess = np.nonzero(np.isclose(X[:, 0], 0))[0].astype(np.int32) if case != "zero_operator" else np.zeros(0, np.int32)
+    b = np.random.default_rng(0).uniform(-1, 1, fes.ndofs)
+    if case == "nan_rhs":
+        b[5] = np.nan
+    x = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    esst = dev(ess, torch.int32) if ess.size else None
+    xr, itr, nr = op.pcg(b, ess, rel_tol=1e-10, max_iter=300, jacobi=jacobi)
+    assert op.last_pcg_status == expect
+    if case == "nan_rhs":
+        with pytest.raises(E.ECM2Error) as ei:
+            form.PCG(dev(b), x, ess=esst, rel_tol=1e-10, max_iter=300, jacobi=jacobi)
+        assert ei.value.code == 8  # ECM2_ERR_NUMERIC
+        return
+    it, nrm = form.PCG(dev(b), x, ess=esst, rel_tol=1e-10, max_iter=300, jacobi=jacobi)
+    assert it == itr
+    assert E.pcg_last_converged() == (expect == 1)
+    if case == "indefinite_mid":
+        assert it > 1
+    if it > 0:
+        assert relerr(host(x), xr) < 1e-9
+    if case == "negative_start":
+        assert it == 0 and nrm < 0 and nrm == pytest.approx(nr, rel=1e-12)
+
+
 def test_golden_vectors():
     g = np.load(f"{GOLDEN}/oracle_golden.npz")
     for order in (1, 2, 3):

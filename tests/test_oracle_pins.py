@@ -177,6 +177,98 @@ def test_pcg_oracle_solves():
     assert relerr(r, b) < 1e-9
 
 
+def _cgsolver_numpy(op, b, ess, rel_tol, max_iter, jacobi):
+    """CGSolver::Mult (linalg/solvers.cpp:869-1049) restated in numpy over the oracle's Mult
+    with ConstrainedOperator DIAG_ONE: (x, final_iter, status) with the oracle's status codes
+    (1 converged, 2 max_iter, 3 (B r, r) < 0, 4 (A d, d) == 0, 5 non-finite)."""
+    def A(v):
+        z = v.copy()
+        z[ess] = 0.0
+        y = op.mult(z)
+        y[ess] = v[ess]
+        return y
+    dinv = None
+    if jacobi:
+        dg = op.diagonal()
+        dg[ess] = 1.0
+        dinv = 1.0 / dg
+    B = (lambda v: dinv * v) if jacobi else (lambda v: v)
+    r = b.copy()
+    x = np.zeros_like(b)
+    d = B(r)
+    nom = d @ r
+    if not np.isfinite(nom):
+        return x, 0, 5
+    if nom < 0:
+        return x, 0, 3
+    r0 = nom * rel_tol * rel_tol
+    if nom <= r0:
+        return x, 0, 1
+    z = A(d)
+    den = z @ d
+    if not np.isfinite(den):
+        return x, 0, 5
+    if den == 0:
+        return x, 0, 4
+    i = 1
+    while True:
+        alpha = nom / den
+        x = x + alpha * d
+        r = r - alpha * z
+        z = B(r)
+        betanom = r @ z
+        if not np.isfinite(betanom):
+            return x, i, 5
+        if betanom < 0:
+            return x, i, 3
+        if betanom <= r0:
+            return x, i, 1
+        i += 1
+        if i > max_iter:
+            return x, max_iter, 2
+        d = z + (betanom / nom) * d
+        z = A(d)
+        den = d @ z
+        if not np.isfinite(den):
+            return x, i, 5
+        if den == 0:
+            return x, i, 4
+        nom = betanom
+
+
+@pytest.mark.parametrize("case", ["spd", "indefinite_mid", "indefinite_first", "negative_start",
+                                  "zero_operator", "nan_rhs"])
+def test_pcg_oracle_stops_like_cgsolver(case):
+    """The oracle's CGSolver restatement stops where CGSolver does (solvers.cpp:893-1004), against
+    an independent numpy restatement: converged; (B r, r) < 0 in the loop (a mass coefficient of
+    -30 on x > 0.7 makes the Jacobi diagonal indefinite: not converged, final_iter = i) and at the
+    start (final_iter 0, final_norm = nom); (A d, d) == 0 (a zero operator, no preconditioner);
+    a NaN right-hand side (MFEM_VERIFY(IsFinite(nom)) aborts: status 5)."""
+    en, gm, nd, xyz = O.cartesian_mesh(4, 4, 4, order=2, transform=nonaligned)
+    P = O.quad_points(en, O.default_q1d(2))
+    ess = np.nonzero(np.isclose(xyz[:, 0], 0))[0]
+    amp, beta, jacobi, expect = {"spd": (-1.0, 0.5, True, 1), "indefinite_mid": (30.0, 0.05, True, 3),
+                                 "indefinite_first": (40.0, 0.05, True, 3), "negative_start": (60.0, 0.05, True, 3),
+                                 "zero_operator": (0.0, 0.0, False, 4), "nan_rhs": (-1.0, 0.5, True, 5)}[case]
+    alpha = np.where(P[..., 0] > 0.7, -amp, 1.0) if case != "zero_operator" else np.zeros(P.shape[:-1])
+    op = O.OracleOperator(en, gm, nd, 2, alpha=alpha, beta=beta)
+    b = np.random.default_rng(0).uniform(-1, 1, nd)
+    if case == "zero_operator":
+        ess = np.zeros(0, np.int64)
+    if case == "nan_rhs":
+        b[5] = np.nan
+    x, it, fn = op.pcg(b, ess, rel_tol=1e-10, max_iter=300, jacobi=jacobi)
+    xr, itr, st = _cgsolver_numpy(op, b, ess, 1e-10, 300, jacobi)
+    assert op.last_pcg_status == st == expect
+    assert it == itr
+    if case == "indefinite_mid":
+        assert it > 1
+    if expect in (1, 3) and it > 0:
+        assert relerr(x, xr) < 1e-9
+    if case == "negative_start":
+        assert it == 0 and fn < 0
+
+
 def test_golden_vectors_regression():
     """tests/golden/oracle_golden.npz (written by tests/golden/make_golden.py from this
     oracle): guards the restatement against unintended changes."""

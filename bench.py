@@ -200,14 +200,14 @@ def time_mults(apply, x, y, steps, warmup, world, dist, torch):
     for _ in range(warmup):
         apply(x, y)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
         apply(x, y)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     return time.perf_counter() - t0
@@ -229,7 +229,7 @@ def kernel_ms(forms, apply, x, y, steps, torch, settle_s=0.06, world=1, dist=Non
         apply(x, y)
     torch.cuda.synchronize()
     n = max(1, min(5000, int(settle_s / max((time.perf_counter() - t0) / 8, 1e-6))))
-    if world > 1:
+    if dist is not None:
         t = torch.tensor([n], dtype=torch.int64, device="cuda")
         dist.broadcast(t, 0)
         n = int(t.item())
@@ -505,6 +505,11 @@ def main():
                          "one-GPU line, 0 otherwise")
     ap.add_argument("--sdirk", type=int, default=1, choices=[0, 1],
                     help="one-GPU line: also time one ex16p SDIRK33 step on this workload's mesh (sdirk_step)")
+    ap.add_argument("--rank-path", type=int, default=0, choices=[0, 1],
+                    help="1 with --gpus 1 (under torch.distributed.run): take the RCCL rank branch the N > 1 run "
+                         "takes -- process group, RCCL unique id broadcast, one-part z-slab Partition, "
+                         "ParBilinearForm over a one-rank communicator, cross-rank reductions -- so a one-GPU "
+                         "test executes that code before a multi-GPU run does")
     ap.add_argument("--deadline", type=float, default=900.0,
                     help="seconds after which a rank prints its last stage and exits non-zero (0: none)")
     args = ap.parse_args()
@@ -522,7 +527,9 @@ def main():
     import torch.distributed as dist
 
     torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
-    if world > 1:
+    par = world > 1 or args.rank_path == 1  # the RCCL rank branch (one process per GPU)
+    if par:
+        os.environ.setdefault("MASTER_PORT", "29511")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dl.at("init_process_group")
         dist.init_process_group("nccl", rank=rank, world_size=world,
@@ -567,7 +574,7 @@ def main():
     else:
         mesh, fes = cartesian_space(E, nx, ny, nz_total, order, args.numbering, args.mesh)
     variant = variant_key(args)
-    nsub = world if world > 1 else args.loopback
+    nsub = world if par else args.loopback
     mass, diff = bench_integrators(E)
     form = None
     keep = []
@@ -588,7 +595,7 @@ def main():
         xs.uniform_(-1.0, 1.0, generator=torch.Generator(device="cuda").manual_seed(1))
         ys = torch.empty_like(xs)
         kf = kernel_ms([f], f.Mult, xs, ys, args.steps, torch)
-        dtf = time_mults(f.Mult, xs, ys, args.steps, args.warmup, 1, dist, torch)
+        dtf = time_mults(f.Mult, xs, ys, args.steps, args.warmup, 1, None, torch)
         lay = qdata_layout(E, f)
         lat, units, runs = f.AddressingInfo()
         lslot, xruns = f.PlanInfo()
@@ -605,7 +612,7 @@ def main():
                 "note": note}
 
     dl.at("assemble")
-    if nsub <= 1:
+    if nsub <= 1 and not par:
         form = serial_form(compress)
         alpha, T = keep[0], keep[1]
         n_true = fes.ndofs
@@ -623,7 +630,7 @@ def main():
             er = E.partition_bricks(mesh, nsub)
         else:
             er = E.partition_slabs_z(mesh, nsub)
-        if world > 1:
+        if par:
             rid = [E.rccl_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(rid, src=0)
             part = E.Partition(fes, er, rank, world, decomposition=decomp)
@@ -667,11 +674,12 @@ def main():
     torch.cuda.synchronize()
 
     dl.at("kernel timing")
-    if world > 1:
+    pdist = dist if par else None
+    if par:
         dist.barrier()  # all ranks settle together
-    kms = kernel_ms(timed_forms, apply, x, y, args.steps, torch, world=world, dist=dist)
+    kms = kernel_ms(timed_forms, apply, x, y, args.steps, torch, world=world, dist=pdist)
     dl.at("timed Mults")
-    dt = time_mults(apply, x, y, args.steps, args.warmup, world, dist, torch)
+    dt = time_mults(apply, x, y, args.steps, args.warmup, world, pdist, torch)
     abytes = sum(f.algorithmic_bytes() for f in timed_forms)
     nd = (order + 1) ** 3
     mbytes = sum(min_bytes(f, f.part.ne_local if hasattr(f, "part") else fes.ne, nd, f.true_size
@@ -689,7 +697,7 @@ def main():
     # aggregate over ranks: total true dofs, max time; kernel ms per Mult (interior + boundary
     # launches of one Mult when partitioned); bytes per GPU
     tot = torch.tensor([float(n_true), dt, abytes, kms, qbytes, mbytes], dtype=torch.float64, device="cuda")
-    if world > 1:
+    if par:
         dl.at("reduce results")
         s = tot.clone()
         for i in (0, 2, 4, 5):
@@ -704,7 +712,7 @@ def main():
     lattice = timed_forms[0].AddressingInfo()
 
     subs = {}
-    serial_main = world == 1 and args.loopback <= 1 and args.workload != "c3"
+    serial_main = not par and args.loopback <= 1 and args.workload != "c3"
     if serial_main and args.full_layout and compress:
         dl.at("full layout")
         del apply
@@ -765,7 +773,7 @@ def main():
         dl.at("stream copy peak")
         stream = stream_copy_peak(E, torch)
         cpu = None
-        if not args.no_cpu_baseline and world == 1 and args.loopback <= 1:
+        if not args.no_cpu_baseline and not par and args.loopback <= 1:
             dl.at("cpu baseline")
             cpu = cpu_baseline(fes, mesh, alpha, T, args.cpu_baseline_seconds, args.workload)
         line = {
@@ -786,7 +794,7 @@ def main():
                 "ndofs": int(ndofs_total),
                 "elements": int(fes.ne),
                 "order": order, "q1d": order + 2,
-                "launch": "stream launches" if world == 1 else par_launch_label(args.schedule, args.par_graph),
+                "launch": "stream launches" if not par else par_launch_label(args.schedule, args.par_graph),
                 "kernel": ["auto", "tpe", "wpe", "unfused", "line"][timed_forms[0].info()["kernel"]],
                 "qdata_layout": layout,
                 "numbering": ("entity (the reference's FiniteElementSpace numbering)" if args.workload == "c3" or
@@ -795,7 +803,7 @@ def main():
                 "lattice_units": list(lattice[:2]), "summation_runs": lattice[2],
                 "qdata_bytes_stored": qbytes_total / world,
                 "parallelism": (f"domain decomposition, {PART_NAME[args.partition]} x{world} ({decomp}, {args.schedule} schedule), RCCL shared-DoF exchange"
-                                if world > 1 else
+                                if par else
                                 (f"loopback {PART_NAME[args.partition]} x{args.loopback} on one GPU" if args.loopback > 1 else "single GPU")),
             },
             "roofline": roofline(args.workload + variant, world, layout, kavg_ms, bytes_total / world,
@@ -816,7 +824,7 @@ def main():
             line["pcg"] = pcg
         print(json.dumps(line), flush=True)
     dl.at("teardown")
-    if world > 1:
+    if par:
         # release the forms (ncclCommDestroy of the operator's communicator) on every rank
         # while all ranks are alive, then tear down torch's process group
         del apply, timed_forms, pform

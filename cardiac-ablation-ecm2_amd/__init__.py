@@ -436,9 +436,26 @@ def _check_points(c, v, tails, ne, nq, flat_ok=False):
         raise ECM2Error(f"{name}: expected shape ({ne}, {nq}) + one of {tails}, got {shp}")
 
 
-def _integrator_args(c, keep, ne=None, nq=None):
+def _check_field(c, T, ndofs):
+    """A grid-function coefficient's field must be a CUDA float64 L-vector of the form's space (the
+    local [owned | ghost] L-vector for a partitioned form): the snapshot and coefficient kernels read
+    ndofs doubles from it."""
+    import torch
+    name = type(c).__name__
+    if not isinstance(T, torch.Tensor) or not T.is_cuda or T.dtype != torch.float64:
+        raise ECM2Error(f"{name}: expected a CUDA float64 tensor, got {type(T).__name__} {getattr(T, 'dtype', '')}")
+    if ndofs is not None and T.numel() != ndofs:
+        raise ECM2Error(f"{name}: {T.numel()} values, the form's L-vector has {ndofs}")
+    if not T.is_contiguous():
+        raise ECM2Error(f"{name}: the field must be contiguous")
+
+
+def _integrator_args(c, keep, ne=None, nq=None, ndofs=None):
     """(coefficient kind, data pointer, params pointer) of a coefficient for the C ABI; ne, nq: the
-    form's elements and quadrature points per element (checked against per-point tensors)."""
+    form's elements and quadrature points per element (checked against per-point tensors); ndofs: its
+    L-vector size (checked against grid-function fields)."""
+    if isinstance(c, (GridFunctionCoefficient, AffineGridFunctionCoefficient, PerfusionCoefficient)):
+        _check_field(c, c.T, ndofs)
     if isinstance(c, ConstantCoefficient):
         arr = (ctypes.c_double * 1)(c.value)
         keep.append(arr)
@@ -568,7 +585,7 @@ class BilinearForm:
         """BilinearForm::AddDomainIntegrator(integ[, elem_marker]): with a marker (0 / 1 per
         attribute) the integrator acts on the elements whose attribute a has elem_marker[a-1]."""
         info = self.info()
-        kind, data, params = _integrator_args(integ.coeff, self._keep, info["ne"], info["q1d"] ** 3)
+        kind, data, params = _integrator_args(integ.coeff, self._keep, info["ne"], info["q1d"] ** 3, info["ndofs"])
         if elem_marker is None:
             _check(_lib.ecm2_pa_form_add_integrator(self._h, integ.kind, kind, data, params))
         else:
@@ -929,7 +946,8 @@ class ParBilinearForm:
 
     def AddDomainIntegrator(self, integ, elem_marker=None):
         kind, data, params = _integrator_args(integ.coeff, self._keep, self.part.ne_local,
-                                              (self._q1d or self.part.fes.order + 2) ** 3)
+                                              (self._q1d or self.part.fes.order + 2) ** 3,
+                                              self.part.n_owned + self.part.n_ghost)
         if elem_marker is None:
             _check(_par_lib().ecm2_par_form_add_integrator(self._h, integ.kind, kind, data, params))
         else:

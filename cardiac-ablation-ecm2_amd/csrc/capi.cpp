@@ -102,7 +102,8 @@ ecm2::CoeffDesc make_coeff(int coeff_kind, const double *data, const double *par
       for (int i = 0; i < c.dim(); i++) { c.cv[i] = data[i]; }
    }
    else { ECM2_VERIFY(false, ecm2::ERR_ARG, "unknown coefficient kind " << coeff_kind); }
-   if (c.gridfunc()) { NEED(data); }
+   // (a null grid function is refused by PAForm::add_integrator unless the form has no dofs: a rank
+   // with an empty local space passes an empty tensor's null data pointer)
    return c;
 }
 } // namespace

@@ -410,12 +410,22 @@ __global__ void k_ess_save_zero(int n, const int *__restrict__ idx, double *__re
    if (i < n) { saved[i] = v[idx[i]]; v[idx[i]] = 0.0; }
 }
 
-// ... then v[ess] = y[ess] = saved (DIAG_ONE rows)
-__global__ void k_ess_restore(int n, const int *__restrict__ idx, const double *__restrict__ saved,
-                              double *__restrict__ v, double *__restrict__ y)
+// ... then v[ess] = y[ess] = saved (DIAG_ONE rows); sq_parts (optional): the block's sum of saved^2,
+// the ess rows' part of (A v, v) = (A v~, v~) + sum_ess v^2 with v~ = v, ess zeroed
+__global__ void __launch_bounds__(256)
+k_ess_restore(int n, const int *__restrict__ idx, const double *__restrict__ saved, double *__restrict__ v,
+              double *__restrict__ y, double *__restrict__ sq_parts)
 {
    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-   if (i < n) { v[idx[i]] = saved[i]; y[idx[i]] = saved[i]; }
+   double sq = 0.0;
+   if (i < n)
+   {
+      const double sv = saved[i];
+      v[idx[i]] = sv;
+      y[idx[i]] = sv;
+      sq = sv * sv;
+   }
+   if (sq_parts) { dot_park(sq, sq_parts); }
 }
 
 __global__ void k_pcg_precond(int n, const double *__restrict__ dinv, const double *__restrict__ r,
@@ -696,10 +706,20 @@ void ess_save_zero(int n, const int *idx, double *v, double *saved, hipStream_t 
    ECM2_HIP(hipGetLastError());
 }
 
-void ess_restore(int n, const int *idx, const double *saved, double *v, double *y, hipStream_t s)
+void ess_restore(int n, const int *idx, const double *saved, double *v, double *y, hipStream_t s, double *sq_parts)
 {
    if (n <= 0) { return; }
-   hipLaunchKernelGGL(k_ess_restore, dim3(grid_for(n, 256)), dim3(256), 0, s, n, idx, saved, v, y);
+   hipLaunchKernelGGL(k_ess_restore, dim3(grid_for(n, 256)), dim3(256), 0, s, n, idx, saved, v, y, sq_parts);
+   ECM2_HIP(hipGetLastError());
+}
+
+int ess_parts(int n) { return n > 0 ? grid_for(n, 256) : 0; }
+
+void dot_final(int nparts, const double *partials, double *out, hipStream_t s, const PcgCtl *ctl,
+               const PcgStop *stop, double *hout)
+{
+   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, s, nparts, partials, out, hout, ctl, to_check(stop),
+                      stop ? 1 : 0);
    ECM2_HIP(hipGetLastError());
 }
 

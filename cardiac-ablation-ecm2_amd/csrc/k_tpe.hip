@@ -1014,7 +1014,8 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                const double *__restrict__ x, const double *__restrict__ xg, const double *__restrict__ tsn,
                double *__restrict__ y, double *__restrict__ yg, const Basis1D b, const Basis1D bw,
                const int *__restrict__ lane_flags, double *__restrict__ part, const int *__restrict__ treg,
-               int pstride, const int *__restrict__ lmap, const QPts qw, const PointLaw law_d, const PointLaw law_m)
+               int pstride, const int *__restrict__ lmap, const QPts qw, const PointLaw law_d, const PointLaw law_m,
+               double *__restrict__ en)
 {
    static_assert(RM == 1 || RM == 3, "lattice blocks only");
    static_assert(D == 3 && Q == 4, "p = 2");
@@ -1223,6 +1224,31 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 #pragma unroll
       for (int qz = 0; qz < Q; qz++) { plane(qz); }
    }  // wave_on
+   if (en)  // (uniform) the Mult's energy x^T A x = sum_e X_e . (A_e X_e), one partial per workgroup
+   {
+      // CGSolver's den = (A d, d) (solvers.cpp:993) without a dot pass: the element outputs are
+      // complete here and X_e is still in the lattice image (ConstrainedOperator's zeroed ess entries
+      // included); PAForm::mult_energy documents the ess correction.  Fixed order: lanes, then waves.
+      __shared__ double red[WPG];
+      double e_l = 0.0;
+      if (wave_on && active)
+      {
+#pragma unroll
+         for (int dz = 0; dz < D; dz++)
+#pragma unroll
+            for (int dy = 0; dy < D; dy++)
+#pragma unroll
+               for (int dx = 0; dx < D; dx++)
+               {
+                  const double xv = sPL[tsl_slot(2 * ex + dx, 2 * ey + dy, 2 * ez + dz)].x;
+                  e_l += xv * Yo[(dz * D + dy) * D + dx];
+               }
+      }
+      for (int off = 32; off > 0; off >>= 1) { e_l += __shfl_down(e_l, off, 64); }
+      if (lane == 0) { red[w] = e_l; }
+      __syncthreads();
+      if (threadIdx.x == 0) { en[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]); }
+   }
    tpe_assemble_store<D, SPLIT, false, true, true, XRS>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0, blk, lane,
                                                        active, n_owned, y, yg, part, &sU[0][0][0], w, wave_on, rg, regf,
                                                        pstride, lmap ? lmap + (size_t)blk * NLP : nullptr);
@@ -1557,7 +1583,7 @@ void launch_tpe(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipS
 #define ECM2_TS(RM, MM, LAW)                                                                                        \
    hipLaunchKernelGGL((k_apply_tpe_ts<3, 4, SPLIT, RM, MM, LAW>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end,     \
                       a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.tsnap, a.y, a.yg, b, bw, a.lane_flags, a.part,     \
-                      a.treg, a.part_stride, a.lmap, qw, a.law_d, a.law_m)
+                      a.treg, a.part_stride, a.lmap, qw, a.law_d, a.law_m, a.en)
 #define ECM2_TS_MM(RM, LAW)                                                                                         \
    if (!MASS) { ECM2_TS(RM, 0, LAW); }                                                                              \
    else if (a.tmass == 1) { ECM2_TS(RM, 1, LAW); }                                                                  \

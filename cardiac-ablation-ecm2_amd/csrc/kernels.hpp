@@ -245,6 +245,8 @@ struct ApplyArgs
    const int *brick_off = nullptr;  // host [nblk + 1], bricks whose first element lies in block b
    int brick_bz = 0;                // 0: no bricks
    double *part_brick = nullptr;    // partial slots [nbrick][surface] of shared lattice points
+   // k_apply_tpe_ts: the Mult's energy x^T A x as one partial per workgroup (en[workgroup]), or null
+   double *en = nullptr;
 };
 
 // Partial-slot order of a brick's surface lattice points (2 x 2 x bz elements, lattice
@@ -523,7 +525,13 @@ void pcg_finish_x(int n, const double *alpha, const double *d, double *x, hipStr
 void pcg_check(const double *v, const PcgStop &stop, hipStream_t s);
 // saved[i] = v[idx[i]], v[idx[i]] = 0  /  v[idx[i]] = y[idx[i]] = saved[i]
 void ess_save_zero(int n, const int *idx, double *v, double *saved, hipStream_t s);
-void ess_restore(int n, const int *idx, const double *saved, double *v, double *y, hipStream_t s);
+void ess_restore(int n, const int *idx, const double *saved, double *v, double *y, hipStream_t s,
+                 double *sq_parts = nullptr);
+// ess_restore's blocks: sq_parts[block] = the block's sum of saved^2 (fixed order), ess_parts(n) of them
+int ess_parts(int n);
+// the second pass of a deterministic dot over nparts given partials (+ optional stopping test)
+void dot_final(int nparts, const double *partials, double *out, hipStream_t s, const PcgCtl *ctl = nullptr,
+               const PcgStop *stop = nullptr, double *hout = nullptr);
 //   z = dinv .* r  (dinv may be null -> z = r)
 void pcg_precond(int n, const double *dinv, const double *r, double *z, hipStream_t s);
 void reciprocal(int n, const double *a, double *out, hipStream_t s);

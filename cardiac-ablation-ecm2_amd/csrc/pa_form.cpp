@@ -1417,6 +1417,23 @@ void PAForm::mult(const double *x, double *y, hipStream_t s)
    record_stop(s);
 }
 
+int PAForm::energy_parts() const
+{
+   const bool ts = assembled_ && use_partials() && resolved_mode_ == KERNEL_TPE && layout_.kind == QLAYOUT_AFFINE &&
+                   layout_.tsnap && have_diff_ && D_ == 3 && Q_ == 4;
+   return ts && ndofs_ > 0 ? (layout_.nblk() + 3) / 4 : 0;
+}
+
+void PAForm::mult_energy(const double *x, double *y, double *en, hipStream_t s)
+{
+   ECM2_VERIFY(energy_parts() > 0, ERR_UNSUPPORTED, "this form's Mult does not fold the energy");
+   ECM2_VERIFY(x && y && en, ERR_ARG, "null vector");
+   record_start(s);
+   apply_blocks(x, nullptr, y, nullptr, 0, layout_.nblk(), s, false, en);
+   record_stop(s);
+   finish_shared(0, n_sh_, y, nullptr, s);
+}
+
 void PAForm::add_mult(const double *x, double *y, double a, hipStream_t s)
 {
    ECM2_VERIFY(ndofs_ == 0 || y, ERR_ARG, "null vector");
@@ -1498,7 +1515,7 @@ ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, doubl
 }
 
 void PAForm::apply_blocks(const double *x, const double *xg, double *y, double *yg, int b0, int b1,
-                          hipStream_t s, bool latency)
+                          hipStream_t s, bool latency, double *en)
 {
    ECM2_VERIFY(assembled_, ERR_STATE, "apply before Assemble");
    ECM2_VERIFY(resolved_mode_ != KERNEL_UNFUSED, ERR_UNSUPPORTED, "block apply needs a fused kernel");
@@ -1512,6 +1529,7 @@ void PAForm::apply_blocks(const double *x, const double *xg, double *y, double *
    }
    ApplyArgs a = apply_args(x, xg, y, yg, b0, b1);
    a.latency = latency && layout_.kind == QLAYOUT_AFFINE && have_mass_ && have_diff_ && !layout_.tsnap;
+   a.en = en;  // (mult_energy: the snapshot kernel only)
    if (resolved_mode_ == KERNEL_TPE)
    {
       kern::apply_tpe(D_, Q_, have_mass_, have_diff_, a, basis_, rowtab_.data(), s);

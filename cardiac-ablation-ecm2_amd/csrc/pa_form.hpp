@@ -134,6 +134,12 @@ public:
    // localX / localY too, bilinearform_ext.hpp:75), AddMult is stream-serial per form: two calls
    // on the same form must be ordered (same stream or an event), not run concurrently.
    void add_mult(const double *x, double *y, double a, hipStream_t s);
+   // The Mult with its energy x^T A x folded in (CGSolver's den = (A d, d), solvers.cpp:993, without
+   // a dot pass over the vectors): energy_parts() partials (one per workgroup of the single apply
+   // launch, summed in a fixed order by the caller) -- or 0 when this form's kernel does not fold it
+   // (only the coefficient-snapshot kernel k_apply_tpe_ts does; the caller then runs the dot).
+   int energy_parts() const;
+   void mult_energy(const double *x, double *y, double *en, hipStream_t s);
    bool assembled() const { return assembled_; }
    // Incremented by every assemble(): whoever caches device pointers or launches of this form
    // (the distributed form's HIP graphs) rebuilds them when it changes.
@@ -146,7 +152,7 @@ public:
    // latency: small block range on a critical path (the p <= 2 AFFINE kernel then gives each
    // block a workgroup with one quadrature plane per wave).
    void apply_blocks(const double *x, const double *xg, double *y, double *yg, int b0, int b1,
-                     hipStream_t s, bool latency = false);
+                     hipStream_t s, bool latency = false, double *en = nullptr);
    void finish_shared(int i0, int i1, double *y, double *yg, hipStream_t s);
    int n_shared() const { return n_sh_; }
    int n_shared_owned() const { return n_sh_owned_; }

@@ -165,6 +165,23 @@ PCGResult pcg_solve(LinOp &A, const int *ess, int n_ess, const double *b, double
       A.mult(in, out, s);
       kern::ess_restore(n_ess, ess, w.saved.data(), in, out, s);
    };
+   // den = (A d, d) folded into the Mult where the operator can (serial snapshot forms): the
+   // kernel's element energies sum_e d~_e . A_e d~_e (d~ = d with the ess entries zeroed, as the
+   // constrained Mult sees it) plus the DIAG_ONE rows' sum_ess d_i^2 -- the same value as the dot of
+   // d and A d up to the summation order -- one partial per workgroup, summed in a fixed order by
+   // dot_final: no pass over the two vectors (2 streams and a launch per iteration).
+   const int nen = direct ? A.energy_parts() : 0;
+   if (nen > 0 && (int)w.partials.size() < nen + kern::ess_parts(n_ess))
+   {
+      w.partials.resize(nen + kern::ess_parts(n_ess));
+      partials = w.partials.data();
+   }
+   auto cmult_den = [&](double *in, double *out, const kern::PcgCtl *c, const kern::PcgStop *stop) {
+      if (n_ess) { kern::ess_save_zero(n_ess, ess, in, w.saved.data(), s); }
+      A.mult_energy(in, out, partials, s);
+      if (n_ess) { kern::ess_restore(n_ess, ess, w.saved.data(), in, out, s, partials + nen); }
+      kern::dot_final(nen + kern::ess_parts(n_ess), partials, den, s, c, stop, c ? nullptr : w.hs_dev);
+   };
    if (jacobi)
    {
       // OperatorJacobiSmoother on the constrained operator: ess rows get diag 1
@@ -204,8 +221,12 @@ PCGResult pcg_solve(LinOp &A, const int *ess, int n_ess, const double *b, double
       // kernel of a previous solve writes the mirror any more: every solve ends synchronised)
       ECM2_HIP(hipMemsetAsync(w.ctl.data(), 0, sizeof(kern::PcgCtl), s));
       *w.hctl = kern::PcgCtl{};
-      cmult(d, z);
-      dot(z, d, den);
+      if (nen > 0) { cmult_den(d, z, nullptr, nullptr); }
+      else
+      {
+         cmult(d, z);
+         dot(z, d, den);
+      }
       const double den0 = readback(den);
       ECM2_VERIFY(std::isfinite(den0), ERR_NUMERIC, "PCG: den = " << den0);
       if (den0 != 0.0)
@@ -259,12 +280,17 @@ PCGResult pcg_solve(LinOp &A, const int *ess, int n_ess, const double *b, double
             if (i >= max_iter) { break; }
             // x += alpha d, d = M^{-1} r + beta d
             kern::pcg_update_xd(n, nom, den, betanom, x, d, r, dinv, s, ctl);
-            cmult(d, z);
-            // den = (A d, d) and its test (after ++i: final_iter = i + 1 on a den == 0 stop)
+            // z = A d, den = (A d, d) and its test (after ++i: final_iter = i + 1 on a den == 0 stop)
             const kern::PcgStop dstop{r0, i + 1, max_iter, ctl, w.hctl_dev, betanom, 1};
-            if (direct) { kern::dot(n, d, z, partials, den, s, nullptr, ctl, &dstop); }
+            if (nen > 0) { cmult_den(d, z, ctl, &dstop); }
+            else if (direct)
+            {
+               cmult(d, z);
+               kern::dot(n, d, z, partials, den, s, nullptr, ctl, &dstop);
+            }
             else
             {
+               cmult(d, z);
                dot(d, z, den, ctl);
                kern::pcg_check(den, dstop, s);
             }

@@ -36,6 +36,14 @@ public:
    virtual void sum_scalars(double *dev, int n, hipStream_t s) { (void)dev; (void)n; (void)s; }
    // true when sum_scalars communicates (a locally reduced scalar is not yet global)
    virtual bool distributed() const { return false; }
+   // The Mult with its energy x^T A x folded in as energy_parts() partials (PAForm::mult_energy),
+   // or 0 when this operator does not fold it
+   virtual int energy_parts() const { return 0; }
+   virtual void mult_energy(const double *x, double *y, double *en, hipStream_t s)
+   {
+      (void)x; (void)y; (void)en; (void)s;
+      ECM2_VERIFY(false, ERR_UNSUPPORTED, "this operator does not fold the Mult's energy");
+   }
 };
 
 class FormOp : public LinOp
@@ -45,6 +53,8 @@ public:
    int size() const override { return f_.ndofs(); }
    void mult(const double *x, double *y, hipStream_t s) override { f_.mult(x, y, s); }
    void diagonal(double *d, hipStream_t s) override { f_.assemble_diagonal(d, s); }
+   int energy_parts() const override { return f_.energy_parts(); }
+   void mult_energy(const double *x, double *y, double *en, hipStream_t s) override { f_.mult_energy(x, y, en, s); }
 
 private:
    PAForm &f_;

@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""VERDICT r5 item 6, CPU evidence: is the smooth-state SDIRK33 gap at configs[4] size (2.9e-7 between the
+device step and oracle/ode.py, gpurun_out/r5/tests1.txt) intrinsic to the computation?
+
+The oracle (CPU, test infrastructure) is run against ITSELF on Cartesian 68^3 at p = 4 (20.3M DoF), with
+the same state, the same T = M_alpha + c dt K_beta, K = K_beta, the same Dirichlet dofs and the same fixed
+PCG iteration count per stage, once in the mesh's element order and once with the elements randomly
+permuted: the operator is the same, only the rounding of each Mult changes (the CSR transpose sums a
+dof's element contributions in the new order).  The printed relerr(u1 - u0, u2 - u0) is the gap that
+rounding alone produces; it is compared for the smooth state u0 = 37 + 20 exp(-4 |x - 1/2|^2) and a
+uniform-random state, and for 8 fixed iterations and converged stage solves.
+Usage: python3 profiles/r6/sdirk_smooth_cpu.py [iters ...]   (run here, 8 CPU threads)"""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
+import oracle as O  # noqa: E402
+import ode as ODE  # noqa: E402
+from helpers import alpha_bioheat, k_of_T, relerr, temperature  # noqa: E402
+
+sys.path.insert(0, ROOT)
+import __graft_entry__ as G  # noqa: E402
+
+E = G._load_pkg()
+E.load_library()
+
+
+def main():
+    n, order, dt = 68, 4, 0.02
+    m = E.Mesh.MakeCartesian3D(n, n, n)
+    fes = E.H1Space(m, order, E.NUMBERING_STRUCTURED)
+    en, gm = m.element_nodes(), fes.gather_map()
+    P = O.quad_points(en, O.default_q1d(order))
+    alpha, beta = alpha_bioheat(P) / 3.6e6, k_of_T(temperature(P))
+    del P
+    c = ODE.implicit_coeff(23)
+    ess = fes.boundary_dofs()
+    X = fes.dof_coords()
+    states = {"smooth": 37.0 + 20.0 * np.exp(-4.0 * np.sum((X - 0.5) ** 2, axis=1)),
+              "random": np.random.default_rng(68).uniform(-1.0, 1.0, fes.ndofs)}
+    perm = np.random.default_rng(7).permutation(fes.ne)
+    orders = {"natural": np.arange(fes.ne), "permuted": perm}
+    runs = [(8, 0.0)] + [(int(a), 1e-12) for a in sys.argv[1:]]
+    print(f"# configs[4]: Cartesian {n}^3, p = {order}, {fes.ndofs} DoF, SDIRK33 dt = {dt}, "
+          f"{ess.size} Dirichlet dofs, oracle threads = {O.num_threads()}", flush=True)
+    res = {}
+    for oname, o in orders.items():
+        Tr = O.OracleOperator(en[o], gm[o], fes.ndofs, order, alpha=alpha[o], beta=c * dt * beta[o])
+        Kr = O.OracleOperator(en[o], gm[o], fes.ndofs, order, beta=beta[o])
+        for max_iter, tol in runs:
+            its = []
+
+            def solve(us):
+                rhs = -Kr.mult(us)
+                rhs[ess] = 0.0
+                xs, it, _ = Tr.pcg(rhs, ess, rel_tol=tol, max_iter=max_iter if tol == 0 else 100000)
+                its.append(it)
+                return xs
+
+            for sname, u0 in states.items():
+                t0 = time.time()
+                res[(oname, max_iter, tol, sname)] = ODE.step(23, solve, u0, dt)
+                print(f"{oname:8s} {sname:6s} stage solves {'fixed ' + str(max_iter) if tol == 0 else 'rel_tol 1e-12'}: "
+                      f"iterations {its[-3:]}  {time.time() - t0:.1f} s", flush=True)
+        del Tr, Kr
+    print("# relerr(u_natural - u0, u_permuted - u0): the gap rounding alone produces", flush=True)
+    for max_iter, tol in runs:
+        for sname, u0 in states.items():
+            a = res[("natural", max_iter, tol, sname)] - u0
+            b = res[("permuted", max_iter, tol, sname)] - u0
+            lab = f"fixed {max_iter} iterations" if tol == 0 else "converged (rel_tol 1e-12)"
+            print(f"{sname:6s} state, {lab:28s}: relerr = {relerr(b, a):.3e}   |u1 - u0|_inf = {np.abs(a).max():.3e}")
+
+
+if __name__ == "__main__":
+    main()

@@ -460,6 +460,108 @@ def test_c4_full_size_eight_way_members():
     assert relerr(y, ref) <= RTOL
 
 
+def _c5_group(m, fes, er, nranks, alpha_fn, beta_fn, q1d):
+    """The 8 z-slab members of configs[4] (OVERLAP, the serial schedule), each with its own
+    quadrature-point coefficients; alpha_fn / beta_fn map points to values (None: integrator absent)."""
+    forms, parts = [], []
+    for r in range(nranks):
+        part = E.Partition(fes, er, r, nranks, decomposition="overlap")
+        pf = E.ParBilinearForm(part)
+        P = E.quadrature_points_subset(m, q1d, part.elems)
+        if alpha_fn is not None:
+            pf.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(alpha_fn(P).reshape(part.ne_local, -1)))))
+        pf.AddDomainIntegrator(E.DiffusionIntegrator(E.QuadratureCoefficient(dev(beta_fn(P).reshape(part.ne_local, -1)))))
+        pf.Assemble()
+        forms.append(pf)
+        parts.append(part)
+        del P
+    return forms, parts
+
+
+def test_c5_full_size_eight_way_members():
+    """configs[4] split 8 ways at size: Cartesian 68^3 at p = 4 (20.3M DoF) in 8
+    z-slabs (CartesianPartitioning rounding: 8 or 9 element layers per rank), OVERLAP, every rank's
+    elements in 2 x 2 x 1 bricks + the line kernel; every member's rows alone (ParGroup.MultMember,
+    what one rank computes on its GPU) and the whole group against one oracle Mult of the full mesh
+    -- the p = 4 analogue of test_c4_full_size_eight_way_members."""
+    n, nranks, order = 68, 8, 4
+    m = E.Mesh.MakeCartesian3D(n, n, n)
+    fes = E.H1Space(m, order, E.NUMBERING_STRUCTURED)
+    assert fes.ndofs == 20346417
+    er = E.partition_slabs_z(m, nranks)
+    q1d = O.default_q1d(order)
+    forms, parts = _c5_group(m, fes, er, nranks, alpha_bioheat, lambda P: k_of_T(temperature(P)), q1d)
+    xg = np.random.default_rng(68).uniform(-1, 1, fes.ndofs)
+    xs = [dev(xg[p.owned_global]) for p in parts]
+    ys = [torch.full((p.n_owned,), float("nan"), dtype=torch.float64, device="cuda") for p in parts]
+    Pg = O.quad_points(m.element_nodes(), q1d)
+    ref = O.OracleOperator(m.element_nodes(), fes.gather_map(), fes.ndofs, order, alpha=alpha_bioheat(Pg),
+                           beta=k_of_T(temperature(Pg))).mult(xg)
+    del Pg
+    group = E.ParGroup(forms)
+    for r in range(nranks):
+        group.MultMember(r, xs, ys)
+    y = np.full(fes.ndofs, np.nan)
+    for part, yt in zip(parts, ys):
+        y[part.owned_global] = host(yt)
+    assert relerr(y, ref) <= RTOL
+    for yt in ys:
+        yt.fill_(float("nan"))
+    group.Mult(xs, ys)
+    for part, yt in zip(parts, ys):
+        y[part.owned_global] = host(yt)
+    assert relerr(y, ref) <= RTOL
+
+
+def test_c5_full_size_eight_way_sdirk():
+    """configs[4]'s implicit step on its 8-way split: one SDIRK33 step of
+    M du/dt = -K u (ode.cpp:834-859, ex16p.cpp:373-470) at 68^3 p = 4 through Operator(group) -- T and
+    K as 8-member loopback groups, the group's dots global, Dirichlet dofs held, each stage a
+    constrained Jacobi-PCG with a fixed 8 iterations -- against the same step on the serial form (itself
+    pinned to oracle/ode.py by test_c5_sdirk_step_full_size)."""
+    n, nranks, order, dt, iters = 68, 8, 4, 0.02, 8
+    m = E.Mesh.MakeCartesian3D(n, n, n)
+    fes = E.H1Space(m, order, E.NUMBERING_STRUCTURED)
+    er = E.partition_slabs_z(m, nranks)
+    q1d = O.default_q1d(order)
+    c = E.ode_implicit_coeff(23)
+    a_fn = lambda P: alpha_bioheat(P) / 3.6e6
+    b_fn = lambda P: k_of_T(temperature(P))
+    ess = fes.boundary_dofs()
+    u0 = np.random.default_rng(69).uniform(-1.0, 1.0, fes.ndofs)
+    # the serial form's step
+    P = O.quad_points(m.element_nodes(), q1d)
+    T = _serial_form(fes, None, a_fn(P), c * dt * b_fn(P))
+    K = _serial_form(fes, None, None, b_fn(P))
+    del P
+    u = dev(u0)
+    ns, it, conv = E.ode_step(23, E.Operator(T), E.Operator(K), dt, u, ess=dev(ess, torch.int32), rel_tol=0.0,
+                              max_iter=iters)
+    assert ns == 3 and it == 3 * iters
+    us = host(u)
+    del T, K, u
+    # the group's step
+    Tf, parts = _c5_group(m, fes, er, nranks, a_fn, lambda P: c * dt * b_fn(P), q1d)
+    Kf, _ = _c5_group(m, fes, er, nranks, None, b_fn, q1d)
+    Tg, Kg = E.ParGroup(Tf), E.ParGroup(Kf)
+    ug = dev(np.concatenate([u0[p.owned_global] for p in parts]))
+    idx, o = [], 0
+    for p in parts:
+        idx.append(np.nonzero(np.isin(p.owned_global, ess))[0] + o)
+        o += p.n_owned
+    essg = dev(np.concatenate(idx).astype(np.int32), torch.int32)
+    ns, it, conv = E.ode_step(23, E.Operator(Tg), E.Operator(Kg), dt, ug, ess=essg, rel_tol=0.0, max_iter=iters)
+    assert ns == 3 and it == 3 * iters
+    ugh = host(ug)
+    uh = np.empty(fes.ndofs)
+    o = 0
+    for p in parts:
+        uh[p.owned_global] = ugh[o: o + p.n_owned]
+        o += p.n_owned
+    assert np.array_equal(uh[ess], u0[ess])
+    assert relerr(uh - u0, us - u0) < 1e-9
+
+
 @pytest.mark.parametrize("decomp", ["rap", "overlap"])
 def test_c4_eight_way_boxes(decomp):
     """The 2 x 2 x 2 box split of configs[3] (bench.py --partition boxes; SURVEY §8(d) names

@@ -323,3 +323,12 @@ def test_point_coefficients_are_checked_before_the_gpu():
         E._check_points(E.VectorCoefficient(None), np.zeros((ne, nq, 3)), ((3,),), ne, nq)
     # the grid-function kinds map to the ABI's kinds without touching the data
     assert E.COEFF_GRIDFUNC == 10 and E.GridFunctionCoefficient(None).T is None
+    # ... and their fields are checked the same way: float32, a host tensor, or a field
+    # whose length is not the form's L-vector size never reaches the snapshot kernels
+    for T in (torch.zeros(125, dtype=torch.float32), torch.zeros(125, dtype=torch.float64), None):
+        for c in (E.GridFunctionCoefficient(T), E.AffineGridFunctionCoefficient(T, 1.0, 0.1, 37.0),
+                  E.PerfusionCoefficient(T, 1.0, 0.1, 0.5, 0.02, 37.0, 50.0)):
+            with pytest.raises(E.ECM2Error):
+                E._integrator_args(c, [], ne, nq, 125)
+    with pytest.raises(E.ECM2Error):
+        E._check_field(E.GridFunctionCoefficient(None), np.zeros(125), 125)

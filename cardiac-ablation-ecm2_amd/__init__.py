@@ -106,6 +106,7 @@ def load_library(path: str = LIB_PATH):
         "ecm2_pa_form_set_geometry_compression": (i32, [vp, i32]),
         "ecm2_pa_form_set_coefficient_snapshot": (i32, [vp, i32]),
         "ecm2_pa_form_coefficient_snapshot": (i32, [vp, ip]),
+        "ecm2_pa_form_energy_parts": (i32, [vp, ip]),
         "ecm2_pa_form_qdata_bytes": (i32, [vp, dp]),
         "ecm2_pa_form_brick_info": (i32, [vp, ip, ip]),
         "ecm2_pa_form_addressing_info": (i32, [vp, ip, ip, ctypes.POINTER(ctypes.c_long)]),
@@ -657,6 +658,12 @@ class BilinearForm:
         v = [ctypes.c_int() for _ in range(3)]
         _check(_lib.ecm2_pa_form_snapshot_info(self._h, *[ctypes.byref(a) for a in v]))
         return bool(v[0].value), v[1].value, bool(v[2].value)
+
+    def EnergyParts(self):
+        """Partials of x^T A x the Mult writes when PCG folds its den = (A d, d) into it (0: a dot pass)."""
+        v = ctypes.c_int()
+        _check(_lib.ecm2_pa_form_energy_parts(self._h, ctypes.byref(v)))
+        return v.value
 
     def AssembleDiagonal(self, diag, stream=None):
         _check(_lib.ecm2_pa_form_assemble_diagonal(self._h, _dev_ptr(diag), _stream(stream)))

@@ -420,6 +420,11 @@ int ecm2_pa_form_snapshot_info(const ecm2_pa_form *f, int *on, int *mass_values,
    });
 }
 
+int ecm2_pa_form_energy_parts(const ecm2_pa_form *f, int *parts)
+{
+   return guard([&] { NEED(f); NEED(parts); *parts = f->f->energy_parts(); });
+}
+
 int ecm2_pa_form_set_bricks(ecm2_pa_form *f, int bz)
 {
    return guard([&] { NEED(f); f->f->set_line_bricks(bz); });

@@ -248,7 +248,6 @@ __global__ void k_copy_values(int n, const int *__restrict__ idx, const double *
    if (i < n) { y[idx[i]] = x[idx[i]]; }
 }
 
-constexpr int kDotBlocks = 1024;
 
 // CGSolver's stopping tests (solvers.cpp:950-1000) as the device-driven loop runs them.
 // kind 0: the test of iteration `it` on betanom = (B r, r): not finite -> MFEM_VERIFY's abort
@@ -299,7 +298,7 @@ __device__ void pcg_check_one(double v, const PcgCheck &c)
    }
 }
 
-// Deterministic dot, pass 1: each of kDotBlocks workgroups writes its grid-stride sum.  (A
+// Deterministic dot, pass 1: each workgroup writes its sum (a fixed order per workgroup).  (A
 // one-pass form -- the last workgroup to arrive on a counter sums the parks -- was measured slower:
 // the 1,024 arrivals on one counter serialise, 16.6 vs 6.5 us per dot at a rank's 1.28M dofs,
 // profiles/r5/dot_probe.txt.)
@@ -313,34 +312,54 @@ __device__ __forceinline__ void dot_park(double s, double *__restrict__ partials
 }
 
 // (ctl: read only when no check writes it in the same kernel -- no __restrict__ on it)
+// A flat grid of contiguous chunks: workgroup b sums pairs [b kStepChunk, (b + 1) kStepChunk) -- grid-stride
+// loops stream 15-35% slower on this chip (profiles/r6/copy_probe.json: a 16-byte copy 6.67 TB/s flat against
+// 4.4-5.4 TB/s grid-stride).
+constexpr int kStepK = 4, kStepChunk = 256 * kStepK;
 __global__ void __launch_bounds__(256)
 k_dot_partial(int n, const double *__restrict__ a, const double *__restrict__ b, double *__restrict__ partials,
               const PcgCtl *ctl)
 {
    if (ctl && ctl->done) { return; }  // (wave-uniform)
    double s = 0.0;
-   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+   const long n2 = n / 2, base = (long)blockIdx.x * kStepChunk + threadIdx.x;
+   const v2d *a2 = reinterpret_cast<const v2d *>(a), *b2 = reinterpret_cast<const v2d *>(b);
+#pragma unroll
+   for (int k = 0; k < kStepK; k++)
    {
-      s += a[i] * b[i];
+      const long i = base + 256 * k;
+      if (i < n2)
+      {
+         const v2d u = a2[i], v = b2[i];
+         s += u.x * v.x;
+         s += u.y * v.y;
+      }
    }
+   if ((n & 1) && blockIdx.x == gridDim.x - 1 && threadIdx.x == 255) { s += a[n - 1] * b[n - 1]; }
    dot_park(s, partials);
 }
 
-// pass 2 (one workgroup): the partials in a fixed order; optionally a stopping test on the result
-__global__ void __launch_bounds__(256)
+// pass 2 (one workgroup of kFinalThreads): the partials in a fixed order; optionally a stopping test on
+// the result.  (1,024 threads: the 4,921 energy partials of a C4 Mult are 5 loads per thread, not 20 --
+// a latency-bound single workgroup, 8.5 -> ~4 us per PCG iteration, profiles/r6/gpu3.)
+constexpr int kFinalThreads = 1024;
+__global__ void __launch_bounds__(kFinalThreads)
 k_dot_final(int nparts, const double *__restrict__ partials, double *__restrict__ out, double *__restrict__ hout,
             const PcgCtl *ctl, PcgCheck chk, int with_check)
 {
    if (ctl && ctl->done) { return; }
-   __shared__ double red[4];
+   constexpr int NW = kFinalThreads / 64;
+   __shared__ double red[NW];
    double s = 0.0;
-   for (int i = threadIdx.x; i < nparts; i += blockDim.x) { s += partials[i]; }
+   for (int i = threadIdx.x; i < nparts; i += kFinalThreads) { s += partials[i]; }
    for (int off = 32; off > 0; off >>= 1) { s += __shfl_down(s, off, 64); }
    if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6] = s; }
    __syncthreads();
    if (threadIdx.x == 0)
    {
-      const double v = (red[0] + red[1]) + (red[2] + red[3]);
+      double v = 0.0;
+#pragma unroll
+      for (int k = 0; k < NW; k += 2) { v += red[k] + red[k + 1]; }
       *out = v;
       if (hout) { *hout = v; }  // mapped pinned host mirror (the solver's read-back)
       if (with_check) { pcg_check_one(v, chk); }
@@ -348,11 +367,15 @@ k_dot_final(int nparts, const double *__restrict__ partials, double *__restrict_
 }
 
 // The residual half of CGSolver's update (solvers.cpp:930-947): alpha = nom/den; r -= alpha A d;
-// z = dinv .* r (jacobi) and the partial sums of r.z (or r.r) in the fixed grid-stride order of
-// k_dot_partial, finished by k_dot_final.  z holds A d on entry; z is not stored (k_pcg_update_xd
-// forms it again from r where it is consumed: 4 vector streams here instead of 8).  x += alpha d is
-// deferred to k_pcg_update_xd (or k_pcg_finish_x after the stop), which reads d anyway.  Same
-// arithmetic per entry as CGSolver's add / Mult(prec) / Dot.  alpha_out: alpha of the last step run.
+// z = dinv .* r (jacobi) and the partial sums of r.z (or r.r), one per workgroup in a fixed order,
+// finished by k_dot_final.  z holds A d on entry; z is not stored (k_pcg_update_xd forms it again from
+// r where it is consumed: 4 vector streams here instead of 8).  x += alpha d is deferred to
+// k_pcg_update_xd (or k_pcg_finish_x after the stop), which reads d anyway.  Same arithmetic per entry
+// as CGSolver's add / Mult(prec) / Dot.  alpha_out: alpha of the last step run.  16-byte accesses, a
+// grid-stride loop over kStepBlocks workgroups.  (The flat chunked grid of k_dot_partial was tried here
+// too: a GPU test later in the same process aborted in garbage collection with it, reproducibly, and
+// passed with this form -- profiles/r6/gpu5-gpu9; not diagnosed further, so this form stays.)
+constexpr int kStepBlocks = 1024;
 __global__ void __launch_bounds__(256)
 k_pcg_step_r(int n, const double *__restrict__ nom, const double *__restrict__ den, const double *__restrict__ z,
              double *__restrict__ r, const double *__restrict__ dinv, double *__restrict__ partials,
@@ -362,12 +385,31 @@ k_pcg_step_r(int n, const double *__restrict__ nom, const double *__restrict__ d
    const double alpha = *nom / *den;
    if (blockIdx.x == 0 && threadIdx.x == 0) { *alpha_out = alpha; }
    double s = 0.0;
-   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+   const long n2 = n / 2, stride = (long)gridDim.x * blockDim.x, t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   const v2d *z2 = reinterpret_cast<const v2d *>(z), *q2 = reinterpret_cast<const v2d *>(dinv);
+   v2d *r2 = reinterpret_cast<v2d *>(r);
+   for (long i = t; i < n2; i += stride)
    {
+      const v2d rn = r2[i] + (-alpha) * z2[i];
+      r2[i] = rn;
+      if (dinv)
+      {
+         const v2d q = q2[i];
+         s += rn.x * (q.x * rn.x);
+         s += rn.y * (q.y * rn.y);
+      }
+      else
+      {
+         s += rn.x * rn.x;
+         s += rn.y * rn.y;
+      }
+   }
+   if ((n & 1) && t == stride - 1)  // the odd tail
+   {
+      const long i = n - 1;
       const double rn = r[i] + (-alpha) * z[i];
       r[i] = rn;
-      if (dinv) { s += rn * (dinv[i] * rn); }
-      else { s += rn * rn; }
+      s += dinv ? rn * (dinv[i] * rn) : rn * rn;
    }
    dot_park(s, partials);
 }
@@ -381,13 +423,27 @@ k_pcg_update_xd(int n, const double *__restrict__ nom, const double *__restrict_
                 const double *__restrict__ betanom, double *__restrict__ x, double *__restrict__ d,
                 const double *__restrict__ r, const double *__restrict__ dinv, const PcgCtl *ctl)
 {
-   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-   if (i >= n || (ctl && ctl->done)) { return; }
+   // 16-byte accesses: entries 2i, 2i + 1 per lane (the last lane of an odd n takes the tail)
+   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x, n2 = n / 2;
+   if (i > n2 || (ctl && ctl->done)) { return; }
    const double alpha = *nom / *den, beta = *betanom / *nom;
-   const double dold = d[i];
-   x[i] = x[i] + alpha * dold;
-   const double z = dinv ? dinv[i] * r[i] : r[i];
-   d[i] = z + beta * dold;
+   if (i < n2)
+   {
+      v2d *x2 = reinterpret_cast<v2d *>(x), *d2 = reinterpret_cast<v2d *>(d);
+      const v2d *r2 = reinterpret_cast<const v2d *>(r), *q2 = reinterpret_cast<const v2d *>(dinv);
+      const v2d dold = d2[i];
+      x2[i] = x2[i] + alpha * dold;
+      const v2d z = dinv ? q2[i] * r2[i] : r2[i];
+      d2[i] = z + beta * dold;
+   }
+   else if (n & 1)
+   {
+      const long j = n - 1;
+      const double dold = d[j];
+      x[j] = x[j] + alpha * dold;
+      const double z = dinv ? dinv[j] * r[j] : r[j];
+      d[j] = z + beta * dold;
+   }
 }
 
 // After the loop: the stopping iteration's x += alpha d, when the stop came from its betanom test
@@ -455,20 +511,13 @@ __global__ void k_add_scaled(int n, const double *x, double c, const double *__r
 // the access shape of the guide's 6.29 TB/s float4-copy figure.
 // STREAM copy for the roofline reference: 16-byte nontemporal accesses, four independent
 // loads in flight per thread before their stores (one in flight per thread measured ~5.4 TB/s).
+// HBM copy peak (bench.py's stream_copy_gbs): one 16-byte nontemporal load and store per thread, a flat
+// grid -- the fastest form of profiles/calib/copy_probe.hip (6.67 TB/s; the grid-stride form this
+// replaces read 4.6-5.4 TB/s, profiles/r6/copy_probe.json).
 __global__ void __launch_bounds__(256) k_stream_copy(long n2, const v2d *__restrict__ a, v2d *__restrict__ b)
 {
-   constexpr int U = 4;
-   const long stride = (long)gridDim.x * blockDim.x;
-   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-   for (; i + (U - 1) * stride < n2; i += U * stride)
-   {
-      v2d v[U];
-#pragma unroll
-      for (int u = 0; u < U; u++) { v[u] = __builtin_nontemporal_load(a + i + u * stride); }
-#pragma unroll
-      for (int u = 0; u < U; u++) { __builtin_nontemporal_store(v[u], b + i + u * stride); }
-   }
-   for (; i < n2; i += stride) { __builtin_nontemporal_store(__builtin_nontemporal_load(a + i), b + i); }
+   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < n2) { __builtin_nontemporal_store(__builtin_nontemporal_load(a + i), b + i); }
 }
 
 // Read-only stream: one 16-byte nontemporal load per thread per step, 8 workgroups of 256
@@ -653,6 +702,8 @@ void copy_values(int n, const int *idx, const double *x, double *y, hipStream_t 
    ECM2_HIP(hipGetLastError());
 }
 
+int step_parts(int n) { return std::max(1, (int)((n / 2 + kStepChunk - 1) / kStepChunk)); }
+
 static PcgCheck to_check(const PcgStop *stop)
 {
    return stop ? PcgCheck{stop->r0, stop->it, stop->max_iter, stop->ctl, stop->host, stop->betanom, stop->kind}
@@ -662,8 +713,9 @@ static PcgCheck to_check(const PcgStop *stop)
 void dot(int n, const double *a, const double *b, double *partials, double *out, hipStream_t s, double *hout,
          const PcgCtl *ctl, const PcgStop *stop)
 {
-   hipLaunchKernelGGL(k_dot_partial, dim3(kDotBlocks), dim3(256), 0, s, n, a, b, partials, ctl);
-   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, s, kDotBlocks, partials, out, hout, ctl, to_check(stop),
+   const int nb = step_parts(n);
+   hipLaunchKernelGGL(k_dot_partial, dim3(nb), dim3(256), 0, s, n, a, b, partials, ctl);
+   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(kFinalThreads), 0, s, nb, partials, out, hout, ctl, to_check(stop),
                       stop ? 1 : 0);
    ECM2_HIP(hipGetLastError());
 }
@@ -671,8 +723,9 @@ void dot(int n, const double *a, const double *b, double *partials, double *out,
 void pcg_step_r(int n, const double *nom, const double *den, const double *z, double *r, const double *dinv,
                 double *partials, double *out, double *alpha, hipStream_t s, const PcgCtl *ctl, const PcgStop *stop)
 {
-   hipLaunchKernelGGL(k_pcg_step_r, dim3(kDotBlocks), dim3(256), 0, s, n, nom, den, z, r, dinv, partials, alpha, ctl);
-   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, s, kDotBlocks, partials, out, nullptr, ctl, to_check(stop),
+   const int nb = kStepBlocks;
+   hipLaunchKernelGGL(k_pcg_step_r, dim3(nb), dim3(256), 0, s, n, nom, den, z, r, dinv, partials, alpha, ctl);
+   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(kFinalThreads), 0, s, nb, partials, out, nullptr, ctl, to_check(stop),
                       stop ? 1 : 0);
    ECM2_HIP(hipGetLastError());
 }
@@ -681,8 +734,8 @@ void pcg_update_xd(int n, const double *nom, const double *den, const double *be
                    const double *r, const double *dinv, hipStream_t s, const PcgCtl *ctl)
 {
    if (n == 0) { return; }
-   hipLaunchKernelGGL(k_pcg_update_xd, dim3(grid_for(n, 256)), dim3(256), 0, s, n, nom, den, betanom, x, d, r, dinv,
-                      ctl);
+   hipLaunchKernelGGL(k_pcg_update_xd, dim3(grid_for(n / 2 + 1, 256)), dim3(256), 0, s, n, nom, den, betanom, x, d,
+                      r, dinv, ctl);
    ECM2_HIP(hipGetLastError());
 }
 
@@ -718,7 +771,7 @@ int ess_parts(int n) { return n > 0 ? grid_for(n, 256) : 0; }
 void dot_final(int nparts, const double *partials, double *out, hipStream_t s, const PcgCtl *ctl,
                const PcgStop *stop, double *hout)
 {
-   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, s, nparts, partials, out, hout, ctl, to_check(stop),
+   hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(kFinalThreads), 0, s, nparts, partials, out, hout, ctl, to_check(stop),
                       stop ? 1 : 0);
    ECM2_HIP(hipGetLastError());
 }
@@ -747,8 +800,9 @@ void stream_copy(long n, const double *a, double *b, hipStream_t s)
 {
    ECM2_VERIFY(n % 2 == 0 && ((uintptr_t)a % 16) == 0 && ((uintptr_t)b % 16) == 0, ERR_ARG,
                "stream_copy needs 16-byte aligned even-length arrays");
-   hipLaunchKernelGGL(k_stream_copy, dim3(256 * 64), dim3(256), 0, s, n / 2, reinterpret_cast<const v2d *>(a),
-                      reinterpret_cast<v2d *>(b));
+   const long n2 = n / 2;
+   hipLaunchKernelGGL(k_stream_copy, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, s, n2,
+                      reinterpret_cast<const v2d *>(a), reinterpret_cast<v2d *>(b));
    ECM2_HIP(hipGetLastError());
 }
 

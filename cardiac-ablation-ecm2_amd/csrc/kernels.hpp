@@ -504,7 +504,7 @@ struct PcgStop
    const double *betanom = nullptr;
    int kind = 0;
 };
-// Deterministic two-pass dot: result written to *out (device).  partials: kDotPartials doubles.
+// Deterministic two-pass dot: result written to *out (device).  partials: max(step_parts(n), kDotPartials).
 // hout (optional): device pointer of mapped pinned host memory that also receives the result.
 // stop (serial solver): a stopping test on *out in the same launch.
 constexpr int kDotPartials = 1024;
@@ -515,6 +515,9 @@ void dot(int n, const double *a, const double *b, double *partials, double *out,
 //               (r.r without dinv), deterministic; stop (serial): betanom test in the same launch;
 //   pcg_update_xd: x += (nom/den) d; d = dinv .* r + (betanom/nom) d;
 //   pcg_finish_x (after the loop): x += *alpha d if the loop stopped at a betanom test.
+// the partial sums of dot's first pass (one per workgroup of its flat grid; pcg_step_r writes kDotPartials):
+// the partials buffer must hold them
+int step_parts(int n);
 void pcg_step_r(int n, const double *nom, const double *den, const double *z, double *r, const double *dinv,
                 double *partials, double *out, double *alpha, hipStream_t s, const PcgCtl *ctl = nullptr,
                 const PcgStop *stop = nullptr);

@@ -171,9 +171,10 @@ PCGResult pcg_solve(LinOp &A, const int *ess, int n_ess, const double *b, double
    // d and A d up to the summation order -- one partial per workgroup, summed in a fixed order by
    // dot_final: no pass over the two vectors (2 streams and a launch per iteration).
    const int nen = direct ? A.energy_parts() : 0;
-   if (nen > 0 && (int)w.partials.size() < nen + kern::ess_parts(n_ess))
+   const int nparts = std::max({kern::kDotPartials, kern::step_parts(n), nen + kern::ess_parts(n_ess)});
+   if ((int)w.partials.size() < nparts)
    {
-      w.partials.resize(nen + kern::ess_parts(n_ess));
+      w.partials.resize(nparts);
       partials = w.partials.data();
    }
    auto cmult_den = [&](double *in, double *out, const kern::PcgCtl *c, const kern::PcgStop *stop) {

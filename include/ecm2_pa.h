@@ -206,6 +206,10 @@ int ecm2_pa_form_coefficient_snapshot(const ecm2_pa_form *f, int *on);
  * per element (constant or same-field mass law); *law_at_point 1 = the field itself is interpolated and
  * the laws applied at the point, 0 = an affine / identity law applied to the snapshot's dofs. */
 int ecm2_pa_form_snapshot_info(const ecm2_pa_form *f, int *on, int *mass_values, int *law_at_point);
+/* Introspection (no reference counterpart): the number of partial sums of x^T A x the form's Mult
+ * writes when ecm2_pcg_solve folds CGSolver's den = (A d, d) (solvers.cpp:993) into it -- one per
+ * workgroup of the coefficient-snapshot kernel -- or 0 when the solver runs the dot pass instead. */
+int ecm2_pa_form_energy_parts(const ecm2_pa_form *f, int *parts);
 /* BilinearForm::AddDomainIntegrator(new MassIntegrator(Q)) / DiffusionIntegrator(Q)
  * (bilinearform.cpp:231-242).  data: CONSTANT -> data[0] (host);
  * QUAD -> device [ne][nq]; GRIDFUNC_AFFINE -> device L-vector T with

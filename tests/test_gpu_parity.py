@@ -467,6 +467,42 @@ def test_coefficient_snapshot(numbering, mass):
     assert not f3.CoefficientSnapshot()
 
 
+@pytest.mark.parametrize("numbering", [E.NUMBERING_STRUCTURED, E.NUMBERING_ENTITY])
+@pytest.mark.parametrize("with_ess", [True, False])
+def test_pcg_energy_folded_den(numbering, with_ess):
+    """CGSolver's den = (A d, d) folded into the snapshot kernel's element energies (sum_e d~_e . A_e d~_e
+    with the ess entries zeroed, plus sum_ess d_i^2 for the DIAG_ONE rows; PAForm::mult_energy): the
+    device PCG on a snapshot form takes that path (EnergyParts() > 0) and returns CGSolver's iterates --
+    x after a fixed 6 iterations and a converging solve's stopping iteration and x -- against the oracle
+    (solvers.cpp:869-1004), with and without essential dofs, in both numberings."""
+    n, order = 8, 2
+    sfc = numbering == E.NUMBERING_ENTITY
+    m = E.Mesh.MakeCartesian3D(n, n, n, 1.0, 0.7, 1.3, sfc_ordering=sfc)
+    fes = E.H1Space(m, order, numbering)
+    en = m.element_nodes()
+    q1d = O.default_q1d(order)
+    T = temperature(fes.dof_coords())
+    scale, slope, tref = 0.05, 0.0012, 37.0
+    a = alpha_bioheat(O.quad_points(en, q1d)) / 3.6e6
+    form = E.BilinearForm(fes, element_order="faces" if sfc else "auto")
+    form.AddDomainIntegrator(E.MassIntegrator(E.QuadratureCoefficient(dev(a.reshape(fes.ne, -1)))))
+    form.AddDomainIntegrator(E.DiffusionIntegrator(E.AffineGridFunctionCoefficient(dev(T), scale, slope, tref)))
+    form.Assemble()
+    assert form.CoefficientSnapshot() and form.EnergyParts() == ((fes.ne + 63) // 64 + 3) // 4
+    Tq = O.interp_evector(T[fes.gather_map()], order, q1d)
+    op = O.OracleOperator(en, fes.gather_map(), fes.ndofs, order, alpha=a, beta=scale * (1.0 + slope * (Tq - tref)))
+    ess = fes.boundary_dofs() if with_ess else np.zeros(0, np.int32)
+    esst = dev(ess, torch.int32) if ess.size else None
+    b = np.random.default_rng(23).uniform(-1, 1, fes.ndofs)
+    x = torch.empty(fes.ndofs, dtype=torch.float64, device="cuda")
+    it, nrm = form.PCG(dev(b), x, ess=esst, rel_tol=0.0, max_iter=6, jacobi=True)
+    xr, itr, nr = op.pcg(b, ess, rel_tol=0.0, max_iter=6, jacobi=True)
+    assert it == itr == 6 and relerr(host(x), xr) < 1e-11 and nrm == pytest.approx(nr, rel=1e-9)
+    it, nrm = form.PCG(dev(b), x, ess=esst, rel_tol=1e-8, max_iter=500, jacobi=True)
+    xr, itr, nr = op.pcg(b, ess, rel_tol=1e-8, max_iter=500, jacobi=True)
+    assert it == itr and E.pcg_last_converged() and relerr(host(x), xr) < 1e-10
+
+
 @pytest.mark.parametrize("snap", [True, False])
 def test_marker_diagonal_keeps_assemble_time_state(snap):
     """Diffusion k(T) added first, then a MassIntegrator(perfusion(T)) restricted to attribute 1; T

@@ -681,7 +681,82 @@ __device__ __forceinline__ unsigned lattice_xyz(int j)
    static_assert(D == 3, "p = 2 lattice table");
    return kLatXYZ3.v[j];
 }
-// The padded LDS slot (tsl_slot, kernels.hpp) of each lattice slot j, for k_apply_tpe_ts's gather.
+// The gather's order of the lattice slots: entry p (lane p % 64 of the gather's step p / 64) holds
+// lattice slot j | its padded LDS slot << 16.  Within each 64-slot step the slots are dealt into the
+// eight 8-lane groups of ds_write_b128 (32 banks: 8 slots of 16 bytes) so that a group's slots differ
+// mod 8 as far as the step's residues allow (greedy: the residue with the most slots left first).  In
+// slot order the padded rows put two lanes of a group on one bank 63 times per wave (0.35 conflict cycles
+// per LDS instruction of the kernel); dealt, 40 (a model of the 27 x 4 reads and 12 writes per wave,
+// profiles/r6/lds_model.py -> lds_model.txt).  A step's lanes still read the same map / snapshot lines.
+struct LatticeTsGather
+{
+   static constexpr int N = tpe_lattice_points(3);
+   unsigned v[N];
+   constexpr LatticeTsGather() : v()
+   {
+      int lds[N] = {};
+      for (int Z = 0; Z < 9; Z++)
+         for (int Y = 0; Y < 9; Y++)
+            for (int X = 0; X < 9; X++) { lds[tpe_lattice_slot(3, X, Y, Z)] = tsl_slot(X, Y, Z); }
+      for (int k0 = 0; k0 < N; k0 += 64)
+      {
+         const int m = N - k0 < 64 ? N - k0 : 64;
+         bool taken[64] = {};
+         int out = 0;
+         while (out < m)
+         {
+            const int gsize = m - out < 8 ? m - out : 8;
+            bool used[8] = {};
+            for (int t = 0; t < gsize; t++)
+            {
+               int cnt[8] = {};
+               for (int i = 0; i < m; i++)
+               {
+                  if (!taken[i]) { cnt[lds[k0 + i] & 7]++; }
+               }
+               int best = -1;
+               for (int r = 0; r < 8; r++)
+               {
+                  if (cnt[r] && !used[r] && (best < 0 || cnt[r] > cnt[best])) { best = r; }
+               }
+               if (best < 0)  // every residue left is in the group already: the largest
+               {
+                  for (int r = 0; r < 8; r++)
+                  {
+                     if (cnt[r] && (best < 0 || cnt[r] > cnt[best])) { best = r; }
+                  }
+               }
+               for (int i = 0; i < m; i++)
+               {
+                  if (!taken[i] && (lds[k0 + i] & 7) == best)
+                  {
+                     taken[i] = true;
+                     v[k0 + out] = (unsigned)(k0 + i) | (unsigned)lds[k0 + i] << 16;
+                     out++;
+                     break;
+                  }
+               }
+               used[best] = true;
+            }
+         }
+      }
+   }
+};
+constexpr bool ts_gather_is_permutation()
+{
+   constexpr LatticeTsGather g;
+   bool seen[LatticeTsGather::N] = {};
+   for (int p = 0; p < LatticeTsGather::N; p++)
+   {
+      const int j = (int)(g.v[p] & 0xffff);
+      if (j >= LatticeTsGather::N || seen[j] || (p / 64) != (j / 64)) { return false; }
+      seen[j] = true;
+   }
+   return true;
+}
+static_assert(ts_gather_is_permutation(), "the gather order permutes the slots within each 64-slot step");
+__constant__ LatticeTsGather kLatTsGather3 = LatticeTsGather();
+// The padded LDS slot (tsl_slot, kernels.hpp) of each lattice slot j (regular blocks: slot order).
 struct LatticeTsl
 {
    static constexpr int N = tpe_lattice_points(3);
@@ -1071,9 +1146,24 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 #pragma unroll
       for (int k = 0; k < (NLP + 63) / 64; k++)
       {
-         const int j = lane + 64 * k;
-         if (j < NLP)
+         const int p = lane + 64 * k;
+         if (p < NLP)
          {
+            // lattice-map blocks: the slots dealt for the writes' banks (the lanes of a step still read the
+            // same map and snapshot lines); regular blocks: slot order (j = p), whose x / T' gathers of a
+            // step stay on few lines -- dealt, they cost the structured Mult 3% (profiles/r6/ab_gather.txt)
+            int j, ls;
+            if (RM == 3)
+            {
+               const unsigned g = kLatTsGather3.v[p];
+               j = (int)(g & 0xffff);
+               ls = (int)(g >> 16);
+            }
+            else
+            {
+               j = p;
+               ls = kLatTsl3.v[p];
+            }
             int d;
             if (RM == 3) { d = bdof(lm[j]); }
             else
@@ -1082,7 +1172,7 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                d = rg.base + (int)(v & 31) * rg.sx + (int)((v >> 5) & 31) * rg.sy + (int)(v >> 10) * rg.sz;
             }
             // (lattice-map blocks: the snapshot is stored in their slot order, a contiguous read)
-            sPL[kLatTsl3.v[j]] = v2d{(!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned], RM == 3 ? tsn[(size_t)blk * NLP + j] : tsn[d]};
+            sPL[ls] = v2d{(!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned], RM == 3 ? tsn[(size_t)blk * NLP + j] : tsn[d]};
          }
       }
    }

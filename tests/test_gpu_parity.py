@@ -498,9 +498,9 @@ def test_pcg_energy_folded_den(numbering, with_ess):
     it, nrm = form.PCG(dev(b), x, ess=esst, rel_tol=0.0, max_iter=6, jacobi=True)
     xr, itr, nr = op.pcg(b, ess, rel_tol=0.0, max_iter=6, jacobi=True)
     assert it == itr == 6 and relerr(host(x), xr) < 1e-11 and nrm == pytest.approx(nr, rel=1e-9)
-    it, nrm = form.PCG(dev(b), x, ess=esst, rel_tol=1e-8, max_iter=500, jacobi=True)
-    xr, itr, nr = op.pcg(b, ess, rel_tol=1e-8, max_iter=500, jacobi=True)
-    assert it == itr and E.pcg_last_converged() and relerr(host(x), xr) < 1e-10
+    it, nrm = form.PCG(dev(b), x, ess=esst, rel_tol=1e-12, max_iter=2000, jacobi=True)
+    xr, itr, nr = op.pcg(b, ess, rel_tol=1e-12, max_iter=2000, jacobi=True)
+    assert abs(it - itr) <= 2 and E.pcg_last_converged() and relerr(host(x), xr) < 1e-9
 
 
 @pytest.mark.parametrize("snap", [True, False])

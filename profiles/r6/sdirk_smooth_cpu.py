@@ -9,7 +9,9 @@ permuted: the operator is the same, only the rounding of each Mult changes (the 
 dof's element contributions in the new order).  The printed relerr(u1 - u0, u2 - u0) is the gap that
 rounding alone produces; it is compared for the smooth state u0 = 37 + 20 exp(-4 |x - 1/2|^2) and a
 uniform-random state, and for 8 fixed iterations and converged stage solves.
-Usage: python3 profiles/r6/sdirk_smooth_cpu.py [iters ...]   (run here, 8 CPU threads)"""
+Usage: python3 profiles/r6/sdirk_smooth_cpu.py [--converged]   (run here, 8 CPU threads; --converged adds the
+smooth state with converged stage solves, ~45 min per element order, and writes tests/golden/sdirk_c5_smooth.npz,
+the fixture of tests/test_gpu_configs.py::test_c5_sdirk_smooth_converged)"""
 import os
 import sys
 import time
@@ -31,6 +33,7 @@ E.load_library()
 
 def main():
     n, order, dt = 68, 4, 0.02
+    converged = "--converged" in sys.argv
     m = E.Mesh.MakeCartesian3D(n, n, n)
     fes = E.H1Space(m, order, E.NUMBERING_STRUCTURED)
     en, gm = m.element_nodes(), fes.gather_map()
@@ -44,36 +47,46 @@ def main():
               "random": np.random.default_rng(68).uniform(-1.0, 1.0, fes.ndofs)}
     perm = np.random.default_rng(7).permutation(fes.ne)
     orders = {"natural": np.arange(fes.ne), "permuted": perm}
-    runs = [(8, 0.0)] + [(int(a), 1e-12) for a in sys.argv[1:]]
+    # fixed 8 iterations per stage for both states; converged stage solves (rel_tol 1e-12) for the smooth one
+    runs = [(8, 0.0, s_) for s_ in states] + ([(100000, 1e-12, "smooth")] if converged else [])
     print(f"# configs[4]: Cartesian {n}^3, p = {order}, {fes.ndofs} DoF, SDIRK33 dt = {dt}, "
           f"{ess.size} Dirichlet dofs, oracle threads = {O.num_threads()}", flush=True)
     res = {}
     for oname, o in orders.items():
         Tr = O.OracleOperator(en[o], gm[o], fes.ndofs, order, alpha=alpha[o], beta=c * dt * beta[o])
         Kr = O.OracleOperator(en[o], gm[o], fes.ndofs, order, beta=beta[o])
-        for max_iter, tol in runs:
+        for max_iter, tol, sname in runs:
             its = []
 
             def solve(us):
                 rhs = -Kr.mult(us)
                 rhs[ess] = 0.0
-                xs, it, _ = Tr.pcg(rhs, ess, rel_tol=tol, max_iter=max_iter if tol == 0 else 100000)
+                xs, it, _ = Tr.pcg(rhs, ess, rel_tol=tol, max_iter=max_iter)
                 its.append(it)
                 return xs
 
-            for sname, u0 in states.items():
-                t0 = time.time()
-                res[(oname, max_iter, tol, sname)] = ODE.step(23, solve, u0, dt)
-                print(f"{oname:8s} {sname:6s} stage solves {'fixed ' + str(max_iter) if tol == 0 else 'rel_tol 1e-12'}: "
-                      f"iterations {its[-3:]}  {time.time() - t0:.1f} s", flush=True)
+            t0 = time.time()
+            u1 = ODE.step(23, solve, states[sname], dt)
+            res[(oname, tol, sname)] = u1
+            print(f"{oname:8s} {sname:6s} stage solves {'fixed ' + str(max_iter) if tol == 0 else 'rel_tol 1e-12'}: "
+                  f"iterations {its}  {time.time() - t0:.1f} s", flush=True)
+            if tol > 0 and oname == "natural":
+                # the golden values for tests/test_gpu_configs.py::test_c5_sdirk_smooth_converged
+                idx = np.sort(np.random.default_rng(2026).choice(fes.ndofs, 20000, replace=False)).astype(np.int64)
+                u0 = states[sname]
+                np.savez_compressed(os.path.join(ROOT, "tests", "golden", "sdirk_c5_smooth.npz"), idx=idx, u1=u1[idx],
+                                    u0=u0[idx], du_norm2=np.linalg.norm(u1 - u0), du_max=np.abs(u1 - u0).max(),
+                                    iterations=np.array(its), ndofs=np.array(fes.ndofs))
+                print("wrote tests/golden/sdirk_c5_smooth.npz", flush=True)
         del Tr, Kr
-    print("# relerr(u_natural - u0, u_permuted - u0): the gap rounding alone produces", flush=True)
-    for max_iter, tol in runs:
-        for sname, u0 in states.items():
-            a = res[("natural", max_iter, tol, sname)] - u0
-            b = res[("permuted", max_iter, tol, sname)] - u0
-            lab = f"fixed {max_iter} iterations" if tol == 0 else "converged (rel_tol 1e-12)"
-            print(f"{sname:6s} state, {lab:28s}: relerr = {relerr(b, a):.3e}   |u1 - u0|_inf = {np.abs(a).max():.3e}")
+    print("# relerr(u_natural - u0, u_permuted - u0): the gap the rounding of each Mult alone produces", flush=True)
+    for max_iter, tol, sname in runs:
+        u0 = states[sname]
+        a = res[("natural", tol, sname)] - u0
+        b = res[("permuted", tol, sname)] - u0
+        lab = f"fixed {max_iter} iterations" if tol == 0 else "converged (rel_tol 1e-12)"
+        print(f"{sname:6s} state, {lab:28s}: relerr = {relerr(b, a):.3e}   |u1 - u0|_inf = {np.abs(a).max():.3e}",
+              flush=True)
 
 
 if __name__ == "__main__":

@@ -348,10 +348,19 @@ k_dot_final(int nparts, const double *__restrict__ partials, double *__restrict_
             const PcgCtl *ctl, PcgCheck chk, int with_check)
 {
    if (ctl && ctl->done) { return; }
-   constexpr int NW = kFinalThreads / 64;
+   constexpr int NW = kFinalThreads / 64, U = 8;
    __shared__ double red[NW];
-   double s = 0.0;
-   for (int i = threadIdx.x; i < nparts; i += kFinalThreads) { s += partials[i]; }
+   // eight loads in flight per thread (a fixed order: eight running sums, then their pairwise sum), for
+   // long partial lists: one partial per brick (78,608 at C5) took 77 dependent loads per thread
+   double a[U] = {};
+   int i = threadIdx.x;
+   for (; i + (U - 1) * kFinalThreads < nparts; i += U * kFinalThreads)
+   {
+#pragma unroll
+      for (int u = 0; u < U; u++) { a[u] += partials[i + u * kFinalThreads]; }
+   }
+   for (; i < nparts; i += kFinalThreads) { a[0] += partials[i]; }
+   double s = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
    for (int off = 32; off > 0; off >>= 1) { s += __shfl_down(s, off, 64); }
    if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6] = s; }
    __syncthreads();

@@ -1420,8 +1420,9 @@ void PAForm::mult(const double *x, double *y, hipStream_t s)
 int PAForm::energy_parts() const
 {
    // the coefficient-snapshot kernel (p = 2), one partial per 4-block workgroup.  (The p >= 3 brick kernel
-   // folding the same sums slowed its plain Mult by 3% and the PCG iteration by 2.4%: rejected,
-   // profiles/r6/ab_brick_energy.txt.)
+   // folding the same sums was measured twice and rejected: every instantiation carrying the running sum
+   // slowed the plain Mult by 3%; a separate instantiation cost the PCG's Mult what the dot pass it removed
+   // cost -- profiles/r6/ab_brick_energy.txt.)
    const bool ts = assembled_ && use_partials() && resolved_mode_ == KERNEL_TPE && layout_.kind == QLAYOUT_AFFINE &&
                    layout_.tsnap && have_diff_ && D_ == 3 && Q_ == 4;
    return ts && ndofs_ > 0 ? (layout_.nblk() + 3) / 4 : 0;

@@ -282,6 +282,9 @@ def test_c5_full_size_drop_in():
     assert relerr(yh, op.mult(x)) <= RTOL
 
 
+SMOOTH_TOL = 1e-8  # converged stages (rel_tol 1e-12); see profiles/r6/sdirk_smooth_cpu.txt
+
+
 def _serial_form(fes, P, alpha, beta):
     f = E.BilinearForm(fes)
     if alpha is not None:
@@ -376,6 +379,41 @@ def test_c5_sdirk_step_full_size():
     ur = ODE.step(23, solve, u0, dt)
     assert np.array_equal(uh[ess], u0[ess])
     assert relerr(uh - u0, ur - u0) < 1e-9
+
+
+def test_c5_sdirk_smooth_converged():
+    """configs[4]'s step from the SMOOTH state with converged stage solves: one SDIRK33
+    step at 68^3 p = 4 (20.3M DoF) from u0 = 37 + 20 exp(-4 |x - 1/2|^2), each stage a constrained
+    Jacobi-PCG to rel_tol 1e-12, against the oracle's step on the same mesh (tests/golden/sdirk_c5_smooth.npz,
+    written by profiles/r6/sdirk_smooth_cpu.py --converged: u1 at 20,000 seeded dofs; the oracle needs ~50 min
+    on 8 threads).  With 8 fixed iterations the smooth state amplifies rounding (profiles/r6/sdirk_smooth_cpu.txt:
+    the oracle against itself with permuted elements differs by as much as the device did, 2.9e-7); converged
+    solves remove that."""
+    g = np.load(f"{GOLDEN}/sdirk_c5_smooth.npz")
+    n, order, dt = 68, 4, 0.02
+    m = E.Mesh.MakeCartesian3D(n, n, n)
+    fes = E.H1Space(m, order, E.NUMBERING_STRUCTURED)
+    assert fes.ndofs == int(g["ndofs"])
+    en = m.element_nodes()
+    P = O.quad_points(en, O.default_q1d(order))
+    alpha, beta = alpha_bioheat(P) / 3.6e6, k_of_T(temperature(P))
+    del P
+    c = E.ode_implicit_coeff(23)
+    T = _serial_form(fes, None, alpha, c * dt * beta)
+    K = _serial_form(fes, None, None, beta)
+    del alpha, beta
+    ess = fes.boundary_dofs()
+    X = fes.dof_coords()
+    u0 = 37.0 + 20.0 * np.exp(-4.0 * np.sum((X - 0.5) ** 2, axis=1))
+    idx = g["idx"]
+    assert np.array_equal(u0[idx], g["u0"])
+    u = dev(u0)
+    ns, it, conv = E.ode_step(23, E.Operator(T), E.Operator(K), dt, u, ess=dev(ess, torch.int32), rel_tol=1e-12,
+                              max_iter=100000)
+    assert ns == 3 and conv
+    uh = host(u)
+    assert np.array_equal(uh[ess], u0[ess])
+    assert relerr(uh[idx] - u0[idx], g["u1"] - g["u0"]) < SMOOTH_TOL
 
 
 # ---------------------------------------------------------------------------------------

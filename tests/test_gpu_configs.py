@@ -282,7 +282,7 @@ def test_c5_full_size_drop_in():
     assert relerr(yh, op.mult(x)) <= RTOL
 
 
-SMOOTH_TOL = 1e-8  # converged stages (rel_tol 1e-12); see profiles/r6/sdirk_smooth_cpu.txt
+SMOOTH_TOL = 1e-12  # converged stages (rel_tol 1e-12): measured 5.8e-15 (profiles/r6/gpu17_tests.txt)
 
 
 def _serial_form(fes, P, alpha, beta):
@@ -413,7 +413,9 @@ def test_c5_sdirk_smooth_converged():
     assert ns == 3 and conv
     uh = host(u)
     assert np.array_equal(uh[ess], u0[ess])
-    assert relerr(uh[idx] - u0[idx], g["u1"] - g["u0"]) < SMOOTH_TOL
+    err = relerr(uh[idx] - u0[idx], g["u1"] - g["u0"])
+    print(f"c5 smooth converged SDIRK33: device stage iterations {it} (oracle {g['iterations'].tolist()}), relerr {err:.3e}")
+    assert err < SMOOTH_TOL
 
 
 # ---------------------------------------------------------------------------------------

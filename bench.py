@@ -816,7 +816,10 @@ def main():
             line["pcg_iteration"] = {"iterations": args.pcg_iters, "iteration_ms": round(pcg_it, 5),
                                      "mdof_iter_per_s": round(fes.ndofs / (pcg_it * 1e-3) / 1e6, 1),
                                      "note": "marginal time per Jacobi-PCG iteration on the serial form (ecm2_pcg_solve: the "
-                                             "device-driven loop), no ess: Mult + vector passes + two dots"}
+                                             "device-driven loop), no ess: Mult + two fused vector passes "
+                                             "(step_r with (B r, r), update_xd) + (A d, d), folded into "
+                                             "the Mult's element energies on the snapshot kernel, a dot "
+                                             "pass otherwise"}
         if reasm is not None:
             line["reassembly_ms"] = reasm  # Assemble after a k(T) change, plan kept (outside the timed region)
         line.update(subs)

@@ -17,6 +17,13 @@ namespace
 {
 using namespace dev;
 
+// ECM2_SF_W3 (an A/B build): k_apply_tpe_sf (AFFINE / map-addressed blocks, what a
+// z-slab rank runs) compiled for three waves per SIMD -- 168 VGPRs, 53,248 B of LDS per workgroup.
+#ifndef ECM2_SF_W3
+#define ECM2_SF_W3 0
+#endif
+constexpr bool kSfW3 = ECM2_SF_W3;
+
 // Rows per wave of the LDS region the cross-wave face exchange uses (3 faces of D x D).
 template <int D>
 struct XwaveRows
@@ -52,7 +59,7 @@ struct TpeReg
 // MAYREG: regf may be nonzero (per block).
 // XR: rows per wave of xb (a kernel whose waves stage more than XwaveRows rows passes its stride, so
 // a wave's sends land in its own region while the other waves may still read theirs).
-template <int D, bool SPLIT, bool SIGNS, bool XW, bool MAYREG = false, int XR = XwaveRows<D>::R>
+template <int D, bool SPLIT, bool SIGNS, bool XW, bool MAYREG = false, int XR = XwaveRows<D>::R, bool XREUSE = false>
 __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], const int *__restrict__ mp, int fl,
                                                    int blk, int lane, bool active, int n_owned,
                                                    double *__restrict__ y, double *__restrict__ yg,
@@ -61,7 +68,10 @@ __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], cons
                                                    const int *__restrict__ lm = nullptr)
 {
    constexpr int ND = D * D * D;
-   static_assert(XR >= XwaveRows<D>::R, "staging rows");
+   // XREUSE: the z faces reuse the x faces' rows (the y merge's barrier orders every wave's x-face
+   // reads before any z-face write), so 2 D^2 rows per wave suffice
+   static_assert(XR >= (XREUSE ? 2 * D * D : XwaveRows<D>::R), "staging rows");
+   auto xrow = [](int dir) { return (XREUSE ? (dir & 1) : dir) * D * D; };
    const bool rr = MAYREG && regf == 1, rs = MAYREG && regf != 0, rl = MAYREG && regf == 2;
    // A lattice-map block's store entries are loaded here, before the face merges: their latency
    // (the map left L2 while the block computed) overlaps the shuffles and barriers instead of
@@ -97,7 +107,7 @@ __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], cons
 #pragma unroll
          for (int j = 0; j < D; j++)
 #pragma unroll
-            for (int i = 0; i < D; i++) { xb[((w * XR) + dir * D * D + j * D + i) * 64 + lane] = Yo[face(0, i, j)]; }
+            for (int i = 0; i < D; i++) { xb[((w * XR) + xrow(dir) + j * D + i) * 64 + lane] = Yo[face(0, i, j)]; }
       }
       if (wave_on)
       {
@@ -122,7 +132,7 @@ __device__ __forceinline__ void tpe_assemble_store(double (&Yo)[D * D * D], cons
 #pragma unroll
                for (int i = 0; i < D; i++)
                {
-                  Yo[face(D - 1, i, j)] += xb[((pw * XR) + dir * D * D + j * D + i) * 64 + lane - 3 * delta];
+                  Yo[face(D - 1, i, j)] += xb[((pw * XR) + xrow(dir) + j * D + i) * 64 + lane - 3 * delta];
                }
          }
       }
@@ -345,7 +355,7 @@ k_apply_tpe_pf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 // 349-362) and the mass setup's W alpha det J, never stored.
 // PW: point values per quadrature point (2: the pair; 1: a diffusion-only form's W beta [/ det J]).
 template <int D, int Q, bool SPLIT, int RM, bool TL = false, int PW = 2>
-__global__ void __launch_bounds__(256, 1)
+__global__ void __launch_bounds__(256, (kSfW3 && !TL) ? 3 : 1)
 k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
                const double *__restrict__ qdd, const double *__restrict__ qdm,
                const double *__restrict__ x, const double *__restrict__ xg,
@@ -353,10 +363,20 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                const int *__restrict__ lane_flags, double *__restrict__ part, const int *__restrict__ treg,
                int pstride, const int *__restrict__ lmap, const QPts qp)
 {
-   constexpr int ND = D * D * D, NQ = Q * Q * Q, NR = Q * Q, XR = XwaveRows<D>::R, WPG = 4;
+   constexpr int ND = D * D * D, NQ = Q * Q * Q, NR = Q * Q, WPG = 4;
+   // W3 (kSfW3, the three-waves-per-SIMD build): the last x value stays in a register and the face
+   // exchange reuses its rows, so three workgroups fit a CU's LDS (26 rows: 159,744 B)
+   constexpr bool W3 = kSfW3 && !TL;
+   constexpr int XR = W3 ? (ND - 1 > 2 * D * D ? ND - 1 : 2 * D * D) : XwaveRows<D>::R;
+   constexpr int XL = W3 ? ND - 1 : ND;  // x values staged in LDS
    __shared__ double sX[WPG][XR][64];  // gathered x; then the cross-wave face exchange
    const int lane = threadIdx.x & 63;
    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: block data in SGPRs
+   double xl = 0.0;                                                  // W3: x value ND - 1
+   auto put_x = [&](int a, double v) {
+      if (a < XL) { sX[w][a][lane] = v; }
+      else { xl = v; }
+   };
    // (round-robin dispatch: the XCD-contiguous order of the lattice kernels is 2.6% slower here,
    // profiles/r5/ab_xcd.txt)
    const int blk = blk_begin + (int)blockIdx.x * WPG + w;
@@ -401,7 +421,7 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
       // are in flight instead of 4 (profiles/r2_ab_pf2.txt: C4 kernel -4.3%); the plane loop is
       // unrolled so the rotation is static.  Map-addressed kernels (RM = 0) keep the ping-pong:
       // unrolled, their register demand exceeds 256 VGPRs; at p = 1 the third buffer costs a wave/SIMD.
-      constexpr bool PF2 = RM != 0 && D == 3 && !TL;  // TL: the runtime plane loop keeps the geometry live once
+      constexpr bool PF2 = RM != 0 && D == 3 && !TL && !W3;  // TL: the runtime plane loop keeps the geometry live once
       v2d ra[PF2 ? 3 : 1][Q];
       if constexpr (PF2)
       {
@@ -426,7 +446,7 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 #pragma unroll
                for (int dx = 0; dx < D; dx++)
                {
-                  sX[w][(dz * D + dy) * D + dx][lane] = x[d0 + dx * rg.sx + dy * rg.sy + dz * rg.sz];
+                  put_x((dz * D + dy) * D + dx, x[d0 + dx * rg.sx + dy * rg.sy + dz * rg.sz]);
                }
       }
       else if (RM >= 2 && regf == 2)
@@ -440,7 +460,7 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
             const int X = (D - 1) * (lane & 3) + a % D, Y = (D - 1) * ((lane >> 2) & 3) + (a / D) % D,
                       Z = (D - 1) * (lane >> 4) + a / (D * D);
             const int d = bdof(lm[tpe_lattice_slot(D, X, Y, Z)]);
-            sX[w][a][lane] = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
+            put_x(a, (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned]);
          }
       }
       else
@@ -451,7 +471,7 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
             const int g = mp[a * 64];
             const int d = bdof(g);
             const double v = (!SPLIT || d < n_owned) ? x[d] : xg[d - n_owned];
-            sX[w][a][lane] = bneg(g) ? -v : v;
+            put_x(a, bneg(g) ? -v : v);
          }
       }
       auto plane = [&](const int qz) {
@@ -483,7 +503,8 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 #pragma unroll
                for (int dz = 0; dz < D; dz++)
                {
-                  const double c = sX[w][(dz * D + dy) * D + dx][ll];
+                  const int a = (dz * D + dy) * D + dx;
+                  const double c = a < XL ? sX[w][a][ll] : xl;
                   zb += bz[dz] * c;
                   zg += gz[dz] * c;
                }
@@ -655,7 +676,7 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
          for (int qz = 0; qz < Q; qz++) { plane(qz); }
       }
    }  // wave_on
-   tpe_assemble_store<D, SPLIT, RM == 0 || RM == 2, true, RM != 0>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0,
+   tpe_assemble_store<D, SPLIT, RM == 0 || RM == 2, true, RM != 0, XR, W3>(Yo, mp, wave_on ? lane_flags[(size_t)blk * 64 + lane] : 0,
                                                          blk, lane, active, n_owned, y, yg, part, &sX[0][0][0], w,
                                                          wave_on, rg, regf, pstride,
                                                          lmap ? lmap + (size_t)blk * tpe_lattice_points(D) : nullptr);

@@ -428,7 +428,7 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
          load_row(0, ra[0]);
          load_row(1, ra[1]);
       }
-      else { load_row(0, ca); }
+      else if constexpr (!W3) { load_row(0, ca); }
       if (RM == 3) { regf = 2; }  // every block lattice-map: no treg row in the gather's chain
       else if (RM)
       {
@@ -608,9 +608,20 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
 #pragma unroll
                for (int dx = 0; dx < D; dx++)
                {
-                  SB[dy][dx] += by * T0[dx];
-                  SB[dy][dx] += gy * T1[dx];
-                  SG[dy][dx] += by * T2[dx];
+                  if constexpr (W3)
+                  {
+                     // no plane sums (36 VGPRs): the row's y-transpose goes straight through the
+                     // z-transpose into the outputs (54 more FMAs per row)
+                     const double pb = by * T0[dx] + gy * T1[dx], pg = by * T2[dx];
+#pragma unroll
+                     for (int dz = 0; dz < D; dz++) { Yo[(dz * D + dy) * D + dx] += bz[dz] * pb + gz[dz] * pg; }
+                  }
+                  else
+                  {
+                     SB[dy][dx] += by * T0[dx];
+                     SB[dy][dx] += gy * T1[dx];
+                     SG[dy][dx] += by * T2[dx];
+                  }
                }
             }
          };
@@ -624,6 +635,16 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                __builtin_amdgcn_sched_barrier(0);  // rows stay in program order (no interleaving)
                load_row(row + 2 < NR ? row + 2 : NR - 1, ra[(row + 2) % 3]);
                row_body(qy, ra[row % 3]);
+            }
+         }
+         else if constexpr (W3)
+         {
+            // one row buffer, no prefetch: the third wave per SIMD hides the row's latency
+#pragma unroll
+            for (int qy = 0; qy < Q; qy++)
+            {
+               load_row(qz * Q + qy, ca);
+               row_body(qy, ca);
             }
          }
          else if constexpr (Q % 2 == 0)
@@ -655,7 +676,7 @@ k_apply_tpe_sf(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
             }
          }
 #pragma unroll
-         for (int dz = 0; dz < D; dz++)
+         for (int dz = 0; dz < D && !W3; dz++)
 #pragma unroll
             for (int dy = 0; dy < D; dy++)
 #pragma unroll

@@ -3,15 +3,22 @@
 device step and oracle/ode.py, gpurun_out/r5/tests1.txt) intrinsic to the computation?
 
 The oracle (CPU, test infrastructure) is run against ITSELF on Cartesian 68^3 at p = 4 (20.3M DoF), with
-the same state, the same T = M_alpha + c dt K_beta, K = K_beta, the same Dirichlet dofs and the same fixed
-PCG iteration count per stage, once in the mesh's element order and once with the elements randomly
-permuted: the operator is the same, only the rounding of each Mult changes (the CSR transpose sums a
-dof's element contributions in the new order).  The printed relerr(u1 - u0, u2 - u0) is the gap that
-rounding alone produces; it is compared for the smooth state u0 = 37 + 20 exp(-4 |x - 1/2|^2) and a
-uniform-random state, and for 8 fixed iterations and converged stage solves.
-Usage: python3 profiles/r6/sdirk_smooth_cpu.py [--converged]   (run here, 8 CPU threads; --converged adds the
-smooth state with converged stage solves, ~45 min per element order, and writes tests/golden/sdirk_c5_smooth.npz,
-the fixture of tests/test_gpu_configs.py::test_c5_sdirk_smooth_converged)"""
+the same T = M_alpha + c dt K_beta, K = K_beta, the same Dirichlet dofs and the same fixed PCG iteration
+count per stage, changing one thing the exact result does not depend on:
+  default     the elements randomly permuted (the CSR transpose sums a dof's element contributions in
+              another order) -- smooth and uniform-random states, fixed 8 and (--converged) converged solves;
+  --perturb   the point coefficients moved by <= 1 ulp;
+  --shift     the smooth state u0 = 37 + 20 exp(-4 |x - 1/2|^2) against u0 - 37 (K 1 = 0).
+Results (profiles/r6/sdirk_smooth_cpu.txt, _ulp.txt, _shift.txt): permuted 1.3e-11 and ulp 2.2e-10 leave the
+cancellation inside each element's product alike and barely move the step; the shift changes it and moves the
+oracle's own fixed-8 step by 3.8e-7 -- the size of the device's gap.  With converged solves the permuted oracle
+moves by 7.7e-15, the device by 5.8e-15 (tests/test_gpu_configs.py::test_c5_sdirk_smooth_converged).
+Usage: python3 profiles/r6/sdirk_smooth_cpu.py [--converged | --fixed8-fixture | --perturb | --shift]   (run here, 8 CPU threads;
+--perturb compares the natural order with the same order and the point coefficients moved by <= 1 ulp;
+--converged adds the smooth state with converged stage solves, ~45 min per element order, and writes
+tests/golden/sdirk_c5_smooth.npz, the fixture of tests/test_gpu_configs.py::test_c5_sdirk_smooth_converged;
+--fixed8-fixture runs only the natural order's smooth step with 8 fixed iterations per stage and writes
+tests/golden/sdirk_c5_smooth_fixed8.npz, the fixture of test_c5_sdirk_smooth_fixed8)"""
 import os
 import sys
 import time
@@ -49,12 +56,28 @@ def main():
     orders = {"natural": np.arange(fes.ne), "permuted": perm}
     # fixed 8 iterations per stage for both states; converged stage solves (rel_tol 1e-12) for the smooth one
     runs = [(8, 0.0, s_) for s_ in states] + ([(100000, 1e-12, "smooth")] if converged else [])
+    fixture8 = "--fixed8-fixture" in sys.argv
+    if fixture8:  # only the natural order's smooth fixed-8 step, as the fixture of test_c5_sdirk_smooth_fixed8
+        runs, orders = [(8, 0.0, "smooth")], {"natural": orders["natural"]}
+    coef = {k: (alpha, beta) for k in orders}
+    if "--perturb" in sys.argv:
+        # the same element order, the point coefficients moved by at most one unit in the last place (a
+        # random -1 / 0 / +1 ulp per point): the size of the rounding a different setup arithmetic leaves
+        # in W alpha det J and W beta adj(J) adj(J)^T / det J
+        rng = np.random.default_rng(11)
+        ulp = lambda a: a + np.spacing(np.abs(a)) * rng.integers(-1, 2, a.shape)  # noqa: E731
+        orders = {"natural": orders["natural"], "ulp": orders["natural"]}
+        coef = {"natural": (alpha, beta), "ulp": (ulp(alpha), ulp(beta))}
+    if "--shift" in sys.argv:
+        shift_experiment(fes, order, en, gm, alpha, beta, c, dt, ess, states["smooth"])
+        return
     print(f"# configs[4]: Cartesian {n}^3, p = {order}, {fes.ndofs} DoF, SDIRK33 dt = {dt}, "
           f"{ess.size} Dirichlet dofs, oracle threads = {O.num_threads()}", flush=True)
     res = {}
     for oname, o in orders.items():
-        Tr = O.OracleOperator(en[o], gm[o], fes.ndofs, order, alpha=alpha[o], beta=c * dt * beta[o])
-        Kr = O.OracleOperator(en[o], gm[o], fes.ndofs, order, beta=beta[o])
+        al, be = coef[oname]
+        Tr = O.OracleOperator(en[o], gm[o], fes.ndofs, order, alpha=al[o], beta=c * dt * be[o])
+        Kr = O.OracleOperator(en[o], gm[o], fes.ndofs, order, beta=be[o])
         for max_iter, tol, sname in runs:
             its = []
 
@@ -70,6 +93,14 @@ def main():
             res[(oname, tol, sname)] = u1
             print(f"{oname:8s} {sname:6s} stage solves {'fixed ' + str(max_iter) if tol == 0 else 'rel_tol 1e-12'}: "
                   f"iterations {its}  {time.time() - t0:.1f} s", flush=True)
+            if fixture8:
+                idx = np.sort(np.random.default_rng(2026).choice(fes.ndofs, 20000, replace=False)).astype(np.int64)
+                u0 = states[sname]
+                np.savez_compressed(os.path.join(ROOT, "tests", "golden", "sdirk_c5_smooth_fixed8.npz"), idx=idx,
+                                    u1=u1[idx], u0=u0[idx], du_norm2=np.linalg.norm(u1 - u0),
+                                    du_max=np.abs(u1 - u0).max(), iterations=np.array(its), ndofs=np.array(fes.ndofs))
+                print("wrote tests/golden/sdirk_c5_smooth_fixed8.npz", flush=True)
+                return
             if tol > 0 and oname == "natural":
                 # the golden values for tests/test_gpu_configs.py::test_c5_sdirk_smooth_converged
                 idx = np.sort(np.random.default_rng(2026).choice(fes.ndofs, 20000, replace=False)).astype(np.int64)
@@ -79,14 +110,44 @@ def main():
                                     iterations=np.array(its), ndofs=np.array(fes.ndofs))
                 print("wrote tests/golden/sdirk_c5_smooth.npz", flush=True)
         del Tr, Kr
-    print("# relerr(u_natural - u0, u_permuted - u0): the gap the rounding of each Mult alone produces", flush=True)
+    other = [k for k in orders if k != "natural"][0]
+    print(f"# relerr(u_natural - u0, u_{other} - u0): the gap "
+          + ("the rounding of each Mult alone produces" if other == "permuted" else
+             "one-ulp changes of the point coefficients produce"), flush=True)
     for max_iter, tol, sname in runs:
         u0 = states[sname]
         a = res[("natural", tol, sname)] - u0
-        b = res[("permuted", tol, sname)] - u0
+        b = res[(other, tol, sname)] - u0
         lab = f"fixed {max_iter} iterations" if tol == 0 else "converged (rel_tol 1e-12)"
         print(f"{sname:6s} state, {lab:28s}: relerr = {relerr(b, a):.3e}   |u1 - u0|_inf = {np.abs(a).max():.3e}",
               flush=True)
+
+
+def shift_experiment(fes, order, en, gm, alpha, beta, c, dt, ess, u0):
+    """The smooth state u0 and u0 - 37 (K 1 = 0: the same step in exact arithmetic), 8 fixed iterations per stage,
+    natural element order: relerr between the two steps' u1 - u0 (the oracle moved by an exact-arithmetic identity)."""
+    Tr = O.OracleOperator(en, gm, fes.ndofs, order, alpha=alpha, beta=c * dt * beta)
+    Kr = O.OracleOperator(en, gm, fes.ndofs, order, beta=beta)
+    print(f"# configs[4], {fes.ndofs} DoF: the smooth state and the same state minus its constant 37, 8 fixed "
+          f"iterations per stage, oracle threads = {O.num_threads()}", flush=True)
+    du = {}
+    for name, us0 in (("smooth", u0), ("shifted", u0 - 37.0)):
+        its = []
+
+        def solve(us):
+            rhs = -Kr.mult(us)
+            rhs[ess] = 0.0
+            xs, it, _ = Tr.pcg(rhs, ess, rel_tol=0.0, max_iter=8)
+            its.append(it)
+            return xs
+
+        t0 = time.time()
+        u1 = ODE.step(23, solve, us0, dt)
+        du[name] = u1 - us0
+        print(f"{name:8s}: iterations {its}  |K u0|_2 = {np.linalg.norm(Kr.mult(us0)):.6e}  {time.time() - t0:.1f} s",
+              flush=True)
+    print(f"relerr(du_smooth, du_shifted) = {relerr(du['shifted'], du['smooth']):.3e}  (the rounding of 37 K 1 alone)",
+          flush=True)
 
 
 if __name__ == "__main__":

@@ -465,7 +465,7 @@ struct BrickShapeC
 {
    static constexpr int NE = 4 * BZ, DD = D * D, QQ = Q * Q, DQ = D * Q, ND = D * D * D;
    static constexpr int LX = 2 * (D - 1) + 1, LY = LX, LZ = BZ * (D - 1) + 1, NB = LX * LY * LZ;
-   static constexpr int SURF = 2 * LX * LY + 2 * (LZ - 2) * LX + 2 * (LZ - 2) * (LY - 2);
+   static constexpr int SURF = brick_surface_points(D, BZ);
    static constexpr int L2S = (DQ > DD ? DQ : DD) <= 32 ? 32 : 64;  // lanes per element, line stages
    static constexpr int S3 = ((QQ + 15) / 16) * 16;                 // lanes per element, z stage
    static constexpr int DS = (QQ <= Q + 32 * ((QQ - Q + 31) / 32)) ? Q + 32 * ((QQ - Q + 31) / 32) : QQ;

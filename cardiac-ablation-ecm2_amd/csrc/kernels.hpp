@@ -270,14 +270,34 @@ __host__ __device__ constexpr int lattice_surface_index(int LX, int LY, int LZ, 
    if (X == LX - 1) { return b2 + (LZ - 2) * (LY - 2) + (Z - 1) * (LY - 2) + (Y - 1); }
    return -1;
 }
+// Brick partial slots: the same face groups, each group starting on a multiple of kBrickSlotAlign
+// doubles (ECM2_BRICK_SLOT_ALIGN, an A/B build: 16 = every group on its own 128-B lines).
+#ifndef ECM2_BRICK_SLOT_ALIGN
+#define ECM2_BRICK_SLOT_ALIGN 1
+#endif
+constexpr int kBrickSlotAlign = ECM2_BRICK_SLOT_ALIGN;
+__host__ __device__ constexpr int slot_align_up(int n) { return (n + kBrickSlotAlign - 1) / kBrickSlotAlign * kBrickSlotAlign; }
 __host__ __device__ constexpr int brick_surface_points(int D, int bz)
 {
-   return lattice_surface_points(2 * D - 1, 2 * D - 1, bz * (D - 1) + 1);
+   const int LX = 2 * D - 1, LY = LX, LZ = bz * (D - 1) + 1;
+   return 2 * slot_align_up(LX * LY) + 2 * slot_align_up((LZ - 2) * LX) + 2 * slot_align_up((LZ - 2) * (LY - 2));
 }
 __host__ __device__ constexpr int brick_surface_index(int D, int bz, int X, int Y, int Z)
 {
-   return lattice_surface_index(2 * D - 1, 2 * D - 1, bz * (D - 1) + 1, X, Y, Z);
+   const int LX = 2 * D - 1, LY = LX, LZ = bz * (D - 1) + 1;
+   const int gz = slot_align_up(LX * LY), gy = slot_align_up((LZ - 2) * LX), gx = slot_align_up((LZ - 2) * (LY - 2));
+   if (Z == 0) { return Y * LX + X; }
+   if (Z == LZ - 1) { return gz + Y * LX + X; }
+   if (Y == 0) { return 2 * gz + (Z - 1) * LX + X; }
+   if (Y == LY - 1) { return 2 * gz + gy + (Z - 1) * LX + X; }
+   if (X == 0) { return 2 * gz + 2 * gy + (Z - 1) * (LY - 2) + (Y - 1); }
+   if (X == LX - 1) { return 2 * gz + 2 * gy + gx + (Z - 1) * (LY - 2) + (Y - 1); }
+   return -1;
 }
+static_assert(kBrickSlotAlign != 1 || (brick_surface_points(5, 1) == lattice_surface_points(9, 9, 5) &&
+                                       brick_surface_index(5, 1, 3, 4, 2) == lattice_surface_index(9, 9, 5, 3, 4, 2) &&
+                                       brick_surface_index(5, 1, 8, 4, 2) == lattice_surface_index(9, 9, 5, 8, 4, 2)),
+              "unaligned brick slots are the lattice's face-grouped order");
 // the same for a p <= 2 block (4 x 4 x 4 elements, lattice 4 (D-1) + 1 per side)
 __host__ __device__ inline int tpe_surface_points(int D)
 {

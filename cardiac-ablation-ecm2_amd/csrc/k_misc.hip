@@ -455,129 +455,6 @@ k_pcg_update_xd(int n, const double *__restrict__ nom, const double *__restrict_
    }
 }
 
-// One CGSolver iteration's vector work in one cooperative launch (serial forms; solvers.cpp:930-990):
-// phase 1 is k_pcg_step_r's (alpha = nom/den, r -= alpha A d, the workgroup's part of (B r, r)) with
-// z = dinv .* r kept in registers; a grid barrier; every workgroup then sums the partials in one fixed
-// order (the same betanom everywhere), workgroup 0 runs the stopping test, and phase 2 is
-// k_pcg_update_xd's (x += alpha d, d = z + beta d) from the z in registers -- or, when this iteration's
-// test stops the loop, k_pcg_finish_x's x += alpha d.  8 vector streams instead of 10 and one launch
-// instead of three.  Workgroup b takes the contiguous pairs [b 256 K, (b + 1) 256 K) (a flat grid, like
-// k_dot_partial).  The partials and the arrival counter are written through to memory (agent-scope
-// relaxed atomics after the stores have drained: the other XCDs' L2s never hold them; the write-through
-// form of profiles/calib/lastholder_probe.hip).  The launch is cooperative (every workgroup resident),
-// and the barrier gives up after ~1 s (betanom := NaN, so the solve fails with ECM2_ERR_NUMERIC instead
-// of hanging).
-constexpr int kFusedThreads = 256;
-template <int KR, int KL>
-__global__ void __launch_bounds__(kFusedThreads, KR <= 16 ? 4 : 2)
-k_pcg_fused(int n, const double *__restrict__ nom, const double *__restrict__ den, const double *__restrict__ z,
-            double *__restrict__ r, const double *__restrict__ dinv, double *__restrict__ x, double *__restrict__ d,
-            double *__restrict__ partials, unsigned long long *__restrict__ arrivals, double *__restrict__ betanom_out,
-            double *__restrict__ alpha_out, PcgCheck chk)
-{
-   constexpr int K = KR + KL;
-   if (chk.ctl->done) { return; }  // (every workgroup alike: only this kernel's workgroup 0 writes it, after the barrier)
-   const int G = gridDim.x;
-   const double alpha = *nom / *den;
-   const long n2 = n / 2, base = (long)blockIdx.x * (kFusedThreads * K) + threadIdx.x;
-   const bool tail_lane = (n & 1) && blockIdx.x == 0 && threadIdx.x == 0;  // entry n - 1
-   const v2d *z2 = reinterpret_cast<const v2d *>(z), *q2 = reinterpret_cast<const v2d *>(dinv);
-   v2d *r2 = reinterpret_cast<v2d *>(r);
-   // z of the thread's first KR pairs in registers, of the next KL in LDS (KL 16-byte rows of the workgroup)
-   v2d zz[KR];
-   __shared__ v2d zl[KL > 0 ? KL : 1][kFusedThreads];
-   auto zput = [&](int k, v2d v) {
-      if (k < KR) { zz[k < KR ? k : 0] = v; }
-      else { zl[k < KR ? 0 : k - KR][threadIdx.x] = v; }
-   };
-   auto zget = [&](int k) -> v2d { return k < KR ? zz[k < KR ? k : 0] : zl[k < KR ? 0 : k - KR][threadIdx.x]; };
-   double s = 0.0, zt = 0.0;
-#pragma unroll
-   for (int k = 0; k < K; k++)
-   {
-      const long i = base + (long)kFusedThreads * k;
-      if (i < n2)
-      {
-         const v2d rn = r2[i] + (-alpha) * z2[i];
-         r2[i] = rn;
-         const v2d zn = dinv ? q2[i] * rn : rn;
-         zput(k, zn);
-         s += rn.x * zn.x;
-         s += rn.y * zn.y;
-      }
-   }
-   if (tail_lane)
-   {
-      const long i = n - 1;
-      const double rn = r[i] + (-alpha) * z[i];
-      r[i] = rn;
-      zt = dinv ? dinv[i] * rn : rn;
-      s += rn * zt;
-   }
-   // the workgroup's partial, written through
-   __shared__ double red[kFusedThreads / 64];
-   __shared__ double bn_sh;
-   for (int off = 32; off > 0; off >>= 1) { s += __shfl_down(s, off, 64); }
-   if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6] = s; }
-   __syncthreads();
-   if (threadIdx.x == 0)
-   {
-      __hip_atomic_store(partials + blockIdx.x, (red[0] + red[1]) + (red[2] + red[3]), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_s_waitcnt(0);
-      const unsigned long long old = __hip_atomic_fetch_add(arrivals, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned long long target = (old / G + 1) * G;
-      bool ok = false;
-      for (int spin = 0; spin < (1 << 22); spin++)
-      {
-         if (__hip_atomic_load(arrivals, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) { ok = true; break; }
-         __builtin_amdgcn_s_sleep(4);
-      }
-      bn_sh = ok ? 0.0 : __builtin_nan("");
-   }
-   __syncthreads();
-   // betanom: every workgroup sums the G partials in the same order
-   double v = 0.0;
-   for (int j = threadIdx.x; j < G; j += kFusedThreads)
-   {
-      v += __hip_atomic_load(partials + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-   }
-   for (int off = 32; off > 0; off >>= 1) { v += __shfl_down(v, off, 64); }
-   __syncthreads();
-   if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6] = v; }
-   __syncthreads();
-   const double bn = ((red[0] + red[1]) + (red[2] + red[3])) + bn_sh;
-   if (blockIdx.x == 0 && threadIdx.x == 0)
-   {
-      *alpha_out = alpha;
-      *betanom_out = bn;
-      pcg_check_one(bn, chk);
-   }
-   // this iteration's test, as pcg_check_one decides it (kind 0)
-   const bool stop = !isfinite(bn) || bn < 0.0 || bn <= chk.r0 || chk.it + 1 > chk.max_iter;
-   if (stop && !isfinite(bn)) { return; }  // (MFEM_VERIFY's abort: x is not finished)
-   const double beta = bn / *nom;
-   v2d *x2 = reinterpret_cast<v2d *>(x), *d2 = reinterpret_cast<v2d *>(d);
-#pragma unroll
-   for (int k = 0; k < K; k++)
-   {
-      const long i = base + (long)kFusedThreads * k;
-      if (i < n2)
-      {
-         const v2d dold = d2[i];
-         x2[i] = x2[i] + alpha * dold;
-         if (!stop) { d2[i] = zget(k) + beta * dold; }
-      }
-   }
-   if (tail_lane)
-   {
-      const long j = n - 1;
-      const double dold = d[j];
-      x[j] = x[j] + alpha * dold;
-      if (!stop) { d[j] = zt + beta * dold; }
-   }
-}
-
 // After the loop: the stopping iteration's x += alpha d, when the stop came from its betanom test
 // (converged, max_iter, (B r, r) < 0: CGSolver has already added alpha d then); a den == 0 stop
 // comes after k_pcg_update_xd has run (x complete).
@@ -870,67 +747,6 @@ void pcg_update_xd(int n, const double *nom, const double *den, const double *be
                       r, dinv, ctl);
    ECM2_HIP(hipGetLastError());
 }
-
-namespace
-{
-template <int KR, int KL>
-int fused_grid(int n)
-{
-   constexpr int K = KR + KL;
-   static int per_cu = -1, cus = 0;
-   if (per_cu < 0)
-   {
-      int dev = 0, coop = 0;
-      ECM2_HIP(hipGetDevice(&dev));
-      ECM2_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-      ECM2_HIP(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev));
-      per_cu = 0;
-      if (coop) { ECM2_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pcg_fused<KR, KL>, kFusedThreads, 0)); }
-   }
-   // every workgroup resident, and one partial each in the solver's kDotPartials
-   const long need = (n / 2 + (long)kFusedThreads * K - 1) / ((long)kFusedThreads * K);
-   return per_cu > 0 && need <= std::min<long>((long)per_cu * cus, kDotPartials) ? (int)std::max<long>(need, 1) : 0;
-}
-template <int KR, int KL>
-bool launch_fused(int n, const double *nom, const double *den, const double *z, double *r, const double *dinv,
-                  double *x, double *d, double *partials, unsigned long long *arrivals, double *betanom,
-                  double *alpha, const PcgStop &stop, hipStream_t s)
-{
-   const int G = fused_grid<KR, KL>(n);
-   if (G <= 0) { return false; }
-   PcgCheck chk = to_check(&stop);
-   void *args[] = {&n, &nom, &den, &z, &r, &dinv, &x, &d, &partials, &arrivals, &betanom, &alpha, &chk};
-   ECM2_HIP(hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&k_pcg_fused<KR, KL>), dim3(std::max(G, 1)),
-                                       dim3(kFusedThreads), args, 0, s));
-   return true;
-}
-} // namespace
-
-// the forms pcg_fused runs, smallest first: pairs per thread in registers + in LDS (16 + 9: 36,864 B of LDS,
-// four workgroups per CU, 6.5M pairs on 256 CUs; 32 + 19: 77,824 B, two per CU, 6.7M pairs)
-#define ECM2_FUSED_FORMS(X) X(16, 0) X(16, 9) X(32, 0) X(32, 8) X(32, 19)
-int pcg_fused_ok(int n)
-{
-   if (n < 2) { return 0; }
-#define ECM2_TRY(R, L) \
-   if (fused_grid<R, L>(n)) { return R * 100 + L; }
-   ECM2_FUSED_FORMS(ECM2_TRY)
-#undef ECM2_TRY
-   return 0;
-}
-
-void pcg_fused(int k, int n, const double *nom, const double *den, const double *z, double *r, const double *dinv,
-               double *x, double *d, double *partials, unsigned long long *arrivals, double *betanom, double *alpha,
-               const PcgStop &stop, hipStream_t s)
-{
-   bool ok = false;
-#define ECM2_RUN(R, L) \
-   if (k == R * 100 + L) { ok = launch_fused<R, L>(n, nom, den, z, r, dinv, x, d, partials, arrivals, betanom, alpha, stop, s); }
-   ECM2_FUSED_FORMS(ECM2_RUN)
-#undef ECM2_RUN
-   ECM2_VERIFY(ok, ERR_INTERNAL, "fused PCG step: form " << k << " does not cover " << n << " entries");
-}
-#undef ECM2_FUSED_FORMS
 
 void pcg_finish_x(int n, const double *alpha, const double *d, double *x, hipStream_t s, const PcgCtl *ctl)
 {

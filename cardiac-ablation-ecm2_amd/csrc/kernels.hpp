@@ -544,14 +544,6 @@ void pcg_step_r(int n, const double *nom, const double *den, const double *z, do
 void pcg_update_xd(int n, const double *nom, const double *den, const double *betanom, double *x, double *d,
                    const double *r, const double *dinv, hipStream_t s, const PcgCtl *ctl = nullptr);
 void pcg_finish_x(int n, const double *alpha, const double *d, double *x, hipStream_t s, const PcgCtl *ctl);
-//   pcg_fused (serial forms): pcg_step_r + its test + pcg_update_xd (or, on a stop, pcg_finish_x's x += alpha d)
-//   in one cooperative launch with z = dinv .* r in registers and LDS: 8 vector streams.  pcg_fused_ok(n): the
-//   form it runs with (0: n too large for one resident grid's registers and LDS, or no cooperative launch).
-//   partials: >= the grid (<= kDotPartials); arrivals: a zeroed device counter for the grid barrier.
-int pcg_fused_ok(int n);
-void pcg_fused(int k, int n, const double *nom, const double *den, const double *z, double *r, const double *dinv,
-               double *x, double *d, double *partials, unsigned long long *arrivals, double *betanom, double *alpha,
-               const PcgStop &stop, hipStream_t s);
 // a stopping test alone (after a distributed dot's all-reduce)
 void pcg_check(const double *v, const PcgStop &stop, hipStream_t s);
 // saved[i] = v[idx[i]], v[idx[i]] = 0  /  v[idx[i]] = y[idx[i]] = saved[i]

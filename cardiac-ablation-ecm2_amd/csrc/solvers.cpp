@@ -1,8 +1,6 @@
 // solvers.cpp -- see solvers.hpp.
 #include "solvers.hpp"
 
-#include <cstdlib>
-#include <string>
 #include <thread>
 
 #include <algorithm>
@@ -94,7 +92,6 @@ struct PCGWork
    DeviceArray<double> r, d, z, saved, dinv, partials, scal;
    double *hs = nullptr, *hs_dev = nullptr;
    DeviceArray<kern::PcgCtl> ctl;                          // the device-driven loop's state
-   DeviceArray<unsigned long long> arrivals;               // the fused step's grid-barrier counter
    kern::PcgCtl *hctl = nullptr, *hctl_dev = nullptr;      // its mapped pinned mirror
    ~PCGWork()
    {
@@ -113,7 +110,6 @@ struct PCGWork
       if (jacobi) { grow(dinv, std::max(n, 1)); }
       grow(partials, kern::kDotPartials);
       grow(scal, 4);
-      if (arrivals.size() < 1) { arrivals.resize(1); }
       if (!hs)
       {
          ECM2_HIP(hipHostMalloc(&hs, 4 * sizeof(double), hipHostMallocMapped));
@@ -225,7 +221,6 @@ PCGResult pcg_solve(LinOp &A, const int *ess, int n_ess, const double *b, double
       // the device-driven loop's state, reset before the read-back below idles the stream (no
       // kernel of a previous solve writes the mirror any more: every solve ends synchronised)
       ECM2_HIP(hipMemsetAsync(w.ctl.data(), 0, sizeof(kern::PcgCtl), s));
-      ECM2_HIP(hipMemsetAsync(w.arrivals.data(), 0, sizeof(unsigned long long), s));
       *w.hctl = kern::PcgCtl{};
       if (nen > 0) { cmult_den(d, z, nullptr, nullptr); }
       else
@@ -272,33 +267,20 @@ PCGResult pcg_solve(LinOp &A, const int *ess, int n_ess, const double *b, double
                if (spin > 256) { std::this_thread::yield(); }
             }
          };
-         // serial forms: the iteration's vector work as one cooperative launch (pcg_fused: 8 streams, the
-         // stopping iteration's x += alpha d included); ECM2_PCG_FUSED=0 keeps the three-launch form
-         const char *fe = std::getenv("ECM2_PCG_FUSED");
-         const int fused = direct && !(fe && std::string(fe) == "0") ? kern::pcg_fused_ok(n) : 0;
          for (int i = 1;; i++)
          {
             if (i > 1 && stopped_by(i - 1)) { break; }
+            // r -= alpha A d, betanom = r.(M^{-1} r) in one pass, its test
             const kern::PcgStop stop{r0, i, max_iter, ctl, w.hctl_dev};
-            if (fused)
+            kern::pcg_step_r(n, nom, den, z, r, dinv, partials, betanom, alpha, s, ctl, direct ? &stop : nullptr);
+            if (!direct)
             {
-               // r -= alpha A d, betanom and its test, then x += alpha d, d = M^{-1} r + beta d
-               kern::pcg_fused(fused, n, nom, den, z, r, dinv, x, d, partials, w.arrivals.data(), betanom, alpha, stop, s);
-               if (i >= max_iter) { break; }
+               A.sum_scalars(betanom, 1, s);
+               kern::pcg_check(betanom, stop, s);
             }
-            else
-            {
-               // r -= alpha A d, betanom = r.(M^{-1} r) in one pass, its test
-               kern::pcg_step_r(n, nom, den, z, r, dinv, partials, betanom, alpha, s, ctl, direct ? &stop : nullptr);
-               if (!direct)
-               {
-                  A.sum_scalars(betanom, 1, s);
-                  kern::pcg_check(betanom, stop, s);
-               }
-               if (i >= max_iter) { break; }
-               // x += alpha d, d = M^{-1} r + beta d
-               kern::pcg_update_xd(n, nom, den, betanom, x, d, r, dinv, s, ctl);
-            }
+            if (i >= max_iter) { break; }
+            // x += alpha d, d = M^{-1} r + beta d
+            kern::pcg_update_xd(n, nom, den, betanom, x, d, r, dinv, s, ctl);
             // z = A d, den = (A d, d) and its test (after ++i: final_iter = i + 1 on a den == 0 stop)
             const kern::PcgStop dstop{r0, i + 1, max_iter, ctl, w.hctl_dev, betanom, 1};
             if (nen > 0) { cmult_den(d, z, ctl, &dstop); }
@@ -315,8 +297,8 @@ PCGResult pcg_solve(LinOp &A, const int *ess, int n_ess, const double *b, double
             }
             std::swap(nom, betanom);  // nom <- betanom
          }
-         // the stopping iteration's x += alpha d (a betanom stop; the fused step has added it)
-         if (!fused) { kern::pcg_finish_x(n, alpha, d, x, s, ctl); }
+         // the stopping iteration's x += alpha d (a betanom stop)
+         kern::pcg_finish_x(n, alpha, d, x, s, ctl);
          ECM2_HIP(hipStreamSynchronize(s));
          const int done = *(volatile int *)&hm->done;
          ECM2_VERIFY(done != kern::PCG_RUNNING, ERR_INTERNAL, "device PCG loop ended without a stop");

@@ -3,11 +3,12 @@
 # kernel), one pass per workload, same tree, same box: rocprofv3 kernel-trace stats,
 # the FETCH_SIZE and WRITE_SIZE passes (separate: TCC slots), reduced (pmc_reduce.py) and pinned
 # with provenance (pmc_pin.py; COMMIT = the tree's commit), then the bench line that reads the pin.
-# Usage: COMMIT=<sha> bash profiles/collect_r6.sh <set: a | b>
+# Usage: COMMIT=<sha> bash profiles/collect_r6.sh <set: a | b | c>
 #   a: c4 (the headline: structured, affine + the k(T) coefficient snapshot), c4pen (the Pennes operator:
 #      both coefficients laws of one field, no per-point stream), c4ex16 (ex16p's M + dt K(u_alpha_gf))
 #   b: c4ent (the reference's numbering with the snapshot), c3 (fichera r6)
-# (the TRILINEAR and brick kernels did not change in round 6: their round-5 pins describe HEAD)
+#   c: the kernels round 6 did not change, re-pinned at the round's final tree: c5 (bricks), c4tri (TRILINEAR
+#      lattice kernel), c4enttrijac (the drop-in configuration), c5tri (TRILINEAR_E bricks)
 set -uo pipefail
 SET=${1:-a}
 O=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/collect_r6
@@ -37,6 +38,11 @@ if [ "$SET" = a ]; then
   one c4 affine_ts apply --workload c4 --steps 50 --warmup 5 || exit 1
   one c4pen affine_tsm apply --workload c4 --coefficients pennes --steps 50 --warmup 5 || exit 1
   one c4ex16 affine_tsm apply --workload c4 --coefficients ex16 --steps 50 --warmup 5 || exit 1
+elif [ "$SET" = c ]; then
+  one c5 affine_e apply_brick --workload c5 --steps 30 --warmup 5 || exit 1
+  one c4tri trilinear apply --workload c4 --mesh trilinear --steps 30 --warmup 5 || exit 1
+  one c4enttrijac trilinear apply --workload c4 --numbering entity --mesh trilinear --geometry-input jacobians --steps 30 --warmup 5 || exit 1
+  one c5tri trilinear_e apply_brick --workload c5 --mesh trilinear --steps 30 --warmup 5 || exit 1
 else
   # b: the reference's numbering (RM 3: the dealt gather) and configs[2]
   one c4ent affine_ts apply --workload c4 --numbering entity --steps 50 --warmup 5 || exit 1

@@ -107,6 +107,7 @@ def load_library(path: str = LIB_PATH):
         "ecm2_pa_form_set_coefficient_snapshot": (i32, [vp, i32]),
         "ecm2_pa_form_coefficient_snapshot": (i32, [vp, ip]),
         "ecm2_pa_form_energy_parts": (i32, [vp, ip]),
+        "ecm2_pa_form_flux_diagonal": (i32, [vp, ip]),
         "ecm2_pa_form_qdata_bytes": (i32, [vp, dp]),
         "ecm2_pa_form_brick_info": (i32, [vp, ip, ip]),
         "ecm2_pa_form_addressing_info": (i32, [vp, ip, ip, ctypes.POINTER(ctypes.c_long)]),
@@ -658,6 +659,12 @@ class BilinearForm:
         v = [ctypes.c_int() for _ in range(3)]
         _check(_lib.ecm2_pa_form_snapshot_info(self._h, *[ctypes.byref(a) for a in v]))
         return bool(v[0].value), v[1].value, bool(v[2].value)
+
+    def FluxDiagonal(self) -> bool:
+        """Axis-aligned elements: the snapshot kernel applies adj(J) adj(J)^T / det J as a diagonal."""
+        v = ctypes.c_int()
+        _check(_lib.ecm2_pa_form_flux_diagonal(self._h, ctypes.byref(v)))
+        return bool(v.value)
 
     def EnergyParts(self):
         """Partials of x^T A x the Mult writes when PCG folds its den = (A d, d) into it (0: a dot pass)."""

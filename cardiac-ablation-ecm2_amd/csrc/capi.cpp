@@ -420,6 +420,11 @@ int ecm2_pa_form_snapshot_info(const ecm2_pa_form *f, int *on, int *mass_values,
    });
 }
 
+int ecm2_pa_form_flux_diagonal(const ecm2_pa_form *f, int *on)
+{
+   return guard([&] { NEED(f); NEED(on); *on = f->f->flux_diagonal() ? 1 : 0; });
+}
+
 int ecm2_pa_form_energy_parts(const ecm2_pa_form *f, int *parts)
 {
    return guard([&] { NEED(f); NEED(parts); *parts = f->f->energy_parts(); });

@@ -338,6 +338,15 @@ __global__ void k_setup_jac(const int *__restrict__ pos, int kind, int ne, int N
    write_qdata(pos, kind, NQ, e, q, W[q], J, cm, cd, qd_diff, qd_mass);
 }
 
+// Any nonzero off-diagonal C entry (C12, C13, C23: p0.y, p1.x, p2.x of the blocked [blk][3][64] pairs)?
+__global__ void k_affine_offdiag(long n, int ne, const double *__restrict__ qd_fac, int *__restrict__ flag)
+{
+   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   if (t >= n || t >= ne) { return; }  // (t = blk 64 + lane: the element's position)
+   const v2d *p = reinterpret_cast<const v2d *>(qd_fac + (t >> 6) * 3 * 128) + (t & 63);
+   if (p[0].y != 0.0 || p[64].x != 0.0 || p[128].x != 0.0) { atomicOr(flag, 1); }
+}
+
 // AFFINE layout from the corners of parallelepiped elements (kernels.hpp).  J is the
 // reference-cube edge matrix [x_100 - x_000 | x_010 - x_000 | x_001 - x_000] (the trilinear
 // Jacobian of GeometricFactors, mesh.cpp:15220-15273, when the element is affine); the
@@ -1088,6 +1097,20 @@ void affine_expand(const QLayout &L, int Q, const double *qd_fac, const double *
    ECM2_Q_BLOCKED_CASES(k_affine_expand, n, blk, L.ne, qd_fac, qd_pair, L.pw, qd_diff, qd_mass, qm1)
 }
 #undef ECM2_Q_BLOCKED_CASES
+
+bool affine_c_diagonal(const QLayout &L, const double *qd_fac, int *dflag, hipStream_t s)
+{
+   ECM2_VERIFY(L.kind == QLAYOUT_AFFINE, ERR_INTERNAL, "C diagonal test: blocked AFFINE layout only");
+   if (L.ne == 0) { return true; }
+   ECM2_HIP(hipMemsetAsync(dflag, 0, sizeof(int), s));
+   const long n = (long)L.nblk() * 64;
+   hipLaunchKernelGGL(k_affine_offdiag, dim3(grid_for(n, 256)), dim3(256), 0, s, n, L.ne, qd_fac, dflag);
+   ECM2_HIP(hipGetLastError());
+   int h = 1;
+   ECM2_HIP(hipMemcpyAsync(&h, dflag, sizeof(int), hipMemcpyDeviceToHost, s));
+   ECM2_HIP(hipStreamSynchronize(s));
+   return h == 0;
+}
 
 void setup_affine(const QLayout &L, int Q, const double *enodes, const double *J, const double *W,
                   const CoeffDesc *cm, const CoeffDesc *cd, const double *cm_q, const double *cd_q,

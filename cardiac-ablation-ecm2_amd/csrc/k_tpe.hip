@@ -1124,7 +1124,7 @@ k_apply_tpe_tlb(int ne, int blk_begin, int blk_end, int n_owned, const int *__re
 // per-point stream at all.  x and T' are gathered once per lattice point (the block's 729 lattice
 // slots, as k_apply_tpe_tlb) into one LDS region that the cross-wave face exchange reuses afterwards.
 // Lattice blocks only (RM 1 regular, 3 lattice-map), p = 2.
-template <int D, int Q, bool SPLIT, int RM, int MM, bool LAW>
+template <int D, int Q, bool SPLIT, int RM, int MM, bool LAW, bool CD>
 __global__ void __launch_bounds__(256, 2)
 k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__restrict__ gmap,
                const double *__restrict__ qdd, const double *__restrict__ qdm,
@@ -1307,9 +1307,19 @@ k_apply_tpe_ts(int ne, int blk_begin, int blk_end, int n_owned, const int *__res
                }
                if (MM == 1) { mc = cur[qx]; }
                const double m = MASS ? mc * u : 0.0;  // W alpha det J u
-               double fx = ce[0].x * ux, fy = ce[0].y * ux, fz = ce[1].x * ux;
-               fx += ce[0].y * uy; fy += ce[1].y * uy; fz += ce[2].x * uy;
-               fx += ce[1].x * uz; fy += ce[2].x * uz; fz += ce[2].y * uz;
+               double fx, fy, fz;
+               if constexpr (CD)
+               {
+                  // axis-aligned elements (C diagonal, checked at setup): the same values as the general
+                  // product below, whose off-diagonal terms then add exact zeros
+                  fx = ce[0].x * ux; fy = ce[1].y * uy; fz = ce[2].y * uz;
+               }
+               else
+               {
+                  fx = ce[0].x * ux; fy = ce[0].y * ux; fz = ce[1].x * ux;
+                  fx += ce[0].y * uy; fy += ce[1].y * uy; fz += ce[2].x * uy;
+                  fx += ce[1].x * uz; fy += ce[2].x * uz; fz += ce[2].y * uz;
+               }
                fx *= wb; fy *= wb; fz *= wb;
 #pragma unroll
                for (int dx = 0; dx < D; dx++)
@@ -1712,22 +1722,26 @@ void launch_tpe(const ApplyArgs &a, const Basis1D &b, const double *rowtab, hipS
             for (int q = 0; q < MAX_Q1D; q++) { bw.B[q + MQ * d] = a.qw[q] * b.B[q + MQ * d]; }
          QPts qw = {};
          for (int q = 0; q < MAX_Q1D; q++) { qw.x[q] = a.qw[q]; }
-#define ECM2_TS(RM, MM, LAW)                                                                                        \
-   hipLaunchKernelGGL((k_apply_tpe_ts<3, 4, SPLIT, RM, MM, LAW>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end,     \
+#define ECM2_TS(RM, MM, LAW, CD)                                                                                    \
+   hipLaunchKernelGGL((k_apply_tpe_ts<3, 4, SPLIT, RM, MM, LAW, CD>), grid, block, 0, s, a.ne, a.blk_begin, a.blk_end, \
                       a.n_owned, a.gmap, a.qdd, a.qdm, a.x, a.xg, a.tsnap, a.y, a.yg, b, bw, a.lane_flags, a.part,     \
                       a.treg, a.part_stride, a.lmap, qw, a.law_d, a.law_m, a.en)
-#define ECM2_TS_MM(RM, LAW)                                                                                         \
-   if (!MASS) { ECM2_TS(RM, 0, LAW); }                                                                              \
-   else if (a.tmass == 1) { ECM2_TS(RM, 1, LAW); }                                                                  \
-   else { ECM2_TS(RM, 2, LAW); }
+#define ECM2_TS_MM(RM, LAW, CD)                                                                                     \
+   if (!MASS) { ECM2_TS(RM, 0, LAW, CD); }                                                                          \
+   else if (a.tmass == 1) { ECM2_TS(RM, 1, LAW, CD); }                                                              \
+   else { ECM2_TS(RM, 2, LAW, CD); }
+#define ECM2_TS_LAW(RM, CD)                                                                                         \
+   if (a.tlaw) { ECM2_TS_MM(RM, true, CD) } else { ECM2_TS_MM(RM, false, CD) }
+         // (axis-aligned meshes: the diagonal flux product, a.cdiag)
          if (a.treg_all)
          {
-            if (a.tlaw) { ECM2_TS_MM(1, true) } else { ECM2_TS_MM(1, false) }
+            if (a.cdiag) { ECM2_TS_LAW(1, true) } else { ECM2_TS_LAW(1, false) }
          }
          else
          {
-            if (a.tlaw) { ECM2_TS_MM(3, true) } else { ECM2_TS_MM(3, false) }
+            if (a.cdiag) { ECM2_TS_LAW(3, true) } else { ECM2_TS_LAW(3, false) }
          }
+#undef ECM2_TS_LAW
 #undef ECM2_TS_MM
 #undef ECM2_TS
       }

@@ -226,6 +226,7 @@ struct ApplyArgs
    const double *tsnap = nullptr;
    int tsnap_kind = 0;              // QLayout::tsnap
    int tmass = 0, tlaw = 0;         // QLayout::tmass, QLayout::tlaw
+   int cdiag = 0;                   // snapshot forms: every element's C = adj(J) adj(J)^T / det J diagonal
    PointLaw law_d, law_m;           // tlaw = 1: the diffusion and mass laws at the point
    double qw[MAX_Q1D] = {};
    int xwave = 0;                   // the merge plan has cross-wave faces (AFFINE / TRILINEAR forms)
@@ -409,6 +410,9 @@ void setup_from_nodes(const QLayout &L, int Q, const double *enodes, const doubl
 // AFFINE / AFFINE_E layout (see above) from the corners of parallelepiped elements; needs the
 // diffusion coefficient (cd); cm null: a diffusion-only form (L.pw = 1, AFFINE only).
 // J (optional, device, MFEM layout NQ x 3 x 3 x NE) replaces the corners.
+// AFFINE (blocked) C factors: are all off-diagonal entries exactly zero (axis-aligned elements)?  dflag: one
+// device int of scratch.  Synchronises the stream.
+bool affine_c_diagonal(const QLayout &L, const double *qd_fac, int *dflag, hipStream_t s);
 void setup_affine(const QLayout &L, int Q, const double *enodes, const double *J, const double *W,
                   const CoeffDesc *cm, const CoeffDesc *cd, const double *cm_q, const double *cd_q,
                   double *qd_fac, double *qd_pair, hipStream_t s);

@@ -77,6 +77,7 @@ public:
    // with the snapshot: the mass values (QLayout::tmass) and where the laws are applied (QLayout::tlaw)
    int snapshot_mass() const { return layout_.tmass; }
    int snapshot_law_at_point() const { return layout_.tlaw; }
+   bool flux_diagonal() const { return cdiag_ && layout_.tsnap; }
    // bytes of quadrature data the form stores (diffusion + mass + the coefficient snapshot)
    size_t qdata_bytes() const { return qd_diff_.bytes() + qd_mass_.bytes() + tsnap_.bytes(); }
 
@@ -254,6 +255,8 @@ private:
    DeviceArray<int> breg_;          // LINE bricks, lattice-numbered: [nbrick][8] (base, sx, sy, sz, face mask)
    DeviceArray<int> treg_;          // TPE blocks: [nblk][8] (base, sx, sy, sz, face mask, -, -, flag 1 regular / 2 lattice slots)
    bool treg_all_ = false;          // every TPE block regular: face-grouped slots only
+   bool cdiag_ = false;             // snapshot forms: every element's C diagonal (axis-aligned: the diagonal flux)
+   DeviceArray<int> cdflag_;        // its test's device scratch
    bool tlat_all_ = false;          // every TPE block a lattice-map block (treg flag 2)
    int n_treg_ = 0;                 // regular TPE blocks
    int n_tlat_ = 0;                 // TPE blocks with face-grouped slots but map-addressed dofs (treg flag 2)

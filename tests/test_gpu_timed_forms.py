@@ -101,6 +101,47 @@ def test_timed_snapshot_forms(n, numbering):
     _check_form(mesh, fes, form, keep, 100 + n)
 
 
+@pytest.mark.parametrize("numbering,coefficients", [("structured", "bioheat"), ("entity", "bioheat"),
+                                                   ("structured", "pennes")])
+def test_snapshot_diagonal_flux_is_the_general_product(monkeypatch, numbering, coefficients):
+    """Axis-aligned elements (the Cartesian forms): the snapshot kernel's diagonal flux product
+    (k_apply_tpe_ts<..., CD = true>, FluxDiagonal()) gives bit for bit the general product's y
+    (ECM2_CDIAG=0 at Assemble), whose off-diagonal terms add exact zeros; a sheared (still affine) mesh
+    keeps the general product."""
+    order = "faces" if numbering == "entity" else "auto"
+
+    def build(mesh, fes, keep):
+        if coefficients == "pennes":
+            return B.bench_law_form(E, torch, mesh, fes, keep, "pennes")
+        return B.bench_form(E, torch, mesh, fes, keep, element_order=order)
+
+    ys, x = [], None
+    for env in ("0", "1"):
+        monkeypatch.setenv("ECM2_CDIAG", env)
+        mesh, fes = B.cartesian_space(E, 16, 16, 16, 2, numbering, "affine")
+        keep = []
+        form = build(mesh, fes, keep)
+        assert form.CoefficientSnapshot() and form.FluxDiagonal() == (env == "1")
+        if x is None:
+            x = torch.as_tensor(np.random.default_rng(16).uniform(-1, 1, fes.ndofs)).cuda()
+        y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+        form.Mult(x, y)
+        ys.append(y)
+        if env == "1" and coefficients == "bioheat":
+            _check_form(mesh, fes, form, keep, 16)
+    assert torch.equal(ys[0], ys[1])
+    monkeypatch.delenv("ECM2_CDIAG")
+    mesh, fes = B.cartesian_space(E, 16, 16, 16, 2, numbering, "affine")
+    v = mesh.vertices()
+    v[:, 0] += 0.25 * v[:, 1]
+    mesh.set_vertices(v)
+    keep = []
+    form = build(mesh, fes, keep)
+    assert form.CoefficientSnapshot() and not form.FluxDiagonal()
+    if coefficients == "bioheat":
+        _check_form(mesh, fes, form, keep, 17)
+
+
 @pytest.mark.parametrize("variant", ["trilinear", "drop_in"])
 def test_timed_trilinear_forms(variant):
     """configs[3] size, bench.py's trilinear and drop_in sub-objects: interior vertices moved

@@ -545,6 +545,8 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
                 double *__restrict__ y, double *__restrict__ yg, const Basis1D *__restrict__ btab,
                 double *__restrict__ part, const QPts qp)
 {
+   // G: 0 per-point qdata, 1 AFFINE_E, 2 TRILINEAR_E, 3 AFFINE_E with every C diagonal (axis-aligned elements:
+   // the general product's values, whose off-diagonal terms would add exact zeros)
    constexpr bool AFF = G != 0;  // a compressed layout: point pairs + per-element data
    using S = BrickShapeC<D, Q, BZ>;
    constexpr int NE = S::NE, DD = S::DD, QQ = S::QQ, DQ = S::DQ, SA = S::SA, SB = S::SB, DS = S::DS;
@@ -618,6 +620,12 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
       }
 #pragma unroll
       for (int c = 0; c < (G == 1 ? 6 : 0); c++) { cc[c] = qdd[(size_t)e * 6 + c]; }
+      if (G == 3)
+      {
+         cc[0] = qdd[(size_t)e * 6];
+         cc[3] = qdd[(size_t)e * 6 + 3];
+         cc[5] = qdd[(size_t)e * 6 + 5];
+      }
    }
    else { line_load_qdata<D, Q, true, true, 0>(qv, e, l3c, qdd, qdm, qp); }
 
@@ -729,6 +737,14 @@ k_apply_brick_c(int k_begin, int k_end, const int *__restrict__ belem, const int
             fx = A[0][0] * t0; fx += A[0][1] * t1; fx += A[0][2] * t2;
             fy = A[1][0] * t0; fy += A[1][1] * t1; fy += A[1][2] * t2;
             fz = A[2][0] * t0; fz += A[2][1] * t1; fz += A[2][2] * t2;
+            m = pa[qz].y * u;
+         }
+         else if (G == 3)
+         {
+            const double wb = pa[qz].x;
+            fx = wb * (cc[0] * gx);
+            fy = wb * (cc[3] * gy);
+            fz = wb * (cc[5] * gz);
             m = pa[qz].y * u;
          }
          else if (AFF)
@@ -1062,7 +1078,8 @@ void launch_brick(const ApplyArgs &a, hipStream_t s)
    hipLaunchKernelGGL((k_apply_brick_c<D, Q, BZ, SP, GG, RG>), grid, block, 0, s, k0, k1, a.belem, a.bmap,    \
                       a.breg, a.n_owned, a.qdd, a.qdm, a.x, a.xg, a.y, a.yg, a.btab, a.part_brick, a.qp)
 #define ECM2_BRICK_G(SP, RG)                    \
-   if (g == 1) { ECM2_BRICK(SP, 1, RG); }       \
+   if (g == 1 && a.cdiag) { ECM2_BRICK(SP, 3, RG); } \
+   else if (g == 1) { ECM2_BRICK(SP, 1, RG); }  \
    else if (g == 2) { ECM2_BRICK(SP, 2, RG); }  \
    else { ECM2_BRICK(SP, 0, RG); }
    if (split) { ECM2_BRICK_G(true, false) }

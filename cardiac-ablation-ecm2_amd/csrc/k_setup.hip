@@ -347,6 +347,15 @@ __global__ void k_affine_offdiag(long n, int ne, const double *__restrict__ qd_f
    if (p[0].y != 0.0 || p[64].x != 0.0 || p[128].x != 0.0) { atomicOr(flag, 1); }
 }
 
+// AFFINE_E: C per element [e][6] = (C11, C12, C13, C22, C23, C33)
+__global__ void k_affine_e_offdiag(int ne, const double *__restrict__ qd_fac, int *__restrict__ flag)
+{
+   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+   if (e >= ne) { return; }
+   const double *c = qd_fac + e * 6;
+   if (c[1] != 0.0 || c[2] != 0.0 || c[4] != 0.0) { atomicOr(flag, 1); }
+}
+
 // AFFINE layout from the corners of parallelepiped elements (kernels.hpp).  J is the
 // reference-cube edge matrix [x_100 - x_000 | x_010 - x_000 | x_001 - x_000] (the trilinear
 // Jacobian of GeometricFactors, mesh.cpp:15220-15273, when the element is affine); the
@@ -1100,11 +1109,16 @@ void affine_expand(const QLayout &L, int Q, const double *qd_fac, const double *
 
 bool affine_c_diagonal(const QLayout &L, const double *qd_fac, int *dflag, hipStream_t s)
 {
-   ECM2_VERIFY(L.kind == QLAYOUT_AFFINE, ERR_INTERNAL, "C diagonal test: blocked AFFINE layout only");
+   ECM2_VERIFY(L.kind == QLAYOUT_AFFINE || L.kind == QLAYOUT_AFFINE_E, ERR_INTERNAL,
+               "C diagonal test: AFFINE / AFFINE_E layouts only");
    if (L.ne == 0) { return true; }
    ECM2_HIP(hipMemsetAsync(dflag, 0, sizeof(int), s));
-   const long n = (long)L.nblk() * 64;
-   hipLaunchKernelGGL(k_affine_offdiag, dim3(grid_for(n, 256)), dim3(256), 0, s, n, L.ne, qd_fac, dflag);
+   if (L.kind == QLAYOUT_AFFINE)
+   {
+      const long n = (long)L.nblk() * 64;
+      hipLaunchKernelGGL(k_affine_offdiag, dim3(grid_for(n, 256)), dim3(256), 0, s, n, L.ne, qd_fac, dflag);
+   }
+   else { hipLaunchKernelGGL(k_affine_e_offdiag, dim3(grid_for(L.ne, 256)), dim3(256), 0, s, L.ne, qd_fac, dflag); }
    ECM2_HIP(hipGetLastError());
    int h = 1;
    ECM2_HIP(hipMemcpyAsync(&h, dflag, sizeof(int), hipMemcpyDeviceToHost, s));

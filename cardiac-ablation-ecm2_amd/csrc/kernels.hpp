@@ -410,7 +410,7 @@ void setup_from_nodes(const QLayout &L, int Q, const double *enodes, const doubl
 // AFFINE / AFFINE_E layout (see above) from the corners of parallelepiped elements; needs the
 // diffusion coefficient (cd); cm null: a diffusion-only form (L.pw = 1, AFFINE only).
 // J (optional, device, MFEM layout NQ x 3 x 3 x NE) replaces the corners.
-// AFFINE (blocked) C factors: are all off-diagonal entries exactly zero (axis-aligned elements)?  dflag: one
+// AFFINE (blocked) / AFFINE_E C factors: are all off-diagonal entries exactly zero (axis-aligned elements)?  dflag: one
 // device int of scratch.  Synchronises the stream.
 bool affine_c_diagonal(const QLayout &L, const double *qd_fac, int *dflag, hipStream_t s);
 void setup_affine(const QLayout &L, int Q, const double *enodes, const double *J, const double *W,

@@ -1282,7 +1282,7 @@ void PAForm::setup_qdata(hipStream_t s)
       kern::setup_affine(layout_, Q_, jac_ ? nullptr : enodes_.data(), jac_, W_.data(), cm, cd, cm_q, cd_q,
                          qd_diff_.data(), qd_mass_.data(), s);
       cdiag_ = false;
-      if (layout_.tsnap && layout_.kind == QLAYOUT_AFFINE)
+      if ((layout_.tsnap && layout_.kind == QLAYOUT_AFFINE) || layout_.kind == QLAYOUT_AFFINE_E)
       {
          if (cdflag_.size() < 1) { cdflag_.resize(1); }
          const char *e = std::getenv("ECM2_CDIAG");  // (A/B aid: 0 keeps the general flux product)
@@ -1493,7 +1493,7 @@ ApplyArgs PAForm::apply_args(const double *x, const double *xg, double *y, doubl
    a.tsnap_kind = layout_.tsnap;
    a.tmass = layout_.tmass;
    a.tlaw = layout_.tlaw;
-   a.cdiag = cdiag_ && layout_.tsnap ? 1 : 0;
+   a.cdiag = cdiag_ && (layout_.tsnap || layout_.kind == QLAYOUT_AFFINE_E) ? 1 : 0;
    if (layout_.tsnap && layout_.tlaw)
    {
       a.law_d = point_law_of(cdiff_);

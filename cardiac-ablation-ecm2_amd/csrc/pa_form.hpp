@@ -77,7 +77,7 @@ public:
    // with the snapshot: the mass values (QLayout::tmass) and where the laws are applied (QLayout::tlaw)
    int snapshot_mass() const { return layout_.tmass; }
    int snapshot_law_at_point() const { return layout_.tlaw; }
-   bool flux_diagonal() const { return cdiag_ && layout_.tsnap; }
+   bool flux_diagonal() const { return cdiag_ && (layout_.tsnap || layout_.kind == QLAYOUT_AFFINE_E); }
    // bytes of quadrature data the form stores (diffusion + mass + the coefficient snapshot)
    size_t qdata_bytes() const { return qd_diff_.bytes() + qd_mass_.bytes() + tsnap_.bytes(); }
 

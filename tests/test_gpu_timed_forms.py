@@ -142,6 +142,26 @@ def test_snapshot_diagonal_flux_is_the_general_product(monkeypatch, numbering, c
         _check_form(mesh, fes, form, keep, 17)
 
 
+def test_brick_diagonal_flux_is_the_general_product(monkeypatch):
+    """The same for the p = 4 brick kernel on AFFINE_E (k_apply_brick_c, G = 3 on axis-aligned elements):
+    bit for bit the general product, and the oracle's Mult."""
+    ys, x = [], None
+    for env in ("0", "1"):
+        monkeypatch.setenv("ECM2_CDIAG", env)
+        mesh, fes = B.cartesian_space(E, 8, 8, 8, 4, "structured", "affine")
+        keep = []
+        form = B.bench_form(E, torch, mesh, fes, keep)
+        assert form.info()["layout"] == E.QLAYOUT_AFFINE_E and form.FluxDiagonal() == (env == "1")
+        if x is None:
+            x = torch.as_tensor(np.random.default_rng(8).uniform(-1, 1, fes.ndofs)).cuda()
+        y = torch.full((fes.ndofs,), float("nan"), dtype=torch.float64, device="cuda")
+        form.Mult(x, y)
+        ys.append(y)
+        if env == "1":
+            _check_form(mesh, fes, form, keep, 8)
+    assert torch.equal(ys[0], ys[1])
+
+
 @pytest.mark.parametrize("variant", ["trilinear", "drop_in"])
 def test_timed_trilinear_forms(variant):
     """configs[3] size, bench.py's trilinear and drop_in sub-objects: interior vertices moved

@@ -211,8 +211,9 @@ int ecm2_pa_form_snapshot_info(const ecm2_pa_form *f, int *on, int *mass_values,
  * workgroup of the coefficient-snapshot kernel -- or 0 when the solver runs the dot pass instead. */
 int ecm2_pa_form_energy_parts(const ecm2_pa_form *f, int *parts);
 /* Introspection (no reference counterpart): *on = 1 when the last Assemble found every element's
- * adj(J) adj(J)^T / det J diagonal (axis-aligned hexahedra) and the coefficient-snapshot kernel applies
- * it as a diagonal -- the general product's values, whose off-diagonal terms would add exact zeros. */
+ * adj(J) adj(J)^T / det J diagonal (axis-aligned hexahedra) and the apply kernel uses it as a diagonal -- the
+ * coefficient-snapshot kernel (p = 2) or the brick kernel (AFFINE_E, p >= 3) -- with the general product's
+ * values, whose off-diagonal terms would add exact zeros. */
 int ecm2_pa_form_flux_diagonal(const ecm2_pa_form *f, int *on);
 /* BilinearForm::AddDomainIntegrator(new MassIntegrator(Q)) / DiffusionIntegrator(Q)
  * (bilinearform.cpp:231-242).  data: CONSTANT -> data[0] (host);

@@ -3,7 +3,7 @@
 # kernel), one pass per workload, same tree, same box: rocprofv3 kernel-trace stats,
 # the FETCH_SIZE and WRITE_SIZE passes (separate: TCC slots), reduced (pmc_reduce.py) and pinned
 # with provenance (pmc_pin.py; COMMIT = the tree's commit), then the bench line that reads the pin.
-# Usage: COMMIT=<sha> bash profiles/collect_r6.sh <set: a | b | c>
+# Usage: COMMIT=<sha> bash profiles/collect_r6.sh <set: a | b | c | d>
 #   a: c4 (the headline: structured, affine + the k(T) coefficient snapshot), c4pen (the Pennes operator:
 #      both coefficients laws of one field, no per-point stream), c4ex16 (ex16p's M + dt K(u_alpha_gf))
 #   b: c4ent (the reference's numbering with the snapshot), c3 (fichera r6)
@@ -38,6 +38,9 @@ if [ "$SET" = a ]; then
   one c4 affine_ts apply --workload c4 --steps 50 --warmup 5 || exit 1
   one c4pen affine_tsm apply --workload c4 --coefficients pennes --steps 50 --warmup 5 || exit 1
   one c4ex16 affine_tsm apply --workload c4 --coefficients ex16 --steps 50 --warmup 5 || exit 1
+elif [ "$SET" = d ]; then
+  # the brick kernel after its diagonal flux (G = 3)
+  one c5 affine_e apply_brick --workload c5 --steps 30 --warmup 5 || exit 1
 elif [ "$SET" = c ]; then
   one c5 affine_e apply_brick --workload c5 --steps 30 --warmup 5 || exit 1
   one c4tri trilinear apply --workload c4 --mesh trilinear --steps 30 --warmup 5 || exit 1

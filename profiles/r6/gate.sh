@@ -1,7 +1,7 @@
 # round-6 gate at HEAD: the whole GPU suite (as the driver runs it), smoke(), the default bench line (the driver's
 # command) twice, and a kernel trace (rocprofv3 --kernel-trace --stats) of the default line -- gpurun_out/r6/gate/
 set -o pipefail
-O=gpurun_out/r6/gate
+O=${O:-gpurun_out/r6/gate}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread --durations=15 \

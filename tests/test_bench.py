@@ -60,7 +60,10 @@ def test_bench_single_gpu_line():
     assert b["value"] == pytest.approx(b["config"]["ndofs"] / (b["ms_per_step"] * 1e-3) / 1e6, rel=1e-3)
     assert b["config"]["numbering"].startswith("structured") and b["config"]["mesh"] == "affine"
     # the one-GPU line carries the marginal Jacobi-PCG iteration (MDoF*iter/s)
-    assert b["pcg_iteration"]["iterations"] == 20 and b["pcg_iteration"]["iteration_ms"] > b["ms_per_step"]
+    # (an iteration holds one apply kernel; against ms_per_step it need not be slower at this launch-bound
+    # size: the device-driven loop enqueues iterations ahead, the timed Mults are host-issued one by one)
+    assert b["pcg_iteration"]["iterations"] == 20
+    assert b["pcg_iteration"]["iteration_ms"] > b["roofline"]["kernel_ms_avg"]
     # and one ex16p SDIRK33 step (configs[4]'s unit of work) on the same mesh
     st = b["sdirk_step"]
     assert st["stage_solves"] == 3 and st["converged"] and st["pcg_iterations"] > 3 and st["step_ms"] > st["solves_ms"]
@@ -93,4 +96,4 @@ def test_bench_loopback_group_and_member_lines():
     p = run_bench(*SMALL, "--loopback", "2", "--member", "-1", "--pcg-iters", "5")
     assert len(p["pcg"]["member_iteration_ms"]) == 2 and p["pcg"]["slowest_member_iteration_ms"] > 0
     s = run_bench(*SMALL, "--variants", "0", "--pcg-iters", "5")
-    assert s["pcg_iteration"]["iteration_ms"] > s["ms_per_step"]
+    assert s["pcg_iteration"]["iteration_ms"] > s["roofline"]["kernel_ms_avg"]  # (as in the single-GPU line)

@@ -207,10 +207,15 @@ def time_mults(apply, x, y, steps, warmup, world, dist, torch):
     for _ in range(steps):
         apply(x, y)
     torch.cuda.synchronize()
+    # this rank's K steps end at its own synchronize; the closing barrier still brackets the region
+    # (no rank leaves before every rank's steps are done), but its own latency -- an RCCL all-reduce
+    # and a synchronize, tens of microseconds at 8 ranks against a ~1.3 ms region of 20 C4 Mults --
+    # is not a Mult's.  The caller takes the MAX of these per-rank times over the ranks.
+    t1 = time.perf_counter()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    return time.perf_counter() - t0
+    return t1 - t0
 
 
 def kernel_ms(forms, apply, x, y, steps, torch, settle_s=0.06, world=1, dist=None):

@@ -97,3 +97,41 @@ def test_bench_loopback_group_and_member_lines():
     assert len(p["pcg"]["member_iteration_ms"]) == 2 and p["pcg"]["slowest_member_iteration_ms"] > 0
     s = run_bench(*SMALL, "--variants", "0", "--pcg-iters", "5")
     assert s["pcg_iteration"]["iteration_ms"] > s["roofline"]["kernel_ms_avg"]  # (as in the single-GPU line)
+
+
+def _timed_region_worker(rank, port, out):
+    """One rank of bench.py's timed region over gloo: rank 1's Mults take 20 ms each, rank 0's nothing."""
+    import importlib.util
+    import time
+    import types
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    fake = types.SimpleNamespace(cuda=types.SimpleNamespace(synchronize=lambda: None))
+    delay = 0.02 if rank == 1 else 0.0
+    dt = b.time_mults(lambda x, y: time.sleep(delay), None, None, 5, 1, 2, dist, fake)
+    t = torch.tensor([dt], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)  # as bench.py reduces the ranks' times
+    with open(os.path.join(out, f"r{rank}.json"), "w") as f:
+        json.dump({"dt": dt, "max": float(t[0])}, f)
+    dist.destroy_process_group()
+
+
+def test_timed_region_is_per_rank_and_maxed(tmp_path):
+    """bench.py time_mults: the opening barrier aligns the ranks, a rank's time ends at its own last
+    synchronize (the closing barrier brackets the region but is not in it), the line takes the MAX."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_timed_region_worker, args=(port, str(tmp_path)), nprocs=2, join=True)
+    r0 = json.load(open(tmp_path / "r0.json"))
+    r1 = json.load(open(tmp_path / "r1.json"))
+    assert r1["dt"] >= 5 * 0.02 and r0["dt"] < 0.05  # rank 0 does not wait for rank 1 inside its time
+    assert r0["max"] == r1["max"] == r1["dt"]
